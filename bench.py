@@ -1,0 +1,323 @@
+"""bench.py — shuffle GB/s/node (partition + exchange), TeraSort 100-byte records.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload terasort|zipf|small]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL over xGMI)
+
+A step = one full shuffle of the rank's resident input: every map batch is partitioned by the
+gfx950 kernels (P1-P3) and, for N > 1, its partition-aligned share is exchanged with every other
+GPU (ncclAllToAllv, overlapped with the next launch group on a second stream).  At N = 1 the
+reduce side resolves its blocks zero-copy from the index tables (no bytes move).
+Inputs are generated on the device before timing (counter-based) and stay in HBM.
+
+value = input bytes of all ranks / max-over-ranks wall time of K steps, in GB/s (1e9 B/s).
+Rank 0 prints ONE JSON line; everything else goes to stderr.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from sparkucx_amd import native as N  # noqa: E402
+from sparkucx_amd.shuffle import Node  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+XGMI_LINK_GBS = 153.0     # per xGMI link, per direction (task statement; 7 links per GPU)
+METRIC = "shuffle GB/s/node (partition+exchange), TeraSort 100B recs at 1/2/4/8 GPUs"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def uniform_bounds(R: int, key_len: int = 10) -> bytes:
+    """bound i = floor((i+1) * 2^64 / R) as the big-endian key prefix (oracle: o_range_bounds_uniform)."""
+    out = bytearray()
+    for i in range(R - 1):
+        v = ((i + 1) << 64) // R
+        out += v.to_bytes(8, "big") + bytes(key_len - 8)
+    return bytes(out)
+
+
+WORKLOADS = {
+    # name: (record size, R, generator, partitioner kind, key_len, per-GPU records at N=1 / N>1)
+    "terasort": (100, 200, N.GEN_TERASORT, N.PART_RANGE_BYTES, 10, 1_000_000_000, 1_250_000_000),
+    "zipf": (100, 200, N.GEN_ZIPF, N.PART_MURMUR3_LONG, 8, 1_000_000_000, 1_000_000_000),
+    "small": (16, 10000, N.GEN_SMALL, N.PART_MURMUR3_LONG, 8, 1 << 30, 1 << 30),
+}
+
+
+def cpu_baseline(args) -> dict | None:
+    """Oracle CPU shuffle (Spark sort-shuffle write to /dev/shm files + UCX-style two-phase fetch)
+    on a bounded sample of the same workload: config 1's shape (1 GB, R=200, 8 map tasks)."""
+    try:
+        from oracle import oracle as O  # test infrastructure: timed as the baseline only
+    except Exception as e:  # pragma: no cover
+        log("cpu baseline unavailable:", e)
+        return None
+    n, maps = args.cpu_records, 8
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    recs = O.gen_terasort(0x5EED0001, 0, n)
+    part = O.terasort_partitioner(200)
+    d = "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else None
+    tmp = tempfile.mkdtemp(prefix="sux_cpu_", dir=d)
+    times = []
+    try:
+        for i in range(args.cpu_reps + 1):
+            r = O.cpu_shuffle(part, recs, 100, maps, threads, tmp)
+            if r.bytes_fetched != recs.size:
+                raise RuntimeError("cpu baseline fetched the wrong byte count")
+            if i:
+                times.append((r.total_s, r.map_s, r.fetch_s))
+    finally:
+        try:
+            os.rmdir(tmp)
+        except OSError:
+            pass
+    times.sort()
+    t, tm, tf = times[len(times) // 2]
+    return {"value": round(recs.size / t / 1e9, 3), "unit": "GB/s", "cores": threads,
+            "kind": "port",
+            "sample": f"TeraSort {n} x 100 B ({recs.size / 1e9:.2f} GB), R=200, {maps} map tasks, "
+                      f"{threads} threads; Spark-style write to {'/dev/shm' if d else '/tmp'} files "
+                      f"+ two-phase offset/block fetch; median of {len(times)} "
+                      f"(map {tm:.3f}s, fetch {tf:.3f}s)"}
+
+
+def load_traffic(kernel: str) -> float | None:
+    """Per-launch HBM bytes of `kernel` from the committed PMC summary (profiles/pmc_r01.json,
+    written by profiles/collect_pmc.py; FETCH_SIZE x2 + WRITE_SIZE per the microarch guide)."""
+    p = os.path.join(ROOT, "profiles", "pmc_r01.json")
+    try:
+        with open(p) as f:
+            return json.load(f)["kernels"][kernel]["hbm_bytes_per_launch"]
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="terasort", choices=sorted(WORKLOADS))
+    ap.add_argument("--records", type=int, default=0, help="records per GPU (0 = workload default)")
+    ap.add_argument("--map-records", type=int, default=1 << 20, help="records per map batch")
+    ap.add_argument("--group-maps", type=int, default=8, help="map batches per kernel launch group")
+    ap.add_argument("--cpu-records", type=int, default=10_000_000)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-reps", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    rs, R, gen, kind, key_len, n1, nN = WORKLOADS[args.workload]
+    n = args.records or (n1 if world == 1 else nN)
+    rpm, gm = args.map_records, args.group_maps
+    maps = -(-n // rpm)
+    groups = -(-maps // gm)
+    group_recs = gm * rpm
+
+    # ---- node + communicator bootstrap (unique id carried by torch.distributed) ----------
+    comm_id = None
+    if world > 1:
+        t = torch.zeros(128, dtype=torch.uint8, device=dev)
+        if rank == 0:
+            t.copy_(torch.frombuffer(bytearray(N.unique_id()), dtype=torch.uint8))
+        dist.broadcast(t, 0)
+        comm_id = bytes(t.cpu().numpy())
+    node = Node(device=local, rank=rank, world_size=world, comm_id=comm_id)
+    if kind == N.PART_RANGE_BYTES:
+        part = node.partitioner(kind, R, key_offset=0, key_len=key_len, bounds=uniform_bounds(R))
+    else:
+        part = node.partitioner(kind, R, key_offset=0, key_len=key_len, seed=42)
+
+    # ---- resident input (generated on device, untimed) ---------------------------------------
+    seed = {"terasort": 0x5EED0002, "zipf": 0x5EED0004, "small": 0x5EED0005}[args.workload]
+    data = torch.empty(n * rs, dtype=torch.uint8, device=dev)
+    chunk = 1 << 27
+    for c0 in range(0, n, chunk):
+        c1 = min(n, c0 + chunk)
+        node.generate(gen, seed, rank * n + c0, c1 - c0, rs, zipf_s=1.1, zipf_n=1 << 24,
+                      out=data[c0 * rs:c1 * rs])
+    index = torch.empty(maps * (R + 1), dtype=torch.int64, device=dev)
+    ws_bytes = node.workspace_size(part, rs, rpm, min(n, group_recs))
+    comp = torch.cuda.current_stream(dev)
+
+    if world == 1:
+        out = torch.empty(n * rs, dtype=torch.uint8, device=dev)
+        index_be = torch.empty(maps * (R + 1) * 8, dtype=torch.uint8, device=dev)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+
+        def step():
+            for g in range(groups):
+                r0 = g * group_recs
+                r1 = min(n, r0 + group_recs)
+                m0 = g * gm
+                mg = -(-(r1 - r0) // rpm)
+                node.partition_maps(part, data[r0 * rs:r1 * rs], rs, rpm, num_records=r1 - r0,
+                                    out=out[r0 * rs:r1 * rs],
+                                    index=index[m0 * (R + 1):(m0 + mg) * (R + 1)],
+                                    index_be=index_be[m0 * (R + 1) * 8:(m0 + mg) * (R + 1) * 8],
+                                    workspace=ws, stream=comp)
+    else:
+        comm = torch.cuda.Stream(dev)
+        send = [torch.empty(group_recs * rs, dtype=torch.uint8, device=dev) for _ in range(2)]
+        # receive ring (Spark's reducer consumes fetched blocks as a stream, maxBytesInFlight);
+        # 1.5x the group's bytes absorbs uneven partition sizes
+        recv = [torch.empty(int(group_recs * rs * 1.5) + (1 << 20), dtype=torch.uint8,
+                            device=dev) for _ in range(2)]
+        ws = [torch.empty(ws_bytes, dtype=torch.uint8, device=dev) for _ in range(2)]
+        gidx = [torch.empty(world * gm * (R + 1), dtype=torch.int64, device=dev) for _ in range(2)]
+        peer = [torch.empty(world, dtype=torch.int64, device=dev) for _ in range(2)]
+        part_done = [torch.cuda.Event() for _ in range(2)]
+        send_free = [torch.cuda.Event() for _ in range(2)]
+        xfer_ev = []
+        stats = {"recv_bytes": 0, "remote_bytes": 0}
+
+        def exchange(j):
+            s = j % 2
+            r0 = j * group_recs
+            r1 = min(n, r0 + group_recs)
+            m0 = j * gm
+            mg = -(-(r1 - r0) // rpm)
+            comm.wait_event(part_done[s])
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(comm)
+            rb = node.exchange_group(send[s], index[m0 * (R + 1):(m0 + mg) * (R + 1)], mg, R,
+                                     gidx[s], recv[s], stream=comm)
+            e1.record(comm)
+            xfer_ev.append((e0, e1))
+            send_free[s].record(comm)
+            stats["recv_bytes"] += int(rb.sum())
+            stats["remote_bytes"] += int(rb.sum() - rb[rank])
+
+        def step():
+            for k in range(groups):
+                s = k % 2
+                r0 = k * group_recs
+                r1 = min(n, r0 + group_recs)
+                m0 = k * gm
+                mg = -(-(r1 - r0) // rpm)
+                if k >= 2:
+                    comp.wait_event(send_free[s])
+                node.partition_maps_peer_major(part, data[r0 * rs:r1 * rs], rs, rpm, world,
+                                               num_records=r1 - r0, out=send[s],
+                                               index=index[m0 * (R + 1):(m0 + mg) * (R + 1)],
+                                               peer_bytes=peer[s], workspace=ws[s], stream=comp)
+                part_done[s].record(comp)
+                if k >= 1:
+                    exchange(k - 1)
+            exchange(groups - 1)
+            comp.wait_stream(comm)
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    log(f"[rank {rank}] {args.workload}: {n} records x {rs} B = {n * rs / 1e9:.1f} GB/GPU, "
+        f"R={R}, {maps} maps of {rpm}, {groups} launch groups of {gm} maps, world={world}")
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    node.kernel_times()  # drop warm-up timings
+    node.set_kernel_timing(True)
+    if world > 1:
+        xfer_ev.clear()
+        stats["recv_bytes"] = stats["remote_bytes"] = 0
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    t1 = time.perf_counter()
+    node.set_kernel_timing(False)
+    kt = node.kernel_times()
+
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    total_bytes = n * rs * world * args.steps
+    value = total_bytes / elapsed / 1e9
+
+    # ---- roofline of the dominant kernel (scatter) + the whole map-side pass --------------
+    launches, sc_ms = kt["scatter"]
+    recs_per_launch = n * args.steps / max(1, launches)
+    alg = 2 * recs_per_launch * rs                       # read + write every record once
+    sc_avg = sc_ms / max(1, launches) / 1e3
+    achieved = alg / sc_avg / 1e9 if sc_avg else None
+    map_ms = kt["hist"][1] + kt["scan"][1] + kt["scatter"][1]
+    map_alg = (2 * n * rs + 8 * (R + 1) * maps) * args.steps
+    map_side = map_alg / (map_ms / 1e3) / 1e9 if map_ms else None
+    traffic = load_traffic("k_scatter")
+    result = {
+        "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (counter-based generator, resident in HBM before timing)",
+        "config": {"workload": f"{args.workload}: {n} x {rs}-byte records per GPU "
+                               f"({n * rs / 1e9:.0f} GB/GPU, {n * rs * world / 1e9:.0f} GB total), "
+                               f"R={R}, map batches of {rpm} records, {gm} maps per launch group"
+                               + (", zero-copy local block resolve" if world == 1 else
+                                  ", partition-aligned ncclAllToAllv exchange"),
+                   "global_batch": n * world, "seq_len": rs, "parallelism": f"shuffle{world}"},
+        "roofline": {"bound": "hbm", "achieved": None if achieved is None else round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": None if achieved is None else round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "kernel": "k_scatter",
+                     "alg_bytes_per_launch": int(alg),
+                     "avg_launch_ms": round(sc_avg * 1e3, 4)},
+        "roofline_map_side": {"bound": "hbm",
+                              "achieved": None if map_side is None else round(map_side, 1),
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": None if map_side is None else round(map_side / HBM_PEAK_GBS, 4),
+                              "kernels_ms": {k: round(v[1], 3) for k, v in kt.items()},
+                              "launches": {k: v[0] for k, v in kt.items()}},
+        "cpu_baseline": None,
+    }
+    if world > 1:
+        torch.cuda.synchronize(dev)
+        xms = sum(a.elapsed_time(b) for a, b in xfer_ev)
+        remote = stats["remote_bytes"]
+        peak = (world - 1) * XGMI_LINK_GBS
+        ach = remote / (xms / 1e3) / 1e9 if xms else None
+        result["roofline_exchange"] = {
+            "bound": "xgmi", "achieved": None if ach is None else round(ach, 1), "peak": peak,
+            "unit": "GB/s", "frac": None if ach is None else round(ach / peak, 4),
+            "remote_bytes_per_rank": remote // args.steps, "exchange_ms": round(xms, 2)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    node.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

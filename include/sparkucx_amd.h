@@ -1,0 +1,239 @@
+/*
+ * sparkucx_amd.h — C-ABI of the MI355X shuffle data path (libsparkucx_amd.so).
+ *
+ * This is the drop-in boundary under SparkUCX's Spark-3.0 plugin surface.  Every entry point
+ * names the reference interface it replaces (paths relative to the reference checkout,
+ * src/main/{scala,java}/org/apache/spark/shuffle/...).  A JNI shim binds these
+ * symbols 1:1; nothing in this header uses C++ or torch types.
+ *
+ * Conventions:
+ *   - every function returns SUX_OK (0) or a negative SUX_E* code; sux_last_error() gives the
+ *     message of the last failure on the calling thread; no C++ exception crosses the boundary;
+ *   - handles are opaque; device pointers are plain `void*` in the node's HIP device space;
+ *   - `stream` arguments are hipStream_t passed as `void*`; NULL = the HIP null stream.  A task
+ *     thread that wants its own ordering domain (the analog of UcxNode.getThreadLocalWorker,
+ *     UcxNode.java:147-176) passes its own stream or hipStreamPerThread;
+ *   - all integers are fixed-width; byte counts are uint64_t.
+ */
+#ifndef SPARKUCX_AMD_H_
+#define SPARKUCX_AMD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SUX_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------------------------- */
+#define SUX_OK 0
+#define SUX_EINVAL -1  /* bad argument (IllegalArgumentException / assume() failure)         */
+#define SUX_ENOMEM -2  /* device or host allocation failed                                    */
+#define SUX_EHIP -3    /* HIP runtime error                                                   */
+#define SUX_ECOMM -4   /* RCCL error (UcxException on the transport in the reference)        */
+#define SUX_ENOENT -5  /* unknown shuffle / map output / block (SparkException "Unknown block") */
+#define SUX_ESTATE -6  /* wrong lifecycle state (IllegalStateException "must be initialized") */
+#define SUX_ERANGE -7  /* size limit exceeded (SparkException "Metadata block size ...")      */
+
+/* ---- partitioners ---------------------------------------------------- */
+/* Spark RangePartitioner over an unsigned lexicographic byte key (TeraSort's 10-byte key):
+ * pid = #{ i : bounds[i] < key }  (RangePartitioner.getPartition [ext], bounds strictly rising). */
+#define SUX_PART_RANGE_BYTES 1
+/* Spark SQL HashPartitioning of one LongType column: pmod(Murmur3_x86_32.hashLong(key, seed), R),
+ * key = little-endian int64 at key_offset (UnsafeRow word order).                              */
+#define SUX_PART_MURMUR3_LONG 2
+/* Spark SQL HashPartitioning of one IntegerType column: pmod(hashInt(key, seed), R).           */
+#define SUX_PART_MURMUR3_INT 3
+/* Spark SQL HashPartitioning of one BinaryType column: pmod(hashUnsafeBytes(key, seed), R)
+ * (legacy tail-byte mixing, see oracle/oracle.c).                                              */
+#define SUX_PART_MURMUR3_BYTES 4
+/* RDD HashPartitioner on a java.lang.Long key: nonNegativeMod(Long.hashCode(key), R).          */
+#define SUX_PART_HASH_LONG 5
+/* RDD HashPartitioner on a java.lang.Integer key: nonNegativeMod(key, R).                      */
+#define SUX_PART_HASH_INT 6
+
+typedef struct sux_partitioner_desc {
+  int32_t kind;           /* SUX_PART_*                                                        */
+  int32_t num_partitions; /* R, 1 .. 32768 (LDS-resident counters)                            */
+  int32_t key_offset;     /* byte offset of the key inside a record                            */
+  int32_t key_len;        /* key bytes: RANGE 1..16, MURMUR3_BYTES 1..64, LONG 8, INT 4        */
+  int32_t seed;           /* Murmur3 seed (Spark SQL uses 42)                                  */
+  int32_t ascending;      /* RANGE only: 1 = ascending (Spark default), 0 = descending         */
+  const uint8_t* range_bounds; /* RANGE only: host array of (R-1)*key_len bytes, strictly rising */
+} sux_partitioner_desc;
+
+/* ---- node (UcxNode, UcxNode.java:60-96 / close :194-221) -------------------------------- */
+typedef struct sux_node sux_node;
+typedef struct sux_partitioner sux_partitioner;
+typedef struct sux_buffer sux_buffer;
+
+typedef struct sux_conf {
+  int32_t device;     /* HIP device ordinal this executor owns                                 */
+  int32_t rank;       /* rank of this executor in the node's exchange group                    */
+  int32_t world_size; /* executors (GPUs) in the exchange group; 1 = local resolve only        */
+  int32_t num_streams;/* internal streams (compute + comm); 0 = default (2)                    */
+  uint8_t comm_id[128];         /* RCCL unique id from sux_comm_unique_id(), world_size > 1    */
+  uint64_t min_buffer_size;     /* spark.shuffle.ucx.memory.minBufferSize (UcxShuffleConf.scala:66-72) */
+  uint64_t min_allocation_size; /* spark.shuffle.ucx.memory.minAllocationSize (:74-81)         */
+  uint64_t metadata_block_size; /* 2*spark.shuffle.ucx.rkeySize (:32-40): directory slot bytes */
+} sux_conf;
+
+/* Fill defaults (UcxShuffleConf.scala:17-90): 1 KiB min buffer, 4 MiB min allocation, 300 B slot. */
+void sux_conf_init(sux_conf* conf);
+
+int sux_abi_version(void);
+/* Message of the last failed call on this thread; returns the full length. */
+int sux_last_error(char* buf, size_t len);
+
+/* Bootstrap of the exchange group.  Replaces the executor->driver tag-send of worker addresses
+ * (UcxNode.startExecutor, UcxNode.java:130-145; RpcConnectionCallback.java:47-89): rank 0 makes
+ * the id and any side channel (Spark RPC, torch.distributed store) carries the 128 bytes. */
+int sux_comm_unique_id(uint8_t out[128]);
+
+int sux_node_create(const sux_conf* conf, int is_driver, sux_node** out);
+int sux_node_destroy(sux_node* node);
+
+/* ---- partitioner object: P1 (UcxShuffleManager.getWriter picks the writer, :36-50) ---------- */
+int sux_partitioner_create(sux_node* node, const sux_partitioner_desc* desc, sux_partitioner** out);
+int sux_partitioner_destroy(sux_partitioner* part);
+
+/* ---- map side, stateless: P1+P2+P3 over device-resident map batches ------------------------ *
+ * Partition `num_records` fixed-size records (record_size % 4 == 0, 4 .. 4096) laid out as
+ * consecutive map batches of `records_per_map` records (the last one may be shorter).  For each
+ * map batch m the output is Spark's sort-shuffle data file restated on the GPU: its records
+ * regrouped by partition id 0..R-1, stable within a partition, written to
+ * d_out + m*records_per_map*record_size, and its index file: R+1 cumulative
+ * byte offsets starting at 0, native int64 into d_index[m*(R+1) ..] and, if d_index_be is not
+ * NULL, big-endian bytes into d_index_be[m*(R+1)*8 ..] — the exact bytes of IndexShuffleBlockResolver.
+ * d_pids (nullable) receives each record's partition id as uint16 in input order.
+ * Workspace: sux_partition_workspace_size().  Everything is enqueued on `stream`; no host sync. */
+int sux_partition_workspace_size(const sux_partitioner* part, uint32_t record_size,
+                                 uint64_t records_per_map, uint64_t num_records, uint64_t* bytes);
+int sux_partition_maps(sux_node* node, const sux_partitioner* part, const void* d_records,
+                       uint32_t record_size, uint64_t records_per_map, uint64_t num_records,
+                       void* d_out, int64_t* d_index, uint8_t* d_index_be, uint16_t* d_pids,
+                       void* d_workspace, uint64_t workspace_bytes, void* stream);
+
+/* Same as sux_partition_maps, but the output is laid out for the exchange: peer-major
+ * [peer h][map m][partitions owned by h (floor(hR/W) .. floor((h+1)R/W))], so that every peer's
+ * share of the whole group is ONE contiguous byte range and the all-to-all needs no repacking.
+ * The index tables are still each map's logical data-file offsets (Spark's index file bytes).
+ * d_peer_bytes (device, `world` u64) receives the bytes destined to each peer. */
+int sux_partition_maps_peer_major(sux_node* node, const sux_partitioner* part,
+                                  const void* d_records, uint32_t record_size,
+                                  uint64_t records_per_map, uint64_t num_records, int32_t world,
+                                  void* d_send, int64_t* d_index, uint8_t* d_index_be,
+                                  uint64_t* d_peer_bytes, void* d_workspace,
+                                  uint64_t workspace_bytes, void* stream);
+
+/* Exchange plan of one peer-major group (host arithmetic, no device access; usable on CPU):
+ * from the all-gathered index tables gathered[g][m][0..R] (world*num_maps*(R+1) int64) compute,
+ * for `rank`, the byte counts/displacements of ncclAllToAllv.  Received layout on rank h:
+ * [source g][map m of g][partitions owned by h]. */
+int sux_plan_group(int32_t world, int32_t rank, int32_t num_maps, int32_t num_partitions,
+                   const int64_t* gathered_index, uint64_t* sendcounts, uint64_t* sdispls,
+                   uint64_t* recvcounts, uint64_t* rdispls);
+/* Byte offset, inside rank `rank`'s receive buffer, of block (source g, map m, partition p);
+ * p must be owned by `rank`.  Returns -1 if not. */
+int64_t sux_plan_block_offset(int32_t world, int32_t rank, int32_t num_maps,
+                              int32_t num_partitions, const int64_t* gathered_index, int32_t g,
+                              int32_t m, int32_t p);
+
+/* One pipelined exchange step over the node's RCCL communicator: all-gather this rank's
+ * num_maps index tables into d_gathered_index (device, world*num_maps*(R+1) int64), bring them
+ * to the host (the only host sync), plan (sux_plan_group) and ncclAllToAllv d_send -> d_recv.
+ * recv_bytes (host, world u64, nullable) receives the per-source byte counts. */
+int sux_exchange_group(sux_node* node, const void* d_send, const int64_t* d_index,
+                       int32_t num_maps, int32_t num_partitions, int64_t* d_gathered_index,
+                       void* d_recv, uint64_t recv_capacity, uint64_t* recv_bytes, void* stream);
+
+/* Partition ids only (P1), uint16 per record; used by tests and by the exchange planner. */
+int sux_partition_ids(sux_node* node, const sux_partitioner* part, const void* d_records,
+                      uint32_t record_size, uint64_t num_records, uint16_t* d_pids, void* stream);
+
+/* ---- shuffle lifecycle: CommonUcxShuffleManager.registerShuffleCommon :39-56 ---------------- */
+typedef struct sux_handle_desc {
+  int32_t shuffle_id;
+  int32_t num_maps;       /* directory slots: sized by MAP count (fixes quirk Q1, :27)          */
+  int32_t num_partitions;
+  int32_t record_size;
+  uint64_t directory_bytes; /* num_maps * metadata_block_size                                  */
+} sux_handle_desc;
+
+int sux_register_shuffle(sux_node* node, int32_t shuffle_id, int32_t num_maps,
+                         int32_t num_partitions, int32_t record_size, sux_handle_desc* out);
+/* CommonUcxShuffleManager.unregisterShuffle :73-77 + CommonUcxShuffleBlockResolver.removeShuffle :116-121 */
+int sux_unregister_shuffle(sux_node* node, int32_t shuffle_id);
+
+/* getWriter(...).write(records) + UcxShuffleBlockResolver.writeIndexFileAndCommit
+ * (compat/spark_3_0/UcxShuffleBlockResolver.scala:33-51 -> CommonUcxShuffleBlockResolver.scala:33-107):
+ * partition one map batch held in device memory into a pooled device buffer owned by the node,
+ * build its index, and publish the map's directory slot (the 300-byte driver descriptor analog).
+ * An empty map output publishes nothing (UcxShuffleBlockResolver.scala:42-45). */
+int sux_write_map_output(sux_node* node, int32_t shuffle_id, int32_t map_index,
+                         const sux_partitioner* part, const void* d_records, uint64_t num_records,
+                         void* stream);
+/* writeIndexFileAndCommit for a map output produced elsewhere: `d_data` (data_bytes, device)
+ * is adopted by copy; `lengths` are R host int64 partition lengths (Spark's lengths[]). */
+int sux_commit_map_output(sux_node* node, int32_t shuffle_id, int32_t map_index,
+                          const void* d_data, uint64_t data_bytes, const int64_t* lengths,
+                          void* stream);
+/* Read back a committed map's index file bytes ((R+1)*8 big-endian, host buffer). */
+int sux_map_output_index(sux_node* node, int32_t shuffle_id, int32_t map_index,
+                         uint8_t* out_index_be, uint64_t out_len);
+
+/* ---- exchange: the reduce-side fetch as a partition-aligned all-to-all -------- *
+ * Collective over the node's group: every rank calls it after committing its map outputs.
+ * Rank h receives partitions [floor(h*R/G), floor((h+1)*R/G)) of every map of every rank.
+ * Replaces the driver-table GET (UcxWorkerWrapper.fetchDriverMetadataBuffer :176-196) by an
+ * all-gather of index tables, and the phase-1/phase-2 GETs (UcxShuffleClient.java:50-127,
+ * OnOffsetsFetchCallback.java:44-92) by ncclAllToAllv over xGMI. */
+int sux_exchange(sux_node* node, int32_t shuffle_id, void* stream);
+/* Reduce-partition ownership of a rank: [*start, *end). */
+int sux_owned_partitions(sux_node* node, int32_t shuffle_id, int32_t rank, int32_t* start,
+                         int32_t* end);
+
+/* ---- fetch: UcxShuffleClient.fetchBlocks (reducer/compat/spark_3_0/UcxShuffleClient.java:94-127) */
+typedef struct sux_block_id {
+  int32_t map_index;    /* mapIdToBlockIndex(mapTaskId) (compat/spark_3_0/UcxShuffleReader.scala:42-50) */
+  int32_t start_reduce; /* ShuffleBlockId.reduceId, or ShuffleBlockBatchId.startReduceId         */
+  int32_t end_reduce;   /* start+1 for ShuffleBlockId, ShuffleBlockBatchId.endReduceId          */
+  int32_t reserved;
+} sux_block_id;
+
+/* Fetch `n` blocks into one contiguous pooled device buffer, in request order (the layout of
+ * OnOffsetsFetchCallback.java:75-87); sizes[i] = off[end]-off[start] (:53-72); block i starts at
+ * sum(sizes[0..i)).  The buffer is refcounted: one reference per block, like the slices of
+ * OnBlocksFetchCallback.java:33-57; sux_buffer_release() drops one, the last returns it to the
+ * pool.  Blocks must be local to this rank (own maps at G=1, owned partitions after exchange).
+ * Unlike the reference (which never calls onBlockFetchFailure), a missing block fails the call
+ * with SUX_ENOENT and names it in sux_last_error(). */
+int sux_fetch_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* blocks, int32_t n,
+                     int64_t* sizes, sux_buffer** out, void* stream);
+/* Zero-copy resolve: device address and size of each block (no copy; local blocks only). */
+int sux_resolve_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* blocks, int32_t n,
+                       uint64_t* dev_addrs, int64_t* sizes);
+int sux_buffer_info(sux_buffer* buf, void** dev_ptr, uint64_t* size, uint64_t* capacity);
+int sux_buffer_retain(sux_buffer* buf, int32_t count);
+int sux_buffer_release(sux_buffer* buf);
+
+/* ---- measurement hooks ------------------------------------------------------------------ */
+/* When enabled, the node brackets each partition-kernel launch with HIP events on the launch
+ * stream; sux_kernel_times() returns per-kernel {launches, total_ms} for kernels
+ * 0=hist 1=scan 2=scatter 3=gather-copy (order fixed), and resets them. */
+int sux_set_kernel_timing(sux_node* node, int enable);
+int sux_kernel_times(sux_node* node, int64_t* launches, double* total_ms, int32_t nkernels);
+
+/* ---- synthetic inputs (counter-based; identical bytes to oracle/oracle.c) --------------- */
+#define SUX_GEN_TERASORT 1 /* 100-byte records: 10-byte key + row id + filler                  */
+#define SUX_GEN_SMALL 2    /* 16-byte records: int64 uniform key + int64 value                  */
+#define SUX_GEN_ZIPF 3     /* 100-byte records: int64 Zipf(s) key over `zipf_n` keys + filler   */
+int sux_generate(sux_node* node, int32_t kind, uint64_t seed, uint64_t first_record,
+                 uint64_t num_records, double zipf_s, uint64_t zipf_n, void* d_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPARKUCX_AMD_H_ */

@@ -1,0 +1,235 @@
+"""numpy/ctypes wrapper of oracle/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+The CPU restatement of the reference path (see oracle.c's header for the file:line map and the
+pinning status).  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module; the product path (sparkucx_amd) never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+RANGE_BYTES, MURMUR3_LONG, MURMUR3_INT, MURMUR3_BYTES, HASH_LONG, HASH_INT = 1, 2, 3, 4, 5, 6
+
+
+class Part(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("num_partitions", C.c_int32), ("key_offset", C.c_int32),
+                ("key_len", C.c_int32), ("seed", C.c_int32), ("ascending", C.c_int32),
+                ("range_bounds", C.c_void_p)]
+
+
+class CpuResult(C.Structure):
+    _fields_ = [("map_s", C.c_double), ("fetch_s", C.c_double), ("total_s", C.c_double),
+                ("bytes_in", C.c_uint64), ("bytes_fetched", C.c_uint64),
+                ("checksum", C.c_uint64)]
+
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        P, U64, I32, U32 = C.c_void_p, C.c_uint64, C.c_int32, C.c_uint32
+        sig = {
+            "o_mix64": (U64, [U64]),
+            "o_gen_terasort": (None, [U64, U64, U64, P]),
+            "o_gen_small": (None, [U64, U64, U64, P]),
+            "o_gen_zipf": (None, [U64, U64, U64, C.c_double, U64, P]),
+            "o_zipf_table_size": (C.c_int, [U64]),
+            "o_zipf_table": (None, [C.c_double, U64, P, P]),
+            "o_murmur3_hash_int": (I32, [I32, I32]),
+            "o_murmur3_hash_long": (I32, [C.c_int64, I32]),
+            "o_murmur3_hash_unsafe_bytes": (I32, [P, I32, I32]),
+            "o_pmod": (I32, [I32, I32]),
+            "o_non_negative_mod": (I32, [I32, I32]),
+            "o_range_bounds_uniform": (None, [I32, I32, P]),
+            "o_get_partition": (I32, [C.POINTER(Part), P]),
+            "o_partition_ids": (None, [C.POINTER(Part), P, U64, U32, P]),
+            "o_write_map": (None, [C.POINTER(Part), P, U64, U32, P, P, P, P]),
+            "o_index_from_lengths": (None, [P, I32, P, P]),
+            "o_fetch_blocks": (C.c_int64, [P, P, I32, I32, P, I32, P, P]),
+            "o_owner_start": (I32, [I32, I32, I32]),
+            "o_cpu_shuffle": (C.c_int, [C.POINTER(Part), P, U64, U32, I32, I32, C.c_char_p,
+                                        C.POINTER(CpuResult)]),
+            "o_checksum": (U64, [P, U64]),
+        }
+        for k, (r, a) in sig.items():
+            f = getattr(L, k)
+            f.restype, f.argtypes = r, a
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+# ---- generators --------------------------------------------------------------------------
+def gen_terasort(seed: int, first: int, n: int) -> np.ndarray:
+    out = np.empty(n * 100, np.uint8)
+    lib().o_gen_terasort(seed, first, n, _p(out))
+    return out
+
+
+def gen_small(seed: int, first: int, n: int) -> np.ndarray:
+    out = np.empty(n * 16, np.uint8)
+    lib().o_gen_small(seed, first, n, _p(out))
+    return out
+
+
+def gen_zipf(seed: int, first: int, n: int, s: float = 1.1, zipf_n: int = 1 << 24) -> np.ndarray:
+    out = np.empty(n * 100, np.uint8)
+    lib().o_gen_zipf(seed, first, n, s, zipf_n, _p(out))
+    return out
+
+
+def zipf_table(s: float, zipf_n: int):
+    nb = lib().o_zipf_table_size(zipf_n)
+    b = np.empty(nb + 1, np.uint64)
+    t = np.empty(nb + 1, np.uint64)
+    lib().o_zipf_table(s, zipf_n, _p(b), _p(t))
+    return b, t
+
+
+# ---- hashing ----------------------------------------------------------------------------------
+def murmur3_int(v: int, seed: int) -> int:
+    return lib().o_murmur3_hash_int(v, seed)
+
+
+def murmur3_long(v: int, seed: int) -> int:
+    return lib().o_murmur3_hash_long(v, seed)
+
+
+def murmur3_bytes(b: bytes, seed: int) -> int:
+    arr = np.frombuffer(bytes(b) or b"\0", np.uint8).copy()
+    return lib().o_murmur3_hash_unsafe_bytes(_p(arr), len(b), seed)
+
+
+def pmod(a: int, n: int) -> int:
+    return lib().o_pmod(a, n)
+
+
+# ---- partitioners / map write ------------------------------------------------------------------
+class Partitioner:
+    def __init__(self, kind: int, R: int, key_offset: int = 0, key_len: int = 8, seed: int = 42,
+                 ascending: bool = True, bounds: bytes | None = None):
+        self.kind, self.R, self.key_offset, self.key_len = kind, R, key_offset, key_len
+        self.seed, self.ascending = seed, ascending
+        self._b = None if bounds is None else np.frombuffer(bytes(bounds) or b"\0", np.uint8).copy()
+        self.bounds = bounds
+        self.c = Part(kind, R, key_offset, key_len, seed, int(ascending),
+                      None if self._b is None else self._b.ctypes.data)
+
+    def ids(self, recs: np.ndarray, rec_size: int) -> np.ndarray:
+        n = recs.size // rec_size
+        out = np.empty(max(n, 1), np.uint16)
+        lib().o_partition_ids(C.byref(self.c), _p(recs), n, rec_size, _p(out))
+        return out[:n]
+
+
+def uniform_range_bounds(R: int, key_len: int = 10) -> bytes:
+    out = np.zeros(max(1, (R - 1) * key_len), np.uint8)
+    lib().o_range_bounds_uniform(R, key_len, _p(out))
+    return out[: (R - 1) * key_len].tobytes()
+
+
+def terasort_partitioner(R: int) -> Partitioner:
+    return Partitioner(RANGE_BYTES, R, 0, 10, bounds=uniform_range_bounds(R, 10))
+
+
+def write_map(part: Partitioner, recs: np.ndarray, rec_size: int):
+    """Returns (data bytes, lengths[R] i64, index[R+1] i64, index_be bytes)."""
+    n = recs.size // rec_size
+    out = np.empty(max(1, n * rec_size), np.uint8)
+    lengths = np.empty(part.R, np.int64)
+    index = np.empty(part.R + 1, np.int64)
+    index_be = np.empty((part.R + 1) * 8, np.uint8)
+    lib().o_write_map(C.byref(part.c), _p(recs), n, rec_size, _p(out), _p(lengths), _p(index),
+                      _p(index_be))
+    return out[: n * rec_size], lengths, index, index_be.tobytes()
+
+
+def write_maps(part: Partitioner, recs: np.ndarray, rec_size: int, rpm: int):
+    """Concatenated map-major outputs of consecutive maps (what sux_partition_maps produces)."""
+    n = recs.size // rec_size
+    datas, idxs, bes = [], [], []
+    for m0 in range(0, n, rpm):
+        d, _, ix, be = write_map(part, recs[m0 * rec_size:min(n, m0 + rpm) * rec_size], rec_size)
+        datas.append(d)
+        idxs.append(ix)
+        bes.append(be)
+    if not datas:
+        return np.empty(0, np.uint8), np.zeros(part.R + 1, np.int64), b""
+    return np.concatenate(datas), np.concatenate(idxs), b"".join(bes)
+
+
+def owner_start(h: int, R: int, G: int) -> int:
+    return (h * R) // G
+
+
+def peer_major(part: Partitioner, recs: np.ndarray, rec_size: int, rpm: int, world: int):
+    """Oracle of sux_partition_maps_peer_major: [peer h][map m][partitions owned by h]."""
+    n = recs.size // rec_size
+    maps = []
+    for m0 in range(0, n, rpm):
+        d, _, ix, _ = write_map(part, recs[m0 * rec_size:min(n, m0 + rpm) * rec_size], rec_size)
+        maps.append((d, ix))
+    chunks, peer_bytes = [], []
+    for h in range(world):
+        lo, hi = owner_start(h, part.R, world), owner_start(h + 1, part.R, world)
+        b = 0
+        for d, ix in maps:
+            chunks.append(d[ix[lo]:ix[hi]])
+            b += int(ix[hi] - ix[lo])
+        peer_bytes.append(b)
+    data = np.concatenate(chunks) if chunks else np.empty(0, np.uint8)
+    index = np.concatenate([ix for _, ix in maps]) if maps else np.zeros(0, np.int64)
+    return data, index, np.array(peer_bytes, np.int64)
+
+
+def fetch_blocks(map_data: list[np.ndarray], map_index_be: list[bytes], R: int, blocks):
+    """UcxShuffleClient.fetchBlocks restated: returns (contiguous bytes, sizes)."""
+    nm = len(map_data)
+    datas = [np.ascontiguousarray(d) if d.size else np.zeros(1, np.uint8) for d in map_data]
+    idx = [np.frombuffer(b, np.uint8).copy() for b in map_index_be]
+    dp = (C.c_void_p * max(1, nm))(*[d.ctypes.data for d in datas])
+    ip = (C.c_void_p * max(1, nm))(*[i.ctypes.data for i in idx])
+    flat = []
+    for b in blocks:
+        flat += [b[0], b[1], b[2] if len(b) > 2 else b[1] + 1]
+    bl = np.array(flat or [0], np.int32)
+    sizes = np.zeros(max(1, len(blocks)), np.int64)
+    total = lib().o_fetch_blocks(dp, ip, nm, R, _p(bl), len(blocks), _p(sizes), None)
+    if total < 0:
+        raise ValueError("invalid block")
+    dst = np.empty(max(1, total), np.uint8)
+    lib().o_fetch_blocks(dp, ip, nm, R, _p(bl), len(blocks), _p(sizes), _p(dst))
+    return dst[:total].tobytes(), sizes[:len(blocks)].tolist()
+
+
+def checksum(a: np.ndarray) -> int:
+    return int(lib().o_checksum(_p(a), a.size))
+
+
+def cpu_shuffle(part: Partitioner, recs: np.ndarray, rec_size: int, num_maps: int, threads: int,
+                directory: str = "/dev/shm") -> CpuResult:
+    res = CpuResult()
+    rc = lib().o_cpu_shuffle(C.byref(part.c), _p(recs), recs.size // rec_size, rec_size, num_maps,
+                             threads, directory.encode(), C.byref(res))
+    if rc != 0:
+        raise RuntimeError("cpu shuffle failed")
+    return res

@@ -1,0 +1,1109 @@
+// sux_api.cpp — C-ABI of libsparkucx_amd.so (include/sparkucx_amd.h).
+//
+// Host runtime around the gfx950 kernels: node lifecycle (UcxNode), device memory pool
+// (MemoryPool/RegisteredMemory), per-shuffle directory (driver metadata table), map commit
+// (CommonUcxShuffleBlockResolver), fetch (UcxShuffleClient + callbacks) and the RCCL exchange.
+// No C++ exception crosses the boundary: every entry point is wrapped in guard().
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/sparkucx_amd.h"
+#include "sux_internal.h"
+
+// ============================================================================================
+// errors
+// ============================================================================================
+namespace {
+thread_local std::string g_err;
+
+struct SuxError {
+  int code;
+  std::string msg;
+};
+
+[[noreturn]] void raise(int code, const std::string& msg) { throw SuxError{code, msg}; }
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) raise(SUX_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+void nccl_check(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess) raise(SUX_ECOMM, std::string(what) + ": " + ncclGetErrorString(r));
+}
+void require(bool ok, int code, const std::string& msg) {
+  if (!ok) raise(code, msg);
+}
+
+template <class F>
+int guard(F&& f) {
+  try {
+    f();
+    return SUX_OK;
+  } catch (const SuxError& e) {
+    g_err = e.msg;
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    g_err = "host allocation failed";
+    return SUX_ENOMEM;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return SUX_EINVAL;
+  } catch (...) {
+    g_err = "unknown error";
+    return SUX_EINVAL;
+  }
+}
+}  // namespace
+
+// ============================================================================================
+// kernel timing (sux_set_kernel_timing / sux_kernel_times)
+// ============================================================================================
+namespace sux {
+struct Timer {
+  std::mutex mu;
+  bool enabled = false;
+  struct Rec {
+    int slot;
+    hipEvent_t a, b;
+  };
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> spare;
+  hipEvent_t open[kNumSlots] = {};
+
+  hipEvent_t get() {
+    if (!spare.empty()) {
+      hipEvent_t e = spare.back();
+      spare.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    hip_check(hipEventCreate(&e), "hipEventCreate");
+    return e;
+  }
+  ~Timer() {
+    for (auto& r : recs) {
+      (void)hipEventDestroy(r.a);
+      (void)hipEventDestroy(r.b);
+    }
+    for (auto e : spare) (void)hipEventDestroy(e);
+  }
+};
+
+void timer_begin(Timer* t, int slot, hipStream_t s) {
+  if (!t || !t->enabled) return;
+  std::lock_guard<std::mutex> lk(t->mu);
+  hipEvent_t e = t->get();
+  (void)hipEventRecord(e, s);
+  t->open[slot] = e;
+}
+
+void timer_end(Timer* t, int slot, hipStream_t s) {
+  if (!t || !t->enabled) return;
+  std::lock_guard<std::mutex> lk(t->mu);
+  if (!t->open[slot]) return;
+  hipEvent_t e = t->get();
+  (void)hipEventRecord(e, s);
+  t->recs.push_back({slot, t->open[slot], e});
+  t->open[slot] = nullptr;
+}
+}  // namespace sux
+
+// ============================================================================================
+// device memory pool — MemoryPool.java semantics on HBM
+// ============================================================================================
+namespace {
+struct PoolBuf {
+  uint8_t* ptr = nullptr;
+  uint64_t cap = 0;  // size class
+};
+
+class DevicePool {
+ public:
+  DevicePool(uint64_t min_buf, uint64_t min_alloc) : min_buf_(min_buf), min_alloc_(min_alloc) {}
+  ~DevicePool() {
+    for (void* p : allocations_) (void)hipFree(p);
+  }
+
+  // MemoryPool.roundUpToTheNextPowerOf2 (:137-151)
+  uint64_t size_class(uint64_t n) const {
+    if (n < min_buf_) return min_buf_;
+    uint64_t c = 1;
+    while (c < n) c <<= 1;
+    return c;
+  }
+
+  // MemoryPool.get (:153-162) + AllocatorStack.get (:52-82): LIFO reuse, slab-allocate classes
+  // below minAllocationSize in one registration (preallocate :89-114).
+  PoolBuf get(uint64_t n) {
+    uint64_t cls = size_class(n ? n : 1);
+    std::lock_guard<std::mutex> lk(mu_);
+    auto& st = stacks_[cls];
+    st.requests++;
+    if (st.free.empty()) {
+      if (cls < min_alloc_) {
+        uint64_t count = min_alloc_ / cls;
+        uint8_t* p = alloc(count * cls);
+        for (uint64_t i = 0; i < count; ++i) st.free.push_back(PoolBuf{p + i * cls, cls});
+        st.preallocs++;
+      } else {
+        st.free.push_back(PoolBuf{alloc(cls), cls});
+      }
+      st.allocs++;
+    }
+    PoolBuf b = st.free.back();
+    st.free.pop_back();
+    return b;
+  }
+
+  // MemoryPool.put (:164-168)
+  void put(const PoolBuf& b) {
+    if (!b.ptr) return;
+    std::lock_guard<std::mutex> lk(mu_);
+    stacks_[b.cap].free.push_back(b);
+  }
+
+ private:
+  uint8_t* alloc(uint64_t bytes) {
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) raise(SUX_ENOMEM, "hipMalloc(" + std::to_string(bytes) + ") failed");
+    allocations_.push_back(p);
+    return static_cast<uint8_t*>(p);
+  }
+  struct Stack {
+    std::vector<PoolBuf> free;
+    uint64_t requests = 0, allocs = 0, preallocs = 0;
+  };
+  uint64_t min_buf_, min_alloc_;
+  std::mutex mu_;
+  std::map<uint64_t, Stack> stacks_;
+  std::vector<void*> allocations_;
+};
+
+// per-map directory slot: the analog of the 300-byte driver descriptor (DriverMetadata,
+// UcxWorkerWrapper.scala:27-65) plus the index file it points at
+struct MapSlot {
+  bool present = false;
+  int32_t owner = -1;
+  PoolBuf data;
+  uint64_t bytes = 0;
+  std::vector<int64_t> index;  // R+1 cumulative offsets (the index file, native order)
+  uint64_t recv_off = 0;       // after exchange: offset of this map's owned-range blocks in recv
+};
+
+struct Shuffle {
+  int32_t id = 0, num_maps = 0, R = 0, rec_size = 0;
+  std::vector<MapSlot> maps;
+  std::vector<uint8_t> directory;  // num_maps * metadata_block_size bytes (big-endian fields)
+  bool exchanged = false;
+  PoolBuf recv;
+  uint64_t recv_bytes = 0;
+};
+
+int32_t owner_lo(int32_t h, int32_t R, int32_t G) { return (int32_t)(((int64_t)h * R) / G); }
+}  // namespace
+
+struct sux_node {
+  sux_conf conf{};
+  bool is_driver = false;
+  ncclComm_t comm = nullptr;
+  std::unique_ptr<DevicePool> pool;
+  sux::Timer timer;
+  std::mutex mu;
+  std::map<int32_t, std::unique_ptr<Shuffle>> shuffles;
+
+  void bind() { hip_check(hipSetDevice(conf.device), "hipSetDevice"); }
+
+  // NULL = the HIP null stream (torch's default stream).  Per-task-thread streams, the analog
+  // of UcxNode.getThreadLocalWorker (UcxNode.java:147-176), are passed in by the caller
+  // (e.g. hipStreamPerThread from a JNI task thread).
+  hipStream_t stream(void* s) { return static_cast<hipStream_t>(s); }
+
+  Shuffle& shuffle(int32_t id) {
+    auto it = shuffles.find(id);
+    require(it != shuffles.end(), SUX_ENOENT, "unknown shuffle " + std::to_string(id));
+    return *it->second;
+  }
+};
+
+struct sux_partitioner {
+  sux_node* node = nullptr;
+  sux_partitioner_desc desc{};
+  sux::PartDev pd{};
+  void* d_bounds = nullptr;
+  void* d_lut = nullptr;
+};
+
+struct sux_buffer {
+  sux_node* node = nullptr;
+  PoolBuf buf;
+  PoolBuf aux;  // copy descriptors
+  uint64_t size = 0;
+  std::atomic<int32_t> refs{1};
+};
+
+// ============================================================================================
+// helpers
+// ============================================================================================
+namespace {
+void check_record_size(uint32_t rs) {
+  require(rs >= 4 && rs <= (uint32_t)sux::kMaxRecordSize && rs % 4 == 0, SUX_EINVAL,
+          "record_size must be a multiple of 4 in [4, 4096], got " + std::to_string(rs));
+}
+
+void check_key_fits(const sux_partitioner* p, uint32_t rs) {
+  require(p->desc.key_offset >= 0 && (uint64_t)p->desc.key_offset + p->desc.key_len <= rs,
+          SUX_EINVAL, "key [" + std::to_string(p->desc.key_offset) + ", +" +
+                          std::to_string(p->desc.key_len) + ") does not fit a " +
+                          std::to_string(rs) + "-byte record");
+}
+
+void store_be64(uint8_t* p, uint64_t v) {
+  for (int k = 0; k < 8; ++k) p[k] = (uint8_t)(v >> (56 - 8 * k));
+}
+void store_be32(uint8_t* p, uint32_t v) {
+  for (int k = 0; k < 4; ++k) p[k] = (uint8_t)(v >> (24 - 8 * k));
+}
+
+// Descriptor of one committed map, written into its directory slot (big-endian like the
+// reference's putLong/putInt, CommonUcxShuffleBlockResolver.scala:80-87):
+// |u64 index dev addr|u64 data dev addr|i32 owner rank|i32 R|u64 data bytes| = 32 bytes
+constexpr uint64_t kSlotBytes = 32;
+
+void publish_slot(sux_node* n, Shuffle& sh, int32_t m, uint64_t index_addr) {
+  MapSlot& s = sh.maps[m];
+  uint64_t blk = n->conf.metadata_block_size;
+  require(kSlotBytes <= blk, SUX_ERANGE,
+          "Metadata block size " + std::to_string(kSlotBytes) + " is greater then configured (" +
+              std::to_string(blk) + ")");
+  uint8_t* d = sh.directory.data() + (uint64_t)m * blk;
+  store_be64(d, index_addr);
+  store_be64(d + 8, (uint64_t)(uintptr_t)s.data.ptr);
+  store_be32(d + 16, (uint32_t)s.owner);
+  store_be32(d + 20, (uint32_t)sh.R);
+  store_be64(d + 24, s.bytes);
+}
+
+struct Group {
+  sux::MapGroup g{};
+  sux::Workspace ws{};
+};
+
+Group make_group(const sux_partitioner* part, const void* recs, uint32_t rs, uint64_t rpm,
+                 uint64_t n) {
+  check_record_size(rs);
+  check_key_fits(part, rs);
+  require(rpm > 0, SUX_EINVAL, "records_per_map must be > 0");
+  uint64_t maps = (n + rpm - 1) / rpm;
+  require(maps <= 0xFFFFFFFFull, SUX_EINVAL, "too many maps in one group");
+  require(n < (1ull << 32), SUX_ERANGE, "a launch group holds < 2^32 records");
+  require(((uintptr_t)recs & 3) == 0, SUX_EINVAL, "records must be 4-byte aligned");
+  Group G;
+  uint32_t R = (uint32_t)part->desc.num_partitions;
+  uint32_t tile = sux::choose_tile_recs(R, rs, rpm);
+  G.g.recs = static_cast<const uint8_t*>(recs);
+  G.g.records_per_map = rpm;
+  G.g.num_records = n;
+  G.g.num_maps = (uint32_t)maps;
+  G.g.rec_size = rs;
+  G.g.tile_recs = tile;
+  G.g.tiles_per_map = (uint32_t)((rpm + tile - 1) / tile);
+  G.ws = sux::workspace_layout(R, rs, rpm, n, tile, true);
+  return G;
+}
+
+void run_group(sux_node* node, const sux_partitioner* part, const Group& G, int32_t world,
+               void* d_out, int64_t* d_index, uint8_t* d_index_be, uint16_t* d_pids,
+               uint64_t* d_peer_bytes, void* d_ws, uint64_t ws_bytes, hipStream_t s) {
+  require(d_ws || G.ws.total == 0, SUX_EINVAL, "workspace is NULL");
+  require(ws_bytes >= G.ws.total, SUX_EINVAL,
+          "workspace too small: need " + std::to_string(G.ws.total) + " bytes");
+  require(d_out && d_index, SUX_EINVAL, "output or index pointer is NULL");
+  require(((uintptr_t)d_out & 3) == 0 && ((uintptr_t)d_index & 7) == 0 &&
+              ((uintptr_t)d_index_be & 7) == 0 && ((uintptr_t)d_ws & 255) == 0,
+          SUX_EINVAL, "output (4 B), index (8 B) and workspace (256 B) must be aligned");
+  if (G.g.num_records == 0) return;
+  sux::LayoutDesc lay{world, G.g.rec_size};
+  hip_check(sux::launch_partition_group(part->pd, G.g, lay, static_cast<uint8_t*>(d_out), d_index,
+                                        d_index_be, d_pids, static_cast<uint8_t*>(d_ws), G.ws,
+                                        d_peer_bytes, &node->timer, s),
+            "partition launch");
+}
+}  // namespace
+
+// ============================================================================================
+// C-ABI
+// ============================================================================================
+extern "C" {
+
+void sux_conf_init(sux_conf* c) {
+  if (!c) return;
+  std::memset(c, 0, sizeof *c);
+  c->world_size = 1;
+  c->min_buffer_size = 1024;                 // spark.shuffle.ucx.memory.minBufferSize
+  c->min_allocation_size = 4ull << 20;       // spark.shuffle.ucx.memory.minAllocationSize
+  c->metadata_block_size = 2 * 150;          // 2 * spark.shuffle.ucx.rkeySize
+}
+
+int sux_abi_version(void) { return SUX_ABI_VERSION; }
+
+int sux_last_error(char* buf, size_t len) {
+  if (buf && len) {
+    size_t k = std::min(len - 1, g_err.size());
+    std::memcpy(buf, g_err.data(), k);
+    buf[k] = 0;
+  }
+  return (int)g_err.size();
+}
+
+int sux_comm_unique_id(uint8_t out[128]) {
+  return guard([&] {
+    require(out != nullptr, SUX_EINVAL, "out is NULL");
+    ncclUniqueId id;
+    nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
+    static_assert(sizeof(id) == 128, "ncclUniqueId is 128 bytes");
+    std::memcpy(out, &id, 128);
+  });
+}
+
+int sux_node_create(const sux_conf* conf, int is_driver, sux_node** out) {
+  return guard([&] {
+    require(conf && out, SUX_EINVAL, "conf/out is NULL");
+    require(conf->world_size >= 1 && conf->rank >= 0 && conf->rank < conf->world_size, SUX_EINVAL,
+            "rank/world_size out of range");
+    require(conf->min_buffer_size > 0 && conf->min_allocation_size > 0, SUX_EINVAL,
+            "pool sizes must be positive");
+    int ndev = 0;
+    hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+    require(conf->device >= 0 && conf->device < ndev, SUX_EINVAL,
+            "device " + std::to_string(conf->device) + " not present (" + std::to_string(ndev) +
+                " devices)");
+    auto n = std::make_unique<sux_node>();
+    n->conf = *conf;
+    n->is_driver = is_driver != 0;
+    n->bind();
+    n->pool = std::make_unique<DevicePool>(conf->min_buffer_size, conf->min_allocation_size);
+    if (conf->world_size > 1) {
+      ncclUniqueId id;
+      std::memcpy(&id, conf->comm_id, 128);
+      nccl_check(ncclCommInitRank(&n->comm, conf->world_size, id, conf->rank), "ncclCommInitRank");
+    }
+    *out = n.release();
+  });
+}
+
+int sux_node_destroy(sux_node* node) {
+  return guard([&] {
+    if (!node) return;
+    node->bind();
+    (void)hipDeviceSynchronize();
+    for (auto& kv : node->shuffles) {
+      for (auto& m : kv.second->maps) node->pool->put(m.data);
+      node->pool->put(kv.second->recv);
+    }
+    node->shuffles.clear();
+    if (node->comm) (void)ncclCommDestroy(node->comm);
+    delete node;
+  });
+}
+
+// ---- partitioner ----------------------------------------------------------------------------
+int sux_partitioner_create(sux_node* node, const sux_partitioner_desc* d, sux_partitioner** out) {
+  return guard([&] {
+    require(node && d && out, SUX_EINVAL, "NULL argument");
+    const int R = d->num_partitions;
+    require(R >= 1 && R <= sux::kMaxPartitions, SUX_EINVAL,
+            "num_partitions must be in [1, 32768], got " + std::to_string(R));
+    require(d->key_offset >= 0, SUX_EINVAL, "key_offset < 0");
+    switch (d->kind) {
+      case SUX_PART_RANGE_BYTES:
+        require(d->key_len >= 1 && d->key_len <= 16, SUX_EINVAL, "range key_len must be 1..16");
+        require(R == 1 || d->range_bounds, SUX_EINVAL, "range partitioner needs R-1 bounds");
+        break;
+      case SUX_PART_MURMUR3_LONG:
+      case SUX_PART_HASH_LONG:
+        require(d->key_len == 8, SUX_EINVAL, "long key needs key_len 8");
+        break;
+      case SUX_PART_MURMUR3_INT:
+      case SUX_PART_HASH_INT:
+        require(d->key_len == 4, SUX_EINVAL, "int key needs key_len 4");
+        break;
+      case SUX_PART_MURMUR3_BYTES:
+        require(d->key_len >= 1 && d->key_len <= 4096, SUX_EINVAL, "binary key_len must be >= 1");
+        break;
+      default:
+        raise(SUX_EINVAL, "unknown partitioner kind " + std::to_string(d->kind));
+    }
+    node->bind();
+    auto p = std::make_unique<sux_partitioner>();
+    p->node = node;
+    p->desc = *d;
+    p->desc.range_bounds = nullptr;
+    p->pd.kind = d->kind;
+    p->pd.R = R;
+    p->pd.key_offset = d->key_offset;
+    p->pd.key_len = d->key_len;
+    p->pd.seed = d->seed;
+    p->pd.ascending = d->ascending;
+    if (d->kind == SUX_PART_RANGE_BYTES && R > 1) {
+      const int L = d->key_len;
+      // strictly rising bounds (RangePartitioner.determineBounds guarantees it)
+      for (int i = 1; i + 1 < R; ++i)
+        require(std::memcmp(d->range_bounds + (size_t)(i - 1) * L, d->range_bounds + (size_t)i * L,
+                            (size_t)L) < 0,
+                SUX_EINVAL, "range bounds must be strictly increasing (bound " +
+                                std::to_string(i) + ")");
+      std::vector<uint64_t> packed(2 * (size_t)(R - 1));
+      for (int i = 0; i + 1 < R; ++i) {
+        uint8_t k[16] = {0};
+        std::memcpy(k, d->range_bounds + (size_t)i * L, (size_t)L);
+        uint64_t hi = 0, lo = 0;
+        for (int b = 0; b < 8; ++b) hi = (hi << 8) | k[b];
+        for (int b = 8; b < 16; ++b) lo = (lo << 8) | k[b];
+        packed[2 * i] = hi;
+        packed[2 * i + 1] = lo;
+      }
+      // top-12-bit lookup: candidate answer interval per key prefix
+      const int bits = 12;
+      std::vector<uint32_t> lut((size_t)1 << bits);
+      auto count_less = [&](uint64_t hi, uint64_t lo) {  // #{bounds < (hi, lo)}
+        int a = 0, b = R - 1;
+        while (a < b) {
+          int mid = (a + b) / 2;
+          bool less = packed[2 * mid] < hi || (packed[2 * mid] == hi && packed[2 * mid + 1] < lo);
+          if (less) a = mid + 1; else b = mid;
+        }
+        return a;
+      };
+      for (uint64_t v = 0; v < lut.size(); ++v) {
+        uint64_t kmin = v << (64 - bits), kmax = kmin | (~0ull >> bits);
+        uint32_t a = (uint32_t)count_less(kmin, 0), b = (uint32_t)count_less(kmax, ~0ull);
+        lut[v] = a | (b << 16);
+      }
+      hip_check(hipMalloc(&p->d_bounds, packed.size() * 8), "hipMalloc(bounds)");
+      hip_check(hipMemcpy(p->d_bounds, packed.data(), packed.size() * 8, hipMemcpyHostToDevice),
+                "hipMemcpy(bounds)");
+      hip_check(hipMalloc(&p->d_lut, lut.size() * 4), "hipMalloc(lut)");
+      hip_check(hipMemcpy(p->d_lut, lut.data(), lut.size() * 4, hipMemcpyHostToDevice),
+                "hipMemcpy(lut)");
+      p->pd.bounds = static_cast<const uint64_t*>(p->d_bounds);
+      p->pd.lut = static_cast<const uint32_t*>(p->d_lut);
+      p->pd.lut_bits = bits;
+    }
+    *out = p.release();
+  });
+}
+
+int sux_partitioner_destroy(sux_partitioner* p) {
+  return guard([&] {
+    if (!p) return;
+    p->node->bind();
+    if (p->d_bounds) (void)hipFree(p->d_bounds);
+    if (p->d_lut) (void)hipFree(p->d_lut);
+    delete p;
+  });
+}
+
+// ---- stateless map side ----------------------------------------------------------------------
+int sux_partition_workspace_size(const sux_partitioner* part, uint32_t rs, uint64_t rpm,
+                                 uint64_t n, uint64_t* bytes) {
+  return guard([&] {
+    require(part && bytes, SUX_EINVAL, "NULL argument");
+    Group G = make_group(part, nullptr, rs, rpm, n);
+    *bytes = G.ws.total;
+  });
+}
+
+int sux_partition_maps(sux_node* node, const sux_partitioner* part, const void* d_records,
+                       uint32_t rs, uint64_t rpm, uint64_t n, void* d_out, int64_t* d_index,
+                       uint8_t* d_index_be, uint16_t* d_pids, void* d_ws, uint64_t ws_bytes,
+                       void* stream) {
+  return guard([&] {
+    require(node && part, SUX_EINVAL, "NULL node/partitioner");
+    require(d_records || n == 0, SUX_EINVAL, "records pointer is NULL");
+    node->bind();
+    Group G = make_group(part, d_records, rs, rpm, n);
+    run_group(node, part, G, 1, d_out, d_index, d_index_be, d_pids, nullptr, d_ws, ws_bytes,
+              node->stream(stream));
+  });
+}
+
+int sux_partition_maps_peer_major(sux_node* node, const sux_partitioner* part,
+                                  const void* d_records, uint32_t rs, uint64_t rpm, uint64_t n,
+                                  int32_t world, void* d_send, int64_t* d_index,
+                                  uint8_t* d_index_be, uint64_t* d_peer_bytes, void* d_ws,
+                                  uint64_t ws_bytes, void* stream) {
+  return guard([&] {
+    require(node && part, SUX_EINVAL, "NULL node/partitioner");
+    require(world >= 1 && world <= part->desc.num_partitions, SUX_EINVAL,
+            "world must be in [1, R]");
+    require(d_records || n == 0, SUX_EINVAL, "records pointer is NULL");
+    node->bind();
+    Group G = make_group(part, d_records, rs, rpm, n);
+    run_group(node, part, G, world, d_send, d_index, d_index_be, nullptr, d_peer_bytes, d_ws,
+              ws_bytes, node->stream(stream));
+  });
+}
+
+int sux_partition_ids(sux_node* node, const sux_partitioner* part, const void* d_records,
+                      uint32_t rs, uint64_t n, uint16_t* d_pids, void* stream) {
+  return guard([&] {
+    require(node && part && (d_records || n == 0) && (d_pids || n == 0), SUX_EINVAL,
+            "NULL argument");
+    check_record_size(rs);
+    check_key_fits(part, rs);
+    node->bind();
+    hip_check(sux::launch_partition_ids(part->pd, static_cast<const uint8_t*>(d_records), rs, n,
+                                        d_pids, node->stream(stream)),
+              "pid launch");
+  });
+}
+
+// ---- exchange plan (host arithmetic) -----------------------------------------------------------
+int sux_plan_group(int32_t W, int32_t rank, int32_t M, int32_t R, const int64_t* gi,
+                   uint64_t* sendcounts, uint64_t* sdispls, uint64_t* recvcounts,
+                   uint64_t* rdispls) {
+  return guard([&] {
+    require(W >= 1 && rank >= 0 && rank < W && M >= 0 && R >= W, SUX_EINVAL, "bad plan shape");
+    require(gi || M == 0, SUX_EINVAL, "gathered index is NULL");
+    const int64_t stride = (int64_t)R + 1;
+    auto idx = [&](int g, int m, int p) { return gi[((int64_t)g * M + m) * stride + p]; };
+    uint64_t sacc = 0, racc = 0;
+    for (int h = 0; h < W; ++h) {
+      int lo = owner_lo(h, R, W), hi = owner_lo(h + 1, R, W);
+      uint64_t s = 0;
+      for (int m = 0; m < M; ++m) s += (uint64_t)(idx(rank, m, hi) - idx(rank, m, lo));
+      if (sendcounts) sendcounts[h] = s;
+      if (sdispls) sdispls[h] = sacc;
+      sacc += s;
+    }
+    int lo = owner_lo(rank, R, W), hi = owner_lo(rank + 1, R, W);
+    for (int g = 0; g < W; ++g) {
+      uint64_t r = 0;
+      for (int m = 0; m < M; ++m) r += (uint64_t)(idx(g, m, hi) - idx(g, m, lo));
+      if (recvcounts) recvcounts[g] = r;
+      if (rdispls) rdispls[g] = racc;
+      racc += r;
+    }
+  });
+}
+
+int64_t sux_plan_block_offset(int32_t W, int32_t rank, int32_t M, int32_t R, const int64_t* gi,
+                              int32_t g, int32_t m, int32_t p) {
+  if (!gi || W < 1 || rank < 0 || rank >= W || g < 0 || g >= W || m < 0 || m >= M || R < W)
+    return -1;
+  int lo = owner_lo(rank, R, W), hi = owner_lo(rank + 1, R, W);
+  if (p < lo || p >= hi) return -1;
+  const int64_t stride = (int64_t)R + 1;
+  auto idx = [&](int gg, int mm, int pp) { return gi[((int64_t)gg * M + mm) * stride + pp]; };
+  int64_t off = 0;
+  for (int gg = 0; gg < g; ++gg)
+    for (int mm = 0; mm < M; ++mm) off += idx(gg, mm, hi) - idx(gg, mm, lo);
+  for (int mm = 0; mm < m; ++mm) off += idx(g, mm, hi) - idx(g, mm, lo);
+  return off + idx(g, m, p) - idx(g, m, lo);
+}
+
+int sux_exchange_group(sux_node* node, const void* d_send, const int64_t* d_index, int32_t M,
+                       int32_t R, int64_t* d_gathered, void* d_recv, uint64_t recv_capacity,
+                       uint64_t* recv_bytes, void* stream) {
+  return guard([&] {
+    require(node && d_index && d_gathered, SUX_EINVAL, "NULL argument");
+    const int W = node->conf.world_size, rank = node->conf.rank;
+    require(R >= W && M >= 1, SUX_EINVAL, "need R >= world and >= 1 map");
+    node->bind();
+    hipStream_t s = node->stream(stream);
+    const size_t per_rank = (size_t)M * (R + 1);
+    std::vector<int64_t> host(per_rank * W);
+    if (W == 1) {
+      hip_check(hipMemcpyAsync(d_gathered, d_index, per_rank * 8, hipMemcpyDeviceToDevice, s),
+                "copy index");
+    } else {
+      nccl_check(ncclAllGather(d_index, d_gathered, per_rank, ncclInt64, node->comm, s),
+                 "ncclAllGather(index)");
+    }
+    hip_check(hipMemcpyAsync(host.data(), d_gathered, host.size() * 8, hipMemcpyDeviceToHost, s),
+              "D2H gathered index");
+    hip_check(hipStreamSynchronize(s), "sync gathered index");
+    std::vector<uint64_t> sc(W), sd(W), rc(W), rd(W);
+    int rc_plan = sux_plan_group(W, rank, M, R, host.data(), sc.data(), sd.data(), rc.data(),
+                                 rd.data());
+    require(rc_plan == SUX_OK, rc_plan, g_err);
+    uint64_t total = rd[W - 1] + rc[W - 1];
+    require(total <= recv_capacity, SUX_ERANGE,
+            "receive buffer too small: need " + std::to_string(total) + " bytes");
+    if (recv_bytes)
+      for (int g = 0; g < W; ++g) recv_bytes[g] = rc[g];
+    if (W == 1) {
+      if (total)
+        hip_check(hipMemcpyAsync(d_recv, d_send, total, hipMemcpyDeviceToDevice, s), "self copy");
+      return;
+    }
+    require(d_send && d_recv, SUX_EINVAL, "send/recv buffer is NULL");
+    std::vector<size_t> a(W), b(W), c(W), d(W);
+    for (int h = 0; h < W; ++h) {
+      a[h] = sc[h];
+      b[h] = sd[h];
+      c[h] = rc[h];
+      d[h] = rd[h];
+    }
+    nccl_check(ncclAllToAllv(d_send, a.data(), b.data(), d_recv, c.data(), d.data(), ncclUint8,
+                             node->comm, s),
+               "ncclAllToAllv");
+  });
+}
+
+// ---- shuffle lifecycle ---------------------------------------------------------------------
+int sux_register_shuffle(sux_node* node, int32_t shuffle_id, int32_t num_maps, int32_t R,
+                         int32_t rec_size, sux_handle_desc* out) {
+  return guard([&] {
+    require(node, SUX_EINVAL, "NULL node");
+    require(num_maps >= 0 && R >= 1 && R <= sux::kMaxPartitions, SUX_EINVAL,
+            "bad num_maps/num_partitions");
+    check_record_size((uint32_t)rec_size);
+    std::lock_guard<std::mutex> lk(node->mu);
+    require(!node->shuffles.count(shuffle_id), SUX_ESTATE,
+            "shuffle " + std::to_string(shuffle_id) + " already registered");
+    auto sh = std::make_unique<Shuffle>();
+    sh->id = shuffle_id;
+    sh->num_maps = num_maps;
+    sh->R = R;
+    sh->rec_size = rec_size;
+    sh->maps.resize((size_t)num_maps);
+    sh->directory.assign((size_t)num_maps * node->conf.metadata_block_size, 0);
+    if (out) {
+      out->shuffle_id = shuffle_id;
+      out->num_maps = num_maps;
+      out->num_partitions = R;
+      out->record_size = rec_size;
+      out->directory_bytes = sh->directory.size();
+    }
+    node->shuffles[shuffle_id] = std::move(sh);
+  });
+}
+
+int sux_unregister_shuffle(sux_node* node, int32_t shuffle_id) {
+  return guard([&] {
+    require(node, SUX_EINVAL, "NULL node");
+    node->bind();
+    std::lock_guard<std::mutex> lk(node->mu);
+    auto it = node->shuffles.find(shuffle_id);
+    require(it != node->shuffles.end(), SUX_ENOENT, "unknown shuffle " + std::to_string(shuffle_id));
+    hip_check(hipDeviceSynchronize(), "sync before unregister");
+    for (auto& m : it->second->maps) node->pool->put(m.data);
+    node->pool->put(it->second->recv);
+    node->shuffles.erase(it);
+  });
+}
+
+int sux_write_map_output(sux_node* node, int32_t shuffle_id, int32_t map_index,
+                         const sux_partitioner* part, const void* d_records, uint64_t n,
+                         void* stream) {
+  return guard([&] {
+    require(node && part, SUX_EINVAL, "NULL node/partitioner");
+    node->bind();
+    hipStream_t s = node->stream(stream);
+    std::unique_lock<std::mutex> lk(node->mu);
+    Shuffle& sh = node->shuffle(shuffle_id);
+    require(map_index >= 0 && map_index < sh.num_maps, SUX_EINVAL,
+            "map index " + std::to_string(map_index) + " out of [0, " +
+                std::to_string(sh.num_maps) + ")");
+    require(part->desc.num_partitions == sh.R, SUX_EINVAL,
+            "partitioner has " + std::to_string(part->desc.num_partitions) +
+                " partitions, shuffle has " + std::to_string(sh.R));
+    const int R = sh.R;
+    const uint32_t rs = (uint32_t)sh.rec_size;
+    // UcxShuffleBlockResolver.scala:42-45: an empty data file publishes nothing
+    if (n == 0) return;
+    // IndexShuffleBlockResolver [ext]: another attempt already committed -> keep the first
+    if (sh.maps[map_index].present) return;
+    lk.unlock();
+    Group G = make_group(part, d_records, rs, n, n);
+    PoolBuf data = node->pool->get(n * rs);
+    PoolBuf ws = node->pool->get(G.ws.total);
+    PoolBuf idx = node->pool->get(8 * (uint64_t)(R + 1));
+    std::vector<int64_t> host((size_t)R + 1);
+    try {
+      run_group(node, part, G, 1, data.ptr, reinterpret_cast<int64_t*>(idx.ptr), nullptr, nullptr,
+                nullptr, ws.ptr, ws.cap, s);
+      hip_check(hipMemcpyAsync(host.data(), idx.ptr, host.size() * 8, hipMemcpyDeviceToHost, s),
+                "D2H index");
+      // CommonUcxShuffleBlockResolver.scala:101-103: block until the map output is published
+      hip_check(hipStreamSynchronize(s), "sync map output");
+    } catch (...) {
+      node->pool->put(data);
+      node->pool->put(ws);
+      node->pool->put(idx);
+      throw;
+    }
+    node->pool->put(ws);
+    node->pool->put(idx);
+    lk.lock();
+    MapSlot& slot = sh.maps[map_index];
+    if (slot.present) {  // lost a race with another attempt
+      node->pool->put(data);
+      return;
+    }
+    slot.present = true;
+    slot.owner = node->conf.rank;
+    slot.data = data;
+    slot.bytes = n * rs;
+    slot.index = std::move(host);
+    sh.exchanged = false;
+    publish_slot(node, sh, map_index, 0);
+  });
+}
+
+int sux_commit_map_output(sux_node* node, int32_t shuffle_id, int32_t map_index,
+                          const void* d_data, uint64_t bytes, const int64_t* lengths,
+                          void* stream) {
+  return guard([&] {
+    require(node && lengths, SUX_EINVAL, "NULL argument");
+    node->bind();
+    hipStream_t s = node->stream(stream);
+    std::lock_guard<std::mutex> lk(node->mu);
+    Shuffle& sh = node->shuffle(shuffle_id);
+    require(map_index >= 0 && map_index < sh.num_maps, SUX_EINVAL, "map index out of range");
+    std::vector<int64_t> index((size_t)sh.R + 1);
+    int64_t acc = 0;
+    for (int r = 0; r < sh.R; ++r) {
+      require(lengths[r] >= 0, SUX_EINVAL, "negative partition length");
+      index[r] = acc;
+      acc += lengths[r];
+    }
+    index[sh.R] = acc;
+    require((uint64_t)acc == bytes, SUX_EINVAL,
+            "sum(lengths) = " + std::to_string(acc) + " != data bytes " + std::to_string(bytes));
+    if (bytes == 0 || sh.maps[map_index].present) return;
+    require(d_data, SUX_EINVAL, "data pointer is NULL");
+    PoolBuf data = node->pool->get(bytes);
+    hip_check(hipMemcpyAsync(data.ptr, d_data, bytes, hipMemcpyDeviceToDevice, s), "adopt data");
+    hip_check(hipStreamSynchronize(s), "sync commit");
+    MapSlot& slot = sh.maps[map_index];
+    slot.present = true;
+    slot.owner = node->conf.rank;
+    slot.data = data;
+    slot.bytes = bytes;
+    slot.index = std::move(index);
+    sh.exchanged = false;
+    publish_slot(node, sh, map_index, 0);
+  });
+}
+
+int sux_map_output_index(sux_node* node, int32_t shuffle_id, int32_t map_index, uint8_t* out,
+                         uint64_t out_len) {
+  return guard([&] {
+    require(node && out, SUX_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(node->mu);
+    Shuffle& sh = node->shuffle(shuffle_id);
+    require(map_index >= 0 && map_index < sh.num_maps, SUX_EINVAL, "map index out of range");
+    const MapSlot& slot = sh.maps[map_index];
+    require(slot.present, SUX_ENOENT, "map " + std::to_string(map_index) + " has no output");
+    require(out_len >= 8 * (uint64_t)(sh.R + 1), SUX_EINVAL, "index buffer too small");
+    for (int r = 0; r <= sh.R; ++r) store_be64(out + 8 * (size_t)r, (uint64_t)slot.index[r]);
+  });
+}
+
+int sux_owned_partitions(sux_node* node, int32_t shuffle_id, int32_t rank, int32_t* start,
+                         int32_t* end) {
+  return guard([&] {
+    require(node && start && end, SUX_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(node->mu);
+    Shuffle& sh = node->shuffle(shuffle_id);
+    const int W = node->conf.world_size;
+    require(rank >= 0 && rank < W, SUX_EINVAL, "rank out of range");
+    *start = owner_lo(rank, sh.R, W);
+    *end = owner_lo(rank + 1, sh.R, W);
+  });
+}
+
+// Shuffle-level exchange: directory all-reduce, then grouped ncclSend/ncclRecv of every map's
+// owned-range byte slice (no repacking: the map output already is contiguous per partition).
+int sux_exchange(sux_node* node, int32_t shuffle_id, void* stream) {
+  return guard([&] {
+    require(node, SUX_EINVAL, "NULL node");
+    node->bind();
+    hipStream_t s = node->stream(stream);
+    std::lock_guard<std::mutex> lk(node->mu);
+    Shuffle& sh = node->shuffle(shuffle_id);
+    const int W = node->conf.world_size, me = node->conf.rank, R = sh.R, M = sh.num_maps;
+    if (W == 1) {
+      sh.exchanged = true;
+      return;
+    }
+    require(R >= W, SUX_EINVAL, "need at least one partition per rank");
+    // 1. directory: rows [owner+1, index[0..R]] of the maps this rank owns; sum-all-reduce
+    const size_t row = (size_t)R + 2;
+    std::vector<int64_t> dir(row * (size_t)M, 0);
+    for (int m = 0; m < M; ++m) {
+      const MapSlot& sl = sh.maps[m];
+      if (!sl.present || sl.owner != me) continue;
+      dir[row * m] = me + 1;
+      for (int r = 0; r <= R; ++r) dir[row * m + 1 + r] = sl.index[r];
+    }
+    if (M > 0) {
+      PoolBuf tmp = node->pool->get(dir.size() * 8);
+      hip_check(hipMemcpyAsync(tmp.ptr, dir.data(), dir.size() * 8, hipMemcpyHostToDevice, s),
+                "H2D directory");
+      nccl_check(ncclAllReduce(tmp.ptr, tmp.ptr, dir.size(), ncclInt64, ncclSum, node->comm, s),
+                 "ncclAllReduce(directory)");
+      hip_check(hipMemcpyAsync(dir.data(), tmp.ptr, dir.size() * 8, hipMemcpyDeviceToHost, s),
+                "D2H directory");
+      hip_check(hipStreamSynchronize(s), "sync directory");
+      node->pool->put(tmp);
+    }
+    // 2. adopt remote rows, size the receive buffer
+    const int lo = owner_lo(me, R, W), hi = owner_lo(me + 1, R, W);
+    uint64_t total = 0;
+    for (int m = 0; m < M; ++m) {
+      int64_t owner = dir[row * m] - 1;
+      require(owner >= -1 && owner < W, SUX_ESTATE,
+              "map " + std::to_string(m) + " committed by more than one rank");
+      if (owner < 0 || owner == me) continue;
+      MapSlot& sl = sh.maps[m];
+      sl.present = true;
+      sl.owner = (int32_t)owner;
+      sl.index.assign(dir.begin() + row * m + 1, dir.begin() + row * (m + 1));
+      sl.recv_off = total;
+      total += (uint64_t)(sl.index[hi] - sl.index[lo]);
+    }
+    node->pool->put(sh.recv);
+    sh.recv = total ? node->pool->get(total) : PoolBuf{};
+    sh.recv_bytes = total;
+    // 3. data: per map-chunk groups, identical chunk boundaries on every rank
+    const int kChunk = 64;
+    for (int m0 = 0; m0 < M; m0 += kChunk) {
+      nccl_check(ncclGroupStart(), "ncclGroupStart");
+      for (int m = m0; m < std::min(M, m0 + kChunk); ++m) {
+        const MapSlot& sl = sh.maps[m];
+        if (!sl.present) continue;
+        if (sl.owner == me) {
+          for (int h = 0; h < W; ++h) {
+            if (h == me) continue;
+            int64_t a = sl.index[owner_lo(h, R, W)], b = sl.index[owner_lo(h + 1, R, W)];
+            if (b > a)
+              nccl_check(ncclSend(sl.data.ptr + a, (size_t)(b - a), ncclUint8, h, node->comm, s),
+                         "ncclSend");
+          }
+        } else {
+          int64_t bytes = sl.index[hi] - sl.index[lo];
+          if (bytes > 0)
+            nccl_check(ncclRecv(sh.recv.ptr + sl.recv_off, (size_t)bytes, ncclUint8, sl.owner,
+                                node->comm, s),
+                       "ncclRecv");
+        }
+      }
+      nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+    }
+    hip_check(hipStreamSynchronize(s), "sync exchange");
+    sh.exchanged = true;
+  });
+}
+
+// ---- fetch -----------------------------------------------------------------------------------
+namespace {
+// Resolve one block to (device address, size); throws SUX_ENOENT for a block not local here.
+void resolve(sux_node* node, Shuffle& sh, const sux_block_id& b, uint64_t* addr, int64_t* size) {
+  const int R = sh.R;
+  auto name = [&] {
+    return "shuffle_" + std::to_string(sh.id) + "_" + std::to_string(b.map_index) + "_" +
+           std::to_string(b.start_reduce) +
+           (b.end_reduce != b.start_reduce + 1 ? "_" + std::to_string(b.end_reduce) : "");
+  };
+  require(b.map_index >= 0 && b.map_index < sh.num_maps && b.start_reduce >= 0 &&
+              b.end_reduce > b.start_reduce && b.end_reduce <= R,
+          SUX_EINVAL, "malformed block " + name());
+  const MapSlot& sl = sh.maps[b.map_index];
+  require(sl.present, SUX_ENOENT, "Unknown block " + name() + ": map output not committed");
+  const int64_t a = sl.index[b.start_reduce], e = sl.index[b.end_reduce];
+  *size = e - a;
+  if (sl.owner == node->conf.rank) {
+    *addr = (uint64_t)(uintptr_t)(sl.data.ptr + a);
+    return;
+  }
+  const int W = node->conf.world_size, me = node->conf.rank;
+  const int lo = owner_lo(me, R, W), hi = owner_lo(me + 1, R, W);
+  require(sh.exchanged, SUX_ESTATE, "block " + name() + " is remote and the shuffle is not exchanged");
+  require(b.start_reduce >= lo && b.end_reduce <= hi, SUX_ENOENT,
+          "block " + name() + " is not owned by rank " + std::to_string(me));
+  *addr = (uint64_t)(uintptr_t)(sh.recv.ptr + sl.recv_off + (a - sl.index[lo]));
+}
+}  // namespace
+
+int sux_resolve_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* blocks, int32_t n,
+                       uint64_t* addrs, int64_t* sizes) {
+  return guard([&] {
+    require(node && (blocks || n == 0) && (addrs || n == 0) && (sizes || n == 0) && n >= 0,
+            SUX_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(node->mu);
+    Shuffle& sh = node->shuffle(shuffle_id);
+    for (int i = 0; i < n; ++i) resolve(node, sh, blocks[i], &addrs[i], &sizes[i]);
+  });
+}
+
+int sux_fetch_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* blocks, int32_t n,
+                     int64_t* sizes, sux_buffer** out, void* stream) {
+  return guard([&] {
+    require(node && out && (blocks || n == 0) && (sizes || n == 0) && n >= 0, SUX_EINVAL,
+            "NULL argument");
+    node->bind();
+    hipStream_t s = node->stream(stream);
+    std::vector<sux::CopyDesc> desc((size_t)n);
+    uint64_t total = 0;
+    {
+      std::lock_guard<std::mutex> lk(node->mu);
+      Shuffle& sh = node->shuffle(shuffle_id);
+      // phase 1 (UcxShuffleClient.submitFetchOffsets :50-92 / OnOffsetsFetchCallback :53-72):
+      // sizes from the index tables of the directory
+      for (int i = 0; i < n; ++i) {
+        uint64_t a;
+        resolve(node, sh, blocks[i], &a, &sizes[i]);
+        desc[i].src = reinterpret_cast<const uint8_t*>(a);
+        desc[i].bytes = (uint64_t)sizes[i];
+        total += (uint64_t)sizes[i];
+      }
+    }
+    auto buf = std::make_unique<sux_buffer>();
+    buf->node = node;
+    buf->size = total;
+    buf->refs = n > 0 ? n : 1;  // one reference per block slice (OnBlocksFetchCallback :35)
+    // OnOffsetsFetchCallback :75-76: one pooled buffer for the whole request
+    buf->buf = node->pool->get(total ? total : 1);
+    if (total) {
+      // phase 2 (:80-87): block i -> contiguous destination at a running offset
+      std::vector<uint32_t> first((size_t)n);
+      uint64_t pos = 0, chunks = 0;
+      const uint64_t kChunk = 64 * 1024;
+      for (int i = 0; i < n; ++i) {
+        desc[i].dst = buf->buf.ptr + pos;
+        pos += desc[i].bytes;
+        first[i] = (uint32_t)chunks;
+        chunks += desc[i].bytes ? (desc[i].bytes + kChunk - 1) / kChunk : 1;
+      }
+      require(chunks < (1ull << 31), SUX_ERANGE, "fetch request too large");
+      const uint64_t dbytes = desc.size() * sizeof(sux::CopyDesc), fbytes = first.size() * 4;
+      buf->aux = node->pool->get(dbytes + 256 + fbytes);
+      uint8_t* d_desc = buf->aux.ptr;
+      uint8_t* d_first = buf->aux.ptr + ((dbytes + 255) / 256) * 256;
+      hip_check(hipMemcpyAsync(d_desc, desc.data(), dbytes, hipMemcpyHostToDevice, s), "H2D desc");
+      hip_check(hipMemcpyAsync(d_first, first.data(), fbytes, hipMemcpyHostToDevice, s),
+                "H2D chunks");
+      hip_check(sux::launch_gather_copy(reinterpret_cast<const sux::CopyDesc*>(d_desc), (uint32_t)n,
+                                        (uint32_t)chunks, reinterpret_cast<const uint32_t*>(d_first),
+                                        &node->timer, s),
+                "gather copy");
+      // completion is delivered to the caller like OnBlocksFetchCallback.onSuccess: the blocks
+      // are in place when this call returns
+      hip_check(hipStreamSynchronize(s), "sync fetch");
+    }
+    *out = buf.release();
+  });
+}
+
+int sux_buffer_info(sux_buffer* b, void** ptr, uint64_t* size, uint64_t* cap) {
+  return guard([&] {
+    require(b, SUX_EINVAL, "NULL buffer");
+    if (ptr) *ptr = b->buf.ptr;
+    if (size) *size = b->size;
+    if (cap) *cap = b->buf.cap;
+  });
+}
+
+int sux_buffer_retain(sux_buffer* b, int32_t count) {
+  return guard([&] {
+    require(b && count > 0, SUX_EINVAL, "bad retain");
+    b->refs += count;
+  });
+}
+
+// NioManagedBuffer.release override (OnBlocksFetchCallback.java:45-53): the last release
+// returns the pooled buffer.
+int sux_buffer_release(sux_buffer* b) {
+  return guard([&] {
+    require(b, SUX_EINVAL, "NULL buffer");
+    int32_t left = --b->refs;
+    require(left >= 0, SUX_ESTATE, "buffer released more often than referenced");
+    if (left == 0) {
+      b->node->pool->put(b->buf);
+      b->node->pool->put(b->aux);
+      delete b;
+    }
+  });
+}
+
+// ---- measurement -----------------------------------------------------------------------------
+int sux_set_kernel_timing(sux_node* node, int enable) {
+  return guard([&] {
+    require(node, SUX_EINVAL, "NULL node");
+    std::lock_guard<std::mutex> lk(node->timer.mu);
+    node->timer.enabled = enable != 0;
+  });
+}
+
+int sux_kernel_times(sux_node* node, int64_t* launches, double* total_ms, int32_t nk) {
+  return guard([&] {
+    require(node && launches && total_ms && nk >= 0, SUX_EINVAL, "NULL argument");
+    node->bind();
+    std::lock_guard<std::mutex> lk(node->timer.mu);
+    for (int k = 0; k < nk; ++k) {
+      launches[k] = 0;
+      total_ms[k] = 0;
+    }
+    for (auto& r : node->timer.recs) {
+      hip_check(hipEventSynchronize(r.b), "hipEventSynchronize");
+      float ms = 0;
+      hip_check(hipEventElapsedTime(&ms, r.a, r.b), "hipEventElapsedTime");
+      if (r.slot < nk) {
+        launches[r.slot]++;
+        total_ms[r.slot] += ms;
+      }
+      node->timer.spare.push_back(r.a);
+      node->timer.spare.push_back(r.b);
+    }
+    node->timer.recs.clear();
+  });
+}
+
+// ---- generators --------------------------------------------------------------------------------
+int sux_generate(sux_node* node, int32_t kind, uint64_t seed, uint64_t first, uint64_t n,
+                 double zipf_s, uint64_t zipf_n, void* d_out, void* stream) {
+  return guard([&] {
+    require(node && (d_out || n == 0), SUX_EINVAL, "NULL argument");
+    require(kind == SUX_GEN_TERASORT || kind == SUX_GEN_SMALL || kind == SUX_GEN_ZIPF, SUX_EINVAL,
+            "unknown generator");
+    node->bind();
+    hipStream_t s = node->stream(stream);
+    void* zb = nullptr;
+    void* zt = nullptr;
+    int nb = 0;
+    if (kind == SUX_GEN_ZIPF) {
+      require(zipf_n >= 1 && zipf_s > 0, SUX_EINVAL, "zipf needs n >= 1 and s > 0");
+      nb = sux::zipf_table_size(zipf_n);
+      std::vector<uint64_t> b((size_t)nb + 1), t((size_t)nb + 1);
+      sux::zipf_table(zipf_s, zipf_n, b.data(), t.data());
+      hip_check(hipMalloc(&zb, b.size() * 8), "hipMalloc(zipf)");
+      hip_check(hipMalloc(&zt, t.size() * 8), "hipMalloc(zipf)");
+      hip_check(hipMemcpy(zb, b.data(), b.size() * 8, hipMemcpyHostToDevice), "H2D zipf");
+      hip_check(hipMemcpy(zt, t.data(), t.size() * 8, hipMemcpyHostToDevice), "H2D zipf");
+    }
+    hipError_t e = sux::launch_generate(kind, seed, first, n, static_cast<const uint64_t*>(zb),
+                                        static_cast<const uint64_t*>(zt), nb,
+                                        static_cast<uint8_t*>(d_out), s);
+    if (zb) {
+      (void)hipStreamSynchronize(s);
+      (void)hipFree(zb);
+      (void)hipFree(zt);
+    }
+    hip_check(e, "generate launch");
+  });
+}
+
+}  // extern "C"

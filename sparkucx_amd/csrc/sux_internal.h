@@ -1,0 +1,93 @@
+// sux_internal.h — internal declarations shared by the C-ABI (sux_api.cpp) and the gfx950
+// kernels (sux_partition.hip, sux_gen.hip, sux_copy.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+namespace sux {
+
+constexpr int kMaxPartitions = 32768;  // LDS histogram: 128 KiB of u32 counters at the limit
+constexpr int kMaxRecordSize = 4096;
+
+// Device-side partitioner (P1).  Range bounds are pre-packed as (hi, lo) big-endian words so a
+// key compare is two unsigned 64-bit compares.
+struct PartDev {
+  int32_t kind;
+  int32_t R;
+  int32_t key_offset;
+  int32_t key_len;
+  int32_t seed;
+  int32_t ascending;
+  const uint64_t* bounds;  // 2*(R-1) words: bounds[2i] = hi, bounds[2i+1] = lo (RANGE only)
+  // top-bits lookup: for key prefix v = hi >> (64 - lut_bits), the answer lies in
+  // [lut[v] & 0xFFFF, lut[v] >> 16]; 0 bits = no table (RANGE only)
+  const uint32_t* lut;
+  int32_t lut_bits;
+  int32_t pad;
+};
+
+// Per-launch geometry of a group of consecutive map batches.
+struct MapGroup {
+  const uint8_t* recs;       // first record of map 0 of the group
+  uint64_t records_per_map;  // records of every map but possibly the last
+  uint64_t num_records;      // records in the whole group
+  uint32_t num_maps;
+  uint32_t rec_size;
+  uint32_t tile_recs;      // records per tile (one wave's work in hist/scatter)
+  uint32_t tiles_per_map;  // ceil(records_per_map / tile_recs)
+};
+
+// Workspace carve-up (sizes in bytes), computed by workspace_layout().
+struct Workspace {
+  uint64_t counts_off, counts_bytes;  // u32 [map][R][tiles]  -> exclusive tile prefix in place
+  uint64_t totals_off, totals_bytes;  // u64 [map][R] partition record counts
+  uint64_t base_off, base_bytes;      // u64 [map][R] destination record offset of (map, p)
+  uint64_t pids_off, pids_bytes;      // u16 [records] when the caller passes no pid buffer
+  uint64_t total;
+};
+Workspace workspace_layout(uint32_t R, uint32_t rec_size, uint64_t records_per_map,
+                           uint64_t num_records, uint32_t tile_recs, bool need_pids);
+uint32_t choose_tile_recs(uint32_t R, uint32_t rec_size, uint64_t records_per_map);
+
+// Destination layout of a group (K2b): map-major (Spark data files side by side), or
+// peer-major for the exchange ([peer][map][partitions owned by peer]).
+struct LayoutDesc {
+  int32_t world;  // 1 = map-major
+  uint32_t rec_size;
+};
+
+// Kernel timing slots (sux_kernel_times order).
+enum KernelSlot { kHist = 0, kScan = 1, kScatter = 2, kCopy = 3, kNumSlots = 4 };
+struct Timer;  // owned by the node; nullptr = no timing
+void timer_begin(Timer* t, int slot, hipStream_t s);
+void timer_end(Timer* t, int slot, hipStream_t s);
+
+// Launchers (sux_partition.hip).  All enqueue on `s` and return the hipError_t of the launch.
+hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const LayoutDesc& lay,
+                                  uint8_t* d_out, int64_t* d_index, uint8_t* d_index_be,
+                                  uint16_t* d_pids, uint8_t* d_ws, const Workspace& ws,
+                                  uint64_t* d_peer_bytes, Timer* timer, hipStream_t s);
+hipError_t launch_partition_ids(const PartDev& pd, const uint8_t* recs, uint32_t rec_size,
+                                uint64_t n, uint16_t* d_pids, hipStream_t s);
+
+// Batched device copy (sux_copy.hip): n descriptors {src, dst, bytes}.
+struct CopyDesc {
+  const uint8_t* src;
+  uint8_t* dst;
+  uint64_t bytes;
+};
+hipError_t launch_gather_copy(const CopyDesc* d_desc, uint32_t n, uint32_t chunks_total,
+                              const uint32_t* d_chunk_first, Timer* timer, hipStream_t s);
+
+// Generators (sux_gen.hip).
+hipError_t launch_generate(int kind, uint64_t seed, uint64_t first, uint64_t n,
+                           const uint64_t* d_zipf_bounds, const uint64_t* d_zipf_thresh,
+                           int zipf_nb, uint8_t* d_out, hipStream_t s);
+
+// Host-side Zipf table (bit-identical construction to oracle/oracle.c).
+int zipf_table_size(uint64_t zipf_n);
+void zipf_table(double s, uint64_t zipf_n, uint64_t* bounds, uint64_t* thresh);
+
+}  // namespace sux

@@ -1,0 +1,528 @@
+// sux_partition.hip — map-side hot path for gfx950.
+//
+// One launch group = M consecutive map batches.  Four kernels:
+//   K1 k_hist      one wave per tile: key -> partition id (P1), pid store, wave-private LDS
+//                  histogram, counts[m][p][t] (partition-major).
+//   K2a k_tile_scan one wave per (map, partition): exclusive scan of counts over tiles in place,
+//                  totals[m][p].
+//   K2b k_group_scan one workgroup per group: per-map index tables (P3, native + big-endian) and
+//                  the destination base of every (map, partition) for the chosen layout.
+//   K3 k_scatter   one wave per tile: walks its records in input order 64 at a time, ranks
+//                  equal partition ids with a ballot match (stable), and copies each record to
+//                  base + tile prefix + rank.  This is the HBM-bound kernel.
+//
+// Stability: a wave owns a contiguous tile and visits it in order; within 64 lanes the rank is
+// the popcount of lower lanes with the same pid; tiles are ordered by the tile-major prefix.
+// So records keep input order inside a partition, as Spark's writers do (P2).
+#include <hip/hip_runtime.h>
+
+#include "sux_internal.h"
+
+namespace sux {
+
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+constexpr int kWave = 64;
+
+// ------------------------------------------------------------------------------------------
+// P1: partition functions (Spark semantics, oracle/oracle.c o_get_partition)
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+__device__ __forceinline__ uint32_t mix_k1(uint32_t k1) {
+  k1 *= 0xcc9e2d51u;
+  k1 = rotl32(k1, 15);
+  return k1 * 0x1b873593u;
+}
+__device__ __forceinline__ uint32_t mix_h1(uint32_t h1, uint32_t k1) {
+  h1 ^= k1;
+  h1 = rotl32(h1, 13);
+  return h1 * 5u + 0xe6546b64u;
+}
+__device__ __forceinline__ uint32_t fmix32(uint32_t h1, uint32_t len) {
+  h1 ^= len;
+  h1 ^= h1 >> 16;
+  h1 *= 0x85ebca6bu;
+  h1 ^= h1 >> 13;
+  h1 *= 0xc2b2ae35u;
+  return h1 ^ (h1 >> 16);
+}
+__device__ __forceinline__ int32_t pmod(int32_t a, int32_t n) {
+  int32_t r = a % n;
+  return r < 0 ? (r + n) % n : r;
+}
+
+__device__ __forceinline__ uint32_t ld_u32(const uint8_t* p, int off) {
+  if ((off & 3) == 0) return *reinterpret_cast<const uint32_t*>(p + off);
+  return (uint32_t)p[off] | ((uint32_t)p[off + 1] << 8) | ((uint32_t)p[off + 2] << 16) |
+         ((uint32_t)p[off + 3] << 24);
+}
+
+// Big-endian (hi, lo) words of a key of `len` (1..16) bytes, bytes past len zeroed.
+__device__ __forceinline__ void load_key_be(const uint8_t* rec, int off, int len, uint64_t& hi,
+                                            uint64_t& lo) {
+  uint32_t w0 = ld_u32(rec, off);
+  uint32_t w1 = len > 4 ? ld_u32(rec, off + 4) : 0u;
+  uint32_t w2 = len > 8 ? ld_u32(rec, off + 8) : 0u;
+  uint32_t w3 = len > 12 ? ld_u32(rec, off + 12) : 0u;
+  hi = ((uint64_t)__builtin_bswap32(w0) << 32) | __builtin_bswap32(w1);
+  lo = ((uint64_t)__builtin_bswap32(w2) << 32) | __builtin_bswap32(w3);
+  if (len < 8) {
+    hi &= ~0ull << (8 * (8 - len));
+    lo = 0;
+  } else if (len < 16) {
+    lo = (len == 8) ? 0 : (lo & (~0ull << (8 * (16 - len))));
+  }
+}
+
+__device__ __forceinline__ int range_search(const PartDev& pd, uint64_t hi, uint64_t lo) {
+  int a = 0, b = pd.R - 1;  // answer = #{bounds < key} in [a, b]
+  if (pd.lut_bits) {
+    uint32_t e = pd.lut[hi >> (64 - pd.lut_bits)];
+    a = e & 0xFFFFu;
+    b = e >> 16;
+  }
+  while (a < b) {
+    int mid = (a + b) >> 1;
+    uint64_t bh = pd.bounds[2 * mid], bl = pd.bounds[2 * mid + 1];
+    bool less = (bh < hi) || (bh == hi && bl < lo);  // bound < key
+    if (less) a = mid + 1; else b = mid;
+  }
+  return a;
+}
+
+__device__ __forceinline__ int get_partition(const PartDev& pd, const uint8_t* rec) {
+  switch (pd.kind) {
+    case 1: {  // SUX_PART_RANGE_BYTES
+      uint64_t hi, lo;
+      load_key_be(rec, pd.key_offset, pd.key_len, hi, lo);
+      int p = range_search(pd, hi, lo);
+      return pd.ascending ? p : (pd.R - 1) - p;
+    }
+    case 2: {  // SUX_PART_MURMUR3_LONG
+      uint32_t lo32 = ld_u32(rec, pd.key_offset), hi32 = ld_u32(rec, pd.key_offset + 4);
+      uint32_t h1 = mix_h1((uint32_t)pd.seed, mix_k1(lo32));
+      h1 = mix_h1(h1, mix_k1(hi32));
+      return pmod((int32_t)fmix32(h1, 8), pd.R);
+    }
+    case 3: {  // SUX_PART_MURMUR3_INT
+      uint32_t v = ld_u32(rec, pd.key_offset);
+      return pmod((int32_t)fmix32(mix_h1((uint32_t)pd.seed, mix_k1(v)), 4), pd.R);
+    }
+    case 4: {  // SUX_PART_MURMUR3_BYTES (legacy hashUnsafeBytes)
+      const int off = pd.key_offset, len = pd.key_len, aligned = len - len % 4;
+      uint32_t h1 = (uint32_t)pd.seed;
+      for (int i = 0; i < aligned; i += 4) h1 = mix_h1(h1, mix_k1(ld_u32(rec, off + i)));
+      for (int i = aligned; i < len; ++i)
+        h1 = mix_h1(h1, mix_k1((uint32_t)(int32_t)(int8_t)rec[off + i]));
+      return pmod((int32_t)fmix32(h1, (uint32_t)len), pd.R);
+    }
+    case 5: {  // SUX_PART_HASH_LONG: nonNegativeMod(Long.hashCode)
+      uint32_t h = ld_u32(rec, pd.key_offset) ^ ld_u32(rec, pd.key_offset + 4);
+      int32_t r = (int32_t)h % pd.R;
+      return r + (r < 0 ? pd.R : 0);
+    }
+    case 6: {  // SUX_PART_HASH_INT
+      int32_t r = (int32_t)ld_u32(rec, pd.key_offset) % pd.R;
+      return r + (r < 0 ? pd.R : 0);
+    }
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// geometry helpers
+// ------------------------------------------------------------------------------------------
+struct TileRange {
+  uint32_t map, tile;
+  uint64_t begin, end;  // record indices within the group
+};
+
+__device__ __forceinline__ TileRange tile_range(const MapGroup& g, uint32_t gtile) {
+  TileRange tr;
+  tr.map = gtile / g.tiles_per_map;
+  tr.tile = gtile - tr.map * g.tiles_per_map;
+  uint64_t map_begin = (uint64_t)tr.map * g.records_per_map;
+  uint64_t map_end = map_begin + g.records_per_map;
+  if (map_end > g.num_records) map_end = g.num_records;
+  tr.begin = map_begin + (uint64_t)tr.tile * g.tile_recs;
+  tr.end = tr.begin + g.tile_recs;
+  if (tr.end > map_end) tr.end = map_end;
+  if (tr.begin > tr.end) tr.begin = tr.end;
+  return tr;
+}
+
+// ------------------------------------------------------------------------------------------
+// K1: partition ids + per-tile histogram
+// ------------------------------------------------------------------------------------------
+template <int WPG>
+__global__ __launch_bounds__(WPG * kWave) void k_hist(PartDev pd, MapGroup g, uint16_t* pids,
+                                                      uint32_t* counts) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const uint32_t gtile = blockIdx.x * WPG + wave;
+  const uint32_t total_tiles = g.num_maps * g.tiles_per_map;
+  const int R = pd.R;
+  uint32_t* hist = lds + wave * R;
+  for (int p = lane; p < R; p += kWave) hist[p] = 0;
+  __builtin_amdgcn_wave_barrier();
+  if (gtile >= total_tiles) return;
+  const TileRange tr = tile_range(g, gtile);
+  for (uint64_t i = tr.begin + lane; i < tr.end; i += kWave) {
+    int p = get_partition(pd, g.recs + i * g.rec_size);
+    pids[i] = (uint16_t)p;
+    atomicAdd(&hist[p], 1u);
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  uint32_t* dst = counts + ((uint64_t)tr.map * R) * g.tiles_per_map + tr.tile;
+  for (int p = lane; p < R; p += kWave) dst[(uint64_t)p * g.tiles_per_map] = hist[p];
+}
+
+// ------------------------------------------------------------------------------------------
+// K2a: exclusive scan over tiles of each (map, partition) row; row totals
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    uint32_t t = __shfl_up(v, d, kWave);
+    if (lane >= d) v += t;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(256) void k_tile_scan(uint32_t* counts, uint64_t* totals,
+                                                   uint32_t rows, uint32_t tiles) {
+  const int lane = threadIdx.x % kWave;
+  const uint32_t row = blockIdx.x * 4 + threadIdx.x / kWave;
+  if (row >= rows) return;
+  uint32_t* c = counts + (uint64_t)row * tiles;
+  uint32_t carry = 0;
+  for (uint32_t t0 = 0; t0 < tiles; t0 += kWave) {
+    uint32_t t = t0 + lane;
+    uint32_t v = t < tiles ? c[t] : 0u;
+    uint32_t inc = wave_incl_scan(v, lane);
+    if (t < tiles) c[t] = carry + inc - v;
+    carry += __shfl(inc, kWave - 1, kWave);
+  }
+  if (lane == 0) totals[row] = carry;
+}
+
+// ------------------------------------------------------------------------------------------
+// K2b: per-group scans -> index tables and destination bases
+// ------------------------------------------------------------------------------------------
+constexpr int kScanThreads = 1024;
+
+// Block-wide exclusive scan of one u64 per thread; returns the exclusive prefix, *total = sum.
+__device__ uint64_t block_excl_scan(uint64_t v, uint64_t* sh, uint64_t* total) {
+  const int lane = threadIdx.x % kWave, wave = threadIdx.x / kWave;
+  constexpr int nw = kScanThreads / kWave;
+  uint64_t inc = v;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    uint64_t t = __shfl_up(inc, d, kWave);
+    if (lane >= d) inc += t;
+  }
+  if (lane == kWave - 1) sh[wave] = inc;
+  __syncthreads();
+  if (wave == 0) {
+    uint64_t w = lane < nw ? sh[lane] : 0;
+    uint64_t wi = w;
+#pragma unroll
+    for (int d = 1; d < nw; d <<= 1) {
+      uint64_t t = __shfl_up(wi, d, kWave);
+      if (lane >= d) wi += t;
+    }
+    if (lane < nw) sh[kWave + lane] = wi - w;
+    if (lane == nw - 1) sh[2 * kWave] = wi;
+  }
+  __syncthreads();
+  uint64_t r = sh[kWave + wave] + inc - v;
+  *total = sh[2 * kWave];
+  __syncthreads();
+  return r;
+}
+
+__device__ __forceinline__ uint64_t bswap64(uint64_t v) {
+  return ((uint64_t)__builtin_bswap32((uint32_t)v) << 32) | __builtin_bswap32((uint32_t)(v >> 32));
+}
+
+// Position of (m, p) in the peer-major order (h, m, p in [lo_h, hi_h)).
+__device__ __forceinline__ void peer_major_pos(uint64_t j, uint32_t M, int R, int G, uint32_t& m,
+                                               uint32_t& p) {
+  // find h with M*lo_h <= j < M*lo_{h+1}; lo_h = floor(h*R/G)
+  int h = 0;
+  while (h + 1 < G && (uint64_t)M * (uint64_t)(((int64_t)(h + 1) * R) / G) <= j) ++h;
+  uint32_t lo = (uint32_t)(((int64_t)h * R) / G), hi = (uint32_t)(((int64_t)(h + 1) * R) / G);
+  uint64_t r = j - (uint64_t)M * lo;
+  uint32_t w = hi - lo;
+  m = (uint32_t)(r / w);
+  p = lo + (uint32_t)(r % w);
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_group_scan(const uint64_t* totals,
+                                                             uint64_t* base, int64_t* index,
+                                                             uint8_t* index_be, uint64_t* peer_bytes,
+                                                             uint32_t M, int R, int G,
+                                                             uint32_t rec_size) {
+  __shared__ uint64_t sh[2 * kWave + 1];
+  const uint64_t L = (uint64_t)M * R;
+  // pass A: (m, p) order -> map-local index tables; also the map-major base (G == 1)
+  uint64_t carry = 0;
+  for (uint64_t j0 = 0; j0 < L; j0 += kScanThreads) {
+    uint64_t j = j0 + threadIdx.x;
+    uint64_t v = j < L ? totals[j] : 0;
+    uint64_t tot;
+    uint64_t ex = carry + block_excl_scan(v, sh, &tot);
+    if (j < L) {
+      if (G == 1) base[j] = ex;  // map-major layout: the (m, p) prefix is the destination
+      base[L + j] = ex;          // (m, p)-order prefix, read back for the index tables below
+    }
+    carry += tot;
+  }
+  __syncthreads();
+  // index tables: off_m[p] = (A[m][p] - A[m][0]) * S ; off_m[R] = (A[m+1][0] - A[m][0]) * S
+  const uint64_t* A = base + L;
+  const uint64_t LR1 = (uint64_t)M * (R + 1);
+  for (uint64_t k = threadIdx.x; k < LR1; k += kScanThreads) {
+    uint32_t m = (uint32_t)(k / (R + 1)), p = (uint32_t)(k % (R + 1));
+    uint64_t a0 = A[(uint64_t)m * R];
+    uint64_t ap = (p < (uint32_t)R) ? A[(uint64_t)m * R + p]
+                                    : (m + 1 < M ? A[(uint64_t)(m + 1) * R] : carry);
+    int64_t off = (int64_t)((ap - a0) * rec_size);
+    index[k] = off;
+    if (index_be) reinterpret_cast<uint64_t*>(index_be)[k] = bswap64((uint64_t)off);
+  }
+  if (G == 1) {
+    if (threadIdx.x == 0 && peer_bytes) peer_bytes[0] = carry * rec_size;
+    return;
+  }
+  // pass B: peer-major order (h, m, p) -> destination bases in the send buffer
+  carry = 0;
+  for (uint64_t j0 = 0; j0 < L; j0 += kScanThreads) {
+    uint64_t j = j0 + threadIdx.x;
+    uint32_t m = 0, p = 0;
+    uint64_t v = 0;
+    if (j < L) {
+      peer_major_pos(j, M, R, G, m, p);
+      v = totals[(uint64_t)m * R + p];
+    }
+    uint64_t tot;
+    uint64_t ex = carry + block_excl_scan(v, sh, &tot);
+    if (j < L) base[(uint64_t)m * R + p] = ex;
+    carry += tot;
+  }
+  __syncthreads();
+  if (peer_bytes && threadIdx.x < (unsigned)G) {
+    // bytes for peer h = sum over m, p in h's range
+    int h = threadIdx.x;
+    uint32_t lo = (uint32_t)(((int64_t)h * R) / G), hi = (uint32_t)(((int64_t)(h + 1) * R) / G);
+    uint64_t s = 0;
+    for (uint32_t m = 0; m < M; ++m)
+      for (uint32_t p = lo; p < hi; ++p) s += totals[(uint64_t)m * R + p];
+    peer_bytes[h] = s * rec_size;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K3: stable scatter
+// ------------------------------------------------------------------------------------------
+template <uint32_t S>
+__device__ __forceinline__ void copy_record(const uint8_t* __restrict__ src,
+                                           uint8_t* __restrict__ dst, uint32_t rs) {
+  if constexpr (S != 0) {
+#pragma unroll
+    for (uint32_t k = 0; k + 16 <= S; k += 16)
+      *reinterpret_cast<u32x4a4*>(dst + k) = *reinterpret_cast<const u32x4a4*>(src + k);
+#pragma unroll
+    for (uint32_t k = S - S % 16; k < S; k += 4)
+      *reinterpret_cast<uint32_t*>(dst + k) = *reinterpret_cast<const uint32_t*>(src + k);
+  } else {
+    uint32_t k = 0;
+    for (; k + 16 <= rs; k += 16)
+      *reinterpret_cast<u32x4a4*>(dst + k) = *reinterpret_cast<const u32x4a4*>(src + k);
+    for (; k < rs; k += 4)
+      *reinterpret_cast<uint32_t*>(dst + k) = *reinterpret_cast<const uint32_t*>(src + k);
+  }
+}
+
+template <int WPG, uint32_t S>
+__global__ __launch_bounds__(WPG * kWave) void k_scatter(MapGroup g, int R, int pid_bits,
+                                                         const uint16_t* __restrict__ pids,
+                                                         const uint32_t* __restrict__ prefix,
+                                                         const uint64_t* __restrict__ base,
+                                                         uint8_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const uint32_t gtile = blockIdx.x * WPG + wave;
+  if (gtile >= g.num_maps * g.tiles_per_map) return;
+  const TileRange tr = tile_range(g, gtile);
+  if (tr.begin >= tr.end) return;
+  const uint32_t rs = S ? S : g.rec_size;
+  // running destination (in records, relative to the group output) of every partition
+  uint32_t* run = lds + wave * R;
+  const uint64_t* bm = base + (uint64_t)tr.map * R;
+  const uint32_t* pm = prefix + (uint64_t)tr.map * R * g.tiles_per_map + tr.tile;
+  for (int p = lane; p < R; p += kWave)
+    run[p] = (uint32_t)(bm[p] + pm[(uint64_t)p * g.tiles_per_map]);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  for (uint64_t i0 = tr.begin; i0 < tr.end; i0 += kWave) {
+    const uint64_t i = i0 + lane;
+    const bool valid = i < tr.end;
+    const uint32_t pid = valid ? pids[i] : 0u;
+    uint64_t peers = __ballot(valid);
+    for (int b = 0; b < pid_bits; ++b) {
+      const bool bit = (pid >> b) & 1u;
+      const uint64_t m = __ballot(bit);
+      peers &= bit ? m : ~m;
+    }
+    uint32_t r0 = 0;
+    if (valid) r0 = run[pid];
+    __builtin_amdgcn_wave_barrier();
+    if (valid && (peers & lt_mask) == 0) run[pid] = r0 + (uint32_t)__popcll(peers);
+    __builtin_amdgcn_wave_barrier();
+    if (valid) {
+      const uint32_t dst = r0 + (uint32_t)__popcll(peers & lt_mask);
+      copy_record<S>(g.recs + i * rs, out + (uint64_t)dst * rs, rs);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// pid-only kernel (sux_partition_ids)
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pids(PartDev pd, const uint8_t* recs, uint32_t rs,
+                                              uint64_t n, uint16_t* pids) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * 256)
+    pids[i] = (uint16_t)get_partition(pd, recs + i * rs);
+}
+
+// ------------------------------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------------------------------
+uint32_t choose_tile_recs(uint32_t R, uint32_t rec_size, uint64_t records_per_map) {
+  (void)rec_size;
+  uint32_t t = 1024;
+  while (t < 4u * R && t < (1u << 22)) t <<= 1;
+  // no point in tiles longer than a map
+  uint64_t cap = ((records_per_map + kWave - 1) / kWave) * kWave;
+  if (cap < t) t = (uint32_t)(cap < kWave ? kWave : cap);
+  return t;
+}
+
+static uint64_t align_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+
+Workspace workspace_layout(uint32_t R, uint32_t rec_size, uint64_t records_per_map,
+                           uint64_t num_records, uint32_t tile_recs, bool need_pids) {
+  (void)rec_size;
+  Workspace w{};
+  uint64_t maps = records_per_map ? (num_records + records_per_map - 1) / records_per_map : 0;
+  if (maps == 0) maps = 1;
+  uint64_t tiles = (records_per_map + tile_recs - 1) / tile_recs;
+  if (tiles == 0) tiles = 1;
+  uint64_t off = 0;
+  w.counts_off = off;
+  w.counts_bytes = align_up(maps * R * tiles * 4, 256);
+  off += w.counts_bytes;
+  w.totals_off = off;
+  w.totals_bytes = align_up(maps * R * 8, 256);
+  off += w.totals_bytes;
+  w.base_off = off;
+  w.base_bytes = align_up(2 * maps * R * 8, 256);  // base + (m,p)-order scratch
+  off += w.base_bytes;
+  w.pids_off = off;
+  w.pids_bytes = need_pids ? align_up(num_records * 2, 256) : 0;
+  off += w.pids_bytes;
+  w.total = off;
+  return w;
+}
+
+static int waves_per_group(int R) { return (R * 4 * 4 <= 64 * 1024) ? 4 : 1; }
+
+// Dynamic LDS above 64 KiB must be opted into per kernel (gfx950 allows 160 KiB per workgroup).
+static void allow_lds(const void* fn, size_t lds) {
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+}
+
+template <int WPG>
+static hipError_t launch_scatter(uint32_t S, dim3 grid, size_t lds, hipStream_t s, const MapGroup& g,
+                                 int R, int bits, const uint16_t* pids, const uint32_t* prefix,
+                                 const uint64_t* base, uint8_t* out) {
+  allow_lds(reinterpret_cast<const void*>(&k_scatter<WPG, 100>), lds);
+  allow_lds(reinterpret_cast<const void*>(&k_scatter<WPG, 16>), lds);
+  allow_lds(reinterpret_cast<const void*>(&k_scatter<WPG, 0>), lds);
+  switch (S) {
+    case 100:
+      hipLaunchKernelGGL((k_scatter<WPG, 100>), grid, dim3(WPG * kWave), lds, s, g, R, bits, pids,
+                         prefix, base, out);
+      break;
+    case 16:
+      hipLaunchKernelGGL((k_scatter<WPG, 16>), grid, dim3(WPG * kWave), lds, s, g, R, bits, pids,
+                         prefix, base, out);
+      break;
+    default:
+      hipLaunchKernelGGL((k_scatter<WPG, 0>), grid, dim3(WPG * kWave), lds, s, g, R, bits, pids,
+                         prefix, base, out);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const LayoutDesc& lay,
+                                  uint8_t* d_out, int64_t* d_index, uint8_t* d_index_be,
+                                  uint16_t* d_pids, uint8_t* d_ws, const Workspace& ws,
+                                  uint64_t* d_peer_bytes, Timer* timer, hipStream_t s) {
+  const int R = pd.R;
+  const int wpg = waves_per_group(R);
+  const uint32_t total_tiles = g.num_maps * g.tiles_per_map;
+  const dim3 grid((total_tiles + wpg - 1) / wpg);
+  const size_t lds = (size_t)wpg * R * 4;
+  uint32_t* counts = reinterpret_cast<uint32_t*>(d_ws + ws.counts_off);
+  uint64_t* totals = reinterpret_cast<uint64_t*>(d_ws + ws.totals_off);
+  uint64_t* base = reinterpret_cast<uint64_t*>(d_ws + ws.base_off);
+  uint16_t* pids = d_pids ? d_pids : reinterpret_cast<uint16_t*>(d_ws + ws.pids_off);
+  int bits = 0;
+  while ((1 << bits) < R) ++bits;
+
+  allow_lds(reinterpret_cast<const void*>(&k_hist<1>), lds);
+  timer_begin(timer, kHist, s);
+  if (wpg == 4)
+    hipLaunchKernelGGL((k_hist<4>), grid, dim3(4 * kWave), lds, s, pd, g, pids, counts);
+  else
+    hipLaunchKernelGGL((k_hist<1>), grid, dim3(kWave), lds, s, pd, g, pids, counts);
+  timer_end(timer, kHist, s);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+
+  timer_begin(timer, kScan, s);
+  const uint32_t rows = g.num_maps * (uint32_t)R;
+  hipLaunchKernelGGL(k_tile_scan, dim3((rows + 3) / 4), dim3(256), 0, s, counts, totals, rows,
+                     g.tiles_per_map);
+  hipLaunchKernelGGL(k_group_scan, dim3(1), dim3(kScanThreads), 0, s, totals, base, d_index,
+                     d_index_be, d_peer_bytes, g.num_maps, R, lay.world, g.rec_size);
+  timer_end(timer, kScan, s);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+
+  timer_begin(timer, kScatter, s);
+  if (wpg == 4)
+    e = launch_scatter<4>(g.rec_size, grid, lds, s, g, R, bits, pids, counts, base, d_out);
+  else
+    e = launch_scatter<1>(g.rec_size, grid, lds, s, g, R, bits, pids, counts, base, d_out);
+  timer_end(timer, kScatter, s);
+  return e;
+}
+
+hipError_t launch_partition_ids(const PartDev& pd, const uint8_t* recs, uint32_t rec_size,
+                                uint64_t n, uint16_t* d_pids, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  uint64_t blocks = (n + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(k_pids, dim3((uint32_t)blocks), dim3(256), 0, s, pd, recs, rec_size, n,
+                     d_pids);
+  return hipGetLastError();
+}
+
+}  // namespace sux

@@ -1,0 +1,159 @@
+"""ctypes binding of libsparkucx_amd.so (include/sparkucx_amd.h).
+
+This is plumbing for tests and bench.py: every call goes straight through the C-ABI into the
+gfx950 kernels.  There is no CPU fallback — if the shared library is missing, importing
+`load()` raises and the caller fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsparkucx_amd.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "sparkucx_amd.h")
+
+# status codes / constants (mirrors include/sparkucx_amd.h)
+SUX_OK, SUX_EINVAL, SUX_ENOMEM, SUX_EHIP, SUX_ECOMM, SUX_ENOENT, SUX_ESTATE, SUX_ERANGE = (
+    0, -1, -2, -3, -4, -5, -6, -7)
+PART_RANGE_BYTES, PART_MURMUR3_LONG, PART_MURMUR3_INT, PART_MURMUR3_BYTES = 1, 2, 3, 4
+PART_HASH_LONG, PART_HASH_INT = 5, 6
+GEN_TERASORT, GEN_SMALL, GEN_ZIPF = 1, 2, 3
+KERNELS = ("hist", "scan", "scatter", "copy")
+
+
+class SuxError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+class Conf(C.Structure):
+    _fields_ = [("device", C.c_int32), ("rank", C.c_int32), ("world_size", C.c_int32),
+                ("num_streams", C.c_int32), ("comm_id", C.c_uint8 * 128),
+                ("min_buffer_size", C.c_uint64), ("min_allocation_size", C.c_uint64),
+                ("metadata_block_size", C.c_uint64)]
+
+
+class PartitionerDesc(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("num_partitions", C.c_int32), ("key_offset", C.c_int32),
+                ("key_len", C.c_int32), ("seed", C.c_int32), ("ascending", C.c_int32),
+                ("range_bounds", C.c_void_p)]
+
+
+class HandleDesc(C.Structure):
+    _fields_ = [("shuffle_id", C.c_int32), ("num_maps", C.c_int32),
+                ("num_partitions", C.c_int32), ("record_size", C.c_int32),
+                ("directory_bytes", C.c_uint64)]
+
+
+class BlockId(C.Structure):
+    _fields_ = [("map_index", C.c_int32), ("start_reduce", C.c_int32),
+                ("end_reduce", C.c_int32), ("reserved", C.c_int32)]
+
+
+P, I32, I64, U64, U32, SZ = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_uint32, C.c_size_t
+_SIGS = {
+    "sux_conf_init": (None, [C.POINTER(Conf)]),
+    "sux_abi_version": (C.c_int, []),
+    "sux_last_error": (C.c_int, [C.c_char_p, SZ]),
+    "sux_comm_unique_id": (C.c_int, [P]),
+    "sux_node_create": (C.c_int, [C.POINTER(Conf), C.c_int, C.POINTER(P)]),
+    "sux_node_destroy": (C.c_int, [P]),
+    "sux_partitioner_create": (C.c_int, [P, C.POINTER(PartitionerDesc), C.POINTER(P)]),
+    "sux_partitioner_destroy": (C.c_int, [P]),
+    "sux_partition_workspace_size": (C.c_int, [P, U32, U64, U64, C.POINTER(U64)]),
+    "sux_partition_maps": (C.c_int, [P, P, P, U32, U64, U64, P, P, P, P, P, U64, P]),
+    "sux_partition_maps_peer_major": (C.c_int, [P, P, P, U32, U64, U64, I32, P, P, P, P, P, U64,
+                                                P]),
+    "sux_plan_group": (C.c_int, [I32, I32, I32, I32, P, P, P, P, P]),
+    "sux_plan_block_offset": (I64, [I32, I32, I32, I32, P, I32, I32, I32]),
+    "sux_exchange_group": (C.c_int, [P, P, P, I32, I32, P, P, U64, P, P]),
+    "sux_partition_ids": (C.c_int, [P, P, P, U32, U64, P, P]),
+    "sux_register_shuffle": (C.c_int, [P, I32, I32, I32, I32, C.POINTER(HandleDesc)]),
+    "sux_unregister_shuffle": (C.c_int, [P, I32]),
+    "sux_write_map_output": (C.c_int, [P, I32, I32, P, P, U64, P]),
+    "sux_commit_map_output": (C.c_int, [P, I32, I32, P, U64, P, P]),
+    "sux_map_output_index": (C.c_int, [P, I32, I32, P, U64]),
+    "sux_exchange": (C.c_int, [P, I32, P]),
+    "sux_owned_partitions": (C.c_int, [P, I32, I32, C.POINTER(I32), C.POINTER(I32)]),
+    "sux_fetch_blocks": (C.c_int, [P, I32, P, I32, P, C.POINTER(P), P]),
+    "sux_resolve_blocks": (C.c_int, [P, I32, P, I32, P, P]),
+    "sux_buffer_info": (C.c_int, [P, C.POINTER(P), C.POINTER(U64), C.POINTER(U64)]),
+    "sux_buffer_retain": (C.c_int, [P, I32]),
+    "sux_buffer_release": (C.c_int, [P]),
+    "sux_set_kernel_timing": (C.c_int, [P, C.c_int]),
+    "sux_kernel_times": (C.c_int, [P, P, P, I32]),
+    "sux_generate": (C.c_int, [P, I32, U64, U64, U64, C.c_double, U64, P, P]),
+}
+
+_lib = None
+
+
+def header_symbols() -> list[str]:
+    """Every function the public header declares."""
+    with open(HEADER_PATH) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|int64_t)\s+(sux_\w+)\s*\(", text, re.M)))
+
+
+def load() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `make -C sparkucx_amd/csrc` "
+                          "(there is no CPU fallback for the shuffle path)")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    buf = C.create_string_buffer(4096)
+    load().sux_last_error(buf, len(buf))
+    return buf.value.decode(errors="replace")
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != SUX_OK:
+        raise SuxError(rc, f"{what}: {last_error()}")
+
+
+def default_conf(device=0, rank=0, world_size=1, comm_id: bytes | None = None, **kw) -> Conf:
+    c = Conf()
+    load().sux_conf_init(C.byref(c))
+    c.device, c.rank, c.world_size = device, rank, world_size
+    if comm_id is not None:
+        C.memmove(c.comm_id, comm_id, 128)
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+HIP_H2D, HIP_D2H, HIP_D2D = 1, 2, 3
+_hip = None
+
+
+def hip_memcpy(dst: int, src: int, nbytes: int, kind: int) -> None:
+    """Synchronous hipMemcpy through the HIP runtime already loaded in this process."""
+    global _hip
+    if _hip is None:
+        load()
+        _hip = C.CDLL("libamdhip64.so.7")
+        _hip.hipMemcpy.restype = C.c_int
+        _hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    rc = _hip.hipMemcpy(dst, src, nbytes, kind)
+    if rc != 0:
+        raise SuxError(SUX_EHIP, f"hipMemcpy failed ({rc})")
+
+
+def unique_id() -> bytes:
+    buf = (C.c_uint8 * 128)()
+    check(load().sux_comm_unique_id(buf), "sux_comm_unique_id")
+    return bytes(buf)

@@ -1,0 +1,266 @@
+"""Thin torch-facing wrappers over the C-ABI (device tensors in, device tensors out).
+
+Used by tests/ and bench.py.  torch is only plumbing here: it allocates HBM and provides the
+stream; every byte of the shuffle path is moved by the library's gfx950 kernels.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import native as N
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def _stream(stream) -> int | None:
+    if stream is None:
+        return torch.cuda.current_stream().cuda_stream
+    return stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+
+
+class Partitioner:
+    def __init__(self, node: "Node", kind: int, num_partitions: int, key_offset: int = 0,
+                 key_len: int = 8, seed: int = 42, ascending: bool = True,
+                 bounds: bytes | None = None):
+        self.node, self.kind, self.R = node, kind, num_partitions
+        self.key_offset, self.key_len = key_offset, key_len
+        self._bounds = None if bounds is None else C.create_string_buffer(bytes(bounds), len(bounds))
+        d = N.PartitionerDesc(kind, num_partitions, key_offset, key_len, seed, int(ascending),
+                              C.cast(self._bounds, C.c_void_p) if self._bounds is not None else None)
+        h = C.c_void_p()
+        N.check(N.load().sux_partitioner_create(node.h, C.byref(d), C.byref(h)),
+                "sux_partitioner_create")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            N.check(N.load().sux_partitioner_destroy(self.h), "sux_partitioner_destroy")
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Node:
+    """One executor's shuffle node on one GPU (UcxNode analog)."""
+
+    def __init__(self, device: int = 0, rank: int = 0, world_size: int = 1,
+                 comm_id: bytes | None = None, is_driver: bool = False, **conf):
+        self.lib = N.load()
+        self.device = device
+        c = N.default_conf(device, rank, world_size, comm_id, **conf)
+        h = C.c_void_p()
+        N.check(self.lib.sux_node_create(C.byref(c), int(is_driver), C.byref(h)), "sux_node_create")
+        self.h = h
+        self.rank, self.world_size = rank, world_size
+        self.dev = torch.device("cuda", device)
+
+    def close(self):
+        if self.h:
+            N.check(self.lib.sux_node_destroy(self.h), "sux_node_destroy")
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- partitioners ----------------------------------------------------------------------
+    def partitioner(self, kind, num_partitions, **kw) -> Partitioner:
+        return Partitioner(self, kind, num_partitions, **kw)
+
+    # ---- inputs ------------------------------------------------------------------------------
+    def generate(self, kind: int, seed: int, first: int, n: int, record_size: int,
+                 zipf_s: float = 1.1, zipf_n: int = 1 << 24, out: torch.Tensor | None = None,
+                 stream=None) -> torch.Tensor:
+        if out is None:
+            out = torch.empty(n * record_size, dtype=torch.uint8, device=self.dev)
+        N.check(self.lib.sux_generate(self.h, kind, seed, first, n, zipf_s, zipf_n, _ptr(out),
+                                      _stream(stream)), "sux_generate")
+        return out
+
+    # ---- stateless map side ------------------------------------------------------------------
+    def workspace_size(self, part: Partitioner, record_size: int, records_per_map: int,
+                       num_records: int) -> int:
+        v = C.c_uint64()
+        N.check(self.lib.sux_partition_workspace_size(part.h, record_size, records_per_map,
+                                                      num_records, C.byref(v)),
+                "sux_partition_workspace_size")
+        return v.value
+
+    def partition_maps(self, part: Partitioner, records: torch.Tensor, record_size: int,
+                       records_per_map: int, num_records: int | None = None,
+                       out: torch.Tensor | None = None, index: torch.Tensor | None = None,
+                       index_be: torch.Tensor | None = None, pids: torch.Tensor | None = None,
+                       workspace: torch.Tensor | None = None, want_be: bool = True,
+                       stream=None):
+        n = records.numel() // record_size if num_records is None else num_records
+        maps = max(1, -(-n // records_per_map))
+        R = part.R
+        if out is None:
+            out = torch.empty(max(1, n * record_size), dtype=torch.uint8, device=self.dev)
+        if index is None:
+            index = torch.empty(maps * (R + 1), dtype=torch.int64, device=self.dev)
+        if index_be is None and want_be:
+            index_be = torch.empty(maps * (R + 1) * 8, dtype=torch.uint8, device=self.dev)
+        if workspace is None:
+            workspace = torch.empty(max(1, self.workspace_size(part, record_size, records_per_map,
+                                                               n)),
+                                    dtype=torch.uint8, device=self.dev)
+        N.check(self.lib.sux_partition_maps(self.h, part.h, _ptr(records), record_size,
+                                            records_per_map, n, _ptr(out), _ptr(index),
+                                            _ptr(index_be), _ptr(pids), _ptr(workspace),
+                                            workspace.numel(), _stream(stream)),
+                "sux_partition_maps")
+        return out, index, index_be
+
+    def partition_maps_peer_major(self, part: Partitioner, records: torch.Tensor,
+                                  record_size: int, records_per_map: int, world: int,
+                                  num_records: int | None = None, out=None, index=None,
+                                  index_be=None, peer_bytes=None, workspace=None, stream=None):
+        n = records.numel() // record_size if num_records is None else num_records
+        maps = max(1, -(-n // records_per_map))
+        R = part.R
+        if out is None:
+            out = torch.empty(max(1, n * record_size), dtype=torch.uint8, device=self.dev)
+        if index is None:
+            index = torch.empty(maps * (R + 1), dtype=torch.int64, device=self.dev)
+        if peer_bytes is None:
+            peer_bytes = torch.zeros(world, dtype=torch.int64, device=self.dev)
+        if workspace is None:
+            workspace = torch.empty(max(1, self.workspace_size(part, record_size, records_per_map,
+                                                               n)),
+                                    dtype=torch.uint8, device=self.dev)
+        N.check(self.lib.sux_partition_maps_peer_major(
+            self.h, part.h, _ptr(records), record_size, records_per_map, n, world, _ptr(out),
+            _ptr(index), _ptr(index_be), _ptr(peer_bytes), _ptr(workspace), workspace.numel(),
+            _stream(stream)), "sux_partition_maps_peer_major")
+        return out, index, peer_bytes
+
+    def partition_ids(self, part: Partitioner, records: torch.Tensor, record_size: int,
+                      stream=None) -> torch.Tensor:
+        n = records.numel() // record_size
+        pids = torch.empty(max(1, n), dtype=torch.int16, device=self.dev)
+        N.check(self.lib.sux_partition_ids(self.h, part.h, _ptr(records), record_size, n,
+                                           _ptr(pids), _stream(stream)), "sux_partition_ids")
+        return pids[:n]
+
+    def exchange_group(self, send: torch.Tensor, index: torch.Tensor, num_maps: int, R: int,
+                       gathered: torch.Tensor, recv: torch.Tensor, stream=None) -> np.ndarray:
+        rb = (C.c_uint64 * self.world_size)()
+        N.check(self.lib.sux_exchange_group(self.h, _ptr(send), _ptr(index), num_maps, R,
+                                            _ptr(gathered), _ptr(recv), recv.numel(), rb,
+                                            _stream(stream)), "sux_exchange_group")
+        return np.frombuffer(rb, dtype=np.uint64).copy()
+
+    # ---- shuffle lifecycle / plugin surface -----------------------------------------------------
+    def register_shuffle(self, shuffle_id: int, num_maps: int, num_partitions: int,
+                         record_size: int) -> N.HandleDesc:
+        d = N.HandleDesc()
+        N.check(self.lib.sux_register_shuffle(self.h, shuffle_id, num_maps, num_partitions,
+                                              record_size, C.byref(d)), "sux_register_shuffle")
+        return d
+
+    def unregister_shuffle(self, shuffle_id: int):
+        N.check(self.lib.sux_unregister_shuffle(self.h, shuffle_id), "sux_unregister_shuffle")
+
+    def write_map_output(self, shuffle_id: int, map_index: int, part: Partitioner,
+                         records: torch.Tensor, num_records: int, stream=None):
+        N.check(self.lib.sux_write_map_output(self.h, shuffle_id, map_index, part.h,
+                                              _ptr(records), num_records, _stream(stream)),
+                "sux_write_map_output")
+
+    def commit_map_output(self, shuffle_id: int, map_index: int, data: torch.Tensor | None,
+                          lengths, stream=None):
+        arr = np.ascontiguousarray(np.asarray(lengths, dtype=np.int64))
+        nbytes = 0 if data is None else data.numel()
+        N.check(self.lib.sux_commit_map_output(self.h, shuffle_id, map_index, _ptr(data), nbytes,
+                                               arr.ctypes.data, _stream(stream)),
+                "sux_commit_map_output")
+
+    def map_output_index(self, shuffle_id: int, map_index: int, R: int) -> bytes:
+        buf = (C.c_uint8 * (8 * (R + 1)))()
+        N.check(self.lib.sux_map_output_index(self.h, shuffle_id, map_index, buf, len(buf)),
+                "sux_map_output_index")
+        return bytes(buf)
+
+    def exchange(self, shuffle_id: int, stream=None):
+        N.check(self.lib.sux_exchange(self.h, shuffle_id, _stream(stream)), "sux_exchange")
+
+    def owned_partitions(self, shuffle_id: int, rank: int | None = None) -> tuple[int, int]:
+        a, b = C.c_int32(), C.c_int32()
+        N.check(self.lib.sux_owned_partitions(self.h, shuffle_id, self.rank if rank is None else rank,
+                                              C.byref(a), C.byref(b)), "sux_owned_partitions")
+        return a.value, b.value
+
+    @staticmethod
+    def _blocks(blocks):
+        arr = (N.BlockId * max(1, len(blocks)))()
+        for i, b in enumerate(blocks):
+            m, s = b[0], b[1]
+            e = b[2] if len(b) > 2 else s + 1
+            arr[i] = N.BlockId(m, s, e, 0)
+        return arr
+
+    def fetch_blocks(self, shuffle_id: int, blocks, stream=None):
+        """Returns (FetchedBuffer, sizes[list])."""
+        arr = self._blocks(blocks)
+        sizes = (C.c_int64 * max(1, len(blocks)))()
+        h = C.c_void_p()
+        N.check(self.lib.sux_fetch_blocks(self.h, shuffle_id, arr, len(blocks), sizes,
+                                          C.byref(h), _stream(stream)), "sux_fetch_blocks")
+        return FetchedBuffer(self, h, len(blocks)), list(sizes)[:len(blocks)]
+
+    def resolve_blocks(self, shuffle_id: int, blocks):
+        arr = self._blocks(blocks)
+        addrs = (C.c_uint64 * max(1, len(blocks)))()
+        sizes = (C.c_int64 * max(1, len(blocks)))()
+        N.check(self.lib.sux_resolve_blocks(self.h, shuffle_id, arr, len(blocks), addrs, sizes),
+                "sux_resolve_blocks")
+        return list(addrs)[:len(blocks)], list(sizes)[:len(blocks)]
+
+    # ---- measurement -------------------------------------------------------------------------
+    def set_kernel_timing(self, on: bool):
+        N.check(self.lib.sux_set_kernel_timing(self.h, int(on)), "sux_set_kernel_timing")
+
+    def kernel_times(self) -> dict:
+        n = len(N.KERNELS)
+        launches, ms = (C.c_int64 * n)(), (C.c_double * n)()
+        N.check(self.lib.sux_kernel_times(self.h, launches, ms, n), "sux_kernel_times")
+        return {k: (launches[i], ms[i]) for i, k in enumerate(N.KERNELS)}
+
+
+class FetchedBuffer:
+    """Pooled device buffer of a fetch (refcounted; one reference per block)."""
+
+    def __init__(self, node: Node, h, refs: int):
+        self.node, self.h, self.refs = node, h, max(1, refs)
+
+    def info(self):
+        p, size, cap = C.c_void_p(), C.c_uint64(), C.c_uint64()
+        N.check(self.node.lib.sux_buffer_info(self.h, C.byref(p), C.byref(size), C.byref(cap)),
+                "sux_buffer_info")
+        return p.value, size.value, cap.value
+
+    def to_bytes(self) -> bytes:
+        p, size, _ = self.info()
+        if size == 0:
+            return b""
+        host = (C.c_uint8 * size)()
+        torch.cuda.synchronize(self.node.dev)
+        N.hip_memcpy(C.addressof(host), p, size, N.HIP_D2H)
+        return bytes(host)
+
+    def release(self, count: int = 1):
+        for _ in range(count):
+            N.check(self.node.lib.sux_buffer_release(self.h), "sux_buffer_release")
+        self.refs -= count

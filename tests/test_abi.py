@@ -1,0 +1,74 @@
+"""CPU: the C-ABI library loads, exports every header symbol, and its host-only logic is right.
+
+No compute call is made here (there is no GPU in the CPU job); the exchange planner is pure host
+arithmetic and is checked against a direct restatement.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from sparkucx_amd import native as N
+
+
+def test_library_loads_and_exports_every_header_symbol():
+    lib = N.load()
+    declared = N.header_symbols()
+    assert len(declared) >= 30
+    missing = [s for s in declared if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(declared) == set(N._SIGS), set(declared) ^ set(N._SIGS)
+    assert lib.sux_abi_version() == 1
+
+
+def test_conf_defaults_mirror_ucx_shuffle_conf():
+    c = N.default_conf()
+    assert c.world_size == 1 and c.rank == 0
+    assert c.min_buffer_size == 1024          # spark.shuffle.ucx.memory.minBufferSize
+    assert c.min_allocation_size == 4 << 20   # spark.shuffle.ucx.memory.minAllocationSize
+    assert c.metadata_block_size == 300       # 2 * spark.shuffle.ucx.rkeySize
+
+
+def test_null_arguments_fail_with_einval_and_message():
+    lib = N.load()
+    assert lib.sux_node_create(None, 0, None) == N.SUX_EINVAL
+    assert "NULL" in N.last_error()
+    assert lib.sux_partitioner_create(None, None, None) == N.SUX_EINVAL
+    assert lib.sux_buffer_release(None) == N.SUX_EINVAL
+    assert lib.sux_plan_group(2, 0, 1, 1, None, None, None, None, None) == N.SUX_EINVAL
+
+
+def _plan_ref(W, rank, M, R, gi):
+    lo = lambda h: (h * R) // W  # noqa: E731
+    sc = [sum(int(gi[rank, m, lo(h + 1)] - gi[rank, m, lo(h)]) for m in range(M)) for h in range(W)]
+    rc = [sum(int(gi[g, m, lo(rank + 1)] - gi[g, m, lo(rank)]) for m in range(M)) for g in range(W)]
+    sd = np.concatenate([[0], np.cumsum(sc)[:-1]]).tolist()
+    rd = np.concatenate([[0], np.cumsum(rc)[:-1]]).tolist()
+    return sc, sd, rc, rd
+
+
+@pytest.mark.parametrize("W,M,R", [(1, 1, 1), (2, 3, 8), (4, 2, 200), (8, 5, 200), (3, 4, 10)])
+def test_plan_group_matches_restatement(W, M, R):
+    rng = np.random.default_rng(W * 100 + M)
+    lengths = rng.integers(0, 5, size=(W, M, R)) * 100
+    gi = np.zeros((W, M, R + 1), np.int64)
+    gi[:, :, 1:] = np.cumsum(lengths, axis=2)
+    lib = N.load()
+    for rank in range(W):
+        out = [(C.c_uint64 * W)() for _ in range(4)]
+        rc = lib.sux_plan_group(W, rank, M, R, gi.ctypes.data, *out)
+        assert rc == 0, N.last_error()
+        got = [list(o) for o in out]
+        assert got == [list(x) for x in _plan_ref(W, rank, M, R, gi)]
+        # block offsets tile rank's receive buffer exactly, in [source][map][partition] order
+        lo, hi = (rank * R) // W, ((rank + 1) * R) // W
+        pos = 0
+        for g in range(W):
+            for m in range(M):
+                for p in range(lo, hi):
+                    off = lib.sux_plan_block_offset(W, rank, M, R, gi.ctypes.data, g, m, p)
+                    assert off == pos
+                    pos += int(gi[g, m, p + 1] - gi[g, m, p])
+        assert pos == sum(got[2])
+        if hi < R:
+            assert lib.sux_plan_block_offset(W, rank, M, R, gi.ctypes.data, 0, 0, hi) == -1

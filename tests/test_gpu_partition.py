@@ -1,0 +1,271 @@
+"""GPU parity: the gfx950 map-side path (P1-P3) through the C-ABI against the CPU oracle.
+
+Bit-exact on output bytes, index tables (native + Spark big-endian bytes) and partition ids.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from sparkucx_amd import native as N
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def sha(b):
+    return hashlib.sha256(bytes(b)).hexdigest()
+
+
+def to_dev(a: np.ndarray) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def host(t: torch.Tensor) -> np.ndarray:
+    return t.cpu().numpy()
+
+
+def gpu_part(node, opart: O.Partitioner):
+    return node.partitioner(opart.kind, opart.R, key_offset=opart.key_offset,
+                            key_len=opart.key_len, seed=opart.seed, ascending=opart.ascending,
+                            bounds=opart.bounds)
+
+
+def check_maps(node, opart, recs, rs, rpm, also_pids=True):
+    n = recs.size // rs
+    gp = gpu_part(node, opart)
+    drecs = to_dev(recs) if recs.size else torch.zeros(1, dtype=torch.uint8, device="cuda")
+    pids = torch.empty(max(1, n), dtype=torch.int16, device="cuda") if also_pids else None
+    out, index, index_be = node.partition_maps(gp, drecs, rs, rpm, num_records=n, pids=pids)
+    torch.cuda.synchronize()
+    want_data, want_index, want_be = O.write_maps(opart, recs, rs, rpm)
+    maps = -(-n // rpm) if n else 0
+    assert host(out)[: n * rs].tobytes() == bytes(want_data), "data bytes differ"
+    if maps:
+        assert host(index)[: maps * (opart.R + 1)].tolist() == want_index.tolist()
+        assert host(index_be)[: maps * (opart.R + 1) * 8].tobytes() == want_be
+    if also_pids and n:
+        assert (host(pids)[:n].view(np.uint16) == opart.ids(recs, rs)).all()
+    return out, index, index_be
+
+
+# ---- partitioner kinds ----------------------------------------------------------------------------
+@pytest.mark.parametrize("R", [1, 2, 7, 200, 1000, 5000])
+def test_terasort_range_partitioner(gpu_node, R):
+    recs = O.gen_terasort(1, 0, 20000)
+    check_maps(gpu_node, O.terasort_partitioner(R), recs, 100, 20000)
+
+
+def test_range_descending_short_key_odd_offset(gpu_node):
+    recs = O.gen_terasort(2, 0, 5000)
+    b = O.uniform_range_bounds(33, 5)
+    for asc in (True, False):
+        check_maps(gpu_node, O.Partitioner(O.RANGE_BYTES, 33, 3, 5, ascending=asc, bounds=b),
+                   recs, 100, 5000)
+
+
+def test_range_keys_equal_to_bounds(gpu_node):
+    R = 50
+    bounds = O.uniform_range_bounds(R, 10)
+    recs = O.gen_terasort(3, 0, 4 * (R - 1)).reshape(-1, 100)
+    for i in range(R - 1):  # exact bound, and bound with last byte +1
+        recs[4 * i, :10] = np.frombuffer(bounds[i * 10:(i + 1) * 10], np.uint8)
+        recs[4 * i + 1, :10] = recs[4 * i, :10]
+        recs[4 * i + 1, 9] = 1
+    check_maps(gpu_node, O.Partitioner(O.RANGE_BYTES, R, 0, 10, bounds=bounds), recs.ravel(), 100,
+               recs.shape[0])
+
+
+@pytest.mark.parametrize("kind,key_len,off", [(O.MURMUR3_LONG, 8, 0), (O.MURMUR3_LONG, 8, 12),
+                                              (O.MURMUR3_INT, 4, 0), (O.MURMUR3_INT, 4, 6),
+                                              (O.HASH_LONG, 8, 0), (O.HASH_INT, 4, 4),
+                                              (O.MURMUR3_BYTES, 10, 0), (O.MURMUR3_BYTES, 13, 3),
+                                              (O.MURMUR3_BYTES, 1, 7)])
+def test_hash_partitioners(gpu_node, kind, key_len, off):
+    recs = O.gen_zipf(9, 0, 20000, 1.1, 1 << 20)
+    check_maps(gpu_node, O.Partitioner(kind, 200, off, key_len, seed=42), recs, 100, 7000)
+
+
+def test_zipf_skew_config4_shape(gpu_node):
+    recs = O.gen_zipf(0x5EED0004, 0, 200000, 1.1, 1 << 24)
+    check_maps(gpu_node, O.Partitioner(O.MURMUR3_LONG, 200, 0, 8, seed=42), recs, 100, 65536)
+
+
+def test_small_records_10k_partitions(gpu_node):
+    recs = O.gen_small(0x5EED0005, 0, 1 << 18)
+    check_maps(gpu_node, O.Partitioner(O.MURMUR3_LONG, 10000, 0, 8, seed=42), recs, 16, 1 << 17)
+
+
+def test_max_partitions(gpu_node):
+    recs = O.gen_small(5, 0, 100000)
+    check_maps(gpu_node, O.Partitioner(O.HASH_LONG, 32768, 0, 8), recs, 16, 100000)
+
+
+# ---- shapes and edge cases ---------------------------------------------------------------------
+@pytest.mark.parametrize("n,rpm", [(0, 10), (1, 1), (63, 63), (64, 10), (1000, 333), (4097, 4096),
+                                   (10000, 3000), (100000, 99999)])
+def test_ragged_maps(gpu_node, n, rpm):
+    recs = O.gen_terasort(4, 0, n)
+    check_maps(gpu_node, O.terasort_partitioner(200), recs, 100, rpm)
+
+
+@pytest.mark.parametrize("rs", [4, 8, 12, 16, 20, 64, 100, 128, 260, 4096])
+def test_record_sizes(gpu_node, rs):
+    n = 3000 if rs < 1000 else 300
+    raw = O.gen_terasort(6, 0, n * rs // 100 + 1)[: n * rs]
+    key_len = 4 if rs < 8 else 8
+    kind = O.HASH_INT if rs < 8 else O.MURMUR3_LONG
+    check_maps(gpu_node, O.Partitioner(kind, 97, 0, key_len, seed=42), raw, rs, 1000)
+
+
+def test_record_size_and_key_validation(gpu_node):
+    gp = gpu_node.partitioner(O.MURMUR3_LONG, 10, key_offset=0, key_len=8)
+    x = torch.zeros(1000, dtype=torch.uint8, device="cuda")
+    for rs in (0, 3, 6, 5000):
+        with pytest.raises(N.SuxError) as e:
+            gpu_node.partition_maps(gp, x, rs, 10, num_records=1)
+        assert e.value.code == N.SUX_EINVAL
+    gp2 = gpu_node.partitioner(O.MURMUR3_LONG, 10, key_offset=12, key_len=8)
+    with pytest.raises(N.SuxError, match="does not fit"):
+        gpu_node.partition_maps(gp2, x, 16, 10, num_records=2)
+    with pytest.raises(N.SuxError, match="strictly increasing"):
+        gpu_node.partitioner(O.RANGE_BYTES, 3, key_len=2, bounds=b"\x05\x00\x05\x00")
+    with pytest.raises(N.SuxError):
+        gpu_node.partitioner(O.MURMUR3_LONG, 40000, key_len=8)
+
+
+# ---- golden fixtures -------------------------------------------------------------------------------
+GEN = {"gen_terasort": O.gen_terasort, "gen_zipf": O.gen_zipf, "gen_small": O.gen_small}
+GEN_DEV = {"gen_terasort": N.GEN_TERASORT, "gen_zipf": N.GEN_ZIPF, "gen_small": N.GEN_SMALL}
+
+
+@pytest.mark.parametrize("name", ["terasort_4096_R7.json", "terasort_4096_R200.json",
+                                  "zipf_4096_R200.json", "small_65536_R10000.json",
+                                  "terasort_10000_rpm3000_R200.json"])
+def test_golden_fixtures_on_gpu(gpu_node, name):
+    with open(os.path.join(GOLD, name)) as f:
+        g = json.load(f)
+    rs, n = g["record_size"], g["num_records"]
+    # device generator reproduces the fixture's input bytes
+    args = g["gen_args"]
+    if g["generator"] == "gen_zipf":
+        d = gpu_node.generate(N.GEN_ZIPF, args[0], args[1], args[2], rs, zipf_s=args[3], zipf_n=args[4])
+    else:
+        d = gpu_node.generate(GEN_DEV[g["generator"]], args[0], args[1], args[2], rs)
+    torch.cuda.synchronize()
+    assert sha(host(d)) == g["input_sha256"]
+    kw = dict(g["partitioner"])
+    bounds = bytes.fromhex(kw.pop("bounds")) if "bounds" in kw else None
+    gp = gpu_node.partitioner(kw["kind"], kw["R"], key_offset=kw.get("key_offset", 0),
+                              key_len=kw.get("key_len", 8), seed=kw.get("seed", 42), bounds=bounds)
+    pids = torch.empty(n, dtype=torch.int16, device="cuda")
+    out, index, index_be = gpu_node.partition_maps(gp, d, rs, g["records_per_map"], pids=pids)
+    torch.cuda.synchronize()
+    maps = -(-n // g["records_per_map"])
+    assert sha(host(pids).view(np.uint16).astype("<u2").tobytes()) == g["pids_sha256"]
+    assert sha(host(out)) == g["data_sha256"]
+    assert sha(host(index_be)[: maps * (kw["R"] + 1) * 8]) == g["index_be_sha256"]
+
+
+def test_device_generators_match_oracle(gpu_node):
+    for kind, f, rs in [(N.GEN_TERASORT, O.gen_terasort, 100), (N.GEN_SMALL, O.gen_small, 16)]:
+        d = gpu_node.generate(kind, 77, 12345, 3000, rs)
+        torch.cuda.synchronize()
+        assert (host(d) == f(77, 12345, 3000)).all()
+    d = gpu_node.generate(N.GEN_ZIPF, 78, 999, 3000, 100, zipf_s=1.1, zipf_n=1 << 24)
+    torch.cuda.synchronize()
+    assert (host(d) == O.gen_zipf(78, 999, 3000, 1.1, 1 << 24)).all()
+
+
+# ---- exchange layout (peer-major) ------------------------------------------------------------------
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_peer_major_layout(gpu_node, world):
+    R, rpm = 200, 7000
+    recs = O.gen_terasort(8, 0, 30000)
+    opart = O.terasort_partitioner(R)
+    gp = gpu_part(gpu_node, opart)
+    out, index, peer = gpu_node.partition_maps_peer_major(gp, to_dev(recs), 100, rpm, world)
+    torch.cuda.synchronize()
+    want, want_index, want_peer = O.peer_major(opart, recs, 100, rpm, world)
+    assert host(out).tobytes() == bytes(want)
+    assert host(index).tolist() == want_index.tolist()
+    assert host(peer).tolist() == want_peer.tolist()
+
+
+def test_exchange_group_single_rank(gpu_node):
+    R, rpm = 64, 5000
+    recs = O.gen_terasort(10, 0, 12000)
+    opart = O.terasort_partitioner(R)
+    gp = gpu_part(gpu_node, opart)
+    send, index, peer = gpu_node.partition_maps_peer_major(gp, to_dev(recs), 100, rpm, 1)
+    maps = -(-12000 // rpm)
+    gathered = torch.empty(maps * (R + 1), dtype=torch.int64, device="cuda")
+    recv = torch.empty(recs.size, dtype=torch.uint8, device="cuda")
+    rb = gpu_node.exchange_group(send, index, maps, R, gathered, recv)
+    torch.cuda.synchronize()
+    assert rb.tolist() == [recs.size]
+    assert host(recv).tobytes() == host(send).tobytes()
+    small = torch.empty(10, dtype=torch.uint8, device="cuda")
+    with pytest.raises(N.SuxError) as e:
+        gpu_node.exchange_group(send, index, maps, R, gathered, small)
+    assert e.value.code == N.SUX_ERANGE
+
+
+# ---- full-size properties (BASELINE-scale batches, size-independent checks) ----------------------
+def test_large_batch_properties(gpu_node):
+    """10^8 TeraSort records (10 GB, config-2 batch scale): multiset preserved, stable, sorted by
+    partition, index consistent — all checked on the device."""
+    n, rs, R, rpm = 100_000_000, 100, 200, 1 << 24
+    opart = O.terasort_partitioner(R)
+    gp = gpu_part(gpu_node, opart)
+    d = gpu_node.generate(N.GEN_TERASORT, 0x5EED0002, 0, n, rs)
+    out, index, index_be = gpu_node.partition_maps(gp, d, rs, rpm)
+    torch.cuda.synchronize()
+    maps = -(-n // rpm)
+    idx = index.view(maps, R + 1)
+    counts = torch.tensor([min(rpm, n - m * rpm) for m in range(maps)], device="cuda") * rs
+    assert (idx[:, 0] == 0).all() and (idx[:, -1] == counts).all()
+    assert (idx[:, 1:] >= idx[:, :-1]).all()
+    sa = torch.zeros(25, dtype=torch.int64, device="cuda")
+    sb = torch.zeros(25, dtype=torch.int64, device="cuda")
+    for c0 in range(0, n, 10_000_000):
+        c1 = min(n, c0 + 10_000_000)
+        sa += d[c0 * rs:c1 * rs].view(-1, rs).view(torch.int32).to(torch.int64).sum(0)
+        sb += out[c0 * rs:c1 * rs].view(-1, rs).view(torch.int32).to(torch.int64).sum(0)
+    assert torch.equal(sa, sb), "column sums differ: records lost or duplicated"
+    # per map: pids of the output are non-decreasing, row ids rise inside every partition
+    pids_out = gpu_node.partition_ids(gp, out, rs).to(torch.int32) & 0xFFFF
+    rows = out.view(n, rs).view(torch.int32)[:, 3:5].contiguous().view(torch.int64).view(-1)
+    for m in range(maps):
+        s, e = m * rpm, min(n, (m + 1) * rpm)
+        p = pids_out[s:e]
+        assert (p[1:] >= p[:-1]).all()
+        same = p[1:] == p[:-1]
+        r = rows[s:e]
+        assert (r[1:][same] > r[:-1][same]).all(), "unstable within a partition"
+        # index agrees with the partition boundaries
+        cnt = torch.bincount(p, minlength=R) * rs
+        assert torch.equal(torch.cumsum(cnt, 0), idx[m, 1:])
+    # spot-check one map byte-for-byte against the oracle
+    m = maps - 1
+    s, e = m * rpm, n
+    sub = O.gen_terasort(0x5EED0002, s, e - s)
+    want, _, want_index, _ = O.write_map(opart, sub, rs)
+    assert host(out[s * rs:e * rs]).tobytes() == bytes(want)
+
+
+def test_kernel_timing_counts_launches(gpu_node):
+    recs = O.gen_terasort(12, 0, 50000)
+    gp = gpu_part(gpu_node, O.terasort_partitioner(200))
+    gpu_node.set_kernel_timing(True)
+    for _ in range(3):
+        gpu_node.partition_maps(gp, to_dev(recs), 100, 20000)
+    torch.cuda.synchronize()
+    t = gpu_node.kernel_times()
+    gpu_node.set_kernel_timing(False)
+    assert t["hist"][0] == 3 and t["scatter"][0] == 3 and t["scan"][0] == 3
+    assert t["scatter"][1] > 0
