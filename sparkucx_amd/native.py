@@ -98,6 +98,18 @@ def header_symbols() -> list[str]:
     return sorted(set(re.findall(r"^\s*(?:int|void|int64_t)\s+(sux_\w+)\s*\(", text, re.M)))
 
 
+def _init_torch_hip_first() -> None:
+    """In a torch process, torch must initialise the shared HIP runtime before this library's
+    load-time code-object registration runs; otherwise the runtime reports no device to torch
+    (and to us).  Without a GPU (the CPU test job) this is a no-op."""
+    try:
+        import torch
+    except ImportError:
+        return
+    if torch.cuda.is_available():
+        torch.cuda.init()
+
+
 def load() -> C.CDLL:
     global _lib
     if _lib is not None:
@@ -105,6 +117,7 @@ def load() -> C.CDLL:
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} is missing: build it with `make -C sparkucx_amd/csrc` "
                           "(there is no CPU fallback for the shuffle path)")
+    _init_torch_hip_first()
     lib = C.CDLL(LIB_PATH)
     for name, (res, args) in _SIGS.items():
         fn = getattr(lib, name)

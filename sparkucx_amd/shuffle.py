@@ -56,6 +56,9 @@ class Node:
                  comm_id: bytes | None = None, is_driver: bool = False, **conf):
         self.lib = N.load()
         self.device = device
+        # torch must bring up its HIP context first: its lazy init refuses the device once another
+        # user of the (shared) HIP runtime in this process has initialised it
+        torch.cuda.init()
         c = N.default_conf(device, rank, world_size, comm_id, **conf)
         h = C.c_void_p()
         N.check(self.lib.sux_node_create(C.byref(c), int(is_driver), C.byref(h)), "sux_node_create")
