@@ -16,6 +16,8 @@
 // So records keep input order inside a partition, as Spark's writers do (P2).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "sux_internal.h"
 
 namespace sux {
@@ -390,6 +392,148 @@ __global__ __launch_bounds__(WPG * kWave) void k_scatter(MapGroup g, int R, int 
 }
 
 // ------------------------------------------------------------------------------------------
+// v2 kernels: a wave stages CH records of its tile in LDS with fully coalesced 16-byte loads
+// (1 KiB per wave instruction), works on them there, and (scatter) writes them out record-
+// coalesced: consecutive lanes store consecutive dwords, so a wave instruction covers ~2.5
+// whole records instead of touching 64 cache lines.
+// ------------------------------------------------------------------------------------------
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <uint32_t S, uint32_t CH>
+struct Stage {
+  static constexpr uint32_t kUnits = (CH * S + 12 + 15) / 16;  // 16-B units incl. a <=12 B head
+  static constexpr uint32_t kPer = (kUnits + kWave - 1) / kWave;
+  static constexpr uint32_t kBufBytes = kUnits * 16;
+};
+
+// Load the 16-byte units covering [a, a + len) into `dst` (a is 4-byte aligned); returns the
+// offset of `a` in dst.  Every unit holds a requested byte, so no load leaves the buffer's pages.
+template <uint32_t PER>
+__device__ __forceinline__ uint32_t stage_units(const uint8_t* a, uint32_t len, u32x4* dst,
+                                                int lane) {
+  const uintptr_t p = reinterpret_cast<uintptr_t>(a);
+  const uint32_t head = (uint32_t)(p & 15u);
+  const u32x4* src = reinterpret_cast<const u32x4*>(p - head);
+  const uint32_t units = (head + len + 15) >> 4;
+  u32x4 v[PER];
+#pragma unroll
+  for (uint32_t k = 0; k < PER; ++k) {
+    const uint32_t u = lane + k * kWave;
+    if (u < units) v[k] = src[u];
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < PER; ++k) {
+    const uint32_t u = lane + k * kWave;
+    if (u < units) dst[u] = v[k];
+  }
+  return head;
+}
+
+template <uint32_t S, uint32_t CH>
+__host__ __device__ constexpr uint32_t hist2_wave_bytes(int R) {
+  return Stage<S, CH>::kBufBytes + (((uint32_t)R * 4 + 15) / 16) * 16;
+}
+template <uint32_t S, uint32_t CH>
+__host__ __device__ constexpr uint32_t scatter2_wave_bytes(int R) {
+  return Stage<S, CH>::kBufBytes + CH * 4 + (((uint32_t)R * 4 + 15) / 16) * 16;
+}
+
+template <uint32_t S, uint32_t CH>
+__global__ __launch_bounds__(256) void k_hist2(PartDev pd, MapGroup g, uint16_t* __restrict__ pids,
+                                               uint32_t* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  using St = Stage<S, CH>;
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int R = pd.R;
+  uint8_t* wb = lds8 + wave * hist2_wave_bytes<S, CH>(R);
+  u32x4* buf = reinterpret_cast<u32x4*>(wb);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(wb + St::kBufBytes);
+  for (int p = lane; p < R; p += kWave) hist[p] = 0;
+  const uint32_t gtile = blockIdx.x * 4 + wave;
+  if (gtile >= g.num_maps * g.tiles_per_map) return;
+  const TileRange tr = tile_range(g, gtile);
+  for (uint64_t c0 = tr.begin; c0 < tr.end; c0 += CH) {
+    const uint32_t nrec = (uint32_t)min<uint64_t>(CH, tr.end - c0);
+    const uint32_t head = stage_units<St::kPer>(g.recs + c0 * S, nrec * S, buf, lane);
+    __builtin_amdgcn_wave_barrier();
+    const uint8_t* b = reinterpret_cast<const uint8_t*>(buf) + head;
+#pragma unroll
+    for (uint32_t j = 0; j < CH / kWave; ++j) {
+      const uint32_t r = j * kWave + lane;
+      if (r < nrec) {
+        const int p = get_partition(pd, b + r * S);
+        pids[c0 + r] = (uint16_t)p;
+        atomicAdd(&hist[p], 1u);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  uint32_t* dst = counts + ((uint64_t)tr.map * R) * g.tiles_per_map + tr.tile;
+  for (int p = lane; p < R; p += kWave) dst[(uint64_t)p * g.tiles_per_map] = hist[p];
+}
+
+template <uint32_t S, uint32_t CH>
+__global__ __launch_bounds__(256) void k_scatter2(MapGroup g, int R, int pid_bits,
+                                                  const uint16_t* __restrict__ pids,
+                                                  const uint32_t* __restrict__ prefix,
+                                                  const uint64_t* __restrict__ base,
+                                                  uint8_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  using St = Stage<S, CH>;
+  constexpr uint32_t W = S / 4;  // dwords per record
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const uint32_t gtile = blockIdx.x * 4 + wave;
+  if (gtile >= g.num_maps * g.tiles_per_map) return;
+  const TileRange tr = tile_range(g, gtile);
+  if (tr.begin >= tr.end) return;
+  uint8_t* wb = lds8 + wave * scatter2_wave_bytes<S, CH>(R);
+  u32x4* buf = reinterpret_cast<u32x4*>(wb);
+  uint32_t* dest = reinterpret_cast<uint32_t*>(wb + St::kBufBytes);
+  uint32_t* run = dest + CH;
+  const uint64_t* bm = base + (uint64_t)tr.map * R;
+  const uint32_t* pm = prefix + (uint64_t)tr.map * R * g.tiles_per_map + tr.tile;
+  for (int p = lane; p < R; p += kWave)
+    run[p] = (uint32_t)(bm[p] + pm[(uint64_t)p * g.tiles_per_map]);
+  __builtin_amdgcn_wave_barrier();
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  uint32_t* out32 = reinterpret_cast<uint32_t*>(out);
+  for (uint64_t c0 = tr.begin; c0 < tr.end; c0 += CH) {
+    const uint32_t nrec = (uint32_t)min<uint64_t>(CH, tr.end - c0);
+    const uint32_t head = stage_units<St::kPer>(g.recs + c0 * S, nrec * S, buf, lane);
+    // destinations, in input order (stable: lane order inside 64, chunk order across)
+#pragma unroll
+    for (uint32_t j = 0; j < CH / kWave; ++j) {
+      const uint32_t r = j * kWave + lane;
+      const bool valid = r < nrec;
+      const uint32_t pid = valid ? pids[c0 + r] : 0u;
+      uint64_t peers = __ballot(valid);
+      for (int bb = 0; bb < pid_bits; ++bb) {
+        const bool bit = (pid >> bb) & 1u;
+        const uint64_t m = __ballot(bit);
+        peers &= bit ? m : ~m;
+      }
+      uint32_t r0 = 0;
+      if (valid) r0 = run[pid];
+      __builtin_amdgcn_wave_barrier();
+      if (valid && (peers & lt_mask) == 0) run[pid] = r0 + (uint32_t)__popcll(peers);
+      if (valid) dest[r] = r0 + (uint32_t)__popcll(peers & lt_mask);
+      __builtin_amdgcn_wave_barrier();
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // record-coalesced write-out: lane -> dword d of the chunk, in input order
+    const uint32_t* bw = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(buf) + head);
+    const uint32_t total = nrec * W;
+#pragma unroll 4
+    for (uint32_t d = lane; d < total; d += kWave) {
+      const uint32_t r = d / W, w = d - r * W;
+      out32[(uint64_t)dest[r] * W + w] = bw[d];
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // pid-only kernel (sux_partition_ids)
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_pids(PartDev pd, const uint8_t* recs, uint32_t rs,
@@ -406,6 +550,10 @@ uint32_t choose_tile_recs(uint32_t R, uint32_t rec_size, uint64_t records_per_ma
   (void)rec_size;
   uint32_t t = 1024;
   while (t < 4u * R && t < (1u << 22)) t <<= 1;
+  if (const char* e = getenv("SUX_TILE_RECS")) {  // tuning override (power of two, >= 64)
+    uint32_t v = (uint32_t)strtoul(e, nullptr, 10);
+    if (v >= 64 && (v & (v - 1)) == 0) t = v;
+  }
   // no point in tiles longer than a map
   uint64_t cap = ((records_per_map + kWave - 1) / kWave) * kWave;
   if (cap < t) t = (uint32_t)(cap < kWave ? kWave : cap);
@@ -486,9 +634,42 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   int bits = 0;
   while ((1 << bits) < R) ++bits;
 
+  // v2 (LDS-staged) kernels for the two record shapes of the configs; v1 otherwise
+  static const bool force_v1 = [] {
+    const char* e = getenv("SUX_KERNEL");
+    return e && e[0] == 'v' && e[1] == '1';
+  }();
+  const bool v2 = !force_v1 && (g.rec_size == 100 || g.rec_size == 16) && R <= 4096;
+  const dim3 grid4((total_tiles + 3) / 4);
+  size_t lds_h = 0, lds_s = 0;
+  static const bool ch64 = [] {
+    const char* e = getenv("SUX_CHUNK");
+    return e && atoi(e) == 64;
+  }();
+  if (v2) {
+    lds_h = 4 * (size_t)(g.rec_size == 100 ? (ch64 ? hist2_wave_bytes<100, 64>(R)
+                                                   : hist2_wave_bytes<100, 128>(R))
+                                           : hist2_wave_bytes<16, 512>(R));
+    lds_s = 4 * (size_t)(g.rec_size == 100 ? (ch64 ? scatter2_wave_bytes<100, 64>(R)
+                                                   : scatter2_wave_bytes<100, 128>(R))
+                                           : scatter2_wave_bytes<16, 512>(R));
+    allow_lds(reinterpret_cast<const void*>(&k_hist2<100, 64>), lds_h);
+    allow_lds(reinterpret_cast<const void*>(&k_scatter2<100, 64>), lds_s);
+    allow_lds(reinterpret_cast<const void*>(&k_hist2<100, 128>), lds_h);
+    allow_lds(reinterpret_cast<const void*>(&k_hist2<16, 512>), lds_h);
+    allow_lds(reinterpret_cast<const void*>(&k_scatter2<100, 128>), lds_s);
+    allow_lds(reinterpret_cast<const void*>(&k_scatter2<16, 512>), lds_s);
+  }
+
   allow_lds(reinterpret_cast<const void*>(&k_hist<1>), lds);
   timer_begin(timer, kHist, s);
-  if (wpg == 4)
+  if (v2 && g.rec_size == 100 && ch64)
+    hipLaunchKernelGGL((k_hist2<100, 64>), grid4, dim3(256), lds_h, s, pd, g, pids, counts);
+  else if (v2 && g.rec_size == 100)
+    hipLaunchKernelGGL((k_hist2<100, 128>), grid4, dim3(256), lds_h, s, pd, g, pids, counts);
+  else if (v2)
+    hipLaunchKernelGGL((k_hist2<16, 512>), grid4, dim3(256), lds_h, s, pd, g, pids, counts);
+  else if (wpg == 4)
     hipLaunchKernelGGL((k_hist<4>), grid, dim3(4 * kWave), lds, s, pd, g, pids, counts);
   else
     hipLaunchKernelGGL((k_hist<1>), grid, dim3(kWave), lds, s, pd, g, pids, counts);
@@ -507,7 +688,19 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   if (e != hipSuccess) return e;
 
   timer_begin(timer, kScatter, s);
-  if (wpg == 4)
+  if (v2 && g.rec_size == 100 && ch64) {
+    hipLaunchKernelGGL((k_scatter2<100, 64>), grid4, dim3(256), lds_s, s, g, R, bits, pids,
+                       counts, base, d_out);
+    e = hipGetLastError();
+  } else if (v2 && g.rec_size == 100) {
+    hipLaunchKernelGGL((k_scatter2<100, 128>), grid4, dim3(256), lds_s, s, g, R, bits, pids,
+                       counts, base, d_out);
+    e = hipGetLastError();
+  } else if (v2) {
+    hipLaunchKernelGGL((k_scatter2<16, 512>), grid4, dim3(256), lds_s, s, g, R, bits, pids,
+                       counts, base, d_out);
+    e = hipGetLastError();
+  } else if (wpg == 4)
     e = launch_scatter<4>(g.rec_size, grid, lds, s, g, R, bits, pids, counts, base, d_out);
   else
     e = launch_scatter<1>(g.rec_size, grid, lds, s, g, R, bits, pids, counts, base, d_out);
