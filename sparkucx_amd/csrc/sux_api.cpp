@@ -472,8 +472,9 @@ int sux_partitioner_create(sux_node* node, const sux_partitioner_desc* d, sux_pa
         packed[2 * i] = hi;
         packed[2 * i + 1] = lo;
       }
-      // top-12-bit lookup: candidate answer interval per key prefix
-      const int bits = 12;
+      // top-10-bit lookup (4 KiB, LDS-resident in the v3 kernels): candidate answer interval
+      // per key prefix
+      const int bits = sux::kLutBits;
       std::vector<uint32_t> lut((size_t)1 << bits);
       auto count_less = [&](uint64_t hi, uint64_t lo) {  // #{bounds < (hi, lo)}
         int a = 0, b = R - 1;

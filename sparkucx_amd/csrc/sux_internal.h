@@ -10,6 +10,7 @@ namespace sux {
 
 constexpr int kMaxPartitions = 32768;  // LDS histogram: 128 KiB of u32 counters at the limit
 constexpr int kMaxRecordSize = 4096;
+constexpr int kLutBits = 10;  // range-partitioner prefix lookup: 1024 u32 entries
 
 // Device-side partitioner (P1).  Range bounds are pre-packed as (hi, lo) big-endian words so a
 // key compare is two unsigned 64-bit compares.

@@ -153,6 +153,15 @@ __device__ __forceinline__ TileRange tile_range(const MapGroup& g, uint32_t gtil
   return tr;
 }
 
+// Workgroup b -> work index, so that the ~gridDim/8 workgroups the dispatcher deals to one XCD
+// (b, b+8, b+16, ...) get one contiguous range of tiles.  A bijection on [0, n); placement is a
+// speed hint only, never a correctness assumption.
+__device__ __forceinline__ uint32_t xcd_map(uint32_t b, uint32_t n) {
+  const uint32_t per = (n + 7) / 8, rem = n % 8, x = b % 8, k = b / 8;
+  if (rem == 0 || x < rem) return x * per + k;
+  return rem * per + (x - rem) * (per - 1) + k;
+}
+
 // ------------------------------------------------------------------------------------------
 // K1: partition ids + per-tile histogram
 // ------------------------------------------------------------------------------------------
@@ -199,12 +208,21 @@ __global__ __launch_bounds__(256) void k_tile_scan(uint32_t* counts, uint64_t* t
   if (row >= rows) return;
   uint32_t* c = counts + (uint64_t)row * tiles;
   uint32_t carry = 0;
-  for (uint32_t t0 = 0; t0 < tiles; t0 += kWave) {
-    uint32_t t = t0 + lane;
-    uint32_t v = t < tiles ? c[t] : 0u;
-    uint32_t inc = wave_incl_scan(v, lane);
-    if (t < tiles) c[t] = carry + inc - v;
-    carry += __shfl(inc, kWave - 1, kWave);
+  constexpr int U = 8;  // all loads of 8 x 64 tiles in flight before the first scan
+  for (uint32_t t0 = 0; t0 < tiles; t0 += kWave * U) {
+    uint32_t v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint32_t t = t0 + k * kWave + lane;
+      v[k] = t < tiles ? c[t] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint32_t t = t0 + k * kWave + lane;
+      const uint32_t inc = wave_incl_scan(v[k], lane);
+      if (t < tiles) c[t] = carry + inc - v[k];
+      carry += __shfl(inc, kWave - 1, kWave);
+    }
   }
   if (lane == 0) totals[row] = carry;
 }
@@ -483,7 +501,7 @@ __global__ __launch_bounds__(256) void k_scatter2(MapGroup g, int R, int pid_bit
   using St = Stage<S, CH>;
   constexpr uint32_t W = S / 4;  // dwords per record
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-  const uint32_t gtile = blockIdx.x * 4 + wave;
+  const uint32_t gtile = xcd_map(blockIdx.x, gridDim.x) * 4 + wave;
   if (gtile >= g.num_maps * g.tiles_per_map) return;
   const TileRange tr = tile_range(g, gtile);
   if (tr.begin >= tr.end) return;
@@ -531,6 +549,124 @@ __global__ __launch_bounds__(256) void k_scatter2(MapGroup g, int R, int pid_bit
     }
     __builtin_amdgcn_wave_barrier();
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// v3 hist: register streaming.  Each lane loads the key dwords of RPL records straight to
+// registers (all loads issued before the first use), the range table (bounds + 10-bit prefix
+// LUT) lives in LDS so no dependent global load stalls the stream, and workgroups are mapped
+// XCD-contiguously (T1) so neighbouring tiles share an L2.
+// ------------------------------------------------------------------------------------------
+
+template <bool TAB>
+__device__ __forceinline__ int range_search_t(int R, const uint64_t* bounds, const uint32_t* lut,
+                                              uint64_t hi, uint64_t lo) {
+  const uint32_t e = lut[hi >> (64 - kLutBits)];
+  int a = e & 0xFFFFu, b = e >> 16;
+  while (a < b) {
+    const int mid = (a + b) >> 1;
+    const uint64_t bh = bounds[2 * mid], bl = bounds[2 * mid + 1];
+    if ((bh < hi) || (bh == hi && bl < lo)) a = mid + 1; else b = mid;
+  }
+  return a;
+}
+
+// P1 from preloaded little-endian key dwords (key at a 4-byte aligned record offset).
+template <int KW, bool TAB>
+__device__ __forceinline__ int partition_words(const PartDev& pd, const uint32_t (&w)[KW],
+                                               const uint64_t* bounds, const uint32_t* lut) {
+  const int R = pd.R;
+  switch (pd.kind) {
+    case 1: {
+      if (R == 1) return 0;
+      uint64_t hi = (uint64_t)__builtin_bswap32(w[0]) << 32, lo = 0;
+      if constexpr (KW > 1) hi |= __builtin_bswap32(w[1]);
+      if constexpr (KW > 2) lo = (uint64_t)__builtin_bswap32(w[2]) << 32;
+      if constexpr (KW > 3) lo |= __builtin_bswap32(w[3]);
+      const int len = pd.key_len;
+      if (len < 8) {
+        hi &= ~0ull << (8 * (8 - len));
+        lo = 0;
+      } else if (len < 16) {
+        lo = (len == 8) ? 0 : (lo & (~0ull << (8 * (16 - len))));
+      }
+      const int p = range_search_t<TAB>(R, bounds, lut, hi, lo);
+      return pd.ascending ? p : (R - 1) - p;
+    }
+    case 2: {
+      uint32_t h1 = mix_h1((uint32_t)pd.seed, mix_k1(w[0]));
+      if constexpr (KW > 1) h1 = mix_h1(h1, mix_k1(w[1]));
+      return pmod((int32_t)fmix32(h1, 8), R);
+    }
+    case 3:
+      return pmod((int32_t)fmix32(mix_h1((uint32_t)pd.seed, mix_k1(w[0])), 4), R);
+    case 5: {
+      uint32_t h = w[0];
+      if constexpr (KW > 1) h ^= w[1];
+      const int32_t r = (int32_t)h % R;
+      return r + (r < 0 ? R : 0);
+    }
+    case 6: {
+      const int32_t r = (int32_t)w[0] % R;
+      return r + (r < 0 ? R : 0);
+    }
+  }
+  return 0;
+}
+
+template <int KW, int RPL, bool TAB>
+__global__ __launch_bounds__(256) void k_hist3(PartDev pd, MapGroup g, uint16_t* __restrict__ pids,
+                                               uint32_t* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t ldsq[];
+  const int R = pd.R;
+  const int nb = TAB ? 2 * (R - 1) : 0;
+  uint64_t* sb = ldsq;
+  uint32_t* slut = reinterpret_cast<uint32_t*>(ldsq + nb);
+  uint32_t* hist_all = slut + (TAB ? (1 << kLutBits) : 0);
+  if constexpr (TAB) {
+    for (int i = threadIdx.x; i < nb; i += 256) sb[i] = pd.bounds[i];
+    for (int i = threadIdx.x; i < (1 << kLutBits); i += 256) slut[i] = pd.lut[i];
+  }
+  for (int i = threadIdx.x; i < 4 * R; i += 256) hist_all[i] = 0;
+  __syncthreads();
+  const uint64_t* bounds = TAB ? sb : pd.bounds;
+  const uint32_t* lut = TAB ? slut : pd.lut;
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  uint32_t* hist = hist_all + wave * R;
+  const uint32_t gtile = xcd_map(blockIdx.x, gridDim.x) * 4 + wave;
+  if (gtile >= g.num_maps * g.tiles_per_map) return;
+  const TileRange tr = tile_range(g, gtile);
+  const uint8_t* keys = g.recs + pd.key_offset;
+  for (uint64_t i0 = tr.begin; i0 < tr.end; i0 += kWave * RPL) {
+    uint32_t w[RPL][KW];
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) {
+      const uint64_t i = i0 + k * kWave + lane;
+      const uint32_t* rp = reinterpret_cast<const uint32_t*>(keys + (i < tr.end ? i : tr.begin) * g.rec_size);
+#pragma unroll
+      for (int c = 0; c < KW; ++c) w[k][c] = rp[c];
+    }
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) {
+      const uint64_t i = i0 + k * kWave + lane;
+      if (i < tr.end) {
+        const int p = partition_words<KW, TAB>(pd, w[k], bounds, lut);
+        pids[i] = (uint16_t)p;
+        atomicAdd(&hist[p], 1u);
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  uint32_t* dst = counts + ((uint64_t)tr.map * R) * g.tiles_per_map + tr.tile;
+  for (int p = lane; p < R; p += kWave) dst[(uint64_t)p * g.tiles_per_map] = hist[p];
+}
+
+template <int KW, bool TAB>
+static void launch_hist3_kw(dim3 grid, size_t lds, hipStream_t s, const PartDev& pd,
+                            const MapGroup& g, uint16_t* pids, uint32_t* counts) {
+  constexpr int RPL = 4;
+  hipLaunchKernelGGL((k_hist3<KW, RPL, TAB>), grid, dim3(256), lds, s, pd, g, pids, counts);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -618,65 +754,71 @@ static hipError_t launch_scatter(uint32_t S, dim3 grid, size_t lds, hipStream_t 
   return hipGetLastError();
 }
 
+// Kernel variants (A/B only; defaults are the fastest measured).  SUX_HIST = v1|v2|v3,
+// SUX_SCATTER = v1|v2.
+static int env_variant(const char* name, int dflt) {
+  const char* e = getenv(name);
+  if (e && e[0] == 'v' && e[1] >= '1' && e[1] <= '9') return e[1] - '0';
+  return dflt;
+}
+
 hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const LayoutDesc& lay,
                                   uint8_t* d_out, int64_t* d_index, uint8_t* d_index_be,
                                   uint16_t* d_pids, uint8_t* d_ws, const Workspace& ws,
                                   uint64_t* d_peer_bytes, Timer* timer, hipStream_t s) {
   const int R = pd.R;
-  const int wpg = waves_per_group(R);
+  const uint32_t S = g.rec_size;
   const uint32_t total_tiles = g.num_maps * g.tiles_per_map;
-  const dim3 grid((total_tiles + wpg - 1) / wpg);
-  const size_t lds = (size_t)wpg * R * 4;
   uint32_t* counts = reinterpret_cast<uint32_t*>(d_ws + ws.counts_off);
   uint64_t* totals = reinterpret_cast<uint64_t*>(d_ws + ws.totals_off);
   uint64_t* base = reinterpret_cast<uint64_t*>(d_ws + ws.base_off);
   uint16_t* pids = d_pids ? d_pids : reinterpret_cast<uint16_t*>(d_ws + ws.pids_off);
   int bits = 0;
   while ((1 << bits) < R) ++bits;
+  const int wpg = waves_per_group(R);
+  const dim3 grid1((total_tiles + wpg - 1) / wpg), grid4((total_tiles + 3) / 4);
+  const size_t lds1 = (size_t)wpg * R * 4;
 
-  // v2 (LDS-staged) kernels for the two record shapes of the configs; v1 otherwise
-  static const bool force_v1 = [] {
-    const char* e = getenv("SUX_KERNEL");
-    return e && e[0] == 'v' && e[1] == '1';
-  }();
-  const bool v2 = !force_v1 && (g.rec_size == 100 || g.rec_size == 16) && R <= 4096;
-  const dim3 grid4((total_tiles + 3) / 4);
-  size_t lds_h = 0, lds_s = 0;
-  static const bool ch64 = [] {
-    const char* e = getenv("SUX_CHUNK");
-    return e && atoi(e) == 64;
-  }();
-  if (v2) {
-    lds_h = 4 * (size_t)(g.rec_size == 100 ? (ch64 ? hist2_wave_bytes<100, 64>(R)
-                                                   : hist2_wave_bytes<100, 128>(R))
-                                           : hist2_wave_bytes<16, 512>(R));
-    lds_s = 4 * (size_t)(g.rec_size == 100 ? (ch64 ? scatter2_wave_bytes<100, 64>(R)
-                                                   : scatter2_wave_bytes<100, 128>(R))
-                                           : scatter2_wave_bytes<16, 512>(R));
-    allow_lds(reinterpret_cast<const void*>(&k_hist2<100, 64>), lds_h);
-    allow_lds(reinterpret_cast<const void*>(&k_scatter2<100, 64>), lds_s);
-    allow_lds(reinterpret_cast<const void*>(&k_hist2<100, 128>), lds_h);
-    allow_lds(reinterpret_cast<const void*>(&k_hist2<16, 512>), lds_h);
-    allow_lds(reinterpret_cast<const void*>(&k_scatter2<100, 128>), lds_s);
-    allow_lds(reinterpret_cast<const void*>(&k_scatter2<16, 512>), lds_s);
-  }
-
-  allow_lds(reinterpret_cast<const void*>(&k_hist<1>), lds);
+  // ---- K1: pids + tile histograms
+  static const int hv = env_variant("SUX_HIST", 3);
+  const bool shaped = (S == 100 || S == 16) && R <= 4096;  // v2 instantiations
+  const bool words = pd.kind != 4 && pd.key_offset % 4 == 0 && pd.key_len <= 16;
+  int hist = 1;
+  if (hv >= 3 && words && R <= 4096) hist = 3;
+  else if (hv >= 2 && shaped) hist = 2;
   timer_begin(timer, kHist, s);
-  if (v2 && g.rec_size == 100 && ch64)
-    hipLaunchKernelGGL((k_hist2<100, 64>), grid4, dim3(256), lds_h, s, pd, g, pids, counts);
-  else if (v2 && g.rec_size == 100)
-    hipLaunchKernelGGL((k_hist2<100, 128>), grid4, dim3(256), lds_h, s, pd, g, pids, counts);
-  else if (v2)
-    hipLaunchKernelGGL((k_hist2<16, 512>), grid4, dim3(256), lds_h, s, pd, g, pids, counts);
-  else if (wpg == 4)
-    hipLaunchKernelGGL((k_hist<4>), grid, dim3(4 * kWave), lds, s, pd, g, pids, counts);
-  else
-    hipLaunchKernelGGL((k_hist<1>), grid, dim3(kWave), lds, s, pd, g, pids, counts);
+  if (hist == 3) {
+    const bool tab = pd.kind == 1 && R > 1 && (size_t)(R - 1) * 16 + (4u << kLutBits) + 16u * R <= 64 * 1024;
+    const size_t lds = (tab ? (size_t)(R - 1) * 16 + (4u << kLutBits) : 0) + 16u * R;
+    const int kw = (pd.key_len + 3) / 4;
+#define SUX_H3(KW)                                                              \
+  (tab ? launch_hist3_kw<KW, true>(grid4, lds, s, pd, g, pids, counts)           \
+       : launch_hist3_kw<KW, false>(grid4, lds, s, pd, g, pids, counts))
+    if (kw <= 1) SUX_H3(1);
+    else if (kw == 2) SUX_H3(2);
+    else if (kw == 3) SUX_H3(3);
+    else SUX_H3(4);
+#undef SUX_H3
+  } else if (hist == 2) {
+    const size_t lds = 4 * (size_t)(S == 100 ? hist2_wave_bytes<100, 128>(R) : hist2_wave_bytes<16, 512>(R));
+    allow_lds(reinterpret_cast<const void*>(&k_hist2<100, 128>), lds);
+    allow_lds(reinterpret_cast<const void*>(&k_hist2<16, 512>), lds);
+    if (S == 100)
+      hipLaunchKernelGGL((k_hist2<100, 128>), grid4, dim3(256), lds, s, pd, g, pids, counts);
+    else
+      hipLaunchKernelGGL((k_hist2<16, 512>), grid4, dim3(256), lds, s, pd, g, pids, counts);
+  } else {
+    allow_lds(reinterpret_cast<const void*>(&k_hist<1>), lds1);
+    if (wpg == 4)
+      hipLaunchKernelGGL((k_hist<4>), grid1, dim3(4 * kWave), lds1, s, pd, g, pids, counts);
+    else
+      hipLaunchKernelGGL((k_hist<1>), grid1, dim3(kWave), lds1, s, pd, g, pids, counts);
+  }
   timer_end(timer, kHist, s);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
 
+  // ---- K2: scans -> index tables + destination bases
   timer_begin(timer, kScan, s);
   const uint32_t rows = g.num_maps * (uint32_t)R;
   hipLaunchKernelGGL(k_tile_scan, dim3((rows + 3) / 4), dim3(256), 0, s, counts, totals, rows,
@@ -687,23 +829,26 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   e = hipGetLastError();
   if (e != hipSuccess) return e;
 
+  // ---- K3: stable scatter
+  static const int sv = env_variant("SUX_SCATTER", 2);
   timer_begin(timer, kScatter, s);
-  if (v2 && g.rec_size == 100 && ch64) {
-    hipLaunchKernelGGL((k_scatter2<100, 64>), grid4, dim3(256), lds_s, s, g, R, bits, pids,
-                       counts, base, d_out);
+  if (sv >= 2 && shaped) {
+    const size_t lds = 4 * (size_t)(S == 100 ? scatter2_wave_bytes<100, 128>(R)
+                                             : scatter2_wave_bytes<16, 512>(R));
+    allow_lds(reinterpret_cast<const void*>(&k_scatter2<100, 128>), lds);
+    allow_lds(reinterpret_cast<const void*>(&k_scatter2<16, 512>), lds);
+    if (S == 100)
+      hipLaunchKernelGGL((k_scatter2<100, 128>), grid4, dim3(256), lds, s, g, R, bits, pids,
+                         counts, base, d_out);
+    else
+      hipLaunchKernelGGL((k_scatter2<16, 512>), grid4, dim3(256), lds, s, g, R, bits, pids,
+                         counts, base, d_out);
     e = hipGetLastError();
-  } else if (v2 && g.rec_size == 100) {
-    hipLaunchKernelGGL((k_scatter2<100, 128>), grid4, dim3(256), lds_s, s, g, R, bits, pids,
-                       counts, base, d_out);
-    e = hipGetLastError();
-  } else if (v2) {
-    hipLaunchKernelGGL((k_scatter2<16, 512>), grid4, dim3(256), lds_s, s, g, R, bits, pids,
-                       counts, base, d_out);
-    e = hipGetLastError();
-  } else if (wpg == 4)
-    e = launch_scatter<4>(g.rec_size, grid, lds, s, g, R, bits, pids, counts, base, d_out);
-  else
-    e = launch_scatter<1>(g.rec_size, grid, lds, s, g, R, bits, pids, counts, base, d_out);
+  } else if (wpg == 4) {
+    e = launch_scatter<4>(S, grid1, lds1, s, g, R, bits, pids, counts, base, d_out);
+  } else {
+    e = launch_scatter<1>(S, grid1, lds1, s, g, R, bits, pids, counts, base, d_out);
+  }
   timer_end(timer, kScatter, s);
   return e;
 }
