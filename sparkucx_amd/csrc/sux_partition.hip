@@ -662,6 +662,245 @@ __global__ __launch_bounds__(256) void k_hist3(PartDev pd, MapGroup g, uint16_t*
   for (int p = lane; p < R; p += kWave) dst[(uint64_t)p * g.tiles_per_map] = hist[p];
 }
 
+// ------------------------------------------------------------------------------------------
+// v4 scatter: run writer.  One 256-thread workgroup owns 4 consecutive hist tiles of a map and
+// walks them in chunks of C records staged in LDS.  Per chunk it counts partition ids per wave
+// (ballot match, stable), scans them into a partition-sorted order of the chunk, and writes
+// every partition's run as ALIGNED 16-byte units of the destination: the sub-16-byte tail of a
+// run is kept in LDS (`carry`) and completed by the next chunk, so except at the two ends of
+// the workgroup's range every store is a full, aligned global_store_dwordx4 along a contiguous
+// run — the pattern that streams at copy speed (tools/hbm_probe: copy_x4 vs perm100_dword).
+// ------------------------------------------------------------------------------------------
+template <uint32_t S, uint32_t C>
+struct Sc4 {
+  static constexpr uint32_t W = S / 4;                       // dwords per record
+  static constexpr uint32_t kBuf = Stage<S, C>::kBufBytes;   // staged records
+  static constexpr uint32_t kSrc = ((C * 2 + 15) / 16) * 16; // u16 sorted -> chunk index
+  static constexpr uint32_t kPer = (Stage<S, C>::kUnits + 255) / 256;
+  // per-partition state, bytes per partition: pos u64, carry u32x4, wcnt 4 x u32,
+  // cstart/ustart u32 (R+1), first u32
+  static __host__ __device__ constexpr uint32_t lds_bytes(int R) {
+    return kBuf + kSrc + (uint32_t)R * (8 + 16 + 16 + 4) + ((uint32_t)R + 1) * 8 + 16;
+  }
+};
+
+// Exclusive block scan (256 threads) of `R` u64 values held in LDS `v` (in place); returns the
+// total.  Each thread scans a contiguous slice, then one wave scans the 256 slice sums.
+__device__ __forceinline__ uint64_t block_scan_lds(uint64_t* v, int R, uint64_t* tmp) {
+  const int t = threadIdx.x;
+  const int per = (R + 255) / 256;
+  const int lo = t * per, hi = min(R, lo + per);
+  uint64_t s = 0;
+  for (int i = lo; i < hi; ++i) s += v[i];
+  tmp[t] = s;
+  __syncthreads();
+  if (t < kWave) {
+    uint64_t a = tmp[4 * t], b = tmp[4 * t + 1], c = tmp[4 * t + 2], d = tmp[4 * t + 3];
+    uint64_t tot = a + b + c + d, inc = tot;
+#pragma unroll
+    for (int dd = 1; dd < kWave; dd <<= 1) {
+      uint64_t x = __shfl_up(inc, dd, kWave);
+      if (t >= dd) inc += x;
+    }
+    uint64_t ex = inc - tot;
+    tmp[4 * t] = ex;
+    tmp[4 * t + 1] = ex + a;
+    tmp[4 * t + 2] = ex + a + b;
+    tmp[4 * t + 3] = ex + a + b + c;
+    if (t == kWave - 1) tmp[256] = inc;
+  }
+  __syncthreads();
+  uint64_t run = tmp[t];
+  for (int i = lo; i < hi; ++i) {
+    uint64_t x = v[i];
+    v[i] = run;
+    run += x;
+  }
+  const uint64_t total = tmp[256];
+  __syncthreads();
+  return total;
+}
+
+template <uint32_t S, uint32_t C>
+__global__ __launch_bounds__(256) void k_scatter4(MapGroup g, int R, int pid_bits,
+                                                  const uint16_t* __restrict__ pids,
+                                                  const uint32_t* __restrict__ prefix,
+                                                  const uint64_t* __restrict__ base,
+                                                  uint8_t* __restrict__ out, uint32_t wg_per_map) {
+  using K = Sc4<S, C>;
+  constexpr uint32_t W = K::W, RPW = C / 4;  // records per wave per chunk
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  u32x4* buf = reinterpret_cast<u32x4*>(lds8);
+  uint16_t* srcidx = reinterpret_cast<uint16_t*>(lds8 + K::kBuf);
+  uint8_t* st = lds8 + K::kBuf + K::kSrc;
+  uint64_t* pos = reinterpret_cast<uint64_t*>(st);              // [R] dest byte of next run byte
+  u32x4* carry = reinterpret_cast<u32x4*>(st + 8 * R);          // [R] pending sub-16B tail
+  uint32_t* wcnt = reinterpret_cast<uint32_t*>(st + 24 * R);    // [4][R] per-wave counts/prefix
+  uint32_t* first = wcnt + 4 * R;                               // [R] head unit still partial
+  uint64_t* scan = reinterpret_cast<uint64_t*>(first + R);      // [R+1] (cstart<<32 | ustart)
+  __shared__ uint64_t tmp[257];
+
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const uint32_t wg = xcd_map(blockIdx.x, gridDim.x);
+  const uint32_t map = wg / wg_per_map, q4 = (wg - map * wg_per_map) * 4;
+  const uint64_t map_begin = (uint64_t)map * g.records_per_map;
+  uint64_t map_end = map_begin + g.records_per_map;
+  if (map_end > g.num_records) map_end = g.num_records;
+  const uint64_t begin = min(map_begin + (uint64_t)q4 * g.tile_recs, map_end);
+  const uint64_t end = min(begin + 4ull * g.tile_recs, map_end);
+  if (begin >= end) return;  // uniform for the workgroup
+
+  // initial state: destination of this workgroup's first record of every partition
+  const uint64_t* bm = base + (uint64_t)map * R;
+  const uint32_t* pm = prefix + (uint64_t)map * R * g.tiles_per_map + q4;
+  for (int p = tid; p < R; p += 256) {
+    const uint64_t d = (bm[p] + pm[(uint64_t)p * g.tiles_per_map]) * S;
+    pos[p] = d;
+    first[p] = (uint32_t)(d & 15) >> 2;  // foreign dwords in the first unit (0 = aligned)
+  }
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  uint32_t* out32 = reinterpret_cast<uint32_t*>(out);
+
+  for (uint64_t c0 = begin; c0 < end; c0 += C) {
+    const uint32_t n = (uint32_t)min<uint64_t>(C, end - c0);
+    // 1. stage the chunk (16-byte coalesced loads, all issued before the LDS writes)
+    uint32_t head;
+    {
+      const uint8_t* a = g.recs + c0 * S;
+      head = (uint32_t)(reinterpret_cast<uintptr_t>(a) & 15u);
+      const u32x4* src = reinterpret_cast<const u32x4*>(a - head);
+      const uint32_t units = (head + n * S + 15) >> 4;
+      u32x4 v[K::kPer];
+#pragma unroll
+      for (uint32_t k = 0; k < K::kPer; ++k) {
+        const uint32_t u = tid + k * 256;
+        if (u < units) v[k] = src[u];
+      }
+      for (int p = tid; p < 4 * R; p += 256) wcnt[p] = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < K::kPer; ++k) {
+        const uint32_t u = tid + k * 256;
+        if (u < units) buf[u] = v[k];
+      }
+    }
+    __syncthreads();
+    // 2. per-wave stable ranks (wave w owns chunk records [w*RPW, (w+1)*RPW))
+    uint32_t my_pid[RPW / kWave], my_rank[RPW / kWave];
+    uint32_t* wc = wcnt + wave * R;
+#pragma unroll
+    for (uint32_t j = 0; j < RPW / kWave; ++j) {
+      const uint32_t r = wave * RPW + j * kWave + lane;
+      const bool valid = r < n;
+      const uint32_t pid = valid ? pids[c0 + r] : 0u;
+      uint64_t peers = __ballot(valid);
+      for (int bb = 0; bb < pid_bits; ++bb) {
+        const bool bit = (pid >> bb) & 1u;
+        const uint64_t m = __ballot(bit);
+        peers &= bit ? m : ~m;
+      }
+      uint32_t r0 = 0;
+      if (valid) r0 = wc[pid];
+      __builtin_amdgcn_wave_barrier();
+      if (valid && (peers & lt_mask) == 0) wc[pid] = r0 + (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+      my_pid[j] = valid ? pid : 0xFFFFFFFFu;
+      my_rank[j] = r0 + (uint32_t)__popcll(peers & lt_mask);
+    }
+    __syncthreads();
+    // 3. cross-wave prefix, chunk counts, full 16-B units per partition; scan both
+    for (int p = tid; p < R; p += 256) {
+      uint32_t a = wcnt[p], b = wcnt[R + p], c = wcnt[2 * R + p], d = wcnt[3 * R + p];
+      wcnt[p] = 0;
+      wcnt[R + p] = a;
+      wcnt[2 * R + p] = a + b;
+      wcnt[3 * R + p] = a + b + c;
+      const uint32_t cnt = a + b + c + d;
+      const uint32_t full = (uint32_t)(((pos[p] & 15) + (uint64_t)cnt * S) >> 4);
+      scan[p] = ((uint64_t)cnt << 32) | full;
+    }
+    __syncthreads();
+    const uint64_t tot = block_scan_lds(scan, R, tmp);
+    if (tid == 0) scan[R] = tot;
+    __syncthreads();
+    // 4. partition-sorted position of every chunk record
+#pragma unroll
+    for (uint32_t j = 0; j < RPW / kWave; ++j) {
+      const uint32_t pid = my_pid[j];
+      if (pid != 0xFFFFFFFFu) {
+        const uint32_t sp = (uint32_t)(scan[pid] >> 32) + wcnt[wave * R + pid] + my_rank[j];
+        srcidx[sp] = (uint16_t)(wave * RPW + j * kWave + lane);
+      }
+    }
+    __syncthreads();
+    // 5. write every full destination unit of every run
+    const uint32_t U = (uint32_t)scan[R];
+    const uint32_t* bw = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(buf) + head);
+    for (uint32_t q = tid; q < U; q += 256) {
+      int lo = 0, hi = R - 1;  // last p with ustart[p] <= q
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((uint32_t)scan[mid] <= q) lo = mid; else hi = mid - 1;
+      }
+      const int p = lo;
+      const uint32_t k = q - (uint32_t)scan[p];
+      const uint64_t ps = pos[p];
+      const uint32_t cdw = (uint32_t)(ps & 15) >> 2, cs = (uint32_t)(scan[p] >> 32);
+      uint32_t val[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint32_t v = 4 * k + c;
+        if (v < cdw) {
+          val[c] = carry[p][c];
+        } else {
+          const uint32_t t = v - cdw, rr = t / W, ww = t - rr * W;
+          val[c] = bw[(uint32_t)srcidx[cs + rr] * W + ww];
+        }
+      }
+      const uint64_t A = (ps & ~15ull) + 16ull * k;
+      const uint32_t skip = (k == 0) ? first[p] : 0u;
+      if (skip == 0) {
+        *reinterpret_cast<u32x4*>(out + A) = u32x4{val[0], val[1], val[2], val[3]};
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if ((uint32_t)c >= skip) out32[(A >> 2) + c] = val[c];
+      }
+    }
+    __syncthreads();
+    // 6. advance: new tail (carry) and position of every partition
+    for (int p = tid; p < R; p += 256) {
+      const uint32_t cnt = (uint32_t)(scan[p + 1] >> 32) - (uint32_t)(scan[p] >> 32);
+      if (cnt == 0) continue;
+      const uint64_t ps = pos[p];
+      const uint32_t cdw = (uint32_t)(ps & 15) >> 2, cs = (uint32_t)(scan[p] >> 32);
+      const uint64_t np = ps + (uint64_t)cnt * S;
+      const uint32_t ndw = (uint32_t)(np & 15) >> 2, total = cdw + cnt * W;
+      const u32x4 old = carry[p];
+      uint32_t nv[4] = {0, 0, 0, 0};
+      for (uint32_t c = 0; c < ndw; ++c) {
+        const uint32_t v = total - ndw + c;
+        if (v < cdw) {
+          nv[c] = old[v];
+        } else {
+          const uint32_t t = v - cdw, rr = t / W, ww = t - rr * W;
+          nv[c] = bw[(uint32_t)srcidx[cs + rr] * W + ww];
+        }
+      }
+      carry[p] = u32x4{nv[0], nv[1], nv[2], nv[3]};
+      if (((ps & 15) + (uint64_t)cnt * S) >= 16) first[p] = 0;  // head unit has been written
+      pos[p] = np;
+    }
+    __syncthreads();
+  }
+  // 7. flush the tails (the next workgroup's range completes these units)
+  for (int p = tid; p < R; p += 256) {
+    const uint64_t ps = pos[p];
+    const uint32_t cdw = (uint32_t)(ps & 15) >> 2;
+    const u32x4 cv = carry[p];
+    for (uint32_t c = first[p]; c < cdw; ++c) out32[((ps & ~15ull) >> 2) + c] = cv[c];
+  }
+}
+
 template <int KW, bool TAB>
 static void launch_hist3_kw(dim3 grid, size_t lds, hipStream_t s, const PartDev& pd,
                             const MapGroup& g, uint16_t* pids, uint32_t* counts) {
@@ -830,9 +1069,30 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   if (e != hipSuccess) return e;
 
   // ---- K3: stable scatter
-  static const int sv = env_variant("SUX_SCATTER", 2);
+  static const int sv = env_variant("SUX_SCATTER", 4);
+  static const bool c256 = [] {
+    const char* e = getenv("SUX_S4C");
+    return e && atoi(e) == 256;
+  }();
+  const bool run_writer = sv >= 4 && S == 100 && R <= 1024 &&
+                          (reinterpret_cast<uintptr_t>(d_out) & 15) == 0;
   timer_begin(timer, kScatter, s);
-  if (sv >= 2 && shaped) {
+  if (run_writer) {
+    const uint32_t wpm = (g.tiles_per_map + 3) / 4;
+    const dim3 grid((uint32_t)(g.num_maps * wpm));
+    if (c256) {
+      const size_t lds = Sc4<100, 256>::lds_bytes(R);
+      allow_lds(reinterpret_cast<const void*>(&k_scatter4<100, 256>), lds);
+      hipLaunchKernelGGL((k_scatter4<100, 256>), grid, dim3(256), lds, s, g, R, bits, pids, counts,
+                         base, d_out, wpm);
+    } else {
+      const size_t lds = Sc4<100, 512>::lds_bytes(R);
+      allow_lds(reinterpret_cast<const void*>(&k_scatter4<100, 512>), lds);
+      hipLaunchKernelGGL((k_scatter4<100, 512>), grid, dim3(256), lds, s, g, R, bits, pids, counts,
+                         base, d_out, wpm);
+    }
+    e = hipGetLastError();
+  } else if (sv >= 2 && shaped) {
     const size_t lds = 4 * (size_t)(S == 100 ? scatter2_wave_bytes<100, 128>(R)
                                              : scatter2_wave_bytes<16, 512>(R));
     allow_lds(reinterpret_cast<const void*>(&k_scatter2<100, 128>), lds);
