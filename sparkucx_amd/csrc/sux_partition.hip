@@ -614,6 +614,33 @@ __device__ __forceinline__ int partition_words(const PartDev& pd, const uint32_t
   return 0;
 }
 
+template <int KW>
+struct KeyVec;
+template <>
+struct KeyVec<1> {
+  typedef uint32_t T;
+  static __device__ __forceinline__ void get(T v, uint32_t (&w)[1]) { w[0] = v; }
+};
+template <>
+struct KeyVec<2> {
+  typedef uint32_t T __attribute__((ext_vector_type(2), aligned(4)));
+  static __device__ __forceinline__ void get(T v, uint32_t (&w)[2]) { w[0] = v.x; w[1] = v.y; }
+};
+template <>
+struct KeyVec<3> {
+  typedef uint32_t T __attribute__((ext_vector_type(3), aligned(4)));
+  static __device__ __forceinline__ void get(T v, uint32_t (&w)[3]) {
+    w[0] = v.x; w[1] = v.y; w[2] = v.z;
+  }
+};
+template <>
+struct KeyVec<4> {
+  typedef uint32_t T __attribute__((ext_vector_type(4), aligned(4)));
+  static __device__ __forceinline__ void get(T v, uint32_t (&w)[4]) {
+    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+  }
+};
+
 template <int KW, int RPL, bool TAB>
 __global__ __launch_bounds__(256) void k_hist3(PartDev pd, MapGroup g, uint16_t* __restrict__ pids,
                                                uint32_t* __restrict__ counts) {
@@ -622,7 +649,8 @@ __global__ __launch_bounds__(256) void k_hist3(PartDev pd, MapGroup g, uint16_t*
   const int nb = TAB ? 2 * (R - 1) : 0;
   uint64_t* sb = ldsq;
   uint32_t* slut = reinterpret_cast<uint32_t*>(ldsq + nb);
-  uint32_t* hist_all = slut + (TAB ? (1 << kLutBits) : 0);
+  uint16_t* pbuf_all = reinterpret_cast<uint16_t*>(slut + (TAB ? (1 << kLutBits) : 0));
+  uint32_t* hist_all = reinterpret_cast<uint32_t*>(pbuf_all + 4 * kWave * RPL);
   if constexpr (TAB) {
     for (int i = threadIdx.x; i < nb; i += 256) sb[i] = pd.bounds[i];
     for (int i = threadIdx.x; i < (1 << kLutBits); i += 256) slut[i] = pd.lut[i];
@@ -633,27 +661,40 @@ __global__ __launch_bounds__(256) void k_hist3(PartDev pd, MapGroup g, uint16_t*
   const uint32_t* lut = TAB ? slut : pd.lut;
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   uint32_t* hist = hist_all + wave * R;
+  uint16_t* pbuf = pbuf_all + wave * kWave * RPL;
   const uint32_t gtile = xcd_map(blockIdx.x, gridDim.x) * 4 + wave;
   if (gtile >= g.num_maps * g.tiles_per_map) return;
   const TileRange tr = tile_range(g, gtile);
   const uint8_t* keys = g.recs + pd.key_offset;
+  typedef typename KeyVec<KW>::T KV;
   for (uint64_t i0 = tr.begin; i0 < tr.end; i0 += kWave * RPL) {
-    uint32_t w[RPL][KW];
+    KV kv[RPL];
 #pragma unroll
     for (int k = 0; k < RPL; ++k) {
       const uint64_t i = i0 + k * kWave + lane;
-      const uint32_t* rp = reinterpret_cast<const uint32_t*>(keys + (i < tr.end ? i : tr.begin) * g.rec_size);
-#pragma unroll
-      for (int c = 0; c < KW; ++c) w[k][c] = rp[c];
+      kv[k] = *reinterpret_cast<const KV*>(keys + (i < tr.end ? i : tr.begin) * g.rec_size);
     }
+    // whole 8-record groups of this block go out as 16-byte pid stores via LDS
+    const bool packed = (tr.end - i0 >= (uint64_t)kWave * RPL) &&
+                        ((reinterpret_cast<uintptr_t>(pids + i0) & 15) == 0);
 #pragma unroll
     for (int k = 0; k < RPL; ++k) {
       const uint64_t i = i0 + k * kWave + lane;
       if (i < tr.end) {
-        const int p = partition_words<KW, TAB>(pd, w[k], bounds, lut);
-        pids[i] = (uint16_t)p;
+        uint32_t w[KW];
+        KeyVec<KW>::get(kv[k], w);
+        const int p = partition_words<KW, TAB>(pd, w, bounds, lut);
         atomicAdd(&hist[p], 1u);
+        if (packed) pbuf[k * kWave + lane] = (uint16_t)p;
+        else pids[i] = (uint16_t)p;
       }
+    }
+    if (packed) {
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      if (lane < kWave * RPL / 8)
+        reinterpret_cast<u32x4*>(pids + i0)[lane] = reinterpret_cast<const u32x4*>(pbuf)[lane];
+      __builtin_amdgcn_wave_barrier();
     }
   }
   __builtin_amdgcn_wave_barrier();
@@ -901,6 +942,207 @@ __global__ __launch_bounds__(256) void k_scatter4(MapGroup g, int R, int pid_bit
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// v5 scatter: the chunk is staged straight into a partition-sorted LDS image laid out in
+// DESTINATION-UNIT space.  Partition p's run of this chunk starts at LDS unit lbase[p] at the
+// same phase (pos[p] mod 16) it has in the output, with p's carried tail in front of it, so the
+// LDS unit q maps to ONE aligned 16-byte destination unit dstu[q].  The writer is then
+// ds_read_b128 + global_store_dwordx4 per unit.  The staging loads are issued before the ranking
+// so their latency hides behind it.
+// ------------------------------------------------------------------------------------------
+template <uint32_t S, uint32_t C>
+struct Sc5 {
+  static constexpr uint32_t W = S / 4;
+  static constexpr uint32_t kUnits = (C * S + 12 + 15) / 16;  // staged global units (<=12 B head)
+  static constexpr uint32_t kPer = (kUnits + 255) / 256;
+  // sum_p ceil((cd_p + cnt_p*W)/4) <= (C*W + 6R)/4 + 1
+  static __host__ __device__ constexpr uint32_t space(int R) {
+    return (C * S) / 16 + (3u * R + 1) / 2 + 1;
+  }
+  static __host__ __device__ constexpr uint32_t lds_bytes(int R) {
+    return space(R) * 16 + space(R) * 4 + C * 4 + (uint32_t)R * (8 + 16 + 16 + 8 + 4 + 4) + 16;
+  }
+};
+constexpr uint32_t kNoUnit = 0xFFFFFFFFu;    // tail unit still partial: becomes the carry
+constexpr uint32_t kUnitMask = (1u << 29) - 1;  // dstu: unit index | (foreign head dwords << 29)
+
+template <uint32_t S, uint32_t C>
+__global__ __launch_bounds__(256) void k_scatter5(MapGroup g, int R, int pid_bits,
+                                                  const uint16_t* __restrict__ pids,
+                                                  const uint32_t* __restrict__ prefix,
+                                                  const uint64_t* __restrict__ base,
+                                                  uint8_t* __restrict__ out, uint32_t wg_per_map) {
+  using K = Sc5<S, C>;
+  constexpr uint32_t W = K::W, RPW = C / 4, NG = (RPW + kWave - 1) / kWave;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  const uint32_t SP = K::space(R);
+  u32x4* img = reinterpret_cast<u32x4*>(lds8);                  // [SP] sorted image
+  uint32_t* img32 = reinterpret_cast<uint32_t*>(lds8);
+  u32x4* carry = img + SP;                                       // [R] pending tail dwords
+  uint64_t* pos = reinterpret_cast<uint64_t*>(carry + R);        // [R] next output byte of p
+  uint64_t* lbase = pos + R;                                     // [R] image unit of p's run
+  uint32_t* dstu = reinterpret_cast<uint32_t*>(lbase + R);       // [SP] destination unit
+  uint32_t* recoff = dstu + SP;                                  // [C] image byte of record
+  uint32_t* wcnt = recoff + C;                                   // [4][R]
+  uint32_t* cnt = wcnt + 4 * R;                                  // [R]
+  uint32_t* first = cnt + R;                                     // [R] foreign head dwords
+  __shared__ uint64_t tmp[257];
+
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const uint32_t wg = xcd_map(blockIdx.x, gridDim.x);
+  const uint32_t map = wg / wg_per_map, q4 = (wg - map * wg_per_map) * 4;
+  const uint64_t map_begin = (uint64_t)map * g.records_per_map;
+  const uint64_t map_end = min(map_begin + g.records_per_map, g.num_records);
+  const uint64_t begin = min(map_begin + (uint64_t)q4 * g.tile_recs, map_end);
+  const uint64_t end = min(begin + 4ull * g.tile_recs, map_end);
+  if (begin >= end) return;  // uniform for the workgroup
+
+  const uint64_t* bm = base + (uint64_t)map * R;
+  const uint32_t* pm = prefix + (uint64_t)map * R * g.tiles_per_map + q4;
+  for (int p = tid; p < R; p += 256) {
+    const uint64_t d = (bm[p] + pm[(uint64_t)p * g.tiles_per_map]) * S;
+    pos[p] = d;
+    first[p] = (uint32_t)(d & 15) >> 2;
+    carry[p] = u32x4{0, 0, 0, 0};
+  }
+  for (int i = tid; i < 4 * R; i += 256) wcnt[i] = 0;
+  __syncthreads();
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  uint32_t* out32 = reinterpret_cast<uint32_t*>(out);
+
+  for (uint64_t c0 = begin; c0 < end; c0 += C) {
+    const uint32_t n = (uint32_t)min<uint64_t>(C, end - c0);
+    // 1. issue the pid loads and the staging loads (clamped: no branches, all in flight)
+    uint32_t pidv[NG];
+#pragma unroll
+    for (uint32_t j = 0; j < NG; ++j) {
+      const uint32_t r = wave * RPW + min(j * kWave + lane, RPW - 1);
+      pidv[j] = pids[c0 + min(r, n - 1)];
+    }
+    const uint8_t* a = g.recs + c0 * S;
+    const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(a) & 15u);
+    const u32x4* src = reinterpret_cast<const u32x4*>(a - head);
+    const uint32_t units = (head + n * S + 15) >> 4;
+    u32x4 v[K::kPer];
+#pragma unroll
+    for (uint32_t k = 0; k < K::kPer; ++k) v[k] = src[min(tid + k * 256u, units - 1)];
+    // 2. stable per-wave ranks
+    uint32_t my_pid[NG], my_rank[NG];
+    uint32_t* wc = wcnt + wave * R;
+#pragma unroll
+    for (uint32_t j = 0; j < NG; ++j) {
+      const uint32_t r = wave * RPW + j * kWave + lane;
+      const bool valid = (j * kWave + lane < RPW) && r < n;
+      const uint32_t pid = valid ? pidv[j] : 0u;
+      uint64_t peers = __ballot(valid);
+      for (int bb = 0; bb < pid_bits; ++bb) {
+        const bool bit = (pid >> bb) & 1u;
+        const uint64_t m = __ballot(bit);
+        peers &= bit ? m : ~m;
+      }
+      uint32_t r0 = 0;
+      if (valid) r0 = wc[pid];
+      __builtin_amdgcn_wave_barrier();
+      if (valid && (peers & lt_mask) == 0) wc[pid] = r0 + (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+      my_pid[j] = valid ? pid : kNoUnit;
+      my_rank[j] = r0 + (uint32_t)__popcll(peers & lt_mask);
+    }
+    __syncthreads();
+    // 3. per partition: cross-wave prefix, count, image units (carry + run, rounded up)
+    for (int p = tid; p < R; p += 256) {
+      const uint32_t x0 = wcnt[p], x1 = wcnt[R + p], x2 = wcnt[2 * R + p], x3 = wcnt[3 * R + p];
+      wcnt[p] = 0;
+      wcnt[R + p] = x0;
+      wcnt[2 * R + p] = x0 + x1;
+      wcnt[3 * R + p] = x0 + x1 + x2;
+      const uint32_t c = x0 + x1 + x2 + x3;
+      cnt[p] = c;
+      const uint32_t cd = (uint32_t)(pos[p] & 15) >> 2;
+      lbase[p] = (cd + c * W + 3) >> 2;
+    }
+    __syncthreads();
+    block_scan_lds(lbase, R, tmp);  // ends with a barrier
+    // 4. image offsets of the records, destination units they own, carries in front of runs
+    for (int p = tid; p < R; p += 256) {
+      const uint32_t c = cnt[p], cd = (uint32_t)(pos[p] & 15) >> 2, lb = (uint32_t)lbase[p];
+      const uint32_t full = (cd + c * W) >> 2, space = (cd + c * W + 3) >> 2;
+      const u32x4 cv = carry[p];
+      for (uint32_t i = 0; i < cd; ++i) img32[4 * lb + i] = cv[i];
+      if (space) {  // unit 0 starts in the carry or at the run's first byte: owned here
+        const uint32_t u0 = (uint32_t)(pos[p] >> 4);
+        dstu[lb] = full ? (u0 | (first[p] << 29)) : kNoUnit;
+      }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < NG; ++j) {
+      const uint32_t p = my_pid[j];
+      if (p == kNoUnit) continue;
+      const uint32_t jr = wcnt[wave * R + p] + my_rank[j];
+      const uint32_t c = cnt[p], cd = (uint32_t)(pos[p] & 15) >> 2, lb = (uint32_t)lbase[p];
+      const uint32_t o = 4 * cd + jr * S;  // byte of this record in p's run image
+      recoff[wave * RPW + j * kWave + lane] = 16 * lb + o;
+      const uint32_t full = (cd + c * W) >> 2, space = (cd + c * W + 3) >> 2;
+      const uint32_t u0 = (uint32_t)(pos[p] >> 4);
+      for (uint32_t k = (o + 15) >> 4; k * 16 < o + S && k < space; ++k)
+        if (k) dstu[lb + k] = k < full ? (u0 + k) : kNoUnit;
+    }
+    __syncthreads();
+    // 5. staged units -> image (dword granular: records sit at 4-byte phases)
+#pragma unroll
+    for (uint32_t k = 0; k < K::kPer; ++k) {
+      const uint32_t u = tid + k * 256;
+      if (u < units) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int32_t b = (int32_t)(16 * u + 4 * c) - (int32_t)head;
+          if (b >= 0 && (uint32_t)b < n * S) {
+            const uint32_t r = (uint32_t)b / S, off = (uint32_t)b - r * S;
+            img32[(recoff[r] + off) >> 2] = v[k][c];
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // 6. writer: one aligned 16-byte store per completed destination unit
+    const uint32_t U = (uint32_t)tmp[256];
+    for (uint32_t q = tid; q < U; q += 256) {
+      const uint32_t d = dstu[q];
+      if (d == kNoUnit) continue;
+      const u32x4 x = img[q];
+      const uint32_t skip = d >> 29;
+      const uint64_t A = (uint64_t)(d & kUnitMask) * 16;
+      if (skip == 0) {
+        *reinterpret_cast<u32x4*>(out + A) = x;
+      } else {
+#pragma unroll
+        for (uint32_t c = 0; c < 4; ++c)
+          if (c >= skip) out32[(A >> 2) + c] = x[c];
+      }
+    }
+    __syncthreads();
+    // 7. new carries and positions
+    for (int p = tid; p < R; p += 256) {
+      const uint32_t c = cnt[p];
+      if (c == 0) continue;
+      const uint32_t cd = (uint32_t)(pos[p] & 15) >> 2, lb = (uint32_t)lbase[p];
+      const uint32_t full = (cd + c * W) >> 2, rest = (cd + c * W) & 3;
+      if (rest) carry[p] = img[lb + full];
+      if (full) first[p] = 0;
+      pos[p] += (uint64_t)c * S;
+    }
+    for (int i = tid; i < 4 * R; i += 256) wcnt[i] = 0;
+    __syncthreads();
+  }
+  // 8. flush the tails (the next range's workgroup writes the rest of these units)
+  for (int p = tid; p < R; p += 256) {
+    const uint64_t ps = pos[p];
+    const uint32_t cd = (uint32_t)(ps & 15) >> 2;
+    const u32x4 cv = carry[p];
+    for (uint32_t c = first[p]; c < cd; ++c) out32[((ps & ~15ull) >> 2) + c] = cv[c];
+  }
+}
+
 template <int KW, bool TAB>
 static void launch_hist3_kw(dim3 grid, size_t lds, hipStream_t s, const PartDev& pd,
                             const MapGroup& g, uint16_t* pids, uint32_t* counts) {
@@ -1027,8 +1269,9 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   else if (hv >= 2 && shaped) hist = 2;
   timer_begin(timer, kHist, s);
   if (hist == 3) {
-    const bool tab = pd.kind == 1 && R > 1 && (size_t)(R - 1) * 16 + (4u << kLutBits) + 16u * R <= 64 * 1024;
-    const size_t lds = (tab ? (size_t)(R - 1) * 16 + (4u << kLutBits) : 0) + 16u * R;
+    const bool tab = pd.kind == 1 && R > 1 &&
+                     (size_t)(R - 1) * 16 + (4u << kLutBits) + 2048 + 16u * R <= 64 * 1024;
+    const size_t lds = (tab ? (size_t)(R - 1) * 16 + (4u << kLutBits) : 0) + 2048 + 16u * R;
     const int kw = (pd.key_len + 3) / 4;
 #define SUX_H3(KW)                                                              \
   (tab ? launch_hist3_kw<KW, true>(grid4, lds, s, pd, g, pids, counts)           \
@@ -1069,7 +1312,14 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   if (e != hipSuccess) return e;
 
   // ---- K3: stable scatter
-  static const int sv = env_variant("SUX_SCATTER", 4);
+  static const int sv = env_variant("SUX_SCATTER", 5);
+  static const bool c128 = [] {
+    const char* e = getenv("SUX_S5C");
+    return e && atoi(e) == 128;
+  }();
+  const bool unit_writer = sv >= 5 && S == 100 && R <= 1024 &&
+                           (reinterpret_cast<uintptr_t>(d_out) & 15) == 0 &&
+                           g.num_records * S < (1ull << 33);
   static const bool c256 = [] {
     const char* e = getenv("SUX_S4C");
     return e && atoi(e) == 256;
@@ -1077,7 +1327,22 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   const bool run_writer = sv >= 4 && S == 100 && R <= 1024 &&
                           (reinterpret_cast<uintptr_t>(d_out) & 15) == 0;
   timer_begin(timer, kScatter, s);
-  if (run_writer) {
+  if (unit_writer) {
+    const uint32_t wpm = (g.tiles_per_map + 3) / 4;
+    const dim3 grid((uint32_t)(g.num_maps * wpm));
+    if (c128) {
+      const size_t lds = Sc5<100, 128>::lds_bytes(R);
+      allow_lds(reinterpret_cast<const void*>(&k_scatter5<100, 128>), lds);
+      hipLaunchKernelGGL((k_scatter5<100, 128>), grid, dim3(256), lds, s, g, R, bits, pids, counts,
+                         base, d_out, wpm);
+    } else {
+      const size_t lds = Sc5<100, 256>::lds_bytes(R);
+      allow_lds(reinterpret_cast<const void*>(&k_scatter5<100, 256>), lds);
+      hipLaunchKernelGGL((k_scatter5<100, 256>), grid, dim3(256), lds, s, g, R, bits, pids, counts,
+                         base, d_out, wpm);
+    }
+    e = hipGetLastError();
+  } else if (run_writer) {
     const uint32_t wpm = (g.tiles_per_map + 3) / 4;
     const dim3 grid((uint32_t)(g.num_maps * wpm));
     if (c256) {
