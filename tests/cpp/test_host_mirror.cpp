@@ -1,0 +1,195 @@
+// test_host_mirror.cpp — the C++ plugin mirror (include/sparkucx_amd/ucx_shuffle.hpp) end to end
+// on one GPU, checked against the CPU oracle (oracle/oracle.c, test infrastructure).
+// Reads like the reference's own flow: registerShuffle -> getWriter(...).write -> index commit ->
+// getReader(...).read / UcxShuffleClient.fetchBlocks -> listener callbacks -> release.
+#include <hip/hip_runtime_api.h>
+
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/sparkucx_amd/ucx_shuffle.hpp"
+#include "../../oracle/oracle.h"
+
+using namespace sparkucx;
+
+static int failures = 0;
+#define EXPECT(cond, ...)                                      \
+  do {                                                         \
+    if (!(cond)) {                                             \
+      ++failures;                                              \
+      fprintf(stderr, "FAIL %s:%d: %s  ", __FILE__, __LINE__, #cond); \
+      fprintf(stderr, __VA_ARGS__);                            \
+      fprintf(stderr, "\n");                                   \
+    }                                                          \
+  } while (0)
+
+#define HIP_OK(x)                                  \
+  do {                                             \
+    if ((x) != hipSuccess) {                       \
+      fprintf(stderr, "%s failed\n", #x);          \
+      exit(2);                                     \
+    }                                              \
+  } while (0)
+
+static std::vector<uint8_t> d2h(const void* p, uint64_t n) {
+  std::vector<uint8_t> h(n);
+  if (n && hipMemcpy(h.data(), p, n, hipMemcpyDeviceToHost) != hipSuccess) {
+    fprintf(stderr, "hipMemcpy failed\n");
+    exit(2);
+  }
+  return h;
+}
+
+int main() {
+  const int R = 50, S = 100, M = 4, per = 3000;
+  const int counts[M] = {per, per, per, 1700};
+  std::vector<uint8_t> bounds((R - 1) * 10);
+  o_range_bounds_uniform(R, 10, bounds.data());
+  sux_partitioner_desc pdesc{SUX_PART_RANGE_BYTES, R, 0, 10, 42, 1, bounds.data()};
+  o_part opart{1, R, 0, 10, 42, 1, bounds.data()};
+
+  // executor components must be initialised before writers (IllegalStateException analog)
+  {
+    UcxShuffleManager m(UcxShuffleConf(std::map<std::string, std::string>{{"spark.shuffle.ucx.gpu.device", "0"}}), false);
+    bool threw = false;
+    try {
+      UcxShuffleHandle h;
+      m.getWriter(h, 1, 0);
+    } catch (const UcxException& e) {
+      threw = e.code() == SUX_ESTATE;
+    }
+    EXPECT(threw, "getWriter before the node starts must throw IllegalStateException-like");
+  }
+
+  UcxShuffleConf conf(std::map<std::string, std::string>{{"spark.shuffle.ucx.memory.minBufferSize", "1k"},
+                       {"spark.shuffle.ucx.memory.minAllocationSize", "4"},
+                       {"spark.shuffle.ucx.rkeySize", "150"}});
+  EXPECT(conf.minRegistrationSize() == (4u << 20), "minAllocationSize bare number is MiB");
+  EXPECT(conf.metadataBlockSize() == 300, "metadata block = 2 * rkeySize");
+  UcxShuffleManager manager(conf, /*isDriver=*/true);
+  UcxShuffleHandle h = manager.registerShuffle(7, M, pdesc, S);
+  EXPECT(h.desc.directory_bytes == (uint64_t)M * 300, "directory sized by maps (Q1 fix)");
+
+  // map side: inputs on the device, one writer per map task (attempt id 100+i, partition i)
+  std::vector<std::vector<uint8_t>> in(M), want_data(M), want_be(M);
+  std::vector<std::vector<int64_t>> want_len(M), want_idx(M);
+  std::map<int64_t, int> mapIdToBlockIndex;
+  uint64_t first = 0;
+  for (int i = 0; i < M; ++i) {
+    in[i].resize((size_t)counts[i] * S);
+    o_gen_terasort(9, first, counts[i], in[i].data());
+    void* dev = nullptr;
+    HIP_OK(hipMalloc(&dev, in[i].size()));
+    HIP_OK(hipMemcpy(dev, in[i].data(), in[i].size(), hipMemcpyHostToDevice));
+    UcxShuffleWriter w = manager.getWriter(h, 100 + i, i);
+    w.write(dev, counts[i]);
+    HIP_OK(hipFree(dev));
+    want_data[i].resize(in[i].size());
+    want_len[i].resize(R);
+    want_idx[i].resize(R + 1);
+    want_be[i].resize(8 * (R + 1));
+    o_write_map(&opart, in[i].data(), counts[i], S, want_data[i].data(), want_len[i].data(),
+                want_idx[i].data(), want_be[i].data());
+    EXPECT(w.getPartitionLengths() == want_len[i], "map %d lengths", i);
+    EXPECT(manager.shuffleBlockResolver().getIndexFile(7, i, R) == want_be[i], "map %d index", i);
+    mapIdToBlockIndex[100 + i] = i;
+    first += counts[i];
+  }
+
+  // reduce side: batch fetch of [10, 23) from every map, through the reader
+  {
+    UcxShuffleReader reader = manager.getReader(h, 10, 23, mapIdToBlockIndex);
+    auto got = reader.read();
+    EXPECT(got.failures.empty(), "reader failures: %zu", got.failures.size());
+    EXPECT(got.blocks.size() == (size_t)M, "blocks: %zu", got.blocks.size());
+    for (auto& kv : got.blocks) {
+      ShuffleBlockId b = ShuffleBlockId::parse(kv.first);
+      int m = mapIdToBlockIndex[b.mapId];
+      int64_t s = want_idx[m][10], e = want_idx[m][23];
+      auto bytes = d2h(kv.second.devicePtr(), kv.second.size());
+      EXPECT((int64_t)bytes.size() == e - s, "block %s size", kv.first.c_str());
+      EXPECT(std::memcmp(bytes.data(), want_data[m].data() + s, bytes.size()) == 0,
+             "block %s bytes", kv.first.c_str());
+      kv.second.release();
+    }
+  }
+
+  // single blocks through the client, including failures the reference never reports
+  {
+    struct Collect : BlockFetchingListener {
+      std::map<std::string, std::vector<uint8_t>> ok;
+      std::vector<std::string> failed;
+      void onBlockFetchSuccess(const std::string& id, ManagedBuffer b) override {
+        ok[id] = d2h(b.devicePtr(), b.size());
+        b.release();
+      }
+      void onBlockFetchFailure(const std::string& id, const std::exception&) override {
+        failed.push_back(id);
+      }
+    } l;
+    UcxShuffleClient client(7, manager.ucxNode(), mapIdToBlockIndex);
+    std::vector<std::string> ids = {"shuffle_7_102_0",  "shuffle_7_100_49", "shuffle_7_103_5_9",
+                                    "shuffle_7_999_1",  "bogus_block",      "shuffle_7_101_3"};
+    client.fetchBlocks("localhost", 0, "exec-1", ids, l);
+    EXPECT(l.failed.size() == 2, "two failures expected, got %zu", l.failed.size());
+    auto check_block = [&](const std::string& id, int m, int s, int e) {
+      auto it = l.ok.find(id);
+      EXPECT(it != l.ok.end(), "missing %s", id.c_str());
+      if (it == l.ok.end()) return;
+      int64_t a = want_idx[m][s], b = want_idx[m][e];
+      EXPECT((int64_t)it->second.size() == b - a &&
+                 std::memcmp(it->second.data(), want_data[m].data() + a, b - a) == 0,
+             "bytes of %s", id.c_str());
+    };
+    check_block("shuffle_7_102_0", 2, 0, 1);
+    check_block("shuffle_7_100_49", 0, 49, 50);
+    check_block("shuffle_7_103_5_9", 3, 5, 9);
+    check_block("shuffle_7_101_3", 1, 3, 4);
+  }
+
+  // writeIndexFileAndCommit of an externally produced map output (second shuffle)
+  {
+    UcxShuffleHandle h2 = manager.registerShuffle(8, 2, pdesc, S);
+    void* dev = nullptr;
+    HIP_OK(hipMalloc(&dev, want_data[1].size()));
+    HIP_OK(hipMemcpy(dev, want_data[1].data(), want_data[1].size(), hipMemcpyHostToDevice));
+    manager.shuffleBlockResolver().writeIndexFileAndCommit(8, 555, want_len[1], dev,
+                                                           want_data[1].size(), 1);
+    HIP_OK(hipFree(dev));
+    EXPECT(manager.shuffleBlockResolver().getIndexFile(8, 1, R) == want_be[1], "committed index");
+    // a mismatching length table is refused
+    bool threw = false;
+    std::vector<int64_t> bad = want_len[1];
+    bad[0] += 100;
+    try {
+      manager.shuffleBlockResolver().writeIndexFileAndCommit(8, 556, bad, nullptr, 0, 0);
+    } catch (const UcxException& e) {
+      threw = e.code() == SUX_EINVAL;
+    }
+    EXPECT(threw, "bad lengths must be refused");
+    UcxShuffleReader reader = manager.getReader(h2, 0, R, {{555, 1}});
+    auto got = reader.read();
+    EXPECT(got.blocks.size() == 1 && got.failures.empty(), "whole-map batch");
+    if (!got.blocks.empty()) {
+      auto bytes = d2h(got.blocks[0].second.devicePtr(), got.blocks[0].second.size());
+      EXPECT(bytes == want_data[1], "whole-map bytes");
+      got.blocks[0].second.release();
+    }
+    // map 0 of shuffle 8 was never committed: its block fails
+    UcxShuffleReader r0 = manager.getReader(h2, 0, 1, {{554, 0}});
+    EXPECT(r0.read().failures.size() == 1, "uncommitted map must fail");
+    EXPECT(manager.unregisterShuffle(8), "unregister");
+    EXPECT(!manager.unregisterShuffle(8), "second unregister is false");
+  }
+
+  manager.stop();
+  if (failures) {
+    fprintf(stderr, "%d failure(s)\n", failures);
+    return 1;
+  }
+  printf("host mirror ok\n");
+  return 0;
+}
