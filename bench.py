@@ -114,6 +114,8 @@ def main():
     ap.add_argument("--records", type=int, default=0, help="records per GPU (0 = workload default)")
     ap.add_argument("--map-records", type=int, default=1 << 20, help="records per map batch")
     ap.add_argument("--group-maps", type=int, default=8, help="map batches per kernel launch group")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="N=1: launch groups dealt round-robin to this many HIP streams")
     ap.add_argument("--cpu-records", type=int, default=10_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-reps", type=int, default=3)
@@ -167,9 +169,13 @@ def main():
     if world == 1:
         out = torch.empty(n * rs, dtype=torch.uint8, device=dev)
         index_be = torch.empty(maps * (R + 1) * 8, dtype=torch.uint8, device=dev)
-        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        ns = max(1, args.streams)
+        streams = [comp] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
+        wss = [torch.empty(ws_bytes, dtype=torch.uint8, device=dev) for _ in range(ns)]
 
         def step():
+            for s in streams[1:]:
+                s.wait_stream(comp)
             for g in range(groups):
                 r0 = g * group_recs
                 r1 = min(n, r0 + group_recs)
@@ -179,7 +185,9 @@ def main():
                                     out=out[r0 * rs:r1 * rs],
                                     index=index[m0 * (R + 1):(m0 + mg) * (R + 1)],
                                     index_be=index_be[m0 * (R + 1) * 8:(m0 + mg) * (R + 1) * 8],
-                                    workspace=ws, stream=comp)
+                                    workspace=wss[g % ns], stream=streams[g % ns])
+            for s in streams[1:]:
+                comp.wait_stream(s)
     else:
         comm = torch.cuda.Stream(dev)
         send = [torch.empty(group_recs * rs, dtype=torch.uint8, device=dev) for _ in range(2)]
@@ -283,6 +291,7 @@ def main():
         "config": {"workload": f"{args.workload}: {n} x {rs}-byte records per GPU "
                                f"({n * rs / 1e9:.0f} GB/GPU, {n * rs * world / 1e9:.0f} GB total), "
                                f"R={R}, map batches of {rpm} records, {gm} maps per launch group"
+                               + (f" on {args.streams} streams" if world == 1 and args.streams > 1 else "")
                                + (", zero-copy local block resolve" if world == 1 else
                                   ", partition-aligned ncclAllToAllv exchange"),
                    "global_batch": n * world, "seq_len": rs, "parallelism": f"shuffle{world}"},

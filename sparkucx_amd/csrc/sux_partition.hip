@@ -966,7 +966,7 @@ struct Sc5 {
 constexpr uint32_t kNoUnit = 0xFFFFFFFFu;    // tail unit still partial: becomes the carry
 constexpr uint32_t kUnitMask = (1u << 29) - 1;  // dstu: unit index | (foreign head dwords << 29)
 
-template <uint32_t S, uint32_t C>
+template <uint32_t S, uint32_t C, bool NT>
 __global__ __launch_bounds__(256) void k_scatter5(MapGroup g, int R, int pid_bits,
                                                   const uint16_t* __restrict__ pids,
                                                   const uint32_t* __restrict__ prefix,
@@ -1113,7 +1113,10 @@ __global__ __launch_bounds__(256) void k_scatter5(MapGroup g, int R, int pid_bit
       const uint32_t skip = d >> 29;
       const uint64_t A = (uint64_t)(d & kUnitMask) * 16;
       if (skip == 0) {
-        *reinterpret_cast<u32x4*>(out + A) = x;
+        if constexpr (NT)
+          __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(out + A));
+        else
+          *reinterpret_cast<u32x4*>(out + A) = x;
       } else {
 #pragma unroll
         for (uint32_t c = 0; c < 4; ++c)
@@ -1328,19 +1331,25 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
                           (reinterpret_cast<uintptr_t>(d_out) & 15) == 0;
   timer_begin(timer, kScatter, s);
   if (unit_writer) {
+    static const bool nt = [] {
+      const char* e = getenv("SUX_NT_STORE");
+      return e && e[0] == '1';
+    }();
     const uint32_t wpm = (g.tiles_per_map + 3) / 4;
     const dim3 grid((uint32_t)(g.num_maps * wpm));
+#define SUX_S5(CC, NTV)                                                                        \
+  do {                                                                                        \
+    const size_t lds = Sc5<100, CC>::lds_bytes(R);                                            \
+    allow_lds(reinterpret_cast<const void*>(&k_scatter5<100, CC, NTV>), lds);                 \
+    hipLaunchKernelGGL((k_scatter5<100, CC, NTV>), grid, dim3(256), lds, s, g, R, bits, pids, \
+                       counts, base, d_out, wpm);                                             \
+  } while (0)
     if (c128) {
-      const size_t lds = Sc5<100, 128>::lds_bytes(R);
-      allow_lds(reinterpret_cast<const void*>(&k_scatter5<100, 128>), lds);
-      hipLaunchKernelGGL((k_scatter5<100, 128>), grid, dim3(256), lds, s, g, R, bits, pids, counts,
-                         base, d_out, wpm);
+      if (nt) SUX_S5(128, true); else SUX_S5(128, false);
     } else {
-      const size_t lds = Sc5<100, 256>::lds_bytes(R);
-      allow_lds(reinterpret_cast<const void*>(&k_scatter5<100, 256>), lds);
-      hipLaunchKernelGGL((k_scatter5<100, 256>), grid, dim3(256), lds, s, g, R, bits, pids, counts,
-                         base, d_out, wpm);
+      if (nt) SUX_S5(256, true); else SUX_S5(256, false);
     }
+#undef SUX_S5
     e = hipGetLastError();
   } else if (run_writer) {
     const uint32_t wpm = (g.tiles_per_map + 3) / 4;

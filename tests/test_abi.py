@@ -72,3 +72,11 @@ def test_plan_group_matches_restatement(W, M, R):
         assert pos == sum(got[2])
         if hi < R:
             assert lib.sux_plan_block_offset(W, rank, M, R, gi.ctypes.data, 0, 0, hi) == -1
+
+
+def test_bench_bounds_match_oracle():
+    import bench
+    from oracle import oracle as O
+
+    for R in (2, 7, 200, 10000):
+        assert bench.uniform_bounds(R) == O.uniform_range_bounds(R, 10)
