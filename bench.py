@@ -114,6 +114,11 @@ def main():
     ap.add_argument("--records", type=int, default=0, help="records per GPU (0 = workload default)")
     ap.add_argument("--map-records", type=int, default=1 << 20, help="records per map batch")
     ap.add_argument("--group-maps", type=int, default=8, help="map batches per kernel launch group")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "ipc"],
+                    help="N>1 exchange: ncclAllToAllv, or one-sided pull over HIP IPC")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="test mode: every rank on cuda:0, gloo process group, ipc transport "
+                         "(exercises the N>1 pipeline on a 1-GPU box; not a benchmark)")
     ap.add_argument("--streams", type=int, default=1,
                     help="N=1: launch groups dealt round-robin to this many HIP streams")
     ap.add_argument("--cpu-records", type=int, default=10_000_000)
@@ -127,11 +132,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    rehearse = args.rehearse_one_gpu and world > 1
+    if rehearse:
+        args.transport, local = "ipc", 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+    ctl = torch.device("cpu") if rehearse else dev  # device of the small control collectives
 
     rs, R, gen, kind, key_len, n1, nN = WORKLOADS[args.workload]
     n = args.records or (n1 if world == 1 else nN)
@@ -142,13 +154,15 @@ def main():
 
     # ---- node + communicator bootstrap (unique id carried by torch.distributed) ----------
     comm_id = None
-    if world > 1:
+    if world > 1 and args.transport == "rccl":
         t = torch.zeros(128, dtype=torch.uint8, device=dev)
         if rank == 0:
             t.copy_(torch.frombuffer(bytearray(N.unique_id()), dtype=torch.uint8))
         dist.broadcast(t, 0)
         comm_id = bytes(t.cpu().numpy())
-    node = Node(device=local, rank=rank, world_size=world, comm_id=comm_id)
+    # the ipc transport needs no RCCL communicator inside the library
+    node = Node(device=local, rank=rank if comm_id else 0, world_size=world if comm_id else 1,
+                comm_id=comm_id)
     if kind == N.PART_RANGE_BYTES:
         part = node.partitioner(kind, R, key_offset=0, key_len=key_len, bounds=uniform_bounds(R))
     else:
@@ -190,44 +204,73 @@ def main():
                 comp.wait_stream(s)
     else:
         comm = torch.cuda.Stream(dev)
-        send = [torch.empty(group_recs * rs, dtype=torch.uint8, device=dev) for _ in range(2)]
+        # send-buffer ring: rccl frees slot s when ITS all-to-all is done (2 slots); ipc frees
+        # slot s only when every peer has pulled from it, which rank-locally is known once the
+        # NEXT group's all-gather completed (3 slots keep partition(k) off that dependency)
+        NB = 3 if args.transport == "ipc" else 2
+        send = [torch.empty(group_recs * rs, dtype=torch.uint8, device=dev) for _ in range(NB)]
         # receive ring (Spark's reducer consumes fetched blocks as a stream, maxBytesInFlight);
         # 1.5x the group's bytes absorbs uneven partition sizes
         recv = [torch.empty(int(group_recs * rs * 1.5) + (1 << 20), dtype=torch.uint8,
                             device=dev) for _ in range(2)]
         ws = [torch.empty(ws_bytes, dtype=torch.uint8, device=dev) for _ in range(2)]
-        gidx = [torch.empty(world * gm * (R + 1), dtype=torch.int64, device=dev) for _ in range(2)]
+        # one all-gathered index table per group (kept for the exact byte accounting)
+        gidx = torch.empty(groups, world * gm * (R + 1), dtype=torch.int64, device=dev)
+        rbytes = torch.zeros(groups, dtype=torch.int64, device=dev)
         peer = [torch.empty(world, dtype=torch.int64, device=dev) for _ in range(2)]
-        part_done = [torch.cuda.Event() for _ in range(2)]
-        send_free = [torch.cuda.Event() for _ in range(2)]
+        part_done = [torch.cuda.Event() for _ in range(NB)]
+        send_free = [torch.cuda.Event() for _ in range(NB)]
         xfer_ev = []
-        stats = {"recv_bytes": 0, "remote_bytes": 0}
+        if args.transport == "ipc":
+            # rkey analog: map every peer's two send buffers once
+            srcs = []
+            for sb in send:
+                hs = [None] * world
+                dist.all_gather_object(hs, node.ipc_handle(sb))
+                srcs.append(torch.tensor([sb.data_ptr() if g == rank else node.ipc_open(hs[g])
+                                          for g in range(world)], dtype=torch.int64, device=dev))
 
         def exchange(j):
-            s = j % 2
+            s = j % NB
             r0 = j * group_recs
             r1 = min(n, r0 + group_recs)
             m0 = j * gm
             mg = -(-(r1 - r0) // rpm)
+            gi = gidx[j, :world * mg * (R + 1)]
+            ix = index[m0 * (R + 1):(m0 + mg) * (R + 1)]
             comm.wait_event(part_done[s])
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(comm)
-            rb = node.exchange_group(send[s], index[m0 * (R + 1):(m0 + mg) * (R + 1)], mg, R,
-                                     gidx[s], recv[s], stream=comm)
+            if args.transport == "ipc":
+                with torch.cuda.stream(comm):
+                    # completes only after every rank finished partition(j) and pull(j-1)
+                    if rehearse:  # gloo: through the host (synchronous; a test of the logic)
+                        comm.synchronize()
+                        parts = [torch.empty(ix.numel(), dtype=torch.int64) for _ in range(world)]
+                        dist.all_gather(parts, ix.cpu())
+                        gi.copy_(torch.cat(parts).to(dev))
+                    else:
+                        dist.all_gather_into_tensor(gi, ix)
+                    send_free[(j - 1) % NB].record(comm)
+                    node.pull_group(world, rank, srcs[s], gi, mg, R, recv[j % 2],
+                                    rbytes[j:j + 1], stream=comm)
+            else:
+                rb = node.exchange_group(send[s], ix, mg, R, gi, recv[j % 2], stream=comm)
+                rbytes[j] = int(rb.sum())
+                send_free[s].record(comm)
             e1.record(comm)
             xfer_ev.append((e0, e1))
-            send_free[s].record(comm)
-            stats["recv_bytes"] += int(rb.sum())
-            stats["remote_bytes"] += int(rb.sum() - rb[rank])
 
         def step():
             for k in range(groups):
-                s = k % 2
+                s = k % NB
                 r0 = k * group_recs
                 r1 = min(n, r0 + group_recs)
                 m0 = k * gm
                 mg = -(-(r1 - r0) // rpm)
-                if k >= 2:
+                if k >= NB:
+                    # rccl: the all-to-all of k-2 has read send[s]; ipc: the all-gather of k-2
+                    # completed, so every peer finished pulling group k-3 out of send[s]
                     comp.wait_event(send_free[s])
                 node.partition_maps_peer_major(part, data[r0 * rs:r1 * rs], rs, rpm, world,
                                                num_records=r1 - r0, out=send[s],
@@ -254,7 +297,6 @@ def main():
     node.set_kernel_timing(True)
     if world > 1:
         xfer_ev.clear()
-        stats["recv_bytes"] = stats["remote_bytes"] = 0
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -266,7 +308,7 @@ def main():
 
     elapsed = t1 - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=ctl)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     ms_per_step = elapsed / args.steps * 1e3
@@ -293,7 +335,9 @@ def main():
                                f"R={R}, map batches of {rpm} records, {gm} maps per launch group"
                                + (f" on {args.streams} streams" if world == 1 and args.streams > 1 else "")
                                + (", zero-copy local block resolve" if world == 1 else
-                                  ", partition-aligned ncclAllToAllv exchange"),
+                                  ", partition-aligned ncclAllToAllv exchange"
+                                  if args.transport == "rccl" else
+                                  ", partition-aligned one-sided IPC pull exchange"),
                    "global_batch": n * world, "seq_len": rs, "parallelism": f"shuffle{world}"},
         "roofline": {"bound": "hbm", "achieved": None if achieved is None else round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -312,7 +356,18 @@ def main():
     if world > 1:
         torch.cuda.synchronize(dev)
         xms = sum(a.elapsed_time(b) for a, b in xfer_ev)
-        remote = stats["remote_bytes"]
+        # exact off-GPU bytes per step from the all-gathered index tables
+        gh = gidx.cpu().numpy()
+        lo, hi = (rank * R) // world, ((rank + 1) * R) // world
+        remote = 0
+        for j in range(groups):
+            mg = -(-(min(n, (j + 1) * group_recs) - j * group_recs) // rpm)
+            t = gh[j, :world * mg * (R + 1)].reshape(world, mg, R + 1)
+            own = t[:, :, hi] - t[:, :, lo]
+            remote += int(own.sum() - own[rank].sum())
+        if int(rbytes.min().item()) < 0:
+            raise RuntimeError("exchange overflowed a receive buffer")
+        remote *= args.steps
         peak = (world - 1) * XGMI_LINK_GBS
         ach = remote / (xms / 1e3) / 1e9 if xms else None
         result["roofline_exchange"] = {

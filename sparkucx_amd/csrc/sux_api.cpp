@@ -662,6 +662,50 @@ int sux_exchange_group(sux_node* node, const void* d_send, const int64_t* d_inde
   });
 }
 
+// ---- one-sided exchange over HIP IPC ----------------------------------------------------------
+int sux_ipc_get_handle(sux_node* node, const void* d_ptr, uint8_t out[64]) {
+  return guard([&] {
+    require(node && d_ptr && out, SUX_EINVAL, "NULL argument");
+    node->bind();
+    hipIpcMemHandle_t h;
+    static_assert(sizeof(h) == 64, "hipIpcMemHandle_t is 64 bytes");
+    hip_check(hipIpcGetMemHandle(&h, const_cast<void*>(d_ptr)), "hipIpcGetMemHandle");
+    std::memcpy(out, &h, 64);
+  });
+}
+
+int sux_ipc_open(sux_node* node, const uint8_t handle[64], void** d_ptr) {
+  return guard([&] {
+    require(node && handle && d_ptr, SUX_EINVAL, "NULL argument");
+    node->bind();
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handle, 64);
+    hip_check(hipIpcOpenMemHandle(d_ptr, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+  });
+}
+
+int sux_ipc_close(sux_node* node, void* d_ptr) {
+  return guard([&] {
+    require(node && d_ptr, SUX_EINVAL, "NULL argument");
+    node->bind();
+    hip_check(hipIpcCloseMemHandle(d_ptr), "hipIpcCloseMemHandle");
+  });
+}
+
+int sux_pull_group(sux_node* node, int32_t W, int32_t rank, const uint64_t* d_src_ptrs,
+                   const int64_t* d_gathered, int32_t M, int32_t R, void* d_recv, uint64_t cap,
+                   uint64_t* d_recv_bytes, void* stream) {
+  return guard([&] {
+    require(node && d_src_ptrs && d_gathered && d_recv, SUX_EINVAL, "NULL argument");
+    require(W >= 1 && rank >= 0 && rank < W && M >= 1 && R >= W, SUX_EINVAL, "bad pull shape");
+    node->bind();
+    hip_check(sux::launch_pull(W, rank, d_src_ptrs, d_gathered, M, R,
+                               static_cast<uint8_t*>(d_recv), cap, d_recv_bytes,
+                               node->stream(stream)),
+              "pull launch");
+  });
+}
+
 // ---- shuffle lifecycle ---------------------------------------------------------------------
 int sux_register_shuffle(sux_node* node, int32_t shuffle_id, int32_t num_maps, int32_t R,
                          int32_t rec_size, sux_handle_desc* out) {

@@ -54,3 +54,85 @@ hipError_t launch_gather_copy(const CopyDesc* d_desc, uint32_t n, uint32_t chunk
 }
 
 }  // namespace sux
+
+namespace sux {
+
+// ---------------------------------------------------------------------------------------------
+// One-sided pull of a peer-major launch group (sux_pull_group).  Workgroup b serves source
+// g = b / per_src and strides over that source's range.  Every workgroup first derives, from the
+// all-gathered index tables, where this rank's share sits in g's send buffer and where it goes
+// in the receive buffer (the arithmetic of sux_plan_group, done on the device).
+// ---------------------------------------------------------------------------------------------
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+__device__ __forceinline__ int32_t owner_lo_d(int32_t h, int32_t R, int32_t W) {
+  return (int32_t)(((int64_t)h * R) / W);
+}
+
+__global__ __launch_bounds__(256) void k_pull(int32_t W, int32_t me, const uint64_t* __restrict__ srcs,
+                                              const int64_t* __restrict__ gi, int32_t M, int32_t R,
+                                              uint8_t* __restrict__ recv, uint64_t cap,
+                                              uint64_t* recv_bytes, uint32_t per_src) {
+  __shared__ uint64_t red[3][256];
+  const int32_t g = blockIdx.x / per_src;
+  const uint32_t slot = blockIdx.x - g * per_src;
+  const int64_t stride = (int64_t)R + 1;
+  const int32_t lo = owner_lo_d(me, R, W), hi = owner_lo_d(me + 1, R, W);
+  // per thread partial sums: [0] offset of my share in g's buffer, [1] its size,
+  // [2] bytes from sources before g (my receive offset), [3] everything (total received)
+  uint64_t a = 0, b = 0, c = 0, tot = 0;
+  for (int32_t t = threadIdx.x; t < W * M; t += 256) {
+    const int32_t gg = t / M, m = t - gg * M;
+    const int64_t* ix = gi + ((int64_t)gg * M + m) * stride;
+    const uint64_t mine = (uint64_t)(ix[hi] - ix[lo]);
+    tot += mine;
+    if (gg < g) c += mine;
+    if (gg == g) {
+      b += mine;
+      a += (uint64_t)(ix[lo] - ix[0]);  // shares of peers < me in g's peer-major buffer
+    }
+  }
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = b;
+  red[2][threadIdx.x] = c;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s)
+      for (int k = 0; k < 3; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + s];
+    __syncthreads();
+  }
+  const uint64_t src_off = red[0][0], size = red[1][0], dst_off = red[2][0];
+  __syncthreads();
+  red[0][threadIdx.x] = tot;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[0][threadIdx.x] += red[0][threadIdx.x + s];
+    __syncthreads();
+  }
+  const uint64_t total = red[0][0];
+  if (blockIdx.x == 0 && threadIdx.x == 0 && recv_bytes) *recv_bytes = total > cap ? ~0ull : total;
+  if (total > cap) return;
+  // g's buffer is [peer h][map m][partitions of h]: my share starts after every peer h < me,
+  // i.e. at sum_m sum_{h<me} (ix[hi_h] - ix[lo_h]) = sum_m (ix[lo_me] - ix[0]), and holds my
+  // ranges of maps 0..M-1 in order — exactly the [source][map][partition] receive layout.
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(srcs[g]) + src_off;
+  uint8_t* dst = recv + dst_off;
+  // 16-byte pieces (4-byte aligned on both sides), then the dword tail
+  const uint64_t n16 = size / 16;
+  for (uint64_t i = (uint64_t)slot * 256 + threadIdx.x; i < n16; i += (uint64_t)per_src * 256)
+    *reinterpret_cast<u32x4a4*>(dst + 16 * i) = *reinterpret_cast<const u32x4a4*>(src + 16 * i);
+  for (uint64_t i = n16 * 16 + ((uint64_t)slot * 256 + threadIdx.x) * 4; i < size;
+       i += (uint64_t)per_src * 256 * 4)
+    *reinterpret_cast<uint32_t*>(dst + i) = *reinterpret_cast<const uint32_t*>(src + i);
+}
+
+hipError_t launch_pull(int32_t W, int32_t me, const uint64_t* srcs, const int64_t* gi, int32_t M,
+                       int32_t R, uint8_t* recv, uint64_t cap, uint64_t* recv_bytes,
+                       hipStream_t s) {
+  const uint32_t per_src = 1024 / (uint32_t)(W > 0 ? W : 1) + 1;
+  hipLaunchKernelGGL(k_pull, dim3(per_src * W), dim3(256), 0, s, W, me, srcs, gi, M, R, recv, cap,
+                     recv_bytes, per_src);
+  return hipGetLastError();
+}
+
+}  // namespace sux

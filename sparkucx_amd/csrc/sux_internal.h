@@ -82,6 +82,11 @@ struct CopyDesc {
 hipError_t launch_gather_copy(const CopyDesc* d_desc, uint32_t n, uint32_t chunks_total,
                               const uint32_t* d_chunk_first, Timer* timer, hipStream_t s);
 
+// One-sided pull of a peer-major group from mapped peer buffers (sux_copy.hip).
+hipError_t launch_pull(int32_t W, int32_t me, const uint64_t* srcs, const int64_t* gi, int32_t M,
+                       int32_t R, uint8_t* recv, uint64_t cap, uint64_t* recv_bytes,
+                       hipStream_t s);
+
 // Generators (sux_gen.hip).
 hipError_t launch_generate(int kind, uint64_t seed, uint64_t first, uint64_t n,
                            const uint64_t* d_zipf_bounds, const uint64_t* d_zipf_thresh,

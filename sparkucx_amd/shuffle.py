@@ -165,6 +165,28 @@ class Node:
                                             _stream(stream)), "sux_exchange_group")
         return np.frombuffer(rb, dtype=np.uint64).copy()
 
+    # ---- one-sided exchange over HIP IPC ----------------------------------------------------
+    def ipc_handle(self, t: torch.Tensor) -> bytes:
+        buf = (C.c_uint8 * 64)()
+        N.check(self.lib.sux_ipc_get_handle(self.h, _ptr(t), buf), "sux_ipc_get_handle")
+        return bytes(buf)
+
+    def ipc_open(self, handle: bytes) -> int:
+        hb = (C.c_uint8 * 64).from_buffer_copy(handle)
+        p = C.c_void_p()
+        N.check(self.lib.sux_ipc_open(self.h, hb, C.byref(p)), "sux_ipc_open")
+        return p.value
+
+    def ipc_close(self, ptr: int):
+        N.check(self.lib.sux_ipc_close(self.h, ptr), "sux_ipc_close")
+
+    def pull_group(self, world: int, rank: int, src_ptrs: torch.Tensor, gathered: torch.Tensor,
+                   num_maps: int, R: int, recv: torch.Tensor, recv_bytes: torch.Tensor | None = None,
+                   stream=None):
+        N.check(self.lib.sux_pull_group(self.h, world, rank, _ptr(src_ptrs), _ptr(gathered),
+                                        num_maps, R, _ptr(recv), recv.numel(), _ptr(recv_bytes),
+                                        _stream(stream)), "sux_pull_group")
+
     # ---- shuffle lifecycle / plugin surface -----------------------------------------------------
     def register_shuffle(self, shuffle_id: int, num_maps: int, num_partitions: int,
                          record_size: int) -> N.HandleDesc:
