@@ -213,11 +213,11 @@ def main():
         # 1.5x the group's bytes absorbs uneven partition sizes
         recv = [torch.empty(int(group_recs * rs * 1.5) + (1 << 20), dtype=torch.uint8,
                             device=dev) for _ in range(2)]
-        ws = [torch.empty(ws_bytes, dtype=torch.uint8, device=dev) for _ in range(2)]
+        ws = [torch.empty(ws_bytes, dtype=torch.uint8, device=dev) for _ in range(NB)]
         # one all-gathered index table per group (kept for the exact byte accounting)
         gidx = torch.empty(groups, world * gm * (R + 1), dtype=torch.int64, device=dev)
         rbytes = torch.zeros(groups, dtype=torch.int64, device=dev)
-        peer = [torch.empty(world, dtype=torch.int64, device=dev) for _ in range(2)]
+        peer = [torch.empty(world, dtype=torch.int64, device=dev) for _ in range(NB)]
         part_done = [torch.cuda.Event() for _ in range(NB)]
         send_free = [torch.cuda.Event() for _ in range(NB)]
         xfer_ev = []

@@ -153,16 +153,18 @@ int sux_exchange_group(sux_node* node, const void* d_send, const int64_t* d_inde
  * The GET model of UcxShuffleClient (UcxShuffleClient.java:50-127, OnOffsetsFetchCallback.java
  * :80-87) with the peers' send buffers mapped into this process instead of registered with UCX
  * (ucp_mem_map/rkey, CommonUcxShuffleBlockResolver.scala:45-66): export a device buffer's IPC
- * handle (64 bytes, carried by any side channel like the reference's rkeys), open the peers'
- * handles, then pull.  sux_pull_group reads, from every source g's peer-major send buffer, the
+ * descriptor (handle of its allocation + the buffer's offset in it, carried by any side channel
+ * like the reference's address + rkey descriptor, :80-87), open the peers' descriptors, then
+ * pull.  sux_pull_group reads, from every source g's peer-major send buffer, the
  * range holding this rank's partitions and writes it to d_recv at the sux_plan_group layout.
  * Offsets are computed on the device from the all-gathered index tables (d_gathered_index,
  * world*num_maps*(R+1) int64), so no host synchronisation is needed; the caller orders the pull
  * after every source's partition step (e.g. after the index all-gather completes).
  * d_recv_bytes (device u64, nullable) receives the bytes pulled; a capacity overflow pulls
  * nothing and stores UINT64_MAX there. */
-int sux_ipc_get_handle(sux_node* node, const void* d_ptr, uint8_t out[64]);
-int sux_ipc_open(sux_node* node, const uint8_t handle[64], void** d_ptr);
+#define SUX_IPC_DESC_BYTES 72 /* 64-byte hipIpcMemHandle of the allocation + u64 offset in it */
+int sux_ipc_export(sux_node* node, const void* d_ptr, uint8_t out[SUX_IPC_DESC_BYTES]);
+int sux_ipc_open(sux_node* node, const uint8_t desc[SUX_IPC_DESC_BYTES], void** d_ptr);
 int sux_ipc_close(sux_node* node, void* d_ptr);
 int sux_pull_group(sux_node* node, int32_t world, int32_t rank, const uint64_t* d_src_ptrs,
                    const int64_t* d_gathered_index, int32_t num_maps, int32_t num_partitions,

@@ -220,6 +220,7 @@ struct sux_node {
   sux::Timer timer;
   std::mutex mu;
   std::map<int32_t, std::unique_ptr<Shuffle>> shuffles;
+  std::map<void*, void*> ipc_bases;  // opened peer pointer -> mapped allocation base
 
   void bind() { hip_check(hipSetDevice(conf.device), "hipSetDevice"); }
 
@@ -663,24 +664,37 @@ int sux_exchange_group(sux_node* node, const void* d_send, const int64_t* d_inde
 }
 
 // ---- one-sided exchange over HIP IPC ----------------------------------------------------------
-int sux_ipc_get_handle(sux_node* node, const void* d_ptr, uint8_t out[64]) {
+int sux_ipc_export(sux_node* node, const void* d_ptr, uint8_t out[SUX_IPC_DESC_BYTES]) {
   return guard([&] {
     require(node && d_ptr && out, SUX_EINVAL, "NULL argument");
     node->bind();
+    // the handle names the whole allocation (allocators sub-allocate): ship the offset too
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    hip_check(hipMemGetAddressRange(&base, &size, const_cast<void*>(d_ptr)),
+              "hipMemGetAddressRange");
     hipIpcMemHandle_t h;
     static_assert(sizeof(h) == 64, "hipIpcMemHandle_t is 64 bytes");
-    hip_check(hipIpcGetMemHandle(&h, const_cast<void*>(d_ptr)), "hipIpcGetMemHandle");
+    hip_check(hipIpcGetMemHandle(&h, base), "hipIpcGetMemHandle");
+    const uint64_t off = (uint64_t)((const uint8_t*)d_ptr - (const uint8_t*)base);
     std::memcpy(out, &h, 64);
+    std::memcpy(out + 64, &off, 8);
   });
 }
 
-int sux_ipc_open(sux_node* node, const uint8_t handle[64], void** d_ptr) {
+int sux_ipc_open(sux_node* node, const uint8_t desc[SUX_IPC_DESC_BYTES], void** d_ptr) {
   return guard([&] {
-    require(node && handle && d_ptr, SUX_EINVAL, "NULL argument");
+    require(node && desc && d_ptr, SUX_EINVAL, "NULL argument");
     node->bind();
     hipIpcMemHandle_t h;
-    std::memcpy(&h, handle, 64);
-    hip_check(hipIpcOpenMemHandle(d_ptr, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    uint64_t off;
+    std::memcpy(&h, desc, 64);
+    std::memcpy(&off, desc + 64, 8);
+    void* base = nullptr;
+    hip_check(hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    *d_ptr = static_cast<uint8_t*>(base) + off;
+    std::lock_guard<std::mutex> lk(node->mu);
+    node->ipc_bases[*d_ptr] = base;
   });
 }
 
@@ -688,7 +702,15 @@ int sux_ipc_close(sux_node* node, void* d_ptr) {
   return guard([&] {
     require(node && d_ptr, SUX_EINVAL, "NULL argument");
     node->bind();
-    hip_check(hipIpcCloseMemHandle(d_ptr), "hipIpcCloseMemHandle");
+    void* base = nullptr;
+    {
+      std::lock_guard<std::mutex> lk(node->mu);
+      auto it = node->ipc_bases.find(d_ptr);
+      require(it != node->ipc_bases.end(), SUX_ENOENT, "pointer was not opened by sux_ipc_open");
+      base = it->second;
+      node->ipc_bases.erase(it);
+    }
+    hip_check(hipIpcCloseMemHandle(base), "hipIpcCloseMemHandle");
   });
 }
 

@@ -86,7 +86,7 @@ _SIGS = {
     "sux_set_kernel_timing": (C.c_int, [P, C.c_int]),
     "sux_kernel_times": (C.c_int, [P, P, P, I32]),
     "sux_generate": (C.c_int, [P, I32, U64, U64, U64, C.c_double, U64, P, P]),
-    "sux_ipc_get_handle": (C.c_int, [P, P, P]),
+    "sux_ipc_export": (C.c_int, [P, P, P]),
     "sux_ipc_open": (C.c_int, [P, P, C.POINTER(P)]),
     "sux_ipc_close": (C.c_int, [P, P]),
     "sux_pull_group": (C.c_int, [P, I32, I32, P, P, I32, I32, P, U64, P, P]),

@@ -167,12 +167,13 @@ class Node:
 
     # ---- one-sided exchange over HIP IPC ----------------------------------------------------
     def ipc_handle(self, t: torch.Tensor) -> bytes:
-        buf = (C.c_uint8 * 64)()
-        N.check(self.lib.sux_ipc_get_handle(self.h, _ptr(t), buf), "sux_ipc_get_handle")
+        """72-byte descriptor: IPC handle of t's allocation + t's offset in it."""
+        buf = (C.c_uint8 * 72)()
+        N.check(self.lib.sux_ipc_export(self.h, _ptr(t), buf), "sux_ipc_export")
         return bytes(buf)
 
     def ipc_open(self, handle: bytes) -> int:
-        hb = (C.c_uint8 * 64).from_buffer_copy(handle)
+        hb = (C.c_uint8 * 72).from_buffer_copy(handle)
         p = C.c_void_p()
         N.check(self.lib.sux_ipc_open(self.h, hb, C.byref(p)), "sux_ipc_open")
         return p.value
