@@ -30,6 +30,7 @@ PASSES = [
     ["SQ_INSTS_VMEM_WR", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_INSTS_SALU",
      "SQ_LDS_IDX_ACTIVE", "SQ_ACTIVE_INST_VMEM", "SQ_ACTIVE_INST_LDS", "SQ_INST_LEVEL_VMEM"],
     ["TA_TA_BUSY", "TA_ADDR_STALLED_BY_TC_CYCLES", "GRBM_GUI_ACTIVE", "GRBM_COUNT"],
+    ["TCC_HIT_sum", "TCC_MISS_sum"],
 ]
 KERNELS = {"k_hist": "hist", "k_scatter": "scatter", "k_tile_scan": "tile_scan",
            "k_group_scan": "group_scan", "k_gather_copy": "copy"}

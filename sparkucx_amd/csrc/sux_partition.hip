@@ -16,6 +16,7 @@
 // So records keep input order inside a partition, as Spark's writers do (P2).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "sux_internal.h"
@@ -1146,6 +1147,257 @@ __global__ __launch_bounds__(256) void k_scatter5(MapGroup g, int R, int pid_bit
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// v6 scatter: v5's destination-unit image, re-shaped for one big workgroup per CU.
+//   - NW waves (NW*64 threads) and C-record chunks (C*S bytes, ~100 KB at C=1024): a partition's
+//     run per chunk is ~C/R records long, so a chunk writes R runs of ~C*S/R bytes and the
+//     partial 128-B lines at run ends are few and stay in L2 until the next chunk completes them
+//     (one workgroup per CU keeps <= R open lines per CU).
+//   - Software pipelined: the next chunk's pids and records are loaded into registers right
+//     after this chunk's records were moved into the LDS image, so the loads fly while this
+//     chunk's image is written out and its carries are folded.
+//   - Each workgroup walks `tpw` consecutive tiles of one map (a longer range amortises the
+//     per-range setup: R prefix reads and R tail flushes).
+//   - Record dwords enter the image with a per-lane dword rotation ((lane>>3)&3) so that the
+//     8 lanes sharing a bank row in one ds_write_b32 write 4 different banks of it.
+// ------------------------------------------------------------------------------------------
+template <uint32_t S, uint32_t C, uint32_t NW>
+struct Sc6 {
+  static constexpr uint32_t NT = NW * kWave;
+  static constexpr uint32_t W = S / 4;
+  static constexpr uint32_t RPW = C / NW;  // records per wave per chunk
+  static constexpr uint32_t NG = (RPW + kWave - 1) / kWave;
+  static constexpr uint32_t kUnits = (C * S + 12 + 15) / 16;
+  static constexpr uint32_t kPer = (kUnits + NT - 1) / NT;
+  static_assert(C % NW == 0 && RPW % kWave == 0, "whole 64-record groups per wave");
+  static __host__ __device__ constexpr uint32_t space(int R) {
+    return (C * S) / 16 + (3u * R + 1) / 2 + 1;
+  }
+  // img[SP] u32x4 | carry[R] u32x4 | pos[R] u64 | dstu[SP] | recoff[C] | wcnt[NW][R] | cnt[R]
+  // | first[R] | lbase[R] | scan tmp[NW + 1]   (all u32 past pos)
+  static __host__ __device__ constexpr uint32_t lds_bytes(int R) {
+    return space(R) * 16 + (uint32_t)R * 24 + space(R) * 4 + C * 4 + NW * (uint32_t)R * 4 +
+           3u * R * 4 + (NW + 1) * 4;
+  }
+};
+
+// Exclusive scan of R u32 in LDS (in place) by NT threads; returns the total (all threads).
+template <uint32_t NT>
+__device__ __forceinline__ uint32_t block_scan_u32(uint32_t* v, int R, uint32_t* tmp) {
+  constexpr uint32_t NW = NT / kWave;
+  const int t = threadIdx.x, lane = t % kWave, wave = t / kWave;
+  const int per = (R + NT - 1) / NT;
+  const int lo = t * per, hi = min(R, lo + per);
+  uint32_t s = 0;
+  for (int i = lo; i < hi; ++i) s += v[i];
+  const uint32_t inc = wave_incl_scan(s, lane);
+  if (lane == kWave - 1) tmp[wave] = inc;
+  __syncthreads();
+  if (wave == 0) {
+    const uint32_t x = lane < (int)NW ? tmp[lane] : 0u;
+    const uint32_t xi = wave_incl_scan(x, lane);
+    if (lane < (int)NW) tmp[lane] = xi - x;
+    if (lane == (int)NW - 1) tmp[NW] = xi;
+  }
+  __syncthreads();
+  uint32_t run = tmp[wave] + inc - s;
+  for (int i = lo; i < hi; ++i) {
+    const uint32_t x = v[i];
+    v[i] = run;
+    run += x;
+  }
+  const uint32_t total = tmp[NW];
+  __syncthreads();
+  return total;
+}
+
+template <uint32_t S, uint32_t C, uint32_t NW>
+__global__ __launch_bounds__(NW * 64) void k_scatter6(MapGroup g, int R, int pid_bits,
+                                                     const uint16_t* __restrict__ pids,
+                                                     const uint32_t* __restrict__ prefix,
+                                                     const uint64_t* __restrict__ base,
+                                                     uint8_t* __restrict__ out, uint32_t tpw,
+                                                     uint32_t wg_per_map) {
+  using K = Sc6<S, C, NW>;
+  constexpr uint32_t NT = K::NT, W = K::W, RPW = K::RPW, NG = K::NG, PER = K::kPer;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  const uint32_t SP = K::space(R);
+  u32x4* img = reinterpret_cast<u32x4*>(lds8);
+  uint32_t* img32 = reinterpret_cast<uint32_t*>(lds8);
+  u32x4* carry = img + SP;
+  uint64_t* pos = reinterpret_cast<uint64_t*>(carry + R);
+  uint32_t* dstu = reinterpret_cast<uint32_t*>(pos + R);
+  uint32_t* recoff = dstu + SP;
+  uint32_t* wcnt = recoff + C;
+  uint32_t* cnt = wcnt + NW * R;
+  uint32_t* first = cnt + R;
+  uint32_t* lbase = first + R;
+  uint32_t* tmp = lbase + R;
+
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const uint32_t wg = xcd_map(blockIdx.x, gridDim.x);
+  const uint32_t map = wg / wg_per_map, t0 = (wg - map * wg_per_map) * tpw;
+  const uint64_t map_begin = (uint64_t)map * g.records_per_map;
+  const uint64_t map_end = min(map_begin + g.records_per_map, g.num_records);
+  const uint64_t begin = min(map_begin + (uint64_t)t0 * g.tile_recs, map_end);
+  const uint64_t end = min(begin + (uint64_t)tpw * g.tile_recs, map_end);
+  if (begin >= end) return;  // uniform for the workgroup
+
+  const uint64_t* bm = base + (uint64_t)map * R;
+  const uint32_t* pm = prefix + (uint64_t)map * R * g.tiles_per_map + t0;
+  for (int p = tid; p < R; p += NT) {
+    const uint64_t d = (bm[p] + pm[(uint64_t)p * g.tiles_per_map]) * S;
+    pos[p] = d;
+    first[p] = (uint32_t)(d & 15) >> 2;
+    carry[p] = u32x4{0, 0, 0, 0};
+  }
+  for (int i = tid; i < (int)NW * R; i += NT) wcnt[i] = 0;
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  uint32_t* out32 = reinterpret_cast<uint32_t*>(out);
+  const uint32_t rot = (uint32_t)(lane >> 3) & 3u;
+
+  // prologue: loads of chunk 0
+  uint32_t pidv[NG];
+  u32x4 v[PER];
+  auto issue = [&](uint64_t c0) {
+    const uint32_t n = (uint32_t)min<uint64_t>(C, end - c0);
+#pragma unroll
+    for (uint32_t j = 0; j < NG; ++j) {
+      const uint32_t r = wave * RPW + j * kWave + lane;
+      pidv[j] = pids[c0 + min(r, n - 1)];
+    }
+    const uint8_t* a = g.recs + c0 * S;
+    const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(a) & 15u);
+    const u32x4* src = reinterpret_cast<const u32x4*>(a - head);
+    const uint32_t units = (head + n * S + 15) >> 4;
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) v[k] = src[min(tid + k * NT, units - 1)];
+  };
+  issue(begin);
+  __syncthreads();
+
+  for (uint64_t c0 = begin; c0 < end; c0 += C) {
+    const uint32_t n = (uint32_t)min<uint64_t>(C, end - c0);
+    const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(g.recs + c0 * S) & 15u);
+    const uint32_t units = (head + n * S + 15) >> 4;
+    // 1. stable per-wave ranks (ballot match over the pid bits)
+    uint32_t my_pid[NG], my_rank[NG];
+    uint32_t* wc = wcnt + wave * R;
+#pragma unroll
+    for (uint32_t j = 0; j < NG; ++j) {
+      const uint32_t r = wave * RPW + j * kWave + lane;
+      const bool valid = r < n;
+      const uint32_t pid = valid ? pidv[j] : 0u;
+      uint64_t peers = __ballot(valid);
+      for (int bb = 0; bb < pid_bits; ++bb) {
+        const bool bit = (pid >> bb) & 1u;
+        const uint64_t m = __ballot(bit);
+        peers &= bit ? m : ~m;
+      }
+      uint32_t r0 = 0;
+      if (valid) r0 = wc[pid];
+      __builtin_amdgcn_wave_barrier();
+      if (valid && (peers & lt_mask) == 0) wc[pid] = r0 + (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+      my_pid[j] = valid ? pid : kNoUnit;
+      my_rank[j] = r0 + (uint32_t)__popcll(peers & lt_mask);
+    }
+    __syncthreads();
+    // 2. per partition: cross-wave prefix, count, image units (carry + run, rounded up)
+    for (int p = tid; p < R; p += NT) {
+      uint32_t s = 0;
+#pragma unroll
+      for (uint32_t w = 0; w < NW; ++w) {
+        const uint32_t x = wcnt[w * R + p];
+        wcnt[w * R + p] = s;
+        s += x;
+      }
+      cnt[p] = s;
+      const uint32_t cd = (uint32_t)(pos[p] & 15) >> 2;
+      lbase[p] = (cd + s * W + 3) >> 2;
+    }
+    __syncthreads();
+    const uint32_t U = block_scan_u32<NT>(lbase, R, tmp);  // ends with a barrier
+    // 3. carries in front of the runs, record image offsets, destination units
+    for (int p = tid; p < R; p += NT) {
+      const uint32_t c = cnt[p], cd = (uint32_t)(pos[p] & 15) >> 2, lb = lbase[p];
+      const uint32_t full = (cd + c * W) >> 2, sp = (cd + c * W + 3) >> 2;
+      const u32x4 cv = carry[p];
+      for (uint32_t i = 0; i < cd; ++i) img32[4 * lb + i] = cv[i];
+      if (sp) dstu[lb] = full ? ((uint32_t)(pos[p] >> 4) | (first[p] << 29)) : kNoUnit;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < NG; ++j) {
+      const uint32_t p = my_pid[j];
+      if (p == kNoUnit) continue;
+      const uint32_t jr = wcnt[wave * R + p] + my_rank[j];
+      const uint32_t c = cnt[p], cd = (uint32_t)(pos[p] & 15) >> 2, lb = lbase[p];
+      const uint32_t o = 4 * cd + jr * S;
+      recoff[wave * RPW + j * kWave + lane] = 16 * lb + o;
+      const uint32_t full = (cd + c * W) >> 2, sp = (cd + c * W + 3) >> 2;
+      const uint32_t u0 = (uint32_t)(pos[p] >> 4);
+      for (uint32_t k = (o + 15) >> 4; k * 16 < o + S && k < sp; ++k)
+        if (k) dstu[lb + k] = k < full ? (u0 + k) : kNoUnit;
+    }
+    __syncthreads();
+    // 4. records -> image (dword granular, rotated per lane octet against bank conflicts)
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) {
+      const uint32_t u = tid + k * NT;
+      if (u < units) {
+#pragma unroll
+        for (uint32_t cc = 0; cc < 4; ++cc) {
+          const uint32_t c = (cc + rot) & 3u;
+          const int32_t b = (int32_t)(16 * u + 4 * c) - (int32_t)head;
+          if (b >= 0 && (uint32_t)b < n * S) {
+            const uint32_t r = (uint32_t)b / S, off = (uint32_t)b - r * S;
+            const uint32_t x = c == 0 ? v[k][0] : c == 1 ? v[k][1] : c == 2 ? v[k][2] : v[k][3];
+            img32[(recoff[r] + off) >> 2] = x;
+          }
+        }
+      }
+    }
+    // 5. the registers are free: start the next chunk's loads
+    if (c0 + C < end) issue(c0 + C);
+    __syncthreads();
+    // 6. writer: one aligned 16-byte store per completed destination unit
+    for (uint32_t q = tid; q < U; q += NT) {
+      const uint32_t d = dstu[q];
+      if (d == kNoUnit) continue;
+      const u32x4 x = img[q];
+      const uint32_t skip = d >> 29;
+      const uint64_t A = (uint64_t)(d & kUnitMask) * 16;
+      if (skip == 0) {
+        *reinterpret_cast<u32x4*>(out + A) = x;
+      } else {
+#pragma unroll
+        for (uint32_t c = 0; c < 4; ++c)
+          if (c >= skip) out32[(A >> 2) + c] = x[c];
+      }
+    }
+    __syncthreads();
+    // 7. new carries and positions
+    for (int p = tid; p < R; p += NT) {
+      const uint32_t c = cnt[p];
+      if (c == 0) continue;
+      const uint32_t cd = (uint32_t)(pos[p] & 15) >> 2, lb = lbase[p];
+      const uint32_t full = (cd + c * W) >> 2, rest = (cd + c * W) & 3;
+      if (rest) carry[p] = img[lb + full];
+      if (full) first[p] = 0;
+      pos[p] += (uint64_t)c * S;
+    }
+    for (int i = tid; i < (int)NW * R; i += NT) wcnt[i] = 0;
+    __syncthreads();
+  }
+  // 8. flush the tails (the next range's workgroup writes the rest of these units)
+  for (int p = tid; p < R; p += NT) {
+    const uint64_t ps = pos[p];
+    const uint32_t cd = (uint32_t)(ps & 15) >> 2;
+    const u32x4 cv = carry[p];
+    for (uint32_t c = first[p]; c < cd; ++c) out32[((ps & ~15ull) >> 2) + c] = cv[c];
+  }
+}
+
 template <int KW, bool TAB>
 static void launch_hist3_kw(dim3 grid, size_t lds, hipStream_t s, const PartDev& pd,
                             const MapGroup& g, uint16_t* pids, uint32_t* counts) {
@@ -1315,7 +1567,7 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   if (e != hipSuccess) return e;
 
   // ---- K3: stable scatter
-  static const int sv = env_variant("SUX_SCATTER", 5);
+  static const int sv = env_variant("SUX_SCATTER", 6);
   static const bool c128 = [] {
     const char* e = getenv("SUX_S5C");
     return e && atoi(e) == 128;
@@ -1329,8 +1581,52 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   }();
   const bool run_writer = sv >= 4 && S == 100 && R <= 1024 &&
                           (reinterpret_cast<uintptr_t>(d_out) & 15) == 0;
+  // v6 configuration: SUX_S6=C (records per chunk: 1024 | 512 | 384 | 256), SUX_S6_TPW=tiles
+  static const int s6c = [] {
+    const char* e = getenv("SUX_S6");
+    return e ? atoi(e) : 1024;
+  }();
+  static const int s6tpw = [] {
+    const char* e = getenv("SUX_S6_TPW");
+    return e ? atoi(e) : 0;
+  }();
+  size_t lds6 = 0;
+  int c6 = 0;
+  if (sv >= 6 && S == 100 && (reinterpret_cast<uintptr_t>(d_out) & 15) == 0 &&
+      g.num_records * S < (1ull << 33)) {
+    for (int c : {1024, 512, 384, 256}) {
+      if (c > s6c) continue;
+      const size_t b = c == 1024 ? Sc6<100, 1024, 16>::lds_bytes(R)
+                     : c == 512  ? Sc6<100, 512, 8>::lds_bytes(R)
+                     : c == 384  ? Sc6<100, 384, 6>::lds_bytes(R)
+                                 : Sc6<100, 256, 4>::lds_bytes(R);
+      if (b <= 160 * 1024) {
+        c6 = c;
+        lds6 = b;
+        break;
+      }
+    }
+  }
   timer_begin(timer, kScatter, s);
-  if (unit_writer) {
+  if (c6) {
+    uint32_t tpw = s6tpw > 0 ? (uint32_t)s6tpw
+                             : (uint32_t)std::max<uint64_t>(1, (8ull * c6 + g.tile_recs - 1) / g.tile_recs);
+    if (tpw > g.tiles_per_map) tpw = g.tiles_per_map;
+    const uint32_t wpm = (g.tiles_per_map + tpw - 1) / tpw;
+    const dim3 grid((uint32_t)(g.num_maps * wpm));
+#define SUX_S6L(CC, NWV)                                                                         \
+  do {                                                                                          \
+    allow_lds(reinterpret_cast<const void*>(&k_scatter6<100, CC, NWV>), lds6);                  \
+    hipLaunchKernelGGL((k_scatter6<100, CC, NWV>), grid, dim3(NWV * kWave), lds6, s, g, R, bits, \
+                       pids, counts, base, d_out, tpw, wpm);                                     \
+  } while (0)
+    if (c6 == 1024) SUX_S6L(1024, 16);
+    else if (c6 == 512) SUX_S6L(512, 8);
+    else if (c6 == 384) SUX_S6L(384, 6);
+    else SUX_S6L(256, 4);
+#undef SUX_S6L
+    e = hipGetLastError();
+  } else if (unit_writer) {
     static const bool nt = [] {
       const char* e = getenv("SUX_NT_STORE");
       return e && e[0] == '1';
