@@ -113,7 +113,9 @@ def main():
     ap.add_argument("--workload", default="terasort", choices=sorted(WORKLOADS))
     ap.add_argument("--records", type=int, default=0, help="records per GPU (0 = workload default)")
     ap.add_argument("--map-records", type=int, default=1 << 20, help="records per map batch")
-    ap.add_argument("--group-maps", type=int, default=8, help="map batches per kernel launch group")
+    ap.add_argument("--group-maps", type=int, default=32,
+                    help="map batches per kernel launch group (32 x 100 MB: the 256 MiB "
+                         "Infinity Cache's write-back of one group's output is amortised)")
     ap.add_argument("--transport", default="rccl", choices=["rccl", "ipc"],
                     help="N>1 exchange: ncclAllToAllv, or one-sided pull over HIP IPC")
     ap.add_argument("--rehearse-one-gpu", action="store_true",

@@ -1148,6 +1148,131 @@ __global__ __launch_bounds__(256) void k_scatter5(MapGroup g, int R, int pid_bit
 }
 
 // ------------------------------------------------------------------------------------------
+// v4 hist: coalesced streaming.  v3's per-lane key loads (one 12-byte access per record, 64
+// lines per wave-instruction) kept the texture addresser stalled on the L1 (PMC:
+// TA_ADDR_STALLED_BY_TC ~72 % of TA busy) at ~4 TB/s.  Here every wave reads its tile as
+// contiguous 16-byte units (1 KiB per wave-instruction), drops each CH-record chunk into a
+// wave-private LDS stage, and reads the keys back from LDS (stride S/4 dwords: S/4 odd for
+// S=100, so the 32 lanes of a ds_read_b32 hit 32 different banks).  The next chunk's loads are
+// issued right after the stage is written, so they fly during the key math.
+// ------------------------------------------------------------------------------------------
+template <uint32_t S, uint32_t CH>
+struct Hs4 {
+  static constexpr uint32_t kUnits = (CH * S + 12 + 15) / 16;
+  static constexpr uint32_t kPer = (kUnits + kWave - 1) / kWave;
+  static constexpr uint32_t kStage = kPer * kWave * 16;  // bytes per wave
+  // stage[4] | bounds 2(R-1) u64 | lut | hist[4][R] u32
+  static __host__ __device__ constexpr uint32_t lds_bytes(int R, bool tab) {
+    return 4 * kStage + (tab ? (uint32_t)(R - 1) * 16 + (4u << kLutBits) : 0u) + 16u * R;
+  }
+};
+
+template <uint32_t S, uint32_t CH, int KW, bool TAB>
+__global__ __launch_bounds__(256) void k_hist4(PartDev pd, MapGroup g, uint16_t* __restrict__ pids,
+                                               uint32_t* __restrict__ counts) {
+  using H = Hs4<S, CH>;
+  constexpr uint32_t PER = H::kPer;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  const int R = pd.R;
+  const int nb = TAB ? 2 * (R - 1) : 0;
+  u32x4* stage_all = reinterpret_cast<u32x4*>(lds8);
+  uint64_t* sb = reinterpret_cast<uint64_t*>(lds8 + 4 * H::kStage);
+  uint32_t* slut = reinterpret_cast<uint32_t*>(sb + nb);
+  uint32_t* hist_all = slut + (TAB ? (1 << kLutBits) : 0);
+  if constexpr (TAB) {
+    for (int i = threadIdx.x; i < nb; i += 256) sb[i] = pd.bounds[i];
+    for (int i = threadIdx.x; i < (1 << kLutBits); i += 256) slut[i] = pd.lut[i];
+  }
+  for (int i = threadIdx.x; i < 4 * R; i += 256) hist_all[i] = 0;
+  __syncthreads();
+  const uint64_t* bounds = TAB ? sb : pd.bounds;
+  const uint32_t* lut = TAB ? slut : pd.lut;
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  uint32_t* hist = hist_all + wave * R;
+  u32x4* stage = stage_all + wave * (H::kStage / 16);
+  const uint32_t* st32 = reinterpret_cast<const uint32_t*>(stage);
+  const uint32_t ntiles = g.num_maps * g.tiles_per_map;
+  const uint32_t Q = (g.tile_recs + 3) / 4;  // records per wave per tile
+  uint64_t wb = 0, we = 0;                    // this wave's range of the current tile
+
+  auto issue = [&](uint64_t c0, u32x4 (&v)[PER]) {
+    const uint32_t n = (uint32_t)min<uint64_t>(CH, we - c0);
+    const uint8_t* a = g.recs + c0 * S;
+    const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(a) & 15u);
+    const u32x4* src = reinterpret_cast<const u32x4*>(a - head);
+    const uint32_t units = (head + n * S + 15) >> 4;
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) v[k] = src[min(lane + k * kWave, units - 1)];
+  };
+  // chunk c0 (held in v) -> stage -> keys -> pids + histogram; if `next` v is refilled with
+  // the chunk at c0 + 2CH.  Every lane stores a pid (lanes past the chunk's end repeat the last
+  // record's), so a step issues a fixed set of memory instructions.
+  auto step = [&](uint64_t c0, u32x4 (&v)[PER], bool next) {
+    const uint32_t n = (uint32_t)min<uint64_t>(CH, we - c0);
+    const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(g.recs + c0 * S) & 15u);
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) stage[lane + k * kWave] = v[k];
+    if (next) issue(c0 + 2 * CH, v);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+    for (uint32_t j = 0; j < CH / kWave; ++j) {
+      const uint32_t r = j * kWave + lane;
+      const uint32_t rr = r < n ? r : n - 1;
+      const uint32_t o = (head + rr * S + (uint32_t)pd.key_offset) >> 2;
+      uint32_t w[KW];
+#pragma unroll
+      for (int q = 0; q < KW; ++q) w[q] = st32[o + q];
+      const int p = partition_words<KW, TAB>(pd, w, bounds, lut);
+      if (r < n) atomicAdd(&hist[p], 1u);
+      pids[c0 + rr] = (uint16_t)p;
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
+
+  // Persistent: the workgroup walks tiles gridDim.x apart (the table above is loaded once);
+  // the 4 waves split a tile, so a tile takes a quarter of a wave's time and the launch's tail
+  // is short.  Two chunks in flight per wave (register double buffer): HBM wants ~200 KB in
+  // flight per CU.  The steady-state loop has no conditional memory instruction, so the
+  // compiler's wait for the older buffer is a counted vmcnt that leaves the younger in flight.
+  for (uint32_t gt = blockIdx.x; gt < ntiles; gt += gridDim.x) {
+    const TileRange tr = tile_range(g, gt);
+    wb = min(tr.begin + (uint64_t)wave * Q, tr.end);
+    we = min(wb + Q, tr.end);
+    u32x4 va[PER], vb[PER];
+    const uint32_t nch = (uint32_t)((we - wb + CH - 1) / CH);
+    if (nch >= 4) {
+      issue(wb, va);
+      issue(wb + CH, vb);
+      uint32_t i = 0;
+      for (; i + 3 < nch; i += 2) {
+        step(wb + (uint64_t)i * CH, va, true);
+        step(wb + (uint64_t)(i + 1) * CH, vb, true);
+      }
+      // tail: 2 or 3 chunks left (the third is loaded into va by the first tail step)
+      step(wb + (uint64_t)i * CH, va, i + 2 < nch);
+      step(wb + (uint64_t)(i + 1) * CH, vb, false);
+      if (i + 2 < nch) step(wb + (uint64_t)(i + 2) * CH, va, false);
+    } else if (nch > 0) {
+      issue(wb, va);
+      if (nch > 1) issue(wb + CH, vb);
+      step(wb, va, nch > 2);
+      if (nch > 1) step(wb + CH, vb, false);
+      if (nch > 2) step(wb + 2 * CH, va, false);
+    }
+    // an empty tile (the tail of a short last map) still publishes its zero counts
+    __syncthreads();
+    uint32_t* dst = counts + ((uint64_t)tr.map * R) * g.tiles_per_map + tr.tile;
+    for (int p = threadIdx.x; p < R; p += 256) {
+      dst[(uint64_t)p * g.tiles_per_map] =
+          hist_all[p] + hist_all[R + p] + hist_all[2 * R + p] + hist_all[3 * R + p];
+      hist_all[p] = hist_all[R + p] = hist_all[2 * R + p] = hist_all[3 * R + p] = 0;
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // v6 scatter: v5's destination-unit image, re-shaped for one big workgroup per CU.
 //   - NW waves (NW*64 threads) and C-record chunks (C*S bytes, ~100 KB at C=1024): a partition's
 //     run per chunk is ~C/R records long, so a chunk writes R runs of ~C*S/R bytes and the
@@ -1420,7 +1545,9 @@ __global__ __launch_bounds__(256) void k_pids(PartDev pd, const uint8_t* recs, u
 // ------------------------------------------------------------------------------------------
 uint32_t choose_tile_recs(uint32_t R, uint32_t rec_size, uint64_t records_per_map) {
   (void)rec_size;
-  uint32_t t = 1024;
+  // 4096 records (400 KB at S=100) per tile: fewer counters to scan, and the partial 128-B
+  // lines at tile seams are rarer (measured: 1024 -> 4096 takes ~1 ms off a 100 GB step)
+  uint32_t t = 4096;
   while (t < 4u * R && t < (1u << 22)) t <<= 1;
   if (const char* e = getenv("SUX_TILE_RECS")) {  // tuning override (power of two, >= 64)
     uint32_t v = (uint32_t)strtoul(e, nullptr, 10);
@@ -1516,14 +1643,48 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   const size_t lds1 = (size_t)wpg * R * 4;
 
   // ---- K1: pids + tile histograms
-  static const int hv = env_variant("SUX_HIST", 3);
+  static const int hv = env_variant("SUX_HIST", 4);
   const bool shaped = (S == 100 || S == 16) && R <= 4096;  // v2 instantiations
   const bool words = pd.kind != 4 && pd.key_offset % 4 == 0 && pd.key_len <= 16;
   int hist = 1;
-  if (hv >= 3 && words && R <= 4096) hist = 3;
+  if (hv >= 4 && words && R <= 4096 && S == 100 && (pd.key_offset + pd.key_len) <= (int)S) hist = 4;
+  else if (hv >= 3 && words && R <= 4096) hist = 3;
   else if (hv >= 2 && shaped) hist = 2;
   timer_begin(timer, kHist, s);
-  if (hist == 3) {
+  if (hist == 4) {
+    static const int hch = [] {
+      const char* e = getenv("SUX_H4CH");
+      return e ? atoi(e) : 64;
+    }();
+    const bool tab = pd.kind == 1 && R > 1 &&
+                     Hs4<100, 128>::lds_bytes(R, true) <= 160 * 1024;
+    const int kw = (pd.key_len + 3) / 4;
+#define SUX_H4(CHV, KW)                                                                            \
+  do {                                                                                             \
+    const size_t lds = Hs4<100, CHV>::lds_bytes(R, tab);                                           \
+    const dim3 gridp(std::min<uint32_t>(total_tiles, 256u * std::max<uint32_t>(1, (160u * 1024) / (uint32_t)lds))); \
+    if (tab) {                                                                                     \
+      allow_lds(reinterpret_cast<const void*>(&k_hist4<100, CHV, KW, true>), lds);                \
+      hipLaunchKernelGGL((k_hist4<100, CHV, KW, true>), gridp, dim3(256), lds, s, pd, g, pids,     \
+                         counts);                                                                  \
+    } else {                                                                                       \
+      allow_lds(reinterpret_cast<const void*>(&k_hist4<100, CHV, KW, false>), lds);               \
+      hipLaunchKernelGGL((k_hist4<100, CHV, KW, false>), gridp, dim3(256), lds, s, pd, g, pids,    \
+                         counts);                                                                  \
+    }                                                                                              \
+  } while (0)
+#define SUX_H4K(CHV)                 \
+  do {                               \
+    if (kw <= 1) SUX_H4(CHV, 1);     \
+    else if (kw == 2) SUX_H4(CHV, 2); \
+    else if (kw == 3) SUX_H4(CHV, 3); \
+    else SUX_H4(CHV, 4);             \
+  } while (0)
+    if (hch == 128) SUX_H4K(128);
+    else SUX_H4K(64);
+#undef SUX_H4K
+#undef SUX_H4
+  } else if (hist == 3) {
     const bool tab = pd.kind == 1 && R > 1 &&
                      (size_t)(R - 1) * 16 + (4u << kLutBits) + 2048 + 16u * R <= 64 * 1024;
     const size_t lds = (tab ? (size_t)(R - 1) * 16 + (4u << kLutBits) : 0) + 2048 + 16u * R;

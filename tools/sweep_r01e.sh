@@ -1,0 +1,14 @@
+#!/bin/bash
+set -o pipefail
+mkdir -p gpurun_out/sw5
+timeout -k 10 300 python -u -m pytest tests/test_gpu_partition.py -x -q --timeout 200 --timeout-method thread > gpurun_out/sw5/tests.log 2>&1 || { tail -30 gpurun_out/sw5/tests.log; exit 1; }
+tail -2 gpurun_out/sw5/tests.log
+tools/sweep.sh gpurun_out/sw5 \
+ ";--steps 3 --warmup 1" \
+ "SUX_TILE_RECS=4096;--steps 3 --warmup 1" \
+ "SUX_TILE_RECS=2048;--steps 3 --warmup 1" \
+ ";--steps 3 --warmup 1 --group-maps 32" \
+ ";--steps 3 --warmup 1 --streams 2" \
+ ";--steps 3 --warmup 1 --group-maps 16 --streams 2" \
+ "SUX_TILE_RECS=4096;--steps 3 --warmup 1 --group-maps 32"
+cat gpurun_out/sw5/sweep.txt
