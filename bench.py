@@ -123,6 +123,9 @@ def main():
                          "(exercises the N>1 pipeline on a 1-GPU box; not a benchmark)")
     ap.add_argument("--streams", type=int, default=1,
                     help="N=1: launch groups dealt round-robin to this many HIP streams")
+    ap.add_argument("--reserve-cus", type=int, default=-1,
+                    help="CUs kept free of map-side kernels for the exchange (-1: 32 if N>1, "
+                         "else 0)")
     ap.add_argument("--cpu-records", type=int, default=10_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-reps", type=int, default=3)
@@ -181,6 +184,13 @@ def main():
     index = torch.empty(maps * (R + 1), dtype=torch.int64, device=dev)
     ws_bytes = node.workspace_size(part, rs, rpm, min(n, group_recs))
     comp = torch.cuda.current_stream(dev)
+    reserve = args.reserve_cus if args.reserve_cus >= 0 else (32 if world > 1 else 0)
+    if reserve > 0:
+        # map-side kernels on a CU-masked stream that leaves `reserve` CUs (spread over the 8
+        # XCDs) to the exchange: the partition kernels fill every CU they get (LDS-bound), so
+        # an unmasked partition would starve the overlapped all-to-all of CUs
+        comp = torch.cuda.ExternalStream(node.cu_stream(reserve, complement=True), device=dev)
+        comp.wait_stream(torch.cuda.current_stream(dev))  # the generated input
 
     if world == 1:
         out = torch.empty(n * rs, dtype=torch.uint8, device=dev)
@@ -336,6 +346,7 @@ def main():
                                f"({n * rs / 1e9:.0f} GB/GPU, {n * rs * world / 1e9:.0f} GB total), "
                                f"R={R}, map batches of {rpm} records, {gm} maps per launch group"
                                + (f" on {args.streams} streams" if world == 1 and args.streams > 1 else "")
+                               + (f", map side on {256 - reserve} CUs" if reserve > 0 else "")
                                + (", zero-copy local block resolve" if world == 1 else
                                   ", partition-aligned ncclAllToAllv exchange"
                                   if args.transport == "rccl" else

@@ -240,6 +240,17 @@ int sux_buffer_info(sux_buffer* buf, void** dev_ptr, uint64_t* size, uint64_t* c
 int sux_buffer_retain(sux_buffer* buf, int32_t count);
 int sux_buffer_release(sux_buffer* buf);
 
+/* ---- CU-partitioned streams (exchange/compute overlap) ---------------------------------- *
+ * A non-blocking HIP stream (returned as void*) whose kernels run on `num_cus` of the device's
+ * CUs, spread evenly over all 8 XCDs x 4 shader engines (use a multiple of 32: an SE with fewer
+ * CUs than its peers becomes the straggler), or on the other CUs when `complement` is non-zero
+ * (hipExtStreamCreateWithCUMask).  The map-side kernels fill every CU they are given (LDS-bound
+ * occupancy), so a pipeline that overlaps the all-to-all of launch group k with the partition
+ * of group k+1 runs the partition on a complement stream and leaves `num_cus` CUs to the
+ * collective.  No reference counterpart: UCX moves bytes with the NIC, not with cores. */
+int sux_stream_create(sux_node* node, int32_t num_cus, int32_t complement, void** out_stream);
+int sux_stream_destroy(sux_node* node, void* stream);
+
 /* ---- measurement hooks ------------------------------------------------------------------ */
 /* When enabled, the node brackets each partition-kernel launch with HIP events on the launch
  * stream; sux_kernel_times() returns per-kernel {launches, total_ms} for kernels

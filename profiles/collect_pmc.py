@@ -96,7 +96,7 @@ def main():
     ap.add_argument("--summarize-only", action="store_true")
     a, bench_args = ap.parse_known_args()
     if not bench_args:
-        bench_args = ["--steps", "1", "--warmup", "1", "--records", "250000000",
+        bench_args = ["--steps", "1", "--warmup", "1", "--records", "268435456",
                       "--no-cpu-baseline"]
     os.makedirs(a.out, exist_ok=True)
     dirs = []

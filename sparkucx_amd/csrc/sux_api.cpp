@@ -1106,6 +1106,55 @@ int sux_buffer_release(sux_buffer* b) {
   });
 }
 
+// ---- CU-partitioned streams -------------------------------------------------------------------
+// CU-mask bit of the k-th reserved CU.  Measured (tools/cu_probe: HW_REG_XCC_ID + HW_REG_HW_ID
+// of the workgroups of masked streams, profiles/r01_cu_probe_*.txt): the driver maps the mask
+// symmetrically, bit b -> XCD b % 8, shader engine (b / 8) % 4, CU slot b / 32, and ignores a
+// mask that leaves an XCD without CUs.  A kernel's workgroups are dealt evenly over the XCDs and,
+// inside one, over its 4 SEs, so an SE that lost more CUs than the others is the launch's
+// straggler (4 of SE0's 8 CUs reserved on every XCD ran the scatter 1.5x slower).  Bits 0..C-1
+// take the reserved CUs round-robin over all 32 (XCD, SE) pairs: keep C a multiple of 32.
+static uint32_t reserved_cu(uint32_t k) { return k; }
+
+int sux_stream_create(sux_node* node, int32_t num_cus, int32_t complement, void** out) {
+  return guard([&] {
+    require(node && out, SUX_EINVAL, "NULL argument");
+    node->bind();
+    hipDeviceProp_t prop;
+    hip_check(hipGetDeviceProperties(&prop, node->conf.device), "hipGetDeviceProperties");
+    const uint32_t P = (uint32_t)prop.multiProcessorCount;
+    require(num_cus >= 0 && (uint32_t)num_cus <= P, SUX_EINVAL,
+            "num_cus must be in [0, " + std::to_string(P) + "]");
+    hipStream_t st = nullptr;
+    if (num_cus == 0 || (uint32_t)num_cus == P) {
+      // nothing to partition: an ordinary stream (all CUs, or all CUs for the complement of 0)
+      require(!(num_cus == (int32_t)P && complement), SUX_EINVAL, "empty CU set");
+      require(!(num_cus == 0 && !complement), SUX_EINVAL, "empty CU set");
+      hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+    } else {
+      std::vector<uint32_t> mask((P + 31) / 32, 0u);
+      std::vector<uint8_t> pick(P, 0);
+      for (uint32_t k = 0; k < (uint32_t)num_cus; ++k) {
+        uint32_t i = reserved_cu(k);
+        pick[i] = 1;
+      }
+      for (uint32_t i = 0; i < P; ++i)
+        if (pick[i] != (complement ? 1 : 0)) mask[i / 32] |= 1u << (i % 32);
+      hip_check(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()),
+                "hipExtStreamCreateWithCUMask");
+    }
+    *out = st;
+  });
+}
+
+int sux_stream_destroy(sux_node* node, void* stream) {
+  return guard([&] {
+    require(node && stream, SUX_EINVAL, "NULL argument");
+    node->bind();
+    hip_check(hipStreamDestroy(static_cast<hipStream_t>(stream)), "hipStreamDestroy");
+  });
+}
+
 // ---- measurement -----------------------------------------------------------------------------
 int sux_set_kernel_timing(sux_node* node, int enable) {
   return guard([&] {

@@ -90,6 +90,8 @@ _SIGS = {
     "sux_ipc_open": (C.c_int, [P, P, C.POINTER(P)]),
     "sux_ipc_close": (C.c_int, [P, P]),
     "sux_pull_group": (C.c_int, [P, I32, I32, P, P, I32, I32, P, U64, P, P]),
+    "sux_stream_create": (C.c_int, [P, I32, I32, C.POINTER(P)]),
+    "sux_stream_destroy": (C.c_int, [P, P]),
 }
 
 _lib = None

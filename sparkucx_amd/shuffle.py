@@ -65,9 +65,12 @@ class Node:
         self.h = h
         self.rank, self.world_size = rank, world_size
         self.dev = torch.device("cuda", device)
+        self._streams: list[int] = []
 
     def close(self):
         if self.h:
+            for st in list(self._streams):
+                self.destroy_stream(st)
             N.check(self.lib.sux_node_destroy(self.h), "sux_node_destroy")
             self.h = None
 
@@ -255,6 +258,20 @@ class Node:
         return list(addrs)[:len(blocks)], list(sizes)[:len(blocks)]
 
     # ---- measurement -------------------------------------------------------------------------
+    def cu_stream(self, num_cus: int, complement: bool = False) -> int:
+        """hipStream_t (as int) running on `num_cus` CUs spread over the XCDs, or on the other CUs
+        (complement).  Wrap with torch.cuda.ExternalStream; destroy with destroy_stream()."""
+        out = C.c_void_p()
+        N.check(self.lib.sux_stream_create(self.h, int(num_cus), int(bool(complement)),
+                                           C.byref(out)), "sux_stream_create")
+        self._streams.append(out.value)
+        return out.value
+
+    def destroy_stream(self, stream: int):
+        if stream in self._streams:
+            self._streams.remove(stream)
+            N.check(self.lib.sux_stream_destroy(self.h, C.c_void_p(stream)), "sux_stream_destroy")
+
     def set_kernel_timing(self, on: bool):
         N.check(self.lib.sux_set_kernel_timing(self.h, int(on)), "sux_set_kernel_timing")
 

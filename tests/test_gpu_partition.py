@@ -269,3 +269,30 @@ def test_kernel_timing_counts_launches(gpu_node):
     gpu_node.set_kernel_timing(False)
     assert t["hist"][0] == 3 and t["scatter"][0] == 3 and t["scan"][0] == 3
     assert t["scatter"][1] > 0
+
+
+def test_cu_masked_stream(gpu_node):
+    """Partition on a stream that leaves 32 CUs free (the N>1 compute stream) — same bytes."""
+    recs = O.gen_terasort(11, 0, 300_000)
+    opart = O.terasort_partitioner(200)
+    gp = gpu_part(gpu_node, opart)
+    st = gpu_node.cu_stream(32, complement=True)
+    try:
+        ts = torch.cuda.ExternalStream(st)
+        drecs = to_dev(recs)
+        ts.wait_stream(torch.cuda.current_stream())
+        out, index, index_be = gpu_node.partition_maps(gp, drecs, 100, 100_000, stream=ts)
+        ts.synchronize()
+        want_data, want_index, want_be = O.write_maps(opart, recs, 100, 100_000)
+        assert host(out).tobytes() == bytes(want_data)
+        assert host(index).tolist() == want_index.tolist()
+        # the reserved side: 32 CUs only
+        st2 = gpu_node.cu_stream(32, complement=False)
+        ts2 = torch.cuda.ExternalStream(st2)
+        ts2.wait_stream(torch.cuda.current_stream())
+        out2, _, _ = gpu_node.partition_maps(gp, drecs, 100, 100_000, stream=ts2)
+        ts2.synchronize()
+        assert host(out2).tobytes() == bytes(want_data)
+        gpu_node.destroy_stream(st2)
+    finally:
+        gpu_node.destroy_stream(st)
