@@ -1,19 +1,24 @@
 // sux_partition.hip — map-side hot path for gfx950.
 //
-// One launch group = M consecutive map batches.  Four kernels:
-//   K1 k_hist      one wave per tile: key -> partition id (P1), pid store, wave-private LDS
-//                  histogram, counts[m][p][t] (partition-major).
+// One launch group = M consecutive map batches (default 32 x 100 MB).  Four kernels:
+//   K1 hist      key -> partition id (P1), pid store, LDS histograms, counts[m][p][tile]
+//                (partition-major).  Default k_hist4: persistent; a workgroup's 4 waves split a
+//                4096-record tile, read it as coalesced 16-byte units through a wave LDS stage
+//                with two chunks in flight, and look keys up in an LDS range table.
 //   K2a k_tile_scan one wave per (map, partition): exclusive scan of counts over tiles in place,
-//                  totals[m][p].
+//                totals[m][p].
 //   K2b k_group_scan one workgroup per group: per-map index tables (P3, native + big-endian) and
-//                  the destination base of every (map, partition) for the chosen layout.
-//   K3 k_scatter   one wave per tile: walks its records in input order 64 at a time, ranks
-//                  equal partition ids with a ballot match (stable), and copies each record to
-//                  base + tile prefix + rank.  This is the HBM-bound kernel.
+//                the destination base of every (map, partition) for the chosen layout.
+//   K3 scatter   stable regroup of the records by pid (P2).  Default k_scatter7: persistent, one
+//                1024-thread workgroup per CU, 1024-record chunks staged straight into a
+//                partition-sorted LDS image in destination-unit space, written out as aligned
+//                16-byte stores; the next chunk's loads fly during the write-out.
+// Older shapes (other record sizes, R beyond the LDS image) use the v1/v2/v3/v6 kernels below.
 //
-// Stability: a wave owns a contiguous tile and visits it in order; within 64 lanes the rank is
-// the popcount of lower lanes with the same pid; tiles are ordered by the tile-major prefix.
-// So records keep input order inside a partition, as Spark's writers do (P2).
+// Stability: records are visited in input order (waves in order inside a chunk, chunks in order
+// inside a tile range, tile ranges ordered by the partition-major tile prefix); equal pids inside
+// 64 lanes are ranked by a ballot match.  So records keep input order inside a partition, as
+// Spark's writers do (P2).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -705,449 +710,6 @@ __global__ __launch_bounds__(256) void k_hist3(PartDev pd, MapGroup g, uint16_t*
 }
 
 // ------------------------------------------------------------------------------------------
-// v4 scatter: run writer.  One 256-thread workgroup owns 4 consecutive hist tiles of a map and
-// walks them in chunks of C records staged in LDS.  Per chunk it counts partition ids per wave
-// (ballot match, stable), scans them into a partition-sorted order of the chunk, and writes
-// every partition's run as ALIGNED 16-byte units of the destination: the sub-16-byte tail of a
-// run is kept in LDS (`carry`) and completed by the next chunk, so except at the two ends of
-// the workgroup's range every store is a full, aligned global_store_dwordx4 along a contiguous
-// run — the pattern that streams at copy speed (tools/hbm_probe: copy_x4 vs perm100_dword).
-// ------------------------------------------------------------------------------------------
-template <uint32_t S, uint32_t C>
-struct Sc4 {
-  static constexpr uint32_t W = S / 4;                       // dwords per record
-  static constexpr uint32_t kBuf = Stage<S, C>::kBufBytes;   // staged records
-  static constexpr uint32_t kSrc = ((C * 2 + 15) / 16) * 16; // u16 sorted -> chunk index
-  static constexpr uint32_t kPer = (Stage<S, C>::kUnits + 255) / 256;
-  // per-partition state, bytes per partition: pos u64, carry u32x4, wcnt 4 x u32,
-  // cstart/ustart u32 (R+1), first u32
-  static __host__ __device__ constexpr uint32_t lds_bytes(int R) {
-    return kBuf + kSrc + (uint32_t)R * (8 + 16 + 16 + 4) + ((uint32_t)R + 1) * 8 + 16;
-  }
-};
-
-// Exclusive block scan (256 threads) of `R` u64 values held in LDS `v` (in place); returns the
-// total.  Each thread scans a contiguous slice, then one wave scans the 256 slice sums.
-__device__ __forceinline__ uint64_t block_scan_lds(uint64_t* v, int R, uint64_t* tmp) {
-  const int t = threadIdx.x;
-  const int per = (R + 255) / 256;
-  const int lo = t * per, hi = min(R, lo + per);
-  uint64_t s = 0;
-  for (int i = lo; i < hi; ++i) s += v[i];
-  tmp[t] = s;
-  __syncthreads();
-  if (t < kWave) {
-    uint64_t a = tmp[4 * t], b = tmp[4 * t + 1], c = tmp[4 * t + 2], d = tmp[4 * t + 3];
-    uint64_t tot = a + b + c + d, inc = tot;
-#pragma unroll
-    for (int dd = 1; dd < kWave; dd <<= 1) {
-      uint64_t x = __shfl_up(inc, dd, kWave);
-      if (t >= dd) inc += x;
-    }
-    uint64_t ex = inc - tot;
-    tmp[4 * t] = ex;
-    tmp[4 * t + 1] = ex + a;
-    tmp[4 * t + 2] = ex + a + b;
-    tmp[4 * t + 3] = ex + a + b + c;
-    if (t == kWave - 1) tmp[256] = inc;
-  }
-  __syncthreads();
-  uint64_t run = tmp[t];
-  for (int i = lo; i < hi; ++i) {
-    uint64_t x = v[i];
-    v[i] = run;
-    run += x;
-  }
-  const uint64_t total = tmp[256];
-  __syncthreads();
-  return total;
-}
-
-template <uint32_t S, uint32_t C>
-__global__ __launch_bounds__(256) void k_scatter4(MapGroup g, int R, int pid_bits,
-                                                  const uint16_t* __restrict__ pids,
-                                                  const uint32_t* __restrict__ prefix,
-                                                  const uint64_t* __restrict__ base,
-                                                  uint8_t* __restrict__ out, uint32_t wg_per_map) {
-  using K = Sc4<S, C>;
-  constexpr uint32_t W = K::W, RPW = C / 4;  // records per wave per chunk
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
-  u32x4* buf = reinterpret_cast<u32x4*>(lds8);
-  uint16_t* srcidx = reinterpret_cast<uint16_t*>(lds8 + K::kBuf);
-  uint8_t* st = lds8 + K::kBuf + K::kSrc;
-  uint64_t* pos = reinterpret_cast<uint64_t*>(st);              // [R] dest byte of next run byte
-  u32x4* carry = reinterpret_cast<u32x4*>(st + 8 * R);          // [R] pending sub-16B tail
-  uint32_t* wcnt = reinterpret_cast<uint32_t*>(st + 24 * R);    // [4][R] per-wave counts/prefix
-  uint32_t* first = wcnt + 4 * R;                               // [R] head unit still partial
-  uint64_t* scan = reinterpret_cast<uint64_t*>(first + R);      // [R+1] (cstart<<32 | ustart)
-  __shared__ uint64_t tmp[257];
-
-  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
-  const uint32_t wg = xcd_map(blockIdx.x, gridDim.x);
-  const uint32_t map = wg / wg_per_map, q4 = (wg - map * wg_per_map) * 4;
-  const uint64_t map_begin = (uint64_t)map * g.records_per_map;
-  uint64_t map_end = map_begin + g.records_per_map;
-  if (map_end > g.num_records) map_end = g.num_records;
-  const uint64_t begin = min(map_begin + (uint64_t)q4 * g.tile_recs, map_end);
-  const uint64_t end = min(begin + 4ull * g.tile_recs, map_end);
-  if (begin >= end) return;  // uniform for the workgroup
-
-  // initial state: destination of this workgroup's first record of every partition
-  const uint64_t* bm = base + (uint64_t)map * R;
-  const uint32_t* pm = prefix + (uint64_t)map * R * g.tiles_per_map + q4;
-  for (int p = tid; p < R; p += 256) {
-    const uint64_t d = (bm[p] + pm[(uint64_t)p * g.tiles_per_map]) * S;
-    pos[p] = d;
-    first[p] = (uint32_t)(d & 15) >> 2;  // foreign dwords in the first unit (0 = aligned)
-  }
-  const uint64_t lt_mask = (1ull << lane) - 1ull;
-  uint32_t* out32 = reinterpret_cast<uint32_t*>(out);
-
-  for (uint64_t c0 = begin; c0 < end; c0 += C) {
-    const uint32_t n = (uint32_t)min<uint64_t>(C, end - c0);
-    // 1. stage the chunk (16-byte coalesced loads, all issued before the LDS writes)
-    uint32_t head;
-    {
-      const uint8_t* a = g.recs + c0 * S;
-      head = (uint32_t)(reinterpret_cast<uintptr_t>(a) & 15u);
-      const u32x4* src = reinterpret_cast<const u32x4*>(a - head);
-      const uint32_t units = (head + n * S + 15) >> 4;
-      u32x4 v[K::kPer];
-#pragma unroll
-      for (uint32_t k = 0; k < K::kPer; ++k) {
-        const uint32_t u = tid + k * 256;
-        if (u < units) v[k] = src[u];
-      }
-      for (int p = tid; p < 4 * R; p += 256) wcnt[p] = 0;
-#pragma unroll
-      for (uint32_t k = 0; k < K::kPer; ++k) {
-        const uint32_t u = tid + k * 256;
-        if (u < units) buf[u] = v[k];
-      }
-    }
-    __syncthreads();
-    // 2. per-wave stable ranks (wave w owns chunk records [w*RPW, (w+1)*RPW))
-    uint32_t my_pid[RPW / kWave], my_rank[RPW / kWave];
-    uint32_t* wc = wcnt + wave * R;
-#pragma unroll
-    for (uint32_t j = 0; j < RPW / kWave; ++j) {
-      const uint32_t r = wave * RPW + j * kWave + lane;
-      const bool valid = r < n;
-      const uint32_t pid = valid ? pids[c0 + r] : 0u;
-      uint64_t peers = __ballot(valid);
-      for (int bb = 0; bb < pid_bits; ++bb) {
-        const bool bit = (pid >> bb) & 1u;
-        const uint64_t m = __ballot(bit);
-        peers &= bit ? m : ~m;
-      }
-      uint32_t r0 = 0;
-      if (valid) r0 = wc[pid];
-      __builtin_amdgcn_wave_barrier();
-      if (valid && (peers & lt_mask) == 0) wc[pid] = r0 + (uint32_t)__popcll(peers);
-      __builtin_amdgcn_wave_barrier();
-      my_pid[j] = valid ? pid : 0xFFFFFFFFu;
-      my_rank[j] = r0 + (uint32_t)__popcll(peers & lt_mask);
-    }
-    __syncthreads();
-    // 3. cross-wave prefix, chunk counts, full 16-B units per partition; scan both
-    for (int p = tid; p < R; p += 256) {
-      uint32_t a = wcnt[p], b = wcnt[R + p], c = wcnt[2 * R + p], d = wcnt[3 * R + p];
-      wcnt[p] = 0;
-      wcnt[R + p] = a;
-      wcnt[2 * R + p] = a + b;
-      wcnt[3 * R + p] = a + b + c;
-      const uint32_t cnt = a + b + c + d;
-      const uint32_t full = (uint32_t)(((pos[p] & 15) + (uint64_t)cnt * S) >> 4);
-      scan[p] = ((uint64_t)cnt << 32) | full;
-    }
-    __syncthreads();
-    const uint64_t tot = block_scan_lds(scan, R, tmp);
-    if (tid == 0) scan[R] = tot;
-    __syncthreads();
-    // 4. partition-sorted position of every chunk record
-#pragma unroll
-    for (uint32_t j = 0; j < RPW / kWave; ++j) {
-      const uint32_t pid = my_pid[j];
-      if (pid != 0xFFFFFFFFu) {
-        const uint32_t sp = (uint32_t)(scan[pid] >> 32) + wcnt[wave * R + pid] + my_rank[j];
-        srcidx[sp] = (uint16_t)(wave * RPW + j * kWave + lane);
-      }
-    }
-    __syncthreads();
-    // 5. write every full destination unit of every run
-    const uint32_t U = (uint32_t)scan[R];
-    const uint32_t* bw = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(buf) + head);
-    for (uint32_t q = tid; q < U; q += 256) {
-      int lo = 0, hi = R - 1;  // last p with ustart[p] <= q
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if ((uint32_t)scan[mid] <= q) lo = mid; else hi = mid - 1;
-      }
-      const int p = lo;
-      const uint32_t k = q - (uint32_t)scan[p];
-      const uint64_t ps = pos[p];
-      const uint32_t cdw = (uint32_t)(ps & 15) >> 2, cs = (uint32_t)(scan[p] >> 32);
-      uint32_t val[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const uint32_t v = 4 * k + c;
-        if (v < cdw) {
-          val[c] = carry[p][c];
-        } else {
-          const uint32_t t = v - cdw, rr = t / W, ww = t - rr * W;
-          val[c] = bw[(uint32_t)srcidx[cs + rr] * W + ww];
-        }
-      }
-      const uint64_t A = (ps & ~15ull) + 16ull * k;
-      const uint32_t skip = (k == 0) ? first[p] : 0u;
-      if (skip == 0) {
-        *reinterpret_cast<u32x4*>(out + A) = u32x4{val[0], val[1], val[2], val[3]};
-      } else {
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if ((uint32_t)c >= skip) out32[(A >> 2) + c] = val[c];
-      }
-    }
-    __syncthreads();
-    // 6. advance: new tail (carry) and position of every partition
-    for (int p = tid; p < R; p += 256) {
-      const uint32_t cnt = (uint32_t)(scan[p + 1] >> 32) - (uint32_t)(scan[p] >> 32);
-      if (cnt == 0) continue;
-      const uint64_t ps = pos[p];
-      const uint32_t cdw = (uint32_t)(ps & 15) >> 2, cs = (uint32_t)(scan[p] >> 32);
-      const uint64_t np = ps + (uint64_t)cnt * S;
-      const uint32_t ndw = (uint32_t)(np & 15) >> 2, total = cdw + cnt * W;
-      const u32x4 old = carry[p];
-      uint32_t nv[4] = {0, 0, 0, 0};
-      for (uint32_t c = 0; c < ndw; ++c) {
-        const uint32_t v = total - ndw + c;
-        if (v < cdw) {
-          nv[c] = old[v];
-        } else {
-          const uint32_t t = v - cdw, rr = t / W, ww = t - rr * W;
-          nv[c] = bw[(uint32_t)srcidx[cs + rr] * W + ww];
-        }
-      }
-      carry[p] = u32x4{nv[0], nv[1], nv[2], nv[3]};
-      if (((ps & 15) + (uint64_t)cnt * S) >= 16) first[p] = 0;  // head unit has been written
-      pos[p] = np;
-    }
-    __syncthreads();
-  }
-  // 7. flush the tails (the next workgroup's range completes these units)
-  for (int p = tid; p < R; p += 256) {
-    const uint64_t ps = pos[p];
-    const uint32_t cdw = (uint32_t)(ps & 15) >> 2;
-    const u32x4 cv = carry[p];
-    for (uint32_t c = first[p]; c < cdw; ++c) out32[((ps & ~15ull) >> 2) + c] = cv[c];
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// v5 scatter: the chunk is staged straight into a partition-sorted LDS image laid out in
-// DESTINATION-UNIT space.  Partition p's run of this chunk starts at LDS unit lbase[p] at the
-// same phase (pos[p] mod 16) it has in the output, with p's carried tail in front of it, so the
-// LDS unit q maps to ONE aligned 16-byte destination unit dstu[q].  The writer is then
-// ds_read_b128 + global_store_dwordx4 per unit.  The staging loads are issued before the ranking
-// so their latency hides behind it.
-// ------------------------------------------------------------------------------------------
-template <uint32_t S, uint32_t C>
-struct Sc5 {
-  static constexpr uint32_t W = S / 4;
-  static constexpr uint32_t kUnits = (C * S + 12 + 15) / 16;  // staged global units (<=12 B head)
-  static constexpr uint32_t kPer = (kUnits + 255) / 256;
-  // sum_p ceil((cd_p + cnt_p*W)/4) <= (C*W + 6R)/4 + 1
-  static __host__ __device__ constexpr uint32_t space(int R) {
-    return (C * S) / 16 + (3u * R + 1) / 2 + 1;
-  }
-  static __host__ __device__ constexpr uint32_t lds_bytes(int R) {
-    return space(R) * 16 + space(R) * 4 + C * 4 + (uint32_t)R * (8 + 16 + 16 + 8 + 4 + 4) + 16;
-  }
-};
-constexpr uint32_t kNoUnit = 0xFFFFFFFFu;    // tail unit still partial: becomes the carry
-constexpr uint32_t kUnitMask = (1u << 29) - 1;  // dstu: unit index | (foreign head dwords << 29)
-
-template <uint32_t S, uint32_t C, bool NT>
-__global__ __launch_bounds__(256) void k_scatter5(MapGroup g, int R, int pid_bits,
-                                                  const uint16_t* __restrict__ pids,
-                                                  const uint32_t* __restrict__ prefix,
-                                                  const uint64_t* __restrict__ base,
-                                                  uint8_t* __restrict__ out, uint32_t wg_per_map) {
-  using K = Sc5<S, C>;
-  constexpr uint32_t W = K::W, RPW = C / 4, NG = (RPW + kWave - 1) / kWave;
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
-  const uint32_t SP = K::space(R);
-  u32x4* img = reinterpret_cast<u32x4*>(lds8);                  // [SP] sorted image
-  uint32_t* img32 = reinterpret_cast<uint32_t*>(lds8);
-  u32x4* carry = img + SP;                                       // [R] pending tail dwords
-  uint64_t* pos = reinterpret_cast<uint64_t*>(carry + R);        // [R] next output byte of p
-  uint64_t* lbase = pos + R;                                     // [R] image unit of p's run
-  uint32_t* dstu = reinterpret_cast<uint32_t*>(lbase + R);       // [SP] destination unit
-  uint32_t* recoff = dstu + SP;                                  // [C] image byte of record
-  uint32_t* wcnt = recoff + C;                                   // [4][R]
-  uint32_t* cnt = wcnt + 4 * R;                                  // [R]
-  uint32_t* first = cnt + R;                                     // [R] foreign head dwords
-  __shared__ uint64_t tmp[257];
-
-  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
-  const uint32_t wg = xcd_map(blockIdx.x, gridDim.x);
-  const uint32_t map = wg / wg_per_map, q4 = (wg - map * wg_per_map) * 4;
-  const uint64_t map_begin = (uint64_t)map * g.records_per_map;
-  const uint64_t map_end = min(map_begin + g.records_per_map, g.num_records);
-  const uint64_t begin = min(map_begin + (uint64_t)q4 * g.tile_recs, map_end);
-  const uint64_t end = min(begin + 4ull * g.tile_recs, map_end);
-  if (begin >= end) return;  // uniform for the workgroup
-
-  const uint64_t* bm = base + (uint64_t)map * R;
-  const uint32_t* pm = prefix + (uint64_t)map * R * g.tiles_per_map + q4;
-  for (int p = tid; p < R; p += 256) {
-    const uint64_t d = (bm[p] + pm[(uint64_t)p * g.tiles_per_map]) * S;
-    pos[p] = d;
-    first[p] = (uint32_t)(d & 15) >> 2;
-    carry[p] = u32x4{0, 0, 0, 0};
-  }
-  for (int i = tid; i < 4 * R; i += 256) wcnt[i] = 0;
-  __syncthreads();
-  const uint64_t lt_mask = (1ull << lane) - 1ull;
-  uint32_t* out32 = reinterpret_cast<uint32_t*>(out);
-
-  for (uint64_t c0 = begin; c0 < end; c0 += C) {
-    const uint32_t n = (uint32_t)min<uint64_t>(C, end - c0);
-    // 1. issue the pid loads and the staging loads (clamped: no branches, all in flight)
-    uint32_t pidv[NG];
-#pragma unroll
-    for (uint32_t j = 0; j < NG; ++j) {
-      const uint32_t r = wave * RPW + min(j * kWave + lane, RPW - 1);
-      pidv[j] = pids[c0 + min(r, n - 1)];
-    }
-    const uint8_t* a = g.recs + c0 * S;
-    const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(a) & 15u);
-    const u32x4* src = reinterpret_cast<const u32x4*>(a - head);
-    const uint32_t units = (head + n * S + 15) >> 4;
-    u32x4 v[K::kPer];
-#pragma unroll
-    for (uint32_t k = 0; k < K::kPer; ++k) v[k] = src[min(tid + k * 256u, units - 1)];
-    // 2. stable per-wave ranks
-    uint32_t my_pid[NG], my_rank[NG];
-    uint32_t* wc = wcnt + wave * R;
-#pragma unroll
-    for (uint32_t j = 0; j < NG; ++j) {
-      const uint32_t r = wave * RPW + j * kWave + lane;
-      const bool valid = (j * kWave + lane < RPW) && r < n;
-      const uint32_t pid = valid ? pidv[j] : 0u;
-      uint64_t peers = __ballot(valid);
-      for (int bb = 0; bb < pid_bits; ++bb) {
-        const bool bit = (pid >> bb) & 1u;
-        const uint64_t m = __ballot(bit);
-        peers &= bit ? m : ~m;
-      }
-      uint32_t r0 = 0;
-      if (valid) r0 = wc[pid];
-      __builtin_amdgcn_wave_barrier();
-      if (valid && (peers & lt_mask) == 0) wc[pid] = r0 + (uint32_t)__popcll(peers);
-      __builtin_amdgcn_wave_barrier();
-      my_pid[j] = valid ? pid : kNoUnit;
-      my_rank[j] = r0 + (uint32_t)__popcll(peers & lt_mask);
-    }
-    __syncthreads();
-    // 3. per partition: cross-wave prefix, count, image units (carry + run, rounded up)
-    for (int p = tid; p < R; p += 256) {
-      const uint32_t x0 = wcnt[p], x1 = wcnt[R + p], x2 = wcnt[2 * R + p], x3 = wcnt[3 * R + p];
-      wcnt[p] = 0;
-      wcnt[R + p] = x0;
-      wcnt[2 * R + p] = x0 + x1;
-      wcnt[3 * R + p] = x0 + x1 + x2;
-      const uint32_t c = x0 + x1 + x2 + x3;
-      cnt[p] = c;
-      const uint32_t cd = (uint32_t)(pos[p] & 15) >> 2;
-      lbase[p] = (cd + c * W + 3) >> 2;
-    }
-    __syncthreads();
-    block_scan_lds(lbase, R, tmp);  // ends with a barrier
-    // 4. image offsets of the records, destination units they own, carries in front of runs
-    for (int p = tid; p < R; p += 256) {
-      const uint32_t c = cnt[p], cd = (uint32_t)(pos[p] & 15) >> 2, lb = (uint32_t)lbase[p];
-      const uint32_t full = (cd + c * W) >> 2, space = (cd + c * W + 3) >> 2;
-      const u32x4 cv = carry[p];
-      for (uint32_t i = 0; i < cd; ++i) img32[4 * lb + i] = cv[i];
-      if (space) {  // unit 0 starts in the carry or at the run's first byte: owned here
-        const uint32_t u0 = (uint32_t)(pos[p] >> 4);
-        dstu[lb] = full ? (u0 | (first[p] << 29)) : kNoUnit;
-      }
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < NG; ++j) {
-      const uint32_t p = my_pid[j];
-      if (p == kNoUnit) continue;
-      const uint32_t jr = wcnt[wave * R + p] + my_rank[j];
-      const uint32_t c = cnt[p], cd = (uint32_t)(pos[p] & 15) >> 2, lb = (uint32_t)lbase[p];
-      const uint32_t o = 4 * cd + jr * S;  // byte of this record in p's run image
-      recoff[wave * RPW + j * kWave + lane] = 16 * lb + o;
-      const uint32_t full = (cd + c * W) >> 2, space = (cd + c * W + 3) >> 2;
-      const uint32_t u0 = (uint32_t)(pos[p] >> 4);
-      for (uint32_t k = (o + 15) >> 4; k * 16 < o + S && k < space; ++k)
-        if (k) dstu[lb + k] = k < full ? (u0 + k) : kNoUnit;
-    }
-    __syncthreads();
-    // 5. staged units -> image (dword granular: records sit at 4-byte phases)
-#pragma unroll
-    for (uint32_t k = 0; k < K::kPer; ++k) {
-      const uint32_t u = tid + k * 256;
-      if (u < units) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int32_t b = (int32_t)(16 * u + 4 * c) - (int32_t)head;
-          if (b >= 0 && (uint32_t)b < n * S) {
-            const uint32_t r = (uint32_t)b / S, off = (uint32_t)b - r * S;
-            img32[(recoff[r] + off) >> 2] = v[k][c];
-          }
-        }
-      }
-    }
-    __syncthreads();
-    // 6. writer: one aligned 16-byte store per completed destination unit
-    const uint32_t U = (uint32_t)tmp[256];
-    for (uint32_t q = tid; q < U; q += 256) {
-      const uint32_t d = dstu[q];
-      if (d == kNoUnit) continue;
-      const u32x4 x = img[q];
-      const uint32_t skip = d >> 29;
-      const uint64_t A = (uint64_t)(d & kUnitMask) * 16;
-      if (skip == 0) {
-        if constexpr (NT)
-          __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(out + A));
-        else
-          *reinterpret_cast<u32x4*>(out + A) = x;
-      } else {
-#pragma unroll
-        for (uint32_t c = 0; c < 4; ++c)
-          if (c >= skip) out32[(A >> 2) + c] = x[c];
-      }
-    }
-    __syncthreads();
-    // 7. new carries and positions
-    for (int p = tid; p < R; p += 256) {
-      const uint32_t c = cnt[p];
-      if (c == 0) continue;
-      const uint32_t cd = (uint32_t)(pos[p] & 15) >> 2, lb = (uint32_t)lbase[p];
-      const uint32_t full = (cd + c * W) >> 2, rest = (cd + c * W) & 3;
-      if (rest) carry[p] = img[lb + full];
-      if (full) first[p] = 0;
-      pos[p] += (uint64_t)c * S;
-    }
-    for (int i = tid; i < 4 * R; i += 256) wcnt[i] = 0;
-    __syncthreads();
-  }
-  // 8. flush the tails (the next range's workgroup writes the rest of these units)
-  for (int p = tid; p < R; p += 256) {
-    const uint64_t ps = pos[p];
-    const uint32_t cd = (uint32_t)(ps & 15) >> 2;
-    const u32x4 cv = carry[p];
-    for (uint32_t c = first[p]; c < cd; ++c) out32[((ps & ~15ull) >> 2) + c] = cv[c];
-  }
-}
-
-// ------------------------------------------------------------------------------------------
 // v4 hist: coalesced streaming.  v3's per-lane key loads (one 12-byte access per record, 64
 // lines per wave-instruction) kept the texture addresser stalled on the L1 (PMC:
 // TA_ADDR_STALLED_BY_TC ~72 % of TA busy) at ~4 TB/s.  Here every wave reads its tile as
@@ -1286,6 +848,25 @@ __global__ __launch_bounds__(256) void k_hist4(PartDev pd, MapGroup g, uint16_t*
 //   - Record dwords enter the image with a per-lane dword rotation ((lane>>3)&3) so that the
 //     8 lanes sharing a bank row in one ds_write_b32 write 4 different banks of it.
 // ------------------------------------------------------------------------------------------
+// destination-unit words of the v6/v7 image: unit index (29 bits) | foreign head dwords << 29
+constexpr uint32_t kNoUnit = 0xFFFFFFFFu;       // tail unit still partial: becomes the carry
+constexpr uint32_t kUnitMask = (1u << 29) - 1;
+
+// Diagnostic build only (-DSUX_STAMPS, tools/stamps.hip): thread 0 of workgroups < 64 records
+// s_memtime at the phase boundaries of its first 16 chunks.  No stamp executes otherwise.
+#ifdef SUX_STAMPS
+__device__ uint64_t g_stamps[64][16][8];
+#define SUX_STAMP(ci, ph)                                                        \
+  do {                                                                           \
+    if (threadIdx.x == 0 && blockIdx.x < 64 && (ci) < 16)                        \
+      g_stamps[blockIdx.x][(ci)][(ph)] = __builtin_amdgcn_s_memtime();          \
+  } while (0)
+#else
+#define SUX_STAMP(ci, ph) \
+  do {                    \
+  } while (0)
+#endif
+
 template <uint32_t S, uint32_t C, uint32_t NW>
 struct Sc6 {
   static constexpr uint32_t NT = NW * kWave;
@@ -1401,7 +982,9 @@ __global__ __launch_bounds__(NW * 64) void k_scatter6(MapGroup g, int R, int pid
   issue(begin);
   __syncthreads();
 
-  for (uint64_t c0 = begin; c0 < end; c0 += C) {
+  uint32_t ci = 0;
+  for (uint64_t c0 = begin; c0 < end; c0 += C, ++ci) {
+    SUX_STAMP(ci, 0);
     const uint32_t n = (uint32_t)min<uint64_t>(C, end - c0);
     const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(g.recs + c0 * S) & 15u);
     const uint32_t units = (head + n * S + 15) >> 4;
@@ -1428,6 +1011,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter6(MapGroup g, int R, int pid
       my_rank[j] = r0 + (uint32_t)__popcll(peers & lt_mask);
     }
     __syncthreads();
+    SUX_STAMP(ci, 1);
     // 2. per partition: cross-wave prefix, count, image units (carry + run, rounded up)
     for (int p = tid; p < R; p += NT) {
       uint32_t s = 0;
@@ -1443,6 +1027,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter6(MapGroup g, int R, int pid
     }
     __syncthreads();
     const uint32_t U = block_scan_u32<NT>(lbase, R, tmp);  // ends with a barrier
+    SUX_STAMP(ci, 2);
     // 3. carries in front of the runs, record image offsets, destination units
     for (int p = tid; p < R; p += NT) {
       const uint32_t c = cnt[p], cd = (uint32_t)(pos[p] & 15) >> 2, lb = lbase[p];
@@ -1465,6 +1050,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter6(MapGroup g, int R, int pid
         if (k) dstu[lb + k] = k < full ? (u0 + k) : kNoUnit;
     }
     __syncthreads();
+    SUX_STAMP(ci, 3);
     // 4. records -> image (dword granular, rotated per lane octet against bank conflicts)
 #pragma unroll
     for (uint32_t k = 0; k < PER; ++k) {
@@ -1482,9 +1068,11 @@ __global__ __launch_bounds__(NW * 64) void k_scatter6(MapGroup g, int R, int pid
         }
       }
     }
+    SUX_STAMP(ci, 4);
     // 5. the registers are free: start the next chunk's loads
     if (c0 + C < end) issue(c0 + C);
     __syncthreads();
+    SUX_STAMP(ci, 5);
     // 6. writer: one aligned 16-byte store per completed destination unit
     for (uint32_t q = tid; q < U; q += NT) {
       const uint32_t d = dstu[q];
@@ -1501,6 +1089,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter6(MapGroup g, int R, int pid
       }
     }
     __syncthreads();
+    SUX_STAMP(ci, 6);
     // 7. new carries and positions
     for (int p = tid; p < R; p += NT) {
       const uint32_t c = cnt[p];
@@ -1513,6 +1102,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter6(MapGroup g, int R, int pid
     }
     for (int i = tid; i < (int)NW * R; i += NT) wcnt[i] = 0;
     __syncthreads();
+    SUX_STAMP(ci, 7);
   }
   // 8. flush the tails (the next range's workgroup writes the rest of these units)
   for (int p = tid; p < R; p += NT) {
@@ -1520,6 +1110,337 @@ __global__ __launch_bounds__(NW * 64) void k_scatter6(MapGroup g, int R, int pid
     const uint32_t cd = (uint32_t)(ps & 15) >> 2;
     const u32x4 cv = carry[p];
     for (uint32_t c = first[p]; c < cd; ++c) out32[((ps & ~15ull) >> 2) + c] = cv[c];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// v7 scatter: v6 with the per-chunk bookkeeping cut down (tools/stamps: v6 spent 57 % of a
+// chunk's cycles in rank/prefix/scan/offsets/carries, none of it overlapping memory at one
+// workgroup per CU).  R <= NW*64, so thread p owns partition p for the whole range and keeps
+// its output cursor in registers; per-wave counters are stored partition-major (NW contiguous
+// u32 = NW/4 ds_read_b128); prefix over waves and the scan of image units are one fused phase
+// (wave scan + NW wave totals); records read one packed {lb, cd, full, sp} per partition; the
+// destination-unit loop of a record is a fixed, predicated trip count.
+// ------------------------------------------------------------------------------------------
+template <uint32_t S, uint32_t C, uint32_t NW>
+struct Sc7 {
+  static constexpr uint32_t NT = NW * kWave;
+  static constexpr uint32_t W = S / 4;
+  static constexpr uint32_t RPW = C / NW;
+  static constexpr uint32_t NG = (RPW + kWave - 1) / kWave;
+  static constexpr uint32_t kUnits = (C * S + 12 + 15) / 16;
+  static constexpr uint32_t kPer = (kUnits + NT - 1) / NT;
+  static constexpr uint32_t kRecUnits = (S + 15) / 16 + 1;  // units that can start in a record
+  static_assert(C % NW == 0 && RPW % kWave == 0 && NW % 4 == 0, "shape");
+  static __host__ __device__ constexpr uint32_t space(int R) {
+    return (C * S) / 16 + (3u * R + 1) / 2 + 1;
+  }
+  // img[SP] u32x4 | pinfo[R] u32x4 | carry[R] u32x4 | dstu[SP] | recoff[C] | wcnt[R][NW]
+  // | u0[R] | tmp[NW + 1]
+  static __host__ __device__ constexpr uint32_t lds_bytes(int R) {
+    return space(R) * 16 + (uint32_t)R * 32 + space(R) * 4 + C * 4 + NW * (uint32_t)R * 4 +
+           (uint32_t)R * 4 + (NW + 1) * 4;
+  }
+};
+
+template <uint32_t S, uint32_t C, uint32_t NW, uint32_t DEPTH>
+__global__ __launch_bounds__(NW * 64) void k_scatter7(MapGroup g, int R, int pid_bits,
+                                                     const uint16_t* __restrict__ pids,
+                                                     const uint32_t* __restrict__ prefix,
+                                                     const uint64_t* __restrict__ base,
+                                                     uint8_t* __restrict__ out, uint32_t tpw,
+                                                     uint32_t wg_per_map) {
+  using K = Sc7<S, C, NW>;
+  constexpr uint32_t NT = K::NT, W = K::W, RPW = K::RPW, NG = K::NG, PER = K::kPer;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  const uint32_t SP = K::space(R);
+  u32x4* img = reinterpret_cast<u32x4*>(lds8);
+  uint32_t* img32 = reinterpret_cast<uint32_t*>(lds8);
+  u32x4* pinfo = img + SP;   // {lb, cd, full, sp}
+  u32x4* carry = pinfo + R;  // pending tail dwords of p
+  uint32_t* dstu = reinterpret_cast<uint32_t*>(carry + R);
+  uint32_t* recoff = dstu + SP;
+  uint32_t* wcnt = recoff + C;  // [R][NW]
+  uint32_t* u0s = wcnt + NW * R;
+  uint32_t* tmp = u0s + R;
+
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const bool owner = tid < R;  // thread p owns partition p: cursor and head state in registers
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  uint32_t* out32 = reinterpret_cast<uint32_t*>(out);
+  const uint32_t rot = (uint32_t)(lane >> 3) & 3u;
+
+  // Persistent: workgroup b walks work items slot(b), slot(b) + G, ... where an item is `tpw`
+  // tiles of one map and slot() keeps the items an XCD works on at one time adjacent.  The chunk
+  // stream runs across item seams: the first chunk of the next item is loaded while the last
+  // chunk of this one is written out.
+  const uint32_t nitems = g.num_maps * wg_per_map;
+  const uint32_t G = gridDim.x;
+  struct Item {
+    uint32_t map, t0;
+    uint64_t begin, end;
+  };
+  auto item_of = [&](uint32_t it) {
+    Item x;
+    x.map = it / wg_per_map;
+    x.t0 = (it - x.map * wg_per_map) * tpw;
+    const uint64_t map_begin = (uint64_t)x.map * g.records_per_map;
+    const uint64_t map_end = min(map_begin + g.records_per_map, g.num_records);
+    x.begin = min(map_begin + (uint64_t)x.t0 * g.tile_recs, map_end);
+    x.end = min(x.begin + (uint64_t)tpw * g.tile_recs, map_end);
+    return x;
+  };
+  const uint32_t it = xcd_map(blockIdx.x, G);
+  if (it >= nitems) return;
+  const Item cur = item_of(it);
+
+  uint64_t pos = 0;
+  uint32_t first = 0;
+  auto begin_item = [&](const Item& x) {
+    if (owner) {
+      pos = (base[(uint64_t)x.map * R + tid] +
+             prefix[(uint64_t)x.map * R * g.tiles_per_map + (uint64_t)tid * g.tiles_per_map + x.t0]) * S;
+      first = (uint32_t)(pos & 15) >> 2;
+      carry[tid] = u32x4{0, 0, 0, 0};
+    }
+  };
+  // the tails of this item's runs: the next range's workgroup writes the rest of these units
+  auto end_item = [&]() {
+    if (owner) {
+      const uint32_t cd = (uint32_t)(pos & 15) >> 2;
+      const u32x4 cv = carry[tid];
+      for (uint32_t cc = first; cc < cd; ++cc) out32[((pos & ~15ull) >> 2) + cc] = cv[cc];
+    }
+  };
+
+  // Chunk stream: a cursor walks (item, chunk) pairs; `issue` always emits the same loads
+  // (a finished stream loads one unit of the input again) so that the compiler's waits for the
+  // older of two register buffers are counted and leave the younger one in flight.
+  struct Cur {
+    uint32_t it;
+    uint64_t c0, end;
+    bool valid;
+  };
+  auto first_cur = [&](uint32_t it0) {
+    Cur k;
+    k.it = it0;
+    k.valid = it0 < nitems;
+    const Item x = item_of(k.valid ? it0 : 0);
+    k.c0 = x.begin;
+    k.end = x.end;
+    return k;
+  };
+  auto next_cur = [&](const Cur& k) {
+    Cur nk = k;
+    nk.c0 = k.c0 + C;
+    if (nk.c0 >= k.end) nk = first_cur(k.it + G);
+    return nk;
+  };
+  auto issue = [&](const Cur& k, uint32_t (&pidv)[NG], u32x4 (&v)[PER]) {
+    const uint32_t n = k.valid ? (uint32_t)min<uint64_t>(C, k.end - k.c0) : 1u;
+    const uint64_t c0 = k.valid ? k.c0 : 0;
+#pragma unroll
+    for (uint32_t j = 0; j < NG; ++j) {
+      const uint32_t r = wave * RPW + j * kWave + lane;
+      pidv[j] = pids[c0 + min(r, n - 1)];
+    }
+    const uint8_t* a = g.recs + c0 * S;
+    const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(a) & 15u);
+    const u32x4* src = reinterpret_cast<const u32x4*>(a - head);
+    const uint32_t units = (head + n * S + 15) >> 4;
+#pragma unroll
+    for (uint32_t k2 = 0; k2 < PER; ++k2) v[k2] = src[min(tid + k2 * NT, units - 1)];
+  };
+
+  if (owner) {
+#pragma unroll
+    for (uint32_t w = 0; w < NW; w += 4)
+      reinterpret_cast<u32x4*>(wcnt + tid * NW)[w / 4] = u32x4{0, 0, 0, 0};
+  }
+  begin_item(cur);
+  uint32_t ci = 0;
+  // one chunk: pids and records in (pidv, v); `ahead` is the chunk DEPTH positions later, loaded
+  // into the same registers once they are free.  Returns false after the stream's last chunk.
+  auto process = [&](const Cur& k, const Cur& ahead, uint32_t (&pidv)[NG], u32x4 (&v)[PER]) {
+    SUX_STAMP(ci, 0);
+    const uint64_t c0 = k.c0;
+    const uint32_t n = (uint32_t)min<uint64_t>(C, k.end - c0);
+    const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(g.recs + c0 * S) & 15u);
+    const uint32_t units = (head + n * S + 15) >> 4;
+    const Cur nk = next_cur(k);
+    const bool seam = nk.it != k.it, more = nk.valid;
+    // 1. stable per-wave ranks (ballot match over the pid bits)
+    uint32_t my_pid[NG], my_rank[NG];
+#pragma unroll
+    for (uint32_t j = 0; j < NG; ++j) {
+      const uint32_t r = wave * RPW + j * kWave + lane;
+      const bool valid = r < n;
+      const uint32_t pid = valid ? pidv[j] : 0u;
+      uint64_t peers = __ballot(valid);
+      for (int bb = 0; bb < pid_bits; ++bb) {
+        const bool bit = (pid >> bb) & 1u;
+        const uint64_t m = __ballot(bit);
+        peers &= bit ? m : ~m;
+      }
+      uint32_t* wc = wcnt + pid * NW + wave;
+      uint32_t r0 = 0;
+      if (valid) r0 = *wc;
+      __builtin_amdgcn_wave_barrier();
+      if (valid && (peers & lt_mask) == 0) *wc = r0 + (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+      my_pid[j] = valid ? pid : kNoUnit;
+      my_rank[j] = r0 + (uint32_t)__popcll(peers & lt_mask);
+    }
+    __syncthreads();
+    SUX_STAMP(ci, 1);
+    // 2. fused: prefix over waves (registers), count, image units, scan of units over R
+    uint32_t c = 0, cd = 0, sp = 0, full = 0;
+    if (owner) {
+      u32x4* row = reinterpret_cast<u32x4*>(wcnt + tid * NW);
+      u32x4 x[NW / 4];
+#pragma unroll
+      for (uint32_t q = 0; q < NW / 4; ++q) x[q] = row[q];
+#pragma unroll
+      for (uint32_t q = 0; q < NW / 4; ++q) {
+        u32x4 y;
+        y[0] = c;
+        y[1] = c + x[q][0];
+        y[2] = y[1] + x[q][1];
+        y[3] = y[2] + x[q][2];
+        c = y[3] + x[q][3];
+        row[q] = y;
+      }
+      cd = (uint32_t)(pos & 15) >> 2;
+      full = (cd + c * W) >> 2;
+      sp = (cd + c * W + 3) >> 2;
+    }
+    const uint32_t incl = wave_incl_scan(sp, lane);
+    if (lane == kWave - 1) tmp[wave] = incl;
+    __syncthreads();
+    SUX_STAMP(ci, 2);
+    uint32_t lb = incl - sp, U = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < NW; ++w) {
+      const uint32_t t = tmp[w];
+      lb += (w < (uint32_t)wave) ? t : 0u;
+      U += t;
+    }
+    if (owner) {
+      pinfo[tid] = u32x4{lb, cd, full, sp};
+      u0s[tid] = (uint32_t)(pos >> 4);
+      const u32x4 cv = carry[tid];
+#pragma unroll
+      for (uint32_t i = 0; i < 3; ++i)
+        if (i < cd) img32[4 * lb + i] = cv[i];
+      if (sp) dstu[lb] = full ? ((uint32_t)(pos >> 4) | (first << 29)) : kNoUnit;
+    }
+    __syncthreads();
+    SUX_STAMP(ci, 3);
+    // 3. record image offsets and the destination units that start inside each record
+#pragma unroll
+    for (uint32_t j = 0; j < NG; ++j) {
+      const uint32_t p = my_pid[j];
+      if (p == kNoUnit) continue;
+      const u32x4 pi = pinfo[p];
+      const uint32_t jr = wcnt[p * NW + wave] + my_rank[j];
+      const uint32_t o = 4 * pi[1] + jr * S;
+      recoff[wave * RPW + j * kWave + lane] = 16 * pi[0] + o;
+      const uint32_t u0 = u0s[p];
+      const uint32_t k0 = (o + 15) >> 4;
+#pragma unroll
+      for (uint32_t t = 0; t < K::kRecUnits; ++t) {
+        const uint32_t k = k0 + t;
+        if (k > 0 && k * 16 < o + S && k < pi[3]) dstu[pi[0] + k] = k < pi[2] ? (u0 + k) : kNoUnit;
+      }
+    }
+    __syncthreads();
+    SUX_STAMP(ci, 4);
+    // 4. records -> image (dword granular, rotated per lane octet against bank conflicts)
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) {
+      const uint32_t u = tid + k * NT;
+      if (u < units) {
+#pragma unroll
+        for (uint32_t cc = 0; cc < 4; ++cc) {
+          const uint32_t q = (cc + rot) & 3u;
+          const int32_t b = (int32_t)(16 * u + 4 * q) - (int32_t)head;
+          if (b >= 0 && (uint32_t)b < n * S) {
+            const uint32_t r = (uint32_t)b / S, off = (uint32_t)b - r * S;
+            const uint32_t x = q == 0 ? v[k][0] : q == 1 ? v[k][1] : q == 2 ? v[k][2] : v[k][3];
+            img32[(recoff[r] + off) >> 2] = x;
+          }
+        }
+      }
+    }
+    // 5. the registers are free: start the loads of the chunk DEPTH ahead
+    issue(ahead, pidv, v);
+    __syncthreads();
+    SUX_STAMP(ci, 5);
+    // 6. writer: one aligned 16-byte store per completed destination unit
+    for (uint32_t q = tid; q < U; q += NT) {
+      const uint32_t d = dstu[q];
+      if (d == kNoUnit) continue;
+      const u32x4 x = img[q];
+      const uint32_t skip = d >> 29;
+      const uint64_t A = (uint64_t)(d & kUnitMask) * 16;
+      if (skip == 0) {
+        *reinterpret_cast<u32x4*>(out + A) = x;
+      } else {
+#pragma unroll
+        for (uint32_t cc = 0; cc < 4; ++cc)
+          if (cc >= skip) out32[(A >> 2) + cc] = x[cc];
+      }
+    }
+    __syncthreads();
+    SUX_STAMP(ci, 6);
+    // 7. new carries and cursors (owner threads), counters cleared for the next chunk; at an
+    //    item seam the tails are flushed and the next item's cursors loaded (owner-local state)
+    if (owner) {
+      if (c) {
+        if ((cd + c * W) & 3) carry[tid] = img[lb + full];
+        if (full) first = 0;
+        pos += (uint64_t)c * S;
+      }
+#pragma unroll
+      for (uint32_t w = 0; w < NW; w += 4)
+        reinterpret_cast<u32x4*>(wcnt + tid * NW)[w / 4] = u32x4{0, 0, 0, 0};
+    }
+    if (seam) {
+      end_item();
+      if (more) begin_item(item_of(nk.it));
+    }
+    __syncthreads();
+    SUX_STAMP(ci, 7);
+    ++ci;
+    return more;
+  };
+
+  uint32_t pa[NG];
+  u32x4 va[PER];
+  Cur k = first_cur(it);
+  if constexpr (DEPTH == 1) {
+    issue(k, pa, va);
+    __syncthreads();
+    while (true) {
+      const Cur k1 = next_cur(k);
+      if (!process(k, k1, pa, va)) break;
+      k = k1;
+    }
+  } else {
+    uint32_t pb[NG];
+    u32x4 vb[PER];
+    Cur k1 = next_cur(k);
+    issue(k, pa, va);
+    issue(k1, pb, vb);
+    __syncthreads();
+    while (true) {
+      const Cur k2 = next_cur(k1);
+      if (!process(k, k2, pa, va)) break;
+      const Cur k3 = next_cur(k2);
+      if (!process(k1, k3, pb, vb)) break;
+      k = k2;
+      k1 = k3;
+    }
   }
 }
 
@@ -1727,22 +1648,11 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   e = hipGetLastError();
   if (e != hipSuccess) return e;
 
-  // ---- K3: stable scatter
-  static const int sv = env_variant("SUX_SCATTER", 6);
-  static const bool c128 = [] {
-    const char* e = getenv("SUX_S5C");
-    return e && atoi(e) == 128;
-  }();
-  const bool unit_writer = sv >= 5 && S == 100 && R <= 1024 &&
-                           (reinterpret_cast<uintptr_t>(d_out) & 15) == 0 &&
-                           g.num_records * S < (1ull << 33);
-  static const bool c256 = [] {
-    const char* e = getenv("SUX_S4C");
-    return e && atoi(e) == 256;
-  }();
-  const bool run_writer = sv >= 4 && S == 100 && R <= 1024 &&
-                          (reinterpret_cast<uintptr_t>(d_out) & 15) == 0;
-  // v6 configuration: SUX_S6=C (records per chunk: 1024 | 512 | 384 | 256), SUX_S6_TPW=tiles
+  // ---- K3: stable scatter.  S = 100 (TeraSort rows): v7 for R <= 512, v6 for the R whose
+  // LDS image still fits; any other shape: the v2 (R <= 4096, S in {16, 100}) or v1 kernels.
+  static const int sv = env_variant("SUX_SCATTER", 7);
+  // tuning overrides: SUX_S6=C (v6 records per chunk: 1024 | 512 | 384 | 256), SUX_S6_TPW=tiles
+  // per work item, SUX_S7=2|3 (v7 at 768-record chunks with 2 | 1 chunks in flight)
   static const int s6c = [] {
     const char* e = getenv("SUX_S6");
     return e ? atoi(e) : 1024;
@@ -1768,8 +1678,33 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
       }
     }
   }
+  const bool v7 = c6 == 1024 && sv >= 7 && R <= 512 &&
+                  Sc7<100, 1024, 16>::lds_bytes(R) <= 160 * 1024;
   timer_begin(timer, kScatter, s);
-  if (c6) {
+  if (v7) {
+    uint32_t tpw = s6tpw > 0 ? (uint32_t)s6tpw
+                             : (uint32_t)std::max<uint64_t>(1, (8ull * 1024 + g.tile_recs - 1) / g.tile_recs);
+    if (tpw > g.tiles_per_map) tpw = g.tiles_per_map;
+    const uint32_t wpm = (g.tiles_per_map + tpw - 1) / tpw;
+    // persistent: one 1024-thread workgroup per CU (LDS-bound) walks the items
+    const dim3 grid((uint32_t)std::min<uint64_t>((uint64_t)g.num_maps * wpm, 256));
+#define SUX_S7L(CC, NWV, DV)                                                                     \
+  do {                                                                                          \
+    const size_t lds7 = Sc7<100, CC, NWV>::lds_bytes(R);                                        \
+    allow_lds(reinterpret_cast<const void*>(&k_scatter7<100, CC, NWV, DV>), lds7);              \
+    hipLaunchKernelGGL((k_scatter7<100, CC, NWV, DV>), grid, dim3(NWV * kWave), lds7, s, g, R,   \
+                       bits, pids, counts, base, d_out, tpw, wpm);                               \
+  } while (0)
+    static const int s7 = [] {
+      const char* e = getenv("SUX_S7");
+      return e ? atoi(e) : 1;
+    }();
+    if (s7 == 2) SUX_S7L(768, 12, 2);
+    else if (s7 == 3) SUX_S7L(768, 12, 1);
+    else SUX_S7L(1024, 16, 1);
+#undef SUX_S7L
+    e = hipGetLastError();
+  } else if (c6) {
     uint32_t tpw = s6tpw > 0 ? (uint32_t)s6tpw
                              : (uint32_t)std::max<uint64_t>(1, (8ull * c6 + g.tile_recs - 1) / g.tile_recs);
     if (tpw > g.tiles_per_map) tpw = g.tiles_per_map;
@@ -1786,42 +1721,6 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
     else if (c6 == 384) SUX_S6L(384, 6);
     else SUX_S6L(256, 4);
 #undef SUX_S6L
-    e = hipGetLastError();
-  } else if (unit_writer) {
-    static const bool nt = [] {
-      const char* e = getenv("SUX_NT_STORE");
-      return e && e[0] == '1';
-    }();
-    const uint32_t wpm = (g.tiles_per_map + 3) / 4;
-    const dim3 grid((uint32_t)(g.num_maps * wpm));
-#define SUX_S5(CC, NTV)                                                                        \
-  do {                                                                                        \
-    const size_t lds = Sc5<100, CC>::lds_bytes(R);                                            \
-    allow_lds(reinterpret_cast<const void*>(&k_scatter5<100, CC, NTV>), lds);                 \
-    hipLaunchKernelGGL((k_scatter5<100, CC, NTV>), grid, dim3(256), lds, s, g, R, bits, pids, \
-                       counts, base, d_out, wpm);                                             \
-  } while (0)
-    if (c128) {
-      if (nt) SUX_S5(128, true); else SUX_S5(128, false);
-    } else {
-      if (nt) SUX_S5(256, true); else SUX_S5(256, false);
-    }
-#undef SUX_S5
-    e = hipGetLastError();
-  } else if (run_writer) {
-    const uint32_t wpm = (g.tiles_per_map + 3) / 4;
-    const dim3 grid((uint32_t)(g.num_maps * wpm));
-    if (c256) {
-      const size_t lds = Sc4<100, 256>::lds_bytes(R);
-      allow_lds(reinterpret_cast<const void*>(&k_scatter4<100, 256>), lds);
-      hipLaunchKernelGGL((k_scatter4<100, 256>), grid, dim3(256), lds, s, g, R, bits, pids, counts,
-                         base, d_out, wpm);
-    } else {
-      const size_t lds = Sc4<100, 512>::lds_bytes(R);
-      allow_lds(reinterpret_cast<const void*>(&k_scatter4<100, 512>), lds);
-      hipLaunchKernelGGL((k_scatter4<100, 512>), grid, dim3(256), lds, s, g, R, bits, pids, counts,
-                         base, d_out, wpm);
-    }
     e = hipGetLastError();
   } else if (sv >= 2 && shaped) {
     const size_t lds = 4 * (size_t)(S == 100 ? scatter2_wave_bytes<100, 128>(R)

@@ -57,6 +57,21 @@ __global__ void k_keys(const uint32_t* __restrict__ a, size_t nrec, uint32_t* si
   if (acc == 0x12345678u) sink[0] = acc;
 }
 
+// the scatter's write pattern: a 1024-thread workgroup copies 100 KB chunks (coalesced reads)
+// and writes each as `runs` runs of 100KB/runs bytes, run r of chunk c at region r, offset c*len:
+// consecutive chunks extend every region sequentially (as partition p's output does)
+__global__ __launch_bounds__(1024) void k_runcopy(const u32x4* __restrict__ a, u32x4* __restrict__ b,
+                                                  size_t n, uint32_t runs, uint32_t shift) {
+  const uint32_t chunk_units = 6400, per_run = chunk_units / runs;  // 16-B units
+  const size_t chunks = n / chunk_units, region = chunks * per_run;
+  for (size_t c = blockIdx.x; c < chunks; c += gridDim.x) {
+    for (uint32_t u = threadIdx.x; u < chunk_units; u += 1024) {
+      const uint32_t r = u / per_run, k = u - r * per_run;
+      if (r < runs) b[r * region + c * per_run + k + shift] = a[c * chunk_units + u];
+    }
+  }
+}
+
 template <class F>
 static float time_it(F f, int reps) {
   hipEvent_t a, b;
@@ -106,5 +121,10 @@ int main(int argc, char** argv) {
   printf("perm100_dword  %8.1f GB/s (read+write)\n", gbs(2.0 * bytes, t));
   t = time_it([&] { hipLaunchKernelGGL(k_keys, dim3(G), dim3(256), 0, 0, (const uint32_t*)a, nrec, sink); }, reps);
   printf("keys100_read   %8.1f GB/s (record bytes / time)\n", gbs(bytes, t));
+  for (uint32_t shift : {0u, 3u})
+    for (uint32_t runs : {1u, 50u, 200u, 800u}) {
+      t = time_it([&] { hipLaunchKernelGGL(k_runcopy, dim3(256 * 2), dim3(1024), 0, 0, (const u32x4*)a, (u32x4*)b, n4 - 8, runs, shift); }, reps);
+      printf("runcopy %4u runs/100KB (%5u B runs) start+%2u B %8.1f GB/s (read+write)\n", runs, 102400 / runs, 16 * shift, gbs(2.0 * bytes, t));
+    }
   return 0;
 }

@@ -65,19 +65,20 @@ int main(int argc, char** argv) {
   const int G = 256 * 8;
   const size_t sizes[] = {32u << 20, 64u << 20, 100000000, 128u << 20, 200000000, 256u << 20,
                           400000000, 838860800, 1u << 30};
-  printf("%10s %9s %9s %9s %9s %9s | %s\n", "slice_MB", "read", "tiles", "copy", "rd+copy",
-         "copy|rd", "GB/s: read=S/t copy=2S/t rd+copy=3S/t copy|rd=2S/(t_rd+copy - t_read)");
+  printf("%10s %9s %9s %9s %9s %9s %9s %9s | %s\n", "slice_MB", "read", "tiles", "copy", "rd+copy",
+         "copy|rd", "rd+rd", "rd|rd", "GB/s: read=S/t copy=2S/t rd+copy=3S/t copy|rd=2S/(t_rd+copy - t_read) rd|rd=S/(t_rd+rd - t_read)");
   for (size_t S : sizes) {
     const size_t n4 = S / 16, slices = total / S;
-    float t_read = 0, t_tiles = 0, t_copy = 0, t_both = 0;
-    for (int mode = 0; mode < 4; ++mode) {
+    float t_read = 0, t_tiles = 0, t_copy = 0, t_both = 0, t_rr = 0;
+    for (int mode = 0; mode < 5; ++mode) {
       CK(hipDeviceSynchronize());
       CK(hipEventRecord(e0));
       for (size_t s = 0; s < slices; ++s) {
         const u32x4* src = reinterpret_cast<const u32x4*>(a + s * S);
         u32x4* dst = reinterpret_cast<u32x4*>(b + s * S);
-        if (mode == 0 || mode == 3)
+        if (mode == 0 || mode == 3 || mode == 4)
           hipLaunchKernelGGL(k_read, dim3(G), dim3(256), 0, 0, src, n4, sink);
+        if (mode == 4) hipLaunchKernelGGL(k_read, dim3(G), dim3(256), 0, 0, src, n4, sink);
         if (mode == 1) {
           const size_t per = 6400;  // 100 KB per wave
           const size_t waves = (n4 + per - 1) / per;
@@ -91,11 +92,12 @@ int main(int argc, char** argv) {
       float ms;
       CK(hipEventElapsedTime(&ms, e0, e1));
       ms /= slices;
-      (mode == 0 ? t_read : mode == 1 ? t_tiles : mode == 2 ? t_copy : t_both) = ms;
+      (mode == 0 ? t_read : mode == 1 ? t_tiles : mode == 2 ? t_copy : mode == 3 ? t_both : t_rr) = ms;
     }
     auto g = [](double bytes, float ms) { return bytes / (ms * 1e-3) / 1e9; };
-    printf("%10.1f %9.1f %9.1f %9.1f %9.1f %9.1f\n", S / 1e6, g(S, t_read), g(S, t_tiles),
-           g(2.0 * S, t_copy), g(3.0 * S, t_both), g(2.0 * S, t_both - t_read));
+    printf("%10.1f %9.1f %9.1f %9.1f %9.1f %9.1f %9.1f %9.1f\n", S / 1e6, g(S, t_read), g(S, t_tiles),
+           g(2.0 * S, t_copy), g(3.0 * S, t_both), g(2.0 * S, t_both - t_read), g(2.0 * S, t_rr),
+           g(S, t_rr - t_read));
   }
   return 0;
 }

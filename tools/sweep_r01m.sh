@@ -1,0 +1,12 @@
+#!/bin/bash
+set -o pipefail
+mkdir -p gpurun_out/sw13
+timeout -k 10 300 python -u -m pytest tests/test_gpu_partition.py -x -q --timeout 200 --timeout-method thread > gpurun_out/sw13/tests.log 2>&1 || { tail -40 gpurun_out/sw13/tests.log; exit 1; }
+tail -2 gpurun_out/sw13/tests.log
+timeout -k 10 120 tools/stamps > gpurun_out/sw13/stamps.txt 2>&1 || { cat gpurun_out/sw13/stamps.txt; exit 1; }
+cat gpurun_out/sw13/stamps.txt
+tools/sweep.sh gpurun_out/sw13 \
+ ";--steps 3 --warmup 1" \
+ "SUX_S6_TPW=16;--steps 3 --warmup 1" \
+ "SUX_SCATTER=v7;--steps 3 --warmup 1"
+cat gpurun_out/sw13/sweep.txt
