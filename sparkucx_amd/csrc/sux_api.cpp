@@ -546,8 +546,8 @@ int sux_partition_maps_peer_major(sux_node* node, const sux_partitioner* part,
                                   uint64_t ws_bytes, void* stream) {
   return guard([&] {
     require(node && part, SUX_EINVAL, "NULL node/partitioner");
-    require(world >= 1 && world <= part->desc.num_partitions, SUX_EINVAL,
-            "world must be in [1, R]");
+    require(world >= 1 && world <= part->desc.num_partitions && world <= 1024, SUX_EINVAL,
+            "world must be in [1, min(R, 1024)]");
     require(d_records || n == 0, SUX_EINVAL, "records pointer is NULL");
     node->bind();
     Group G = make_group(part, d_records, rs, rpm, n);

@@ -233,6 +233,33 @@ __global__ __launch_bounds__(256) void k_tile_scan(uint32_t* counts, uint64_t* t
   if (lane == 0) totals[row] = carry;
 }
 
+// Few tiles per map (large R: 10,000 partitions x 16 tiles): one thread per row, so a row of
+// T <= 64 counters is not a whole (mostly idle) wave.
+__global__ __launch_bounds__(256) void k_tile_scan_rows(uint32_t* counts, uint64_t* totals,
+                                                        uint32_t rows, uint32_t tiles) {
+  const uint32_t row = blockIdx.x * 256 + threadIdx.x;
+  if (row >= rows) return;
+  uint32_t* c = counts + (uint64_t)row * tiles;
+  uint32_t carry = 0;
+  uint32_t t = 0;
+  for (; t + 8 <= tiles; t += 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = c[t + k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      c[t + k] = carry;
+      carry += v[k];
+    }
+  }
+  for (; t < tiles; ++t) {
+    const uint32_t v = c[t];
+    c[t] = carry;
+    carry += v;
+  }
+  totals[row] = carry;
+}
+
 // ------------------------------------------------------------------------------------------
 // K2b: per-group scans -> index tables and destination bases
 // ------------------------------------------------------------------------------------------
@@ -272,81 +299,108 @@ __device__ __forceinline__ uint64_t bswap64(uint64_t v) {
   return ((uint64_t)__builtin_bswap32((uint32_t)v) << 32) | __builtin_bswap32((uint32_t)(v >> 32));
 }
 
-// Position of (m, p) in the peer-major order (h, m, p in [lo_h, hi_h)).
-__device__ __forceinline__ void peer_major_pos(uint64_t j, uint32_t M, int R, int G, uint32_t& m,
-                                               uint32_t& p) {
-  // find h with M*lo_h <= j < M*lo_{h+1}; lo_h = floor(h*R/G)
-  int h = 0;
-  while (h + 1 < G && (uint64_t)M * (uint64_t)(((int64_t)(h + 1) * R) / G) <= j) ++h;
-  uint32_t lo = (uint32_t)(((int64_t)h * R) / G), hi = (uint32_t)(((int64_t)(h + 1) * R) / G);
-  uint64_t r = j - (uint64_t)M * lo;
-  uint32_t w = hi - lo;
-  m = (uint32_t)(r / w);
-  p = lo + (uint32_t)(r % w);
+__device__ __forceinline__ uint32_t owner_of(uint32_t p, int R, int G) {
+  // largest h with floor(h*R/G) <= p
+  return (uint32_t)((((uint64_t)p + 1) * G + R - 1) / R) - 1;
 }
 
-__global__ __launch_bounds__(kScanThreads) void k_group_scan(const uint64_t* totals,
-                                                             uint64_t* base, int64_t* index,
-                                                             uint8_t* index_be, uint64_t* peer_bytes,
-                                                             uint32_t M, int R, int G,
-                                                             uint32_t rec_size) {
+// K2b: one workgroup per map.  In-map exclusive scan of the partition totals -> the map's index
+// file (P3: native and big-endian), and
+//   G == 1 (map-major data files): base[m][p] = m * records_per_map + prefix (all maps but the
+//          last are full, so map m's data file starts at record m * records_per_map);
+//   G > 1  (peer-major send layout): prefix -> pre[m][p], per-peer sums -> mh[m][h].
+// Maps are independent, so the launch has M workgroups (was one workgroup over M x R).
+__global__ __launch_bounds__(kScanThreads) void k_map_scan(const uint64_t* __restrict__ totals,
+                                                           uint64_t* __restrict__ base,
+                                                           uint64_t* __restrict__ pre,
+                                                           uint64_t* __restrict__ mh,
+                                                           int64_t* __restrict__ index,
+                                                           uint8_t* __restrict__ index_be,
+                                                           uint64_t* __restrict__ peer_bytes,
+                                                           int R, int G, uint32_t rec_size,
+                                                           uint64_t records_per_map,
+                                                           uint64_t num_records) {
   __shared__ uint64_t sh[2 * kWave + 1];
-  const uint64_t L = (uint64_t)M * R;
-  // pass A: (m, p) order -> map-local index tables; also the map-major base (G == 1)
+  __shared__ unsigned long long hs[1024];
+  const uint32_t m = blockIdx.x;
+  const uint64_t* tm = totals + (uint64_t)m * R;
+  int64_t* im = index + (uint64_t)m * (R + 1);
+  uint64_t* ibe = index_be ? reinterpret_cast<uint64_t*>(index_be) + (uint64_t)m * (R + 1) : nullptr;
+  if (G > 1)
+    for (int h = threadIdx.x; h < G; h += kScanThreads) hs[h] = 0;
+  uint64_t carry = 0;
+  for (int p0 = 0; p0 < R; p0 += kScanThreads) {
+    const int p = p0 + threadIdx.x;
+    const uint64_t v = p < R ? tm[p] : 0;
+    uint64_t tot;
+    const uint64_t ex = carry + block_excl_scan(v, sh, &tot);  // barriers inside
+    if (p < R) {
+      const int64_t off = (int64_t)(ex * rec_size);
+      im[p] = off;
+      if (ibe) ibe[p] = bswap64((uint64_t)off);
+      if (G == 1) {
+        base[(uint64_t)m * R + p] = (uint64_t)m * records_per_map + ex;
+      } else {
+        pre[(uint64_t)m * R + p] = ex;
+        atomicAdd(&hs[owner_of((uint32_t)p, R, G)], (unsigned long long)v);
+      }
+    }
+    carry += tot;
+  }
+  if (threadIdx.x == 0) {
+    const int64_t off = (int64_t)(carry * rec_size);
+    im[R] = off;
+    if (ibe) ibe[R] = bswap64((uint64_t)off);
+    if (G == 1 && m == 0 && peer_bytes) peer_bytes[0] = num_records * rec_size;
+  }
+  if (G > 1) {
+    __syncthreads();
+    for (int h = threadIdx.x; h < G; h += kScanThreads) mh[(uint64_t)m * G + h] = hs[h];
+  }
+}
+
+// G > 1: per-peer byte counts, then an exclusive scan of mh in peer-major (h, m) order, in place:
+// mh[m][h] becomes the send-buffer record offset of (peer h, map m).
+__global__ __launch_bounds__(kScanThreads) void k_peer_off(uint64_t* __restrict__ mh,
+                                                           uint64_t* __restrict__ peer_bytes,
+                                                           uint32_t M, int G, uint32_t rec_size) {
+  __shared__ uint64_t sh[2 * kWave + 1];
+  if (peer_bytes)
+    for (int h = threadIdx.x; h < G; h += kScanThreads) {
+      uint64_t t = 0;
+      for (uint32_t m = 0; m < M; ++m) t += mh[(uint64_t)m * G + h];
+      peer_bytes[h] = t * rec_size;
+    }
+  __syncthreads();
+  const uint64_t L = (uint64_t)M * G;
   uint64_t carry = 0;
   for (uint64_t j0 = 0; j0 < L; j0 += kScanThreads) {
-    uint64_t j = j0 + threadIdx.x;
-    uint64_t v = j < L ? totals[j] : 0;
-    uint64_t tot;
-    uint64_t ex = carry + block_excl_scan(v, sh, &tot);
+    const uint64_t j = j0 + threadIdx.x;  // j = h * M + m
+    uint64_t v = 0, idx = 0;
     if (j < L) {
-      if (G == 1) base[j] = ex;  // map-major layout: the (m, p) prefix is the destination
-      base[L + j] = ex;          // (m, p)-order prefix, read back for the index tables below
-    }
-    carry += tot;
-  }
-  __syncthreads();
-  // index tables: off_m[p] = (A[m][p] - A[m][0]) * S ; off_m[R] = (A[m+1][0] - A[m][0]) * S
-  const uint64_t* A = base + L;
-  const uint64_t LR1 = (uint64_t)M * (R + 1);
-  for (uint64_t k = threadIdx.x; k < LR1; k += kScanThreads) {
-    uint32_t m = (uint32_t)(k / (R + 1)), p = (uint32_t)(k % (R + 1));
-    uint64_t a0 = A[(uint64_t)m * R];
-    uint64_t ap = (p < (uint32_t)R) ? A[(uint64_t)m * R + p]
-                                    : (m + 1 < M ? A[(uint64_t)(m + 1) * R] : carry);
-    int64_t off = (int64_t)((ap - a0) * rec_size);
-    index[k] = off;
-    if (index_be) reinterpret_cast<uint64_t*>(index_be)[k] = bswap64((uint64_t)off);
-  }
-  if (G == 1) {
-    if (threadIdx.x == 0 && peer_bytes) peer_bytes[0] = carry * rec_size;
-    return;
-  }
-  // pass B: peer-major order (h, m, p) -> destination bases in the send buffer
-  carry = 0;
-  for (uint64_t j0 = 0; j0 < L; j0 += kScanThreads) {
-    uint64_t j = j0 + threadIdx.x;
-    uint32_t m = 0, p = 0;
-    uint64_t v = 0;
-    if (j < L) {
-      peer_major_pos(j, M, R, G, m, p);
-      v = totals[(uint64_t)m * R + p];
+      const uint64_t h = j / M, m = j - h * M;
+      idx = m * G + h;
+      v = mh[idx];
     }
     uint64_t tot;
-    uint64_t ex = carry + block_excl_scan(v, sh, &tot);
-    if (j < L) base[(uint64_t)m * R + p] = ex;
+    const uint64_t ex = carry + block_excl_scan(v, sh, &tot);
+    if (j < L) mh[idx] = ex;
     carry += tot;
   }
-  __syncthreads();
-  if (peer_bytes && threadIdx.x < (unsigned)G) {
-    // bytes for peer h = sum over m, p in h's range
-    int h = threadIdx.x;
-    uint32_t lo = (uint32_t)(((int64_t)h * R) / G), hi = (uint32_t)(((int64_t)(h + 1) * R) / G);
-    uint64_t s = 0;
-    for (uint32_t m = 0; m < M; ++m)
-      for (uint32_t p = lo; p < hi; ++p) s += totals[(uint64_t)m * R + p];
-    peer_bytes[h] = s * rec_size;
-  }
+}
+
+// G > 1: base[m][p] = offset of (owner(p), m) + prefix of p inside its owner's range of map m.
+__global__ __launch_bounds__(256) void k_peer_base(const uint64_t* __restrict__ pre,
+                                                   const uint64_t* __restrict__ mh,
+                                                   uint64_t* __restrict__ base, uint32_t M, int R,
+                                                   int G) {
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= (uint64_t)M * R) return;
+  const uint64_t m = j / R;
+  const uint32_t p = (uint32_t)(j - m * R);
+  const uint32_t h = owner_of(p, R, G);
+  const uint32_t lo = (uint32_t)(((int64_t)h * R) / G);
+  base[j] = mh[m * G + h] + pre[j] - pre[m * R + lo];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1258,7 +1312,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter7(MapGroup g, int R, int pid
       reinterpret_cast<u32x4*>(wcnt + tid * NW)[w / 4] = u32x4{0, 0, 0, 0};
   }
   begin_item(cur);
-  uint32_t ci = 0;
+  [[maybe_unused]] uint32_t ci = 0;  // chunk counter for the diagnostic stamps
   // one chunk: pids and records in (pidv, v); `ahead` is the chunk DEPTH positions later, loaded
   // into the same registers once they are free.  Returns false after the stream's last chunk.
   auto process = [&](const Cur& k, const Cur& ahead, uint32_t (&pidv)[NG], u32x4 (&v)[PER]) {
@@ -1498,7 +1552,8 @@ Workspace workspace_layout(uint32_t R, uint32_t rec_size, uint64_t records_per_m
   w.totals_bytes = align_up(maps * R * 8, 256);
   off += w.totals_bytes;
   w.base_off = off;
-  w.base_bytes = align_up(2 * maps * R * 8, 256);  // base + (m,p)-order scratch
+  // base [M][R] | in-map prefix [M][R] | per-(map, peer) sums [M][min(R, 1024)] (peer-major)
+  w.base_bytes = align_up((2 * maps * R + maps * (R < 1024 ? R : 1024)) * 8, 256);
   off += w.base_bytes;
   w.pids_off = off;
   w.pids_bytes = need_pids ? align_up(num_records * 2, 256) : 0;
@@ -1640,10 +1695,24 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   // ---- K2: scans -> index tables + destination bases
   timer_begin(timer, kScan, s);
   const uint32_t rows = g.num_maps * (uint32_t)R;
-  hipLaunchKernelGGL(k_tile_scan, dim3((rows + 3) / 4), dim3(256), 0, s, counts, totals, rows,
-                     g.tiles_per_map);
-  hipLaunchKernelGGL(k_group_scan, dim3(1), dim3(kScanThreads), 0, s, totals, base, d_index,
-                     d_index_be, d_peer_bytes, g.num_maps, R, lay.world, g.rec_size);
+  if (g.tiles_per_map <= 64)
+    hipLaunchKernelGGL(k_tile_scan_rows, dim3((rows + 255) / 256), dim3(256), 0, s, counts, totals,
+                       rows, g.tiles_per_map);
+  else
+    hipLaunchKernelGGL(k_tile_scan, dim3((rows + 3) / 4), dim3(256), 0, s, counts, totals, rows,
+                       g.tiles_per_map);
+  const uint64_t L = (uint64_t)g.num_maps * R;
+  uint64_t* pre = base + L;
+  uint64_t* mh = base + 2 * L;
+  hipLaunchKernelGGL(k_map_scan, dim3(g.num_maps), dim3(kScanThreads), 0, s, totals, base, pre, mh,
+                     d_index, d_index_be, lay.world == 1 ? d_peer_bytes : nullptr, R, lay.world,
+                     g.rec_size, g.records_per_map, g.num_records);
+  if (lay.world > 1) {
+    hipLaunchKernelGGL(k_peer_off, dim3(1), dim3(kScanThreads), 0, s, mh, d_peer_bytes,
+                       g.num_maps, lay.world, g.rec_size);
+    hipLaunchKernelGGL(k_peer_base, dim3((uint32_t)((L + 255) / 256)), dim3(256), 0, s, pre, mh,
+                       base, g.num_maps, R, lay.world);
+  }
   timer_end(timer, kScan, s);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
