@@ -260,6 +260,23 @@ __global__ __launch_bounds__(256) void k_tile_scan_rows(uint32_t* counts, uint64
   totals[row] = carry;
 }
 
+// Tile-major counts [map][tile][p] (the small-record path): one thread per (map, p) walks the
+// tiles; a wave reads 64 consecutive counters of one tile row per step.
+__global__ __launch_bounds__(256) void k_tile_scan_tm(uint32_t* counts, uint64_t* totals,
+                                                      uint32_t maps, uint32_t R, uint32_t tiles) {
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;  // m * R + p
+  if (j >= (uint64_t)maps * R) return;
+  const uint64_t m = j / R, p = j - m * R;
+  uint32_t* c = counts + m * tiles * R + p;
+  uint32_t carry = 0;
+  for (uint32_t t = 0; t < tiles; ++t) {
+    const uint32_t v = c[(uint64_t)t * R];
+    c[(uint64_t)t * R] = carry;
+    carry += v;
+  }
+  totals[j] = carry;
+}
+
 // ------------------------------------------------------------------------------------------
 // K2b: per-group scans -> index tables and destination bases
 // ------------------------------------------------------------------------------------------
@@ -1498,6 +1515,136 @@ __global__ __launch_bounds__(NW * 64) void k_scatter7(MapGroup g, int R, int pid
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Small records (S = 16, SURVEY.md config C5: 16-byte key/value rows, 10,000 partitions).
+// A record is one aligned 16-byte unit and R is far too large for per-wave counters, so:
+//   k_hist16   persistent workgroups of 1024 threads, one tile at a time; every lane loads whole
+//              records (coalesced 16-byte units, 8 in flight per lane), hashes the key from its
+//              registers and counts into ONE per-workgroup LDS histogram of R counters.
+//   k_scatter16 persistent 1024-thread workgroups, one tile range at a time with an LDS cursor
+//              per partition.  The tile is cut into 64-record groups dealt to the waves in order;
+//              a group ranks its equal pids with a ballot match, then, when the LDS turn counter
+//              reaches it, reads and advances the cursors of its pids and hands the turn on.  Only
+//              that short step is serialised; loads and the 16-byte stores are not.
+// ------------------------------------------------------------------------------------------
+template <int KW>
+__global__ __launch_bounds__(1024) void k_hist16(PartDev pd, MapGroup g, uint16_t* __restrict__ pids,
+                                                uint32_t* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t hist[];  // [R]
+  const int R = pd.R;
+  const uint32_t ntiles = g.num_maps * g.tiles_per_map;
+  const u32x4* recs = reinterpret_cast<const u32x4*>(g.recs);
+  const int kw0 = pd.key_offset / 4;
+  for (int p = threadIdx.x; p < R; p += 1024) hist[p] = 0;
+  __syncthreads();
+  for (uint32_t gt = blockIdx.x; gt < ntiles; gt += gridDim.x) {
+    const TileRange tr = tile_range(g, gt);
+    for (uint64_t i0 = tr.begin; i0 < tr.end; i0 += 8 * 1024) {
+      u32x4 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint64_t i = i0 + k * 1024 + threadIdx.x;
+        v[k] = recs[i < tr.end ? i : tr.begin];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint64_t i = i0 + k * 1024 + threadIdx.x;
+        if (i < tr.end) {
+          uint32_t w[KW];
+#pragma unroll
+          for (int q = 0; q < KW; ++q) {
+            const int d = kw0 + q;
+            w[q] = d == 0 ? v[k][0] : d == 1 ? v[k][1] : d == 2 ? v[k][2] : v[k][3];
+          }
+          const int p = partition_words<KW, false>(pd, w, pd.bounds, pd.lut);
+          atomicAdd(&hist[p], 1u);
+          pids[i] = (uint16_t)p;
+        }
+      }
+    }
+    __syncthreads();
+    // tile-major counts [map][tile][p]: one contiguous row per tile (a partition-major column
+    // would touch R lines at a 4*tiles stride for R 4-byte counters)
+    uint32_t* dst = counts + ((uint64_t)tr.map * g.tiles_per_map + tr.tile) * R;
+    for (int p = threadIdx.x; p < R; p += 1024) {
+      dst[p] = hist[p];
+      hist[p] = 0;
+    }
+    __syncthreads();
+  }
+}
+
+template <uint32_t NW>
+__global__ __launch_bounds__(NW * 64) void k_scatter16(MapGroup g, int R, int pid_bits,
+                                                       const uint16_t* __restrict__ pids,
+                                                       const uint32_t* __restrict__ prefix,
+                                                       const uint64_t* __restrict__ base,
+                                                       uint8_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t cur[];  // [R] next output record of p
+  __shared__ uint32_t turn;
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const uint32_t ntiles = g.num_maps * g.tiles_per_map;
+  const u32x4* recs = reinterpret_cast<const u32x4*>(g.recs);
+  u32x4* out4 = reinterpret_cast<u32x4*>(out);
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  for (uint32_t gt = xcd_map(blockIdx.x, gridDim.x); gt < ntiles; gt += gridDim.x) {
+    const TileRange tr = tile_range(g, gt);
+    const uint64_t* bm = base + (uint64_t)tr.map * R;
+    const uint32_t* pm = prefix + ((uint64_t)tr.map * g.tiles_per_map + tr.tile) * R;  // tile-major
+    for (int p = tid; p < R; p += NW * kWave) cur[p] = (uint32_t)(bm[p] + pm[p]);
+    if (tid == 0) turn = 0;
+    __syncthreads();
+    const uint32_t ngroups = (uint32_t)((tr.end - tr.begin + kWave - 1) / kWave);
+    // group q = wave + k * NW; the loads of the next two groups of this wave are in flight
+    // during this group's turn (clamped, unconditional: the compiler's waits stay counted)
+    auto load = [&](uint32_t qq, uint32_t& pv, u32x4& rv) {
+      const uint64_t i = tr.begin + (uint64_t)qq * kWave + lane;
+      const uint64_t ii = i < tr.end ? i : tr.end - 1;
+      pv = pids[ii];
+      rv = recs[ii];
+    };
+    uint32_t q = wave;
+    uint32_t pid0, pid1;
+    u32x4 rec0, rec1;
+    load(q, pid0, rec0);
+    load(q + NW, pid1, rec1);
+    while (q < ngroups) {
+      const uint64_t i = tr.begin + (uint64_t)q * kWave + lane;
+      const bool valid = i < tr.end;
+      uint32_t pid2;
+      u32x4 rec2;
+      load(q + 2 * NW, pid2, rec2);
+      const uint32_t p = valid ? pid0 : 0u;
+      uint64_t peers = __ballot(valid);
+      for (int bb = 0; bb < pid_bits; ++bb) {
+        const bool bit = (p >> bb) & 1u;
+        const uint64_t m = __ballot(bit);
+        peers &= bit ? m : ~m;
+      }
+      // this group's turn: groups update the cursors in input order (stability)
+      for (uint32_t spin = 0; __hip_atomic_load(&turn, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q;
+           ++spin) {
+        __builtin_amdgcn_s_sleep(1);
+        if (spin > (1u << 22)) break;  // never reached: a guard against a hang, not a path
+      }
+      uint32_t r0 = 0;
+      if (valid) r0 = cur[p];
+      __builtin_amdgcn_wave_barrier();
+      if (valid && (peers & lt_mask) == 0) cur[p] = r0 + (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&turn, q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (valid) out4[(uint64_t)r0 + (uint32_t)__popcll(peers & lt_mask)] = rec0;
+      pid0 = pid1;
+      rec0 = rec1;
+      pid1 = pid2;
+      rec1 = rec2;
+      q += NW;
+    }
+    __syncthreads();
+  }
+}
+
 template <int KW, bool TAB>
 static void launch_hist3_kw(dim3 grid, size_t lds, hipStream_t s, const PartDev& pd,
                             const MapGroup& g, uint16_t* pids, uint32_t* counts) {
@@ -1622,12 +1769,32 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   static const int hv = env_variant("SUX_HIST", 4);
   const bool shaped = (S == 100 || S == 16) && R <= 4096;  // v2 instantiations
   const bool words = pd.kind != 4 && pd.key_offset % 4 == 0 && pd.key_len <= 16;
+  // small records with many partitions: k_hist16 + tile-major counts + k_scatter16, together
+  static const int sv = env_variant("SUX_SCATTER", 7);
+  const bool s16 = hv >= 4 && sv >= 7 && words && S == 16 && R > 1024 &&
+                   (reinterpret_cast<uintptr_t>(g.recs) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(d_out) & 15) == 0;
   int hist = 1;
-  if (hv >= 4 && words && R <= 4096 && S == 100 && (pd.key_offset + pd.key_len) <= (int)S) hist = 4;
+  if (s16) hist = 16;
+  else if (hv >= 4 && words && R <= 4096 && S == 100 && (pd.key_offset + pd.key_len) <= (int)S) hist = 4;
   else if (hv >= 3 && words && R <= 4096) hist = 3;
   else if (hv >= 2 && shaped) hist = 2;
   timer_begin(timer, kHist, s);
-  if (hist == 4) {
+  if (hist == 16) {
+    const size_t lds = (size_t)R * 4;
+    const int kw = (pd.key_len + 3) / 4;
+    const dim3 gridp(std::min<uint32_t>(total_tiles, 256u * std::max<uint32_t>(1, (160u * 1024) / (uint32_t)lds)));
+#define SUX_H16(KW)                                                                        \
+  do {                                                                                     \
+    allow_lds(reinterpret_cast<const void*>(&k_hist16<KW>), lds);                          \
+    hipLaunchKernelGGL((k_hist16<KW>), gridp, dim3(1024), lds, s, pd, g, pids, counts);     \
+  } while (0)
+    if (kw <= 1) SUX_H16(1);
+    else if (kw == 2) SUX_H16(2);
+    else if (kw == 3) SUX_H16(3);
+    else SUX_H16(4);
+#undef SUX_H16
+  } else if (hist == 4) {
     static const int hch = [] {
       const char* e = getenv("SUX_H4CH");
       return e ? atoi(e) : 64;
@@ -1695,7 +1862,10 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   // ---- K2: scans -> index tables + destination bases
   timer_begin(timer, kScan, s);
   const uint32_t rows = g.num_maps * (uint32_t)R;
-  if (g.tiles_per_map <= 64)
+  if (s16)
+    hipLaunchKernelGGL(k_tile_scan_tm, dim3((rows + 255) / 256), dim3(256), 0, s, counts, totals,
+                       g.num_maps, (uint32_t)R, g.tiles_per_map);
+  else if (g.tiles_per_map <= 64)
     hipLaunchKernelGGL(k_tile_scan_rows, dim3((rows + 255) / 256), dim3(256), 0, s, counts, totals,
                        rows, g.tiles_per_map);
   else
@@ -1719,7 +1889,6 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
 
   // ---- K3: stable scatter.  S = 100 (TeraSort rows): v7 for R <= 512, v6 for the R whose
   // LDS image still fits; any other shape: the v2 (R <= 4096, S in {16, 100}) or v1 kernels.
-  static const int sv = env_variant("SUX_SCATTER", 7);
   // tuning overrides: SUX_S6=C (v6 records per chunk: 1024 | 512 | 384 | 256), SUX_S6_TPW=tiles
   // per work item, SUX_S7=2|3 (v7 at 768-record chunks with 2 | 1 chunks in flight)
   static const int s6c = [] {
@@ -1750,7 +1919,15 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   const bool v7 = c6 == 1024 && sv >= 7 && R <= 512 &&
                   Sc7<100, 1024, 16>::lds_bytes(R) <= 160 * 1024;
   timer_begin(timer, kScatter, s);
-  if (v7) {
+  if (s16) {
+    const size_t lds = (size_t)R * 4;
+    allow_lds(reinterpret_cast<const void*>(&k_scatter16<16>), lds);
+    const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(2, (160u * 1024) / (uint32_t)lds));
+    const dim3 grid(std::min<uint32_t>(total_tiles, 256u * per_cu));
+    hipLaunchKernelGGL((k_scatter16<16>), grid, dim3(1024), lds, s, g, R, bits, pids, counts, base,
+                       d_out);
+    e = hipGetLastError();
+  } else if (v7) {
     uint32_t tpw = s6tpw > 0 ? (uint32_t)s6tpw
                              : (uint32_t)std::max<uint64_t>(1, (8ull * 1024 + g.tile_recs - 1) / g.tile_recs);
     if (tpw > g.tiles_per_map) tpw = g.tiles_per_map;
