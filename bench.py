@@ -94,6 +94,29 @@ def cpu_baseline(args) -> dict | None:
                       f"(map {tm:.3f}s, fetch {tf:.3f}s)"}
 
 
+def reduce_sort(node, recs, ns: int, rs: int, dev) -> dict:
+    """Reduce-side consumer: stable GPU sort of one reduce partition's
+    worth of TeraSort records by their 10-byte key (the reader's ExternalSorter step).  Reported
+    as record bytes sorted per second; the algorithmic bytes are 2 x records x S (read and write
+    each record once), the radix passes over 16-byte (key, index) pairs come on top."""
+    out = torch.empty(ns * rs, dtype=torch.uint8, device=dev)
+    ws = torch.empty(node.sort_workspace_size(ns, rs), dtype=torch.uint8, device=dev)
+    for _ in range(2):  # warm-up
+        node.sort_records(recs, rs, N.SORT_BYTES, 0, 10, num_records=ns, out=out, workspace=ws)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 5
+    e0.record()
+    for _ in range(reps):
+        node.sort_records(recs, rs, N.SORT_BYTES, 0, 10, num_records=ns, out=out, workspace=ws)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    return {"records": ns, "record_bytes": ns * rs, "ms": round(ms, 3),
+            "GB/s": round(ns * rs / (ms / 1e3) / 1e9, 1), "key": "10-byte unsigned, stable",
+            "alg_bytes": 2 * ns * rs}
+
+
 def load_traffic(kernel: str) -> float | None:
     """Per-launch HBM bytes of `kernel` from the committed PMC summary (profiles/pmc_r01.json,
     written by profiles/collect_pmc.py; FETCH_SIZE x2 + WRITE_SIZE per the microarch guide)."""
@@ -126,6 +149,9 @@ def main():
     ap.add_argument("--reserve-cus", type=int, default=-1,
                     help="CUs kept free of map-side kernels for the exchange (-1: 32 if N>1, "
                          "else 0)")
+    ap.add_argument("--reduce-sort-records", type=int, default=-1,
+                    help="N=1: also time the reduce-side sort (sux_sort_records) of one reduce "
+                         "partition's worth of records (-1: records/R; 0: skip)")
     ap.add_argument("--cpu-records", type=int, default=10_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-reps", type=int, default=3)
@@ -387,6 +413,11 @@ def main():
             "bound": "xgmi", "achieved": None if ach is None else round(ach, 1), "peak": peak,
             "unit": "GB/s", "frac": None if ach is None else round(ach / peak, 4),
             "remote_bytes_per_rank": remote // args.steps, "exchange_ms": round(xms, 2)}
+    if world == 1:
+        ns = args.reduce_sort_records if args.reduce_sort_records >= 0 else n // R
+        ns = min(ns, n)
+        if ns > 0 and args.workload == "terasort":
+            result["reduce_sort"] = reduce_sort(node, out[:ns * rs], ns, rs, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:

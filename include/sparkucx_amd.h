@@ -240,6 +240,24 @@ int sux_buffer_info(sux_buffer* buf, void** dev_ptr, uint64_t* size, uint64_t* c
 int sux_buffer_retain(sux_buffer* buf, int32_t count);
 int sux_buffer_release(sux_buffer* buf);
 
+/* ---- reduce side: sort by key ------------------------------------- *
+ * After the fetch, Spark's reader sorts the partition's records when the dependency has a key
+ * ordering (ExternalSorter, compat/spark_3_0/UcxShuffleReader.scala:138-154; TeraSort's reduce).
+ * sux_sort_records is that sort on the GPU: `n` fixed-size records (record_size % 4 == 0) from
+ * d_in are written to d_out (out of place) in ascending key order; records with equal keys keep
+ * their input order, so sorting the canonical map-ordered concatenation of a partition's blocks
+ * (sux_fetch_blocks) gives one deterministic answer where Spark's depends on fetch order (Q4).
+ * Keys: SUX_SORT_BYTES = key_len (1..12) bytes compared unsigned lexicographically (TeraSort's
+ * 10-byte keys); SUX_SORT_LONG / SUX_SORT_INT = signed little-endian int64 / int32 (Spark's
+ * LongType / IntegerType orderings).  Workspace: sux_sort_workspace_size (about 32 B/record). */
+#define SUX_SORT_BYTES 1
+#define SUX_SORT_LONG 2
+#define SUX_SORT_INT 3
+int sux_sort_workspace_size(uint64_t n, uint32_t record_size, uint64_t* bytes);
+int sux_sort_records(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
+                     uint32_t record_size, int32_t key_offset, int32_t key_len, void* d_out,
+                     void* d_ws, uint64_t ws_bytes, void* stream);
+
 /* ---- CU-partitioned streams (exchange/compute overlap) ---------------------------------- *
  * A non-blocking HIP stream (returned as void*) whose kernels run on `num_cus` of the device's
  * CUs, spread evenly over all 8 XCDs x 4 shader engines (use a multiple of 32: an SE with fewer

@@ -233,3 +233,30 @@ def cpu_shuffle(part: Partitioner, recs: np.ndarray, rec_size: int, num_maps: in
     if rc != 0:
         raise RuntimeError("cpu shuffle failed")
     return res
+
+
+SORT_BYTES, SORT_LONG, SORT_INT = 1, 2, 3
+
+
+def sort_records(recs: np.ndarray, rec_size: int, kind: int, key_offset: int,
+                 key_len: int) -> np.ndarray:
+    """Reduce-side sort: the reader's ExternalSorter step when the
+    dependency has a key ordering (compat/spark_3_0/UcxShuffleReader.scala:138-154).  Stable in
+    input order for equal keys — the canonical answer for a map-ordered concatenation (Spark's
+    own order for equal keys depends on the fetch order, quirk Q4).  Keys: unsigned byte
+    lexicographic (TeraSort's comparator), or signed little-endian int64 / int32 (Spark's
+    LongType / IntegerType orderings)."""
+    rows = np.ascontiguousarray(recs).reshape(-1, rec_size)
+    n = rows.shape[0]
+    if n == 0:
+        return rows.reshape(-1).copy()
+    key = np.ascontiguousarray(rows[:, key_offset:key_offset + key_len])
+    if kind == SORT_BYTES:
+        order = np.argsort(key.view(np.dtype((np.void, key_len))).ravel(), kind="stable")
+    elif kind == SORT_LONG:
+        order = np.argsort(key.view("<i8").ravel(), kind="stable")
+    elif kind == SORT_INT:
+        order = np.argsort(key.view("<i4").ravel(), kind="stable")
+    else:
+        raise ValueError(f"unknown sort key kind {kind}")
+    return rows[order].reshape(-1)

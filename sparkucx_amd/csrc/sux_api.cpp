@@ -1106,6 +1106,111 @@ int sux_buffer_release(sux_buffer* b) {
   });
 }
 
+// ---- reduce-side sort ----------------------------------------------------
+namespace {
+struct SortPlan {
+  uint64_t n;
+  uint32_t rs;
+  sux::MapGroup g{};
+  sux::Workspace ws{};
+  uint64_t pairs_bytes, part_off, index_off, total;
+};
+
+void sort_plan(uint64_t n, uint32_t rs, SortPlan& P) {
+  check_record_size(rs);
+  require(n < (1ull << 32), SUX_ERANGE, "sort: fewer than 2^32 records per call");
+  P.n = n;
+  P.rs = rs;
+  const uint32_t R = 1u << sux::kRadixBits;
+  const uint64_t rpm = n ? n : 1;
+  const uint32_t tile = sux::choose_tile_recs(R, 16, rpm);
+  P.g.records_per_map = rpm;
+  P.g.num_records = n;
+  P.g.num_maps = 1;
+  P.g.rec_size = 16;
+  P.g.tile_recs = tile;
+  P.g.tiles_per_map = (uint32_t)((rpm + tile - 1) / tile);
+  P.ws = sux::workspace_layout(R, 16, rpm, n, tile, true);
+  auto up = [](uint64_t v) { return (v + 255) / 256 * 256; };
+  P.pairs_bytes = up(16 * (n ? n : 1));
+  P.part_off = 2 * P.pairs_bytes;
+  P.index_off = P.part_off + up(P.ws.total);
+  P.total = P.index_off + up(8ull * (R + 1));
+}
+
+int sort_key_bits(int32_t kind, int32_t key_len) {
+  switch (kind) {
+    case SUX_SORT_BYTES:
+      require(key_len >= 1 && key_len <= 12, SUX_EINVAL, "sort: byte keys of 1..12 bytes");
+      return 8 * key_len;
+    case SUX_SORT_LONG:
+      require(key_len == 8, SUX_EINVAL, "sort: a long key is 8 bytes");
+      return 64;
+    case SUX_SORT_INT:
+      require(key_len == 4, SUX_EINVAL, "sort: an int key is 4 bytes");
+      return 32;
+  }
+  raise(SUX_EINVAL, "sort: unknown key kind " + std::to_string(kind));
+  return 0;
+}
+}  // namespace
+
+int sux_sort_workspace_size(uint64_t n, uint32_t record_size, uint64_t* bytes) {
+  return guard([&] {
+    require(bytes, SUX_EINVAL, "NULL argument");
+    SortPlan P;
+    sort_plan(n, record_size, P);
+    *bytes = P.total;
+  });
+}
+
+int sux_sort_records(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
+                     uint32_t record_size, int32_t key_offset, int32_t key_len, void* d_out,
+                     void* d_ws, uint64_t ws_bytes, void* stream) {
+  return guard([&] {
+    require(node, SUX_EINVAL, "NULL node");
+    const int bits = sort_key_bits(key_kind, key_len);
+    require(key_offset >= 0 && (uint64_t)key_offset + key_len <= record_size, SUX_EINVAL,
+            "sort: the key does not fit the record");
+    SortPlan P;
+    sort_plan(n, record_size, P);
+    if (n == 0) return;
+    require(d_in && d_out && d_ws, SUX_EINVAL, "NULL buffer");
+    require(ws_bytes >= P.total, SUX_EINVAL,
+            "sort workspace too small: need " + std::to_string(P.total) + " bytes");
+    require(((uintptr_t)d_in & 3) == 0 && ((uintptr_t)d_out & 3) == 0 &&
+                ((uintptr_t)d_ws & 255) == 0,
+            SUX_EINVAL, "records (4 B) and workspace (256 B) must be aligned");
+    require(d_in != d_out, SUX_EINVAL, "sort is out of place");
+    node->bind();
+    hipStream_t s = node->stream(stream);
+    uint8_t* ws = static_cast<uint8_t*>(d_ws);
+    uint8_t* pa = ws;
+    uint8_t* pb = ws + P.pairs_bytes;
+    int64_t* index = reinterpret_cast<int64_t*>(ws + P.index_off);
+    hip_check(sux::launch_sort_pairs(static_cast<const uint8_t*>(d_in), n, record_size, key_kind,
+                                     key_offset, key_len, pa, s),
+              "sort pairs");
+    sux::PartDev pd{};
+    pd.kind = sux::kPartRadix;
+    pd.R = 1 << sux::kRadixBits;
+    pd.key_offset = 0;
+    pd.key_len = 16;
+    pd.ascending = 1;
+    sux::LayoutDesc lay{1, 16};
+    // the key occupies bits [128 - bits, 128) of the big-endian pair; least significant digit first
+    for (int sh = 128 - bits; sh < 128; sh += sux::kRadixBits) {
+      pd.seed = sh;
+      P.g.recs = pa;
+      hip_check(sux::launch_partition_group(pd, P.g, lay, pb, index, nullptr, nullptr,
+                                            ws + P.part_off, P.ws, nullptr, &node->timer, s),
+                "sort digit pass");
+      std::swap(pa, pb);
+    }
+    hip_check(sux::launch_gather_records(d_in, pa, n, record_size, d_out, s), "sort gather");
+  });
+}
+
 // ---- CU-partitioned streams -------------------------------------------------------------------
 // CU-mask bit of the k-th reserved CU.  Measured (tools/cu_probe: HW_REG_XCC_ID + HW_REG_HW_ID
 // of the workgroups of masked streams, profiles/r01_cu_probe_*.txt): the driver maps the mask

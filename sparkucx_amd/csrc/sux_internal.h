@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <string>
 
 namespace sux {
@@ -86,6 +87,14 @@ hipError_t launch_gather_copy(const CopyDesc* d_desc, uint32_t n, uint32_t chunk
 hipError_t launch_pull(int32_t W, int32_t me, const uint64_t* srcs, const int64_t* gi, int32_t M,
                        int32_t R, uint8_t* recv, uint64_t cap, uint64_t* recv_bytes,
                        hipStream_t s);
+
+// Reduce-side sort (sux_sort.hip): (key, index) pairs, and the final gather of whole records.
+constexpr int kPartRadix = 7;  // internal partitioner: 12-bit digit (shift in PartDev::seed)
+constexpr int kRadixBits = 12;
+hipError_t launch_sort_pairs(const uint8_t* in, uint64_t n, uint32_t rs, int kind, int key_offset,
+                             int key_len, void* pairs, hipStream_t s);
+hipError_t launch_gather_records(const void* in, const void* pairs, uint64_t n, uint32_t rs,
+                                 void* out, hipStream_t s);
 
 // Generators (sux_gen.hip).
 hipError_t launch_generate(int kind, uint64_t seed, uint64_t first, uint64_t n,

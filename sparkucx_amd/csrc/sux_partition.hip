@@ -133,6 +133,15 @@ __device__ __forceinline__ int get_partition(const PartDev& pd, const uint8_t* r
       int32_t r = (int32_t)ld_u32(rec, pd.key_offset) % pd.R;
       return r + (r < 0 ? pd.R : 0);
     }
+    case kPartRadix: {  // internal: digit of the big-endian 128-bit (key, index) pair
+      const uint64_t hi = ((uint64_t)__builtin_bswap32(ld_u32(rec, 0)) << 32) |
+                          __builtin_bswap32(ld_u32(rec, 4));
+      const uint64_t lo = ((uint64_t)__builtin_bswap32(ld_u32(rec, 8)) << 32) |
+                          __builtin_bswap32(ld_u32(rec, 12));
+      const int sh = pd.seed;
+      const uint64_t v = sh >= 64 ? (hi >> (sh - 64)) : ((lo >> sh) | (sh ? (hi << (64 - sh)) : 0));
+      return (int)(v & (uint64_t)(pd.R - 1));
+    }
   }
   return 0;
 }
@@ -260,21 +269,41 @@ __global__ __launch_bounds__(256) void k_tile_scan_rows(uint32_t* counts, uint64
   totals[row] = carry;
 }
 
-// Tile-major counts [map][tile][p] (the small-record path): one thread per (map, p) walks the
-// tiles; a wave reads 64 consecutive counters of one tile row per step.
+// Tile-major counts [map][tile][p] (the small-record path and the sort's digit passes).  A
+// workgroup owns 16 partitions of one map; its 16 x 16 threads each sum one of 16 segments of
+// the tile column (reads: 16 consecutive counters of one tile row per wave quarter), the 16
+// segment sums of a partition are scanned in LDS, and every thread rewrites its segment.
 __global__ __launch_bounds__(256) void k_tile_scan_tm(uint32_t* counts, uint64_t* totals,
                                                       uint32_t maps, uint32_t R, uint32_t tiles) {
-  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;  // m * R + p
-  if (j >= (uint64_t)maps * R) return;
-  const uint64_t m = j / R, p = j - m * R;
-  uint32_t* c = counts + m * tiles * R + p;
-  uint32_t carry = 0;
-  for (uint32_t t = 0; t < tiles; ++t) {
-    const uint32_t v = c[(uint64_t)t * R];
-    c[(uint64_t)t * R] = carry;
-    carry += v;
+  __shared__ uint32_t seg[16][17];
+  const uint32_t pl = threadIdx.x % 16, sg = threadIdx.x / 16;
+  const uint32_t pgroups = (R + 15) / 16;
+  const uint32_t m = blockIdx.x / pgroups, p = (blockIdx.x - m * pgroups) * 16 + pl;
+  const uint32_t per = (tiles + 15) / 16, t0 = min(sg * per, tiles), t1 = min(t0 + per, tiles);
+  uint32_t* c = counts + (uint64_t)m * tiles * R + p;
+  uint32_t sum = 0;
+  if (p < R)
+    for (uint32_t t = t0; t < t1; ++t) sum += c[(uint64_t)t * R];
+  seg[pl][sg] = sum;
+  __syncthreads();
+  if (sg == 0) {
+    uint32_t run = 0;
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t x = seg[pl][k];
+      seg[pl][k] = run;
+      run += x;
+    }
+    if (p < R) totals[(uint64_t)m * R + p] = run;
   }
-  totals[j] = carry;
+  __syncthreads();
+  if (p < R) {
+    uint32_t carry = seg[pl][sg];
+    for (uint32_t t = t0; t < t1; ++t) {
+      const uint32_t v = c[(uint64_t)t * R];
+      c[(uint64_t)t * R] = carry;
+      carry += v;
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -687,6 +716,15 @@ __device__ __forceinline__ int partition_words(const PartDev& pd, const uint32_t
       const int32_t r = (int32_t)w[0] % R;
       return r + (r < 0 ? R : 0);
     }
+    case kPartRadix:  // internal (sux_sort_records): digit of the big-endian 128-bit pair
+      if constexpr (KW == 4) {
+        const uint64_t hi = ((uint64_t)__builtin_bswap32(w[0]) << 32) | __builtin_bswap32(w[1]);
+        const uint64_t lo = ((uint64_t)__builtin_bswap32(w[2]) << 32) | __builtin_bswap32(w[3]);
+        const int sh = pd.seed;
+        const uint64_t v = sh >= 64 ? (hi >> (sh - 64)) : ((lo >> sh) | (sh ? (hi << (64 - sh)) : 0));
+        return (int)(v & (uint64_t)(R - 1));
+      }
+      return 0;
   }
   return 0;
 }
@@ -1863,8 +1901,8 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   timer_begin(timer, kScan, s);
   const uint32_t rows = g.num_maps * (uint32_t)R;
   if (s16)
-    hipLaunchKernelGGL(k_tile_scan_tm, dim3((rows + 255) / 256), dim3(256), 0, s, counts, totals,
-                       g.num_maps, (uint32_t)R, g.tiles_per_map);
+    hipLaunchKernelGGL(k_tile_scan_tm, dim3(g.num_maps * ((R + 15) / 16)), dim3(256), 0, s, counts,
+                       totals, g.num_maps, (uint32_t)R, g.tiles_per_map);
   else if (g.tiles_per_map <= 64)
     hipLaunchKernelGGL(k_tile_scan_rows, dim3((rows + 255) / 256), dim3(256), 0, s, counts, totals,
                        rows, g.tiles_per_map);

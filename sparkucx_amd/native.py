@@ -20,6 +20,7 @@ SUX_OK, SUX_EINVAL, SUX_ENOMEM, SUX_EHIP, SUX_ECOMM, SUX_ENOENT, SUX_ESTATE, SUX
 PART_RANGE_BYTES, PART_MURMUR3_LONG, PART_MURMUR3_INT, PART_MURMUR3_BYTES = 1, 2, 3, 4
 PART_HASH_LONG, PART_HASH_INT = 5, 6
 GEN_TERASORT, GEN_SMALL, GEN_ZIPF = 1, 2, 3
+SORT_BYTES, SORT_LONG, SORT_INT = 1, 2, 3
 KERNELS = ("hist", "scan", "scatter", "copy")
 
 
@@ -92,6 +93,8 @@ _SIGS = {
     "sux_pull_group": (C.c_int, [P, I32, I32, P, P, I32, I32, P, U64, P, P]),
     "sux_stream_create": (C.c_int, [P, I32, I32, C.POINTER(P)]),
     "sux_stream_destroy": (C.c_int, [P, P]),
+    "sux_sort_workspace_size": (C.c_int, [U64, U32, C.POINTER(U64)]),
+    "sux_sort_records": (C.c_int, [P, I32, P, U64, U32, I32, I32, P, P, U64, P]),
 }
 
 _lib = None

@@ -258,6 +258,29 @@ class Node:
         return list(addrs)[:len(blocks)], list(sizes)[:len(blocks)]
 
     # ---- measurement -------------------------------------------------------------------------
+    def sort_records(self, records: torch.Tensor, record_size: int, key_kind: int,
+                     key_offset: int, key_len: int, num_records: int | None = None,
+                     out: torch.Tensor | None = None, workspace: torch.Tensor | None = None,
+                     stream=None) -> torch.Tensor:
+        """Stable GPU sort of fixed-size records by key (reduce side, UcxShuffleReader's
+        ExternalSorter step).  Returns `out` (records in ascending key order)."""
+        n = records.numel() // record_size if num_records is None else num_records
+        if out is None:
+            out = torch.empty(max(1, n * record_size), dtype=torch.uint8, device=self.dev)
+        if workspace is None:
+            workspace = torch.empty(max(1, self.sort_workspace_size(n, record_size)),
+                                    dtype=torch.uint8, device=self.dev)
+        N.check(self.lib.sux_sort_records(self.h, key_kind, _ptr(records), n, record_size,
+                                          key_offset, key_len, _ptr(out), _ptr(workspace),
+                                          workspace.numel(), _stream(stream)), "sux_sort_records")
+        return out
+
+    def sort_workspace_size(self, n: int, record_size: int) -> int:
+        b = C.c_uint64()
+        N.check(self.lib.sux_sort_workspace_size(n, record_size, C.byref(b)),
+                "sux_sort_workspace_size")
+        return b.value
+
     def cu_stream(self, num_cus: int, complement: bool = False) -> int:
         """hipStream_t (as int) running on `num_cus` CUs spread over the XCDs, or on the other CUs
         (complement).  Wrap with torch.cuda.ExternalStream; destroy with destroy_stream()."""
