@@ -174,6 +174,27 @@ int sux_pull_group(sux_node* node, int32_t world, int32_t rank, const uint64_t* 
 int sux_partition_ids(sux_node* node, const sux_partitioner* part, const void* d_records,
                       uint32_t record_size, uint64_t num_records, uint16_t* d_pids, void* stream);
 
+/* ---- variable-length records: Spark SQL's UnsafeRowSerializer framing ----------------------
+ * Replaces the same P1-P3 step as sux_partition_maps (the UnsafeShuffleWriter chosen at
+ * compat/spark_3_0/UcxShuffleManager.scala:37-46 and the index write at
+ * compat/spark_3_0/UcxShuffleBlockResolver.scala:35) for rows of differing size: Spark SQL's
+ * UnsafeRowSerializer frames each row as a 4-byte big-endian length + the UnsafeRow, so a row is
+ * 4 + 8k bytes.  Record i = d_data[d_offsets[i] - d_offsets[0], d_offsets[i+1] - d_offsets[0])
+ * (num_records + 1 device u64 offsets, every one a multiple of 4, rows < 64 KiB).  The key the
+ * partitioner reads lies at key_offset inside each row (e.g. 12: the frame length, the 8-byte null
+ * bitset, then the first fixed-width field); rows must hold it.  d_pids_in (optional, device u16
+ * per record, each < R) replaces the partitioner with ids the caller projected itself (Spark SQL
+ * computes them from the partitioning expressions); then d_pids is not written.
+ * Map m's data file occupies the same byte range of d_out as its rows occupy in d_data; its index
+ * (R + 1 int64, native and optionally big-endian) holds byte offsets.  R <= 16384. */
+int sux_partition_varlen_workspace_size(const sux_partitioner* part, uint64_t records_per_map,
+                                        uint64_t num_records, uint64_t* bytes);
+int sux_partition_varlen(sux_node* node, const sux_partitioner* part, const void* d_data,
+                         const uint64_t* d_offsets, uint64_t records_per_map,
+                         uint64_t num_records, const uint16_t* d_pids_in, void* d_out,
+                         int64_t* d_index, uint8_t* d_index_be, uint16_t* d_pids,
+                         void* d_workspace, uint64_t workspace_bytes, void* stream);
+
 /* ---- shuffle lifecycle: CommonUcxShuffleManager.registerShuffleCommon :39-56 ---------------- */
 typedef struct sux_handle_desc {
   int32_t shuffle_id;

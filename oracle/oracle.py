@@ -260,3 +260,74 @@ def sort_records(recs: np.ndarray, rec_size: int, kind: int, key_offset: int,
     else:
         raise ValueError(f"unknown sort key kind {kind}")
     return rows[order].reshape(-1)
+
+
+# ---- variable-length rows -----------------------------------------------
+def gen_unsafe_rows(seed: int, n: int, max_payload_words: int = 12,
+                    key_mod: int | None = None) -> tuple[np.ndarray, np.ndarray]:
+    """n rows in Spark SQL's UnsafeRowSerializer framing [ext: spark-sql UnsafeRowSerializer
+    writeValue = writeInt(row.getSizeInBytes) + row.writeToStream]: a 4-byte big-endian length L,
+    then an UnsafeRow of L bytes = 8-byte null bitset (0) | int64 key (little-endian, the row's
+    first fixed-width field) | k payload words, k uniform in [0, max_payload_words].  The key sits
+    at byte 12 of each framed row.  Returns (data u8, offsets i64[n + 1])."""
+    rng = np.random.default_rng(seed)
+    k = rng.integers(0, max_payload_words + 1, n)
+    L = 8 * (2 + k)
+    offs = np.zeros(n + 1, np.int64)
+    np.cumsum(4 + L, out=offs[1:])
+    data = rng.integers(0, 256, int(offs[-1]), dtype=np.uint8)
+    keys = rng.integers(-(1 << 63), (1 << 63) - 1, n, dtype=np.int64, endpoint=True)
+    if key_mod:
+        keys %= key_mod
+    starts = offs[:-1]
+    data[starts[:, None] + np.arange(4)] = L.astype(">u4").view(np.uint8).reshape(n, 4)
+    data[starts[:, None] + 4 + np.arange(8)] = 0
+    data[starts[:, None] + 12 + np.arange(8)] = keys.astype("<i8").view(np.uint8).reshape(n, 8)
+    return data, offs
+
+
+def varlen_ids(part: Partitioner, data: np.ndarray, offs: np.ndarray) -> np.ndarray:
+    """P1 on each row's key: the key bytes [key_offset, +key_len) of every row gathered into a
+    fixed-width array, then the same partitioner (oracle.c o_partition_ids) at key_offset 0."""
+    n = offs.size - 1
+    if n == 0:
+        return np.empty(0, np.uint16)
+    kl = part.key_len
+    keys = np.ascontiguousarray(data[(offs[:-1] - offs[0] + part.key_offset)[:, None]
+                                     + np.arange(kl)])
+    p0 = Partitioner(part.kind, part.R, 0, kl, part.seed, part.ascending, part.bounds)
+    return p0.ids(keys.reshape(-1), kl)
+
+
+def varlen_write_maps(part: Partitioner | None, data: np.ndarray, offs: np.ndarray, rpm: int,
+                      R: int | None = None, pids: np.ndarray | None = None):
+    """P2+P3 for variable-length rows: per map (runs of rpm rows), a stable regroup of the rows by
+    pid — the serialized rows of partition 0, then 1, ..., R-1, each in input order (what Spark's
+    UnsafeShuffleWriter emits for UnsafeRowSerializer output with compression off) — written at
+    the map's own byte range, and its (R+1) cumulative BYTE offsets (the index file,
+    IndexShuffleBlockResolver.writeIndexFileAndCommit via compat/spark_3_0/
+    UcxShuffleBlockResolver.scala:35).  Returns (out, index i64[maps*(R+1)], index_be, pids)."""
+    n = offs.size - 1
+    R = part.R if R is None else R
+    if pids is None:
+        pids = varlen_ids(part, data, offs)
+    pids = pids.astype(np.int64)
+    base = offs - offs[0]
+    lens = np.diff(offs)
+    out = np.empty(int(base[-1]), np.uint8)
+    idx, be = [], []
+    for m0 in range(0, n, rpm):
+        m1 = min(n, m0 + rpm)
+        order = m0 + np.argsort(pids[m0:m1], kind="stable")
+        ln = lens[order]
+        src = np.repeat(base[order], ln) + (np.arange(int(ln.sum())) -
+                                            np.repeat(np.cumsum(ln) - ln, ln))
+        out[base[m0]:base[m1]] = data[src]
+        sizes = np.bincount(pids[m0:m1], weights=lens[m0:m1], minlength=R).astype(np.int64)
+        ix = np.zeros(R + 1, np.int64)
+        np.cumsum(sizes, out=ix[1:])
+        idx.append(ix)
+        be.append(ix.astype(">i8").tobytes())
+    if not idx:
+        return out, np.zeros(0, np.int64), b"", pids.astype(np.uint16)
+    return out, np.concatenate(idx), b"".join(be), pids.astype(np.uint16)

@@ -570,6 +570,73 @@ int sux_partition_ids(sux_node* node, const sux_partitioner* part, const void* d
   });
 }
 
+// ---- variable-length records (Spark SQL UnsafeRowSerializer framing) ---------------------------
+namespace {
+struct VGroup {
+  sux::VarGroup g;
+  sux::VarWorkspace ws;
+};
+VGroup make_vgroup(const sux_partitioner* part, const void* data, const uint64_t* offs,
+                   uint64_t rpm, uint64_t n) {
+  require(rpm > 0, SUX_EINVAL, "records_per_map must be > 0");
+  const uint64_t maps = (n + rpm - 1) / rpm;
+  require(maps <= 0xFFFFFFFFull, SUX_EINVAL, "too many maps in one group");
+  require(n < (1ull << 32), SUX_ERANGE, "a launch group holds < 2^32 records");
+  const int R = part->desc.num_partitions;
+  require(R <= sux::kMaxVarPartitions, SUX_EINVAL,
+          "variable-length records support num_partitions <= " +
+              std::to_string(sux::kMaxVarPartitions));
+  require(((uintptr_t)data & 3) == 0 && ((uintptr_t)offs & 7) == 0, SUX_EINVAL,
+          "data must be 4-byte and offsets 8-byte aligned");
+  VGroup G;
+  const uint32_t tile = sux::choose_varlen_tile((uint32_t)R);
+  G.g.data = static_cast<const uint8_t*>(data);
+  G.g.offs = offs;
+  G.g.records_per_map = rpm;
+  G.g.num_records = n;
+  G.g.num_maps = (uint32_t)maps;
+  G.g.tile_recs = tile;
+  G.g.tiles_per_map = (uint32_t)((rpm + tile - 1) / tile);
+  G.g.pad = 0;
+  G.ws = sux::varlen_workspace_layout((uint32_t)R, rpm, n, tile);
+  return G;
+}
+}  // namespace
+
+int sux_partition_varlen_workspace_size(const sux_partitioner* part, uint64_t rpm, uint64_t n,
+                                        uint64_t* bytes) {
+  return guard([&] {
+    require(part && bytes, SUX_EINVAL, "NULL argument");
+    *bytes = make_vgroup(part, nullptr, nullptr, rpm, n).ws.total;
+  });
+}
+
+int sux_partition_varlen(sux_node* node, const sux_partitioner* part, const void* d_data,
+                         const uint64_t* d_offsets, uint64_t rpm, uint64_t n,
+                         const uint16_t* d_pids_in, void* d_out, int64_t* d_index,
+                         uint8_t* d_index_be, uint16_t* d_pids, void* d_ws, uint64_t ws_bytes,
+                         void* stream) {
+  return guard([&] {
+    require(node && part, SUX_EINVAL, "NULL node/partitioner");
+    require(d_offsets || n == 0, SUX_EINVAL, "offsets pointer is NULL");
+    node->bind();
+    VGroup G = make_vgroup(part, d_data, d_offsets, rpm, n);
+    require(d_ws || G.ws.total == 0, SUX_EINVAL, "workspace is NULL");
+    require(ws_bytes >= G.ws.total, SUX_EINVAL,
+            "workspace too small: need " + std::to_string(G.ws.total) + " bytes");
+    require(d_out && d_index, SUX_EINVAL, "output or index pointer is NULL");
+    require(((uintptr_t)d_out & 3) == 0 && ((uintptr_t)d_index & 7) == 0 &&
+                ((uintptr_t)d_index_be & 7) == 0 && ((uintptr_t)d_ws & 255) == 0,
+            SUX_EINVAL, "output (4 B), index (8 B) and workspace (256 B) must be aligned");
+    if (n == 0) return;
+    hip_check(sux::launch_varlen_group(part->pd, G.g, static_cast<uint8_t*>(d_out), d_index,
+                                       d_index_be, d_pids_in, d_pids,
+                                       static_cast<uint8_t*>(d_ws), G.ws, &node->timer,
+                                       node->stream(stream)),
+              "variable-length partition launch");
+  });
+}
+
 // ---- exchange plan (host arithmetic) -----------------------------------------------------------
 int sux_plan_group(int32_t W, int32_t rank, int32_t M, int32_t R, const int64_t* gi,
                    uint64_t* sendcounts, uint64_t* sdispls, uint64_t* recvcounts,

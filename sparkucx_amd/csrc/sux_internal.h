@@ -9,7 +9,8 @@
 
 namespace sux {
 
-constexpr int kMaxPartitions = 32768;  // LDS histogram: 128 KiB of u32 counters at the limit
+constexpr int kMaxPartitions = 32768;
+constexpr int kMaxVarPartitions = 16384;  // k_vscatter: one u64 LDS cursor per partition  // LDS histogram: 128 KiB of u32 counters at the limit
 constexpr int kMaxRecordSize = 4096;
 constexpr int kLutBits = 10;  // range-partitioner prefix lookup: 1024 u32 entries
 
@@ -39,6 +40,24 @@ struct MapGroup {
   uint32_t rec_size;
   uint32_t tile_recs;      // records per tile (one wave's work in hist/scatter)
   uint32_t tiles_per_map;  // ceil(records_per_map / tile_recs)
+};
+
+// Per-launch geometry of a group of variable-length record maps (sux_varlen.hip): record i is
+// data[offs[i] - offs[0], offs[i+1] - offs[0]).
+struct VarGroup {
+  const uint8_t* data;
+  const uint64_t* offs;      // num_records + 1 offsets (device)
+  uint64_t records_per_map;
+  uint64_t num_records;
+  uint32_t num_maps;
+  uint32_t tile_recs;
+  uint32_t tiles_per_map;
+  uint32_t pad;
+};
+
+// Workspace of the variable-length path: u64 tile counts [M][R][T] | totals [M][R] | bases | pids
+struct VarWorkspace {
+  uint64_t counts_off, totals_off, base_off, pids_off, total;
 };
 
 // Workspace carve-up (sizes in bytes), computed by workspace_layout().
@@ -71,6 +90,17 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
                                   uint8_t* d_out, int64_t* d_index, uint8_t* d_index_be,
                                   uint16_t* d_pids, uint8_t* d_ws, const Workspace& ws,
                                   uint64_t* d_peer_bytes, Timer* timer, hipStream_t s);
+hipError_t launch_varlen_group(const PartDev& pd, const VarGroup& g, uint8_t* d_out,
+                               int64_t* d_index, uint8_t* d_index_be, const uint16_t* d_pids_in,
+                               uint16_t* d_pids, uint8_t* d_ws, const VarWorkspace& ws,
+                               Timer* timer, hipStream_t s);
+VarWorkspace varlen_workspace_layout(uint32_t R, uint64_t records_per_map, uint64_t num_records,
+                                     uint32_t tile_recs);
+uint32_t choose_varlen_tile(uint32_t R);
+// K2b of the variable-length path (sux_partition.hip, k_map_scan): per-(map, partition) byte
+// totals -> index tables in bytes + byte bases of every (map, partition) run
+hipError_t launch_varlen_map_scan(const VarGroup& g, int R, const uint64_t* totals, uint64_t* base,
+                                  int64_t* d_index, uint8_t* d_index_be, hipStream_t s);
 hipError_t launch_partition_ids(const PartDev& pd, const uint8_t* recs, uint32_t rec_size,
                                 uint64_t n, uint16_t* d_pids, hipStream_t s);
 

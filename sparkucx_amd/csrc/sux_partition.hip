@@ -32,119 +32,8 @@ typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 
 constexpr int kWave = 64;
 
-// ------------------------------------------------------------------------------------------
-// P1: partition functions (Spark semantics, oracle/oracle.c o_get_partition)
-// ------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
-__device__ __forceinline__ uint32_t mix_k1(uint32_t k1) {
-  k1 *= 0xcc9e2d51u;
-  k1 = rotl32(k1, 15);
-  return k1 * 0x1b873593u;
-}
-__device__ __forceinline__ uint32_t mix_h1(uint32_t h1, uint32_t k1) {
-  h1 ^= k1;
-  h1 = rotl32(h1, 13);
-  return h1 * 5u + 0xe6546b64u;
-}
-__device__ __forceinline__ uint32_t fmix32(uint32_t h1, uint32_t len) {
-  h1 ^= len;
-  h1 ^= h1 >> 16;
-  h1 *= 0x85ebca6bu;
-  h1 ^= h1 >> 13;
-  h1 *= 0xc2b2ae35u;
-  return h1 ^ (h1 >> 16);
-}
-__device__ __forceinline__ int32_t pmod(int32_t a, int32_t n) {
-  int32_t r = a % n;
-  return r < 0 ? (r + n) % n : r;
-}
-
-__device__ __forceinline__ uint32_t ld_u32(const uint8_t* p, int off) {
-  if ((off & 3) == 0) return *reinterpret_cast<const uint32_t*>(p + off);
-  return (uint32_t)p[off] | ((uint32_t)p[off + 1] << 8) | ((uint32_t)p[off + 2] << 16) |
-         ((uint32_t)p[off + 3] << 24);
-}
-
-// Big-endian (hi, lo) words of a key of `len` (1..16) bytes, bytes past len zeroed.
-__device__ __forceinline__ void load_key_be(const uint8_t* rec, int off, int len, uint64_t& hi,
-                                            uint64_t& lo) {
-  uint32_t w0 = ld_u32(rec, off);
-  uint32_t w1 = len > 4 ? ld_u32(rec, off + 4) : 0u;
-  uint32_t w2 = len > 8 ? ld_u32(rec, off + 8) : 0u;
-  uint32_t w3 = len > 12 ? ld_u32(rec, off + 12) : 0u;
-  hi = ((uint64_t)__builtin_bswap32(w0) << 32) | __builtin_bswap32(w1);
-  lo = ((uint64_t)__builtin_bswap32(w2) << 32) | __builtin_bswap32(w3);
-  if (len < 8) {
-    hi &= ~0ull << (8 * (8 - len));
-    lo = 0;
-  } else if (len < 16) {
-    lo = (len == 8) ? 0 : (lo & (~0ull << (8 * (16 - len))));
-  }
-}
-
-__device__ __forceinline__ int range_search(const PartDev& pd, uint64_t hi, uint64_t lo) {
-  int a = 0, b = pd.R - 1;  // answer = #{bounds < key} in [a, b]
-  if (pd.lut_bits) {
-    uint32_t e = pd.lut[hi >> (64 - pd.lut_bits)];
-    a = e & 0xFFFFu;
-    b = e >> 16;
-  }
-  while (a < b) {
-    int mid = (a + b) >> 1;
-    uint64_t bh = pd.bounds[2 * mid], bl = pd.bounds[2 * mid + 1];
-    bool less = (bh < hi) || (bh == hi && bl < lo);  // bound < key
-    if (less) a = mid + 1; else b = mid;
-  }
-  return a;
-}
-
-__device__ __forceinline__ int get_partition(const PartDev& pd, const uint8_t* rec) {
-  switch (pd.kind) {
-    case 1: {  // SUX_PART_RANGE_BYTES
-      uint64_t hi, lo;
-      load_key_be(rec, pd.key_offset, pd.key_len, hi, lo);
-      int p = range_search(pd, hi, lo);
-      return pd.ascending ? p : (pd.R - 1) - p;
-    }
-    case 2: {  // SUX_PART_MURMUR3_LONG
-      uint32_t lo32 = ld_u32(rec, pd.key_offset), hi32 = ld_u32(rec, pd.key_offset + 4);
-      uint32_t h1 = mix_h1((uint32_t)pd.seed, mix_k1(lo32));
-      h1 = mix_h1(h1, mix_k1(hi32));
-      return pmod((int32_t)fmix32(h1, 8), pd.R);
-    }
-    case 3: {  // SUX_PART_MURMUR3_INT
-      uint32_t v = ld_u32(rec, pd.key_offset);
-      return pmod((int32_t)fmix32(mix_h1((uint32_t)pd.seed, mix_k1(v)), 4), pd.R);
-    }
-    case 4: {  // SUX_PART_MURMUR3_BYTES (legacy hashUnsafeBytes)
-      const int off = pd.key_offset, len = pd.key_len, aligned = len - len % 4;
-      uint32_t h1 = (uint32_t)pd.seed;
-      for (int i = 0; i < aligned; i += 4) h1 = mix_h1(h1, mix_k1(ld_u32(rec, off + i)));
-      for (int i = aligned; i < len; ++i)
-        h1 = mix_h1(h1, mix_k1((uint32_t)(int32_t)(int8_t)rec[off + i]));
-      return pmod((int32_t)fmix32(h1, (uint32_t)len), pd.R);
-    }
-    case 5: {  // SUX_PART_HASH_LONG: nonNegativeMod(Long.hashCode)
-      uint32_t h = ld_u32(rec, pd.key_offset) ^ ld_u32(rec, pd.key_offset + 4);
-      int32_t r = (int32_t)h % pd.R;
-      return r + (r < 0 ? pd.R : 0);
-    }
-    case 6: {  // SUX_PART_HASH_INT
-      int32_t r = (int32_t)ld_u32(rec, pd.key_offset) % pd.R;
-      return r + (r < 0 ? pd.R : 0);
-    }
-    case kPartRadix: {  // internal: digit of the big-endian 128-bit (key, index) pair
-      const uint64_t hi = ((uint64_t)__builtin_bswap32(ld_u32(rec, 0)) << 32) |
-                          __builtin_bswap32(ld_u32(rec, 4));
-      const uint64_t lo = ((uint64_t)__builtin_bswap32(ld_u32(rec, 8)) << 32) |
-                          __builtin_bswap32(ld_u32(rec, 12));
-      const int sh = pd.seed;
-      const uint64_t v = sh >= 64 ? (hi >> (sh - 64)) : ((lo >> sh) | (sh ? (hi << (64 - sh)) : 0));
-      return (int)(v & (uint64_t)(pd.R - 1));
-    }
-  }
-  return 0;
-}
+// P1: partition functions — sux_p1.h
+#include "sux_p1.h"
 
 // ------------------------------------------------------------------------------------------
 // geometry helpers
@@ -365,7 +254,8 @@ __global__ __launch_bounds__(kScanThreads) void k_map_scan(const uint64_t* __res
                                                            uint64_t* __restrict__ peer_bytes,
                                                            int R, int G, uint32_t rec_size,
                                                            uint64_t records_per_map,
-                                                           uint64_t num_records) {
+                                                           uint64_t num_records,
+                                                           const uint64_t* __restrict__ map_offs) {
   __shared__ uint64_t sh[2 * kWave + 1];
   __shared__ unsigned long long hs[1024];
   const uint32_t m = blockIdx.x;
@@ -384,7 +274,9 @@ __global__ __launch_bounds__(kScanThreads) void k_map_scan(const uint64_t* __res
       const int64_t off = (int64_t)(ex * rec_size);
       im[p] = off;
       if (ibe) ibe[p] = bswap64((uint64_t)off);
-      if (G == 1) {
+      if (map_offs) {  // variable-length records: bases and offsets in bytes
+        base[(uint64_t)m * R + p] = (map_offs[(uint64_t)m * records_per_map] - map_offs[0]) + ex;
+      } else if (G == 1) {
         base[(uint64_t)m * R + p] = (uint64_t)m * records_per_map + ex;
       } else {
         pre[(uint64_t)m * R + p] = ex;
@@ -1464,11 +1356,18 @@ __global__ __launch_bounds__(NW * 64) void k_scatter7(MapGroup g, int R, int pid
     }
     __syncthreads();
     SUX_STAMP(ci, 4);
-    // 4. records -> image (dword granular, rotated per lane octet against bank conflicts)
+    // 4. records -> image.  A staged unit whose 16 bytes lie inside one record goes in as ONE
+    //    4-byte-aligned ds_write_b128 (the record's image offset is only 4-byte aligned); a unit
+    //    that straddles two records goes dword by dword, rotated per lane octet against bank
+    //    conflicts.
 #pragma unroll
     for (uint32_t k = 0; k < PER; ++k) {
       const uint32_t u = tid + k * NT;
-      if (u < units) {
+      const int32_t b0 = (int32_t)(16 * u) - (int32_t)head;
+      const uint32_t r0 = b0 >= 0 ? (uint32_t)b0 / S : 0u, off0 = (uint32_t)b0 - r0 * S;
+      if (u < units && b0 >= 0 && (uint32_t)b0 + 16 <= n * S && off0 + 16 <= S) {
+        *reinterpret_cast<u32x4a4*>(img32 + ((recoff[r0] + off0) >> 2)) = v[k];
+      } else if (u < units) {
 #pragma unroll
         for (uint32_t cc = 0; cc < 4; ++cc) {
           const uint32_t q = (cc + rot) & 3u;
@@ -1914,7 +1813,7 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   uint64_t* mh = base + 2 * L;
   hipLaunchKernelGGL(k_map_scan, dim3(g.num_maps), dim3(kScanThreads), 0, s, totals, base, pre, mh,
                      d_index, d_index_be, lay.world == 1 ? d_peer_bytes : nullptr, R, lay.world,
-                     g.rec_size, g.records_per_map, g.num_records);
+                     g.rec_size, g.records_per_map, g.num_records, nullptr);
   if (lay.world > 1) {
     hipLaunchKernelGGL(k_peer_off, dim3(1), dim3(kScanThreads), 0, s, mh, d_peer_bytes,
                        g.num_maps, lay.world, g.rec_size);
@@ -2034,6 +1933,15 @@ hipError_t launch_partition_ids(const PartDev& pd, const uint8_t* recs, uint32_t
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(k_pids, dim3((uint32_t)blocks), dim3(256), 0, s, pd, recs, rec_size, n,
                      d_pids);
+  return hipGetLastError();
+}
+
+hipError_t launch_varlen_map_scan(const VarGroup& g, int R, const uint64_t* totals, uint64_t* base,
+                                  int64_t* d_index, uint8_t* d_index_be, hipStream_t s) {
+  const uint64_t L = (uint64_t)g.num_maps * R;
+  hipLaunchKernelGGL(k_map_scan, dim3(g.num_maps), dim3(kScanThreads), 0, s, totals, base,
+                     base + L, base + 2 * L, d_index, d_index_be, nullptr, R, 1, 1u,
+                     g.records_per_map, g.num_records, g.offs);
   return hipGetLastError();
 }
 

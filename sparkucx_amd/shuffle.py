@@ -160,6 +160,45 @@ class Node:
                                            _ptr(pids), _stream(stream)), "sux_partition_ids")
         return pids[:n]
 
+    def varlen_workspace_size(self, part: Partitioner, records_per_map: int,
+                              num_records: int) -> int:
+        b = C.c_uint64()
+        N.check(self.lib.sux_partition_varlen_workspace_size(part.h, records_per_map, num_records,
+                                                             C.byref(b)),
+                "sux_partition_varlen_workspace_size")
+        return b.value
+
+    def partition_varlen(self, part: Partitioner, data: torch.Tensor, offsets: torch.Tensor,
+                         records_per_map: int, pids_in: torch.Tensor | None = None,
+                         out: torch.Tensor | None = None, index: torch.Tensor | None = None,
+                         index_be: torch.Tensor | None = None, pids: torch.Tensor | None = None,
+                         workspace: torch.Tensor | None = None, want_be: bool = True,
+                         stream=None):
+        """Variable-length rows (Spark SQL UnsafeRowSerializer framing): row i is
+        data[offsets[i] - offsets[0] : offsets[i+1] - offsets[0]] (offsets: int64, n + 1, device).
+        Returns (out, index, index_be); map m's data file is out[offsets[m*rpm] - offsets[0] :
+        offsets[min((m+1)*rpm, n)] - offsets[0]] and its index holds byte offsets."""
+        n = offsets.numel() - 1
+        maps = max(1, -(-n // records_per_map))
+        R = part.R
+        if out is None:
+            out = torch.empty(max(4, data.numel()), dtype=torch.uint8, device=self.dev)
+        if index is None:
+            index = torch.empty(maps * (R + 1), dtype=torch.int64, device=self.dev)
+        if index_be is None and want_be:
+            index_be = torch.empty(maps * (R + 1) * 8, dtype=torch.uint8, device=self.dev)
+        if workspace is None:
+            workspace = torch.empty(max(1, self.varlen_workspace_size(part, records_per_map,
+                                                                      max(n, 0))),
+                                    dtype=torch.uint8, device=self.dev)
+        N.check(self.lib.sux_partition_varlen(self.h, part.h, _ptr(data), _ptr(offsets),
+                                              records_per_map, max(n, 0), _ptr(pids_in),
+                                              _ptr(out), _ptr(index), _ptr(index_be), _ptr(pids),
+                                              _ptr(workspace), workspace.numel(),
+                                              _stream(stream)),
+                "sux_partition_varlen")
+        return out, index, index_be
+
     def exchange_group(self, send: torch.Tensor, index: torch.Tensor, num_maps: int, R: int,
                        gathered: torch.Tensor, recv: torch.Tensor, stream=None) -> np.ndarray:
         rb = (C.c_uint64 * self.world_size)()
