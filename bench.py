@@ -117,6 +117,58 @@ def reduce_sort(node, recs, ns: int, rs: int, dev) -> dict:
             "alg_bytes": 2 * ns * rs}
 
 
+def gen_unsafe_rows_dev(n: int, seed: int, dev, max_words: int = 12):
+    """Synthetic Spark SQL UnsafeRowSerializer stream on the device (same framing as
+    oracle.gen_unsafe_rows, other random draws): 4-byte BE length L | 8-byte null bitset |
+    int64 key | k payload words, k uniform in [0, max_words]."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    k = torch.randint(0, max_words + 1, (n,), device=dev, generator=g)
+    L = 8 * (2 + k)
+    offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(4 + L, 0, out=offs[1:])
+    total = int(offs[-1].item())
+    data = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=g)
+    st = offs[:-1]
+    for b in range(4):
+        data[st + b] = ((L >> (8 * (3 - b))) & 255).to(torch.uint8)
+    for b in range(4, 12):
+        data[st + b] = 0
+    return data, offs
+
+
+def varlen_leg(node, rows: int, rpm: int, R: int, dev) -> dict:
+    """§8f item 3: the map side over variable-length UnsafeRow-framed rows (sux_partition_varlen,
+    Spark SQL hash of the int64 key at byte 12, R partitions).  GB/s of row bytes; the algorithmic
+    HBM bytes are 2 x row bytes (read + write each row) + 44 B per row (offsets read twice, the
+    key, the pid written and read back)."""
+    data, offs = gen_unsafe_rows_dev(rows, 77, dev)
+    part = node.partitioner(N.PART_MURMUR3_LONG, R, key_offset=12, key_len=8)
+    out = torch.empty_like(data)
+    maps = -(-rows // rpm)
+    index = torch.empty(maps * (R + 1), dtype=torch.int64, device=dev)
+    be = torch.empty(maps * (R + 1) * 8, dtype=torch.uint8, device=dev)
+    ws = torch.empty(node.varlen_workspace_size(part, rpm, rows), dtype=torch.uint8, device=dev)
+    run = lambda: node.partition_varlen(part, data, offs, rpm, out=out, index=index, index_be=be,
+                                        workspace=ws)
+    for _ in range(2):
+        run()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 5
+    e0.record()
+    for _ in range(reps):
+        run()
+    e1.record()
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    nb = data.numel()
+    alg = 2 * nb + 44 * rows
+    return {"rows": rows, "row_bytes": nb, "avg_row": round(nb / rows, 1), "R": R,
+            "rows_per_map": rpm, "ms": round(ms, 3), "GB/s": round(nb / (ms / 1e3) / 1e9, 1),
+            "alg_bytes": alg, "alg_GB/s": round(alg / (ms / 1e3) / 1e9, 1)}
+
+
 def load_traffic(kernel: str) -> float | None:
     """Per-launch HBM bytes of `kernel` from the committed PMC summary (profiles/pmc_r01.json,
     written by profiles/collect_pmc.py; FETCH_SIZE x2 + WRITE_SIZE per the microarch guide)."""
@@ -152,6 +204,9 @@ def main():
     ap.add_argument("--reduce-sort-records", type=int, default=-1,
                     help="N=1: also time the reduce-side sort (sux_sort_records) of one reduce "
                          "partition's worth of records (-1: records/R; 0: skip)")
+    ap.add_argument("--varlen-rows", type=int, default=-1,
+                    help="N=1: also time the map side over variable-length UnsafeRow-framed rows "
+                         "(sux_partition_varlen; -1: 32 Mi rows in 1 Mi-row maps; 0: skip)")
     ap.add_argument("--cpu-records", type=int, default=10_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-reps", type=int, default=3)
@@ -418,6 +473,9 @@ def main():
         ns = min(ns, n)
         if ns > 0 and args.workload == "terasort":
             result["reduce_sort"] = reduce_sort(node, out[:ns * rs], ns, rs, dev)
+    if world == 1 and args.varlen_rows != 0:
+        vr = args.varlen_rows if args.varlen_rows > 0 else 32 << 20
+        result["varlen"] = varlen_leg(node, vr, min(vr, 1 << 20), 200, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:

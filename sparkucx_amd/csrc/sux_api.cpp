@@ -589,7 +589,7 @@ VGroup make_vgroup(const sux_partitioner* part, const void* data, const uint64_t
   require(((uintptr_t)data & 3) == 0 && ((uintptr_t)offs & 7) == 0, SUX_EINVAL,
           "data must be 4-byte and offsets 8-byte aligned");
   VGroup G;
-  const uint32_t tile = sux::choose_varlen_tile((uint32_t)R);
+  const uint32_t tile = sux::choose_varlen_tile((uint32_t)R, n);
   G.g.data = static_cast<const uint8_t*>(data);
   G.g.offs = offs;
   G.g.records_per_map = rpm;

@@ -96,7 +96,7 @@ hipError_t launch_varlen_group(const PartDev& pd, const VarGroup& g, uint8_t* d_
                                Timer* timer, hipStream_t s);
 VarWorkspace varlen_workspace_layout(uint32_t R, uint64_t records_per_map, uint64_t num_records,
                                      uint32_t tile_recs);
-uint32_t choose_varlen_tile(uint32_t R);
+uint32_t choose_varlen_tile(uint32_t R, uint64_t rows);
 // K2b of the variable-length path (sux_partition.hip, k_map_scan): per-(map, partition) byte
 // totals -> index tables in bytes + byte bases of every (map, partition) run
 hipError_t launch_varlen_map_scan(const VarGroup& g, int R, const uint64_t* totals, uint64_t* base,

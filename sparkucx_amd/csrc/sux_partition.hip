@@ -57,14 +57,7 @@ __device__ __forceinline__ TileRange tile_range(const MapGroup& g, uint32_t gtil
   return tr;
 }
 
-// Workgroup b -> work index, so that the ~gridDim/8 workgroups the dispatcher deals to one XCD
-// (b, b+8, b+16, ...) get one contiguous range of tiles.  A bijection on [0, n); placement is a
-// speed hint only, never a correctness assumption.
-__device__ __forceinline__ uint32_t xcd_map(uint32_t b, uint32_t n) {
-  const uint32_t per = (n + 7) / 8, rem = n % 8, x = b % 8, k = b / 8;
-  if (rem == 0 || x < rem) return x * per + k;
-  return rem * per + (x - rem) * (per - 1) + k;
-}
+// xcd_map: sux_p1.h
 
 // ------------------------------------------------------------------------------------------
 // K1: partition ids + per-tile histogram
@@ -556,97 +549,7 @@ __global__ __launch_bounds__(256) void k_scatter2(MapGroup g, int R, int pid_bit
 // XCD-contiguously (T1) so neighbouring tiles share an L2.
 // ------------------------------------------------------------------------------------------
 
-template <bool TAB>
-__device__ __forceinline__ int range_search_t(int R, const uint64_t* bounds, const uint32_t* lut,
-                                              uint64_t hi, uint64_t lo) {
-  const uint32_t e = lut[hi >> (64 - kLutBits)];
-  int a = e & 0xFFFFu, b = e >> 16;
-  while (a < b) {
-    const int mid = (a + b) >> 1;
-    const uint64_t bh = bounds[2 * mid], bl = bounds[2 * mid + 1];
-    if ((bh < hi) || (bh == hi && bl < lo)) a = mid + 1; else b = mid;
-  }
-  return a;
-}
-
-// P1 from preloaded little-endian key dwords (key at a 4-byte aligned record offset).
-template <int KW, bool TAB>
-__device__ __forceinline__ int partition_words(const PartDev& pd, const uint32_t (&w)[KW],
-                                               const uint64_t* bounds, const uint32_t* lut) {
-  const int R = pd.R;
-  switch (pd.kind) {
-    case 1: {
-      if (R == 1) return 0;
-      uint64_t hi = (uint64_t)__builtin_bswap32(w[0]) << 32, lo = 0;
-      if constexpr (KW > 1) hi |= __builtin_bswap32(w[1]);
-      if constexpr (KW > 2) lo = (uint64_t)__builtin_bswap32(w[2]) << 32;
-      if constexpr (KW > 3) lo |= __builtin_bswap32(w[3]);
-      const int len = pd.key_len;
-      if (len < 8) {
-        hi &= ~0ull << (8 * (8 - len));
-        lo = 0;
-      } else if (len < 16) {
-        lo = (len == 8) ? 0 : (lo & (~0ull << (8 * (16 - len))));
-      }
-      const int p = range_search_t<TAB>(R, bounds, lut, hi, lo);
-      return pd.ascending ? p : (R - 1) - p;
-    }
-    case 2: {
-      uint32_t h1 = mix_h1((uint32_t)pd.seed, mix_k1(w[0]));
-      if constexpr (KW > 1) h1 = mix_h1(h1, mix_k1(w[1]));
-      return pmod((int32_t)fmix32(h1, 8), R);
-    }
-    case 3:
-      return pmod((int32_t)fmix32(mix_h1((uint32_t)pd.seed, mix_k1(w[0])), 4), R);
-    case 5: {
-      uint32_t h = w[0];
-      if constexpr (KW > 1) h ^= w[1];
-      const int32_t r = (int32_t)h % R;
-      return r + (r < 0 ? R : 0);
-    }
-    case 6: {
-      const int32_t r = (int32_t)w[0] % R;
-      return r + (r < 0 ? R : 0);
-    }
-    case kPartRadix:  // internal (sux_sort_records): digit of the big-endian 128-bit pair
-      if constexpr (KW == 4) {
-        const uint64_t hi = ((uint64_t)__builtin_bswap32(w[0]) << 32) | __builtin_bswap32(w[1]);
-        const uint64_t lo = ((uint64_t)__builtin_bswap32(w[2]) << 32) | __builtin_bswap32(w[3]);
-        const int sh = pd.seed;
-        const uint64_t v = sh >= 64 ? (hi >> (sh - 64)) : ((lo >> sh) | (sh ? (hi << (64 - sh)) : 0));
-        return (int)(v & (uint64_t)(R - 1));
-      }
-      return 0;
-  }
-  return 0;
-}
-
-template <int KW>
-struct KeyVec;
-template <>
-struct KeyVec<1> {
-  typedef uint32_t T;
-  static __device__ __forceinline__ void get(T v, uint32_t (&w)[1]) { w[0] = v; }
-};
-template <>
-struct KeyVec<2> {
-  typedef uint32_t T __attribute__((ext_vector_type(2), aligned(4)));
-  static __device__ __forceinline__ void get(T v, uint32_t (&w)[2]) { w[0] = v.x; w[1] = v.y; }
-};
-template <>
-struct KeyVec<3> {
-  typedef uint32_t T __attribute__((ext_vector_type(3), aligned(4)));
-  static __device__ __forceinline__ void get(T v, uint32_t (&w)[3]) {
-    w[0] = v.x; w[1] = v.y; w[2] = v.z;
-  }
-};
-template <>
-struct KeyVec<4> {
-  typedef uint32_t T __attribute__((ext_vector_type(4), aligned(4)));
-  static __device__ __forceinline__ void get(T v, uint32_t (&w)[4]) {
-    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-  }
-};
+// range_search_t, partition_words, KeyVec: sux_p1.h
 
 template <int KW, int RPL, bool TAB>
 __global__ __launch_bounds__(256) void k_hist3(PartDev pd, MapGroup g, uint16_t* __restrict__ pids,
