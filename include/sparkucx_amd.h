@@ -195,6 +195,29 @@ int sux_partition_varlen(sux_node* node, const sux_partitioner* part, const void
                          int64_t* d_index, uint8_t* d_index_be, uint16_t* d_pids,
                          void* d_workspace, uint64_t workspace_bytes, void* stream);
 
+/* ---- compressed map outputs: spark.shuffle.compress=true, lz4 codec ------------------------
+ * Replaces the per-partition compression stream Spark's writers open around each partition
+ * segment ([ext] SerializerManager.wrapStream -> LZ4CompressionCodec.compressedOutputStream =
+ * lz4-java LZ4BlockOutputStream(out, spark.io.compression.lz4.blockSize), inside the writer
+ * chosen at compat/spark_3_0/UcxShuffleManager.scala:36-50).  Input: num_maps consecutive map
+ * outputs in d_data (data_bytes in all) with their native index tables d_index
+ * (num_maps * (R + 1) int64, as sux_partition_maps / sux_partition_varlen write them).  Output:
+ * every non-empty (map, partition) run as its own LZ4Block stream (21-byte chunk headers with
+ * XXH32 checksums, raw chunks where LZ4 does not shrink them, an end mark), maps consecutive in
+ * d_out, their index tables (native + optional big-endian) and the total in *d_out_bytes
+ * (device u64).  d_out must hold sux_compress_bound bytes.  block_size: multiple of 4 in
+ * [64, 65536] (Spark's default 32768). */
+int sux_compress_bound(uint64_t data_bytes, int32_t num_maps, int32_t num_partitions,
+                       int32_t block_size, uint64_t* bytes);
+int sux_compress_workspace_size(uint64_t data_bytes, int32_t num_maps, int32_t num_partitions,
+                                int32_t block_size, uint64_t* bytes);
+int sux_compress_map_outputs(sux_node* node, const void* d_data, uint64_t data_bytes,
+                             const int64_t* d_index, int32_t num_maps, int32_t num_partitions,
+                             int32_t block_size, void* d_out, uint64_t out_capacity,
+                             int64_t* d_out_index, uint8_t* d_out_index_be,
+                             uint64_t* d_out_bytes, void* d_workspace, uint64_t workspace_bytes,
+                             void* stream);
+
 /* ---- shuffle lifecycle: CommonUcxShuffleManager.registerShuffleCommon :39-56 ---------------- */
 typedef struct sux_handle_desc {
   int32_t shuffle_id;

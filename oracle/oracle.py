@@ -66,6 +66,12 @@ def lib() -> C.CDLL:
             "o_cpu_shuffle": (C.c_int, [C.POINTER(Part), P, U64, U32, I32, I32, C.c_char_p,
                                         C.POINTER(CpuResult)]),
             "o_checksum": (U64, [P, U64]),
+            "o_xxh32": (U32, [P, U64, U32]),
+            "o_lz4_compress_block": (I32, [P, I32, I32, P]),
+            "o_lz4_decompress_block": (I32, [P, I32, P, I32]),
+            "o_lz4_stream": (U64, [P, U64, U32, I32, P]),
+            "o_lz4_map_outputs": (U64, [P, P, I32, I32, U32, I32, P, P]),
+            "o_lz4_unframe": (C.c_int64, [P, U64, P, U64]),
         }
         for k, (r, a) in sig.items():
             f = getattr(L, k)
@@ -331,3 +337,53 @@ def varlen_write_maps(part: Partitioner | None, data: np.ndarray, offs: np.ndarr
     if not idx:
         return out, np.zeros(0, np.int64), b"", pids.astype(np.uint16)
     return out, np.concatenate(idx), b"".join(be), pids.astype(np.uint16)
+
+
+# ---- compressed map outputs (oracle/lz4.c) -------------------------------
+LZ4_HASH_BITS = 11  # the GPU compressor's table (sux_lz4.hip)
+
+
+def xxh32(b: np.ndarray, seed: int = 0x9747B28C) -> int:
+    b = np.ascontiguousarray(b, np.uint8)
+    return int(lib().o_xxh32(_p(b), b.size, seed))
+
+
+def lz4_compress_block(b: np.ndarray, hash_bits: int = LZ4_HASH_BITS) -> bytes | None:
+    """The GPU parse restated; None = stored raw."""
+    b = np.ascontiguousarray(b, np.uint8)
+    out = np.empty(max(16, b.size), np.uint8)
+    n = lib().o_lz4_compress_block(_p(b), b.size, hash_bits, _p(out))
+    return None if n == 0 else out[:n].tobytes()
+
+
+def lz4_decompress_block(src: bytes, size: int) -> bytes:
+    s = np.frombuffer(src, np.uint8).copy() if src else np.zeros(1, np.uint8)
+    out = np.empty(max(1, size), np.uint8)
+    n = lib().o_lz4_decompress_block(_p(s), len(src), _p(out), size)
+    if n != size:
+        raise ValueError(f"malformed LZ4 block ({n})")
+    return out[:size].tobytes()
+
+
+def lz4_map_outputs(data: np.ndarray, index: np.ndarray, maps: int, R: int, block_size: int,
+                    hash_bits: int = LZ4_HASH_BITS):
+    """Compressed map outputs: (out bytes, index i64[maps*(R+1)], index_be bytes)."""
+    data = np.ascontiguousarray(data, np.uint8)
+    index = np.ascontiguousarray(index, np.int64)
+    runs = maps * R
+    cap = data.size + (data.size // block_size + runs + 1) * 21 + runs * 21 + 64
+    out = np.empty(cap, np.uint8)
+    oix = np.empty(maps * (R + 1), np.int64)
+    n = lib().o_lz4_map_outputs(_p(data) if data.size else None, _p(index), maps, R, block_size,
+                                hash_bits, _p(out), _p(oix))
+    return out[:n].tobytes(), oix, oix.astype(">i8").tobytes()
+
+
+def lz4_unframe(stream: bytes, cap: int) -> bytes:
+    """Decode concatenated LZ4BlockOutputStream streams (checks magic, lengths, checksums)."""
+    s = np.frombuffer(stream, np.uint8).copy() if stream else np.zeros(1, np.uint8)
+    out = np.empty(max(1, cap), np.uint8)
+    n = lib().o_lz4_unframe(_p(s), len(stream), _p(out), cap)
+    if n < 0:
+        raise ValueError("malformed LZ4Block stream")
+    return out[:n].tobytes()

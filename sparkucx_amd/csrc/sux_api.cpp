@@ -637,6 +637,68 @@ int sux_partition_varlen(sux_node* node, const sux_partitioner* part, const void
   });
 }
 
+// ---- compressed map outputs (spark.shuffle.compress with the lz4 codec) ------------------------
+namespace {
+void check_lz4_args(uint64_t data_bytes, int32_t maps, int32_t R, int32_t bs) {
+  require(maps >= 1 && R >= 1 && R <= sux::kMaxPartitions, SUX_EINVAL,
+          "num_maps must be >= 1 and num_partitions in [1, 32768]");
+  require(bs >= 64 && bs <= 65536 && bs % 4 == 0, SUX_EINVAL,
+          "block_size must be a multiple of 4 in [64, 65536], got " + std::to_string(bs));
+  require((uint64_t)maps * R < (1ull << 31), SUX_ERANGE, "too many (map, partition) runs");
+  require(sux::lz4_chunk_bound(data_bytes, (uint64_t)maps * R, (uint32_t)bs) < (1ull << 32),
+          SUX_ERANGE, "too many compression chunks in one call");
+}
+}  // namespace
+
+int sux_compress_bound(uint64_t data_bytes, int32_t num_maps, int32_t R, int32_t block_size,
+                       uint64_t* bytes) {
+  return guard([&] {
+    require(bytes, SUX_EINVAL, "NULL argument");
+    check_lz4_args(data_bytes, num_maps, R, block_size);
+    *bytes = sux::lz4_output_bound(data_bytes, (uint64_t)num_maps * R, (uint32_t)block_size);
+  });
+}
+
+int sux_compress_workspace_size(uint64_t data_bytes, int32_t num_maps, int32_t R,
+                                int32_t block_size, uint64_t* bytes) {
+  return guard([&] {
+    require(bytes, SUX_EINVAL, "NULL argument");
+    check_lz4_args(data_bytes, num_maps, R, block_size);
+    *bytes = sux::lz4_workspace_layout(data_bytes, (uint32_t)num_maps, (uint32_t)R,
+                                       (uint32_t)block_size).total;
+  });
+}
+
+int sux_compress_map_outputs(sux_node* node, const void* d_data, uint64_t data_bytes,
+                             const int64_t* d_index, int32_t num_maps, int32_t R,
+                             int32_t block_size, void* d_out, uint64_t out_capacity,
+                             int64_t* d_out_index, uint8_t* d_out_index_be,
+                             uint64_t* d_out_bytes, void* d_ws, uint64_t ws_bytes, void* stream) {
+  return guard([&] {
+    require(node && d_index && d_out && d_out_index, SUX_EINVAL, "NULL argument");
+    require(d_data || data_bytes == 0, SUX_EINVAL, "data pointer is NULL");
+    check_lz4_args(data_bytes, num_maps, R, block_size);
+    const sux::Lz4Workspace w = sux::lz4_workspace_layout(data_bytes, (uint32_t)num_maps,
+                                                          (uint32_t)R, (uint32_t)block_size);
+    require(d_ws && ws_bytes >= w.total, SUX_EINVAL,
+            "workspace too small: need " + std::to_string(w.total) + " bytes");
+    require(((uintptr_t)d_ws & 255) == 0 && ((uintptr_t)d_out_index & 7) == 0 &&
+                ((uintptr_t)d_out_index_be & 7) == 0 && ((uintptr_t)d_index & 7) == 0,
+            SUX_EINVAL, "index (8 B) and workspace (256 B) must be aligned");
+    const uint64_t need =
+        sux::lz4_output_bound(data_bytes, (uint64_t)num_maps * R, (uint32_t)block_size);
+    require(out_capacity >= need, SUX_EINVAL,
+            "output capacity too small: need sux_compress_bound = " + std::to_string(need));
+    node->bind();
+    hip_check(sux::launch_lz4_compress(static_cast<const uint8_t*>(d_data), d_index,
+                                       (uint32_t)num_maps, (uint32_t)R, (uint32_t)block_size,
+                                       static_cast<uint8_t*>(d_out), d_out_index, d_out_index_be,
+                                       d_out_bytes, static_cast<uint8_t*>(d_ws), w,
+                                       node->stream(stream)),
+              "compress launch");
+  });
+}
+
 // ---- exchange plan (host arithmetic) -----------------------------------------------------------
 int sux_plan_group(int32_t W, int32_t rank, int32_t M, int32_t R, const int64_t* gi,
                    uint64_t* sendcounts, uint64_t* sdispls, uint64_t* recvcounts,

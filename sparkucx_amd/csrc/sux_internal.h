@@ -101,6 +101,25 @@ uint32_t choose_varlen_tile(uint32_t R, uint64_t rows);
 // totals -> index tables in bytes + byte bases of every (map, partition) run
 hipError_t launch_varlen_map_scan(const VarGroup& g, int R, const uint64_t* totals, uint64_t* base,
                                   int64_t* d_index, uint8_t* d_index_be, hipStream_t s);
+// ---- compressed map outputs (sux_lz4.hip) ----
+struct Lz4Chunk {            // one <= blockSize piece of a (map, partition) run
+  uint64_t src;              // byte offset in the map-output buffer
+  uint32_t len, run, last;   // bytes, run id (map * R + partition), last piece of its run
+  uint32_t clen, csum, pad;  // LZ4 block bytes (0: stored raw), XXH32 & 0x0FFFFFFF
+};
+struct Lz4Workspace {
+  uint64_t map_base_off, nb_off, b0_off, nchunks_off, chunks_off, sz_off, off_off, rs_off,
+      base_off, temp_off, temp_bytes, scratch_off, chunk_bound, total;
+};
+uint64_t lz4_chunk_bound(uint64_t data_bytes, uint64_t runs, uint32_t bs);
+uint64_t lz4_output_bound(uint64_t data_bytes, uint64_t runs, uint32_t bs);
+Lz4Workspace lz4_workspace_layout(uint64_t data_bytes, uint32_t maps, uint32_t R, uint32_t bs);
+hipError_t launch_lz4_compress(const uint8_t* d_data, const int64_t* d_index, uint32_t maps,
+                               uint32_t R, uint32_t bs, uint8_t* d_out, int64_t* d_out_index,
+                               uint8_t* d_out_index_be, uint64_t* d_out_bytes, uint8_t* d_ws,
+                               const Lz4Workspace& w, hipStream_t s);
+hipError_t launch_rows_index(const uint64_t* sizes, uint32_t maps, uint32_t R, uint64_t* base,
+                             int64_t* d_index, uint8_t* d_index_be, hipStream_t s);
 hipError_t launch_partition_ids(const PartDev& pd, const uint8_t* recs, uint32_t rec_size,
                                 uint64_t n, uint16_t* d_pids, hipStream_t s);
 

@@ -1,0 +1,465 @@
+// sux_lz4.hip — compressed map outputs (spark.shuffle.compress=true with
+// Spark's default lz4 codec): every non-empty (map, partition) run of a map output becomes its own
+// lz4-java LZ4BlockOutputStream stream, as Spark's writers wrap each partition segment in a fresh
+// compressed stream [ext: Spark 3.0 LZ4CompressionCodec.compressedOutputStream =
+// new LZ4BlockOutputStream(s, spark.io.compression.lz4.blockSize)].  Stream layout (lz4-java
+// 1.7.1 [ext]): per chunk of <= blockSize bytes a 21-byte header
+//   "LZ4Block" | token = method | level | compressed length LE32 | original length LE32 |
+//   XXH32(original, 0x9747b28c) & 0x0FFFFFFF LE32
+// then the LZ4 block (method 0x20) or the raw bytes (method 0x10, when compressing does not
+// shrink the chunk); close() appends an end mark (method 0x10, all lengths and checksum 0).
+// level = max(0, ceil(log2(blockSize)) - 10).  An empty run writes nothing (streams open lazily).
+//
+// Kernels (one launch each, sizes bounded on the host so nothing waits on the device):
+//   k_lz4_map_base  map data starts (maps are consecutive: prefix of index[m][R])
+//   k_lz4_runs      chunks per run -> (rocprim scan) -> k_lz4_fill: chunk table, map-major
+//   k_lz4_compress  one wave per chunk: LZ4 block format, window-parallel parse (below)
+//   k_xxh32         4 lanes per chunk (XXH32's four accumulators), 16 chunks per wave
+//   k_lz4_sizes     framed size of every chunk (+ the end mark on a run's last chunk)
+//                   -> (rocprim scan) -> output offsets; run sizes -> k_map_scan -> index
+//   k_lz4_emit      one wave per chunk: header + payload (compressed or raw) + end mark
+//
+// The parse (deterministic; oracle.c o_lz4_compress_block restates it):
+//   positions are visited in windows of 64 (one per lane).  A window is hashed when the parse
+//   enters it: candidate = the hash table entry as it stood at the window's start (the latest
+//   earlier position with that hash, else position 0; entries (position << 32 | its 4 bytes) so
+//   candidates are verified from LDS), then every lane's position is max-merged into the table.  A position
+//   starts a match if its 4 bytes equal the candidate's, the offset is 1..65535 and it lies at
+//   or before len - 12 (LZ4's MFLIMIT).  Matches extend forward while input bytes agree, up to
+//   len - 5 (LASTLITERALS), greedily from the current position; windows wholly inside a match
+//   are skipped (not hashed).  Chunks that would not shrink are stored raw.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include <rocprim/rocprim.hpp>
+
+#include "sux_internal.h"
+
+namespace sux {
+
+namespace {
+constexpr int kLWave = 64;
+constexpr int kLz4Hdr = 21;
+constexpr uint32_t kXxhSeed = 0x9747b28cu;
+constexpr uint32_t P1 = 2654435761u, P2 = 2246822519u, P3 = 3266489917u, P4 = 668265263u,
+                   P5 = 374761393u;
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+// 4 bytes at any byte address: two aligned dword loads (the second only when the bytes straddle),
+// funnel-shifted.  Never reads outside the aligned dwords holding the 4 bytes.
+__device__ __forceinline__ uint32_t ld32u(const uint8_t* p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t sh = (uint32_t)(a & 3u) * 8u;
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+  const uint32_t lo = q[0];
+  const uint32_t hi = q[sh ? 1 : 0];
+  return sh ? ((lo >> sh) | (hi << (32u - sh))) : lo;
+}
+
+// Wave-cooperative copy of n bytes, any alignment on either side: byte stores up to dst's first
+// dword boundary, dword stores for the body (source funnel-shifted), byte stores for the tail.
+__device__ __forceinline__ void wave_copy(uint8_t* dst, const uint8_t* src, uint32_t n, int lane) {
+  const uint32_t head = min(n, (uint32_t)((4u - (reinterpret_cast<uintptr_t>(dst) & 3u)) & 3u));
+  if ((uint32_t)lane < head) dst[lane] = src[lane];
+  const uint32_t nd = (n - head) / 4u;
+  uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + head);
+  const uint8_t* s = src + head;
+  uint32_t k = lane;
+  for (; k + 3u * kLWave < nd; k += 4u * kLWave) {
+    uint32_t v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = ld32u(s + 4u * (k + u * kLWave));
+#pragma unroll
+    for (int u = 0; u < 4; ++u) d32[k + u * kLWave] = v[u];
+  }
+  for (; k < nd; k += kLWave) d32[k] = ld32u(s + 4u * k);
+  const uint32_t done = head + 4u * nd;
+  if ((uint32_t)lane < n - done) dst[done + lane] = src[done + lane];
+}
+
+__device__ __forceinline__ uint32_t ext_bytes(uint32_t v) { return v >= 15u ? (v - 15u) / 255u + 1u : 0u; }
+
+// lane-parallel LZ4 length extension: (v - 15) as 255s then the remainder
+__device__ __forceinline__ void put_ext(uint8_t* d, uint32_t v, int lane) {
+  const uint32_t nb = ext_bytes(v);
+  for (uint32_t k = lane; k < nb; k += kLWave) d[k] = (k + 1 < nb) ? 255u : (uint8_t)((v - 15u) % 255u);
+}
+
+__host__ __device__ __forceinline__ int lz4_level(uint32_t bs) {
+  const int l = 32 - __builtin_clz(bs - 1u);
+  return l > 10 ? l - 10 : 0;
+}
+}  // namespace
+
+__global__ __launch_bounds__(256) void k_lz4_map_base(const int64_t* __restrict__ index, int maps,
+                                                      int R, uint64_t* __restrict__ map_base) {
+  __shared__ uint64_t part[256];
+  // one workgroup: per-thread serial sums over a slice of maps, then a block scan of the slices
+  const int t = threadIdx.x, per = (maps + 255) / 256;
+  const int m0 = min(maps, t * per), m1 = min(maps, m0 + per);
+  uint64_t s = 0;
+  for (int m = m0; m < m1; ++m) s += (uint64_t)index[(uint64_t)m * (R + 1) + R];
+  part[t] = s;
+  __syncthreads();
+  if (t == 0) {
+    uint64_t c = 0;
+    for (int i = 0; i < 256; ++i) { const uint64_t v = part[i]; part[i] = c; c += v; }
+    map_base[maps] = c;
+  }
+  __syncthreads();
+  uint64_t c = part[t];
+  for (int m = m0; m < m1; ++m) {
+    map_base[m] = c;
+    c += (uint64_t)index[(uint64_t)m * (R + 1) + R];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_lz4_runs(const int64_t* __restrict__ index, int maps,
+                                                  int R, uint32_t bs, uint32_t* __restrict__ nb) {
+  const uint64_t r = blockIdx.x * 256ull + threadIdx.x;
+  if (r >= (uint64_t)maps * R) return;
+  const uint64_t m = r / R, p = r - m * R;
+  const int64_t* im = index + m * (R + 1);
+  const uint64_t L = (uint64_t)(im[p + 1] - im[p]);
+  nb[r] = (uint32_t)((L + bs - 1) / bs);
+}
+
+__global__ __launch_bounds__(256) void k_lz4_fill(const int64_t* __restrict__ index, int maps,
+                                                  int R, uint32_t bs,
+                                                  const uint64_t* __restrict__ map_base,
+                                                  const uint32_t* __restrict__ b0,
+                                                  Lz4Chunk* __restrict__ chunks,
+                                                  uint32_t* __restrict__ nchunks) {
+  const uint64_t r = blockIdx.x * 256ull + threadIdx.x;
+  const uint64_t runs = (uint64_t)maps * R;
+  if (r >= runs) return;
+  const uint64_t m = r / R, p = r - m * R;
+  const int64_t* im = index + m * (R + 1);
+  const uint64_t start = map_base[m] + (uint64_t)im[p];
+  const uint64_t L = (uint64_t)(im[p + 1] - im[p]);
+  const uint32_t n = (uint32_t)((L + bs - 1) / bs);
+  for (uint32_t k = 0; k < n; ++k) {
+    Lz4Chunk c;
+    c.src = start + (uint64_t)k * bs;
+    c.len = (uint32_t)min((uint64_t)bs, L - (uint64_t)k * bs);
+    c.run = (uint32_t)r;
+    c.last = (k + 1 == n) ? 1u : 0u;
+    c.clen = 0;
+    c.csum = 0;
+    c.pad = 0;
+    chunks[b0[r] + k] = c;
+  }
+  if (r + 1 == runs) *nchunks = b0[r] + n;
+}
+
+// One wave per chunk.  HB = hash bits (table of 2^HB u64 entries per wave in LDS).
+template <int HB>
+__global__ __launch_bounds__(256) void k_lz4_compress(const uint8_t* __restrict__ data,
+                                                      Lz4Chunk* __restrict__ chunks,
+                                                      const uint32_t* __restrict__ nchunks,
+                                                      uint8_t* __restrict__ scratch) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long ltab[];
+  const int wave = threadIdx.x / kLWave, lane = threadIdx.x % kLWave;
+  unsigned long long* tab = ltab + (size_t)wave * (1u << HB);
+  const uint32_t n = *nchunks;
+  for (uint32_t b = blockIdx.x * 4u + wave; b < n; b += gridDim.x * 4u) {
+    const Lz4Chunk C = chunks[b];
+    const uint8_t* src = data + C.src;
+    const uint32_t len = C.len;
+    uint8_t* dst = scratch + ((C.src + 16ull * b) & ~3ull);
+    bool raw = len < 13;
+    uint32_t op = 0, anchor = 0, cur = 0;
+    if (!raw) {
+      // every entry starts as position 0 with position 0's true bytes (a verifiable candidate)
+      const unsigned long long e0 = ld32u(src);
+      for (uint32_t i = lane; i < (1u << HB); i += kLWave) tab[i] = e0;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      const uint32_t last = len - 12;         // last position a match may start at
+      const uint32_t mlimit = len - 5;        // matches end at or before this
+      const uint32_t nwin = last / kLWave + 1;
+      uint32_t w = 0;
+      while (w < nwin) {
+        const uint32_t pos = w * kLWave + lane;
+        const bool in = pos <= last;
+        const uint32_t seq = ld32u(src + (in ? pos : 0u));
+        const uint32_t h = (seq * P1) >> (32 - HB);
+        const unsigned long long e = tab[h];
+        const uint32_t cpos = (uint32_t)(e >> 32), cseq = (uint32_t)e;
+        const bool m = in && cpos < pos && pos - cpos <= 65535u && cseq == seq;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (in) atomicMax(&tab[h], ((unsigned long long)pos << 32) | seq);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        const uint64_t mm = __ballot(m);
+        uint32_t nextw = w + 1;
+        while (true) {
+          const uint32_t rel = cur > w * kLWave ? cur - w * kLWave : 0u;
+          if (rel >= (uint32_t)kLWave) break;
+          const uint64_t mk = mm & (~0ull << rel);
+          if (!mk) break;
+          const int j = __builtin_ctzll(mk);
+          const uint32_t p = w * kLWave + j;
+          const uint32_t c = (uint32_t)__shfl((int)cpos, j, kLWave);
+          // forward extension, 256 bytes per round
+          uint32_t ml = 4;
+          while (true) {
+            const uint32_t lim = mlimit - (p + ml);  // bytes still allowed
+            const uint32_t o = 4u * lane;
+            uint32_t eq = 0;
+            if (o < lim) {
+              const uint32_t x = ld32u(src + p + ml + o) ^ ld32u(src + c + ml + o);
+              eq = x ? (uint32_t)(__builtin_ctz(x) >> 3) : 4u;
+              eq = min(eq, lim - o);
+            }
+            const uint64_t stop = __ballot(eq < 4u);
+            if (stop) {
+              const int s = __builtin_ctzll(stop);
+              ml += 4u * s + (uint32_t)__shfl((int)eq, s, kLWave);
+              break;
+            }
+            ml += 4u * kLWave;
+          }
+          const uint32_t LL = p - anchor;
+          const uint32_t need = 1u + ext_bytes(LL) + LL + 2u + ext_bytes(ml - 4u);
+          if (op + need >= len) { raw = true; break; }
+          uint8_t* d = dst + op;
+          if (lane == 0) d[0] = (uint8_t)((min(LL, 15u) << 4) | min(ml - 4u, 15u));
+          put_ext(d + 1, LL, lane);
+          const uint32_t lo = 1u + ext_bytes(LL);
+          wave_copy(d + lo, src + anchor, LL, lane);
+          const uint32_t off = p - c;
+          if (lane == 0) {
+            d[lo + LL] = (uint8_t)off;
+            d[lo + LL + 1] = (uint8_t)(off >> 8);
+          }
+          put_ext(d + lo + LL + 2, ml - 4u, lane);
+          op += need;
+          cur = p + ml;
+          anchor = cur;
+          if (cur >= (w + 1) * kLWave) { nextw = cur / kLWave; break; }
+        }
+        if (raw) break;
+        w = nextw;
+      }
+      if (!raw) {
+        const uint32_t LL = len - anchor;
+        const uint32_t need = 1u + ext_bytes(LL) + LL;
+        if (op + need >= len) {
+          raw = true;
+        } else {
+          uint8_t* d = dst + op;
+          if (lane == 0) d[0] = (uint8_t)(min(LL, 15u) << 4);
+          put_ext(d + 1, LL, lane);
+          wave_copy(d + 1 + ext_bytes(LL), src + anchor, LL, lane);
+          op += need;
+        }
+      }
+    }
+    if (lane == 0) chunks[b].clen = raw ? 0u : op;
+  }
+}
+
+// XXH32 (seed 0x9747b28c) of every chunk's original bytes, masked to 28 bits as lz4-java's
+// StreamingXXHash32.asChecksum() does.  Lanes 4g..4g+3 run the four stripe accumulators of
+// chunk 16 * wave + g; the tail and avalanche on the group's first lane.
+__global__ __launch_bounds__(256) void k_xxh32(const uint8_t* __restrict__ data,
+                                               Lz4Chunk* __restrict__ chunks,
+                                               const uint32_t* __restrict__ nchunks) {
+  const uint32_t n = *nchunks;
+  const int lane = threadIdx.x % kLWave, sub = lane & 3;
+  const uint32_t gw = (blockIdx.x * 256u + threadIdx.x) / kLWave;
+  const uint32_t waves = gridDim.x * 4u;
+  for (uint32_t b0 = gw * 16u; b0 < n; b0 += waves * 16u) {
+    const uint32_t b = min(b0 + (uint32_t)(lane >> 2), n - 1);
+    const Lz4Chunk C = chunks[b];
+    const uint8_t* s = data + C.src;
+    const uint32_t len = C.len, stripes = len / 16u;
+    uint32_t v = sub == 0 ? kXxhSeed + P1 + P2 : sub == 1 ? kXxhSeed + P2 : sub == 2 ? kXxhSeed : kXxhSeed - P1;
+    uint32_t k = 0;
+    for (; k + 8 <= stripes; k += 8) {
+      uint32_t x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = ld32u(s + 16u * (k + u) + 4u * sub);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v = rotl(v + x[u] * P2, 13) * P1;
+    }
+    for (; k < stripes; ++k) v = rotl(v + ld32u(s + 16u * k + 4u * sub) * P2, 13) * P1;
+    const int base = lane & ~3;
+    const uint32_t v1 = __shfl((int)v, base, kLWave), v2 = __shfl((int)v, base + 1, kLWave);
+    const uint32_t v3 = __shfl((int)v, base + 2, kLWave), v4 = __shfl((int)v, base + 3, kLWave);
+    if (sub == 0 && b0 + (uint32_t)(lane >> 2) < n) {
+      uint32_t h = len >= 16 ? rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18) : kXxhSeed + P5;
+      h += len;
+      uint32_t i = stripes * 16u;
+      for (; i + 4 <= len; i += 4) h = rotl(h + ld32u(s + i) * P3, 17) * P4;
+      for (; i < len; ++i) h = rotl(h + (uint32_t)s[i] * P5, 11) * P1;
+      h ^= h >> 15;
+      h *= P2;
+      h ^= h >> 13;
+      h *= P3;
+      h ^= h >> 16;
+      chunks[b].csum = h & 0x0FFFFFFFu;
+    }
+  }
+}
+
+// framed bytes of chunk b (0 past the chunk count: the scan runs over the host-side bound)
+__global__ __launch_bounds__(256) void k_lz4_sizes(const Lz4Chunk* __restrict__ chunks,
+                                                   const uint32_t* __restrict__ nchunks,
+                                                   uint64_t bound, uint64_t* __restrict__ sz) {
+  const uint64_t b = blockIdx.x * 256ull + threadIdx.x;
+  if (b >= bound) return;
+  uint64_t v = 0;
+  if (b < *nchunks) {
+    const Lz4Chunk C = chunks[b];
+    v = kLz4Hdr + (C.clen ? C.clen : C.len) + (C.last ? kLz4Hdr : 0);
+  }
+  sz[b] = v;
+}
+
+// per-run framed bytes: first chunk's offset to the last chunk's end (0 for an empty run)
+__global__ __launch_bounds__(256) void k_lz4_run_sizes(const uint32_t* __restrict__ b0,
+                                                       const uint64_t* __restrict__ off,
+                                                       const uint64_t* __restrict__ sz,
+                                                       uint64_t runs,
+                                                       const uint32_t* __restrict__ nchunks,
+                                                       uint64_t* __restrict__ rs,
+                                                       uint64_t* __restrict__ total) {
+  const uint64_t r = blockIdx.x * 256ull + threadIdx.x;
+  if (r >= runs) return;
+  const uint32_t first = b0[r];
+  const uint32_t end = (r + 1 < runs) ? b0[r + 1] : *nchunks;
+  rs[r] = end > first ? (off[end - 1] + sz[end - 1] - off[first]) : 0ull;
+  if (r + 1 == runs && total) *total = end > 0 ? off[end - 1] + sz[end - 1] : 0ull;
+}
+
+__global__ __launch_bounds__(256) void k_lz4_emit(const uint8_t* __restrict__ data,
+                                                  const Lz4Chunk* __restrict__ chunks,
+                                                  const uint32_t* __restrict__ nchunks,
+                                                  const uint8_t* __restrict__ scratch,
+                                                  const uint64_t* __restrict__ off, int level,
+                                                  uint8_t* __restrict__ out) {
+  const int wave = threadIdx.x / kLWave, lane = threadIdx.x % kLWave;
+  const uint32_t n = *nchunks;
+  for (uint32_t b = blockIdx.x * 4u + wave; b < n; b += gridDim.x * 4u) {
+    const Lz4Chunk C = chunks[b];
+    uint8_t* d = out + off[b];
+    const bool raw = C.clen == 0;
+    const uint32_t plen = raw ? C.len : C.clen;
+    if (lane < kLz4Hdr) {
+      const char* magic = "LZ4Block";
+      uint8_t v;
+      if (lane < 8) v = (uint8_t)magic[lane];
+      else if (lane == 8) v = (uint8_t)((raw ? 0x10 : 0x20) | level);
+      else {
+        const int f = (lane - 9) / 4, sh = 8 * ((lane - 9) % 4);
+        const uint32_t x = f == 0 ? plen : f == 1 ? C.len : C.csum;
+        v = (uint8_t)(x >> sh);
+      }
+      d[lane] = v;
+    }
+    const uint8_t* s = raw ? data + C.src : scratch + ((C.src + 16ull * b) & ~3ull);
+    wave_copy(d + kLz4Hdr, s, plen, lane);
+    if (C.last && lane < kLz4Hdr) {
+      const char* magic = "LZ4Block";
+      d[kLz4Hdr + plen + lane] =
+          lane < 8 ? (uint8_t)magic[lane] : lane == 8 ? (uint8_t)(0x10 | level) : (uint8_t)0;
+    }
+  }
+}
+
+// ---- host-side launcher -----------------------------------------------------------------------
+uint64_t lz4_chunk_bound(uint64_t data_bytes, uint64_t runs, uint32_t bs) {
+  return data_bytes / bs + runs + 1;
+}
+
+uint64_t lz4_output_bound(uint64_t data_bytes, uint64_t runs, uint32_t bs) {
+  return data_bytes + lz4_chunk_bound(data_bytes, runs, bs) * kLz4Hdr + runs * kLz4Hdr;
+}
+
+static size_t scan_temp_bytes(uint64_t n32, uint64_t n64) {
+  size_t a = 0, b = 0;
+  (void)rocprim::exclusive_scan(nullptr, a, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u,
+                                (size_t)n32, rocprim::plus<uint32_t>());
+  (void)rocprim::exclusive_scan(nullptr, b, (const uint64_t*)nullptr, (uint64_t*)nullptr, 0ull,
+                                (size_t)n64, rocprim::plus<uint64_t>());
+  return std::max(a, b);
+}
+
+static uint64_t up256(uint64_t x) { return (x + 255) & ~255ull; }
+
+Lz4Workspace lz4_workspace_layout(uint64_t data_bytes, uint32_t maps, uint32_t R, uint32_t bs) {
+  Lz4Workspace w{};
+  const uint64_t runs = (uint64_t)maps * R;
+  const uint64_t cb = lz4_chunk_bound(data_bytes, runs, bs);
+  uint64_t o = 0;
+  w.map_base_off = o;  o += up256((maps + 1) * 8ull);
+  w.nb_off = o;        o += up256(runs * 4);
+  w.b0_off = o;        o += up256(runs * 4);
+  w.nchunks_off = o;   o += 256;
+  w.chunks_off = o;    o += up256(cb * sizeof(Lz4Chunk));
+  w.sz_off = o;        o += up256(cb * 8);
+  w.off_off = o;       o += up256(cb * 8);
+  w.rs_off = o;        o += up256(runs * 8);
+  w.base_off = o;      o += up256(3 * runs * 8);
+  w.temp_off = o;
+  w.temp_bytes = up256(scan_temp_bytes(runs, cb));
+  o += w.temp_bytes;
+  w.scratch_off = o;   o += up256(data_bytes + 16 * cb + 64);
+  w.chunk_bound = cb;
+  w.total = o;
+  return w;
+}
+
+hipError_t launch_lz4_compress(const uint8_t* d_data, const int64_t* d_index, uint32_t maps,
+                               uint32_t R, uint32_t bs, uint8_t* d_out, int64_t* d_out_index,
+                               uint8_t* d_out_index_be, uint64_t* d_out_bytes, uint8_t* d_ws,
+                               const Lz4Workspace& w, hipStream_t s) {
+  const uint64_t runs = (uint64_t)maps * R;
+  uint64_t* map_base = reinterpret_cast<uint64_t*>(d_ws + w.map_base_off);
+  uint32_t* nb = reinterpret_cast<uint32_t*>(d_ws + w.nb_off);
+  uint32_t* b0 = reinterpret_cast<uint32_t*>(d_ws + w.b0_off);
+  uint32_t* nchunks = reinterpret_cast<uint32_t*>(d_ws + w.nchunks_off);
+  Lz4Chunk* chunks = reinterpret_cast<Lz4Chunk*>(d_ws + w.chunks_off);
+  uint64_t* sz = reinterpret_cast<uint64_t*>(d_ws + w.sz_off);
+  uint64_t* off = reinterpret_cast<uint64_t*>(d_ws + w.off_off);
+  uint64_t* rs = reinterpret_cast<uint64_t*>(d_ws + w.rs_off);
+  uint64_t* base = reinterpret_cast<uint64_t*>(d_ws + w.base_off);
+  void* temp = d_ws + w.temp_off;
+  uint8_t* scratch = d_ws + w.scratch_off;
+  const uint32_t rg = (uint32_t)((runs + 255) / 256);
+  hipLaunchKernelGGL(k_lz4_map_base, dim3(1), dim3(256), 0, s, d_index, (int)maps, (int)R, map_base);
+  hipLaunchKernelGGL(k_lz4_runs, dim3(rg), dim3(256), 0, s, d_index, (int)maps, (int)R, bs, nb);
+  size_t tb = w.temp_bytes;
+  hipError_t e = rocprim::exclusive_scan(temp, tb, nb, b0, 0u, (size_t)runs,
+                                         rocprim::plus<uint32_t>(), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_lz4_fill, dim3(rg), dim3(256), 0, s, d_index, (int)maps, (int)R, bs, map_base,
+                     b0, chunks, nchunks);
+  const uint32_t cg = (uint32_t)std::min<uint64_t>((w.chunk_bound + 3) / 4, 8192);
+  constexpr int HB = 11;
+  const size_t lds = 4 * (size_t(1) << HB) * 8;
+  hipLaunchKernelGGL((k_lz4_compress<HB>), dim3(cg), dim3(256), lds, s, d_data, chunks, nchunks,
+                     scratch);
+  const uint32_t xg = (uint32_t)std::min<uint64_t>((w.chunk_bound + 63) / 64, 4096);
+  hipLaunchKernelGGL(k_xxh32, dim3(xg), dim3(256), 0, s, d_data, chunks, nchunks);
+  const uint32_t bg = (uint32_t)((w.chunk_bound + 255) / 256);
+  hipLaunchKernelGGL(k_lz4_sizes, dim3(bg), dim3(256), 0, s, chunks, nchunks, w.chunk_bound, sz);
+  tb = w.temp_bytes;
+  e = rocprim::exclusive_scan(temp, tb, sz, off, 0ull, (size_t)w.chunk_bound,
+                              rocprim::plus<uint64_t>(), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_lz4_run_sizes, dim3(rg), dim3(256), 0, s, b0, off, sz, runs, nchunks, rs,
+                     d_out_bytes);
+  e = launch_rows_index(rs, maps, R, base, d_out_index, d_out_index_be, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_lz4_emit, dim3(cg), dim3(256), 0, s, d_data, chunks, nchunks, scratch, off,
+                     lz4_level(bs), d_out);
+  return hipGetLastError();
+}
+
+}  // namespace sux

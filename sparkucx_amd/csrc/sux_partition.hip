@@ -1848,4 +1848,14 @@ hipError_t launch_varlen_map_scan(const VarGroup& g, int R, const uint64_t* tota
   return hipGetLastError();
 }
 
+// Index tables from per-(map, partition) byte sizes (sux_lz4.hip's compressed runs).
+hipError_t launch_rows_index(const uint64_t* sizes, uint32_t maps, uint32_t R, uint64_t* base,
+                             int64_t* d_index, uint8_t* d_index_be, hipStream_t s) {
+  const uint64_t L = (uint64_t)maps * R;
+  hipLaunchKernelGGL(k_map_scan, dim3(maps), dim3(kScanThreads), 0, s, sizes, base, base + L,
+                     base + 2 * L, d_index, d_index_be, nullptr, (int)R, 1, 1u, 0ull, 0ull,
+                     nullptr);
+  return hipGetLastError();
+}
+
 }  // namespace sux

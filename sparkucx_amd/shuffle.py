@@ -199,6 +199,49 @@ class Node:
                 "sux_partition_varlen")
         return out, index, index_be
 
+    def compress_bound(self, data_bytes: int, num_maps: int, R: int, block_size: int = 32768) -> int:
+        b = C.c_uint64()
+        N.check(self.lib.sux_compress_bound(data_bytes, num_maps, R, block_size, C.byref(b)),
+                "sux_compress_bound")
+        return b.value
+
+    def compress_workspace_size(self, data_bytes: int, num_maps: int, R: int,
+                                block_size: int = 32768) -> int:
+        b = C.c_uint64()
+        N.check(self.lib.sux_compress_workspace_size(data_bytes, num_maps, R, block_size,
+                                                     C.byref(b)), "sux_compress_workspace_size")
+        return b.value
+
+    def compress_map_outputs(self, data: torch.Tensor, index: torch.Tensor, num_maps: int, R: int,
+                             block_size: int = 32768, data_bytes: int | None = None,
+                             out: torch.Tensor | None = None, out_index=None, out_index_be=None,
+                             out_bytes: torch.Tensor | None = None,
+                             workspace: torch.Tensor | None = None, want_be: bool = True,
+                             stream=None):
+        """spark.shuffle.compress=true (lz4): every (map, partition) run of the consecutive map
+        outputs in `data` -> its own LZ4BlockOutputStream stream.  Returns (out, out_index,
+        out_index_be, out_bytes) with out_bytes a 1-element device int64 tensor (the total)."""
+        nb = data.numel() if data_bytes is None else data_bytes
+        if out is None:
+            out = torch.empty(max(16, self.compress_bound(nb, num_maps, R, block_size)),
+                              dtype=torch.uint8, device=self.dev)
+        if out_index is None:
+            out_index = torch.empty(num_maps * (R + 1), dtype=torch.int64, device=self.dev)
+        if out_index_be is None and want_be:
+            out_index_be = torch.empty(num_maps * (R + 1) * 8, dtype=torch.uint8, device=self.dev)
+        if out_bytes is None:
+            out_bytes = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        if workspace is None:
+            workspace = torch.empty(self.compress_workspace_size(nb, num_maps, R, block_size),
+                                    dtype=torch.uint8, device=self.dev)
+        N.check(self.lib.sux_compress_map_outputs(self.h, _ptr(data), nb, _ptr(index), num_maps, R,
+                                                  block_size, _ptr(out), out.numel(),
+                                                  _ptr(out_index), _ptr(out_index_be),
+                                                  _ptr(out_bytes), _ptr(workspace),
+                                                  workspace.numel(), _stream(stream)),
+                "sux_compress_map_outputs")
+        return out, out_index, out_index_be, out_bytes
+
     def exchange_group(self, send: torch.Tensor, index: torch.Tensor, num_maps: int, R: int,
                        gathered: torch.Tensor, recv: torch.Tensor, stream=None) -> np.ndarray:
         rb = (C.c_uint64 * self.world_size)()
