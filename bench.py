@@ -137,7 +137,7 @@ def gen_unsafe_rows_dev(n: int, seed: int, dev, max_words: int = 12):
     return data, offs
 
 
-def varlen_leg(node, rows: int, rpm: int, R: int, dev) -> dict:
+def varlen_leg(node, rows: int, rpm: int, R: int, dev, compress: bool = False) -> dict:
     """§8f item 3: the map side over variable-length UnsafeRow-framed rows (sux_partition_varlen,
     Spark SQL hash of the int64 key at byte 12, R partitions).  GB/s of row bytes; the algorithmic
     HBM bytes are 2 x row bytes (read + write each row) + 44 B per row (offsets read twice, the
@@ -164,9 +164,39 @@ def varlen_leg(node, rows: int, rpm: int, R: int, dev) -> dict:
     ms = e0.elapsed_time(e1) / reps
     nb = data.numel()
     alg = 2 * nb + 44 * rows
-    return {"rows": rows, "row_bytes": nb, "avg_row": round(nb / rows, 1), "R": R,
-            "rows_per_map": rpm, "ms": round(ms, 3), "GB/s": round(nb / (ms / 1e3) / 1e9, 1),
-            "alg_bytes": alg, "alg_GB/s": round(alg / (ms / 1e3) / 1e9, 1)}
+    res = {"rows": rows, "row_bytes": nb, "avg_row": round(nb / rows, 1), "R": R,
+           "rows_per_map": rpm, "ms": round(ms, 3), "GB/s": round(nb / (ms / 1e3) / 1e9, 1),
+           "alg_bytes": alg, "alg_GB/s": round(alg / (ms / 1e3) / 1e9, 1)}
+    if compress:
+        res["compress"] = compress_leg(node, out, index, maps, R, dev)
+    return res
+
+
+def compress_leg(node, data, index, maps: int, R: int, dev, bs: int = 32768) -> dict:
+    """§8f item 3: spark.shuffle.compress=true (lz4) over map outputs already in HBM
+    (sux_compress_map_outputs: one LZ4Block stream per (map, partition) run).  GB/s of
+    uncompressed map-output bytes; ratio = framed output / input."""
+    nb = data.numel()
+    out = torch.empty(node.compress_bound(nb, maps, R, bs), dtype=torch.uint8, device=dev)
+    oix = torch.empty(maps * (R + 1), dtype=torch.int64, device=dev)
+    obe = torch.empty(maps * (R + 1) * 8, dtype=torch.uint8, device=dev)
+    ob = torch.zeros(1, dtype=torch.int64, device=dev)
+    ws = torch.empty(node.compress_workspace_size(nb, maps, R, bs), dtype=torch.uint8, device=dev)
+    run = lambda: node.compress_map_outputs(data, index, maps, R, bs, out=out, out_index=oix,
+                                            out_index_be=obe, out_bytes=ob, workspace=ws)
+    run()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 3
+    e0.record()
+    for _ in range(reps):
+        run()
+    e1.record()
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    return {"input_bytes": nb, "maps": maps, "R": R, "block_size": bs, "ms": round(ms, 3),
+            "GB/s": round(nb / (ms / 1e3) / 1e9, 1),
+            "ratio": round(int(ob.item()) / nb, 4)}
 
 
 def load_traffic(kernel: str) -> float | None:
@@ -207,6 +237,10 @@ def main():
     ap.add_argument("--varlen-rows", type=int, default=-1,
                     help="N=1: also time the map side over variable-length UnsafeRow-framed rows "
                          "(sux_partition_varlen; -1: 32 Mi rows in 1 Mi-row maps; 0: skip)")
+    ap.add_argument("--compress-maps", type=int, default=-1,
+                    help="N=1: also time sux_compress_map_outputs (lz4, 32 KiB chunks) over the "
+                         "first map outputs (-1: one launch group; 0: skip); the varlen leg's "
+                         "rows are compressed too")
     ap.add_argument("--cpu-records", type=int, default=10_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-reps", type=int, default=3)
@@ -473,9 +507,16 @@ def main():
         ns = min(ns, n)
         if ns > 0 and args.workload == "terasort":
             result["reduce_sort"] = reduce_sort(node, out[:ns * rs], ns, rs, dev)
+    if world == 1 and args.compress_maps != 0:
+        cm = min(maps, args.compress_maps if args.compress_maps > 0 else gm)
+        if cm:
+            # maps are consecutive in `out`: the first cm map outputs
+            nb = sum(int(index[m * (R + 1) + R].item()) for m in range(cm))
+            result["compress"] = compress_leg(node, out[:nb], index[:cm * (R + 1)], cm, R, dev)
     if world == 1 and args.varlen_rows != 0:
         vr = args.varlen_rows if args.varlen_rows > 0 else 32 << 20
-        result["varlen"] = varlen_leg(node, vr, min(vr, 1 << 20), 200, dev)
+        result["varlen"] = varlen_leg(node, vr, min(vr, 1 << 20), 200, dev,
+                                      compress=args.compress_maps != 0)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:

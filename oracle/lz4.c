@@ -20,7 +20,8 @@
  *     are literals; the last match starts >= 12 bytes before the end.  The decoder below is
  *     cross-checked against the system liblz4 (LZ4_decompress_safe / LZ4_compress_default) in
  *     tests/test_oracle_lz4.py.
- *   - o_lz4_compress_block restates the GPU compressor's own parse (sux_lz4.hip header), so the
+ *   - o_lz4_compress_block restates the GPU compressor's own parse (u32 table entries =
+ *     position << 16 | 16-bit tag; 4-byte confirmation in the parse) (sux_lz4.hip header), so the
  *     GPU bytes are checked bit for bit; the payload of lz4-java's own compressor (liblz4's
  *     greedy parse with acceleration) differs and is not what is compared — any valid block
  *     decodes to the same bytes, which is what a Spark reader observes.
@@ -86,11 +87,11 @@ static uint8_t* put_ext(uint8_t* d, uint32_t v) {
 int32_t o_lz4_compress_block(const uint8_t* src, int32_t len, int32_t hash_bits, uint8_t* dst) {
   if (len < 13) return 0;
   const uint32_t H = 1u << hash_bits;
-  uint64_t tab[1u << 16];
+  uint32_t tab[1u << 16];
   uint32_t cand[64];
   uint8_t ok[64];
   /* every entry starts as position 0 with position 0's true bytes */
-  for (uint32_t i = 0; i < H; ++i) tab[i] = rd32(src);
+  for (uint32_t i = 0; i < H; ++i) tab[i] = rd32(src) >> 16;
   const uint32_t last = (uint32_t)len - 12, mlimit = (uint32_t)len - 5, nwin = last / 64 + 1;
   uint32_t op = 0, anchor = 0, cur = 0, w = 0;
   while (w < nwin) {
@@ -102,16 +103,16 @@ int32_t o_lz4_compress_block(const uint8_t* src, int32_t len, int32_t hash_bits,
       if (pos > last) continue;
       const uint32_t seq = rd32(src + pos);
       const uint32_t h = (seq * XP1) >> (32 - hash_bits);
-      const uint64_t e = tab[h];
-      cand[l] = (uint32_t)(e >> 32);
-      ok[l] = cand[l] < pos && pos - cand[l] <= 65535u && (uint32_t)e == seq;
+      const uint32_t e = tab[h];
+      cand[l] = e >> 16;
+      ok[l] = cand[l] < pos && pos - cand[l] <= 65535u && (e & 0xFFFFu) == (seq >> 16);
     }
     for (uint32_t l = 0; l < 64; ++l) {
       const uint32_t pos = w * 64 + l;
       if (pos > last) continue;
       const uint32_t seq = rd32(src + pos);
       const uint32_t h = (seq * XP1) >> (32 - hash_bits);
-      const uint64_t v = ((uint64_t)pos << 32) | seq;
+      const uint32_t v = (pos << 16) | (seq >> 16);
       if (v > tab[h]) tab[h] = v;
     }
     uint32_t nextw = w + 1;
@@ -121,8 +122,12 @@ int32_t o_lz4_compress_block(const uint8_t* src, int32_t len, int32_t hash_bits,
       while (j < 64 && !ok[j]) ++j;
       if (j >= 64) break;
       const uint32_t p = w * 64 + j, c = cand[j];
-      uint32_t ml = 4;
+      uint32_t ml = 0;
       while (p + ml < mlimit && src[p + ml] == src[c + ml]) ++ml;
+      if (ml < 4) { /* tag collision */
+        ok[j] = 0;
+        continue;
+      }
       const uint32_t LL = p - anchor;
       const uint32_t need = 1 + ext_len(LL) + LL + 2 + ext_len(ml - 4);
       if (op + need >= (uint32_t)len) return 0;

@@ -22,14 +22,15 @@
 // The parse (deterministic; oracle.c o_lz4_compress_block restates it):
 //   positions are visited in windows of 64 (one per lane).  A window is hashed when the parse
 //   enters it: candidate = the hash table entry as it stood at the window's start (the latest
-//   earlier position with that hash, else position 0; entries (position << 32 | its 4 bytes) so
-//   candidates are verified from LDS), then every lane's position is max-merged into the table.  A position
-//   starts a match if its 4 bytes equal the candidate's, the offset is 1..65535 and it lies at
-//   or before len - 12 (LZ4's MFLIMIT).  Matches extend forward while input bytes agree, up to
+//   earlier position with that hash, else position 0; u32 entries = position << 16 | the high
+//   16 bits of its 4 bytes), then every lane's position is max-merged into the table.  A
+//   position is a match candidate if the tags agree, the offset is 1..65535 and it lies at or
+//   before len - 12 (LZ4's MFLIMIT); the parse takes it if all 4 bytes agree.  Matches extend forward while input bytes agree, up to
 //   len - 5 (LASTLITERALS), greedily from the current position; windows wholly inside a match
 //   are skipped (not hashed).  Chunks that would not shrink are stored raw.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 
 #include <rocprim/rocprim.hpp>
@@ -41,6 +42,7 @@ namespace sux {
 namespace {
 constexpr int kLWave = 64;
 constexpr int kLz4Hdr = 21;
+constexpr int kLz4HashBits = 11;  // oracle.py LZ4_HASH_BITS
 constexpr uint32_t kXxhSeed = 0x9747b28cu;
 constexpr uint32_t P1 = 2654435761u, P2 = 2246822519u, P3 = 3266489917u, P4 = 668265263u,
                    P5 = 374761393u;
@@ -50,12 +52,15 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return (x << r) | 
 // 4 bytes at any byte address: two aligned dword loads (the second only when the bytes straddle),
 // funnel-shifted.  Never reads outside the aligned dwords holding the 4 bytes.
 __device__ __forceinline__ uint32_t ld32u(const uint8_t* p) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const uint32_t sh = (uint32_t)(a & 3u) * 8u;
-  const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+  const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3u);
+  // pointer arithmetic (not an integer round trip) keeps the global address space: global_load,
+  // not flat_load (whose lgkmcnt share would make every LDS wait drain the loads in flight)
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(p - mis);
+  uint32_t k = mis ? 1u : 0u;
+  asm volatile("" : "+v"(k));  // opaque: both loads stay unconditional (no branch, counted vmcnt)
   const uint32_t lo = q[0];
-  const uint32_t hi = q[sh ? 1 : 0];
-  return sh ? ((lo >> sh) | (hi << (32u - sh))) : lo;
+  const uint32_t hi = q[k];
+  return __builtin_amdgcn_alignbyte(hi, lo, mis);  // ({hi, lo} >> 8 * mis), = lo when aligned
 }
 
 // Wave-cooperative copy of n bytes, any alignment on either side: byte stores up to dst's first
@@ -160,9 +165,9 @@ __global__ __launch_bounds__(256) void k_lz4_compress(const uint8_t* __restrict_
                                                       Lz4Chunk* __restrict__ chunks,
                                                       const uint32_t* __restrict__ nchunks,
                                                       uint8_t* __restrict__ scratch) {
-  extern __shared__ __attribute__((aligned(16))) unsigned long long ltab[];
+  extern __shared__ __attribute__((aligned(16))) uint32_t ltab[];
   const int wave = threadIdx.x / kLWave, lane = threadIdx.x % kLWave;
-  unsigned long long* tab = ltab + (size_t)wave * (1u << HB);
+  uint32_t* tab = ltab + (size_t)wave * (1u << HB);
   const uint32_t n = *nchunks;
   for (uint32_t b = blockIdx.x * 4u + wave; b < n; b += gridDim.x * 4u) {
     const Lz4Chunk C = chunks[b];
@@ -173,28 +178,30 @@ __global__ __launch_bounds__(256) void k_lz4_compress(const uint8_t* __restrict_
     uint32_t op = 0, anchor = 0, cur = 0;
     if (!raw) {
       // every entry starts as position 0 with position 0's true bytes (a verifiable candidate)
-      const unsigned long long e0 = ld32u(src);
+      const uint32_t e0 = ld32u(src) >> 16;
       for (uint32_t i = lane; i < (1u << HB); i += kLWave) tab[i] = e0;
       __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       const uint32_t last = len - 12;         // last position a match may start at
       const uint32_t mlimit = len - 5;        // matches end at or before this
       const uint32_t nwin = last / kLWave + 1;
       uint32_t w = 0;
+      // the 4 bytes at this lane's position of the NEXT window are loaded while the current
+      // window is parsed (the parse only ever moves forward)
+      uint32_t pf = ld32u(src + min((uint32_t)lane, last));
       while (w < nwin) {
         const uint32_t pos = w * kLWave + lane;
         const bool in = pos <= last;
-        const uint32_t seq = ld32u(src + (in ? pos : 0u));
+        const uint32_t seq = pf;
+        pf = ld32u(src + min(pos + kLWave, last));
         const uint32_t h = (seq * P1) >> (32 - HB);
-        const unsigned long long e = tab[h];
-        const uint32_t cpos = (uint32_t)(e >> 32), cseq = (uint32_t)e;
-        const bool m = in && cpos < pos && pos - cpos <= 65535u && cseq == seq;
+        const uint32_t e = tab[h];
+        const uint32_t cpos = e >> 16;
+        // 16-bit tag check here; the parse confirms all 4 bytes before taking a match
+        const bool m = in && cpos < pos && pos - cpos <= 65535u && (e & 0xFFFFu) == (seq >> 16);
         __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (in) atomicMax(&tab[h], ((unsigned long long)pos << 32) | seq);
+        if (in) atomicMax(&tab[h], (pos << 16) | (seq >> 16));
         __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        const uint64_t mm = __ballot(m);
+        uint64_t mm = __ballot(m);
         uint32_t nextw = w + 1;
         while (true) {
           const uint32_t rel = cur > w * kLWave ? cur - w * kLWave : 0u;
@@ -204,8 +211,8 @@ __global__ __launch_bounds__(256) void k_lz4_compress(const uint8_t* __restrict_
           const int j = __builtin_ctzll(mk);
           const uint32_t p = w * kLWave + j;
           const uint32_t c = (uint32_t)__shfl((int)cpos, j, kLWave);
-          // forward extension, 256 bytes per round
-          uint32_t ml = 4;
+          // forward comparison from the first byte, 256 bytes per round
+          uint32_t ml = 0;
           while (true) {
             const uint32_t lim = mlimit - (p + ml);  // bytes still allowed
             const uint32_t o = 4u * lane;
@@ -222,6 +229,10 @@ __global__ __launch_bounds__(256) void k_lz4_compress(const uint8_t* __restrict_
               break;
             }
             ml += 4u * kLWave;
+          }
+          if (ml < 4) {  // tag collision: no match here
+            mm &= ~(1ull << j);
+            continue;
           }
           const uint32_t LL = p - anchor;
           const uint32_t need = 1u + ext_bytes(LL) + LL + 2u + ext_bytes(ml - 4u);
@@ -243,6 +254,7 @@ __global__ __launch_bounds__(256) void k_lz4_compress(const uint8_t* __restrict_
           if (cur >= (w + 1) * kLWave) { nextw = cur / kLWave; break; }
         }
         if (raw) break;
+        if (nextw != w + 1) pf = ld32u(src + min(nextw * kLWave + lane, last));
         w = nextw;
       }
       if (!raw) {
@@ -441,10 +453,22 @@ hipError_t launch_lz4_compress(const uint8_t* d_data, const int64_t* d_index, ui
   hipLaunchKernelGGL(k_lz4_fill, dim3(rg), dim3(256), 0, s, d_index, (int)maps, (int)R, bs, map_base,
                      b0, chunks, nchunks);
   const uint32_t cg = (uint32_t)std::min<uint64_t>((w.chunk_bound + 3) / 4, 8192);
-  constexpr int HB = 11;
-  const size_t lds = 4 * (size_t(1) << HB) * 8;
-  hipLaunchKernelGGL((k_lz4_compress<HB>), dim3(cg), dim3(256), lds, s, d_data, chunks, nchunks,
-                     scratch);
+  static const int hb = [] {
+    const char* e = getenv("SUX_LZ4_HB");
+    return e ? atoi(e) : kLz4HashBits;
+  }();
+  const size_t lds = 4 * (size_t(1) << hb) * 4;
+  if (hb == 10)
+    hipLaunchKernelGGL((k_lz4_compress<10>), dim3(cg), dim3(256), lds, s, d_data, chunks, nchunks,
+                       scratch);
+  else if (hb == 12) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lz4_compress<12>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((k_lz4_compress<12>), dim3(cg), dim3(256), lds, s, d_data, chunks, nchunks,
+                       scratch);
+  } else
+    hipLaunchKernelGGL((k_lz4_compress<11>), dim3(cg), dim3(256), lds, s, d_data, chunks, nchunks,
+                       scratch);
   const uint32_t xg = (uint32_t)std::min<uint64_t>((w.chunk_bound + 63) / 64, 4096);
   hipLaunchKernelGGL(k_xxh32, dim3(xg), dim3(256), 0, s, d_data, chunks, nchunks);
   const uint32_t bg = (uint32_t)((w.chunk_bound + 255) / 256);

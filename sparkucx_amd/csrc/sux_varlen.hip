@@ -173,7 +173,6 @@ __global__ __launch_bounds__(WPG * kVWave) void k_vhist2(PartDev pd, VarGroup g,
     }
   }
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   uint64_t* dst = counts + ((uint64_t)map * R) * g.tiles_per_map + tile;
   for (int p = lane; p < R; p += kVWave) dst[(uint64_t)p * g.tiles_per_map] = hist[p];
 }
@@ -207,7 +206,6 @@ __global__ __launch_bounds__(WPG * kVWave) void k_vscatter2(VarGroup g, int R, i
   const uint64_t* pm = prefix + (uint64_t)map * R * g.tiles_per_map + tile;
   for (int p = lane; p < R; p += kVWave) cur[p] = bm[p] + pm[(uint64_t)p * g.tiles_per_map];
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   if (tb >= te) return;
   const uint64_t lt_mask = (1ull << lane) - 1ull;
   const uint64_t o0 = g.offs[0];
@@ -253,7 +251,6 @@ __global__ __launch_bounds__(WPG * kVWave) void k_vscatter2(VarGroup g, int R, i
     info[2 * lane] = a | ((uint64_t)dw << 44);
     info[2 * lane + 1] = d;
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     if (!tiny) {
     // first 128 bytes of every row, 8 lanes per row
     const uint32_t pc = (uint32_t)lane & 7u;
