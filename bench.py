@@ -199,6 +199,35 @@ def compress_leg(node, data, index, maps: int, R: int, dev, bs: int = 32768) -> 
             "ratio": round(int(ob.item()) / nb, 4)}
 
 
+def files_leg(node, out, index, maps: int, R: int, dev) -> dict:
+    """§8f item 3: Spark's on-disk files from device map outputs (sux_write_map_files: pinned
+    double-buffered D2H + temp file + commit; sux_read_file_blocks back for every map).  PCIe-
+    and page-cache-bound; written to /dev/shm (tmpfs) so the disk is not what is measured."""
+    import shutil
+    import tempfile
+    root = "/dev/shm" if os.path.isdir("/dev/shm") else None
+    d = tempfile.mkdtemp(prefix="sux_files_", dir=root)
+    try:
+        dps = [os.path.join(d, f"shuffle_0_{m}_0.data") for m in range(maps)]
+        ips = [os.path.join(d, f"shuffle_0_{m}_0.index") for m in range(maps)]
+        nb = sum(int(index[m * (R + 1) + R].item()) for m in range(maps))
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        node.write_map_files(out[:nb], index[:maps * (R + 1)], maps, R, dps, ips)
+        tw = time.perf_counter() - t0
+        buf = torch.empty(int(index[R].item()) + 16, dtype=torch.uint8, device=dev)
+        t0 = time.perf_counter()
+        for m in range(maps):
+            node.read_file_blocks(dps[m], ips[m], R, 0, R, out=buf)
+        torch.cuda.synchronize(dev)
+        tr = time.perf_counter() - t0
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    return {"maps": maps, "bytes": nb, "dir": root or "tmp", "write_s": round(tw, 3),
+            "write_GB/s": round(nb / tw / 1e9, 2), "read_s": round(tr, 3),
+            "read_GB/s": round(nb / tr / 1e9, 2)}
+
+
 def load_traffic(kernel: str) -> float | None:
     """Per-launch HBM bytes of `kernel` from the committed PMC summary (profiles/pmc_r01.json,
     written by profiles/collect_pmc.py; FETCH_SIZE x2 + WRITE_SIZE per the microarch guide)."""
@@ -241,6 +270,9 @@ def main():
                     help="N=1: also time sux_compress_map_outputs (lz4, 32 KiB chunks) over the "
                          "first map outputs (-1: one launch group; 0: skip); the varlen leg's "
                          "rows are compressed too")
+    ap.add_argument("--file-maps", type=int, default=-1,
+                    help="N=1: also time writing/reading Spark's data + index files for this "
+                         "many map outputs (sux_write_map_files; -1: 8; 0: skip)")
     ap.add_argument("--cpu-records", type=int, default=10_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-reps", type=int, default=3)
@@ -513,6 +545,9 @@ def main():
             # maps are consecutive in `out`: the first cm map outputs
             nb = sum(int(index[m * (R + 1) + R].item()) for m in range(cm))
             result["compress"] = compress_leg(node, out[:nb], index[:cm * (R + 1)], cm, R, dev)
+    if world == 1 and args.file_maps != 0:
+        fm = min(maps, args.file_maps if args.file_maps > 0 else 8)
+        result["files"] = files_leg(node, out, index, fm, R, dev)
     if world == 1 and args.varlen_rows != 0:
         vr = args.varlen_rows if args.varlen_rows > 0 else 32 << 20
         result["varlen"] = varlen_leg(node, vr, min(vr, 1 << 20), 200, dev,

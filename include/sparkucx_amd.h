@@ -36,6 +36,7 @@ extern "C" {
 #define SUX_ENOENT -5  /* unknown shuffle / map output / block (SparkException "Unknown block") */
 #define SUX_ESTATE -6  /* wrong lifecycle state (IllegalStateException "must be initialized") */
 #define SUX_ERANGE -7  /* size limit exceeded (SparkException "Metadata block size ...")      */
+#define SUX_EIO -8     /* file I/O error (IOException "fail to rename file ...")              */
 
 /* ---- partitioners ---------------------------------------------------- */
 /* Spark RangePartitioner over an unsigned lexicographic byte key (TeraSort's 10-byte key):
@@ -217,6 +218,27 @@ int sux_compress_map_outputs(sux_node* node, const void* d_data, uint64_t data_b
                              int64_t* d_out_index, uint8_t* d_out_index_be,
                              uint64_t* d_out_bytes, void* d_workspace, uint64_t workspace_bytes,
                              void* stream);
+
+/* ---- Spark's on-disk shuffle files (local-disk fallback / external shuffle service) ---------
+ * sux_index_file_commit: IndexShuffleBlockResolver.writeIndexFileAndCommit [ext] (the super call
+ * at compat/spark_3_0/UcxShuffleBlockResolver.scala:35), host-only: if index_path + data_path
+ * already hold a consistent committed pair (index = R+1 BE offsets from 0, data length = their
+ * sum) its lengths are returned (*reused = 1) and data_tmp is deleted; otherwise the index is
+ * written to a temp file and both files are replaced by rename (data_tmp may be NULL).
+ * sux_write_map_files: num_maps consecutive device map outputs + their native index tables ->
+ * one data + index file pair per map (pinned double-buffered D2H, temp file, commit as above);
+ * lengths_out (num_maps * R, optional) receives the committed lengths.
+ * sux_read_file_blocks: the bytes of partitions [start, end) of one map's files
+ * (IndexShuffleBlockResolver.getBlockData [ext] for a ShuffleBlockBatchId) into device memory. */
+int sux_index_file_commit(const char* index_path, const char* data_path, const char* data_tmp,
+                          const int64_t* lengths, int32_t num_partitions, int64_t* lengths_out,
+                          int32_t* reused);
+int sux_write_map_files(sux_node* node, const void* d_data, const int64_t* d_index,
+                        int32_t num_maps, int32_t num_partitions, const char* const* data_paths,
+                        const char* const* index_paths, int64_t* lengths_out, void* stream);
+int sux_read_file_blocks(sux_node* node, const char* data_path, const char* index_path,
+                         int32_t num_partitions, int32_t start_partition, int32_t end_partition,
+                         void* d_dst, uint64_t capacity, uint64_t* bytes, void* stream);
 
 /* ---- shuffle lifecycle: CommonUcxShuffleManager.registerShuffleCommon :39-56 ---------------- */
 typedef struct sux_handle_desc {

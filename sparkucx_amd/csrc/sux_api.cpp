@@ -7,7 +7,13 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <cerrno>
+#include <cstdio>
 #include <atomic>
 #include <cstring>
 #include <map>
@@ -571,6 +577,8 @@ int sux_partition_ids(sux_node* node, const sux_partitioner* part, const void* d
 }
 
 // ---- variable-length records (Spark SQL UnsafeRowSerializer framing) ---------------------------
+}  // extern "C"
+
 namespace {
 struct VGroup {
   sux::VarGroup g;
@@ -602,6 +610,8 @@ VGroup make_vgroup(const sux_partitioner* part, const void* data, const uint64_t
   return G;
 }
 }  // namespace
+
+extern "C" {
 
 int sux_partition_varlen_workspace_size(const sux_partitioner* part, uint64_t rpm, uint64_t n,
                                         uint64_t* bytes) {
@@ -638,6 +648,8 @@ int sux_partition_varlen(sux_node* node, const sux_partitioner* part, const void
 }
 
 // ---- compressed map outputs (spark.shuffle.compress with the lz4 codec) ------------------------
+}  // extern "C"
+
 namespace {
 void check_lz4_args(uint64_t data_bytes, int32_t maps, int32_t R, int32_t bs) {
   require(maps >= 1 && R >= 1 && R <= sux::kMaxPartitions, SUX_EINVAL,
@@ -649,6 +661,8 @@ void check_lz4_args(uint64_t data_bytes, int32_t maps, int32_t R, int32_t bs) {
           SUX_ERANGE, "too many compression chunks in one call");
 }
 }  // namespace
+
+extern "C" {
 
 int sux_compress_bound(uint64_t data_bytes, int32_t num_maps, int32_t R, int32_t block_size,
                        uint64_t* bytes) {
@@ -696,6 +710,258 @@ int sux_compress_map_outputs(sux_node* node, const void* d_data, uint64_t data_b
                                        d_out_bytes, static_cast<uint8_t*>(d_ws), w,
                                        node->stream(stream)),
               "compress launch");
+  });
+}
+
+// ---- local-disk shuffle files (Spark's on-disk format) -------------------------------------------
+// The reference keeps Spark's files (it mmaps the committed data file,
+// CommonUcxShuffleBlockResolver.scala:45-58) and commits through
+// IndexShuffleBlockResolver.writeIndexFileAndCommit [ext] (super call at
+// compat/spark_3_0/UcxShuffleBlockResolver.scala:35).  These entry points write / read that format
+// from device-resident map outputs, so Spark's local-disk fallback and external shuffle service
+// can serve the GPU's outputs.
+}  // extern "C"
+
+namespace {
+std::mutex g_commit_mu;  // the `synchronized` around Spark's check-and-commit
+
+int64_t be64(const uint8_t* p) {
+  uint64_t v = 0;
+  for (int k = 0; k < 8; ++k) v = (v << 8) | p[k];
+  return (int64_t)v;
+}
+
+bool file_size(const std::string& path, int64_t& size) {
+  struct stat st;
+  if (stat(path.c_str(), &st) != 0) return false;
+  size = (int64_t)st.st_size;
+  return true;
+}
+
+// IndexShuffleBlockResolver.checkIndexAndDataFile [ext]: the committed lengths, or false.
+// A missing file has length 0 (java.io.File.length()).
+bool check_index_and_data(const std::string& index, const std::string& data, int R,
+                          std::vector<int64_t>& lengths) {
+  int64_t isz = 0, dsz = 0;
+  if (!file_size(index, isz)) isz = 0;
+  if (isz != (int64_t)(R + 1) * 8) return false;
+  std::vector<uint8_t> buf((size_t)(R + 1) * 8);
+  FILE* f = fopen(index.c_str(), "rb");
+  if (!f) return false;
+  const size_t got = fread(buf.data(), 1, buf.size(), f);
+  fclose(f);
+  if (got != buf.size() || be64(buf.data()) != 0) return false;
+  lengths.assign(R, 0);
+  int64_t sum = 0;
+  for (int i = 0; i < R; ++i) {
+    lengths[i] = be64(buf.data() + 8 * (i + 1)) - be64(buf.data() + 8 * i);
+    sum += lengths[i];
+  }
+  if (!file_size(data, dsz)) dsz = 0;
+  return dsz == sum;
+}
+
+void write_all(int fd, const uint8_t* p, size_t n, const std::string& what) {
+  while (n) {
+    const ssize_t w = ::write(fd, p, n);
+    if (w < 0 && errno == EINTR) continue;
+    require(w > 0, SUX_EIO, "write " + what + ": " + std::strerror(errno));
+    p += w;
+    n -= (size_t)w;
+  }
+}
+
+std::string tmp_name(const std::string& path) {
+  static std::atomic<uint64_t> ctr{0};
+  return path + "." + std::to_string((long)getpid()) + "." + std::to_string(ctr++) + ".tmp";
+}
+
+// writeIndexFileAndCommit's body: keep an already committed, consistent pair (another attempt
+// of the same map won); otherwise write the index, replace both files by rename.
+bool commit_pair(const std::string& index, const std::string& data, const std::string& data_tmp,
+                 const int64_t* lengths, int R, int64_t* lengths_out) {
+  const std::string itmp = tmp_name(index);
+  std::lock_guard<std::mutex> lk(g_commit_mu);
+  std::vector<int64_t> existing;
+  bool reused = false;
+  if (check_index_and_data(index, data, R, existing)) {
+    if (lengths_out) std::memcpy(lengths_out, existing.data(), (size_t)R * 8);
+    if (!data_tmp.empty()) ::unlink(data_tmp.c_str());
+    reused = true;
+  } else {
+    std::vector<uint8_t> buf((size_t)(R + 1) * 8);
+    int64_t off = 0;
+    for (int i = 0; i <= R; ++i) {
+      store_be64(buf.data() + 8 * i, (uint64_t)off);
+      if (i < R) off += lengths[i];
+    }
+    const int fd = ::open(itmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    require(fd >= 0, SUX_EIO, "open " + itmp + ": " + std::strerror(errno));
+    try {
+      write_all(fd, buf.data(), buf.size(), itmp);
+    } catch (...) {
+      ::close(fd);
+      ::unlink(itmp.c_str());
+      throw;
+    }
+    ::close(fd);
+    ::unlink(index.c_str());
+    ::unlink(data.c_str());
+    if (::rename(itmp.c_str(), index.c_str()) != 0) {
+      ::unlink(itmp.c_str());
+      raise(SUX_EIO, "fail to rename file " + itmp + " to " + index);
+    }
+    if (!data_tmp.empty() && ::access(data_tmp.c_str(), F_OK) == 0 &&
+        ::rename(data_tmp.c_str(), data.c_str()) != 0)
+      raise(SUX_EIO, "fail to rename file " + data_tmp + " to " + data);
+    if (lengths_out) std::memcpy(lengths_out, lengths, (size_t)R * 8);
+  }
+  ::unlink(itmp.c_str());  // the finally block
+  return reused;
+}
+
+// Two pinned staging buffers: the D2H copy of chunk k+1 runs while chunk k is written.
+struct Staging {
+  static constexpr size_t kChunk = 32u << 20;
+  uint8_t* h[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  Staging() {
+    for (int i = 0; i < 2; ++i) {
+      hip_check(hipHostMalloc(reinterpret_cast<void**>(&h[i]), kChunk, hipHostMallocDefault),
+                "hipHostMalloc(staging)");
+      hip_check(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming), "hipEventCreate");
+    }
+  }
+  ~Staging() {
+    for (int i = 0; i < 2; ++i) {
+      if (h[i]) (void)hipHostFree(h[i]);
+      if (ev[i]) (void)hipEventDestroy(ev[i]);
+    }
+  }
+};
+}  // namespace
+
+extern "C" {
+
+int sux_index_file_commit(const char* index_path, const char* data_path, const char* data_tmp,
+                          const int64_t* lengths, int32_t R, int64_t* lengths_out,
+                          int32_t* reused) {
+  return guard([&] {
+    require(index_path && data_path && (lengths || R == 0), SUX_EINVAL, "NULL argument");
+    require(R >= 0, SUX_EINVAL, "num_partitions < 0");
+    const bool r = commit_pair(index_path, data_path, data_tmp ? data_tmp : "", lengths, R,
+                               lengths_out);
+    if (reused) *reused = r ? 1 : 0;
+  });
+}
+
+int sux_write_map_files(sux_node* node, const void* d_data, const int64_t* d_index,
+                        int32_t num_maps, int32_t R, const char* const* data_paths,
+                        const char* const* index_paths, int64_t* lengths_out, void* stream) {
+  return guard([&] {
+    require(node && d_index && data_paths && index_paths, SUX_EINVAL, "NULL argument");
+    require(num_maps >= 1 && R >= 1, SUX_EINVAL, "num_maps and num_partitions must be >= 1");
+    node->bind();
+    hipStream_t s = node->stream(stream);
+    std::vector<int64_t> ix((size_t)num_maps * (R + 1));
+    hip_check(hipMemcpyAsync(ix.data(), d_index, ix.size() * 8, hipMemcpyDeviceToHost, s),
+              "hipMemcpy(index)");
+    hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    Staging st;
+    uint64_t base = 0;
+    for (int32_t m = 0; m < num_maps; ++m) {
+      const int64_t* im = ix.data() + (size_t)m * (R + 1);
+      require(im[0] == 0, SUX_EINVAL, "index table of map " + std::to_string(m) + " does not start at 0");
+      std::vector<int64_t> lengths(R);
+      for (int p = 0; p < R; ++p) lengths[p] = im[p + 1] - im[p];
+      const uint64_t n = (uint64_t)im[R];
+      require(d_data || n == 0, SUX_EINVAL, "data pointer is NULL");
+      const std::string data = data_paths[m], index = index_paths[m], tmp = tmp_name(data);
+      const int fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+      require(fd >= 0, SUX_EIO, "open " + tmp + ": " + std::strerror(errno));
+      try {
+        const uint8_t* src = static_cast<const uint8_t*>(d_data) + base;
+        const uint64_t nch = (n + Staging::kChunk - 1) / Staging::kChunk;
+        auto issue = [&](uint64_t k) {
+          const uint64_t a = k * Staging::kChunk, len = std::min<uint64_t>(Staging::kChunk, n - a);
+          hip_check(hipMemcpyAsync(st.h[k & 1], src + a, len, hipMemcpyDeviceToHost, s),
+                    "hipMemcpy(data)");
+          hip_check(hipEventRecord(st.ev[k & 1], s), "hipEventRecord");
+        };
+        if (nch) issue(0);
+        for (uint64_t k = 0; k < nch; ++k) {
+          hip_check(hipEventSynchronize(st.ev[k & 1]), "hipEventSynchronize");
+          if (k + 1 < nch) issue(k + 1);
+          const uint64_t a = k * Staging::kChunk, len = std::min<uint64_t>(Staging::kChunk, n - a);
+          write_all(fd, st.h[k & 1], len, tmp);
+        }
+      } catch (...) {
+        ::close(fd);
+        ::unlink(tmp.c_str());
+        throw;
+      }
+      require(::close(fd) == 0, SUX_EIO, "close " + tmp);
+      commit_pair(index, data, tmp, lengths.data(), R,
+                  lengths_out ? lengths_out + (size_t)m * R : nullptr);
+      base += n;
+    }
+  });
+}
+
+int sux_read_file_blocks(sux_node* node, const char* data_path, const char* index_path, int32_t R,
+                         int32_t start_partition, int32_t end_partition, void* d_dst,
+                         uint64_t capacity, uint64_t* bytes, void* stream) {
+  return guard([&] {
+    require(node && data_path && index_path && bytes, SUX_EINVAL, "NULL argument");
+    require(0 <= start_partition && start_partition <= end_partition && end_partition <= R,
+            SUX_EINVAL, "partition range must satisfy 0 <= start <= end <= R");
+    std::vector<int64_t> lengths;
+    {
+      int64_t isz = 0;
+      require(file_size(index_path, isz) && isz == (int64_t)(R + 1) * 8, SUX_EIO,
+              std::string("index file ") + index_path + " is not " + std::to_string(R + 1) +
+                  " offsets");
+    }
+    std::vector<uint8_t> ib((size_t)(R + 1) * 8);
+    FILE* f = fopen(index_path, "rb");
+    require(f != nullptr, SUX_EIO, std::string("open ") + index_path);
+    const size_t got = fread(ib.data(), 1, ib.size(), f);
+    fclose(f);
+    require(got == ib.size(), SUX_EIO, std::string("read ") + index_path);
+    const int64_t a = be64(ib.data() + 8 * start_partition), e = be64(ib.data() + 8 * end_partition);
+    require(0 <= a && a <= e, SUX_EIO, "index offsets decrease");
+    const uint64_t n = (uint64_t)(e - a);
+    require(n <= capacity && (d_dst || n == 0), SUX_ERANGE,
+            "blocks need " + std::to_string(n) + " bytes, capacity " + std::to_string(capacity));
+    *bytes = n;
+    if (n == 0) return;
+    node->bind();
+    hipStream_t s = node->stream(stream);
+    const int fd = ::open(data_path, O_RDONLY);
+    require(fd >= 0, SUX_EIO, std::string("open ") + data_path + ": " + std::strerror(errno));
+    Staging st;
+    try {
+      const uint64_t nch = (n + Staging::kChunk - 1) / Staging::kChunk;
+      for (uint64_t k = 0; k < nch; ++k) {
+        const uint64_t o = k * Staging::kChunk, len = std::min<uint64_t>(Staging::kChunk, n - o);
+        if (k >= 2) hip_check(hipEventSynchronize(st.ev[k & 1]), "hipEventSynchronize");
+        uint64_t done = 0;
+        while (done < len) {
+          const ssize_t r = ::pread(fd, st.h[k & 1] + done, len - done, (off_t)(a + o + done));
+          if (r < 0 && errno == EINTR) continue;
+          require(r > 0, SUX_EIO, std::string("read ") + data_path + ": short file");
+          done += (uint64_t)r;
+        }
+        hip_check(hipMemcpyAsync(static_cast<uint8_t*>(d_dst) + o, st.h[k & 1], len,
+                                 hipMemcpyHostToDevice, s), "hipMemcpy(blocks)");
+        hip_check(hipEventRecord(st.ev[k & 1], s), "hipEventRecord");
+      }
+      hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    } catch (...) {
+      ::close(fd);
+      throw;
+    }
+    ::close(fd);
   });
 }
 

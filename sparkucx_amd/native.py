@@ -74,6 +74,10 @@ _SIGS = {
     "sux_partition_ids": (C.c_int, [P, P, P, U32, U64, P, P]),
     "sux_partition_varlen_workspace_size": (C.c_int, [P, U64, U64, C.POINTER(U64)]),
     "sux_partition_varlen": (C.c_int, [P, P, P, P, U64, U64, P, P, P, P, P, P, U64, P]),
+    "sux_index_file_commit": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, P, I32, P, P]),
+    "sux_write_map_files": (C.c_int, [P, P, P, I32, I32, P, P, P, P]),
+    "sux_read_file_blocks": (C.c_int, [P, C.c_char_p, C.c_char_p, I32, I32, I32, P, U64,
+                                       C.POINTER(U64), P]),
     "sux_compress_bound": (C.c_int, [U64, I32, I32, I32, C.POINTER(U64)]),
     "sux_compress_workspace_size": (C.c_int, [U64, I32, I32, I32, C.POINTER(U64)]),
     "sux_compress_map_outputs": (C.c_int, [P, P, U64, P, I32, I32, I32, P, U64, P, P, P, P, U64,

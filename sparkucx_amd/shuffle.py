@@ -6,6 +6,7 @@ stream; every byte of the shuffle path is moved by the library's gfx950 kernels.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 import torch
@@ -198,6 +199,33 @@ class Node:
                                               _stream(stream)),
                 "sux_partition_varlen")
         return out, index, index_be
+
+    # ---- Spark's on-disk files ---------------------------------------------------------------
+    def write_map_files(self, data: torch.Tensor, index: torch.Tensor, num_maps: int, R: int,
+                        data_paths: list[str], index_paths: list[str], stream=None) -> np.ndarray:
+        """Consecutive device map outputs -> one committed data + index file pair per map
+        (IndexShuffleBlockResolver.writeIndexFileAndCommit semantics).  Returns the committed
+        lengths, int64[num_maps, R] (an already committed pair's lengths win)."""
+        dp = (C.c_char_p * num_maps)(*[p.encode() for p in data_paths])
+        ip = (C.c_char_p * num_maps)(*[p.encode() for p in index_paths])
+        out = np.zeros(num_maps * R, np.int64)
+        N.check(self.lib.sux_write_map_files(self.h, _ptr(data), _ptr(index), num_maps, R, dp, ip,
+                                             out.ctypes.data, _stream(stream)),
+                "sux_write_map_files")
+        return out.reshape(num_maps, R)
+
+    def read_file_blocks(self, data_path: str, index_path: str, R: int, start: int, end: int,
+                         out: torch.Tensor | None = None, capacity: int | None = None,
+                         stream=None) -> torch.Tensor:
+        """Partitions [start, end) of one map's files into device memory."""
+        if out is None:
+            cap = capacity if capacity is not None else os.path.getsize(data_path)
+            out = torch.empty(max(1, cap), dtype=torch.uint8, device=self.dev)
+        n = C.c_uint64()
+        N.check(self.lib.sux_read_file_blocks(self.h, data_path.encode(), index_path.encode(), R,
+                                              start, end, _ptr(out), out.numel(), C.byref(n),
+                                              _stream(stream)), "sux_read_file_blocks")
+        return out[:n.value]
 
     def compress_bound(self, data_bytes: int, num_maps: int, R: int, block_size: int = 32768) -> int:
         b = C.c_uint64()
@@ -412,3 +440,18 @@ class FetchedBuffer:
         for _ in range(count):
             N.check(self.node.lib.sux_buffer_release(self.h), "sux_buffer_release")
         self.refs -= count
+
+
+def index_file_commit(index_path: str, data_path: str, data_tmp: str | None,
+                      lengths) -> tuple[np.ndarray, bool]:
+    """IndexShuffleBlockResolver.writeIndexFileAndCommit (host only, no device).  Returns
+    (committed lengths, reused an existing consistent pair)."""
+    ln = np.ascontiguousarray(lengths, np.int64)
+    out = np.zeros(ln.size, np.int64)
+    reused = C.c_int32()
+    N.check(N.load().sux_index_file_commit(index_path.encode(), data_path.encode(),
+                                           None if data_tmp is None else data_tmp.encode(),
+                                           ln.ctypes.data if ln.size else None, ln.size,
+                                           out.ctypes.data if ln.size else None,
+                                           C.byref(reused)), "sux_index_file_commit")
+    return out, bool(reused.value)
