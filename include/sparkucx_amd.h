@@ -323,6 +323,15 @@ int sux_sort_workspace_size(uint64_t n, uint32_t record_size, uint64_t* bytes);
 int sux_sort_records(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
                      uint32_t record_size, int32_t key_offset, int32_t key_len, void* d_out,
                      void* d_ws, uint64_t ws_bytes, void* stream);
+/* Segmented: the records are num_segments consecutive runs (a reducer's partitions, e.g. the
+ * canonical per-partition concatenations from sux_fetch_blocks), run k = records
+ * [d_segment_offsets[k], d_segment_offsets[k+1]) (num_segments + 1 device int64, from 0 to n);
+ * every run is sorted in place of itself, all in one call.  Key bytes + segment-id bytes (1 for
+ * <= 256 segments, 2 for <= 65536, else 3) must fit 12.  Same workspace as sux_sort_records. */
+int sux_sort_segments(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
+                      uint32_t record_size, int32_t key_offset, int32_t key_len,
+                      const int64_t* d_segment_offsets, int32_t num_segments, void* d_out,
+                      void* d_ws, uint64_t ws_bytes, void* stream);
 
 /* ---- CU-partitioned streams (exchange/compute overlap) ---------------------------------- *
  * A non-blocking HIP stream (returned as void*) whose kernels run on `num_cus` of the device's

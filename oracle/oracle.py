@@ -268,6 +268,15 @@ def sort_records(recs: np.ndarray, rec_size: int, kind: int, key_offset: int,
     return rows[order].reshape(-1)
 
 
+def sort_segments(recs: np.ndarray, rec_size: int, kind: int, key_offset: int, key_len: int,
+                  seg_offsets) -> np.ndarray:
+    """sort_records applied to every run [seg_offsets[k], seg_offsets[k+1]) of records."""
+    rows = np.ascontiguousarray(recs).reshape(-1, rec_size)
+    parts = [sort_records(rows[a:b].reshape(-1), rec_size, kind, key_offset, key_len)
+             for a, b in zip(seg_offsets[:-1], seg_offsets[1:])]
+    return np.concatenate(parts) if parts else rows.reshape(-1).copy()
+
+
 # ---- variable-length rows (SURVEY.md §8f item 3) -----------------------------------------------
 def gen_unsafe_rows(seed: int, n: int, max_payload_words: int = 12,
                     key_mod: int | None = None) -> tuple[np.ndarray, np.ndarray]:

@@ -1559,50 +1559,78 @@ int sux_sort_workspace_size(uint64_t n, uint32_t record_size, uint64_t* bytes) {
   });
 }
 
+namespace {
+void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
+               uint32_t record_size, int32_t key_offset, int32_t key_len, const int64_t* d_seg,
+               int32_t nseg, void* d_out, void* d_ws, uint64_t ws_bytes, void* stream) {
+  require(node, SUX_EINVAL, "NULL node");
+  int bits = sort_key_bits(key_kind, key_len);
+  int sbytes = 0;
+  if (d_seg) {
+    require(nseg >= 1, SUX_EINVAL, "sort: num_segments must be >= 1");
+    sbytes = nseg <= 1 ? 0 : nseg <= 256 ? 1 : nseg <= 65536 ? 2 : 3;
+    require(bits / 8 + sbytes <= 12, SUX_EINVAL,
+            "sort: key bytes + segment-id bytes (" + std::to_string(sbytes) + ") exceed 12");
+    bits += 8 * sbytes;
+  }
+  require(key_offset >= 0 && (uint64_t)key_offset + key_len <= record_size, SUX_EINVAL,
+          "sort: the key does not fit the record");
+  SortPlan P;
+  sort_plan(n, record_size, P);
+  if (n == 0) return;
+  require(d_in && d_out && d_ws, SUX_EINVAL, "NULL buffer");
+  require(ws_bytes >= P.total, SUX_EINVAL,
+          "sort workspace too small: need " + std::to_string(P.total) + " bytes");
+  require(((uintptr_t)d_in & 3) == 0 && ((uintptr_t)d_out & 3) == 0 &&
+              ((uintptr_t)d_ws & 255) == 0,
+          SUX_EINVAL, "records (4 B) and workspace (256 B) must be aligned");
+  require(d_in != d_out, SUX_EINVAL, "sort is out of place");
+  node->bind();
+  hipStream_t s = node->stream(stream);
+  uint8_t* ws = static_cast<uint8_t*>(d_ws);
+  uint8_t* pa = ws;
+  uint8_t* pb = ws + P.pairs_bytes;
+  int64_t* index = reinterpret_cast<int64_t*>(ws + P.index_off);
+  hip_check(sux::launch_sort_pairs(static_cast<const uint8_t*>(d_in), n, record_size, key_kind,
+                                   key_offset, key_len, d_seg, nseg, sbytes, pa, s),
+            "sort pairs");
+  sux::PartDev pd{};
+  pd.kind = sux::kPartRadix;
+  pd.R = 1 << sux::kRadixBits;
+  pd.key_offset = 0;
+  pd.key_len = 16;
+  pd.ascending = 1;
+  sux::LayoutDesc lay{1, 16};
+  // the key occupies bits [128 - bits, 128) of the big-endian pair; least significant digit first
+  for (int sh = 128 - bits; sh < 128; sh += sux::kRadixBits) {
+    pd.seed = sh;
+    P.g.recs = pa;
+    hip_check(sux::launch_partition_group(pd, P.g, lay, pb, index, nullptr, nullptr,
+                                          ws + P.part_off, P.ws, nullptr, &node->timer, s),
+              "sort digit pass");
+    std::swap(pa, pb);
+  }
+  hip_check(sux::launch_gather_records(d_in, pa, n, record_size, d_out, s), "sort gather");
+}
+}  // namespace
+
 int sux_sort_records(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
                      uint32_t record_size, int32_t key_offset, int32_t key_len, void* d_out,
                      void* d_ws, uint64_t ws_bytes, void* stream) {
   return guard([&] {
-    require(node, SUX_EINVAL, "NULL node");
-    const int bits = sort_key_bits(key_kind, key_len);
-    require(key_offset >= 0 && (uint64_t)key_offset + key_len <= record_size, SUX_EINVAL,
-            "sort: the key does not fit the record");
-    SortPlan P;
-    sort_plan(n, record_size, P);
-    if (n == 0) return;
-    require(d_in && d_out && d_ws, SUX_EINVAL, "NULL buffer");
-    require(ws_bytes >= P.total, SUX_EINVAL,
-            "sort workspace too small: need " + std::to_string(P.total) + " bytes");
-    require(((uintptr_t)d_in & 3) == 0 && ((uintptr_t)d_out & 3) == 0 &&
-                ((uintptr_t)d_ws & 255) == 0,
-            SUX_EINVAL, "records (4 B) and workspace (256 B) must be aligned");
-    require(d_in != d_out, SUX_EINVAL, "sort is out of place");
-    node->bind();
-    hipStream_t s = node->stream(stream);
-    uint8_t* ws = static_cast<uint8_t*>(d_ws);
-    uint8_t* pa = ws;
-    uint8_t* pb = ws + P.pairs_bytes;
-    int64_t* index = reinterpret_cast<int64_t*>(ws + P.index_off);
-    hip_check(sux::launch_sort_pairs(static_cast<const uint8_t*>(d_in), n, record_size, key_kind,
-                                     key_offset, key_len, pa, s),
-              "sort pairs");
-    sux::PartDev pd{};
-    pd.kind = sux::kPartRadix;
-    pd.R = 1 << sux::kRadixBits;
-    pd.key_offset = 0;
-    pd.key_len = 16;
-    pd.ascending = 1;
-    sux::LayoutDesc lay{1, 16};
-    // the key occupies bits [128 - bits, 128) of the big-endian pair; least significant digit first
-    for (int sh = 128 - bits; sh < 128; sh += sux::kRadixBits) {
-      pd.seed = sh;
-      P.g.recs = pa;
-      hip_check(sux::launch_partition_group(pd, P.g, lay, pb, index, nullptr, nullptr,
-                                            ws + P.part_off, P.ws, nullptr, &node->timer, s),
-                "sort digit pass");
-      std::swap(pa, pb);
-    }
-    hip_check(sux::launch_gather_records(d_in, pa, n, record_size, d_out, s), "sort gather");
+    sort_impl(node, key_kind, d_in, n, record_size, key_offset, key_len, nullptr, 0, d_out, d_ws,
+              ws_bytes, stream);
+  });
+}
+
+int sux_sort_segments(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
+                      uint32_t record_size, int32_t key_offset, int32_t key_len,
+                      const int64_t* d_segment_offsets, int32_t num_segments, void* d_out,
+                      void* d_ws, uint64_t ws_bytes, void* stream) {
+  return guard([&] {
+    require(d_segment_offsets, SUX_EINVAL, "NULL segment offsets");
+    sort_impl(node, key_kind, d_in, n, record_size, key_offset, key_len, d_segment_offsets,
+              num_segments, d_out, d_ws, ws_bytes, stream);
   });
 }
 

@@ -141,7 +141,8 @@ hipError_t launch_pull(int32_t W, int32_t me, const uint64_t* srcs, const int64_
 constexpr int kPartRadix = 7;  // internal partitioner: 12-bit digit (shift in PartDev::seed)
 constexpr int kRadixBits = 12;
 hipError_t launch_sort_pairs(const uint8_t* in, uint64_t n, uint32_t rs, int kind, int key_offset,
-                             int key_len, void* pairs, hipStream_t s);
+                             int key_len, const int64_t* seg, int nseg, int sbytes, void* pairs,
+                             hipStream_t s);
 hipError_t launch_gather_records(const void* in, const void* pairs, uint64_t n, uint32_t rs,
                                  void* out, hipStream_t s);
 

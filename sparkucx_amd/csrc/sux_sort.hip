@@ -10,6 +10,8 @@
 //                   the internal radix partitioner (kind 7, R = 4096: k_hist16 + k_scatter16)
 //   k_gather_records out record j = in record pairs[j].index (coalesced dword writes)
 // Equal keys keep their input order (every pass is stable and the index is never a digit).
+// Segmented (sux_sort_segments): the record's segment id, big-endian, sits above the key bytes,
+// so one sort orders every segment (a reducer's partitions) in place.
 #include <hip/hip_runtime.h>
 
 #include "sux_internal.h"
@@ -20,7 +22,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(256) void k_sort_pairs(const uint8_t* __restrict__ in, uint64_t n,
                                                     uint32_t rs, int kind, int key_offset,
-                                                    int key_len, u32x4* __restrict__ pairs) {
+                                                    int key_len, const int64_t* __restrict__ seg,
+                                                    int nseg, int sbytes,
+                                                    u32x4* __restrict__ pairs) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const uint8_t* r = in + i * rs + key_offset;
@@ -37,6 +41,15 @@ __global__ __launch_bounds__(256) void k_sort_pairs(const uint8_t* __restrict__ 
     const int w = kind == 2 ? 8 : 4;
     for (int k = 0; k < w; ++k) kb[k] = r[w - 1 - k];
     kb[0] ^= 0x80u;
+  }
+  if (sbytes) {  // segmented: the segment id (big-endian) above the key
+    int lo = 0, hi = nseg;  // last segment whose start is <= i
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if ((uint64_t)seg[mid] <= i) lo = mid; else hi = mid;
+    }
+    for (int k = 11; k >= sbytes; --k) kb[k] = kb[k - sbytes];
+    for (int k = 0; k < sbytes; ++k) kb[k] = (uint8_t)((uint32_t)lo >> (8 * (sbytes - 1 - k)));
   }
   u32x4 p;
   p[0] = (uint32_t)kb[0] | ((uint32_t)kb[1] << 8) | ((uint32_t)kb[2] << 16) | ((uint32_t)kb[3] << 24);
@@ -60,10 +73,11 @@ __global__ __launch_bounds__(256) void k_gather_records(const uint32_t* __restri
 }
 
 hipError_t launch_sort_pairs(const uint8_t* in, uint64_t n, uint32_t rs, int kind, int key_offset,
-                             int key_len, void* pairs, hipStream_t s) {
+                             int key_len, const int64_t* seg, int nseg, int sbytes, void* pairs,
+                             hipStream_t s) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_sort_pairs, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, in, n, rs,
-                     kind, key_offset, key_len, static_cast<u32x4*>(pairs));
+                     kind, key_offset, key_len, seg, nseg, sbytes, static_cast<u32x4*>(pairs));
   return hipGetLastError();
 }
 

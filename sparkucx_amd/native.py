@@ -105,6 +105,7 @@ _SIGS = {
     "sux_stream_destroy": (C.c_int, [P, P]),
     "sux_sort_workspace_size": (C.c_int, [U64, U32, C.POINTER(U64)]),
     "sux_sort_records": (C.c_int, [P, I32, P, U64, U32, I32, I32, P, P, U64, P]),
+    "sux_sort_segments": (C.c_int, [P, I32, P, U64, U32, I32, I32, P, I32, P, P, U64, P]),
 }
 
 _lib = None

@@ -385,6 +385,25 @@ class Node:
                                           workspace.numel(), _stream(stream)), "sux_sort_records")
         return out
 
+    def sort_segments(self, records: torch.Tensor, record_size: int, key_kind: int,
+                      key_offset: int, key_len: int, segment_offsets: torch.Tensor,
+                      num_records: int | None = None, out: torch.Tensor | None = None,
+                      workspace: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+        """Sort every run [segment_offsets[k], segment_offsets[k+1]) of records by key, stably,
+        in one call (a reducer's partitions).  segment_offsets: device int64, num_segments + 1."""
+        n = records.numel() // record_size if num_records is None else num_records
+        if out is None:
+            out = torch.empty(max(1, n * record_size), dtype=torch.uint8, device=self.dev)
+        if workspace is None:
+            workspace = torch.empty(max(1, self.sort_workspace_size(n, record_size)),
+                                    dtype=torch.uint8, device=self.dev)
+        N.check(self.lib.sux_sort_segments(self.h, key_kind, _ptr(records), n, record_size,
+                                           key_offset, key_len, _ptr(segment_offsets),
+                                           segment_offsets.numel() - 1, _ptr(out),
+                                           _ptr(workspace), workspace.numel(), _stream(stream)),
+                "sux_sort_segments")
+        return out
+
     def sort_workspace_size(self, n: int, record_size: int) -> int:
         b = C.c_uint64()
         N.check(self.lib.sux_sort_workspace_size(n, record_size, C.byref(b)),

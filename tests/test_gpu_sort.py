@@ -114,3 +114,30 @@ def test_large_sort_properties(gpu_node):
     assert (lo[1:][eq] >= lo[:-1][eq]).all()
     # multiset: per-column byte sums agree (the generator's row id sits in bytes 10..17)
     assert torch.equal(a.sum(0, dtype=torch.int64), b.sum(0, dtype=torch.int64))
+
+
+@pytest.mark.parametrize("nseg", [1, 2, 25, 300, 70_000])
+def test_segmented_sort(gpu_node, nseg):
+    """Every run sorted in place of itself (a reducer's owned partitions in one call); empty
+    runs, 1-record runs and segment-id widths of 0..3 bytes."""
+    n = 200_000
+    rng = np.random.default_rng(nseg)
+    cuts = np.sort(rng.integers(0, n + 1, nseg - 1))
+    seg = np.concatenate([[0], cuts, [n]]).astype(np.int64)
+    recs = O.gen_terasort(24, 0, n)
+    key_len = 10 if nseg <= 65536 else 9
+    segs = torch.from_numpy(seg).cuda()
+    out = gpu_node.sort_segments(to_dev(recs), 100, N.SORT_BYTES, 0, key_len, segs)
+    torch.cuda.synchronize()
+    exp = O.sort_segments(recs, 100, O.SORT_BYTES, 0, key_len, seg)
+    assert out.cpu().numpy()[: n * 100].tobytes() == exp.tobytes()
+
+
+def test_segmented_sort_long_keys(gpu_node):
+    recs = O.gen_small(25, 0, 100_000)
+    seg = np.array([0, 10, 10, 50_000, 99_999, 100_000], np.int64)
+    out = gpu_node.sort_segments(to_dev(recs), 16, N.SORT_LONG, 0, 8,
+                                 torch.from_numpy(seg).cuda())
+    torch.cuda.synchronize()
+    exp = O.sort_segments(recs, 16, O.SORT_LONG, 0, 8, seg)
+    assert out.cpu().numpy()[: recs.size].tobytes() == exp.tobytes()
