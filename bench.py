@@ -255,6 +255,10 @@ def main():
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="test mode: every rank on cuda:0, gloo process group, ipc transport "
                          "(exercises the N>1 pipeline on a 1-GPU box; not a benchmark)")
+    ap.add_argument("--rccl-at-one", action="store_true",
+                    help="test mode at N=1: run the N>1 pipeline (peer-major partition, "
+                         "overlapped ncclAllGather + ncclAllToAllv) on a one-rank RCCL "
+                         "communicator, so the RCCL calls run on a 1-GPU box")
     ap.add_argument("--streams", type=int, default=1,
                     help="N=1: launch groups dealt round-robin to this many HIP streams")
     ap.add_argument("--reserve-cus", type=int, default=-1,
@@ -296,6 +300,10 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=dev)
     ctl = torch.device("cpu") if rehearse else dev  # device of the small control collectives
+    # the N>1 pipeline (peer-major map outputs + overlapped exchange); at N=1 only on request
+    pipelined = world > 1 or args.rccl_at_one
+    if args.rccl_at_one:
+        args.transport = "rccl"
 
     rs, R, gen, kind, key_len, n1, nN = WORKLOADS[args.workload]
     n = args.records or (n1 if world == 1 else nN)
@@ -306,7 +314,9 @@ def main():
 
     # ---- node + communicator bootstrap (unique id carried by torch.distributed) ----------
     comm_id = None
-    if world > 1 and args.transport == "rccl":
+    if world == 1 and args.rccl_at_one:
+        comm_id = N.unique_id()
+    elif world > 1 and args.transport == "rccl":
         t = torch.zeros(128, dtype=torch.uint8, device=dev)
         if rank == 0:
             t.copy_(torch.frombuffer(bytearray(N.unique_id()), dtype=torch.uint8))
@@ -331,7 +341,7 @@ def main():
     index = torch.empty(maps * (R + 1), dtype=torch.int64, device=dev)
     ws_bytes = node.workspace_size(part, rs, rpm, min(n, group_recs))
     comp = torch.cuda.current_stream(dev)
-    reserve = args.reserve_cus if args.reserve_cus >= 0 else (32 if world > 1 else 0)
+    reserve = args.reserve_cus if args.reserve_cus >= 0 else (32 if pipelined else 0)
     if reserve > 0:
         # map-side kernels on a CU-masked stream that leaves `reserve` CUs (spread over the 8
         # XCDs) to the exchange: the partition kernels fill every CU they get (LDS-bound), so
@@ -339,7 +349,7 @@ def main():
         comp = torch.cuda.ExternalStream(node.cu_stream(reserve, complement=True), device=dev)
         comp.wait_stream(torch.cuda.current_stream(dev))  # the generated input
 
-    if world == 1:
+    if not pipelined:
         out = torch.empty(n * rs, dtype=torch.uint8, device=dev)
         index_be = torch.empty(maps * (R + 1) * 8, dtype=torch.uint8, device=dev)
         ns = max(1, args.streams)
@@ -454,7 +464,7 @@ def main():
     barrier()
     node.kernel_times()  # drop warm-up timings
     node.set_kernel_timing(True)
-    if world > 1:
+    if pipelined:
         xfer_ev.clear()
     barrier()
     t0 = time.perf_counter()
@@ -494,7 +504,7 @@ def main():
                                f"R={R}, map batches of {rpm} records, {gm} maps per launch group"
                                + (f" on {args.streams} streams" if world == 1 and args.streams > 1 else "")
                                + (f", map side on {256 - reserve} CUs" if reserve > 0 else "")
-                               + (", zero-copy local block resolve" if world == 1 else
+                               + (", zero-copy local block resolve" if not pipelined else
                                   ", partition-aligned ncclAllToAllv exchange"
                                   if args.transport == "rccl" else
                                   ", partition-aligned one-sided IPC pull exchange"),
@@ -513,7 +523,7 @@ def main():
                               "launches": {k: v[0] for k, v in kt.items()}},
         "cpu_baseline": None,
     }
-    if world > 1:
+    if pipelined:
         torch.cuda.synchronize(dev)
         xms = sum(a.elapsed_time(b) for a, b in xfer_ev)
         # exact off-GPU bytes per step from the all-gathered index tables
@@ -529,30 +539,30 @@ def main():
             raise RuntimeError("exchange overflowed a receive buffer")
         remote *= args.steps
         peak = (world - 1) * XGMI_LINK_GBS
-        ach = remote / (xms / 1e3) / 1e9 if xms else None
+        ach = remote / (xms / 1e3) / 1e9 if xms and remote else None
         result["roofline_exchange"] = {
             "bound": "xgmi", "achieved": None if ach is None else round(ach, 1), "peak": peak,
             "unit": "GB/s", "frac": None if ach is None else round(ach / peak, 4),
             "remote_bytes_per_rank": remote // args.steps, "exchange_ms": round(xms, 2)}
-    if world == 1:
+    if not pipelined:
         ns = args.reduce_sort_records if args.reduce_sort_records >= 0 else n // R
         ns = min(ns, n)
         if ns > 0 and args.workload == "terasort":
             result["reduce_sort"] = reduce_sort(node, out[:ns * rs], ns, rs, dev)
-    if world == 1 and args.compress_maps != 0:
+    if not pipelined and args.compress_maps != 0:
         cm = min(maps, args.compress_maps if args.compress_maps > 0 else gm)
         if cm:
             # maps are consecutive in `out`: the first cm map outputs
             nb = sum(int(index[m * (R + 1) + R].item()) for m in range(cm))
             result["compress"] = compress_leg(node, out[:nb], index[:cm * (R + 1)], cm, R, dev)
-    if world == 1 and args.file_maps != 0:
+    if not pipelined and args.file_maps != 0:
         fm = min(maps, args.file_maps if args.file_maps > 0 else 8)
         result["files"] = files_leg(node, out, index, fm, R, dev)
-    if world == 1 and args.varlen_rows != 0:
+    if not pipelined and args.varlen_rows != 0:
         vr = args.varlen_rows if args.varlen_rows > 0 else 32 << 20
         result["varlen"] = varlen_leg(node, vr, min(vr, 1 << 20), 200, dev,
                                       compress=args.compress_maps != 0)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not pipelined and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
         print(json.dumps(result), flush=True)

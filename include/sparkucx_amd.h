@@ -75,7 +75,7 @@ typedef struct sux_conf {
   int32_t rank;       /* rank of this executor in the node's exchange group                    */
   int32_t world_size; /* executors (GPUs) in the exchange group; 1 = local resolve only        */
   int32_t num_streams;/* internal streams (compute + comm); 0 = default (2)                    */
-  uint8_t comm_id[128];         /* RCCL unique id from sux_comm_unique_id(), world_size > 1    */
+  uint8_t comm_id[128];         /* RCCL unique id from sux_comm_unique_id(); all-zero = no comm at world_size 1 */
   uint64_t min_buffer_size;     /* spark.shuffle.ucx.memory.minBufferSize (UcxShuffleConf.scala:66-72) */
   uint64_t min_allocation_size; /* spark.shuffle.ucx.memory.minAllocationSize (:74-81)         */
   uint64_t metadata_block_size; /* 2*spark.shuffle.ucx.rkeySize (:32-40): directory slot bytes */

@@ -399,7 +399,11 @@ int sux_node_create(const sux_conf* conf, int is_driver, sux_node** out) {
     n->is_driver = is_driver != 0;
     n->bind();
     n->pool = std::make_unique<DevicePool>(conf->min_buffer_size, conf->min_allocation_size);
-    if (conf->world_size > 1) {
+    // a communicator for world_size > 1, or at world_size 1 when a unique id is supplied (the
+    // exchange then runs through RCCL with one rank: the single-GPU rehearsal of the N > 1 path)
+    bool have_id = false;
+    for (int i = 0; i < 128; ++i) have_id |= conf->comm_id[i] != 0;
+    if (conf->world_size > 1 || have_id) {
       ncclUniqueId id;
       std::memcpy(&id, conf->comm_id, 128);
       nccl_check(ncclCommInitRank(&n->comm, conf->world_size, id, conf->rank), "ncclCommInitRank");
@@ -1020,7 +1024,7 @@ int sux_exchange_group(sux_node* node, const void* d_send, const int64_t* d_inde
     hipStream_t s = node->stream(stream);
     const size_t per_rank = (size_t)M * (R + 1);
     std::vector<int64_t> host(per_rank * W);
-    if (W == 1) {
+    if (!node->comm) {
       hip_check(hipMemcpyAsync(d_gathered, d_index, per_rank * 8, hipMemcpyDeviceToDevice, s),
                 "copy index");
     } else {
@@ -1039,7 +1043,7 @@ int sux_exchange_group(sux_node* node, const void* d_send, const int64_t* d_inde
             "receive buffer too small: need " + std::to_string(total) + " bytes");
     if (recv_bytes)
       for (int g = 0; g < W; ++g) recv_bytes[g] = rc[g];
-    if (W == 1) {
+    if (!node->comm) {
       if (total)
         hip_check(hipMemcpyAsync(d_recv, d_send, total, hipMemcpyDeviceToDevice, s), "self copy");
       return;

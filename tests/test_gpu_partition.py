@@ -215,6 +215,29 @@ def test_exchange_group_single_rank(gpu_node):
     assert e.value.code == N.SUX_ERANGE
 
 
+def test_exchange_group_rccl_one_rank():
+    """The RCCL calls of sux_exchange_group (ncclAllGather of the index tables, ncclAllToAllv of
+    the peer-major ranges) on a one-rank communicator: the argument plumbing the 8-GPU run uses."""
+    from sparkucx_amd.shuffle import Node
+    R, rpm, n = 64, 5000, 12000
+    recs = O.gen_terasort(11, 0, n)
+    opart = O.terasort_partitioner(R)
+    with Node(device=0, rank=0, world_size=1, comm_id=N.unique_id()) as node:
+        gp = gpu_part(node, opart)
+        send, index, peer = node.partition_maps_peer_major(gp, to_dev(recs), 100, rpm, 1)
+        maps = -(-n // rpm)
+        gathered = torch.empty(maps * (R + 1), dtype=torch.int64, device="cuda")
+        recv = torch.empty(recs.size, dtype=torch.uint8, device="cuda")
+        for _ in range(3):  # repeated groups on one communicator
+            recv.zero_()
+            rb = node.exchange_group(send, index, maps, R, gathered, recv)
+            torch.cuda.synchronize()
+            assert rb.tolist() == [recs.size]
+            assert host(recv).tobytes() == host(send).tobytes()
+            assert host(gathered).tolist() == host(index).tolist()
+        gp.close()
+
+
 # ---- full-size properties (BASELINE-scale batches, size-independent checks) ----------------------
 def test_large_batch_properties(gpu_node):
     """10^8 TeraSort records (10 GB, config-2 batch scale): multiset preserved, stable, sorted by
