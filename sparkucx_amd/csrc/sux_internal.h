@@ -66,6 +66,7 @@ struct Workspace {
   uint64_t totals_off, totals_bytes;  // u64 [map][R] partition record counts
   uint64_t base_off, base_bytes;      // u64 [map][R] destination record offset of (map, p)
   uint64_t pids_off, pids_bytes;      // u16 [records] when the caller passes no pid buffer
+  uint64_t op_off, op_bytes;          // one-pass kernel's sync words + scan tables (S = 100)
   uint64_t total;
 };
 Workspace workspace_layout(uint32_t R, uint32_t rec_size, uint64_t records_per_map,
@@ -78,6 +79,15 @@ struct LayoutDesc {
   int32_t world;  // 1 = map-major
   uint32_t rec_size;
 };
+
+// One-pass map side (sux_onepass.hip): fixed 100-byte records, map batch held on chip.
+uint64_t onepass_sync_bytes(uint32_t R);
+bool onepass_eligible(const PartDev& pd, const MapGroup& g, int world, const void* d_out,
+                      const uint64_t* d_peer_bytes, hipStream_t s, uint32_t* grid_out,
+                      uint32_t* cs_out);
+hipError_t launch_onepass(const PartDev& pd, const MapGroup& g, uint8_t* d_out, int64_t* d_index,
+                          uint8_t* d_index_be, uint16_t* d_pids, uint8_t* d_sync, uint32_t grid,
+                          uint32_t cs, hipStream_t s);
 
 // Kernel timing slots (sux_kernel_times order).
 enum KernelSlot { kHist = 0, kScan = 1, kScatter = 2, kCopy = 3, kNumSlots = 4 };

@@ -1,0 +1,556 @@
+// sux_onepass.hip — one-pass map side for fixed-size records, gfx950.
+//
+// The three-kernel path (sux_partition.hip: K1 hist, K2 scans, K3 scatter) needs a map batch's
+// whole histogram before its first record can be placed, so every record crosses the fabric
+// three times (K1 reads it for its key, K3 reads and writes it): 3·N·S bytes of HBM traffic for
+// the 2·N·S algorithmic bytes, and the XCD↔IOD fabric, not HBM, is what bounds both kernels.
+//
+// Here a map batch is held ON CHIP while its histogram forms.  One persistent launch, one
+// 1024-thread workgroup per CU (LDS-bound).  For every map batch each workgroup takes one slice
+// of ≤ 1024 records (≤ 100 KB at S = 100; one record per thread) into registers:
+//   count   key → partition id (P1, as K1), stable per-wave ranks by ballot match (as K3), the
+//           slice's per-partition counts published write-through (sc1) to the sync workspace;
+//   scan    two levels, each run by the LAST arriver of its level (agent-scope atomic counter,
+//           the value its add returned tells it so): a group of 32 consecutive slices (the
+//           workgroups one XCD gets under xcd_map) → exclusive prefix of every slice per
+//           partition + group totals; then the last group → partition totals, the map's index
+//           file (P3, native + big-endian) and every group's offsets, published through one
+//           done-flag per group;
+//   place   the slice goes registers → partition-sorted LDS image in destination-unit space →
+//           aligned 16-byte stores (K3 v7's image), each run's head/tail unit partial (dword
+//           stores of only this slice's dwords; the neighbouring slice writes the rest).
+// Pipelined one map deep: map m+1 is counted and its scan is in flight while map m is placed,
+// and map m+2's loads fly during map m's write-out.  A map batch therefore holds at most
+// gridDim × 1024 records (2^18 = 26 MB at 256 CUs); every record is read once and written once.
+//
+// Visibility (MI355X_MICROARCH.md, inter-workgroup hand-offs): every handed-off word is stored
+// sc1 and loaded sc1, each storing wave drains with s_waitcnt vmcnt(0) before its workgroup's
+// one lane signals (agent-scope add or sc1 flag store), consumers poll with sc1 loads and read
+// behind a workgroup barrier.  Every spin is bounded (s_memrealtime): a grid that is not fully
+// resident sets the abort word and the launch drains instead of hanging.
+//
+// Stability: slices are consecutive record ranges in slice order, records inside a slice in
+// order (waves in order, ballot ranks inside a wave), so a partition keeps input order — the
+// byte layout of the three-kernel path and of Spark's writers (P2), bit for bit.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+
+#include "sux_internal.h"
+
+namespace sux {
+
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+namespace onepass {
+constexpr int kWave = 64;
+}
+using onepass::kWave;
+
+// P1: partition functions — sux_p1.h
+#include "sux_p1.h"
+
+namespace onepass {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr uint32_t kGroup = 32;           // slices per scan group
+constexpr uint32_t kMaxGroups = 8;
+constexpr uint64_t kSpinTicks = 200000000;  // s_memrealtime runs at 100 MHz: 2 s
+
+// sync words (u32), one 256-byte line each
+constexpr uint32_t kLine = 64;
+constexpr uint32_t kGroupCtr = 0;                     // [g] at g * kLine
+constexpr uint32_t kTopCtr = kMaxGroups * kLine;
+constexpr uint32_t kDone = (kMaxGroups + 1) * kLine;  // [g] at kDone + g * kLine
+constexpr uint32_t kAbort = (2 * kMaxGroups + 1) * kLine;
+constexpr uint32_t kSyncWords = (2 * kMaxGroups + 2) * kLine;
+
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t add_agent(uint32_t* p, uint32_t v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    uint32_t t = __shfl_up(v, d, kWave);
+    if (lane >= d) v += t;
+  }
+  return v;
+}
+
+__device__ __forceinline__ uint64_t bswap64(uint64_t v) {
+  return ((uint64_t)__builtin_bswap32((uint32_t)v) << 32) | __builtin_bswap32((uint32_t)(v >> 32));
+}
+
+template <uint32_t S, uint32_t NW>
+struct Shape {
+  static constexpr uint32_t NT = NW * kWave;
+  static constexpr uint32_t C = NT;  // records per slice: one per thread
+  static constexpr uint32_t W = S / 4;
+  static constexpr uint32_t kUnits = (C * S + 12 + 15) / 16;
+  static constexpr uint32_t kPer = (kUnits + NT - 1) / NT;
+  static constexpr uint32_t kRecUnits = (S + 15) / 16 + 1;
+  static_assert(S % 4 == 0 && NW % 4 == 0, "shape");
+  // image units: the slice's bytes + per-run head padding (<= 3 dwords) and tail slack,
+  // rounded to 4 so that the u32x4 arrays behind dstu[SP] stay 16-byte aligned
+  static __host__ __device__ constexpr uint32_t space(int R) {
+    return ((C * S) / 16 + (3u * R + 1) / 2 + 1 + 3) & ~3u;
+  }
+  // img[SP] u32x4 | dstu[SP] | pinfo[R] u32x4 | recoff[C] | wcnt[R][NW] | u0s[R] | tmp[NW] | flags[4]
+  static __host__ __device__ constexpr uint32_t lds_bytes(int R) {
+    return space(R) * 16 + space(R) * 4 + (uint32_t)R * 16 + C * 4 + NW * (uint32_t)R * 4 +
+           (uint32_t)R * 4 + NW * 4 + 16;
+  }
+};
+
+struct SyncWs {
+  uint32_t* sync;  // kSyncWords
+  uint32_t* cnt;   // [2][nwg][R]  slice counts (double-buffered by map parity)
+  uint32_t* gpre;  // [2][nwg][R]  exclusive prefix of the slice inside its group
+  uint32_t* gtot;  // [2][kMaxGroups][R]
+  uint32_t* goff;  // [2][kMaxGroups][R]  map-level partition offset + preceding groups
+};
+
+template <uint32_t S, uint32_t NW, int KW>
+__global__ __launch_bounds__(NW * 64) void k_onepass(PartDev pd, MapGroup g,
+                                                     uint8_t* __restrict__ out,
+                                                     int64_t* __restrict__ index,
+                                                     uint8_t* __restrict__ index_be,
+                                                     uint16_t* __restrict__ pids, SyncWs sw,
+                                                     uint32_t cs) {
+  using K = Shape<S, NW>;
+  constexpr uint32_t NT = K::NT, W = K::W, PER = K::kPer;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  const int R = pd.R;
+  const uint32_t SP = K::space(R);
+  u32x4* img = reinterpret_cast<u32x4*>(lds8);
+  uint32_t* img32 = reinterpret_cast<uint32_t*>(lds8);
+  uint32_t* dstu = reinterpret_cast<uint32_t*>(img + SP);
+  u32x4* pinfo = reinterpret_cast<u32x4*>(dstu + SP);  // {lb, cd | keep << 8, full, sp}
+  uint32_t* recoff = reinterpret_cast<uint32_t*>(pinfo + R);
+  uint32_t* wcnt = recoff + K::C;  // [R][NW]
+  uint32_t* u0s = wcnt + NW * R;
+  uint32_t* tmp = u0s + R;
+  int* flags = reinterpret_cast<int*>(tmp + NW);
+
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const bool owner = tid < R;  // thread p owns partition p
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  const uint32_t nwg = gridDim.x;
+  const uint32_t s = xcd_map(blockIdx.x, nwg);  // this workgroup's slice of every map
+  const uint32_t grp = s / kGroup, ngr = (nwg + kGroup - 1) / kGroup;
+  const uint32_t gsz = min(kGroup, nwg - grp * kGroup);
+  const uint32_t M = g.num_maps;
+  int pid_bits = 0;
+  while ((1 << pid_bits) < R) ++pid_bits;
+  uint32_t* out32 = reinterpret_cast<uint32_t*>(out);
+  const uint32_t rot = (uint32_t)(lane >> 3) & 3u;
+
+  auto slice_of = [&](uint32_t m, uint64_t& c0, uint32_t& n) {
+    const uint64_t mb = (uint64_t)m * g.records_per_map;
+    const uint64_t me = min(mb + g.records_per_map, g.num_records);
+    const uint64_t a = min(mb + (uint64_t)s * cs, me);
+    c0 = a;
+    n = (uint32_t)(min(a + cs, me) - a);
+  };
+  // loads of map m's slice: coalesced 16-byte units + this thread's record key.  A map past
+  // the last (or an empty slice) loads record 0 of the group instead, so that every issue is
+  // the same instruction sequence (the compiler's counted waits then leave the younger set in
+  // flight).
+  auto issue = [&](uint32_t m, u32x4 (&v)[PER], uint32_t (&kv)[KW]) {
+    uint64_t c0 = 0;
+    uint32_t n = 0;
+    if (m < M) slice_of(m, c0, n);
+    if (n == 0) {
+      c0 = 0;
+      n = 1;
+    }
+    const uint8_t* a = g.recs + c0 * S;
+    const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(a) & 15u);
+    const u32x4* src = reinterpret_cast<const u32x4*>(a - head);
+    const uint32_t units = (head + n * S + 15) >> 4;
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) v[k] = src[min(tid + k * NT, units - 1)];
+    const uint32_t r = min((uint32_t)tid, n - 1);
+    const uint32_t* kp = reinterpret_cast<const uint32_t*>(a + (size_t)r * S + pd.key_offset);
+    typename KeyVec<KW>::T kvv = *reinterpret_cast<const typename KeyVec<KW>::T*>(kp);
+    KeyVec<KW>::get(kvv, kv);
+  };
+  auto abort_now = [&]() {
+    st_sc1(sw.sync + kAbort, 1u);
+    if (M) index[(uint64_t)(M - 1) * (R + 1)] = -1;  // the host sees a broken index table
+  };
+
+  // ---- level 2: the last group of map m: partition totals, index file, group offsets ------
+  auto top_leader = [&](uint32_t m) {
+    const uint32_t par = m & 1u;
+    uint32_t gt[kMaxGroups];
+    uint32_t T = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kMaxGroups; ++q) {
+      gt[q] = (owner && q < ngr) ? ld_sc1(sw.gtot + ((uint64_t)par * kMaxGroups + q) * R + tid) : 0u;
+      T += gt[q];
+    }
+    const uint32_t incl = wave_incl_scan(T, lane);
+    if (lane == kWave - 1) tmp[wave] = incl;
+    __syncthreads();
+    uint32_t ex = incl - T, tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < NW; ++w) {
+      const uint32_t t = tmp[w];
+      ex += (w < (uint32_t)wave) ? t : 0u;
+      tot += t;
+    }
+    int64_t* im = index + (uint64_t)m * (R + 1);
+    uint64_t* ibe = index_be ? reinterpret_cast<uint64_t*>(index_be) + (uint64_t)m * (R + 1) : nullptr;
+    if (owner) {
+      uint32_t acc = ex;
+#pragma unroll
+      for (uint32_t q = 0; q < kMaxGroups; ++q) {
+        if (q < ngr) st_sc1(sw.goff + ((uint64_t)par * kMaxGroups + q) * R + tid, acc);
+        acc += gt[q];
+      }
+      const int64_t off = (int64_t)ex * S;
+      im[tid] = off;
+      if (ibe) ibe[tid] = bswap64((uint64_t)off);
+    }
+    if (tid == 0) {
+      const int64_t off = (int64_t)tot * S;
+      im[R] = off;
+      if (ibe) ibe[R] = bswap64((uint64_t)off);
+    }
+    drain();
+    __syncthreads();
+    if (tid < (int)ngr) st_sc1(sw.sync + kDone + tid * kLine, m + 1);
+  };
+  // ---- level 1: the last slice of a group: slice prefixes inside the group, group totals --
+  auto group_leader = [&](uint32_t m) {
+    const uint32_t par = m & 1u;
+    if (owner) {
+      const uint64_t row0 = (uint64_t)par * nwg + grp * kGroup;
+      uint32_t acc = 0;
+#pragma unroll
+      for (uint32_t j0 = 0; j0 < kGroup; j0 += 8) {
+        uint32_t cv[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j)
+          cv[j] = (j0 + j < gsz) ? ld_sc1(sw.cnt + (row0 + j0 + j) * R + tid) : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) {
+          if (j0 + j < gsz) st_sc1(sw.gpre + (row0 + j0 + j) * R + tid, acc);
+          acc += cv[j];
+        }
+      }
+      st_sc1(sw.gtot + ((uint64_t)par * kMaxGroups + grp) * R + tid, acc);
+    }
+    drain();
+    __syncthreads();
+    if (tid == 0) flags[1] = add_agent(sw.sync + kTopCtr, 1u) == (m + 1) * ngr - 1;
+    __syncthreads();
+    if (flags[1]) top_leader(m);
+  };
+
+  // ---- count: pids, stable ranks, per-wave counts -> owner prefix rows; publish + arrive ---
+  auto count = [&](uint32_t m, const uint32_t (&kv)[KW], uint32_t& my_pid, uint32_t& my_rank,
+                   uint32_t& c_own) {
+    uint64_t c0;
+    uint32_t n;
+    slice_of(m, c0, n);
+    const bool valid = (uint32_t)tid < n;
+    uint32_t w[KW];
+#pragma unroll
+    for (int q = 0; q < KW; ++q) w[q] = kv[q];
+    const uint32_t pid = valid ? (uint32_t)partition_words<KW, false>(pd, w, pd.bounds, pd.lut) : 0u;
+    uint64_t peers = __ballot(valid);
+    for (int bb = 0; bb < pid_bits; ++bb) {
+      const bool bit = (pid >> bb) & 1u;
+      const uint64_t mk = __ballot(bit);
+      peers &= bit ? mk : ~mk;
+    }
+    if (valid && (peers & lt_mask) == 0) wcnt[pid * NW + wave] = (uint32_t)__popcll(peers);
+    my_pid = valid ? pid : kNone;
+    my_rank = (uint32_t)__popcll(peers & lt_mask);
+    if (pids && valid) pids[c0 + tid] = (uint16_t)pid;
+    __syncthreads();
+    c_own = 0;
+    if (owner) {
+      u32x4* row = reinterpret_cast<u32x4*>(wcnt + tid * NW);
+      u32x4 x[NW / 4];
+#pragma unroll
+      for (uint32_t q = 0; q < NW / 4; ++q) x[q] = row[q];
+#pragma unroll
+      for (uint32_t q = 0; q < NW / 4; ++q) {
+        u32x4 y;
+        y[0] = c_own;
+        y[1] = c_own + x[q][0];
+        y[2] = y[1] + x[q][1];
+        y[3] = y[2] + x[q][2];
+        c_own = y[3] + x[q][3];
+        row[q] = y;
+      }
+      st_sc1(sw.cnt + ((uint64_t)(m & 1u) * nwg + s) * R + tid, c_own);
+    }
+    drain();
+    __syncthreads();
+    if (tid == 0) flags[0] = add_agent(sw.sync + kGroupCtr + grp * kLine, 1u) == (m + 1) * gsz - 1;
+    __syncthreads();
+    if (flags[0]) group_leader(m);
+  };
+  auto zero_wcnt = [&]() {
+    if (owner) {
+#pragma unroll
+      for (uint32_t q = 0; q < NW / 4; ++q) reinterpret_cast<u32x4*>(wcnt + tid * NW)[q] = u32x4{0, 0, 0, 0};
+    }
+  };
+
+  // ---- place map m (records in X), count map m+1 (keys in Y), load map m+2 into X ---------
+  auto process = [&](uint32_t m, u32x4 (&vx)[PER], uint32_t (&kx)[KW], uint32_t& px, uint32_t& rx,
+                     uint32_t& cx, u32x4 (&vy)[PER], uint32_t (&ky)[KW], uint32_t& py,
+                     uint32_t& ry, uint32_t& cy) -> bool {
+    // A. wait for map m's offsets
+    if (tid == 0) {
+      flags[2] = 0;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (ld_sc1(sw.sync + kDone + grp * kLine) < m + 1) {
+        if (ld_sc1(sw.sync + kAbort)) {
+          flags[2] = 1;
+          break;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
+          abort_now();
+          flags[2] = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+      }
+    }
+    __syncthreads();
+    if (flags[2]) return false;
+    // B. run geometry: destination of this slice's run of p, its image units, scan over p
+    uint64_t c0;
+    uint32_t n;
+    slice_of(m, c0, n);
+    const uint64_t mbase = (uint64_t)m * g.records_per_map * S;  // map m's data file
+    const uint64_t mal = mbase & ~15ull;
+    uint32_t sp = 0, u0 = 0, cd = 0, full = 0, keep = 0;
+    if (owner) {
+      const uint32_t par = m & 1u;
+      const uint32_t off = ld_sc1(sw.goff + ((uint64_t)par * kMaxGroups + grp) * R + tid) +
+                           ld_sc1(sw.gpre + ((uint64_t)par * nwg + s) * R + tid);
+      const uint64_t pos = mbase + (uint64_t)off * S;
+      u0 = (uint32_t)((pos - mal) >> 4);
+      cd = (uint32_t)(pos & 15) >> 2;
+      if (cx) {
+        const uint32_t dw = cd + cx * W;
+        full = dw >> 2;
+        sp = (dw + 3) >> 2;
+        keep = dw & 3u;
+      }
+    }
+    const uint32_t incl = wave_incl_scan(sp, lane);
+    if (lane == kWave - 1) tmp[wave] = incl;
+    __syncthreads();
+    uint32_t lb = incl - sp, U = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < NW; ++w) {
+      const uint32_t t = tmp[w];
+      lb += (w < (uint32_t)wave) ? t : 0u;
+      U += t;
+    }
+    if (owner) {
+      pinfo[tid] = u32x4{lb, cd | (keep << 8), full, sp};
+      u0s[tid] = u0;
+      if (sp) dstu[lb] = u0 | (cd << 28);  // head unit: its first cd dwords are the previous slice's
+    }
+    __syncthreads();
+    // C. record image offsets, destination units that start inside each record
+    if (px != kNone) {
+      const u32x4 pi = pinfo[px];
+      const uint32_t pcd = pi[1] & 0xFFu, pkeep = pi[1] >> 8;
+      const uint32_t jr = wcnt[px * NW + wave] + rx;
+      const uint32_t o = 4 * pcd + jr * S;
+      recoff[tid] = 16 * pi[0] + o;
+      const uint32_t u0 = u0s[px];
+      const uint32_t k0 = (o + 15) >> 4;
+#pragma unroll
+      for (uint32_t t = 0; t < K::kRecUnits; ++t) {
+        const uint32_t k = k0 + t;
+        if (k > 0 && k * 16 < o + S && k < pi[3])
+          dstu[pi[0] + k] = (u0 + k) | (k == pi[2] ? (pkeep << 30) : 0u);
+      }
+    }
+    __syncthreads();
+    // D. records -> image (K3 v7 step 4)
+    {
+      const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(g.recs + c0 * S) & 15u);
+      const uint32_t units = n ? (head + n * S + 15) >> 4 : 0u;
+#pragma unroll
+      for (uint32_t k = 0; k < PER; ++k) {
+        const uint32_t u = tid + k * NT;
+        const int32_t b0 = (int32_t)(16 * u) - (int32_t)head;
+        const uint32_t r0 = b0 >= 0 ? (uint32_t)b0 / S : 0u, off0 = (uint32_t)b0 - r0 * S;
+        if (u < units && b0 >= 0 && (uint32_t)b0 + 16 <= n * S && off0 + 16 <= S) {
+          *reinterpret_cast<u32x4a4*>(img32 + ((recoff[r0] + off0) >> 2)) = vx[k];
+        } else if (u < units) {
+#pragma unroll
+          for (uint32_t cc = 0; cc < 4; ++cc) {
+            const uint32_t q = (cc + rot) & 3u;
+            const int32_t b = (int32_t)(16 * u + 4 * q) - (int32_t)head;
+            if (b >= 0 && (uint32_t)b < n * S) {
+              const uint32_t r = (uint32_t)b / S, off = (uint32_t)b - r * S;
+              const uint32_t x = q == 0 ? vx[k][0] : q == 1 ? vx[k][1] : q == 2 ? vx[k][2] : vx[k][3];
+              img32[(recoff[r] + off) >> 2] = x;
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // E/F. count map m+1 (its loads were issued one map ago) and start its scan
+    zero_wcnt();
+    __syncthreads();
+    if (m + 1 < M) count(m + 1, ky, py, ry, cy);
+    // G. the X registers are free: load map m+2
+    issue(m + 2, vx, kx);
+    // H. write map m's image: aligned 16-byte units, partial head/tail units as dwords
+    for (uint32_t q = tid; q < U; q += NT) {
+      const uint32_t d = dstu[q];
+      const u32x4 x = img[q];
+      const uint64_t A = mal + (uint64_t)(d & 0x0FFFFFFFu) * 16;
+      const uint32_t skip = (d >> 28) & 3u, keep = d >> 30;
+      if (skip == 0 && keep == 0) {
+        *reinterpret_cast<u32x4*>(out + A) = x;
+      } else {
+        const uint32_t e = keep ? keep : 4u;
+#pragma unroll
+        for (uint32_t cc = 0; cc < 4; ++cc)
+          if (cc >= skip && cc < e) out32[(A >> 2) + cc] = x[cc];
+      }
+    }
+    __syncthreads();
+    (void)vy;
+    return true;
+  };
+
+  if (M == 0) return;
+  u32x4 va[PER], vb[PER];
+  uint32_t ka[KW], kb[KW];
+  uint32_t pa = kNone, ra = 0, ca = 0, pb = kNone, rb = 0, cb = 0;
+  issue(0, va, ka);
+  zero_wcnt();
+  __syncthreads();
+  count(0, ka, pa, ra, ca);
+  issue(1, vb, kb);
+  // one copy of the loop body: the two register sets swap roles by register moves (31 per map)
+  for (uint32_t m = 0; m < M; ++m) {
+    if (!process(m, va, ka, pa, ra, ca, vb, kb, pb, rb, cb)) return;
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) {
+      const u32x4 t = va[k];
+      va[k] = vb[k];
+      vb[k] = t;
+    }
+#pragma unroll
+    for (int q = 0; q < KW; ++q) {
+      const uint32_t t = ka[q];
+      ka[q] = kb[q];
+      kb[q] = t;
+    }
+    pa = pb;
+    ra = rb;
+    ca = cb;
+  }
+}
+
+}  // namespace onepass
+
+// ------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------
+namespace {
+using onepass::Shape;
+constexpr uint32_t kOpS = 100, kOpNW = 12;  // 768-record slices: two register sets fit 168 VGPRs
+
+int stream_cus(hipStream_t s) {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  uint32_t mask[32] = {0};
+  const uint32_t words = (uint32_t)std::min(32, (cus + 31) / 32);
+  if (s && hipExtStreamGetCUMask(s, words, mask) == hipSuccess) {
+    int n = 0;
+    for (uint32_t i = 0; i < words; ++i) n += __builtin_popcount(mask[i]);
+    if (n > 0 && n < cus) return n;
+  }
+  return cus;
+}
+}  // namespace
+
+uint64_t onepass_sync_bytes(uint32_t R) {
+  const uint64_t words = onepass::kSyncWords + 2ull * 2 * 256 * R + 2ull * 2 * onepass::kMaxGroups * R;
+  return (words * 4 + 255) / 256 * 256;
+}
+
+bool onepass_eligible(const PartDev& pd, const MapGroup& g, int world, const void* d_out,
+                      const uint64_t* d_peer_bytes, hipStream_t s, uint32_t* grid_out,
+                      uint32_t* cs_out) {
+  // SUX_ONEPASS=0 selects the three-kernel path (read per launch: the parity tests run both)
+  const char* env = getenv("SUX_ONEPASS");
+  if ((env && env[0] == '0') || world != 1 || d_peer_bytes || g.rec_size != kOpS) return false;
+  if (pd.kind == 4 || pd.key_offset % 4 || pd.key_len < 1 || pd.key_len > 16 ||
+      pd.key_offset + pd.key_len > (int)kOpS)
+    return false;
+  if (pd.R < 1 || pd.R > (int)Shape<kOpS, kOpNW>::NT ||
+      Shape<kOpS, kOpNW>::lds_bytes(pd.R) > 160 * 1024)
+    return false;
+  if ((reinterpret_cast<uintptr_t>(d_out) & 15) || g.records_per_map * kOpS >= (1ull << 32))
+    return false;
+  const int cus = stream_cus(s);
+  if (cus < 1 || cus > 256) return false;
+  const uint64_t cs = (g.records_per_map + cus - 1) / cus;
+  if (cs > Shape<kOpS, kOpNW>::C) return false;
+  if (grid_out) *grid_out = (uint32_t)cus;
+  if (cs_out) *cs_out = (uint32_t)cs;
+  return true;
+}
+
+hipError_t launch_onepass(const PartDev& pd, const MapGroup& g, uint8_t* d_out, int64_t* d_index,
+                          uint8_t* d_index_be, uint16_t* d_pids, uint8_t* d_sync, uint32_t grid,
+                          uint32_t cs, hipStream_t s) {
+  const int R = pd.R;
+  onepass::SyncWs sw;
+  uint32_t* w = reinterpret_cast<uint32_t*>(d_sync);
+  sw.sync = w;
+  sw.cnt = w + onepass::kSyncWords;
+  sw.gpre = sw.cnt + 2ull * 256 * R;
+  sw.gtot = sw.gpre + 2ull * 256 * R;
+  sw.goff = sw.gtot + 2ull * onepass::kMaxGroups * R;
+  hipError_t e = hipMemsetAsync(sw.sync, 0, onepass::kSyncWords * 4, s);
+  if (e != hipSuccess) return e;
+  const size_t lds = Shape<kOpS, kOpNW>::lds_bytes(R);
+  const int kw = (pd.key_len + 3) / 4;
+#define SUX_OP(KW)                                                                              \
+  do {                                                                                          \
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&onepass::k_onepass<kOpS, kOpNW, KW>), \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);            \
+    hipLaunchKernelGGL((onepass::k_onepass<kOpS, kOpNW, KW>), dim3(grid), dim3(kOpNW * kWave),   \
+                       lds, s, pd, g, d_out, d_index, d_index_be, d_pids, sw, cs);              \
+  } while (0)
+  if (kw <= 1) SUX_OP(1);
+  else if (kw == 2) SUX_OP(2);
+  else if (kw == 3) SUX_OP(3);
+  else SUX_OP(4);
+#undef SUX_OP
+  return hipGetLastError();
+}
+
+}  // namespace sux

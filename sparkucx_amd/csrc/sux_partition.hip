@@ -1525,7 +1525,6 @@ static uint64_t align_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
 
 Workspace workspace_layout(uint32_t R, uint32_t rec_size, uint64_t records_per_map,
                            uint64_t num_records, uint32_t tile_recs, bool need_pids) {
-  (void)rec_size;
   Workspace w{};
   uint64_t maps = records_per_map ? (num_records + records_per_map - 1) / records_per_map : 0;
   if (maps == 0) maps = 1;
@@ -1545,6 +1544,9 @@ Workspace workspace_layout(uint32_t R, uint32_t rec_size, uint64_t records_per_m
   w.pids_off = off;
   w.pids_bytes = need_pids ? align_up(num_records * 2, 256) : 0;
   off += w.pids_bytes;
+  w.op_off = off;
+  w.op_bytes = (rec_size == 100 && R <= 1024) ? onepass_sync_bytes(R) : 0;
+  off += w.op_bytes;
   w.total = off;
   return w;
 }
@@ -1594,6 +1596,15 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
                                   uint64_t* d_peer_bytes, Timer* timer, hipStream_t s) {
   const int R = pd.R;
   const uint32_t S = g.rec_size;
+  // one pass (sux_onepass.hip) whenever a map batch fits on chip: every record read once
+  uint32_t op_grid = 0, op_cs = 0;
+  if (ws.op_bytes && onepass_eligible(pd, g, lay.world, d_out, d_peer_bytes, s, &op_grid, &op_cs)) {
+    timer_begin(timer, kScatter, s);
+    const hipError_t eo = launch_onepass(pd, g, d_out, d_index, d_index_be, d_pids,
+                                         d_ws + ws.op_off, op_grid, op_cs, s);
+    timer_end(timer, kScatter, s);
+    return eo;
+  }
   const uint32_t total_tiles = g.num_maps * g.tiles_per_map;
   uint32_t* counts = reinterpret_cast<uint32_t*>(d_ws + ws.counts_off);
   uint64_t* totals = reinterpret_cast<uint64_t*>(d_ws + ws.totals_off);

@@ -281,7 +281,11 @@ def test_large_batch_properties(gpu_node):
     assert host(out[s * rs:e * rs]).tobytes() == bytes(want)
 
 
-def test_kernel_timing_counts_launches(gpu_node):
+@pytest.mark.parametrize("onepass", ["1", "0"])
+def test_kernel_timing_counts_launches(gpu_node, monkeypatch, onepass):
+    """Three-kernel path: hist + scan + scatter per launch group; one pass: one launch, timed
+    in the scatter slot (the bench's roofline kernel)."""
+    monkeypatch.setenv("SUX_ONEPASS", onepass)
     recs = O.gen_terasort(12, 0, 50000)
     gp = gpu_part(gpu_node, O.terasort_partitioner(200))
     gpu_node.set_kernel_timing(True)
@@ -290,7 +294,8 @@ def test_kernel_timing_counts_launches(gpu_node):
     torch.cuda.synchronize()
     t = gpu_node.kernel_times()
     gpu_node.set_kernel_timing(False)
-    assert t["hist"][0] == 3 and t["scatter"][0] == 3 and t["scan"][0] == 3
+    k = 0 if onepass == "1" else 3
+    assert t["hist"][0] == k and t["scatter"][0] == 3 and t["scan"][0] == k
     assert t["scatter"][1] > 0
 
 
