@@ -1,9 +1,10 @@
 """GPU parity of the one-pass map side (sux_onepass.hip) — map batch held on chip, one launch.
 
-The one-pass kernel is chosen automatically for 100-byte records when a map batch fits the grid
-(<= 1024 records per CU) and R's LDS image fits; SUX_ONEPASS=0 forces the three-kernel path.
+The one-pass kernel is opt-in (SUX_ONEPASS=1, read per launch) for 100-byte records when a map
+batch fits the grid (<= 256 records per workgroup, 2 workgroups per CU) and R's LDS image fits;
+otherwise, and by default, the three-kernel path runs.
 Both are checked bit-exact against the oracle (P1-P3: data bytes, native + big-endian index,
-pids), and against each other at full map size (2^18-record maps, size-independent check).
+pids), and against each other at full map size (131072-record maps, size-independent check).
 """
 import numpy as np
 import pytest
@@ -53,8 +54,8 @@ def test_range_R(gpu_node, monkeypatch, R, onepass):
 
 
 @pytest.mark.parametrize("n,rpm", [(1, 1), (255, 255), (256, 256), (257, 257), (1000, 7),
-                                   (5000, 1024), (70000, 65536), (196608, 196608),
-                                   (300000, 196607), (262145, 131072)])
+                                   (5000, 1024), (70000, 65536), (131072, 131072),
+                                   (300000, 131071), (262145, 131072)])
 def test_map_shapes(gpu_node, monkeypatch, n, rpm):
     """Slices of 1..1024 records, empty slices, ragged last maps, many maps per launch."""
     recs = O.gen_terasort(22, 0, n)
@@ -98,9 +99,9 @@ def test_unaligned_record_base(gpu_node, monkeypatch):
 
 @pytest.mark.parametrize("R", [200, 256])
 def test_full_size_maps_equal_three_kernel_path(gpu_node, monkeypatch, R):
-    """64 maps of 196608 TeraSort records (1.26 GB, the bench map shape): one-pass output,
+    """64 maps of 131072 TeraSort records (0.84 GB, the bench map shape): one-pass output,
     index tables and pids identical to the three-kernel path's (both parity-checked above)."""
-    n, rpm = 64 * 196608, 196608
+    n, rpm = 64 * 131072, 131072
     opart = O.terasort_partitioner(R)
     d = gpu_node.generate(N.GEN_TERASORT, 0x5EED0002, 0, n, 100)
     monkeypatch.setenv("SUX_ONEPASS", "1")
@@ -117,7 +118,7 @@ def test_full_size_maps_equal_three_kernel_path(gpu_node, monkeypatch, R):
 def test_repeated_launches_same_workspace(gpu_node, monkeypatch):
     """The sync words are reset per launch: back-to-back launches on one workspace agree."""
     monkeypatch.setenv("SUX_ONEPASS", "1")
-    n, rpm = 3 * 196608, 196608
+    n, rpm = 3 * 131072, 131072
     opart = O.terasort_partitioner(200)
     gp = gpu_part(gpu_node, opart)
     d = gpu_node.generate(N.GEN_TERASORT, 7, 0, n, 100)
