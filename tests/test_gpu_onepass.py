@@ -133,3 +133,25 @@ def test_repeated_launches_same_workspace(gpu_node, monkeypatch):
     want_data, want_index, _ = O.write_maps(opart, host(d), 100, rpm)
     assert host(outs[0][0]).tobytes() == bytes(want_data)
     gp.close()
+
+
+def test_cu_masked_stream(gpu_node, monkeypatch):
+    """On a stream masked to 224 CUs the grid is sized to the stream's CUs (448 workgroups, all
+    resident) — the same bytes as the oracle."""
+    monkeypatch.setenv("SUX_ONEPASS", "1")
+    recs = O.gen_terasort(26, 0, 250_000)
+    opart = O.terasort_partitioner(200)
+    gp = gpu_part(gpu_node, opart)
+    st = gpu_node.cu_stream(32, complement=True)
+    try:
+        ts = torch.cuda.ExternalStream(st)
+        drecs = torch.from_numpy(recs).cuda()
+        ts.wait_stream(torch.cuda.current_stream())
+        out, index, _ = gpu_node.partition_maps(gp, drecs, 100, 100_000, stream=ts)
+        ts.synchronize()
+        want_data, want_index, _ = O.write_maps(opart, recs, 100, 100_000)
+        assert host(out).tobytes() == bytes(want_data)
+        assert host(index).tolist() == want_index.tolist()
+    finally:
+        gpu_node.destroy_stream(st)
+        gp.close()
