@@ -229,9 +229,9 @@ def files_leg(node, out, index, maps: int, R: int, dev) -> dict:
 
 
 def load_traffic(kernel: str) -> float | None:
-    """Per-launch HBM bytes of `kernel` from the committed PMC summary (profiles/pmc_r01.json,
+    """Per-launch HBM bytes of `kernel` from the committed PMC summary (profiles/pmc_r01_v10.json,
     written by profiles/collect_pmc.py; FETCH_SIZE x2 + WRITE_SIZE per the microarch guide)."""
-    p = os.path.join(ROOT, "profiles", "pmc_r01.json")
+    p = os.path.join(ROOT, "profiles", "pmc_r01_v10.json")
     try:
         with open(p) as f:
             return json.load(f)["kernels"][kernel]["hbm_bytes_per_launch"]

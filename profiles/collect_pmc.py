@@ -97,7 +97,8 @@ def main():
     a, bench_args = ap.parse_known_args()
     if not bench_args:
         bench_args = ["--steps", "1", "--warmup", "1", "--records", "268435456",
-                      "--no-cpu-baseline"]
+                      "--no-cpu-baseline", "--varlen-rows", "0", "--compress-maps", "0",
+                      "--file-maps", "0", "--reduce-sort-records", "0"]
     os.makedirs(a.out, exist_ok=True)
     dirs = []
     for i, cs in enumerate(PASSES):
@@ -108,10 +109,14 @@ def main():
     res = summarize(dirs)
     summary = {"bench_args": bench_args, "note": "per-dispatch means; hbm bytes = 2*FETCH_SIZE + "
                "WRITE_SIZE (KiB->B), MI355X_MICROARCH.md §HBM", "kernels": res}
-    # bench.py reads the scatter entry under the plain name
-    for k, v in list(res.items()):
-        if k.startswith("k_scatter"):
-            summary["kernels"].setdefault("k_scatter", v)
+    # bench.py reads the map-side scatter entry under the plain name (the default k_scatter7,
+    # never the reduce-sort's k_scatter16 if that leg ran)
+    for pref in ("k_scatter7", "k_scatter6", "k_scatter"):
+        hit = [k for k in res if k.startswith(pref) and not k.startswith("k_scatter16")]
+        if hit:
+            summary["kernels"]["k_scatter"] = res[hit[0]]
+            summary["k_scatter_is"] = hit[0]
+            break
     path = os.path.join(ROOT, "profiles", f"pmc_{a.tag}.json")
     with open(os.path.join(a.out, f"pmc_{a.tag}.json"), "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
