@@ -1512,7 +1512,7 @@ struct SortPlan {
   uint32_t rs;
   sux::MapGroup g{};
   sux::Workspace ws{};
-  uint64_t pairs_bytes, part_off, index_off, total;
+  uint64_t pairs_bytes, part_off, index_off, span_off, total;
 };
 
 void sort_plan(uint64_t n, uint32_t rs, SortPlan& P) {
@@ -1534,7 +1534,19 @@ void sort_plan(uint64_t n, uint32_t rs, SortPlan& P) {
   P.pairs_bytes = up(16 * (n ? n : 1));
   P.part_off = 2 * P.pairs_bytes;
   P.index_off = P.part_off + up(P.ws.total);
-  P.total = P.index_off + up(8ull * (R + 1));
+  P.span_off = P.index_off + up(8ull * (R + 1));
+  P.total = P.span_off + up(sux::kSortSpanBytes);
+}
+
+// True when bits [lo, hi) of the big-endian 128-bit pair differ between some records.  `span` is
+// the AND of key words 0..2 then their OR (pair bytes 0..11 = the 96 high bits, byte 0 first).
+bool span_varies(const uint32_t* span, int lo, int hi) {
+  for (int b = std::max(lo, 32); b < std::min(hi, 128); ++b) {
+    const int byte = 15 - b / 8;  // memory byte of the pair holding bit b
+    const uint32_t diff = span[byte / 4] ^ span[3 + byte / 4];
+    if ((diff >> (8 * (byte % 4) + b % 8)) & 1u) return true;
+  }
+  return false;
 }
 
 int sort_key_bits(int32_t kind, int32_t key_len) {
@@ -1596,8 +1608,13 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
   uint8_t* pb = ws + P.pairs_bytes;
   int64_t* index = reinterpret_cast<int64_t*>(ws + P.index_off);
   hip_check(sux::launch_sort_pairs(static_cast<const uint8_t*>(d_in), n, record_size, key_kind,
-                                   key_offset, key_len, d_seg, nseg, sbytes, pa, s),
+                                   key_offset, key_len, d_seg, nseg, sbytes, pa, ws + P.span_off, s),
             "sort pairs");
+  // which digits vary: one 24-byte read-back (the only host wait in the sort)
+  uint32_t span[6];
+  hip_check(hipMemcpyAsync(span, ws + P.span_off, sizeof span, hipMemcpyDeviceToHost, s),
+            "sort key span");
+  hip_check(hipStreamSynchronize(s), "sort key span");
   sux::PartDev pd{};
   pd.kind = sux::kPartRadix;
   pd.R = 1 << sux::kRadixBits;
@@ -1607,6 +1624,8 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
   sux::LayoutDesc lay{1, 16};
   // the key occupies bits [128 - bits, 128) of the big-endian pair; least significant digit first
   for (int sh = 128 - bits; sh < 128; sh += sux::kRadixBits) {
+    static const bool all_passes = std::getenv("SUX_SORT_ALL_PASSES") != nullptr;  // A/B runs
+    if (!all_passes && !span_varies(span, sh, sh + sux::kRadixBits)) continue;  // identity pass
     pd.seed = sh;
     P.g.recs = pa;
     hip_check(sux::launch_partition_group(pd, P.g, lay, pb, index, nullptr, nullptr,

@@ -4,7 +4,9 @@
 //
 // LSD radix sort over 16-byte (key, index) pairs, then one gather of the whole records:
 //   k_sort_pairs    record i -> pair {key as big-endian bytes [0, 12), i as u32 LE at [12, 16)};
-//                   signed keys get their sign bit flipped so unsigned order = signed order
+//                   signed keys get their sign bit flipped so unsigned order = signed order;
+//                   also the AND / OR of all key words (k_span_reduce), so that digit passes
+//                   whose bits never vary are skipped
 //   digit passes    stable partitions of the pairs by a 12-bit digit of the big-endian 128-bit
 //                   pair value (least significant key digit first) — the map-side kernels with
 //                   the internal radix partitioner (kind 7, R = 4096: k_hist16 + k_scatter16)
@@ -20,13 +22,9 @@ namespace sux {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(256) void k_sort_pairs(const uint8_t* __restrict__ in, uint64_t n,
-                                                    uint32_t rs, int kind, int key_offset,
-                                                    int key_len, const int64_t* __restrict__ seg,
-                                                    int nseg, int sbytes,
-                                                    u32x4* __restrict__ pairs) {
-  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
+__device__ inline u32x4 make_pair(const uint8_t* __restrict__ in, uint64_t i, uint32_t rs, int kind,
+                                  int key_offset, int key_len, const int64_t* __restrict__ seg,
+                                  int nseg, int sbytes) {
   const uint8_t* r = in + i * rs + key_offset;
   uint8_t kb[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   if (kind == 1 && (key_offset & 3) == 0) {  // unsigned bytes, dword-aligned: dword loads
@@ -56,7 +54,62 @@ __global__ __launch_bounds__(256) void k_sort_pairs(const uint8_t* __restrict__ 
   p[1] = (uint32_t)kb[4] | ((uint32_t)kb[5] << 8) | ((uint32_t)kb[6] << 16) | ((uint32_t)kb[7] << 24);
   p[2] = (uint32_t)kb[8] | ((uint32_t)kb[9] << 8) | ((uint32_t)kb[10] << 16) | ((uint32_t)kb[11] << 24);
   p[3] = (uint32_t)i;
-  pairs[i] = p;
+  return p;
+}
+
+// Grid-stride pair build that also records which key bits vary: each workgroup writes the AND and
+// the OR of its pairs' key words to part[block][0..5]; k_span_reduce folds them.  A digit whose
+// bits are equal in AND and OR is the same for every record, so its pass is the identity and the
+// host skips it (Spark long / int keys of small magnitude leave the top digits constant).
+__global__ __launch_bounds__(256) void k_sort_pairs(const uint8_t* __restrict__ in, uint64_t n,
+                                                    uint32_t rs, int kind, int key_offset,
+                                                    int key_len, const int64_t* __restrict__ seg,
+                                                    int nseg, int sbytes,
+                                                    u32x4* __restrict__ pairs,
+                                                    uint32_t* __restrict__ part) {
+  uint32_t a0 = ~0u, a1 = ~0u, a2 = ~0u, o0 = 0, o1 = 0, o2 = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * 256) {
+    const u32x4 p = make_pair(in, i, rs, kind, key_offset, key_len, seg, nseg, sbytes);
+    pairs[i] = p;
+    a0 &= p[0]; a1 &= p[1]; a2 &= p[2];
+    o0 |= p[0]; o1 |= p[1]; o2 |= p[2];
+  }
+  for (int m = 32; m >= 1; m >>= 1) {
+    a0 &= __shfl_xor(a0, m); a1 &= __shfl_xor(a1, m); a2 &= __shfl_xor(a2, m);
+    o0 |= __shfl_xor(o0, m); o1 |= __shfl_xor(o1, m); o2 |= __shfl_xor(o2, m);
+  }
+  __shared__ uint32_t red[4][6];
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[wv][0] = a0; red[wv][1] = a1; red[wv][2] = a2;
+    red[wv][3] = o0; red[wv][4] = o1; red[wv][5] = o2;
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    uint32_t v = red[0][threadIdx.x];
+    for (int w = 1; w < 4; ++w)
+      v = threadIdx.x < 3 ? (v & red[w][threadIdx.x]) : (v | red[w][threadIdx.x]);
+    part[blockIdx.x * 8 + threadIdx.x] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_span_reduce(const uint32_t* __restrict__ part,
+                                                     uint32_t blocks, uint32_t* __restrict__ span) {
+  __shared__ uint32_t red[256][6];
+  uint32_t v[6] = {~0u, ~0u, ~0u, 0, 0, 0};
+  for (uint32_t b = threadIdx.x; b < blocks; b += 256)
+    for (int k = 0; k < 6; ++k) v[k] = k < 3 ? (v[k] & part[b * 8 + k]) : (v[k] | part[b * 8 + k]);
+  for (int k = 0; k < 6; ++k) red[threadIdx.x][k] = v[k];
+  __syncthreads();
+  for (uint32_t h = 128; h >= 1; h >>= 1) {
+    if (threadIdx.x < h)
+      for (int k = 0; k < 6; ++k)
+        red[threadIdx.x][k] = k < 3 ? (red[threadIdx.x][k] & red[threadIdx.x + h][k])
+                                    : (red[threadIdx.x][k] | red[threadIdx.x + h][k]);
+    __syncthreads();
+  }
+  if (threadIdx.x < 6) span[threadIdx.x] = red[0][threadIdx.x];
 }
 
 __global__ __launch_bounds__(256) void k_gather_records(const uint32_t* __restrict__ in,
@@ -74,10 +127,16 @@ __global__ __launch_bounds__(256) void k_gather_records(const uint32_t* __restri
 
 hipError_t launch_sort_pairs(const uint8_t* in, uint64_t n, uint32_t rs, int kind, int key_offset,
                              int key_len, const int64_t* seg, int nseg, int sbytes, void* pairs,
-                             hipStream_t s) {
+                             void* span_ws, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_sort_pairs, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, in, n, rs,
-                     kind, key_offset, key_len, seg, nseg, sbytes, static_cast<u32x4*>(pairs));
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, kSortSpanBlocks);
+  uint32_t* part = static_cast<uint32_t*>(span_ws) + 8;
+  hipLaunchKernelGGL(k_sort_pairs, dim3(blocks), dim3(256), 0, s, in, n, rs, kind, key_offset,
+                     key_len, seg, nseg, sbytes, static_cast<u32x4*>(pairs), part);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_span_reduce, dim3(1), dim3(256), 0, s, part, blocks,
+                     static_cast<uint32_t*>(span_ws));
   return hipGetLastError();
 }
 

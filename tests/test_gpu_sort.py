@@ -141,3 +141,43 @@ def test_segmented_sort_long_keys(gpu_node):
     torch.cuda.synchronize()
     exp = O.sort_segments(recs, 16, O.SORT_LONG, 0, 8, seg)
     assert out.cpu().numpy()[: recs.size].tobytes() == exp.tobytes()
+
+
+def _long_recs(keys: np.ndarray) -> np.ndarray:
+    recs = np.zeros((keys.size, 16), np.uint8)
+    recs[:, :8] = keys.astype("<i8").view(np.uint8).reshape(-1, 8)
+    recs[:, 8:] = np.arange(keys.size, dtype="<u8").view(np.uint8).reshape(-1, 8)
+    return recs.ravel()
+
+
+@pytest.mark.parametrize("lo,hi,n", [(0, 1 << 20, 1_500_000),   # top digits constant: skipped
+                                     (7, 8, 100_000),            # one key: every pass skipped
+                                     (-3, 3, 200_000),           # sign flips: every digit varies
+                                     (1 << 40, (1 << 40) + 4096, 600_000)])
+def test_long_keys_constant_digits(gpu_node, lo, hi, n):
+    """Digit passes whose bits never vary are skipped (k_sort_pairs' AND/OR key span): the
+    result must still be the oracle's, including the grid-stride walk past 2048 x 256 records."""
+    keys = np.random.default_rng(n).integers(lo, hi, n, dtype=np.int64)
+    recs = _long_recs(keys)
+    got = gpu_sort(gpu_node, recs, 16, N.SORT_LONG, 0, 8)
+    assert got.tobytes() == O.sort_records(recs, 16, O.SORT_LONG, 0, 8).tobytes()
+
+
+def test_byte_keys_one_varying_middle_byte(gpu_node):
+    recs = O.gen_terasort(26, 0, 50_000).reshape(-1, 100)
+    recs[:, :10] = 0x5A
+    recs[:, 4] = np.random.default_rng(4).integers(0, 256, recs.shape[0], dtype=np.uint8)
+    got = gpu_sort(gpu_node, recs.ravel(), 100, N.SORT_BYTES, 0, 10)
+    assert got.tobytes() == O.sort_records(recs.ravel(), 100, O.SORT_BYTES, 0, 10).tobytes()
+
+
+def test_segmented_sort_equal_keys(gpu_node):
+    """Keys all equal: only the segment-id digits are sorted; each run keeps its order."""
+    recs = _long_recs(np.full(30_000, 42, np.int64))
+    seg = np.array([0, 7, 7, 20_000, 30_000], np.int64)
+    out = gpu_node.sort_segments(to_dev(recs), 16, N.SORT_LONG, 0, 8,
+                                 torch.from_numpy(seg).cuda())
+    torch.cuda.synchronize()
+    exp = O.sort_segments(recs, 16, O.SORT_LONG, 0, 8, seg)
+    assert out.cpu().numpy()[: recs.size].tobytes() == exp.tobytes()
+    assert exp.tobytes() == recs.tobytes()
