@@ -1515,14 +1515,25 @@ struct SortPlan {
   uint64_t pairs_bytes, part_off, index_off, span_off, total;
 };
 
-void sort_plan(uint64_t n, uint32_t rs, SortPlan& P) {
+// Digit widths a sort may use: kSortMinDigitBits .. kSortMaxDigitBits; the workspace is sized for
+// the widest so that the caller's buffer fits whichever width the key length selects.
+constexpr int kSortMinDigitBits = 8;
+constexpr int kSortMaxDigitBits = 15;
+constexpr int kSortDefaultMaxDigitBits = 12;
+
+void sort_plan(uint64_t n, uint32_t rs, SortPlan& P, int digit_bits) {
   check_record_size(rs);
   require(n < (1ull << 32), SUX_ERANGE, "sort: fewer than 2^32 records per call");
   P.n = n;
   P.rs = rs;
-  const uint32_t R = 1u << sux::kRadixBits;
+  const uint32_t R = 1u << digit_bits;
   const uint64_t rpm = n ? n : 1;
-  const uint32_t tile = sux::choose_tile_recs(R, 16, rpm);
+  uint32_t tile = sux::choose_tile_recs(R, 16, rpm);
+  // long sorts: longer tiles while >= 256 of them remain (fewer counters for k_tile_scan_tm to
+  // scan; profiles/r01_v13/sort_tile_sweep.txt: 32 Mi pairs 6.04 -> 5.73 ms at 65536, while 5 M
+  // pairs lose 55 % there, hence the tile-count floor)
+  if (!std::getenv("SUX_TILE_RECS"))
+    while (tile < 65536 && rpm / (2ull * tile) >= 256) tile *= 2;
   P.g.records_per_map = rpm;
   P.g.num_records = n;
   P.g.num_maps = 1;
@@ -1569,9 +1580,13 @@ int sort_key_bits(int32_t kind, int32_t key_len) {
 int sux_sort_workspace_size(uint64_t n, uint32_t record_size, uint64_t* bytes) {
   return guard([&] {
     require(bytes, SUX_EINVAL, "NULL argument");
-    SortPlan P;
-    sort_plan(n, record_size, P);
-    *bytes = P.total;
+    uint64_t most = 0;
+    for (int d = kSortMinDigitBits; d <= kSortMaxDigitBits; ++d) {
+      SortPlan P;
+      sort_plan(n, record_size, P, d);
+      most = std::max(most, P.total);
+    }
+    *bytes = most;
   });
 }
 
@@ -1591,8 +1606,17 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
   }
   require(key_offset >= 0 && (uint64_t)key_offset + key_len <= record_size, SUX_EINVAL,
           "sort: the key does not fit the record");
+  // fewest passes at <= max_digit bits each, then the narrowest digit giving that pass count
+  // (80-bit TeraSort keys: 6 passes of 14 bits instead of 7 of 12)
+  static const int max_digit = [] {
+    const char* e = std::getenv("SUX_SORT_MAX_DIGIT_BITS");  // sweep override
+    const int v = e ? std::atoi(e) : kSortDefaultMaxDigitBits;
+    return std::min(std::max(v, kSortMinDigitBits), kSortMaxDigitBits);
+  }();
+  const int passes = (bits + max_digit - 1) / max_digit;
+  const int digit = std::max(kSortMinDigitBits, (bits + passes - 1) / passes);
   SortPlan P;
-  sort_plan(n, record_size, P);
+  sort_plan(n, record_size, P, digit);
   if (n == 0) return;
   require(d_in && d_out && d_ws, SUX_EINVAL, "NULL buffer");
   require(ws_bytes >= P.total, SUX_EINVAL,
@@ -1617,15 +1641,15 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
   hip_check(hipStreamSynchronize(s), "sort key span");
   sux::PartDev pd{};
   pd.kind = sux::kPartRadix;
-  pd.R = 1 << sux::kRadixBits;
+  pd.R = 1 << digit;
   pd.key_offset = 0;
   pd.key_len = 16;
   pd.ascending = 1;
   sux::LayoutDesc lay{1, 16};
   // the key occupies bits [128 - bits, 128) of the big-endian pair; least significant digit first
-  for (int sh = 128 - bits; sh < 128; sh += sux::kRadixBits) {
+  for (int sh = 128 - bits; sh < 128; sh += digit) {
     static const bool all_passes = std::getenv("SUX_SORT_ALL_PASSES") != nullptr;  // A/B runs
-    if (!all_passes && !span_varies(span, sh, sh + sux::kRadixBits)) continue;  // identity pass
+    if (!all_passes && !span_varies(span, sh, sh + digit)) continue;  // identity pass
     pd.seed = sh;
     P.g.recs = pa;
     hip_check(sux::launch_partition_group(pd, P.g, lay, pb, index, nullptr, nullptr,

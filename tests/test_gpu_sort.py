@@ -181,3 +181,13 @@ def test_segmented_sort_equal_keys(gpu_node):
     exp = O.sort_segments(recs, 16, O.SORT_LONG, 0, 8, seg)
     assert out.cpu().numpy()[: recs.size].tobytes() == exp.tobytes()
     assert exp.tobytes() == recs.tobytes()
+
+
+def test_long_sort_long_tiles(gpu_node):
+    """17 Mi records: the sort plan grows its tiles to 65536 records (>= 256 tiles remain);
+    bit-exact against the oracle."""
+    n = 17 << 20
+    keys = np.random.default_rng(17).integers(-(1 << 62), 1 << 62, n, dtype=np.int64)
+    recs = _long_recs(keys)
+    got = gpu_sort(gpu_node, recs, 16, N.SORT_LONG, 0, 8)
+    assert got.tobytes() == O.sort_records(recs, 16, O.SORT_LONG, 0, 8).tobytes()
