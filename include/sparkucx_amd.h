@@ -315,7 +315,10 @@ int sux_buffer_release(sux_buffer* buf);
  * (sux_fetch_blocks) gives one deterministic answer where Spark's depends on fetch order (Q4).
  * Keys: SUX_SORT_BYTES = key_len (1..12) bytes compared unsigned lexicographically (TeraSort's
  * 10-byte keys); SUX_SORT_LONG / SUX_SORT_INT = signed little-endian int64 / int32 (Spark's
- * LongType / IntegerType orderings).  Workspace: sux_sort_workspace_size (about 32 B/record). */
+ * LongType / IntegerType orderings).  Workspace: sux_sort_workspace_size (about 32 B/record).
+ * The call waits on `stream` once, after the key pass, to read back which key bits vary (24
+ * bytes): digit passes over bits that never vary are skipped, so it cannot be captured into a
+ * HIP graph.  The output is complete when the stream's later work runs. */
 #define SUX_SORT_BYTES 1
 #define SUX_SORT_LONG 2
 #define SUX_SORT_INT 3
