@@ -1631,8 +1631,12 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
   uint8_t* pa = ws;
   uint8_t* pb = ws + P.pairs_bytes;
   int64_t* index = reinterpret_cast<int64_t*>(ws + P.index_off);
+  // records of <= 16 bytes (with the segment id) travel inside the pairs: no gather at the end
+  static const bool no_inline = std::getenv("SUX_SORT_GATHER") != nullptr;  // A/B runs
+  const bool inline_rec = !no_inline && record_size + (uint32_t)sbytes <= 16;
   hip_check(sux::launch_sort_pairs(static_cast<const uint8_t*>(d_in), n, record_size, key_kind,
-                                   key_offset, key_len, d_seg, nseg, sbytes, pa, ws + P.span_off, s),
+                                   key_offset, key_len, d_seg, nseg, sbytes, pa, ws + P.span_off,
+                                   inline_rec, s),
             "sort pairs");
   // which digits vary: one 24-byte read-back (the only host wait in the sort)
   uint32_t span[6];
@@ -1657,7 +1661,12 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
               "sort digit pass");
     std::swap(pa, pb);
   }
-  hip_check(sux::launch_gather_records(d_in, pa, n, record_size, d_out, s), "sort gather");
+  if (inline_rec)
+    hip_check(sux::launch_unpair_records(pa, n, record_size, key_kind, key_offset, key_len, sbytes,
+                                         d_out, s),
+              "sort unpair");
+  else
+    hip_check(sux::launch_gather_records(d_in, pa, n, record_size, d_out, s), "sort gather");
 }
 }  // namespace
 

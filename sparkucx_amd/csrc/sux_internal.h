@@ -152,7 +152,9 @@ constexpr int kPartRadix = 7;  // internal partitioner: 12-bit digit (shift in P
 constexpr int kRadixBits = 12;
 hipError_t launch_sort_pairs(const uint8_t* in, uint64_t n, uint32_t rs, int kind, int key_offset,
                              int key_len, const int64_t* seg, int nseg, int sbytes, void* pairs,
-                             void* span_ws, hipStream_t s);
+                             void* span_ws, bool inline_rec, hipStream_t s);
+hipError_t launch_unpair_records(const void* pairs, uint64_t n, uint32_t rs, int kind,
+                                 int key_offset, int key_len, int sbytes, void* out, hipStream_t s);
 // span_ws: 8 u32 (AND of key words 0..2, OR of key words 0..2) + kSortSpanBlocks x 8 u32 partials
 constexpr uint32_t kSortSpanBlocks = 2048;
 constexpr uint64_t kSortSpanBytes = 4ull * 8 * (kSortSpanBlocks + 1);

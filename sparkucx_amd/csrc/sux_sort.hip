@@ -22,6 +22,11 @@ namespace sux {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// Pair bytes: [0, kbytes) the order key (segment id big-endian, then the key big-endian, sign
+// flipped for signed kinds); then either the record index as u32 LE at [12, 16) (gather mode) or,
+// when record_size + segment bytes <= 16 (inline mode), the record's other bytes in record order
+// at [kbytes, kbytes + rs - key_len): the pair IS the record, and k_unpair_records rebuilds it in
+// one streaming pass instead of the random-access gather.  Digits only ever cover the key bytes.
 __device__ inline u32x4 make_pair(const uint8_t* __restrict__ in, uint64_t i, uint32_t rs, int kind,
                                   int key_offset, int key_len, const int64_t* __restrict__ seg,
                                   int nseg, int sbytes) {
@@ -50,11 +55,69 @@ __device__ inline u32x4 make_pair(const uint8_t* __restrict__ in, uint64_t i, ui
     for (int k = 0; k < sbytes; ++k) kb[k] = (uint8_t)((uint32_t)lo >> (8 * (sbytes - 1 - k)));
   }
   u32x4 p;
+  p[3] = (uint32_t)i;
   p[0] = (uint32_t)kb[0] | ((uint32_t)kb[1] << 8) | ((uint32_t)kb[2] << 16) | ((uint32_t)kb[3] << 24);
   p[1] = (uint32_t)kb[4] | ((uint32_t)kb[5] << 8) | ((uint32_t)kb[6] << 16) | ((uint32_t)kb[7] << 24);
   p[2] = (uint32_t)kb[8] | ((uint32_t)kb[9] << 8) | ((uint32_t)kb[10] << 16) | ((uint32_t)kb[11] << 24);
-  p[3] = (uint32_t)i;
   return p;
+}
+
+// Inline mode, at 128-bit word level (a byte loop with run-time indices costs ~3x the bandwidth
+// time): rec = the record as a little-endian u128; the pair's memory bytes, also a LE u128, are
+// seg (big-endian, sbytes) | order key (klen bytes) | the record's other bytes in record order.
+typedef unsigned __int128 u128;
+__device__ inline u128 shl(u128 x, int b) { return b >= 128 ? (u128)0 : x << b; }
+__device__ inline u128 shr(u128 x, int b) { return b >= 128 ? (u128)0 : x >> b; }
+__device__ inline u128 lowmask(int nbytes) { return nbytes >= 16 ? ~(u128)0 : shl(1, 8 * nbytes) - 1; }
+
+__device__ inline u128 load_rec(const uint8_t* rec, uint32_t rs) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(rec);
+  u128 v = w[0];
+  if (rs > 4) v |= (u128)w[1] << 32;
+  if (rs > 8) v |= (u128)w[2] << 64;
+  if (rs > 12) v |= (u128)w[3] << 96;
+  return v;
+}
+
+__device__ inline u128 inline_pair(u128 rec, int kind, int off, int klen, uint32_t seg_be,
+                                   int sbytes, uint32_t rs) {
+  u128 key = shr(rec, 8 * off) & lowmask(klen);
+  if (kind == 2) key = (u128)(__builtin_bswap64((uint64_t)key) ^ 0x80ull);
+  else if (kind == 3) key = (u128)(__builtin_bswap32((uint32_t)key) ^ 0x80u);
+  const u128 rest = (rec & lowmask(off)) | shl(shr(rec, 8 * (off + klen)) & lowmask((int)rs - off - klen), 8 * off);
+  return (u128)seg_be | shl(key, 8 * sbytes) | shl(rest, 8 * (sbytes + klen));
+}
+
+__device__ inline u128 inline_unpair(u128 pr, int kind, int off, int klen, int sbytes, uint32_t rs) {
+  u128 key = shr(pr, 8 * sbytes) & lowmask(klen);
+  if (kind == 2) key = (u128)__builtin_bswap64((uint64_t)key ^ 0x80ull);
+  else if (kind == 3) key = (u128)__builtin_bswap32((uint32_t)key ^ 0x80u);
+  const u128 rest = shr(pr, 8 * (sbytes + klen)) & lowmask((int)rs - klen);
+  return (rest & lowmask(off)) | shl(key, 8 * off) | shl(shr(rest, 8 * off), 8 * (off + klen));
+}
+
+// Inline mode's final pass: sorted pair j -> output record j.  Streaming: 16 B read, rs B written.
+__global__ __launch_bounds__(256) void k_unpair_records(const u32x4* __restrict__ pairs, uint64_t n,
+                                                        uint32_t rs, int kind, int key_offset,
+                                                        int key_len, int sbytes,
+                                                        uint32_t* __restrict__ out) {
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  const u32x4 p = pairs[j];
+  const u128 pr = (u128)p[0] | ((u128)p[1] << 32) | ((u128)p[2] << 64) | ((u128)p[3] << 96);
+  const u128 rec = inline_unpair(pr, kind, key_offset, key_len, sbytes, rs);
+  uint32_t* dst = out + j * (rs / 4);
+  if (rs == 16 && ((uintptr_t)out & 15) == 0) {
+    u32x4 v;
+    v[0] = (uint32_t)rec; v[1] = (uint32_t)(rec >> 32); v[2] = (uint32_t)(rec >> 64);
+    v[3] = (uint32_t)(rec >> 96);
+    *reinterpret_cast<u32x4*>(dst) = v;
+    return;
+  }
+  dst[0] = (uint32_t)rec;
+  if (rs > 4) dst[1] = (uint32_t)(rec >> 32);
+  if (rs > 8) dst[2] = (uint32_t)(rec >> 64);
+  if (rs > 12) dst[3] = (uint32_t)(rec >> 96);
 }
 
 // Grid-stride pair build that also records which key bits vary: each workgroup writes the AND and
@@ -66,11 +129,28 @@ __global__ __launch_bounds__(256) void k_sort_pairs(const uint8_t* __restrict__ 
                                                     int key_len, const int64_t* __restrict__ seg,
                                                     int nseg, int sbytes,
                                                     u32x4* __restrict__ pairs,
-                                                    uint32_t* __restrict__ part) {
+                                                    uint32_t* __restrict__ part, int inline_rec) {
   uint32_t a0 = ~0u, a1 = ~0u, a2 = ~0u, o0 = 0, o1 = 0, o2 = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * 256) {
-    const u32x4 p = make_pair(in, i, rs, kind, key_offset, key_len, seg, nseg, sbytes);
+    u32x4 p;
+    if (inline_rec) {
+      uint32_t seg_be = 0;
+      if (sbytes) {  // last segment whose start is <= i, big-endian in sbytes bytes
+        int lo = 0, hi = nseg;
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if ((uint64_t)seg[mid] <= i) lo = mid; else hi = mid;
+        }
+        seg_be = __builtin_bswap32((uint32_t)lo) >> (8 * (4 - sbytes));
+      }
+      const u128 pr = inline_pair(load_rec(in + i * rs, rs), kind, key_offset, key_len, seg_be,
+                                  sbytes, rs);
+      p[0] = (uint32_t)pr; p[1] = (uint32_t)(pr >> 32); p[2] = (uint32_t)(pr >> 64);
+      p[3] = (uint32_t)(pr >> 96);
+    } else {
+      p = make_pair(in, i, rs, kind, key_offset, key_len, seg, nseg, sbytes);
+    }
     pairs[i] = p;
     a0 &= p[0]; a1 &= p[1]; a2 &= p[2];
     o0 |= p[0]; o1 |= p[1]; o2 |= p[2];
@@ -127,16 +207,26 @@ __global__ __launch_bounds__(256) void k_gather_records(const uint32_t* __restri
 
 hipError_t launch_sort_pairs(const uint8_t* in, uint64_t n, uint32_t rs, int kind, int key_offset,
                              int key_len, const int64_t* seg, int nseg, int sbytes, void* pairs,
-                             void* span_ws, hipStream_t s) {
+                             void* span_ws, bool inline_rec, hipStream_t s) {
   if (n == 0) return hipSuccess;
   const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, kSortSpanBlocks);
   uint32_t* part = static_cast<uint32_t*>(span_ws) + 8;
   hipLaunchKernelGGL(k_sort_pairs, dim3(blocks), dim3(256), 0, s, in, n, rs, kind, key_offset,
-                     key_len, seg, nseg, sbytes, static_cast<u32x4*>(pairs), part);
+                     key_len, seg, nseg, sbytes, static_cast<u32x4*>(pairs), part,
+                     inline_rec ? 1 : 0);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_span_reduce, dim3(1), dim3(256), 0, s, part, blocks,
                      static_cast<uint32_t*>(span_ws));
+  return hipGetLastError();
+}
+
+hipError_t launch_unpair_records(const void* pairs, uint64_t n, uint32_t rs, int kind,
+                                 int key_offset, int key_len, int sbytes, void* out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_unpair_records, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
+                     static_cast<const u32x4*>(pairs), n, rs, kind, key_offset, key_len, sbytes,
+                     static_cast<uint32_t*>(out));
   return hipGetLastError();
 }
 

@@ -191,3 +191,30 @@ def test_long_sort_long_tiles(gpu_node):
     recs = _long_recs(keys)
     got = gpu_sort(gpu_node, recs, 16, N.SORT_LONG, 0, 8)
     assert got.tobytes() == O.sort_records(recs, 16, O.SORT_LONG, 0, 8).tobytes()
+
+
+@pytest.mark.parametrize("rs,kind,off,klen", [(12, N.SORT_INT, 4, 4), (8, N.SORT_BYTES, 2, 3),
+                                              (16, N.SORT_BYTES, 5, 11), (4, N.SORT_INT, 0, 4),
+                                              (16, N.SORT_LONG, 8, 8)])
+def test_inline_small_records(gpu_node, rs, kind, off, klen):
+    """Records of <= 16 bytes ride inside the sort pairs (no gather): key bytes anywhere in the
+    record, signed and unsigned kinds, ties kept in input order."""
+    n = 70_000
+    rng = np.random.default_rng(rs * 100 + off)
+    recs = rng.integers(0, 256, (n, rs), dtype=np.uint8)
+    recs[: n // 2, off:off + min(klen, 2)] = 7  # many equal leading key bytes / ties
+    got = gpu_sort(gpu_node, recs.ravel(), rs, kind, off, klen)
+    assert got.tobytes() == O.sort_records(recs.ravel(), rs, kind, off, klen).tobytes()
+
+
+@pytest.mark.parametrize("nseg", [3, 300])
+def test_segmented_inline_small_records(gpu_node, nseg):
+    """8-byte records with a 1-2 byte segment id still fit a pair (inline mode)."""
+    n, rs = 50_000, 8
+    rng = np.random.default_rng(nseg)
+    recs = rng.integers(0, 256, n * rs, dtype=np.uint8)
+    seg = np.concatenate([[0], np.sort(rng.integers(0, n + 1, nseg - 1)), [n]]).astype(np.int64)
+    out = gpu_node.sort_segments(to_dev(recs), rs, N.SORT_INT, 4, 4, torch.from_numpy(seg).cuda())
+    torch.cuda.synchronize()
+    exp = O.sort_segments(recs, rs, O.SORT_INT, 4, 4, seg)
+    assert out.cpu().numpy()[: n * rs].tobytes() == exp.tobytes()
