@@ -31,6 +31,7 @@ namespace sux {
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 
 constexpr int kWave = 64;
+constexpr int kScatter16Batch = 4;  // k_scatter16b groups per turn (SUX_S16_GB overrides)
 
 // P1: partition functions — sux_p1.h
 #include "sux_p1.h"
@@ -1485,6 +1486,94 @@ __global__ __launch_bounds__(NW * 64) void k_scatter16(MapGroup g, int R, int pi
   }
 }
 
+// k_scatter16 with the turn handed on once per batch of GB consecutive 64-record groups instead of
+// once per group: a wave ranks GB groups, then in its turn walks their cursor updates back to
+// back (LDS ops of one wave stay in order), so the cross-wave hand-off (acquire spin, release
+// fence) is paid GB x less often.  Same output bytes as k_scatter16 (input order kept).
+template <uint32_t NW, int GB>
+__global__ __launch_bounds__(NW * 64) void k_scatter16b(MapGroup g, int R, int pid_bits,
+                                                        const uint16_t* __restrict__ pids,
+                                                        const uint32_t* __restrict__ prefix,
+                                                        const uint64_t* __restrict__ base,
+                                                        uint8_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t cur[];  // [R] next output record of p
+  __shared__ uint32_t turn;
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const uint32_t ntiles = g.num_maps * g.tiles_per_map;
+  const u32x4* recs = reinterpret_cast<const u32x4*>(g.recs);
+  u32x4* out4 = reinterpret_cast<u32x4*>(out);
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  for (uint32_t gt = xcd_map(blockIdx.x, gridDim.x); gt < ntiles; gt += gridDim.x) {
+    const TileRange tr = tile_range(g, gt);
+    const uint64_t* bm = base + (uint64_t)tr.map * R;
+    const uint32_t* pm = prefix + ((uint64_t)tr.map * g.tiles_per_map + tr.tile) * R;  // tile-major
+    for (int p = tid; p < R; p += NW * kWave) cur[p] = (uint32_t)(bm[p] + pm[p]);
+    if (tid == 0) turn = 0;
+    __syncthreads();
+    const uint32_t ngroups = (uint32_t)((tr.end - tr.begin + kWave - 1) / kWave);
+    const uint32_t nbatch = (ngroups + GB - 1) / GB;
+    uint32_t pa[GB], pb[GB];
+    u32x4 ra[GB], rb[GB];
+    auto load = [&](uint32_t bb, uint32_t (&pv)[GB], u32x4 (&rv)[GB]) {
+#pragma unroll
+      for (int k = 0; k < GB; ++k) {
+        const uint64_t i = tr.begin + ((uint64_t)bb * GB + k) * kWave + lane;
+        const uint64_t ii = i < tr.end ? i : tr.end - 1;  // clamped, unconditional
+        pv[k] = pids[ii];
+        rv[k] = recs[ii];
+      }
+    };
+    uint32_t b = wave;
+    load(b, pa, ra);
+    while (b < nbatch) {
+      load(b + NW, pb, rb);  // next batch in flight during this one's turn
+      uint64_t peers[GB];
+      uint32_t pp[GB];
+      bool valid[GB];
+#pragma unroll
+      for (int k = 0; k < GB; ++k) {
+        const uint64_t i = tr.begin + ((uint64_t)b * GB + k) * kWave + lane;
+        valid[k] = i < tr.end;
+        pp[k] = valid[k] ? pa[k] : 0u;
+        uint64_t pe = __ballot(valid[k]);
+        for (int bb = 0; bb < pid_bits; ++bb) {
+          const bool bit = (pp[k] >> bb) & 1u;
+          const uint64_t m = __ballot(bit);
+          pe &= bit ? m : ~m;
+        }
+        peers[k] = pe;
+      }
+      for (uint32_t spin = 0;
+           __hip_atomic_load(&turn, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != b; ++spin) {
+        __builtin_amdgcn_s_sleep(1);
+        if (spin > (1u << 22)) break;  // never reached: a guard against a hang, not a path
+      }
+      uint32_t dst[GB];
+#pragma unroll
+      for (int k = 0; k < GB; ++k) {
+        uint32_t r0 = 0;
+        if (valid[k]) r0 = cur[pp[k]];
+        __builtin_amdgcn_wave_barrier();
+        if (valid[k] && (peers[k] & lt_mask) == 0) cur[pp[k]] = r0 + (uint32_t)__popcll(peers[k]);
+        __builtin_amdgcn_wave_barrier();
+        dst[k] = r0 + (uint32_t)__popcll(peers[k] & lt_mask);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&turn, b + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+      for (int k = 0; k < GB; ++k)
+        if (valid[k]) out4[dst[k]] = ra[k];
+#pragma unroll
+      for (int k = 0; k < GB; ++k) {
+        pa[k] = pb[k];
+        ra[k] = rb[k];
+      }
+      b += NW;
+    }
+    __syncthreads();
+  }
+}
+
 template <int KW, bool TAB>
 static void launch_hist3_kw(dim3 grid, size_t lds, hipStream_t s, const PartDev& pd,
                             const MapGroup& g, uint16_t* pids, uint32_t* counts) {
@@ -1772,11 +1861,27 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   timer_begin(timer, kScatter, s);
   if (s16) {
     const size_t lds = (size_t)R * 4;
-    allow_lds(reinterpret_cast<const void*>(&k_scatter16<16>), lds);
     const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(2, (160u * 1024) / (uint32_t)lds));
     const dim3 grid(std::min<uint32_t>(total_tiles, 256u * per_cu));
-    hipLaunchKernelGGL((k_scatter16<16>), grid, dim3(1024), lds, s, g, R, bits, pids, counts, base,
-                       d_out);
+    static const int gb = [] {  // groups per turn (1 = k_scatter16); tuning override
+      const char* e = getenv("SUX_S16_GB");
+      return e ? atoi(e) : kScatter16Batch;
+    }();
+    if (gb == 2 || gb == 4) {
+      const void* kf = gb == 2 ? reinterpret_cast<const void*>(&k_scatter16b<16, 2>)
+                               : reinterpret_cast<const void*>(&k_scatter16b<16, 4>);
+      allow_lds(kf, lds);
+      if (gb == 2)
+        hipLaunchKernelGGL((k_scatter16b<16, 2>), grid, dim3(1024), lds, s, g, R, bits, pids,
+                           counts, base, d_out);
+      else
+        hipLaunchKernelGGL((k_scatter16b<16, 4>), grid, dim3(1024), lds, s, g, R, bits, pids,
+                           counts, base, d_out);
+    } else {
+      allow_lds(reinterpret_cast<const void*>(&k_scatter16<16>), lds);
+      hipLaunchKernelGGL((k_scatter16<16>), grid, dim3(1024), lds, s, g, R, bits, pids, counts,
+                         base, d_out);
+    }
     e = hipGetLastError();
   } else if (v7) {
     uint32_t tpw = s6tpw > 0 ? (uint32_t)s6tpw
