@@ -57,16 +57,41 @@ WORKLOADS = {
 }
 
 
+def host_cores() -> dict:
+    """Host CPUs this process may use: os.cpu_count() (nproc of the whole machine), the affinity
+    mask, and the cgroup CPU quota (cgroup v2 cpu.max) — on the GPU box the job's share is set by
+    the quota, while nproc reports every CPU of the machine."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    use = min(aff, quota) if quota else aff
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota": quota, "use": use}
+
+
 def cpu_baseline(args) -> dict | None:
     """Oracle CPU shuffle (Spark sort-shuffle write to /dev/shm files + UCX-style two-phase fetch)
-    on a bounded sample of the same workload: config 1's shape (1 GB, R=200, 8 map tasks)."""
+    on a bounded sample of the same workload: config 1's shape (1 GB, R=200, 8 map tasks), on every
+    host core this job may use (host_cores()['use']; --cpu-threads overrides)."""
     try:
         from oracle import oracle as O  # test infrastructure: timed as the baseline only
     except Exception as e:  # pragma: no cover
         log("cpu baseline unavailable:", e)
         return None
+    hc = host_cores()
     n, maps = args.cpu_records, 8
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    threads = args.cpu_threads if args.cpu_threads > 0 else hc["use"]
+    log(f"cpu baseline: nproc={hc['nproc']} affinity={hc['affinity']} "
+        f"cgroup_quota={hc['cgroup_quota']} -> {threads} threads")
     recs = O.gen_terasort(0x5EED0001, 0, n)
     part = O.terasort_partitioner(200)
     d = "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else None
@@ -87,11 +112,12 @@ def cpu_baseline(args) -> dict | None:
     times.sort()
     t, tm, tf = times[len(times) // 2]
     return {"value": round(recs.size / t / 1e9, 3), "unit": "GB/s", "cores": threads,
-            "kind": "port",
+            "kind": "port", "host": hc,
             "sample": f"TeraSort {n} x 100 B ({recs.size / 1e9:.2f} GB), R=200, {maps} map tasks, "
-                      f"{threads} threads; Spark-style write to {'/dev/shm' if d else '/tmp'} files "
-                      f"+ two-phase offset/block fetch; median of {len(times)} "
-                      f"(map {tm:.3f}s, fetch {tf:.3f}s)"}
+                      f"{threads} threads (nproc {hc['nproc']}, affinity {hc['affinity']}, "
+                      f"cgroup quota {hc['cgroup_quota']}); Spark-style write to "
+                      f"{'/dev/shm' if d else '/tmp'} files + two-phase offset/block fetch; "
+                      f"median of {len(times)} (map {tm:.3f}s, fetch {tf:.3f}s)"}
 
 
 def reduce_sort(node, recs, ns: int, rs: int, dev) -> dict:
@@ -256,14 +282,21 @@ def files_leg(node, out, index, maps: int, R: int, dev) -> dict:
             "read_GB/s": round(nb / tr / 1e9, 2)}
 
 
-def load_traffic(kernel: str) -> float | None:
-    """Per-launch HBM bytes of `kernel` from the committed PMC summary (profiles/pmc_r01_v10.json,
-    written by profiles/collect_pmc.py; FETCH_SIZE x2 + WRITE_SIZE per the microarch guide)."""
-    p = os.path.join(ROOT, "profiles", "pmc_r01_v10.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r02.json")
+
+
+def load_traffic(workload: str, kernel: str) -> dict | None:
+    """HBM bytes per record of `kernel` under `workload`, from the committed PMC summary
+    (profiles/pmc_r02.json, written by profiles/collect_pmc.py: one rocprofv3 pass per counter
+    group; 2 x FETCH_SIZE + WRITE_SIZE per the microarch guide).  The entry is keyed by workload
+    and by the kernel the library reports it launched (sux_kernel_variant), so a line never
+    borrows another kernel's counters; None when that pair was not profiled."""
     try:
-        with open(p) as f:
-            return json.load(f)["kernels"][kernel]["hbm_bytes_per_launch"]
-    except Exception:
+        with open(PMC_FILE) as f:
+            e = json.load(f)["workloads"][workload]["kernels"][kernel]
+        return {"bytes_per_record": e["hbm_bytes_per_launch"] / e["records_per_launch"],
+                "source": f"profiles/pmc_r02.json:{workload}/{kernel}"}
+    except (OSError, KeyError, ValueError, ZeroDivisionError):
         return None
 
 
@@ -306,9 +339,13 @@ def main():
                     help="N=1: also time writing/reading Spark's data + index files for this "
                          "many map outputs (sux_write_map_files; -1: 8; 0: skip)")
     ap.add_argument("--cpu-records", type=int, default=10_000_000)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0: every core this job may use, host_cores())")
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verify", action="store_true",
+                    help="test mode (N>1): check every received block of every group against "
+                         "the CPU oracle; timing is then not a benchmark")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -406,10 +443,12 @@ def main():
         # NEXT group's all-gather completed (3 slots keep partition(k) off that dependency)
         NB = 3 if args.transport == "ipc" else 2
         send = [torch.empty(group_recs * rs, dtype=torch.uint8, device=dev) for _ in range(NB)]
-        # receive ring (Spark's reducer consumes fetched blocks as a stream, maxBytesInFlight);
-        # 1.5x the group's bytes absorbs uneven partition sizes
-        recv = [torch.empty(int(group_recs * rs * 1.5) + (1 << 20), dtype=torch.uint8,
-                            device=dev) for _ in range(2)]
+        # receive ring (Spark's reducer consumes fetched blocks as a stream, maxBytesInFlight).
+        # A rank receives at most every rank's whole group (all keys in its partitions), so
+        # world x group bytes can never overflow, whatever the skew: Zipf's hot owner at 8 GPUs
+        # needs 1.79x (C4).  At C3 that is 2 x 26.8 GB beside 125 GB of input, within 288 GB.
+        recv = [torch.empty(world * group_recs * rs, dtype=torch.uint8, device=dev)
+                for _ in range(2)]
         ws = [torch.empty(ws_bytes, dtype=torch.uint8, device=dev) for _ in range(NB)]
         # one all-gathered index table per group (kept for the exact byte accounting)
         gidx = torch.empty(groups, world * gm * (R + 1), dtype=torch.int64, device=dev)
@@ -457,6 +496,37 @@ def main():
                 send_free[s].record(comm)
             e1.record(comm)
             xfer_ev.append((e0, e1))
+            if args.verify:
+                verify_group(j, recv[j % 2], gi, mg, r0, r1)
+
+        opart = None
+        if args.verify:  # test mode: every received block vs the CPU oracle (checker only)
+            from oracle import oracle as O
+            opart = (O.terasort_partitioner(R) if kind == N.PART_RANGE_BYTES
+                     else O.Partitioner(O.MURMUR3_LONG, R, 0, 8, 42))
+            ogen = {"terasort": O.gen_terasort, "zipf": O.gen_zipf, "small": O.gen_small}[args.workload]
+            lib = N.load()
+
+        def verify_group(j, rbuf, gi, mg, r0, r1):
+            torch.cuda.synchronize(dev)
+            got = rbuf.cpu().numpy()
+            gnp = np.ascontiguousarray(gi.cpu().numpy())
+            lo, hi = (rank * R) // world, ((rank + 1) * R) // world
+            for g in range(world):
+                grecs = ogen(seed, g * n + r0, r1 - r0)
+                for m in range(mg):
+                    a, b = m * rpm, min(r1 - r0, (m + 1) * rpm)
+                    d, _, ix, _ = O.write_map(opart, grecs[a * rs:b * rs], rs)
+                    for p in range(lo, hi):
+                        off = lib.sux_plan_block_offset(world, rank, mg, R, gnp.ctypes.data,
+                                                        g, m, p)
+                        want = d[ix[p]:ix[p + 1]]
+                        if off < 0 or got[off:off + len(want)].tobytes() != want.tobytes():
+                            raise RuntimeError(f"verify: rank {rank} group {j} source {g} "
+                                               f"map {m} partition {p} differs")
+            verified[0] += 1
+
+        verified = [0]
 
         def step():
             for k in range(groups):
@@ -521,7 +591,14 @@ def main():
     map_ms = kt["hist"][1] + kt["scan"][1] + kt["scatter"][1]
     map_alg = (2 * n * rs + 8 * (R + 1) * maps) * args.steps
     map_side = map_alg / (map_ms / 1e3) / 1e9 if map_ms else None
-    traffic = load_traffic("k_scatter")
+    names = {k: node.kernel_variant(i) for i, k in enumerate(N.KERNELS)}
+    tr = {k: load_traffic(args.workload, names[k]) for k in ("hist", "scatter") if names[k]}
+    sc_tr = tr.get("scatter")
+    traffic = round(sc_tr["bytes_per_record"] * recs_per_launch) if sc_tr else None
+    map_traffic = None
+    if sc_tr and (tr.get("hist") or names["hist"] == ""):  # one-pass kernels have no K1
+        per_rec = sc_tr["bytes_per_record"] + (tr["hist"]["bytes_per_record"] if tr.get("hist") else 0)
+        map_traffic = round(per_rec * n)  # per step; the scans' few KB per map are left out
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
@@ -540,13 +617,17 @@ def main():
         "roofline": {"bound": "hbm", "achieved": None if achieved is None else round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": None if achieved is None else round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "kernel": "k_scatter",
+                     "traffic": traffic, "kernel": names["scatter"],
+                     "traffic_source": sc_tr["source"] if sc_tr else None,
                      "alg_bytes_per_launch": int(alg),
                      "avg_launch_ms": round(sc_avg * 1e3, 4)},
         "roofline_map_side": {"bound": "hbm",
                               "achieved": None if map_side is None else round(map_side, 1),
                               "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": None if map_side is None else round(map_side / HBM_PEAK_GBS, 4),
+                              "traffic_per_step": map_traffic,
+                              "alg_bytes_per_step": int(map_alg / args.steps),
+                              "kernels": names,
                               "kernels_ms": {k: round(v[1], 3) for k, v in kt.items()},
                               "launches": {k: v[0] for k, v in kt.items()}},
         "cpu_baseline": None,
@@ -568,6 +649,8 @@ def main():
         remote *= args.steps
         peak = (world - 1) * XGMI_LINK_GBS
         ach = remote / (xms / 1e3) / 1e9 if xms and remote else None
+        if args.verify:
+            result["verified_groups"] = verified[0]
         result["roofline_exchange"] = {
             "bound": "xgmi", "achieved": None if ach is None else round(ach, 1), "peak": peak,
             "unit": "GB/s", "frac": None if ach is None else round(ach / peak, 4),

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define SUX_ABI_VERSION 1
+#define SUX_ABI_VERSION 2
 
 /* ---- status codes ---------------------------------------------------------------------- */
 #define SUX_OK 0
@@ -79,10 +79,22 @@ typedef struct sux_conf {
   uint64_t min_buffer_size;     /* spark.shuffle.ucx.memory.minBufferSize (UcxShuffleConf.scala:66-72) */
   uint64_t min_allocation_size; /* spark.shuffle.ucx.memory.minAllocationSize (:74-81)         */
   uint64_t metadata_block_size; /* 2*spark.shuffle.ucx.rkeySize (:32-40): directory slot bytes */
+  /* spark.shuffle.ucx.memory.preAllocateBuffers (UcxShuffleConf.scala:52-64): num_prealloc
+   * (size, count) pairs preallocated in the device pool when an executor node starts
+   * (MemoryPool.preAlocate, MemoryPool.java:170-176, called for executors only at UcxNode.java:81-83). */
+  uint32_t num_prealloc;
+  uint32_t reserved0;
+  uint64_t prealloc_size[16];
+  uint64_t prealloc_count[16];
 } sux_conf;
+#define SUX_MAX_PREALLOC 16
 
-/* Fill defaults (UcxShuffleConf.scala:17-90): 1 KiB min buffer, 4 MiB min allocation, 300 B slot. */
+/* Fill defaults (UcxShuffleConf.scala:17-90): 1 KiB min buffer, 4 MiB min allocation, 300 B slot,
+ * nothing preallocated. */
 void sux_conf_init(sux_conf* conf);
+/* Parse Spark's preAllocateBuffers string ("4k:1000,16k:500": Utils.byteStringAsBytes sizes,
+ * decimal counts; "" = none) into conf->prealloc_*.  SUX_EINVAL on a malformed entry. */
+int sux_conf_set_prealloc(sux_conf* conf, const char* spec);
 
 int sux_abi_version(void);
 /* Message of the last failed call on this thread; returns the full length. */
@@ -95,6 +107,22 @@ int sux_comm_unique_id(uint8_t out[128]);
 
 int sux_node_create(const sux_conf* conf, int is_driver, sux_node** out);
 int sux_node_destroy(sux_node* node);
+
+/* Host all-gather supplied by the embedding runtime (Spark RPC through the driver in a JVM; a
+ * torch.distributed store or gloo group in tests): every rank of the node's group passes `bytes`
+ * bytes in `send`; on return `recv` holds world_size * bytes, rank r's bytes at r * bytes.  It is
+ * the control plane the reference builds from UCX tag messages (UcxNode.startExecutor,
+ * UcxNode.java:130-145; RpcConnectionCallback.java:47-89).  Return 0 on success.  With a
+ * bootstrap and no RCCL communicator, sux_exchange moves the blocks by one-sided pulls from the
+ * owners' device memory over HIP IPC (xGMI peer reads) — the GET model of the reference — so the
+ * exchange also runs where RCCL cannot (several ranks on one GPU). */
+typedef int (*sux_allgather_fn)(void* ctx, const void* send, uint64_t bytes, void* recv);
+int sux_node_set_bootstrap(sux_node* node, sux_allgather_fn fn, void* ctx);
+
+/* Device pool counters (MemoryPool's close-time stats, MemoryPool.java:30-39): bytes held in
+ * device allocations, get() requests, allocations made, preallocated slabs. */
+int sux_pool_stats(sux_node* node, uint64_t* allocated_bytes, uint64_t* requests, uint64_t* allocs,
+                   uint64_t* preallocs);
 
 /* ---- partitioner object: P1 (UcxShuffleManager.getWriter picks the writer, :36-50) ---------- */
 int sux_partitioner_create(sux_node* node, const sux_partitioner_desc* desc, sux_partitioner** out);
@@ -262,6 +290,20 @@ int sux_unregister_shuffle(sux_node* node, int32_t shuffle_id);
 int sux_write_map_output(sux_node* node, int32_t shuffle_id, int32_t map_index,
                          const sux_partitioner* part, const void* d_records, uint64_t num_records,
                          void* stream);
+/* The same for `num_records` records forming consecutive map tasks first_map_index,
+ * first_map_index + 1, ... of `records_per_map` records each (the last may be shorter): one
+ * launch group, no host wait.  Each map's index is published in its directory slot when the
+ * node next makes progress after the kernels completed (any later call on the shuffle, or
+ * sux_wait_map_outputs), the analog of the reference's completion callbacks running inside
+ * worker.progress() on the calling thread (UcxWorkerWrapper.scala:100-120).  A map already
+ * committed or being written is skipped (first commit wins); d_records must stay valid until
+ * the stream reaches the work.  sux_write_map_output is this call for one map plus the wait
+ * for it (CommonUcxShuffleBlockResolver.scala:101-103 blocks until the map is published). */
+int sux_write_map_outputs(sux_node* node, int32_t shuffle_id, int32_t first_map_index,
+                          const sux_partitioner* part, const void* d_records,
+                          uint64_t records_per_map, uint64_t num_records, void* stream);
+/* Block until every map output enqueued for the shuffle (by any thread) is published. */
+int sux_wait_map_outputs(sux_node* node, int32_t shuffle_id);
 /* writeIndexFileAndCommit for a map output produced elsewhere: `d_data` (data_bytes, device)
  * is adopted by copy; `lengths` are R host int64 partition lengths (Spark's lengths[]). */
 int sux_commit_map_output(sux_node* node, int32_t shuffle_id, int32_t map_index,
@@ -275,8 +317,12 @@ int sux_map_output_index(sux_node* node, int32_t shuffle_id, int32_t map_index,
  * Collective over the node's group: every rank calls it after committing its map outputs.
  * Rank h receives partitions [floor(h*R/G), floor((h+1)*R/G)) of every map of every rank.
  * Replaces the driver-table GET (UcxWorkerWrapper.fetchDriverMetadataBuffer :176-196) by an
- * all-gather of index tables, and the phase-1/phase-2 GETs (UcxShuffleClient.java:50-127,
- * OnOffsetsFetchCallback.java:44-92) by ncclAllToAllv over xGMI. */
+ * all-gather of the committed maps' index tables, and the phase-1/phase-2 GETs
+ * (UcxShuffleClient.java:50-127, OnOffsetsFetchCallback.java:44-92) by grouped ncclSend/ncclRecv
+ * over xGMI (RCCL communicator) or, with a bootstrap and no communicator, by one gather-copy
+ * launch that pulls every owned range from the owners' IPC-mapped map outputs.  The receive
+ * buffer is sized exactly from the gathered index tables; it returns when this rank's blocks are
+ * in place and every rank has finished reading (so owners may unregister afterwards). */
 int sux_exchange(sux_node* node, int32_t shuffle_id, void* stream);
 /* Reduce-partition ownership of a rank: [*start, *end). */
 int sux_owned_partitions(sux_node* node, int32_t shuffle_id, int32_t rank, int32_t* start,
@@ -317,8 +363,9 @@ int sux_buffer_release(sux_buffer* buf);
  * 10-byte keys); SUX_SORT_LONG / SUX_SORT_INT = signed little-endian int64 / int32 (Spark's
  * LongType / IntegerType orderings).  Workspace: sux_sort_workspace_size (about 32 B/record).
  * The call waits on `stream` once, after the key pass, to read back which key bits vary (24
- * bytes): digit passes over bits that never vary are skipped, so it cannot be captured into a
- * HIP graph.  The output is complete when the stream's later work runs. */
+ * bytes): digit passes over bits that never vary are skipped.  While `stream` is being captured
+ * into a HIP graph the call does not wait and runs every digit pass (same bytes), so it can be
+ * captured.  The output is complete when the stream's later work runs. */
 #define SUX_SORT_BYTES 1
 #define SUX_SORT_LONG 2
 #define SUX_SORT_INT 3
@@ -353,6 +400,9 @@ int sux_stream_destroy(sux_node* node, void* stream);
  * 0=hist 1=scan 2=scatter 3=gather-copy (order fixed), and resets them. */
 int sux_set_kernel_timing(sux_node* node, int enable);
 int sux_kernel_times(sux_node* node, int64_t* launches, double* total_ms, int32_t nkernels);
+/* Name of the kernel variant the node last launched for slot 0..3 (e.g. "k_scatter7"), so that a
+ * measurement can be matched with the PMC profile of the kernel that actually ran; "" if none. */
+int sux_kernel_variant(sux_node* node, int32_t slot, char* buf, size_t len);
 
 /* ---- synthetic inputs (counter-based; identical bytes to oracle/oracle.c) --------------- */
 #define SUX_GEN_TERASORT 1 /* 100-byte records: 10-byte key + row id + filler                  */

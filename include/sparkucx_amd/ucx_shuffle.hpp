@@ -97,6 +97,8 @@ class UcxShuffleConf {
     return bare ? (std::stoull(v) << 20) : byteStringAsBytes(v);
   }
   bool useOdp() const { return get(ucx("memory.useOdp"), "false") == "true"; }
+  // :52-64 — "size:count" pairs preallocated by executors (MemoryPool.preAlocate)
+  std::string preAllocateBuffers() const { return get(ucx("memory.preAllocateBuffers"), ""); }
   // GPU extension keys (spark.shuffle.ucx.gpu.*)
   int device() const { return std::stoi(get(ucx("gpu.device"), "0")); }
   int rank() const { return std::stoi(get(ucx("gpu.rank"), "0")); }
@@ -111,6 +113,7 @@ class UcxShuffleConf {
     c.min_buffer_size = minBufferSize();
     c.min_allocation_size = minRegistrationSize();
     c.metadata_block_size = metadataBlockSize();
+    check(sux_conf_set_prealloc(&c, preAllocateBuffers().c_str()), "preAllocateBuffers");
     return c;
   }
 

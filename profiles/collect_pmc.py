@@ -2,10 +2,14 @@
 
 Run ON THE GPU BOX (it spawns `rocprofv3 --pmc ... -- python3 bench.py ...`, one pass each):
 
-    python3 profiles/collect_pmc.py --out gpurun_out/pmc [--tag r01] [bench args...]
+    python3 profiles/collect_pmc.py --out gpurun_out/pmc --workload terasort [bench args...]
+    python3 profiles/collect_pmc.py --merge gpurun_out/pmc --tag r02      (on the CPU side)
 
-Summary: profiles/pmc_<tag>.json with, per kernel, the mean of every counter per dispatch and
-the HBM bytes per launch computed as the MI355X guide prescribes (MI355X_MICROARCH.md §HBM):
+The first form writes <out>/<workload>/summary.json; --merge folds every workload's summary into
+profiles/pmc_<tag>.json = {"workloads": {workload: {"bench_args", "records_per_launch",
+"kernels": {kernel: {...}}}}}, the file bench.py reads its `traffic` from (keyed by workload and
+by the kernel the library reports it launched).  Per kernel: the mean of every counter per
+dispatch and the HBM bytes per launch computed as the MI355X guide prescribes (MI355X_MICROARCH.md §HBM):
 FETCH_SIZE (KiB) is doubled — on gfx950 it reports half the bytes of a wide streaming read —
 and WRITE_SIZE (KiB) is taken as is; FETCH_SIZE and WRITE_SIZE need separate passes (TCC slots).
 This script never imports torch and never touches the GPU itself.
@@ -33,15 +37,22 @@ PASSES = [
     ["TCC_HIT_sum", "TCC_MISS_sum"],
 ]
 KERNELS = {"k_hist": "hist", "k_scatter": "scatter", "k_tile_scan": "tile_scan",
-           "k_group_scan": "group_scan", "k_gather_copy": "copy"}
+           "k_map_scan": "map_scan", "k_onepass": "onepass", "k_sweep": "sweep",
+           "k_gather_copy": "copy"}
+WORKLOAD_ARGS = {  # one PMC run: 8 launch groups of the bench's default shape per workload
+    "terasort": ["--workload", "terasort", "--records", str(8 * 32 * (1 << 20))],
+    "zipf": ["--workload", "zipf", "--records", str(8 * 32 * (1 << 20))],
+    "small": ["--workload", "small", "--records", str(8 * 32 * (1 << 20))],
+}
+COMMON = ["--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--varlen-rows", "0",
+          "--compress-maps", "0", "--file-maps", "0", "--reduce-sort-records", "0"]
 
 
 def short(name: str) -> str | None:
+    """Kernel base name ('k_scatter7'), the name sux_kernel_variant reports."""
     for k in KERNELS:
         if k in name:
-            # keep the template signature (v1/v2 variants) in the key
-            base = name.split("(")[0].replace("void ", "").replace("sux::", "")
-            return base
+            return name.split("(")[0].replace("void ", "").replace("sux::", "").split("<")[0]
     return None
 
 
@@ -92,36 +103,40 @@ def summarize(dirs):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="gpurun_out/pmc")
-    ap.add_argument("--tag", default="r01")
-    ap.add_argument("--summarize-only", action="store_true")
-    a, bench_args = ap.parse_known_args()
-    if not bench_args:
-        bench_args = ["--steps", "1", "--warmup", "1", "--records", "268435456",
-                      "--no-cpu-baseline", "--varlen-rows", "0", "--compress-maps", "0",
-                      "--file-maps", "0", "--reduce-sort-records", "0"]
-    os.makedirs(a.out, exist_ok=True)
-    dirs = []
-    for i, cs in enumerate(PASSES):
-        d = os.path.join(a.out, f"pass{i}")
-        if not a.summarize_only:
-            run_pass(cs, a.out, bench_args, i)
-        dirs.append(d)
+    ap.add_argument("--workload", default="terasort", choices=sorted(WORKLOAD_ARGS))
+    ap.add_argument("--tag", default="r02")
+    ap.add_argument("--merge", default=None, help="fold <dir>/*/summary.json into profiles/pmc_<tag>.json")
+    a, extra = ap.parse_known_args()
+    if a.merge:
+        path = os.path.join(ROOT, "profiles", f"pmc_{a.tag}.json")
+        merged = {"note": "per-dispatch means; hbm bytes = 2*FETCH_SIZE + WRITE_SIZE (KiB->B), "
+                          "MI355X_MICROARCH.md §HBM; written by profiles/collect_pmc.py",
+                  "workloads": {}}
+        if os.path.exists(path):
+            with open(path) as f:
+                merged["workloads"].update(json.load(f).get("workloads", {}))
+        for f in sorted(glob.glob(os.path.join(a.merge, "*", "summary.json"))):
+            with open(f) as fh:
+                sm = json.load(fh)
+            merged["workloads"][sm["workload"]] = sm
+        with open(path, "w") as f:
+            json.dump(merged, f, indent=1, sort_keys=True)
+        print("wrote", path, sorted(merged["workloads"]))
+        return
+    bench_args = WORKLOAD_ARGS[a.workload] + COMMON + extra
+    out = os.path.join(a.out, a.workload)
+    os.makedirs(out, exist_ok=True)
+    dirs = [run_pass(cs, out, bench_args, i) for i, cs in enumerate(PASSES)]
     res = summarize(dirs)
-    summary = {"bench_args": bench_args, "note": "per-dispatch means; hbm bytes = 2*FETCH_SIZE + "
-               "WRITE_SIZE (KiB->B), MI355X_MICROARCH.md §HBM", "kernels": res}
-    # bench.py reads the map-side scatter entry under the plain name (the default k_scatter7,
-    # never the reduce-sort's k_scatter16 if that leg ran)
-    for pref in ("k_scatter7", "k_scatter6", "k_scatter"):
-        hit = [k for k in res if k.startswith(pref) and not k.startswith("k_scatter16")]
-        if hit:
-            summary["kernels"]["k_scatter"] = res[hit[0]]
-            summary["k_scatter_is"] = hit[0]
-            break
-    path = os.path.join(ROOT, "profiles", f"pmc_{a.tag}.json")
-    with open(os.path.join(a.out, f"pmc_{a.tag}.json"), "w") as f:
+    gm = int(bench_args[bench_args.index("--group-maps") + 1]) if "--group-maps" in bench_args else 32
+    rpm = int(bench_args[bench_args.index("--map-records") + 1]) if "--map-records" in bench_args else 1 << 20
+    for e in res.values():
+        e["records_per_launch"] = gm * rpm
+    summary = {"workload": a.workload, "bench_args": bench_args, "records_per_launch": gm * rpm,
+               "kernels": res}
+    with open(os.path.join(out, "summary.json"), "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
     print(json.dumps(summary, indent=1, sort_keys=True))
-    print("wrote", os.path.join(a.out, f"pmc_{a.tag}.json"), "(copy to", path, "to commit)")
 
 
 if __name__ == "__main__":

@@ -15,6 +15,8 @@
 #include <cerrno>
 #include <cstdio>
 #include <atomic>
+#include <climits>
+#include <condition_variable>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -84,6 +86,7 @@ struct Timer {
   std::vector<Rec> recs;
   std::vector<hipEvent_t> spare;
   hipEvent_t open[kNumSlots] = {};
+  const char* variant[kNumSlots] = {};
 
   hipEvent_t get() {
     if (!spare.empty()) {
@@ -110,6 +113,12 @@ void timer_begin(Timer* t, int slot, hipStream_t s) {
   hipEvent_t e = t->get();
   (void)hipEventRecord(e, s);
   t->open[slot] = e;
+}
+
+void timer_note(Timer* t, int slot, const char* kernel) {
+  if (!t || slot < 0 || slot >= kNumSlots) return;
+  std::lock_guard<std::mutex> lk(t->mu);
+  t->variant[slot] = kernel;
 }
 
 void timer_end(Timer* t, int slot, hipStream_t s) {
@@ -139,9 +148,12 @@ class DevicePool {
     for (void* p : allocations_) (void)hipFree(p);
   }
 
-  // MemoryPool.roundUpToTheNextPowerOf2 (:137-151)
+  // MemoryPool.roundUpToTheNextPowerOf2 (:137-151) up to minAllocationSize.  Above it the class
+  // is the next multiple of minAllocationSize (deliberate divergence: map outputs and receive
+  // buffers run to GBs, where power-of-two classes would leave up to half of the HBM idle).
   uint64_t size_class(uint64_t n) const {
     if (n < min_buf_) return min_buf_;
+    if (n > min_alloc_) return (n + min_alloc_ - 1) / min_alloc_ * min_alloc_;
     uint64_t c = 1;
     while (c < n) c <<= 1;
     return c;
@@ -154,6 +166,7 @@ class DevicePool {
     std::lock_guard<std::mutex> lk(mu_);
     auto& st = stacks_[cls];
     st.requests++;
+    requests_++;
     if (st.free.empty()) {
       if (cls < min_alloc_) {
         uint64_t count = min_alloc_ / cls;
@@ -177,12 +190,38 @@ class DevicePool {
     stacks_[b.cap].free.push_back(b);
   }
 
+  // AllocatorStack.preallocate (:89-114): `count` buffers of one class in ONE allocation, the
+  // total capped below 2^31 bytes like the reference's direct-buffer limit.  The class is the
+  // size rounded as get() rounds it (the reference keys the stack by the raw size, so a size
+  // that is not a power of two is never handed out again; here it is).
+  void preallocate(uint64_t size, uint64_t count) {
+    const uint64_t cls = size_class(size ? size : 1);
+    if (cls * count > (uint64_t)INT32_MAX) count = (uint64_t)INT32_MAX / cls;
+    if (count == 0) return;
+    std::lock_guard<std::mutex> lk(mu_);
+    auto& st = stacks_[cls];
+    uint8_t* p = alloc(cls * count);
+    for (uint64_t i = 0; i < count; ++i) st.free.push_back(PoolBuf{p + i * cls, cls});
+    st.preallocs++;
+    st.allocs++;
+    preallocs_++;
+  }
+
+  void stats(uint64_t* bytes, uint64_t* requests, uint64_t* allocs, uint64_t* preallocs) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (bytes) *bytes = allocated_;
+    if (requests) *requests = requests_;
+    if (allocs) *allocs = allocations_.size();
+    if (preallocs) *preallocs = preallocs_;
+  }
+
  private:
-  uint8_t* alloc(uint64_t bytes) {
+  uint8_t* alloc(uint64_t bytes) {  // caller holds mu_
     void* p = nullptr;
     hipError_t e = hipMalloc(&p, bytes);
     if (e != hipSuccess) raise(SUX_ENOMEM, "hipMalloc(" + std::to_string(bytes) + ") failed");
     allocations_.push_back(p);
+    allocated_ += bytes;
     return static_cast<uint8_t*>(p);
   }
   struct Stack {
@@ -193,26 +232,100 @@ class DevicePool {
   std::mutex mu_;
   std::map<uint64_t, Stack> stacks_;
   std::vector<void*> allocations_;
+  uint64_t allocated_ = 0, requests_ = 0, preallocs_ = 0;
+};
+
+// Pinned host staging for index read-backs (reused; freed with the node).
+class HostPool {
+ public:
+  ~HostPool() {
+    for (auto& kv : free_)
+      for (void* p : kv.second) (void)hipHostFree(p);
+  }
+  std::pair<void*, uint64_t> get(uint64_t n) {
+    uint64_t cls = 4096;
+    while (cls < n) cls <<= 1;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      auto& v = free_[cls];
+      if (!v.empty()) {
+        void* p = v.back();
+        v.pop_back();
+        return {p, cls};
+      }
+    }
+    void* p = nullptr;
+    hip_check(hipHostMalloc(&p, cls, hipHostMallocDefault), "hipHostMalloc(index staging)");
+    return {p, cls};
+  }
+  void put(std::pair<void*, uint64_t> b) {
+    if (!b.first) return;
+    std::lock_guard<std::mutex> lk(mu_);
+    free_[b.second].push_back(b.first);
+  }
+
+ private:
+  std::mutex mu_;
+  std::map<uint64_t, std::vector<void*>> free_;
+};
+
+// A pooled device buffer shared by several map slots (one batch of map outputs); the last
+// reference returns it to the pool.
+struct Slab {
+  DevicePool* pool = nullptr;
+  PoolBuf buf;
+  Slab(DevicePool* p, PoolBuf b) : pool(p), buf(b) {}
+  ~Slab() { pool->put(buf); }
+  Slab(const Slab&) = delete;
+  Slab& operator=(const Slab&) = delete;
+};
+
+struct Event {  // one completion event, shared by a write job and a thread that waits on it
+  hipEvent_t e = nullptr;
+  Event() { hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate"); }
+  ~Event() { (void)hipEventDestroy(e); }
+  Event(const Event&) = delete;
+  Event& operator=(const Event&) = delete;
 };
 
 // per-map directory slot: the analog of the 300-byte driver descriptor (DriverMetadata,
 // UcxWorkerWrapper.scala:27-65) plus the index file it points at
 struct MapSlot {
   bool present = false;
+  bool pending = false;  // enqueued by a write job that has not completed yet
   int32_t owner = -1;
-  PoolBuf data;
+  std::shared_ptr<Slab> slab;  // local maps: the device buffer holding the data file
+  uint64_t off = 0;            // byte offset of this map's data file in the slab
   uint64_t bytes = 0;
   std::vector<int64_t> index;  // R+1 cumulative offsets (the index file, native order)
   uint64_t recv_off = 0;       // after exchange: offset of this map's owned-range blocks in recv
+  uint8_t* data() const { return slab ? slab->buf.ptr + off : nullptr; }
+};
+
+// One sux_write_map_outputs call in flight: published by progress() once `done` has fired.
+struct WriteJob {
+  int32_t first = 0;
+  uint32_t maps = 0;
+  uint64_t rpm = 0, n = 0;
+  std::vector<uint8_t> claimed;  // maps of the batch this job publishes
+  std::shared_ptr<Slab> slab;
+  PoolBuf ws;
+  std::pair<void*, uint64_t> hidx{nullptr, 0};  // pinned copy of the batch's index tables
+  std::shared_ptr<Event> done;
 };
 
 struct Shuffle {
   int32_t id = 0, num_maps = 0, R = 0, rec_size = 0;
   std::vector<MapSlot> maps;
   std::vector<uint8_t> directory;  // num_maps * metadata_block_size bytes (big-endian fields)
+  std::vector<std::unique_ptr<WriteJob>> jobs;
+  int busy = 0;        // jobs taken out of `jobs` by a thread that is waiting on them
+  int submitting = 0;  // writes that claimed slots and have not queued their job yet
   bool exchanged = false;
+  bool exchanging = false;
   PoolBuf recv;
   uint64_t recv_bytes = 0;
+  std::map<std::string, void*> ipc_bases;  // opened owner allocations (owner|handle -> base)
 };
 
 int32_t owner_lo(int32_t h, int32_t R, int32_t G) { return (int32_t)(((int64_t)h * R) / G); }
@@ -223,10 +336,14 @@ struct sux_node {
   bool is_driver = false;
   ncclComm_t comm = nullptr;
   std::unique_ptr<DevicePool> pool;
+  HostPool hpool;
   sux::Timer timer;
   std::mutex mu;
+  std::condition_variable cv;  // a write job was published (Shuffle::jobs/busy/submitting moved)
   std::map<int32_t, std::unique_ptr<Shuffle>> shuffles;
   std::map<void*, void*> ipc_bases;  // opened peer pointer -> mapped allocation base
+  sux_allgather_fn boot = nullptr;   // host all-gather of the embedding runtime
+  void* boot_ctx = nullptr;
 
   void bind() { hip_check(hipSetDevice(conf.device), "hipSetDevice"); }
 
@@ -284,20 +401,84 @@ void store_be32(uint8_t* p, uint32_t v) {
 // Descriptor of one committed map, written into its directory slot (big-endian like the
 // reference's putLong/putInt, CommonUcxShuffleBlockResolver.scala:80-87):
 // |u64 index dev addr|u64 data dev addr|i32 owner rank|i32 R|u64 data bytes| = 32 bytes
-constexpr uint64_t kSlotBytes = 32;
 
 void publish_slot(sux_node* n, Shuffle& sh, int32_t m, uint64_t index_addr) {
   MapSlot& s = sh.maps[m];
-  uint64_t blk = n->conf.metadata_block_size;
-  require(kSlotBytes <= blk, SUX_ERANGE,
-          "Metadata block size " + std::to_string(kSlotBytes) + " is greater then configured (" +
-              std::to_string(blk) + ")");
+  const uint64_t blk = n->conf.metadata_block_size;  // >= kSlotBytes (checked at node create)
   uint8_t* d = sh.directory.data() + (uint64_t)m * blk;
   store_be64(d, index_addr);
-  store_be64(d + 8, (uint64_t)(uintptr_t)s.data.ptr);
+  store_be64(d + 8, (uint64_t)(uintptr_t)s.data());
   store_be32(d + 16, (uint32_t)s.owner);
   store_be32(d + 20, (uint32_t)sh.R);
   store_be64(d + 24, s.bytes);
+}
+
+// Publish every write job of `sh` whose kernels have completed (wait = block for all of them):
+// the directory slots of its maps get their index tables.  The analog of the reference's
+// completion callbacks, which run inside worker.progress() on the calling thread
+// (UcxWorkerWrapper.scala:100-120).  Called with `lk` held; waits with it released.
+void progress(sux_node* node, Shuffle& sh, std::unique_lock<std::mutex>& lk, bool wait) {
+  while (!sh.jobs.empty()) {
+    std::vector<std::unique_ptr<WriteJob>> jobs;
+    jobs.swap(sh.jobs);
+    sh.busy += (int)jobs.size();
+    std::vector<char> done(jobs.size(), 0);
+    hipError_t err = hipSuccess;
+    lk.unlock();
+    for (size_t i = 0; i < jobs.size() && err == hipSuccess; ++i) {
+      hipError_t e = wait ? hipEventSynchronize(jobs[i]->done->e) : hipEventQuery(jobs[i]->done->e);
+      if (e == hipSuccess) done[i] = 1;
+      else if (e != hipErrorNotReady) err = e;
+    }
+    lk.lock();
+    sh.busy -= (int)jobs.size();
+    const int R = sh.R;
+    for (size_t i = 0; i < jobs.size(); ++i) {
+      WriteJob& j = *jobs[i];
+      if (!done[i]) {
+        sh.jobs.push_back(std::move(jobs[i]));
+        continue;
+      }
+      const int64_t* hx = static_cast<const int64_t*>(j.hidx.first);
+      for (uint32_t k = 0; k < j.maps; ++k) {
+        if (!j.claimed[k]) continue;
+        MapSlot& slot = sh.maps[j.first + k];
+        slot.pending = false;
+        slot.present = true;
+        slot.owner = node->conf.rank;
+        slot.slab = j.slab;
+        slot.off = (uint64_t)k * j.rpm * (uint64_t)sh.rec_size;
+        slot.bytes = (uint64_t)hx[(uint64_t)k * (R + 1) + R];
+        slot.index.assign(hx + (uint64_t)k * (R + 1), hx + (uint64_t)(k + 1) * (R + 1));
+        publish_slot(node, sh, j.first + (int32_t)k, 0);
+      }
+      sh.exchanged = false;
+      node->pool->put(j.ws);
+      node->hpool.put(j.hidx);
+      jobs[i].reset();
+    }
+    node->cv.notify_all();
+    hip_check(err, "map output completion");
+    if (!wait) return;
+  }
+}
+
+// Block until no write of `sh` is queued, being waited on by another thread, or being submitted
+// (every claimed slot is published).  Called with `lk` held.
+void drain(sux_node* node, Shuffle& sh, std::unique_lock<std::mutex>& lk) {
+  while (!sh.jobs.empty() || sh.busy > 0 || sh.submitting > 0) {
+    if (!sh.jobs.empty()) progress(node, sh, lk, true);
+    else node->cv.wait(lk);
+  }
+}
+
+// Everything a shuffle holds on the device: slabs (via the slots), receive buffer, IPC mappings.
+void release_shuffle(sux_node* node, Shuffle& sh) {
+  for (auto& kv : sh.ipc_bases) (void)hipIpcCloseMemHandle(kv.second);
+  sh.ipc_bases.clear();
+  for (auto& m : sh.maps) m.slab.reset();
+  node->pool->put(sh.recv);
+  sh.recv = PoolBuf{};
 }
 
 struct Group {
@@ -361,6 +542,56 @@ void sux_conf_init(sux_conf* c) {
   c->metadata_block_size = 2 * 150;          // 2 * spark.shuffle.ucx.rkeySize
 }
 
+// UcxShuffleConf.preallocateBuffersMap (:56-64): "size:count" pairs, comma separated, sizes in
+// Utils.byteStringAsBytes notation (binary multiples), empty entries skipped.
+int sux_conf_set_prealloc(sux_conf* c, const char* spec) {
+  return guard([&] {
+    require(c && spec, SUX_EINVAL, "NULL argument");
+    std::vector<std::pair<uint64_t, uint64_t>> out;
+    std::string all(spec);
+    size_t b = 0;
+    while (b <= all.size()) {
+      size_t e = all.find(',', b);
+      if (e == std::string::npos) e = all.size();
+      std::string ent = all.substr(b, e - b);
+      b = e + 1;
+      auto trim = [](std::string x) {
+        size_t i = x.find_first_not_of(" \t"), j = x.find_last_not_of(" \t");
+        return i == std::string::npos ? std::string() : x.substr(i, j - i + 1);
+      };
+      ent = trim(ent);
+      if (ent.empty()) continue;
+      const size_t colon = ent.find(':');
+      require(colon != std::string::npos && ent.find(':', colon + 1) == std::string::npos,
+              SUX_EINVAL, "preAllocateBuffers entry '" + ent + "' is not size:count");
+      std::string sz = trim(ent.substr(0, colon)), ct = trim(ent.substr(colon + 1));
+      size_t i = 0;
+      while (i < sz.size() && std::isdigit((unsigned char)sz[i])) ++i;
+      require(i > 0, SUX_EINVAL, "bad buffer size '" + sz + "'");
+      uint64_t v = std::stoull(sz.substr(0, i));
+      std::string suf = sz.substr(i);
+      for (auto& ch : suf) ch = (char)std::tolower((unsigned char)ch);
+      int sh = -1;
+      if (suf.empty() || suf == "b") sh = 0;
+      else if (suf == "k" || suf == "kb") sh = 10;
+      else if (suf == "m" || suf == "mb") sh = 20;
+      else if (suf == "g" || suf == "gb") sh = 30;
+      else if (suf == "t" || suf == "tb") sh = 40;
+      require(sh >= 0, SUX_EINVAL, "bad buffer size '" + sz + "'");
+      require(!ct.empty() && ct.find_first_not_of("0123456789") == std::string::npos, SUX_EINVAL,
+              "bad buffer count '" + ct + "'");
+      out.emplace_back(v << sh, std::stoull(ct));
+    }
+    require(out.size() <= SUX_MAX_PREALLOC, SUX_EINVAL,
+            "at most " + std::to_string(SUX_MAX_PREALLOC) + " preAllocateBuffers entries");
+    c->num_prealloc = (uint32_t)out.size();
+    for (size_t k = 0; k < out.size(); ++k) {
+      c->prealloc_size[k] = out[k].first;
+      c->prealloc_count[k] = out[k].second;
+    }
+  });
+}
+
 int sux_abi_version(void) { return SUX_ABI_VERSION; }
 
 int sux_last_error(char* buf, size_t len) {
@@ -389,6 +620,12 @@ int sux_node_create(const sux_conf* conf, int is_driver, sux_node** out) {
             "rank/world_size out of range");
     require(conf->min_buffer_size > 0 && conf->min_allocation_size > 0, SUX_EINVAL,
             "pool sizes must be positive");
+    require(conf->num_prealloc <= SUX_MAX_PREALLOC, SUX_EINVAL, "num_prealloc out of range");
+    // every directory slot holds one 32-byte descriptor (publish_slot); the reference throws
+    // the same way when its descriptor outgrows the slot (CommonUcxShuffleBlockResolver.scala:72-76)
+    require(conf->metadata_block_size >= 32, SUX_ERANGE,
+            "Metadata block size 32 is greater then configured (" +
+                std::to_string(conf->metadata_block_size) + ")");
     int ndev = 0;
     hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
     require(conf->device >= 0 && conf->device < ndev, SUX_EINVAL,
@@ -399,11 +636,15 @@ int sux_node_create(const sux_conf* conf, int is_driver, sux_node** out) {
     n->is_driver = is_driver != 0;
     n->bind();
     n->pool = std::make_unique<DevicePool>(conf->min_buffer_size, conf->min_allocation_size);
+    // UcxNode.java:81-83: executors preallocate the configured buffers
+    if (!n->is_driver)
+      for (uint32_t k = 0; k < conf->num_prealloc; ++k)
+        n->pool->preallocate(conf->prealloc_size[k], conf->prealloc_count[k]);
     // a communicator for world_size > 1, or at world_size 1 when a unique id is supplied (the
     // exchange then runs through RCCL with one rank: the single-GPU rehearsal of the N > 1 path)
     bool have_id = false;
     for (int i = 0; i < 128; ++i) have_id |= conf->comm_id[i] != 0;
-    if (conf->world_size > 1 || have_id) {
+    if (have_id) {
       ncclUniqueId id;
       std::memcpy(&id, conf->comm_id, 128);
       nccl_check(ncclCommInitRank(&n->comm, conf->world_size, id, conf->rank), "ncclCommInitRank");
@@ -412,16 +653,35 @@ int sux_node_create(const sux_conf* conf, int is_driver, sux_node** out) {
   });
 }
 
+int sux_node_set_bootstrap(sux_node* node, sux_allgather_fn fn, void* ctx) {
+  return guard([&] {
+    require(node, SUX_EINVAL, "NULL node");
+    std::lock_guard<std::mutex> lk(node->mu);
+    node->boot = fn;
+    node->boot_ctx = ctx;
+  });
+}
+
+int sux_pool_stats(sux_node* node, uint64_t* bytes, uint64_t* requests, uint64_t* allocs,
+                   uint64_t* preallocs) {
+  return guard([&] {
+    require(node, SUX_EINVAL, "NULL node");
+    node->pool->stats(bytes, requests, allocs, preallocs);
+  });
+}
+
 int sux_node_destroy(sux_node* node) {
   return guard([&] {
     if (!node) return;
     node->bind();
-    (void)hipDeviceSynchronize();
-    for (auto& kv : node->shuffles) {
-      for (auto& m : kv.second->maps) node->pool->put(m.data);
-      node->pool->put(kv.second->recv);
+    {
+      std::unique_lock<std::mutex> lk(node->mu);
+      for (auto& kv : node->shuffles) drain(node, *kv.second, lk);
     }
+    (void)hipDeviceSynchronize();
+    for (auto& kv : node->shuffles) release_shuffle(node, *kv.second);
     node->shuffles.clear();
+    for (auto& kv : node->ipc_bases) (void)hipIpcCloseMemHandle(kv.second);
     if (node->comm) (void)ncclCommDestroy(node->comm);
     delete node;
   });
@@ -1160,71 +1420,143 @@ int sux_unregister_shuffle(sux_node* node, int32_t shuffle_id) {
   return guard([&] {
     require(node, SUX_EINVAL, "NULL node");
     node->bind();
+    std::unique_ptr<Shuffle> gone;
+    {
+      std::unique_lock<std::mutex> lk(node->mu);
+      Shuffle& sh = node->shuffle(shuffle_id);
+      require(!sh.exchanging, SUX_ESTATE, "shuffle " + std::to_string(shuffle_id) + " is exchanging");
+      drain(node, sh, lk);  // writes in flight finish before their slabs go back
+      gone = std::move(node->shuffles[shuffle_id]);
+      node->shuffles.erase(shuffle_id);
+    }
+    // no lock held: readers of this shuffle's buffers are ordered before this call by the
+    // caller (CommonUcxShuffleBlockResolver.removeShuffle runs after the stage)
+    hip_check(hipDeviceSynchronize(), "sync before unregister");
+    release_shuffle(node, *gone);
+  });
+}
+
+int sux_write_map_outputs(sux_node* node, int32_t shuffle_id, int32_t first,
+                          const sux_partitioner* part, const void* d_records, uint64_t rpm,
+                          uint64_t n, void* stream) {
+  return guard([&] {
+    require(node && part, SUX_EINVAL, "NULL node/partitioner");
+    require(d_records || n == 0, SUX_EINVAL, "records pointer is NULL");
+    require(rpm > 0, SUX_EINVAL, "records_per_map must be > 0");
+    node->bind();
+    hipStream_t s = node->stream(stream);
+    const uint64_t maps = (n + rpm - 1) / rpm;
+    auto job = std::make_unique<WriteJob>();
+    int R = 0;
+    uint32_t rs = 0;
+    {
+      std::unique_lock<std::mutex> lk(node->mu);
+      Shuffle& sh = node->shuffle(shuffle_id);
+      require(first >= 0 && (uint64_t)first + maps <= (uint64_t)sh.num_maps, SUX_EINVAL,
+              "maps [" + std::to_string(first) + ", " + std::to_string((uint64_t)first + maps) +
+                  ") out of [0, " + std::to_string(sh.num_maps) + ")");
+      require(part->desc.num_partitions == sh.R, SUX_EINVAL,
+              "partitioner has " + std::to_string(part->desc.num_partitions) +
+                  " partitions, shuffle has " + std::to_string(sh.R));
+      progress(node, sh, lk, false);
+      R = sh.R;
+      rs = (uint32_t)sh.rec_size;
+      // UcxShuffleBlockResolver.scala:42-45: an empty data file publishes nothing;
+      // IndexShuffleBlockResolver [ext]: a map another attempt committed (or is writing) keeps
+      // the first commit
+      job->claimed.assign((size_t)maps, 0);
+      bool any = false;
+      for (uint64_t k = 0; k < maps; ++k) {
+        MapSlot& sl = sh.maps[first + k];
+        if (sl.present || sl.pending) continue;
+        sl.pending = true;
+        job->claimed[k] = 1;
+        any = true;
+      }
+      if (!any) return;
+      sh.submitting++;
+    }
+    job->first = first;
+    job->maps = (uint32_t)maps;
+    job->rpm = rpm;
+    job->n = n;
+    auto unclaim = [&] {  // a failed launch leaves the maps writable again
+      std::lock_guard<std::mutex> lk(node->mu);
+      auto it = node->shuffles.find(shuffle_id);
+      if (it != node->shuffles.end()) {
+        for (uint64_t k = 0; k < maps; ++k)
+          if (job->claimed[k]) it->second->maps[first + k].pending = false;
+        it->second->submitting--;
+      }
+      node->cv.notify_all();
+    };
+    try {
+      Group G = make_group(part, d_records, rs, rpm, n);
+      job->slab = std::make_shared<Slab>(node->pool.get(), node->pool->get(n * rs));
+      job->ws = node->pool->get(G.ws.total + 8 * maps * (uint64_t)(R + 1) + 256);
+      int64_t* d_idx = reinterpret_cast<int64_t*>(job->ws.ptr + (G.ws.total + 255) / 256 * 256);
+      job->hidx = node->hpool.get(8 * maps * (uint64_t)(R + 1));
+      run_group(node, part, G, 1, job->slab->buf.ptr, d_idx, nullptr, nullptr, nullptr,
+                job->ws.ptr, G.ws.total, s);
+      hip_check(hipMemcpyAsync(job->hidx.first, d_idx, 8 * maps * (uint64_t)(R + 1),
+                               hipMemcpyDeviceToHost, s),
+                "D2H index");
+      job->done = std::make_shared<Event>();
+      hip_check(hipEventRecord(job->done->e, s), "hipEventRecord");
+    } catch (...) {
+      unclaim();
+      if (!job->done) {  // nothing reached the stream that still needs the buffers
+        node->pool->put(job->ws);
+        node->hpool.put(job->hidx);
+      } else {
+        (void)hipStreamSynchronize(s);
+        node->pool->put(job->ws);
+        node->hpool.put(job->hidx);
+      }
+      throw;
+    }
     std::lock_guard<std::mutex> lk(node->mu);
     auto it = node->shuffles.find(shuffle_id);
-    require(it != node->shuffles.end(), SUX_ENOENT, "unknown shuffle " + std::to_string(shuffle_id));
-    hip_check(hipDeviceSynchronize(), "sync before unregister");
-    for (auto& m : it->second->maps) node->pool->put(m.data);
-    node->pool->put(it->second->recv);
-    node->shuffles.erase(it);
+    require(it != node->shuffles.end(), SUX_ENOENT, "shuffle unregistered during the write");
+    it->second->jobs.push_back(std::move(job));
+    it->second->submitting--;
+    node->cv.notify_all();
+  });
+}
+
+int sux_wait_map_outputs(sux_node* node, int32_t shuffle_id) {
+  return guard([&] {
+    require(node, SUX_EINVAL, "NULL node");
+    node->bind();
+    std::unique_lock<std::mutex> lk(node->mu);
+    drain(node, node->shuffle(shuffle_id), lk);
   });
 }
 
 int sux_write_map_output(sux_node* node, int32_t shuffle_id, int32_t map_index,
                          const sux_partitioner* part, const void* d_records, uint64_t n,
                          void* stream) {
+  int rc = SUX_OK;
+  if (n == 0) {  // UcxShuffleBlockResolver.scala:42-45; still validates the arguments
+    return guard([&] {
+      require(node && part, SUX_EINVAL, "NULL node/partitioner");
+      std::lock_guard<std::mutex> lk(node->mu);
+      Shuffle& sh = node->shuffle(shuffle_id);
+      require(map_index >= 0 && map_index < sh.num_maps, SUX_EINVAL,
+              "map index " + std::to_string(map_index) + " out of [0, " +
+                  std::to_string(sh.num_maps) + ")");
+    });
+  }
+  rc = sux_write_map_outputs(node, shuffle_id, map_index, part, d_records, n, n, stream);
+  if (rc != SUX_OK) return rc;
+  // CommonUcxShuffleBlockResolver.scala:101-103: block until the map output is published
   return guard([&] {
-    require(node && part, SUX_EINVAL, "NULL node/partitioner");
-    node->bind();
-    hipStream_t s = node->stream(stream);
     std::unique_lock<std::mutex> lk(node->mu);
     Shuffle& sh = node->shuffle(shuffle_id);
-    require(map_index >= 0 && map_index < sh.num_maps, SUX_EINVAL,
-            "map index " + std::to_string(map_index) + " out of [0, " +
-                std::to_string(sh.num_maps) + ")");
-    require(part->desc.num_partitions == sh.R, SUX_EINVAL,
-            "partitioner has " + std::to_string(part->desc.num_partitions) +
-                " partitions, shuffle has " + std::to_string(sh.R));
-    const int R = sh.R;
-    const uint32_t rs = (uint32_t)sh.rec_size;
-    // UcxShuffleBlockResolver.scala:42-45: an empty data file publishes nothing
-    if (n == 0) return;
-    // IndexShuffleBlockResolver [ext]: another attempt already committed -> keep the first
-    if (sh.maps[map_index].present) return;
-    lk.unlock();
-    Group G = make_group(part, d_records, rs, n, n);
-    PoolBuf data = node->pool->get(n * rs);
-    PoolBuf ws = node->pool->get(G.ws.total);
-    PoolBuf idx = node->pool->get(8 * (uint64_t)(R + 1));
-    std::vector<int64_t> host((size_t)R + 1);
-    try {
-      run_group(node, part, G, 1, data.ptr, reinterpret_cast<int64_t*>(idx.ptr), nullptr, nullptr,
-                nullptr, ws.ptr, ws.cap, s);
-      hip_check(hipMemcpyAsync(host.data(), idx.ptr, host.size() * 8, hipMemcpyDeviceToHost, s),
-                "D2H index");
-      // CommonUcxShuffleBlockResolver.scala:101-103: block until the map output is published
-      hip_check(hipStreamSynchronize(s), "sync map output");
-    } catch (...) {
-      node->pool->put(data);
-      node->pool->put(ws);
-      node->pool->put(idx);
-      throw;
+    while (sh.maps[map_index].pending) {
+      if (!sh.jobs.empty()) progress(node, sh, lk, true);
+      else node->cv.wait(lk);
     }
-    node->pool->put(ws);
-    node->pool->put(idx);
-    lk.lock();
-    MapSlot& slot = sh.maps[map_index];
-    if (slot.present) {  // lost a race with another attempt
-      node->pool->put(data);
-      return;
-    }
-    slot.present = true;
-    slot.owner = node->conf.rank;
-    slot.data = data;
-    slot.bytes = n * rs;
-    slot.index = std::move(host);
-    sh.exchanged = false;
-    publish_slot(node, sh, map_index, 0);
   });
 }
 
@@ -1235,28 +1567,53 @@ int sux_commit_map_output(sux_node* node, int32_t shuffle_id, int32_t map_index,
     require(node && lengths, SUX_EINVAL, "NULL argument");
     node->bind();
     hipStream_t s = node->stream(stream);
+    std::vector<int64_t> index;
+    {
+      std::unique_lock<std::mutex> lk(node->mu);
+      Shuffle& sh = node->shuffle(shuffle_id);
+      require(map_index >= 0 && map_index < sh.num_maps, SUX_EINVAL, "map index out of range");
+      index.resize((size_t)sh.R + 1);
+      int64_t acc = 0;
+      for (int r = 0; r < sh.R; ++r) {
+        require(lengths[r] >= 0, SUX_EINVAL, "negative partition length");
+        index[r] = acc;
+        acc += lengths[r];
+      }
+      index[sh.R] = acc;
+      require((uint64_t)acc == bytes, SUX_EINVAL,
+              "sum(lengths) = " + std::to_string(acc) + " != data bytes " + std::to_string(bytes));
+      progress(node, sh, lk, false);
+      if (bytes == 0 || sh.maps[map_index].present || sh.maps[map_index].pending) return;
+      require(d_data, SUX_EINVAL, "data pointer is NULL");
+      sh.maps[map_index].pending = true;
+      sh.submitting++;
+    }
+    std::shared_ptr<Slab> slab;
+    try {
+      slab = std::make_shared<Slab>(node->pool.get(), node->pool->get(bytes));
+      hip_check(hipMemcpyAsync(slab->buf.ptr, d_data, bytes, hipMemcpyDeviceToDevice, s),
+                "adopt data");
+      hip_check(hipStreamSynchronize(s), "sync commit");
+    } catch (...) {
+      std::lock_guard<std::mutex> lk(node->mu);
+      auto it = node->shuffles.find(shuffle_id);
+      if (it != node->shuffles.end()) {
+        it->second->maps[map_index].pending = false;
+        it->second->submitting--;
+      }
+      node->cv.notify_all();
+      throw;
+    }
     std::lock_guard<std::mutex> lk(node->mu);
     Shuffle& sh = node->shuffle(shuffle_id);
-    require(map_index >= 0 && map_index < sh.num_maps, SUX_EINVAL, "map index out of range");
-    std::vector<int64_t> index((size_t)sh.R + 1);
-    int64_t acc = 0;
-    for (int r = 0; r < sh.R; ++r) {
-      require(lengths[r] >= 0, SUX_EINVAL, "negative partition length");
-      index[r] = acc;
-      acc += lengths[r];
-    }
-    index[sh.R] = acc;
-    require((uint64_t)acc == bytes, SUX_EINVAL,
-            "sum(lengths) = " + std::to_string(acc) + " != data bytes " + std::to_string(bytes));
-    if (bytes == 0 || sh.maps[map_index].present) return;
-    require(d_data, SUX_EINVAL, "data pointer is NULL");
-    PoolBuf data = node->pool->get(bytes);
-    hip_check(hipMemcpyAsync(data.ptr, d_data, bytes, hipMemcpyDeviceToDevice, s), "adopt data");
-    hip_check(hipStreamSynchronize(s), "sync commit");
+    sh.submitting--;
+    node->cv.notify_all();
     MapSlot& slot = sh.maps[map_index];
+    slot.pending = false;
     slot.present = true;
     slot.owner = node->conf.rank;
-    slot.data = data;
+    slot.slab = slab;
+    slot.off = 0;
     slot.bytes = bytes;
     slot.index = std::move(index);
     sh.exchanged = false;
@@ -1268,9 +1625,10 @@ int sux_map_output_index(sux_node* node, int32_t shuffle_id, int32_t map_index, 
                          uint64_t out_len) {
   return guard([&] {
     require(node && out, SUX_EINVAL, "NULL argument");
-    std::lock_guard<std::mutex> lk(node->mu);
+    std::unique_lock<std::mutex> lk(node->mu);
     Shuffle& sh = node->shuffle(shuffle_id);
     require(map_index >= 0 && map_index < sh.num_maps, SUX_EINVAL, "map index out of range");
+    progress(node, sh, lk, false);
     const MapSlot& slot = sh.maps[map_index];
     require(slot.present, SUX_ENOENT, "map " + std::to_string(map_index) + " has no output");
     require(out_len >= 8 * (uint64_t)(sh.R + 1), SUX_EINVAL, "index buffer too small");
@@ -1291,85 +1649,280 @@ int sux_owned_partitions(sux_node* node, int32_t shuffle_id, int32_t rank, int32
   });
 }
 
-// Shuffle-level exchange: directory all-reduce, then grouped ncclSend/ncclRecv of every map's
-// owned-range byte slice (no repacking: the map output already is contiguous per partition).
+// ---- shuffle-level exchange -------------------------------------------------------------------
+}  // extern "C"
+
+namespace {
+// One committed map as every rank sees it after the directory all-gather.
+struct DirEntry {
+  int32_t map = -1, owner = -1;
+  std::vector<int64_t> index;
+  uint8_t ipc[SUX_IPC_DESC_BYTES] = {};  // owner's data buffer (bootstrap transport only)
+};
+
+// Host all-gather of `bytes` per rank: the embedding runtime's bootstrap, or RCCL through a
+// device bounce buffer.  The caller holds no node lock.
+void host_allgather(sux_node* node, const void* send, uint64_t bytes, void* recv, hipStream_t s) {
+  const int W = node->conf.world_size;
+  if (node->boot) {
+    const int rc = node->boot(node->boot_ctx, send, bytes, recv);
+    require(rc == 0, SUX_ECOMM, "bootstrap all-gather failed (" + std::to_string(rc) + ")");
+    return;
+  }
+  require(node->comm != nullptr, SUX_ESTATE,
+          "world_size > 1 needs an RCCL communicator (comm_id) or a bootstrap "
+          "(sux_node_set_bootstrap)");
+  const uint64_t pad = (bytes + 255) / 256 * 256;
+  PoolBuf tmp = node->pool->get(pad * (W + 1));
+  try {
+    hip_check(hipMemcpyAsync(tmp.ptr, send, bytes, hipMemcpyHostToDevice, s), "H2D all-gather");
+    nccl_check(ncclAllGather(tmp.ptr, tmp.ptr + pad, pad, ncclUint8, node->comm, s),
+               "ncclAllGather(directory)");
+    for (int r = 0; r < W; ++r)
+      hip_check(hipMemcpyAsync(static_cast<uint8_t*>(recv) + (uint64_t)r * bytes,
+                               tmp.ptr + pad + (uint64_t)r * pad, bytes, hipMemcpyDeviceToHost, s),
+                "D2H all-gather");
+    hip_check(hipStreamSynchronize(s), "sync all-gather");
+  } catch (...) {
+    node->pool->put(tmp);
+    throw;
+  }
+  node->pool->put(tmp);
+}
+
+// DriverMetadata analog (UcxWorkerWrapper.scala:27-65): every rank contributes one entry per
+// map it committed — |i32 map|i32 owner|(R+1) x i64 index|72-byte IPC descriptor| — padded to
+// the largest contribution; the merged table replaces the per-map driver slots fetched by
+// fetchDriverMetadataBuffer (:176-196).
+std::vector<DirEntry> gather_directory(sux_node* node, int R, const std::vector<DirEntry>& mine,
+                                       hipStream_t s) {
+  const int W = node->conf.world_size;
+  const uint64_t E = 8 + 8 * (uint64_t)(R + 1) + SUX_IPC_DESC_BYTES;
+  int64_t cnt = (int64_t)mine.size();
+  std::vector<int64_t> cnts((size_t)W);
+  host_allgather(node, &cnt, 8, cnts.data(), s);
+  int64_t most = 0;
+  for (int64_t c : cnts) most = std::max(most, c);
+  std::vector<DirEntry> all;
+  if (most == 0) return all;
+  std::vector<uint8_t> send((size_t)(most * E), 0), recv((size_t)(most * E * W));
+  for (size_t k = 0; k < mine.size(); ++k) {
+    uint8_t* e = send.data() + k * E;
+    std::memcpy(e, &mine[k].map, 4);
+    std::memcpy(e + 4, &mine[k].owner, 4);
+    std::memcpy(e + 8, mine[k].index.data(), 8 * (size_t)(R + 1));
+    std::memcpy(e + 8 + 8 * (size_t)(R + 1), mine[k].ipc, SUX_IPC_DESC_BYTES);
+  }
+  host_allgather(node, send.data(), send.size(), recv.data(), s);
+  for (int r = 0; r < W; ++r)
+    for (int64_t k = 0; k < cnts[r]; ++k) {
+      const uint8_t* e = recv.data() + ((uint64_t)r * most + k) * E;
+      DirEntry d;
+      std::memcpy(&d.map, e, 4);
+      std::memcpy(&d.owner, e + 4, 4);
+      d.index.resize((size_t)R + 1);
+      std::memcpy(d.index.data(), e + 8, 8 * (size_t)(R + 1));
+      std::memcpy(d.ipc, e + 8 + 8 * (size_t)(R + 1), SUX_IPC_DESC_BYTES);
+      all.push_back(std::move(d));
+    }
+  return all;
+}
+
+void export_ipc(const void* p, uint8_t out[SUX_IPC_DESC_BYTES]) {
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  hip_check(hipMemGetAddressRange(&base, &size, const_cast<void*>(p)), "hipMemGetAddressRange");
+  hipIpcMemHandle_t h;
+  hip_check(hipIpcGetMemHandle(&h, base), "hipIpcGetMemHandle");
+  const uint64_t off = (uint64_t)(static_cast<const uint8_t*>(p) - static_cast<const uint8_t*>(base));
+  std::memcpy(out, &h, 64);
+  std::memcpy(out + 64, &off, 8);
+}
+
+// Copy descriptors -> one gather-copy launch (64 KiB chunks, block i to its own destination).
+void launch_copies(sux_node* node, const std::vector<sux::CopyDesc>& desc, PoolBuf& aux,
+                   hipStream_t s) {
+  if (desc.empty()) return;
+  std::vector<uint32_t> first(desc.size());
+  uint64_t chunks = 0;
+  const uint64_t kChunk = 64 * 1024;
+  for (size_t i = 0; i < desc.size(); ++i) {
+    first[i] = (uint32_t)chunks;
+    chunks += desc[i].bytes ? (desc[i].bytes + kChunk - 1) / kChunk : 1;
+  }
+  require(chunks < (1ull << 31), SUX_ERANGE, "copy request too large");
+  const uint64_t dbytes = desc.size() * sizeof(sux::CopyDesc), fbytes = first.size() * 4;
+  aux = node->pool->get(dbytes + 256 + fbytes);
+  uint8_t* d_desc = aux.ptr;
+  uint8_t* d_first = aux.ptr + ((dbytes + 255) / 256) * 256;
+  hip_check(hipMemcpyAsync(d_desc, desc.data(), dbytes, hipMemcpyHostToDevice, s), "H2D desc");
+  hip_check(hipMemcpyAsync(d_first, first.data(), fbytes, hipMemcpyHostToDevice, s), "H2D chunks");
+  hip_check(sux::launch_gather_copy(reinterpret_cast<const sux::CopyDesc*>(d_desc),
+                                    (uint32_t)desc.size(), (uint32_t)chunks,
+                                    reinterpret_cast<const uint32_t*>(d_first), &node->timer, s),
+            "gather copy");
+}
+
+struct ExchangingFlag {  // clears Shuffle::exchanging on every exit path
+  sux_node* node;
+  int32_t id;
+  ~ExchangingFlag() {
+    std::lock_guard<std::mutex> lk(node->mu);
+    auto it = node->shuffles.find(id);
+    if (it != node->shuffles.end()) it->second->exchanging = false;
+  }
+};
+}  // namespace
+
+extern "C" {
+
+// Shuffle-level exchange: directory all-gather, then every rank's owned range of every remote
+// map moves into one exact-size receive buffer — grouped ncclSend/ncclRecv (RCCL), or one
+// gather-copy of one-sided pulls from the owners' IPC-mapped buffers (bootstrap transport).
 int sux_exchange(sux_node* node, int32_t shuffle_id, void* stream) {
   return guard([&] {
     require(node, SUX_EINVAL, "NULL node");
     node->bind();
     hipStream_t s = node->stream(stream);
-    std::lock_guard<std::mutex> lk(node->mu);
-    Shuffle& sh = node->shuffle(shuffle_id);
-    const int W = node->conf.world_size, me = node->conf.rank, R = sh.R, M = sh.num_maps;
-    if (W == 1) {
-      sh.exchanged = true;
-      return;
+    const int W = node->conf.world_size, me = node->conf.rank;
+    int R = 0, M = 0;
+    std::vector<DirEntry> mine;
+    std::vector<std::shared_ptr<Slab>> keep;  // own map outputs stay alive while peers read
+    std::vector<uint8_t*> own_data;
+    {
+      std::unique_lock<std::mutex> lk(node->mu);
+      Shuffle& sh = node->shuffle(shuffle_id);
+      require(!sh.exchanging, SUX_ESTATE, "shuffle " + std::to_string(shuffle_id) + " is already exchanging");
+      drain(node, sh, lk);
+      if (W == 1) {
+        sh.exchanged = true;
+        return;
+      }
+      R = sh.R;
+      M = sh.num_maps;
+      require(R >= W, SUX_EINVAL, "need at least one partition per rank");
+      sh.exchanging = true;
+      for (int m = 0; m < M; ++m) {
+        const MapSlot& sl = sh.maps[m];
+        if (!sl.present || sl.owner != me || !sl.slab) continue;
+        DirEntry d;
+        d.map = m;
+        d.owner = me;
+        d.index = sl.index;
+        mine.push_back(std::move(d));
+        keep.push_back(sl.slab);
+        own_data.push_back(sl.data());
+      }
     }
-    require(R >= W, SUX_EINVAL, "need at least one partition per rank");
-    // 1. directory: rows [owner+1, index[0..R]] of the maps this rank owns; sum-all-reduce
-    const size_t row = (size_t)R + 2;
-    std::vector<int64_t> dir(row * (size_t)M, 0);
-    for (int m = 0; m < M; ++m) {
-      const MapSlot& sl = sh.maps[m];
-      if (!sl.present || sl.owner != me) continue;
-      dir[row * m] = me + 1;
-      for (int r = 0; r <= R; ++r) dir[row * m + 1 + r] = sl.index[r];
+    ExchangingFlag flag{node, shuffle_id};
+    const bool ipc = node->comm == nullptr;
+    if (ipc)
+      for (size_t k = 0; k < mine.size(); ++k) export_ipc(own_data[k], mine[k].ipc);
+    // 1. directory (replaces the driver table + the phase-1 offset GETs)
+    std::vector<DirEntry> all = gather_directory(node, R, mine, s);
+    std::vector<int32_t> owner_of((size_t)M, -1);
+    std::vector<const DirEntry*> entry((size_t)M, nullptr);
+    for (const auto& d : all) {
+      require(d.map >= 0 && d.map < M && d.owner >= 0 && d.owner < W, SUX_ESTATE,
+              "malformed directory entry");
+      require(owner_of[d.map] < 0, SUX_ESTATE,
+              "map " + std::to_string(d.map) + " committed by more than one rank");
+      owner_of[d.map] = d.owner;
+      entry[d.map] = &d;
     }
-    if (M > 0) {
-      PoolBuf tmp = node->pool->get(dir.size() * 8);
-      hip_check(hipMemcpyAsync(tmp.ptr, dir.data(), dir.size() * 8, hipMemcpyHostToDevice, s),
-                "H2D directory");
-      nccl_check(ncclAllReduce(tmp.ptr, tmp.ptr, dir.size(), ncclInt64, ncclSum, node->comm, s),
-                 "ncclAllReduce(directory)");
-      hip_check(hipMemcpyAsync(dir.data(), tmp.ptr, dir.size() * 8, hipMemcpyDeviceToHost, s),
-                "D2H directory");
-      hip_check(hipStreamSynchronize(s), "sync directory");
-      node->pool->put(tmp);
-    }
-    // 2. adopt remote rows, size the receive buffer
+    // 2. receive layout: remote maps in map order, each holding this rank's owned range
     const int lo = owner_lo(me, R, W), hi = owner_lo(me + 1, R, W);
+    std::vector<uint64_t> roff((size_t)M, 0);
     uint64_t total = 0;
     for (int m = 0; m < M; ++m) {
-      int64_t owner = dir[row * m] - 1;
-      require(owner >= -1 && owner < W, SUX_ESTATE,
-              "map " + std::to_string(m) + " committed by more than one rank");
-      if (owner < 0 || owner == me) continue;
+      if (owner_of[m] < 0 || owner_of[m] == me) continue;
+      roff[m] = total;
+      total += (uint64_t)(entry[m]->index[hi] - entry[m]->index[lo]);
+    }
+    PoolBuf recv = total ? node->pool->get(total) : PoolBuf{};
+    PoolBuf aux;
+    std::map<std::string, void*> opened;
+    try {
+      if (!ipc) {
+        // 3a. RCCL: identical chunk boundaries on every rank (grouped calls of <= 64 maps)
+        std::vector<uint8_t*> src((size_t)M, nullptr);
+        for (size_t k = 0; k < mine.size(); ++k) src[mine[k].map] = own_data[k];
+        const int kChunk = 64;
+        for (int m0 = 0; m0 < M; m0 += kChunk) {
+          nccl_check(ncclGroupStart(), "ncclGroupStart");
+          for (int m = m0; m < std::min(M, m0 + kChunk); ++m) {
+            if (owner_of[m] < 0) continue;
+            const std::vector<int64_t>& ix = entry[m]->index;
+            if (owner_of[m] == me) {
+              for (int h = 0; h < W; ++h) {
+                if (h == me) continue;
+                const int64_t a = ix[owner_lo(h, R, W)], b = ix[owner_lo(h + 1, R, W)];
+                if (b > a)
+                  nccl_check(ncclSend(src[m] + a, (size_t)(b - a), ncclUint8, h, node->comm, s),
+                             "ncclSend");
+              }
+            } else if (ix[hi] > ix[lo]) {
+              nccl_check(ncclRecv(recv.ptr + roff[m], (size_t)(ix[hi] - ix[lo]), ncclUint8,
+                                  owner_of[m], node->comm, s),
+                         "ncclRecv");
+            }
+          }
+          nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+        }
+        hip_check(hipStreamSynchronize(s), "sync exchange");
+      } else {
+        // 3b. bootstrap: one-sided pulls (the GET model of OnOffsetsFetchCallback.java:80-87)
+        std::vector<sux::CopyDesc> desc;
+        for (int m = 0; m < M; ++m) {
+          if (owner_of[m] < 0 || owner_of[m] == me) continue;
+          const std::vector<int64_t>& ix = entry[m]->index;
+          if (ix[hi] == ix[lo]) continue;
+          std::string key(reinterpret_cast<const char*>(entry[m]->ipc), 64);
+          key += std::to_string(owner_of[m]);
+          void*& base = opened[key];
+          if (!base) {
+            hipIpcMemHandle_t h;
+            std::memcpy(&h, entry[m]->ipc, 64);
+            hip_check(hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess),
+                      "hipIpcOpenMemHandle");
+          }
+          uint64_t off;
+          std::memcpy(&off, entry[m]->ipc + 64, 8);
+          desc.push_back({static_cast<const uint8_t*>(base) + off + ix[lo], recv.ptr + roff[m],
+                          (uint64_t)(ix[hi] - ix[lo])});
+        }
+        launch_copies(node, desc, aux, s);
+        hip_check(hipStreamSynchronize(s), "sync pulls");
+        // every rank has finished reading its owners' buffers before anyone returns
+        int64_t one = 1;
+        std::vector<int64_t> ack((size_t)W);
+        host_allgather(node, &one, 8, ack.data(), s);
+      }
+    } catch (...) {
+      for (auto& kv : opened) (void)hipIpcCloseMemHandle(kv.second);
+      node->pool->put(recv);
+      node->pool->put(aux);
+      throw;
+    }
+    node->pool->put(aux);
+    for (auto& kv : opened) (void)hipIpcCloseMemHandle(kv.second);
+    // 4. adopt the remote rows
+    std::lock_guard<std::mutex> lk(node->mu);
+    Shuffle& sh = node->shuffle(shuffle_id);
+    for (int m = 0; m < M; ++m) {
+      if (owner_of[m] < 0 || owner_of[m] == me) continue;
       MapSlot& sl = sh.maps[m];
       sl.present = true;
-      sl.owner = (int32_t)owner;
-      sl.index.assign(dir.begin() + row * m + 1, dir.begin() + row * (m + 1));
-      sl.recv_off = total;
-      total += (uint64_t)(sl.index[hi] - sl.index[lo]);
+      sl.owner = owner_of[m];
+      sl.slab.reset();
+      sl.off = 0;
+      sl.index = entry[m]->index;
+      sl.bytes = (uint64_t)sl.index[R];
+      sl.recv_off = roff[m];
     }
     node->pool->put(sh.recv);
-    sh.recv = total ? node->pool->get(total) : PoolBuf{};
+    sh.recv = recv;
     sh.recv_bytes = total;
-    // 3. data: per map-chunk groups, identical chunk boundaries on every rank
-    const int kChunk = 64;
-    for (int m0 = 0; m0 < M; m0 += kChunk) {
-      nccl_check(ncclGroupStart(), "ncclGroupStart");
-      for (int m = m0; m < std::min(M, m0 + kChunk); ++m) {
-        const MapSlot& sl = sh.maps[m];
-        if (!sl.present) continue;
-        if (sl.owner == me) {
-          for (int h = 0; h < W; ++h) {
-            if (h == me) continue;
-            int64_t a = sl.index[owner_lo(h, R, W)], b = sl.index[owner_lo(h + 1, R, W)];
-            if (b > a)
-              nccl_check(ncclSend(sl.data.ptr + a, (size_t)(b - a), ncclUint8, h, node->comm, s),
-                         "ncclSend");
-          }
-        } else {
-          int64_t bytes = sl.index[hi] - sl.index[lo];
-          if (bytes > 0)
-            nccl_check(ncclRecv(sh.recv.ptr + sl.recv_off, (size_t)bytes, ncclUint8, sl.owner,
-                                node->comm, s),
-                       "ncclRecv");
-        }
-      }
-      nccl_check(ncclGroupEnd(), "ncclGroupEnd");
-    }
-    hip_check(hipStreamSynchronize(s), "sync exchange");
     sh.exchanged = true;
   });
 }
@@ -1392,7 +1945,7 @@ void resolve(sux_node* node, Shuffle& sh, const sux_block_id& b, uint64_t* addr,
   const int64_t a = sl.index[b.start_reduce], e = sl.index[b.end_reduce];
   *size = e - a;
   if (sl.owner == node->conf.rank) {
-    *addr = (uint64_t)(uintptr_t)(sl.data.ptr + a);
+    *addr = (uint64_t)(uintptr_t)(sl.data() + a);
     return;
   }
   const int W = node->conf.world_size, me = node->conf.rank;
@@ -1409,8 +1962,9 @@ int sux_resolve_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* b
   return guard([&] {
     require(node && (blocks || n == 0) && (addrs || n == 0) && (sizes || n == 0) && n >= 0,
             SUX_EINVAL, "NULL argument");
-    std::lock_guard<std::mutex> lk(node->mu);
+    std::unique_lock<std::mutex> lk(node->mu);
     Shuffle& sh = node->shuffle(shuffle_id);
+    drain(node, sh, lk);
     for (int i = 0; i < n; ++i) resolve(node, sh, blocks[i], &addrs[i], &sizes[i]);
   });
 }
@@ -1425,8 +1979,9 @@ int sux_fetch_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* blo
     std::vector<sux::CopyDesc> desc((size_t)n);
     uint64_t total = 0;
     {
-      std::lock_guard<std::mutex> lk(node->mu);
+      std::unique_lock<std::mutex> lk(node->mu);
       Shuffle& sh = node->shuffle(shuffle_id);
+      drain(node, sh, lk);  // maps written without a wait are published first
       // phase 1 (UcxShuffleClient.submitFetchOffsets :50-92 / OnOffsetsFetchCallback :53-72):
       // sizes from the index tables of the directory
       for (int i = 0; i < n; ++i) {
@@ -1599,6 +2154,10 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
   int sbytes = 0;
   if (d_seg) {
     require(nseg >= 1, SUX_EINVAL, "sort: num_segments must be >= 1");
+    // the segment id rides above the key in at most 3 bytes: more segments would alias segment
+    // k with k mod 2^24 and interleave their records
+    require(nseg <= (1 << 24), SUX_ERANGE,
+            "sort: at most 2^24 segments per call, got " + std::to_string(nseg));
     sbytes = nseg <= 1 ? 0 : nseg <= 256 ? 1 : nseg <= 65536 ? 2 : 3;
     require(bits / 8 + sbytes <= 12, SUX_EINVAL,
             "sort: key bytes + segment-id bytes (" + std::to_string(sbytes) + ") exceed 12");
@@ -1638,11 +2197,19 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
                                    key_offset, key_len, d_seg, nseg, sbytes, pa, ws + P.span_off,
                                    inline_rec, s),
             "sort pairs");
-  // which digits vary: one 24-byte read-back (the only host wait in the sort)
-  uint32_t span[6];
-  hip_check(hipMemcpyAsync(span, ws + P.span_off, sizeof span, hipMemcpyDeviceToHost, s),
-            "sort key span");
-  hip_check(hipStreamSynchronize(s), "sort key span");
+  // which digits vary: one 24-byte read-back (the only host wait in the sort).  A stream being
+  // captured into a HIP graph cannot be waited on: then every digit pass runs (the skipped
+  // passes are identity permutations, so the bytes are the same) and the call stays async.
+  static const bool all_passes = std::getenv("SUX_SORT_ALL_PASSES") != nullptr;  // A/B runs
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  hip_check(hipStreamIsCapturing(s, &cap), "hipStreamIsCapturing");
+  const bool run_all = all_passes || cap != hipStreamCaptureStatusNone;
+  uint32_t span[6] = {0, 0, 0, ~0u, ~0u, ~0u};  // AND = 0, OR = ~0: every bit varies
+  if (!run_all) {
+    hip_check(hipMemcpyAsync(span, ws + P.span_off, sizeof span, hipMemcpyDeviceToHost, s),
+              "sort key span");
+    hip_check(hipStreamSynchronize(s), "sort key span");
+  }
   sux::PartDev pd{};
   pd.kind = sux::kPartRadix;
   pd.R = 1 << digit;
@@ -1652,8 +2219,7 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
   sux::LayoutDesc lay{1, 16};
   // the key occupies bits [128 - bits, 128) of the big-endian pair; least significant digit first
   for (int sh = 128 - bits; sh < 128; sh += digit) {
-    static const bool all_passes = std::getenv("SUX_SORT_ALL_PASSES") != nullptr;  // A/B runs
-    if (!all_passes && !span_varies(span, sh, sh + digit)) continue;  // identity pass
+    if (!run_all && !span_varies(span, sh, sh + digit)) continue;  // identity pass
     pd.seed = sh;
     P.g.recs = pa;
     hip_check(sux::launch_partition_group(pd, P.g, lay, pb, index, nullptr, nullptr,
@@ -1769,6 +2335,16 @@ int sux_kernel_times(sux_node* node, int64_t* launches, double* total_ms, int32_
       node->timer.spare.push_back(r.b);
     }
     node->timer.recs.clear();
+  });
+}
+
+int sux_kernel_variant(sux_node* node, int32_t slot, char* buf, size_t len) {
+  return guard([&] {
+    require(node && buf && len > 0, SUX_EINVAL, "NULL argument");
+    require(slot >= 0 && slot < sux::kNumSlots, SUX_EINVAL, "slot out of range");
+    std::lock_guard<std::mutex> lk(node->timer.mu);
+    const char* v = node->timer.variant[slot] ? node->timer.variant[slot] : "";
+    std::snprintf(buf, len, "%s", v);
   });
 }
 

@@ -117,13 +117,16 @@ __global__ __launch_bounds__(256) void k_pull(int32_t W, int32_t me, const uint6
   // ranges of maps 0..M-1 in order — exactly the [source][map][partition] receive layout.
   const uint8_t* src = reinterpret_cast<const uint8_t*>(srcs[g]) + src_off;
   uint8_t* dst = recv + dst_off;
-  // 16-byte pieces (4-byte aligned on both sides), then the dword tail
-  const uint64_t n16 = size / 16;
-  for (uint64_t i = (uint64_t)slot * 256 + threadIdx.x; i < n16; i += (uint64_t)per_src * 256)
+  // 16-byte pieces when both sides are 4-byte aligned, then whole dwords, then single bytes:
+  // never a byte past `size` (compressed map outputs are byte-granular)
+  const bool al4 = (((uintptr_t)src | (uintptr_t)dst) & 3) == 0;
+  const uint64_t n16 = al4 ? size / 16 : 0, n4 = al4 ? size / 4 : 0;
+  const uint64_t t0 = (uint64_t)slot * 256 + threadIdx.x, step = (uint64_t)per_src * 256;
+  for (uint64_t i = t0; i < n16; i += step)
     *reinterpret_cast<u32x4a4*>(dst + 16 * i) = *reinterpret_cast<const u32x4a4*>(src + 16 * i);
-  for (uint64_t i = n16 * 16 + ((uint64_t)slot * 256 + threadIdx.x) * 4; i < size;
-       i += (uint64_t)per_src * 256 * 4)
-    *reinterpret_cast<uint32_t*>(dst + i) = *reinterpret_cast<const uint32_t*>(src + i);
+  for (uint64_t i = n16 * 4 + t0; i < n4; i += step)
+    *reinterpret_cast<uint32_t*>(dst + 4 * i) = *reinterpret_cast<const uint32_t*>(src + 4 * i);
+  for (uint64_t i = n4 * 4 + t0; i < size; i += step) dst[i] = src[i];
 }
 
 hipError_t launch_pull(int32_t W, int32_t me, const uint64_t* srcs, const int64_t* gi, int32_t M,

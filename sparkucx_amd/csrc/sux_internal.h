@@ -94,6 +94,8 @@ enum KernelSlot { kHist = 0, kScan = 1, kScatter = 2, kCopy = 3, kNumSlots = 4 }
 struct Timer;  // owned by the node; nullptr = no timing
 void timer_begin(Timer* t, int slot, hipStream_t s);
 void timer_end(Timer* t, int slot, hipStream_t s);
+// Name of the kernel variant last launched in `slot` (a string literal), for sux_kernel_variant.
+void timer_note(Timer* t, int slot, const char* kernel);
 
 // Launchers (sux_partition.hip).  All enqueue on `s` and return the hipError_t of the launch.
 hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const LayoutDesc& lay,

@@ -1688,6 +1688,7 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   // one pass (sux_onepass.hip) whenever a map batch fits on chip: every record read once
   uint32_t op_grid = 0, op_cs = 0;
   if (ws.op_bytes && onepass_eligible(pd, g, lay.world, d_out, d_peer_bytes, s, &op_grid, &op_cs)) {
+    timer_note(timer, kScatter, "k_onepass");
     timer_begin(timer, kScatter, s);
     const hipError_t eo = launch_onepass(pd, g, d_out, d_index, d_index_be, d_pids,
                                          d_ws + ws.op_off, op_grid, op_cs, s);
@@ -1719,6 +1720,8 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   else if (hv >= 4 && words && R <= 4096 && S == 100 && (pd.key_offset + pd.key_len) <= (int)S) hist = 4;
   else if (hv >= 3 && words && R <= 4096) hist = 3;
   else if (hv >= 2 && shaped) hist = 2;
+  timer_note(timer, kHist, hist == 16 ? "k_hist16" : hist == 4 ? "k_hist4" : hist == 3 ? "k_hist3"
+                          : hist == 2 ? "k_hist2" : "k_hist");
   timer_begin(timer, kHist, s);
   if (hist == 16) {
     const size_t lds = (size_t)R * 4;
@@ -1860,6 +1863,7 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
                   Sc7<100, 1024, 16>::lds_bytes(R) <= 160 * 1024;
   timer_begin(timer, kScatter, s);
   if (s16) {
+    timer_note(timer, kScatter, "k_scatter16b");
     const size_t lds = (size_t)R * 4;
     const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(2, (160u * 1024) / (uint32_t)lds));
     const dim3 grid(std::min<uint32_t>(total_tiles, 256u * per_cu));
@@ -1884,6 +1888,7 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
     }
     e = hipGetLastError();
   } else if (v7) {
+    timer_note(timer, kScatter, "k_scatter7");
     uint32_t tpw = s6tpw > 0 ? (uint32_t)s6tpw
                              : (uint32_t)std::max<uint64_t>(1, (8ull * 1024 + g.tile_recs - 1) / g.tile_recs);
     if (tpw > g.tiles_per_map) tpw = g.tiles_per_map;
@@ -1907,6 +1912,7 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
 #undef SUX_S7L
     e = hipGetLastError();
   } else if (c6) {
+    timer_note(timer, kScatter, "k_scatter6");
     uint32_t tpw = s6tpw > 0 ? (uint32_t)s6tpw
                              : (uint32_t)std::max<uint64_t>(1, (8ull * c6 + g.tile_recs - 1) / g.tile_recs);
     if (tpw > g.tiles_per_map) tpw = g.tiles_per_map;
@@ -1925,6 +1931,7 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
 #undef SUX_S6L
     e = hipGetLastError();
   } else if (sv >= 2 && shaped) {
+    timer_note(timer, kScatter, "k_scatter2");
     const size_t lds = 4 * (size_t)(S == 100 ? scatter2_wave_bytes<100, 128>(R)
                                              : scatter2_wave_bytes<16, 512>(R));
     allow_lds(reinterpret_cast<const void*>(&k_scatter2<100, 128>), lds);
@@ -1937,8 +1944,10 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
                          counts, base, d_out);
     e = hipGetLastError();
   } else if (wpg == 4) {
+    timer_note(timer, kScatter, "k_scatter");
     e = launch_scatter<4>(S, grid1, lds1, s, g, R, bits, pids, counts, base, d_out);
   } else {
+    timer_note(timer, kScatter, "k_scatter");
     e = launch_scatter<1>(S, grid1, lds1, s, g, R, bits, pids, counts, base, d_out);
   }
   timer_end(timer, kScatter, s);

@@ -396,6 +396,7 @@ hipError_t launch_varlen_group(const PartDev& pd, const VarGroup& g, uint8_t* d_
   }
   const bool v2 = ver >= 2;
   const bool hist2 = v2 && kw > 0 && !d_pids_in;
+  timer_note(timer, kHist, "k_vhist");
   timer_begin(timer, kHist, s);
   if (hist2) {
     const size_t lds = (size_t)wpg * R * 4;
@@ -440,6 +441,7 @@ hipError_t launch_varlen_group(const PartDev& pd, const VarGroup& g, uint8_t* d_
   timer_end(timer, kScan, s);
   if (e != hipSuccess) return e;
   if (d_pids_in) pids = const_cast<uint16_t*>(d_pids_in);
+  timer_note(timer, kScatter, "k_vscatter");
   timer_begin(timer, kScatter, s);
   if (v2) {
     const size_t lds = (size_t)wpg * (R + 2 * kVWave) * 8;

@@ -34,7 +34,13 @@ class Conf(C.Structure):
     _fields_ = [("device", C.c_int32), ("rank", C.c_int32), ("world_size", C.c_int32),
                 ("num_streams", C.c_int32), ("comm_id", C.c_uint8 * 128),
                 ("min_buffer_size", C.c_uint64), ("min_allocation_size", C.c_uint64),
-                ("metadata_block_size", C.c_uint64)]
+                ("metadata_block_size", C.c_uint64), ("num_prealloc", C.c_uint32),
+                ("reserved0", C.c_uint32), ("prealloc_size", C.c_uint64 * 16),
+                ("prealloc_count", C.c_uint64 * 16)]
+
+
+# int (*sux_allgather_fn)(void* ctx, const void* send, uint64_t bytes, void* recv)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p)
 
 
 class PartitionerDesc(C.Structure):
@@ -57,6 +63,12 @@ class BlockId(C.Structure):
 P, I32, I64, U64, U32, SZ = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_uint32, C.c_size_t
 _SIGS = {
     "sux_conf_init": (None, [C.POINTER(Conf)]),
+    "sux_conf_set_prealloc": (C.c_int, [C.POINTER(Conf), C.c_char_p]),
+    "sux_node_set_bootstrap": (C.c_int, [P, ALLGATHER_FN, P]),
+    "sux_pool_stats": (C.c_int, [P, C.POINTER(U64), C.POINTER(U64), C.POINTER(U64),
+                                 C.POINTER(U64)]),
+    "sux_write_map_outputs": (C.c_int, [P, I32, I32, P, P, U64, U64, P]),
+    "sux_wait_map_outputs": (C.c_int, [P, I32]),
     "sux_abi_version": (C.c_int, []),
     "sux_last_error": (C.c_int, [C.c_char_p, SZ]),
     "sux_comm_unique_id": (C.c_int, [P]),
@@ -96,6 +108,7 @@ _SIGS = {
     "sux_buffer_release": (C.c_int, [P]),
     "sux_set_kernel_timing": (C.c_int, [P, C.c_int]),
     "sux_kernel_times": (C.c_int, [P, P, P, I32]),
+    "sux_kernel_variant": (C.c_int, [P, I32, C.c_char_p, SZ]),
     "sux_generate": (C.c_int, [P, I32, U64, U64, U64, C.c_double, U64, P, P]),
     "sux_ipc_export": (C.c_int, [P, P, P]),
     "sux_ipc_open": (C.c_int, [P, P, C.POINTER(P)]),
@@ -158,12 +171,17 @@ def check(rc: int, what: str = "") -> None:
         raise SuxError(rc, f"{what}: {last_error()}")
 
 
-def default_conf(device=0, rank=0, world_size=1, comm_id: bytes | None = None, **kw) -> Conf:
+def default_conf(device=0, rank=0, world_size=1, comm_id: bytes | None = None,
+                 prealloc: str | None = None, **kw) -> Conf:
+    """sux_conf with the reference's defaults; `prealloc` is Spark's
+    spark.shuffle.ucx.memory.preAllocateBuffers string ("4k:1000,16k:500")."""
     c = Conf()
     load().sux_conf_init(C.byref(c))
     c.device, c.rank, c.world_size = device, rank, world_size
     if comm_id is not None:
         C.memmove(c.comm_id, comm_id, 128)
+    if prealloc is not None:
+        check(load().sux_conf_set_prealloc(C.byref(c), prealloc.encode()), "sux_conf_set_prealloc")
     for k, v in kw.items():
         setattr(c, k, v)
     return c

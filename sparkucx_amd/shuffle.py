@@ -75,6 +75,24 @@ class Node:
             N.check(self.lib.sux_node_destroy(self.h), "sux_node_destroy")
             self.h = None
 
+    def set_bootstrap(self, allgather):
+        """Control plane for the exchange without RCCL: `allgather(b: bytes) -> list[bytes]` (one
+        entry per rank, rank order), e.g. torch.distributed.all_gather_object over gloo."""
+        def fn(_ctx, send, nbytes, recv):
+            try:
+                parts = allgather(C.string_at(send, nbytes))
+                C.memmove(recv, b"".join(parts), nbytes * len(parts))
+                return 0
+            except Exception:  # pragma: no cover - reported as SUX_ECOMM by the library
+                return -1
+        self._boot = N.ALLGATHER_FN(fn)  # kept alive as long as the node
+        N.check(self.lib.sux_node_set_bootstrap(self.h, self._boot, None), "sux_node_set_bootstrap")
+
+    def pool_stats(self) -> dict:
+        v = [C.c_uint64() for _ in range(4)]
+        N.check(self.lib.sux_pool_stats(self.h, *[C.byref(x) for x in v]), "sux_pool_stats")
+        return dict(zip(("allocated_bytes", "requests", "allocs", "preallocs"), [x.value for x in v]))
+
     def __enter__(self):
         return self
 
@@ -318,6 +336,17 @@ class Node:
                                               _ptr(records), num_records, _stream(stream)),
                 "sux_write_map_output")
 
+    def write_map_outputs(self, shuffle_id: int, first_map: int, part: Partitioner,
+                          records: torch.Tensor, records_per_map: int, num_records: int,
+                          stream=None):
+        """Consecutive map tasks first_map.. in one launch group; published lazily (no wait)."""
+        N.check(self.lib.sux_write_map_outputs(self.h, shuffle_id, first_map, part.h,
+                                               _ptr(records), records_per_map, num_records,
+                                               _stream(stream)), "sux_write_map_outputs")
+
+    def wait_map_outputs(self, shuffle_id: int):
+        N.check(self.lib.sux_wait_map_outputs(self.h, shuffle_id), "sux_wait_map_outputs")
+
     def commit_map_output(self, shuffle_id: int, map_index: int, data: torch.Tensor | None,
                           lengths, stream=None):
         arr = np.ascontiguousarray(np.asarray(lengths, dtype=np.int64))
@@ -432,6 +461,12 @@ class Node:
         launches, ms = (C.c_int64 * n)(), (C.c_double * n)()
         N.check(self.lib.sux_kernel_times(self.h, launches, ms, n), "sux_kernel_times")
         return {k: (launches[i], ms[i]) for i, k in enumerate(N.KERNELS)}
+
+    def kernel_variant(self, slot: int) -> str:
+        """Kernel last launched for slot 0=hist 1=scan 2=scatter 3=copy (e.g. 'k_scatter7')."""
+        buf = C.create_string_buffer(64)
+        N.check(self.lib.sux_kernel_variant(self.h, slot, buf, len(buf)), "sux_kernel_variant")
+        return buf.value.decode()
 
 
 class FetchedBuffer:

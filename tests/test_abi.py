@@ -18,7 +18,8 @@ def test_library_loads_and_exports_every_header_symbol():
     missing = [s for s in declared if not hasattr(lib, s)]
     assert not missing, missing
     assert set(declared) == set(N._SIGS), set(declared) ^ set(N._SIGS)
-    assert lib.sux_abi_version() == 1
+    assert lib.sux_abi_version() == 2
+    assert C.sizeof(N.Conf) == 432  # sux_conf of ABI v2 (prealloc pairs appended)
 
 
 def test_conf_defaults_mirror_ucx_shuffle_conf():
@@ -27,6 +28,33 @@ def test_conf_defaults_mirror_ucx_shuffle_conf():
     assert c.min_buffer_size == 1024          # spark.shuffle.ucx.memory.minBufferSize
     assert c.min_allocation_size == 4 << 20   # spark.shuffle.ucx.memory.minAllocationSize
     assert c.metadata_block_size == 300       # 2 * spark.shuffle.ucx.rkeySize
+
+
+@pytest.mark.parametrize("spec,want", [
+    ("", []),
+    ("4k:1000,16k:500", [(4096, 1000), (16384, 500)]),    # UcxShuffleConf.scala:53 doc example
+    (" 1m : 3 ,, 2048:1", [(1 << 20, 3), (2048, 1)]),      # trimmed, empty entries skipped
+    ("1g:2,8kb:4,100b:7", [(1 << 30, 2), (8192, 4), (100, 7)]),
+])
+def test_prealloc_spec_parses_like_spark(spec, want):
+    c = N.default_conf(prealloc=spec)
+    got = [(c.prealloc_size[k], c.prealloc_count[k]) for k in range(c.num_prealloc)]
+    assert got == want
+
+
+@pytest.mark.parametrize("spec", ["4k", "4k:1:2", "x:1", "4q:1", "4k:-1", "4k:1e3"])
+def test_prealloc_spec_rejects_malformed_entries(spec):
+    with pytest.raises(N.SuxError) as e:
+        N.default_conf(prealloc=spec)
+    assert e.value.code == N.SUX_EINVAL
+
+
+def test_bootstrap_and_pool_entry_points_validate_arguments():
+    lib = N.load()
+    assert lib.sux_node_set_bootstrap(None, N.ALLGATHER_FN(0), None) == N.SUX_EINVAL
+    assert lib.sux_pool_stats(None, None, None, None, None) == N.SUX_EINVAL
+    assert lib.sux_wait_map_outputs(None, 0) == N.SUX_EINVAL
+    assert lib.sux_write_map_outputs(None, 0, 0, None, None, 1, 0, None) == N.SUX_EINVAL
 
 
 def test_null_arguments_fail_with_einval_and_message():

@@ -1,4 +1,6 @@
-"""GPU, multi-process: bench.py's N>1 pipeline (ipc transport) rehearsed with 2 ranks on cuda:0."""
+"""GPU, multi-process: bench.py's N>1 pipeline (ipc transport) rehearsed with several ranks on
+cuda:0, TeraSort and Zipf keys, with --verify: every received (source, map, partition) block of
+every launch group is compared with the CPU oracle inside the run."""
 import json
 import os
 import socket
@@ -17,19 +19,34 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_bench_two_ranks_one_gpu():
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
-           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rehearse-one-gpu",
-           "--records", "3000000", "--map-records", "262144", "--group-maps", "2",
-           "--steps", "2", "--warmup", "1"]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300,
+def _run(world, *args, timeout=300):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={world}", "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--rehearse-one-gpu", *args]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout,
                        env=dict(os.environ, OMP_NUM_THREADS="1"))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
-    res = json.loads(lines[0])
+    return json.loads(lines[0])
+
+
+def test_bench_two_ranks_one_gpu():
+    res = _run(2, "--records", "3000000", "--map-records", "262144", "--group-maps", "2",
+               "--steps", "2", "--warmup", "1")
     assert res["n_gpus"] == 2 and res["value"] > 0
     ex = res["roofline_exchange"]
     # uniform keys: about half of each rank's bytes leave it
     assert 0.4 < ex["remote_bytes_per_rank"] / (3_000_000 * 100) < 0.6
+
+
+@pytest.mark.parametrize("workload", ["terasort", "zipf"])
+def test_bench_eight_ranks_verified(workload):
+    # 3 launch groups of 2 maps (the last one short), every block of every group checked
+    n, rpm = 100_000, 20_000
+    res = _run(8, "--workload", workload, "--records", str(n), "--map-records", str(rpm),
+               "--group-maps", "2", "--steps", "1", "--warmup", "0", "--verify")
+    assert res["n_gpus"] == 8
+    assert res["verified_groups"] == 3
+    ex = res["roofline_exchange"]
+    assert ex["remote_bytes_per_rank"] > 0

@@ -14,6 +14,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "tests", "cpp", "test_host_mirror")
 
 
+THREADS = os.path.join(ROOT, "tests", "cpp", "test_threads")
+
+
+def test_cpp_eight_task_threads():
+    """P12: 8 host threads with their own streams write and fetch concurrently (test_threads.cpp)."""
+    assert os.path.exists(THREADS), "build it first: make -C tests/cpp"
+    r = subprocess.run([THREADS], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "threads ok" in r.stdout
+
+
 def test_cpp_host_mirror():
     assert os.path.exists(BIN), "build it first: make -C tests/cpp"
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=120)
