@@ -285,6 +285,59 @@ def files_leg(node, out, index, maps: int, R: int, dev) -> dict:
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r02.json")
 
 
+def plugin_leg(node, part, data, rs: int, R: int, rpm: int, gm: int, groups: int, dev,
+               reps: int = 3) -> dict:
+    """The drop-in path as Spark drives it, timed end to end through the
+    C-ABI: registerShuffle -> getWriter(...).write for every map task (sux_write_map_outputs, one
+    launch group of `gm` map tasks per call, published on completion) -> the reduce side resolving
+    every (map, reduce partition) block (sux_resolve_blocks, the zero-copy local read at N = 1)
+    -> unregisterShuffle.  GB/s of input bytes, to set beside the stateless `value`; plus one
+    reducer's fetch (sux_fetch_blocks: its partition from every map into one pooled buffer,
+    OnOffsetsFetchCallback's copy)."""
+    maps = groups * gm
+    n = maps * rpm
+    stream = torch.cuda.current_stream(dev)
+    # every (map, reduce partition) block, reducer by reducer
+    blocks = np.stack([np.tile(np.arange(maps), R), np.repeat(np.arange(R), maps)], 1).astype(np.int32)
+
+    def one(sid):
+        node.register_shuffle(sid, maps, R, rs)
+        for g in range(groups):
+            r0 = g * gm * rpm
+            node.write_map_outputs(sid, g * gm, part, data[r0 * rs:(r0 + gm * rpm) * rs], rpm,
+                                   gm * rpm, stream=stream)
+        addrs, sizes = node.resolve_blocks(sid, blocks)  # waits for every map's publication
+        assert int(sizes.sum()) == n * rs
+        return sid
+
+    one(1000)
+    node.unregister_shuffle(1000)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(reps):
+        one(1001 + k)
+        node.unregister_shuffle(1001 + k)
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / reps
+    # one reducer's fetch of partition R//2 from every map
+    sid = one(2000)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    buf, sizes = node.fetch_blocks(sid, [(m, R // 2) for m in range(maps)], stream=stream)
+    ft = time.perf_counter() - t0
+    fb = sum(sizes)
+    buf.release(maps)
+    node.unregister_shuffle(sid)
+    st = node.pool_stats()
+    return {"maps": maps, "records": n, "bytes": n * rs, "ms": round(dt * 1e3, 3),
+            "GB/s": round(n * rs / dt / 1e9, 1),
+            "path": "register -> write_map_outputs x%d (%d maps each) -> resolve %d blocks -> "
+                    "unregister" % (groups, gm, len(blocks)),
+            "fetch_one_reducer": {"blocks": maps, "bytes": fb, "ms": round(ft * 1e3, 3),
+                                  "GB/s": round(fb / ft / 1e9, 1)},
+            "pool": st}
+
+
 def load_traffic(workload: str, kernel: str) -> dict | None:
     """HBM bytes per record of `kernel` under `workload`, from the committed PMC summary
     (profiles/pmc_r02.json, written by profiles/collect_pmc.py: one rocprofv3 pass per counter
@@ -338,6 +391,9 @@ def main():
     ap.add_argument("--file-maps", type=int, default=-1,
                     help="N=1: also time writing/reading Spark's data + index files for this "
                          "many map outputs (sux_write_map_files; -1: 8; 0: skip)")
+    ap.add_argument("--plugin-groups", type=int, default=-1,
+                    help="N=1: also time the plugin path (register -> write -> resolve -> "
+                         "unregister) over this many launch groups of map tasks (-1: 8; 0: skip)")
     ap.add_argument("--cpu-records", type=int, default=10_000_000)
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (0: every core this job may use, host_cores())")
@@ -670,6 +726,10 @@ def main():
     if not pipelined and args.file_maps != 0:
         fm = min(maps, args.file_maps if args.file_maps > 0 else 8)
         result["files"] = files_leg(node, out, index, fm, R, dev)
+    if not pipelined and args.plugin_groups != 0:
+        pg = min(groups, args.plugin_groups if args.plugin_groups > 0 else 8)
+        if pg and n >= pg * group_recs:
+            result["plugin"] = plugin_leg(node, part, data, rs, R, rpm, gm, pg, dev)
     if not pipelined and args.varlen_rows != 0:
         vr = args.varlen_rows if args.varlen_rows > 0 else 32 << 20
         result["varlen"] = varlen_leg(node, vr, min(vr, 1 << 20), 200, dev,

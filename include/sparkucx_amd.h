@@ -304,8 +304,15 @@ int sux_write_map_outputs(sux_node* node, int32_t shuffle_id, int32_t first_map_
                           uint64_t records_per_map, uint64_t num_records, void* stream);
 /* Block until every map output enqueued for the shuffle (by any thread) is published. */
 int sux_wait_map_outputs(sux_node* node, int32_t shuffle_id);
-/* writeIndexFileAndCommit for a map output produced elsewhere: `d_data` (data_bytes, device)
- * is adopted by copy; `lengths` are R host int64 partition lengths (Spark's lengths[]). */
+/* sux_write_map_output for records the JVM serialized into host memory (Spark's serializer
+ * output): the bytes are staged into a pooled device buffer on `stream`, then partitioned as
+ * above; blocks until the map is published. */
+int sux_write_map_output_host(sux_node* node, int32_t shuffle_id, int32_t map_index,
+                              const sux_partitioner* part, const void* host_records,
+                              uint64_t num_records, void* stream);
+/* writeIndexFileAndCommit for a map output produced elsewhere: `d_data` (data_bytes, device or
+ * host memory — a data file Spark's own writer produced) is adopted by copy; `lengths` are R host
+ * int64 partition lengths (Spark's lengths[]). */
 int sux_commit_map_output(sux_node* node, int32_t shuffle_id, int32_t map_index,
                           const void* d_data, uint64_t data_bytes, const int64_t* lengths,
                           void* stream);
@@ -349,6 +356,9 @@ int sux_fetch_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* blo
 int sux_resolve_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* blocks, int32_t n,
                        uint64_t* dev_addrs, int64_t* sizes);
 int sux_buffer_info(sux_buffer* buf, void** dev_ptr, uint64_t* size, uint64_t* capacity);
+/* Copy bytes [offset, offset + len) of a fetched buffer to host memory (the reducer's
+ * deserialization side, NioManagedBuffer.nioByteBuffer); waits for the copy. */
+int sux_buffer_read(sux_buffer* buf, uint64_t offset, void* host_dst, uint64_t len, void* stream);
 int sux_buffer_retain(sux_buffer* buf, int32_t count);
 int sux_buffer_release(sux_buffer* buf);
 

@@ -1560,6 +1560,32 @@ int sux_write_map_output(sux_node* node, int32_t shuffle_id, int32_t map_index,
   });
 }
 
+int sux_write_map_output_host(sux_node* node, int32_t shuffle_id, int32_t map_index,
+                              const sux_partitioner* part, const void* host_records, uint64_t n,
+                              void* stream) {
+  int rs = 0;
+  int rc = guard([&] {
+    require(node && part && (host_records || n == 0), SUX_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(node->mu);
+    rs = node->shuffle(shuffle_id).rec_size;
+  });
+  if (rc != SUX_OK || n == 0)
+    return rc != SUX_OK ? rc : sux_write_map_output(node, shuffle_id, map_index, part, nullptr, 0, stream);
+  PoolBuf stage;
+  rc = guard([&] {
+    node->bind();
+    stage = node->pool->get(n * (uint64_t)rs);
+    hip_check(hipMemcpyAsync(stage.ptr, host_records, n * (uint64_t)rs, hipMemcpyHostToDevice,
+                             node->stream(stream)),
+              "H2D records");
+  });
+  if (rc == SUX_OK) rc = sux_write_map_output(node, shuffle_id, map_index, part, stage.ptr, n, stream);
+  // the write waited for its map (or failed before launching): the staging buffer is free
+  (void)hipStreamSynchronize(node->stream(stream));
+  node->pool->put(stage);
+  return rc;
+}
+
 int sux_commit_map_output(sux_node* node, int32_t shuffle_id, int32_t map_index,
                           const void* d_data, uint64_t bytes, const int64_t* lengths,
                           void* stream) {
@@ -1591,8 +1617,7 @@ int sux_commit_map_output(sux_node* node, int32_t shuffle_id, int32_t map_index,
     std::shared_ptr<Slab> slab;
     try {
       slab = std::make_shared<Slab>(node->pool.get(), node->pool->get(bytes));
-      hip_check(hipMemcpyAsync(slab->buf.ptr, d_data, bytes, hipMemcpyDeviceToDevice, s),
-                "adopt data");
+      hip_check(hipMemcpyAsync(slab->buf.ptr, d_data, bytes, hipMemcpyDefault, s), "adopt data");
       hip_check(hipStreamSynchronize(s), "sync commit");
     } catch (...) {
       std::lock_guard<std::mutex> lk(node->mu);
@@ -2035,6 +2060,20 @@ int sux_buffer_info(sux_buffer* b, void** ptr, uint64_t* size, uint64_t* cap) {
     if (ptr) *ptr = b->buf.ptr;
     if (size) *size = b->size;
     if (cap) *cap = b->buf.cap;
+  });
+}
+
+int sux_buffer_read(sux_buffer* b, uint64_t offset, void* dst, uint64_t len, void* stream) {
+  return guard([&] {
+    require(b && (dst || len == 0), SUX_EINVAL, "NULL argument");
+    require(offset <= b->size && len <= b->size - offset, SUX_ERANGE,
+            "read of [" + std::to_string(offset) + ", +" + std::to_string(len) +
+                ") past a buffer of " + std::to_string(b->size) + " bytes");
+    if (len == 0) return;
+    b->node->bind();
+    hipStream_t s = b->node->stream(stream);
+    hip_check(hipMemcpyAsync(dst, b->buf.ptr + offset, len, hipMemcpyDeviceToHost, s), "D2H block");
+    hip_check(hipStreamSynchronize(s), "sync block read");
   });
 }
 

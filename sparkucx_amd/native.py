@@ -105,6 +105,8 @@ _SIGS = {
     "sux_resolve_blocks": (C.c_int, [P, I32, P, I32, P, P]),
     "sux_buffer_info": (C.c_int, [P, C.POINTER(P), C.POINTER(U64), C.POINTER(U64)]),
     "sux_buffer_retain": (C.c_int, [P, I32]),
+    "sux_buffer_read": (C.c_int, [P, U64, P, U64, P]),
+    "sux_write_map_output_host": (C.c_int, [P, I32, I32, P, P, U64, P]),
     "sux_buffer_release": (C.c_int, [P]),
     "sux_set_kernel_timing": (C.c_int, [P, C.c_int]),
     "sux_kernel_times": (C.c_int, [P, P, P, I32]),

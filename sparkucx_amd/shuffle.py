@@ -372,6 +372,12 @@ class Node:
 
     @staticmethod
     def _blocks(blocks):
+        """sux_block_id array from (map, start[, end]) tuples or an int (n, 2|3) numpy array."""
+        if isinstance(blocks, np.ndarray):
+            b = np.zeros((max(1, len(blocks)), 4), np.int32)
+            b[:len(blocks), :2] = blocks[:, :2]
+            b[:len(blocks), 2] = blocks[:, 2] if blocks.shape[1] > 2 else blocks[:, 1] + 1
+            return (N.BlockId * len(b)).from_buffer_copy(b.tobytes())
         arr = (N.BlockId * max(1, len(blocks)))()
         for i, b in enumerate(blocks):
             m, s = b[0], b[1]
@@ -394,7 +400,9 @@ class Node:
         sizes = (C.c_int64 * max(1, len(blocks)))()
         N.check(self.lib.sux_resolve_blocks(self.h, shuffle_id, arr, len(blocks), addrs, sizes),
                 "sux_resolve_blocks")
-        return list(addrs)[:len(blocks)], list(sizes)[:len(blocks)]
+        k = len(blocks)
+        return (np.frombuffer(addrs, np.uint64)[:k].copy(),
+                np.frombuffer(sizes, np.int64)[:k].copy())
 
     # ---- measurement -------------------------------------------------------------------------
     def sort_records(self, records: torch.Tensor, record_size: int, key_kind: int,

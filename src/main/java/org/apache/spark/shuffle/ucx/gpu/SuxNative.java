@@ -1,0 +1,89 @@
+/*
+ * SuxNative — the JNI surface of libsparkucx_amd.so (include/sparkucx_amd.h), one static native
+ * method per function of src/main/native/sux_jni.c.  Handles are longs; a failed call throws
+ * SuxException carrying the SUX_E* code and the library's message.
+ */
+package org.apache.spark.shuffle.ucx.gpu;
+
+import java.nio.ByteBuffer;
+
+public final class SuxNative {
+  private SuxNative() {}
+
+  static {
+    // libsparkucx_amd_jni.so links libsparkucx_amd.so (rpath $ORIGIN); both ship in the jar's
+    // native directory or on java.library.path
+    System.loadLibrary("sparkucx_amd_jni");
+    if (abiVersion() != ABI_VERSION) {
+      throw new UnsatisfiedLinkError("libsparkucx_amd ABI " + abiVersion() + ", plugin built for "
+          + ABI_VERSION);
+    }
+  }
+
+  public static final int ABI_VERSION = 2;
+
+  // status codes (SUX_*)
+  public static final int OK = 0, EINVAL = -1, ENOMEM = -2, EHIP = -3, ECOMM = -4, ENOENT = -5,
+      ESTATE = -6, ERANGE = -7, EIO = -8;
+  // partitioner kinds (SUX_PART_*)
+  public static final int PART_RANGE_BYTES = 1, PART_MURMUR3_LONG = 2, PART_MURMUR3_INT = 3,
+      PART_MURMUR3_BYTES = 4, PART_HASH_LONG = 5, PART_HASH_INT = 6;
+
+  // ---- node (UcxNode) ----
+  public static native int abiVersion();
+  public static native byte[] commUniqueId();
+  public static native long nodeCreate(int device, int rank, int worldSize, byte[] commId,
+                                       long minBufferSize, long minAllocationSize,
+                                       long metadataBlockSize, String preAllocateBuffers,
+                                       boolean isDriver);
+  public static native void nodeDestroy(long node);
+  /** Returns a context to pass to releaseBootstrap once the node is destroyed. */
+  public static native long setBootstrap(long node, Bootstrap bootstrap);
+  public static native void releaseBootstrap(long ctx);
+  public static native long[] poolStats(long node);
+  public static native long streamCreate(long node);
+  public static native void streamDestroy(long node, long stream);
+
+  // ---- partitioner ----
+  public static native long partitionerCreate(long node, int kind, int numPartitions, int keyOffset,
+                                              int keyLen, int seed, boolean ascending,
+                                              byte[] rangeBounds);
+  public static native void partitionerDestroy(long part);
+
+  // ---- shuffle lifecycle ----
+  /** Returns the directory bytes (num_maps * metadataBlockSize). */
+  public static native long registerShuffle(long node, int shuffleId, int numMaps,
+                                            int numPartitions, int recordSize);
+  public static native void unregisterShuffle(long node, int shuffleId);
+
+  // ---- map side ----
+  public static native void writeMapOutputHost(long node, int shuffleId, int mapIndex, long part,
+                                               ByteBuffer records, long numRecords, int recordSize,
+                                               long stream);
+  public static native void writeMapOutputs(long node, int shuffleId, int firstMapIndex, long part,
+                                            long deviceRecords, long recordsPerMap,
+                                            long numRecords, long stream);
+  public static native void waitMapOutputs(long node, int shuffleId);
+  public static native void commitMapOutput(long node, int shuffleId, int mapIndex,
+                                            ByteBuffer data, long dataBytes, long[] lengths,
+                                            long stream);
+  public static native byte[] mapOutputIndex(long node, int shuffleId, int mapIndex,
+                                             int numPartitions);
+
+  // ---- exchange ----
+  public static native void exchange(long node, int shuffleId, long stream);
+  public static native int[] ownedPartitions(long node, int shuffleId, int rank);
+
+  // ---- fetch ----
+  public static native long fetchBlocks(long node, int shuffleId, int[] blocks, long[] sizes,
+                                        long stream);
+  public static native long bufferDevicePtr(long buf);
+  public static native void bufferRead(long buf, long offset, ByteBuffer dst, long len,
+                                       long stream);
+  public static native void bufferRetain(long buf, int count);
+  public static native void bufferRelease(long buf);
+
+  // ---- Spark's on-disk files ----
+  public static native boolean indexFileCommit(String indexPath, String dataPath, String dataTmp,
+                                               long[] lengths, long[] lengthsOut);
+}

@@ -1,0 +1,418 @@
+/*
+ * sux_jni.c — JNI binding of libsparkucx_amd.so for the JVM plugin classes
+ * (org.apache.spark.shuffle.ucx.gpu.SuxNative, src/main/java/.../gpu/SuxNative.java).
+ *
+ * Every native method of SuxNative is one function here and calls the C-ABI of
+ * include/sparkucx_amd.h; nothing else.  Conventions:
+ *   - handles (sux_node*, sux_partitioner*, sux_buffer*, hipStream_t) travel as jlong;
+ *   - a negative SUX_E* status becomes a thrown org.apache.spark.shuffle.ucx.gpu.SuxException
+ *     (RuntimeException, like org.openucx.jucx.UcxException in the reference) carrying the code
+ *     and sux_last_error(); the caller (UcxShuffleClient) turns fetch errors into
+ *     BlockFetchingListener.onBlockFetchFailure, which the reference never calls;
+ *   - host byte ranges come in as direct ByteBuffers (GetDirectBufferAddress, no copy): Spark's
+ *     serializer output, an mmapped data file, or a reducer's staging buffer;
+ *   - the bootstrap all-gather calls back into a Java object (GpuNode's control plane over
+ *     Spark RPC) on the thread that called exchange().
+ *
+ * Build (needs a JDK, absent from this image): src/main/native/Makefile.
+ */
+#include <jni.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../../include/sparkucx_amd.h"
+
+#define SUX_JNI_CLASS "org/apache/spark/shuffle/ucx/gpu/SuxNative"
+#define SUX_EXC_CLASS "org/apache/spark/shuffle/ucx/gpu/SuxException"
+#define FN(name) Java_org_apache_spark_shuffle_ucx_gpu_SuxNative_##name
+
+/* ---- errors ------------------------------------------------------------------------------ */
+static void throw_sux(JNIEnv* env, int rc, const char* what) {
+  char msg[2048];
+  char err[1792];
+  sux_last_error(err, sizeof err);
+  snprintf(msg, sizeof msg, "%s: %s", what, err);
+  jclass cls = (*env)->FindClass(env, SUX_EXC_CLASS);
+  if (!cls) return; /* NoClassDefFoundError already pending */
+  jmethodID ctor = (*env)->GetMethodID(env, cls, "<init>", "(ILjava/lang/String;)V");
+  if (!ctor) return;
+  jstring js = (*env)->NewStringUTF(env, msg);
+  jthrowable t = (jthrowable)(*env)->NewObject(env, cls, ctor, (jint)rc, js);
+  if (t) (*env)->Throw(env, t);
+}
+
+/* returns non-zero (and leaves an exception pending) when rc is an error */
+static int failed(JNIEnv* env, int rc, const char* what) {
+  if (rc == SUX_OK) return 0;
+  throw_sux(env, rc, what);
+  return 1;
+}
+
+static void* direct(JNIEnv* env, jobject buf, jlong need, const char* what) {
+  if (!buf) {
+    throw_sux(env, SUX_EINVAL, what);
+    return NULL;
+  }
+  void* p = (*env)->GetDirectBufferAddress(env, buf);
+  jlong cap = (*env)->GetDirectBufferCapacity(env, buf);
+  if (!p || cap < need) {
+    char m[256];
+    snprintf(m, sizeof m, "%s: a direct ByteBuffer of >= %lld bytes is required", what,
+             (long long)need);
+    (*env)->ThrowNew(env, (*env)->FindClass(env, "java/lang/IllegalArgumentException"), m);
+    return NULL;
+  }
+  return p;
+}
+
+#define NODE(h) ((sux_node*)(intptr_t)(h))
+#define PART(h) ((sux_partitioner*)(intptr_t)(h))
+#define BUF(h) ((sux_buffer*)(intptr_t)(h))
+#define STREAM(h) ((void*)(intptr_t)(h))
+
+/* ---- node: UcxNode ctor / close (UcxNode.java:60-96, :194-221) ---------------------------- */
+JNIEXPORT jint JNICALL FN(abiVersion)(JNIEnv* env, jclass cls) {
+  (void)env;
+  (void)cls;
+  return sux_abi_version();
+}
+
+JNIEXPORT jbyteArray JNICALL FN(commUniqueId)(JNIEnv* env, jclass cls) {
+  (void)cls;
+  uint8_t id[128];
+  if (failed(env, sux_comm_unique_id(id), "commUniqueId")) return NULL;
+  jbyteArray out = (*env)->NewByteArray(env, 128);
+  if (out) (*env)->SetByteArrayRegion(env, out, 0, 128, (const jbyte*)id);
+  return out;
+}
+
+JNIEXPORT jlong JNICALL FN(nodeCreate)(JNIEnv* env, jclass cls, jint device, jint rank,
+                                       jint worldSize, jbyteArray commId, jlong minBufferSize,
+                                       jlong minAllocationSize, jlong metadataBlockSize,
+                                       jstring preAllocateBuffers, jboolean isDriver) {
+  (void)cls;
+  sux_conf c;
+  sux_conf_init(&c);
+  c.device = device;
+  c.rank = rank;
+  c.world_size = worldSize;
+  c.min_buffer_size = (uint64_t)minBufferSize;
+  c.min_allocation_size = (uint64_t)minAllocationSize;
+  c.metadata_block_size = (uint64_t)metadataBlockSize;
+  if (commId) {
+    if ((*env)->GetArrayLength(env, commId) != 128) {
+      throw_sux(env, SUX_EINVAL, "nodeCreate: the RCCL unique id is 128 bytes");
+      return 0;
+    }
+    (*env)->GetByteArrayRegion(env, commId, 0, 128, (jbyte*)c.comm_id);
+  }
+  if (preAllocateBuffers) {
+    const char* spec = (*env)->GetStringUTFChars(env, preAllocateBuffers, NULL);
+    int rc = sux_conf_set_prealloc(&c, spec);
+    (*env)->ReleaseStringUTFChars(env, preAllocateBuffers, spec);
+    if (failed(env, rc, "spark.shuffle.ucx.memory.preAllocateBuffers")) return 0;
+  }
+  sux_node* n = NULL;
+  if (failed(env, sux_node_create(&c, isDriver ? 1 : 0, &n), "UcxNode")) return 0;
+  return (jlong)(intptr_t)n;
+}
+
+JNIEXPORT void JNICALL FN(nodeDestroy)(JNIEnv* env, jclass cls, jlong node) {
+  (void)cls;
+  failed(env, sux_node_destroy(NODE(node)), "UcxNode.close");
+}
+
+/* Bootstrap: the node calls back into Bootstrap.allGather(byte[]) -> byte[] (world * bytes). */
+typedef struct {
+  JavaVM* vm;
+  jobject target; /* global ref to an org.apache.spark.shuffle.ucx.gpu.Bootstrap */
+  jmethodID all_gather;
+} boot_ctx;
+
+static int boot_allgather(void* vctx, const void* send, uint64_t bytes, void* recv) {
+  boot_ctx* b = (boot_ctx*)vctx;
+  JNIEnv* env = NULL;
+  int attached = 0;
+  if ((*b->vm)->GetEnv(b->vm, (void**)&env, JNI_VERSION_1_8) != JNI_OK) {
+    if ((*b->vm)->AttachCurrentThread(b->vm, (void**)&env, NULL) != JNI_OK) return -1;
+    attached = 1;
+  }
+  int rc = -1;
+  jbyteArray in = (*env)->NewByteArray(env, (jsize)bytes);
+  if (in) {
+    (*env)->SetByteArrayRegion(env, in, 0, (jsize)bytes, (const jbyte*)send);
+    jbyteArray out = (jbyteArray)(*env)->CallObjectMethod(env, b->target, b->all_gather, in);
+    if (!(*env)->ExceptionCheck(env) && out) {
+      jsize n = (*env)->GetArrayLength(env, out);
+      if (bytes == 0 || n % (jsize)bytes == 0) {
+        (*env)->GetByteArrayRegion(env, out, 0, n, (jbyte*)recv);
+        rc = 0;
+      }
+    }
+    if ((*env)->ExceptionCheck(env)) (*env)->ExceptionClear(env); /* reported as SUX_ECOMM */
+  }
+  if (attached) (*b->vm)->DetachCurrentThread(b->vm);
+  return rc;
+}
+
+JNIEXPORT jlong JNICALL FN(setBootstrap)(JNIEnv* env, jclass cls, jlong node, jobject bootstrap) {
+  (void)cls;
+  boot_ctx* b = (boot_ctx*)calloc(1, sizeof *b);
+  if (!b) {
+    throw_sux(env, SUX_ENOMEM, "setBootstrap");
+    return 0;
+  }
+  (*env)->GetJavaVM(env, &b->vm);
+  b->target = (*env)->NewGlobalRef(env, bootstrap);
+  jclass bc = (*env)->GetObjectClass(env, bootstrap);
+  b->all_gather = (*env)->GetMethodID(env, bc, "allGather", "([B)[B");
+  if (!b->all_gather || failed(env, sux_node_set_bootstrap(NODE(node), boot_allgather, b),
+                               "setBootstrap")) {
+    (*env)->DeleteGlobalRef(env, b->target);
+    free(b);
+    return 0;
+  }
+  return (jlong)(intptr_t)b; /* freed by releaseBootstrap after nodeDestroy */
+}
+
+JNIEXPORT void JNICALL FN(releaseBootstrap)(JNIEnv* env, jclass cls, jlong ctx) {
+  (void)cls;
+  boot_ctx* b = (boot_ctx*)(intptr_t)ctx;
+  if (!b) return;
+  (*env)->DeleteGlobalRef(env, b->target);
+  free(b);
+}
+
+JNIEXPORT jlongArray JNICALL FN(poolStats)(JNIEnv* env, jclass cls, jlong node) {
+  (void)cls;
+  uint64_t v[4] = {0, 0, 0, 0};
+  if (failed(env, sux_pool_stats(NODE(node), &v[0], &v[1], &v[2], &v[3]), "poolStats")) return NULL;
+  jlongArray out = (*env)->NewLongArray(env, 4);
+  if (out) (*env)->SetLongArrayRegion(env, out, 0, 4, (const jlong*)v);
+  return out;
+}
+
+/* ---- per-task-thread stream (UcxNode.getThreadLocalWorker, UcxNode.java:147-176) --------- */
+JNIEXPORT jlong JNICALL FN(streamCreate)(JNIEnv* env, jclass cls, jlong node) {
+  (void)cls;
+  void* s = NULL;
+  /* complement of 0 reserved CUs = an ordinary stream on every CU */
+  if (failed(env, sux_stream_create(NODE(node), 0, 1, &s), "streamCreate")) return 0;
+  return (jlong)(intptr_t)s;
+}
+
+JNIEXPORT void JNICALL FN(streamDestroy)(JNIEnv* env, jclass cls, jlong node, jlong stream) {
+  (void)cls;
+  failed(env, sux_stream_destroy(NODE(node), STREAM(stream)), "streamDestroy");
+}
+
+/* ---- partitioner (the dependency's Partitioner, P1) --------------------------------------- */
+JNIEXPORT jlong JNICALL FN(partitionerCreate)(JNIEnv* env, jclass cls, jlong node, jint kind,
+                                              jint numPartitions, jint keyOffset, jint keyLen,
+                                              jint seed, jboolean ascending,
+                                              jbyteArray rangeBounds) {
+  (void)cls;
+  sux_partitioner_desc d;
+  memset(&d, 0, sizeof d);
+  d.kind = kind;
+  d.num_partitions = numPartitions;
+  d.key_offset = keyOffset;
+  d.key_len = keyLen;
+  d.seed = seed;
+  d.ascending = ascending ? 1 : 0;
+  jbyte* b = NULL;
+  if (rangeBounds) {
+    b = (*env)->GetByteArrayElements(env, rangeBounds, NULL);
+    d.range_bounds = (const uint8_t*)b;
+  }
+  sux_partitioner* p = NULL;
+  int rc = sux_partitioner_create(NODE(node), &d, &p);
+  if (b) (*env)->ReleaseByteArrayElements(env, rangeBounds, b, JNI_ABORT);
+  if (failed(env, rc, "partitioner")) return 0;
+  return (jlong)(intptr_t)p;
+}
+
+JNIEXPORT void JNICALL FN(partitionerDestroy)(JNIEnv* env, jclass cls, jlong part) {
+  (void)cls;
+  failed(env, sux_partitioner_destroy(PART(part)), "partitionerDestroy");
+}
+
+/* ---- shuffle lifecycle (CommonUcxShuffleManager.scala:39-91) ------------------------------ */
+JNIEXPORT jlong JNICALL FN(registerShuffle)(JNIEnv* env, jclass cls, jlong node, jint shuffleId,
+                                            jint numMaps, jint numPartitions, jint recordSize) {
+  (void)cls;
+  sux_handle_desc h;
+  if (failed(env, sux_register_shuffle(NODE(node), shuffleId, numMaps, numPartitions, recordSize, &h),
+             "registerShuffle"))
+    return 0;
+  return (jlong)h.directory_bytes;
+}
+
+JNIEXPORT void JNICALL FN(unregisterShuffle)(JNIEnv* env, jclass cls, jlong node, jint shuffleId) {
+  (void)cls;
+  failed(env, sux_unregister_shuffle(NODE(node), shuffleId), "unregisterShuffle");
+}
+
+/* ---- map side (getWriter(...).write + writeIndexFileAndCommit) ----------------------------- */
+JNIEXPORT void JNICALL FN(writeMapOutputHost)(JNIEnv* env, jclass cls, jlong node, jint shuffleId,
+                                              jint mapIndex, jlong part, jobject records,
+                                              jlong numRecords, jint recordSize, jlong stream) {
+  (void)cls;
+  void* p = direct(env, records, numRecords * (jlong)recordSize, "writeMapOutputHost");
+  if (!p && numRecords) return;
+  failed(env, sux_write_map_output_host(NODE(node), shuffleId, mapIndex, PART(part), p,
+                                        (uint64_t)numRecords, STREAM(stream)),
+         "ShuffleWriter.write");
+}
+
+JNIEXPORT void JNICALL FN(writeMapOutputs)(JNIEnv* env, jclass cls, jlong node, jint shuffleId,
+                                           jint firstMapIndex, jlong part, jlong deviceRecords,
+                                           jlong recordsPerMap, jlong numRecords, jlong stream) {
+  (void)cls;
+  failed(env, sux_write_map_outputs(NODE(node), shuffleId, firstMapIndex, PART(part),
+                                    (const void*)(intptr_t)deviceRecords, (uint64_t)recordsPerMap,
+                                    (uint64_t)numRecords, STREAM(stream)),
+         "writeMapOutputs");
+}
+
+JNIEXPORT void JNICALL FN(waitMapOutputs)(JNIEnv* env, jclass cls, jlong node, jint shuffleId) {
+  (void)cls;
+  failed(env, sux_wait_map_outputs(NODE(node), shuffleId), "waitMapOutputs");
+}
+
+JNIEXPORT void JNICALL FN(commitMapOutput)(JNIEnv* env, jclass cls, jlong node, jint shuffleId,
+                                           jint mapIndex, jobject data, jlong dataBytes,
+                                           jlongArray lengths, jlong stream) {
+  (void)cls;
+  void* p = dataBytes ? direct(env, data, dataBytes, "writeIndexFileAndCommit") : NULL;
+  if (!p && dataBytes) return;
+  jlong* len = (*env)->GetLongArrayElements(env, lengths, NULL);
+  int rc = sux_commit_map_output(NODE(node), shuffleId, mapIndex, p, (uint64_t)dataBytes,
+                                 (const int64_t*)len, STREAM(stream));
+  (*env)->ReleaseLongArrayElements(env, lengths, len, JNI_ABORT);
+  failed(env, rc, "writeIndexFileAndCommit");
+}
+
+JNIEXPORT jbyteArray JNICALL FN(mapOutputIndex)(JNIEnv* env, jclass cls, jlong node,
+                                                jint shuffleId, jint mapIndex, jint numPartitions) {
+  (void)cls;
+  const jsize n = 8 * (numPartitions + 1);
+  uint8_t* tmp = (uint8_t*)malloc((size_t)n);
+  if (!tmp) {
+    throw_sux(env, SUX_ENOMEM, "mapOutputIndex");
+    return NULL;
+  }
+  int rc = sux_map_output_index(NODE(node), shuffleId, mapIndex, tmp, (uint64_t)n);
+  jbyteArray out = NULL;
+  if (!failed(env, rc, "mapOutputIndex")) {
+    out = (*env)->NewByteArray(env, n);
+    if (out) (*env)->SetByteArrayRegion(env, out, 0, n, (const jbyte*)tmp);
+  }
+  free(tmp);
+  return out;
+}
+
+/* ---- exchange (the all-to-all that replaces the reducers' remote GETs) -------------------- */
+JNIEXPORT void JNICALL FN(exchange)(JNIEnv* env, jclass cls, jlong node, jint shuffleId,
+                                    jlong stream) {
+  (void)cls;
+  failed(env, sux_exchange(NODE(node), shuffleId, STREAM(stream)), "exchange");
+}
+
+JNIEXPORT jintArray JNICALL FN(ownedPartitions)(JNIEnv* env, jclass cls, jlong node,
+                                                jint shuffleId, jint rank) {
+  (void)cls;
+  int32_t se[2];
+  if (failed(env, sux_owned_partitions(NODE(node), shuffleId, rank, &se[0], &se[1]),
+             "ownedPartitions"))
+    return NULL;
+  jintArray out = (*env)->NewIntArray(env, 2);
+  if (out) (*env)->SetIntArrayRegion(env, out, 0, 2, (const jint*)se);
+  return out;
+}
+
+/* ---- fetch: UcxShuffleClient.fetchBlocks (reducer/compat/spark_3_0/UcxShuffleClient.java:94) */
+/* blocks = {mapIndex, startReduce, endReduce} triples; sizes[i] <- bytes of block i; returns
+ * the pooled buffer (one reference per block, OnBlocksFetchCallback.java:35-53). */
+JNIEXPORT jlong JNICALL FN(fetchBlocks)(JNIEnv* env, jclass cls, jlong node, jint shuffleId,
+                                        jintArray blocks, jlongArray sizes, jlong stream) {
+  (void)cls;
+  const jsize n3 = (*env)->GetArrayLength(env, blocks);
+  if (n3 % 3 != 0 || (*env)->GetArrayLength(env, sizes) < n3 / 3) {
+    throw_sux(env, SUX_EINVAL, "fetchBlocks: blocks are (map, start, end) triples");
+    return 0;
+  }
+  const int32_t n = n3 / 3;
+  sux_block_id* ids = (sux_block_id*)calloc((size_t)(n ? n : 1), sizeof *ids);
+  int64_t* sz = (int64_t*)calloc((size_t)(n ? n : 1), sizeof *sz);
+  jint* b = (*env)->GetIntArrayElements(env, blocks, NULL);
+  if (!ids || !sz || !b) {
+    free(ids);
+    free(sz);
+    if (b) (*env)->ReleaseIntArrayElements(env, blocks, b, JNI_ABORT);
+    throw_sux(env, SUX_ENOMEM, "fetchBlocks");
+    return 0;
+  }
+  for (int32_t i = 0; i < n; ++i) {
+    ids[i].map_index = b[3 * i];
+    ids[i].start_reduce = b[3 * i + 1];
+    ids[i].end_reduce = b[3 * i + 2];
+  }
+  (*env)->ReleaseIntArrayElements(env, blocks, b, JNI_ABORT);
+  sux_buffer* out = NULL;
+  int rc = sux_fetch_blocks(NODE(node), shuffleId, ids, n, sz, &out, STREAM(stream));
+  if (rc == SUX_OK) (*env)->SetLongArrayRegion(env, sizes, 0, n, (const jlong*)sz);
+  free(ids);
+  free(sz);
+  if (failed(env, rc, "fetchBlocks")) return 0;
+  return (jlong)(intptr_t)out;
+}
+
+JNIEXPORT jlong JNICALL FN(bufferDevicePtr)(JNIEnv* env, jclass cls, jlong buf) {
+  (void)cls;
+  void* p = NULL;
+  if (failed(env, sux_buffer_info(BUF(buf), &p, NULL, NULL), "bufferDevicePtr")) return 0;
+  return (jlong)(intptr_t)p;
+}
+
+JNIEXPORT void JNICALL FN(bufferRead)(JNIEnv* env, jclass cls, jlong buf, jlong offset,
+                                      jobject dst, jlong len, jlong stream) {
+  (void)cls;
+  void* p = direct(env, dst, len, "bufferRead");
+  if (!p && len) return;
+  failed(env, sux_buffer_read(BUF(buf), (uint64_t)offset, p, (uint64_t)len, STREAM(stream)),
+         "ManagedBuffer.nioByteBuffer");
+}
+
+JNIEXPORT void JNICALL FN(bufferRetain)(JNIEnv* env, jclass cls, jlong buf, jint count) {
+  (void)cls;
+  failed(env, sux_buffer_retain(BUF(buf), count), "ManagedBuffer.retain");
+}
+
+JNIEXPORT void JNICALL FN(bufferRelease)(JNIEnv* env, jclass cls, jlong buf) {
+  (void)cls;
+  failed(env, sux_buffer_release(BUF(buf)), "ManagedBuffer.release");
+}
+
+/* ---- Spark's on-disk files (local-disk fallback / external shuffle service) -------------- */
+JNIEXPORT jboolean JNICALL FN(indexFileCommit)(JNIEnv* env, jclass cls, jstring indexPath,
+                                               jstring dataPath, jstring dataTmp,
+                                               jlongArray lengths, jlongArray lengthsOut) {
+  (void)cls;
+  const char* ip = (*env)->GetStringUTFChars(env, indexPath, NULL);
+  const char* dp = (*env)->GetStringUTFChars(env, dataPath, NULL);
+  const char* tp = dataTmp ? (*env)->GetStringUTFChars(env, dataTmp, NULL) : NULL;
+  const jsize R = (*env)->GetArrayLength(env, lengths);
+  jlong* len = (*env)->GetLongArrayElements(env, lengths, NULL);
+  jlong* out = lengthsOut ? (*env)->GetLongArrayElements(env, lengthsOut, NULL) : NULL;
+  int32_t reused = 0;
+  int rc = sux_index_file_commit(ip, dp, tp, (const int64_t*)len, R, (int64_t*)out, &reused);
+  if (out) (*env)->ReleaseLongArrayElements(env, lengthsOut, out, rc == SUX_OK ? 0 : JNI_ABORT);
+  (*env)->ReleaseLongArrayElements(env, lengths, len, JNI_ABORT);
+  if (tp) (*env)->ReleaseStringUTFChars(env, dataTmp, tp);
+  (*env)->ReleaseStringUTFChars(env, dataPath, dp);
+  (*env)->ReleaseStringUTFChars(env, indexPath, ip);
+  if (failed(env, rc, "writeIndexFileAndCommit")) return JNI_FALSE;
+  return reused ? JNI_TRUE : JNI_FALSE;
+}
