@@ -20,11 +20,10 @@
  *     are literals; the last match starts >= 12 bytes before the end.  The decoder below is
  *     cross-checked against the system liblz4 (LZ4_decompress_safe / LZ4_compress_default) in
  *     tests/test_oracle_lz4.py.
- *   - o_lz4_compress_block restates the GPU compressor's own parse (u32 table entries =
- *     position << 16 | 16-bit tag; 4-byte confirmation in the parse) (sux_lz4.hip header), so the
- *     GPU bytes are checked bit for bit; the payload of lz4-java's own compressor (liblz4's
- *     greedy parse with acceleration) differs and is not what is compared — any valid block
- *     decodes to the same bytes, which is what a Spark reader observes.
+ *   - o_lz4_compress_default restates liblz4's LZ4_compress_default (the compressor lz4-java's
+ *     JNI instance calls for every chunk), so a GPU stream is compared byte for byte with what
+ *     Spark's writer emits; tests/test_oracle_lz4.py pins the restatement to the system
+ *     liblz4.so.1.9.3 on every input it tries.
  */
 #include <stdint.h>
 #include <string.h>
@@ -73,87 +72,133 @@ uint32_t o_xxh32(const uint8_t* p, uint64_t len, uint32_t seed) {
   return h;
 }
 
-static uint32_t ext_len(uint32_t v) { return v >= 15 ? (v - 15) / 255 + 1 : 0; }
-static uint8_t* put_ext(uint8_t* d, uint32_t v) {
-  if (v < 15) return d;
-  v -= 15;
-  while (v >= 255) { *d++ = 255; v -= 255; }
-  *d++ = (uint8_t)v;
-  return d;
+/* LZ4_compress_default of liblz4 1.9.3 [ext, not vendored; the system liblz4.so.1.9.3 is the
+ * pin, tests/test_oracle_lz4.py], as lz4-java's JNI compressor calls it for every chunk of an
+ * LZ4BlockOutputStream (maxDestLen = LZ4_compressBound, so the output is never limited):
+ * LZ4_compress_fast(acceleration 1) -> LZ4_compress_fast_extState on a freshly zeroed state ->
+ * LZ4_compress_generic(byU16 table for inputs below LZ4_64Klimit, noDict, noDictIssue).
+ *   - hash = (read32(p) * 2654435761) >> (32 - 13), 8192 u16 entries holding positions; an entry
+ *     never written reads 0 — position 0 — and is a real candidate;
+ *   - inputs below LZ4_minLength (13) are one literal run;
+ *   - position 0 goes into the table, the search starts at 1; the search visits forwardIp with
+ *     step 1 for 64 probes, then 2, 3, ... (step = searchMatchNb++ >> 6, searchMatchNb from 64);
+ *     a probe is abandoned — last literals — when the NEXT forwardIp passes len - 11
+ *     (mflimitPlusOne), before the probe's own insertion; every other probe is inserted, then
+ *     compared (4 bytes);
+ *   - a match is extended backwards while ip > anchor, match > 0 and the previous bytes agree,
+ *     then forwards (LZ4_count) up to len - 5 (matchlimit);
+ *   - after a match: stop if ip >= len - 11; insert ip - 2; probe ip itself (insert, compare):
+ *     a hit is a new sequence with no literals; otherwise the search restarts at ip + 1.
+ * Returns the LZ4 block size (always > 0). */
+int32_t o_lz4_compress_default(const uint8_t* src, int32_t len, uint8_t* dst) {
+  static const uint32_t kMinLength = 13, kMfLimit = 12, kLastLiterals = 5, kSkip = 6;
+  uint16_t tab[1u << 13];
+  memset(tab, 0, sizeof tab);
+  const uint32_t n = (uint32_t)len;
+  uint8_t* op = dst;
+  uint8_t* token = NULL;
+  uint32_t anchor = 0, ip = 0, match = 0;
+#define O_H(p) ((rd32(src + (p)) * XP1) >> 19)
+  if (n >= kMinLength) {
+    const uint32_t mflimit1 = n - kMfLimit + 1, matchlimit = n - kLastLiterals;
+    tab[O_H(0)] = 0;
+    ip = 1;
+    uint32_t fh = O_H(ip);
+    for (;;) {
+      /* find a match */
+      {
+        uint32_t fip = ip, step = 1, nb = 1u << kSkip;
+        for (;;) {
+          const uint32_t h = fh, cur = fip;
+          const uint32_t mi = tab[h];
+          ip = fip;
+          fip += step;
+          step = nb++ >> kSkip;
+          if (fip > mflimit1) goto last_literals;
+          match = mi;
+          fh = O_H(fip);
+          tab[h] = (uint16_t)cur;
+          if (rd32(src + match) == rd32(src + ip)) break;
+        }
+      }
+      /* catch up */
+      while (ip > anchor && match > 0 && src[ip - 1] == src[match - 1]) {
+        --ip;
+        --match;
+      }
+      /* literals */
+      {
+        const uint32_t ll = ip - anchor;
+        token = op++;
+        if (ll >= 15) {
+          *token = 15 << 4;
+          uint32_t r = ll - 15;
+          for (; r >= 255; r -= 255) *op++ = 255;
+          *op++ = (uint8_t)r;
+        } else {
+          *token = (uint8_t)(ll << 4);
+        }
+        memcpy(op, src + anchor, ll);
+        op += ll;
+      }
+      for (;;) { /* _next_match */
+        const uint32_t off = ip - match;
+        *op++ = (uint8_t)off;
+        *op++ = (uint8_t)(off >> 8);
+        uint32_t mc = 0;
+        while (ip + 4 + mc < matchlimit && src[ip + 4 + mc] == src[match + 4 + mc]) ++mc;
+        ip += mc + 4;
+        if (mc >= 15) {
+          *token += 15;
+          mc -= 15;
+          for (; mc >= 255; mc -= 255) *op++ = 255;
+          *op++ = (uint8_t)mc;
+        } else {
+          *token += (uint8_t)mc;
+        }
+        anchor = ip;
+        if (ip >= mflimit1) goto last_literals;
+        tab[O_H(ip - 2)] = (uint16_t)(ip - 2);
+        /* test next position */
+        const uint32_t h = O_H(ip), mi = tab[h];
+        tab[h] = (uint16_t)ip;
+        if (rd32(src + mi) == rd32(src + ip)) {
+          token = op++;
+          *token = 0;
+          match = mi;
+          continue;
+        }
+        break;
+      }
+      fh = O_H(++ip);
+    }
+  }
+last_literals: {
+    const uint32_t ll = n - anchor;
+    if (ll >= 15) {
+      *op++ = 15 << 4;
+      uint32_t r = ll - 15;
+      for (; r >= 255; r -= 255) *op++ = 255;
+      *op++ = (uint8_t)r;
+    } else {
+      *op++ = (uint8_t)(ll << 4);
+    }
+    memcpy(op, src + anchor, ll);
+    op += ll;
+  }
+#undef O_H
+  return (int32_t)(op - dst);
 }
 
-/* The GPU parse (sux_lz4.hip k_lz4_compress), sequentially.  Returns the block size, or 0 when
- * the chunk is stored raw (len < 13, or the LZ4 block would not be shorter than len). */
-int32_t o_lz4_compress_block(const uint8_t* src, int32_t len, int32_t hash_bits, uint8_t* dst) {
-  if (len < 13) return 0;
-  const uint32_t H = 1u << hash_bits;
-  uint32_t tab[1u << 16];
-  uint32_t cand[64];
-  uint8_t ok[64];
-  /* every entry starts as position 0 with position 0's true bytes */
-  for (uint32_t i = 0; i < H; ++i) tab[i] = rd32(src) >> 16;
-  const uint32_t last = (uint32_t)len - 12, mlimit = (uint32_t)len - 5, nwin = last / 64 + 1;
-  uint32_t op = 0, anchor = 0, cur = 0, w = 0;
-  while (w < nwin) {
-    /* hash the window: candidates from the table as it stood at the window's start */
-    for (uint32_t l = 0; l < 64; ++l) {
-      const uint32_t pos = w * 64 + l;
-      ok[l] = 0;
-      cand[l] = 0;
-      if (pos > last) continue;
-      const uint32_t seq = rd32(src + pos);
-      const uint32_t h = (seq * XP1) >> (32 - hash_bits);
-      const uint32_t e = tab[h];
-      cand[l] = e >> 16;
-      ok[l] = cand[l] < pos && pos - cand[l] <= 65535u && (e & 0xFFFFu) == (seq >> 16);
-    }
-    for (uint32_t l = 0; l < 64; ++l) {
-      const uint32_t pos = w * 64 + l;
-      if (pos > last) continue;
-      const uint32_t seq = rd32(src + pos);
-      const uint32_t h = (seq * XP1) >> (32 - hash_bits);
-      const uint32_t v = (pos << 16) | (seq >> 16);
-      if (v > tab[h]) tab[h] = v;
-    }
-    uint32_t nextw = w + 1;
-    for (;;) {
-      const uint32_t rel = cur > w * 64 ? cur - w * 64 : 0;
-      uint32_t j = rel;
-      while (j < 64 && !ok[j]) ++j;
-      if (j >= 64) break;
-      const uint32_t p = w * 64 + j, c = cand[j];
-      uint32_t ml = 0;
-      while (p + ml < mlimit && src[p + ml] == src[c + ml]) ++ml;
-      if (ml < 4) { /* tag collision */
-        ok[j] = 0;
-        continue;
-      }
-      const uint32_t LL = p - anchor;
-      const uint32_t need = 1 + ext_len(LL) + LL + 2 + ext_len(ml - 4);
-      if (op + need >= (uint32_t)len) return 0;
-      uint8_t* d = dst + op;
-      *d++ = (uint8_t)(((LL < 15 ? LL : 15) << 4) | (ml - 4 < 15 ? ml - 4 : 15));
-      d = put_ext(d, LL);
-      memcpy(d, src + anchor, LL);
-      d += LL;
-      *d++ = (uint8_t)(p - c);
-      *d++ = (uint8_t)((p - c) >> 8);
-      d = put_ext(d, ml - 4);
-      op += need;
-      cur = p + ml;
-      anchor = cur;
-      if (cur >= (w + 1) * 64) { nextw = cur / 64; break; }
-    }
-    w = nextw;
-  }
-  const uint32_t LL = (uint32_t)len - anchor;
-  const uint32_t need = 1 + ext_len(LL) + LL;
-  if (op + need >= (uint32_t)len) return 0;
-  uint8_t* d = dst + op;
-  *d++ = (uint8_t)((LL < 15 ? LL : 15) << 4);
-  d = put_ext(d, LL);
-  memcpy(d, src + anchor, LL);
-  return (int32_t)(op + need);
+/* lz4-java's LZ4BlockOutputStream.flushBufferedData: the chunk is stored raw when the LZ4 block
+ * is not shorter.  Returns the LZ4 block size, or 0 for a raw chunk. */
+int32_t o_lz4_compress_block(const uint8_t* src, int32_t len, uint8_t* dst) {
+  uint8_t tmp[65536 + 65536 / 255 + 16 + 64];
+  if (len <= 0 || len > 65536) return 0;
+  const int32_t c = o_lz4_compress_default(src, len, tmp);
+  if (c >= len) return 0;
+  memcpy(dst, tmp, (size_t)c);
+  return c;
 }
 
 /* LZ4 block decoder (spec restatement).  Returns the decoded size, or -1 on malformed input. */
@@ -203,14 +248,14 @@ static int lz4_level(uint32_t bs) {
 
 /* One LZ4BlockOutputStream stream of src[0, n) (n > 0); returns its size.  dst must hold
  * n + (n / bs + 1) * 21 + 21 bytes. */
-uint64_t o_lz4_stream(const uint8_t* src, uint64_t n, uint32_t bs, int32_t hash_bits, uint8_t* dst) {
+uint64_t o_lz4_stream(const uint8_t* src, uint64_t n, uint32_t bs, uint8_t* dst) {
   const int level = lz4_level(bs);
   uint64_t o = 0;
   for (uint64_t a = 0; a < n; a += bs) {
     const uint32_t len = (uint32_t)(n - a < bs ? n - a : bs);
     uint8_t* h = dst + o;
     memcpy(h, "LZ4Block", 8);
-    const int32_t c = o_lz4_compress_block(src + a, (int32_t)len, hash_bits, h + 21);
+    const int32_t c = o_lz4_compress_block(src + a, (int32_t)len, h + 21);
     if (c == 0) memcpy(h + 21, src + a, len);
     h[8] = (uint8_t)((c ? 0x20 : 0x10) | level);
     wr32(h + 9, c ? (uint32_t)c : len);
@@ -228,7 +273,7 @@ uint64_t o_lz4_stream(const uint8_t* src, uint64_t n, uint32_t bs, int32_t hash_
 /* Every (map, partition) run of consecutive map outputs -> its stream (empty runs: nothing),
  * and the per-map index of the compressed output (R + 1 int64 per map, native). */
 uint64_t o_lz4_map_outputs(const uint8_t* data, const int64_t* index, int32_t maps, int32_t R,
-                           uint32_t bs, int32_t hash_bits, uint8_t* out, int64_t* out_index) {
+                           uint32_t bs, uint8_t* out, int64_t* out_index) {
   uint64_t in = 0, o = 0;
   for (int32_t m = 0; m < maps; ++m) {
     const int64_t* im = index + (int64_t)m * (R + 1);
@@ -237,7 +282,7 @@ uint64_t o_lz4_map_outputs(const uint8_t* data, const int64_t* index, int32_t ma
     for (int32_t p = 0; p < R; ++p) {
       om[p] = (int64_t)(o - mo);
       const uint64_t L = (uint64_t)(im[p + 1] - im[p]);
-      if (L) o += o_lz4_stream(data + in + im[p], L, bs, hash_bits, out + o);
+      if (L) o += o_lz4_stream(data + in + im[p], L, bs, out + o);
     }
     om[R] = (int64_t)(o - mo);
     in += (uint64_t)im[R];

@@ -69,11 +69,12 @@ uint64_t o_checksum(const uint8_t* p, uint64_t n);
 
 /* compressed map outputs (lz4.c) */
 uint32_t o_xxh32(const uint8_t* p, uint64_t len, uint32_t seed);
-int32_t o_lz4_compress_block(const uint8_t* src, int32_t len, int32_t hash_bits, uint8_t* dst);
+int32_t o_lz4_compress_default(const uint8_t* src, int32_t len, uint8_t* dst);
+int32_t o_lz4_compress_block(const uint8_t* src, int32_t len, uint8_t* dst);
 int32_t o_lz4_decompress_block(const uint8_t* src, int32_t slen, uint8_t* dst, int32_t cap);
-uint64_t o_lz4_stream(const uint8_t* src, uint64_t n, uint32_t bs, int32_t hash_bits, uint8_t* dst);
+uint64_t o_lz4_stream(const uint8_t* src, uint64_t n, uint32_t bs, uint8_t* dst);
 uint64_t o_lz4_map_outputs(const uint8_t* data, const int64_t* index, int32_t maps, int32_t R,
-                           uint32_t bs, int32_t hash_bits, uint8_t* out, int64_t* out_index);
+                           uint32_t bs, uint8_t* out, int64_t* out_index);
 int64_t o_lz4_unframe(const uint8_t* s, uint64_t n, uint8_t* dst, uint64_t cap);
 
 #ifdef __cplusplus

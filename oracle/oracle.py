@@ -67,10 +67,11 @@ def lib() -> C.CDLL:
                                         C.POINTER(CpuResult)]),
             "o_checksum": (U64, [P, U64]),
             "o_xxh32": (U32, [P, U64, U32]),
-            "o_lz4_compress_block": (I32, [P, I32, I32, P]),
+            "o_lz4_compress_default": (I32, [P, I32, P]),
+            "o_lz4_compress_block": (I32, [P, I32, P]),
             "o_lz4_decompress_block": (I32, [P, I32, P, I32]),
-            "o_lz4_stream": (U64, [P, U64, U32, I32, P]),
-            "o_lz4_map_outputs": (U64, [P, P, I32, I32, U32, I32, P, P]),
+            "o_lz4_stream": (U64, [P, U64, U32, P]),
+            "o_lz4_map_outputs": (U64, [P, P, I32, I32, U32, P, P]),
             "o_lz4_unframe": (C.c_int64, [P, U64, P, U64]),
         }
         for k, (r, a) in sig.items():
@@ -349,19 +350,25 @@ def varlen_write_maps(part: Partitioner | None, data: np.ndarray, offs: np.ndarr
 
 
 # ---- compressed map outputs (oracle/lz4.c) -------------------------------
-LZ4_HASH_BITS = 11  # the GPU compressor's table (sux_lz4.hip)
-
-
 def xxh32(b: np.ndarray, seed: int = 0x9747B28C) -> int:
     b = np.ascontiguousarray(b, np.uint8)
     return int(lib().o_xxh32(_p(b), b.size, seed))
 
 
-def lz4_compress_block(b: np.ndarray, hash_bits: int = LZ4_HASH_BITS) -> bytes | None:
-    """The GPU parse restated; None = stored raw."""
+def lz4_compress_default(b: np.ndarray) -> bytes:
+    """liblz4 1.9.3 LZ4_compress_default restated (oracle/lz4.c): the LZ4 block, always."""
+    b = np.ascontiguousarray(b, np.uint8)
+    out = np.empty(b.size + b.size // 255 + 16, np.uint8)
+    n = lib().o_lz4_compress_default(_p(b) if b.size else None, b.size, _p(out))
+    return out[:n].tobytes()
+
+
+def lz4_compress_block(b: np.ndarray) -> bytes | None:
+    """One LZ4BlockOutputStream chunk's payload: the LZ4 block, or None = stored raw (the block
+    would not be shorter, lz4-java's rule)."""
     b = np.ascontiguousarray(b, np.uint8)
     out = np.empty(max(16, b.size), np.uint8)
-    n = lib().o_lz4_compress_block(_p(b), b.size, hash_bits, _p(out))
+    n = lib().o_lz4_compress_block(_p(b) if b.size else None, b.size, _p(out))
     return None if n == 0 else out[:n].tobytes()
 
 
@@ -374,8 +381,7 @@ def lz4_decompress_block(src: bytes, size: int) -> bytes:
     return out[:size].tobytes()
 
 
-def lz4_map_outputs(data: np.ndarray, index: np.ndarray, maps: int, R: int, block_size: int,
-                    hash_bits: int = LZ4_HASH_BITS):
+def lz4_map_outputs(data: np.ndarray, index: np.ndarray, maps: int, R: int, block_size: int):
     """Compressed map outputs: (out bytes, index i64[maps*(R+1)], index_be bytes)."""
     data = np.ascontiguousarray(data, np.uint8)
     index = np.ascontiguousarray(index, np.int64)
@@ -384,7 +390,7 @@ def lz4_map_outputs(data: np.ndarray, index: np.ndarray, maps: int, R: int, bloc
     out = np.empty(cap, np.uint8)
     oix = np.empty(maps * (R + 1), np.int64)
     n = lib().o_lz4_map_outputs(_p(data) if data.size else None, _p(index), maps, R, block_size,
-                                hash_bits, _p(out), _p(oix))
+                                _p(out), _p(oix))
     return out[:n].tobytes(), oix, oix.astype(">i8").tobytes()
 
 

@@ -13,21 +13,13 @@
 // Kernels (one launch each, sizes bounded on the host so nothing waits on the device):
 //   k_lz4_map_base  map data starts (maps are consecutive: prefix of index[m][R])
 //   k_lz4_runs      chunks per run -> (rocprim scan) -> k_lz4_fill: chunk table, map-major
-//   k_lz4_compress  one wave per chunk: LZ4 block format, window-parallel parse (below)
+//   k_lz4_default   one wave per chunk: liblz4's LZ4_compress_default, exactly (below)
 //   k_xxh32         4 lanes per chunk (XXH32's four accumulators), 16 chunks per wave
 //   k_lz4_sizes     framed size of every chunk (+ the end mark on a run's last chunk)
 //                   -> (rocprim scan) -> output offsets; run sizes -> k_map_scan -> index
 //   k_lz4_emit      one wave per chunk: header + payload (compressed or raw) + end mark
 //
-// The parse (deterministic; oracle.c o_lz4_compress_block restates it):
-//   positions are visited in windows of 64 (one per lane).  A window is hashed when the parse
-//   enters it: candidate = the hash table entry as it stood at the window's start (the latest
-//   earlier position with that hash, else position 0; u32 entries = position << 16 | the high
-//   16 bits of its 4 bytes), then every lane's position is max-merged into the table.  A
-//   position is a match candidate if the tags agree, the offset is 1..65535 and it lies at or
-//   before len - 12 (LZ4's MFLIMIT); the parse takes it if all 4 bytes agree.  Matches extend forward while input bytes agree, up to
-//   len - 5 (LASTLITERALS), greedily from the current position; windows wholly inside a match
-//   are skipped (not hashed).  Chunks that would not shrink are stored raw.
+// The parse is liblz4 1.9.3's LZ4_compress_default, byte for byte (k_lz4_default below).
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -42,7 +34,6 @@ namespace sux {
 namespace {
 constexpr int kLWave = 64;
 constexpr int kLz4Hdr = 21;
-constexpr int kLz4HashBits = 11;  // oracle.py LZ4_HASH_BITS
 constexpr uint32_t kXxhSeed = 0x9747b28cu;
 constexpr uint32_t P1 = 2654435761u, P2 = 2246822519u, P3 = 3266489917u, P4 = 668265263u,
                    P5 = 374761393u;
@@ -86,11 +77,6 @@ __device__ __forceinline__ void wave_copy(uint8_t* dst, const uint8_t* src, uint
 
 __device__ __forceinline__ uint32_t ext_bytes(uint32_t v) { return v >= 15u ? (v - 15u) / 255u + 1u : 0u; }
 
-// lane-parallel LZ4 length extension: (v - 15) as 255s then the remainder
-__device__ __forceinline__ void put_ext(uint8_t* d, uint32_t v, int lane) {
-  const uint32_t nb = ext_bytes(v);
-  for (uint32_t k = lane; k < nb; k += kLWave) d[k] = (k + 1 < nb) ? 255u : (uint8_t)((v - 15u) % 255u);
-}
 
 __host__ __device__ __forceinline__ int lz4_level(uint32_t bs) {
   const int l = 32 - __builtin_clz(bs - 1u);
@@ -159,119 +145,212 @@ __global__ __launch_bounds__(256) void k_lz4_fill(const int64_t* __restrict__ in
   if (r + 1 == runs) *nchunks = b0[r] + n;
 }
 
-// One wave per chunk.  HB = hash bits (table of 2^HB u64 entries per wave in LDS).
-template <int HB>
-__global__ __launch_bounds__(256) void k_lz4_compress(const uint8_t* __restrict__ data,
-                                                      Lz4Chunk* __restrict__ chunks,
-                                                      const uint32_t* __restrict__ nchunks,
-                                                      uint8_t* __restrict__ scratch) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t ltab[];
+// One wave per chunk: liblz4 1.9.3's LZ4_compress_default (oracle/lz4.c o_lz4_compress_default
+// restates it; tests pin both to the system liblz4), the compressor lz4-java's JNI instance runs
+// for every chunk of Spark's LZ4BlockOutputStream.  The hash table is liblz4's: 8192 u16
+// positions (byU16, 13-bit hash of the 4 bytes at a position), zeroed per chunk — a never
+// written entry reads as position 0 and is a real candidate.  The parse is sequential by
+// definition; the wave runs it exactly, parallelising what can be:
+//   - the match search probes positions q_i = q_0 + sum(step) (step 1 for 64 probes, then 2,
+//     3, ...: liblz4's acceleration schedule), 64 probes per round, one per lane.  Probe i sees
+//     the table as liblz4 would: the entry of the latest earlier probe of this round with the
+//     same hash (13-ballot match), else the table as it stood before the round.  The first
+//     probe whose candidate's 4 bytes agree ends the search; only the probes up to it are
+//     inserted (later lanes never happened).  A probe whose successor would pass len - 11 ends
+//     the parse (last literals) before its own insertion, as in liblz4;
+//   - the backward catch-up, the forward match count (LZ4_count up to len - 5) and the literal
+//     copies are wave-wide compares / copies;
+//   - the table updates after a match (ip - 2, then the probe of ip itself) are single-lane.
+// A chunk whose block would not be shorter than the chunk is stored raw (lz4-java's rule); the
+// parse stops as soon as that is certain, so the scratch never needs more than the chunk's bytes.
+constexpr int kLz4TabBits = 13;          // liblz4: LZ4_HASHLOG + 1 for byU16 tables
+constexpr int kLz4Waves = 2;             // waves per workgroup: 2 x 16 KiB of tables
+
+__device__ __forceinline__ uint32_t lz4_hash(uint32_t seq) { return (seq * P1) >> (32 - kLz4TabBits); }
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
+// bytes of an LZ4 length field beyond its 4-bit token nibble: (v - 15) as 255s then the rest
+__device__ __forceinline__ void put_len(uint8_t* d, uint32_t v, int lane) {
+  const uint32_t nb = ext_bytes(v);
+  for (uint32_t k = lane; k < nb; k += kLWave) d[k] = (k + 1 < nb) ? 255u : (uint8_t)((v - 15u) % 255u);
+}
+
+__global__ __launch_bounds__(kLz4Waves * kLWave) void k_lz4_default(
+    const uint8_t* __restrict__ data, Lz4Chunk* __restrict__ chunks,
+    const uint32_t* __restrict__ nchunks, uint8_t* __restrict__ scratch) {
+  __shared__ __attribute__((aligned(16))) uint16_t ltab[kLz4Waves][1u << kLz4TabBits];
   const int wave = threadIdx.x / kLWave, lane = threadIdx.x % kLWave;
-  uint32_t* tab = ltab + (size_t)wave * (1u << HB);
+  uint16_t* tab = ltab[wave];
+  const uint64_t lt = (1ull << lane) - 1ull;
   const uint32_t n = *nchunks;
-  for (uint32_t b = blockIdx.x * 4u + wave; b < n; b += gridDim.x * 4u) {
+  for (uint32_t b = blockIdx.x * kLz4Waves + wave; b < n; b += gridDim.x * kLz4Waves) {
     const Lz4Chunk C = chunks[b];
     const uint8_t* src = data + C.src;
     const uint32_t len = C.len;
     uint8_t* dst = scratch + ((C.src + 16ull * b) & ~3ull);
-    bool raw = len < 13;
-    uint32_t op = 0, anchor = 0, cur = 0;
+    bool raw = len < 13;  // LZ4_minLength: one literal run, never shorter than the chunk
     if (!raw) {
-      // every entry starts as position 0 with position 0's true bytes (a verifiable candidate)
-      const uint32_t e0 = ld32u(src) >> 16;
-      for (uint32_t i = lane; i < (1u << HB); i += kLWave) tab[i] = e0;
-      __builtin_amdgcn_wave_barrier();
-      const uint32_t last = len - 12;         // last position a match may start at
-      const uint32_t mlimit = len - 5;        // matches end at or before this
-      const uint32_t nwin = last / kLWave + 1;
-      uint32_t w = 0;
-      // the 4 bytes at this lane's position of the NEXT window are loaded while the current
-      // window is parsed (the parse only ever moves forward)
-      uint32_t pf = ld32u(src + min((uint32_t)lane, last));
-      while (w < nwin) {
-        const uint32_t pos = w * kLWave + lane;
-        const bool in = pos <= last;
-        const uint32_t seq = pf;
-        pf = ld32u(src + min(pos + kLWave, last));
-        const uint32_t h = (seq * P1) >> (32 - HB);
-        const uint32_t e = tab[h];
-        const uint32_t cpos = e >> 16;
-        // 16-bit tag check here; the parse confirms all 4 bytes before taking a match
-        const bool m = in && cpos < pos && pos - cpos <= 65535u && (e & 0xFFFFu) == (seq >> 16);
-        __builtin_amdgcn_wave_barrier();
-        if (in) atomicMax(&tab[h], (pos << 16) | (seq >> 16));
-        __builtin_amdgcn_wave_barrier();
-        uint64_t mm = __ballot(m);
-        uint32_t nextw = w + 1;
+      // LZ4_initStream: a zeroed table
+      typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+      for (uint32_t i = lane; i < (1u << kLz4TabBits) / 8; i += kLWave)
+        reinterpret_cast<u4*>(tab)[i] = u4{0u, 0u, 0u, 0u};
+      wave_lds_sync();
+      const uint32_t mflimit1 = len - 11, matchlimit = len - 5;
+      uint32_t anchor = 0, op = 0, ip = 1, match = 0;
+      bool last = false;  // go to the last literals
+      // ---- find a match from ip (liblz4's do-while search), 64 probes per round
+      auto search = [&]() -> bool {  // true: (ip, match) is a match; false: last literals
+        uint32_t q0 = ip, probe0 = 0;
         while (true) {
-          const uint32_t rel = cur > w * kLWave ? cur - w * kLWave : 0u;
-          if (rel >= (uint32_t)kLWave) break;
-          const uint64_t mk = mm & (~0ull << rel);
-          if (!mk) break;
-          const int j = __builtin_ctzll(mk);
-          const uint32_t p = w * kLWave + j;
-          const uint32_t c = (uint32_t)__shfl((int)cpos, j, kLWave);
-          // forward comparison from the first byte, 256 bytes per round
-          uint32_t ml = 0;
-          while (true) {
-            const uint32_t lim = mlimit - (p + ml);  // bytes still allowed
-            const uint32_t o = 4u * lane;
-            uint32_t eq = 0;
-            if (o < lim) {
-              const uint32_t x = ld32u(src + p + ml + o) ^ ld32u(src + c + ml + o);
-              eq = x ? (uint32_t)(__builtin_ctz(x) >> 3) : 4u;
-              eq = min(eq, lim - o);
-            }
-            const uint64_t stop = __ballot(eq < 4u);
-            if (stop) {
-              const int s = __builtin_ctzll(stop);
-              ml += 4u * s + (uint32_t)__shfl((int)eq, s, kLWave);
-              break;
-            }
-            ml += 4u * kLWave;
+          const uint32_t i = probe0 + (uint32_t)lane;
+          const uint32_t s = i == 0 ? 1u : (63u + i) >> 6;
+          uint32_t incl = s;
+#pragma unroll
+          for (int d = 1; d < kLWave; d <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_up((int)incl, d, kLWave);
+            if (lane >= d) incl += t;
           }
-          if (ml < 4) {  // tag collision: no match here
-            mm &= ~(1ull << j);
+          const uint32_t q = q0 + incl - s, nxt = q + s;
+          const bool live = nxt <= mflimit1;  // monotone over the lanes
+          const uint32_t seq = ld32u(src + (live ? q : 0u));
+          const uint32_t h = lz4_hash(seq);
+          uint64_t peers = __ballot(live);
+#pragma unroll
+          for (int bb = 0; bb < kLz4TabBits; ++bb) {
+            const bool bit = (h >> bb) & 1u;
+            const uint64_t m = __ballot(bit);
+            peers &= bit ? m : ~m;
+          }
+          const uint64_t prev = peers & lt;
+          const uint32_t from_tab = tab[h];
+          const uint32_t pl = prev ? 63u - (uint32_t)__builtin_clzll(prev) : 0u;
+          const uint32_t qprev = (uint32_t)__shfl((int)q, (int)pl, kLWave);
+          const uint32_t m = prev ? qprev : from_tab;
+          const bool hit = live && ld32u(src + m) == seq;
+          const uint64_t hits = __ballot(hit), lives = __ballot(live);
+          const uint64_t commit = hits ? (lives & ((2ull << __builtin_ctzll(hits)) - 1ull)) : lives;
+          wave_lds_sync();  // every lane read the table before any insertion of this round
+          const uint64_t later = peers & ~lt & ~(1ull << lane) & commit;
+          if (((commit >> lane) & 1ull) && !later) tab[h] = (uint16_t)q;
+          wave_lds_sync();
+          if (hits) {
+            const int f = __builtin_ctzll(hits);
+            ip = (uint32_t)__shfl((int)q, f, kLWave);
+            match = (uint32_t)__shfl((int)m, f, kLWave);
+            return true;
+          }
+          if (~lives) return false;  // a probe's successor passed mflimitPlusOne
+          q0 = (uint32_t)__shfl((int)nxt, kLWave - 1, kLWave);
+          probe0 += kLWave;
+        }
+      };
+      // emits one sequence (literals [anchor, ip) + the match at ip); false = the block cannot be
+      // shorter than the chunk (stored raw)
+      auto sequence = [&]() -> bool {
+        // forward count (LZ4_count): equal bytes from ip + 4 / match + 4 up to matchlimit
+        uint32_t mc = 0;
+        while (true) {
+          const uint32_t a = ip + 4u + mc;
+          const uint32_t lim = matchlimit > a ? matchlimit - a : 0u;
+          const uint32_t o = 4u * (uint32_t)lane;
+          uint32_t eq = 0;
+          if (o < lim) {
+            const uint32_t x = ld32u(src + a + o) ^ ld32u(src + match + 4u + mc + o);
+            eq = x ? (uint32_t)(__builtin_ctz(x) >> 3) : 4u;
+            eq = min(eq, lim - o);
+          }
+          const uint64_t stop = __ballot(eq < 4u);
+          if (stop) {
+            const int sl = __builtin_ctzll(stop);
+            mc += 4u * (uint32_t)sl + (uint32_t)__shfl((int)eq, sl, kLWave);
+            break;
+          }
+          mc += 4u * kLWave;
+        }
+        const uint32_t ll = ip - anchor;
+        const uint32_t need = 1u + ext_bytes(ll) + ll + 2u + ext_bytes(mc);
+        if (op + need >= len) return false;
+        uint8_t* d = dst + op;
+        if (lane == 0) d[0] = (uint8_t)((min(ll, 15u) << 4) | min(mc, 15u));
+        put_len(d + 1, ll, lane);
+        const uint32_t lo = 1u + ext_bytes(ll);
+        wave_copy(d + lo, src + anchor, ll, lane);
+        const uint32_t off = ip - match;
+        if (lane == 0) {
+          d[lo + ll] = (uint8_t)off;
+          d[lo + ll + 1] = (uint8_t)(off >> 8);
+        }
+        put_len(d + lo + ll + 2, mc, lane);
+        op += need;
+        ip += mc + 4u;
+        anchor = ip;
+        return true;
+      };
+      while (!last && !raw) {
+        if (!search()) {
+          last = true;
+          break;
+        }
+        // catch up: extend backwards while ip > anchor, match > 0 and the bytes before agree
+        while (true) {
+          const uint32_t room = min(ip - anchor, match);
+          if (room == 0) break;
+          const uint32_t k = (uint32_t)lane + 1u;
+          const bool eq = k <= room && src[ip - k] == src[match - k];
+          const uint64_t ne = __ballot(!eq);
+          const uint32_t back = ne ? (uint32_t)__builtin_ctzll(ne) : (uint32_t)kLWave;
+          ip -= back;
+          match -= back;
+          if (back < (uint32_t)kLWave) break;
+        }
+        // the match, then liblz4's immediate re-probes at the match end
+        while (true) {
+          if (!sequence()) {
+            raw = true;
+            break;
+          }
+          if (ip >= mflimit1) {
+            last = true;
+            break;
+          }
+          const uint32_t h2 = lz4_hash(ld32u(src + ip - 2u));
+          const uint32_t seq = ld32u(src + ip);
+          const uint32_t h = lz4_hash(seq);
+          if (lane == 0) tab[h2] = (uint16_t)(ip - 2u);
+          wave_lds_sync();
+          const uint32_t mi = tab[h];
+          wave_lds_sync();
+          if (lane == 0) tab[h] = (uint16_t)ip;
+          wave_lds_sync();
+          if (ld32u(src + mi) == seq) {  // a new sequence with no literals
+            match = mi;
             continue;
           }
-          const uint32_t LL = p - anchor;
-          const uint32_t need = 1u + ext_bytes(LL) + LL + 2u + ext_bytes(ml - 4u);
-          if (op + need >= len) { raw = true; break; }
-          uint8_t* d = dst + op;
-          if (lane == 0) d[0] = (uint8_t)((min(LL, 15u) << 4) | min(ml - 4u, 15u));
-          put_ext(d + 1, LL, lane);
-          const uint32_t lo = 1u + ext_bytes(LL);
-          wave_copy(d + lo, src + anchor, LL, lane);
-          const uint32_t off = p - c;
-          if (lane == 0) {
-            d[lo + LL] = (uint8_t)off;
-            d[lo + LL + 1] = (uint8_t)(off >> 8);
-          }
-          put_ext(d + lo + LL + 2, ml - 4u, lane);
-          op += need;
-          cur = p + ml;
-          anchor = cur;
-          if (cur >= (w + 1) * kLWave) { nextw = cur / kLWave; break; }
+          ip += 1u;  // the search restarts after the probed position
+          break;
         }
-        if (raw) break;
-        if (nextw != w + 1) pf = ld32u(src + min(nextw * kLWave + lane, last));
-        w = nextw;
       }
       if (!raw) {
-        const uint32_t LL = len - anchor;
-        const uint32_t need = 1u + ext_bytes(LL) + LL;
+        const uint32_t ll = len - anchor;
+        const uint32_t need = 1u + ext_bytes(ll) + ll;
         if (op + need >= len) {
           raw = true;
         } else {
           uint8_t* d = dst + op;
-          if (lane == 0) d[0] = (uint8_t)(min(LL, 15u) << 4);
-          put_ext(d + 1, LL, lane);
-          wave_copy(d + 1 + ext_bytes(LL), src + anchor, LL, lane);
+          if (lane == 0) d[0] = (uint8_t)(min(ll, 15u) << 4);
+          put_len(d + 1, ll, lane);
+          wave_copy(d + 1 + ext_bytes(ll), src + anchor, ll, lane);
           op += need;
         }
       }
+      if (lane == 0) chunks[b].clen = raw ? 0u : op;
+    } else if (lane == 0) {
+      chunks[b].clen = 0u;
     }
-    if (lane == 0) chunks[b].clen = raw ? 0u : op;
   }
 }
 
@@ -453,22 +532,10 @@ hipError_t launch_lz4_compress(const uint8_t* d_data, const int64_t* d_index, ui
   hipLaunchKernelGGL(k_lz4_fill, dim3(rg), dim3(256), 0, s, d_index, (int)maps, (int)R, bs, map_base,
                      b0, chunks, nchunks);
   const uint32_t cg = (uint32_t)std::min<uint64_t>((w.chunk_bound + 3) / 4, 8192);
-  static const int hb = [] {
-    const char* e = getenv("SUX_LZ4_HB");
-    return e ? atoi(e) : kLz4HashBits;
-  }();
-  const size_t lds = 4 * (size_t(1) << hb) * 4;
-  if (hb == 10)
-    hipLaunchKernelGGL((k_lz4_compress<10>), dim3(cg), dim3(256), lds, s, d_data, chunks, nchunks,
-                       scratch);
-  else if (hb == 12) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lz4_compress<12>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((k_lz4_compress<12>), dim3(cg), dim3(256), lds, s, d_data, chunks, nchunks,
-                       scratch);
-  } else
-    hipLaunchKernelGGL((k_lz4_compress<11>), dim3(cg), dim3(256), lds, s, d_data, chunks, nchunks,
-                       scratch);
+  const uint32_t zg = (uint32_t)std::min<uint64_t>((w.chunk_bound + kLz4Waves - 1) / kLz4Waves,
+                                                   256u * 16u);
+  hipLaunchKernelGGL(k_lz4_default, dim3(zg), dim3(kLz4Waves * kLWave), 0, s, d_data, chunks,
+                     nchunks, scratch);
   const uint32_t xg = (uint32_t)std::min<uint64_t>((w.chunk_bound + 63) / 64, 4096);
   hipLaunchKernelGGL(k_xxh32, dim3(xg), dim3(256), 0, s, d_data, chunks, nchunks);
   const uint32_t bg = (uint32_t)((w.chunk_bound + 255) / 256);

@@ -1,9 +1,11 @@
 """GPU parity: compressed map outputs (spark.shuffle.compress=true with the
-lz4 codec) — sux_compress_map_outputs against oracle/lz4.c.
+lz4 codec) — sux_compress_map_outputs against oracle/lz4.c and against the system liblz4.
 
-Bit-exact: the framed streams (headers, XXH32 checksums, LZ4 blocks of the GPU parse restated in
-o_lz4_compress_block, raw chunks, end marks) and the index tables.  Independently, every stream
-decodes — through the oracle's LZ4Block reader and the system liblz4 — to the uncompressed run.
+Bit-exact: the framed streams (headers, XXH32 checksums, LZ4 blocks, raw chunks, end marks) and
+the index tables vs the oracle, whose compressor restates liblz4's LZ4_compress_default; and,
+independently of the oracle, every chunk the GPU compressed is byte-for-byte the system
+liblz4.so.1.9.3's LZ4_compress_default of that chunk (every raw chunk one liblz4 could not
+shrink) — the bytes lz4-java's JNI compressor gives Spark's LZ4BlockOutputStream.
 """
 import numpy as np
 import pytest
@@ -101,8 +103,7 @@ def test_synthetic_runs(gpu_node, pattern):
     check(gpu_node, data, index.ravel(), maps, R, 32768)
 
 
-def test_liblz4_decodes_gpu_blocks(gpu_node):
-    """The GPU's LZ4 blocks through the system liblz4 decoder (skipped if it is absent)."""
+def _liblz4():
     import ctypes as C
     import ctypes.util
     name = ctypes.util.find_library("lz4") or "liblz4.so.1"
@@ -110,19 +111,63 @@ def test_liblz4_decodes_gpu_blocks(gpu_node):
         L = C.CDLL(name)
     except OSError:
         pytest.skip("system liblz4 not present")
+    L.LZ4_compress_default.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int]
     L.LZ4_decompress_safe.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int]
-    data, index, maps = partitioned(O.gen_zipf(35, 0, 20_000), 100, 8, 20_000, kind="hash")
-    got, gix, _ = run_gpu(gpu_node, data, index, maps, 8, 32768)
-    i, blocks = 0, 0
-    while i < len(got):
-        method, clen, olen = got[i + 8] & 0xF0, int.from_bytes(got[i + 9:i + 13], "little"), \
-            int.from_bytes(got[i + 13:i + 17], "little")
-        if method == 0x20:
-            out = C.create_string_buffer(olen)
-            assert L.LZ4_decompress_safe(got[i + 21:i + 21 + clen], out, clen, olen) == olen
-            blocks += 1
-        i += 21 + clen
-    assert blocks > 0
+    return L
+
+
+def _workload(kind):
+    if kind == "terasort":
+        return partitioned(O.gen_terasort(35, 0, 30_000), 100, 16, 15_000) + (16,)
+    if kind == "zipf":
+        return partitioned(O.gen_zipf(35, 0, 30_000), 100, 8, 15_000, kind="hash") + (8,)
+    if kind == "small":
+        return partitioned(O.gen_small(36, 0, 200_000), 16, 32, 100_000, kind="hash") + (32,)
+    if kind == "rows":
+        d, o = O.gen_unsafe_rows(37, 40_000, key_mod=500)
+        out, ix, _, _ = O.varlen_write_maps(O.Partitioner(O.MURMUR3_LONG, 10, 12, 8), d, o, 20_000)
+        return out, ix, 2, 10
+    rng = np.random.default_rng(5)
+    n = 300_000
+    data = rng.integers(0, 256, n, dtype=np.uint8)
+    data[rng.random(n) < (0.9 if kind == "sparse" else 0.5)] = 0
+    return data, np.array([0, n // 3, n // 3, n], np.int64), 1, 3
+
+
+@pytest.mark.parametrize("kind", ["terasort", "zipf", "small", "rows", "sparse", "half"])
+def test_gpu_chunks_are_liblz4_compress_default(gpu_node, kind):
+    """Every chunk of every GPU stream vs the system liblz4, not via the oracle."""
+    import ctypes as C
+    L = _liblz4()
+    data, index, maps, R = _workload(kind)
+    bs = 32768
+    got, gix, _ = run_gpu(gpu_node, data, index, maps, R, bs)
+    base_in = base_out = 0
+    compressed = 0
+    for m in range(maps):
+        im = index[m * (R + 1):(m + 1) * (R + 1)]
+        om = gix[m * (R + 1):(m + 1) * (R + 1)]
+        for p in range(R):
+            raw = data[base_in + im[p]:base_in + im[p + 1]].tobytes()
+            enc = got[base_out + om[p]:base_out + om[p + 1]]
+            i = 0
+            for a in range(0, len(raw), bs):
+                chunk = raw[a:a + bs]
+                method = enc[i + 8] & 0xF0
+                clen = int.from_bytes(enc[i + 9:i + 13], "little")
+                cap = len(chunk) + len(chunk) // 255 + 16
+                buf = C.create_string_buffer(cap)
+                nw = L.LZ4_compress_default(chunk, buf, len(chunk), cap)
+                want = buf.raw[:nw]
+                if len(want) < len(chunk):
+                    assert method == 0x20 and enc[i + 21:i + 21 + clen] == want, (kind, m, p, a)
+                    compressed += 1
+                else:
+                    assert method == 0x10 and enc[i + 21:i + 21 + clen] == chunk, (kind, m, p, a)
+                i += 21 + clen
+        base_in += int(im[R])
+        base_out += int(om[R])
+    assert compressed > 0
 
 
 def test_empty_and_single(gpu_node):

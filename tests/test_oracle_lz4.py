@@ -1,7 +1,9 @@
 """CPU: the compressed-map-output oracle (oracle/lz4.c) pinned against
-independent implementations present in this image: XXH32 against the python xxhash module, the
-LZ4 block format against the system liblz4 (LZ4_decompress_safe decodes the oracle's blocks;
-the oracle's decoder decodes LZ4_compress_default's blocks)."""
+independent implementations present in this image: XXH32 against the python xxhash module, and
+the LZ4 compressor against the system liblz4 1.9.3 — o_lz4_compress_default must produce
+LZ4_compress_default's bytes exactly (the compressor lz4-java's JNI instance runs for Spark), on
+every input below, including the shapes the GPU kernel finds hardest (no match at all, matches
+from the never-written table entries that read as position 0, overlapping matches, long runs)."""
 import ctypes as C
 import ctypes.util
 
@@ -31,6 +33,14 @@ needs_lz4 = pytest.mark.skipif(LZ4 is None, reason="system liblz4 not present")
 
 def samples():
     rng = np.random.default_rng(7)
+    yield np.frombuffer(b"abcdabcdabcdabcd" * 3, np.uint8)                # 48 B, overlap
+    yield np.frombuffer(b"x" * 12 + b"y", np.uint8)                        # min length
+    yield np.frombuffer(bytes(range(200)) + bytes(range(200)), np.uint8)   # one far match
+    z = rng.integers(0, 256, 5000, dtype=np.uint8)
+    z[:4] = z[4000:4004]                                                   # hit via entry 0
+    yield z
+    yield np.concatenate([rng.integers(0, 256, 3000, dtype=np.uint8), np.zeros(3000, np.uint8),
+                          rng.integers(0, 256, 3000, dtype=np.uint8)])
     yield np.zeros(0, np.uint8)
     yield np.zeros(13, np.uint8)
     yield np.zeros(40_000, np.uint8)
@@ -64,6 +74,45 @@ def test_blocks_decode_with_liblz4():
             n = LZ4.LZ4_decompress_safe(blk, out, len(blk), chunk.size)
             assert n == chunk.size and out.raw == chunk.tobytes()
             assert O.lz4_decompress_block(blk, chunk.size) == chunk.tobytes()
+
+
+def _liblz4_compress(s: np.ndarray) -> bytes:
+    cap = s.size + s.size // 255 + 16
+    out = C.create_string_buffer(cap)
+    n = LZ4.LZ4_compress_default(s.tobytes(), out, s.size, cap)
+    assert n > 0
+    return out.raw[:n]
+
+
+@needs_lz4
+def test_compress_default_is_liblz4_bit_exact():
+    for s in samples():
+        for a in range(0, max(1, s.size), 65536):
+            chunk = s[a:a + 65536]
+            assert O.lz4_compress_default(chunk) == _liblz4_compress(chunk), (s.size, a)
+
+
+@needs_lz4
+@pytest.mark.parametrize("kind", ["terasort", "zipf", "small", "rows", "text", "runs"])
+def test_compress_default_is_liblz4_bit_exact_on_workloads(kind):
+    """32 KiB chunks (Spark's spark.io.compression.lz4.blockSize) of every workload's bytes."""
+    rng = np.random.default_rng(11)
+    if kind == "terasort":
+        data = O.gen_terasort(3, 0, 4000)
+    elif kind == "zipf":
+        data = O.gen_zipf(3, 0, 4000)
+    elif kind == "small":
+        data = O.gen_small(3, 0, 30000)
+    elif kind == "rows":
+        data = O.gen_unsafe_rows(5, 6000, key_mod=101)[0]
+    elif kind == "text":
+        words = [b"shuffle", b"spark", b"partition", b"record", b"the", b"of", b"GPU", b" ", b"\n"]
+        data = np.frombuffer(b"".join(words[i] for i in rng.integers(0, len(words), 60000)), np.uint8)
+    else:
+        data = np.repeat(rng.integers(0, 256, 4000, dtype=np.uint8), rng.integers(1, 40, 4000))
+    for a in range(0, data.size, 32768):
+        chunk = data[a:a + 32768]
+        assert O.lz4_compress_default(chunk) == _liblz4_compress(chunk), (kind, a)
 
 
 @needs_lz4
