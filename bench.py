@@ -338,6 +338,42 @@ def plugin_leg(node, part, data, rs: int, R: int, rpm: int, gm: int, groups: int
             "pool": st}
 
 
+def self_check(node, part, data, out, index, n: int, rs: int, rpm: int, R: int,
+               group_recs: int, dev) -> dict:
+    """Untimed check of the map outputs of one step written into a zeroed buffer, with no CPU
+    oracle (the data are 100 GB): every map's index table starts at 0, rises, and ends at the
+    map's bytes; its output holds the same multiset of 4-byte words as its input (sum and sum
+    of squares); and the partition ids of its output records (the independent k_pids kernel)
+    never decrease and count exactly the index table's run lengths.  A sweep's number is only
+    reported when its bytes pass this."""
+    maps = -(-n // rpm)
+    ix = index[:maps * (R + 1)].view(maps, R + 1)
+    lens = torch.full((maps,), rpm * rs, dtype=torch.int64, device=dev)
+    lens[-1] = (n - (maps - 1) * rpm) * rs
+    if not (bool((ix[:, 0] == 0).all()) and bool((ix[:, 1:] >= ix[:, :-1]).all())
+            and torch.equal(ix[:, R], lens)):
+        raise RuntimeError("self-check: index tables are not each map's run offsets")
+    for r0 in range(0, n, group_recs):
+        r1 = min(n, r0 + group_recs)
+        for a, b in ((data, out),):
+            wa = a[r0 * rs:r1 * rs].view(torch.int32).to(torch.int64)
+            wb = b[r0 * rs:r1 * rs].view(torch.int32).to(torch.int64)
+            if int(wa.sum()) != int(wb.sum()) or int((wa * wa).sum()) != int((wb * wb).sum()):
+                raise RuntimeError(f"self-check: records [{r0}, {r1}) are not a permutation")
+            del wa, wb
+        pid = node.partition_ids(part, out[r0 * rs:r1 * rs], rs).to(torch.int64)
+        m0 = r0 // rpm
+        for m in range(m0, -(-r1 // rpm)):
+            p = pid[(m * rpm - r0):(min(r1, (m + 1) * rpm) - r0)]
+            cnt = torch.bincount(p, minlength=R) * rs
+            if not (bool((p[1:] >= p[:-1]).all()) and torch.equal(cnt, ix[m, 1:] - ix[m, :-1])):
+                raise RuntimeError(f"self-check: map {m} is not grouped by partition as indexed")
+    torch.cuda.synchronize(dev)
+    return {"maps": maps, "records": n, "ok": True,
+            "checks": "index offsets; word multiset per launch group; output pids (k_pids) "
+                      "non-decreasing per map with counts = index runs"}
+
+
 def load_traffic(workload: str, kernel: str) -> dict | None:
     """HBM bytes per record of `kernel` under `workload`, from the committed PMC summary
     (profiles/pmc_r02.json, written by profiles/collect_pmc.py: one rocprofv3 pass per counter
@@ -373,8 +409,16 @@ def main():
                     help="test mode at N=1: run the N>1 pipeline (peer-major partition, "
                          "overlapped ncclAllGather + ncclAllToAllv) on a one-rank RCCL "
                          "communicator, so the RCCL calls run on a 1-GPU box")
+    ap.add_argument("--map-pipeline", type=int, default=1,
+                    help="N=1: 1 = one sux_partition_maps_pipelined call per step (launch "
+                         "groups on the node's two map streams, co-resident K1/K3 shapes); "
+                         "0 = one sux_partition_maps call per launch group on --streams streams")
     ap.add_argument("--streams", type=int, default=1,
-                    help="N=1: launch groups dealt round-robin to this many HIP streams")
+                    help="N=1 with --map-pipeline 0: launch groups dealt round-robin to this "
+                         "many HIP streams")
+    ap.add_argument("--tuning", default="",
+                    help="node tuning table overrides, 'field=value,...' (sux_tuning fields; "
+                         "sweeps only — the defaults are the measured best)")
     ap.add_argument("--reserve-cus", type=int, default=-1,
                     help="CUs kept free of map-side kernels for the exchange (-1: 32 if N>1, "
                          "else 0)")
@@ -394,6 +438,9 @@ def main():
     ap.add_argument("--plugin-groups", type=int, default=-1,
                     help="N=1: also time the plugin path (register -> write -> resolve -> "
                          "unregister) over this many launch groups of map tasks (-1: 8; 0: skip)")
+    ap.add_argument("--self-check", type=int, default=1,
+                    help="N=1: after the timed steps, run one more step into a zeroed output "
+                         "and check it (index offsets, record multiset, partition grouping)")
     ap.add_argument("--cpu-records", type=int, default=10_000_000)
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (0: every core this job may use, host_cores())")
@@ -446,6 +493,9 @@ def main():
     # the ipc transport needs no RCCL communicator inside the library
     node = Node(device=local, rank=rank if comm_id else 0, world_size=world if comm_id else 1,
                 comm_id=comm_id)
+    if args.tuning:
+        node.set_tuning(**{k.strip(): int(v) for k, v in
+                           (kv.split("=") for kv in args.tuning.split(",") if kv.strip())})
     if kind == N.PART_RANGE_BYTES:
         part = node.partitioner(kind, R, key_offset=0, key_len=key_len, bounds=uniform_bounds(R))
     else:
@@ -477,7 +527,7 @@ def main():
         streams = [comp] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
         wss = [torch.empty(ws_bytes, dtype=torch.uint8, device=dev) for _ in range(ns)]
 
-        def step():
+        def step_groups():
             for s in streams[1:]:
                 s.wait_stream(comp)
             for g in range(groups):
@@ -492,6 +542,13 @@ def main():
                                     workspace=wss[g % ns], stream=streams[g % ns])
             for s in streams[1:]:
                 comp.wait_stream(s)
+
+        def step_pipelined():
+            node.partition_maps_pipelined(part, data, rs, rpm, num_records=n,
+                                          group_records=group_recs, out=out, index=index,
+                                          index_be=index_be, stream=comp)
+
+        step = step_pipelined if args.map_pipeline else step_groups
     else:
         comm = torch.cuda.Stream(dev)
         # send-buffer ring: rccl frees slot s when ITS all-to-all is done (2 slots); ipc frees
@@ -646,7 +703,12 @@ def main():
     achieved = alg / sc_avg / 1e9 if sc_avg else None
     map_ms = kt["hist"][1] + kt["scan"][1] + kt["scatter"][1]
     map_alg = (2 * n * rs + 8 * (R + 1) * maps) * args.steps
-    map_side = map_alg / (map_ms / 1e3) / 1e9 if map_ms else None
+    # N=1: the step IS the map side, and with two launch groups in flight the kernels overlap,
+    # so the map side's time is the wall clock of the timed steps (the kernel sum would count
+    # the overlapped K1 twice); N>1: the map kernels run one after another on one stream
+    overlapped = not pipelined and (args.map_pipeline or args.streams > 1)
+    map_time_ms = elapsed * 1e3 if not pipelined else map_ms
+    map_side = map_alg / (map_time_ms / 1e3) / 1e9 if map_time_ms else None
     names = {k: node.kernel_variant(i) for i, k in enumerate(N.KERNELS)}
     tr = {k: load_traffic(args.workload, names[k]) for k in ("hist", "scatter") if names[k]}
     sc_tr = tr.get("scatter")
@@ -663,7 +725,10 @@ def main():
         "config": {"workload": f"{args.workload}: {n} x {rs}-byte records per GPU "
                                f"({n * rs / 1e9:.0f} GB/GPU, {n * rs * world / 1e9:.0f} GB total), "
                                f"R={R}, map batches of {rpm} records, {gm} maps per launch group"
-                               + (f" on {args.streams} streams" if world == 1 and args.streams > 1 else "")
+                               + (", two launch groups in flight (sux_partition_maps_pipelined)"
+                                  if not pipelined and args.map_pipeline else
+                                  f" on {args.streams} streams" if not pipelined and args.streams > 1
+                                  else "")
                                + (f", map side on {256 - reserve} CUs" if reserve > 0 else "")
                                + (", zero-copy local block resolve" if not pipelined else
                                   ", partition-aligned ncclAllToAllv exchange"
@@ -683,6 +748,9 @@ def main():
                               "frac": None if map_side is None else round(map_side / HBM_PEAK_GBS, 4),
                               "traffic_per_step": map_traffic,
                               "alg_bytes_per_step": int(map_alg / args.steps),
+                              "time": ("wall clock of the timed steps (launch groups overlap)"
+                                       if overlapped else "wall clock of the timed steps"
+                                       if not pipelined else "sum of the map kernels' durations"),
                               "kernels": names,
                               "kernels_ms": {k: round(v[1], 3) for k, v in kt.items()},
                               "launches": {k: v[0] for k, v in kt.items()}},
@@ -711,6 +779,13 @@ def main():
             "bound": "xgmi", "achieved": None if ach is None else round(ach, 1), "peak": peak,
             "unit": "GB/s", "frac": None if ach is None else round(ach / peak, 4),
             "remote_bytes_per_rank": remote // args.steps, "exchange_ms": round(xms, 2)}
+    if not pipelined and args.self_check:
+        out.zero_()
+        index.zero_()
+        step()
+        torch.cuda.synchronize(dev)
+        result["self_check"] = self_check(node, part, data, out, index, n, rs, rpm, R,
+                                          group_recs, dev)
     if not pipelined:
         ns = args.reduce_sort_records if args.reduce_sort_records >= 0 else n // R
         ns = min(ns, n)

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define SUX_ABI_VERSION 2
+#define SUX_ABI_VERSION 3
 
 /* ---- status codes ---------------------------------------------------------------------- */
 #define SUX_OK 0
@@ -124,6 +124,36 @@ int sux_node_set_bootstrap(sux_node* node, sux_allgather_fn fn, void* ctx);
 int sux_pool_stats(sux_node* node, uint64_t* allocated_bytes, uint64_t* requests, uint64_t* allocs,
                    uint64_t* preallocs);
 
+/* Kernel tuning table of one node.  Every field 0 = the measured default (DESIGN.md §4 records
+ * the sweeps behind each); a value outside a field's listed set is SUX_EINVAL.  Set it between
+ * calls (not while another thread is inside a call on the same node); workspace sizes follow
+ * it (tile_records), so query sux_partition_workspace_size after a change.  No knob changes a
+ * byte of any output: every variant is parity-tested against the CPU oracle. */
+typedef struct sux_tuning {
+  int32_t hist_kernel;      /* newest K1 variant allowed: 1, 2, 3, 4                            */
+  int32_t scatter_kernel;   /* newest K3 variant allowed: 1, 2, 6, 7                            */
+  int32_t coresident;       /* 1: in calls that keep two launch groups in flight, K3 shapes that
+                               leave a K1 workgroup room on the CU (measured slower: opt-in);
+                               0 or -1: not                                                     */
+  int32_t scatter_chunk;    /* k_scatter7 records per chunk: 1024, 768 (0: 768 co-resident)     */
+  int32_t scatter_depth;    /* k_scatter7 chunks loaded ahead: 1, 2 (768-record chunks only)     */
+  int32_t hist_stage;       /* k_hist4 records per LDS stage: 64, 128 (0: 64)                   */
+  int32_t s6_chunk;         /* k_scatter6 largest records per chunk: 1024, 512, 384, 256         */
+  int32_t tiles_per_item;   /* k_scatter6/7 tiles per work item (0: 8 chunks' worth), 1 .. 4096  */
+  int32_t small_groups;     /* k_scatter16b record groups per turn: 1, 2, 4                       */
+  int32_t tile_records;     /* K1 tile: power of two in [64, 2^22] (0: 4096, or more for big R)  */
+  int32_t onepass;          /* 1: the one-pass kernel whenever a map batch fits on chip          */
+  int32_t varlen_kernel;    /* variable-length rows: 1, 2                                        */
+  int32_t varlen_tile;      /* variable-length K1 tile: multiple of 64 in [64, 65536]            */
+  int32_t sort_max_digit_bits; /* widest radix digit of sux_sort_records: 8 .. 16                */
+  int32_t sort_gather;      /* 1: records gathered after the sort instead of riding in the pairs */
+  int32_t sort_all_passes;  /* 1: every digit pass runs (no key-span read-back)                  */
+  int32_t hist_wgs_per_cu;  /* k_hist4 workgroups per CU: 1 .. 8 (0: as many as LDS allows)     */
+  int32_t reserved[15];
+} sux_tuning;
+int sux_node_set_tuning(sux_node* node, const sux_tuning* tuning);
+int sux_node_get_tuning(sux_node* node, sux_tuning* tuning);
+
 /* ---- partitioner object: P1 (UcxShuffleManager.getWriter picks the writer, :36-50) ---------- */
 int sux_partitioner_create(sux_node* node, const sux_partitioner_desc* desc, sux_partitioner** out);
 int sux_partitioner_destroy(sux_partitioner* part);
@@ -144,6 +174,20 @@ int sux_partition_maps(sux_node* node, const sux_partitioner* part, const void* 
                        uint32_t record_size, uint64_t records_per_map, uint64_t num_records,
                        void* d_out, int64_t* d_index, uint8_t* d_index_be, uint16_t* d_pids,
                        void* d_workspace, uint64_t workspace_bytes, void* stream);
+
+/* sux_partition_maps over many map batches at once, the way Spark runs map tasks: several in
+ * flight.  The records are cut into launch groups of `group_records` (a multiple of
+ * records_per_map; 0 = 2^27 records' worth of whole maps) and the groups are dealt to two
+ * node-owned streams, so that while group g scatters (K3, one LDS-bound workgroup per CU) group
+ * g+1 histograms (K1's launch gaps and tail fill with the other group's work).  Output, index tables and
+ * d_index_be exactly as ONE sux_partition_maps call over all num_records would write them.  The
+ * node owns the two group workspaces (pool memory, kept for the next call).  Ordered after the
+ * work already on `stream`; the work it enqueues is joined back into `stream` (no host sync). */
+int sux_partition_maps_pipelined(sux_node* node, const sux_partitioner* part,
+                                 const void* d_records, uint32_t record_size,
+                                 uint64_t records_per_map, uint64_t num_records,
+                                 uint64_t group_records, void* d_out, int64_t* d_index,
+                                 uint8_t* d_index_be, void* stream);
 
 /* Same as sux_partition_maps, but the output is laid out for the exchange: peer-major
  * [peer h][map m][partitions owned by h (floor(hR/W) .. floor((h+1)R/W))], so that every peer's

@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <atomic>
 #include <climits>
+#include <initializer_list>
 #include <condition_variable>
 #include <cstring>
 #include <map>
@@ -344,6 +345,20 @@ struct sux_node {
   std::map<void*, void*> ipc_bases;  // opened peer pointer -> mapped allocation base
   sux_allgather_fn boot = nullptr;   // host all-gather of the embedding runtime
   void* boot_ctx = nullptr;
+  sux_tuning tuning{};               // all zero = measured defaults (resolve_tuning)
+  // sux_partition_maps_pipelined: two map streams, their group workspaces, fork/join events
+  hipStream_t pipe[2] = {nullptr, nullptr};
+  PoolBuf pipe_ws[2];
+  hipEvent_t pipe_ev[3] = {nullptr, nullptr, nullptr};
+  uint32_t pipe_next = 0;            // round robin of sux_write_map_outputs batches
+  std::mutex pipe_mu;                // guards the above and every fork/join on them
+
+  void make_pipe() {  // pipe_mu held
+    for (hipStream_t& p : pipe)
+      if (!p) hip_check(hipStreamCreateWithFlags(&p, hipStreamNonBlocking), "map stream");
+    for (hipEvent_t& e : pipe_ev)
+      if (!e) hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "map event");
+  }
 
   void bind() { hip_check(hipSetDevice(conf.device), "hipSetDevice"); }
 
@@ -486,6 +501,29 @@ struct Group {
   sux::Workspace ws{};
 };
 
+// The node's tuning table with every default filled in.  `pipelined`: the call keeps two launch
+// groups in flight (sux_partition_maps_pipelined, sux_write_map_outputs); the co-resident K1/K3
+// shapes are then possible, but measured slower (profiles/r02_sw_b: 1331 vs 1437 GB/s on
+// TeraSort 100 GB: a K1 beside K3 takes K3's HBM share), so they are opt-in.
+sux::Tuning resolve_tuning(const sux_tuning& t, bool pipelined) {
+  sux::Tuning r;
+  if (t.hist_kernel) r.hist_kernel = t.hist_kernel;
+  if (t.scatter_kernel) r.scatter_kernel = t.scatter_kernel;
+  r.coresident = t.coresident > 0 && pipelined;
+  r.scatter_chunk = t.scatter_chunk ? t.scatter_chunk : r.coresident ? 768 : 1024;
+  if (t.scatter_depth) r.scatter_depth = t.scatter_depth;
+  if (t.hist_stage) r.hist_stage = t.hist_stage;
+  r.hist_wgs_per_cu = t.hist_wgs_per_cu;
+  if (t.s6_chunk) r.s6_chunk = t.s6_chunk;
+  r.tiles_per_item = t.tiles_per_item;
+  if (t.small_groups) r.small_groups = t.small_groups;
+  r.tile_records = t.tile_records;
+  r.onepass = t.onepass == 1;
+  if (t.varlen_kernel) r.varlen_kernel = t.varlen_kernel;
+  r.varlen_tile = t.varlen_tile;
+  return r;
+}
+
 Group make_group(const sux_partitioner* part, const void* recs, uint32_t rs, uint64_t rpm,
                  uint64_t n) {
   check_record_size(rs);
@@ -497,7 +535,7 @@ Group make_group(const sux_partitioner* part, const void* recs, uint32_t rs, uin
   require(((uintptr_t)recs & 3) == 0, SUX_EINVAL, "records must be 4-byte aligned");
   Group G;
   uint32_t R = (uint32_t)part->desc.num_partitions;
-  uint32_t tile = sux::choose_tile_recs(R, rs, rpm);
+  uint32_t tile = sux::choose_tile_recs(R, rs, rpm, resolve_tuning(part->node->tuning, false));
   G.g.recs = static_cast<const uint8_t*>(recs);
   G.g.records_per_map = rpm;
   G.g.num_records = n;
@@ -511,7 +549,8 @@ Group make_group(const sux_partitioner* part, const void* recs, uint32_t rs, uin
 
 void run_group(sux_node* node, const sux_partitioner* part, const Group& G, int32_t world,
                void* d_out, int64_t* d_index, uint8_t* d_index_be, uint16_t* d_pids,
-               uint64_t* d_peer_bytes, void* d_ws, uint64_t ws_bytes, hipStream_t s) {
+               uint64_t* d_peer_bytes, void* d_ws, uint64_t ws_bytes, hipStream_t s,
+               bool pipelined = false) {
   require(d_ws || G.ws.total == 0, SUX_EINVAL, "workspace is NULL");
   require(ws_bytes >= G.ws.total, SUX_EINVAL,
           "workspace too small: need " + std::to_string(G.ws.total) + " bytes");
@@ -523,7 +562,8 @@ void run_group(sux_node* node, const sux_partitioner* part, const Group& G, int3
   sux::LayoutDesc lay{world, G.g.rec_size};
   hip_check(sux::launch_partition_group(part->pd, G.g, lay, static_cast<uint8_t*>(d_out), d_index,
                                         d_index_be, d_pids, static_cast<uint8_t*>(d_ws), G.ws,
-                                        d_peer_bytes, &node->timer, s),
+                                        d_peer_bytes, resolve_tuning(node->tuning, pipelined),
+                                        &node->timer, s),
             "partition launch");
 }
 }  // namespace
@@ -670,6 +710,58 @@ int sux_pool_stats(sux_node* node, uint64_t* bytes, uint64_t* requests, uint64_t
   });
 }
 
+int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
+  return guard([&] {
+    require(t, SUX_EINVAL, "NULL tuning");
+    auto in = [](int32_t v, std::initializer_list<int32_t> ok) {
+      if (v == 0) return true;
+      for (int32_t o : ok)
+        if (v == o) return true;
+      return false;
+    };
+    require(in(t->hist_kernel, {1, 2, 3, 4}), SUX_EINVAL, "hist_kernel must be 1..4");
+    require(in(t->scatter_kernel, {1, 2, 6, 7}), SUX_EINVAL, "scatter_kernel must be 1, 2, 6 or 7");
+    require(t->coresident >= -1 && t->coresident <= 1, SUX_EINVAL, "coresident must be -1, 0 or 1");
+    require(in(t->scatter_chunk, {768, 1024}), SUX_EINVAL, "scatter_chunk must be 768 or 1024");
+    require(in(t->scatter_depth, {1, 2}), SUX_EINVAL, "scatter_depth must be 1 or 2");
+    require(t->scatter_depth != 2 || t->scatter_chunk == 768, SUX_EINVAL,
+            "scatter_depth 2 needs scatter_chunk 768");
+    require(in(t->hist_stage, {64, 128}), SUX_EINVAL, "hist_stage must be 64 or 128");
+    require(t->hist_wgs_per_cu >= 0 && t->hist_wgs_per_cu <= 8, SUX_EINVAL,
+            "hist_wgs_per_cu must be 0..8");
+    require(in(t->s6_chunk, {256, 384, 512, 1024}), SUX_EINVAL, "s6_chunk must be 256..1024");
+    require(t->tiles_per_item >= 0 && t->tiles_per_item <= 4096, SUX_EINVAL,
+            "tiles_per_item must be 0..4096");
+    require(in(t->small_groups, {1, 2, 4}), SUX_EINVAL, "small_groups must be 1, 2 or 4");
+    require(t->tile_records == 0 || (t->tile_records >= 64 && t->tile_records <= (1 << 22) &&
+                                     (t->tile_records & (t->tile_records - 1)) == 0),
+            SUX_EINVAL, "tile_records must be a power of two in [64, 2^22]");
+    require(t->onepass == 0 || t->onepass == 1, SUX_EINVAL, "onepass must be 0 or 1");
+    require(in(t->varlen_kernel, {1, 2}), SUX_EINVAL, "varlen_kernel must be 1 or 2");
+    require(t->varlen_tile == 0 || (t->varlen_tile >= 64 && t->varlen_tile <= 65536 &&
+                                    t->varlen_tile % 64 == 0),
+            SUX_EINVAL, "varlen_tile must be a multiple of 64 in [64, 65536]");
+    require(t->sort_max_digit_bits == 0 ||
+                (t->sort_max_digit_bits >= 8 && t->sort_max_digit_bits <= 16),
+            SUX_EINVAL, "sort_max_digit_bits must be 8..16");
+    require(t->sort_gather == 0 || t->sort_gather == 1, SUX_EINVAL, "sort_gather must be 0 or 1");
+    require(t->sort_all_passes == 0 || t->sort_all_passes == 1, SUX_EINVAL,
+            "sort_all_passes must be 0 or 1");
+    for (int32_t r : t->reserved) require(r == 0, SUX_EINVAL, "reserved tuning fields must be 0");
+    require(node, SUX_EINVAL, "NULL node");
+    std::lock_guard<std::mutex> lk(node->mu);
+    node->tuning = *t;
+  });
+}
+
+int sux_node_get_tuning(sux_node* node, sux_tuning* t) {
+  return guard([&] {
+    require(node && t, SUX_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(node->mu);
+    *t = node->tuning;
+  });
+}
+
 int sux_node_destroy(sux_node* node) {
   return guard([&] {
     if (!node) return;
@@ -679,6 +771,12 @@ int sux_node_destroy(sux_node* node) {
       for (auto& kv : node->shuffles) drain(node, *kv.second, lk);
     }
     (void)hipDeviceSynchronize();
+    for (int i = 0; i < 2; ++i) {
+      if (node->pipe[i]) (void)hipStreamDestroy(node->pipe[i]);
+      node->pool->put(node->pipe_ws[i]);
+    }
+    for (hipEvent_t e : node->pipe_ev)
+      if (e) (void)hipEventDestroy(e);
     for (auto& kv : node->shuffles) release_shuffle(node, *kv.second);
     node->shuffles.clear();
     for (auto& kv : node->ipc_bases) (void)hipIpcCloseMemHandle(kv.second);
@@ -809,6 +907,51 @@ int sux_partition_maps(sux_node* node, const sux_partitioner* part, const void* 
   });
 }
 
+int sux_partition_maps_pipelined(sux_node* node, const sux_partitioner* part,
+                                 const void* d_records, uint32_t rs, uint64_t rpm, uint64_t n,
+                                 uint64_t group_records, void* d_out, int64_t* d_index,
+                                 uint8_t* d_index_be, void* stream) {
+  return guard([&] {
+    require(node && part, SUX_EINVAL, "NULL node/partitioner");
+    require(d_records || n == 0, SUX_EINVAL, "records pointer is NULL");
+    require(rpm > 0, SUX_EINVAL, "records_per_map must be > 0");
+    if (group_records == 0) group_records = std::max<uint64_t>(1, (1ull << 27) / rpm) * rpm;
+    require(group_records % rpm == 0, SUX_EINVAL, "group_records must be whole maps");
+    require(group_records < (1ull << 32), SUX_ERANGE, "a launch group holds < 2^32 records");
+    node->bind();
+    if (n == 0) return;
+    const uint64_t R = (uint64_t)part->desc.num_partitions;
+    const uint64_t first = std::min(n, group_records);
+    // every group's workspace fits in the first (largest) group's
+    const Group G0 = make_group(part, d_records, rs, rpm, first);
+    std::lock_guard<std::mutex> lk(node->pipe_mu);
+    node->make_pipe();
+    for (int i = 0; i < 2; ++i) {
+      if (node->pipe_ws[i].cap < G0.ws.total) {
+        hip_check(hipStreamSynchronize(node->pipe[i]), "map stream drain");
+        node->pool->put(node->pipe_ws[i]);
+        node->pipe_ws[i] = node->pool->get(G0.ws.total);
+      }
+    }
+    hipStream_t s = node->stream(stream);
+    hip_check(hipEventRecord(node->pipe_ev[0], s), "fork");
+    for (hipStream_t p : node->pipe) hip_check(hipStreamWaitEvent(p, node->pipe_ev[0], 0), "fork");
+    const uint8_t* recs = static_cast<const uint8_t*>(d_records);
+    uint8_t* out = static_cast<uint8_t*>(d_out);
+    for (uint64_t r0 = 0, g = 0; r0 < n; r0 += group_records, ++g) {
+      const uint64_t r1 = std::min(n, r0 + group_records), m0 = r0 / rpm;
+      const Group G = make_group(part, recs + r0 * rs, rs, rpm, r1 - r0);
+      run_group(node, part, G, 1, out + r0 * rs, d_index + m0 * (R + 1),
+                d_index_be ? d_index_be + m0 * (R + 1) * 8 : nullptr, nullptr, nullptr,
+                node->pipe_ws[g % 2].ptr, node->pipe_ws[g % 2].cap, node->pipe[g % 2], true);
+    }
+    for (int i = 0; i < 2; ++i) {
+      hip_check(hipEventRecord(node->pipe_ev[1 + i], node->pipe[i]), "join");
+      hip_check(hipStreamWaitEvent(s, node->pipe_ev[1 + i], 0), "join");
+    }
+  });
+}
+
 int sux_partition_maps_peer_major(sux_node* node, const sux_partitioner* part,
                                   const void* d_records, uint32_t rs, uint64_t rpm, uint64_t n,
                                   int32_t world, void* d_send, int64_t* d_index,
@@ -861,7 +1004,8 @@ VGroup make_vgroup(const sux_partitioner* part, const void* data, const uint64_t
   require(((uintptr_t)data & 3) == 0 && ((uintptr_t)offs & 7) == 0, SUX_EINVAL,
           "data must be 4-byte and offsets 8-byte aligned");
   VGroup G;
-  const uint32_t tile = sux::choose_varlen_tile((uint32_t)R, n);
+  const uint32_t tile =
+      sux::choose_varlen_tile((uint32_t)R, n, resolve_tuning(part->node->tuning, false));
   G.g.data = static_cast<const uint8_t*>(data);
   G.g.offs = offs;
   G.g.records_per_map = rpm;
@@ -905,7 +1049,8 @@ int sux_partition_varlen(sux_node* node, const sux_partitioner* part, const void
     if (n == 0) return;
     hip_check(sux::launch_varlen_group(part->pd, G.g, static_cast<uint8_t*>(d_out), d_index,
                                        d_index_be, d_pids_in, d_pids,
-                                       static_cast<uint8_t*>(d_ws), G.ws, &node->timer,
+                                       static_cast<uint8_t*>(d_ws), G.ws,
+                                       resolve_tuning(node->tuning, false), &node->timer,
                                        node->stream(stream)),
               "variable-length partition launch");
   });
@@ -1490,26 +1635,39 @@ int sux_write_map_outputs(sux_node* node, int32_t shuffle_id, int32_t first,
       }
       node->cv.notify_all();
     };
+    // Map tasks run several at a time in Spark (one per executor core): consecutive batches go
+    // round robin to the node's two map streams, so that one batch's K1 runs beside the other's
+    // K3 (the co-resident shapes of sux_partition_maps_pipelined).  Forked from the caller's
+    // stream (its input is ready there) and joined back into it (the caller may reuse the
+    // input buffer after its own stream's later work, as with a launch on `stream` itself).
+    hipStream_t ms = s;
     try {
       Group G = make_group(part, d_records, rs, rpm, n);
       job->slab = std::make_shared<Slab>(node->pool.get(), node->pool->get(n * rs));
       job->ws = node->pool->get(G.ws.total + 8 * maps * (uint64_t)(R + 1) + 256);
       int64_t* d_idx = reinterpret_cast<int64_t*>(job->ws.ptr + (G.ws.total + 255) / 256 * 256);
       job->hidx = node->hpool.get(8 * maps * (uint64_t)(R + 1));
+      std::lock_guard<std::mutex> plk(node->pipe_mu);
+      node->make_pipe();
+      ms = node->pipe[node->pipe_next++ & 1];
+      hip_check(hipEventRecord(node->pipe_ev[0], s), "fork");
+      hip_check(hipStreamWaitEvent(ms, node->pipe_ev[0], 0), "fork");
       run_group(node, part, G, 1, job->slab->buf.ptr, d_idx, nullptr, nullptr, nullptr,
-                job->ws.ptr, G.ws.total, s);
+                job->ws.ptr, G.ws.total, ms, true);
       hip_check(hipMemcpyAsync(job->hidx.first, d_idx, 8 * maps * (uint64_t)(R + 1),
-                               hipMemcpyDeviceToHost, s),
+                               hipMemcpyDeviceToHost, ms),
                 "D2H index");
       job->done = std::make_shared<Event>();
-      hip_check(hipEventRecord(job->done->e, s), "hipEventRecord");
+      hip_check(hipEventRecord(job->done->e, ms), "hipEventRecord");
+      hip_check(hipStreamWaitEvent(s, job->done->e, 0), "join");
     } catch (...) {
       unclaim();
       if (!job->done) {  // nothing reached the stream that still needs the buffers
+        (void)hipStreamSynchronize(ms);
         node->pool->put(job->ws);
         node->hpool.put(job->hidx);
       } else {
-        (void)hipStreamSynchronize(s);
+        (void)hipStreamSynchronize(ms);
         node->pool->put(job->ws);
         node->hpool.put(job->hidx);
       }
@@ -2122,12 +2280,11 @@ void sort_plan(uint64_t n, uint32_t rs, SortPlan& P, int digit_bits) {
   P.rs = rs;
   const uint32_t R = 1u << digit_bits;
   const uint64_t rpm = n ? n : 1;
-  uint32_t tile = sux::choose_tile_recs(R, 16, rpm);
+  uint32_t tile = sux::choose_tile_recs(R, 16, rpm, sux::Tuning{});
   // long sorts: longer tiles while >= 256 of them remain (fewer counters for k_tile_scan_tm to
   // scan; profiles/r01_v13/sort_tile_sweep.txt: 32 Mi pairs 6.04 -> 5.73 ms at 65536, while 5 M
   // pairs lose 55 % there, hence the tile-count floor)
-  if (!std::getenv("SUX_TILE_RECS"))
-    while (tile < 65536 && rpm / (2ull * tile) >= 256) tile *= 2;
+  while (tile < 65536 && rpm / (2ull * tile) >= 256) tile *= 2;
   P.g.records_per_map = rpm;
   P.g.num_records = n;
   P.g.num_maps = 1;
@@ -2206,11 +2363,11 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
           "sort: the key does not fit the record");
   // fewest passes at <= max_digit bits each, then the narrowest digit giving that pass count
   // (80-bit TeraSort keys: 6 passes of 14 bits instead of 7 of 12)
-  static const int max_digit = [] {
-    const char* e = std::getenv("SUX_SORT_MAX_DIGIT_BITS");  // sweep override
-    const int v = e ? std::atoi(e) : kSortDefaultMaxDigitBits;
-    return std::min(std::max(v, kSortMinDigitBits), kSortMaxDigitBits);
-  }();
+  const int max_digit = std::min(
+      std::max(node->tuning.sort_max_digit_bits ? node->tuning.sort_max_digit_bits
+                                                : kSortDefaultMaxDigitBits,
+               kSortMinDigitBits),
+      kSortMaxDigitBits);
   const int passes = (bits + max_digit - 1) / max_digit;
   const int digit = std::max(kSortMinDigitBits, (bits + passes - 1) / passes);
   SortPlan P;
@@ -2230,8 +2387,7 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
   uint8_t* pb = ws + P.pairs_bytes;
   int64_t* index = reinterpret_cast<int64_t*>(ws + P.index_off);
   // records of <= 16 bytes (with the segment id) travel inside the pairs: no gather at the end
-  static const bool no_inline = std::getenv("SUX_SORT_GATHER") != nullptr;  // A/B runs
-  const bool inline_rec = !no_inline && record_size + (uint32_t)sbytes <= 16;
+  const bool inline_rec = node->tuning.sort_gather != 1 && record_size + (uint32_t)sbytes <= 16;
   hip_check(sux::launch_sort_pairs(static_cast<const uint8_t*>(d_in), n, record_size, key_kind,
                                    key_offset, key_len, d_seg, nseg, sbytes, pa, ws + P.span_off,
                                    inline_rec, s),
@@ -2239,7 +2395,7 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
   // which digits vary: one 24-byte read-back (the only host wait in the sort).  A stream being
   // captured into a HIP graph cannot be waited on: then every digit pass runs (the skipped
   // passes are identity permutations, so the bytes are the same) and the call stays async.
-  static const bool all_passes = std::getenv("SUX_SORT_ALL_PASSES") != nullptr;  // A/B runs
+  const bool all_passes = node->tuning.sort_all_passes == 1;
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   hip_check(hipStreamIsCapturing(s, &cap), "hipStreamIsCapturing");
   const bool run_all = all_passes || cap != hipStreamCaptureStatusNone;
@@ -2262,7 +2418,8 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
     pd.seed = sh;
     P.g.recs = pa;
     hip_check(sux::launch_partition_group(pd, P.g, lay, pb, index, nullptr, nullptr,
-                                          ws + P.part_off, P.ws, nullptr, &node->timer, s),
+                                          ws + P.part_off, P.ws, nullptr,
+                                          resolve_tuning(node->tuning, false), &node->timer, s),
               "sort digit pass");
     std::swap(pa, pb);
   }

@@ -31,6 +31,25 @@ struct PartDev {
   int32_t pad;
 };
 
+// Kernel tuning of one launch: the node's sux_tuning with every default filled in (sux_api.cpp,
+// resolve_tuning).  Replaces round 1's process-wide environment overrides.
+struct Tuning {
+  int hist_kernel = 4;      // newest K1 variant allowed
+  int scatter_kernel = 7;   // newest K3 variant allowed
+  bool coresident = false;  // K1/K3 shapes that share a CU (two launch groups in flight)
+  int scatter_chunk = 1024; // k_scatter7 records per chunk: 1024 | 768
+  int scatter_depth = 1;    // k_scatter7 chunks loaded ahead (768-record chunks: 1 | 2)
+  int hist_stage = 64;      // k_hist4 records per LDS stage: 64 | 128
+  int hist_wgs_per_cu = 0;  // k_hist4 workgroups per CU (0: as many as LDS allows)
+  int s6_chunk = 1024;      // k_scatter6 largest chunk
+  int tiles_per_item = 0;   // k_scatter6/7 tiles per work item (0: 8 chunks' worth)
+  int small_groups = 4;     // k_scatter16b record groups per turn: 1 | 2 | 4
+  int tile_records = 0;     // K1 tile override (0: choose_tile_recs's rule)
+  bool onepass = false;     // the one-pass kernel when a map batch fits on chip
+  int varlen_kernel = 2;    // variable-length rows: 1 | 2
+  int varlen_tile = 0;      // variable-length K1 tile override
+};
+
 // Per-launch geometry of a group of consecutive map batches.
 struct MapGroup {
   const uint8_t* recs;       // first record of map 0 of the group
@@ -71,7 +90,8 @@ struct Workspace {
 };
 Workspace workspace_layout(uint32_t R, uint32_t rec_size, uint64_t records_per_map,
                            uint64_t num_records, uint32_t tile_recs, bool need_pids);
-uint32_t choose_tile_recs(uint32_t R, uint32_t rec_size, uint64_t records_per_map);
+uint32_t choose_tile_recs(uint32_t R, uint32_t rec_size, uint64_t records_per_map,
+                          const Tuning& tn);
 
 // Destination layout of a group (K2b): map-major (Spark data files side by side), or
 // peer-major for the exchange ([peer][map][partitions owned by peer]).
@@ -101,14 +121,15 @@ void timer_note(Timer* t, int slot, const char* kernel);
 hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const LayoutDesc& lay,
                                   uint8_t* d_out, int64_t* d_index, uint8_t* d_index_be,
                                   uint16_t* d_pids, uint8_t* d_ws, const Workspace& ws,
-                                  uint64_t* d_peer_bytes, Timer* timer, hipStream_t s);
+                                  uint64_t* d_peer_bytes, const Tuning& tn, Timer* timer,
+                                  hipStream_t s);
 hipError_t launch_varlen_group(const PartDev& pd, const VarGroup& g, uint8_t* d_out,
                                int64_t* d_index, uint8_t* d_index_be, const uint16_t* d_pids_in,
                                uint16_t* d_pids, uint8_t* d_ws, const VarWorkspace& ws,
-                               Timer* timer, hipStream_t s);
+                               const Tuning& tn, Timer* timer, hipStream_t s);
 VarWorkspace varlen_workspace_layout(uint32_t R, uint64_t records_per_map, uint64_t num_records,
                                      uint32_t tile_recs);
-uint32_t choose_varlen_tile(uint32_t R, uint64_t rows);
+uint32_t choose_varlen_tile(uint32_t R, uint64_t rows, const Tuning& tn);
 // K2b of the variable-length path (sux_partition.hip, k_map_scan): per-(map, partition) byte
 // totals -> index tables in bytes + byte bases of every (map, partition) run
 hipError_t launch_varlen_map_scan(const VarGroup& g, int R, const uint64_t* totals, uint64_t* base,

@@ -574,11 +574,10 @@ uint64_t onepass_sync_bytes(uint32_t R) {
 bool onepass_eligible(const PartDev& pd, const MapGroup& g, int world, const void* d_out,
                       const uint64_t* d_peer_bytes, hipStream_t s, uint32_t* grid_out,
                       uint32_t* cs_out) {
-  // opt-in (SUX_ONEPASS=1, read per launch: the parity tests run both paths).  Measured on
-  // MI355X at R = 200 it is slower than the three-kernel path: a slice's run
-  // of one partition is only ~C/R records, so its writes are short misaligned runs.
-  const char* env = getenv("SUX_ONEPASS");
-  if (!(env && env[0] == '1') || world != 1 || d_peer_bytes || g.rec_size != kOpS) return false;
+  // opt-in (sux_tuning.onepass; the launcher checks it).  Measured on MI355X at R = 200 it is
+  // slower than the three-kernel path: a slice's run of one partition is only
+  // ~C/R records, so its writes are short misaligned runs.
+  if (world != 1 || d_peer_bytes || g.rec_size != kOpS) return false;
   if (pd.kind == 4 || pd.key_offset % 4 || pd.key_len < 1 || pd.key_len > 16 ||
       pd.key_offset + pd.key_len > (int)kOpS)
     return false;

@@ -31,7 +31,6 @@ namespace sux {
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 
 constexpr int kWave = 64;
-constexpr int kScatter16Batch = 4;  // k_scatter16b groups per turn (SUX_S16_GB overrides)
 
 // P1: partition functions — sux_p1.h
 #include "sux_p1.h"
@@ -625,6 +624,8 @@ __global__ __launch_bounds__(256) void k_hist3(PartDev pd, MapGroup g, uint16_t*
 // ------------------------------------------------------------------------------------------
 template <uint32_t S, uint32_t CH>
 struct Hs4 {
+  // a step reads CH records with CH / 64 record slots per lane: CH < 64 would read none
+  static_assert(CH % kWave == 0 && CH >= kWave, "k_hist4 stages whole waves of records");
   static constexpr uint32_t kUnits = (CH * S + 12 + 15) / 16;
   static constexpr uint32_t kPer = (kUnits + kWave - 1) / kWave;
   static constexpr uint32_t kStage = kPer * kWave * 16;  // bytes per wave
@@ -1594,16 +1595,15 @@ __global__ __launch_bounds__(256) void k_pids(PartDev pd, const uint8_t* recs, u
 // ------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------
-uint32_t choose_tile_recs(uint32_t R, uint32_t rec_size, uint64_t records_per_map) {
+uint32_t choose_tile_recs(uint32_t R, uint32_t rec_size, uint64_t records_per_map,
+                          const Tuning& tn) {
   (void)rec_size;
   // 4096 records (400 KB at S=100) per tile: fewer counters to scan, and the partial 128-B
   // lines at tile seams are rarer (measured: 1024 -> 4096 takes ~1 ms off a 100 GB step)
   uint32_t t = 4096;
   while (t < 4u * R && t < (1u << 22)) t <<= 1;
-  if (const char* e = getenv("SUX_TILE_RECS")) {  // tuning override (power of two, >= 64)
-    uint32_t v = (uint32_t)strtoul(e, nullptr, 10);
-    if (v >= 64 && (v & (v - 1)) == 0) t = v;
-  }
+  const uint32_t v = (uint32_t)tn.tile_records;  // tuning override (power of two, >= 64)
+  if (v >= 64 && (v & (v - 1)) == 0) t = v;
   // no point in tiles longer than a map
   uint64_t cap = ((records_per_map + kWave - 1) / kWave) * kWave;
   if (cap < t) t = (uint32_t)(cap < kWave ? kWave : cap);
@@ -1671,23 +1671,16 @@ static hipError_t launch_scatter(uint32_t S, dim3 grid, size_t lds, hipStream_t 
   return hipGetLastError();
 }
 
-// Kernel variants (A/B only; defaults are the fastest measured).  SUX_HIST = v1|v2|v3,
-// SUX_SCATTER = v1|v2.
-static int env_variant(const char* name, int dflt) {
-  const char* e = getenv(name);
-  if (e && e[0] == 'v' && e[1] >= '1' && e[1] <= '9') return e[1] - '0';
-  return dflt;
-}
-
 hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const LayoutDesc& lay,
                                   uint8_t* d_out, int64_t* d_index, uint8_t* d_index_be,
                                   uint16_t* d_pids, uint8_t* d_ws, const Workspace& ws,
-                                  uint64_t* d_peer_bytes, Timer* timer, hipStream_t s) {
+                                  uint64_t* d_peer_bytes, const Tuning& tn, Timer* timer,
+                                  hipStream_t s) {
   const int R = pd.R;
   const uint32_t S = g.rec_size;
   // one pass (sux_onepass.hip) whenever a map batch fits on chip: every record read once
   uint32_t op_grid = 0, op_cs = 0;
-  if (ws.op_bytes && onepass_eligible(pd, g, lay.world, d_out, d_peer_bytes, s, &op_grid, &op_cs)) {
+  if (tn.onepass && ws.op_bytes && onepass_eligible(pd, g, lay.world, d_out, d_peer_bytes, s, &op_grid, &op_cs)) {
     timer_note(timer, kScatter, "k_onepass");
     timer_begin(timer, kScatter, s);
     const hipError_t eo = launch_onepass(pd, g, d_out, d_index, d_index_be, d_pids,
@@ -1707,11 +1700,11 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   const size_t lds1 = (size_t)wpg * R * 4;
 
   // ---- K1: pids + tile histograms
-  static const int hv = env_variant("SUX_HIST", 4);
+  const int hv = tn.hist_kernel;
   const bool shaped = (S == 100 || S == 16) && R <= 4096;  // v2 instantiations
   const bool words = pd.kind != 4 && pd.key_offset % 4 == 0 && pd.key_len <= 16;
   // small records with many partitions: k_hist16 + tile-major counts + k_scatter16, together
-  static const int sv = env_variant("SUX_SCATTER", 7);
+  const int sv = tn.scatter_kernel;
   const bool s16 = hv >= 4 && sv >= 7 && words && S == 16 && R > 1024 &&
                    (reinterpret_cast<uintptr_t>(g.recs) & 15) == 0 &&
                    (reinterpret_cast<uintptr_t>(d_out) & 15) == 0;
@@ -1738,17 +1731,17 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
     else SUX_H16(4);
 #undef SUX_H16
   } else if (hist == 4) {
-    static const int hch = [] {
-      const char* e = getenv("SUX_H4CH");
-      return e ? atoi(e) : 64;
-    }();
+    const int hch = tn.hist_stage;
     const bool tab = pd.kind == 1 && R > 1 &&
                      Hs4<100, 128>::lds_bytes(R, true) <= 160 * 1024;
     const int kw = (pd.key_len + 3) / 4;
+    (void)tab;
 #define SUX_H4(CHV, KW)                                                                            \
   do {                                                                                             \
     const size_t lds = Hs4<100, CHV>::lds_bytes(R, tab);                                           \
-    const dim3 gridp(std::min<uint32_t>(total_tiles, 256u * std::max<uint32_t>(1, (160u * 1024) / (uint32_t)lds))); \
+    uint32_t per_cu = std::max<uint32_t>(1, (160u * 1024) / (uint32_t)lds);                        \
+    if (tn.hist_wgs_per_cu > 0) per_cu = std::min<uint32_t>(per_cu, (uint32_t)tn.hist_wgs_per_cu); \
+    const dim3 gridp(std::min<uint32_t>(total_tiles, 256u * per_cu));                              \
     if (tab) {                                                                                     \
       allow_lds(reinterpret_cast<const void*>(&k_hist4<100, CHV, KW, true>), lds);                \
       hipLaunchKernelGGL((k_hist4<100, CHV, KW, true>), gridp, dim3(256), lds, s, pd, g, pids,     \
@@ -1832,16 +1825,11 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
 
   // ---- K3: stable scatter.  S = 100 (TeraSort rows): v7 for R <= 512, v6 for the R whose
   // LDS image still fits; any other shape: the v2 (R <= 4096, S in {16, 100}) or v1 kernels.
-  // tuning overrides: SUX_S6=C (v6 records per chunk: 1024 | 512 | 384 | 256), SUX_S6_TPW=tiles
-  // per work item, SUX_S7=2|3 (v7 at 768-record chunks with 2 | 1 chunks in flight)
-  static const int s6c = [] {
-    const char* e = getenv("SUX_S6");
-    return e ? atoi(e) : 1024;
-  }();
-  static const int s6tpw = [] {
-    const char* e = getenv("SUX_S6_TPW");
-    return e ? atoi(e) : 0;
-  }();
+  // tuning (Tuning): s6_chunk caps the v6 chunk, tiles_per_item sets the v6/v7 work item,
+  // scatter_chunk/scatter_depth pick the v7 shape (768-record chunks leave room for a K1
+  // workgroup on the CU: the co-resident pipeline)
+  const int s6c = tn.s6_chunk;
+  const int s6tpw = tn.tiles_per_item;
   size_t lds6 = 0;
   int c6 = 0;
   if (sv >= 6 && S == 100 && (reinterpret_cast<uintptr_t>(d_out) & 15) == 0 &&
@@ -1867,10 +1855,7 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
     const size_t lds = (size_t)R * 4;
     const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(2, (160u * 1024) / (uint32_t)lds));
     const dim3 grid(std::min<uint32_t>(total_tiles, 256u * per_cu));
-    static const int gb = [] {  // groups per turn (1 = k_scatter16); tuning override
-      const char* e = getenv("SUX_S16_GB");
-      return e ? atoi(e) : kScatter16Batch;
-    }();
+    const int gb = tn.small_groups;  // groups per turn (1 = k_scatter16)
     if (gb == 2 || gb == 4) {
       const void* kf = gb == 2 ? reinterpret_cast<const void*>(&k_scatter16b<16, 2>)
                                : reinterpret_cast<const void*>(&k_scatter16b<16, 4>);
@@ -1902,12 +1887,8 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
     hipLaunchKernelGGL((k_scatter7<100, CC, NWV, DV>), grid, dim3(NWV * kWave), lds7, s, g, R,   \
                        bits, pids, counts, base, d_out, tpw, wpm);                               \
   } while (0)
-    static const int s7 = [] {
-      const char* e = getenv("SUX_S7");
-      return e ? atoi(e) : 1;
-    }();
-    if (s7 == 2) SUX_S7L(768, 12, 2);
-    else if (s7 == 3) SUX_S7L(768, 12, 1);
+    if (tn.scatter_chunk == 768 && tn.scatter_depth == 2) SUX_S7L(768, 12, 2);
+    else if (tn.scatter_chunk == 768) SUX_S7L(768, 12, 1);
     else SUX_S7L(1024, 16, 1);
 #undef SUX_S7L
     e = hipGetLastError();

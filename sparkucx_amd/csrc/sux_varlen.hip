@@ -355,12 +355,8 @@ VarWorkspace varlen_workspace_layout(uint32_t R, uint64_t records_per_map, uint6
   return w;
 }
 
-uint32_t choose_varlen_tile(uint32_t R, uint64_t rows) {
-  static const uint32_t env = [] {
-    const char* e = getenv("SUX_VTILE");
-    return e ? (uint32_t)atoi(e) : 0u;
-  }();
-  if (env >= 64 && env % 64 == 0) return env;
+uint32_t choose_varlen_tile(uint32_t R, uint64_t rows, const Tuning& tn) {
+  if (tn.varlen_tile >= 64 && tn.varlen_tile % 64 == 0) return (uint32_t)tn.varlen_tile;
   uint32_t t = 512;
   while (t < 2 * R && t < 65536) t <<= 1;  // counts stay <= 4 B per record
   // longer tiles (longer per-partition runs per wave) while >= 16 Ki tiles keep every CU busy
@@ -371,7 +367,7 @@ uint32_t choose_varlen_tile(uint32_t R, uint64_t rows) {
 hipError_t launch_varlen_group(const PartDev& pd, const VarGroup& g, uint8_t* d_out,
                                int64_t* d_index, uint8_t* d_index_be, const uint16_t* d_pids_in,
                                uint16_t* d_pids, uint8_t* d_ws, const VarWorkspace& ws,
-                               Timer* timer, hipStream_t s) {
+                               const Tuning& tn, Timer* timer, hipStream_t s) {
   const int R = pd.R;
   uint64_t* counts = reinterpret_cast<uint64_t*>(d_ws + ws.counts_off);
   uint64_t* totals = reinterpret_cast<uint64_t*>(d_ws + ws.totals_off);
@@ -383,10 +379,7 @@ hipError_t launch_varlen_group(const PartDev& pd, const VarGroup& g, uint8_t* d_
   const bool four = (size_t)(R + 2 * kVWave) * 8 * 4 <= 64 * 1024;  // 4 waves per workgroup while LDS allows
   const uint32_t wpg = four ? 4 : 1;
   const dim3 grid((total_tiles + wpg - 1) / wpg);
-  static const int ver = [] {
-    const char* e = getenv("SUX_VARLEN");
-    return e ? atoi(e) : 2;
-  }();
+  const int ver = tn.varlen_kernel;
   // v2 needs: a fixed-width key at a 4-aligned offset (or caller ids) and >= 16 bytes of rows
   int kw = 0;
   if (pd.key_offset % 4 == 0) {

@@ -39,6 +39,16 @@ class Conf(C.Structure):
                 ("prealloc_count", C.c_uint64 * 16)]
 
 
+TUNING_FIELDS = ("hist_kernel", "scatter_kernel", "coresident", "scatter_chunk", "scatter_depth",
+                 "hist_stage", "s6_chunk", "tiles_per_item", "small_groups", "tile_records",
+                 "onepass", "varlen_kernel", "varlen_tile", "sort_max_digit_bits", "sort_gather",
+                 "sort_all_passes", "hist_wgs_per_cu")
+
+
+class Tuning(C.Structure):
+    _fields_ = [(f, C.c_int32) for f in TUNING_FIELDS] + [("reserved", C.c_int32 * 15)]
+
+
 # int (*sux_allgather_fn)(void* ctx, const void* send, uint64_t bytes, void* recv)
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p)
 
@@ -65,6 +75,9 @@ _SIGS = {
     "sux_conf_init": (None, [C.POINTER(Conf)]),
     "sux_conf_set_prealloc": (C.c_int, [C.POINTER(Conf), C.c_char_p]),
     "sux_node_set_bootstrap": (C.c_int, [P, ALLGATHER_FN, P]),
+    "sux_node_set_tuning": (C.c_int, [P, C.POINTER(Tuning)]),
+    "sux_node_get_tuning": (C.c_int, [P, C.POINTER(Tuning)]),
+    "sux_partition_maps_pipelined": (C.c_int, [P, P, P, U32, U64, U64, U64, P, P, P, P]),
     "sux_pool_stats": (C.c_int, [P, C.POINTER(U64), C.POINTER(U64), C.POINTER(U64),
                                  C.POINTER(U64)]),
     "sux_write_map_outputs": (C.c_int, [P, I32, I32, P, P, U64, U64, P]),

@@ -88,6 +88,21 @@ class Node:
         self._boot = N.ALLGATHER_FN(fn)  # kept alive as long as the node
         N.check(self.lib.sux_node_set_bootstrap(self.h, self._boot, None), "sux_node_set_bootstrap")
 
+    def tuning(self) -> dict:
+        t = N.Tuning()
+        N.check(self.lib.sux_node_get_tuning(self.h, C.byref(t)), "sux_node_get_tuning")
+        return {f: getattr(t, f) for f in N.TUNING_FIELDS}
+
+    def set_tuning(self, **fields) -> dict:
+        """Update fields of the node's kernel tuning table (sux_tuning; 0 = default); returns
+        the previous table so a caller can restore it."""
+        old = self.tuning()
+        t = N.Tuning()
+        for f, v in {**old, **fields}.items():
+            setattr(t, f, int(v))
+        N.check(self.lib.sux_node_set_tuning(self.h, C.byref(t)), "sux_node_set_tuning")
+        return old
+
     def pool_stats(self) -> dict:
         v = [C.c_uint64() for _ in range(4)]
         N.check(self.lib.sux_pool_stats(self.h, *[C.byref(x) for x in v]), "sux_pool_stats")
@@ -146,6 +161,30 @@ class Node:
                                             _ptr(index_be), _ptr(pids), _ptr(workspace),
                                             workspace.numel(), _stream(stream)),
                 "sux_partition_maps")
+        return out, index, index_be
+
+    def partition_maps_pipelined(self, part: Partitioner, records: torch.Tensor,
+                                 record_size: int, records_per_map: int,
+                                 num_records: int | None = None, group_records: int = 0,
+                                 out: torch.Tensor | None = None,
+                                 index: torch.Tensor | None = None,
+                                 index_be: torch.Tensor | None = None, want_be: bool = True,
+                                 stream=None):
+        """sux_partition_maps_pipelined: launch groups of whole maps on the node's two map
+        streams (node-owned workspaces), joined back into `stream`."""
+        n = records.numel() // record_size if num_records is None else num_records
+        maps = max(1, -(-n // records_per_map))
+        R = part.R
+        if out is None:
+            out = torch.empty(max(1, n * record_size), dtype=torch.uint8, device=self.dev)
+        if index is None:
+            index = torch.empty(maps * (R + 1), dtype=torch.int64, device=self.dev)
+        if index_be is None and want_be:
+            index_be = torch.empty(maps * (R + 1) * 8, dtype=torch.uint8, device=self.dev)
+        N.check(self.lib.sux_partition_maps_pipelined(
+            self.h, part.h, _ptr(records), record_size, records_per_map, n, group_records,
+            _ptr(out), _ptr(index), _ptr(index_be), _stream(stream)),
+            "sux_partition_maps_pipelined")
         return out, index, index_be
 
     def partition_maps_peer_major(self, part: Partitioner, records: torch.Tensor,

@@ -20,7 +20,7 @@ public final class SuxNative {
     }
   }
 
-  public static final int ABI_VERSION = 2;
+  public static final int ABI_VERSION = 3;
 
   // status codes (SUX_*)
   public static final int OK = 0, EINVAL = -1, ENOMEM = -2, EHIP = -3, ECOMM = -4, ENOENT = -5,

@@ -22,3 +22,16 @@ def gpu_node():
     node = Node(device=0)
     yield node
     node.close()
+
+
+@pytest.fixture
+def tuned(gpu_node):
+    """Set fields of the session node's tuning table for one test; restored afterwards."""
+    saved = gpu_node.tuning()
+
+    def set_(**fields):
+        gpu_node.set_tuning(**fields)
+        return gpu_node
+
+    yield set_
+    gpu_node.set_tuning(**saved)

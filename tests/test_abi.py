@@ -18,8 +18,9 @@ def test_library_loads_and_exports_every_header_symbol():
     missing = [s for s in declared if not hasattr(lib, s)]
     assert not missing, missing
     assert set(declared) == set(N._SIGS), set(declared) ^ set(N._SIGS)
-    assert lib.sux_abi_version() == 2
+    assert lib.sux_abi_version() == 3
     assert C.sizeof(N.Conf) == 432  # sux_conf of ABI v2 (prealloc pairs appended)
+    assert C.sizeof(N.Tuning) == 128  # sux_tuning of ABI v3: 17 knobs + 15 reserved
 
 
 def test_conf_defaults_mirror_ucx_shuffle_conf():
@@ -55,6 +56,43 @@ def test_bootstrap_and_pool_entry_points_validate_arguments():
     assert lib.sux_pool_stats(None, None, None, None, None) == N.SUX_EINVAL
     assert lib.sux_wait_map_outputs(None, 0) == N.SUX_EINVAL
     assert lib.sux_write_map_outputs(None, 0, 0, None, None, 1, 0, None) == N.SUX_EINVAL
+
+
+@pytest.mark.parametrize("field,value", [
+    ("hist_kernel", 5), ("scatter_kernel", 3), ("coresident", 2), ("scatter_chunk", 512),
+    ("scatter_depth", 3), ("hist_stage", 32), ("hist_wgs_per_cu", 9), ("s6_chunk", 100), ("tiles_per_item", -1),
+    ("small_groups", 3), ("tile_records", 96), ("tile_records", 32), ("onepass", 2),
+    ("varlen_kernel", 3), ("varlen_tile", 100), ("sort_max_digit_bits", 17), ("sort_gather", 2),
+    ("sort_all_passes", -1), ("reserved", 1)])
+def test_tuning_table_rejects_values_outside_each_fields_set(field, value):
+    """sux_node_set_tuning validates the whole table before it looks at the node, so every
+    field's range is checkable without a GPU: an out-of-set value is EINVAL naming the field."""
+    lib = N.load()
+    t = N.Tuning()
+    if field == "reserved":
+        t.reserved[3] = value
+    else:
+        setattr(t, field, value)
+    assert lib.sux_node_set_tuning(None, C.byref(t)) == N.SUX_EINVAL
+    buf = C.create_string_buffer(256)
+    lib.sux_last_error(buf, 256)
+    assert field.split("_")[0] in buf.value.decode()
+
+
+@pytest.mark.parametrize("fields", [{}, {"coresident": -1}, {"coresident": 1, "hist_stage": 128},
+                                    {"scatter_chunk": 768, "scatter_depth": 2},
+                                    {"tile_records": 1 << 22, "varlen_tile": 65536},
+                                    {"sort_max_digit_bits": 8, "onepass": 1}])
+def test_tuning_table_accepts_listed_values(fields):
+    lib = N.load()
+    t = N.Tuning()
+    for f, v in fields.items():
+        setattr(t, f, v)
+    assert lib.sux_node_set_tuning(None, C.byref(t)) == N.SUX_EINVAL  # valid table, no node
+    buf = C.create_string_buffer(256)
+    lib.sux_last_error(buf, 256)
+    assert buf.value.decode() == "NULL node"
+    assert lib.sux_node_get_tuning(None, C.byref(t)) == N.SUX_EINVAL
 
 
 def test_null_arguments_fail_with_einval_and_message():

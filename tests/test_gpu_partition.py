@@ -282,10 +282,10 @@ def test_large_batch_properties(gpu_node):
 
 
 @pytest.mark.parametrize("onepass", ["1", "0"])
-def test_kernel_timing_counts_launches(gpu_node, monkeypatch, onepass):
+def test_kernel_timing_counts_launches(gpu_node, tuned, onepass):
     """Three-kernel path: hist + scan + scatter per launch group; one pass: one launch, timed
     in the scatter slot (the bench's roofline kernel)."""
-    monkeypatch.setenv("SUX_ONEPASS", onepass)
+    tuned(onepass=int(onepass))
     recs = O.gen_terasort(12, 0, 50000)
     gp = gpu_part(gpu_node, O.terasort_partitioner(200))
     gpu_node.set_kernel_timing(True)

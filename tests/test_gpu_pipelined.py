@@ -1,0 +1,191 @@
+"""GPU parity: the pipelined map side (sux_partition_maps_pipelined, two launch groups in flight
+on the node's map streams with the co-resident K1/K3 shapes) and every kernel shape the node's
+tuning table (sux_tuning) can select, against the CPU oracle — bit-exact on data bytes, native
+index tables and Spark's big-endian index bytes.  No tuning value may change a byte.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from sparkucx_amd import native as N
+
+pytestmark = pytest.mark.gpu
+
+
+def host(t):
+    return t.cpu().numpy()
+
+
+def gpu_part(node, p):
+    return node.partitioner(p.kind, p.R, key_offset=p.key_offset, key_len=p.key_len, seed=p.seed,
+                            ascending=p.ascending, bounds=p.bounds)
+
+
+def expect(opart, recs, rs, rpm, out, index, index_be):
+    n = recs.size // rs
+    maps = -(-n // rpm)
+    want_data, want_index, want_be = O.write_maps(opart, recs, rs, rpm)
+    assert host(out)[: n * rs].tobytes() == bytes(want_data), "data bytes differ"
+    assert host(index)[: maps * (opart.R + 1)].tolist() == want_index.tolist()
+    if index_be is not None:
+        assert host(index_be)[: maps * (opart.R + 1) * 8].tobytes() == want_be
+
+
+@pytest.mark.parametrize("R,n,rpm,gmaps", [
+    (200, 7 * 20000 + 1234, 20000, 2),     # 4 groups, ragged last map and group
+    (200, 9 * 8192, 8192, 1),              # one map per group: 9 groups over 2 streams
+    (64, 50000, 50000, 3),                 # one group only (the second stream idles)
+    (512, 6 * 30000, 30000, 2),            # v7's largest R
+    (1000, 5 * 12000 + 17, 12000, 2),      # v6 territory
+    (7, 3 * 4096, 4096, 1),
+])
+def test_pipelined_matches_oracle(gpu_node, R, n, rpm, gmaps):
+    recs = O.gen_terasort(31, 0, n)
+    opart = O.terasort_partitioner(R)
+    gp = gpu_part(gpu_node, opart)
+    d = torch.from_numpy(recs).cuda()
+    out, index, index_be = gpu_node.partition_maps_pipelined(gp, d, 100, rpm,
+                                                             group_records=gmaps * rpm)
+    torch.cuda.synchronize()
+    expect(opart, recs, 100, rpm, out, index, index_be)
+    gp.close()
+
+
+@pytest.mark.parametrize("kind,key_len,off", [(O.MURMUR3_LONG, 8, 0), (O.HASH_INT, 4, 4),
+                                              (O.MURMUR3_BYTES, 12, 8)])
+@pytest.mark.parametrize("co", [1, -1])
+def test_pipelined_coresident_shapes(gpu_node, tuned, co):
+    tuned(coresident=co, hist_wgs_per_cu=1 if co == 1 else 0)
+    n, rpm = 5 * 30000 + 77, 30000
+    recs = O.gen_terasort(38, 0, n)
+    opart = O.terasort_partitioner(200)
+    gp = gpu_part(gpu_node, opart)
+    out, index, index_be = gpu_node.partition_maps_pipelined(gp, torch.from_numpy(recs).cuda(),
+                                                             100, rpm, group_records=2 * rpm)
+    torch.cuda.synchronize()
+    expect(opart, recs, 100, rpm, out, index, index_be)
+    gp.close()
+
+
+def test_pipelined_hash_kinds_and_skew(gpu_node, kind, key_len, off):
+    recs = O.gen_zipf(32, 0, 60000, 1.1, 1 << 12)
+    opart = O.Partitioner(kind, 200, off, key_len, seed=42)
+    gp = gpu_part(gpu_node, opart)
+    out, index, index_be = gpu_node.partition_maps_pipelined(gp, torch.from_numpy(recs).cuda(),
+                                                             100, 10000, group_records=20000)
+    torch.cuda.synchronize()
+    expect(opart, recs, 100, 10000, out, index, index_be)
+    gp.close()
+
+
+def test_pipelined_small_records_and_default_group(gpu_node):
+    """16-byte records with many partitions (the k_hist16/k_scatter16b path), default group."""
+    recs = O.gen_small(33, 0, 300000)
+    opart = O.Partitioner(O.MURMUR3_LONG, 5000, 0, 8, seed=42)
+    gp = gpu_part(gpu_node, opart)
+    out, index, index_be = gpu_node.partition_maps_pipelined(gp, torch.from_numpy(recs).cuda(),
+                                                             16, 100000)
+    torch.cuda.synchronize()
+    expect(opart, recs, 16, 100000, out, index, index_be)
+    gp.close()
+
+
+def test_pipelined_on_a_side_stream_and_repeated(gpu_node):
+    """Ordered after the caller's stream (input generated there) and joined back into it; the
+    node's group workspaces are reused by the next call (and grow when a group is larger)."""
+    opart = O.terasort_partitioner(200)
+    gp = gpu_part(gpu_node, opart)
+    s = torch.cuda.Stream()
+    for n, rpm, g in [(40000, 10000, 1), (160000, 20000, 3), (40000, 10000, 2)]:
+        with torch.cuda.stream(s):
+            d = gpu_node.generate(N.GEN_TERASORT, 34, 0, n, 100, stream=s)
+            out, index, index_be = gpu_node.partition_maps_pipelined(
+                gp, d, 100, rpm, group_records=g * rpm, stream=s)
+            ix = index.clone()  # on s: must see the joined result
+        s.synchronize()
+        expect(opart, O.gen_terasort(34, 0, n), 100, rpm, out, ix, index_be)
+    gp.close()
+
+
+def test_pipelined_full_size_equals_single_launch_path(gpu_node):
+    """0.84 GB (64 maps of 131072 TeraSort records, the bench map shape) in 8-map groups:
+    identical bytes to one sux_partition_maps launch over the same input."""
+    n, rpm, R = 64 * 131072, 131072, 200
+    opart = O.terasort_partitioner(R)
+    gp = gpu_part(gpu_node, opart)
+    d = gpu_node.generate(N.GEN_TERASORT, 0x5EED0002, 0, n, 100)
+    a = gpu_node.partition_maps_pipelined(gp, d, 100, rpm, group_records=8 * rpm)
+    b = gpu_node.partition_maps(gp, d, 100, rpm)
+    torch.cuda.synchronize()
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    idx = a[1].view(-1, R + 1)
+    assert bool((idx[:, R] == rpm * 100).all()) and bool((idx[:, 1:] >= idx[:, :-1]).all())
+    gp.close()
+
+
+def test_pipelined_rejects_partial_map_groups(gpu_node):
+    gp = gpu_part(gpu_node, O.terasort_partitioner(8))
+    d = torch.zeros(1000 * 100, dtype=torch.uint8, device="cuda")
+    with pytest.raises(N.SuxError) as e:
+        gpu_node.partition_maps_pipelined(gp, d, 100, 300, group_records=500)
+    assert e.value.code == N.SUX_EINVAL
+    gp.close()
+
+
+# ---- every shape the tuning table selects, bit-exact ----------------------------------------
+TUNINGS = [
+    {"scatter_chunk": 768},                              # the co-resident K3 shape
+    {"scatter_chunk": 768, "hist_wgs_per_cu": 1},
+    {"coresident": -1},
+    {"scatter_chunk": 768, "scatter_depth": 2},
+    {"scatter_chunk": 1024, "hist_stage": 128},
+    {"hist_stage": 64, "hist_wgs_per_cu": 2},
+    {"tiles_per_item": 1},
+    {"tiles_per_item": 64},
+    {"scatter_kernel": 6},
+    {"scatter_kernel": 6, "s6_chunk": 384},
+    {"scatter_kernel": 2, "hist_kernel": 2},
+    {"scatter_kernel": 1, "hist_kernel": 1},
+    {"hist_kernel": 3},
+    {"tile_records": 1024},
+]
+
+
+@pytest.mark.parametrize("tn", TUNINGS, ids=lambda t: ",".join(f"{k}={v}" for k, v in t.items()))
+@pytest.mark.parametrize("R", [200, 512])
+def test_tuning_shapes_are_bit_exact(gpu_node, tuned, tn, R):
+    tuned(**tn)
+    n, rpm = 3 * 40000 + 999, 40000
+    recs = O.gen_terasort(35, 0, n)
+    opart = O.terasort_partitioner(R)
+    gp = gpu_part(gpu_node, opart)
+    ws = torch.empty(gpu_node.workspace_size(gp, 100, rpm, n), dtype=torch.uint8, device="cuda")
+    out, index, index_be = gpu_node.partition_maps(gp, torch.from_numpy(recs).cuda(), 100, rpm,
+                                                   num_records=n, workspace=ws)
+    torch.cuda.synchronize()
+    expect(opart, recs, 100, rpm, out, index, index_be)
+    gp.close()
+
+
+@pytest.mark.parametrize("groups", [1, 2, 4])
+def test_small_record_groups_per_turn_bit_exact(gpu_node, tuned, groups):
+    tuned(small_groups=groups)
+    recs = O.gen_small(36, 0, 200000)
+    opart = O.Partitioner(O.MURMUR3_LONG, 3000, 0, 8, seed=42)
+    gp = gpu_part(gpu_node, opart)
+    out, index, index_be = gpu_node.partition_maps(gp, torch.from_numpy(recs).cuda(), 16, 50000)
+    torch.cuda.synchronize()
+    expect(opart, recs, 16, 50000, out, index, index_be)
+    gp.close()
+
+
+def test_kernel_variant_reports_the_coresident_shape(gpu_node, tuned):
+    """The timing slots name the variant that ran (bench.py's roofline cites it)."""
+    gp = gpu_part(gpu_node, O.terasort_partitioner(200))
+    d = gpu_node.generate(N.GEN_TERASORT, 37, 0, 100000, 100)
+    gpu_node.partition_maps_pipelined(gp, d, 100, 25000, group_records=50000)
+    torch.cuda.synchronize()
+    assert gpu_node.kernel_variant(0) == "k_hist4" and gpu_node.kernel_variant(2) == "k_scatter7"
+    gp.close()

@@ -6,7 +6,7 @@ tag=${1:-r01}; shift
 out=gpurun_out/$tag
 mkdir -p $out
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-echo "== tests" && timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $out/tests.log 2>&1 || { tail -30 $out/tests.log; exit 1; }
+echo "== tests" && timeout -k 10 800 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $out/tests.log 2>&1 || { tail -30 $out/tests.log; exit 1; }
 tail -3 $out/tests.log
 echo "== smoke" && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || { tail -30 $out/smoke.log; exit 1; }
 echo "== bench" && timeout -k 10 400 python -u bench.py "$@" > $out/bench.json 2> $out/bench.err || { tail -30 $out/bench.err; exit 1; }
