@@ -685,6 +685,7 @@ def main():
     t1 = time.perf_counter()
     node.set_kernel_timing(False)
     kt = node.kernel_times()
+    node.check()  # no kernel recorded a failure in the device error word
 
     elapsed = t1 - t0
     if world > 1:

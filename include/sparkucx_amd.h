@@ -149,9 +149,16 @@ typedef struct sux_tuning {
   int32_t sort_gather;      /* 1: records gathered after the sort instead of riding in the pairs */
   int32_t sort_all_passes;  /* 1: every digit pass runs (no key-span read-back)                  */
   int32_t hist_wgs_per_cu;  /* k_hist4 workgroups per CU: 1 .. 8 (0: as many as LDS allows)     */
-  int32_t reserved[15];
+  int32_t small_kernel;     /* 16-byte records, R > 1024: 1 turn-taking scatter, 2 sorted chunks
+                               (0: 2 while R <= 16384)                                          */
+  int32_t reserved[14];
 } sux_tuning;
 int sux_node_set_tuning(sux_node* node, const sux_tuning* tuning);
+/* Waits for the device, then reports (and clears) failures the kernels recorded in the node's
+ * device error word: a bounded in-kernel wait that timed out (the kernel stopped without
+ * writing through it).  SUX_EHIP names the failure; SUX_OK when none.  The asynchronous calls
+ * cannot return such a failure themselves; call this after synchronising on their stream. */
+int sux_node_check(sux_node* node);
 int sux_node_get_tuning(sux_node* node, sux_tuning* tuning);
 
 /* ---- partitioner object: P1 (UcxShuffleManager.getWriter picks the writer, :36-50) ---------- */

@@ -45,7 +45,8 @@ WORKLOAD_ARGS = {  # one PMC run: 8 launch groups of the bench's default shape p
     "small": ["--workload", "small", "--records", str(8 * 32 * (1 << 20))],
 }
 COMMON = ["--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--varlen-rows", "0",
-          "--compress-maps", "0", "--file-maps", "0", "--reduce-sort-records", "0"]
+          "--compress-maps", "0", "--file-maps", "0", "--reduce-sort-records", "0",
+          "--plugin-groups", "0", "--self-check", "0"]
 
 
 def short(name: str) -> str | None:

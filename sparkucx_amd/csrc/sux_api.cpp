@@ -346,6 +346,7 @@ struct sux_node {
   sux_allgather_fn boot = nullptr;   // host all-gather of the embedding runtime
   void* boot_ctx = nullptr;
   sux_tuning tuning{};               // all zero = measured defaults (resolve_tuning)
+  uint32_t* d_err = nullptr;         // device error word (sux::kErr* bits), sux_node_check
   // sux_partition_maps_pipelined: two map streams, their group workspaces, fork/join events
   hipStream_t pipe[2] = {nullptr, nullptr};
   PoolBuf pipe_ws[2];
@@ -521,6 +522,7 @@ sux::Tuning resolve_tuning(const sux_tuning& t, bool pipelined) {
   r.onepass = t.onepass == 1;
   if (t.varlen_kernel) r.varlen_kernel = t.varlen_kernel;
   r.varlen_tile = t.varlen_tile;
+  r.small_kernel = t.small_kernel;
   return r;
 }
 
@@ -543,6 +545,7 @@ Group make_group(const sux_partitioner* part, const void* recs, uint32_t rs, uin
   G.g.rec_size = rs;
   G.g.tile_recs = tile;
   G.g.tiles_per_map = (uint32_t)((rpm + tile - 1) / tile);
+  G.g.err = part->node->d_err;
   G.ws = sux::workspace_layout(R, rs, rpm, n, tile, true);
   return G;
 }
@@ -676,6 +679,8 @@ int sux_node_create(const sux_conf* conf, int is_driver, sux_node** out) {
     n->is_driver = is_driver != 0;
     n->bind();
     n->pool = std::make_unique<DevicePool>(conf->min_buffer_size, conf->min_allocation_size);
+    hip_check(hipMalloc(&n->d_err, sizeof(uint32_t)), "hipMalloc(error word)");
+    hip_check(hipMemset(n->d_err, 0, sizeof(uint32_t)), "hipMemset(error word)");
     // UcxNode.java:81-83: executors preallocate the configured buffers
     if (!n->is_driver)
       for (uint32_t k = 0; k < conf->num_prealloc; ++k)
@@ -729,6 +734,7 @@ int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
     require(in(t->hist_stage, {64, 128}), SUX_EINVAL, "hist_stage must be 64 or 128");
     require(t->hist_wgs_per_cu >= 0 && t->hist_wgs_per_cu <= 8, SUX_EINVAL,
             "hist_wgs_per_cu must be 0..8");
+    require(in(t->small_kernel, {1, 2}), SUX_EINVAL, "small_kernel must be 1 or 2");
     require(in(t->s6_chunk, {256, 384, 512, 1024}), SUX_EINVAL, "s6_chunk must be 256..1024");
     require(t->tiles_per_item >= 0 && t->tiles_per_item <= 4096, SUX_EINVAL,
             "tiles_per_item must be 0..4096");
@@ -751,6 +757,27 @@ int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
     require(node, SUX_EINVAL, "NULL node");
     std::lock_guard<std::mutex> lk(node->mu);
     node->tuning = *t;
+  });
+}
+
+int sux_node_check(sux_node* node) {
+  return guard([&] {
+    require(node, SUX_EINVAL, "NULL node");
+    node->bind();
+    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    uint32_t w = 0;
+    hip_check(hipMemcpy(&w, node->d_err, sizeof w, hipMemcpyDeviceToHost), "read error word");
+    if (w == 0) return;
+    hip_check(hipMemset(node->d_err, 0, sizeof w), "clear error word");
+    std::string what;
+    if (w & sux::kErrTurnTimeout)
+      what += "a small-record scatter wave timed out waiting for its turn (the launch stopped "
+              "without writing its remaining records); ";
+    raise(SUX_EHIP, "device error word 0x" + [&] {
+      char b[16];
+      std::snprintf(b, sizeof b, "%x", w);
+      return std::string(b);
+    }() + ": " + what);
   });
 }
 
@@ -777,6 +804,7 @@ int sux_node_destroy(sux_node* node) {
     }
     for (hipEvent_t e : node->pipe_ev)
       if (e) (void)hipEventDestroy(e);
+    if (node->d_err) (void)hipFree(node->d_err);
     for (auto& kv : node->shuffles) release_shuffle(node, *kv.second);
     node->shuffles.clear();
     for (auto& kv : node->ipc_bases) (void)hipIpcCloseMemHandle(kv.second);
@@ -2417,6 +2445,7 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
     if (!run_all && !span_varies(span, sh, sh + digit)) continue;  // identity pass
     pd.seed = sh;
     P.g.recs = pa;
+    P.g.err = node->d_err;
     hip_check(sux::launch_partition_group(pd, P.g, lay, pb, index, nullptr, nullptr,
                                           ws + P.part_off, P.ws, nullptr,
                                           resolve_tuning(node->tuning, false), &node->timer, s),

@@ -41,6 +41,7 @@ struct Tuning {
   int scatter_depth = 1;    // k_scatter7 chunks loaded ahead (768-record chunks: 1 | 2)
   int hist_stage = 64;      // k_hist4 records per LDS stage: 64 | 128
   int hist_wgs_per_cu = 0;  // k_hist4 workgroups per CU (0: as many as LDS allows)
+  int small_kernel = 0;     // 16-byte records, R > 1024: 1 turn-taking k_scatter16b, 2 sorted chunks
   int s6_chunk = 1024;      // k_scatter6 largest chunk
   int tiles_per_item = 0;   // k_scatter6/7 tiles per work item (0: 8 chunks' worth)
   int small_groups = 4;     // k_scatter16b record groups per turn: 1 | 2 | 4
@@ -59,7 +60,10 @@ struct MapGroup {
   uint32_t rec_size;
   uint32_t tile_recs;      // records per tile (one wave's work in hist/scatter)
   uint32_t tiles_per_map;  // ceil(records_per_map / tile_recs)
+  uint32_t* err;           // the node's device error word (kErr* bits), or nullptr
 };
+// Device error word bits (sux_node_check turns a set word into SUX_EHIP).
+constexpr uint32_t kErrTurnTimeout = 1u;  // k_scatter16/16b: a wave waited 2^22 sleeps for its turn
 
 // Per-launch geometry of a group of variable-length record maps (sux_varlen.hip): record i is
 // data[offs[i] - offs[0], offs[i+1] - offs[0]).

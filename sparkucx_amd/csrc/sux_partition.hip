@@ -1416,6 +1416,26 @@ __global__ __launch_bounds__(1024) void k_hist16(PartDev pd, MapGroup g, uint16_
   }
 }
 
+// Wait until the LDS turn counter reaches `want`.  Bounded: after 2^22 sleeps (far beyond any
+// legitimate wait) the wave sets the node's device error word (sux_node_check reports it) and
+// the workgroup's stop flag, and every wave of the workgroup leaves without touching the
+// cursors again; a wave that sees the stop flag while it waits leaves too.  Returns false then.
+__device__ __forceinline__ bool wait_turn(uint32_t* turn, uint32_t want, uint32_t* stop,
+                                          uint32_t* err) {
+  for (uint32_t spin = 0;; ++spin) {
+    if (__hip_atomic_load(turn, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == want) return true;
+    if (__hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
+    if (spin > (1u << 22)) {
+      if (__lane_id() == 0) {
+        if (err) atomicOr(err, kErrTurnTimeout);
+        __hip_atomic_store(stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 template <uint32_t NW>
 __global__ __launch_bounds__(NW * 64) void k_scatter16(MapGroup g, int R, int pid_bits,
                                                        const uint16_t* __restrict__ pids,
@@ -1423,12 +1443,13 @@ __global__ __launch_bounds__(NW * 64) void k_scatter16(MapGroup g, int R, int pi
                                                        const uint64_t* __restrict__ base,
                                                        uint8_t* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) uint32_t cur[];  // [R] next output record of p
-  __shared__ uint32_t turn;
+  __shared__ uint32_t turn, stop;
   const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
   const uint32_t ntiles = g.num_maps * g.tiles_per_map;
   const u32x4* recs = reinterpret_cast<const u32x4*>(g.recs);
   u32x4* out4 = reinterpret_cast<u32x4*>(out);
   const uint64_t lt_mask = (1ull << lane) - 1ull;
+  if (tid == 0) stop = 0;
   for (uint32_t gt = xcd_map(blockIdx.x, gridDim.x); gt < ntiles; gt += gridDim.x) {
     const TileRange tr = tile_range(g, gt);
     const uint64_t* bm = base + (uint64_t)tr.map * R;
@@ -1464,11 +1485,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter16(MapGroup g, int R, int pi
         peers &= bit ? m : ~m;
       }
       // this group's turn: groups update the cursors in input order (stability)
-      for (uint32_t spin = 0; __hip_atomic_load(&turn, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q;
-           ++spin) {
-        __builtin_amdgcn_s_sleep(1);
-        if (spin > (1u << 22)) break;  // never reached: a guard against a hang, not a path
-      }
+      if (!wait_turn(&turn, q, &stop, g.err)) break;
       uint32_t r0 = 0;
       if (valid) r0 = cur[p];
       __builtin_amdgcn_wave_barrier();
@@ -1484,6 +1501,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter16(MapGroup g, int R, int pi
       q += NW;
     }
     __syncthreads();
+    if (stop) return;  // a turn timed out: the error word is set, nothing more is written
   }
 }
 
@@ -1498,12 +1516,13 @@ __global__ __launch_bounds__(NW * 64) void k_scatter16b(MapGroup g, int R, int p
                                                         const uint64_t* __restrict__ base,
                                                         uint8_t* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) uint32_t cur[];  // [R] next output record of p
-  __shared__ uint32_t turn;
+  __shared__ uint32_t turn, stop;
   const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
   const uint32_t ntiles = g.num_maps * g.tiles_per_map;
   const u32x4* recs = reinterpret_cast<const u32x4*>(g.recs);
   u32x4* out4 = reinterpret_cast<u32x4*>(out);
   const uint64_t lt_mask = (1ull << lane) - 1ull;
+  if (tid == 0) stop = 0;
   for (uint32_t gt = xcd_map(blockIdx.x, gridDim.x); gt < ntiles; gt += gridDim.x) {
     const TileRange tr = tile_range(g, gt);
     const uint64_t* bm = base + (uint64_t)tr.map * R;
@@ -1544,11 +1563,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter16b(MapGroup g, int R, int p
         }
         peers[k] = pe;
       }
-      for (uint32_t spin = 0;
-           __hip_atomic_load(&turn, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != b; ++spin) {
-        __builtin_amdgcn_s_sleep(1);
-        if (spin > (1u << 22)) break;  // never reached: a guard against a hang, not a path
-      }
+      if (!wait_turn(&turn, b, &stop, g.err)) break;
       uint32_t dst[GB];
 #pragma unroll
       for (int k = 0; k < GB; ++k) {
@@ -1572,6 +1587,187 @@ __global__ __launch_bounds__(NW * 64) void k_scatter16b(MapGroup g, int R, int p
       b += NW;
     }
     __syncthreads();
+    if (stop) return;  // a turn timed out: the error word is set, nothing more is written
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_scatter16s: the small-record scatter without turns (R <= kS16sMaxR).  A persistent
+// 1024-thread workgroup walks tile ranges in 4096-record chunks; a chunk's stable rank of every
+// record among the chunk's records of its partition comes from sorting the chunk's
+// (pid, position) keys in LDS, not from waves taking turns on the cursors:
+//   1. LSD radix passes of 7 pid bits over the 4096 keys (two for R <= 16384): a wave owns 256
+//      consecutive positions and ranks them group by group with a ballot match against its own
+//      per-digit counters; one block scan over (digit, wave) gives every wave's digit offsets, so
+//      each pass is stable and needs no atomics;
+//   2. run starts of the sorted keys (rs[p] = first sorted position of p), then every record's
+//      destination cursor[p] + (sorted position - rs[p]); run ends advance the cursors;
+//   3. every thread stores the records it loaded, in input order (16-byte stores).
+// Three barriers per pass and three for the rest; the next chunk's pids and records are in
+// flight the whole time.  Same bytes as k_scatter16 / k_scatter16b.
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t kS16sChunk = 4096;    // records per chunk: 4 per thread of 1024
+constexpr uint32_t kS16sIdxBits = 12;    // log2(kS16sChunk)
+constexpr uint32_t kS16sDigit = 7;       // pid bits per LDS radix pass
+constexpr int kS16sMaxR = 16384;         // two passes; cursors + run starts fit the LDS
+
+struct Sc16s {
+  static constexpr uint32_t NT = 1024, NW = 16, PT = kS16sChunk / NT, NB = 1u << kS16sDigit;
+  // cur[R] u32 | rs[R] u16 (padded) | keys[2][chunk] u32 | wc[2][NW][NB] u32 | wsum[NW] u32
+  static __host__ __device__ constexpr uint32_t lds_bytes(int R) {
+    return (uint32_t)R * 4 + ((uint32_t)R * 2 + 15) / 16 * 16 + 2 * kS16sChunk * 4 +
+           2 * NW * NB * 4 + NW * 4;
+  }
+};
+
+__global__ __launch_bounds__(1024) void k_scatter16s(MapGroup g, int R, int pid_bits,
+                                                     const uint16_t* __restrict__ pids,
+                                                     const uint32_t* __restrict__ prefix,
+                                                     const uint64_t* __restrict__ base,
+                                                     uint8_t* __restrict__ out) {
+  using K = Sc16s;
+  constexpr uint32_t NT = K::NT, NW = K::NW, PT = K::PT, NB = K::NB, CH = kS16sChunk;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  uint32_t* cur = reinterpret_cast<uint32_t*>(lds8);
+  uint16_t* rs = reinterpret_cast<uint16_t*>(cur + R);
+  uint32_t* keys0 = reinterpret_cast<uint32_t*>(lds8 + (uint32_t)R * 4 + ((uint32_t)R * 2 + 15) / 16 * 16);
+  uint32_t* keys1 = keys0 + CH;
+  uint32_t* wc0 = keys1 + CH;  // [2][NW][NB]
+  uint32_t* wsum = wc0 + 2 * NW * NB;
+
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  const uint32_t ntiles = g.num_maps * g.tiles_per_map;
+  const u32x4* recs = reinterpret_cast<const u32x4*>(g.recs);
+  u32x4* out4 = reinterpret_cast<u32x4*>(out);
+  const int passes = pid_bits <= (int)kS16sDigit ? 1 : 2;
+
+  for (uint32_t i = tid; i < 2 * NW * NB; i += NT) wc0[i] = 0;
+  for (uint32_t gt = xcd_map(blockIdx.x, gridDim.x); gt < ntiles; gt += gridDim.x) {
+    const TileRange tr = tile_range(g, gt);
+    const uint64_t* bm = base + (uint64_t)tr.map * R;
+    const uint32_t* pm = prefix + ((uint64_t)tr.map * g.tiles_per_map + tr.tile) * R;  // tile-major
+    for (int p = tid; p < R; p += NT) cur[p] = (uint32_t)(bm[p] + pm[p]);
+    const uint32_t nchunks = (uint32_t)((tr.end - tr.begin + CH - 1) / CH);
+    // element e = wave * 256 + j * 64 + lane: a wave's positions are contiguous and visited in
+    // order, which is what keeps every radix pass stable
+    uint32_t pv[PT];
+    u32x4 rv[PT];
+    auto load = [&](uint32_t c, uint32_t (&p)[PT], u32x4 (&r)[PT]) {
+      const uint64_t c0 = tr.begin + (uint64_t)(c < nchunks ? c : 0) * CH;
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) {
+        const uint64_t i = c0 + wave * (PT * kWave) + j * kWave + lane;
+        const uint64_t ii = i < tr.end ? i : tr.end - 1;  // clamped, unconditional
+        p[j] = pids[ii];
+        r[j] = recs[ii];
+      }
+    };
+    if (nchunks) load(0, pv, rv);
+    __syncthreads();  // cursors ready
+    for (uint32_t c = 0; c < nchunks; ++c) {
+      const uint32_t n = (uint32_t)min<uint64_t>(CH, tr.end - tr.begin - (uint64_t)c * CH);
+      uint32_t pn[PT];
+      u32x4 rn[PT];
+      load(c + 1, pn, rn);  // the next chunk flies during this one
+      // 1. LSD radix passes over (pid << 12 | position)
+      uint32_t* kin = keys0;
+      uint32_t* kout = keys1;
+      for (int d = 0; d < passes; ++d) {
+        uint32_t* wc = wc0 + (d & 1) * NW * NB;
+        const uint32_t sh = kS16sIdxBits + d * kS16sDigit;
+        uint32_t key[PT], dig[PT], rank[PT];
+#pragma unroll
+        for (uint32_t j = 0; j < PT; ++j) {
+          const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+          const bool valid = e < n;
+          key[j] = d == 0 ? ((pv[j] << kS16sIdxBits) | e) : (valid ? kin[e] : 0u);
+          dig[j] = valid ? (key[j] >> sh) & (NB - 1) : 0u;
+          uint64_t peers = __ballot(valid);
+#pragma unroll
+          for (uint32_t bb = 0; bb < kS16sDigit; ++bb) {
+            const bool bit = (dig[j] >> bb) & 1u;
+            const uint64_t m = __ballot(bit);
+            peers &= bit ? m : ~m;
+          }
+          uint32_t* w = wc + wave * NB + dig[j];
+          uint32_t r0 = 0;
+          if (valid) r0 = *w;
+          __builtin_amdgcn_wave_barrier();
+          if (valid && (peers & lt_mask) == 0) *w = r0 + (uint32_t)__popcll(peers);
+          __builtin_amdgcn_wave_barrier();
+          rank[j] = valid ? r0 + (uint32_t)__popcll(peers & lt_mask) : ~0u;
+        }
+        __syncthreads();
+        // block exclusive scan of the counters in (digit, wave) order: thread t owns digit
+        // t / 8 and waves 2(t % 8), 2(t % 8) + 1
+        {
+          const uint32_t dg = tid / (NW / 2), w0 = 2 * (tid % (NW / 2));
+          const uint32_t a = wc[w0 * NB + dg], b = wc[(w0 + 1) * NB + dg];
+          const uint32_t incl = wave_incl_scan(a + b, lane);
+          if (lane == kWave - 1) wsum[wave] = incl;
+          __syncthreads();
+          uint32_t before = 0;
+#pragma unroll
+          for (uint32_t w = 0; w < NW; ++w) before += w < (uint32_t)wave ? wsum[w] : 0u;
+          const uint32_t ex = before + incl - (a + b);
+          wc[w0 * NB + dg] = ex;
+          wc[(w0 + 1) * NB + dg] = ex + a;
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < PT; ++j)
+          if (rank[j] != ~0u) kout[wc[wave * NB + dig[j]] + rank[j]] = key[j];
+        __syncthreads();
+        // this counter set is next used at least one barrier later (next chunk or pass)
+        for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
+        uint32_t* t = kin;
+        kin = kout;
+        kout = t;
+      }
+      // 2. run starts, destinations (into the free key buffer, by position), cursor advances
+      uint32_t* dsta = kout;
+      uint32_t endp[PT], endv[PT];
+#pragma unroll
+      for (uint32_t k = 0; k < PT; ++k) {
+        const uint32_t s = tid + k * NT;
+        endp[k] = ~0u;
+        if (s < n) {
+          const uint32_t p = kin[s] >> kS16sIdxBits;
+          if (s == 0 || (kin[s - 1] >> kS16sIdxBits) != p) rs[p] = (uint16_t)s;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t k = 0; k < PT; ++k) {
+        const uint32_t s = tid + k * NT;
+        if (s < n) {
+          const uint32_t key = kin[s], p = key >> kS16sIdxBits;
+          const uint32_t dst = cur[p] + (s - rs[p]);
+          dsta[key & (CH - 1)] = dst;
+          if (s + 1 == n || (kin[s + 1] >> kS16sIdxBits) != p) {
+            endp[k] = p;
+            endv[k] = dst + 1;
+          }
+        }
+      }
+      __syncthreads();
+      // 3. stores in input order; the cursors move on (every read of them is behind the barrier)
+#pragma unroll
+      for (uint32_t k = 0; k < PT; ++k)
+        if (endp[k] != ~0u) cur[endp[k]] = endv[k];
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) {
+        const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+        if (e < n) out4[dsta[e]] = rv[j];
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) {
+        pv[j] = pn[j];
+        rv[j] = rn[j];
+      }
+      __syncthreads();
+    }
   }
 }
 
@@ -1850,7 +2046,16 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   const bool v7 = c6 == 1024 && sv >= 7 && R <= 512 &&
                   Sc7<100, 1024, 16>::lds_bytes(R) <= 160 * 1024;
   timer_begin(timer, kScatter, s);
-  if (s16) {
+  const bool sorted16 = s16 && R <= kS16sMaxR && tn.small_kernel != 1;
+  if (sorted16) {
+    timer_note(timer, kScatter, "k_scatter16s");
+    const size_t lds = Sc16s::lds_bytes(R);
+    allow_lds(reinterpret_cast<const void*>(&k_scatter16s), lds);
+    const dim3 grid(std::min<uint32_t>(total_tiles, 256u));  // one LDS-bound workgroup per CU
+    hipLaunchKernelGGL(k_scatter16s, grid, dim3(1024), lds, s, g, R, bits, pids, counts, base,
+                       d_out);
+    e = hipGetLastError();
+  } else if (s16) {
     timer_note(timer, kScatter, "k_scatter16b");
     const size_t lds = (size_t)R * 4;
     const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(2, (160u * 1024) / (uint32_t)lds));

@@ -42,11 +42,11 @@ class Conf(C.Structure):
 TUNING_FIELDS = ("hist_kernel", "scatter_kernel", "coresident", "scatter_chunk", "scatter_depth",
                  "hist_stage", "s6_chunk", "tiles_per_item", "small_groups", "tile_records",
                  "onepass", "varlen_kernel", "varlen_tile", "sort_max_digit_bits", "sort_gather",
-                 "sort_all_passes", "hist_wgs_per_cu")
+                 "sort_all_passes", "hist_wgs_per_cu", "small_kernel")
 
 
 class Tuning(C.Structure):
-    _fields_ = [(f, C.c_int32) for f in TUNING_FIELDS] + [("reserved", C.c_int32 * 15)]
+    _fields_ = [(f, C.c_int32) for f in TUNING_FIELDS] + [("reserved", C.c_int32 * 14)]
 
 
 # int (*sux_allgather_fn)(void* ctx, const void* send, uint64_t bytes, void* recv)
@@ -77,6 +77,7 @@ _SIGS = {
     "sux_node_set_bootstrap": (C.c_int, [P, ALLGATHER_FN, P]),
     "sux_node_set_tuning": (C.c_int, [P, C.POINTER(Tuning)]),
     "sux_node_get_tuning": (C.c_int, [P, C.POINTER(Tuning)]),
+    "sux_node_check": (C.c_int, [P]),
     "sux_partition_maps_pipelined": (C.c_int, [P, P, P, U32, U64, U64, U64, P, P, P, P]),
     "sux_pool_stats": (C.c_int, [P, C.POINTER(U64), C.POINTER(U64), C.POINTER(U64),
                                  C.POINTER(U64)]),

@@ -103,6 +103,10 @@ class Node:
         N.check(self.lib.sux_node_set_tuning(self.h, C.byref(t)), "sux_node_set_tuning")
         return old
 
+    def check(self):
+        """sux_node_check: raise if a kernel recorded a failure in the device error word."""
+        N.check(self.lib.sux_node_check(self.h), "sux_node_check")
+
     def pool_stats(self) -> dict:
         v = [C.c_uint64() for _ in range(4)]
         N.check(self.lib.sux_pool_stats(self.h, *[C.byref(x) for x in v]), "sux_pool_stats")

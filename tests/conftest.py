@@ -35,3 +35,4 @@ def tuned(gpu_node):
 
     yield set_
     gpu_node.set_tuning(**saved)
+    gpu_node.check()  # no kernel recorded a failure under the test's tuning

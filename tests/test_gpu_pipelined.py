@@ -52,8 +52,6 @@ def test_pipelined_matches_oracle(gpu_node, R, n, rpm, gmaps):
     gp.close()
 
 
-@pytest.mark.parametrize("kind,key_len,off", [(O.MURMUR3_LONG, 8, 0), (O.HASH_INT, 4, 4),
-                                              (O.MURMUR3_BYTES, 12, 8)])
 @pytest.mark.parametrize("co", [1, -1])
 def test_pipelined_coresident_shapes(gpu_node, tuned, co):
     tuned(coresident=co, hist_wgs_per_cu=1 if co == 1 else 0)
@@ -68,6 +66,8 @@ def test_pipelined_coresident_shapes(gpu_node, tuned, co):
     gp.close()
 
 
+@pytest.mark.parametrize("kind,key_len,off", [(O.MURMUR3_LONG, 8, 0), (O.HASH_INT, 4, 4),
+                                              (O.MURMUR3_BYTES, 12, 8)])
 def test_pipelined_hash_kinds_and_skew(gpu_node, kind, key_len, off):
     recs = O.gen_zipf(32, 0, 60000, 1.1, 1 << 12)
     opart = O.Partitioner(kind, 200, off, key_len, seed=42)
@@ -169,9 +169,11 @@ def test_tuning_shapes_are_bit_exact(gpu_node, tuned, tn, R):
     gp.close()
 
 
-@pytest.mark.parametrize("groups", [1, 2, 4])
-def test_small_record_groups_per_turn_bit_exact(gpu_node, tuned, groups):
-    tuned(small_groups=groups)
+@pytest.mark.parametrize("kernel,groups", [(1, 1), (1, 2), (1, 4), (2, 0)])
+def test_small_record_kernels_bit_exact(gpu_node, tuned, kernel, groups):
+    """Both small-record scatters: turn-taking k_scatter16b (1, 2, 4 groups per turn) and the
+    turn-free sorted-chunk k_scatter16s."""
+    tuned(small_kernel=kernel, small_groups=groups)
     recs = O.gen_small(36, 0, 200000)
     opart = O.Partitioner(O.MURMUR3_LONG, 3000, 0, 8, seed=42)
     gp = gpu_part(gpu_node, opart)
@@ -179,6 +181,35 @@ def test_small_record_groups_per_turn_bit_exact(gpu_node, tuned, groups):
     torch.cuda.synchronize()
     expect(opart, recs, 16, 50000, out, index, index_be)
     gp.close()
+    gpu_node.check()
+
+
+@pytest.mark.parametrize("R,n,rpm,skew", [
+    (1025, 70000, 70000, None),         # just above the per-wave-counter limit
+    (10000, 300000, 100000, None),      # C5's R; 4096-record chunks + a ragged tail per tile
+    (10000, 123457, 123457, "one"),     # every record in one partition: 4096-long runs
+    (10000, 200000, 50000, "zipf"),     # Zipf-skewed keys
+    (16384, 150000, 75000, None),       # largest R of the sorted-chunk kernel (14 pid bits)
+    (16385, 100000, 100000, None),      # one above: the turn-taking kernel
+    (4096, 5000, 1000, None),           # maps shorter than one chunk
+])
+def test_sorted_chunk_scatter_shapes(gpu_node, R, n, rpm, skew):
+    if skew == "zipf":
+        recs = O.gen_zipf(39, 0, n, 1.1, 1 << 12)
+        recs = recs.reshape(-1, 100)[:, :16].copy().ravel()
+    else:
+        recs = O.gen_small(39, 0, n)
+    if skew == "one":
+        recs.reshape(-1, 16)[:, :8] = 7
+    opart = O.Partitioner(O.MURMUR3_LONG, R, 0, 8, seed=42)
+    gp = gpu_part(gpu_node, opart)
+    out, index, index_be = gpu_node.partition_maps(gp, torch.from_numpy(recs).cuda(), 16, rpm)
+    torch.cuda.synchronize()
+    expect(opart, recs, 16, rpm, out, index, index_be)
+    want = "k_scatter16s" if R <= 16384 else "k_scatter16b"
+    assert gpu_node.kernel_variant(2) == want
+    gp.close()
+    gpu_node.check()
 
 
 def test_kernel_variant_reports_the_coresident_shape(gpu_node, tuned):
