@@ -338,6 +338,9 @@ def plugin_leg(node, part, data, rs: int, R: int, rpm: int, gm: int, groups: int
             "pool": st}
 
 
+GROUP_BYTES = 32 * (1 << 20) * 100  # the default launch group: 3.36 GB of input
+
+
 def self_check(node, part, data, out, index, n: int, rs: int, rpm: int, R: int,
                group_recs: int, dev) -> dict:
     """Untimed check of the map outputs of one step written into a zeroed buffer, with no CPU
@@ -382,9 +385,11 @@ def load_traffic(workload: str, kernel: str) -> dict | None:
     borrows another kernel's counters; None when that pair was not profiled."""
     try:
         with open(PMC_FILE) as f:
-            e = json.load(f)["workloads"][workload]["kernels"][kernel]
-        return {"bytes_per_record": e["hbm_bytes_per_launch"] / e["records_per_launch"],
-                "source": f"profiles/pmc_r02.json:{workload}/{kernel}"}
+            ks = json.load(f)["workloads"][workload]["kernels"]
+        # a slot that runs several kernels ("k_bucket16a+k_bucket16b") sums their bytes
+        per = sum(ks[k]["hbm_bytes_per_launch"] / ks[k]["records_per_launch"]
+                  for k in kernel.split("+"))
+        return {"bytes_per_record": per, "source": f"profiles/pmc_r02.json:{workload}/{kernel}"}
     except (OSError, KeyError, ValueError, ZeroDivisionError):
         return None
 
@@ -397,9 +402,10 @@ def main():
     ap.add_argument("--workload", default="terasort", choices=sorted(WORKLOADS))
     ap.add_argument("--records", type=int, default=0, help="records per GPU (0 = workload default)")
     ap.add_argument("--map-records", type=int, default=1 << 20, help="records per map batch")
-    ap.add_argument("--group-maps", type=int, default=32,
-                    help="map batches per kernel launch group (32 x 100 MB: the 256 MiB "
-                         "Infinity Cache's write-back of one group's output is amortised)")
+    ap.add_argument("--group-maps", type=int, default=0,
+                    help="map batches per kernel launch group (0: ~3.4 GB of input per group — "
+                         "32 x 100 MB TeraSort maps, 200 x 16 MB small-record maps: the 256 MiB "
+                         "Infinity Cache's write-back and the launch tails are amortised)")
     ap.add_argument("--transport", default="rccl", choices=["rccl", "ipc"],
                     help="N>1 exchange: ncclAllToAllv, or one-sided pull over HIP IPC")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
@@ -476,6 +482,8 @@ def main():
     rs, R, gen, kind, key_len, n1, nN = WORKLOADS[args.workload]
     n = args.records or (n1 if world == 1 else nN)
     rpm, gm = args.map_records, args.group_maps
+    if gm <= 0:
+        gm = max(1, round(GROUP_BYTES / (rpm * rs)))
     maps = -(-n // rpm)
     groups = -(-maps // gm)
     group_recs = gm * rpm

@@ -149,9 +149,10 @@ typedef struct sux_tuning {
   int32_t sort_gather;      /* 1: records gathered after the sort instead of riding in the pairs */
   int32_t sort_all_passes;  /* 1: every digit pass runs (no key-span read-back)                  */
   int32_t hist_wgs_per_cu;  /* k_hist4 workgroups per CU: 1 .. 8 (0: as many as LDS allows)     */
-  int32_t small_kernel;     /* 16-byte records, R > 1024: 1 turn-taking scatter, 2 sorted chunks
-                               (0: 2 while R <= 16384)                                          */
-  int32_t reserved[14];
+  int32_t small_kernel;     /* 16-byte records, R > 1024: 1 turn-taking scatter, 2 sorted chunks,
+                               3 two passes through bucket order (R <= 16384)                    */
+  int32_t small_waves;      /* two-pass small-record kernels: waves per workgroup, 8 or 16      */
+  int32_t reserved[13];
 } sux_tuning;
 int sux_node_set_tuning(sux_node* node, const sux_tuning* tuning);
 /* Waits for the device, then reports (and clears) failures the kernels recorded in the node's

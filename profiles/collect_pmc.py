@@ -39,10 +39,11 @@ PASSES = [
 KERNELS = {"k_hist": "hist", "k_scatter": "scatter", "k_tile_scan": "tile_scan",
            "k_map_scan": "map_scan", "k_onepass": "onepass", "k_sweep": "sweep",
            "k_gather_copy": "copy"}
-WORKLOAD_ARGS = {  # one PMC run: 8 launch groups of the bench's default shape per workload
-    "terasort": ["--workload", "terasort", "--records", str(8 * 32 * (1 << 20))],
-    "zipf": ["--workload", "zipf", "--records", str(8 * 32 * (1 << 20))],
-    "small": ["--workload", "small", "--records", str(8 * 32 * (1 << 20))],
+WORKLOAD_ARGS = {  # one PMC run: 8 launch groups of 32 maps x 2^20 records per workload (the
+    # traffic per record is what bench.py reads; it does not depend on the group size)
+    "terasort": ["--workload", "terasort", "--records", str(8 * 32 * (1 << 20)), "--group-maps", "32"],
+    "zipf": ["--workload", "zipf", "--records", str(8 * 32 * (1 << 20)), "--group-maps", "32"],
+    "small": ["--workload", "small", "--records", str(8 * 32 * (1 << 20)), "--group-maps", "32"],
 }
 COMMON = ["--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--varlen-rows", "0",
           "--compress-maps", "0", "--file-maps", "0", "--reduce-sort-records", "0",

@@ -506,6 +506,8 @@ struct Group {
 // groups in flight (sux_partition_maps_pipelined, sux_write_map_outputs); the co-resident K1/K3
 // shapes are then possible, but measured slower (profiles/r02_sw_b: 1331 vs 1437 GB/s on
 // TeraSort 100 GB: a K1 beside K3 takes K3's HBM share), so they are opt-in.
+constexpr int kDefaultSmallKernel = 2;  // sorted chunks (profiles/r02_small_b)
+
 sux::Tuning resolve_tuning(const sux_tuning& t, bool pipelined) {
   sux::Tuning r;
   if (t.hist_kernel) r.hist_kernel = t.hist_kernel;
@@ -522,7 +524,8 @@ sux::Tuning resolve_tuning(const sux_tuning& t, bool pipelined) {
   r.onepass = t.onepass == 1;
   if (t.varlen_kernel) r.varlen_kernel = t.varlen_kernel;
   r.varlen_tile = t.varlen_tile;
-  r.small_kernel = t.small_kernel;
+  r.small_kernel = t.small_kernel ? t.small_kernel : kDefaultSmallKernel;
+  if (t.small_waves) r.small_waves = t.small_waves;
   return r;
 }
 
@@ -546,7 +549,7 @@ Group make_group(const sux_partitioner* part, const void* recs, uint32_t rs, uin
   G.g.tile_recs = tile;
   G.g.tiles_per_map = (uint32_t)((rpm + tile - 1) / tile);
   G.g.err = part->node->d_err;
-  G.ws = sux::workspace_layout(R, rs, rpm, n, tile, true);
+  G.ws = sux::workspace_layout(R, rs, rpm, n, tile, true, sux::small_two_pass_shape(R, rs));
   return G;
 }
 
@@ -734,7 +737,8 @@ int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
     require(in(t->hist_stage, {64, 128}), SUX_EINVAL, "hist_stage must be 64 or 128");
     require(t->hist_wgs_per_cu >= 0 && t->hist_wgs_per_cu <= 8, SUX_EINVAL,
             "hist_wgs_per_cu must be 0..8");
-    require(in(t->small_kernel, {1, 2}), SUX_EINVAL, "small_kernel must be 1 or 2");
+    require(in(t->small_kernel, {1, 2, 3}), SUX_EINVAL, "small_kernel must be 1, 2 or 3");
+    require(in(t->small_waves, {8, 16}), SUX_EINVAL, "small_waves must be 8 or 16");
     require(in(t->s6_chunk, {256, 384, 512, 1024}), SUX_EINVAL, "s6_chunk must be 256..1024");
     require(t->tiles_per_item >= 0 && t->tiles_per_item <= 4096, SUX_EINVAL,
             "tiles_per_item must be 0..4096");

@@ -41,7 +41,9 @@ struct Tuning {
   int scatter_depth = 1;    // k_scatter7 chunks loaded ahead (768-record chunks: 1 | 2)
   int hist_stage = 64;      // k_hist4 records per LDS stage: 64 | 128
   int hist_wgs_per_cu = 0;  // k_hist4 workgroups per CU (0: as many as LDS allows)
-  int small_kernel = 0;     // 16-byte records, R > 1024: 1 turn-taking k_scatter16b, 2 sorted chunks
+  int small_kernel = 0;     // 16-byte records, R > 1024: 1 turn-taking k_scatter16b, 2 sorted
+                            // chunks, 3 two passes through bucket order (needs the temp copy)
+  int small_waves = 8;      // two-pass small-record kernels: waves per workgroup (8 | 16)
   int s6_chunk = 1024;      // k_scatter6 largest chunk
   int tiles_per_item = 0;   // k_scatter6/7 tiles per work item (0: 8 chunks' worth)
   int small_groups = 4;     // k_scatter16b record groups per turn: 1 | 2 | 4
@@ -90,10 +92,16 @@ struct Workspace {
   uint64_t base_off, base_bytes;      // u64 [map][R] destination record offset of (map, p)
   uint64_t pids_off, pids_bytes;      // u16 [records] when the caller passes no pid buffer
   uint64_t op_off, op_bytes;          // one-pass kernel's sync words + scan tables (S = 100)
+  uint64_t tmp_off, tmp_bytes;        // two-pass small-record scatter: records grouped by bucket
   uint64_t total;
 };
+// Small records whose map side may take the two-pass scatter (it needs the temp copy).
+inline bool small_two_pass_shape(uint32_t R, uint32_t rec_size) {
+  return rec_size == 16 && R > 1024 && R <= 16384;
+}
 Workspace workspace_layout(uint32_t R, uint32_t rec_size, uint64_t records_per_map,
-                           uint64_t num_records, uint32_t tile_recs, bool need_pids);
+                           uint64_t num_records, uint32_t tile_recs, bool need_pids,
+                           bool small_tmp = false);
 uint32_t choose_tile_recs(uint32_t R, uint32_t rec_size, uint64_t records_per_map,
                           const Tuning& tn);
 

@@ -1771,6 +1771,302 @@ __global__ __launch_bounds__(1024) void k_scatter16s(MapGroup g, int R, int pid_
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Two-pass small-record scatter (16-byte records, R > 1024): C5 writes ~0.4 record per
+// partition per 4096-record chunk, so a one-pass scatter stores every record alone — a partial
+// 128-B line each (PMC: 32 B written per 16-B record) at a random address.  Instead:
+//   pass A (k_bucket16a) regroups every tile by bucket = pid >> 6 (<= 256 buckets) into the
+//          workspace's temp buffer, at the bucket's final position: bucket h of map m starts at
+//          base[m][64h], the tile's share after the earlier tiles' (the K2 tile prefix summed
+//          over the bucket's 64 partitions).  A chunk is stable-sorted by bucket in LDS and
+//          written in sorted order: runs of ~26 records per bucket instead of ~0.4;
+//   pass B (k_bucket16b) takes one (map, bucket) segment — its output range is the same
+//          range of the output, [base[m][64h], base[m][64h+64]) — recomputes each record's pid
+//          from its key, stable-sorts by the low 6 bits in LDS and writes the segment back in
+//          order: one contiguous, fully coalesced range per segment.
+// 16 + 2 + 16 (A) and 16 + 16 (B) bytes per record, every write a long run.  Stable: pass A
+// keeps input order inside a bucket, pass B inside a partition.
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t kB16Lo = 6;         // partitions per bucket: 64
+constexpr uint32_t kB16PT = 4;         // records per thread per LDS chunk (chunk = 256 x waves)
+
+template <uint32_t NW>  // stage[chunk] u32x4 | wc[NW][256] u32 | cb[256] u32 | wsum[NW] | hs[chunk] u8
+struct B16a {
+  static constexpr uint32_t NB = 256, CH = NW * kWave * kB16PT;
+  static constexpr uint32_t lds_bytes() { return CH * 16 + NW * NB * 4 + NB * 4 + NW * 4 + CH; }
+};
+template <uint32_t NW>  // stage[chunk] u32x4 | wc[NW][64] u32 | cur[64] u32 | wsum[NW] | los[chunk] u8
+struct B16b {
+  static constexpr uint32_t NB = 1u << kB16Lo, CH = NW * kWave * kB16PT;
+  static constexpr uint32_t lds_bytes() { return CH * 16 + NW * NB * 4 + NB * 4 + NW * 4 + CH; }
+};
+
+// Stable in-wave rank of `dig` (DB bits) against the wave's running per-digit counters wcw[]:
+// lanes of the group in lane order after the wave's earlier groups.  ~0 for invalid lanes.
+template <uint32_t DB>
+__device__ __forceinline__ uint32_t wave_rank(uint32_t dig, bool valid, uint32_t* wcw, uint64_t lt_mask) {
+  uint64_t peers = __ballot(valid);
+#pragma unroll
+  for (uint32_t bb = 0; bb < DB; ++bb) {
+    const bool bit = (dig >> bb) & 1u;
+    const uint64_t m = __ballot(bit);
+    peers &= bit ? m : ~m;
+  }
+  uint32_t r0 = 0;
+  if (valid) r0 = wcw[dig];
+  __builtin_amdgcn_wave_barrier();
+  if (valid && (peers & lt_mask) == 0) wcw[dig] = r0 + (uint32_t)__popcll(peers);
+  __builtin_amdgcn_wave_barrier();
+  return valid ? r0 + (uint32_t)__popcll(peers & lt_mask) : ~0u;
+}
+
+// Block exclusive scan of wc[NW][NB] in (digit, wave) order, in place (NW*64 threads, NB*NW
+// entries, E = NB/64 consecutive entries per thread).  Two barriers.
+template <uint32_t NB, uint32_t NW>
+__device__ __forceinline__ void scan_digit_wave(uint32_t* wc, uint32_t* wsum, int tid, int lane, int wave) {
+  constexpr uint32_t E = NB / kWave;
+  static_assert(E >= 1 && NW % E == 0, "entries per thread");
+  const uint32_t dg = (uint32_t)tid * E / NW, w0 = ((uint32_t)tid * E) % NW;
+  uint32_t v[E], sum = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < E; ++k) {
+    v[k] = wc[(w0 + k) * NB + dg];
+    sum += v[k];
+  }
+  const uint32_t incl = wave_incl_scan(sum, lane);
+  if (lane == kWave - 1) wsum[wave] = incl;
+  __syncthreads();
+  uint32_t run = incl - sum;
+#pragma unroll
+  for (uint32_t w = 0; w < NW; ++w) run += w < (uint32_t)wave ? wsum[w] : 0u;
+#pragma unroll
+  for (uint32_t k = 0; k < E; ++k) {
+    wc[(w0 + k) * NB + dg] = run;
+    run += v[k];
+  }
+  __syncthreads();
+}
+
+template <uint32_t NW>
+__global__ __launch_bounds__(NW * 64) void k_bucket16a(MapGroup g, int R,
+                                                    const uint16_t* __restrict__ pids,
+                                                    const uint32_t* __restrict__ prefix,
+                                                    const uint64_t* __restrict__ base,
+                                                    uint8_t* __restrict__ tmp) {
+  constexpr uint32_t NB = B16a<NW>::NB, CH = B16a<NW>::CH, PT = kB16PT, NT = NW * kWave;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  u32x4* stage = reinterpret_cast<u32x4*>(lds8);
+  uint32_t* wc = reinterpret_cast<uint32_t*>(stage + CH);  // [NW][NB]
+  uint32_t* cb = wc + NW * NB;
+  uint32_t* wsum = cb + NB;
+  uint8_t* hs = reinterpret_cast<uint8_t*>(wsum + NW);
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  const uint32_t ntiles = g.num_maps * g.tiles_per_map;
+  const uint32_t nbk = ((uint32_t)R + (1u << kB16Lo) - 1) >> kB16Lo;
+  const u32x4* recs = reinterpret_cast<const u32x4*>(g.recs);
+  u32x4* t4 = reinterpret_cast<u32x4*>(tmp);
+  for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
+  for (uint32_t gt = xcd_map(blockIdx.x, gridDim.x); gt < ntiles; gt += gridDim.x) {
+    const TileRange tr = tile_range(g, gt);
+    if (tid < (int)nbk) {  // bucket cursor: its base + the earlier tiles' records of its partitions
+      const uint32_t p0 = (uint32_t)tid << kB16Lo, p1 = min(p0 + (1u << kB16Lo), (uint32_t)R);
+      const uint32_t* pm = prefix + ((uint64_t)tr.map * g.tiles_per_map + tr.tile) * R;
+      uint32_t s = 0;
+      for (uint32_t p = p0; p < p1; ++p) s += pm[p];
+      cb[tid] = (uint32_t)base[(uint64_t)tr.map * R + p0] + s;
+    }
+    const uint32_t nchunks = (uint32_t)((tr.end - tr.begin + CH - 1) / CH);
+    uint32_t pv[PT];
+    u32x4 rv[PT];
+    auto load = [&](uint32_t c, uint32_t (&p)[PT], u32x4 (&r)[PT]) {
+      const uint64_t c0 = tr.begin + (uint64_t)(c < nchunks ? c : 0) * CH;
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) {
+        const uint64_t i = c0 + wave * (PT * kWave) + j * kWave + lane;
+        const uint64_t ii = i < tr.end ? i : tr.end - 1;
+        p[j] = pids[ii];
+        r[j] = recs[ii];
+      }
+    };
+    if (nchunks) load(0, pv, rv);
+    __syncthreads();
+    for (uint32_t c = 0; c < nchunks; ++c) {
+      const uint32_t n = (uint32_t)min<uint64_t>(CH, tr.end - tr.begin - (uint64_t)c * CH);
+      uint32_t pn[PT];
+      u32x4 rn[PT];
+      load(c + 1, pn, rn);
+      uint32_t h[PT], rank[PT];
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) {
+        const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+        h[j] = (pv[j] >> kB16Lo) & (NB - 1);
+        rank[j] = wave_rank<8>(h[j], e < n, wc + wave * NB, lt_mask);
+      }
+      __syncthreads();
+      scan_digit_wave<NB, NW>(wc, wsum, tid, lane, wave);
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j)
+        if (rank[j] != ~0u) {
+          const uint32_t pos = wc[wave * NB + h[j]] + rank[j];
+          stage[pos] = rv[j];
+          hs[pos] = (uint8_t)h[j];
+        }
+      __syncthreads();
+      // sorted order: consecutive positions of a bucket go to consecutive temp records
+#pragma unroll
+      for (uint32_t k = 0; k < PT; ++k) {
+        const uint32_t i = tid + k * NT;
+        if (i < n) {
+          const uint32_t b = hs[i];
+          const uint64_t dst = (uint64_t)cb[b] + (i - wc[b]);  // wc[0 * NB + b]: bucket start
+          if (dst < g.num_records) t4[dst] = stage[i];         // (a bad pid cannot fault)
+        }
+      }
+      uint32_t ncb = 0;
+      if (tid < (int)nbk) {
+        const uint32_t end = (uint32_t)tid + 1 < NB ? wc[tid + 1] : n;
+        ncb = cb[tid] + (end - wc[tid]);
+      }
+      __syncthreads();
+      if (tid < (int)nbk) cb[tid] = ncb;
+      for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) {
+        pv[j] = pn[j];
+        rv[j] = rn[j];
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Pass B walks a stream of (segment, chunk) pairs: the next chunk's records — across a segment
+// seam too, with the next segment's 64 cursors — are loaded while this chunk is sorted and
+// written, so no chunk waits for its loads.
+template <int KW, uint32_t NW>
+__global__ __launch_bounds__(NW * 64) void k_bucket16b(PartDev pd, MapGroup g,
+                                                    const uint64_t* __restrict__ base,
+                                                    const uint64_t* __restrict__ totals,
+                                                    const uint8_t* __restrict__ tmp,
+                                                    uint8_t* __restrict__ out) {
+  constexpr uint32_t NB = B16b<NW>::NB, CH = B16b<NW>::CH, PT = kB16PT, NT = NW * kWave;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  u32x4* stage = reinterpret_cast<u32x4*>(lds8);
+  uint32_t* wc = reinterpret_cast<uint32_t*>(stage + CH);  // [NW][NB]
+  uint32_t* cur = wc + NW * NB;
+  uint32_t* wsum = cur + NB;
+  uint8_t* los = reinterpret_cast<uint8_t*>(wsum + NW);
+  const int R = pd.R;
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  const uint32_t nbk = ((uint32_t)R + NB - 1) / NB;
+  const uint32_t nitems = g.num_maps * nbk, G = gridDim.x;
+  const int kw0 = pd.key_offset / 4;
+  const u32x4* t4 = reinterpret_cast<const u32x4*>(tmp);
+  u32x4* out4 = reinterpret_cast<u32x4*>(out);
+
+  struct Cur {
+    uint32_t it, p0;
+    uint64_t c0, b1;
+    bool valid, first;
+  };
+  auto seg = [&](uint32_t it) {  // first chunk of segment `it` (an empty segment: c0 == b1)
+    Cur k;
+    k.it = it;
+    k.valid = it < nitems;
+    k.first = true;
+    const uint32_t m = k.valid ? it / nbk : 0, hb = k.valid ? it - m * nbk : 0;
+    k.p0 = hb * NB;
+    const uint32_t p1 = min(k.p0 + NB, (uint32_t)R);
+    const uint64_t* bm = base + (uint64_t)m * R;
+    k.c0 = bm[k.p0];
+    k.b1 = bm[p1 - 1] + totals[(uint64_t)m * R + p1 - 1];
+    return k;
+  };
+  auto next = [&](const Cur& k) {
+    Cur nk = k;
+    nk.first = false;
+    nk.c0 = k.c0 + CH;
+    if (nk.c0 >= k.b1) nk = seg(k.it + G);
+    return nk;
+  };
+  // loads of chunk k (clamped, unconditional) and, at a segment's first chunk, its cursors
+  auto issue = [&](const Cur& k, u32x4 (&r)[PT], uint32_t& cv) {
+    const uint32_t n = k.valid && k.b1 > k.c0 ? (uint32_t)min<uint64_t>(CH, k.b1 - k.c0) : 1u;
+    const uint64_t c0 = k.valid && k.b1 > k.c0 ? k.c0 : 0;
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j) {
+      const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+      r[j] = t4[c0 + (e < n ? e : n - 1)];
+    }
+    if (k.valid && k.first && tid < (int)NB) {
+      const uint32_t m = k.it / nbk;
+      const uint32_t p = min(k.p0 + (uint32_t)tid, (uint32_t)R - 1);
+      cv = (uint32_t)base[(uint64_t)m * R + p];
+    }
+  };
+
+  for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
+  Cur k = seg(xcd_map(blockIdx.x, G));
+  u32x4 rv[PT];
+  uint32_t cv = 0;
+  issue(k, rv, cv);
+  while (k.valid) {
+    if (k.first && tid < (int)NB) cur[tid] = cv;  // nothing reads cur until the write phase
+    const Cur nk = next(k);
+    u32x4 rn[PT];
+    uint32_t cn = cv;
+    issue(nk, rn, cn);
+    const uint32_t n = k.b1 > k.c0 ? (uint32_t)min<uint64_t>(CH, k.b1 - k.c0) : 0u;
+    uint32_t lo[PT], rank[PT];
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j) {
+      const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+      uint32_t w[KW];
+#pragma unroll
+      for (int q = 0; q < KW; ++q) {
+        const int d = kw0 + q;
+        w[q] = d == 0 ? rv[j][0] : d == 1 ? rv[j][1] : d == 2 ? rv[j][2] : rv[j][3];
+      }
+      lo[j] = ((uint32_t)partition_words<KW, false>(pd, w, pd.bounds, pd.lut) - k.p0) & (NB - 1);
+      rank[j] = wave_rank<kB16Lo>(lo[j], e < n, wc + wave * NB, lt_mask);
+    }
+    __syncthreads();
+    scan_digit_wave<NB, NW>(wc, wsum, tid, lane, wave);
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j)
+      if (rank[j] != ~0u) {
+        const uint32_t pos = wc[wave * NB + lo[j]] + rank[j];
+        stage[pos] = rv[j];
+        los[pos] = (uint8_t)lo[j];
+      }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < PT; ++q) {
+      const uint32_t i = tid + q * NT;
+      if (i < n) {
+        const uint32_t l = los[i];
+        const uint64_t dst = (uint64_t)cur[l] + (i - wc[l]);
+        if (dst < g.num_records) out4[dst] = stage[i];  // (a bad pid cannot fault)
+      }
+    }
+    uint32_t ncur = 0;
+    if (tid < (int)NB) {
+      const uint32_t end = (uint32_t)tid + 1 < NB ? wc[tid + 1] : n;
+      ncur = cur[tid] + (end - wc[tid]);
+    }
+    __syncthreads();
+    if (tid < (int)NB) cur[tid] = ncur;
+    for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j) rv[j] = rn[j];
+    cv = cn;
+    k = nk;
+  }
+}
+
 template <int KW, bool TAB>
 static void launch_hist3_kw(dim3 grid, size_t lds, hipStream_t s, const PartDev& pd,
                             const MapGroup& g, uint16_t* pids, uint32_t* counts) {
@@ -1793,11 +2089,16 @@ __global__ __launch_bounds__(256) void k_pids(PartDev pd, const uint8_t* recs, u
 // ------------------------------------------------------------------------------------------
 uint32_t choose_tile_recs(uint32_t R, uint32_t rec_size, uint64_t records_per_map,
                           const Tuning& tn) {
-  (void)rec_size;
   // 4096 records (400 KB at S=100) per tile: fewer counters to scan, and the partial 128-B
   // lines at tile seams are rarer (measured: 1024 -> 4096 takes ~1 ms off a 100 GB step)
   uint32_t t = 4096;
   while (t < 4u * R && t < (1u << 22)) t <<= 1;
+  // small records, many partitions: the sorted-chunk scatter re-reads R cursors per tile
+  // (32 Ki records measured best at R = 10000, profiles/r02_small_b); the two-pass scatter's
+  // pass A walks whole tiles too (one tile per persistent workgroup at a time: a launch group
+  // needs >> 256 tiles)
+  if (small_two_pass_shape(R, rec_size) && tn.small_kernel == 2) t = 32768;
+  if (small_two_pass_shape(R, rec_size) && tn.small_kernel == 3) t = 32768;
   const uint32_t v = (uint32_t)tn.tile_records;  // tuning override (power of two, >= 64)
   if (v >= 64 && (v & (v - 1)) == 0) t = v;
   // no point in tiles longer than a map
@@ -1809,7 +2110,8 @@ uint32_t choose_tile_recs(uint32_t R, uint32_t rec_size, uint64_t records_per_ma
 static uint64_t align_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
 
 Workspace workspace_layout(uint32_t R, uint32_t rec_size, uint64_t records_per_map,
-                           uint64_t num_records, uint32_t tile_recs, bool need_pids) {
+                           uint64_t num_records, uint32_t tile_recs, bool need_pids,
+                           bool small_tmp) {
   Workspace w{};
   uint64_t maps = records_per_map ? (num_records + records_per_map - 1) / records_per_map : 0;
   if (maps == 0) maps = 1;
@@ -1832,6 +2134,9 @@ Workspace workspace_layout(uint32_t R, uint32_t rec_size, uint64_t records_per_m
   w.op_off = off;
   w.op_bytes = (rec_size == 100 && R <= 1024) ? onepass_sync_bytes(R) : 0;
   off += w.op_bytes;
+  w.tmp_off = off;  // the two-pass small-record scatter's bucketed copy of the records
+  w.tmp_bytes = small_tmp ? align_up(num_records * rec_size, 256) : 0;
+  off += w.tmp_bytes;
   w.total = off;
   return w;
 }
@@ -2046,8 +2351,40 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   const bool v7 = c6 == 1024 && sv >= 7 && R <= 512 &&
                   Sc7<100, 1024, 16>::lds_bytes(R) <= 160 * 1024;
   timer_begin(timer, kScatter, s);
+  const bool two16 = s16 && small_two_pass_shape((uint32_t)R, S) && tn.small_kernel == 3 &&
+                     ws.tmp_bytes >= g.num_records * 16;
   const bool sorted16 = s16 && R <= kS16sMaxR && tn.small_kernel != 1;
-  if (sorted16) {
+  if (two16) {
+    timer_note(timer, kScatter, "k_bucket16a+k_bucket16b");
+    uint8_t* tmp = d_ws + ws.tmp_off;
+    const uint32_t items = g.num_maps * (((uint32_t)R + B16b<8>::NB - 1) / B16b<8>::NB);
+    const int kw = (pd.key_len + 3) / 4;
+    // wave count per workgroup: 8 = two 512-thread workgroups per CU (their phases interleave),
+    // 16 = one 1024-thread workgroup (tuning small_waves; default 8)
+    const bool w16 = tn.small_waves == 16;
+#define SUX_B16(NWV)                                                                             \
+  do {                                                                                           \
+    allow_lds(reinterpret_cast<const void*>(&k_bucket16a<NWV>), B16a<NWV>::lds_bytes());         \
+    hipLaunchKernelGGL((k_bucket16a<NWV>), dim3(std::min<uint32_t>(total_tiles, 256u * (16 / NWV))), \
+                       dim3(NWV * kWave), B16a<NWV>::lds_bytes(), s, g, R, pids, counts, base, tmp); \
+    const dim3 gridb(std::min<uint32_t>(items, 256u * (16 / NWV)));                              \
+    if (kw <= 1) SUX_B16B(1, NWV);                                                               \
+    else if (kw == 2) SUX_B16B(2, NWV);                                                          \
+    else if (kw == 3) SUX_B16B(3, NWV);                                                          \
+    else SUX_B16B(4, NWV);                                                                       \
+  } while (0)
+#define SUX_B16B(KW, NWV)                                                                        \
+  do {                                                                                           \
+    allow_lds(reinterpret_cast<const void*>(&k_bucket16b<KW, NWV>), B16b<NWV>::lds_bytes());     \
+    hipLaunchKernelGGL((k_bucket16b<KW, NWV>), gridb, dim3(NWV * kWave), B16b<NWV>::lds_bytes(), \
+                       s, pd, g, base, totals, tmp, d_out);                                      \
+  } while (0)
+    if (w16) SUX_B16(16);
+    else SUX_B16(8);
+#undef SUX_B16
+#undef SUX_B16B
+    e = hipGetLastError();
+  } else if (sorted16) {
     timer_note(timer, kScatter, "k_scatter16s");
     const size_t lds = Sc16s::lds_bytes(R);
     allow_lds(reinterpret_cast<const void*>(&k_scatter16s), lds);

@@ -169,11 +169,11 @@ def test_tuning_shapes_are_bit_exact(gpu_node, tuned, tn, R):
     gp.close()
 
 
-@pytest.mark.parametrize("kernel,groups", [(1, 1), (1, 2), (1, 4), (2, 0)])
+@pytest.mark.parametrize("kernel,groups", [(1, 1), (1, 2), (1, 4), (2, 0), (3, 0), (3, -1)])
 def test_small_record_kernels_bit_exact(gpu_node, tuned, kernel, groups):
-    """Both small-record scatters: turn-taking k_scatter16b (1, 2, 4 groups per turn) and the
-    turn-free sorted-chunk k_scatter16s."""
-    tuned(small_kernel=kernel, small_groups=groups)
+    """Every small-record scatter: turn-taking k_scatter16b (1, 2, 4 groups per turn), the
+    turn-free sorted-chunk k_scatter16s and the two-pass bucketed k_bucket16a + k_bucket16b."""
+    tuned(small_kernel=kernel, small_groups=max(groups, 0), small_waves=16 if groups < 0 else 0)
     recs = O.gen_small(36, 0, 200000)
     opart = O.Partitioner(O.MURMUR3_LONG, 3000, 0, 8, seed=42)
     gp = gpu_part(gpu_node, opart)
@@ -192,8 +192,13 @@ def test_small_record_kernels_bit_exact(gpu_node, tuned, kernel, groups):
     (16384, 150000, 75000, None),       # largest R of the sorted-chunk kernel (14 pid bits)
     (16385, 100000, 100000, None),      # one above: the turn-taking kernel
     (4096, 5000, 1000, None),           # maps shorter than one chunk
+    (2000, 300000, 300000, "one"),      # one bucket holds the whole map (many LDS chunks)
+    (1100, 90000, 30000, "zipf"),       # a short last bucket (1100 = 17 x 64 + 12)
 ])
-def test_sorted_chunk_scatter_shapes(gpu_node, R, n, rpm, skew):
+@pytest.mark.parametrize("kernel", [2, 3, 316])
+def test_sorted_chunk_scatter_shapes(gpu_node, tuned, kernel, R, n, rpm, skew):
+    """kernel 316: the two-pass path with 16-wave workgroups"""
+    tuned(small_kernel=min(kernel, 3), small_waves=16 if kernel == 316 else 0)
     if skew == "zipf":
         recs = O.gen_zipf(39, 0, n, 1.1, 1 << 12)
         recs = recs.reshape(-1, 100)[:, :16].copy().ravel()
@@ -206,7 +211,8 @@ def test_sorted_chunk_scatter_shapes(gpu_node, R, n, rpm, skew):
     out, index, index_be = gpu_node.partition_maps(gp, torch.from_numpy(recs).cuda(), 16, rpm)
     torch.cuda.synchronize()
     expect(opart, recs, 16, rpm, out, index, index_be)
-    want = "k_scatter16s" if R <= 16384 else "k_scatter16b"
+    want = ("k_scatter16b" if R > 16384 else "k_scatter16s" if kernel == 2
+            else "k_bucket16a+k_bucket16b")
     assert gpu_node.kernel_variant(2) == want
     gp.close()
     gpu_node.check()
