@@ -300,14 +300,25 @@ def plugin_leg(node, part, data, rs: int, R: int, rpm: int, gm: int, groups: int
     # every (map, reduce partition) block, reducer by reducer
     blocks = np.stack([np.tile(np.arange(maps), R), np.repeat(np.arange(R), maps)], 1).astype(np.int32)
 
-    def one(sid):
+    phase = {"register": 0.0, "write": 0.0, "wait": 0.0, "resolve": 0.0, "unregister": 0.0}
+
+    def one(sid, acc=None):
+        t = [time.perf_counter()]
         node.register_shuffle(sid, maps, R, rs)
+        t.append(time.perf_counter())
         for g in range(groups):
             r0 = g * gm * rpm
             node.write_map_outputs(sid, g * gm, part, data[r0 * rs:(r0 + gm * rpm) * rs], rpm,
                                    gm * rpm, stream=stream)
-        addrs, sizes = node.resolve_blocks(sid, blocks)  # waits for every map's publication
+        t.append(time.perf_counter())
+        node.wait_map_outputs(sid)  # every map published (Spark: the map stage's end)
+        t.append(time.perf_counter())
+        addrs, sizes = node.resolve_blocks(sid, blocks)
+        t.append(time.perf_counter())
         assert int(sizes.sum()) == n * rs
+        if acc is not None:
+            for k, a, b in zip(("register", "write", "wait", "resolve"), t, t[1:]):
+                acc[k] += b - a
         return sid
 
     one(1000)
@@ -315,8 +326,10 @@ def plugin_leg(node, part, data, rs: int, R: int, rpm: int, gm: int, groups: int
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(reps):
-        one(1001 + k)
+        one(1001 + k, phase)
+        tu = time.perf_counter()
         node.unregister_shuffle(1001 + k)
+        phase["unregister"] += time.perf_counter() - tu
     torch.cuda.synchronize(dev)
     dt = (time.perf_counter() - t0) / reps
     # one reducer's fetch of partition R//2 from every map
@@ -331,6 +344,7 @@ def plugin_leg(node, part, data, rs: int, R: int, rpm: int, gm: int, groups: int
     st = node.pool_stats()
     return {"maps": maps, "records": n, "bytes": n * rs, "ms": round(dt * 1e3, 3),
             "GB/s": round(n * rs / dt / 1e9, 1),
+            "phase_ms": {k: round(v / reps * 1e3, 3) for k, v in phase.items()},
             "path": "register -> write_map_outputs x%d (%d maps each) -> resolve %d blocks -> "
                     "unregister" % (groups, gm, len(blocks)),
             "fetch_one_reducer": {"blocks": maps, "bytes": fb, "ms": round(ft * 1e3, 3),
@@ -443,7 +457,7 @@ def main():
                          "many map outputs (sux_write_map_files; -1: 8; 0: skip)")
     ap.add_argument("--plugin-groups", type=int, default=-1,
                     help="N=1: also time the plugin path (register -> write -> resolve -> "
-                         "unregister) over this many launch groups of map tasks (-1: 8; 0: skip)")
+                         "unregister) over this many launch groups of map tasks (-1: 16; 0: skip)")
     ap.add_argument("--self-check", type=int, default=1,
                     help="N=1: after the timed steps, run one more step into a zeroed output "
                          "and check it (index offsets, record multiset, partition grouping)")
@@ -811,7 +825,10 @@ def main():
         fm = min(maps, args.file_maps if args.file_maps > 0 else 8)
         result["files"] = files_leg(node, out, index, fm, R, dev)
     if not pipelined and args.plugin_groups != 0:
-        pg = min(groups, args.plugin_groups if args.plugin_groups > 0 else 8)
+        # the stateless output is no longer needed: its HBM goes to the plugin path's slabs
+        out = None
+        torch.cuda.empty_cache()
+        pg = min(groups, args.plugin_groups if args.plugin_groups > 0 else 16)
         if pg and n >= pg * group_recs:
             result["plugin"] = plugin_leg(node, part, data, rs, R, rpm, gm, pg, dev)
     if not pipelined and args.varlen_rows != 0:

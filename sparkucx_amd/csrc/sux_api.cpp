@@ -48,9 +48,12 @@ void hip_check(hipError_t e, const char* what) {
 void nccl_check(ncclResult_t r, const char* what) {
   if (r != ncclSuccess) raise(SUX_ECOMM, std::string(what) + ": " + ncclGetErrorString(r));
 }
-void require(bool ok, int code, const std::string& msg) {
-  if (!ok) raise(code, msg);
-}
+// A failed check throws SuxError; the message expression is evaluated only then (some checks run
+// once per block of a fetch).
+#define require(ok, code, ...)                    \
+  do {                                            \
+    if (!(ok)) raise((code), (__VA_ARGS__));      \
+  } while (0)
 
 template <class F>
 int guard(F&& f) {
@@ -2152,11 +2155,12 @@ void resolve(sux_node* node, Shuffle& sh, const sux_block_id& b, uint64_t* addr,
            std::to_string(b.start_reduce) +
            (b.end_reduce != b.start_reduce + 1 ? "_" + std::to_string(b.end_reduce) : "");
   };
-  require(b.map_index >= 0 && b.map_index < sh.num_maps && b.start_reduce >= 0 &&
-              b.end_reduce > b.start_reduce && b.end_reduce <= R,
-          SUX_EINVAL, "malformed block " + name());
+  // (messages are built only on failure: this runs once per block of every fetch)
+  if (!(b.map_index >= 0 && b.map_index < sh.num_maps && b.start_reduce >= 0 &&
+        b.end_reduce > b.start_reduce && b.end_reduce <= R))
+    raise(SUX_EINVAL, "malformed block " + name());
   const MapSlot& sl = sh.maps[b.map_index];
-  require(sl.present, SUX_ENOENT, "Unknown block " + name() + ": map output not committed");
+  if (!sl.present) raise(SUX_ENOENT, "Unknown block " + name() + ": map output not committed");
   const int64_t a = sl.index[b.start_reduce], e = sl.index[b.end_reduce];
   *size = e - a;
   if (sl.owner == node->conf.rank) {
@@ -2165,9 +2169,10 @@ void resolve(sux_node* node, Shuffle& sh, const sux_block_id& b, uint64_t* addr,
   }
   const int W = node->conf.world_size, me = node->conf.rank;
   const int lo = owner_lo(me, R, W), hi = owner_lo(me + 1, R, W);
-  require(sh.exchanged, SUX_ESTATE, "block " + name() + " is remote and the shuffle is not exchanged");
-  require(b.start_reduce >= lo && b.end_reduce <= hi, SUX_ENOENT,
-          "block " + name() + " is not owned by rank " + std::to_string(me));
+  if (!sh.exchanged)
+    raise(SUX_ESTATE, "block " + name() + " is remote and the shuffle is not exchanged");
+  if (!(b.start_reduce >= lo && b.end_reduce <= hi))
+    raise(SUX_ENOENT, "block " + name() + " is not owned by rank " + std::to_string(me));
   *addr = (uint64_t)(uintptr_t)(sh.recv.ptr + sl.recv_off + (a - sl.index[lo]));
 }
 }  // namespace
