@@ -754,9 +754,12 @@ __global__ __launch_bounds__(256) void k_hist4(PartDev pd, MapGroup g, uint16_t*
 //   - Record dwords enter the image with a per-lane dword rotation ((lane>>3)&3) so that the
 //     8 lanes sharing a bank row in one ds_write_b32 write 4 different banks of it.
 // ------------------------------------------------------------------------------------------
-// destination-unit words of the v6/v7 image: unit index (29 bits) | foreign head dwords << 29
+// destination-unit words of the v6/v7 image: unit index (30 bits: a launch group's output
+// up to 16 GiB) | foreign head dwords (0..3) << 30
+constexpr uint32_t kSkipShift = 30;
 constexpr uint32_t kNoUnit = 0xFFFFFFFFu;       // tail unit still partial: becomes the carry
-constexpr uint32_t kUnitMask = (1u << 29) - 1;
+constexpr uint32_t kUnitMask = (1u << kSkipShift) - 1;
+constexpr uint64_t kImageMaxBytes = (1ull << (kSkipShift + 4)) - 64;  // kNoUnit never a real unit
 
 // Diagnostic build only (-DSUX_STAMPS, tools/stamps.hip): thread 0 of workgroups < 64 records
 // s_memtime at the phase boundaries of its first 16 chunks.  No stamp executes otherwise.
@@ -940,7 +943,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter6(MapGroup g, int R, int pid
       const uint32_t full = (cd + c * W) >> 2, sp = (cd + c * W + 3) >> 2;
       const u32x4 cv = carry[p];
       for (uint32_t i = 0; i < cd; ++i) img32[4 * lb + i] = cv[i];
-      if (sp) dstu[lb] = full ? ((uint32_t)(pos[p] >> 4) | (first[p] << 29)) : kNoUnit;
+      if (sp) dstu[lb] = full ? ((uint32_t)(pos[p] >> 4) | (first[p] << kSkipShift)) : kNoUnit;
     }
 #pragma unroll
     for (uint32_t j = 0; j < NG; ++j) {
@@ -984,7 +987,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter6(MapGroup g, int R, int pid
       const uint32_t d = dstu[q];
       if (d == kNoUnit) continue;
       const u32x4 x = img[q];
-      const uint32_t skip = d >> 29;
+      const uint32_t skip = d >> kSkipShift;
       const uint64_t A = (uint64_t)(d & kUnitMask) * 16;
       if (skip == 0) {
         *reinterpret_cast<u32x4*>(out + A) = x;
@@ -1238,7 +1241,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter7(MapGroup g, int R, int pid
 #pragma unroll
       for (uint32_t i = 0; i < 3; ++i)
         if (i < cd) img32[4 * lb + i] = cv[i];
-      if (sp) dstu[lb] = full ? ((uint32_t)(pos >> 4) | (first << 29)) : kNoUnit;
+      if (sp) dstu[lb] = full ? ((uint32_t)(pos >> 4) | (first << kSkipShift)) : kNoUnit;
     }
     __syncthreads();
     SUX_STAMP(ci, 3);
@@ -1294,7 +1297,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter7(MapGroup g, int R, int pid
       const uint32_t d = dstu[q];
       if (d == kNoUnit) continue;
       const u32x4 x = img[q];
-      const uint32_t skip = d >> 29;
+      const uint32_t skip = d >> kSkipShift;
       const uint64_t A = (uint64_t)(d & kUnitMask) * 16;
       if (skip == 0) {
         *reinterpret_cast<u32x4*>(out + A) = x;
@@ -2334,7 +2337,7 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   size_t lds6 = 0;
   int c6 = 0;
   if (sv >= 6 && S == 100 && (reinterpret_cast<uintptr_t>(d_out) & 15) == 0 &&
-      g.num_records * S < (1ull << 33)) {
+      g.num_records * S < kImageMaxBytes) {
     for (int c : {1024, 512, 384, 256}) {
       if (c > s6c) continue;
       const size_t b = c == 1024 ? Sc6<100, 1024, 16>::lds_bytes(R)

@@ -226,3 +226,30 @@ def test_kernel_variant_reports_the_coresident_shape(gpu_node, tuned):
     torch.cuda.synchronize()
     assert gpu_node.kernel_variant(0) == "k_hist4" and gpu_node.kernel_variant(2) == "k_scatter7"
     gp.close()
+
+
+def test_launch_group_over_8_gib_keeps_the_image_scatter(gpu_node):
+    """One 2^27-record TeraSort map (13.4 GB; r01 fell back to k_scatter2 above 8 GiB of group
+    output, 29-bit image units).  Checked on the device without the oracle: the index is the
+    map's run offsets, and every run p equals the input records whose k_pids id is p, in input
+    order (stable) — for the first, a middle and the last partitions in full, and the runs that
+    straddle the 8 GiB output offset."""
+    n, R = 1 << 27, 200
+    gp = gpu_part(gpu_node, O.terasort_partitioner(R))
+    d = gpu_node.generate(N.GEN_TERASORT, 41, 0, n, 100)
+    out, index, _ = gpu_node.partition_maps(gp, d, 100, n, want_be=False)
+    torch.cuda.synchronize()
+    assert gpu_node.kernel_variant(2) == "k_scatter7"
+    ix = index[:R + 1]
+    assert int(ix[0]) == 0 and int(ix[R]) == n * 100 and bool((ix[1:] >= ix[:-1]).all())
+    pids = gpu_node.partition_ids(gp, d, 100).to(torch.int64)
+    cnt = torch.bincount(pids, minlength=R) * 100
+    assert torch.equal(cnt, ix[1:] - ix[:-1])
+    rows = d.view(n, 100)
+    ixh = ix.cpu().tolist()
+    over = [p for p in range(R) if ixh[p] < (8 << 30) <= ixh[p + 1]]
+    for p in sorted({0, R // 2, R - 1, *over, *(q + 1 for q in over if q + 1 < R)}):
+        want = rows[pids == p].reshape(-1)
+        assert torch.equal(out[ixh[p]:ixh[p + 1]], want), p
+    del pids, rows
+    gp.close()
