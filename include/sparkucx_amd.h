@@ -131,11 +131,12 @@ int sux_pool_stats(sux_node* node, uint64_t* allocated_bytes, uint64_t* requests
  * byte of any output: every variant is parity-tested against the CPU oracle. */
 typedef struct sux_tuning {
   int32_t hist_kernel;      /* newest K1 variant allowed: 1, 2, 3, 4                            */
-  int32_t scatter_kernel;   /* newest K3 variant allowed: 1, 2, 6, 7                            */
+  int32_t scatter_kernel;   /* newest K3 variant allowed: 1, 2, 6, 7, 8                         */
   int32_t coresident;       /* 1: in calls that keep two launch groups in flight, K3 shapes that
                                leave a K1 workgroup room on the CU (measured slower: opt-in);
                                0 or -1: not                                                     */
-  int32_t scatter_chunk;    /* k_scatter7 records per chunk: 1024, 768 (0: 768 co-resident)     */
+  int32_t scatter_chunk;    /* k_scatter7 records per chunk: 1024, 768, 512 (0: 768 co-resident,
+                               else 1024); 512 = 512-thread workgroups, two per CU at small R   */
   int32_t scatter_depth;    /* k_scatter7 chunks loaded ahead: 1, 2 (768-record chunks only)     */
   int32_t hist_stage;       /* k_hist4 records per LDS stage: 64, 128 (0: 64)                   */
   int32_t s6_chunk;         /* k_scatter6 largest records per chunk: 1024, 512, 384, 256         */

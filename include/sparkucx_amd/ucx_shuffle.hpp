@@ -117,6 +117,21 @@ class UcxShuffleConf {
     return c;
   }
 
+  // spark.shuffle.ucx.gpu.tuning.<field>: the node's kernel tuning table (0 / unset = default)
+  sux_tuning tuning() const {
+    static const char* const kFields[] = {
+        "hist_kernel", "scatter_kernel", "coresident", "scatter_chunk", "scatter_depth",
+        "hist_stage", "s6_chunk", "tiles_per_item", "small_groups", "tile_records", "onepass",
+        "varlen_kernel", "varlen_tile", "sort_max_digit_bits", "sort_gather", "sort_all_passes",
+        "hist_wgs_per_cu", "small_kernel", "small_waves"};
+    sux_tuning t;
+    std::memset(&t, 0, sizeof t);
+    int32_t* f = reinterpret_cast<int32_t*>(&t);
+    for (size_t i = 0; i < sizeof kFields / sizeof kFields[0]; ++i)
+      f[i] = std::stoi(get(ucx(std::string("gpu.tuning.") + kFields[i]), "0"));
+    return t;
+  }
+
  private:
   std::map<std::string, std::string> conf_;
 };
@@ -130,7 +145,11 @@ class UcxNode {
     sux_conf c = conf.toNative();
     if (commId) std::memcpy(c.comm_id, commId, 128);
     check(sux_node_create(&c, isDriver ? 1 : 0, &node_), "UcxNode");
+    const sux_tuning t = conf.tuning();
+    check(sux_node_set_tuning(node_, &t), "spark.shuffle.ucx.gpu.tuning");
   }
+  // device-side failures recorded by the kernels (sux_node_check)
+  void check() const { sparkucx::check(sux_node_check(node_), "device error word"); }
   ~UcxNode() { close(); }
   UcxNode(const UcxNode&) = delete;
   UcxNode& operator=(const UcxNode&) = delete;

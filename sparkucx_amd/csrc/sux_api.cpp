@@ -731,9 +731,11 @@ int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
       return false;
     };
     require(in(t->hist_kernel, {1, 2, 3, 4}), SUX_EINVAL, "hist_kernel must be 1..4");
-    require(in(t->scatter_kernel, {1, 2, 6, 7}), SUX_EINVAL, "scatter_kernel must be 1, 2, 6 or 7");
+    require(in(t->scatter_kernel, {1, 2, 6, 7, 8}), SUX_EINVAL,
+            "scatter_kernel must be 1, 2, 6, 7 or 8");
     require(t->coresident >= -1 && t->coresident <= 1, SUX_EINVAL, "coresident must be -1, 0 or 1");
-    require(in(t->scatter_chunk, {768, 1024}), SUX_EINVAL, "scatter_chunk must be 768 or 1024");
+    require(in(t->scatter_chunk, {512, 768, 1024}), SUX_EINVAL,
+            "scatter_chunk must be 512, 768 or 1024");
     require(in(t->scatter_depth, {1, 2}), SUX_EINVAL, "scatter_depth must be 1 or 2");
     require(t->scatter_depth != 2 || t->scatter_chunk == 768, SUX_EINVAL,
             "scatter_depth 2 needs scatter_chunk 768");

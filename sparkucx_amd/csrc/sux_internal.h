@@ -35,7 +35,7 @@ struct PartDev {
 // resolve_tuning).  Replaces round 1's process-wide environment overrides.
 struct Tuning {
   int hist_kernel = 4;      // newest K1 variant allowed
-  int scatter_kernel = 7;   // newest K3 variant allowed
+  int scatter_kernel = 8;   // newest K3 variant allowed
   bool coresident = false;  // K1/K3 shapes that share a CU (two launch groups in flight)
   int scatter_chunk = 1024; // k_scatter7 records per chunk: 1024 | 768
   int scatter_depth = 1;    // k_scatter7 chunks loaded ahead (768-record chunks: 1 | 2)

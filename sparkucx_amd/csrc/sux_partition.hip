@@ -1361,6 +1361,317 @@ __global__ __launch_bounds__(NW * 64) void k_scatter7(MapGroup g, int R, int pid
 }
 
 // ------------------------------------------------------------------------------------------
+// v8 scatter: v7 writing whole 128-byte lines.  v7 writes every completed 16-byte unit, so each
+// partition run of a chunk (~5 records at R = 200) starts and ends inside a line — the copy
+// pattern measured at 3.7 TB/s against 5.2+ for line-aligned runs (round-1 hbm_probe).  Here a
+// partition's region in the chunk image starts at the LINE that holds its cursor: the line's
+// earlier dwords (this workgroup's from the previous chunk, or another range's at an item start)
+// come first, the writer stores only the region's complete lines, and the rest of the last line
+// is carried to the next chunk in the registers of four "carry" threads per partition (2 units
+// each) instead of LDS.  A line holding another range's dwords (item start) is stored dword by
+// dword without them; an item's last partial line is flushed dword by dword.  The per-record
+// loop that tagged destination units (v7 phase 3) becomes one partition byte per image unit.
+// R <= 215 at C = 1024 (LDS) and 4R <= NT (carry threads).
+// ------------------------------------------------------------------------------------------
+template <uint32_t S, uint32_t C, uint32_t NW>
+struct Sc8 {
+  static constexpr uint32_t NT = NW * kWave;
+  static constexpr uint32_t W = S / 4;
+  static constexpr uint32_t RPW = C / NW;
+  static constexpr uint32_t NG = (RPW + kWave - 1) / kWave;
+  static constexpr uint32_t kUnits = (C * S + 12 + 15) / 16;
+  static constexpr uint32_t kPer = (kUnits + NT - 1) / NT;
+  static_assert(C % NW == 0 && RPW % kWave == 0 && NW % 4 == 0 && S % 4 == 0, "shape");
+  // a region: <= 31 dwords of the cursor's line + W*c dwords, in units
+  static __host__ __device__ constexpr uint32_t space(int R) {
+    return (C * S) / 16 + (17u * R + 1) / 2 + 1;
+  }
+  // img[SP] u32x4 | pinfo[R] u32x4 | recoff[C] | wcnt[R][NW] | lunit[R] | fhead[R] | lpos[R]
+  // | tmp[NW + 1] | upid[SP] u8
+  static __host__ __device__ constexpr uint32_t lds_bytes(int R) {
+    return space(R) * 16 + (uint32_t)R * 16 + C * 4 + NW * (uint32_t)R * 4 + 3u * R * 4 +
+           (NW + 1) * 4 + space(R);
+  }
+  static __host__ __device__ constexpr bool fits(int R) {
+    return R >= 1 && 4u * (uint32_t)R <= NT && lds_bytes(R) <= 160u * 1024;
+  }
+};
+
+template <uint32_t S, uint32_t C, uint32_t NW>
+__global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid_bits,
+                                                     const uint16_t* __restrict__ pids,
+                                                     const uint32_t* __restrict__ prefix,
+                                                     const uint64_t* __restrict__ base,
+                                                     uint8_t* __restrict__ out, uint32_t tpw,
+                                                     uint32_t wg_per_map) {
+  using K = Sc8<S, C, NW>;
+  constexpr uint32_t NT = K::NT, W = K::W, RPW = K::RPW, NG = K::NG, PER = K::kPer;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  const uint32_t SP = K::space(R);
+  u32x4* img = reinterpret_cast<u32x4*>(lds8);
+  uint32_t* img32 = reinterpret_cast<uint32_t*>(lds8);
+  u32x4* pinfo = img + SP;  // {lb, cd, full lines, sp}
+  uint32_t* recoff = reinterpret_cast<uint32_t*>(pinfo + R);
+  uint32_t* wcnt = recoff + C;  // [R][NW]
+  uint32_t* lunit = wcnt + NW * R;  // unit index of the line holding p's cursor
+  uint32_t* fhead = lunit + R;      // dwords of that line that belong to another range
+  uint32_t* lpos = fhead + R;       // p's cursor in dwords (flush at an item end)
+  uint32_t* tmp = lpos + R;
+  uint8_t* upid = reinterpret_cast<uint8_t*>(tmp + NW + 1);
+
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const bool owner = tid < R;
+  const uint32_t cp = (uint32_t)tid >> 2, cj = (uint32_t)tid & 3u;  // carry thread: (p, quarter)
+  const bool carrier = cp < (uint32_t)R;
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  uint32_t* out32 = reinterpret_cast<uint32_t*>(out);
+  u32x4* out4 = reinterpret_cast<u32x4*>(out);
+  const uint32_t rot = (uint32_t)(lane >> 3) & 3u;
+
+  const uint32_t nitems = g.num_maps * wg_per_map;
+  const uint32_t G = gridDim.x;
+  struct Item {
+    uint32_t map, t0;
+    uint64_t begin, end;
+  };
+  auto item_of = [&](uint32_t it) {
+    Item x;
+    x.map = it / wg_per_map;
+    x.t0 = (it - x.map * wg_per_map) * tpw;
+    const uint64_t map_begin = (uint64_t)x.map * g.records_per_map;
+    const uint64_t map_end = min(map_begin + g.records_per_map, g.num_records);
+    x.begin = min(map_begin + (uint64_t)x.t0 * g.tile_recs, map_end);
+    x.end = min(x.begin + (uint64_t)tpw * g.tile_recs, map_end);
+    return x;
+  };
+  const uint32_t it = xcd_map(blockIdx.x, G);
+  if (it >= nitems) return;
+
+  uint64_t pos = 0;  // owner: p's output cursor (bytes)
+  auto begin_item = [&](const Item& x) {
+    if (owner) {
+      pos = (base[(uint64_t)x.map * R + tid] +
+             prefix[(uint64_t)x.map * R * g.tiles_per_map + (uint64_t)tid * g.tiles_per_map + x.t0]) * S;
+      fhead[tid] = (uint32_t)(pos & 127) >> 2;  // the line's earlier dwords: another range's
+    }
+  };
+  struct Cur {
+    uint32_t it;
+    uint64_t c0, end;
+    bool valid;
+  };
+  auto first_cur = [&](uint32_t it0) {
+    Cur k;
+    k.it = it0;
+    k.valid = it0 < nitems;
+    const Item x = item_of(k.valid ? it0 : 0);
+    k.c0 = x.begin;
+    k.end = x.end;
+    return k;
+  };
+  auto next_cur = [&](const Cur& k) {
+    Cur nk = k;
+    nk.c0 = k.c0 + C;
+    if (nk.c0 >= k.end) nk = first_cur(k.it + G);
+    return nk;
+  };
+  auto issue = [&](const Cur& k, uint32_t (&pidv)[NG], u32x4 (&v)[PER]) {
+    const uint32_t n = k.valid ? (uint32_t)min<uint64_t>(C, k.end - k.c0) : 1u;
+    const uint64_t c0 = k.valid ? k.c0 : 0;
+#pragma unroll
+    for (uint32_t j = 0; j < NG; ++j) {
+      const uint32_t r = wave * RPW + j * kWave + lane;
+      pidv[j] = pids[c0 + min(r, n - 1)];
+    }
+    const uint8_t* a = g.recs + c0 * S;
+    const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(a) & 15u);
+    const u32x4* src = reinterpret_cast<const u32x4*>(a - head);
+    const uint32_t units = (head + n * S + 15) >> 4;
+#pragma unroll
+    for (uint32_t k2 = 0; k2 < PER; ++k2) v[k2] = src[min(tid + k2 * NT, units - 1)];
+  };
+
+  if (owner) {
+#pragma unroll
+    for (uint32_t w = 0; w < NW; w += 4)
+      reinterpret_cast<u32x4*>(wcnt + tid * NW)[w / 4] = u32x4{0, 0, 0, 0};
+  }
+  u32x4 cu0{0, 0, 0, 0}, cu1{0, 0, 0, 0};  // carrier: units 2cj, 2cj+1 of p's carried line
+  begin_item(item_of(it));
+  __syncthreads();
+  auto process = [&](const Cur& k, const Cur& ahead, uint32_t (&pidv)[NG], u32x4 (&v)[PER]) {
+    const uint64_t c0 = k.c0;
+    const uint32_t n = (uint32_t)min<uint64_t>(C, k.end - c0);
+    const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(g.recs + c0 * S) & 15u);
+    const uint32_t units = (head + n * S + 15) >> 4;
+    const Cur nk = next_cur(k);
+    const bool seam = nk.it != k.it, more = nk.valid;
+    // 1. stable per-wave ranks (ballot match over the pid bits)
+    uint32_t my_pid[NG], my_rank[NG];
+#pragma unroll
+    for (uint32_t j = 0; j < NG; ++j) {
+      const uint32_t r = wave * RPW + j * kWave + lane;
+      const bool valid = r < n;
+      const uint32_t pid = valid ? pidv[j] : 0u;
+      uint64_t peers = __ballot(valid);
+      for (int bb = 0; bb < pid_bits; ++bb) {
+        const bool bit = (pid >> bb) & 1u;
+        const uint64_t m = __ballot(bit);
+        peers &= bit ? m : ~m;
+      }
+      uint32_t* wc = wcnt + pid * NW + wave;
+      uint32_t r0 = 0;
+      if (valid) r0 = *wc;
+      __builtin_amdgcn_wave_barrier();
+      if (valid && (peers & lt_mask) == 0) *wc = r0 + (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+      my_pid[j] = valid ? pid : 0xFFFFFFFFu;
+      my_rank[j] = r0 + (uint32_t)__popcll(peers & lt_mask);
+    }
+    __syncthreads();
+    // 2. owners: prefix over waves, region = the cursor's line from its start + c records
+    uint32_t c = 0, full = 0, sp = 0;
+    if (owner) {
+      u32x4* row = reinterpret_cast<u32x4*>(wcnt + tid * NW);
+      u32x4 x[NW / 4];
+#pragma unroll
+      for (uint32_t q = 0; q < NW / 4; ++q) x[q] = row[q];
+#pragma unroll
+      for (uint32_t q = 0; q < NW / 4; ++q) {
+        u32x4 y;
+        y[0] = c;
+        y[1] = c + x[q][0];
+        y[2] = y[1] + x[q][1];
+        y[3] = y[2] + x[q][2];
+        c = y[3] + x[q][3];
+        row[q] = y;
+      }
+      const uint32_t cd = (uint32_t)(pos & 127) >> 2;
+      const uint32_t tot = cd + c * W;
+      full = tot >> 5;
+      sp = (tot + 3) >> 2;
+    }
+    const uint32_t incl = wave_incl_scan(sp, lane);
+    if (lane == kWave - 1) tmp[wave] = incl;
+    __syncthreads();
+    uint32_t lb = incl - sp, U = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < NW; ++w) {
+      const uint32_t t = tmp[w];
+      lb += (w < (uint32_t)wave) ? t : 0u;
+      U += t;
+    }
+    if (owner) {
+      pinfo[tid] = u32x4{lb, (uint32_t)(pos & 127) >> 2, full, sp};
+      lunit[tid] = (uint32_t)(pos >> 4) & ~7u;
+    }
+    __syncthreads();
+    // 3. carried units into the region heads, partition bytes of the image, record offsets
+    if (carrier) {
+      const u32x4 pi = pinfo[cp];
+      const uint32_t cdu = (pi[1] + 3) >> 2;  // units holding carried dwords
+      if (2 * cj < cdu) img[pi[0] + 2 * cj] = cu0;
+      if (2 * cj + 1 < cdu) img[pi[0] + 2 * cj + 1] = cu1;
+      for (uint32_t q = pi[0] + cj; q < pi[0] + pi[3]; q += 4) upid[q] = (uint8_t)cp;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < NG; ++j) {
+      const uint32_t p = my_pid[j];
+      if (p == 0xFFFFFFFFu) continue;
+      const u32x4 pi = pinfo[p];
+      const uint32_t jr = wcnt[p * NW + wave] + my_rank[j];
+      recoff[wave * RPW + j * kWave + lane] = 16 * pi[0] + 4 * pi[1] + jr * S;
+    }
+    __syncthreads();
+    // 4. records -> image (as v7: whole 16-byte units inside a record as one ds_write_b128)
+#pragma unroll
+    for (uint32_t k2 = 0; k2 < PER; ++k2) {
+      const uint32_t u = tid + k2 * NT;
+      const int32_t b0 = (int32_t)(16 * u) - (int32_t)head;
+      const uint32_t r0 = b0 >= 0 ? (uint32_t)b0 / S : 0u, off0 = (uint32_t)b0 - r0 * S;
+      if (u < units && b0 >= 0 && (uint32_t)b0 + 16 <= n * S && off0 + 16 <= S) {
+        *reinterpret_cast<u32x4a4*>(img32 + ((recoff[r0] + off0) >> 2)) = v[k2];
+      } else if (u < units) {
+#pragma unroll
+        for (uint32_t cc = 0; cc < 4; ++cc) {
+          const uint32_t q = (cc + rot) & 3u;
+          const int32_t b = (int32_t)(16 * u + 4 * q) - (int32_t)head;
+          if (b >= 0 && (uint32_t)b < n * S) {
+            const uint32_t r = (uint32_t)b / S, off = (uint32_t)b - r * S;
+            const uint32_t x = q == 0 ? v[k2][0] : q == 1 ? v[k2][1] : q == 2 ? v[k2][2] : v[k2][3];
+            img32[(recoff[r] + off) >> 2] = x;
+          }
+        }
+      }
+    }
+    // 5. the registers are free: start the loads of the next chunk
+    issue(ahead, pidv, v);
+    __syncthreads();
+    // 6. writer: the complete lines of every region, line-aligned 16-byte stores; the dwords of
+    //    another range at the head of an item's first line are skipped
+    for (uint32_t q = tid; q < U; q += NT) {
+      const uint32_t p = upid[q];
+      const u32x4 pi = pinfo[p];
+      const uint32_t kq = q - pi[0];
+      if (kq >= 8 * pi[2]) continue;
+      const uint64_t A = (uint64_t)lunit[p] + kq;
+      const u32x4 x = img[q];
+      const uint32_t f = kq < 8 ? fhead[p] : 0u;
+      if (f <= 4 * kq) {
+        out4[A] = x;
+      } else if (f < 4 * kq + 4) {
+#pragma unroll
+        for (uint32_t cc = 0; cc < 4; ++cc)
+          if (4 * kq + cc >= f) out32[4 * A + cc] = x[cc];
+      }
+    }
+    __syncthreads();
+    // 7. carries into the carrier registers, cursors advance; an item's last line is flushed
+    if (carrier) {
+      const u32x4 pi = pinfo[cp];
+      const uint32_t b = pi[0] + 8 * pi[2] + 2 * cj;
+      if (2 * cj < pi[3] - 8 * pi[2]) cu0 = img[b];
+      if (2 * cj + 1 < pi[3] - 8 * pi[2]) cu1 = img[b + 1];
+    }
+    if (owner) {
+      if (full) fhead[tid] = 0;
+      pos += (uint64_t)c * S;
+      lpos[tid] = (uint32_t)(pos >> 2);
+#pragma unroll
+      for (uint32_t w = 0; w < NW; w += 4)
+        reinterpret_cast<u32x4*>(wcnt + tid * NW)[w / 4] = u32x4{0, 0, 0, 0};
+    }
+    if (seam) {
+      __syncthreads();
+      if (carrier) {  // dwords [fhead, cursor) of the cursor's line: this range's, not yet stored
+        const uint32_t dp = lpos[cp], cdn = dp & 31u, f = fhead[cp];
+        const uint64_t L = ((uint64_t)dp & ~31ull);
+#pragma unroll
+        for (uint32_t cc = 0; cc < 8; ++cc) {
+          const uint32_t d = 8 * cj + cc;
+          const uint32_t x = cc < 4 ? cu0[cc] : cu1[cc - 4];
+          if (d >= f && d < cdn) out32[L + d] = x;
+        }
+      }
+      __syncthreads();
+      if (more) begin_item(item_of(nk.it));
+    }
+    __syncthreads();
+    return more;
+  };
+
+  uint32_t pa[NG];
+  u32x4 va[PER];
+  Cur k = first_cur(it);
+  issue(k, pa, va);
+  while (true) {
+    const Cur k1 = next_cur(k);
+    if (!process(k, k1, pa, va)) break;
+    k = k1;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // Small records (S = 16, SURVEY.md config C5: 16-byte key/value rows, 10,000 partitions).
 // A record is one aligned 16-byte unit and R is far too large for per-wave counters, so:
 //   k_hist16   persistent workgroups of 1024 threads, one tile at a time; every lane loads whole
@@ -2351,7 +2662,9 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
       }
     }
   }
-  const bool v7 = c6 == 1024 && sv >= 7 && R <= 512 &&
+  const bool v8 = c6 == 1024 && sv >= 8 && tn.scatter_chunk == 1024 &&
+                  Sc8<100, 1024, 16>::fits(R);
+  const bool v7 = !v8 && c6 == 1024 && sv >= 7 && R <= 512 &&
                   Sc7<100, 1024, 16>::lds_bytes(R) <= 160 * 1024;
   timer_begin(timer, kScatter, s);
   const bool two16 = s16 && small_two_pass_shape((uint32_t)R, S) && tn.small_kernel == 3 &&
@@ -2417,14 +2730,30 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
                          base, d_out);
     }
     e = hipGetLastError();
+  } else if (v8) {
+    timer_note(timer, kScatter, "k_scatter8");
+    uint32_t tpw = s6tpw > 0 ? (uint32_t)s6tpw
+                             : (uint32_t)std::max<uint64_t>(1, (8ull * 1024 + g.tile_recs - 1) / g.tile_recs);
+    if (tpw > g.tiles_per_map) tpw = g.tiles_per_map;
+    const uint32_t wpm = (g.tiles_per_map + tpw - 1) / tpw;
+    const dim3 grid((uint32_t)std::min<uint64_t>((uint64_t)g.num_maps * wpm, 256u));
+    const size_t lds8b = Sc8<100, 1024, 16>::lds_bytes(R);
+    allow_lds(reinterpret_cast<const void*>(&k_scatter8<100, 1024, 16>), lds8b);
+    hipLaunchKernelGGL((k_scatter8<100, 1024, 16>), grid, dim3(1024), lds8b, s, g, R, bits, pids,
+                       counts, base, d_out, tpw, wpm);
+    e = hipGetLastError();
   } else if (v7) {
     timer_note(timer, kScatter, "k_scatter7");
     uint32_t tpw = s6tpw > 0 ? (uint32_t)s6tpw
                              : (uint32_t)std::max<uint64_t>(1, (8ull * 1024 + g.tile_recs - 1) / g.tile_recs);
     if (tpw > g.tiles_per_map) tpw = g.tiles_per_map;
     const uint32_t wpm = (g.tiles_per_map + tpw - 1) / tpw;
-    // persistent: one 1024-thread workgroup per CU (LDS-bound) walks the items
-    const dim3 grid((uint32_t)std::min<uint64_t>((uint64_t)g.num_maps * wpm, 256));
+    // persistent: the workgroups the LDS allows per CU (one 1024-thread workgroup at 1024-record
+    // chunks; 512-record chunks of 512 threads fit twice at small R) walk the items
+    const uint32_t per_cu = tn.scatter_chunk == 512
+        ? std::max<uint32_t>(1, std::min<uint32_t>(2, (160u * 1024) / (uint32_t)Sc7<100, 512, 8>::lds_bytes(R)))
+        : 1u;
+    const dim3 grid((uint32_t)std::min<uint64_t>((uint64_t)g.num_maps * wpm, 256u * per_cu));
 #define SUX_S7L(CC, NWV, DV)                                                                     \
   do {                                                                                          \
     const size_t lds7 = Sc7<100, CC, NWV>::lds_bytes(R);                                        \
@@ -2432,7 +2761,8 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
     hipLaunchKernelGGL((k_scatter7<100, CC, NWV, DV>), grid, dim3(NWV * kWave), lds7, s, g, R,   \
                        bits, pids, counts, base, d_out, tpw, wpm);                               \
   } while (0)
-    if (tn.scatter_chunk == 768 && tn.scatter_depth == 2) SUX_S7L(768, 12, 2);
+    if (tn.scatter_chunk == 512) SUX_S7L(512, 8, 1);
+    else if (tn.scatter_chunk == 768 && tn.scatter_depth == 2) SUX_S7L(768, 12, 2);
     else if (tn.scatter_chunk == 768) SUX_S7L(768, 12, 1);
     else SUX_S7L(1024, 16, 1);
 #undef SUX_S7L

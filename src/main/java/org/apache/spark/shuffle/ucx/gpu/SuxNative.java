@@ -41,6 +41,16 @@ public final class SuxNative {
   public static native long setBootstrap(long node, Bootstrap bootstrap);
   public static native void releaseBootstrap(long ctx);
   public static native long[] poolStats(long node);
+  /** sux_tuning fields in header order (TUNING_FIELDS); 0 = the measured default. */
+  public static native void setTuning(long node, int[] fields);
+  public static native int[] getTuning(long node);
+  /** Throws SuxException(EHIP) when a kernel recorded a failure in the device error word. */
+  public static native void nodeCheck(long node);
+  public static final String[] TUNING_FIELDS = {
+      "hist_kernel", "scatter_kernel", "coresident", "scatter_chunk", "scatter_depth",
+      "hist_stage", "s6_chunk", "tiles_per_item", "small_groups", "tile_records", "onepass",
+      "varlen_kernel", "varlen_tile", "sort_max_digit_bits", "sort_gather", "sort_all_passes",
+      "hist_wgs_per_cu", "small_kernel", "small_waves"};
   public static native long streamCreate(long node);
   public static native void streamDestroy(long node, long stream);
 

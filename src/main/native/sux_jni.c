@@ -193,6 +193,36 @@ JNIEXPORT jlongArray JNICALL FN(poolStats)(JNIEnv* env, jclass cls, jlong node) 
   return out;
 }
 
+/* ---- kernel tuning table (sux_tuning) and the device error word ------------------------------
+ * fields[] in the header's field order (hist_kernel .. small_waves); 0 keeps the default. */
+#define SUX_TUNING_FIELDS ((int)(sizeof(sux_tuning) / sizeof(int32_t)) - 13)
+JNIEXPORT void JNICALL FN(setTuning)(JNIEnv* env, jclass cls, jlong node, jintArray fields) {
+  (void)cls;
+  sux_tuning t;
+  memset(&t, 0, sizeof t);
+  const jsize n = fields ? (*env)->GetArrayLength(env, fields) : 0;
+  if (n > SUX_TUNING_FIELDS) {
+    throw_sux(env, SUX_EINVAL, "setTuning: more fields than sux_tuning has");
+    return;
+  }
+  if (n) (*env)->GetIntArrayRegion(env, fields, 0, n, (jint*)&t);
+  failed(env, sux_node_set_tuning(NODE(node), &t), "setTuning");
+}
+
+JNIEXPORT jintArray JNICALL FN(getTuning)(JNIEnv* env, jclass cls, jlong node) {
+  (void)cls;
+  sux_tuning t;
+  if (failed(env, sux_node_get_tuning(NODE(node), &t), "getTuning")) return NULL;
+  jintArray out = (*env)->NewIntArray(env, SUX_TUNING_FIELDS);
+  if (out) (*env)->SetIntArrayRegion(env, out, 0, SUX_TUNING_FIELDS, (const jint*)&t);
+  return out;
+}
+
+JNIEXPORT void JNICALL FN(nodeCheck)(JNIEnv* env, jclass cls, jlong node) {
+  (void)cls;
+  failed(env, sux_node_check(NODE(node)), "nodeCheck");
+}
+
 /* ---- per-task-thread stream (UcxNode.getThreadLocalWorker, UcxNode.java:147-176) --------- */
 JNIEXPORT jlong JNICALL FN(streamCreate)(JNIEnv* env, jclass cls, jlong node) {
   (void)cls;

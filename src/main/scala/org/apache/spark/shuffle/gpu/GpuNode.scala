@@ -46,7 +46,17 @@ class GpuNode private (conf: SparkConf, isDriver: Boolean) extends Logging {
     if (worldSize > 1 && !isDriver) SuxNative.setBootstrap(handle0, new RpcBootstrap(conf, rank, worldSize))
     else 0L
 
+  // spark.shuffle.ucx.gpu.tuning.<field> = <int>: the node's kernel tuning table (sux_tuning);
+  // unset fields keep the measured defaults
+  locally {
+    val fields = SuxNative.TUNING_FIELDS.map(f => conf.getInt(ucx("gpu.tuning." + f), 0))
+    if (fields.exists(_ != 0)) SuxNative.setTuning(handle0, fields)
+  }
+
   def handle: Long = handle0
+
+  /** Device-side failures the kernels recorded (bounded waits that timed out). */
+  def check(): Unit = SuxNative.nodeCheck(handle0)
 
   private val streams = new ConcurrentHashMap[Long, java.lang.Long]()
   private val threadStream = ThreadLocal.withInitial[java.lang.Long](() => {

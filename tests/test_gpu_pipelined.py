@@ -140,10 +140,13 @@ TUNINGS = [
     {"scatter_chunk": 768, "hist_wgs_per_cu": 1},
     {"coresident": -1},
     {"scatter_chunk": 768, "scatter_depth": 2},
+    {"scatter_chunk": 512},
     {"scatter_chunk": 1024, "hist_stage": 128},
     {"hist_stage": 64, "hist_wgs_per_cu": 2},
     {"tiles_per_item": 1},
     {"tiles_per_item": 64},
+    {"scatter_kernel": 7},
+    {"scatter_kernel": 7, "tiles_per_item": 1},
     {"scatter_kernel": 6},
     {"scatter_kernel": 6, "s6_chunk": 384},
     {"scatter_kernel": 2, "hist_kernel": 2},
@@ -224,22 +227,24 @@ def test_kernel_variant_reports_the_coresident_shape(gpu_node, tuned):
     d = gpu_node.generate(N.GEN_TERASORT, 37, 0, 100000, 100)
     gpu_node.partition_maps_pipelined(gp, d, 100, 25000, group_records=50000)
     torch.cuda.synchronize()
-    assert gpu_node.kernel_variant(0) == "k_hist4" and gpu_node.kernel_variant(2) == "k_scatter7"
+    assert gpu_node.kernel_variant(0) == "k_hist4" and gpu_node.kernel_variant(2) == "k_scatter8"
     gp.close()
 
 
-def test_launch_group_over_8_gib_keeps_the_image_scatter(gpu_node):
+@pytest.mark.parametrize("kernel", [8, 7])
+def test_launch_group_over_8_gib_keeps_the_image_scatter(gpu_node, tuned, kernel):
     """One 2^27-record TeraSort map (13.4 GB; r01 fell back to k_scatter2 above 8 GiB of group
     output, 29-bit image units).  Checked on the device without the oracle: the index is the
     map's run offsets, and every run p equals the input records whose k_pids id is p, in input
     order (stable) — for the first, a middle and the last partitions in full, and the runs that
     straddle the 8 GiB output offset."""
+    tuned(scatter_kernel=kernel)
     n, R = 1 << 27, 200
     gp = gpu_part(gpu_node, O.terasort_partitioner(R))
     d = gpu_node.generate(N.GEN_TERASORT, 41, 0, n, 100)
     out, index, _ = gpu_node.partition_maps(gp, d, 100, n, want_be=False)
     torch.cuda.synchronize()
-    assert gpu_node.kernel_variant(2) == "k_scatter7"
+    assert gpu_node.kernel_variant(2) == f"k_scatter{kernel}"
     ix = index[:R + 1]
     assert int(ix[0]) == 0 and int(ix[R]) == n * 100 and bool((ix[1:] >= ix[:-1]).all())
     pids = gpu_node.partition_ids(gp, d, 100).to(torch.int64)
@@ -252,4 +257,29 @@ def test_launch_group_over_8_gib_keeps_the_image_scatter(gpu_node):
         want = rows[pids == p].reshape(-1)
         assert torch.equal(out[ixh[p]:ixh[p + 1]], want), p
     del pids, rows
+    gp.close()
+
+
+@pytest.mark.parametrize("R,n,rpm,tile,tpi", [
+    (200, 300000, 300000, 4096, 1),     # an item per tile: a seam every 4 chunks
+    (200, 250001, 70001, 4096, 0),      # ragged maps: items end mid-line everywhere
+    (215, 200000, 100000, 4096, 3),     # largest R of k_scatter8 (LDS)
+    (7, 100000, 50000, 4096, 2),        # few partitions: long runs, many full lines per chunk
+    (150, 90000, 90000, 1024, 1),       # short tiles: one chunk per item
+    (220, 60000, 60000, 4096, 0),       # above k_scatter8 LDS: k_scatter7
+])
+def test_line_carry_scatter_shapes(gpu_node, tuned, R, n, rpm, tile, tpi):
+    """k_scatter8 (whole-line writes, carried partial lines): item seams at every tile, runs
+    ending mid-line, a partition absent from most chunks, records skewed into few partitions."""
+    tuned(tile_records=tile, tiles_per_item=tpi)
+    recs = O.gen_zipf(42, 0, n, 1.3, 1 << 10) if R == 7 else O.gen_terasort(42, 0, n)
+    if R == 7:
+        opart = O.Partitioner(O.MURMUR3_LONG, R, 0, 8, seed=42)
+    else:
+        opart = O.terasort_partitioner(R)
+    gp = gpu_part(gpu_node, opart)
+    out, index, index_be = gpu_node.partition_maps(gp, torch.from_numpy(recs).cuda(), 100, rpm)
+    torch.cuda.synchronize()
+    expect(opart, recs, 100, rpm, out, index, index_be)
+    assert gpu_node.kernel_variant(2) == ("k_scatter8" if R <= 215 else "k_scatter7")
     gp.close()
