@@ -144,9 +144,9 @@ class UcxNode {
   UcxNode(const UcxShuffleConf& conf, bool isDriver, const uint8_t* commId = nullptr) {
     sux_conf c = conf.toNative();
     if (commId) std::memcpy(c.comm_id, commId, 128);
-    check(sux_node_create(&c, isDriver ? 1 : 0, &node_), "UcxNode");
+    sparkucx::check(sux_node_create(&c, isDriver ? 1 : 0, &node_), "UcxNode");
     const sux_tuning t = conf.tuning();
-    check(sux_node_set_tuning(node_, &t), "spark.shuffle.ucx.gpu.tuning");
+    sparkucx::check(sux_node_set_tuning(node_, &t), "spark.shuffle.ucx.gpu.tuning");
   }
   // device-side failures recorded by the kernels (sux_node_check)
   void check() const { sparkucx::check(sux_node_check(node_), "device error word"); }
