@@ -1566,13 +1566,21 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
       lunit[tid] = (uint32_t)(pos >> 4) & ~7u;
     }
     __syncthreads();
-    // 3. carried units into the region heads, partition bytes of the image, record offsets
+    // 3. carried units into the region heads, record offsets, and the partition byte of every
+    //    image unit — written by whoever holds the unit's first dword (a carrier for the
+    //    carried head, else the record it starts in), so a hot partition's thousands of units
+    //    are tagged by its records, not by its four carriers
     if (carrier) {
       const u32x4 pi = pinfo[cp];
-      const uint32_t cdu = (pi[1] + 3) >> 2;  // units holding carried dwords
-      if (2 * cj < cdu) img[pi[0] + 2 * cj] = cu0;
-      if (2 * cj + 1 < cdu) img[pi[0] + 2 * cj + 1] = cu1;
-      for (uint32_t q = pi[0] + cj; q < pi[0] + pi[3]; q += 4) upid[q] = (uint8_t)cp;
+      const uint32_t cdu = (pi[1] + 3) >> 2;  // units starting in carried dwords
+      if (2 * cj < cdu) {
+        img[pi[0] + 2 * cj] = cu0;
+        upid[pi[0] + 2 * cj] = (uint8_t)cp;
+      }
+      if (2 * cj + 1 < cdu) {
+        img[pi[0] + 2 * cj + 1] = cu1;
+        upid[pi[0] + 2 * cj + 1] = (uint8_t)cp;
+      }
     }
 #pragma unroll
     for (uint32_t j = 0; j < NG; ++j) {
@@ -1581,6 +1589,11 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
       const u32x4 pi = pinfo[p];
       const uint32_t jr = wcnt[p * NW + wave] + my_rank[j];
       recoff[wave * RPW + j * kWave + lane] = 16 * pi[0] + 4 * pi[1] + jr * S;
+      const uint32_t d0 = pi[1] + jr * W;  // the record's first dword in the region
+      const uint32_t k0 = (d0 + 3) >> 2, k1 = (d0 + W + 3) >> 2;
+#pragma unroll
+      for (uint32_t t = 0; t < (W + 3) / 4 + 1; ++t)
+        if (k0 + t < k1) upid[pi[0] + k0 + t] = (uint8_t)p;
     }
     __syncthreads();
     // 4. records -> image (as v7: whole 16-byte units inside a record as one ds_write_b128)
@@ -2732,8 +2745,14 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
     e = hipGetLastError();
   } else if (v8) {
     timer_note(timer, kScatter, "k_scatter8");
+    // work items of ~two per workgroup: every item seam costs a partial-line flush and a first
+    // line with another range's dwords (profiles/r02_sweeps/r02_k3_c: 2 -> 16 tiles per item
+    // took the scatter from 45.9 to 43.4 ms per 100 GB), but fewer items than workgroups idle CUs
+    const uint64_t total = (uint64_t)g.num_maps * g.tiles_per_map;
     uint32_t tpw = s6tpw > 0 ? (uint32_t)s6tpw
-                             : (uint32_t)std::max<uint64_t>(1, (8ull * 1024 + g.tile_recs - 1) / g.tile_recs);
+                             : (uint32_t)std::max<uint64_t>(
+                                   std::max<uint64_t>(1, (8ull * 1024 + g.tile_recs - 1) / g.tile_recs),
+                                   total / 512);
     if (tpw > g.tiles_per_map) tpw = g.tiles_per_map;
     const uint32_t wpm = (g.tiles_per_map + tpw - 1) / tpw;
     const dim3 grid((uint32_t)std::min<uint64_t>((uint64_t)g.num_maps * wpm, 256u));
