@@ -2451,6 +2451,11 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
   pd.key_len = 16;
   pd.ascending = 1;
   sux::LayoutDesc lay{1, 16};
+  // digit passes: the turn-taking small-record scatter for short sorts (few tiles: 5 M TeraSort
+  // records 1.53 vs 1.69 ms), the sorted-chunk one for long ones (32 Mi int64 rows 2.55 vs
+  // 2.67 ms; profiles/r02_v14/sort_ab.txt) unless the node's tuning names one
+  sux::Tuning sort_tn = resolve_tuning(node->tuning, false);
+  if (node->tuning.small_kernel == 0) sort_tn.small_kernel = n <= (8ull << 20) ? 1 : 2;
   // the key occupies bits [128 - bits, 128) of the big-endian pair; least significant digit first
   for (int sh = 128 - bits; sh < 128; sh += digit) {
     if (!run_all && !span_varies(span, sh, sh + digit)) continue;  // identity pass
@@ -2458,8 +2463,7 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
     P.g.recs = pa;
     P.g.err = node->d_err;
     hip_check(sux::launch_partition_group(pd, P.g, lay, pb, index, nullptr, nullptr,
-                                          ws + P.part_off, P.ws, nullptr,
-                                          resolve_tuning(node->tuning, false), &node->timer, s),
+                                          ws + P.part_off, P.ws, nullptr, sort_tn, &node->timer, s),
               "sort digit pass");
     std::swap(pa, pb);
   }
