@@ -415,6 +415,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="terasort", choices=sorted(WORKLOADS))
     ap.add_argument("--records", type=int, default=0, help="records per GPU (0 = workload default)")
+    ap.add_argument("--partitions", type=int, default=0,
+                    help="reduce partitions R (0 = the workload's; sweeps only)")
     ap.add_argument("--map-records", type=int, default=1 << 20, help="records per map batch")
     ap.add_argument("--group-maps", type=int, default=0,
                     help="map batches per kernel launch group (0: ~3.4 GB of input per group — "
@@ -470,6 +472,12 @@ def main():
                     help="test mode (N>1): check every received block of every group against "
                          "the CPU oracle; timing is then not a benchmark")
     args = ap.parse_args()
+    # stdout carries exactly one JSON line: RCCL and the HIP runtime print banners from C code,
+    # so file descriptor 1 goes to stderr for the whole run and the result is written to a
+    # duplicate of the original stdout
+    result_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -494,6 +502,7 @@ def main():
         args.transport = "rccl"
 
     rs, R, gen, kind, key_len, n1, nN = WORKLOADS[args.workload]
+    R = args.partitions or R
     n = args.records or (n1 if world == 1 else nN)
     rpm, gm = args.map_records, args.group_maps
     if gm <= 0:
@@ -838,7 +847,7 @@ def main():
     if rank == 0 and not pipelined and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        os.write(result_fd, (json.dumps(result) + "\n").encode())
     node.close()
     if world > 1:
         dist.destroy_process_group()

@@ -112,6 +112,9 @@ struct LayoutDesc {
   uint32_t rec_size;
 };
 
+// CUs a stream may use: its CU mask's population, or every CU of the device (sux_onepass.hip).
+int stream_cus(hipStream_t s);
+
 // One-pass map side (sux_onepass.hip): fixed 100-byte records, map batch held on chip.
 uint64_t onepass_sync_bytes(uint32_t R);
 bool onepass_eligible(const PartDev& pd, const MapGroup& g, int world, const void* d_out,

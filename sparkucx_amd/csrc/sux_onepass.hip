@@ -550,6 +550,8 @@ using onepass::Shape;
 constexpr uint32_t kOpS = 100, kOpNW = 4, kOpWgPerCu = 2, kOpMaxWg = 512;
 constexpr int kOpMinW = (int)(kOpWgPerCu * kOpNW / 4);
 
+}  // namespace
+
 int stream_cus(hipStream_t s) {
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
@@ -563,7 +565,6 @@ int stream_cus(hipStream_t s) {
   }
   return cus;
 }
-}  // namespace
 
 uint64_t onepass_sync_bytes(uint32_t R) {
   const uint64_t words = onepass::kSyncWords + (uint64_t)onepass::kCntBufs * kOpMaxWg * R +

@@ -1402,8 +1402,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
                                                      const uint16_t* __restrict__ pids,
                                                      const uint32_t* __restrict__ prefix,
                                                      const uint64_t* __restrict__ base,
-                                                     uint8_t* __restrict__ out, uint32_t tpw,
-                                                     uint32_t wg_per_map) {
+                                                     uint8_t* __restrict__ out) {
   using K = Sc8<S, C, NW>;
   constexpr uint32_t NT = K::NT, W = K::W, RPW = K::RPW, NG = K::NG, PER = K::kPer;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
@@ -1428,24 +1427,28 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
   u32x4* out4 = reinterpret_cast<u32x4*>(out);
   const uint32_t rot = (uint32_t)(lane >> 3) & 3u;
 
-  const uint32_t nitems = g.num_maps * wg_per_map;
-  const uint32_t G = gridDim.x;
+  // Workgroup b walks ONE contiguous range of the launch's tiles, [T r / G, T (r+1) / G) with
+  // r = xcd_map(b) (an XCD's workgroups get neighbouring ranges): balanced to one tile whatever
+  // the grid (a CU-masked stream's 224 CUs as well as 256), cut into items at map boundaries.
+  const uint32_t T = g.num_maps * g.tiles_per_map, G = gridDim.x;
+  const uint32_t rr = xcd_map(blockIdx.x, G);
+  const uint32_t t_lo = (uint32_t)((uint64_t)T * rr / G), t_hi = (uint32_t)((uint64_t)T * (rr + 1) / G);
+  if (t_lo >= t_hi) return;
   struct Item {
     uint32_t map, t0;
     uint64_t begin, end;
   };
-  auto item_of = [&](uint32_t it) {
+  auto item_of = [&](uint32_t t) {  // the item starting at global tile t
     Item x;
-    x.map = it / wg_per_map;
-    x.t0 = (it - x.map * wg_per_map) * tpw;
+    x.map = t / g.tiles_per_map;
+    x.t0 = t - x.map * g.tiles_per_map;
+    const uint32_t t_end = min(t_hi, (x.map + 1) * g.tiles_per_map);
     const uint64_t map_begin = (uint64_t)x.map * g.records_per_map;
     const uint64_t map_end = min(map_begin + g.records_per_map, g.num_records);
     x.begin = min(map_begin + (uint64_t)x.t0 * g.tile_recs, map_end);
-    x.end = min(x.begin + (uint64_t)tpw * g.tile_recs, map_end);
+    x.end = min(map_begin + (uint64_t)(t_end - x.map * g.tiles_per_map) * g.tile_recs, map_end);
     return x;
   };
-  const uint32_t it = xcd_map(blockIdx.x, G);
-  if (it >= nitems) return;
 
   uint64_t pos = 0;  // owner: p's output cursor (bytes)
   auto begin_item = [&](const Item& x) {
@@ -1456,15 +1459,15 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
     }
   };
   struct Cur {
-    uint32_t it;
+    uint32_t it;  // global tile the chunk's item starts at
     uint64_t c0, end;
     bool valid;
   };
-  auto first_cur = [&](uint32_t it0) {
+  auto first_cur = [&](uint32_t t) {
     Cur k;
-    k.it = it0;
-    k.valid = it0 < nitems;
-    const Item x = item_of(k.valid ? it0 : 0);
+    k.it = t;
+    k.valid = t < t_hi;
+    const Item x = item_of(k.valid ? t : t_lo);
     k.c0 = x.begin;
     k.end = x.end;
     return k;
@@ -1472,12 +1475,15 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
   auto next_cur = [&](const Cur& k) {
     Cur nk = k;
     nk.c0 = k.c0 + C;
-    if (nk.c0 >= k.end) nk = first_cur(k.it + G);
+    if (nk.c0 >= k.end) {  // the item ends at its map's end or at the range's end
+      const uint32_t m = k.it / g.tiles_per_map;
+      nk = first_cur(min(t_hi, (m + 1) * g.tiles_per_map));
+    }
     return nk;
   };
   auto issue = [&](const Cur& k, uint32_t (&pidv)[NG], u32x4 (&v)[PER]) {
-    const uint32_t n = k.valid ? (uint32_t)min<uint64_t>(C, k.end - k.c0) : 1u;
-    const uint64_t c0 = k.valid ? k.c0 : 0;
+    const uint32_t n = k.valid && k.end > k.c0 ? (uint32_t)min<uint64_t>(C, k.end - k.c0) : 1u;
+    const uint64_t c0 = k.valid && k.end > k.c0 ? k.c0 : 0;
 #pragma unroll
     for (uint32_t j = 0; j < NG; ++j) {
       const uint32_t r = wave * RPW + j * kWave + lane;
@@ -1497,7 +1503,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
       reinterpret_cast<u32x4*>(wcnt + tid * NW)[w / 4] = u32x4{0, 0, 0, 0};
   }
   u32x4 cu0{0, 0, 0, 0}, cu1{0, 0, 0, 0};  // carrier: units 2cj, 2cj+1 of p's carried line
-  begin_item(item_of(it));
+  begin_item(item_of(t_lo));
   __syncthreads();
   auto process = [&](const Cur& k, const Cur& ahead, uint32_t (&pidv)[NG], u32x4 (&v)[PER]) {
     const uint64_t c0 = k.c0;
@@ -1675,7 +1681,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
 
   uint32_t pa[NG];
   u32x4 va[PER];
-  Cur k = first_cur(it);
+  Cur k = first_cur(t_lo);
   issue(k, pa, va);
   while (true) {
     const Cur k1 = next_cur(k);
@@ -2506,6 +2512,10 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
                                   hipStream_t s) {
   const int R = pd.R;
   const uint32_t S = g.rec_size;
+  // persistent grids are sized to the CUs the stream may use (a CU-masked stream at N > 1):
+  // with static work items, workgroups beyond the resident ones would start only after a
+  // resident one finished ALL its items
+  const uint32_t ncu = (uint32_t)std::max(1, stream_cus(s));
   // one pass (sux_onepass.hip) whenever a map batch fits on chip: every record read once
   uint32_t op_grid = 0, op_cs = 0;
   if (tn.onepass && ws.op_bytes && onepass_eligible(pd, g, lay.world, d_out, d_peer_bytes, s, &op_grid, &op_cs)) {
@@ -2547,7 +2557,7 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   if (hist == 16) {
     const size_t lds = (size_t)R * 4;
     const int kw = (pd.key_len + 3) / 4;
-    const dim3 gridp(std::min<uint32_t>(total_tiles, 256u * std::max<uint32_t>(1, (160u * 1024) / (uint32_t)lds)));
+    const dim3 gridp(std::min<uint32_t>(total_tiles, ncu * std::max<uint32_t>(1, (160u * 1024) / (uint32_t)lds)));
 #define SUX_H16(KW)                                                                        \
   do {                                                                                     \
     allow_lds(reinterpret_cast<const void*>(&k_hist16<KW>), lds);                          \
@@ -2569,7 +2579,7 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
     const size_t lds = Hs4<100, CHV>::lds_bytes(R, tab);                                           \
     uint32_t per_cu = std::max<uint32_t>(1, (160u * 1024) / (uint32_t)lds);                        \
     if (tn.hist_wgs_per_cu > 0) per_cu = std::min<uint32_t>(per_cu, (uint32_t)tn.hist_wgs_per_cu); \
-    const dim3 gridp(std::min<uint32_t>(total_tiles, 256u * per_cu));                              \
+    const dim3 gridp(std::min<uint32_t>(total_tiles, ncu * per_cu));                              \
     if (tab) {                                                                                     \
       allow_lds(reinterpret_cast<const void*>(&k_hist4<100, CHV, KW, true>), lds);                \
       hipLaunchKernelGGL((k_hist4<100, CHV, KW, true>), gridp, dim3(256), lds, s, pd, g, pids,     \
@@ -2694,9 +2704,9 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
 #define SUX_B16(NWV)                                                                             \
   do {                                                                                           \
     allow_lds(reinterpret_cast<const void*>(&k_bucket16a<NWV>), B16a<NWV>::lds_bytes());         \
-    hipLaunchKernelGGL((k_bucket16a<NWV>), dim3(std::min<uint32_t>(total_tiles, 256u * (16 / NWV))), \
+    hipLaunchKernelGGL((k_bucket16a<NWV>), dim3(std::min<uint32_t>(total_tiles, ncu * (16 / NWV))), \
                        dim3(NWV * kWave), B16a<NWV>::lds_bytes(), s, g, R, pids, counts, base, tmp); \
-    const dim3 gridb(std::min<uint32_t>(items, 256u * (16 / NWV)));                              \
+    const dim3 gridb(std::min<uint32_t>(items, ncu * (16 / NWV)));                              \
     if (kw <= 1) SUX_B16B(1, NWV);                                                               \
     else if (kw == 2) SUX_B16B(2, NWV);                                                          \
     else if (kw == 3) SUX_B16B(3, NWV);                                                          \
@@ -2717,7 +2727,7 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
     timer_note(timer, kScatter, "k_scatter16s");
     const size_t lds = Sc16s::lds_bytes(R);
     allow_lds(reinterpret_cast<const void*>(&k_scatter16s), lds);
-    const dim3 grid(std::min<uint32_t>(total_tiles, 256u));  // one LDS-bound workgroup per CU
+    const dim3 grid(std::min<uint32_t>(total_tiles, ncu));  // one LDS-bound workgroup per CU
     hipLaunchKernelGGL(k_scatter16s, grid, dim3(1024), lds, s, g, R, bits, pids, counts, base,
                        d_out);
     e = hipGetLastError();
@@ -2725,7 +2735,7 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
     timer_note(timer, kScatter, "k_scatter16b");
     const size_t lds = (size_t)R * 4;
     const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(2, (160u * 1024) / (uint32_t)lds));
-    const dim3 grid(std::min<uint32_t>(total_tiles, 256u * per_cu));
+    const dim3 grid(std::min<uint32_t>(total_tiles, ncu * per_cu));
     const int gb = tn.small_groups;  // groups per turn (1 = k_scatter16)
     if (gb == 2 || gb == 4) {
       const void* kf = gb == 2 ? reinterpret_cast<const void*>(&k_scatter16b<16, 2>)
@@ -2745,21 +2755,12 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
     e = hipGetLastError();
   } else if (v8) {
     timer_note(timer, kScatter, "k_scatter8");
-    // work items of ~two per workgroup: every item seam costs a partial-line flush and a first
-    // line with another range's dwords (profiles/r02_sweeps/r02_k3_c: 2 -> 16 tiles per item
-    // took the scatter from 45.9 to 43.4 ms per 100 GB), but fewer items than workgroups idle CUs
-    const uint64_t total = (uint64_t)g.num_maps * g.tiles_per_map;
-    uint32_t tpw = s6tpw > 0 ? (uint32_t)s6tpw
-                             : (uint32_t)std::max<uint64_t>(
-                                   std::max<uint64_t>(1, (8ull * 1024 + g.tile_recs - 1) / g.tile_recs),
-                                   total / 512);
-    if (tpw > g.tiles_per_map) tpw = g.tiles_per_map;
-    const uint32_t wpm = (g.tiles_per_map + tpw - 1) / tpw;
-    const dim3 grid((uint32_t)std::min<uint64_t>((uint64_t)g.num_maps * wpm, 256u));
+    // one contiguous, balanced tile range per workgroup (k_scatter8), one workgroup per CU
+    const dim3 grid(std::min<uint32_t>(g.num_maps * g.tiles_per_map, ncu));
     const size_t lds8b = Sc8<100, 1024, 16>::lds_bytes(R);
     allow_lds(reinterpret_cast<const void*>(&k_scatter8<100, 1024, 16>), lds8b);
     hipLaunchKernelGGL((k_scatter8<100, 1024, 16>), grid, dim3(1024), lds8b, s, g, R, bits, pids,
-                       counts, base, d_out, tpw, wpm);
+                       counts, base, d_out);
     e = hipGetLastError();
   } else if (v7) {
     timer_note(timer, kScatter, "k_scatter7");
@@ -2772,7 +2773,7 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
     const uint32_t per_cu = tn.scatter_chunk == 512
         ? std::max<uint32_t>(1, std::min<uint32_t>(2, (160u * 1024) / (uint32_t)Sc7<100, 512, 8>::lds_bytes(R)))
         : 1u;
-    const dim3 grid((uint32_t)std::min<uint64_t>((uint64_t)g.num_maps * wpm, 256u * per_cu));
+    const dim3 grid((uint32_t)std::min<uint64_t>((uint64_t)g.num_maps * wpm, ncu * per_cu));
 #define SUX_S7L(CC, NWV, DV)                                                                     \
   do {                                                                                          \
     const size_t lds7 = Sc7<100, CC, NWV>::lds_bytes(R);                                        \
