@@ -1505,7 +1505,9 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
   u32x4 cu0{0, 0, 0, 0}, cu1{0, 0, 0, 0};  // carrier: units 2cj, 2cj+1 of p's carried line
   begin_item(item_of(t_lo));
   __syncthreads();
+  [[maybe_unused]] uint32_t ci = 0;  // chunk counter for the diagnostic stamps
   auto process = [&](const Cur& k, const Cur& ahead, uint32_t (&pidv)[NG], u32x4 (&v)[PER]) {
+    SUX_STAMP(ci, 0);
     const uint64_t c0 = k.c0;
     const uint32_t n = (uint32_t)min<uint64_t>(C, k.end - c0);
     const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(g.recs + c0 * S) & 15u);
@@ -1535,6 +1537,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
       my_rank[j] = r0 + (uint32_t)__popcll(peers & lt_mask);
     }
     __syncthreads();
+    SUX_STAMP(ci, 1);
     // 2. owners: prefix over waves, region = the cursor's line from its start + c records
     uint32_t c = 0, full = 0, sp = 0;
     if (owner) {
@@ -1560,6 +1563,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
     const uint32_t incl = wave_incl_scan(sp, lane);
     if (lane == kWave - 1) tmp[wave] = incl;
     __syncthreads();
+    SUX_STAMP(ci, 2);
     uint32_t lb = incl - sp, U = 0;
 #pragma unroll
     for (uint32_t w = 0; w < NW; ++w) {
@@ -1572,6 +1576,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
       lunit[tid] = (uint32_t)(pos >> 4) & ~7u;
     }
     __syncthreads();
+    SUX_STAMP(ci, 3);
     // 3. carried units into the region heads, record offsets, and the partition byte of every
     //    image unit — written by whoever holds the unit's first dword (a carrier for the
     //    carried head, else the record it starts in), so a hot partition's thousands of units
@@ -1602,6 +1607,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
         if (k0 + t < k1) upid[pi[0] + k0 + t] = (uint8_t)p;
     }
     __syncthreads();
+    SUX_STAMP(ci, 4);
     // 4. records -> image (as v7: whole 16-byte units inside a record as one ds_write_b128)
 #pragma unroll
     for (uint32_t k2 = 0; k2 < PER; ++k2) {
@@ -1626,6 +1632,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
     // 5. the registers are free: start the loads of the next chunk
     issue(ahead, pidv, v);
     __syncthreads();
+    SUX_STAMP(ci, 5);
     // 6. writer: the complete lines of every region, line-aligned 16-byte stores; the dwords of
     //    another range at the head of an item's first line are skipped
     for (uint32_t q = tid; q < U; q += NT) {
@@ -1645,6 +1652,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
       }
     }
     __syncthreads();
+    SUX_STAMP(ci, 6);
     // 7. carries into the carrier registers, cursors advance; an item's last line is flushed
     if (carrier) {
       const u32x4 pi = pinfo[cp];
@@ -1676,6 +1684,8 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
       if (more) begin_item(item_of(nk.it));
     }
     __syncthreads();
+    SUX_STAMP(ci, 7);
+    ++ci;
     return more;
   };
 

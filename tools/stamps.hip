@@ -1,11 +1,12 @@
-// stamps.hip — per-phase cycle timeline of the v6 scatter (diagnostic build, gfx950).
+// stamps.hip — per-phase cycle timeline of the default scatter (v8 since round 2; diagnostic
+// build, gfx950).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I sparkucx_amd/csrc \
 //          -o tools/stamps tools/stamps.hip
 // Runs the map side (hist + scans + scatter) on 32 maps x 1 Mi x 100-B random records with the
 // Spark SQL murmur3 partitioner (R=200), then prints, for the first 64 scatter workgroups and
 // their chunks 1..15, the mean s_memtime cycles of each phase of the chunk loop:
-//   0-1 rank   1-2 prefix+lbase   2-3 scan   3-4 offsets/dstu   4-5 image fill+issue+barrier
-//   5-6 write-out   6-7 carries   7-0' loop back
+//   v8: 0-1 rank   1-2 prefix+region scan   2-3 region table   3-4 carries in + offsets + unit
+//   tags   4-5 image fill+issue   5-6 write-out (whole lines)   6-7 carries out   7-0' loop back
 #define SUX_STAMPS 1
 #include "../sparkucx_amd/csrc/sux_partition.hip"
 
@@ -16,6 +17,15 @@ namespace sux {
 struct Timer {};
 void timer_begin(Timer*, int, hipStream_t) {}
 void timer_end(Timer*, int, hipStream_t) {}
+void timer_note(Timer*, int, const char*) {}
+int stream_cus(hipStream_t) { return 256; }
+uint64_t onepass_sync_bytes(uint32_t) { return 0; }  // the one-pass path is not built here
+bool onepass_eligible(const PartDev&, const MapGroup&, int, const void*, const uint64_t*,
+                      hipStream_t, uint32_t*, uint32_t*) { return false; }
+hipError_t launch_onepass(const PartDev&, const MapGroup&, uint8_t*, int64_t*, uint8_t*,
+                          uint16_t*, uint8_t*, uint32_t, uint32_t, hipStream_t) {
+  return hipSuccess;
+}
 }  // namespace sux
 
 #define CK(x)                                                                    \
@@ -60,7 +70,8 @@ int main() {
   g.num_records = n;
   g.num_maps = maps;
   g.rec_size = S;
-  g.tile_recs = choose_tile_recs(R, S, rpm);
+  const Tuning tn{};
+  g.tile_recs = choose_tile_recs(R, S, rpm, tn);
   g.tiles_per_map = (uint32_t)((rpm + g.tile_recs - 1) / g.tile_recs);
   Workspace w = workspace_layout(R, S, rpm, n, g.tile_recs, true);
   CK(hipMalloc(&ws, w.total));
@@ -70,7 +81,7 @@ int main() {
   CK(hipEventCreate(&e1));
   for (int rep = 0; rep < 4; ++rep) {
     CK(hipEventRecord(e0, 0));
-    CK(launch_partition_group(pd, g, lay, out, idx, ibe, nullptr, ws, w, nullptr, nullptr, 0));
+    CK(launch_partition_group(pd, g, lay, out, idx, ibe, nullptr, ws, w, nullptr, tn, nullptr, 0));
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float ms;
@@ -90,8 +101,8 @@ int main() {
       acc[7] += (double)(tn[0] - t[7]);
       ++cnt;
     }
-  const char* names[8] = {"rank", "prefix", "scan", "offsets", "fill+issue", "write-out",
-                          "carries", "loop"};
+  const char* names[8] = {"rank", "prefix+scan", "region tbl", "tags+offs", "fill+issue",
+                          "write-out", "carries", "loop"};
   double tot = 0;
   for (int k = 0; k < 8; ++k) tot += acc[k] / cnt;
   printf("chunks sampled: %d, mean cycles per chunk %.0f\n", cnt, tot);
