@@ -186,6 +186,29 @@ int main() {
   }
 
   manager.stop();
+
+  // spark.shuffle.ucx.gpu.tuning.<field> reaches the node's tuning table; a value outside a
+  // field's set is rejected when the node starts
+  {
+    UcxShuffleConf tc(std::map<std::string, std::string>{
+        {"spark.shuffle.ucx.gpu.tuning.scatter_kernel", "7"},
+        {"spark.shuffle.ucx.gpu.tuning.small_kernel", "3"}});
+    UcxNode node(tc, /*isDriver=*/false);
+    sux_tuning t;
+    EXPECT(sux_node_get_tuning(node.native(), &t) == SUX_OK && t.scatter_kernel == 7 &&
+               t.small_kernel == 3 && t.hist_kernel == 0,
+           "tuning keys reach the node");
+    node.check();  // nothing ran: the device error word is clear
+    bool threw = false;
+    try {
+      UcxNode bad(UcxShuffleConf(std::map<std::string, std::string>{
+                      {"spark.shuffle.ucx.gpu.tuning.scatter_chunk", "333"}}),
+                  false);
+    } catch (const UcxException& e) {
+      threw = e.code() == SUX_EINVAL;
+    }
+    EXPECT(threw, "an out-of-set tuning value is EINVAL");
+  }
   if (failures) {
     fprintf(stderr, "%d failure(s)\n", failures);
     return 1;
