@@ -146,7 +146,14 @@ class UcxNode {
     if (commId) std::memcpy(c.comm_id, commId, 128);
     sparkucx::check(sux_node_create(&c, isDriver ? 1 : 0, &node_), "UcxNode");
     const sux_tuning t = conf.tuning();
-    sparkucx::check(sux_node_set_tuning(node_, &t), "spark.shuffle.ucx.gpu.tuning");
+    const int rc = sux_node_set_tuning(node_, &t);
+    if (rc != SUX_OK) {  // the constructor throws: no destructor will release the node
+      char msg[512];
+      sux_last_error(msg, sizeof msg);
+      sux_node_destroy(node_);
+      node_ = nullptr;
+      throw UcxException(rc, std::string("spark.shuffle.ucx.gpu.tuning: ") + msg);
+    }
   }
   // device-side failures recorded by the kernels (sux_node_check)
   void check() const { sparkucx::check(sux_node_check(node_), "device error word"); }
