@@ -372,12 +372,20 @@ def self_check(node, part, data, out, index, n: int, rs: int, rpm: int, R: int,
         raise RuntimeError("self-check: index tables are not each map's run offsets")
     for r0 in range(0, n, group_recs):
         r1 = min(n, r0 + group_recs)
-        for a, b in ((data, out),):
-            wa = a[r0 * rs:r1 * rs].view(torch.int32).to(torch.int64)
-            wb = b[r0 * rs:r1 * rs].view(torch.int32).to(torch.int64)
-            if int(wa.sum()) != int(wb.sum()) or int((wa * wa).sum()) != int((wb * wb).sum()):
-                raise RuntimeError(f"self-check: records [{r0}, {r1}) are not a permutation")
-            del wa, wb
+        # the multiset of a launch group's 4-byte words, summed in bounded slices (int64 copies
+        # of a whole 13 GB group would not fit beside the data)
+        sa = [0, 0]
+        sb = [0, 0]
+        step = 1 << 28
+        for w0 in range(r0 * rs // 4, r1 * rs // 4, step):
+            w1 = min(r1 * rs // 4, w0 + step)
+            for src, acc in ((data, sa), (out, sb)):
+                w = src.view(torch.int32)[w0:w1].to(torch.int64)
+                acc[0] += int(w.sum())
+                acc[1] += int((w * w).sum())
+                del w
+        if sa[0] != sb[0] or sa[1] % (1 << 64) != sb[1] % (1 << 64):
+            raise RuntimeError(f"self-check: records [{r0}, {r1}) are not a permutation")
         pid = node.partition_ids(part, out[r0 * rs:r1 * rs], rs).to(torch.int64)
         m0 = r0 // rpm
         for m in range(m0, -(-r1 // rpm)):

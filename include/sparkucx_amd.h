@@ -153,7 +153,9 @@ typedef struct sux_tuning {
   int32_t small_kernel;     /* 16-byte records, R > 1024: 1 turn-taking scatter, 2 sorted chunks,
                                3 two passes through bucket order (R <= 16384)                    */
   int32_t small_waves;      /* two-pass small-record kernels: waves per workgroup, 8 or 16      */
-  int32_t reserved[13];
+  int32_t scatter_order;    /* k_scatter8 tiles: 1 one contiguous range per workgroup (0), 2
+                               blocks dealt round robin among an XCD's workgroups (slower)     */
+  int32_t reserved[12];
 } sux_tuning;
 int sux_node_set_tuning(sux_node* node, const sux_tuning* tuning);
 /* Waits for the device, then reports (and clears) failures the kernels recorded in the node's

@@ -529,6 +529,7 @@ sux::Tuning resolve_tuning(const sux_tuning& t, bool pipelined) {
   r.varlen_tile = t.varlen_tile;
   r.small_kernel = t.small_kernel ? t.small_kernel : kDefaultSmallKernel;
   if (t.small_waves) r.small_waves = t.small_waves;
+  r.scatter_order = t.scatter_order;
   return r;
 }
 
@@ -744,6 +745,7 @@ int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
             "hist_wgs_per_cu must be 0..8");
     require(in(t->small_kernel, {1, 2, 3}), SUX_EINVAL, "small_kernel must be 1, 2 or 3");
     require(in(t->small_waves, {8, 16}), SUX_EINVAL, "small_waves must be 8 or 16");
+    require(in(t->scatter_order, {1, 2}), SUX_EINVAL, "scatter_order must be 1 or 2");
     require(in(t->s6_chunk, {256, 384, 512, 1024}), SUX_EINVAL, "s6_chunk must be 256..1024");
     require(t->tiles_per_item >= 0 && t->tiles_per_item <= 4096, SUX_EINVAL,
             "tiles_per_item must be 0..4096");

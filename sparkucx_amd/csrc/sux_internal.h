@@ -44,6 +44,7 @@ struct Tuning {
   int small_kernel = 0;     // 16-byte records, R > 1024: 1 turn-taking k_scatter16b, 2 sorted
                             // chunks, 3 two passes through bucket order (needs the temp copy)
   int small_waves = 8;      // two-pass small-record kernels: waves per workgroup (8 | 16)
+  int scatter_order = 0;    // k_scatter8 tile order: 1 contiguous ranges, 2 block-cyclic per XCD
   int s6_chunk = 1024;      // k_scatter6 largest chunk
   int tiles_per_item = 0;   // k_scatter6/7 tiles per work item (0: 8 chunks' worth)
   int small_groups = 4;     // k_scatter16b record groups per turn: 1 | 2 | 4

@@ -1402,7 +1402,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
                                                      const uint16_t* __restrict__ pids,
                                                      const uint32_t* __restrict__ prefix,
                                                      const uint64_t* __restrict__ base,
-                                                     uint8_t* __restrict__ out) {
+                                                     uint8_t* __restrict__ out, uint32_t cyc) {
   using K = Sc8<S, C, NW>;
   constexpr uint32_t NT = K::NT, W = K::W, RPW = K::RPW, NG = K::NG, PER = K::kPer;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
@@ -1430,19 +1430,41 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
   // Workgroup b walks ONE contiguous range of the launch's tiles, [T r / G, T (r+1) / G) with
   // r = xcd_map(b) (an XCD's workgroups get neighbouring ranges): balanced to one tile whatever
   // the grid (a CU-masked stream's 224 CUs as well as 256), cut into items at map boundaries.
+  // cyc > 0 (block-cyclic): the tiles of the `cyc` workgroups sharing an XCD are cut into
+  // 16 * cyc near-equal blocks dealt round robin, so at any time they write close to each other
+  // (a launch of one huge map otherwise spreads an XCD's writes over its whole span).
   const uint32_t T = g.num_maps * g.tiles_per_map, G = gridDim.x;
   const uint32_t rr = xcd_map(blockIdx.x, G);
-  const uint32_t t_lo = (uint32_t)((uint64_t)T * rr / G), t_hi = (uint32_t)((uint64_t)T * (rr + 1) / G);
-  if (t_lo >= t_hi) return;
+  constexpr uint32_t kBlocks = 16;
+  uint32_t blk = 0, nblk = 1, gstride = 1, span_lo = 0, span_n = 0;
+  uint32_t t_lo, t_hi;
+  auto block_range = [&](uint32_t j, uint32_t& lo, uint32_t& hi) {
+    const uint32_t k = blk + j * gstride;
+    lo = span_lo + (uint32_t)((uint64_t)span_n * k / (nblk));
+    hi = span_lo + (uint32_t)((uint64_t)span_n * (k + 1) / (nblk));
+  };
+  if (cyc == 0) {
+    t_lo = (uint32_t)((uint64_t)T * rr / G);
+    t_hi = (uint32_t)((uint64_t)T * (rr + 1) / G);
+  } else {
+    const uint32_t grp = rr / cyc, members = min(cyc, G - grp * cyc);
+    span_lo = (uint32_t)((uint64_t)T * (grp * cyc) / G);
+    span_n = (uint32_t)((uint64_t)T * (grp * cyc + members) / G) - span_lo;
+    nblk = kBlocks * members;
+    gstride = members;
+    blk = rr - grp * cyc;
+    block_range(0, t_lo, t_hi);
+  }
+  if (t_lo >= t_hi && cyc == 0) return;
   struct Item {
     uint32_t map, t0;
     uint64_t begin, end;
   };
-  auto item_of = [&](uint32_t t) {  // the item starting at global tile t
+  auto item_of = [&](uint32_t t, uint32_t hi) {  // the item starting at tile t of a range ending at hi
     Item x;
     x.map = t / g.tiles_per_map;
     x.t0 = t - x.map * g.tiles_per_map;
-    const uint32_t t_end = min(t_hi, (x.map + 1) * g.tiles_per_map);
+    const uint32_t t_end = min(hi, (x.map + 1) * g.tiles_per_map);
     const uint64_t map_begin = (uint64_t)x.map * g.records_per_map;
     const uint64_t map_end = min(map_begin + g.records_per_map, g.num_records);
     x.begin = min(map_begin + (uint64_t)x.t0 * g.tile_recs, map_end);
@@ -1460,24 +1482,38 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
   };
   struct Cur {
     uint32_t it;  // global tile the chunk's item starts at
+    uint32_t bj, hi;  // the range (block) it belongs to and that range's end
     uint64_t c0, end;
     bool valid;
   };
-  auto first_cur = [&](uint32_t t) {
+  auto first_cur = [&](uint32_t t, uint32_t bj, uint32_t hi) {
     Cur k;
     k.it = t;
-    k.valid = t < t_hi;
-    const Item x = item_of(k.valid ? t : t_lo);
+    k.bj = bj;
+    k.hi = hi;
+    k.valid = t < hi;
+    const Item x = item_of(k.valid ? t : t_lo, k.valid ? hi : t_hi);
     k.c0 = x.begin;
     k.end = x.end;
     return k;
   };
-  auto next_cur = [&](const Cur& k) {
+  auto next_cur = [&](const Cur& k) {  // pure: called ahead (prefetch) and again (seams)
     Cur nk = k;
     nk.c0 = k.c0 + C;
     if (nk.c0 >= k.end) {  // the item ends at its map's end or at the range's end
       const uint32_t m = k.it / g.tiles_per_map;
-      nk = first_cur(min(t_hi, (m + 1) * g.tiles_per_map));
+      const uint32_t nt = min(k.hi, (m + 1) * g.tiles_per_map);
+      if (nt < k.hi || cyc == 0) {
+        nk = first_cur(nt, k.bj, k.hi);
+      } else {  // block-cyclic: the next non-empty block of this workgroup, if any
+        uint32_t lo = k.hi, hi = k.hi, b = k.bj;
+        while (b + 1 < kBlocks) {
+          ++b;
+          block_range(b, lo, hi);
+          if (lo < hi) break;
+        }
+        nk = lo < hi ? first_cur(lo, b, hi) : first_cur(k.hi, k.bj, k.hi);  // else: invalid, ends
+      }
     }
     return nk;
   };
@@ -1503,7 +1539,13 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
       reinterpret_cast<u32x4*>(wcnt + tid * NW)[w / 4] = u32x4{0, 0, 0, 0};
   }
   u32x4 cu0{0, 0, 0, 0}, cu1{0, 0, 0, 0};  // carrier: units 2cj, 2cj+1 of p's carried line
-  begin_item(item_of(t_lo));
+  // (block-cyclic) the first non-empty block
+  uint32_t b0 = 0;
+  if (cyc) {
+    while (t_lo >= t_hi && b0 + 1 < kBlocks) block_range(++b0, t_lo, t_hi);
+    if (t_lo >= t_hi) return;
+  }
+  begin_item(item_of(t_lo, t_hi));
   __syncthreads();
   [[maybe_unused]] uint32_t ci = 0;  // chunk counter for the diagnostic stamps
   auto process = [&](const Cur& k, const Cur& ahead, uint32_t (&pidv)[NG], u32x4 (&v)[PER]) {
@@ -1681,7 +1723,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
         }
       }
       __syncthreads();
-      if (more) begin_item(item_of(nk.it));
+      if (more) begin_item(item_of(nk.it, nk.hi));
     }
     __syncthreads();
     SUX_STAMP(ci, 7);
@@ -1691,7 +1733,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
 
   uint32_t pa[NG];
   u32x4 va[PER];
-  Cur k = first_cur(t_lo);
+  Cur k = first_cur(t_lo, b0, t_hi);
   issue(k, pa, va);
   while (true) {
     const Cur k1 = next_cur(k);
@@ -2769,8 +2811,14 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
     const dim3 grid(std::min<uint32_t>(g.num_maps * g.tiles_per_map, ncu));
     const size_t lds8b = Sc8<100, 1024, 16>::lds_bytes(R);
     allow_lds(reinterpret_cast<const void*>(&k_scatter8<100, 1024, 16>), lds8b);
+    // tile order: contiguous ranges (default; scatter_order 1) or block-cyclic inside an XCD's
+    // workgroups (2: 2^27-record maps 49.7 -> 50.3 ms, 2^20 42.9 -> 46.3, profiles/r02_m27_b)
+    const uint32_t tiles_per_wg = (g.num_maps * g.tiles_per_map + grid.x - 1) / grid.x;
+    (void)tiles_per_wg;  // block-cyclic measured slower for 2^20 and 2^27-record maps alike
+    const bool cyc = tn.scatter_order == 2;
+    const uint32_t per_xcd = std::max<uint32_t>(1, grid.x / 8);
     hipLaunchKernelGGL((k_scatter8<100, 1024, 16>), grid, dim3(1024), lds8b, s, g, R, bits, pids,
-                       counts, base, d_out);
+                       counts, base, d_out, cyc ? per_xcd : 0u);
     e = hipGetLastError();
   } else if (v7) {
     timer_note(timer, kScatter, "k_scatter7");

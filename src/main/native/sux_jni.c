@@ -195,7 +195,7 @@ JNIEXPORT jlongArray JNICALL FN(poolStats)(JNIEnv* env, jclass cls, jlong node) 
 
 /* ---- kernel tuning table (sux_tuning) and the device error word ------------------------------
  * fields[] in the header's field order (hist_kernel .. small_waves); 0 keeps the default. */
-#define SUX_TUNING_FIELDS ((int)(sizeof(sux_tuning) / sizeof(int32_t)) - 13)
+#define SUX_TUNING_FIELDS ((int)(sizeof(sux_tuning) / sizeof(int32_t)) - 12)
 JNIEXPORT void JNICALL FN(setTuning)(JNIEnv* env, jclass cls, jlong node, jintArray fields) {
   (void)cls;
   sux_tuning t;

@@ -147,6 +147,8 @@ TUNINGS = [
     {"tiles_per_item": 64},
     {"scatter_kernel": 7},
     {"scatter_kernel": 7, "tiles_per_item": 1},
+    {"scatter_order": 2},
+    {"scatter_order": 2, "tile_records": 1024},
     {"scatter_kernel": 6},
     {"scatter_kernel": 6, "s6_chunk": 384},
     {"scatter_kernel": 2, "hist_kernel": 2},
@@ -231,14 +233,14 @@ def test_kernel_variant_reports_the_coresident_shape(gpu_node, tuned):
     gp.close()
 
 
-@pytest.mark.parametrize("kernel", [8, 7])
-def test_launch_group_over_8_gib_keeps_the_image_scatter(gpu_node, tuned, kernel):
+@pytest.mark.parametrize("kernel,order", [(8, 0), (8, 1), (7, 0)])
+def test_launch_group_over_8_gib_keeps_the_image_scatter(gpu_node, tuned, kernel, order):
     """One 2^27-record TeraSort map (13.4 GB; r01 fell back to k_scatter2 above 8 GiB of group
     output, 29-bit image units).  Checked on the device without the oracle: the index is the
     map's run offsets, and every run p equals the input records whose k_pids id is p, in input
     order (stable) — for the first, a middle and the last partitions in full, and the runs that
     straddle the 8 GiB output offset."""
-    tuned(scatter_kernel=kernel)
+    tuned(scatter_kernel=kernel, scatter_order=order)
     n, R = 1 << 27, 200
     gp = gpu_part(gpu_node, O.terasort_partitioner(R))
     d = gpu_node.generate(N.GEN_TERASORT, 41, 0, n, 100)
