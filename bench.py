@@ -393,7 +393,8 @@ def self_check(node, part, data, out, index, n: int, rs: int, rpm: int, R: int,
             cnt = torch.bincount(p, minlength=R) * rs
             if not (bool((p[1:] >= p[:-1]).all()) and torch.equal(cnt, ix[m, 1:] - ix[m, :-1])):
                 raise RuntimeError(f"self-check: map {m} is not grouped by partition as indexed")
-    torch.cuda.synchronize(dev)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
     return {"maps": maps, "records": n, "ok": True,
             "checks": "index offsets; word multiset per launch group; output pids (k_pids) "
                       "non-decreasing per map with counts = index runs"}
