@@ -754,7 +754,7 @@ int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
                                      (t->tile_records & (t->tile_records - 1)) == 0),
             SUX_EINVAL, "tile_records must be a power of two in [64, 2^22]");
     require(t->onepass == 0 || t->onepass == 1, SUX_EINVAL, "onepass must be 0 or 1");
-    require(in(t->varlen_kernel, {1, 2}), SUX_EINVAL, "varlen_kernel must be 1 or 2");
+    require(in(t->varlen_kernel, {1, 2, 3}), SUX_EINVAL, "varlen_kernel must be 1, 2 or 3");
     require(t->varlen_tile == 0 || (t->varlen_tile >= 64 && t->varlen_tile <= 65536 &&
                                     t->varlen_tile % 64 == 0),
             SUX_EINVAL, "varlen_tile must be a multiple of 64 in [64, 65536]");

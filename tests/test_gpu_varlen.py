@@ -133,3 +133,58 @@ def test_full_size_properties(gpu_node):
     run_of = np.searchsorted(ix[0][1:], starts, side="right")
     assert np.array_equal(kp, run_of)
     assert np.array_equal(np.sort(out[: offs[rpm]]), np.sort(data[: offs[rpm]]))
+
+
+# ---- k_vscatter3 (128-byte line image, varlen_kernel 3) ----------------------------------------
+V3_SHAPES = [  # (seed, n, rpm, R, max_payload_words, key_mod, varlen_tile)
+    (20, 1, 1, 7, 12, None, 0),
+    (21, 63, 64, 200, 12, None, 0),
+    (22, 1000, 300, 1, 12, None, 0),
+    (23, 50_000, 7_001, 200, 12, None, 0),
+    (24, 300_000, 100_000, 215, 12, None, 0),
+    (25, 120_000, 40_000, 246, 12, None, 0),   # the LDS limit
+    (26, 120_000, 40_000, 247, 12, None, 0),   # past it: k_vscatter2
+    (27, 50_000, 100, 64, 12, None, 64),       # 500 maps of 2 tiles: items of one map per range
+    (28, 200_000, 200_000, 31, 12, 5, 0),      # 5 distinct keys: hot partitions, long runs
+    (29, 3_000, 1_000, 17, 2_000, None, 0),    # rows up to 16 KiB
+    (30, 400, 150, 9, 8_189, None, 0),         # rows up to 64 KiB - 4: one or two per chunk
+    (31, 100_000, 30_000, 100, 0, None, 64),   # 20-byte rows only
+]
+
+
+@pytest.mark.parametrize("shape", V3_SHAPES, ids=lambda s: f"n{s[1]}-rpm{s[2]}-R{s[3]}-w{s[4]}")
+def test_line_image_scatter(gpu_node, tuned, shape):
+    seed, n, rpm, R, mw, kmod, tile = shape
+    tuned(varlen_kernel=3, varlen_tile=tile)
+    data, offs = O.gen_unsafe_rows(seed, n, max_payload_words=mw, key_mod=kmod)
+    check(gpu_node, R, data, offs, rpm)
+
+
+@pytest.mark.parametrize("lead", [4, 8, 12])
+def test_line_image_scatter_unaligned_buffers(gpu_node, tuned, lead):
+    """Rows and output starting 4, 8 or 12 bytes past a 16-byte boundary: the window's first unit
+    holds bytes before the rows, and every line of the output is shifted."""
+    tuned(varlen_kernel=3)
+    R, rpm = 77, 9_000
+    data, offs = O.gen_unsafe_rows(40 + lead, 30_000)
+    gp = gpu_node.partitioner(O.MURMUR3_LONG, R, key_offset=12, key_len=8)
+    op = O.Partitioner(O.MURMUR3_LONG, R, 12, 8)
+    buf = torch.zeros(data.size + 64, dtype=torch.uint8, device="cuda")
+    buf[lead:lead + data.size] = to_dev(data)
+    obuf = torch.zeros(data.size + 64, dtype=torch.uint8, device="cuda")
+    d = buf[lead:lead + data.size]
+    o = obuf[lead:lead + data.size]
+    out, ix, be = gpu_node.partition_varlen(gp, d, to_dev(offs.astype(np.int64)), rpm, out=o)
+    torch.cuda.synchronize()
+    eo, eix, ebe, _ = O.varlen_write_maps(op, data, offs, rpm, R=R)
+    maps = -(-(offs.size - 1) // rpm)
+    assert np.array_equal(ix.cpu().numpy()[: maps * (R + 1)], eix)
+    assert obuf.cpu().numpy()[lead:lead + data.size].tobytes() == eo.tobytes()
+    assert not obuf[:lead].any() and not obuf[lead + data.size:].any()  # nothing outside
+
+
+def test_line_image_scatter_full_size(gpu_node, tuned):
+    """The bench's shape (1 Mi-row maps, R = 200), 4 maps: bit-exact against the oracle."""
+    tuned(varlen_kernel=3)
+    data, offs = O.gen_unsafe_rows(50, 4 << 20)
+    check(gpu_node, 200, data, offs, 1 << 20)
