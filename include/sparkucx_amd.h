@@ -151,7 +151,8 @@ typedef struct sux_tuning {
   int32_t sort_all_passes;  /* 1: every digit pass runs (no key-span read-back)                  */
   int32_t hist_wgs_per_cu;  /* k_hist4 workgroups per CU: 1 .. 8 (0: as many as LDS allows)     */
   int32_t small_kernel;     /* 16-byte records, R > 1024: 1 turn-taking scatter, 2 sorted chunks,
-                               3 two passes through bucket order (R <= 16384)                    */
+                               3 two passes through bucket order (R <= 16384), 4 two-level
+                               MSD passes without K1 (map-major, R <= 16384)                  */
   int32_t small_waves;      /* two-pass small-record kernels: waves per workgroup, 8 or 16      */
   int32_t scatter_order;    /* k_scatter8 tiles: 1 one contiguous range per workgroup (0), 2
                                blocks dealt round robin among an XCD's workgroups (slower)     */

@@ -743,7 +743,7 @@ int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
     require(in(t->hist_stage, {64, 128}), SUX_EINVAL, "hist_stage must be 64 or 128");
     require(t->hist_wgs_per_cu >= 0 && t->hist_wgs_per_cu <= 8, SUX_EINVAL,
             "hist_wgs_per_cu must be 0..8");
-    require(in(t->small_kernel, {1, 2, 3}), SUX_EINVAL, "small_kernel must be 1, 2 or 3");
+    require(in(t->small_kernel, {1, 2, 3, 4}), SUX_EINVAL, "small_kernel must be 1, 2, 3 or 4");
     require(in(t->small_waves, {8, 16}), SUX_EINVAL, "small_waves must be 8 or 16");
     require(in(t->scatter_order, {1, 2}), SUX_EINVAL, "scatter_order must be 1 or 2");
     require(in(t->s6_chunk, {256, 384, 512, 1024}), SUX_EINVAL, "s6_chunk must be 256..1024");

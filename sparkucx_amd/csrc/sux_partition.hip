@@ -2452,6 +2452,416 @@ __global__ __launch_bounds__(NW * 64) void k_bucket16b(PartDev pd, MapGroup g,
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Two-level (MSD) small-record map side without K1 (16-byte records, 1024 < R <= 16384,
+// map-major layout; tuning small_kernel = 4).  Every pass streams whole lines:
+//   pass A (k_msd16a) reads each 4096-record chunk once, computes every record's pid from its
+//          key, stable-sorts the chunk by bucket = pid >> 5 in LDS and writes it back to the
+//          temp copy AT THE CHUNK'S OWN POSITION (a contiguous write), with the chunk's bucket
+//          starts (u16) in offs[map][chunk][bucket];
+//   K2     (k_msd16_scan) one workgroup per map: bucket totals over the map's chunks ->
+//          segment bases segbase[map][bucket] and the index table's last entry;
+//   pass B (k_msd16b) one (map, bucket) segment at a time: the segment's runs (one ~13-record
+//          run per chunk at R = 10 000) are gathered into LDS, stable-sorted by pid & 31,
+//          written as ONE contiguous output range, and the bucket's 32 index entries (native +
+//          big-endian) are written.  A segment larger than the LDS (skewed keys) is counted
+//          first and then placed piece by piece through per-partition cursors.
+// 16 + 16 (A) and 16 + 16 (B) bytes per record, no pid array, no R-wide histogram: the
+// sorted-chunk scatter (k_hist16 + k_scatter16s) moves 19 + 54 bytes per record, 32 of them as
+// lone 16-byte stores.  Both passes run two 512-thread workgroups per CU, whose load, rank and
+// store phases interleave.  Stable: pass A keeps input order inside a bucket (chunks in order,
+// ranks in order inside a chunk), pass B keeps segment order inside a partition.
+// ------------------------------------------------------------------------------------------
+// Diagnostic build only (tools/msd_stamps.hip defines SUX_MSD_STAMPS): per-phase s_memtime
+// cycles of k_msd16b, summed per workgroup into g_msd_stamps[block][phase].
+#ifdef SUX_MSD_STAMPS
+__device__ unsigned long long* g_msd_stamps;
+#define SUX_MSD_STAMP_INIT()                 \
+  unsigned long long st_acc[5] = {0, 0, 0, 0, 0}; \
+  unsigned long long st_t = __builtin_amdgcn_s_memtime()
+#define SUX_MSD_STAMP(k)                                   \
+  do {                                                     \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    st_acc[k] += t_ - st_t;                                \
+    st_t = t_;                                             \
+  } while (0)
+#define SUX_MSD_STAMP_END()                                              \
+  do {                                                                   \
+    if (threadIdx.x == 0 && g_msd_stamps)                                \
+      for (int k_ = 0; k_ < 5; ++k_) g_msd_stamps[blockIdx.x * 8 + k_] = st_acc[k_]; \
+  } while (0)
+#else
+#define SUX_MSD_STAMP_INIT() do {} while (0)
+#define SUX_MSD_STAMP(k) do {} while (0)
+#define SUX_MSD_STAMP_END() do {} while (0)
+#endif
+constexpr uint32_t kM16Chunk = 4096;      // pass A records per chunk (the run table's unit)
+constexpr uint32_t kM16Lo = 5;            // partitions per bucket: 32
+constexpr uint32_t kM16MaxChunks = 1024;  // chunks per map pass B's run table holds (4 Mi records)
+
+template <uint32_t NW, uint32_t DB>  // stage[CH] u32x4 (its first NW words double as wsum) | wc[NW][2^DB] u32
+struct M16a {
+  static constexpr uint32_t NB = 1u << DB, NT = NW * kWave, PT = kM16Chunk / NT;
+  static constexpr uint32_t lds_bytes() { return kM16Chunk * 16 + NW * NB * 4; }
+};
+template <uint32_t NW, uint32_t PT>  // stage[CAP] u32x4 | wc[NW][64] | cur[64] | wsum[NW] | los[CAP] u8 | rp[MAXCH+1] u32 | ro[MAXCH] u16
+struct M16b {
+  static constexpr uint32_t NB = 64, NT = NW * kWave, CAP = NT * PT;
+  static constexpr uint32_t lds_bytes() {
+    return CAP * 16 + NW * NB * 4 + NB * 4 + NW * 4 + CAP + (kM16MaxChunks + 1) * 4 +
+           kM16MaxChunks * 2;
+  }
+};
+
+// records of map m in the group, and of its chunk c
+__device__ __forceinline__ uint32_t m16_map_len(const MapGroup& g, uint32_t m) {
+  const uint64_t b = (uint64_t)m * g.records_per_map;
+  const uint64_t e = min(b + g.records_per_map, g.num_records);
+  return (uint32_t)(e > b ? e - b : 0);
+}
+__device__ __forceinline__ uint32_t m16_chunk_len(uint32_t map_len, uint32_t c) {
+  const uint32_t b = c * kM16Chunk;
+  return map_len > b ? min(kM16Chunk, map_len - b) : 0u;
+}
+
+template <int KW>
+__device__ __forceinline__ uint32_t m16_pid(const PartDev& pd, const u32x4& r, int kw0) {
+  uint32_t w[KW];
+#pragma unroll
+  for (int q = 0; q < KW; ++q) {
+    const int d = kw0 + q;
+    w[q] = d == 0 ? r[0] : d == 1 ? r[1] : d == 2 ? r[2] : r[3];
+  }
+  return (uint32_t)partition_words<KW, false>(pd, w, pd.bounds, pd.lut);
+}
+
+template <int KW, uint32_t NW, uint32_t DB>
+__global__ __launch_bounds__(NW * 64, 4) void k_msd16a(PartDev pd, MapGroup g, uint32_t cpm,
+                                                 uint32_t nbk, uint16_t* __restrict__ offs,
+                                                 uint16_t* __restrict__ pids_out,
+                                                 uint8_t* __restrict__ tmp) {
+  using K = M16a<NW, DB>;
+  constexpr uint32_t NB = K::NB, NT = K::NT, PT = K::PT, CH = kM16Chunk;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  u32x4* stage = reinterpret_cast<u32x4*>(lds8);
+  uint32_t* wc = reinterpret_cast<uint32_t*>(stage + CH);  // [NW][NB]
+  uint32_t* wsum = reinterpret_cast<uint32_t*>(lds8);       // only inside the scan: stage is idle
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  const int kw0 = pd.key_offset / 4;
+  const u32x4* recs = reinterpret_cast<const u32x4*>(g.recs);
+  u32x4* t4 = reinterpret_cast<u32x4*>(tmp);
+  // one contiguous, balanced range of (map, chunk) items per workgroup
+  const uint32_t items = g.num_maps * cpm, G = gridDim.x, b = xcd_map(blockIdx.x, G);
+  const uint32_t it0 = (uint32_t)((uint64_t)items * b / G), it1 = (uint32_t)((uint64_t)items * (b + 1) / G);
+  struct Item {
+    uint64_t c0;  // first record of the chunk (group index)
+    uint32_t n;   // its records (0 past the range)
+  };
+  auto item = [&](uint32_t it) {
+    const uint32_t m = it / cpm, c = it - m * cpm;
+    Item k;
+    k.c0 = (uint64_t)m * g.records_per_map + (uint64_t)c * CH;
+    k.n = it < it1 ? m16_chunk_len(m16_map_len(g, m), c) : 0u;
+    return k;
+  };
+  auto load = [&](const Item& k, u32x4 (&r)[PT]) {
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j) {
+      const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+      if (e < k.n) r[j] = recs[k.c0 + e];
+    }
+  };
+  for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
+  __syncthreads();
+  u32x4 rv[PT];
+  for (uint32_t it = it0; it < it1; ++it) {
+    const Item k = item(it);
+    load(k, rv);
+    uint32_t h[PT], rank[PT];
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j) {
+      const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+      const bool valid = e < k.n;
+      uint32_t p = 0;
+      if (valid) {
+        p = m16_pid<KW>(pd, rv[j], kw0);
+        if (pids_out) pids_out[k.c0 + e] = (uint16_t)p;
+      }
+      h[j] = (p >> kM16Lo) & (NB - 1);
+      rank[j] = wave_rank<DB>(h[j], valid, wc + wave * NB, lt_mask);
+    }
+    __syncthreads();
+    scan_digit_wave<NB, NW>(wc, wsum, tid, lane, wave);
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j)
+      if (rank[j] != ~0u) stage[wc[wave * NB + h[j]] + rank[j]] = rv[j];
+    __syncthreads();
+    // the chunk goes back to its own place, in bucket order: one contiguous write
+#pragma unroll
+    for (uint32_t q = 0; q < PT; ++q) {
+      const uint32_t i = tid + q * NT;
+      if (i < k.n) t4[k.c0 + i] = stage[i];
+    }
+    for (uint32_t hb = tid; hb < nbk; hb += NT)
+      offs[(uint64_t)it * nbk + hb] = (uint16_t)wc[hb];  // wc[0][hb]: bucket start in the chunk
+    __syncthreads();
+    for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
+    __syncthreads();
+  }
+}
+
+// K2 of the MSD path: one workgroup (kScanThreads) per map.  Bucket totals over the map's chunks
+// (two thread groups of 512 buckets split the chunks), exclusive scan over buckets ->
+// segbase[m][h] (record index in the group's output), the index table's last entry and, at
+// world 1, the peer byte count.
+__global__ __launch_bounds__(kScanThreads) void k_msd16_scan(MapGroup g, uint32_t cpm, uint32_t nbk,
+                                                             const uint16_t* __restrict__ offs,
+                                                             uint64_t* __restrict__ segbase,
+                                                             int64_t* __restrict__ index,
+                                                             uint8_t* __restrict__ index_be,
+                                                             uint64_t* __restrict__ peer_bytes,
+                                                             int R) {
+  constexpr uint32_t HG = 512, NG = kScanThreads / HG;
+  __shared__ uint64_t sh[2 * kWave + 1];
+  __shared__ uint32_t part[kScanThreads];
+  const uint32_t m = blockIdx.x, tid = threadIdx.x;
+  const uint32_t len = m16_map_len(g, m), nch = (len + kM16Chunk - 1) / kM16Chunk;
+  const uint32_t h = tid % HG, cg = tid / HG;
+  uint32_t t = 0;
+  if (h < nbk) {
+    const uint16_t* om = offs + (uint64_t)m * cpm * nbk;
+    for (uint32_t c = cg; c < nch; c += NG) {
+      const uint32_t o = om[(uint64_t)c * nbk + h];
+      const uint32_t e = h + 1 < nbk ? om[(uint64_t)c * nbk + h + 1] : m16_chunk_len(len, c);
+      t += e - o;
+    }
+  }
+  part[tid] = t;
+  __syncthreads();
+  uint64_t v = 0;
+  if (tid < HG)
+    for (uint32_t q = 0; q < NG; ++q) v += part[tid + q * HG];
+  uint64_t tot;
+  const uint64_t ex = block_excl_scan(tid < nbk ? v : 0, sh, &tot);
+  if (tid < nbk) segbase[(uint64_t)m * nbk + tid] = (uint64_t)m * g.records_per_map + ex;
+  if (tid == 0) {
+    const int64_t off = (int64_t)len * g.rec_size;
+    index[(uint64_t)m * (R + 1) + R] = off;
+    if (index_be) reinterpret_cast<uint64_t*>(index_be)[(uint64_t)m * (R + 1) + R] = bswap64((uint64_t)off);
+    if (m == 0 && peer_bytes) peer_bytes[0] = g.num_records * g.rec_size;
+  }
+}
+
+template <int KW, uint32_t NW, uint32_t PT>
+__global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, uint32_t cpm,
+                                                 uint32_t nbk, const uint16_t* __restrict__ offs,
+                                                 const uint64_t* __restrict__ segbase,
+                                                 const uint8_t* __restrict__ tmp,
+                                                 uint8_t* __restrict__ out,
+                                                 int64_t* __restrict__ index,
+                                                 uint8_t* __restrict__ index_be) {
+  using K = M16b<NW, PT>;
+  constexpr uint32_t NB = K::NB, NT = K::NT, CAP = K::CAP, MC = kM16MaxChunks, PB = 1u << kM16Lo;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  u32x4* stage = reinterpret_cast<u32x4*>(lds8);
+  uint32_t* wc = reinterpret_cast<uint32_t*>(stage + CAP);  // [NW][NB]
+  uint32_t* cur = wc + NW * NB;
+  uint32_t* wsum = cur + NB;
+  uint8_t* los = reinterpret_cast<uint8_t*>(wsum + NW);
+  uint32_t* rp = reinterpret_cast<uint32_t*>(los + CAP);   // [MC + 1] run starts in the segment
+  uint16_t* ro = reinterpret_cast<uint16_t*>(rp + MC + 1);  // [MC] run starts in their chunk
+  const int R = pd.R;
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  const int kw0 = pd.key_offset / 4;
+  const u32x4* t4 = reinterpret_cast<const u32x4*>(tmp);
+  u32x4* out4 = reinterpret_cast<u32x4*>(out);
+  uint64_t* ibe = reinterpret_cast<uint64_t*>(index_be);
+  const uint32_t items = g.num_maps * nbk, G = gridDim.x, b = xcd_map(blockIdx.x, G);
+  const uint32_t it0 = (uint32_t)((uint64_t)items * b / G), it1 = (uint32_t)((uint64_t)items * (b + 1) / G);
+
+  struct Seg {
+    uint32_t m, h, nch, T, len;
+    uint64_t mbase, out;  // first record of map m, first output record of the segment
+  };
+  // the global reads a segment's run table starts from (offs pair of chunk tid, segment base),
+  // issued one segment ahead so that build() does not wait for them
+  struct Pre {
+    uint32_t o, e;
+    uint64_t sb;
+  };
+  auto seg = [&](uint32_t it) {
+    Seg s;
+    s.m = it / nbk;
+    s.h = it - s.m * nbk;
+    s.len = m16_map_len(g, s.m);
+    s.nch = (s.len + kM16Chunk - 1) / kM16Chunk;
+    s.mbase = (uint64_t)s.m * g.records_per_map;
+    return s;
+  };
+  auto run_ends = [&](const Seg& s, uint32_t c, uint32_t& o, uint32_t& e) {
+    const uint16_t* oc = offs + ((uint64_t)s.m * cpm + c) * nbk;
+    o = oc[s.h];
+    e = s.h + 1 < nbk ? oc[s.h + 1] : m16_chunk_len(s.len, c);
+  };
+  auto prefetch = [&](uint32_t it) {
+    Pre p{0, 0, 0};
+    if (it < it1) {
+      const Seg s = seg(it);
+      if ((uint32_t)tid < s.nch) run_ends(s, tid, p.o, p.e);
+      p.sb = segbase[it];
+    }
+    return p;
+  };
+  // run table of segment `it` (run c = the bucket's records of chunk c; rp = exclusive prefix
+  // over chunks); all threads, barriers inside
+  auto build = [&](uint32_t it, const Pre& pre) {
+    Seg s = seg(it);
+    s.out = pre.sb;
+    uint32_t carry = 0;
+    for (uint32_t c0 = 0; c0 < s.nch; c0 += NT) {
+      const uint32_t c = c0 + (uint32_t)tid;
+      uint32_t o = pre.o, e = pre.e;
+      if (c0 && c < s.nch) run_ends(s, c, o, e);
+      const uint32_t cnt = c < s.nch ? e - o : 0u;
+      const uint32_t incl = wave_incl_scan(cnt, lane);
+      if (lane == kWave - 1) wsum[wave] = incl;
+      __syncthreads();
+      uint32_t run = carry + incl - cnt, blk = 0;
+#pragma unroll
+      for (uint32_t w = 0; w < NW; ++w) {
+        run += w < (uint32_t)wave ? wsum[w] : 0u;
+        blk += wsum[w];
+      }
+      if (c < s.nch) {
+        rp[c] = run;
+        ro[c] = (uint16_t)o;
+      }
+      carry += blk;
+      __syncthreads();
+    }
+    s.T = carry;
+    return s;
+  };
+  // loads of segment elements [e0, min(T, e0 + CAP)) in wave-contiguous order
+  auto load = [&](const Seg& s, uint32_t e0, u32x4 (&r)[PT]) {
+    const uint32_t lim = min(s.T, e0 + CAP);
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j) {
+      const uint32_t e = e0 + wave * (PT * kWave) + j * kWave + lane;
+      // largest c with rp[c] <= e: a fixed-step search (no data-dependent loop), so the PT
+      // searches interleave their LDS reads instead of running one after another
+      uint32_t lo = 0;
+#pragma unroll
+      for (uint32_t step = MC / 2; step; step >>= 1) {
+        const uint32_t c = lo + step;
+        if (c < s.nch && rp[c] <= e) lo = c;
+      }
+      if (e < lim) r[j] = t4[s.mbase + (uint64_t)lo * kM16Chunk + ro[lo] + (e - rp[lo])];
+    }
+  };
+  auto digit = [&](const Seg& s, const u32x4& r) {
+    return (m16_pid<KW>(pd, r, kw0) - (s.h << kM16Lo)) & (NB - 1);
+  };
+  // stable rank by pid & 31 -> stage/los in sorted order; wc[0][l] = digit starts afterwards
+  auto rank_stage = [&](const Seg& s, uint32_t n, const u32x4 (&r)[PT]) {
+    uint32_t lo[PT], rk[PT];
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j) {
+      const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+      const bool valid = e < n;
+      lo[j] = valid ? digit(s, r[j]) : 0u;
+      rk[j] = wave_rank<kB16Lo>(lo[j], valid, wc + wave * NB, lt_mask);
+    }
+    __syncthreads();
+    scan_digit_wave<NB, NW>(wc, wsum, tid, lane, wave);
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j)
+      if (rk[j] != ~0u) {
+        const uint32_t pos = wc[wave * NB + lo[j]] + rk[j];
+        stage[pos] = r[j];
+        los[pos] = (uint8_t)lo[j];
+      }
+  };
+  auto write_index = [&](const Seg& s, uint32_t start_l) {
+    const uint64_t seg_out = s.out;
+    const uint32_t p = (s.h << kM16Lo) + (uint32_t)tid;  // in-segment record offset of partition p
+    if (tid < (int)PB && p < (uint32_t)R) {
+      const int64_t off = (int64_t)((seg_out - s.mbase + start_l) * g.rec_size);
+      index[(uint64_t)s.m * (R + 1) + p] = off;
+      if (ibe) ibe[(uint64_t)s.m * (R + 1) + p] = bswap64((uint64_t)off);
+    }
+  };
+  // sorted stage -> output through the per-partition cursors; cursors advance; wc cleared
+  auto place = [&](const Seg& s, uint32_t n) {
+#pragma unroll
+    for (uint32_t q = 0; q < PT; ++q) {
+      const uint32_t i = tid + q * NT;
+      if (i < n) {
+        const uint32_t l = los[i];
+        out4[s.mbase + cur[l] + (i - wc[l])] = stage[i];
+      }
+    }
+    uint32_t ncur = 0;
+    if (tid < (int)NB) ncur = cur[tid] + ((uint32_t)tid + 1 < NB ? wc[tid + 1] : n) - wc[tid];
+    __syncthreads();
+    if (tid < (int)NB) cur[tid] = ncur;
+    for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
+    __syncthreads();
+  };
+
+  for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
+  __syncthreads();
+  if (it0 >= it1) return;
+  Seg s = build(it0, prefetch(it0));
+  u32x4 rv[PT];
+  SUX_MSD_STAMP_INIT();
+  for (uint32_t it = it0; it < it1; ++it) {
+    const uint32_t seg_rel = (uint32_t)(s.out - s.mbase);  // in-map record offset of the segment
+    const bool multi = s.T > CAP;
+    if (multi) {
+      // larger than the LDS (skewed keys): count the digits first, then place piece by piece
+      for (uint32_t e0 = 0; e0 < s.T; e0 += CAP) {
+        load(s, e0, rv);
+        const uint32_t n = min(CAP, s.T - e0);
+#pragma unroll
+        for (uint32_t j = 0; j < PT; ++j) {
+          const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+          if (e < n) atomicAdd(&wc[wave * NB + digit(s, rv[j])], 1u);
+        }
+      }
+      __syncthreads();
+      scan_digit_wave<NB, NW>(wc, wsum, tid, lane, wave);
+      if (tid < (int)NB) cur[tid] = seg_rel + wc[tid];
+      write_index(s, tid < (int)NB ? wc[tid] : 0u);
+      __syncthreads();
+      for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
+      __syncthreads();
+    }
+    // one piece (the whole segment) unless multi; an empty segment still writes its index
+    for (uint32_t e0 = 0; e0 == 0 || e0 < s.T; e0 += CAP) {
+      load(s, e0, rv);
+      SUX_MSD_STAMP(0);
+      const uint32_t n = min(CAP, s.T - e0);
+      rank_stage(s, n, rv);
+      __syncthreads();
+      SUX_MSD_STAMP(1);
+      if (!multi) {
+        if (tid < (int)NB) cur[tid] = seg_rel + wc[tid];
+        write_index(s, tid < (int)NB ? wc[tid] : 0u);
+      }
+      __syncthreads();
+      SUX_MSD_STAMP(2);
+      place(s, n);
+      SUX_MSD_STAMP(3);
+    }
+    if (it + 1 < it1) s = build(it + 1, prefetch(it + 1));
+    SUX_MSD_STAMP(4);
+  }
+  SUX_MSD_STAMP_END();
+}
+
 template <int KW, bool TAB>
 static void launch_hist3_kw(dim3 grid, size_t lds, hipStream_t s, const PartDev& pd,
                             const MapGroup& g, uint16_t* pids, uint32_t* counts) {
@@ -2557,6 +2967,26 @@ static hipError_t launch_scatter(uint32_t S, dim3 grid, size_t lds, hipStream_t 
   return hipGetLastError();
 }
 
+// The MSD small-record path (k_msd16a / k_msd16_scan / k_msd16b) applies: tuning small_kernel 4,
+// 16-byte records with a fixed-width key in the first 16 bytes, 1024 < R <= 16384, 16-byte
+// aligned input and output, map-major layout, maps of <= kM16MaxChunks chunks, and a workspace
+// with the temp copy (its chunk-offset table lives in the counts region, the segment bases in
+// the totals region).
+static bool msd16_eligible(const PartDev& pd, const MapGroup& g, const LayoutDesc& lay,
+                           const uint8_t* d_out, const Workspace& ws, const Tuning& tn) {
+  if (tn.small_kernel != 4 || g.rec_size != 16 || lay.world != 1) return false;
+  if (pd.R <= 1024 || pd.R > 16384 || pd.kind == 4 || pd.key_offset % 4 != 0 ||
+      pd.key_offset + pd.key_len > 16)
+    return false;
+  if (((reinterpret_cast<uintptr_t>(g.recs) | reinterpret_cast<uintptr_t>(d_out)) & 15) != 0)
+    return false;
+  const uint64_t cpm = (g.records_per_map + kM16Chunk - 1) / kM16Chunk;
+  const uint64_t nbk = ((uint64_t)pd.R + (1u << kM16Lo) - 1) >> kM16Lo;
+  return cpm >= 1 && cpm <= kM16MaxChunks && ws.tmp_bytes >= g.num_records * 16 &&
+         (uint64_t)g.num_maps * cpm * nbk * 2 <= ws.counts_bytes &&
+         (uint64_t)g.num_maps * nbk * 8 <= ws.totals_bytes;
+}
+
 hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const LayoutDesc& lay,
                                   uint8_t* d_out, int64_t* d_index, uint8_t* d_index_be,
                                   uint16_t* d_pids, uint8_t* d_ws, const Workspace& ws,
@@ -2583,6 +3013,69 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   uint64_t* totals = reinterpret_cast<uint64_t*>(d_ws + ws.totals_off);
   uint64_t* base = reinterpret_cast<uint64_t*>(d_ws + ws.base_off);
   uint16_t* pids = d_pids ? d_pids : reinterpret_cast<uint16_t*>(d_ws + ws.pids_off);
+
+  // ---- small records, many partitions, map-major: the two-level path without K1 (k_msd16*)
+  if (msd16_eligible(pd, g, lay, d_out, ws, tn)) {
+    const uint32_t cpm = (uint32_t)((g.records_per_map + kM16Chunk - 1) / kM16Chunk);
+    const uint32_t nbk = ((uint32_t)R + (1u << kM16Lo) - 1) >> kM16Lo;
+    uint16_t* offs = reinterpret_cast<uint16_t*>(counts);  // [map][chunk][bucket]
+    uint64_t* segbase = totals;                              // [map][bucket]
+    uint8_t* tmp = d_ws + ws.tmp_off;
+    const int kw = (pd.key_len + 3) / 4;
+    // two 512-thread workgroups per CU in both passes: their load / rank / store phases
+    // interleave (one prefetching 1024-thread workgroup measured slower: 9.4 vs 8.4 ms of
+    // pass A per 17 GB step, and pass B spills; profiles/r02_sweeps/msd)
+    constexpr uint32_t NWA = 8, NWB = 8, PTB = 8;
+    timer_note(timer, kHist, "k_msd16a");
+    timer_begin(timer, kHist, s);
+    const dim3 ga(std::min<uint32_t>(g.num_maps * cpm, ncu * 2));
+#define SUX_M16A(KW, DB)                                                                           \
+  do {                                                                                             \
+    constexpr size_t ldsa = M16a<NWA, DB>::lds_bytes();                                            \
+    allow_lds(reinterpret_cast<const void*>(&k_msd16a<KW, NWA, DB>), ldsa);                        \
+    hipLaunchKernelGGL((k_msd16a<KW, NWA, DB>), ga, dim3(NWA * kWave), ldsa, s, pd, g, cpm, nbk,   \
+                       offs, d_pids, tmp);                                                         \
+  } while (0)
+#define SUX_M16AK(DB)                   \
+  do {                                  \
+    if (kw <= 1) SUX_M16A(1, DB);       \
+    else if (kw == 2) SUX_M16A(2, DB);  \
+    else if (kw == 3) SUX_M16A(3, DB);  \
+    else SUX_M16A(4, DB);               \
+  } while (0)
+    if (nbk > 256) SUX_M16AK(9);
+    else SUX_M16AK(8);
+#undef SUX_M16AK
+#undef SUX_M16A
+    timer_end(timer, kHist, s);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    timer_note(timer, kScan, "k_msd16_scan");
+    timer_begin(timer, kScan, s);
+    hipLaunchKernelGGL(k_msd16_scan, dim3(g.num_maps), dim3(kScanThreads), 0, s, g, cpm, nbk, offs,
+                       segbase, d_index, d_index_be, d_peer_bytes, R);
+    timer_end(timer, kScan, s);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    timer_note(timer, kScatter, "k_msd16b");
+    timer_begin(timer, kScatter, s);
+    const dim3 gb(std::min<uint32_t>(g.num_maps * nbk, ncu * 2));
+    constexpr size_t ldsb = M16b<NWB, PTB>::lds_bytes();
+    static_assert(2 * ldsb <= 160 * 1024, "pass B: two workgroups per CU");
+#define SUX_M16B(KW)                                                                               \
+  do {                                                                                             \
+    allow_lds(reinterpret_cast<const void*>(&k_msd16b<KW, NWB, PTB>), ldsb);                      \
+    hipLaunchKernelGGL((k_msd16b<KW, NWB, PTB>), gb, dim3(NWB * kWave), ldsb, s, pd, g, cpm, nbk,  \
+                       offs, segbase, tmp, d_out, d_index, d_index_be);                            \
+  } while (0)
+    if (kw <= 1) SUX_M16B(1);
+    else if (kw == 2) SUX_M16B(2);
+    else if (kw == 3) SUX_M16B(3);
+    else SUX_M16B(4);
+#undef SUX_M16B
+    timer_end(timer, kScatter, s);
+    return hipGetLastError();
+  }
   int bits = 0;
   while ((1 << bits) < R) ++bits;
   const int wpg = waves_per_group(R);

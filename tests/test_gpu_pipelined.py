@@ -174,10 +174,11 @@ def test_tuning_shapes_are_bit_exact(gpu_node, tuned, tn, R):
     gp.close()
 
 
-@pytest.mark.parametrize("kernel,groups", [(1, 1), (1, 2), (1, 4), (2, 0), (3, 0), (3, -1)])
+@pytest.mark.parametrize("kernel,groups", [(1, 1), (1, 2), (1, 4), (2, 0), (3, 0), (3, -1), (4, 0)])
 def test_small_record_kernels_bit_exact(gpu_node, tuned, kernel, groups):
     """Every small-record scatter: turn-taking k_scatter16b (1, 2, 4 groups per turn), the
-    turn-free sorted-chunk k_scatter16s and the two-pass bucketed k_bucket16a + k_bucket16b."""
+    turn-free sorted-chunk k_scatter16s, the two-pass bucketed k_bucket16a + k_bucket16b and
+    the two-level k_msd16a + k_msd16b (no K1)."""
     tuned(small_kernel=kernel, small_groups=max(groups, 0), small_waves=16 if groups < 0 else 0)
     recs = O.gen_small(36, 0, 200000)
     opart = O.Partitioner(O.MURMUR3_LONG, 3000, 0, 8, seed=42)
@@ -200,10 +201,12 @@ def test_small_record_kernels_bit_exact(gpu_node, tuned, kernel, groups):
     (2000, 300000, 300000, "one"),      # one bucket holds the whole map (many LDS chunks)
     (1100, 90000, 30000, "zipf"),       # a short last bucket (1100 = 17 x 64 + 12)
 ])
-@pytest.mark.parametrize("kernel", [2, 3, 316])
+@pytest.mark.parametrize("kernel", [2, 3, 316, 4])
 def test_sorted_chunk_scatter_shapes(gpu_node, tuned, kernel, R, n, rpm, skew):
-    """kernel 316: the two-pass path with 16-wave workgroups"""
-    tuned(small_kernel=min(kernel, 3), small_waves=16 if kernel == 316 else 0)
+    """kernel 316: the two-pass path with 16-wave workgroups; kernel 4: the two-level MSD path
+    (segments larger than its LDS piece in the 'one' and 'zipf' rows)"""
+    tuned(small_kernel=kernel // 100 if kernel > 100 else kernel,
+          small_waves=16 if kernel > 100 else 0)
     if skew == "zipf":
         recs = O.gen_zipf(39, 0, n, 1.1, 1 << 12)
         recs = recs.reshape(-1, 100)[:, :16].copy().ravel()
@@ -217,7 +220,7 @@ def test_sorted_chunk_scatter_shapes(gpu_node, tuned, kernel, R, n, rpm, skew):
     torch.cuda.synchronize()
     expect(opart, recs, 16, rpm, out, index, index_be)
     want = ("k_scatter16b" if R > 16384 else "k_scatter16s" if kernel == 2
-            else "k_bucket16a+k_bucket16b")
+            else "k_msd16b" if kernel == 4 else "k_bucket16a+k_bucket16b")
     assert gpu_node.kernel_variant(2) == want
     gp.close()
     gpu_node.check()
@@ -284,4 +287,55 @@ def test_line_carry_scatter_shapes(gpu_node, tuned, R, n, rpm, tile, tpi):
     torch.cuda.synchronize()
     expect(opart, recs, 100, rpm, out, index, index_be)
     assert gpu_node.kernel_variant(2) == ("k_scatter8" if R <= 215 else "k_scatter7")
+    gp.close()
+
+
+@pytest.mark.parametrize("R,n,rpm,skew", [
+    (10000, 3 * 131072 + 5000, 131072, None),   # 32 chunks per map, ragged last map
+    (10000, 100000, 100000, "hot"),             # 30 % of the records in one partition
+    (8192, 70000, 20000, None),                 # 256 buckets: 8-bit pass A digits
+    (8193, 70000, 20000, None),                 # 257 buckets: 9-bit pass A digits
+    (1025, 4096 * 3, 4096, "one"),              # whole chunks of one partition
+    (3000, 1, 1, None),                         # a single record
+])
+def test_msd16_pids_and_shapes(gpu_node, tuned, R, n, rpm, skew):
+    """The two-level small-record path (small_kernel 4): bytes, both index tables and the
+    caller-requested pid array (written by pass A in input order) equal the oracle's."""
+    tuned(small_kernel=4)
+    recs = O.gen_small(41, 0, n)
+    if skew == "one":
+        recs.reshape(-1, 16)[:, :8] = 3
+    elif skew == "hot":
+        recs.reshape(-1, 16)[: n * 3 // 10: 3, :8] = 11
+    opart = O.Partitioner(O.MURMUR3_LONG, R, 0, 8, seed=42)
+    gp = gpu_part(gpu_node, opart)
+    pids = torch.empty(n, dtype=torch.int16, device="cuda")
+    out, index, index_be = gpu_node.partition_maps(gp, torch.from_numpy(recs).cuda(), 16, rpm,
+                                                   pids=pids)
+    torch.cuda.synchronize()
+    expect(opart, recs, 16, rpm, out, index, index_be)
+    assert (host(pids).view(np.uint16) == opart.ids(recs, 16)).all()
+    assert gpu_node.kernel_variant(0) == "k_msd16a" and gpu_node.kernel_variant(2) == "k_msd16b"
+    gp.close()
+    gpu_node.check()
+
+
+def test_msd16_falls_back_for_the_exchange_layout(gpu_node, tuned):
+    """Peer-major outputs (N > 1) are not map-major: small_kernel 4 keeps the sorted-chunk
+    scatter there, bit-exact."""
+    tuned(small_kernel=4)
+    recs = O.gen_small(42, 0, 60000)
+    opart = O.Partitioner(O.MURMUR3_LONG, 5000, 0, 8, seed=42)
+    gp = gpu_part(gpu_node, opart)
+    d = torch.from_numpy(recs).cuda()
+    out = torch.empty_like(d)
+    index = torch.empty(3 * 5001, dtype=torch.int64, device="cuda")
+    peer = torch.empty(4, dtype=torch.int64, device="cuda")
+    gpu_node.partition_maps_peer_major(gp, d, 16, 20000, 4, out=out, index=index, peer_bytes=peer)
+    torch.cuda.synchronize()
+    assert gpu_node.kernel_variant(2) == "k_scatter16s"
+    want_data, want_index, want_peer = O.peer_major(opart, recs, 16, 20000, 4)
+    assert host(out).tobytes() == want_data.tobytes()
+    assert host(index).tolist() == want_index.tolist()
+    assert host(peer).tolist() == want_peer.tolist()
     gp.close()
