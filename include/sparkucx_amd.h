@@ -156,7 +156,10 @@ typedef struct sux_tuning {
   int32_t small_waves;      /* two-pass small-record kernels: waves per workgroup, 8 or 16      */
   int32_t scatter_order;    /* k_scatter8 tiles: 1 one contiguous range per workgroup (0), 2
                                blocks dealt round robin among an XCD's workgroups (slower)     */
-  int32_t reserved[12];
+  int32_t small_wgs_per_cu; /* two-level small-record kernels (small_kernel 4): workgroups per CU
+                               of each pass, 1 or 2 (0: 2); 1 lets two launch groups' passes
+                               share every CU                                                  */
+  int32_t reserved[11];
 } sux_tuning;
 int sux_node_set_tuning(sux_node* node, const sux_tuning* tuning);
 /* Waits for the device, then reports (and clears) failures the kernels recorded in the node's

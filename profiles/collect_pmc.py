@@ -38,7 +38,7 @@ PASSES = [
 ]
 KERNELS = {"k_hist": "hist", "k_scatter": "scatter", "k_tile_scan": "tile_scan",
            "k_map_scan": "map_scan", "k_onepass": "onepass", "k_sweep": "sweep",
-           "k_gather_copy": "copy"}
+           "k_gather_copy": "copy", "k_msd16": "msd"}
 WORKLOAD_ARGS = {  # one PMC run: 8 launch groups of 32 maps x 2^20 records per workload (the
     # traffic per record is what bench.py reads; it does not depend on the group size)
     "terasort": ["--workload", "terasort", "--records", str(8 * 32 * (1 << 20)), "--group-maps", "32"],
@@ -120,7 +120,9 @@ def main():
         for f in sorted(glob.glob(os.path.join(a.merge, "*", "summary.json"))):
             with open(f) as fh:
                 sm = json.load(fh)
-            merged["workloads"][sm["workload"]] = sm
+            # kernels profiled earlier under the same workload (other tuning shapes) are kept
+            old = merged["workloads"].get(sm["workload"], {}).get("kernels", {})
+            merged["workloads"][sm["workload"]] = dict(sm, kernels={**old, **sm["kernels"]})
         with open(path, "w") as f:
             json.dump(merged, f, indent=1, sort_keys=True)
         print("wrote", path, sorted(merged["workloads"]))

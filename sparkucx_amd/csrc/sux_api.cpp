@@ -509,7 +509,7 @@ struct Group {
 // groups in flight (sux_partition_maps_pipelined, sux_write_map_outputs); the co-resident K1/K3
 // shapes are then possible, but measured slower (profiles/r02_sw_b: 1331 vs 1437 GB/s on
 // TeraSort 100 GB: a K1 beside K3 takes K3's HBM share), so they are opt-in.
-constexpr int kDefaultSmallKernel = 2;  // sorted chunks (profiles/r02_small_b)
+constexpr int kDefaultSmallKernel = 4;  // two-level MSD passes (profiles/r02_sweeps/msd: 752 -> 800 GB/s)
 
 sux::Tuning resolve_tuning(const sux_tuning& t, bool pipelined) {
   sux::Tuning r;
@@ -530,6 +530,7 @@ sux::Tuning resolve_tuning(const sux_tuning& t, bool pipelined) {
   r.small_kernel = t.small_kernel ? t.small_kernel : kDefaultSmallKernel;
   if (t.small_waves) r.small_waves = t.small_waves;
   r.scatter_order = t.scatter_order;
+  if (t.small_wgs_per_cu) r.small_wgs_per_cu = t.small_wgs_per_cu;
   return r;
 }
 
@@ -746,6 +747,7 @@ int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
     require(in(t->small_kernel, {1, 2, 3, 4}), SUX_EINVAL, "small_kernel must be 1, 2, 3 or 4");
     require(in(t->small_waves, {8, 16}), SUX_EINVAL, "small_waves must be 8 or 16");
     require(in(t->scatter_order, {1, 2}), SUX_EINVAL, "scatter_order must be 1 or 2");
+    require(in(t->small_wgs_per_cu, {1, 2}), SUX_EINVAL, "small_wgs_per_cu must be 1 or 2");
     require(in(t->s6_chunk, {256, 384, 512, 1024}), SUX_EINVAL, "s6_chunk must be 256..1024");
     require(t->tiles_per_item >= 0 && t->tiles_per_item <= 4096, SUX_EINVAL,
             "tiles_per_item must be 0..4096");

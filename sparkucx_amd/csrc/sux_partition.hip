@@ -2679,7 +2679,12 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
   u32x4* out4 = reinterpret_cast<u32x4*>(out);
   uint64_t* ibe = reinterpret_cast<uint64_t*>(index_be);
   const uint32_t items = g.num_maps * nbk, G = gridDim.x, b = xcd_map(blockIdx.x, G);
-  const uint32_t it0 = (uint32_t)((uint64_t)items * b / G), it1 = (uint32_t)((uint64_t)items * (b + 1) / G);
+  // segments dealt round robin (segment it to workgroup it % G, an XCD's workgroups taking
+  // consecutive segments): at any moment the grid works on ~G consecutive segments, i.e. on
+  // every bucket of a map or two, so the runs it gathers cover whole chunks of the temp copy
+  // (DRAM rows and L2 lines shared by neighbouring runs are read together), and the outputs it
+  // writes are adjacent.  (One contiguous range of segments per workgroup: 2.45 TB/s.)
+  const uint32_t it0 = b, it1 = items;
 
   struct Seg {
     uint32_t m, h, nch, T, len;
@@ -2720,7 +2725,8 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
     Seg s = seg(it);
     s.out = pre.sb;
     uint32_t carry = 0;
-    for (uint32_t c0 = 0; c0 < s.nch; c0 += NT) {
+    // c0 <= nch: the thread with c == nch writes rp[nch] = T, the search's sentinel
+    for (uint32_t c0 = 0; c0 <= s.nch; c0 += NT) {
       const uint32_t c = c0 + (uint32_t)tid;
       uint32_t o = pre.o, e = pre.e;
       if (c0 && c < s.nch) run_ends(s, c, o, e);
@@ -2734,10 +2740,8 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
         run += w < (uint32_t)wave ? wsum[w] : 0u;
         blk += wsum[w];
       }
-      if (c < s.nch) {
-        rp[c] = run;
-        ro[c] = (uint16_t)o;
-      }
+      if (c < s.nch) ro[c] = (uint16_t)o;
+      if (c <= s.nch) rp[c] = run;
       carry += blk;
       __syncthreads();
     }
@@ -2747,19 +2751,32 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
   // loads of segment elements [e0, min(T, e0 + CAP)) in wave-contiguous order
   auto load = [&](const Seg& s, uint32_t e0, u32x4 (&r)[PT]) {
     const uint32_t lim = min(s.T, e0 + CAP);
+    // run of element e = the largest c with rp[c] <= e: a branch-free search whose PT lookups
+    // interleave step by step (rp[nch] = T > e stops every search inside the segment)
+    uint32_t lo[PT], ev[PT];
 #pragma unroll
     for (uint32_t j = 0; j < PT; ++j) {
-      const uint32_t e = e0 + wave * (PT * kWave) + j * kWave + lane;
-      // largest c with rp[c] <= e: a fixed-step search (no data-dependent loop), so the PT
-      // searches interleave their LDS reads instead of running one after another
-      uint32_t lo = 0;
-#pragma unroll
-      for (uint32_t step = MC / 2; step; step >>= 1) {
-        const uint32_t c = lo + step;
-        if (c < s.nch && rp[c] <= e) lo = c;
-      }
-      if (e < lim) r[j] = t4[s.mbase + (uint64_t)lo * kM16Chunk + ro[lo] + (e - rp[lo])];
+      lo[j] = 0;
+      ev[j] = e0 + wave * (PT * kWave) + j * kWave + lane;
     }
+#pragma unroll
+    for (uint32_t step = MC / 2; step; step >>= 1) {
+      uint32_t v[PT];
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) v[j] = rp[min(lo[j] + step, s.nch)];
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) lo[j] = v[j] <= ev[j] ? min(lo[j] + step, s.nch) : lo[j];
+    }
+#ifdef SUX_MSD_LINEAR  // diagnostic (tools/msd_stamps): contiguous in-map reads, wrong data
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j)
+      if (ev[j] < lim) r[j] = t4[s.mbase + ((uint64_t)s.h * 3350 + ev[j]) % s.len];
+#else
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j)
+      if (ev[j] < lim)
+        r[j] = t4[s.mbase + (uint64_t)lo[j] * kM16Chunk + ro[lo[j]] + (ev[j] - rp[lo[j]])];
+#endif
   };
   auto digit = [&](const Seg& s, const u32x4& r) {
     return (m16_pid<KW>(pd, r, kw0) - (s.h << kM16Lo)) & (NB - 1);
@@ -2817,7 +2834,7 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
   Seg s = build(it0, prefetch(it0));
   u32x4 rv[PT];
   SUX_MSD_STAMP_INIT();
-  for (uint32_t it = it0; it < it1; ++it) {
+  for (uint32_t it = it0; it < it1; it += G) {
     const uint32_t seg_rel = (uint32_t)(s.out - s.mbase);  // in-map record offset of the segment
     const bool multi = s.T > CAP;
     if (multi) {
@@ -2856,7 +2873,7 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
       place(s, n);
       SUX_MSD_STAMP(3);
     }
-    if (it + 1 < it1) s = build(it + 1, prefetch(it + 1));
+    if (it + G < it1) s = build(it + G, prefetch(it + G));
     SUX_MSD_STAMP(4);
   }
   SUX_MSD_STAMP_END();
@@ -3028,7 +3045,8 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
     constexpr uint32_t NWA = 8, NWB = 8, PTB = 8;
     timer_note(timer, kHist, "k_msd16a");
     timer_begin(timer, kHist, s);
-    const dim3 ga(std::min<uint32_t>(g.num_maps * cpm, ncu * 2));
+    const uint32_t wpc = (uint32_t)tn.small_wgs_per_cu;
+    const dim3 ga(std::min<uint32_t>(g.num_maps * cpm, ncu * wpc));
 #define SUX_M16A(KW, DB)                                                                           \
   do {                                                                                             \
     constexpr size_t ldsa = M16a<NWA, DB>::lds_bytes();                                            \
@@ -3059,7 +3077,7 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
     if (e != hipSuccess) return e;
     timer_note(timer, kScatter, "k_msd16b");
     timer_begin(timer, kScatter, s);
-    const dim3 gb(std::min<uint32_t>(g.num_maps * nbk, ncu * 2));
+    const dim3 gb(std::min<uint32_t>(g.num_maps * nbk, ncu * wpc));
     constexpr size_t ldsb = M16b<NWB, PTB>::lds_bytes();
     static_assert(2 * ldsb <= 160 * 1024, "pass B: two workgroups per CU");
 #define SUX_M16B(KW)                                                                               \

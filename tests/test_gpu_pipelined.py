@@ -298,10 +298,12 @@ def test_line_carry_scatter_shapes(gpu_node, tuned, R, n, rpm, tile, tpi):
     (1025, 4096 * 3, 4096, "one"),              # whole chunks of one partition
     (3000, 1, 1, None),                         # a single record
 ])
-def test_msd16_pids_and_shapes(gpu_node, tuned, R, n, rpm, skew):
-    """The two-level small-record path (small_kernel 4): bytes, both index tables and the
-    caller-requested pid array (written by pass A in input order) equal the oracle's."""
-    tuned(small_kernel=4)
+@pytest.mark.parametrize("wpc", [2, 1])
+def test_msd16_pids_and_shapes(gpu_node, tuned, R, n, rpm, skew, wpc):
+    """The two-level small-record path (small_kernel 4, 2 or 1 workgroups per CU): bytes, both
+    index tables and the caller-requested pid array (written by pass A in input order) equal
+    the oracle's."""
+    tuned(small_kernel=4, small_wgs_per_cu=wpc)
     recs = O.gen_small(41, 0, n)
     if skew == "one":
         recs.reshape(-1, 16)[:, :8] = 3

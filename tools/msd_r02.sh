@@ -14,12 +14,8 @@ run() {  # name, extra args
   python3 -c "import json; d=json.load(open('$out/bench_$1.json')); r=d['roofline']; print('$1', d['value'], d['ms_per_step'], r['kernel'], r['avg_launch_ms'], r['frac'], {k: round(v/5,2) for k,v in d['roofline_map_side']['kernels_ms'].items()}, d.get('self_check',{}).get('ok'))"
 }
 echo "== bench"
-#run k2iso --map-pipeline 0 --tuning small_kernel=2
-run k4w8iso --map-pipeline 0 --tuning small_kernel=4,small_waves=8
-#run k4w16iso --map-pipeline 0 --tuning small_kernel=4,small_waves=16
-#run k2 --tuning small_kernel=2
-run k4w8 --tuning small_kernel=4,small_waves=8
-#run k4w16 --tuning small_kernel=4,small_waves=16
-echo "== rocprof k4" && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof -o run --output-format csv -- python3 bench.py --workload small --steps 3 --warmup 1 $legs --self-check 0 --map-pipeline 0 --tuning small_kernel=4,small_waves=8 > $out/prof.json 2> $out/prof.err || { tail -30 $out/prof.err; exit 1; }
-find $out/prof -name '*kernel_stats.csv' -exec cp {} $out/kernel_stats.csv \;
-head -6 $out/kernel_stats.csv | cut -c1-60,200-300
+run k4iso --map-pipeline 0 --tuning small_kernel=4
+run k4 --tuning small_kernel=4
+run k4w1 --tuning small_kernel=4,small_wgs_per_cu=1
+run k4w1iso --map-pipeline 0 --tuning small_kernel=4,small_wgs_per_cu=1
+echo "== stamps" && timeout -k 10 120 ./tools/msd_stamps 200 > $out/stamps.txt 2>&1 || { cat $out/stamps.txt; exit 1; }; cat $out/stamps.txt
