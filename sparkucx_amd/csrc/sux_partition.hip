@@ -2188,8 +2188,8 @@ struct B16b {
 
 // Stable in-wave rank of `dig` (DB bits) against the wave's running per-digit counters wcw[]:
 // lanes of the group in lane order after the wave's earlier groups.  ~0 for invalid lanes.
-template <uint32_t DB>
-__device__ __forceinline__ uint32_t wave_rank(uint32_t dig, bool valid, uint32_t* wcw, uint64_t lt_mask) {
+template <uint32_t DB, typename CT = uint32_t>
+__device__ __forceinline__ uint32_t wave_rank(uint32_t dig, bool valid, CT* wcw, uint64_t lt_mask) {
   uint64_t peers = __ballot(valid);
 #pragma unroll
   for (uint32_t bb = 0; bb < DB; ++bb) {
@@ -2200,7 +2200,7 @@ __device__ __forceinline__ uint32_t wave_rank(uint32_t dig, bool valid, uint32_t
   uint32_t r0 = 0;
   if (valid) r0 = wcw[dig];
   __builtin_amdgcn_wave_barrier();
-  if (valid && (peers & lt_mask) == 0) wcw[dig] = r0 + (uint32_t)__popcll(peers);
+  if (valid && (peers & lt_mask) == 0) wcw[dig] = (CT)(r0 + (uint32_t)__popcll(peers));
   __builtin_amdgcn_wave_barrier();
   return valid ? r0 + (uint32_t)__popcll(peers & lt_mask) : ~0u;
 }
@@ -2496,13 +2496,42 @@ __device__ unsigned long long* g_msd_stamps;
 #define SUX_MSD_STAMP_END() do {} while (0)
 #endif
 constexpr uint32_t kM16Chunk = 4096;      // pass A records per chunk (the run table's unit)
-constexpr uint32_t kM16Lo = 5;            // partitions per bucket: 32
-constexpr uint32_t kM16MaxChunks = 1024;  // chunks per map pass B's run table holds (4 Mi records)
+constexpr uint32_t kM16Lo = 4;            // partitions per bucket: 16
+constexpr uint32_t kM16MaxChunks = 512;   // chunks per map pass B's run table holds (2 Mi records)
 
-template <uint32_t NW, uint32_t DB>  // stage[CH] u32x4 (its first NW words double as wsum) | wc[NW][2^DB] u32
+// Block exclusive scan, in (digit, wave) order, of u16 per-wave digit counters wc[NW][NB]
+// (NW*64 threads; each thread owns E = NB/64 consecutive (digit, wave) entries).  Counts and
+// prefixes fit u16: a chunk holds kM16Chunk records.  Two barriers; wsum[NW] scratch.
+template <uint32_t NB, uint32_t NW>
+__device__ __forceinline__ void scan_digit_wave16(uint16_t* wc, uint32_t* wsum, int tid, int lane,
+                                                  int wave) {
+  constexpr uint32_t E = NB / kWave;
+  uint32_t sum = 0;  // the entries are read twice instead of held (registers are the limit)
+#pragma unroll
+  for (uint32_t k = 0; k < E; ++k) {
+    const uint32_t idx = (uint32_t)tid * E + k, d = idx / NW, w = idx % NW;
+    sum += wc[w * NB + d];
+  }
+  const uint32_t incl = wave_incl_scan(sum, lane);
+  if (lane == kWave - 1) wsum[wave] = incl;
+  __syncthreads();
+  uint32_t run = incl - sum;
+#pragma unroll
+  for (uint32_t w = 0; w < NW; ++w) run += w < (uint32_t)wave ? wsum[w] : 0u;
+#pragma unroll
+  for (uint32_t k = 0; k < E; ++k) {
+    const uint32_t idx = (uint32_t)tid * E + k, d = idx / NW, w = idx % NW;
+    const uint32_t v = wc[w * NB + d];
+    wc[w * NB + d] = (uint16_t)run;
+    run += v;
+  }
+  __syncthreads();
+}
+
+template <uint32_t NW, uint32_t DB>  // stage[CH] u32x4 (its first NW words double as wsum) | wc[NW][2^DB] u16
 struct M16a {
   static constexpr uint32_t NB = 1u << DB, NT = NW * kWave, PT = kM16Chunk / NT;
-  static constexpr uint32_t lds_bytes() { return kM16Chunk * 16 + NW * NB * 4; }
+  static constexpr uint32_t lds_bytes() { return kM16Chunk * 16 + NW * NB * 2; }
 };
 template <uint32_t NW, uint32_t PT>  // stage[CAP] u32x4 | wc[NW][64] | cur[64] | wsum[NW] | los[CAP] u8 | rp[MAXCH+1] u32 | ro[MAXCH] u16
 struct M16b {
@@ -2544,7 +2573,7 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16a(PartDev pd, MapGroup g, u
   constexpr uint32_t NB = K::NB, NT = K::NT, PT = K::PT, CH = kM16Chunk;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
   u32x4* stage = reinterpret_cast<u32x4*>(lds8);
-  uint32_t* wc = reinterpret_cast<uint32_t*>(stage + CH);  // [NW][NB]
+  uint16_t* wc = reinterpret_cast<uint16_t*>(stage + CH);  // [NW][NB]
   uint32_t* wsum = reinterpret_cast<uint32_t*>(lds8);       // only inside the scan: stage is idle
   const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
   const uint64_t lt_mask = (1ull << lane) - 1ull;
@@ -2589,10 +2618,10 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16a(PartDev pd, MapGroup g, u
         if (pids_out) pids_out[k.c0 + e] = (uint16_t)p;
       }
       h[j] = (p >> kM16Lo) & (NB - 1);
-      rank[j] = wave_rank<DB>(h[j], valid, wc + wave * NB, lt_mask);
+      rank[j] = wave_rank<DB, uint16_t>(h[j], valid, wc + wave * NB, lt_mask);
     }
     __syncthreads();
-    scan_digit_wave<NB, NW>(wc, wsum, tid, lane, wave);
+    scan_digit_wave16<NB, NW>(wc, wsum, tid, lane, wave);
 #pragma unroll
     for (uint32_t j = 0; j < PT; ++j)
       if (rank[j] != ~0u) stage[wc[wave * NB + h[j]] + rank[j]] = rv[j];
@@ -2612,7 +2641,7 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16a(PartDev pd, MapGroup g, u
 }
 
 // K2 of the MSD path: one workgroup (kScanThreads) per map.  Bucket totals over the map's chunks
-// (two thread groups of 512 buckets split the chunks), exclusive scan over buckets ->
+// (one thread per bucket), exclusive scan over buckets ->
 // segbase[m][h] (record index in the group's output), the index table's last entry and, at
 // world 1, the peer byte count.
 __global__ __launch_bounds__(kScanThreads) void k_msd16_scan(MapGroup g, uint32_t cpm, uint32_t nbk,
@@ -2622,7 +2651,7 @@ __global__ __launch_bounds__(kScanThreads) void k_msd16_scan(MapGroup g, uint32_
                                                              uint8_t* __restrict__ index_be,
                                                              uint64_t* __restrict__ peer_bytes,
                                                              int R) {
-  constexpr uint32_t HG = 512, NG = kScanThreads / HG;
+  constexpr uint32_t HG = 1024, NG = kScanThreads / HG;  // one thread per bucket (nbk <= 1024)
   __shared__ uint64_t sh[2 * kWave + 1];
   __shared__ uint32_t part[kScanThreads];
   const uint32_t m = blockIdx.x, tid = threadIdx.x;
@@ -2789,7 +2818,7 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
       const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
       const bool valid = e < n;
       lo[j] = valid ? digit(s, r[j]) : 0u;
-      rk[j] = wave_rank<kB16Lo>(lo[j], valid, wc + wave * NB, lt_mask);
+      rk[j] = wave_rank<kM16Lo>(lo[j], valid, wc + wave * NB, lt_mask);
     }
     __syncthreads();
     scan_digit_wave<NB, NW>(wc, wsum, tid, lane, wave);
@@ -3042,7 +3071,7 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
     // two 512-thread workgroups per CU in both passes: their load / rank / store phases
     // interleave (one prefetching 1024-thread workgroup measured slower: 9.4 vs 8.4 ms of
     // pass A per 17 GB step, and pass B spills; profiles/r02_sweeps/msd)
-    constexpr uint32_t NWA = 8, NWB = 8, PTB = 8;
+    constexpr uint32_t NWA = 8, NWB = 4, PTB = 8;
     timer_note(timer, kHist, "k_msd16a");
     timer_begin(timer, kHist, s);
     const uint32_t wpc = (uint32_t)tn.small_wgs_per_cu;
@@ -3061,7 +3090,8 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
     else if (kw == 3) SUX_M16A(3, DB);  \
     else SUX_M16A(4, DB);               \
   } while (0)
-    if (nbk > 256) SUX_M16AK(9);
+    if (nbk > 512) SUX_M16AK(10);
+    else if (nbk > 256) SUX_M16AK(9);
     else SUX_M16AK(8);
 #undef SUX_M16AK
 #undef SUX_M16A
@@ -3077,9 +3107,11 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
     if (e != hipSuccess) return e;
     timer_note(timer, kScatter, "k_msd16b");
     timer_begin(timer, kScatter, s);
-    const dim3 gb(std::min<uint32_t>(g.num_maps * nbk, ncu * wpc));
+    // pass B's 256-thread workgroups are half the size of pass A's: twice as many per CU
+    const dim3 gb(std::min<uint32_t>(g.num_maps * nbk, ncu * 2 * wpc));
     constexpr size_t ldsb = M16b<NWB, PTB>::lds_bytes();
-    static_assert(2 * ldsb <= 160 * 1024, "pass B: two workgroups per CU");
+    static_assert(4 * ldsb <= 160 * 1024, "pass B: four workgroups per CU");
+    static_assert(2 * M16a<NWA, 10>::lds_bytes() <= 160 * 1024, "pass A: two workgroups per CU");
 #define SUX_M16B(KW)                                                                               \
   do {                                                                                             \
     allow_lds(reinterpret_cast<const void*>(&k_msd16b<KW, NWB, PTB>), ldsb);                      \

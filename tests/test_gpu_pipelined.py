@@ -293,8 +293,10 @@ def test_line_carry_scatter_shapes(gpu_node, tuned, R, n, rpm, tile, tpi):
 @pytest.mark.parametrize("R,n,rpm,skew", [
     (10000, 3 * 131072 + 5000, 131072, None),   # 32 chunks per map, ragged last map
     (10000, 100000, 100000, "hot"),             # 30 % of the records in one partition
-    (8192, 70000, 20000, None),                 # 256 buckets: 8-bit pass A digits
-    (8193, 70000, 20000, None),                 # 257 buckets: 9-bit pass A digits
+    (4096, 70000, 20000, None),                 # 256 buckets: 8-bit pass A digits
+    (4097, 70000, 20000, None),                 # 257 buckets: 9-bit pass A digits
+    (8193, 70000, 20000, None),                 # 513 buckets: 10-bit pass A digits
+    (16384, 3 * 65536, 65536, None),            # 1024 buckets, the largest R
     (1025, 4096 * 3, 4096, "one"),              # whole chunks of one partition
     (3000, 1, 1, None),                         # a single record
 ])

@@ -3,7 +3,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I sparkucx_amd/csrc \
 //         -o tools/msd_stamps tools/msd_stamps.hip
 // Runs pass A + scan + pass B over 200 maps x 2^20 16-byte random records (Spark SQL murmur3 of
-// the int64 key, R = 10000) and prints the mean cycles per segment of each phase of pass B,
+// the int64 key, R = 10000, 16-partition buckets: 10-bit pass A digits) and prints the mean cycles per segment of each phase of pass B,
 // over every workgroup:
 //   0 load issue (run search)  1 rank + scan + stage (waits for the loads)  2 cursors + index
 //   3 place (LDS -> HBM)       4 run table of the next segment
@@ -54,7 +54,7 @@ int main(int argc, char** argv) {
   int64_t* idx;
   uint16_t* offs;
   uint64_t* segbase;
-  const uint32_t cpm = (uint32_t)(rpm / kM16Chunk), nbk = (R + 31) / 32;
+  const uint32_t cpm = (uint32_t)(rpm / kM16Chunk), nbk = (R + 15) / 16;
   CK(hipMalloc(&recs, n * S));
   CK(hipMalloc(&out, n * S));
   CK(hipMalloc(&tmp, n * S));
@@ -78,14 +78,14 @@ int main(int argc, char** argv) {
   g.rec_size = S;
   int ncu = 0;
   CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
-  const uint32_t gb = std::min<uint32_t>(maps * nbk, ncu * 2);
+  const uint32_t gb = std::min<uint32_t>(maps * nbk, ncu * 4);
   unsigned long long* st;
   CK(hipMalloc(&st, gb * 8 * 8));
   CK(hipMemset(st, 0, gb * 8 * 8));
   CK(hipMemcpyToSymbol(HIP_SYMBOL(g_msd_stamps), &st, sizeof st));
-  constexpr size_t lda = M16a<8, 9>::lds_bytes(), ldb = M16b<8, 8>::lds_bytes();
-  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_msd16a<2, 8, 9>), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lda));
-  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_msd16b<2, 8, 8>), hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldb));
+  constexpr size_t lda = M16a<8, 10>::lds_bytes(), ldb = M16b<4, 8>::lds_bytes();
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_msd16a<2, 8, 10>), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lda));
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_msd16b<2, 4, 8>), hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldb));
   hipEvent_t e0, e1, e2, e3;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -93,11 +93,11 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e3));
   for (int rep = 0; rep < 2; ++rep) {
     CK(hipEventRecord(e0, 0));
-    hipLaunchKernelGGL((k_msd16a<2, 8, 9>), dim3(std::min<uint32_t>(maps * cpm, ncu * 2)), dim3(512), lda, 0, pd, g, cpm, nbk, offs, (uint16_t*)nullptr, tmp);
+    hipLaunchKernelGGL((k_msd16a<2, 8, 10>), dim3(std::min<uint32_t>(maps * cpm, ncu * 2)), dim3(512), lda, 0, pd, g, cpm, nbk, offs, (uint16_t*)nullptr, tmp);
     CK(hipEventRecord(e1, 0));
     hipLaunchKernelGGL(k_msd16_scan, dim3(maps), dim3(kScanThreads), 0, 0, g, cpm, nbk, offs, segbase, idx, ibe, (uint64_t*)nullptr, (int)R);
     CK(hipEventRecord(e2, 0));
-    hipLaunchKernelGGL((k_msd16b<2, 8, 8>), dim3(gb), dim3(512), ldb, 0, pd, g, cpm, nbk, offs, segbase, tmp, out, idx, ibe);
+    hipLaunchKernelGGL((k_msd16b<2, 4, 8>), dim3(gb), dim3(256), ldb, 0, pd, g, cpm, nbk, offs, segbase, tmp, out, idx, ibe);
     CK(hipEventRecord(e3, 0));
     CK(hipDeviceSynchronize());
   }
