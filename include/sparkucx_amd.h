@@ -159,7 +159,9 @@ typedef struct sux_tuning {
   int32_t small_wgs_per_cu; /* two-level small-record kernels (small_kernel 4): workgroups per CU
                                of each pass, 1 or 2 (0: 2); 1 lets two launch groups' passes
                                share every CU                                                  */
-  int32_t reserved[11];
+  int32_t sort_msd;         /* reduce-side sort: 1 (0) one top-digit pass + per-bucket LDS sort
+                               when the buckets fit, 2 LSD digit passes only                   */
+  int32_t reserved[10];
 } sux_tuning;
 int sux_node_set_tuning(sux_node* node, const sux_tuning* tuning);
 /* Waits for the device, then reports (and clears) failures the kernels recorded in the node's

@@ -124,7 +124,7 @@ class UcxShuffleConf {
         "hist_stage", "s6_chunk", "tiles_per_item", "small_groups", "tile_records", "onepass",
         "varlen_kernel", "varlen_tile", "sort_max_digit_bits", "sort_gather", "sort_all_passes",
         "hist_wgs_per_cu", "small_kernel", "small_waves", "scatter_order",
-        "small_wgs_per_cu"};
+        "small_wgs_per_cu", "sort_msd"};
     sux_tuning t;
     std::memset(&t, 0, sizeof t);
     int32_t* f = reinterpret_cast<int32_t*>(&t);

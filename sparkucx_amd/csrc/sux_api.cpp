@@ -748,6 +748,7 @@ int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
     require(in(t->small_waves, {8, 16}), SUX_EINVAL, "small_waves must be 8 or 16");
     require(in(t->scatter_order, {1, 2}), SUX_EINVAL, "scatter_order must be 1 or 2");
     require(in(t->small_wgs_per_cu, {1, 2}), SUX_EINVAL, "small_wgs_per_cu must be 1 or 2");
+    require(in(t->sort_msd, {1, 2}), SUX_EINVAL, "sort_msd must be 1 or 2");
     require(in(t->s6_chunk, {256, 384, 512, 1024}), SUX_EINVAL, "s6_chunk must be 256..1024");
     require(t->tiles_per_item >= 0 && t->tiles_per_item <= 4096, SUX_EINVAL,
             "tiles_per_item must be 0..4096");
@@ -2460,8 +2461,56 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
   // 2.67 ms; profiles/r02_v14/sort_ab.txt) unless the node's tuning names one
   sux::Tuning sort_tn = resolve_tuning(node->tuning, false);
   if (node->tuning.small_kernel == 0) sort_tn.small_kernel = n <= (8ull << 20) ? 1 : 2;
+  // MSD finish: one stable digit pass over the top tb varying bits, then every bucket sorted in
+  // LDS by the lower varying digits (k_sort_local) — each pair crosses HBM twice after the top
+  // pass instead of twice per digit.  Needs the key span (not under graph capture) and buckets
+  // of <= kSortLocalCap pairs: the largest is read back (a second host wait); a skewed key set
+  // falls back to the LSD passes below, from the untouched pairs.
+  bool done = false;
+  int hb = -1;  // highest varying key bit
+  if (!run_all)
+    for (int b = 127; b >= 128 - bits && hb < 0; --b)
+      if (span_varies(span, b, b + 1)) hb = b;
+  if (!run_all && hb >= 0 && node->tuning.sort_msd != 2) {
+    int tb = kSortMinDigitBits;  // ~1024 pairs per bucket on average, at most 2^14 buckets
+    while (tb < 14 && (n >> tb) > 1024) ++tb;
+    const int top_lo = std::max(hb + 1 - tb, 128 - bits);
+    SortPlan P1;
+    sort_plan(n, record_size, P1, tb);
+    if ((n >> tb) <= sux::kSortLocalCap / 2 && P1.total <= ws_bytes) {
+      int64_t* index1 = reinterpret_cast<int64_t*>(ws + P1.index_off);
+      sux::PartDev pd1 = pd;
+      pd1.R = 1 << tb;
+      pd1.seed = top_lo;
+      P1.g.recs = pa;
+      P1.g.err = node->d_err;
+      hip_check(sux::launch_partition_group(pd1, P1.g, lay, pb, index1, nullptr, nullptr,
+                                            ws + P1.part_off, P1.ws, nullptr, sort_tn,
+                                            &node->timer, s),
+                "sort top digit pass");
+      uint64_t* d_max = reinterpret_cast<uint64_t*>(ws + P1.span_off + 32);
+      sux::SortDigits dg{};
+      hip_check(sux::launch_sort_local(nullptr, nullptr, index1, (uint32_t)pd1.R, dg, d_max, true, s),
+                "sort bucket max");
+      uint64_t maxb = 0;
+      hip_check(hipMemcpyAsync(&maxb, d_max, 8, hipMemcpyDeviceToHost, s), "sort bucket max");
+      hip_check(hipStreamSynchronize(s), "sort bucket max");
+      if (maxb <= sux::kSortLocalCap) {
+        dg.pad = (int32_t)maxb;
+        for (int sh = 128 - bits; sh < top_lo; sh += 8)
+          if (span_varies(span, sh, std::min(sh + 8, top_lo))) dg.push((uint32_t)sh);
+        if (dg.n) {
+          hip_check(sux::launch_sort_local(pb, pa, index1, (uint32_t)pd1.R, dg, nullptr, false, s),
+                    "sort buckets");
+        } else {
+          std::swap(pa, pb);  // the top digit held every varying bit
+        }
+        done = true;
+      }
+    }
+  }
   // the key occupies bits [128 - bits, 128) of the big-endian pair; least significant digit first
-  for (int sh = 128 - bits; sh < 128; sh += digit) {
+  for (int sh = 128 - bits; sh < 128 && !done; sh += digit) {
     if (!run_all && !span_varies(span, sh, sh + digit)) continue;  // identity pass
     pd.seed = sh;
     P.g.recs = pa;

@@ -200,6 +200,23 @@ constexpr uint32_t kSortSpanBlocks = 2048;
 constexpr uint64_t kSortSpanBytes = 4ull * 8 * (kSortSpanBlocks + 1);
 hipError_t launch_gather_records(const void* in, const void* pairs, uint64_t n, uint32_t rs,
                                  void* out, hipStream_t s);
+// MSD finish of the sort (sux_partition.hip): buckets of <= kSortLocalCap pairs sorted in LDS by
+// the listed 8-bit digits (shifts into the big-endian pair, least significant first); with
+// max_only, only the largest bucket (in pairs) is written to d_maxbucket.
+constexpr uint32_t kSortLocalCap = 4096;
+struct SortDigits {
+  uint64_t lo, hi;  // shift of digit d in byte d (lo: digits 0..7, hi: 8..15)
+  int32_t n;
+  int32_t pad;  // the largest bucket, in pairs (picks the kernel shape)
+  void push(uint32_t sh) {
+    if (n < 8) lo |= (uint64_t)sh << (8 * n);
+    else hi |= (uint64_t)sh << (8 * (n - 8));
+    ++n;
+  }
+};
+hipError_t launch_sort_local(const void* in_pairs, void* out_pairs, const int64_t* d_index,
+                             uint32_t R, const SortDigits& dg, uint64_t* d_maxbucket, bool max_only,
+                             hipStream_t s);
 
 // Generators (sux_gen.hip).
 hipError_t launch_generate(int kind, uint64_t seed, uint64_t first, uint64_t n,

@@ -194,8 +194,8 @@ JNIEXPORT jlongArray JNICALL FN(poolStats)(JNIEnv* env, jclass cls, jlong node) 
 }
 
 /* ---- kernel tuning table (sux_tuning) and the device error word ------------------------------
- * fields[] in the header's field order (hist_kernel .. small_wgs_per_cu); 0 keeps the default. */
-#define SUX_TUNING_FIELDS ((int)(sizeof(sux_tuning) / sizeof(int32_t)) - 11)
+ * fields[] in the header's field order (hist_kernel .. sort_msd); 0 keeps the default. */
+#define SUX_TUNING_FIELDS ((int)(sizeof(sux_tuning) / sizeof(int32_t)) - 10)
 JNIEXPORT void JNICALL FN(setTuning)(JNIEnv* env, jclass cls, jlong node, jintArray fields) {
   (void)cls;
   sux_tuning t;

@@ -218,3 +218,26 @@ def test_segmented_inline_small_records(gpu_node, nseg):
     torch.cuda.synchronize()
     exp = O.sort_segments(recs, rs, O.SORT_INT, 4, 4, seg)
     assert out.cpu().numpy()[: n * rs].tobytes() == exp.tobytes()
+
+
+@pytest.mark.parametrize("msd", [1, 2])
+@pytest.mark.parametrize("shape", ["terasort", "skewed_top", "long", "int_inline"])
+def test_msd_finish_and_lsd_agree_with_oracle(gpu_node, tuned, msd, shape):
+    """sort_msd 1: one top-digit pass + every bucket sorted in LDS (k_sort_local); 2: LSD digit
+    passes only.  'skewed_top': 60 % of the keys share their top bytes, so a bucket passes the
+    LDS capacity and the MSD path must fall back to the LSD passes from the untouched pairs."""
+    tuned(sort_msd=msd)
+    if shape == "terasort":
+        recs, rs, kind, off, klen = O.gen_terasort(61, 0, 700_000), 100, N.SORT_BYTES, 0, 10
+    elif shape == "skewed_top":
+        recs = O.gen_terasort(62, 0, 300_000).reshape(-1, 100)
+        recs[: 180_000, :4] = 9
+        recs, rs, kind, off, klen = recs.ravel(), 100, N.SORT_BYTES, 0, 10
+    elif shape == "long":
+        recs, rs, kind, off, klen = O.gen_small(63, 0, 500_000), 16, N.SORT_LONG, 0, 8
+    else:
+        recs, rs, kind, off, klen = O.gen_small(64, 0, 400_000), 16, N.SORT_INT, 8, 4
+    okind = {N.SORT_BYTES: O.SORT_BYTES, N.SORT_LONG: O.SORT_LONG, N.SORT_INT: O.SORT_INT}[kind]
+    got = gpu_sort(gpu_node, recs, rs, kind, off, klen)
+    assert got.tobytes() == O.sort_records(recs, rs, okind, off, klen).tobytes()
+    gpu_node.check()
