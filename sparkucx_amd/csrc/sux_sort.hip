@@ -192,15 +192,31 @@ __global__ __launch_bounds__(256) void k_span_reduce(const uint32_t* __restrict_
   if (threadIdx.x < 6) span[threadIdx.x] = red[0][threadIdx.x];
 }
 
+// One output dword per thread and step: record j = d / W, dword w of it, read from the record
+// the pair names.  When n * W < 2^32 the division is a 32-bit multiply-high by ceil(2^32 / W)
+// plus one correction (the quotient is exact or one too big), not a 64-bit division; only the
+// pair's index word is loaded.
 __global__ __launch_bounds__(256) void k_gather_records(const uint32_t* __restrict__ in,
                                                         const u32x4* __restrict__ pairs,
-                                                        uint64_t n, uint32_t W,
+                                                        uint64_t n, uint32_t W, uint32_t magic,
                                                         uint32_t* __restrict__ out) {
   const uint64_t total = n * W;
+  const uint32_t* idx = reinterpret_cast<const uint32_t*>(pairs) + 3;  // pairs[j][3]
+  if (magic) {
+    const uint32_t t32 = (uint32_t)total;
+    for (uint32_t d = blockIdx.x * 256u + threadIdx.x; d < t32; d += gridDim.x * 256u) {
+      uint32_t j = __umulhi(d, magic);
+      if (j * W > d) --j;
+      const uint32_t w = d - j * W;
+      const uint32_t src = idx[4ull * j];
+      out[d] = in[(uint64_t)src * W + w];
+    }
+    return;
+  }
   for (uint64_t d = (uint64_t)blockIdx.x * 256 + threadIdx.x; d < total;
        d += (uint64_t)gridDim.x * 256) {
     const uint64_t j = d / W, w = d - j * W;
-    const uint32_t src = pairs[j][3];
+    const uint32_t src = idx[4 * j];
     out[d] = in[(uint64_t)src * W + w];
   }
 }
@@ -235,9 +251,13 @@ hipError_t launch_gather_records(const void* in, const void* pairs, uint64_t n, 
   if (n == 0) return hipSuccess;
   const uint64_t total = n * (rs / 4);
   const uint64_t blocks = std::min<uint64_t>((total + 255) / 256, 256ull * 32);
+  const uint32_t W = rs / 4;
+  // ceil(2^32 / W): the 32-bit quotient path when every output dword index fits 32 bits
+  const uint32_t magic = total + W < (1ull << 32) && W > 1
+                             ? (uint32_t)(((1ull << 32) + W - 1) / W) : 0u;
   hipLaunchKernelGGL(k_gather_records, dim3((uint32_t)blocks), dim3(256), 0, s,
-                     static_cast<const uint32_t*>(in), static_cast<const u32x4*>(pairs), n,
-                     rs / 4, static_cast<uint32_t*>(out));
+                     static_cast<const uint32_t*>(in), static_cast<const u32x4*>(pairs), n, W,
+                     magic, static_cast<uint32_t*>(out));
   return hipGetLastError();
 }
 
