@@ -144,7 +144,7 @@ typedef struct sux_tuning {
   int32_t small_groups;     /* k_scatter16b record groups per turn: 1, 2, 4                       */
   int32_t tile_records;     /* K1 tile: power of two in [64, 2^22] (0: 4096, or more for big R)  */
   int32_t onepass;          /* 1: the one-pass kernel whenever a map batch fits on chip          */
-  int32_t varlen_kernel;    /* variable-length rows: 1, 2, 3 (128-B line image)                  */
+  int32_t varlen_kernel;    /* variable-length rows: 1, 2, 3 (128-B line image; 0: 3)            */
   int32_t varlen_tile;      /* variable-length K1 tile: multiple of 64 in [64, 65536]            */
   int32_t sort_max_digit_bits; /* widest radix digit of sux_sort_records: 8 .. 16                */
   int32_t sort_gather;      /* 1: records gathered after the sort instead of riding in the pairs */

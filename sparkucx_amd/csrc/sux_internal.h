@@ -51,7 +51,7 @@ struct Tuning {
   int small_groups = 4;     // k_scatter16b record groups per turn: 1 | 2 | 4
   int tile_records = 0;     // K1 tile override (0: choose_tile_recs's rule)
   bool onepass = false;     // the one-pass kernel when a map batch fits on chip
-  int varlen_kernel = 2;    // variable-length rows: 1 | 2 | 3 (line image)
+  int varlen_kernel = 3;    // variable-length rows: 1 | 2 | 3 (line image; default: 1055 vs 840 GB/s)
   int varlen_tile = 0;      // variable-length K1 tile override
 };
 
