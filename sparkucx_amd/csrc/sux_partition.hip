@@ -2595,10 +2595,11 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16a(PartDev pd, MapGroup g, u
     return k;
   };
   auto load = [&](const Item& k, u32x4 (&r)[PT]) {
+    if (k.n == 0) return;
 #pragma unroll
-    for (uint32_t j = 0; j < PT; ++j) {
+    for (uint32_t j = 0; j < PT; ++j) {  // unconditional (clamped) loads: no per-load wait
       const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
-      if (e < k.n) r[j] = recs[k.c0 + e];
+      r[j] = recs[k.c0 + min(e, k.n - 1)];
     }
   };
   for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
@@ -2780,13 +2781,17 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
   // loads of segment elements [e0, min(T, e0 + CAP)) in wave-contiguous order
   auto load = [&](const Seg& s, uint32_t e0, u32x4 (&r)[PT]) {
     const uint32_t lim = min(s.T, e0 + CAP);
-    // run of element e = the largest c with rp[c] <= e: a branch-free search whose PT lookups
-    // interleave step by step (rp[nch] = T > e stops every search inside the segment)
+    if (lim <= e0) return;
+    // element e's run = the largest c with rp[c] <= e: a branch-free search whose PT lookups
+    // interleave step by step (rp[nch] = T > e stops every search inside the segment).  Lanes
+    // past the piece re-read its last element: the loads are unconditional — a load under a
+    // branch made the compiler wait for every earlier load before the next one's address
+    // (s_waitcnt vmcnt(0) per element), serialising the gather.
     uint32_t lo[PT], ev[PT];
 #pragma unroll
     for (uint32_t j = 0; j < PT; ++j) {
       lo[j] = 0;
-      ev[j] = e0 + wave * (PT * kWave) + j * kWave + lane;
+      ev[j] = min(e0 + wave * (PT * kWave) + j * kWave + lane, lim - 1);
     }
 #pragma unroll
     for (uint32_t step = MC / 2; step; step >>= 1) {
@@ -2796,16 +2801,14 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
 #pragma unroll
       for (uint32_t j = 0; j < PT; ++j) lo[j] = v[j] <= ev[j] ? min(lo[j] + step, s.nch) : lo[j];
     }
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j) {
 #ifdef SUX_MSD_LINEAR  // diagnostic (tools/msd_stamps): contiguous in-map reads, wrong data
-#pragma unroll
-    for (uint32_t j = 0; j < PT; ++j)
-      if (ev[j] < lim) r[j] = t4[s.mbase + ((uint64_t)s.h * 3350 + ev[j]) % s.len];
+      r[j] = t4[s.mbase + ((uint64_t)s.h * 3350 + ev[j]) % s.len];
 #else
-#pragma unroll
-    for (uint32_t j = 0; j < PT; ++j)
-      if (ev[j] < lim)
-        r[j] = t4[s.mbase + (uint64_t)lo[j] * kM16Chunk + ro[lo[j]] + (ev[j] - rp[lo[j]])];
+      r[j] = t4[s.mbase + (uint64_t)lo[j] * kM16Chunk + ro[lo[j]] + (ev[j] - rp[lo[j]])];
 #endif
+    }
   };
   auto digit = [&](const Seg& s, const u32x4& r) {
     return (m16_pid<KW>(pd, r, kw0) - (s.h << kM16Lo)) & (NB - 1);
@@ -2954,9 +2957,9 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 6) void k_sort_local(const u
     if (n == 0 || n > CAP) continue;  // (the host never passes a bucket above CAP)
     u32x4 v[PT];
 #pragma unroll
-    for (uint32_t j = 0; j < PT; ++j) {
+    for (uint32_t j = 0; j < PT; ++j) {  // unconditional (clamped) loads: no per-load wait
       const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
-      if (e < n) v[j] = in[s0 + e];
+      v[j] = in[s0 + min(e, n - 1)];
     }
 #pragma unroll 1
     for (int d = 0; d < (n > 1 ? dg.n : 0); ++d) {
