@@ -453,9 +453,11 @@ __global__ __launch_bounds__(1024) void k_vscatter3(VarGroup g, int R, int pid_b
     const vu32x4* src = reinterpret_cast<const vu32x4*>(a - head);
     const uint32_t ext = any ? (uint32_t)min(kend - o0 - k.w, (uint64_t)kV3Bytes) : 0u;
     const uint32_t units = ext ? (head + ext + 15) >> 4 : 0u;
+    // unconditional (clamped) loads: a load under a per-lane branch makes the compiler wait for
+    // the earlier ones before the next (k_msd16b measured: 2.5x the issue time)
+    if (units == 0) return;
 #pragma unroll
-    for (uint32_t k2 = 0; k2 < PER; ++k2)
-      if (tid + k2 * NT < units) v[k2] = src[tid + k2 * NT];
+    for (uint32_t k2 = 0; k2 < PER; ++k2) v[k2] = src[min(tid + k2 * NT, units - 1)];
   };
 
   uint64_t pos = 0;  // owner: p's output cursor (bytes)
