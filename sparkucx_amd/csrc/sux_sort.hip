@@ -33,11 +33,16 @@ __device__ inline u32x4 make_pair(const uint8_t* __restrict__ in, uint64_t i, ui
   const uint8_t* r = in + i * rs + key_offset;
   uint8_t kb[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   if (kind == 1 && (key_offset & 3) == 0) {  // unsigned bytes, dword-aligned: dword loads
+    // all three loads issued unconditionally (the key's last dword repeated when shorter), then
+    // bytes picked with constant indices: a load per loop trip made every record wait for its
+    // previous key dword
     const uint32_t* r4 = reinterpret_cast<const uint32_t*>(r);
-    for (int q = 0; q < (key_len + 3) / 4; ++q) {
-      const uint32_t w = r4[q];
-      for (int k = 0; k < 4 && 4 * q + k < key_len; ++k) kb[4 * q + k] = (uint8_t)(w >> (8 * k));
-    }
+    const int nd = (key_len + 3) / 4;
+    uint32_t w[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) w[q] = r4[q < nd ? q : nd - 1];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) kb[k] = k < key_len ? (uint8_t)(w[k / 4] >> (8 * (k % 4))) : 0u;
   } else if (kind == 1) {  // unsigned lexicographic bytes
     for (int k = 0; k < key_len; ++k) kb[k] = r[k];
   } else {          // signed little-endian int64 (2) / int32 (3): big-endian, sign bit flipped
