@@ -2755,8 +2755,9 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
     Seg s = seg(it);
     s.out = pre.sb;
     uint32_t carry = 0;
-    // c0 <= nch: the thread with c == nch writes rp[nch] = T, the search's sentinel
-    for (uint32_t c0 = 0; c0 <= s.nch; c0 += NT) {
+    // the last batch's thread 0 also writes rp[nch] = T, the search's sentinel (no extra batch
+    // when nch is a multiple of the workgroup: 2^20-record maps have exactly 256 chunks)
+    for (uint32_t c0 = 0; c0 < s.nch; c0 += NT) {
       const uint32_t c = c0 + (uint32_t)tid;
       uint32_t o = pre.o, e = pre.e;
       if (c0 && c < s.nch) run_ends(s, c, o, e);
@@ -2770,8 +2771,11 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
         run += w < (uint32_t)wave ? wsum[w] : 0u;
         blk += wsum[w];
       }
-      if (c < s.nch) ro[c] = (uint16_t)o;
-      if (c <= s.nch) rp[c] = run;
+      if (c < s.nch) {
+        ro[c] = (uint16_t)o;
+        rp[c] = run;
+      }
+      if (tid == 0 && c0 + NT >= s.nch) rp[s.nch] = carry + blk;
       carry += blk;
       __syncthreads();
     }
