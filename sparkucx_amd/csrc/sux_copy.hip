@@ -31,9 +31,20 @@ __global__ __launch_bounds__(kCopyThreads) void k_gather_copy(const CopyDesc* __
   uint8_t* dst = d.dst + beg;
   const uintptr_t mis = ((uintptr_t)src | (uintptr_t)dst | (uintptr_t)len);
   if ((mis & 15) == 0) {
+    // four 16-byte loads in flight per lane before their stores (one at a time leaves the copy
+    // latency-bound: a load, a wait, a store, per 4 KiB of the chunk)
     const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
     u32x4* d4 = reinterpret_cast<u32x4*>(dst);
-    for (uint64_t k = threadIdx.x; k < len / 16; k += kCopyThreads) d4[k] = s4[k];
+    const uint64_t n16 = len / 16;
+    uint64_t k = threadIdx.x;
+    for (; k + 3 * kCopyThreads < n16; k += 4 * kCopyThreads) {
+      u32x4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = s4[k + u * kCopyThreads];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) d4[k + u * kCopyThreads] = v[u];
+    }
+    for (; k < n16; k += kCopyThreads) d4[k] = s4[k];
   } else if ((mis & 3) == 0) {
     const uint32_t* s1 = reinterpret_cast<const uint32_t*>(src);
     uint32_t* d1 = reinterpret_cast<uint32_t*>(dst);
@@ -122,7 +133,15 @@ __global__ __launch_bounds__(256) void k_pull(int32_t W, int32_t me, const uint6
   const bool al4 = (((uintptr_t)src | (uintptr_t)dst) & 3) == 0;
   const uint64_t n16 = al4 ? size / 16 : 0, n4 = al4 ? size / 4 : 0;
   const uint64_t t0 = (uint64_t)slot * 256 + threadIdx.x, step = (uint64_t)per_src * 256;
-  for (uint64_t i = t0; i < n16; i += step)
+  uint64_t i = t0;
+  for (; i + 3 * step < n16; i += 4 * step) {  // four loads in flight per lane (xGMI latency)
+    u32x4a4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const u32x4a4*>(src + 16 * (i + u * step));
+#pragma unroll
+    for (int u = 0; u < 4; ++u) *reinterpret_cast<u32x4a4*>(dst + 16 * (i + u * step)) = v[u];
+  }
+  for (; i < n16; i += step)
     *reinterpret_cast<u32x4a4*>(dst + 16 * i) = *reinterpret_cast<const u32x4a4*>(src + 16 * i);
   for (uint64_t i = n16 * 4 + t0; i < n4; i += step)
     *reinterpret_cast<uint32_t*>(dst + 4 * i) = *reinterpret_cast<const uint32_t*>(src + 4 * i);
