@@ -528,6 +528,7 @@ sux::Tuning resolve_tuning(const sux_tuning& t, bool pipelined) {
   if (t.varlen_kernel) r.varlen_kernel = t.varlen_kernel;
   r.varlen_tile = t.varlen_tile;
   r.small_kernel = t.small_kernel ? t.small_kernel : kDefaultSmallKernel;
+  r.small_auto = t.small_kernel == 0;
   if (t.small_waves) r.small_waves = t.small_waves;
   r.scatter_order = t.scatter_order;
   if (t.small_wgs_per_cu) r.small_wgs_per_cu = t.small_wgs_per_cu;

@@ -46,6 +46,8 @@ struct Tuning {
   int small_waves = 8;      // two-pass small-record kernels: waves per workgroup (8 | 16)
   int scatter_order = 0;    // k_scatter8 tile order: 1 contiguous ranges, 2 block-cyclic per XCD
   int small_wgs_per_cu = 2; // k_msd16a / k_msd16b workgroups per CU (1: two groups share a CU)
+  bool small_auto = true;   // small_kernel left to the default: the MSD path only when its
+                            // segments are long enough to pay for their fixed cost
   int s6_chunk = 1024;      // k_scatter6 largest chunk
   int tiles_per_item = 0;   // k_scatter6/7 tiles per work item (0: 8 chunks' worth)
   int small_groups = 4;     // k_scatter16b record groups per turn: 1 | 2 | 4

@@ -3161,6 +3161,11 @@ static bool msd16_eligible(const PartDev& pd, const MapGroup& g, const LayoutDes
     return false;
   const uint64_t cpm = (g.records_per_map + kM16Chunk - 1) / kM16Chunk;
   const uint64_t nbk = ((uint64_t)pd.R + (1u << kM16Lo) - 1) >> kM16Lo;
+  // by default only when a (map, bucket) segment holds >= 1024 records on average: a segment
+  // costs ~6 us of run table, search and barriers whatever its size, so short maps run the
+  // sorted-chunk scatter instead (64 Ki-record maps at R = 10 000: 105-record segments, 194 vs
+  // 507 GB/s; 2^20-record maps: 1677-record segments, 1027 vs 750 GB/s)
+  if (tn.small_auto && g.records_per_map < 1024 * nbk) return false;
   return cpm >= 1 && cpm <= kM16MaxChunks && ws.tmp_bytes >= g.num_records * 16 &&
          (uint64_t)g.num_maps * cpm * nbk * 2 <= ws.counts_bytes &&
          (uint64_t)g.num_maps * nbk * 8 <= ws.totals_bytes;

@@ -343,3 +343,19 @@ def test_msd16_falls_back_for_the_exchange_layout(gpu_node, tuned):
     assert host(index).tolist() == want_index.tolist()
     assert host(peer).tolist() == want_peer.tolist()
     gp.close()
+
+
+@pytest.mark.parametrize("rpm,want", [(65536, "k_scatter16s"), (655360, "k_msd16b")])
+def test_default_small_kernel_picks_by_segment_length(gpu_node, rpm, want):
+    """Default tuning: the two-level path only when a (map, 16-partition bucket) segment holds
+    >= 1024 records on average (R = 10 000: maps of >= 640 000 records); shorter maps take the
+    sorted-chunk scatter.  Both bit-exact."""
+    n = 2 * rpm + 12345
+    recs = O.gen_small(43, 0, n)
+    opart = O.Partitioner(O.MURMUR3_LONG, 10000, 0, 8, seed=42)
+    gp = gpu_part(gpu_node, opart)
+    out, index, index_be = gpu_node.partition_maps(gp, torch.from_numpy(recs).cuda(), 16, rpm)
+    torch.cuda.synchronize()
+    expect(opart, recs, 16, rpm, out, index, index_be)
+    assert gpu_node.kernel_variant(2) == want
+    gp.close()
