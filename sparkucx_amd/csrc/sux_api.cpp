@@ -2473,8 +2473,10 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
     for (int b = 127; b >= 128 - bits && hb < 0; --b)
       if (span_varies(span, b, b + 1)) hb = b;
   if (!run_all && hb >= 0 && node->tuning.sort_msd != 2) {
-    int tb = kSortMinDigitBits;  // ~1024 pairs per bucket on average, at most 2^14 buckets
-    while (tb < 14 && (n >> tb) > 1024) ++tb;
+    // at most ~1536 pairs per bucket on average (fewer, fuller buckets: the per-bucket barriers
+    // of the LDS sort are paid fewer times), at most 2^14 buckets
+    int tb = kSortMinDigitBits;
+    while (tb < 14 && (n >> tb) > 1536) ++tb;
     const int top_lo = std::max(hb + 1 - tb, 128 - bits);
     SortPlan P1;
     sort_plan(n, record_size, P1, tb);

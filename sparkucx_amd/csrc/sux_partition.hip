@@ -2941,7 +2941,7 @@ struct SortLocal {
 // <8 waves, 4096 pairs>: two workgroups per CU; <4 waves, 1024 pairs>: six per CU, for the
 // ~600-pair buckets of a 5 M-record reduce partition
 template <uint32_t NW, uint32_t CAP>
-__global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 6) void k_sort_local(const u32x4* __restrict__ in,
+__global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : CAP == 1024 ? 6 : 4) void k_sort_local(const u32x4* __restrict__ in,
                                                         u32x4* __restrict__ out,
                                                         const int64_t* __restrict__ index,
                                                         uint32_t R, SortDigits dg) {
@@ -3027,6 +3027,12 @@ hipError_t launch_sort_local(const void* in_pairs, void* out_pairs, const int64_
   if (dg.pad <= 1024) {
     constexpr size_t lds = SortLocal<4, 1024>::lds_bytes();
     hipLaunchKernelGGL((k_sort_local<4, 1024>), dim3(std::min<uint32_t>(R, 6 * ncu)), dim3(4 * kWave),
+                       lds, s, static_cast<const u32x4*>(in_pairs), static_cast<u32x4*>(out_pairs),
+                       d_index, R, dg);
+  } else if (dg.pad <= 2048) {
+    constexpr size_t lds = SortLocal<4, 2048>::lds_bytes();
+    static_assert(4 * lds <= 160 * 1024, "four workgroups per CU");
+    hipLaunchKernelGGL((k_sort_local<4, 2048>), dim3(std::min<uint32_t>(R, 4 * ncu)), dim3(4 * kWave),
                        lds, s, static_cast<const u32x4*>(in_pairs), static_cast<u32x4*>(out_pairs),
                        d_index, R, dg);
   } else {
