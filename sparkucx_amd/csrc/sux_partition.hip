@@ -1402,7 +1402,8 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
                                                      const uint16_t* __restrict__ pids,
                                                      const uint32_t* __restrict__ prefix,
                                                      const uint64_t* __restrict__ base,
-                                                     uint8_t* __restrict__ out, uint32_t cyc) {
+                                                     uint8_t* __restrict__ out, uint32_t cyc,
+                                                     uint32_t tw0, uint32_t tw1) {
   using K = Sc8<S, C, NW>;
   constexpr uint32_t NT = K::NT, W = K::W, RPW = K::RPW, NG = K::NG, PER = K::kPer;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
@@ -1443,9 +1444,10 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
     lo = span_lo + (uint32_t)((uint64_t)span_n * k / (nblk));
     hi = span_lo + (uint32_t)((uint64_t)span_n * (k + 1) / (nblk));
   };
-  if (cyc == 0) {
-    t_lo = (uint32_t)((uint64_t)T * rr / G);
-    t_hi = (uint32_t)((uint64_t)T * (rr + 1) / G);
+  if (cyc == 0) {  // the launch's tile window [tw0, tw1) (the whole group unless windowed)
+    const uint32_t TW = tw1 - tw0;
+    t_lo = tw0 + (uint32_t)((uint64_t)TW * rr / G);
+    t_hi = tw0 + (uint32_t)((uint64_t)TW * (rr + 1) / G);
   } else {
     const uint32_t grp = rr / cyc, members = min(cyc, G - grp * cyc);
     span_lo = (uint32_t)((uint64_t)T * (grp * cyc) / G);
@@ -3079,6 +3081,10 @@ uint32_t choose_tile_recs(uint32_t R, uint32_t rec_size, uint64_t records_per_ma
   // needs >> 256 tiles)
   if (small_two_pass_shape(R, rec_size) && tn.small_kernel == 2) t = 32768;
   if (small_two_pass_shape(R, rec_size) && tn.small_kernel == 3) t = 32768;
+  // very long maps: longer tiles, so that a map has <= 2048 of them — k_tile_scan gives one wave
+  // to each (map, partition) row of tile counts, and a 2^27-record map at 4096-record tiles has
+  // 32768 per row (3.9 ms of scan per 13.4 GB launch group, profiles/r02_configs)
+  while (t < (1u << 16) && (records_per_map + t - 1) / t > 2048) t <<= 1;
   const uint32_t v = (uint32_t)tn.tile_records;  // tuning override (power of two, >= 64)
   if (v >= 64 && (v & (v - 1)) == 0) t = v;
   // no point in tiles longer than a map
@@ -3504,8 +3510,19 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
     (void)tiles_per_wg;  // block-cyclic measured slower for 2^20 and 2^27-record maps alike
     const bool cyc = tn.scatter_order == 2;
     const uint32_t per_xcd = std::max<uint32_t>(1, grid.x / 8);
-    hipLaunchKernelGGL((k_scatter8<100, 1024, 16>), grid, dim3(1024), lds8b, s, g, R, bits, pids,
-                       counts, base, d_out, cyc ? per_xcd : 0u);
+    // a launch group whose output passes ~4 GB (one 2^27-record map is 13.4 GB) is scattered in
+    // tile windows, one launch each: at any time the grid then writes into a quarter of every
+    // partition's region instead of spreading its 256 x R write streams over the whole output
+    const uint32_t T = g.num_maps * g.tiles_per_map;
+    const uint64_t out_bytes = g.num_records * (uint64_t)S;
+    const uint32_t nwin = cyc ? 1u : (uint32_t)std::min<uint64_t>(
+                                        std::max<uint64_t>(1, (out_bytes + (4ull << 30) - 1) >> 32), T);
+    for (uint32_t w = 0; w < nwin; ++w) {
+      const uint32_t tw0 = (uint32_t)((uint64_t)T * w / nwin), tw1 = (uint32_t)((uint64_t)T * (w + 1) / nwin);
+      const dim3 gw(std::min<uint32_t>(tw1 - tw0, ncu));
+      hipLaunchKernelGGL((k_scatter8<100, 1024, 16>), gw, dim3(1024), lds8b, s, g, R, bits, pids,
+                         counts, base, d_out, cyc ? per_xcd : 0u, tw0, tw1);
+    }
     e = hipGetLastError();
   } else if (v7) {
     timer_note(timer, kScatter, "k_scatter7");
