@@ -1471,7 +1471,14 @@ int sux_exchange_group(sux_node* node, const void* d_send, const int64_t* d_inde
     node->bind();
     hipStream_t s = node->stream(stream);
     const size_t per_rank = (size_t)M * (R + 1);
-    std::vector<int64_t> host(per_rank * W);
+    // pinned staging (node->hpool): the read-back is a true async copy, not a pageable bounce
+    auto hb = node->hpool.get(per_rank * W * 8);
+    struct Put {
+      HostPool& hp;
+      std::pair<void*, uint64_t> b;
+      ~Put() { hp.put(b); }
+    } put{node->hpool, hb};
+    int64_t* host = static_cast<int64_t*>(hb.first);
     if (!node->comm) {
       hip_check(hipMemcpyAsync(d_gathered, d_index, per_rank * 8, hipMemcpyDeviceToDevice, s),
                 "copy index");
@@ -1479,11 +1486,11 @@ int sux_exchange_group(sux_node* node, const void* d_send, const int64_t* d_inde
       nccl_check(ncclAllGather(d_index, d_gathered, per_rank, ncclInt64, node->comm, s),
                  "ncclAllGather(index)");
     }
-    hip_check(hipMemcpyAsync(host.data(), d_gathered, host.size() * 8, hipMemcpyDeviceToHost, s),
+    hip_check(hipMemcpyAsync(host, d_gathered, per_rank * W * 8, hipMemcpyDeviceToHost, s),
               "D2H gathered index");
     hip_check(hipStreamSynchronize(s), "sync gathered index");
     std::vector<uint64_t> sc(W), sd(W), rc(W), rd(W);
-    int rc_plan = sux_plan_group(W, rank, M, R, host.data(), sc.data(), sd.data(), rc.data(),
+    int rc_plan = sux_plan_group(W, rank, M, R, host, sc.data(), sd.data(), rc.data(),
                                  rd.data());
     require(rc_plan == SUX_OK, rc_plan, g_err);
     uint64_t total = rd[W - 1] + rc[W - 1];
