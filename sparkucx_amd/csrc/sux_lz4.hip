@@ -56,10 +56,15 @@ __device__ __forceinline__ uint32_t ld32u(const uint8_t* p) {
 
 // Wave-cooperative copy of n bytes, any alignment on either side: byte stores up to dst's first
 // dword boundary, dword stores for the body (source funnel-shifted), byte stores for the tail.
+// The head and tail bytes are loaded up front (clamped, unconditional), so their loads share the
+// body's first round trip instead of taking one each.
 __device__ __forceinline__ void wave_copy(uint8_t* dst, const uint8_t* src, uint32_t n, int lane) {
+  if (n == 0) return;
   const uint32_t head = min(n, (uint32_t)((4u - (reinterpret_cast<uintptr_t>(dst) & 3u)) & 3u));
-  if ((uint32_t)lane < head) dst[lane] = src[lane];
   const uint32_t nd = (n - head) / 4u;
+  const uint32_t done = head + 4u * nd;
+  const uint8_t hb = src[min((uint32_t)lane, n - 1u)];
+  const uint8_t tb = src[min(done + (uint32_t)lane, n - 1u)];
   uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + head);
   const uint8_t* s = src + head;
   uint32_t k = lane;
@@ -71,8 +76,8 @@ __device__ __forceinline__ void wave_copy(uint8_t* dst, const uint8_t* src, uint
     for (int u = 0; u < 4; ++u) d32[k + u * kLWave] = v[u];
   }
   for (; k < nd; k += kLWave) d32[k] = ld32u(s + 4u * k);
-  const uint32_t done = head + 4u * nd;
-  if ((uint32_t)lane < n - done) dst[done + lane] = src[done + lane];
+  if ((uint32_t)lane < head) dst[lane] = hb;
+  if ((uint32_t)lane < n - done) dst[done + lane] = tb;
 }
 
 __device__ __forceinline__ uint32_t ext_bytes(uint32_t v) { return v >= 15u ? (v - 15u) / 255u + 1u : 0u; }
@@ -203,20 +208,21 @@ __global__ __launch_bounds__(kLz4Waves * kLWave) void k_lz4_default(
       uint32_t anchor = 0, op = 0, ip = 1, match = 0;
       bool last = false;  // go to the last literals
       // ---- find a match from ip (liblz4's do-while search), 64 probes per round
-      auto search = [&]() -> bool {  // true: (ip, match) is a match; false: last literals
-        uint32_t q0 = ip, probe0 = 0;
+      // The words at a round's probes are loaded one round early (probe positions do not depend
+      // on the table); pre holds round 0's, the words at ip + lane.
+      auto search = [&](uint32_t pre) -> bool {  // true: (ip, match) is a match; false: last literals
+        uint32_t q0 = ip, r = 0, seq = pre;
         while (true) {
-          const uint32_t i = probe0 + (uint32_t)lane;
-          const uint32_t s = i == 0 ? 1u : (63u + i) >> 6;
-          uint32_t incl = s;
-#pragma unroll
-          for (int d = 1; d < kLWave; d <<= 1) {
-            const uint32_t t = (uint32_t)__shfl_up((int)incl, d, kLWave);
-            if (lane >= d) incl += t;
-          }
-          const uint32_t q = q0 + incl - s, nxt = q + s;
+          // probe i = 64 r + lane steps by (i == 0 ? 1 : (63 + i) >> 6): r + 1 on lanes >= 1 and
+          // s0 = max(r, 1) on lane 0, so the prefix of the steps has a closed form
+          const uint32_t s0 = r ? r : 1u;
+          const uint32_t s = lane ? r + 1u : s0;
+          const uint32_t q = lane ? q0 + s0 + ((uint32_t)lane - 1u) * (r + 1u) : q0, nxt = q + s;
           const bool live = nxt <= mflimit1;  // monotone over the lanes
-          const uint32_t seq = ld32u(src + (live ? q : 0u));
+          const uint32_t q0n = q0 + s0 + 63u * (r + 1u);  // the next round's first probe
+          const uint32_t qn = lane ? q0n + (r + 1u) + ((uint32_t)lane - 1u) * (r + 2u) : q0n;
+          // clamped: a live probe of the next round lies below mflimit1, so it reads its own word
+          const uint32_t seqn = ld32u(src + min(qn, len - 4u));
           const uint32_t h = lz4_hash(seq);
           uint64_t peers = __ballot(live);
 #pragma unroll
@@ -244,36 +250,51 @@ __global__ __launch_bounds__(kLz4Waves * kLWave) void k_lz4_default(
             return true;
           }
           if (~lives) return false;  // a probe's successor passed mflimitPlusOne
-          q0 = (uint32_t)__shfl((int)nxt, kLWave - 1, kLWave);
-          probe0 += kLWave;
+          q0 = q0n;
+          ++r;
+          seq = seqn;
         }
       };
-      // emits one sequence (literals [anchor, ip) + the match at ip); false = the block cannot be
-      // shorter than the chunk (stored raw)
-      auto sequence = [&]() -> bool {
-        // forward count (LZ4_count): equal bytes from ip + 4 / match + 4 up to matchlimit
+      // LZ4_count: equal bytes from p + 4 / mt + 4 up to matchlimit, 4 per lane per round.  The
+      // first round's loads come from cnt_load, issued by the caller next to other loads (one
+      // memory round trip for both); the addresses stay in the chunk (a round starts at or before
+      // matchlimit), so the loads are unconditional.
+      auto cnt_load = [&](uint32_t p, uint32_t mt, uint32_t mc) -> uint32_t {
+        const uint32_t a = p + 4u + mc;
+        const uint32_t lim = matchlimit > a ? matchlimit - a : 0u;
+        const uint32_t o = 4u * (uint32_t)lane < lim ? 4u * (uint32_t)lane : 0u;
+        return ld32u(src + a + o) ^ ld32u(src + mt + 4u + mc + o);
+      };
+      auto count = [&](uint32_t p, uint32_t mt, uint32_t x) -> uint32_t {
         uint32_t mc = 0;
         while (true) {
-          const uint32_t a = ip + 4u + mc;
+          const uint32_t a = p + 4u + mc;
           const uint32_t lim = matchlimit > a ? matchlimit - a : 0u;
           const uint32_t o = 4u * (uint32_t)lane;
           uint32_t eq = 0;
-          if (o < lim) {
-            const uint32_t x = ld32u(src + a + o) ^ ld32u(src + match + 4u + mc + o);
-            eq = x ? (uint32_t)(__builtin_ctz(x) >> 3) : 4u;
-            eq = min(eq, lim - o);
-          }
+          if (o < lim) eq = min(x ? (uint32_t)(__builtin_ctz(x) >> 3) : 4u, lim - o);
           const uint64_t stop = __ballot(eq < 4u);
           if (stop) {
             const int sl = __builtin_ctzll(stop);
-            mc += 4u * (uint32_t)sl + (uint32_t)__shfl((int)eq, sl, kLWave);
-            break;
+            return mc + 4u * (uint32_t)sl + (uint32_t)__shfl((int)eq, sl, kLWave);
           }
           mc += 4u * kLWave;
+          x = cnt_load(p, mt, mc);
         }
+      };
+      // emits one sequence (literals [anchor, ip) + the match at ip, mc bytes past its first 4);
+      // false = the block cannot be shorter than the chunk (stored raw).  The 4-byte words the
+      // re-probe at the match end hashes are loaded before the sequence's stores (gfx950's vmcnt
+      // counts stores: loads issued after them would wait for them too).
+      uint32_t w2 = 0, w0 = 0, pw = ld32u(src + min(1u + (uint32_t)lane, len - 4u));
+      auto sequence = [&](uint32_t mc) -> bool {
         const uint32_t ll = ip - anchor;
         const uint32_t need = 1u + ext_bytes(ll) + ll + 2u + ext_bytes(mc);
         if (op + need >= len) return false;
+        const uint32_t end = ip + mc + 4u;  // <= matchlimit: both words lie inside the chunk
+        w2 = ld32u(src + end - 2u);
+        w0 = ld32u(src + end);
+        pw = ld32u(src + min(end + 1u + (uint32_t)lane, len - 4u));  // a failed re-probe's search
         uint8_t* d = dst + op;
         if (lane == 0) d[0] = (uint8_t)((min(ll, 15u) << 4) | min(mc, 15u));
         put_len(d + 1, ll, lane);
@@ -286,30 +307,42 @@ __global__ __launch_bounds__(kLz4Waves * kLWave) void k_lz4_default(
         }
         put_len(d + lo + ll + 2, mc, lane);
         op += need;
-        ip += mc + 4u;
+        ip = end;
         anchor = ip;
         return true;
       };
       while (!last && !raw) {
-        if (!search()) {
+        if (!search(pw)) {
           last = true;
           break;
         }
-        // catch up: extend backwards while ip > anchor, match > 0 and the bytes before agree
-        while (true) {
-          const uint32_t room = min(ip - anchor, match);
-          if (room == 0) break;
-          const uint32_t k = (uint32_t)lane + 1u;
-          const bool eq = k <= room && src[ip - k] == src[match - k];
+        // the backward catch-up (extend while ip > anchor, match > 0 and the bytes before agree)
+        // and the forward count from the hit, their first rounds' loads together.  Counting from
+        // the hit is exact: the caught-up bytes and the hit's 4 agree, so the match ends where it
+        // would counting from the caught-up ip, back bytes further on.
+        uint32_t back = 0;
+        uint32_t room = min(ip - anchor, match);
+        const uint32_t k1 = (uint32_t)lane + 1u;
+        uint32_t kc = k1 <= room ? k1 : 0u;  // clamped: the loads are unconditional
+        uint8_t bi = src[ip - kc], bm = src[match - kc];
+        uint32_t mc = count(ip, match, cnt_load(ip, match, 0u));
+        while (room) {
+          const bool eq = k1 <= room && bi == bm;
           const uint64_t ne = __ballot(!eq);
-          const uint32_t back = ne ? (uint32_t)__builtin_ctzll(ne) : (uint32_t)kLWave;
-          ip -= back;
-          match -= back;
-          if (back < (uint32_t)kLWave) break;
+          const uint32_t bk = ne ? (uint32_t)__builtin_ctzll(ne) : (uint32_t)kLWave;
+          ip -= bk;
+          match -= bk;
+          back += bk;
+          if (bk < (uint32_t)kLWave) break;
+          room = min(ip - anchor, match);
+          kc = k1 <= room ? k1 : 0u;
+          bi = src[ip - kc];
+          bm = src[match - kc];
         }
+        mc += back;
         // the match, then liblz4's immediate re-probes at the match end
         while (true) {
-          if (!sequence()) {
+          if (!sequence(mc)) {
             raw = true;
             break;
           }
@@ -317,17 +350,20 @@ __global__ __launch_bounds__(kLz4Waves * kLWave) void k_lz4_default(
             last = true;
             break;
           }
-          const uint32_t h2 = lz4_hash(ld32u(src + ip - 2u));
-          const uint32_t seq = ld32u(src + ip);
-          const uint32_t h = lz4_hash(seq);
+          const uint32_t h2 = lz4_hash(w2);
+          const uint32_t h = lz4_hash(w0);
           if (lane == 0) tab[h2] = (uint16_t)(ip - 2u);
           wave_lds_sync();
           const uint32_t mi = tab[h];
           wave_lds_sync();
           if (lane == 0) tab[h] = (uint16_t)ip;
           wave_lds_sync();
-          if (ld32u(src + mi) == seq) {  // a new sequence with no literals
+          // the candidate's word and the first count round from it, one round trip
+          const uint32_t cand = ld32u(src + mi);
+          const uint32_t x = cnt_load(ip, mi, 0u);
+          if (cand == w0) {  // a new sequence with no literals
             match = mi;
+            mc = count(ip, mi, x);
             continue;
           }
           ip += 1u;  // the search restarts after the probed position
