@@ -337,7 +337,7 @@ def plugin_leg(node, part, data, rs: int, R: int, rpm: int, gm: int, groups: int
     # a running stage do (MemoryPool.get, MemoryPool.java:137-168)
     sid = one(2000)
     torch.cuda.synchronize(dev)
-    req = [(m, R // 2) for m in range(maps)]
+    req = np.stack([np.arange(maps), np.full(maps, R // 2)], 1).astype(np.int32)
     t0 = time.perf_counter()
     buf, sizes = node.fetch_blocks(sid, req, stream=stream)
     ft_first = time.perf_counter() - t0

@@ -2246,12 +2246,22 @@ int sux_fetch_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* blo
       }
       require(chunks < (1ull << 31), SUX_ERANGE, "fetch request too large");
       const uint64_t dbytes = desc.size() * sizeof(sux::CopyDesc), fbytes = first.size() * 4;
-      buf->aux = node->pool->get(dbytes + 256 + fbytes);
+      const uint64_t dpad = ((dbytes + 255) / 256) * 256;
+      buf->aux = node->pool->get(dpad + fbytes);
       uint8_t* d_desc = buf->aux.ptr;
-      uint8_t* d_first = buf->aux.ptr + ((dbytes + 255) / 256) * 256;
-      hip_check(hipMemcpyAsync(d_desc, desc.data(), dbytes, hipMemcpyHostToDevice, s), "H2D desc");
-      hip_check(hipMemcpyAsync(d_first, first.data(), fbytes, hipMemcpyHostToDevice, s),
-                "H2D chunks");
+      uint8_t* d_first = buf->aux.ptr + dpad;
+      // both tables through one pinned staging block: one true async upload instead of two
+      // pageable bounces (the staging returns to node->hpool after the sync below)
+      auto hb = node->hpool.get(dpad + fbytes);
+      struct Put {
+        HostPool& hp;
+        std::pair<void*, uint64_t> b;
+        ~Put() { hp.put(b); }
+      } put{node->hpool, hb};
+      uint8_t* h = static_cast<uint8_t*>(hb.first);
+      std::memcpy(h, desc.data(), dbytes);
+      std::memcpy(h + dpad, first.data(), fbytes);
+      hip_check(hipMemcpyAsync(d_desc, h, dpad + fbytes, hipMemcpyHostToDevice, s), "H2D desc");
       hip_check(sux::launch_gather_copy(reinterpret_cast<const sux::CopyDesc*>(d_desc), (uint32_t)n,
                                         (uint32_t)chunks, reinterpret_cast<const uint32_t*>(d_first),
                                         &node->timer, s),

@@ -421,6 +421,11 @@ class Node:
             b[:len(blocks), :2] = blocks[:, :2]
             b[:len(blocks), 2] = blocks[:, 2] if blocks.shape[1] > 2 else blocks[:, 1] + 1
             return (N.BlockId * len(b)).from_buffer_copy(b.tobytes())
+        if len(blocks) and len({len(b) for b in blocks}) == 1 and len(blocks[0]) in (2, 3):
+            try:  # uniform tuples: one numpy conversion instead of a ctypes object per block
+                return Node._blocks(np.asarray(blocks, dtype=np.int64))
+            except (TypeError, ValueError, OverflowError):
+                pass
         arr = (N.BlockId * max(1, len(blocks)))()
         for i, b in enumerate(blocks):
             m, s = b[0], b[1]
