@@ -273,6 +273,16 @@ class HostPool {
   std::map<uint64_t, std::vector<void*>> free_;
 };
 
+// A HostPool block, returned on every exit path (callers sync the stream that reads it first).
+struct HostLease {
+  HostPool& hp;
+  std::pair<void*, uint64_t> b;
+  HostLease(HostPool& p, uint64_t n) : hp(p), b(p.get(n)) {}
+  ~HostLease() { hp.put(b); }
+  HostLease(const HostLease&) = delete;
+  HostLease& operator=(const HostLease&) = delete;
+};
+
 // A pooled device buffer shared by several map slots (one batch of map outputs); the last
 // reference returns it to the pool.
 struct Slab {
@@ -1472,13 +1482,8 @@ int sux_exchange_group(sux_node* node, const void* d_send, const int64_t* d_inde
     hipStream_t s = node->stream(stream);
     const size_t per_rank = (size_t)M * (R + 1);
     // pinned staging (node->hpool): the read-back is a true async copy, not a pageable bounce
-    auto hb = node->hpool.get(per_rank * W * 8);
-    struct Put {
-      HostPool& hp;
-      std::pair<void*, uint64_t> b;
-      ~Put() { hp.put(b); }
-    } put{node->hpool, hb};
-    int64_t* host = static_cast<int64_t*>(hb.first);
+    HostLease hb(node->hpool, per_rank * W * 8);
+    int64_t* host = static_cast<int64_t*>(hb.b.first);
     if (!node->comm) {
       hip_check(hipMemcpyAsync(d_gathered, d_index, per_rank * 8, hipMemcpyDeviceToDevice, s),
                 "copy index");
@@ -2252,13 +2257,8 @@ int sux_fetch_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* blo
       uint8_t* d_first = buf->aux.ptr + dpad;
       // both tables through one pinned staging block: one true async upload instead of two
       // pageable bounces (the staging returns to node->hpool after the sync below)
-      auto hb = node->hpool.get(dpad + fbytes);
-      struct Put {
-        HostPool& hp;
-        std::pair<void*, uint64_t> b;
-        ~Put() { hp.put(b); }
-      } put{node->hpool, hb};
-      uint8_t* h = static_cast<uint8_t*>(hb.first);
+      HostLease hb(node->hpool, dpad + fbytes);
+      uint8_t* h = static_cast<uint8_t*>(hb.b.first);
       std::memcpy(h, desc.data(), dbytes);
       std::memcpy(h + dpad, first.data(), fbytes);
       hip_check(hipMemcpyAsync(d_desc, h, dpad + fbytes, hipMemcpyHostToDevice, s), "H2D desc");
@@ -2462,10 +2462,14 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
   hip_check(hipStreamIsCapturing(s, &cap), "hipStreamIsCapturing");
   const bool run_all = all_passes || cap != hipStreamCaptureStatusNone;
   uint32_t span[6] = {0, 0, 0, ~0u, ~0u, ~0u};  // AND = 0, OR = ~0: every bit varies
+  // the read-backs land in pinned staging (a true async copy, not a pageable bounce)
+  HostLease hrb(node->hpool, 64);
+  uint8_t* hrd = static_cast<uint8_t*>(hrb.b.first);
   if (!run_all) {
-    hip_check(hipMemcpyAsync(span, ws + P.span_off, sizeof span, hipMemcpyDeviceToHost, s),
+    hip_check(hipMemcpyAsync(hrd, ws + P.span_off, sizeof span, hipMemcpyDeviceToHost, s),
               "sort key span");
     hip_check(hipStreamSynchronize(s), "sort key span");
+    std::memcpy(span, hrd, sizeof span);
   }
   sux::PartDev pd{};
   pd.kind = sux::kPartRadix;
@@ -2513,8 +2517,9 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
       hip_check(sux::launch_sort_local(nullptr, nullptr, index1, (uint32_t)pd1.R, dg, d_max, true, s),
                 "sort bucket max");
       uint64_t maxb = 0;
-      hip_check(hipMemcpyAsync(&maxb, d_max, 8, hipMemcpyDeviceToHost, s), "sort bucket max");
+      hip_check(hipMemcpyAsync(hrd + 32, d_max, 8, hipMemcpyDeviceToHost, s), "sort bucket max");
       hip_check(hipStreamSynchronize(s), "sort bucket max");
+      std::memcpy(&maxb, hrd + 32, 8);
       if (maxb <= sux::kSortLocalCap) {
         dg.pad = (int32_t)maxb;
         for (int sh = 128 - bits; sh < top_lo; sh += 8)
