@@ -147,3 +147,24 @@ def test_bench_bounds_match_oracle():
 
     for R in (2, 7, 200, 10000):
         assert bench.uniform_bounds(R) == O.uniform_range_bounds(R, 10)
+
+
+@pytest.mark.parametrize("blocks", [
+    [(0, 1), (3, 4), (2, 0)],                       # (map, partition): end = start + 1
+    [(0, 1, 5), (3, 4, 4), (2, 0, 9)],              # (map, start, end)
+    [(0, 1), (3, 4, 7)],                            # ragged: the per-block path
+    np.array([[0, 1], [3, 4], [2, 0]], np.int32),
+    np.array([[0, 1, 5], [3, 4, 4]], np.int64),
+    [],
+])
+def test_block_lists_convert_the_same_by_every_path(blocks):
+    """Node._blocks (the sux_block_id array of sux_fetch_blocks / sux_resolve_blocks) gives the same
+    ids for tuples, uniform tuples (one numpy conversion) and arrays."""
+    from sparkucx_amd.shuffle import Node
+
+    arr = Node._blocks(blocks)
+    want = [(int(b[0]), int(b[1]), int(b[2]) if len(b) > 2 else int(b[1]) + 1, 0) for b in blocks]
+    got = [(a.map_index, a.start_reduce, a.end_reduce, a.reserved)
+           for a in arr][:len(want)] if want else []
+    assert got == want
+    assert len(arr) == max(1, len(want))
