@@ -78,30 +78,37 @@ def host_cores() -> dict:
     return {"nproc": nproc, "affinity": aff, "cgroup_quota": quota, "use": use}
 
 
-def cpu_baseline(args) -> dict | None:
+def cpu_baseline(args, seed: int, node=None, part=None, data=None) -> dict | None:
     """Oracle CPU shuffle (Spark sort-shuffle write to /dev/shm files + UCX-style two-phase fetch)
-    on a bounded sample of the same workload: config 1's shape (1 GB, R=200, 8 map tasks), on every
-    host core this job may use (host_cores()['use']; --cpu-threads overrides)."""
+    on a bounded sample of the same workload: the first args.cpu_records TeraSort records of the
+    GPU run (same seed, same counter-based generator), R=200, 8 map tasks, on every host core this
+    job may use (host_cores()['use']; --cpu-threads overrides), median of args.cpu_reps runs after
+    a warm-up.  With node/part/data, the GPU partitions the same records as the
+    same 8 map tasks and its index tables and per-reducer fetch checksums are compared with the
+    CPU's (the two paths are parity-checked against each other)."""
     try:
         from oracle import oracle as O  # test infrastructure: timed as the baseline only
     except Exception as e:  # pragma: no cover
         log("cpu baseline unavailable:", e)
         return None
     hc = host_cores()
-    n, maps = args.cpu_records, 8
+    n, maps, R = args.cpu_records, 8, 200
     threads = args.cpu_threads if args.cpu_threads > 0 else hc["use"]
     log(f"cpu baseline: nproc={hc['nproc']} affinity={hc['affinity']} "
         f"cgroup_quota={hc['cgroup_quota']} -> {threads} threads")
-    recs = O.gen_terasort(0x5EED0001, 0, n)
-    part = O.terasort_partitioner(200)
+    recs = O.gen_terasort(seed, 0, n)
+    opart = O.terasort_partitioner(R)
     d = "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else None
     tmp = tempfile.mkdtemp(prefix="sux_cpu_", dir=d)
     times = []
+    cpu_index = np.zeros(maps * (R + 1), np.int64)
+    checksum = None
     try:
         for i in range(args.cpu_reps + 1):
-            r = O.cpu_shuffle(part, recs, 100, maps, threads, tmp)
+            r = O.cpu_shuffle(opart, recs, 100, maps, threads, tmp, index_out=cpu_index)
             if r.bytes_fetched != recs.size:
                 raise RuntimeError("cpu baseline fetched the wrong byte count")
+            checksum = r.checksum
             if i:
                 times.append((r.total_s, r.map_s, r.fetch_s))
     finally:
@@ -111,13 +118,35 @@ def cpu_baseline(args) -> dict | None:
             pass
     times.sort()
     t, tm, tf = times[len(times) // 2]
-    return {"value": round(recs.size / t / 1e9, 3), "unit": "GB/s", "cores": threads,
-            "kind": "port", "host": hc,
-            "sample": f"TeraSort {n} x 100 B ({recs.size / 1e9:.2f} GB), R=200, {maps} map tasks, "
-                      f"{threads} threads (nproc {hc['nproc']}, affinity {hc['affinity']}, "
-                      f"cgroup quota {hc['cgroup_quota']}); Spark-style write to "
-                      f"{'/dev/shm' if d else '/tmp'} files + two-phase offset/block fetch; "
-                      f"median of {len(times)} (map {tm:.3f}s, fetch {tf:.3f}s)"}
+    out = {"value": round(recs.size / t / 1e9, 3), "unit": "GB/s", "cores": threads,
+           "kind": "port", "host": hc, "seed": hex(seed),
+           "sample": f"TeraSort records [0, {n}) of the GPU run's input (seed {hex(seed)}; "
+                     f"{recs.size / 1e9:.2f} GB), R={R}, {maps} map tasks, "
+                     f"{threads} threads (nproc {hc['nproc']}, affinity {hc['affinity']}, "
+                     f"cgroup quota {hc['cgroup_quota']}); Spark-style write to "
+                     f"{'/dev/shm' if d else '/tmp'} files + two-phase offset/block fetch; "
+                     f"median of {len(times)} after a warm-up (map {tm:.3f}s, fetch {tf:.3f}s)"}
+    if node is not None and data is not None:
+        # the same records, the same 8 map tasks, on the GPU: index tables must be equal and
+        # every reducer's fetched bytes (blocks of all maps in map order) must checksum equal
+        per = -(-n // maps)
+        g_out, g_ix, _ = node.partition_maps(part, data[:n * 100], 100, per, num_records=n)
+        torch.cuda.synchronize()
+        gi = g_ix.cpu().numpy()
+        gb = g_out.cpu().numpy()
+        ix = gi.reshape(maps, R + 1)
+        lib = O.lib()
+        gsum = 0
+        for r_ in range(R):
+            buf = np.concatenate([gb[m * per * 100 + ix[m, r_]:m * per * 100 + ix[m, r_ + 1]]
+                                  for m in range(maps)])
+            gsum = (gsum + int(lib.o_checksum(buf.ctypes.data, buf.size))) % (1 << 64)
+        out["parity"] = {"index_tables_equal": bool(np.array_equal(gi, cpu_index)),
+                         "fetch_checksum_equal": gsum == int(checksum) % (1 << 64),
+                         "maps": maps, "records_per_map": per}
+        if not (out["parity"]["index_tables_equal"] and out["parity"]["fetch_checksum_equal"]):
+            raise RuntimeError(f"cpu baseline and GPU disagree: {out['parity']}")
+    return out
 
 
 def reduce_sort(node, recs, ns: int, rs: int, dev) -> dict:
@@ -282,6 +311,29 @@ def files_leg(node, out, index, maps: int, R: int, dev) -> dict:
             "read_GB/s": round(nb / tr / 1e9, 2)}
 
 
+def maps_2e27_leg(node, part, data, out, n: int, rs: int, R: int, dev, steps: int = 3) -> dict:
+    """SURVEY.md §8(d) C2 as written: map batches of 2^27 records (13.4 GB per map task), one
+    map per launch group, the same sux_partition_maps_pipelined step as `value` (no resolve)."""
+    rpm = 1 << 27
+    maps = -(-n // rpm)
+    index = torch.empty(maps * (R + 1), dtype=torch.int64, device=dev)
+    be = torch.empty(maps * (R + 1) * 8, dtype=torch.uint8, device=dev)
+    run = lambda: node.partition_maps_pipelined(part, data, rs, rpm, num_records=n,
+                                                group_records=rpm, out=out, index=index,
+                                                index_be=be)
+    run()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / steps
+    ix = index.view(maps, R + 1)
+    ok = bool((ix[:, 0] == 0).all()) and int(ix[:, R].sum()) == n * rs
+    return {"records_per_map": rpm, "maps": maps, "steps": steps, "ms_per_step": round(dt * 1e3, 3),
+            "GB/s": round(n * rs / dt / 1e9, 1), "index_consistent": ok}
+
+
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r02.json")
 
 
@@ -358,6 +410,95 @@ def plugin_leg(node, part, data, rs: int, R: int, rpm: int, gm: int, groups: int
                                   "GB/s": round(fb / ft / 1e9, 1),
                                   "first_call_ms": round(ft_first * 1e3, 3)},
             "pool": st}
+
+
+def plugin_leg_multi(node, part, data, rs: int, R: int, rpm: int, gm: int, groups: int,
+                     world: int, rank: int, dev, ctl, xstream) -> dict:
+    """The drop-in path at N > 1, as Spark drives it, through the C-ABI:
+    registerShuffle -> every rank writes its map tasks launch group by launch group
+    (sux_write_map_outputs: peer-major batch slabs) -> the exchange of window g-1 (all ranks' maps
+    of group g-1: sux_exchange_maps, one partition-aligned ncclAllToAllv per round of batches on
+    its own stream) is enqueued after group g's writes, so it overlaps group g's map kernels ->
+    sux_exchange_wait.  Timed (max over ranks) from the first write to the wait; then, untimed,
+    every rank fetches its partitions of every map (UcxShuffleClient.fetchBlocks of one
+    ShuffleBlockBatchId per map) and checks them on the device: partition ids (k_pids) inside
+    its range, non-decreasing per map, run lengths = the map's index file, and the word multiset
+    of all ranks' fetched bytes = the inputs'."""
+    sid = 7000
+    M = groups * world * gm
+    node.register_shuffle(sid, M, R, rs)
+    stream = torch.cuda.current_stream(dev)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for g in range(groups):
+        r0 = g * gm * rpm
+        node.write_map_outputs(sid, (g * world + rank) * gm, part, data[r0 * rs:(r0 + gm * rpm) * rs],
+                               rpm, gm * rpm, stream=stream)
+        if g:
+            node.exchange_maps(sid, (g - 1) * world * gm, world * gm, stream=xstream)
+    node.exchange_maps(sid, (groups - 1) * world * gm, world * gm, stream=xstream)
+    node.exchange_wait(sid)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    tt = torch.tensor([dt], dtype=torch.float64, device=ctl)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    dt = float(tt.item())
+    # ---- untimed device check of everything this rank now serves
+    lo, hi = node.owned_partitions(sid)
+    sums = torch.zeros(4, dtype=torch.int64, device=dev)
+
+    def wsum(buf):
+        acc = torch.zeros(2, dtype=torch.int64, device=dev)
+        w32 = buf.view(torch.int32)
+        for w0 in range(0, w32.numel(), 1 << 28):
+            w = w32[w0:w0 + (1 << 28)].to(torch.int64)
+            acc[0] += w.sum()
+            acc[1] += (w * w).sum()
+        return acc
+
+    sums[:2] += wsum(data[:groups * gm * rpm * rs])
+    fetched = 0
+    for b0 in range(0, M, 64):
+        ms = list(range(b0, min(M, b0 + 64)))
+        buf, sizes = node.fetch_blocks(sid, [(m, lo, hi) for m in ms])
+        ptr, size, _ = buf.info()
+        t = torch.empty(max(4, size), dtype=torch.uint8, device=dev)
+        if size:
+            N.hip_memcpy(t.data_ptr(), ptr, size, N.HIP_D2D)
+        buf.release(len(ms))
+        t = t[:size]
+        fetched += size
+        if size:
+            pid = node.partition_ids(part, t, rs).to(torch.int64)
+            cnt = torch.tensor([sz // rs for sz in sizes], dtype=torch.int64, device=dev)
+            seg = torch.repeat_interleave(torch.arange(len(ms), device=dev), cnt)
+            runs = torch.bincount(seg * (hi - lo) + (pid - lo), minlength=len(ms) * (hi - lo))
+            want = []
+            for m in ms:
+                ix = np.frombuffer(node.map_output_index(sid, m, R), dtype=">i8").astype(np.int64)
+                want.append((ix[lo + 1:hi + 1] - ix[lo:hi]) // rs)
+            want = torch.from_numpy(np.concatenate(want)).to(dev)
+            ok = bool(((pid >= lo) & (pid < hi)).all()) and \
+                bool(((pid[1:] >= pid[:-1]) | (seg[1:] != seg[:-1])).all()) and \
+                torch.equal(runs, want)
+            if not ok:
+                raise RuntimeError(f"plugin leg: rank {rank} maps {ms[0]}..{ms[-1]} fetched "
+                                   "blocks are not this rank's partitions as indexed")
+            sums[2:] += wsum(t)
+    tot = sums.to(ctl)
+    dist.all_reduce(tot)
+    tot = tot.cpu().tolist()
+    if tot[0] != tot[2] or tot[1] != tot[3]:
+        raise RuntimeError("plugin leg: fetched words differ from the inputs' over all ranks")
+    node.unregister_shuffle(sid)
+    n_all = world * groups * gm * rpm
+    return {"maps": M, "records": n_all, "bytes": n_all * rs, "ms": round(dt * 1e3, 3),
+            "GB/s": round(n_all * rs / dt / 1e9, 1), "fetched_bytes_rank": fetched,
+            "self_check": "ok",
+            "path": f"register -> write_map_outputs x{groups} per rank ({gm} maps each) with "
+                    f"sux_exchange_maps of the previous window on a second stream -> "
+                    f"sux_exchange_wait; then fetch + device check of every owned block"}
 
 
 GROUP_BYTES = 32 * (1 << 20) * 100  # the default launch group: 3.36 GB of input
@@ -477,13 +618,19 @@ def main():
     ap.add_argument("--plugin-groups", type=int, default=-1,
                     help="N=1: also time the plugin path (register -> write -> resolve -> "
                          "unregister) over this many launch groups of map tasks (-1: 16; 0: skip)")
+    ap.add_argument("--resolve", type=int, default=1,
+                    help="N=1: the timed step also commits the map outputs in place and resolves "
+                         "every (map, reduce partition) block through sux_resolve_blocks (C2's "
+                         "local block resolve)")
+    ap.add_argument("--maps-2e27", type=int, default=1,
+                    help="N=1 terasort: also time SURVEY C2's 2^27-record map batches (3 steps)")
     ap.add_argument("--self-check", type=int, default=1,
                     help="N=1: after the timed steps, run one more step into a zeroed output "
                          "and check it (index offsets, record multiset, partition grouping)")
     ap.add_argument("--cpu-records", type=int, default=10_000_000)
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (0: every core this job may use, host_cores())")
-    ap.add_argument("--cpu-reps", type=int, default=3)
+    ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true",
                     help="test mode (N>1): check every received block of every group against "
@@ -596,7 +743,32 @@ def main():
                                           group_records=group_recs, out=out, index=index,
                                           index_be=index_be, stream=comp)
 
+        # the reduce side's local block resolve (config C2): every (map, reduce partition) block
+        # of the step's shuffle is resolved through the plugin's C-ABI — the map outputs are
+        # committed in place (sux_adopt_map_outputs: index tables read back on the stream,
+        # published on completion) and sux_resolve_blocks returns each block's device address
+        # and size (OnOffsetsFetchCallback.java:53-72's offsets -> sizes, zero-copy at N = 1)
+        all_blocks = np.stack([np.repeat(np.arange(maps), R), np.tile(np.arange(R), maps)],
+                              1).astype(np.int32)
+        resolved = {"blocks": 0, "bytes": 0}
+        sid_next = [5000]
+
+        def step_resolved(inner):
+            def run():
+                sid = sid_next[0]
+                sid_next[0] += 1
+                node.register_shuffle(sid, maps, R, rs)
+                inner()
+                node.adopt_map_outputs(sid, 0, out, rpm, n, index, stream=comp)
+                _, sizes = node.resolve_blocks(sid, all_blocks)
+                node.unregister_shuffle(sid)
+                resolved["blocks"] += len(sizes)
+                resolved["bytes"] += int(sizes.sum())
+            return run
+
         step = step_pipelined if args.map_pipeline else step_groups
+        if args.resolve:
+            step = step_resolved(step)
     else:
         comm = torch.cuda.Stream(dev)
         # send-buffer ring: rccl frees slot s when ITS all-to-all is done (2 slots); ipc frees
@@ -659,6 +831,8 @@ def main():
             xfer_ev.append((e0, e1))
             if args.verify:
                 verify_group(j, recv[j % 2], gi, mg, r0, r1)
+            if checking[0]:
+                device_check_group(j, recv[j % 2], gi, mg, r0, r1)
 
         opart = None
         if args.verify:  # test mode: every received block vs the CPU oracle (checker only)
@@ -688,6 +862,56 @@ def main():
             verified[0] += 1
 
         verified = [0]
+        checking = [False]
+        # word sums (sum, sum of squares; int64, wrapping) of the inputs / received bytes of the
+        # check step, all-reduced over ranks at its end: every record reaches exactly one owner
+        msums = torch.zeros(4, dtype=torch.int64, device=dev)
+        check_stats = {"groups": 0, "received_bytes": 0, "records": 0}
+
+        def word_sums(buf):
+            acc = torch.zeros(2, dtype=torch.int64, device=dev)
+            w32 = buf.view(torch.int32)
+            step_w = 1 << 28
+            for w0 in range(0, w32.numel(), step_w):
+                w = w32[w0:w0 + step_w].to(torch.int64)
+                acc[0] += w.sum()
+                acc[1] += (w * w).sum()
+                del w
+            return acc
+
+        def device_check_group(j, rbuf, gi, mg, r0, r1):
+            """N > 1 self-check of one launch group's exchange, on the device (no oracle): the
+            received bytes equal the exact sum from the gathered index; every received record's
+            partition id (recomputed by the independent k_pids kernel) lies in this rank's owned
+            range, is non-decreasing within each (source, map) block run and counts exactly the
+            index runs; the word multiset is checked across ranks at the end of the step."""
+            torch.cuda.synchronize(dev)
+            lo, hi = (rank * R) // world, ((rank + 1) * R) // world
+            t = gi.view(world, mg, R + 1)
+            own = t[:, :, hi] - t[:, :, lo]
+            exp = int(own.sum())
+            got = int(rbytes[j].item())
+            if got != exp:
+                raise RuntimeError(f"self-check: rank {rank} group {j} received {got} bytes, "
+                                   f"the gathered index says {exp}")
+            if exp:
+                pid = node.partition_ids(part, rbuf[:exp], rs).to(torch.int64)
+                if not bool(((pid >= lo) & (pid < hi)).all()):
+                    raise RuntimeError(f"self-check: rank {rank} group {j} received a record "
+                                       f"outside its partitions [{lo}, {hi})")
+                cnt = (own // rs).reshape(-1)
+                seg = torch.repeat_interleave(torch.arange(world * mg, device=dev), cnt)
+                rise = (pid[1:] >= pid[:-1]) | (seg[1:] != seg[:-1])
+                runs = torch.bincount(seg * (hi - lo) + (pid - lo), minlength=world * mg * (hi - lo))
+                want = ((t[:, :, lo + 1:hi + 1] - t[:, :, lo:hi]) // rs).reshape(-1)
+                if not (bool(rise.all()) and torch.equal(runs, want)):
+                    raise RuntimeError(f"self-check: rank {rank} group {j}: received blocks are "
+                                       "not grouped by partition as the index says")
+                msums[2:] += word_sums(rbuf[:exp])
+            msums[:2] += word_sums(data[r0 * rs:r1 * rs])
+            check_stats["groups"] += 1
+            check_stats["received_bytes"] += exp
+            check_stats["records"] += exp // rs
 
         def step():
             for k in range(groups):
@@ -808,6 +1032,7 @@ def main():
     if pipelined:
         torch.cuda.synchronize(dev)
         xms = sum(a.elapsed_time(b) for a, b in xfer_ev)
+        xfer_n = len(xfer_ev)
         # exact off-GPU bytes per step from the all-gathered index tables
         gh = gidx.cpu().numpy()
         lo, hi = (rank * R) // world, ((rank + 1) * R) // world
@@ -824,10 +1049,49 @@ def main():
         ach = remote / (xms / 1e3) / 1e9 if xms and remote else None
         if args.verify:
             result["verified_groups"] = verified[0]
+        if args.self_check:
+            # one more (untimed) step with every launch group's exchange checked on the device
+            checking[0] = True
+            step()
+            torch.cuda.synchronize(dev)
+            checking[0] = False
+            tot = msums.to(ctl)
+            if world > 1:
+                dist.all_reduce(tot)
+            tot = tot.cpu().tolist()
+            if tot[0] != tot[2] or tot[1] != tot[3]:
+                raise RuntimeError("self-check: the multiset of exchanged words differs from the "
+                                   "inputs' over all ranks")
+            result["self_check"] = {"ok": True, "groups": check_stats["groups"],
+                                    "received_bytes": check_stats["received_bytes"],
+                                    "checks": "received bytes = gathered-index sums per group; "
+                                              "k_pids of every received record in the owned "
+                                              "range, non-decreasing per (source, map) run, "
+                                              "run counts = index; word multiset over all "
+                                              "ranks = the inputs'"}
         result["roofline_exchange"] = {
             "bound": "xgmi", "achieved": None if ach is None else round(ach, 1), "peak": peak,
             "unit": "GB/s", "frac": None if ach is None else round(ach / peak, 4),
             "remote_bytes_per_rank": remote // args.steps, "exchange_ms": round(xms, 2)}
+    if pipelined and world > 1 and args.plugin_groups != 0:
+        # the stateless pipeline's rings go back first: the plugin leg's slabs and receive
+        # buffers take their HBM
+        send.clear()
+        recv.clear()
+        ws.clear()
+        torch.cuda.empty_cache()
+        if node.world_size == 1:  # ipc transport: the plugin's exchange needs the host bootstrap
+            node = Node(device=local, rank=rank, world_size=world)
+            node.set_bootstrap(lambda b: (lambda out: (dist.all_gather_object(out, b), out)[1])(
+                [None] * world))
+            part = (node.partitioner(kind, R, key_offset=0, key_len=key_len,
+                                     bounds=uniform_bounds(R)) if kind == N.PART_RANGE_BYTES
+                    else node.partitioner(kind, R, key_offset=0, key_len=key_len, seed=42))
+        pg = min(n // group_recs, args.plugin_groups if args.plugin_groups > 0 else 8)
+        if pg:
+            xs = torch.cuda.Stream(dev)
+            result["plugin"] = plugin_leg_multi(node, part, data, rs, R, rpm, gm, pg, world, rank,
+                                                dev, ctl, xs)
     if not pipelined and args.self_check:
         out.zero_()
         index.zero_()
@@ -835,12 +1099,24 @@ def main():
         torch.cuda.synchronize(dev)
         result["self_check"] = self_check(node, part, data, out, index, n, rs, rpm, R,
                                           group_recs, dev)
+    if not pipelined and args.resolve:
+        steps_run = args.warmup + args.steps + (1 if args.self_check else 0)
+        result["resolve"] = {"blocks_per_step": resolved["blocks"] // max(1, steps_run),
+                             "bytes_per_step": resolved["bytes"] // max(1, steps_run),
+                             "path": "sux_register_shuffle -> partition -> sux_adopt_map_outputs "
+                                     "-> sux_resolve_blocks(every (map, reduce) block) -> "
+                                     "sux_unregister_shuffle, inside every timed step"}
+        if resolved["bytes"] != n * rs * steps_run:
+            raise RuntimeError("resolved blocks do not cover the input")
     if not pipelined:
         ns = args.reduce_sort_records if args.reduce_sort_records >= 0 else n // R
         ns = min(ns, n)
         if ns > 0 and args.workload == "terasort":
             result["reduce_sort"] = reduce_sort(node, out[:ns * rs], ns, rs, dev)
             result["reduce_sort_long"] = reduce_sort_long(node, 32 << 20, dev)
+    if not pipelined and args.maps_2e27 and args.workload == "terasort" and n >= (1 << 27) \
+            and rpm != (1 << 27):
+        result["maps_2e27"] = maps_2e27_leg(node, part, data, out, n, rs, R, dev)
     if not pipelined and args.compress_maps != 0:
         cm = min(maps, args.compress_maps if args.compress_maps > 0 else gm)
         if cm:
@@ -862,7 +1138,10 @@ def main():
         result["varlen"] = varlen_leg(node, vr, min(vr, 1 << 20), 200, dev,
                                       compress=args.compress_maps != 0)
     if rank == 0 and not pipelined and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args)
+        cpu_n = min(args.cpu_records, n)
+        args.cpu_records = cpu_n
+        result["cpu_baseline"] = cpu_baseline(
+            args, seed, node, part, data if args.workload == "terasort" and R == 200 else None)
     if rank == 0:
         os.write(result_fd, (json.dumps(result) + "\n").encode())
     node.close()

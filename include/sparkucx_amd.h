@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define SUX_ABI_VERSION 3
+#define SUX_ABI_VERSION 4
 
 /* ---- status codes ---------------------------------------------------------------------- */
 #define SUX_OK 0
@@ -83,7 +83,10 @@ typedef struct sux_conf {
    * (size, count) pairs preallocated in the device pool when an executor node starts
    * (MemoryPool.preAlocate, MemoryPool.java:170-176, called for executors only at UcxNode.java:81-83). */
   uint32_t num_prealloc;
-  uint32_t reserved0;
+  /* spark.shuffle.ucx.gpu.poolLimitMiB: cap on the device pool's allocations in MiB (0 = none).
+   * Past it an allocation fails like a failed hipMalloc; with a spill directory the node then
+   * spills committed map outputs to Spark's files (sux_node_set_spill_dir) and retries. */
+  uint32_t pool_limit_mib;
   uint64_t prealloc_size[16];
   uint64_t prealloc_count[16];
 } sux_conf;
@@ -110,14 +113,28 @@ int sux_node_destroy(sux_node* node);
 
 /* Host all-gather supplied by the embedding runtime (Spark RPC through the driver in a JVM; a
  * torch.distributed store or gloo group in tests): every rank of the node's group passes `bytes`
- * bytes in `send`; on return `recv` holds world_size * bytes, rank r's bytes at r * bytes.  It is
+ * bytes in `send`; on return `recv` holds world_size * bytes, rank r's bytes at r * bytes.  `tag`
+ * names the collective: (shuffle id << 32) | the shuffle's all-gather sequence number — equal on
+ * every rank for the same call, so a control plane keys its rounds by it (not by arrival).  It is
  * the control plane the reference builds from UCX tag messages (UcxNode.startExecutor,
  * UcxNode.java:130-145; RpcConnectionCallback.java:47-89).  Return 0 on success.  With a
  * bootstrap and no RCCL communicator, sux_exchange moves the blocks by one-sided pulls from the
  * owners' device memory over HIP IPC (xGMI peer reads) — the GET model of the reference — so the
  * exchange also runs where RCCL cannot (several ranks on one GPU). */
-typedef int (*sux_allgather_fn)(void* ctx, const void* send, uint64_t bytes, void* recv);
+typedef int (*sux_allgather_fn)(void* ctx, uint64_t tag, const void* send, uint64_t bytes,
+                                void* recv);
 int sux_node_set_bootstrap(sux_node* node, sux_allgather_fn fn, void* ctx);
+
+/* HBM-capacity fallback (the reference serves every block from Spark's disk files,
+ * CommonUcxShuffleBlockResolver.scala:45-58; here map outputs live in HBM): when the device pool
+ * cannot hold a new map output, the node writes committed map outputs of its shuffles (world 1,
+ * or maps whose ranges were already exchanged) to Spark's data + index files under `dir`
+ * (spark.local.dir), frees their device memory and retries.  Spilled blocks are served by
+ * sux_fetch_blocks from the files; sux_resolve_blocks reports them as not device-resident.
+ * NULL or "" disables spilling (allocation failures then return SUX_ENOMEM). */
+int sux_node_set_spill_dir(sux_node* node, const char* dir);
+/* Map outputs spilled so far by this node. */
+int sux_node_spills(sux_node* node, uint64_t* spilled_maps);
 
 /* Device pool counters (MemoryPool's close-time stats, MemoryPool.java:30-39): bytes held in
  * device allocations, get() requests, allocations made, preallocated slabs. */
@@ -161,7 +178,10 @@ typedef struct sux_tuning {
                                share every CU                                                  */
   int32_t sort_msd;         /* reduce-side sort: 1 (0) one top-digit pass + per-bucket LDS sort
                                when the buckets fit, 2 LSD digit passes only                   */
-  int32_t reserved[10];
+  int32_t exchange_self;    /* 1: the exchange also moves this rank's own maps' owned ranges
+                               through its transport into the receive buffer (loopback; at
+                               world 1 it runs the whole RCCL / IPC path on one GPU); 0 or -1: no */
+  int32_t reserved[9];
 } sux_tuning;
 int sux_node_set_tuning(sux_node* node, const sux_tuning* tuning);
 /* Waits for the device, then reports (and clears) failures the kernels recorded in the node's
@@ -377,6 +397,16 @@ int sux_write_map_output_host(sux_node* node, int32_t shuffle_id, int32_t map_in
 int sux_commit_map_output(sux_node* node, int32_t shuffle_id, int32_t map_index,
                           const void* d_data, uint64_t data_bytes, const int64_t* lengths,
                           void* stream);
+/* writeIndexFileAndCommit for map outputs a stateless call (sux_partition_maps*) already wrote
+ * into the caller's device memory: maps first_map_index .. of records_per_map records each, map m
+ * at d_out + m*records_per_map*record_size (the shuffle's record size), native index tables in
+ * d_index (num_maps*(R+1) int64, device).  Nothing is copied: the node keeps the pointers (the
+ * caller keeps the memory alive and unchanged until sux_unregister_shuffle) and reads the index
+ * tables back asynchronously on `stream`; the maps are published like sux_write_map_outputs
+ * (first commit wins).  The Spark analog is a writer whose output Spark did not copy. */
+int sux_adopt_map_outputs(sux_node* node, int32_t shuffle_id, int32_t first_map_index,
+                          const void* d_out, uint64_t records_per_map, uint64_t num_records,
+                          const int64_t* d_index, void* stream);
 /* Read back a committed map's index file bytes ((R+1)*8 big-endian, host buffer). */
 int sux_map_output_index(sux_node* node, int32_t shuffle_id, int32_t map_index,
                          uint8_t* out_index_be, uint64_t out_len);
@@ -385,13 +415,46 @@ int sux_map_output_index(sux_node* node, int32_t shuffle_id, int32_t map_index,
  * Collective over the node's group: every rank calls it after committing its map outputs.
  * Rank h receives partitions [floor(h*R/G), floor((h+1)*R/G)) of every map of every rank.
  * Replaces the driver-table GET (UcxWorkerWrapper.fetchDriverMetadataBuffer :176-196) by an
- * all-gather of the committed maps' index tables, and the phase-1/phase-2 GETs
- * (UcxShuffleClient.java:50-127, OnOffsetsFetchCallback.java:44-92) by grouped ncclSend/ncclRecv
- * over xGMI (RCCL communicator) or, with a bootstrap and no communicator, by one gather-copy
- * launch that pulls every owned range from the owners' IPC-mapped map outputs.  The receive
- * buffer is sized exactly from the gathered index tables; it returns when this rank's blocks are
+ * all-gather of the committed maps' directory entries, and the phase-1/phase-2 GETs
+ * (UcxShuffleClient.java:50-127, OnOffsetsFetchCallback.java:44-92) by one partition-aligned
+ * ncclAllToAllv per round of map batches over xGMI (RCCL communicator) or, with a bootstrap and
+ * no communicator, by the same plan as one-sided pulls from the owners' IPC-mapped batch slabs.
+ * The receive buffer is sized exactly from the gathered index tables.  sux_exchange is
+ * sux_exchange_maps over every map + sux_exchange_wait: it returns when this rank's blocks are
  * in place and every rank has finished reading (so owners may unregister afterwards). */
 int sux_exchange(sux_node* node, int32_t shuffle_id, void* stream);
+/* The exchange of one window of map tasks, asynchronous: every rank calls it with the same
+ * [first_map_index, first_map_index + num_maps) once the maps it writes there are enqueued.  It
+ * waits only for this rank's writes of that window (later batches keep running), all-gathers
+ * their directory entries, and enqueues on `stream` one partition-aligned ncclAllToAllv per round
+ * of batches (round k = every rank's k-th batch of the window; counts/displacements straight from
+ * the index tables; a batch's peer-major slab is the send buffer as it stands), or the same plan
+ * as one-sided IPC pulls.  Maps already exchanged are skipped.  Returns without a host wait on
+ * the data: fetches of the window's blocks on another stream are ordered after it by the node,
+ * and sux_exchange_wait completes it.  Receive memory in flight = the window's owned bytes (the
+ * reader's maxBytesInFlight, UcxShuffleReader.scala:56-70, chooses the window). */
+int sux_exchange_maps(sux_node* node, int32_t shuffle_id, int32_t first_map_index,
+                      int32_t num_maps, void* stream);
+/* Collective: blocks until every exchange enqueued for the shuffle on this rank has completed
+ * and (IPC transport) every rank has finished its pulls, so owners may unregister. */
+int sux_exchange_wait(sux_node* node, int32_t shuffle_id);
+/* The plan of one sux_exchange_maps call for rank `rank` (host arithmetic, no device; the call
+ * runs exactly this on the gathered directory, so every rank's counts agree).  Input: the n
+ * directory entries of the window, per entry its map, owner and batch, and per (entry, peer h)
+ * seg = offset of the map's range for h in its batch slab and len = that range's bytes.
+ * Pieces = the maps of one (owner, batch); round k = every owner's k-th piece, one all-to-all.
+ * Output per round k (counts[k][0..3][h]): sendcounts, sdispls (offsets in this rank's batch
+ * slab), recvcounts, rdispls (offsets in the round's part of the receive buffer) for peer h;
+ * piece_entry[k][g] = the lowest-map entry of owner g's k-th piece (-1: none);
+ * round_base[k] (rounds + 1) = where round k starts in the receive buffer (the last = total);
+ * recv_off[i] = receive-buffer offset of entry i's owned range (UINT64_MAX: not received). */
+typedef struct sux_xplan_entry {
+  int32_t map, owner, batch, reserved;
+} sux_xplan_entry;
+int sux_plan_exchange(int32_t world, int32_t rank, int32_t loopback, int32_t n,
+                      const sux_xplan_entry* entries, const uint64_t* seg, const uint64_t* len,
+                      int32_t max_rounds, int32_t* rounds, uint64_t* counts, int32_t* piece_entry,
+                      uint64_t* round_base, uint64_t* recv_off);
 /* Reduce-partition ownership of a rank: [*start, *end). */
 int sux_owned_partitions(sux_node* node, int32_t shuffle_id, int32_t rank, int32_t* start,
                          int32_t* end);
@@ -417,6 +480,10 @@ int sux_fetch_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* blo
 int sux_resolve_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* blocks, int32_t n,
                        uint64_t* dev_addrs, int64_t* sizes);
 int sux_buffer_info(sux_buffer* buf, void** dev_ptr, uint64_t* size, uint64_t* capacity);
+/* A pooled device buffer of `bytes` with one reference (MemoryPool.get, MemoryPool.java:153-162):
+ * the reducer's own scratch, e.g. the output and workspace of sux_sort_records over a fetched
+ * buffer in the JVM reader, released with sux_buffer_release. */
+int sux_buffer_alloc(sux_node* node, uint64_t bytes, sux_buffer** out);
 /* Copy bytes [offset, offset + len) of a fetched buffer to host memory (the reducer's
  * deserialization side, NioManagedBuffer.nioByteBuffer); waits for the copy. */
 int sux_buffer_read(sux_buffer* buf, uint64_t offset, void* host_dst, uint64_t len, void* stream);

@@ -485,7 +485,8 @@ static void* map_file(const char* path, uint64_t* len) {
 }
 
 int o_cpu_shuffle(const o_part* p, const uint8_t* recs, uint64_t n, uint32_t rec_size,
-                  int32_t num_maps, int32_t threads, const char* dir, o_cpu_result* res) {
+                  int32_t num_maps, int32_t threads, const char* dir, o_cpu_result* res,
+                  int64_t* index_out) {
   cpu_ctx c;
   memset(&c, 0, sizeof c);
   c.p = p;
@@ -524,6 +525,11 @@ int o_cpu_shuffle(const o_part* p, const uint8_t* recs, uint64_t n, uint32_t rec
     for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
   }
   double t2 = now_s();
+  /* (untimed) the committed index files, native order, for a parity check against the GPU */
+  if (index_out && !c.err)
+    for (int m = 0; m < num_maps; ++m)
+      for (int r = 0; r <= c.R; ++r)
+        index_out[(size_t)m * (c.R + 1) + r] = load_be64(c.index_map[m] + 8 * (size_t)r);
   for (int m = 0; m < num_maps; ++m) {
     if (c.data_map[m]) munmap(c.data_map[m], c.data_len[m]);
     if (c.index_map[m]) munmap(c.index_map[m], 8 * (uint64_t)(c.R + 1));

@@ -62,7 +62,8 @@ typedef struct o_cpu_result {
   uint64_t checksum;
 } o_cpu_result;
 int o_cpu_shuffle(const o_part* p, const uint8_t* recs, uint64_t n, uint32_t rec_size,
-                  int32_t num_maps, int32_t threads, const char* dir, o_cpu_result* res);
+                  int32_t num_maps, int32_t threads, const char* dir, o_cpu_result* res,
+                  int64_t* index_out /* nullable: num_maps * (R+1) */);
 
 /* order-independent checksum helpers */
 uint64_t o_checksum(const uint8_t* p, uint64_t n);

@@ -64,7 +64,7 @@ def lib() -> C.CDLL:
             "o_fetch_blocks": (C.c_int64, [P, P, I32, I32, P, I32, P, P]),
             "o_owner_start": (I32, [I32, I32, I32]),
             "o_cpu_shuffle": (C.c_int, [C.POINTER(Part), P, U64, U32, I32, I32, C.c_char_p,
-                                        C.POINTER(CpuResult)]),
+                                        C.POINTER(CpuResult), P]),
             "o_checksum": (U64, [P, U64]),
             "o_xxh32": (U32, [P, U64, U32]),
             "o_lz4_compress_default": (I32, [P, I32, P]),
@@ -233,10 +233,13 @@ def checksum(a: np.ndarray) -> int:
 
 
 def cpu_shuffle(part: Partitioner, recs: np.ndarray, rec_size: int, num_maps: int, threads: int,
-                directory: str = "/dev/shm") -> CpuResult:
+                directory: str = "/dev/shm", index_out: np.ndarray | None = None) -> CpuResult:
+    """CPU baseline shuffle; index_out (int64[num_maps * (R+1)], optional) receives the
+    committed index files (native order) for a parity check."""
     res = CpuResult()
     rc = lib().o_cpu_shuffle(C.byref(part.c), _p(recs), recs.size // rec_size, rec_size, num_maps,
-                             threads, directory.encode(), C.byref(res))
+                             threads, directory.encode(), C.byref(res),
+                             None if index_out is None else _p(index_out))
     if rc != 0:
         raise RuntimeError("cpu shuffle failed")
     return res

@@ -47,6 +47,10 @@ void hip_check(hipError_t e, const char* what) {
 }
 void nccl_check(ncclResult_t r, const char* what) {
   if (r != ncclSuccess) raise(SUX_ECOMM, std::string(what) + ": " + ncclGetErrorString(r));
+  // RCCL's internal HIP calls can leave a stale error in the thread's last-error slot (seen
+  // after a communicator's init/teardown: "invalid device ordinal"); our kernel launches check
+  // hipGetLastError(), so it must not survive a successful RCCL call
+  (void)hipGetLastError();
 }
 // A failed check throws SuxError; the message expression is evaluated only then (some checks run
 // once per block of a fetch).
@@ -163,6 +167,37 @@ class DevicePool {
     return c;
   }
 
+  // Cap on the bytes the pool may hold in device allocations (sux_conf.pool_limit_mib; 0 = none).
+  // Past it get() fails with SUX_ENOMEM exactly like a failed hipMalloc, so the HBM-capacity
+  // fallback (spill to Spark's files) can be exercised without filling 288 GB.
+  void set_limit(uint64_t bytes) { limit_ = bytes; }
+
+  // Returns every free buffer that is a whole allocation of its own (classes >= minAllocationSize)
+  // to the device: after a spill, the memory can serve a different size class.  Slab-allocated
+  // small classes stay (their allocation is shared).  Returns the bytes freed.
+  uint64_t trim() {
+    std::lock_guard<std::mutex> lk(mu_);
+    uint64_t freed = 0;
+    for (auto& kv : stacks_) {
+      if (kv.first < min_alloc_) continue;
+      for (const PoolBuf& b : kv.second.free) {
+        auto it = std::find(allocations_.begin(), allocations_.end(), (void*)b.ptr);
+        if (it == allocations_.end()) continue;  // part of a preallocated slab
+        (void)hipFree(b.ptr);
+        allocations_.erase(it);
+        allocated_ -= b.cap;
+        freed += b.cap;
+      }
+      kv.second.free.erase(std::remove_if(kv.second.free.begin(), kv.second.free.end(),
+                                          [&](const PoolBuf& b) {
+                                            return std::find(allocations_.begin(), allocations_.end(),
+                                                             (void*)b.ptr) == allocations_.end();
+                                          }),
+                           kv.second.free.end());
+    }
+    return freed;
+  }
+
   // MemoryPool.get (:153-162) + AllocatorStack.get (:52-82): LIFO reuse, slab-allocate classes
   // below minAllocationSize in one registration (preallocate :89-114).
   PoolBuf get(uint64_t n) {
@@ -222,6 +257,9 @@ class DevicePool {
  private:
   uint8_t* alloc(uint64_t bytes) {  // caller holds mu_
     void* p = nullptr;
+    if (limit_ && allocated_ + bytes > limit_)
+      raise(SUX_ENOMEM, "device pool limit: " + std::to_string(allocated_) + " + " +
+                            std::to_string(bytes) + " bytes > " + std::to_string(limit_));
     hipError_t e = hipMalloc(&p, bytes);
     if (e != hipSuccess) raise(SUX_ENOMEM, "hipMalloc(" + std::to_string(bytes) + ") failed");
     allocations_.push_back(p);
@@ -232,7 +270,7 @@ class DevicePool {
     std::vector<PoolBuf> free;
     uint64_t requests = 0, allocs = 0, preallocs = 0;
   };
-  uint64_t min_buf_, min_alloc_;
+  uint64_t min_buf_, min_alloc_, limit_ = 0;
   std::mutex mu_;
   std::map<uint64_t, Stack> stacks_;
   std::vector<void*> allocations_;
@@ -283,17 +321,6 @@ struct HostLease {
   HostLease& operator=(const HostLease&) = delete;
 };
 
-// A pooled device buffer shared by several map slots (one batch of map outputs); the last
-// reference returns it to the pool.
-struct Slab {
-  DevicePool* pool = nullptr;
-  PoolBuf buf;
-  Slab(DevicePool* p, PoolBuf b) : pool(p), buf(b) {}
-  ~Slab() { pool->put(buf); }
-  Slab(const Slab&) = delete;
-  Slab& operator=(const Slab&) = delete;
-};
-
 struct Event {  // one completion event, shared by a write job and a thread that waits on it
   hipEvent_t e = nullptr;
   Event() { hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate"); }
@@ -302,25 +329,61 @@ struct Event {  // one completion event, shared by a write job and a thread that
   Event& operator=(const Event&) = delete;
 };
 
+// A device buffer shared by several map slots (one batch of map outputs, or one exchange's
+// receive buffer); the last reference returns it to the pool.  A slab without a pool wraps
+// memory the caller owns (sux_adopt_map_outputs) and frees nothing.  `ready` (receive buffers)
+// fires when the exchange that fills it has completed on its stream.
+struct Slab {
+  DevicePool* pool = nullptr;
+  PoolBuf buf;
+  std::shared_ptr<Event> ready;
+  Slab(DevicePool* p, PoolBuf b) : pool(p), buf(b) {}
+  ~Slab() {
+    if (pool) pool->put(buf);
+  }
+  Slab(const Slab&) = delete;
+  Slab& operator=(const Slab&) = delete;
+};
+
 // per-map directory slot: the analog of the 300-byte driver descriptor (DriverMetadata,
-// UcxWorkerWrapper.scala:27-65) plus the index file it points at
+// UcxWorkerWrapper.scala:27-65) plus the index file it points at.  Where the map's bytes live:
+//   - own maps, map-major (world 1, adopted or committed outputs): Spark's data file at
+//     slab + off;
+//   - own maps written at world > 1: the batch slab is peer-major [peer h][map][h's partitions],
+//     so the map's range for peer h starts at slab + seg[h] (seg has world entries);
+//   - own maps spilled to Spark's files (HBM fallback): spill_data / spill_index;
+//   - after an exchange: this rank's owned range of the map at rslab + recv_off (remote maps,
+//     and own maps when the exchange loops back through the transport).
 struct MapSlot {
   bool present = false;
   bool pending = false;  // enqueued by a write job that has not completed yet
+  bool sent = false;     // own map: its ranges went out in an exchange
   int32_t owner = -1;
+  int32_t batch = -1;    // own maps: the batch (exchange piece) the map belongs to
   std::shared_ptr<Slab> slab;  // local maps: the device buffer holding the data file
-  uint64_t off = 0;            // byte offset of this map's data file in the slab
+  uint64_t off = 0;            // byte offset of this map's data file in the slab (map-major)
+  std::vector<uint64_t> seg;   // per peer: offset of the map's range for that peer in the slab
   uint64_t bytes = 0;
   std::vector<int64_t> index;  // R+1 cumulative offsets (the index file, native order)
-  uint64_t recv_off = 0;       // after exchange: offset of this map's owned-range blocks in recv
+  std::shared_ptr<Slab> rslab; // receive buffer holding this rank's owned range of the map
+  uint64_t recv_off = 0;       // offset of that range in rslab
+  // after an exchange, per rank h: where h serves its owned range of this map — an index into
+  // Shuffle::serve_desc (h's batch slab or receive buffer) and the range's offset there; lets
+  // any rank read any block (a peer read over xGMI, the reference's one-sided GET)
+  std::vector<std::pair<int32_t, uint64_t>> serve;
+  std::string spill_data, spill_index;  // spilled: Spark's data + index files
   uint8_t* data() const { return slab ? slab->buf.ptr + off : nullptr; }
+  bool spilled() const { return !spill_data.empty(); }
 };
 
-// One sux_write_map_outputs call in flight: published by progress() once `done` has fired.
+// One sux_write_map_outputs / sux_adopt_map_outputs call in flight: published by progress()
+// once `done` has fired.
 struct WriteJob {
   int32_t first = 0;
   uint32_t maps = 0;
   uint64_t rpm = 0, n = 0;
+  int32_t world = 1;             // > 1: the slab is peer-major over this many peers
+  int32_t batch = -1;            // batch id of its maps (map-major at world > 1: one per map)
   std::vector<uint8_t> claimed;  // maps of the batch this job publishes
   std::shared_ptr<Slab> slab;
   PoolBuf ws;
@@ -335,11 +398,20 @@ struct Shuffle {
   std::vector<std::unique_ptr<WriteJob>> jobs;
   int busy = 0;        // jobs taken out of `jobs` by a thread that is waiting on them
   int submitting = 0;  // writes that claimed slots and have not queued their job yet
-  bool exchanged = false;
   bool exchanging = false;
-  PoolBuf recv;
-  uint64_t recv_bytes = 0;
-  std::map<std::string, void*> ipc_bases;  // opened owner allocations (owner|handle -> base)
+  int32_t next_batch = 0;
+  // exchanges enqueued and not yet waited for (sux_exchange_wait): their completion events and,
+  // with the IPC transport, whether the closing all-gather (every peer finished its pulls) is due
+  std::vector<std::shared_ptr<Event>> xfers;
+  std::vector<PoolBuf> xfer_aux;                      // their copy descriptors (IPC pulls)
+  std::vector<std::pair<void*, uint64_t>> xfer_host;  // and the descriptors' pinned staging
+  bool ack_due = false;
+  // collective host all-gathers of this shuffle so far: with the shuffle id they tag each one
+  // (every rank issues them in the same order), so a control plane can match contributions
+  uint32_t gathers = 0;
+  std::map<std::string, void*> ipc_bases;  // opened peer allocations (64-byte handle -> base)
+  std::vector<std::string> serve_desc;     // IPC descriptors of the buffers peers serve from
+  std::map<std::string, int32_t> serve_idx;
 };
 
 int32_t owner_lo(int32_t h, int32_t R, int32_t G) { return (int32_t)(((int64_t)h * R) / G); }
@@ -359,6 +431,8 @@ struct sux_node {
   sux_allgather_fn boot = nullptr;   // host all-gather of the embedding runtime
   void* boot_ctx = nullptr;
   sux_tuning tuning{};               // all zero = measured defaults (resolve_tuning)
+  std::string spill_dir;             // spark.local.dir analog: HBM-capacity fallback (sux_node_set_spill_dir)
+  uint64_t spills = 0;               // map outputs spilled so far
   uint32_t* d_err = nullptr;         // device error word (sux::kErr* bits), sux_node_check
   // sux_partition_maps_pipelined: two map streams, their group workspaces, fork/join events
   hipStream_t pipe[2] = {nullptr, nullptr};
@@ -442,6 +516,54 @@ void publish_slot(sux_node* n, Shuffle& sh, int32_t m, uint64_t index_addr) {
   store_be64(d + 24, s.bytes);
 }
 
+// A completed write job's maps get their slots: index tables from the pinned read-back, the
+// data location (map-major offset, or per-peer segments of a peer-major slab) and the batch.
+void publish_job(sux_node* node, Shuffle& sh, WriteJob& j) {
+  const int R = sh.R, W = j.world;
+  const int64_t* hx = static_cast<const int64_t*>(j.hidx.first);
+  auto ix = [&](uint32_t k, int p) { return hx[(uint64_t)k * (R + 1) + p]; };
+  // peer-major: sections [h] of the whole job (every map the kernels wrote, claimed or not)
+  std::vector<uint64_t> run((size_t)W, 0);
+  if (W > 1) {
+    uint64_t acc = 0;
+    for (int h = 0; h < W; ++h) {
+      run[h] = acc;
+      const int lo = owner_lo(h, R, W), hi = owner_lo(h + 1, R, W);
+      for (uint32_t k = 0; k < j.maps; ++k) acc += (uint64_t)(ix(k, hi) - ix(k, lo));
+    }
+  }
+  for (uint32_t k = 0; k < j.maps; ++k) {
+    if (j.claimed[k]) {
+      MapSlot& slot = sh.maps[j.first + k];
+      slot.pending = false;
+      slot.present = true;
+      slot.sent = false;
+      slot.owner = node->conf.rank;
+      slot.slab = j.slab;
+      slot.batch = j.batch >= 0 ? j.batch : sh.next_batch++;  // map-major at W > 1: own piece
+      slot.off = (uint64_t)k * j.rpm * (uint64_t)sh.rec_size;
+      slot.bytes = (uint64_t)ix(k, R);
+      slot.index.assign(hx + (uint64_t)k * (R + 1), hx + (uint64_t)(k + 1) * (R + 1));
+      slot.rslab.reset();
+      if (W > 1) {
+        slot.seg = run;
+      } else {  // map-major: peer h's range of the map is a sub-range of its data file
+        const int NW = node->conf.world_size;
+        slot.seg.resize((size_t)NW);
+        for (int h = 0; h < NW; ++h) slot.seg[h] = slot.off + (uint64_t)ix(k, owner_lo(h, R, NW));
+      }
+      publish_slot(node, sh, j.first + (int32_t)k, 0);
+    }
+    if (W > 1)
+      for (int h = 0; h < W; ++h)
+        run[h] += (uint64_t)(ix(k, owner_lo(h + 1, R, W)) - ix(k, owner_lo(h, R, W)));
+  }
+  node->pool->put(j.ws);
+  node->hpool.put(j.hidx);
+  j.ws = PoolBuf{};
+  j.hidx = {nullptr, 0};
+}
+
 // Publish every write job of `sh` whose kernels have completed (wait = block for all of them):
 // the directory slots of its maps get their index tables.  The analog of the reference's
 // completion callbacks, which run inside worker.progress() on the calling thread
@@ -461,34 +583,49 @@ void progress(sux_node* node, Shuffle& sh, std::unique_lock<std::mutex>& lk, boo
     }
     lk.lock();
     sh.busy -= (int)jobs.size();
-    const int R = sh.R;
     for (size_t i = 0; i < jobs.size(); ++i) {
-      WriteJob& j = *jobs[i];
       if (!done[i]) {
         sh.jobs.push_back(std::move(jobs[i]));
         continue;
       }
-      const int64_t* hx = static_cast<const int64_t*>(j.hidx.first);
-      for (uint32_t k = 0; k < j.maps; ++k) {
-        if (!j.claimed[k]) continue;
-        MapSlot& slot = sh.maps[j.first + k];
-        slot.pending = false;
-        slot.present = true;
-        slot.owner = node->conf.rank;
-        slot.slab = j.slab;
-        slot.off = (uint64_t)k * j.rpm * (uint64_t)sh.rec_size;
-        slot.bytes = (uint64_t)hx[(uint64_t)k * (R + 1) + R];
-        slot.index.assign(hx + (uint64_t)k * (R + 1), hx + (uint64_t)(k + 1) * (R + 1));
-        publish_slot(node, sh, j.first + (int32_t)k, 0);
-      }
-      sh.exchanged = false;
-      node->pool->put(j.ws);
-      node->hpool.put(j.hidx);
+      publish_job(node, sh, *jobs[i]);
       jobs[i].reset();
     }
     node->cv.notify_all();
     hip_check(err, "map output completion");
     if (!wait) return;
+  }
+}
+
+// Wait for (and publish) only the jobs that write maps of [lo, hi), and for writes that claimed a
+// slot there and are still submitting.  Jobs of later map batches keep running: an exchange of
+// batch k does not wait for batch k+1's kernels (the overlap of sux_exchange_maps).
+void drain_range(sux_node* node, Shuffle& sh, std::unique_lock<std::mutex>& lk, int32_t lo,
+                 int32_t hi) {
+  while (true) {
+    std::vector<std::unique_ptr<WriteJob>> mine;
+    for (auto& j : sh.jobs)
+      if (j && j->first < hi && j->first + (int32_t)j->maps > lo) mine.push_back(std::move(j));
+    sh.jobs.erase(std::remove(sh.jobs.begin(), sh.jobs.end(), nullptr), sh.jobs.end());
+    if (!mine.empty()) {
+      sh.busy += (int)mine.size();
+      hipError_t err = hipSuccess;
+      lk.unlock();
+      for (auto& j : mine) {
+        const hipError_t e = hipEventSynchronize(j->done->e);
+        if (e != hipSuccess && err == hipSuccess) err = e;
+      }
+      lk.lock();
+      sh.busy -= (int)mine.size();
+      for (auto& j : mine) publish_job(node, sh, *j);
+      node->cv.notify_all();
+      hip_check(err, "map output completion");
+      continue;
+    }
+    bool pending = false;
+    for (int32_t m = lo; m < hi && !pending; ++m) pending = sh.maps[m].pending;
+    if (!pending) return;
+    node->cv.wait(lk);  // another thread is waiting on, or still submitting, one of those jobs
   }
 }
 
@@ -501,13 +638,20 @@ void drain(sux_node* node, Shuffle& sh, std::unique_lock<std::mutex>& lk) {
   }
 }
 
-// Everything a shuffle holds on the device: slabs (via the slots), receive buffer, IPC mappings.
+// Everything a shuffle holds on the device: slabs and receive buffers (via the slots), IPC
+// mappings, spill files.
 void release_shuffle(sux_node* node, Shuffle& sh) {
+  (void)node;
   for (auto& kv : sh.ipc_bases) (void)hipIpcCloseMemHandle(kv.second);
   sh.ipc_bases.clear();
-  for (auto& m : sh.maps) m.slab.reset();
-  node->pool->put(sh.recv);
-  sh.recv = PoolBuf{};
+  for (auto& m : sh.maps) {
+    m.slab.reset();
+    m.rslab.reset();
+    if (m.spilled()) {  // CommonUcxShuffleBlockResolver.removeShuffle deletes the files too
+      ::unlink(m.spill_data.c_str());
+      ::unlink(m.spill_index.c_str());
+    }
+  }
 }
 
 struct Group {
@@ -698,6 +842,7 @@ int sux_node_create(const sux_conf* conf, int is_driver, sux_node** out) {
     n->is_driver = is_driver != 0;
     n->bind();
     n->pool = std::make_unique<DevicePool>(conf->min_buffer_size, conf->min_allocation_size);
+    n->pool->set_limit((uint64_t)conf->pool_limit_mib << 20);
     hip_check(hipMalloc(&n->d_err, sizeof(uint32_t)), "hipMalloc(error word)");
     hip_check(hipMemset(n->d_err, 0, sizeof(uint32_t)), "hipMemset(error word)");
     // UcxNode.java:81-83: executors preallocate the configured buffers
@@ -723,6 +868,28 @@ int sux_node_set_bootstrap(sux_node* node, sux_allgather_fn fn, void* ctx) {
     std::lock_guard<std::mutex> lk(node->mu);
     node->boot = fn;
     node->boot_ctx = ctx;
+  });
+}
+
+int sux_node_set_spill_dir(sux_node* node, const char* dir) {
+  return guard([&] {
+    require(node, SUX_EINVAL, "NULL node");
+    std::string d = dir ? dir : "";
+    if (!d.empty()) {
+      struct stat st;
+      require(::stat(d.c_str(), &st) == 0 && S_ISDIR(st.st_mode), SUX_EIO,
+              "spill directory " + d + " does not exist");
+    }
+    std::lock_guard<std::mutex> lk(node->mu);
+    node->spill_dir = d;
+  });
+}
+
+int sux_node_spills(sux_node* node, uint64_t* spilled_maps) {
+  return guard([&] {
+    require(node && spilled_maps, SUX_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(node->mu);
+    *spilled_maps = node->spills;
   });
 }
 
@@ -778,6 +945,8 @@ int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
     require(t->sort_gather == 0 || t->sort_gather == 1, SUX_EINVAL, "sort_gather must be 0 or 1");
     require(t->sort_all_passes == 0 || t->sort_all_passes == 1, SUX_EINVAL,
             "sort_all_passes must be 0 or 1");
+    require(t->exchange_self >= -1 && t->exchange_self <= 1, SUX_EINVAL,
+            "exchange_self must be -1, 0 or 1");
     for (int32_t r : t->reserved) require(r == 0, SUX_EINVAL, "reserved tuning fields must be 0");
     require(node, SUX_EINVAL, "NULL node");
     std::lock_guard<std::mutex> lk(node->mu);
@@ -834,6 +1003,7 @@ int sux_node_destroy(sux_node* node) {
     node->shuffles.clear();
     for (auto& kv : node->ipc_bases) (void)hipIpcCloseMemHandle(kv.second);
     if (node->comm) (void)ncclCommDestroy(node->comm);
+    (void)hipGetLastError();  // see nccl_check
     delete node;
   });
 }
@@ -1301,6 +1471,143 @@ struct Staging {
     }
   }
 };
+
+// One map output (n device bytes at src, Spark's lengths[R]) -> a committed data + index file
+// pair: D2H of chunk k+1 overlaps the write() of chunk k; temp file, then commit_pair.
+void write_map_file(const uint8_t* src, uint64_t n, const int64_t* lengths, int R,
+                    const std::string& data, const std::string& index, hipStream_t s,
+                    Staging& st, int64_t* lengths_out) {
+  const std::string tmp = tmp_name(data);
+  const int fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+  require(fd >= 0, SUX_EIO, "open " + tmp + ": " + std::strerror(errno));
+  try {
+    const uint64_t nch = (n + Staging::kChunk - 1) / Staging::kChunk;
+    auto issue = [&](uint64_t k) {
+      const uint64_t a = k * Staging::kChunk, len = std::min<uint64_t>(Staging::kChunk, n - a);
+      hip_check(hipMemcpyAsync(st.h[k & 1], src + a, len, hipMemcpyDeviceToHost, s),
+                "hipMemcpy(data)");
+      hip_check(hipEventRecord(st.ev[k & 1], s), "hipEventRecord");
+    };
+    if (nch) issue(0);
+    for (uint64_t k = 0; k < nch; ++k) {
+      hip_check(hipEventSynchronize(st.ev[k & 1]), "hipEventSynchronize");
+      if (k + 1 < nch) issue(k + 1);
+      const uint64_t a = k * Staging::kChunk, len = std::min<uint64_t>(Staging::kChunk, n - a);
+      write_all(fd, st.h[k & 1], len, tmp);
+    }
+  } catch (...) {
+    ::close(fd);
+    ::unlink(tmp.c_str());
+    throw;
+  }
+  require(::close(fd) == 0, SUX_EIO, "close " + tmp);
+  commit_pair(index, data, tmp, lengths, R, lengths_out);
+}
+
+// Bytes [off, off + n) of a file -> device memory (pinned double buffer: the pread of chunk k+1
+// overlaps the H2D copy of chunk k).  Waits for the copies.
+void read_file_range(const std::string& path, uint64_t off, uint64_t n, uint8_t* dst,
+                     hipStream_t s, Staging& st) {
+  if (n == 0) return;
+  const int fd = ::open(path.c_str(), O_RDONLY);
+  require(fd >= 0, SUX_EIO, "open " + path + ": " + std::strerror(errno));
+  try {
+    const uint64_t nch = (n + Staging::kChunk - 1) / Staging::kChunk;
+    for (uint64_t k = 0; k < nch; ++k) {
+      const uint64_t o = k * Staging::kChunk, len = std::min<uint64_t>(Staging::kChunk, n - o);
+      if (k >= 2) hip_check(hipEventSynchronize(st.ev[k & 1]), "hipEventSynchronize");
+      uint64_t done = 0;
+      while (done < len) {
+        const ssize_t r = ::pread(fd, st.h[k & 1] + done, len - done, (off_t)(off + o + done));
+        if (r < 0 && errno == EINTR) continue;
+        require(r > 0, SUX_EIO, "read " + path + ": short file");
+        done += (uint64_t)r;
+      }
+      hip_check(hipMemcpyAsync(dst + o, st.h[k & 1], len, hipMemcpyHostToDevice, s),
+                "hipMemcpy(blocks)");
+      hip_check(hipEventRecord(st.ev[k & 1], s), "hipEventRecord");
+    }
+    hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+  } catch (...) {
+    ::close(fd);
+    throw;
+  }
+  ::close(fd);
+}
+
+// HBM-capacity fallback: spill whole slabs of committed, device-resident map outputs (world 1:
+// Spark's data files as they stand) to Spark's files under the spill directory until `need`
+// bytes of pool memory were returned, then free the pool's idle allocations.  Returns false
+// when nothing could be spilled.  The reference's map outputs live in such files from the start
+// (CommonUcxShuffleBlockResolver.scala:45-58 mmaps them).
+bool spill_some(sux_node* node, uint64_t need) {
+  std::unique_lock<std::mutex> lk(node->mu);
+  if (node->spill_dir.empty() || node->conf.world_size != 1) return false;
+  // candidate slabs: pool-owned, every map on them published and device-resident; oldest
+  // shuffle and lowest map first (the reducers of early maps run first)
+  std::vector<std::pair<Slab*, std::vector<std::pair<Shuffle*, int32_t>>>> victims;
+  std::map<Slab*, size_t> at;
+  for (auto& kv : node->shuffles) {
+    Shuffle& sh = *kv.second;
+    for (int32_t m = 0; m < sh.num_maps; ++m) {
+      MapSlot& sl = sh.maps[m];
+      if (!(sl.present && !sl.spilled() && sl.slab && sl.slab->pool && sl.owner == node->conf.rank))
+        continue;
+      auto f = at.find(sl.slab.get());
+      if (f == at.end()) {
+        f = at.emplace(sl.slab.get(), victims.size()).first;
+        victims.push_back({sl.slab.get(), {}});
+      }
+      victims[f->second].second.push_back({&sh, m});
+    }
+  }
+  if (victims.empty()) return false;
+  // in-flight readers of these buffers (fetch copies, exchanges) finish first
+  hip_check(hipDeviceSynchronize(), "sync before spill");
+  hipStream_t s = nullptr;
+  hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "spill stream");
+  uint64_t freed = 0;
+  try {
+    Staging st;
+    for (auto& v : victims) {
+      if (freed >= need) break;
+      const uint64_t cap = v.first->buf.cap;
+      for (auto& sm : v.second) {
+        Shuffle& sh = *sm.first;
+        MapSlot& sl = sh.maps[sm.second];
+        const std::string base = node->spill_dir + "/shuffle_" + std::to_string(sh.id) + "_" +
+                                 std::to_string(sm.second) + "_0";
+        std::vector<int64_t> lengths((size_t)sh.R);
+        for (int p = 0; p < sh.R; ++p) lengths[p] = sl.index[p + 1] - sl.index[p];
+        write_map_file(sl.data(), sl.bytes, lengths.data(), sh.R, base + ".data", base + ".index",
+                       s, st, nullptr);
+        sl.spill_data = base + ".data";
+        sl.spill_index = base + ".index";
+        sl.slab.reset();
+        node->spills++;
+      }
+      freed += cap;
+    }
+  } catch (...) {
+    (void)hipStreamDestroy(s);
+    throw;
+  }
+  (void)hipStreamDestroy(s);
+  lk.unlock();
+  node->pool->trim();
+  return freed > 0;
+}
+
+// A pool buffer; on SUX_ENOMEM spill map outputs (if configured) and retry.
+PoolBuf pool_get_or_spill(sux_node* node, uint64_t bytes) {
+  for (int attempt = 0;; ++attempt) {
+    try {
+      return node->pool->get(bytes);
+    } catch (const SuxError& e) {
+      if (e.code != SUX_ENOMEM || attempt >= 64 || !spill_some(node, bytes)) throw;
+    }
+  }
+}
 }  // namespace
 
 extern "C" {
@@ -1338,33 +1645,9 @@ int sux_write_map_files(sux_node* node, const void* d_data, const int64_t* d_ind
       for (int p = 0; p < R; ++p) lengths[p] = im[p + 1] - im[p];
       const uint64_t n = (uint64_t)im[R];
       require(d_data || n == 0, SUX_EINVAL, "data pointer is NULL");
-      const std::string data = data_paths[m], index = index_paths[m], tmp = tmp_name(data);
-      const int fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
-      require(fd >= 0, SUX_EIO, "open " + tmp + ": " + std::strerror(errno));
-      try {
-        const uint8_t* src = static_cast<const uint8_t*>(d_data) + base;
-        const uint64_t nch = (n + Staging::kChunk - 1) / Staging::kChunk;
-        auto issue = [&](uint64_t k) {
-          const uint64_t a = k * Staging::kChunk, len = std::min<uint64_t>(Staging::kChunk, n - a);
-          hip_check(hipMemcpyAsync(st.h[k & 1], src + a, len, hipMemcpyDeviceToHost, s),
-                    "hipMemcpy(data)");
-          hip_check(hipEventRecord(st.ev[k & 1], s), "hipEventRecord");
-        };
-        if (nch) issue(0);
-        for (uint64_t k = 0; k < nch; ++k) {
-          hip_check(hipEventSynchronize(st.ev[k & 1]), "hipEventSynchronize");
-          if (k + 1 < nch) issue(k + 1);
-          const uint64_t a = k * Staging::kChunk, len = std::min<uint64_t>(Staging::kChunk, n - a);
-          write_all(fd, st.h[k & 1], len, tmp);
-        }
-      } catch (...) {
-        ::close(fd);
-        ::unlink(tmp.c_str());
-        throw;
-      }
-      require(::close(fd) == 0, SUX_EIO, "close " + tmp);
-      commit_pair(index, data, tmp, lengths.data(), R,
-                  lengths_out ? lengths_out + (size_t)m * R : nullptr);
+      write_map_file(static_cast<const uint8_t*>(d_data) + base, n, lengths.data(), R,
+                     data_paths[m], index_paths[m], s, st,
+                     lengths_out ? lengths_out + (size_t)m * R : nullptr);
       base += n;
     }
   });
@@ -1398,32 +1681,9 @@ int sux_read_file_blocks(sux_node* node, const char* data_path, const char* inde
     *bytes = n;
     if (n == 0) return;
     node->bind();
-    hipStream_t s = node->stream(stream);
-    const int fd = ::open(data_path, O_RDONLY);
-    require(fd >= 0, SUX_EIO, std::string("open ") + data_path + ": " + std::strerror(errno));
     Staging st;
-    try {
-      const uint64_t nch = (n + Staging::kChunk - 1) / Staging::kChunk;
-      for (uint64_t k = 0; k < nch; ++k) {
-        const uint64_t o = k * Staging::kChunk, len = std::min<uint64_t>(Staging::kChunk, n - o);
-        if (k >= 2) hip_check(hipEventSynchronize(st.ev[k & 1]), "hipEventSynchronize");
-        uint64_t done = 0;
-        while (done < len) {
-          const ssize_t r = ::pread(fd, st.h[k & 1] + done, len - done, (off_t)(a + o + done));
-          if (r < 0 && errno == EINTR) continue;
-          require(r > 0, SUX_EIO, std::string("read ") + data_path + ": short file");
-          done += (uint64_t)r;
-        }
-        hip_check(hipMemcpyAsync(static_cast<uint8_t*>(d_dst) + o, st.h[k & 1], len,
-                                 hipMemcpyHostToDevice, s), "hipMemcpy(blocks)");
-        hip_check(hipEventRecord(st.ev[k & 1], s), "hipEventRecord");
-      }
-      hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
-    } catch (...) {
-      ::close(fd);
-      throw;
-    }
-    ::close(fd);
+    read_file_range(data_path, (uint64_t)a, n, static_cast<uint8_t*>(d_dst), node->stream(stream),
+                    st);
   });
 }
 
@@ -1625,6 +1885,10 @@ int sux_unregister_shuffle(sux_node* node, int32_t shuffle_id) {
       std::unique_lock<std::mutex> lk(node->mu);
       Shuffle& sh = node->shuffle(shuffle_id);
       require(!sh.exchanging, SUX_ESTATE, "shuffle " + std::to_string(shuffle_id) + " is exchanging");
+      // IPC pulls: peers may still read this rank's slabs until the closing all-gather
+      require(!sh.ack_due, SUX_ESTATE,
+              "shuffle " + std::to_string(shuffle_id) +
+                  " has an exchange not yet completed by sux_exchange_wait");
       drain(node, sh, lk);  // writes in flight finish before their slabs go back
       gone = std::move(node->shuffles[shuffle_id]);
       node->shuffles.erase(shuffle_id);
@@ -1658,6 +1922,7 @@ int sux_write_map_outputs(sux_node* node, int32_t shuffle_id, int32_t first,
       require(part->desc.num_partitions == sh.R, SUX_EINVAL,
               "partitioner has " + std::to_string(part->desc.num_partitions) +
                   " partitions, shuffle has " + std::to_string(sh.R));
+      require(sh.R >= node->conf.world_size, SUX_EINVAL, "need at least one partition per rank");
       progress(node, sh, lk, false);
       R = sh.R;
       rs = (uint32_t)sh.rec_size;
@@ -1696,18 +1961,26 @@ int sux_write_map_outputs(sux_node* node, int32_t shuffle_id, int32_t first,
     // stream (its input is ready there) and joined back into it (the caller may reuse the
     // input buffer after its own stream's later work, as with a launch on `stream` itself).
     hipStream_t ms = s;
+    // at world > 1 the batch is written peer-major: every peer's share of it is one contiguous
+    // range, so the exchange sends the slab as it stands (one all-to-all per batch, no repack)
+    const int32_t W = node->conf.world_size;
+    job->world = W;
     try {
       Group G = make_group(part, d_records, rs, rpm, n);
-      job->slab = std::make_shared<Slab>(node->pool.get(), node->pool->get(n * rs));
-      job->ws = node->pool->get(G.ws.total + 8 * maps * (uint64_t)(R + 1) + 256);
+      job->slab = std::make_shared<Slab>(node->pool.get(), pool_get_or_spill(node, n * rs));
+      job->ws = pool_get_or_spill(node, G.ws.total + 8 * maps * (uint64_t)(R + 1) + 256);
       int64_t* d_idx = reinterpret_cast<int64_t*>(job->ws.ptr + (G.ws.total + 255) / 256 * 256);
       job->hidx = node->hpool.get(8 * maps * (uint64_t)(R + 1));
+      {
+        std::lock_guard<std::mutex> lk(node->mu);
+        job->batch = node->shuffle(shuffle_id).next_batch++;
+      }
       std::lock_guard<std::mutex> plk(node->pipe_mu);
       node->make_pipe();
       ms = node->pipe[node->pipe_next++ & 1];
       hip_check(hipEventRecord(node->pipe_ev[0], s), "fork");
       hip_check(hipStreamWaitEvent(ms, node->pipe_ev[0], 0), "fork");
-      run_group(node, part, G, 1, job->slab->buf.ptr, d_idx, nullptr, nullptr, nullptr,
+      run_group(node, part, G, W, job->slab->buf.ptr, d_idx, nullptr, nullptr, nullptr,
                 job->ws.ptr, G.ws.total, ms, true);
       hip_check(hipMemcpyAsync(job->hidx.first, d_idx, 8 * maps * (uint64_t)(R + 1),
                                hipMemcpyDeviceToHost, ms),
@@ -1717,15 +1990,9 @@ int sux_write_map_outputs(sux_node* node, int32_t shuffle_id, int32_t first,
       hip_check(hipStreamWaitEvent(s, job->done->e, 0), "join");
     } catch (...) {
       unclaim();
-      if (!job->done) {  // nothing reached the stream that still needs the buffers
-        (void)hipStreamSynchronize(ms);
-        node->pool->put(job->ws);
-        node->hpool.put(job->hidx);
-      } else {
-        (void)hipStreamSynchronize(ms);
-        node->pool->put(job->ws);
-        node->hpool.put(job->hidx);
-      }
+      (void)hipStreamSynchronize(ms);  // nothing on the stream may still use the buffers
+      node->pool->put(job->ws);
+      node->hpool.put(job->hidx);
       throw;
     }
     std::lock_guard<std::mutex> lk(node->mu);
@@ -1849,13 +2116,90 @@ int sux_commit_map_output(sux_node* node, int32_t shuffle_id, int32_t map_index,
     MapSlot& slot = sh.maps[map_index];
     slot.pending = false;
     slot.present = true;
+    slot.sent = false;
     slot.owner = node->conf.rank;
+    slot.batch = sh.next_batch++;  // a committed data file is its own exchange piece
     slot.slab = slab;
     slot.off = 0;
     slot.bytes = bytes;
     slot.index = std::move(index);
-    sh.exchanged = false;
+    slot.rslab.reset();
+    const int NW = node->conf.world_size;
+    slot.seg.resize((size_t)NW);
+    for (int h = 0; h < NW; ++h) slot.seg[h] = (uint64_t)slot.index[owner_lo(h, sh.R, NW)];
     publish_slot(node, sh, map_index, 0);
+  });
+}
+
+int sux_adopt_map_outputs(sux_node* node, int32_t shuffle_id, int32_t first,
+                          const void* d_out, uint64_t rpm, uint64_t n, const int64_t* d_index,
+                          void* stream) {
+  return guard([&] {
+    require(node && d_index && (d_out || n == 0), SUX_EINVAL, "NULL argument");
+    require(rpm > 0, SUX_EINVAL, "records_per_map must be > 0");
+    if (n == 0) return;
+    node->bind();
+    hipStream_t s = node->stream(stream);
+    const uint64_t maps = (n + rpm - 1) / rpm;
+    auto job = std::make_unique<WriteJob>();
+    int R = 0;
+    {
+      std::unique_lock<std::mutex> lk(node->mu);
+      Shuffle& sh = node->shuffle(shuffle_id);
+      require(first >= 0 && (uint64_t)first + maps <= (uint64_t)sh.num_maps, SUX_EINVAL,
+              "maps [" + std::to_string(first) + ", " + std::to_string((uint64_t)first + maps) +
+                  ") out of [0, " + std::to_string(sh.num_maps) + ")");
+      progress(node, sh, lk, false);
+      R = sh.R;
+      job->claimed.assign((size_t)maps, 0);
+      bool any = false;
+      for (uint64_t k = 0; k < maps; ++k) {
+        MapSlot& sl = sh.maps[first + k];
+        if (sl.present || sl.pending) continue;  // first commit wins
+        sl.pending = true;
+        job->claimed[k] = 1;
+        any = true;
+      }
+      if (!any) return;
+      sh.submitting++;
+      // map-major outputs: one exchange piece per map at world > 1, the whole batch at world 1
+      job->batch = node->conf.world_size == 1 ? sh.next_batch++ : -1;
+    }
+    job->first = first;
+    job->maps = (uint32_t)maps;
+    job->rpm = rpm;
+    job->n = n;
+    job->world = 1;
+    PoolBuf borrowed;
+    borrowed.ptr = static_cast<uint8_t*>(const_cast<void*>(d_out));
+    borrowed.cap = 0;
+    job->slab = std::make_shared<Slab>(nullptr, borrowed);  // not the node's: nothing to free
+    try {
+      job->hidx = node->hpool.get(8 * maps * (uint64_t)(R + 1));
+      hip_check(hipMemcpyAsync(job->hidx.first, d_index, 8 * maps * (uint64_t)(R + 1),
+                               hipMemcpyDeviceToHost, s),
+                "D2H index");
+      job->done = std::make_shared<Event>();
+      hip_check(hipEventRecord(job->done->e, s), "hipEventRecord");
+    } catch (...) {
+      (void)hipStreamSynchronize(s);
+      node->hpool.put(job->hidx);
+      std::lock_guard<std::mutex> lk(node->mu);
+      auto it = node->shuffles.find(shuffle_id);
+      if (it != node->shuffles.end()) {
+        for (uint64_t k = 0; k < maps; ++k)
+          if (job->claimed[k]) it->second->maps[first + k].pending = false;
+        it->second->submitting--;
+      }
+      node->cv.notify_all();
+      throw;
+    }
+    std::lock_guard<std::mutex> lk(node->mu);
+    auto it = node->shuffles.find(shuffle_id);
+    require(it != node->shuffles.end(), SUX_ENOENT, "shuffle unregistered during the commit");
+    it->second->jobs.push_back(std::move(job));
+    it->second->submitting--;
+    node->cv.notify_all();
   });
 }
 
@@ -1891,19 +2235,27 @@ int sux_owned_partitions(sux_node* node, int32_t shuffle_id, int32_t rank, int32
 }  // extern "C"
 
 namespace {
-// One committed map as every rank sees it after the directory all-gather.
+// One committed map as every rank sees it after the directory all-gather: the DriverMetadata
+// slot (UcxWorkerWrapper.scala:27-65) plus what the all-to-all needs — the batch (exchange
+// piece) it belongs to and, per peer h, the offset of its range for h in the batch's slab.
 struct DirEntry {
-  int32_t map = -1, owner = -1;
-  std::vector<int64_t> index;
-  uint8_t ipc[SUX_IPC_DESC_BYTES] = {};  // owner's data buffer (bootstrap transport only)
+  int32_t map = -1, owner = -1, batch = -1;
+  std::vector<int64_t> index;  // R + 1
+  std::vector<uint64_t> seg;   // world
+  uint8_t ipc[SUX_IPC_DESC_BYTES] = {};  // the batch slab (IPC transport only)
 };
 
 // Host all-gather of `bytes` per rank: the embedding runtime's bootstrap, or RCCL through a
 // device bounce buffer.  The caller holds no node lock.
-void host_allgather(sux_node* node, const void* send, uint64_t bytes, void* recv, hipStream_t s) {
+void host_allgather(sux_node* node, uint64_t tag, const void* send, uint64_t bytes, void* recv,
+                    hipStream_t s) {
   const int W = node->conf.world_size;
+  if (W == 1 && !node->boot && !node->comm) {  // one rank, no transport: nothing to gather
+    if (bytes) std::memcpy(recv, send, bytes);
+    return;
+  }
   if (node->boot) {
-    const int rc = node->boot(node->boot_ctx, send, bytes, recv);
+    const int rc = node->boot(node->boot_ctx, tag, send, bytes, recv);
     require(rc == 0, SUX_ECOMM, "bootstrap all-gather failed (" + std::to_string(rc) + ")");
     return;
   }
@@ -1929,18 +2281,22 @@ void host_allgather(sux_node* node, const void* send, uint64_t bytes, void* recv
 }
 
 // DriverMetadata analog (UcxWorkerWrapper.scala:27-65): every rank contributes one entry per
-// map it committed — |i32 map|i32 owner|(R+1) x i64 index|72-byte IPC descriptor| — padded to
-// the largest contribution; the merged table replaces the per-map driver slots fetched by
-// fetchDriverMetadataBuffer (:176-196).
-std::vector<DirEntry> gather_directory(sux_node* node, int R, const std::vector<DirEntry>& mine,
-                                       hipStream_t s) {
+// map of the window it committed — |i32 map|i32 owner|i32 batch|i32 0|(R+1) x i64 index|
+// W x u64 seg|72-byte IPC descriptor| — padded to the largest contribution; the merged table
+// replaces the per-map driver slots fetched by fetchDriverMetadataBuffer (:176-196) and the
+// phase-1 offset GETs (UcxShuffleClient.java:50-92).
+std::vector<DirEntry> gather_directory(sux_node* node, uint64_t tag, int R,
+                                       const std::vector<DirEntry>& mine, hipStream_t s) {
   const int W = node->conf.world_size;
-  const uint64_t E = 8 + 8 * (uint64_t)(R + 1) + SUX_IPC_DESC_BYTES;
+  const uint64_t E = 16 + 8 * (uint64_t)(R + 1) + 8 * (uint64_t)W + SUX_IPC_DESC_BYTES;
   int64_t cnt = (int64_t)mine.size();
   std::vector<int64_t> cnts((size_t)W);
-  host_allgather(node, &cnt, 8, cnts.data(), s);
+  host_allgather(node, tag, &cnt, 8, cnts.data(), s);
   int64_t most = 0;
-  for (int64_t c : cnts) most = std::max(most, c);
+  for (int64_t c : cnts) {
+    require(c >= 0, SUX_ECOMM, "malformed directory count");
+    most = std::max(most, c);
+  }
   std::vector<DirEntry> all;
   if (most == 0) return all;
   std::vector<uint8_t> send((size_t)(most * E), 0), recv((size_t)(most * E * W));
@@ -1948,19 +2304,24 @@ std::vector<DirEntry> gather_directory(sux_node* node, int R, const std::vector<
     uint8_t* e = send.data() + k * E;
     std::memcpy(e, &mine[k].map, 4);
     std::memcpy(e + 4, &mine[k].owner, 4);
-    std::memcpy(e + 8, mine[k].index.data(), 8 * (size_t)(R + 1));
-    std::memcpy(e + 8 + 8 * (size_t)(R + 1), mine[k].ipc, SUX_IPC_DESC_BYTES);
+    std::memcpy(e + 8, &mine[k].batch, 4);
+    std::memcpy(e + 16, mine[k].index.data(), 8 * (size_t)(R + 1));
+    std::memcpy(e + 16 + 8 * (size_t)(R + 1), mine[k].seg.data(), 8 * (size_t)W);
+    std::memcpy(e + 16 + 8 * (size_t)(R + 1) + 8 * (size_t)W, mine[k].ipc, SUX_IPC_DESC_BYTES);
   }
-  host_allgather(node, send.data(), send.size(), recv.data(), s);
+  host_allgather(node, tag + 1, send.data(), send.size(), recv.data(), s);
   for (int r = 0; r < W; ++r)
     for (int64_t k = 0; k < cnts[r]; ++k) {
       const uint8_t* e = recv.data() + ((uint64_t)r * most + k) * E;
       DirEntry d;
       std::memcpy(&d.map, e, 4);
       std::memcpy(&d.owner, e + 4, 4);
+      std::memcpy(&d.batch, e + 8, 4);
       d.index.resize((size_t)R + 1);
-      std::memcpy(d.index.data(), e + 8, 8 * (size_t)(R + 1));
-      std::memcpy(d.ipc, e + 8 + 8 * (size_t)(R + 1), SUX_IPC_DESC_BYTES);
+      std::memcpy(d.index.data(), e + 16, 8 * (size_t)(R + 1));
+      d.seg.resize((size_t)W);
+      std::memcpy(d.seg.data(), e + 16 + 8 * (size_t)(R + 1), 8 * (size_t)W);
+      std::memcpy(d.ipc, e + 16 + 8 * (size_t)(R + 1) + 8 * (size_t)W, SUX_IPC_DESC_BYTES);
       all.push_back(std::move(d));
     }
   return all;
@@ -1978,8 +2339,10 @@ void export_ipc(const void* p, uint8_t out[SUX_IPC_DESC_BYTES]) {
 }
 
 // Copy descriptors -> one gather-copy launch (64 KiB chunks, block i to its own destination).
+// `aux` (device tables) and `hostblk` (their pinned staging) stay with the caller until the
+// stream has run the launch.
 void launch_copies(sux_node* node, const std::vector<sux::CopyDesc>& desc, PoolBuf& aux,
-                   hipStream_t s) {
+                   std::pair<void*, uint64_t>& hostblk, hipStream_t s) {
   if (desc.empty()) return;
   std::vector<uint32_t> first(desc.size());
   uint64_t chunks = 0;
@@ -1990,15 +2353,101 @@ void launch_copies(sux_node* node, const std::vector<sux::CopyDesc>& desc, PoolB
   }
   require(chunks < (1ull << 31), SUX_ERANGE, "copy request too large");
   const uint64_t dbytes = desc.size() * sizeof(sux::CopyDesc), fbytes = first.size() * 4;
-  aux = node->pool->get(dbytes + 256 + fbytes);
-  uint8_t* d_desc = aux.ptr;
-  uint8_t* d_first = aux.ptr + ((dbytes + 255) / 256) * 256;
-  hip_check(hipMemcpyAsync(d_desc, desc.data(), dbytes, hipMemcpyHostToDevice, s), "H2D desc");
-  hip_check(hipMemcpyAsync(d_first, first.data(), fbytes, hipMemcpyHostToDevice, s), "H2D chunks");
-  hip_check(sux::launch_gather_copy(reinterpret_cast<const sux::CopyDesc*>(d_desc),
+  const uint64_t dpad = ((dbytes + 255) / 256) * 256;
+  aux = node->pool->get(dpad + fbytes);
+  hostblk = node->hpool.get(dpad + fbytes);
+  uint8_t* h = static_cast<uint8_t*>(hostblk.first);
+  std::memcpy(h, desc.data(), dbytes);
+  std::memcpy(h + dpad, first.data(), fbytes);
+  hip_check(hipMemcpyAsync(aux.ptr, h, dpad + fbytes, hipMemcpyHostToDevice, s), "H2D desc");
+  hip_check(sux::launch_gather_copy(reinterpret_cast<const sux::CopyDesc*>(aux.ptr),
                                     (uint32_t)desc.size(), (uint32_t)chunks,
-                                    reinterpret_cast<const uint32_t*>(d_first), &node->timer, s),
+                                    reinterpret_cast<const uint32_t*>(aux.ptr + dpad),
+                                    &node->timer, s),
             "gather copy");
+}
+
+// The exchange plan of one window (host arithmetic; every rank computes it from the same
+// gathered directory, so the counts of the collective agree).  A piece = the maps of one batch of
+// one owner; owner g's pieces, in batch order, are its rounds 0, 1, ...; round k is one
+// partition-aligned all-to-all of every owner's k-th piece.  In a piece the maps' ranges for
+// peer h are consecutive in the batch slab (peer-major [h][map][h's partitions]), so h's share of
+// the piece is ONE range [a_h, e_h): sendcounts/sdispls come straight from the index tables,
+// like ncclAllToAllv's counts in SURVEY.md §8(e), and the slab is the send buffer as it stands.
+struct XPlan {
+  int rounds = 0;
+  std::vector<uint64_t> sc, sd, rc, rd;  // [round][peer]
+  std::vector<int32_t> piece;            // [round][owner]: the piece's first (lowest-map) entry
+  std::vector<uint64_t> base;            // [round + 1]: receive-buffer offset of each round
+  std::vector<uint64_t> recv_off;        // [entry]: offset of its owned range (UINT64_MAX: none)
+};
+
+XPlan plan_exchange(int W, int me, bool loopback, int n, const int32_t* map, const int32_t* owner,
+                    const int32_t* batch, const uint64_t* seg, const uint64_t* len) {
+  XPlan P;
+  // pieces per owner, ordered by batch; entries of a piece ordered by map
+  std::vector<std::map<int32_t, std::vector<int32_t>>> pieces((size_t)W);
+  for (int i = 0; i < n; ++i) {
+    require(owner[i] >= 0 && owner[i] < W, SUX_ESTATE, "directory entry with a bad owner");
+    pieces[owner[i]][batch[i]].push_back(i);
+  }
+  for (auto& pg : pieces)
+    for (auto& kv : pg)
+      std::sort(kv.second.begin(), kv.second.end(),
+                [&](int32_t a, int32_t b) { return map[a] < map[b]; });
+  for (auto& pg : pieces) P.rounds = std::max(P.rounds, (int)pg.size());
+  const size_t RW = (size_t)P.rounds * W;
+  P.sc.assign(RW, 0);
+  P.sd.assign(RW, 0);
+  P.rc.assign(RW, 0);
+  P.rd.assign(RW, 0);
+  P.piece.assign(RW, -1);
+  P.base.assign((size_t)P.rounds + 1, 0);
+  P.recv_off.assign((size_t)n, UINT64_MAX);
+  // [a_h, e_h) of a piece for peer h
+  auto span = [&](const std::vector<int32_t>& ents, int h, uint64_t& a, uint64_t& e) {
+    a = UINT64_MAX;
+    e = 0;
+    for (int32_t i : ents) {
+      a = std::min(a, seg[(size_t)i * W + h]);
+      e = std::max(e, seg[(size_t)i * W + h] + len[(size_t)i * W + h]);
+    }
+    if (e < a) e = a;
+  };
+  std::vector<std::map<int32_t, std::vector<int32_t>>::const_iterator> it((size_t)W);
+  for (int g = 0; g < W; ++g) it[g] = pieces[g].begin();
+  uint64_t base = 0;
+  for (int k = 0; k < P.rounds; ++k) {
+    P.base[k] = base;
+    uint64_t racc = 0;
+    for (int g = 0; g < W; ++g) {
+      const size_t kg = (size_t)k * W + g;
+      P.rd[kg] = racc;
+      if (it[g] == pieces[g].end()) continue;
+      const std::vector<int32_t>& ents = it[g]->second;
+      P.piece[kg] = ents.front();
+      if (g == me) {  // this rank's send side of the round
+        for (int h = 0; h < W; ++h) {
+          uint64_t a, e;
+          span(ents, h, a, e);
+          P.sd[(size_t)k * W + h] = a;
+          P.sc[(size_t)k * W + h] = (h == me && !loopback) ? 0 : e - a;
+        }
+      }
+      if (g != me || loopback) {
+        uint64_t a, e;
+        span(ents, me, a, e);
+        P.rc[kg] = e - a;
+        for (int32_t i : ents) P.recv_off[i] = base + racc + (seg[(size_t)i * W + me] - a);
+        racc += e - a;
+      }
+    }
+    for (int g = 0; g < W; ++g)
+      if (it[g] != pieces[g].end()) ++it[g];
+    base += racc;
+  }
+  P.base[P.rounds] = base;
+  return P;
 }
 
 struct ExchangingFlag {  // clears Shuffle::exchanging on every exit path
@@ -2014,161 +2463,320 @@ struct ExchangingFlag {  // clears Shuffle::exchanging on every exit path
 
 extern "C" {
 
-// Shuffle-level exchange: directory all-gather, then every rank's owned range of every remote
-// map moves into one exact-size receive buffer — grouped ncclSend/ncclRecv (RCCL), or one
-// gather-copy of one-sided pulls from the owners' IPC-mapped buffers (bootstrap transport).
-int sux_exchange(sux_node* node, int32_t shuffle_id, void* stream) {
+int sux_plan_exchange(int32_t world, int32_t rank, int32_t loopback, int32_t n,
+                      const sux_xplan_entry* entries, const uint64_t* seg, const uint64_t* len,
+                      int32_t max_rounds, int32_t* rounds, uint64_t* counts, int32_t* piece_entry,
+                      uint64_t* round_base, uint64_t* recv_off) {
+  return guard([&] {
+    require(world >= 1 && rank >= 0 && rank < world && n >= 0 && rounds, SUX_EINVAL, "bad plan shape");
+    require(n == 0 || (entries && seg && len), SUX_EINVAL, "NULL argument");
+    std::vector<int32_t> m((size_t)n), o((size_t)n), b((size_t)n);
+    for (int i = 0; i < n; ++i) {
+      m[i] = entries[i].map;
+      o[i] = entries[i].owner;
+      b[i] = entries[i].batch;
+    }
+    const XPlan P = plan_exchange(world, rank, loopback != 0, n, m.data(), o.data(), b.data(), seg, len);
+    *rounds = P.rounds;
+    require(P.rounds <= max_rounds, SUX_ERANGE, "plan has " + std::to_string(P.rounds) + " rounds");
+    for (int k = 0; k < P.rounds; ++k)
+      for (int h = 0; h < world; ++h) {
+        const size_t kh = (size_t)k * world + h;
+        if (counts) {
+          counts[(size_t)k * 4 * world + h] = P.sc[kh];
+          counts[(size_t)k * 4 * world + world + h] = P.sd[kh];
+          counts[(size_t)k * 4 * world + 2 * world + h] = P.rc[kh];
+          counts[(size_t)k * 4 * world + 3 * world + h] = P.rd[kh];
+        }
+        if (piece_entry) piece_entry[kh] = P.piece[kh];
+      }
+    if (round_base)
+      for (int k = 0; k <= P.rounds; ++k) round_base[k] = P.base[k];
+    if (recv_off)
+      for (int i = 0; i < n; ++i) recv_off[i] = P.recv_off[i];
+  });
+}
+
+// Asynchronous exchange of one window of maps (see the header): directory all-gather, then one
+// partition-aligned ncclAllToAllv per round of batches, or the same plan as one gather-copy of
+// one-sided pulls from the owners' IPC-mapped slabs (bootstrap transport).
+int sux_exchange_maps(sux_node* node, int32_t shuffle_id, int32_t first, int32_t count,
+                      void* stream) {
   return guard([&] {
     require(node, SUX_EINVAL, "NULL node");
     node->bind();
     hipStream_t s = node->stream(stream);
     const int W = node->conf.world_size, me = node->conf.rank;
-    int R = 0, M = 0;
+    bool loopback = false;
+    int R = 0;
+    uint64_t tag = 0;
     std::vector<DirEntry> mine;
-    std::vector<std::shared_ptr<Slab>> keep;  // own map outputs stay alive while peers read
-    std::vector<uint8_t*> own_data;
+    std::vector<std::shared_ptr<Slab>> mine_slab;
     {
       std::unique_lock<std::mutex> lk(node->mu);
       Shuffle& sh = node->shuffle(shuffle_id);
-      require(!sh.exchanging, SUX_ESTATE, "shuffle " + std::to_string(shuffle_id) + " is already exchanging");
-      drain(node, sh, lk);
-      if (W == 1) {
-        sh.exchanged = true;
-        return;
-      }
+      require(first >= 0 && count >= 0 && (int64_t)first + count <= sh.num_maps, SUX_EINVAL,
+              "window [" + std::to_string(first) + ", +" + std::to_string(count) +
+                  ") out of the shuffle's maps");
+      require(!sh.exchanging, SUX_ESTATE,
+              "shuffle " + std::to_string(shuffle_id) + " is already exchanging");
+      loopback = node->tuning.exchange_self > 0;
+      drain_range(node, sh, lk, first, first + count);
+      if (W == 1 && !loopback) return;  // every block is local: resolve reads it in place
       R = sh.R;
-      M = sh.num_maps;
       require(R >= W, SUX_EINVAL, "need at least one partition per rank");
       sh.exchanging = true;
-      for (int m = 0; m < M; ++m) {
+      tag = ((uint64_t)(uint32_t)shuffle_id << 32) | sh.gathers;
+      sh.gathers += 3;
+      for (int m = first; m < first + count; ++m) {
         const MapSlot& sl = sh.maps[m];
-        if (!sl.present || sl.owner != me || !sl.slab) continue;
+        if (!sl.present || sl.owner != me || sl.sent || !sl.slab || sl.spilled()) continue;
         DirEntry d;
         d.map = m;
         d.owner = me;
+        d.batch = sl.batch;
         d.index = sl.index;
+        d.seg = sl.seg;
         mine.push_back(std::move(d));
-        keep.push_back(sl.slab);
-        own_data.push_back(sl.data());
+        mine_slab.push_back(sl.slab);
       }
     }
     ExchangingFlag flag{node, shuffle_id};
     const bool ipc = node->comm == nullptr;
-    if (ipc)
-      for (size_t k = 0; k < mine.size(); ++k) export_ipc(own_data[k], mine[k].ipc);
-    // 1. directory (replaces the driver table + the phase-1 offset GETs)
-    std::vector<DirEntry> all = gather_directory(node, R, mine, s);
-    std::vector<int32_t> owner_of((size_t)M, -1);
-    std::vector<const DirEntry*> entry((size_t)M, nullptr);
-    for (const auto& d : all) {
-      require(d.map >= 0 && d.map < M && d.owner >= 0 && d.owner < W, SUX_ESTATE,
-              "malformed directory entry");
-      require(owner_of[d.map] < 0, SUX_ESTATE,
+    // every batch slab is exported (the IPC transport pulls from it; with either transport any
+    // rank may later read a block its owner serves from it)
+    for (size_t k = 0; k < mine.size(); ++k) export_ipc(mine_slab[k]->buf.ptr, mine[k].ipc);
+    // 1. directory of the window (replaces the driver table + the phase-1 offset GETs)
+    std::vector<DirEntry> all = gather_directory(node, tag, R, mine, s);
+    const int n = (int)all.size();
+    std::vector<int32_t> em((size_t)n), eo((size_t)n), eb((size_t)n);
+    std::vector<uint64_t> seg((size_t)n * W), len((size_t)n * W);
+    std::vector<int32_t> seen((size_t)first + count, -1);
+    for (int i = 0; i < n; ++i) {
+      const DirEntry& d = all[i];
+      require(d.map >= first && d.map < first + count && d.owner >= 0 && d.owner < W,
+              SUX_ESTATE, "malformed directory entry");
+      require(seen[d.map] < 0, SUX_ESTATE,
               "map " + std::to_string(d.map) + " committed by more than one rank");
-      owner_of[d.map] = d.owner;
-      entry[d.map] = &d;
+      seen[d.map] = d.owner;
+      em[i] = d.map;
+      eo[i] = d.owner;
+      eb[i] = d.batch;
+      for (int h = 0; h < W; ++h) {
+        seg[(size_t)i * W + h] = d.seg[h];
+        len[(size_t)i * W + h] =
+            (uint64_t)(d.index[owner_lo(h + 1, R, W)] - d.index[owner_lo(h, R, W)]);
+      }
     }
-    // 2. receive layout: remote maps in map order, each holding this rank's owned range
-    const int lo = owner_lo(me, R, W), hi = owner_lo(me + 1, R, W);
-    std::vector<uint64_t> roff((size_t)M, 0);
-    uint64_t total = 0;
-    for (int m = 0; m < M; ++m) {
-      if (owner_of[m] < 0 || owner_of[m] == me) continue;
-      roff[m] = total;
-      total += (uint64_t)(entry[m]->index[hi] - entry[m]->index[lo]);
-    }
-    PoolBuf recv = total ? node->pool->get(total) : PoolBuf{};
+    // 2. the plan: rounds of partition-aligned all-to-alls, receive layout [round][source]
+    const XPlan P = plan_exchange(W, me, loopback, n, em.data(), eo.data(), eb.data(), seg.data(),
+                                  len.data());
+    const uint64_t total = P.base[P.rounds];
+    auto recv = std::make_shared<Slab>(node->pool.get(), total ? pool_get_or_spill(node, total)
+                                                               : PoolBuf{});
+    // this rank's batch slabs by batch id (the send buffers)
+    std::map<int32_t, uint8_t*> my_slab;
+    for (size_t k = 0; k < mine.size(); ++k) my_slab[mine[k].batch] = mine_slab[k]->buf.ptr;
     PoolBuf aux;
-    std::map<std::string, void*> opened;
+    std::pair<void*, uint64_t> hostblk{nullptr, 0};
     try {
       if (!ipc) {
-        // 3a. RCCL: identical chunk boundaries on every rank (grouped calls of <= 64 maps)
-        std::vector<uint8_t*> src((size_t)M, nullptr);
-        for (size_t k = 0; k < mine.size(); ++k) src[mine[k].map] = own_data[k];
-        const int kChunk = 64;
-        for (int m0 = 0; m0 < M; m0 += kChunk) {
-          nccl_check(ncclGroupStart(), "ncclGroupStart");
-          for (int m = m0; m < std::min(M, m0 + kChunk); ++m) {
-            if (owner_of[m] < 0) continue;
-            const std::vector<int64_t>& ix = entry[m]->index;
-            if (owner_of[m] == me) {
-              for (int h = 0; h < W; ++h) {
-                if (h == me) continue;
-                const int64_t a = ix[owner_lo(h, R, W)], b = ix[owner_lo(h + 1, R, W)];
-                if (b > a)
-                  nccl_check(ncclSend(src[m] + a, (size_t)(b - a), ncclUint8, h, node->comm, s),
-                             "ncclSend");
-              }
-            } else if (ix[hi] > ix[lo]) {
-              nccl_check(ncclRecv(recv.ptr + roff[m], (size_t)(ix[hi] - ix[lo]), ncclUint8,
-                                  owner_of[m], node->comm, s),
-                         "ncclRecv");
-            }
+        // 3a. RCCL: one ncclAllToAllv per round (grouped send/recv over xGMI inside RCCL)
+        std::vector<size_t> a((size_t)W), b((size_t)W), c((size_t)W), d((size_t)W);
+        for (int k = 0; k < P.rounds; ++k) {
+          const int32_t pe = P.piece[(size_t)k * W + me];
+          uint8_t* sendbuf = pe >= 0 ? my_slab.at(all[pe].batch) : nullptr;
+          uint8_t* recvbuf = recv->buf.ptr ? recv->buf.ptr + P.base[k] : nullptr;
+          // RCCL rejects NULL buffers even for zero counts: any device word will do
+          uint8_t* dummy = reinterpret_cast<uint8_t*>(node->d_err);
+          for (int h = 0; h < W; ++h) {
+            const size_t kh = (size_t)k * W + h;
+            a[h] = P.sc[kh];
+            b[h] = P.sd[kh];
+            c[h] = P.rc[kh];
+            d[h] = P.rd[kh];
           }
-          nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+          nccl_check(ncclAllToAllv(sendbuf ? sendbuf : dummy, a.data(), b.data(),
+                                   recvbuf ? recvbuf : dummy, c.data(), d.data(), ncclUint8,
+                                   node->comm, s),
+                     "ncclAllToAllv");
         }
-        hip_check(hipStreamSynchronize(s), "sync exchange");
       } else {
-        // 3b. bootstrap: one-sided pulls (the GET model of OnOffsetsFetchCallback.java:80-87)
+        // 3b. bootstrap: the same plan as one-sided pulls (OnOffsetsFetchCallback.java:80-87's
+        //     GETs, one per (round, source) instead of one per block)
         std::vector<sux::CopyDesc> desc;
-        for (int m = 0; m < M; ++m) {
-          if (owner_of[m] < 0 || owner_of[m] == me) continue;
-          const std::vector<int64_t>& ix = entry[m]->index;
-          if (ix[hi] == ix[lo]) continue;
-          std::string key(reinterpret_cast<const char*>(entry[m]->ipc), 64);
-          key += std::to_string(owner_of[m]);
-          void*& base = opened[key];
-          if (!base) {
-            hipIpcMemHandle_t h;
-            std::memcpy(&h, entry[m]->ipc, 64);
-            hip_check(hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess),
-                      "hipIpcOpenMemHandle");
+        for (int k = 0; k < P.rounds; ++k)
+          for (int g = 0; g < W; ++g) {
+            const size_t kg = (size_t)k * W + g;
+            const int32_t pe = P.piece[kg];
+            if (pe < 0 || P.rc[kg] == 0) continue;
+            const uint8_t* src = nullptr;
+            if (g == me) {
+              src = my_slab.at(all[pe].batch);
+            } else {
+              // one mapping per exported allocation per process (the serve path shares it)
+              std::string key(reinterpret_cast<const char*>(all[pe].ipc), 64);
+              void* base = nullptr;
+              {
+                std::lock_guard<std::mutex> lk(node->mu);
+                auto& ib = node->shuffle(shuffle_id).ipc_bases;
+                auto f = ib.find(key);
+                if (f != ib.end()) base = f->second;
+              }
+              if (!base) {
+                hipIpcMemHandle_t h;
+                std::memcpy(&h, all[pe].ipc, 64);
+                hip_check(hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess),
+                          "hipIpcOpenMemHandle");
+                std::lock_guard<std::mutex> lk(node->mu);
+                node->shuffle(shuffle_id).ipc_bases[key] = base;
+              }
+              uint64_t off;
+              std::memcpy(&off, all[pe].ipc + 64, 8);
+              src = static_cast<const uint8_t*>(base) + off;
+            }
+            desc.push_back({src + seg[(size_t)pe * W + me], recv->buf.ptr + P.base[k] + P.rd[kg],
+                            P.rc[kg]});
           }
-          uint64_t off;
-          std::memcpy(&off, entry[m]->ipc + 64, 8);
-          desc.push_back({static_cast<const uint8_t*>(base) + off + ix[lo], recv.ptr + roff[m],
-                          (uint64_t)(ix[hi] - ix[lo])});
-        }
-        launch_copies(node, desc, aux, s);
-        hip_check(hipStreamSynchronize(s), "sync pulls");
-        // every rank has finished reading its owners' buffers before anyone returns
-        int64_t one = 1;
-        std::vector<int64_t> ack((size_t)W);
-        host_allgather(node, &one, 8, ack.data(), s);
+        launch_copies(node, desc, aux, hostblk, s);
       }
     } catch (...) {
-      for (auto& kv : opened) (void)hipIpcCloseMemHandle(kv.second);
-      node->pool->put(recv);
+      (void)hipStreamSynchronize(s);
       node->pool->put(aux);
+      node->hpool.put(hostblk);
       throw;
     }
-    node->pool->put(aux);
-    for (auto& kv : opened) (void)hipIpcCloseMemHandle(kv.second);
-    // 4. adopt the remote rows
+    auto ev = std::make_shared<Event>();
+    hip_check(hipEventRecord(ev->e, s), "hipEventRecord(exchange)");
+    recv->ready = ev;
+    // 4a. where every rank serves its owned ranges of the window's maps: its receive buffer
+    //     (descriptors all-gathered) at its own plan's offsets, or its own batch slab
+    std::vector<uint8_t> rdesc((size_t)W * SUX_IPC_DESC_BYTES, 0);
+    {
+      std::vector<uint8_t> mine_desc(SUX_IPC_DESC_BYTES, 0);
+      if (recv->buf.ptr) export_ipc(recv->buf.ptr, mine_desc.data());
+      host_allgather(node, tag + 2, mine_desc.data(), SUX_IPC_DESC_BYTES, rdesc.data(), s);
+    }
+    std::vector<std::vector<uint64_t>> peer_off((size_t)W);
+    for (int h = 0; h < W; ++h)
+      peer_off[h] = h == me ? P.recv_off
+                            : plan_exchange(W, h, loopback, n, em.data(), eo.data(), eb.data(),
+                                            seg.data(), len.data()).recv_off;
+    // 4. adopt: remote maps (and, looped back, own maps) now live in the receive buffer
     std::lock_guard<std::mutex> lk(node->mu);
     Shuffle& sh = node->shuffle(shuffle_id);
-    for (int m = 0; m < M; ++m) {
-      if (owner_of[m] < 0 || owner_of[m] == me) continue;
-      MapSlot& sl = sh.maps[m];
-      sl.present = true;
-      sl.owner = owner_of[m];
-      sl.slab.reset();
-      sl.off = 0;
-      sl.index = entry[m]->index;
-      sl.bytes = (uint64_t)sl.index[R];
-      sl.recv_off = roff[m];
+    sh.xfers.push_back(ev);
+    if (aux.ptr) sh.xfer_aux.push_back(aux);
+    if (hostblk.first) sh.xfer_host.push_back(hostblk);
+    // W > 1: the closing all-gather of sux_exchange_wait is due — with IPC pulls the owners'
+    // slabs are read until then, and with either transport a peer read of a block another rank
+    // received needs that rank's exchange complete
+    if (W > 1) sh.ack_due = true;
+    auto serve_id = [&](const uint8_t* d) {
+      std::string k(reinterpret_cast<const char*>(d), SUX_IPC_DESC_BYTES);
+      auto f = sh.serve_idx.find(k);
+      if (f != sh.serve_idx.end()) return f->second;
+      const int32_t id = (int32_t)sh.serve_desc.size();
+      sh.serve_desc.push_back(k);
+      sh.serve_idx[k] = id;
+      return id;
+    };
+    for (int i = 0; i < n; ++i) {
+      MapSlot& sl = sh.maps[em[i]];
+      sl.serve.assign((size_t)W, {-1, 0});
+      for (int h = 0; h < W; ++h) {
+        if (peer_off[h][i] == UINT64_MAX)  // h's own map, not looped back: its batch slab
+          sl.serve[h] = {serve_id(all[i].ipc), seg[(size_t)i * W + h]};
+        else
+          sl.serve[h] = {serve_id(rdesc.data() + (size_t)h * SUX_IPC_DESC_BYTES), peer_off[h][i]};
+      }
+      if (eo[i] == me) sl.sent = true;
+      if (P.recv_off[i] == UINT64_MAX) continue;
+      if (eo[i] != me) {
+        sl.present = true;
+        sl.owner = eo[i];
+        sl.batch = eb[i];
+        sl.slab.reset();
+        sl.off = 0;
+        sl.seg.clear();
+        sl.index = all[i].index;
+        sl.bytes = (uint64_t)sl.index[R];
+      }
+      sl.rslab = recv;
+      sl.recv_off = P.recv_off[i];
     }
-    node->pool->put(sh.recv);
-    sh.recv = recv;
-    sh.recv_bytes = total;
-    sh.exchanged = true;
   });
 }
 
+int sux_exchange_wait(sux_node* node, int32_t shuffle_id) {
+  return guard([&] {
+    require(node, SUX_EINVAL, "NULL node");
+    node->bind();
+    std::vector<std::shared_ptr<Event>> evs;
+    std::vector<PoolBuf> aux;
+    std::vector<std::pair<void*, uint64_t>> host;
+    bool ack = false;
+    uint64_t tag = 0;
+    {
+      std::lock_guard<std::mutex> lk(node->mu);
+      Shuffle& sh = node->shuffle(shuffle_id);
+      require(!sh.exchanging, SUX_ESTATE, "shuffle " + std::to_string(shuffle_id) + " is exchanging");
+      evs.swap(sh.xfers);
+      aux.swap(sh.xfer_aux);
+      host.swap(sh.xfer_host);
+      ack = sh.ack_due;
+      sh.ack_due = false;
+      if (ack) tag = ((uint64_t)(uint32_t)shuffle_id << 32) | sh.gathers++;
+    }
+    hipError_t err = hipSuccess;
+    for (auto& e : evs) {
+      const hipError_t r = hipEventSynchronize(e->e);
+      if (r != hipSuccess && err == hipSuccess) err = r;
+    }
+    for (PoolBuf& b : aux) node->pool->put(b);
+    for (auto& b : host) node->hpool.put(b);
+    hip_check(err, "exchange completion");
+    if (ack) {  // every rank has finished its pulls before anyone may free what was pulled
+      int64_t one = 1;
+      std::vector<int64_t> acks((size_t)node->conf.world_size);
+      host_allgather(node, tag, &one, 8, acks.data(), nullptr);
+    }
+  });
+}
+
+// The whole shuffle's exchange, synchronous: every committed map not yet exchanged, then the wait.
+int sux_exchange(sux_node* node, int32_t shuffle_id, void* stream) {
+  int32_t maps = 0;
+  int rc = guard([&] {
+    require(node, SUX_EINVAL, "NULL node");
+    std::lock_guard<std::mutex> lk(node->mu);
+    maps = node->shuffle(shuffle_id).num_maps;
+  });
+  if (rc != SUX_OK) return rc;
+  rc = sux_exchange_maps(node, shuffle_id, 0, maps, stream);
+  if (rc != SUX_OK) return rc;
+  return sux_exchange_wait(node, shuffle_id);
+}
+
 // ---- fetch -----------------------------------------------------------------------------------
+}  // extern "C"
+
 namespace {
-// Resolve one block to (device address, size); throws SUX_ENOENT for a block not local here.
-void resolve(sux_node* node, Shuffle& sh, const sux_block_id& b, uint64_t* addr, int64_t* size) {
+// Where one block's bytes are: device memory (addr; `ready` = the exchange that fills it, if
+// any) or, for a spilled map, a byte range of Spark's data file.
+struct BlockLoc {
+  uint64_t addr = 0;
+  int64_t size = 0;
+  std::shared_ptr<Slab> hold;  // keeps the device bytes allocated while a copy may read them
+  const Slab* rslab = nullptr;
+  const std::string* file = nullptr;
+  uint64_t file_off = 0;
+};
+
+// Resolve one block; throws SUX_ENOENT for a block not readable here.  At world > 1 a rank
+// reads its owned partitions of every map (after the exchange) and any partitions of its own
+// maps (within one peer's range: an own peer-major slab holds each peer's share separately).
+BlockLoc resolve(sux_node* node, Shuffle& sh, const sux_block_id& b) {
   const int R = sh.R;
   auto name = [&] {
     return "shuffle_" + std::to_string(sh.id) + "_" + std::to_string(b.map_index) + "_" +
@@ -2181,21 +2789,65 @@ void resolve(sux_node* node, Shuffle& sh, const sux_block_id& b, uint64_t* addr,
     raise(SUX_EINVAL, "malformed block " + name());
   const MapSlot& sl = sh.maps[b.map_index];
   if (!sl.present) raise(SUX_ENOENT, "Unknown block " + name() + ": map output not committed");
+  BlockLoc L;
   const int64_t a = sl.index[b.start_reduce], e = sl.index[b.end_reduce];
-  *size = e - a;
-  if (sl.owner == node->conf.rank) {
-    *addr = (uint64_t)(uintptr_t)(sl.data() + a);
-    return;
-  }
+  L.size = e - a;
   const int W = node->conf.world_size, me = node->conf.rank;
   const int lo = owner_lo(me, R, W), hi = owner_lo(me + 1, R, W);
-  if (!sh.exchanged)
-    raise(SUX_ESTATE, "block " + name() + " is remote and the shuffle is not exchanged");
-  if (!(b.start_reduce >= lo && b.end_reduce <= hi))
-    raise(SUX_ENOENT, "block " + name() + " is not owned by rank " + std::to_string(me));
-  *addr = (uint64_t)(uintptr_t)(sh.recv.ptr + sl.recv_off + (a - sl.index[lo]));
+  const bool owned = b.start_reduce >= lo && b.end_reduce <= hi;
+  if (sl.rslab && owned) {  // received (or looped back) by an exchange
+    L.addr = (uint64_t)(uintptr_t)(sl.rslab->buf.ptr + sl.recv_off + (a - sl.index[lo]));
+    L.rslab = sl.rslab.get();
+    L.hold = sl.rslab;
+    return L;
+  }
+  if (sl.owner == me) {
+    if (sl.spilled()) {
+      L.file = &sl.spill_data;
+      L.file_off = (uint64_t)a;
+      return L;
+    }
+    L.hold = sl.slab;
+    if (W == 1 || sl.seg.empty()) {
+      L.addr = (uint64_t)(uintptr_t)(sl.data() + a);
+      return L;
+    }
+    // peer h's range of the map: one contiguous piece of its batch slab
+    int h = 0;
+    while (owner_lo(h + 1, R, W) <= b.start_reduce) ++h;
+    if (b.end_reduce > owner_lo(h + 1, R, W))
+      raise(SUX_EINVAL, "block " + name() + " spans the partition ranges of two ranks; split it");
+    L.addr = (uint64_t)(uintptr_t)(sl.slab->buf.ptr + sl.seg[h] +
+                                   (uint64_t)(a - sl.index[owner_lo(h, R, W)]));
+    return L;
+  }
+  if (sl.serve.empty())
+    raise(SUX_ESTATE, "block " + name() + " is remote and its map has not been exchanged");
+  // another rank's partitions: read where their owner serves them, through the owner's
+  // IPC-mapped HBM (a peer read over xGMI — the one-sided GET of OnOffsetsFetchCallback.java:80-87)
+  int h = 0;
+  while (owner_lo(h + 1, R, W) <= b.start_reduce) ++h;
+  if (b.end_reduce > owner_lo(h + 1, R, W))
+    raise(SUX_EINVAL, "block " + name() + " spans the partition ranges of two ranks; split it");
+  const auto& sv = sl.serve[h];
+  if (sv.first < 0) raise(SUX_ENOENT, "block " + name() + " has no serving rank");
+  const std::string& desc = sh.serve_desc[sv.first];
+  const std::string key = desc.substr(0, 64);  // the allocation's handle (see the pull path)
+  void*& base = sh.ipc_bases[key];
+  if (!base) {
+    hipIpcMemHandle_t hd;
+    std::memcpy(&hd, desc.data(), 64);
+    hip_check(hipIpcOpenMemHandle(&base, hd, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+  }
+  uint64_t doff;
+  std::memcpy(&doff, desc.data() + 64, 8);
+  L.addr = (uint64_t)(uintptr_t)(static_cast<uint8_t*>(base) + doff + sv.second +
+                                 (uint64_t)(a - sl.index[owner_lo(h, R, W)]));
+  return L;
 }
 }  // namespace
+
+extern "C" {
 
 int sux_resolve_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* blocks, int32_t n,
                        uint64_t* addrs, int64_t* sizes) {
@@ -2205,7 +2857,14 @@ int sux_resolve_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* b
     std::unique_lock<std::mutex> lk(node->mu);
     Shuffle& sh = node->shuffle(shuffle_id);
     drain(node, sh, lk);
-    for (int i = 0; i < n; ++i) resolve(node, sh, blocks[i], &addrs[i], &sizes[i]);
+    for (int i = 0; i < n; ++i) {
+      const BlockLoc L = resolve(node, sh, blocks[i]);
+      if (L.file)
+        raise(SUX_ESTATE, "map " + std::to_string(blocks[i].map_index) +
+                              " was spilled to " + *L.file + ": fetch its blocks");
+      addrs[i] = L.addr;
+      sizes[i] = L.size;
+    }
   });
 }
 
@@ -2216,7 +2875,9 @@ int sux_fetch_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* blo
             "NULL argument");
     node->bind();
     hipStream_t s = node->stream(stream);
-    std::vector<sux::CopyDesc> desc((size_t)n);
+    std::vector<BlockLoc> loc((size_t)n);
+    std::vector<std::string> files((size_t)n);  // copies: the slot may be spilled/freed later
+    std::vector<std::shared_ptr<Event>> waits;
     uint64_t total = 0;
     {
       std::unique_lock<std::mutex> lk(node->mu);
@@ -2224,52 +2885,95 @@ int sux_fetch_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* blo
       drain(node, sh, lk);  // maps written without a wait are published first
       // phase 1 (UcxShuffleClient.submitFetchOffsets :50-92 / OnOffsetsFetchCallback :53-72):
       // sizes from the index tables of the directory
+      const Slab* last = nullptr;
       for (int i = 0; i < n; ++i) {
-        uint64_t a;
-        resolve(node, sh, blocks[i], &a, &sizes[i]);
-        desc[i].src = reinterpret_cast<const uint8_t*>(a);
-        desc[i].bytes = (uint64_t)sizes[i];
-        total += (uint64_t)sizes[i];
+        loc[i] = resolve(node, sh, blocks[i]);
+        sizes[i] = loc[i].size;
+        total += (uint64_t)loc[i].size;
+        if (loc[i].file) files[i] = *loc[i].file;
+        // blocks received by an exchange still in flight: the copy waits for it
+        if (loc[i].rslab && loc[i].rslab != last && loc[i].rslab->ready) {
+          waits.push_back(loc[i].rslab->ready);
+          last = loc[i].rslab;
+        }
       }
     }
+    for (auto& w : waits) hip_check(hipStreamWaitEvent(s, w->e, 0), "wait for the exchange");
     auto buf = std::make_unique<sux_buffer>();
     buf->node = node;
     buf->size = total;
     buf->refs = n > 0 ? n : 1;  // one reference per block slice (OnBlocksFetchCallback :35)
     // OnOffsetsFetchCallback :75-76: one pooled buffer for the whole request
-    buf->buf = node->pool->get(total ? total : 1);
-    if (total) {
-      // phase 2 (:80-87): block i -> contiguous destination at a running offset
-      std::vector<uint32_t> first((size_t)n);
-      uint64_t pos = 0, chunks = 0;
-      const uint64_t kChunk = 64 * 1024;
-      for (int i = 0; i < n; ++i) {
-        desc[i].dst = buf->buf.ptr + pos;
-        pos += desc[i].bytes;
-        first[i] = (uint32_t)chunks;
-        chunks += desc[i].bytes ? (desc[i].bytes + kChunk - 1) / kChunk : 1;
+    buf->buf = pool_get_or_spill(node, total ? total : 1);
+    try {
+      if (total) {
+        // phase 2 (:80-87): block i -> contiguous destination at a running offset; device blocks
+        // in one gather-copy launch, spilled blocks read from their files
+        std::vector<sux::CopyDesc> desc;
+        std::vector<uint32_t> first;
+        uint64_t pos = 0, chunks = 0;
+        const uint64_t kChunk = 64 * 1024;
+        std::vector<std::pair<int, uint64_t>> from_file;
+        for (int i = 0; i < n; ++i) {
+          const uint64_t sz = (uint64_t)loc[i].size;
+          if (loc[i].file) {
+            from_file.push_back({i, pos});
+          } else if (sz) {
+            desc.push_back({reinterpret_cast<const uint8_t*>(loc[i].addr), buf->buf.ptr + pos, sz});
+            first.push_back((uint32_t)chunks);
+            chunks += (sz + kChunk - 1) / kChunk;
+          }
+          pos += sz;
+        }
+        require(chunks < (1ull << 31), SUX_ERANGE, "fetch request too large");
+        if (!desc.empty()) {
+          const uint64_t dbytes = desc.size() * sizeof(sux::CopyDesc), fbytes = first.size() * 4;
+          const uint64_t dpad = ((dbytes + 255) / 256) * 256;
+          buf->aux = node->pool->get(dpad + fbytes);
+          uint8_t* d_desc = buf->aux.ptr;
+          uint8_t* d_first = buf->aux.ptr + dpad;
+          // both tables through one pinned staging block: one true async upload instead of two
+          // pageable bounces (the staging returns to node->hpool after the sync below)
+          HostLease hb(node->hpool, dpad + fbytes);
+          uint8_t* h = static_cast<uint8_t*>(hb.b.first);
+          std::memcpy(h, desc.data(), dbytes);
+          std::memcpy(h + dpad, first.data(), fbytes);
+          hip_check(hipMemcpyAsync(d_desc, h, dpad + fbytes, hipMemcpyHostToDevice, s), "H2D desc");
+          hip_check(sux::launch_gather_copy(reinterpret_cast<const sux::CopyDesc*>(d_desc),
+                                            (uint32_t)desc.size(), (uint32_t)chunks,
+                                            reinterpret_cast<const uint32_t*>(d_first),
+                                            &node->timer, s),
+                    "gather copy");
+          // completion is delivered to the caller like OnBlocksFetchCallback.onSuccess: the
+          // blocks are in place when this call returns
+          hip_check(hipStreamSynchronize(s), "sync fetch");
+        }
+        if (!from_file.empty()) {
+          Staging st;
+          for (auto& f : from_file)
+            read_file_range(files[f.first], loc[f.first].file_off, (uint64_t)loc[f.first].size,
+                            buf->buf.ptr + f.second, s, st);
+        }
       }
-      require(chunks < (1ull << 31), SUX_ERANGE, "fetch request too large");
-      const uint64_t dbytes = desc.size() * sizeof(sux::CopyDesc), fbytes = first.size() * 4;
-      const uint64_t dpad = ((dbytes + 255) / 256) * 256;
-      buf->aux = node->pool->get(dpad + fbytes);
-      uint8_t* d_desc = buf->aux.ptr;
-      uint8_t* d_first = buf->aux.ptr + dpad;
-      // both tables through one pinned staging block: one true async upload instead of two
-      // pageable bounces (the staging returns to node->hpool after the sync below)
-      HostLease hb(node->hpool, dpad + fbytes);
-      uint8_t* h = static_cast<uint8_t*>(hb.b.first);
-      std::memcpy(h, desc.data(), dbytes);
-      std::memcpy(h + dpad, first.data(), fbytes);
-      hip_check(hipMemcpyAsync(d_desc, h, dpad + fbytes, hipMemcpyHostToDevice, s), "H2D desc");
-      hip_check(sux::launch_gather_copy(reinterpret_cast<const sux::CopyDesc*>(d_desc), (uint32_t)n,
-                                        (uint32_t)chunks, reinterpret_cast<const uint32_t*>(d_first),
-                                        &node->timer, s),
-                "gather copy");
-      // completion is delivered to the caller like OnBlocksFetchCallback.onSuccess: the blocks
-      // are in place when this call returns
-      hip_check(hipStreamSynchronize(s), "sync fetch");
+    } catch (...) {
+      (void)hipStreamSynchronize(s);
+      node->pool->put(buf->buf);
+      node->pool->put(buf->aux);
+      throw;
     }
+    *out = buf.release();
+  });
+}
+
+int sux_buffer_alloc(sux_node* node, uint64_t bytes, sux_buffer** out) {
+  return guard([&] {
+    require(node && out, SUX_EINVAL, "NULL argument");
+    node->bind();
+    auto buf = std::make_unique<sux_buffer>();
+    buf->node = node;
+    buf->size = bytes;
+    buf->refs = 1;
+    buf->buf = pool_get_or_spill(node, bytes ? bytes : 1);
     *out = buf.release();
   });
 }

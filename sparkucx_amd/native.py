@@ -35,7 +35,7 @@ class Conf(C.Structure):
                 ("num_streams", C.c_int32), ("comm_id", C.c_uint8 * 128),
                 ("min_buffer_size", C.c_uint64), ("min_allocation_size", C.c_uint64),
                 ("metadata_block_size", C.c_uint64), ("num_prealloc", C.c_uint32),
-                ("reserved0", C.c_uint32), ("prealloc_size", C.c_uint64 * 16),
+                ("pool_limit_mib", C.c_uint32), ("prealloc_size", C.c_uint64 * 16),
                 ("prealloc_count", C.c_uint64 * 16)]
 
 
@@ -43,15 +43,15 @@ TUNING_FIELDS = ("hist_kernel", "scatter_kernel", "coresident", "scatter_chunk",
                  "hist_stage", "s6_chunk", "tiles_per_item", "small_groups", "tile_records",
                  "onepass", "varlen_kernel", "varlen_tile", "sort_max_digit_bits", "sort_gather",
                  "sort_all_passes", "hist_wgs_per_cu", "small_kernel", "small_waves", "scatter_order",
-                 "small_wgs_per_cu", "sort_msd")
+                 "small_wgs_per_cu", "sort_msd", "exchange_self")
 
 
 class Tuning(C.Structure):
-    _fields_ = [(f, C.c_int32) for f in TUNING_FIELDS] + [("reserved", C.c_int32 * 10)]
+    _fields_ = [(f, C.c_int32) for f in TUNING_FIELDS] + [("reserved", C.c_int32 * 9)]
 
 
-# int (*sux_allgather_fn)(void* ctx, const void* send, uint64_t bytes, void* recv)
-ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p)
+# int (*sux_allgather_fn)(void* ctx, uint64_t tag, const void* send, uint64_t bytes, void* recv)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p)
 
 
 class PartitionerDesc(C.Structure):
@@ -64,6 +64,11 @@ class HandleDesc(C.Structure):
     _fields_ = [("shuffle_id", C.c_int32), ("num_maps", C.c_int32),
                 ("num_partitions", C.c_int32), ("record_size", C.c_int32),
                 ("directory_bytes", C.c_uint64)]
+
+
+class XPlanEntry(C.Structure):
+    _fields_ = [("map", C.c_int32), ("owner", C.c_int32), ("batch", C.c_int32),
+                ("reserved", C.c_int32)]
 
 
 class BlockId(C.Structure):
@@ -115,10 +120,17 @@ _SIGS = {
     "sux_commit_map_output": (C.c_int, [P, I32, I32, P, U64, P, P]),
     "sux_map_output_index": (C.c_int, [P, I32, I32, P, U64]),
     "sux_exchange": (C.c_int, [P, I32, P]),
+    "sux_exchange_maps": (C.c_int, [P, I32, I32, I32, P]),
+    "sux_exchange_wait": (C.c_int, [P, I32]),
+    "sux_plan_exchange": (C.c_int, [I32, I32, I32, I32, P, P, P, I32, C.POINTER(I32), P, P, P, P]),
+    "sux_adopt_map_outputs": (C.c_int, [P, I32, I32, P, U64, U64, P, P]),
+    "sux_node_set_spill_dir": (C.c_int, [P, C.c_char_p]),
+    "sux_node_spills": (C.c_int, [P, C.POINTER(U64)]),
     "sux_owned_partitions": (C.c_int, [P, I32, I32, C.POINTER(I32), C.POINTER(I32)]),
     "sux_fetch_blocks": (C.c_int, [P, I32, P, I32, P, C.POINTER(P), P]),
     "sux_resolve_blocks": (C.c_int, [P, I32, P, I32, P, P]),
     "sux_buffer_info": (C.c_int, [P, C.POINTER(P), C.POINTER(U64), C.POINTER(U64)]),
+    "sux_buffer_alloc": (C.c_int, [P, U64, C.POINTER(P)]),
     "sux_buffer_retain": (C.c_int, [P, I32]),
     "sux_buffer_read": (C.c_int, [P, U64, P, U64, P]),
     "sux_write_map_output_host": (C.c_int, [P, I32, I32, P, P, U64, P]),

@@ -78,9 +78,12 @@ class Node:
     def set_bootstrap(self, allgather):
         """Control plane for the exchange without RCCL: `allgather(b: bytes) -> list[bytes]` (one
         entry per rank, rank order), e.g. torch.distributed.all_gather_object over gloo."""
-        def fn(_ctx, send, nbytes, recv):
+        def fn(_ctx, _tag, send, nbytes, recv):
+            # (torch.distributed collectives are matched by issue order, so the tag is unused)
             try:
                 parts = allgather(C.string_at(send, nbytes))
+                if len(parts) != self.world_size or any(len(p) != nbytes for p in parts):
+                    return -1  # a contribution of another size: the ranks are out of step
                 C.memmove(recv, b"".join(parts), nbytes * len(parts))
                 return 0
             except Exception:  # pragma: no cover - reported as SUX_ECOMM by the library
@@ -407,6 +410,31 @@ class Node:
     def exchange(self, shuffle_id: int, stream=None):
         N.check(self.lib.sux_exchange(self.h, shuffle_id, _stream(stream)), "sux_exchange")
 
+    def exchange_maps(self, shuffle_id: int, first_map: int, num_maps: int, stream=None):
+        """Asynchronous exchange of the map window [first_map, first_map + num_maps) (collective)."""
+        N.check(self.lib.sux_exchange_maps(self.h, shuffle_id, first_map, num_maps,
+                                           _stream(stream)), "sux_exchange_maps")
+
+    def exchange_wait(self, shuffle_id: int):
+        N.check(self.lib.sux_exchange_wait(self.h, shuffle_id), "sux_exchange_wait")
+
+    def adopt_map_outputs(self, shuffle_id: int, first_map: int, out: torch.Tensor,
+                          records_per_map: int, num_records: int, index: torch.Tensor,
+                          stream=None):
+        """Commit map outputs a stateless partition call wrote (no copy; published lazily)."""
+        N.check(self.lib.sux_adopt_map_outputs(self.h, shuffle_id, first_map, _ptr(out),
+                                               records_per_map, num_records, _ptr(index),
+                                               _stream(stream)), "sux_adopt_map_outputs")
+
+    def set_spill_dir(self, path: str | None):
+        N.check(self.lib.sux_node_set_spill_dir(self.h, None if path is None else path.encode()),
+                "sux_node_set_spill_dir")
+
+    def spills(self) -> int:
+        v = C.c_uint64()
+        N.check(self.lib.sux_node_spills(self.h, C.byref(v)), "sux_node_spills")
+        return v.value
+
     def owned_partitions(self, shuffle_id: int, rank: int | None = None) -> tuple[int, int]:
         a, b = C.c_int32(), C.c_int32()
         N.check(self.lib.sux_owned_partitions(self.h, shuffle_id, self.rank if rank is None else rank,
@@ -523,6 +551,31 @@ class Node:
         buf = C.create_string_buffer(64)
         N.check(self.lib.sux_kernel_variant(self.h, slot, buf, len(buf)), "sux_kernel_variant")
         return buf.value.decode()
+
+
+def plan_exchange(world: int, rank: int, entries, seg, length, loopback: bool = False,
+                  max_rounds: int = 4096) -> dict:
+    """sux_plan_exchange (host arithmetic): entries = [(map, owner, batch)], seg/length =
+    int arrays [n, world].  Returns the per-round all-to-all arguments of `rank`."""
+    n = len(entries)
+    ents = (N.XPlanEntry * max(1, n))(*[N.XPlanEntry(int(m), int(o), int(b), 0)
+                                        for m, o, b in entries])
+    sg = np.ascontiguousarray(np.asarray(seg, dtype=np.uint64).reshape(-1))
+    ln = np.ascontiguousarray(np.asarray(length, dtype=np.uint64).reshape(-1))
+    rounds = C.c_int32()
+    counts = np.zeros((max_rounds, 4, world), np.uint64)
+    piece = np.full((max_rounds, world), -1, np.int32)
+    base = np.zeros(max_rounds + 1, np.uint64)
+    roff = np.zeros(max(1, n), np.uint64)
+    N.check(N.load().sux_plan_exchange(world, rank, int(loopback), n, ents,
+                                       sg.ctypes.data if n else None,
+                                       ln.ctypes.data if n else None, max_rounds,
+                                       C.byref(rounds), counts.ctypes.data, piece.ctypes.data,
+                                       base.ctypes.data, roff.ctypes.data), "sux_plan_exchange")
+    k = rounds.value
+    return {"rounds": k, "sendcounts": counts[:k, 0], "sdispls": counts[:k, 1],
+            "recvcounts": counts[:k, 2], "rdispls": counts[:k, 3], "piece": piece[:k],
+            "round_base": base[:k + 1], "recv_off": roff[:n]}
 
 
 class FetchedBuffer:

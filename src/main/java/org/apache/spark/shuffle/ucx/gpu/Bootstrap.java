@@ -7,8 +7,10 @@ package org.apache.spark.shuffle.ucx.gpu;
 
 public interface Bootstrap {
   /**
-   * Every executor of the node's group passes the same number of bytes; returns the
-   * concatenation of all contributions in rank order.
+   * Every executor of the node's group passes the same number of bytes under the same tag;
+   * returns the concatenation of all contributions in rank order.  The tag names the collective
+   * ((shuffle id << 32) | the shuffle's all-gather sequence number, equal on every executor), so
+   * the control plane matches contributions by tag, never by arrival order.
    */
-  byte[] allGather(byte[] mine);
+  byte[] allGather(long tag, byte[] mine);
 }

@@ -29,6 +29,16 @@ public final class DeviceManagedBuffer extends ManagedBuffer {
     this.stream = stream;
   }
 
+  /** The pooled sux_buffer this block is a slice of (a GPU consumer of several blocks). */
+  public long bufferHandle() {
+    return buffer;
+  }
+
+  /** Offset of the block in that buffer. */
+  public long offset() {
+    return offset;
+  }
+
   /** Device address of the block (for a GPU consumer: no host copy at all). */
   public long devicePointer() {
     return SuxNative.bufferDevicePtr(buffer) + offset;

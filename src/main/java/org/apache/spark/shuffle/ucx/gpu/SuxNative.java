@@ -20,7 +20,7 @@ public final class SuxNative {
     }
   }
 
-  public static final int ABI_VERSION = 3;
+  public static final int ABI_VERSION = 4;
 
   // status codes (SUX_*)
   public static final int OK = 0, EINVAL = -1, ENOMEM = -2, EHIP = -3, ECOMM = -4, ENOENT = -5,
@@ -32,13 +32,18 @@ public final class SuxNative {
   // ---- node (UcxNode) ----
   public static native int abiVersion();
   public static native byte[] commUniqueId();
+  /** poolLimitMiB: spark.shuffle.ucx.gpu.poolLimitMiB (0 = no cap on the device pool). */
   public static native long nodeCreate(int device, int rank, int worldSize, byte[] commId,
                                        long minBufferSize, long minAllocationSize,
                                        long metadataBlockSize, String preAllocateBuffers,
-                                       boolean isDriver);
+                                       int poolLimitMiB, boolean isDriver);
   public static native void nodeDestroy(long node);
-  /** Returns a context to pass to releaseBootstrap once the node is destroyed. */
-  public static native long setBootstrap(long node, Bootstrap bootstrap);
+  /** Returns a context to pass to releaseBootstrap once the node is destroyed.  Every reply of
+   * the bootstrap must be exactly worldSize * the contribution's bytes. */
+  public static native long setBootstrap(long node, Bootstrap bootstrap, int worldSize);
+  /** HBM-capacity fallback: committed map outputs spill to Spark's files under dir. */
+  public static native void setSpillDir(long node, String dir);
+  public static native long spills(long node);
   public static native void releaseBootstrap(long ctx);
   public static native long[] poolStats(long node);
   /** sux_tuning fields in header order (TUNING_FIELDS); 0 = the measured default. */
@@ -51,7 +56,7 @@ public final class SuxNative {
       "hist_stage", "s6_chunk", "tiles_per_item", "small_groups", "tile_records", "onepass",
       "varlen_kernel", "varlen_tile", "sort_max_digit_bits", "sort_gather", "sort_all_passes",
       "hist_wgs_per_cu", "small_kernel", "small_waves", "scatter_order",
-      "small_wgs_per_cu", "sort_msd"};
+      "small_wgs_per_cu", "sort_msd", "exchange_self"};
   public static native long streamCreate(long node);
   public static native void streamDestroy(long node, long stream);
 
@@ -83,12 +88,21 @@ public final class SuxNative {
 
   // ---- exchange ----
   public static native void exchange(long node, int shuffleId, long stream);
+  /** Asynchronous exchange of map tasks [firstMap, firstMap + numMaps) (a collective). */
+  public static native void exchangeMaps(long node, int shuffleId, int firstMap, int numMaps,
+                                         long stream);
+  /** Completes every exchange of the shuffle enqueued by this executor (a collective). */
+  public static native void exchangeWait(long node, int shuffleId);
   public static native int[] ownedPartitions(long node, int shuffleId, int rank);
 
   // ---- fetch ----
   public static native long fetchBlocks(long node, int shuffleId, int[] blocks, long[] sizes,
                                         long stream);
   public static native long bufferDevicePtr(long buf);
+  /** Sort n fixed-size records of a fetched buffer by key on the GPU; returns a new buffer. */
+  public static native long sortRecords(long node, int keyKind, long buf, long n, int recordSize,
+                                        int keyOffset, int keyLen, long stream);
+  public static final int SORT_BYTES = 1, SORT_LONG = 2, SORT_INT = 3;
   public static native void bufferRead(long buf, long offset, ByteBuffer dst, long len,
                                        long stream);
   public static native void bufferRetain(long buf, int count);

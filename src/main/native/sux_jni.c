@@ -90,7 +90,8 @@ JNIEXPORT jbyteArray JNICALL FN(commUniqueId)(JNIEnv* env, jclass cls) {
 JNIEXPORT jlong JNICALL FN(nodeCreate)(JNIEnv* env, jclass cls, jint device, jint rank,
                                        jint worldSize, jbyteArray commId, jlong minBufferSize,
                                        jlong minAllocationSize, jlong metadataBlockSize,
-                                       jstring preAllocateBuffers, jboolean isDriver) {
+                                       jstring preAllocateBuffers, jint poolLimitMiB,
+                                       jboolean isDriver) {
   (void)cls;
   sux_conf c;
   sux_conf_init(&c);
@@ -100,6 +101,7 @@ JNIEXPORT jlong JNICALL FN(nodeCreate)(JNIEnv* env, jclass cls, jint device, jin
   c.min_buffer_size = (uint64_t)minBufferSize;
   c.min_allocation_size = (uint64_t)minAllocationSize;
   c.metadata_block_size = (uint64_t)metadataBlockSize;
+  c.pool_limit_mib = poolLimitMiB > 0 ? (uint32_t)poolLimitMiB : 0u;
   if (commId) {
     if ((*env)->GetArrayLength(env, commId) != 128) {
       throw_sux(env, SUX_EINVAL, "nodeCreate: the RCCL unique id is 128 bytes");
@@ -123,14 +125,16 @@ JNIEXPORT void JNICALL FN(nodeDestroy)(JNIEnv* env, jclass cls, jlong node) {
   failed(env, sux_node_destroy(NODE(node)), "UcxNode.close");
 }
 
-/* Bootstrap: the node calls back into Bootstrap.allGather(byte[]) -> byte[] (world * bytes). */
+/* Bootstrap: the node calls back into Bootstrap.allGather(long tag, byte[]) -> byte[]
+ * (world * bytes; the tag names the collective, see sux_allgather_fn). */
 typedef struct {
   JavaVM* vm;
   jobject target; /* global ref to an org.apache.spark.shuffle.ucx.gpu.Bootstrap */
   jmethodID all_gather;
+  jint world;     /* the node's group size: the reply must be exactly world * bytes */
 } boot_ctx;
 
-static int boot_allgather(void* vctx, const void* send, uint64_t bytes, void* recv) {
+static int boot_allgather(void* vctx, uint64_t tag, const void* send, uint64_t bytes, void* recv) {
   boot_ctx* b = (boot_ctx*)vctx;
   JNIEnv* env = NULL;
   int attached = 0;
@@ -142,10 +146,13 @@ static int boot_allgather(void* vctx, const void* send, uint64_t bytes, void* re
   jbyteArray in = (*env)->NewByteArray(env, (jsize)bytes);
   if (in) {
     (*env)->SetByteArrayRegion(env, in, 0, (jsize)bytes, (const jbyte*)send);
-    jbyteArray out = (jbyteArray)(*env)->CallObjectMethod(env, b->target, b->all_gather, in);
+    jbyteArray out =
+        (jbyteArray)(*env)->CallObjectMethod(env, b->target, b->all_gather, (jlong)tag, in);
     if (!(*env)->ExceptionCheck(env) && out) {
-      jsize n = (*env)->GetArrayLength(env, out);
-      if (bytes == 0 || n % (jsize)bytes == 0) {
+      /* recv holds exactly world * bytes: any other reply (a contribution of another size, a
+       * round matched with the wrong collective) is an error, never a longer copy */
+      const jsize n = (*env)->GetArrayLength(env, out);
+      if ((uint64_t)n == (uint64_t)b->world * bytes) {
         (*env)->GetByteArrayRegion(env, out, 0, n, (jbyte*)recv);
         rc = 0;
       }
@@ -156,8 +163,13 @@ static int boot_allgather(void* vctx, const void* send, uint64_t bytes, void* re
   return rc;
 }
 
-JNIEXPORT jlong JNICALL FN(setBootstrap)(JNIEnv* env, jclass cls, jlong node, jobject bootstrap) {
+JNIEXPORT jlong JNICALL FN(setBootstrap)(JNIEnv* env, jclass cls, jlong node, jobject bootstrap,
+                                         jint worldSize) {
   (void)cls;
+  if (worldSize < 1) {
+    throw_sux(env, SUX_EINVAL, "setBootstrap: world size must be >= 1");
+    return 0;
+  }
   boot_ctx* b = (boot_ctx*)calloc(1, sizeof *b);
   if (!b) {
     throw_sux(env, SUX_ENOMEM, "setBootstrap");
@@ -165,8 +177,9 @@ JNIEXPORT jlong JNICALL FN(setBootstrap)(JNIEnv* env, jclass cls, jlong node, jo
   }
   (*env)->GetJavaVM(env, &b->vm);
   b->target = (*env)->NewGlobalRef(env, bootstrap);
+  b->world = worldSize;
   jclass bc = (*env)->GetObjectClass(env, bootstrap);
-  b->all_gather = (*env)->GetMethodID(env, bc, "allGather", "([B)[B");
+  b->all_gather = (*env)->GetMethodID(env, bc, "allGather", "(J[B)[B");
   if (!b->all_gather || failed(env, sux_node_set_bootstrap(NODE(node), boot_allgather, b),
                                "setBootstrap")) {
     (*env)->DeleteGlobalRef(env, b->target);
@@ -184,6 +197,22 @@ JNIEXPORT void JNICALL FN(releaseBootstrap)(JNIEnv* env, jclass cls, jlong ctx) 
   free(b);
 }
 
+/* HBM-capacity fallback: spill committed map outputs to Spark's files under spark.local.dir. */
+JNIEXPORT void JNICALL FN(setSpillDir)(JNIEnv* env, jclass cls, jlong node, jstring dir) {
+  (void)cls;
+  const char* d = dir ? (*env)->GetStringUTFChars(env, dir, NULL) : NULL;
+  int rc = sux_node_set_spill_dir(NODE(node), d);
+  if (d) (*env)->ReleaseStringUTFChars(env, dir, d);
+  failed(env, rc, "setSpillDir");
+}
+
+JNIEXPORT jlong JNICALL FN(spills)(JNIEnv* env, jclass cls, jlong node) {
+  (void)cls;
+  uint64_t v = 0;
+  if (failed(env, sux_node_spills(NODE(node), &v), "spills")) return 0;
+  return (jlong)v;
+}
+
 JNIEXPORT jlongArray JNICALL FN(poolStats)(JNIEnv* env, jclass cls, jlong node) {
   (void)cls;
   uint64_t v[4] = {0, 0, 0, 0};
@@ -194,8 +223,8 @@ JNIEXPORT jlongArray JNICALL FN(poolStats)(JNIEnv* env, jclass cls, jlong node) 
 }
 
 /* ---- kernel tuning table (sux_tuning) and the device error word ------------------------------
- * fields[] in the header's field order (hist_kernel .. sort_msd); 0 keeps the default. */
-#define SUX_TUNING_FIELDS ((int)(sizeof(sux_tuning) / sizeof(int32_t)) - 10)
+ * fields[] in the header's field order (hist_kernel .. exchange_self); 0 keeps the default. */
+#define SUX_TUNING_FIELDS ((int)(sizeof(sux_tuning) / sizeof(int32_t)) - 9)
 JNIEXPORT void JNICALL FN(setTuning)(JNIEnv* env, jclass cls, jlong node, jintArray fields) {
   (void)cls;
   sux_tuning t;
@@ -350,6 +379,19 @@ JNIEXPORT void JNICALL FN(exchange)(JNIEnv* env, jclass cls, jlong node, jint sh
   failed(env, sux_exchange(NODE(node), shuffleId, STREAM(stream)), "exchange");
 }
 
+/* The exchange of one window of map tasks, asynchronous (stream-ordered), and its completion. */
+JNIEXPORT void JNICALL FN(exchangeMaps)(JNIEnv* env, jclass cls, jlong node, jint shuffleId,
+                                        jint firstMap, jint numMaps, jlong stream) {
+  (void)cls;
+  failed(env, sux_exchange_maps(NODE(node), shuffleId, firstMap, numMaps, STREAM(stream)),
+         "exchangeMaps");
+}
+
+JNIEXPORT void JNICALL FN(exchangeWait)(JNIEnv* env, jclass cls, jlong node, jint shuffleId) {
+  (void)cls;
+  failed(env, sux_exchange_wait(NODE(node), shuffleId), "exchangeWait");
+}
+
 JNIEXPORT jintArray JNICALL FN(ownedPartitions)(JNIEnv* env, jclass cls, jlong node,
                                                 jint shuffleId, jint rank) {
   (void)cls;
@@ -396,6 +438,53 @@ JNIEXPORT jlong JNICALL FN(fetchBlocks)(JNIEnv* env, jclass cls, jlong node, jin
   free(ids);
   free(sz);
   if (failed(env, rc, "fetchBlocks")) return 0;
+  return (jlong)(intptr_t)out;
+}
+
+/* The reader's key sort on the GPU (the ExternalSorter step, UcxShuffleReader.scala:138-154 in
+ * the reference): `n` fixed-size records of a fetched buffer -> a new pooled buffer in ascending
+ * key order, stable (sux_sort_records); the workspace is a pooled buffer released here. */
+JNIEXPORT jlong JNICALL FN(sortRecords)(JNIEnv* env, jclass cls, jlong node, jint keyKind,
+                                        jlong buf, jlong n, jint recordSize, jint keyOffset,
+                                        jint keyLen, jlong stream) {
+  (void)cls;
+  void* src = NULL;
+  uint64_t size = 0;
+  if (failed(env, sux_buffer_info(BUF(buf), &src, &size, NULL), "sortRecords")) return 0;
+  if ((uint64_t)n * (uint64_t)recordSize > size) {
+    throw_sux(env, SUX_EINVAL, "sortRecords: the buffer holds fewer records");
+    return 0;
+  }
+  uint64_t ws_bytes = 0;
+  if (failed(env, sux_sort_workspace_size((uint64_t)n, (uint32_t)recordSize, &ws_bytes),
+             "sortRecords"))
+    return 0;
+  sux_buffer* out = NULL;
+  sux_buffer* ws = NULL;
+  if (failed(env, sux_buffer_alloc(NODE(node), (uint64_t)n * (uint64_t)recordSize, &out),
+             "sortRecords"))
+    return 0;
+  if (failed(env, sux_buffer_alloc(NODE(node), ws_bytes, &ws), "sortRecords")) {
+    sux_buffer_release(out);
+    return 0;
+  }
+  void* dst = NULL;
+  void* w = NULL;
+  sux_buffer_info(out, &dst, NULL, NULL);
+  sux_buffer_info(ws, &w, NULL, NULL);
+  int rc = sux_sort_records(NODE(node), keyKind, src, (uint64_t)n, (uint32_t)recordSize,
+                            keyOffset, keyLen, dst, w, ws_bytes, STREAM(stream));
+  /* the workspace may go back to the pool only after the stream ran the sort (release does not
+   * wait): a one-byte read-back synchronises the stream */
+  if (rc == SUX_OK && n > 0) {
+    uint8_t first;
+    rc = sux_buffer_read(out, 0, &first, 1, STREAM(stream));
+  }
+  sux_buffer_release(ws);
+  if (failed(env, rc, "sortRecords")) {
+    sux_buffer_release(out);
+    return 0;
+  }
   return (jlong)(intptr_t)out;
 }
 

@@ -4,10 +4,11 @@
  * org.apache.spark.shuffle.compat.spark_3_0.UcxLocalDiskShuffleDataIO, as for the reference.
  *
  * Map side: a dependency whose partitioner and rows the GPU restates bit-exactly
- * (GpuPartitioning, FixedWidthRows registered for its shuffle) is written by GpuShuffleWriter;
+ * (GpuPartitioning, and a FixedWidthRowSerializer as the dependency's serializer — its row
+ * layout travels to the executors inside UcxGpuShuffleHandle) is written by GpuShuffleWriter;
  * any other keeps Spark's writer, and the resolver adopts its committed data file into the
- * node's HBM.  Reduce side: UcxShuffleReader fetches through the node (after the node-wide
- * exchange when several GPUs share the shuffle).  The driver's metadata table of the reference
+ * node's HBM.  Reduce side: UcxShuffleReader fetches through the node, after the node-wide
+ * exchange the driver's GpuExchangeCoordinator starts on every executor as map tasks finish.  The driver's metadata table of the reference
  * (registerShuffleCommon, CommonUcxShuffleManager.scala:39-56) becomes each node's directory,
  * sized by the number of MAP tasks (the reference sizes it by partitioner.numPartitions, quirk
  * Q1, and its PUTs overrun the table when maps outnumber reduces).
@@ -19,15 +20,22 @@ import java.util.concurrent.ConcurrentHashMap
 import org.apache.spark.{ShuffleDependency, SparkConf, SparkEnv, TaskContext}
 import org.apache.spark.internal.Logging
 import org.apache.spark.shuffle.compat.spark_3_0.{UcxShuffleBlockResolver, UcxShuffleReader}
-import org.apache.spark.shuffle.gpu.{FixedWidthRows, GpuNode, GpuPartitioning, GpuShuffleWriter}
+import org.apache.spark.shuffle.gpu.{FixedWidthRowSerializer, GpuExchangeCoordinator, GpuNode,
+  GpuPartitioning, GpuRowLayout, GpuShuffleWriter}
 import org.apache.spark.shuffle.sort.SortShuffleManager
 import org.apache.spark.shuffle.ucx.gpu.SuxNative
 import org.apache.spark.util.ShutdownHookManager
 
-/** Handle broadcast to the tasks: Spark's handle + what the node needs to register the shuffle. */
-class UcxGpuShuffleHandle[K, V, C](shuffleId: Int, val numMaps: Int, val recordSize: Int,
+/** Handle broadcast to the tasks: Spark's handle + what the node needs to register the shuffle:
+ * the map count (directory slots) and, for a GPU shuffle, the row layout (a serializable POD, the
+ * analog of the reference's UcxRemoteMemory in UcxShuffleHandle, CommonUcxShuffleManager.scala:99-102). */
+class UcxGpuShuffleHandle[K, V, C](shuffleId: Int, val numMaps: Int,
+                                   val layout: Option[GpuRowLayout],
                                    val baseHandle: BaseShuffleHandle[K, V, C])
-  extends ShuffleHandle(shuffleId)
+  extends ShuffleHandle(shuffleId) {
+  /** The node's record size for this shuffle (4: byte-stream data files of Spark's writers). */
+  def recordSize: Int = layout.map(_.recordSize).getOrElse(4)
+}
 
 class UcxShuffleManager(val conf: SparkConf, isDriver: Boolean) extends SortShuffleManager(conf)
   with Logging {
@@ -37,10 +45,6 @@ class UcxShuffleManager(val conf: SparkConf, isDriver: Boolean) extends SortShuf
 
   override val shuffleBlockResolver = new UcxShuffleBlockResolver(conf)
 
-  /** Fixed-width row layouts by shuffle id, registered by the application (e.g. TeraSort). */
-  val rowLayouts = new ConcurrentHashMap[Int, FixedWidthRows[_, _]]()
-
-  private val registered = ConcurrentHashMap.newKeySet[Int]()
   private val partitioners = new ConcurrentHashMap[Int, java.lang.Long]()
 
   def startUcxNodeIfMissing(): GpuNode = GpuNode.startIfMissing(conf, isDriver)
@@ -49,17 +53,24 @@ class UcxShuffleManager(val conf: SparkConf, isDriver: Boolean) extends SortShuf
                                         dependency: ShuffleDependency[K, V, C]): ShuffleHandle = {
     val base = super.registerShuffle(shuffleId, dependency).asInstanceOf[BaseShuffleHandle[K, V, C]]
     val numMaps = dependency.rdd.partitions.length  // Q1: slots per MAP task
-    val rs = Option(rowLayouts.get(shuffleId)).map(_.recordSize).getOrElse(0)
-    new UcxGpuShuffleHandle(shuffleId, numMaps, rs, base)
+    // the row layout is a property of the dependency's serializer, so it exists when Spark calls
+    // this from the ShuffleDependency constructor (before any id-keyed registration could)
+    val layout = dependency.serializer match {
+      case s: FixedWidthRowSerializer[_, _] => Some(s.layout)
+      case _ => None
+    }
+    val handle = new UcxGpuShuffleHandle(shuffleId, numMaps, layout, base)
+    if (isDriver) {
+      GpuExchangeCoordinator.watch(conf, shuffleId, numMaps, dependency.partitioner.numPartitions,
+        handle.recordSize)
+    }
+    handle
   }
 
   /** The executor's node learns a shuffle on its first task (register is idempotent here). */
-  private def ensureRegistered(h: UcxGpuShuffleHandle[_, _, _], node: GpuNode): Unit = {
-    if (registered.add(h.shuffleId)) {
-      SuxNative.registerShuffle(node.handle, h.shuffleId, h.numMaps,
-        h.baseHandle.dependency.partitioner.numPartitions, math.max(4, h.recordSize))
-    }
-  }
+  private def ensureRegistered(h: UcxGpuShuffleHandle[_, _, _], node: GpuNode): Unit =
+    node.ensureRegistered(h.shuffleId, h.numMaps, h.baseHandle.dependency.partitioner.numPartitions,
+      h.recordSize)
 
   override def getWriter[K, V](handle: ShuffleHandle, mapId: Long, context: TaskContext,
                                metrics: ShuffleWriteMetricsReporter): ShuffleWriter[K, V] = {
@@ -67,7 +78,11 @@ class UcxShuffleManager(val conf: SparkConf, isDriver: Boolean) extends SortShuf
     val node = GpuNode.get  // IllegalStateException before the executor components start
     ensureRegistered(h, node)
     val dep = h.baseHandle.dependency
-    val rows = Option(rowLayouts.get(h.shuffleId)).map(_.asInstanceOf[FixedWidthRows[K, V]])
+    val rows = dep.serializer match {
+      case s: FixedWidthRowSerializer[_, _] if h.layout.isDefined =>
+        Some(s.asInstanceOf[FixedWidthRowSerializer[K, V]].rows)
+      case _ => None
+    }
     val gpu = rows.flatMap(r => GpuPartitioning.of(dep.partitioner, r.keyLen).map(r -> _))
     gpu match {
       case Some((r, p)) =>
@@ -90,19 +105,18 @@ class UcxShuffleManager(val conf: SparkConf, isDriver: Boolean) extends SortShuf
   }
 
   override def unregisterShuffle(shuffleId: Int): Boolean = {
-    if (registered.remove(shuffleId)) {
-      val node = GpuNode.get
-      SuxNative.unregisterShuffle(node.handle, shuffleId)
-      node.forget(shuffleId)
-    }
+    Option(GpuNodeOrNull()).foreach(_.unregister(shuffleId))
     Option(partitioners.remove(shuffleId)).foreach(p => SuxNative.partitionerDestroy(p))
-    rowLayouts.remove(shuffleId)
+    if (isDriver) GpuExchangeCoordinator.forget(shuffleId)
     super.unregisterShuffle(shuffleId)
   }
 
   override def stop(): Unit = synchronized {
-    registered.forEach(id => unregisterShuffle(id))
+    Option(GpuNodeOrNull()).foreach(n => n.registeredShuffles.foreach(id => unregisterShuffle(id)))
     GpuNode.stop()
     super.stop()
   }
+
+  private def GpuNodeOrNull(): GpuNode =
+    try GpuNode.get catch { case _: IllegalStateException => null }
 }

@@ -3,23 +3,31 @@
  * reference calls UcxNode (UcxNode.java:60-96), started lazily and closed at stop().
  *
  *  - configuration: the reference's spark.shuffle.ucx.* keys (UcxShuffleConf.scala:17-90) plus
- *    spark.shuffle.ucx.gpu.* (device, rank and size of the node's exchange group);
+ *    spark.shuffle.ucx.gpu.* (device, rank and size of the node's exchange group, pool cap,
+ *    spill directory, exchange window);
  *  - one HIP stream per task thread, the analog of getThreadLocalWorker (:147-176);
- *  - the exchange group's control plane: an all-gather over Spark RPC through the driver
- *    (GpuBootstrapEndpoint), which replaces the UCX tag messages of the reference's bootstrap;
- *  - exchangeOnce: the node-wide all-to-all of a shuffle, run by the first reduce task of every
- *    executor (a collective: each executor of the group takes part once).
+ *  - the exchange group's control plane over Spark RPC through the driver (GpuControlEndpoint):
+ *    a host all-gather matched by tag, which replaces the UCX tag messages of the reference's
+ *    bootstrap, and the driver -> executor messages of GpuExchangeCoordinator;
+ *  - the exchange: a collective over the group, so it is not run by whichever reduce task comes
+ *    first (an executor without reduce tasks would never join it) but by every executor when the
+ *    driver's coordinator says so — window by window as map tasks finish, the last when the map
+ *    stage completes — on one exchange thread per node; reduce tasks wait for it.
  */
 package org.apache.spark.shuffle.gpu
 
-import java.util.concurrent.ConcurrentHashMap
+import java.util.concurrent.{ConcurrentHashMap, Executors, ThreadFactory, TimeUnit}
 
 import scala.collection.mutable
+import scala.concurrent.{Await, Promise}
+import scala.concurrent.duration.Duration
 
-import org.apache.spark.{SparkConf, SparkEnv}
+import org.apache.spark.{SparkConf, SparkContext, SparkEnv, Success => TaskSuccess}
 import org.apache.spark.internal.Logging
 import org.apache.spark.network.util.JavaUtils
-import org.apache.spark.rpc.{RpcCallContext, RpcEnv, ThreadSafeRpcEndpoint}
+import org.apache.spark.rpc.{RpcCallContext, RpcEndpointRef, RpcEnv, ThreadSafeRpcEndpoint}
+import org.apache.spark.scheduler.{SparkListener, SparkListenerStageCompleted,
+  SparkListenerStageSubmitted, SparkListenerTaskEnd}
 import org.apache.spark.shuffle.ucx.gpu.{Bootstrap, SuxNative}
 import org.apache.spark.util.RpcUtils
 
@@ -40,11 +48,22 @@ class GpuNode private (conf: SparkConf, isDriver: Boolean) extends Logging {
 
   private val handle0: Long = SuxNative.nodeCreate(device, rank, worldSize, null,
     bytes(ucx("memory.minBufferSize"), "1024"), minAllocationSize, metadataBlockSize,
-    conf.get(ucx("memory.preAllocateBuffers"), ""), isDriver)
+    conf.get(ucx("memory.preAllocateBuffers"), ""), conf.getInt(ucx("gpu.poolLimitMiB"), 0),
+    isDriver)
 
   private val bootCtx: Long =
-    if (worldSize > 1 && !isDriver) SuxNative.setBootstrap(handle0, new RpcBootstrap(conf, rank, worldSize))
-    else 0L
+    if (worldSize > 1 && !isDriver) {
+      SuxNative.setBootstrap(handle0, new RpcBootstrap(conf, rank, worldSize), worldSize)
+    } else 0L
+
+  // HBM-capacity fallback: committed map outputs spill to Spark's files under the first local
+  // directory (the reference serves every block from such files)
+  if (!isDriver) {
+    val dirs = conf.get("spark.local.dir", System.getProperty("java.io.tmpdir")).split(",")
+    val d = new java.io.File(dirs.head.trim, s"sparkucx-gpu-$rank")
+    d.mkdirs()
+    SuxNative.setSpillDir(handle0, d.getAbsolutePath)
+  }
 
   // spark.shuffle.ucx.gpu.tuning.<field> = <int>: the node's kernel tuning table (sux_tuning);
   // unset fields keep the measured defaults
@@ -68,21 +87,76 @@ class GpuNode private (conf: SparkConf, isDriver: Boolean) extends Logging {
   /** This task thread's stream (getThreadLocalWorker analog). */
   def threadStream(): Long = threadStream.get()
 
-  private val exchanged = mutable.Set[Int]()
+  // ---- shuffles this node knows (registerShuffleCommon, CommonUcxShuffleManager.scala:39-56:
+  // an executor learns a shuffle from its first task, or from the coordinator's first message)
+  private val registered = ConcurrentHashMap.newKeySet[Int]()
 
-  /** The node-wide exchange of a shuffle, once per executor (the first reduce task runs it). */
-  def exchangeOnce(shuffleId: Int): Unit = exchanged.synchronized {
-    if (!exchanged.contains(shuffleId)) {
-      val t0 = System.nanoTime()
-      SuxNative.exchange(handle0, shuffleId, threadStream())
-      exchanged += shuffleId
-      logInfo(s"shuffle $shuffleId exchanged in ${(System.nanoTime() - t0) / 1e6} ms")
+  def ensureRegistered(shuffleId: Int, numMaps: Int, numPartitions: Int, recordSize: Int): Unit =
+    registered.synchronized {
+      if (!registered.contains(shuffleId)) {
+        SuxNative.registerShuffle(handle0, shuffleId, numMaps, numPartitions, recordSize)
+        registered.add(shuffleId)
+      }
     }
+
+  def unregister(shuffleId: Int): Unit = registered.synchronized {
+    if (registered.remove(shuffleId)) SuxNative.unregisterShuffle(handle0, shuffleId)
+    exchanges.remove(shuffleId)
   }
 
-  def forget(shuffleId: Int): Unit = exchanged.synchronized { exchanged -= shuffleId }
+  def registeredShuffles: Seq[Int] = registered.toArray(Array.empty[Integer]).toSeq.map(_.intValue)
+
+  // ---- the exchange --------------------------------------------------------------------------
+  private val exchangeThread = Executors.newSingleThreadExecutor(new ThreadFactory {
+    override def newThread(r: Runnable): Thread = {
+      val t = new Thread(r, s"sparkucx-gpu-exchange-$rank")
+      t.setDaemon(true)
+      t
+    }
+  })
+  private lazy val exchangeStream: Long = SuxNative.streamCreate(handle0)
+  private val exchanges = new ConcurrentHashMap[Int, Promise[Unit]]()
+  private def promiseOf(id: Int): Promise[Unit] = exchanges.computeIfAbsent(id, _ => Promise[Unit]())
+  private val exchangeTimeout: Duration =
+    Duration(conf.getTimeAsSeconds("spark.network.timeout", "120s"), TimeUnit.SECONDS)
+
+  /** Map tasks [first, first + count) of a shuffle are committed on every executor: enqueue
+   * their exchange (sux_exchange_maps; asynchronous on the exchange stream, so the next maps'
+   * kernels keep running).  Driver messages reach every executor in the same order, so the
+   * collective calls match. */
+  def exchangeWindow(w: GpuControlEndpoint.ExchangeWindow): Unit =
+    exchangeThread.execute(() => {
+      try {
+        ensureRegistered(w.shuffleId, w.numMaps, w.numPartitions, w.recordSize)
+        SuxNative.exchangeMaps(handle0, w.shuffleId, w.first, w.count, exchangeStream)
+      } catch { case e: Throwable => promiseOf(w.shuffleId).tryFailure(e) }
+    })
+
+  /** The map stage completed: finish the shuffle's exchange (sux_exchange_wait). */
+  def exchangeDone(shuffleId: Int): Unit =
+    exchangeThread.execute(() => {
+      try {
+        SuxNative.exchangeWait(handle0, shuffleId)
+        promiseOf(shuffleId).trySuccess(())
+      } catch { case e: Throwable => promiseOf(shuffleId).tryFailure(e) }
+    })
+
+  /** Reduce tasks wait for the exchange (a group of one GPU has nothing to exchange). */
+  def awaitExchange(shuffleId: Int): Unit =
+    if (worldSize > 1) Await.result(promiseOf(shuffleId).future, exchangeTimeout)
+
+  // executors of a group register with the driver's control endpoint, which relays the
+  // coordinator's messages to them
+  if (worldSize > 1 && !isDriver) {
+    val env = SparkEnv.get.rpcEnv
+    val me = env.setupEndpoint(GpuControlEndpoint.EXECUTOR + rank, new GpuExecutorEndpoint(env, this))
+    RpcUtils.makeDriverRef(GpuControlEndpoint.NAME, conf, env)
+      .askSync[Boolean](GpuControlEndpoint.Hello(rank, worldSize, me))
+  }
 
   def close(): Unit = synchronized {
+    exchangeThread.shutdown()
+    exchangeThread.awaitTermination(10, TimeUnit.SECONDS)
     streams.values().forEach(s => SuxNative.streamDestroy(handle0, s))
     streams.clear()
     SuxNative.nodeDestroy(handle0)
@@ -97,7 +171,7 @@ object GpuNode {
   def startIfMissing(conf: SparkConf, isDriver: Boolean): GpuNode = synchronized {
     if (instance == null) {
       if (isDriver && conf.getInt("spark.shuffle.ucx.gpu.worldSize", 1) > 1) {
-        GpuBootstrapEndpoint.setup(SparkEnv.get.rpcEnv, conf.getInt("spark.shuffle.ucx.gpu.worldSize", 1))
+        GpuControlEndpoint.setup(SparkEnv.get.rpcEnv, conf.getInt("spark.shuffle.ucx.gpu.worldSize", 1))
       }
       instance = new GpuNode(conf, isDriver)
     }
@@ -120,40 +194,145 @@ object GpuNode {
   }
 }
 
-/** Host all-gather through the driver endpoint: one ask per round, answered when all ranks
- * of the round have arrived. */
+/** Host all-gather through the driver endpoint: one ask per collective, answered when every rank
+ * contributed to the same tag. */
 private class RpcBootstrap(conf: SparkConf, rank: Int, world: Int) extends Bootstrap {
-  private var round = 0L
-  private lazy val driver = RpcUtils.makeDriverRef(GpuBootstrapEndpoint.NAME, conf, SparkEnv.get.rpcEnv)
+  private lazy val driver = RpcUtils.makeDriverRef(GpuControlEndpoint.NAME, conf, SparkEnv.get.rpcEnv)
 
-  override def allGather(mine: Array[Byte]): Array[Byte] = synchronized {
-    round += 1
-    driver.askSync[Array[Byte]](GpuBootstrapEndpoint.Contribute(round, rank, world, mine))
+  override def allGather(tag: Long, mine: Array[Byte]): Array[Byte] =
+    driver.askSync[Array[Byte]](GpuControlEndpoint.Contribute(tag, rank, world, mine))
+}
+
+private[gpu] object GpuControlEndpoint {
+  val NAME = "SparkUcxGpuControl"
+  val EXECUTOR = "SparkUcxGpuExecutor-"
+  case class Contribute(tag: Long, rank: Int, world: Int, bytes: Array[Byte])
+  case class Hello(rank: Int, world: Int, ref: RpcEndpointRef)
+  /** Map tasks [first, first + count) of a shuffle (numMaps / numPartitions / recordSize: what an
+   * executor that ran none of its tasks needs to register it before the collective). */
+  case class ExchangeWindow(shuffleId: Int, numMaps: Int, numPartitions: Int, recordSize: Int,
+                            first: Int, count: Int)
+  case class ExchangeDone(shuffleId: Int)
+
+  @volatile private var endpoint: RpcEndpointRef = _
+
+  def setup(rpcEnv: RpcEnv, world: Int): Unit =
+    endpoint = rpcEnv.setupEndpoint(NAME, new GpuControlEndpoint(rpcEnv, world))
+
+  /** Driver: relay a coordinator message to every executor of the group, in order. */
+  def broadcast(msg: Any): Unit = Option(endpoint).foreach(_.send(msg))
+}
+
+private class GpuControlEndpoint(override val rpcEnv: RpcEnv, world: Int)
+  extends ThreadSafeRpcEndpoint {
+  import GpuControlEndpoint._
+  private val pending = mutable.Map[Long, Array[(Array[Byte], RpcCallContext)]]()
+  private val executors = new Array[RpcEndpointRef](world)
+
+  override def receive: PartialFunction[Any, Unit] = {
+    case m @ (_: ExchangeWindow | _: ExchangeDone) => executors.filter(_ != null).foreach(_.send(m))
+  }
+
+  override def receiveAndReply(context: RpcCallContext): PartialFunction[Any, Unit] = {
+    case Hello(rank, w, ref) =>
+      require(w == world && rank >= 0 && rank < world, s"executor rank $rank of $w, driver expects $world")
+      executors(rank) = ref
+      context.reply(true)
+    case Contribute(tag, rank, w, bytes) =>
+      require(w == world, s"bootstrap: executor reports world $w, driver expects $world")
+      val slots = pending.getOrElseUpdate(tag, new Array(world))
+      require(slots(rank) == null, s"bootstrap: rank $rank contributed twice to collective $tag")
+      slots(rank) = (bytes, context)
+      if (slots.forall(_ != null)) {
+        pending.remove(tag)
+        if (slots.exists(_._1.length != bytes.length)) {  // ranks out of step: fail them all
+          val e = new IllegalStateException(s"bootstrap: contributions of different sizes to $tag")
+          slots.foreach(_._2.sendFailure(e))
+        } else {
+          val all = slots.flatMap(_._1)
+          slots.foreach(_._2.reply(all))
+        }
+      }
   }
 }
 
-private[gpu] object GpuBootstrapEndpoint {
-  val NAME = "SparkUcxGpuBootstrap"
-  case class Contribute(round: Long, rank: Int, world: Int, bytes: Array[Byte])
-
-  def setup(rpcEnv: RpcEnv, world: Int): Unit =
-    rpcEnv.setupEndpoint(NAME, new GpuBootstrapEndpoint(rpcEnv, world))
+private class GpuExecutorEndpoint(override val rpcEnv: RpcEnv, node: GpuNode)
+  extends ThreadSafeRpcEndpoint {
+  import GpuControlEndpoint._
+  override def receive: PartialFunction[Any, Unit] = {
+    case w: ExchangeWindow => node.exchangeWindow(w)
+    case ExchangeDone(id) => node.exchangeDone(id)
+  }
 }
 
-private class GpuBootstrapEndpoint(override val rpcEnv: RpcEnv, world: Int)
-  extends ThreadSafeRpcEndpoint {
-  import GpuBootstrapEndpoint.Contribute
-  private val pending = mutable.Map[Long, Array[(Array[Byte], RpcCallContext)]]()
+/**
+ * Driver side: starts each GPU shuffle's exchange on every executor.  With
+ * spark.shuffle.ucx.gpu.exchangeWindowMaps = w > 0, window k (maps [k w, (k+1) w)) is exchanged
+ * as soon as all its map tasks have succeeded, while later map tasks still run (the overlap of
+ * the exchange with the next maps; receive memory per window is bounded like the reference's
+ * maxBytesInFlight, UcxShuffleReader.scala:56-70); the remaining maps and the completion follow
+ * the map stage's end.  w = 0: one exchange at the stage's end.
+ */
+object GpuExchangeCoordinator extends Logging {
+  private case class Watch(numMaps: Int, numPartitions: Int, recordSize: Int, window: Int,
+                           done: mutable.BitSet, var sent: Int) {
+    def msg(id: Int, first: Int, count: Int) =
+      GpuControlEndpoint.ExchangeWindow(id, numMaps, numPartitions, recordSize, first, count)
+  }
+  private val watched = new ConcurrentHashMap[Int, Watch]()
+  private val stageShuffle = new ConcurrentHashMap[Int, Int]()
+  @volatile private var listening = false
 
-  override def receiveAndReply(context: RpcCallContext): PartialFunction[Any, Unit] = {
-    case Contribute(round, rank, w, bytes) =>
-      require(w == world, s"bootstrap: executor reports world $w, driver expects $world")
-      val slots = pending.getOrElseUpdate(round, new Array(world))
-      slots(rank) = (bytes, context)
-      if (slots.forall(_ != null)) {
-        val all = slots.flatMap(_._1)
-        slots.foreach(_._2.reply(all))
-        pending.remove(round)
+  def watch(conf: SparkConf, shuffleId: Int, numMaps: Int, numPartitions: Int,
+            recordSize: Int): Unit = {
+    if (conf.getInt("spark.shuffle.ucx.gpu.worldSize", 1) <= 1) return
+    watched.put(shuffleId, Watch(numMaps, numPartitions, recordSize,
+      conf.getInt("spark.shuffle.ucx.gpu.exchangeWindowMaps", 0), mutable.BitSet(), 0))
+    synchronized {
+      if (!listening) {
+        SparkContext.getActive.foreach(_.addSparkListener(Listener))
+        listening = true
+      }
+    }
+  }
+
+  def forget(shuffleId: Int): Unit = watched.remove(shuffleId)
+
+  private def advance(id: Int, w: Watch, stageDone: Boolean): Unit = w.synchronized {
+    if (w.window > 0) {
+      while (w.sent < w.numMaps && (w.sent until math.min(w.numMaps, w.sent + w.window)).forall(w.done)) {
+        val n = math.min(w.window, w.numMaps - w.sent)
+        GpuControlEndpoint.broadcast(w.msg(id, w.sent, n))
+        w.sent += n
+      }
+    }
+    if (stageDone) {
+      if (w.sent < w.numMaps) {
+        GpuControlEndpoint.broadcast(w.msg(id, w.sent, w.numMaps - w.sent))
+        w.sent = w.numMaps
+      }
+      GpuControlEndpoint.broadcast(GpuControlEndpoint.ExchangeDone(id))
+      logInfo(s"shuffle $id: exchange of ${w.numMaps} map outputs started on every executor")
+    }
+  }
+
+  private object Listener extends SparkListener {
+    override def onStageSubmitted(e: SparkListenerStageSubmitted): Unit =
+      e.stageInfo.shuffleDepId.foreach(id => stageShuffle.put(e.stageInfo.stageId, id))
+
+    override def onTaskEnd(e: SparkListenerTaskEnd): Unit = if (e.reason == TaskSuccess) {
+      Option(stageShuffle.get(e.stageId)).flatMap(id => Option(watched.get(id)).map(id -> _))
+        .foreach { case (id, w) =>
+          w.synchronized { w.done += e.taskInfo.index }  // ShuffleMapTask index = map index
+          advance(id, w, stageDone = false)
+        }
+    }
+
+    override def onStageCompleted(e: SparkListenerStageCompleted): Unit =
+      if (e.stageInfo.failureReason.isEmpty) {
+        e.stageInfo.shuffleDepId.foreach { id =>
+          Option(watched.get(id)).foreach(w => advance(id, w, stageDone = true))
+        }
       }
   }
 }

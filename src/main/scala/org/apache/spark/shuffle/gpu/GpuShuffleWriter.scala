@@ -8,8 +8,9 @@
  *
  * GpuPartitioning decides whether a dependency can take this path: its partitioner must be one
  * the kernels restate bit-exactly (RangePartitioner over byte-array keys, HashPartitioner over
- * Long/Int keys) and its rows must serialize to exactly `recordSize` bytes.  Anything else keeps
- * Spark's writer; its committed data file is adopted by the resolver instead.
+ * Long/Int keys) and its serializer must be a FixedWidthRowSerializer (rows of exactly
+ * `recordSize` bytes).  Anything else keeps Spark's writer; its committed data file is adopted
+ * by the resolver instead.
  */
 package org.apache.spark.shuffle.gpu
 
@@ -51,11 +52,139 @@ object GpuPartitioning {
   }
 }
 
-/** A row serializer writing one record as exactly recordSize bytes (key first). */
+/** A row codec: one record is exactly recordSize bytes, the key's keyLen bytes first. */
 trait FixedWidthRows[K, V] extends Serializable {
   def recordSize: Int
   def keyLen: Int
   def write(key: K, value: V, out: ByteBuffer): Unit
+  /** The inverse of write: consumes exactly recordSize bytes of `in`. */
+  def read(in: ByteBuffer): (K, V)
+}
+
+/** What a GPU shuffle's handle carries to every executor (UcxGpuShuffleHandle): the row layout
+ * of its dependency's serializer. */
+case class GpuRowLayout(recordSize: Int, keyOffset: Int, keyLen: Int)
+
+/**
+ * The dependency's serializer for a GPU shuffle: fixed-width rows, no stream header, no length
+ * prefix — the bytes the kernels partition and the bytes Spark's own writers produce with it are
+ * the same, and its deserializer reads either.  A ShuffleDependency is built with it
+ * (`new ShuffledRDD(...).setSerializer(new FixedWidthRowSerializer(rows))`); registerShuffle
+ * finds the layout here, inside the dependency — the shuffle id does not exist before the
+ * dependency's constructor runs, so nothing can be registered by id ahead of it.
+ */
+class FixedWidthRowSerializer[K, V](val rows: FixedWidthRows[K, V])
+  extends org.apache.spark.serializer.Serializer with Serializable {
+
+  def layout: GpuRowLayout = GpuRowLayout(rows.recordSize, 0, rows.keyLen)
+
+  // rows are independent fixed-size byte runs: concatenations are valid streams (batch fetch)
+  override def supportsRelocationOfSerializedObjects: Boolean = true
+
+  override def newInstance(): org.apache.spark.serializer.SerializerInstance =
+    new FixedWidthRowSerializerInstance(rows)
+}
+
+private class FixedWidthRowSerializerInstance[K, V](rows: FixedWidthRows[K, V])
+  extends org.apache.spark.serializer.SerializerInstance {
+  import java.io.{EOFException, InputStream, OutputStream}
+  import org.apache.spark.serializer.{DeserializationStream, SerializationStream}
+  import scala.reflect.ClassTag
+
+  private def unsupported = throw new UnsupportedOperationException(
+    "FixedWidthRowSerializer only streams (key, value) rows")
+  override def serialize[T: ClassTag](t: T): ByteBuffer = unsupported
+  override def deserialize[T: ClassTag](bytes: ByteBuffer): T = unsupported
+  override def deserialize[T: ClassTag](bytes: ByteBuffer, loader: ClassLoader): T = unsupported
+
+  override def serializeStream(s: OutputStream): SerializationStream = new SerializationStream {
+    private val row = ByteBuffer.allocate(rows.recordSize).order(ByteOrder.LITTLE_ENDIAN)
+    private var key: Any = _
+    private var haveKey = false
+    override def writeKey[T: ClassTag](k: T): SerializationStream = { key = k; haveKey = true; this }
+    override def writeValue[T: ClassTag](v: T): SerializationStream = {
+      require(haveKey, "a row is written as writeKey then writeValue")
+      row.clear()
+      rows.write(key.asInstanceOf[K], v.asInstanceOf[V], row)
+      require(row.position() == rows.recordSize, s"row is not ${rows.recordSize} bytes")
+      s.write(row.array(), 0, rows.recordSize)
+      haveKey = false
+      this
+    }
+    override def writeObject[T: ClassTag](t: T): SerializationStream = t match {
+      case (k, v) => writeKey(k); writeValue(v)
+      case _ => unsupported
+    }
+    override def flush(): Unit = s.flush()
+    override def close(): Unit = s.close()
+  }
+
+  override def deserializeStream(s: InputStream): DeserializationStream = new DeserializationStream {
+    private val row = ByteBuffer.allocate(rows.recordSize).order(ByteOrder.LITTLE_ENDIAN)
+    /** The next row, or EOFException at a clean end of stream. */
+    private def next(): (K, V) = {
+      var got = 0
+      while (got < rows.recordSize) {
+        val r = s.read(row.array(), got, rows.recordSize - got)
+        if (r < 0) {
+          if (got == 0) throw new EOFException
+          throw new java.io.IOException(s"truncated row: $got of ${rows.recordSize} bytes")
+        }
+        got += r
+      }
+      row.clear()
+      rows.read(row)
+    }
+    override def readObject[T: ClassTag](): T = next().asInstanceOf[T]
+    override def readKey[T: ClassTag](): T = unsupported
+    override def readValue[T: ClassTag](): T = unsupported
+    override def asKeyValueIterator: Iterator[(Any, Any)] = new Iterator[(Any, Any)] {
+      private var pending: Option[(K, V)] = None
+      private var done = false
+      override def hasNext: Boolean = {
+        if (pending.isEmpty && !done) {
+          try pending = Some(next()) catch { case _: EOFException => done = true; s.close() }
+        }
+        pending.nonEmpty
+      }
+      override def next(): (Any, Any) = {
+        if (!hasNext) throw new NoSuchElementException
+        val kv = pending.get
+        pending = None
+        kv
+      }
+    }
+    override def close(): Unit = s.close()
+  }
+}
+
+/** A key ordering the GPU sort restates bit-exactly (sux_sort_records): when the dependency
+ * orders its keys with one of these, the reader sorts on the GPU instead of ExternalSorter. */
+trait GpuKeyOrdering extends Serializable {
+  def sortKind: Int
+  def keyLen: Int
+}
+
+/** TeraSort's order: unsigned lexicographic over keyLen-byte keys. */
+class UnsignedBytesOrdering(val keyLen: Int) extends Ordering[Array[Byte]] with GpuKeyOrdering {
+  require(keyLen >= 1 && keyLen <= 12, "the GPU sorts byte keys of 1..12 bytes")
+  override def sortKind: Int = SuxNative.SORT_BYTES
+  override def compare(a: Array[Byte], b: Array[Byte]): Int = {
+    var i = 0
+    while (i < keyLen) {
+      val d = (a(i) & 0xff) - (b(i) & 0xff)
+      if (d != 0) return d
+      i += 1
+    }
+    0
+  }
+}
+
+/** Spark's LongType order (signed), for a little-endian int64 key. */
+object SignedLongOrdering extends Ordering[Long] with GpuKeyOrdering {
+  override def sortKind: Int = SuxNative.SORT_LONG
+  override def keyLen: Int = 8
+  override def compare(a: Long, b: Long): Int = java.lang.Long.compare(a, b)
 }
 
 class GpuShuffleWriter[K, V](

@@ -18,9 +18,9 @@ def test_library_loads_and_exports_every_header_symbol():
     missing = [s for s in declared if not hasattr(lib, s)]
     assert not missing, missing
     assert set(declared) == set(N._SIGS), set(declared) ^ set(N._SIGS)
-    assert lib.sux_abi_version() == 3
+    assert lib.sux_abi_version() == 4
     assert C.sizeof(N.Conf) == 432  # sux_conf of ABI v2 (prealloc pairs appended)
-    assert C.sizeof(N.Tuning) == 128  # sux_tuning of ABI v3: 22 knobs + 10 reserved
+    assert C.sizeof(N.Tuning) == 128  # sux_tuning of ABI v4: 23 knobs + 9 reserved
 
 
 def test_conf_defaults_mirror_ucx_shuffle_conf():

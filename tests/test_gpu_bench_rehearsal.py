@@ -38,6 +38,10 @@ def test_bench_two_ranks_one_gpu():
     ex = res["roofline_exchange"]
     # uniform keys: about half of each rank's bytes leave it
     assert 0.4 < ex["remote_bytes_per_rank"] / (3_000_000 * 100) < 0.6
+    # the N>1 device self-check ran over every launch group, and the plugin leg (write ->
+    # windowed sux_exchange_maps -> wait -> fetch) passed its own device check
+    assert res["self_check"]["ok"] and res["self_check"]["groups"] == 6
+    assert res["plugin"]["self_check"] == "ok" and res["plugin"]["maps"] == 5 * 2 * 2
 
 
 @pytest.mark.parametrize("workload", ["terasort", "zipf"])
@@ -50,3 +54,5 @@ def test_bench_eight_ranks_verified(workload):
     assert res["verified_groups"] == 3
     ex = res["roofline_exchange"]
     assert ex["remote_bytes_per_rank"] > 0
+    assert res["self_check"]["ok"] and res["self_check"]["groups"] == 3
+    assert res["plugin"]["self_check"] == "ok" and res["plugin"]["maps"] == 2 * 8 * 2

@@ -1,0 +1,191 @@
+"""GPU, one process: the plugin path's exchange, adoption and HBM-capacity fallback.
+
+- The RCCL transport of sux_exchange_maps with real bytes on one GPU: a one-rank communicator
+  and the loopback (tuning exchange_self = 1), so every owned range of every map goes through
+  ncclAllToAllv rounds into the receive buffer and is fetched from there.  Multi-rank counts are
+  covered on the CPU by tests/test_exchange_plan.py (the same plan function).
+- The IPC transport's loopback at world 1 (pulls from the own batch slabs).
+- sux_adopt_map_outputs: stateless map outputs committed in place, resolved zero-copy.
+- Spill: a device pool capped far below the shuffle's size with a spill directory; committed
+  map outputs go to Spark's files and are fetched back byte-exact
+  (CommonUcxShuffleBlockResolver.scala:45-58 serves every block from such files)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from sparkucx_amd import native as N
+from sparkucx_amd.shuffle import Node
+
+pytestmark = pytest.mark.gpu
+SEED = 0x5EED00E1
+
+
+def _terasort(node, R):
+    opart = O.terasort_partitioner(R)
+    return opart, node.partitioner(N.PART_RANGE_BYTES, R, key_offset=0, key_len=10,
+                                   bounds=opart.bounds)
+
+
+def _write_windows(node, sid, part, M, rpm, windows, batch):
+    keep = []
+    win = [((k * M) // windows, ((k + 1) * M) // windows) for k in range(windows)]
+
+    def write(k):
+        w0, w1 = win[k]
+        for b0 in range(w0, w1, batch):
+            b1 = min(w1, b0 + batch)
+            recs = node.generate(N.GEN_TERASORT, SEED, b0 * rpm, (b1 - b0) * rpm, 100)
+            keep.append(recs)
+            node.write_map_outputs(sid, b0, part, recs, rpm, (b1 - b0) * rpm)
+
+    write(0)
+    for k in range(windows):
+        if k + 1 < windows:
+            write(k + 1)
+        node.exchange_maps(sid, win[k][0], win[k][1] - win[k][0])
+    node.exchange_wait(sid)
+    return keep
+
+
+def _check_all_blocks(node, sid, opart, M, rpm, R, parts=None):
+    want = {m: O.write_map(opart, O.gen_terasort(SEED, m * rpm, rpm), 100) for m in range(M)}
+    parts = parts if parts is not None else range(R)
+    blocks = [(m, p) for p in parts for m in range(M)]
+    buf, sizes = node.fetch_blocks(sid, blocks)
+    got = np.frombuffer(buf.to_bytes(), np.uint8)
+    buf.release(len(blocks))
+    pos = 0
+    for (m, p), sz in zip(blocks, sizes):
+        d, _, ix, _ = want[m]
+        w = d[ix[p]:ix[p + 1]]
+        assert sz == len(w), (m, p)
+        assert got[pos:pos + sz].tobytes() == w.tobytes(), (m, p)
+        pos += sz
+    assert pos == got.size
+
+
+@pytest.mark.parametrize("windows,batch", [(1, 4), (3, 2), (2, 1)])
+def test_rccl_loopback_exchange_maps(windows, batch):
+    """One-rank RCCL communicator + loopback: ncclAllToAllv rounds carry every block."""
+    node = Node(device=0, rank=0, world_size=1, comm_id=N.unique_id())
+    try:
+        node.set_tuning(exchange_self=1)
+        R, M, rpm = 50, 9, 30000
+        opart, part = _terasort(node, R)
+        node.register_shuffle(7, M, R, 100)
+        _write_windows(node, 7, part, M, rpm, windows, batch)
+        # every block now resolves into the receive buffers, not the map slabs
+        addrs, _ = node.resolve_blocks(7, [(m, p) for m in range(M) for p in (0, R - 1)])
+        assert len(set(addrs.tolist())) > 1
+        _check_all_blocks(node, 7, opart, M, rpm, R)
+        node.check()
+        node.unregister_shuffle(7)
+    finally:
+        node.close()
+
+
+def test_ipc_loopback_world1():
+    node = Node(device=0)
+    try:
+        node.set_tuning(exchange_self=1)
+        R, M, rpm = 33, 7, 25000
+        opart, part = _terasort(node, R)
+        node.register_shuffle(8, M, R, 100)
+        _write_windows(node, 8, part, M, rpm, 2, 3)
+        _check_all_blocks(node, 8, opart, M, rpm, R)
+        node.unregister_shuffle(8)
+    finally:
+        node.close()
+
+
+def test_exchange_maps_at_world1_without_loopback_is_local(gpu_node):
+    R, M, rpm = 20, 4, 10000
+    opart, part = _terasort(gpu_node, R)
+    gpu_node.register_shuffle(9, M, R, 100)
+    try:
+        _write_windows(gpu_node, 9, part, M, rpm, 2, 2)
+        _check_all_blocks(gpu_node, 9, opart, M, rpm, R)
+    finally:
+        gpu_node.unregister_shuffle(9)
+
+
+def test_exchange_maps_rejects_a_bad_window(gpu_node):
+    gpu_node.register_shuffle(10, 4, 8, 100)
+    try:
+        with pytest.raises(N.SuxError):
+            gpu_node.exchange_maps(10, 3, 2)
+    finally:
+        gpu_node.unregister_shuffle(10)
+
+
+def test_adopt_map_outputs_resolves_in_place(gpu_node):
+    R, rpm, n = 64, 40000, 5 * 40000 + 12345
+    opart, part = _terasort(gpu_node, R)
+    recs = gpu_node.generate(N.GEN_TERASORT, SEED, 0, n, 100)
+    out, index, _ = gpu_node.partition_maps_pipelined(part, recs, 100, rpm, group_records=2 * rpm)
+    M = -(-n // rpm)
+    gpu_node.register_shuffle(11, M, R, 100)
+    try:
+        gpu_node.adopt_map_outputs(11, 0, out, rpm, n, index)
+        blocks = np.stack([np.repeat(np.arange(M), R), np.tile(np.arange(R), M)], 1)
+        addrs, sizes = gpu_node.resolve_blocks(11, blocks)
+        ix = index.cpu().numpy().reshape(M, R + 1)
+        base = out.data_ptr()
+        for i, (m, p) in enumerate(blocks):
+            assert addrs[i] == base + m * rpm * 100 + ix[m, p]
+            assert sizes[i] == ix[m, p + 1] - ix[m, p]
+        # first commit wins: adopting again changes nothing
+        gpu_node.adopt_map_outputs(11, 0, out, rpm, n, index)
+        want = O.write_maps(opart, O.gen_terasort(SEED, 0, n), 100, rpm)
+        assert gpu_node.map_output_index(11, M - 1, R) == \
+            want[2][(M - 1) * (R + 1) * 8:M * (R + 1) * 8]
+        buf, sz = gpu_node.fetch_blocks(11, [(m, 0, R) for m in range(M)])
+        assert buf.to_bytes() == want[0].tobytes()
+        buf.release(M)
+    finally:
+        gpu_node.unregister_shuffle(11)
+
+
+def test_spill_when_the_pool_is_full(tmp_path):
+    """pool capped at 64 MiB, 12 map outputs of 8 MB: the writer spills committed outputs to
+    Spark's files and every block still fetches byte-exact."""
+    node = Node(device=0, pool_limit_mib=64)
+    try:
+        node.set_spill_dir(str(tmp_path))
+        R, M, rpm = 40, 12, 80000
+        opart, part = _terasort(node, R)
+        node.register_shuffle(12, M, R, 100)
+        keep = []
+        for m in range(M):
+            recs = node.generate(N.GEN_TERASORT, SEED, m * rpm, rpm, 100)
+            keep.append(recs)
+            node.write_map_output(12, m, part, recs, rpm)
+        assert node.spills() > 0
+        files = sorted(p.name for p in tmp_path.iterdir())
+        assert "shuffle_12_0_0.data" in files and "shuffle_12_0_0.index" in files
+        # a spilled map is not device-resident: zero-copy resolve refuses it, fetch reads the file
+        with pytest.raises(N.SuxError) as e:
+            node.resolve_blocks(12, [(0, 0)])
+        assert e.value.code == N.SUX_ESTATE
+        _check_all_blocks(node, 12, opart, M, rpm, R, parts=[0, 7, R - 1])
+        node.unregister_shuffle(12)
+        assert not any(p.name.startswith("shuffle_12_") for p in tmp_path.iterdir())
+    finally:
+        node.close()
+
+
+def test_pool_limit_without_spill_dir_fails_cleanly():
+    node = Node(device=0, pool_limit_mib=16)
+    try:
+        R, rpm = 8, 400000  # 40 MB > the 16 MiB cap
+        _, part = _terasort(node, R)
+        node.register_shuffle(13, 1, R, 100)
+        recs = node.generate(N.GEN_TERASORT, SEED, 0, rpm, 100)
+        with pytest.raises(N.SuxError) as e:
+            node.write_map_output(13, 0, part, recs, rpm)
+        assert e.value.code == N.SUX_ENOMEM
+        # the claim was released: the map can be written once memory allows
+        node.unregister_shuffle(13)
+    finally:
+        node.close()
