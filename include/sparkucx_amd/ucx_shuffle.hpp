@@ -11,7 +11,10 @@
 //   UcxShuffleBlockResolver   compat/spark_3_0/UcxShuffleBlockResolver.scala:19-51,
 //                             CommonUcxShuffleBlockResolver.scala:22-126
 //   UcxShuffleWriter          the Spark writer selected at UcxShuffleManager.scala:36-50, on GPU
-//   UcxShuffleReader          compat/spark_3_0/UcxShuffleReader.scala:28-187 (fetch part)
+//   UcxShuffleReader          compat/spark_3_0/UcxShuffleReader.scala:28-187 (fetch part; rows
+//                             of a GPU shuffle decoded by its row layout and, when the
+//                             dependency's key ordering is one the GPU restates, sorted on the
+//                             GPU in place of ExternalSorter :138-154 — the JVM reader's flow)
 //   UcxShuffleClient          reducer/compat/spark_3_0/UcxShuffleClient.java:30-135
 //   ManagedBuffer             the refcounted NioManagedBuffer slices of OnBlocksFetchCallback.java:33-57
 //   BlockFetchingListener     org.apache.spark.network.shuffle.BlockFetchingListener [ext]
@@ -103,6 +106,10 @@ class UcxShuffleConf {
   int device() const { return std::stoi(get(ucx("gpu.device"), "0")); }
   int rank() const { return std::stoi(get(ucx("gpu.rank"), "0")); }
   int worldSize() const { return std::stoi(get(ucx("gpu.worldSize"), "1")); }
+  // device pool cap in MiB (0 = none): past it map outputs spill (HBM-capacity fallback)
+  uint32_t poolLimitMiB() const { return (uint32_t)std::stoul(get(ucx("gpu.poolLimitMiB"), "0")); }
+  // spill directory (spark.local.dir): "" = no spill
+  std::string spillDir() const { return get(ucx("gpu.spillDir"), ""); }
 
   sux_conf toNative() const {
     sux_conf c;
@@ -113,6 +120,7 @@ class UcxShuffleConf {
     c.min_buffer_size = minBufferSize();
     c.min_allocation_size = minRegistrationSize();
     c.metadata_block_size = metadataBlockSize();
+    c.pool_limit_mib = poolLimitMiB();
     check(sux_conf_set_prealloc(&c, preAllocateBuffers().c_str()), "preAllocateBuffers");
     return c;
   }
@@ -124,7 +132,8 @@ class UcxShuffleConf {
         "hist_stage", "s6_chunk", "tiles_per_item", "small_groups", "tile_records", "onepass",
         "varlen_kernel", "varlen_tile", "sort_max_digit_bits", "sort_gather", "sort_all_passes",
         "hist_wgs_per_cu", "small_kernel", "small_waves", "scatter_order",
-        "small_wgs_per_cu", "sort_msd"};
+        "small_wgs_per_cu", "sort_msd", "exchange_self", "hist_nt", "counts_layout",
+        "scatter_counters"};
     sux_tuning t;
     std::memset(&t, 0, sizeof t);
     int32_t* f = reinterpret_cast<int32_t*>(&t);
@@ -147,7 +156,9 @@ class UcxNode {
     if (commId) std::memcpy(c.comm_id, commId, 128);
     sparkucx::check(sux_node_create(&c, isDriver ? 1 : 0, &node_), "UcxNode");
     const sux_tuning t = conf.tuning();
-    const int rc = sux_node_set_tuning(node_, &t);
+    int rc = sux_node_set_tuning(node_, &t);
+    if (rc == SUX_OK && !conf.spillDir().empty())
+      rc = sux_node_set_spill_dir(node_, conf.spillDir().c_str());
     if (rc != SUX_OK) {  // the constructor throws: no destructor will release the node
       char msg[512];
       sux_last_error(msg, sizeof msg);
@@ -218,6 +229,8 @@ class ManagedBuffer {
       : buf_(buf), dev_(dev), size_(size) {}
   const uint8_t* devicePtr() const { return dev_; }
   uint64_t size() const { return size_; }
+  // the pooled buffer this block is a slice of (a GPU consumer of several blocks)
+  sux_buffer* native() const { return buf_; }
   ManagedBuffer& release() {
     if (buf_) check(sux_buffer_release(buf_), "ManagedBuffer.release");
     buf_ = nullptr;
@@ -294,7 +307,15 @@ class UcxShuffleClient {
   std::map<int64_t, int> mapId2PartitionId_;
 };
 
-// UcxShuffleHandle (CommonUcxShuffleManager.scala:99-102) + the dependency's partitioner
+// The row layout a GPU shuffle carries in its handle (the JVM's GpuRowLayout, from the
+// dependency's FixedWidthRowSerializer): fixed-width rows, the key at keyOffset.
+struct GpuRowLayout {
+  int recordSize = 0, keyOffset = 0, keyLen = 0;
+};
+
+// UcxShuffleHandle (CommonUcxShuffleManager.scala:99-102) + the dependency's partitioner, row
+// layout, key ordering (SUX_SORT_* when it is one the GPU restates: the JVM's GpuKeyOrdering;
+// 0 = none or another ordering) and whether it aggregates (an aggregator keeps Spark's path)
 struct UcxShuffleHandle {
   int shuffleId = 0;
   int numMaps = 0;
@@ -302,6 +323,10 @@ struct UcxShuffleHandle {
   int recordSize = 0;
   sux_handle_desc desc{};
   std::shared_ptr<sux_partitioner> partitioner;
+  bool hasLayout = false;
+  GpuRowLayout layout{};
+  int keyOrdering = 0;
+  bool aggregator = false;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -411,6 +436,64 @@ class UcxShuffleReader {
     return out;
   }
 
+  // The records read() hands to the task, as host rows: the fetched blocks in request order, or,
+  // for a GPU shuffle whose key ordering the GPU restates and that has no aggregator, those rows
+  // sorted by key on the GPU (sux_sort_records over the one pooled fetch buffer; stable, so
+  // equal keys keep the map order — the JVM reader's gpuSorted).  Throws on a fetch failure
+  // (Spark's FetchFailedException).
+  std::vector<uint8_t> readRows(void* stream = nullptr, bool* sortedOnGpu = nullptr) {
+    Fetched f = read(stream);
+    if (!f.failures.empty()) {
+      for (auto& b : f.blocks) b.second.release();
+      throw UcxException(SUX_ENOENT, "fetch of " + f.failures[0].first + " failed: " +
+                                         f.failures[0].second);
+    }
+    uint64_t total = 0;
+    for (auto& b : f.blocks) total += b.second.size();
+    std::vector<uint8_t> rows(total);
+    const bool gpuSort = h_.hasLayout && h_.keyOrdering != 0 && !h_.aggregator &&
+                         !f.blocks.empty() && total % (uint64_t)h_.layout.recordSize == 0;
+    if (sortedOnGpu) *sortedOnGpu = gpuSort && total > 0;
+    if (gpuSort && total > 0) {
+      const uint64_t rs = (uint64_t)h_.layout.recordSize, n = total / rs;
+      sux_node* nd = node_.native();
+      uint64_t wsb = 0;
+      check(sux_sort_workspace_size(n, (uint32_t)rs, &wsb), "sort workspace");
+      sux_buffer *out = nullptr, *ws = nullptr;
+      check(sux_buffer_alloc(nd, total, &out), "sort output");
+      try {
+        check(sux_buffer_alloc(nd, wsb, &ws), "sort workspace");
+        void *dst = nullptr, *w = nullptr;
+        check(sux_buffer_info(out, &dst, nullptr, nullptr), "sux_buffer_info");
+        check(sux_buffer_info(ws, &w, nullptr, nullptr), "sux_buffer_info");
+        // every block is a slice of one pooled buffer, in request order: sort it where it lies
+        check(sux_sort_records(nd, h_.keyOrdering, f.blocks[0].second.devicePtr(), n, (uint32_t)rs,
+                               h_.layout.keyOffset, h_.layout.keyLen, dst, w, wsb, stream),
+              "sortRecords");
+        check(sux_buffer_read(out, 0, rows.data(), total, stream), "sorted rows");  // waits
+      } catch (...) {
+        if (ws) sux_buffer_release(ws);
+        sux_buffer_release(out);
+        for (auto& b : f.blocks) b.second.release();
+        throw;
+      }
+      sux_buffer_release(ws);
+      sux_buffer_release(out);
+    } else {
+      uint64_t off = 0;
+      for (auto& b : f.blocks) {
+        if (b.second.size())
+          check(sux_buffer_read(b.second.native(),
+                                (uint64_t)(b.second.devicePtr() - f.blocks[0].second.devicePtr()),
+                                rows.data() + off, b.second.size(), stream),
+                "block rows");
+        off += b.second.size();
+      }
+    }
+    for (auto& b : f.blocks) b.second.release();
+    return rows;
+  }
+
  private:
   UcxNode& node_;
   UcxShuffleHandle h_;
@@ -439,6 +522,20 @@ class UcxShuffleManager {
 
   // registerShuffle (:25-30) -> registerShuffleCommon (:39-56).  The directory is sized by the
   // number of map tasks (fixes quirk Q1: the reference sizes it by partitioner.numPartitions).
+  // A GPU shuffle: the dependency's serializer gives the row layout (FixedWidthRowSerializer),
+  // its keyOrdering the sort kind (GpuKeyOrdering, or 0), its aggregator whether Spark combines.
+  UcxShuffleHandle registerShuffle(int shuffleId, int numMaps, const sux_partitioner_desc& partitioner,
+                                   const GpuRowLayout& layout, int keyOrdering, bool aggregator) {
+    UcxShuffleHandle h = registerShuffle(shuffleId, numMaps, partitioner, layout.recordSize);
+    h.hasLayout = true;
+    h.layout = layout;
+    h.keyOrdering = keyOrdering;
+    h.aggregator = aggregator;
+    std::lock_guard<std::mutex> lk(mu_);
+    handles_[shuffleId] = h;
+    return h;
+  }
+
   UcxShuffleHandle registerShuffle(int shuffleId, int numMaps, const sux_partitioner_desc& partitioner,
                                    int recordSize) {
     startUcxNodeIfMissing();
@@ -476,6 +573,16 @@ class UcxShuffleManager {
   void exchange(int shuffleId, void* stream = nullptr) {
     requireNode();
     check(sux_exchange(node_->native(), shuffleId, stream), "exchange");
+  }
+  // The JVM coordinator's two messages: a window of committed map tasks (asynchronous on
+  // `stream`), then the completion every reduce task waits for.
+  void exchangeWindow(int shuffleId, int firstMap, int numMaps, void* stream = nullptr) {
+    requireNode();
+    check(sux_exchange_maps(node_->native(), shuffleId, firstMap, numMaps, stream), "exchangeMaps");
+  }
+  void exchangeDone(int shuffleId) {
+    requireNode();
+    check(sux_exchange_wait(node_->native(), shuffleId), "exchangeWait");
   }
 
   // unregisterShuffle (:73-77)

@@ -61,6 +61,10 @@ void nccl_check(ncclResult_t r, const char* what) {
 
 template <class F>
 int guard(F&& f) {
+  // the HIP runtime's per-thread last error is shared with every other library in the process
+  // (RCCL, torch): a stale one would be taken for a failed launch of ours (hipGetLastError after
+  // each launch), so every entry point starts clean
+  (void)hipGetLastError();
   try {
     f();
     return SUX_OK;
@@ -516,6 +520,38 @@ void publish_slot(sux_node* n, Shuffle& sh, int32_t m, uint64_t index_addr) {
   store_be64(d + 24, s.bytes);
 }
 
+// The device error word after a job's kernels completed: a bounded in-kernel wait that timed out
+// (the turn-taking small-record scatter, sux::kErrTurnTimeout) stopped without writing all of its
+// records.  Returns the word and clears it.
+uint32_t take_device_err(sux_node* node) {
+  uint32_t w = 0;
+  hip_check(hipMemcpy(&w, node->d_err, sizeof w, hipMemcpyDeviceToHost), "read error word");
+  if (w) hip_check(hipMemset(node->d_err, 0, sizeof w), "clear error word");
+  return w;
+}
+
+// Jobs whose kernels reported a device error: their maps are not published (the writes may be
+// retried, as after a failed launch); the pool buffers go back.  Called with the node lock held.
+[[noreturn]] void reject_jobs(sux_node* node, Shuffle& sh, std::vector<std::unique_ptr<WriteJob>>& jobs,
+                              uint32_t w) {
+  std::string maps;
+  for (auto& j : jobs) {
+    if (!j) continue;
+    for (uint32_t k = 0; k < j->maps; ++k)
+      if (j->claimed[k]) sh.maps[j->first + k].pending = false;
+    maps += " [" + std::to_string(j->first) + ", " + std::to_string(j->first + (int32_t)j->maps) + ")";
+    node->pool->put(j->ws);
+    node->hpool.put(j->hidx);
+    j.reset();
+  }
+  node->cv.notify_all();
+  char b[16];
+  std::snprintf(b, sizeof b, "%x", w);
+  raise(SUX_EHIP, std::string("device error word 0x") + b +
+                      ": a kernel stopped before writing all records; map outputs of maps" + maps +
+                      " were not published");
+}
+
 // A completed write job's maps get their slots: index tables from the pinned read-back, the
 // data location (map-major offset, or per-peer segments of a peer-major slab) and the batch.
 void publish_job(sux_node* node, Shuffle& sh, WriteJob& j) {
@@ -581,8 +617,19 @@ void progress(sux_node* node, Shuffle& sh, std::unique_lock<std::mutex>& lk, boo
       if (e == hipSuccess) done[i] = 1;
       else if (e != hipErrorNotReady) err = e;
     }
+    uint32_t derr = 0;
+    if (err == hipSuccess && std::find(done.begin(), done.end(), 1) != done.end())
+      derr = take_device_err(node);
     lk.lock();
     sh.busy -= (int)jobs.size();
+    if (derr) {
+      std::vector<std::unique_ptr<WriteJob>> bad;
+      for (size_t i = 0; i < jobs.size(); ++i) {
+        if (done[i]) bad.push_back(std::move(jobs[i]));
+        else sh.jobs.push_back(std::move(jobs[i]));
+      }
+      reject_jobs(node, sh, bad, derr);
+    }
     for (size_t i = 0; i < jobs.size(); ++i) {
       if (!done[i]) {
         sh.jobs.push_back(std::move(jobs[i]));
@@ -615,8 +662,10 @@ void drain_range(sux_node* node, Shuffle& sh, std::unique_lock<std::mutex>& lk, 
         const hipError_t e = hipEventSynchronize(j->done->e);
         if (e != hipSuccess && err == hipSuccess) err = e;
       }
+      const uint32_t derr = err == hipSuccess ? take_device_err(node) : 0u;
       lk.lock();
       sh.busy -= (int)mine.size();
+      if (derr) reject_jobs(node, sh, mine, derr);
       for (auto& j : mine) publish_job(node, sh, *j);
       node->cv.notify_all();
       hip_check(err, "map output completion");
@@ -686,6 +735,9 @@ sux::Tuning resolve_tuning(const sux_tuning& t, bool pipelined) {
   if (t.small_waves) r.small_waves = t.small_waves;
   r.scatter_order = t.scatter_order;
   if (t.small_wgs_per_cu) r.small_wgs_per_cu = t.small_wgs_per_cu;
+  r.hist_nt = t.hist_nt > 0;
+  r.counts_tm = t.counts_layout != 1;
+  if (t.scatter_counters) r.scatter_counters = t.scatter_counters;
   return r;
 }
 
@@ -947,6 +999,9 @@ int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
             "sort_all_passes must be 0 or 1");
     require(t->exchange_self >= -1 && t->exchange_self <= 1, SUX_EINVAL,
             "exchange_self must be -1, 0 or 1");
+    require(t->hist_nt >= -1 && t->hist_nt <= 1, SUX_EINVAL, "hist_nt must be -1, 0 or 1");
+    require(in(t->counts_layout, {1, 2}), SUX_EINVAL, "counts_layout must be 1 or 2");
+    require(in(t->scatter_counters, {1, 2}), SUX_EINVAL, "scatter_counters must be 1 or 2");
     for (int32_t r : t->reserved) require(r == 0, SUX_EINVAL, "reserved tuning fields must be 0");
     require(node, SUX_EINVAL, "NULL node");
     std::lock_guard<std::mutex> lk(node->mu);
@@ -3166,10 +3221,13 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
   hip_check(hipStreamIsCapturing(s, &cap), "hipStreamIsCapturing");
   const bool run_all = all_passes || cap != hipStreamCaptureStatusNone;
   uint32_t span[6] = {0, 0, 0, ~0u, ~0u, ~0u};  // AND = 0, OR = ~0: every bit varies
-  // the read-backs land in pinned staging (a true async copy, not a pageable bounce)
-  HostLease hrb(node->hpool, 64);
-  uint8_t* hrd = static_cast<uint8_t*>(hrb.b.first);
+  // the read-backs land in pinned staging (a true async copy, not a pageable bounce); only a call
+  // that reads back takes it: under graph capture a cold pool would hipHostMalloc mid-capture
+  std::unique_ptr<HostLease> hrb;
+  uint8_t* hrd = nullptr;
   if (!run_all) {
+    hrb = std::make_unique<HostLease>(node->hpool, 64);
+    hrd = static_cast<uint8_t*>(hrb->b.first);
     hip_check(hipMemcpyAsync(hrd, ws + P.span_off, sizeof span, hipMemcpyDeviceToHost, s),
               "sort key span");
     hip_check(hipStreamSynchronize(s), "sort key span");
@@ -3186,7 +3244,11 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
   // records 1.53 vs 1.69 ms), the sorted-chunk one for long ones (32 Mi int64 rows 2.55 vs
   // 2.67 ms; profiles/r02_v14/sort_ab.txt) unless the node's tuning names one
   sux::Tuning sort_tn = resolve_tuning(node->tuning, false);
-  if (node->tuning.small_kernel == 0) sort_tn.small_kernel = n <= (8ull << 20) ? 1 : 2;
+  // the sort's digit passes use the turn-free sorted-chunk scatter: the turn-taking one (10 %
+  // faster on the LSD passes of a 5 M-record sort, profiles/r02_v14/sort_ab.txt) can time out
+  // into the device error word, and the sort returns before its kernels run — nothing would
+  // read it (the MSD finish takes common key sets off the LSD path anyway)
+  if (node->tuning.small_kernel == 0) sort_tn.small_kernel = 2;
   // MSD finish: one stable digit pass over the top tb varying bits, then every bucket sorted in
   // LDS by the lower varying digits (k_sort_local) — each pair crosses HBM twice after the top
   // pass instead of twice per digit.  Needs the key span (not under graph capture) and buckets

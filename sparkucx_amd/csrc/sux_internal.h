@@ -55,6 +55,9 @@ struct Tuning {
   bool onepass = false;     // the one-pass kernel when a map batch fits on chip
   int varlen_kernel = 3;    // variable-length rows: 1 | 2 | 3 (line image; default: 1055 vs 840 GB/s)
   int varlen_tile = 0;      // variable-length K1 tile override
+  bool hist_nt = false;     // k_hist4: non-temporal (streaming) record loads
+  bool counts_tm = true;    // k_hist4 + k_scatter7/8: tile-major counts (MapGroup::counts_tm)
+  int scatter_counters = 2; // k_scatter8 per-wave counters: 1 partition-major, 2 wave-major
 };
 
 // Per-launch geometry of a group of consecutive map batches.
@@ -67,6 +70,10 @@ struct MapGroup {
   uint32_t tile_recs;      // records per tile (one wave's work in hist/scatter)
   uint32_t tiles_per_map;  // ceil(records_per_map / tile_recs)
   uint32_t* err;           // the node's device error word (kErr* bits), or nullptr
+  // K1 -> K2 -> K3 tile counts layout: 0 partition-major [map][p][tile] (a row per (map, p) for
+  // the scan), 1 tile-major [map][tile][p] (k_hist4 with k_scatter7/8: each tile's R counters
+  // are one contiguous store instead of R scattered 4-byte writes)
+  uint32_t counts_tm;
 };
 // Device error word bits (sux_node_check turns a set word into SUX_EHIP).
 constexpr uint32_t kErrTurnTimeout = 1u;  // k_scatter16/16b: a wave waited 2^22 sleeps for its turn

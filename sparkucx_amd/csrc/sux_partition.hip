@@ -635,7 +635,7 @@ struct Hs4 {
   }
 };
 
-template <uint32_t S, uint32_t CH, int KW, bool TAB>
+template <uint32_t S, uint32_t CH, int KW, bool TAB, bool NTL>
 __global__ __launch_bounds__(256) void k_hist4(PartDev pd, MapGroup g, uint16_t* __restrict__ pids,
                                                uint32_t* __restrict__ counts) {
   using H = Hs4<S, CH>;
@@ -670,7 +670,11 @@ __global__ __launch_bounds__(256) void k_hist4(PartDev pd, MapGroup g, uint16_t*
     const u32x4* src = reinterpret_cast<const u32x4*>(a - head);
     const uint32_t units = (head + n * S + 15) >> 4;
 #pragma unroll
-    for (uint32_t k = 0; k < PER; ++k) v[k] = src[min(lane + k * kWave, units - 1)];
+    for (uint32_t k = 0; k < PER; ++k) {
+      const u32x4* a4 = src + min(lane + k * kWave, units - 1);
+      // NTL: the records are streamed once here (K3 reads them again long after they left L2)
+      v[k] = NTL ? __builtin_nontemporal_load(a4) : *a4;
+    }
   };
   // chunk c0 (held in v) -> stage -> keys -> pids + histogram; if `next` v is refilled with
   // the chunk at c0 + 2CH.  Every lane stores a pid (lanes past the chunk's end repeat the last
@@ -728,11 +732,15 @@ __global__ __launch_bounds__(256) void k_hist4(PartDev pd, MapGroup g, uint16_t*
       if (nch > 1) step(wb + CH, vb, false);
       if (nch > 2) step(wb + 2 * CH, va, false);
     }
-    // an empty tile (the tail of a short last map) still publishes its zero counts
+    // an empty tile (the tail of a short last map) still publishes its zero counts; tile-major
+    // counts are one contiguous 4R-byte store per tile, partition-major ones R strided dwords
     __syncthreads();
-    uint32_t* dst = counts + ((uint64_t)tr.map * R) * g.tiles_per_map + tr.tile;
+    const bool tm = g.counts_tm != 0;
+    uint32_t* dst = tm ? counts + ((uint64_t)tr.map * g.tiles_per_map + tr.tile) * R
+                       : counts + ((uint64_t)tr.map * R) * g.tiles_per_map + tr.tile;
+    const uint64_t stride = tm ? 1 : g.tiles_per_map;
     for (int p = threadIdx.x; p < R; p += 256) {
-      dst[(uint64_t)p * g.tiles_per_map] =
+      dst[(uint64_t)p * stride] =
           hist_all[p] + hist_all[R + p] + hist_all[2 * R + p] + hist_all[3 * R + p];
       hist_all[p] = hist_all[R + p] = hist_all[2 * R + p] = hist_all[3 * R + p] = 0;
     }
@@ -1108,7 +1116,8 @@ __global__ __launch_bounds__(NW * 64) void k_scatter7(MapGroup g, int R, int pid
   auto begin_item = [&](const Item& x) {
     if (owner) {
       pos = (base[(uint64_t)x.map * R + tid] +
-             prefix[(uint64_t)x.map * R * g.tiles_per_map + (uint64_t)tid * g.tiles_per_map + x.t0]) * S;
+             prefix[g.counts_tm ? ((uint64_t)x.map * g.tiles_per_map + x.t0) * R + tid
+                                : (uint64_t)x.map * R * g.tiles_per_map + (uint64_t)tid * g.tiles_per_map + x.t0]) * S;
       first = (uint32_t)(pos & 15) >> 2;
       carry[tid] = u32x4{0, 0, 0, 0};
     }
@@ -1386,7 +1395,7 @@ struct Sc8 {
   static __host__ __device__ constexpr uint32_t space(int R) {
     return (C * S) / 16 + (17u * R + 1) / 2 + 1;
   }
-  // img[SP] u32x4 | pinfo[R] u32x4 | recoff[C] | wcnt[R][NW] | lunit[R] | fhead[R] | lpos[R]
+  // img[SP] u32x4 | pinfo[R] u32x4 | recoff[C] | wcnt[NW][R] | lunit[R] | fhead[R] | lpos[R]
   // | tmp[NW + 1] | upid[SP] u8
   static __host__ __device__ constexpr uint32_t lds_bytes(int R) {
     return space(R) * 16 + (uint32_t)R * 16 + C * 4 + NW * (uint32_t)R * 4 + 3u * R * 4 +
@@ -1397,7 +1406,7 @@ struct Sc8 {
   }
 };
 
-template <uint32_t S, uint32_t C, uint32_t NW>
+template <uint32_t S, uint32_t C, uint32_t NW, bool WM>
 __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid_bits,
                                                      const uint16_t* __restrict__ pids,
                                                      const uint32_t* __restrict__ prefix,
@@ -1412,7 +1421,12 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
   uint32_t* img32 = reinterpret_cast<uint32_t*>(lds8);
   u32x4* pinfo = img + SP;  // {lb, cd, full lines, sp}
   uint32_t* recoff = reinterpret_cast<uint32_t*>(pinfo + R);
-  uint32_t* wcnt = recoff + C;  // [R][NW]
+  // per-wave counters, wave-major [NW][R]: a wave's lanes touch R different words of one row
+  // (partition-major [R][NW] put every pid of a wave on 64 / NW banks: 41 % of the LDS cycles
+  // were bank conflicts, profiles/pmc_r02.json)
+  uint32_t* wcnt = recoff + C;
+  // counter of (partition p, wave w): wave-major (WM) or round 2's partition-major [R][NW]
+  auto WC = [&](uint32_t p, uint32_t w) -> uint32_t& { return WM ? wcnt[w * R + p] : wcnt[p * NW + w]; };
   uint32_t* lunit = wcnt + NW * R;  // unit index of the line holding p's cursor
   uint32_t* fhead = lunit + R;      // dwords of that line that belong to another range
   uint32_t* lpos = fhead + R;       // p's cursor in dwords (flush at an item end)
@@ -1478,7 +1492,8 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
   auto begin_item = [&](const Item& x) {
     if (owner) {
       pos = (base[(uint64_t)x.map * R + tid] +
-             prefix[(uint64_t)x.map * R * g.tiles_per_map + (uint64_t)tid * g.tiles_per_map + x.t0]) * S;
+             prefix[g.counts_tm ? ((uint64_t)x.map * g.tiles_per_map + x.t0) * R + tid
+                                : (uint64_t)x.map * R * g.tiles_per_map + (uint64_t)tid * g.tiles_per_map + x.t0]) * S;
       fhead[tid] = (uint32_t)(pos & 127) >> 2;  // the line's earlier dwords: another range's
     }
   };
@@ -1537,8 +1552,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
 
   if (owner) {
 #pragma unroll
-    for (uint32_t w = 0; w < NW; w += 4)
-      reinterpret_cast<u32x4*>(wcnt + tid * NW)[w / 4] = u32x4{0, 0, 0, 0};
+    for (uint32_t w = 0; w < NW; ++w) WC(tid, w) = 0;
   }
   u32x4 cu0{0, 0, 0, 0}, cu1{0, 0, 0, 0};  // carrier: units 2cj, 2cj+1 of p's carried line
   // (block-cyclic) the first non-empty block
@@ -1571,7 +1585,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
         const uint64_t m = __ballot(bit);
         peers &= bit ? m : ~m;
       }
-      uint32_t* wc = wcnt + pid * NW + wave;
+      uint32_t* wc = &WC(pid, wave);
       uint32_t r0 = 0;
       if (valid) r0 = *wc;
       __builtin_amdgcn_wave_barrier();
@@ -1585,19 +1599,13 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
     // 2. owners: prefix over waves, region = the cursor's line from its start + c records
     uint32_t c = 0, full = 0, sp = 0;
     if (owner) {
-      u32x4* row = reinterpret_cast<u32x4*>(wcnt + tid * NW);
-      u32x4 x[NW / 4];
+      uint32_t x[NW];
 #pragma unroll
-      for (uint32_t q = 0; q < NW / 4; ++q) x[q] = row[q];
+      for (uint32_t w = 0; w < NW; ++w) x[w] = WC(tid, w);
 #pragma unroll
-      for (uint32_t q = 0; q < NW / 4; ++q) {
-        u32x4 y;
-        y[0] = c;
-        y[1] = c + x[q][0];
-        y[2] = y[1] + x[q][1];
-        y[3] = y[2] + x[q][2];
-        c = y[3] + x[q][3];
-        row[q] = y;
+      for (uint32_t w = 0; w < NW; ++w) {
+        WC(tid, w) = c;
+        c += x[w];
       }
       const uint32_t cd = (uint32_t)(pos & 127) >> 2;
       const uint32_t tot = cd + c * W;
@@ -1642,7 +1650,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
       const uint32_t p = my_pid[j];
       if (p == 0xFFFFFFFFu) continue;
       const u32x4 pi = pinfo[p];
-      const uint32_t jr = wcnt[p * NW + wave] + my_rank[j];
+      const uint32_t jr = WC(p, wave) + my_rank[j];
       recoff[wave * RPW + j * kWave + lane] = 16 * pi[0] + 4 * pi[1] + jr * S;
       const uint32_t d0 = pi[1] + jr * W;  // the record's first dword in the region
       const uint32_t k0 = (d0 + 3) >> 2, k1 = (d0 + W + 3) >> 2;
@@ -1709,8 +1717,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
       pos += (uint64_t)c * S;
       lpos[tid] = (uint32_t)(pos >> 2);
 #pragma unroll
-      for (uint32_t w = 0; w < NW; w += 4)
-        reinterpret_cast<u32x4*>(wcnt + tid * NW)[w / 4] = u32x4{0, 0, 0, 0};
+      for (uint32_t w = 0; w < NW; ++w) WC(tid, w) = 0;
     }
     if (seam) {
       __syncthreads();
@@ -3183,11 +3190,13 @@ static bool msd16_eligible(const PartDev& pd, const MapGroup& g, const LayoutDes
          (uint64_t)g.num_maps * nbk * 8 <= ws.totals_bytes;
 }
 
-hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const LayoutDesc& lay,
+hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g_in, const LayoutDesc& lay,
                                   uint8_t* d_out, int64_t* d_index, uint8_t* d_index_be,
                                   uint16_t* d_pids, uint8_t* d_ws, const Workspace& ws,
                                   uint64_t* d_peer_bytes, const Tuning& tn, Timer* timer,
                                   hipStream_t s) {
+  MapGroup g = g_in;  // counts_tm is decided below, with the K1 / K3 pair
+  g.counts_tm = 0;
   const int R = pd.R;
   const uint32_t S = g.rec_size;
   // persistent grids are sized to the CUs the stream may use (a CU-masked stream at N > 1):
@@ -3282,12 +3291,35 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   const dim3 grid1((total_tiles + wpg - 1) / wpg), grid4((total_tiles + 3) / 4);
   const size_t lds1 = (size_t)wpg * R * 4;
 
+  const int sv = tn.scatter_kernel;
+  const int s6c = tn.s6_chunk;
+  const int s6tpw = tn.tiles_per_item;
+  size_t lds6 = 0;
+  int c6 = 0;
+  if (sv >= 6 && S == 100 && (reinterpret_cast<uintptr_t>(d_out) & 15) == 0 &&
+      g.num_records * S < kImageMaxBytes) {
+    for (int c : {1024, 512, 384, 256}) {
+      if (c > s6c) continue;
+      const size_t b = c == 1024 ? Sc6<100, 1024, 16>::lds_bytes(R)
+                     : c == 512  ? Sc6<100, 512, 8>::lds_bytes(R)
+                     : c == 384  ? Sc6<100, 384, 6>::lds_bytes(R)
+                                 : Sc6<100, 256, 4>::lds_bytes(R);
+      if (b <= 160 * 1024) {
+        c6 = c;
+        lds6 = b;
+        break;
+      }
+    }
+  }
+  const bool v8 = c6 == 1024 && sv >= 8 && tn.scatter_chunk == 1024 &&
+                  Sc8<100, 1024, 16>::fits(R);
+  const bool v7 = !v8 && c6 == 1024 && sv >= 7 && R <= 512 &&
+                  Sc7<100, 1024, 16>::lds_bytes(R) <= 160 * 1024;
   // ---- K1: pids + tile histograms
   const int hv = tn.hist_kernel;
   const bool shaped = (S == 100 || S == 16) && R <= 4096;  // v2 instantiations
   const bool words = pd.kind != 4 && pd.key_offset % 4 == 0 && pd.key_len <= 16;
   // small records with many partitions: k_hist16 + tile-major counts + k_scatter16, together
-  const int sv = tn.scatter_kernel;
   const bool s16 = hv >= 4 && sv >= 7 && words && S == 16 && R > 1024 &&
                    (reinterpret_cast<uintptr_t>(g.recs) & 15) == 0 &&
                    (reinterpret_cast<uintptr_t>(d_out) & 15) == 0;
@@ -3296,6 +3328,9 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   else if (hv >= 4 && words && R <= 4096 && S == 100 && (pd.key_offset + pd.key_len) <= (int)S) hist = 4;
   else if (hv >= 3 && words && R <= 4096) hist = 3;
   else if (hv >= 2 && shaped) hist = 2;
+  // k_hist4 feeding k_scatter7/8: tile-major counts (one contiguous store per tile; k_hist4 with
+  // strided counts wrote ~2 B per record in partial-line dword stores, profiles/pmc_r02.json)
+  g.counts_tm = (hist == 4 && (v8 || v7) && tn.counts_tm) ? 1u : 0u;
   timer_note(timer, kHist, hist == 16 ? "k_hist16" : hist == 4 ? "k_hist4" : hist == 3 ? "k_hist3"
                           : hist == 2 ? "k_hist2" : "k_hist");
   timer_begin(timer, kHist, s);
@@ -3325,14 +3360,18 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
     uint32_t per_cu = std::max<uint32_t>(1, (160u * 1024) / (uint32_t)lds);                        \
     if (tn.hist_wgs_per_cu > 0) per_cu = std::min<uint32_t>(per_cu, (uint32_t)tn.hist_wgs_per_cu); \
     const dim3 gridp(std::min<uint32_t>(total_tiles, ncu * per_cu));                              \
-    if (tab) {                                                                                     \
-      allow_lds(reinterpret_cast<const void*>(&k_hist4<100, CHV, KW, true>), lds);                \
-      hipLaunchKernelGGL((k_hist4<100, CHV, KW, true>), gridp, dim3(256), lds, s, pd, g, pids,     \
-                         counts);                                                                  \
+    if (tab && tn.hist_nt) {                                                                       \
+      allow_lds(reinterpret_cast<const void*>(&k_hist4<100, CHV, KW, true, true>), lds);          \
+      hipLaunchKernelGGL((k_hist4<100, CHV, KW, true, true>), gridp, dim3(256), lds, s, pd, g,     \
+                         pids, counts);                                                            \
+    } else if (tab) {                                                                              \
+      allow_lds(reinterpret_cast<const void*>(&k_hist4<100, CHV, KW, true, false>), lds);         \
+      hipLaunchKernelGGL((k_hist4<100, CHV, KW, true, false>), gridp, dim3(256), lds, s, pd, g,    \
+                         pids, counts);                                                            \
     } else {                                                                                       \
-      allow_lds(reinterpret_cast<const void*>(&k_hist4<100, CHV, KW, false>), lds);               \
-      hipLaunchKernelGGL((k_hist4<100, CHV, KW, false>), gridp, dim3(256), lds, s, pd, g, pids,    \
-                         counts);                                                                  \
+      allow_lds(reinterpret_cast<const void*>(&k_hist4<100, CHV, KW, false, false>), lds);        \
+      hipLaunchKernelGGL((k_hist4<100, CHV, KW, false, false>), gridp, dim3(256), lds, s, pd, g,   \
+                         pids, counts);                                                            \
     }                                                                                              \
   } while (0)
 #define SUX_H4K(CHV)                 \
@@ -3381,7 +3420,7 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   // ---- K2: scans -> index tables + destination bases
   timer_begin(timer, kScan, s);
   const uint32_t rows = g.num_maps * (uint32_t)R;
-  if (s16)
+  if (s16 || g.counts_tm)
     hipLaunchKernelGGL(k_tile_scan_tm, dim3(g.num_maps * ((R + 15) / 16)), dim3(256), 0, s, counts,
                        totals, g.num_maps, (uint32_t)R, g.tiles_per_map);
   else if (g.tiles_per_map <= 64)
@@ -3411,29 +3450,6 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
   // tuning (Tuning): s6_chunk caps the v6 chunk, tiles_per_item sets the v6/v7 work item,
   // scatter_chunk/scatter_depth pick the v7 shape (768-record chunks leave room for a K1
   // workgroup on the CU: the co-resident pipeline)
-  const int s6c = tn.s6_chunk;
-  const int s6tpw = tn.tiles_per_item;
-  size_t lds6 = 0;
-  int c6 = 0;
-  if (sv >= 6 && S == 100 && (reinterpret_cast<uintptr_t>(d_out) & 15) == 0 &&
-      g.num_records * S < kImageMaxBytes) {
-    for (int c : {1024, 512, 384, 256}) {
-      if (c > s6c) continue;
-      const size_t b = c == 1024 ? Sc6<100, 1024, 16>::lds_bytes(R)
-                     : c == 512  ? Sc6<100, 512, 8>::lds_bytes(R)
-                     : c == 384  ? Sc6<100, 384, 6>::lds_bytes(R)
-                                 : Sc6<100, 256, 4>::lds_bytes(R);
-      if (b <= 160 * 1024) {
-        c6 = c;
-        lds6 = b;
-        break;
-      }
-    }
-  }
-  const bool v8 = c6 == 1024 && sv >= 8 && tn.scatter_chunk == 1024 &&
-                  Sc8<100, 1024, 16>::fits(R);
-  const bool v7 = !v8 && c6 == 1024 && sv >= 7 && R <= 512 &&
-                  Sc7<100, 1024, 16>::lds_bytes(R) <= 160 * 1024;
   timer_begin(timer, kScatter, s);
   const bool two16 = s16 && small_two_pass_shape((uint32_t)R, S) && tn.small_kernel == 3 &&
                      ws.tmp_bytes >= g.num_records * 16;
@@ -3503,7 +3519,9 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
     // one contiguous, balanced tile range per workgroup (k_scatter8), one workgroup per CU
     const dim3 grid(std::min<uint32_t>(g.num_maps * g.tiles_per_map, ncu));
     const size_t lds8b = Sc8<100, 1024, 16>::lds_bytes(R);
-    allow_lds(reinterpret_cast<const void*>(&k_scatter8<100, 1024, 16>), lds8b);
+    const bool wm = tn.scatter_counters != 1;
+    allow_lds(reinterpret_cast<const void*>(&k_scatter8<100, 1024, 16, true>), lds8b);
+    allow_lds(reinterpret_cast<const void*>(&k_scatter8<100, 1024, 16, false>), lds8b);
     // tile order: contiguous ranges (default; scatter_order 1) or block-cyclic inside an XCD's
     // workgroups (2: 2^27-record maps 49.7 -> 50.3 ms, 2^20 42.9 -> 46.3, profiles/r02_m27_b)
     const uint32_t tiles_per_wg = (g.num_maps * g.tiles_per_map + grid.x - 1) / grid.x;
@@ -3520,8 +3538,12 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
     for (uint32_t w = 0; w < nwin; ++w) {
       const uint32_t tw0 = (uint32_t)((uint64_t)T * w / nwin), tw1 = (uint32_t)((uint64_t)T * (w + 1) / nwin);
       const dim3 gw(std::min<uint32_t>(tw1 - tw0, ncu));
-      hipLaunchKernelGGL((k_scatter8<100, 1024, 16>), gw, dim3(1024), lds8b, s, g, R, bits, pids,
-                         counts, base, d_out, cyc ? per_xcd : 0u, tw0, tw1);
+      if (wm)
+        hipLaunchKernelGGL((k_scatter8<100, 1024, 16, true>), gw, dim3(1024), lds8b, s, g, R, bits,
+                           pids, counts, base, d_out, cyc ? per_xcd : 0u, tw0, tw1);
+      else
+        hipLaunchKernelGGL((k_scatter8<100, 1024, 16, false>), gw, dim3(1024), lds8b, s, g, R, bits,
+                           pids, counts, base, d_out, cyc ? per_xcd : 0u, tw0, tw1);
     }
     e = hipGetLastError();
   } else if (v7) {

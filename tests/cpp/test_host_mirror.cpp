@@ -4,6 +4,7 @@
 // getReader(...).read / UcxShuffleClient.fetchBlocks -> listener callbacks -> release.
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -183,6 +184,57 @@ int main() {
     EXPECT(r0.read().failures.size() == 1, "uncommitted map must fail");
     EXPECT(manager.unregisterShuffle(8), "unregister");
     EXPECT(!manager.unregisterShuffle(8), "second unregister is false");
+  }
+
+  // the JVM flow of a GPU shuffle: the handle carries the row layout (100-byte rows, 10-byte key)
+  // and an unsigned-bytes key ordering; map tasks write -> the coordinator's exchange window +
+  // completion -> the reader decodes rows and sorts them on the GPU (ExternalSorter's step)
+  {
+    UcxShuffleHandle h3 = manager.registerShuffle(9, M, pdesc, GpuRowLayout{S, 0, 10}, SUX_SORT_BYTES,
+                                                  /*aggregator=*/false);
+    std::map<int64_t, int> ids3;
+    uint64_t f3 = 0;
+    for (int i = 0; i < M; ++i) {
+      void* dev = nullptr;
+      HIP_OK(hipMalloc(&dev, in[i].size()));
+      HIP_OK(hipMemcpy(dev, in[i].data(), in[i].size(), hipMemcpyHostToDevice));
+      manager.getWriter(h3, 300 + i, i).write(dev, counts[i]);
+      HIP_OK(hipFree(dev));
+      ids3[300 + i] = i;
+      f3 += counts[i];
+    }
+    manager.exchangeWindow(9, 0, M);
+    manager.exchangeDone(9);
+    for (auto range : {std::make_pair(10, 23), std::make_pair(0, R), std::make_pair(49, 50)}) {
+      bool gpu = false;
+      auto rows = manager.getReader(h3, range.first, range.second, ids3).readRows(nullptr, &gpu);
+      // expected: the canonical map-ordered concatenation of the blocks, stably sorted by key
+      std::vector<uint8_t> cat;
+      for (int m = 0; m < M; ++m)
+        cat.insert(cat.end(), want_data[m].begin() + want_idx[m][range.first],
+                   want_data[m].begin() + want_idx[m][range.second]);
+      std::vector<uint32_t> order(cat.size() / S);
+      for (uint32_t k = 0; k < order.size(); ++k) order[k] = k;
+      std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+        return std::memcmp(&cat[(size_t)a * S], &cat[(size_t)b * S], 10) < 0;
+      });
+      std::vector<uint8_t> want(cat.size());
+      for (size_t k = 0; k < order.size(); ++k)
+        std::memcpy(&want[k * S], &cat[(size_t)order[k] * S], S);
+      EXPECT(gpu, "rows of [%d, %d) sorted on the GPU", range.first, range.second);
+      EXPECT(rows == want, "GPU-sorted rows of [%d, %d) equal the stable key sort",
+             range.first, range.second);
+    }
+    // an aggregating dependency keeps Spark's path: the rows come back in fetch order
+    UcxShuffleHandle h4 = h3;
+    h4.aggregator = true;
+    bool gpu = true;
+    auto rows = manager.getReader(h4, 5, 6, ids3).readRows(nullptr, &gpu);
+    std::vector<uint8_t> cat;
+    for (int m = 0; m < M; ++m)
+      cat.insert(cat.end(), want_data[m].begin() + want_idx[m][5], want_data[m].begin() + want_idx[m][6]);
+    EXPECT(!gpu && rows == cat, "aggregating reader: fetch-order rows");
+    EXPECT(manager.unregisterShuffle(9), "unregister 9");
   }
 
   manager.stop();

@@ -20,7 +20,7 @@ def test_library_loads_and_exports_every_header_symbol():
     assert set(declared) == set(N._SIGS), set(declared) ^ set(N._SIGS)
     assert lib.sux_abi_version() == 4
     assert C.sizeof(N.Conf) == 432  # sux_conf of ABI v2 (prealloc pairs appended)
-    assert C.sizeof(N.Tuning) == 128  # sux_tuning of ABI v4: 23 knobs + 9 reserved
+    assert C.sizeof(N.Tuning) == 128  # sux_tuning of ABI v4: 26 knobs + 6 reserved
 
 
 def test_conf_defaults_mirror_ucx_shuffle_conf():

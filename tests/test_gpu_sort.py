@@ -241,3 +241,26 @@ def test_msd_finish_and_lsd_agree_with_oracle(gpu_node, tuned, msd, shape):
     got = gpu_sort(gpu_node, recs, rs, kind, off, klen)
     assert got.tobytes() == O.sort_records(recs, rs, okind, off, klen).tobytes()
     gpu_node.check()
+
+
+def test_sort_records_captured_in_a_graph(gpu_node):
+    """sux_sort_records on a stream being captured into a HIP graph: no host wait, no host
+    allocation mid-capture (every digit pass runs); the replay equals the eager result."""
+    n, rs = 200_000, 100
+    recs = gpu_node.generate(N.GEN_TERASORT, 77, 0, n, rs)
+    want = gpu_node.sort_records(recs, rs, N.SORT_BYTES, 0, 10)
+    torch.cuda.synchronize()
+    out = torch.empty_like(want)
+    ws = torch.empty(gpu_node.sort_workspace_size(n, rs), dtype=torch.uint8, device=recs.device)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        gpu_node.sort_records(recs, rs, N.SORT_BYTES, 0, 10, out=out, workspace=ws, stream=s)
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, want)
+    g.replay()  # a second replay of the same graph
+    torch.cuda.synchronize()
+    assert torch.equal(out, want)
