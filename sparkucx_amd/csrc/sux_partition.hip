@@ -1382,7 +1382,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter7(MapGroup g, int R, int pid
 // loop that tagged destination units (v7 phase 3) becomes one partition byte per image unit.
 // R <= 215 at C = 1024 (LDS) and 4R <= NT (carry threads).
 // ------------------------------------------------------------------------------------------
-template <uint32_t S, uint32_t C, uint32_t NW>
+template <uint32_t S, uint32_t C, uint32_t NW, uint32_t RMAX = 208>
 struct Sc8 {
   static constexpr uint32_t NT = NW * kWave;
   static constexpr uint32_t W = S / 4;
@@ -1395,14 +1395,25 @@ struct Sc8 {
   static __host__ __device__ constexpr uint32_t space(int R) {
     return (C * S) / 16 + (17u * R + 1) / 2 + 1;
   }
-  // img[SP] u32x4 | pinfo[R] u32x4 | recoff[C] | wcnt[NW][R] | lunit[R] | fhead[R] | lpos[R]
-  // | tmp[NW + 1] | upid[SP] u8
+  // pinfo[RMAX] u32x4 | recoff[C] | wcnt[NW][RMAX] | lunit[RMAX] | fhead[RMAX] | lpos[RMAX]
+  // | tmp[NW + 1] (16-B padded) | img[SP] u32x4 | upid[SP] u8.  Every per-partition table sits at a
+  // compile-time offset sized for RMAX partitions: with R-dependent offsets each thread kept one
+  // VGPR of LDS address per table (and per wave row of wcnt) across the chunk loop, the kernel
+  // ran out of its 128 VGPRs and spilled to scratch — and every scratch reload is a vmcnt(0)
+  // that also waits for the next chunk's in-flight loads and the line stores
+  static constexpr uint32_t kPinfo = 0;
+  static constexpr uint32_t kRecoff = kPinfo + RMAX * 16;
+  static constexpr uint32_t kWcnt = kRecoff + C * 4;
+  static constexpr uint32_t kLunit = kWcnt + NW * RMAX * 4;
+  static constexpr uint32_t kFhead = kLunit + RMAX * 4;
+  static constexpr uint32_t kLpos = kFhead + RMAX * 4;
+  static constexpr uint32_t kTmp = kLpos + RMAX * 4;
+  static constexpr uint32_t kImg = (kTmp + (NW + 1) * 4 + 15) / 16 * 16;
   static __host__ __device__ constexpr uint32_t lds_bytes(int R) {
-    return space(R) * 16 + (uint32_t)R * 16 + C * 4 + NW * (uint32_t)R * 4 + 3u * R * 4 +
-           (NW + 1) * 4 + space(R);
+    return kImg + space(R) * 16 + space(R);
   }
   static __host__ __device__ constexpr bool fits(int R) {
-    return R >= 1 && 4u * (uint32_t)R <= NT && lds_bytes(R) <= 160u * 1024;
+    return R >= 1 && (uint32_t)R <= RMAX && 4u * (uint32_t)R <= NT && lds_bytes(R) <= 160u * 1024;
   }
 };
 
@@ -1415,23 +1426,24 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
                                                      uint32_t tw0, uint32_t tw1) {
   using K = Sc8<S, C, NW>;
   constexpr uint32_t NT = K::NT, W = K::W, RPW = K::RPW, NG = K::NG, PER = K::kPer;
+  constexpr uint32_t RM = 208;  // K's RMAX: the tables' compile-time stride
   extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
   const uint32_t SP = K::space(R);
-  u32x4* img = reinterpret_cast<u32x4*>(lds8);
-  uint32_t* img32 = reinterpret_cast<uint32_t*>(lds8);
-  u32x4* pinfo = img + SP;  // {lb, cd, full lines, sp}
-  uint32_t* recoff = reinterpret_cast<uint32_t*>(pinfo + R);
-  // per-wave counters, wave-major [NW][R]: a wave's lanes touch R different words of one row
+  u32x4* img = reinterpret_cast<u32x4*>(lds8 + K::kImg);
+  uint32_t* img32 = reinterpret_cast<uint32_t*>(lds8 + K::kImg);
+  u32x4* pinfo = reinterpret_cast<u32x4*>(lds8 + K::kPinfo);  // {lb, cd, full lines, sp}
+  uint32_t* recoff = reinterpret_cast<uint32_t*>(lds8 + K::kRecoff);
+  // per-wave counters, wave-major [NW][RM]: a wave's lanes touch different words of one row
   // (partition-major [R][NW] put every pid of a wave on 64 / NW banks: 41 % of the LDS cycles
   // were bank conflicts, profiles/pmc_r02.json)
-  uint32_t* wcnt = recoff + C;
+  uint32_t* wcnt = reinterpret_cast<uint32_t*>(lds8 + K::kWcnt);
   // counter of (partition p, wave w): wave-major (WM) or round 2's partition-major [R][NW]
-  auto WC = [&](uint32_t p, uint32_t w) -> uint32_t& { return WM ? wcnt[w * R + p] : wcnt[p * NW + w]; };
-  uint32_t* lunit = wcnt + NW * R;  // unit index of the line holding p's cursor
-  uint32_t* fhead = lunit + R;      // dwords of that line that belong to another range
-  uint32_t* lpos = fhead + R;       // p's cursor in dwords (flush at an item end)
-  uint32_t* tmp = lpos + R;
-  uint8_t* upid = reinterpret_cast<uint8_t*>(tmp + NW + 1);
+  auto WC = [&](uint32_t p, uint32_t w) -> uint32_t& { return WM ? wcnt[w * RM + p] : wcnt[p * NW + w]; };
+  uint32_t* lunit = reinterpret_cast<uint32_t*>(lds8 + K::kLunit);  // unit of the cursor's line
+  uint32_t* fhead = reinterpret_cast<uint32_t*>(lds8 + K::kFhead);  // its dwords of another range
+  uint32_t* lpos = reinterpret_cast<uint32_t*>(lds8 + K::kLpos);    // cursor in dwords (item end)
+  uint32_t* tmp = reinterpret_cast<uint32_t*>(lds8 + K::kTmp);
+  uint8_t* upid = lds8 + K::kImg + (size_t)SP * 16;
 
   const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
   const bool owner = tid < R;
