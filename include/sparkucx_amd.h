@@ -147,8 +147,8 @@ int sux_pool_stats(sux_node* node, uint64_t* allocated_bytes, uint64_t* requests
  * it (tile_records), so query sux_partition_workspace_size after a change.  No knob changes a
  * byte of any output: every variant is parity-tested against the CPU oracle. */
 typedef struct sux_tuning {
-  int32_t hist_kernel;      /* newest K1 variant allowed: 1, 2, 3, 4                            */
-  int32_t scatter_kernel;   /* newest K3 variant allowed: 1, 2, 6, 7, 8                         */
+  int32_t hist_kernel;      /* newest K1 variant allowed: 1, 3, 4 (2 was retired in round 3)    */
+  int32_t scatter_kernel;   /* newest K3 variant allowed: 1, 6, 7, 8 (2 was retired in round 3) */
   int32_t coresident;       /* 1: in calls that keep two launch groups in flight, K3 shapes that
                                leave a K1 workgroup room on the CU (measured slower: opt-in);
                                0 or -1: not                                                     */
@@ -168,9 +168,10 @@ typedef struct sux_tuning {
   int32_t sort_all_passes;  /* 1: every digit pass runs (no key-span read-back)                  */
   int32_t hist_wgs_per_cu;  /* k_hist4 workgroups per CU: 1 .. 8 (0: as many as LDS allows)     */
   int32_t small_kernel;     /* 16-byte records, R > 1024: 1 turn-taking scatter, 2 sorted chunks,
-                               3 two passes through bucket order (R <= 16384), 4 two-level
-                               MSD passes without K1 (map-major, R <= 16384)                  */
-  int32_t small_waves;      /* two-pass small-record kernels: waves per workgroup, 8 or 16      */
+                               4 two-level MSD passes without K1 (map-major, R <= 16384);
+                               3 (two passes through bucket order) was retired in round 3    */
+  int32_t small_waves;      /* 8 or 16; no effect since round 3 (it shaped the retired
+                               small_kernel 3), kept so the table's layout does not move      */
   int32_t scatter_order;    /* k_scatter8 tiles: 1 one contiguous range per workgroup (0), 2
                                blocks dealt round robin among an XCD's workgroups (slower)     */
   int32_t small_wgs_per_cu; /* two-level small-record kernels (small_kernel 4): workgroups per CU
@@ -186,7 +187,9 @@ typedef struct sux_tuning {
                                tile-major (one contiguous store of a tile's R counters)        */
   int32_t scatter_counters; /* k_scatter8 per-wave rank counters in LDS: 1 partition-major
                                [R][waves] (round 2), 2 (0) wave-major [waves][R]               */
-  int32_t reserved[6];
+  int32_t lz4_queue;        /* LZ4 compressor chunk deal: 1 a device work queue (one atomic per
+                               chunk), 2 (0) the fixed grid-stride deal                        */
+  int32_t reserved[5];
 } sux_tuning;
 int sux_node_set_tuning(sux_node* node, const sux_tuning* tuning);
 /* Waits for the device, then reports (and clears) failures the kernels recorded in the node's

@@ -732,12 +732,12 @@ sux::Tuning resolve_tuning(const sux_tuning& t, bool pipelined) {
   r.varlen_tile = t.varlen_tile;
   r.small_kernel = t.small_kernel ? t.small_kernel : kDefaultSmallKernel;
   r.small_auto = t.small_kernel == 0;
-  if (t.small_waves) r.small_waves = t.small_waves;
   r.scatter_order = t.scatter_order;
   if (t.small_wgs_per_cu) r.small_wgs_per_cu = t.small_wgs_per_cu;
   r.hist_nt = t.hist_nt > 0;
   r.counts_tm = t.counts_layout != 1;
   if (t.scatter_counters) r.scatter_counters = t.scatter_counters;
+  r.lz4_queue = t.lz4_queue == 1;
   return r;
 }
 
@@ -962,9 +962,8 @@ int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
         if (v == o) return true;
       return false;
     };
-    require(in(t->hist_kernel, {1, 2, 3, 4}), SUX_EINVAL, "hist_kernel must be 1..4");
-    require(in(t->scatter_kernel, {1, 2, 6, 7, 8}), SUX_EINVAL,
-            "scatter_kernel must be 1, 2, 6, 7 or 8");
+    require(in(t->hist_kernel, {1, 3, 4}), SUX_EINVAL, "hist_kernel must be 1, 3 or 4");
+    require(in(t->scatter_kernel, {1, 6, 7, 8}), SUX_EINVAL, "scatter_kernel must be 1, 6, 7 or 8");
     require(t->coresident >= -1 && t->coresident <= 1, SUX_EINVAL, "coresident must be -1, 0 or 1");
     require(in(t->scatter_chunk, {512, 768, 1024}), SUX_EINVAL,
             "scatter_chunk must be 512, 768 or 1024");
@@ -974,7 +973,7 @@ int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
     require(in(t->hist_stage, {64, 128}), SUX_EINVAL, "hist_stage must be 64 or 128");
     require(t->hist_wgs_per_cu >= 0 && t->hist_wgs_per_cu <= 8, SUX_EINVAL,
             "hist_wgs_per_cu must be 0..8");
-    require(in(t->small_kernel, {1, 2, 3, 4}), SUX_EINVAL, "small_kernel must be 1, 2, 3 or 4");
+    require(in(t->small_kernel, {1, 2, 4}), SUX_EINVAL, "small_kernel must be 1, 2 or 4");
     require(in(t->small_waves, {8, 16}), SUX_EINVAL, "small_waves must be 8 or 16");
     require(in(t->scatter_order, {1, 2}), SUX_EINVAL, "scatter_order must be 1 or 2");
     require(in(t->small_wgs_per_cu, {1, 2}), SUX_EINVAL, "small_wgs_per_cu must be 1 or 2");
@@ -1002,6 +1001,7 @@ int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
     require(t->hist_nt >= -1 && t->hist_nt <= 1, SUX_EINVAL, "hist_nt must be -1, 0 or 1");
     require(in(t->counts_layout, {1, 2}), SUX_EINVAL, "counts_layout must be 1 or 2");
     require(in(t->scatter_counters, {1, 2}), SUX_EINVAL, "scatter_counters must be 1 or 2");
+    require(in(t->lz4_queue, {1, 2}), SUX_EINVAL, "lz4_queue must be 1 or 2");
     for (int32_t r : t->reserved) require(r == 0, SUX_EINVAL, "reserved tuning fields must be 0");
     require(node, SUX_EINVAL, "NULL node");
     std::lock_guard<std::mutex> lk(node->mu);
@@ -1395,6 +1395,7 @@ int sux_compress_map_outputs(sux_node* node, const void* d_data, uint64_t data_b
                                        (uint32_t)num_maps, (uint32_t)R, (uint32_t)block_size,
                                        static_cast<uint8_t*>(d_out), d_out_index, d_out_index_be,
                                        d_out_bytes, static_cast<uint8_t*>(d_ws), w,
+                                       resolve_tuning(node->tuning, false).lz4_queue,
                                        node->stream(stream)),
               "compress launch");
   });

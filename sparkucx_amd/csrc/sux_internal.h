@@ -42,8 +42,7 @@ struct Tuning {
   int hist_stage = 64;      // k_hist4 records per LDS stage: 64 | 128
   int hist_wgs_per_cu = 0;  // k_hist4 workgroups per CU (0: as many as LDS allows)
   int small_kernel = 0;     // 16-byte records, R > 1024: 1 turn-taking k_scatter16b, 2 sorted
-                            // chunks, 3 two passes through bucket order (needs the temp copy)
-  int small_waves = 8;      // two-pass small-record kernels: waves per workgroup (8 | 16)
+                            // chunks, 4 two-level MSD passes (needs the temp copy)
   int scatter_order = 0;    // k_scatter8 tile order: 1 contiguous ranges, 2 block-cyclic per XCD
   int small_wgs_per_cu = 2; // k_msd16a / k_msd16b workgroups per CU (1: two groups share a CU)
   bool small_auto = true;   // small_kernel left to the default: the MSD path only when its
@@ -58,6 +57,7 @@ struct Tuning {
   bool hist_nt = false;     // k_hist4: non-temporal (streaming) record loads
   bool counts_tm = true;    // k_hist4 + k_scatter7/8: tile-major counts (MapGroup::counts_tm)
   int scatter_counters = 2; // k_scatter8 per-wave counters: 1 partition-major, 2 wave-major
+  bool lz4_queue = false;   // k_lz4_default: chunks from a device work queue (else grid-stride)
 };
 
 // Per-launch geometry of a group of consecutive map batches.
@@ -103,10 +103,10 @@ struct Workspace {
   uint64_t base_off, base_bytes;      // u64 [map][R] destination record offset of (map, p)
   uint64_t pids_off, pids_bytes;      // u16 [records] when the caller passes no pid buffer
   uint64_t op_off, op_bytes;          // one-pass kernel's sync words + scan tables (S = 100)
-  uint64_t tmp_off, tmp_bytes;        // two-pass small-record scatter: records grouped by bucket
+  uint64_t tmp_off, tmp_bytes;        // two-level small-record path: pass A's chunk-sorted copy
   uint64_t total;
 };
-// Small records whose map side may take the two-pass scatter (it needs the temp copy).
+// Small records whose map side may take the two-level MSD path (it needs the temp copy).
 inline bool small_two_pass_shape(uint32_t R, uint32_t rec_size) {
   return rec_size == 16 && R > 1024 && R <= 16384;
 }
@@ -176,7 +176,7 @@ Lz4Workspace lz4_workspace_layout(uint64_t data_bytes, uint32_t maps, uint32_t R
 hipError_t launch_lz4_compress(const uint8_t* d_data, const int64_t* d_index, uint32_t maps,
                                uint32_t R, uint32_t bs, uint8_t* d_out, int64_t* d_out_index,
                                uint8_t* d_out_index_be, uint64_t* d_out_bytes, uint8_t* d_ws,
-                               const Lz4Workspace& w, hipStream_t s);
+                               const Lz4Workspace& w, bool queue, hipStream_t s);
 hipError_t launch_rows_index(const uint64_t* sizes, uint32_t maps, uint32_t R, uint64_t* base,
                              int64_t* d_index, uint8_t* d_index_be, hipStream_t s);
 hipError_t launch_partition_ids(const PartDev& pd, const uint8_t* recs, uint32_t rec_size,
@@ -209,7 +209,7 @@ constexpr uint32_t kSortSpanBlocks = 2048;
 constexpr uint64_t kSortSpanBytes = 4ull * 8 * (kSortSpanBlocks + 1);
 hipError_t launch_gather_records(const void* in, const void* pairs, uint64_t n, uint32_t rs,
                                  void* out, hipStream_t s);
-// MSD finish of the sort (sux_partition.hip): buckets of <= kSortLocalCap pairs sorted in LDS by
+// MSD finish of the sort (sux_sort.hip): buckets of <= kSortLocalCap pairs sorted in LDS by
 // the listed 8-bit digits (shifts into the big-endian pair, least significant first); with
 // max_only, only the largest bucket (in pairs) is written to d_maxbucket.
 constexpr uint32_t kSortLocalCap = 4096;

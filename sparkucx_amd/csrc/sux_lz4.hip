@@ -168,6 +168,11 @@ __global__ __launch_bounds__(256) void k_lz4_fill(const int64_t* __restrict__ in
 //   - the table updates after a match (ip - 2, then the probe of ip itself) are single-lane.
 // A chunk whose block would not be shorter than the chunk is stored raw (lz4-java's rule); the
 // parse stops as soon as that is certain, so the scratch never needs more than the chunk's bytes.
+// Chunk deal: Q = false, the fixed grid-stride deal; Q = true, a device work queue (tuning
+// lz4_queue) — lane 0 claims the next chunk with one vector atomic on a counter the launcher
+// zeroes on the same stream, and the index reaches the wave through readfirstlane, so the loop
+// exit is wave-uniform by construction (a scalar register) and the counter only grows: every wave
+// leaves after at most one claim past the last chunk.
 constexpr int kLz4TabBits = 13;          // liblz4: LZ4_HASHLOG + 1 for byU16 tables
 constexpr int kLz4Waves = 2;             // waves per workgroup: 2 x 16 KiB of tables
 
@@ -184,15 +189,23 @@ __device__ __forceinline__ void put_len(uint8_t* d, uint32_t v, int lane) {
   for (uint32_t k = lane; k < nb; k += kLWave) d[k] = (k + 1 < nb) ? 255u : (uint8_t)((v - 15u) % 255u);
 }
 
+__device__ __forceinline__ uint32_t lz4_claim(uint32_t* q, int lane) {
+  uint32_t t = 0;
+  if (lane == 0) t = atomicAdd(q, 1u);
+  return (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)t, 0, kLWave));
+}
+
+template <bool Q>
 __global__ __launch_bounds__(kLz4Waves * kLWave) void k_lz4_default(
     const uint8_t* __restrict__ data, Lz4Chunk* __restrict__ chunks,
-    const uint32_t* __restrict__ nchunks, uint8_t* __restrict__ scratch) {
+    const uint32_t* __restrict__ nchunks, uint8_t* __restrict__ scratch, uint32_t* __restrict__ qctr) {
   __shared__ __attribute__((aligned(16))) uint16_t ltab[kLz4Waves][1u << kLz4TabBits];
   const int wave = threadIdx.x / kLWave, lane = threadIdx.x % kLWave;
   uint16_t* tab = ltab[wave];
   const uint64_t lt = (1ull << lane) - 1ull;
   const uint32_t n = *nchunks;
-  for (uint32_t b = blockIdx.x * kLz4Waves + wave; b < n; b += gridDim.x * kLz4Waves) {
+  for (uint32_t b = Q ? lz4_claim(qctr, lane) : blockIdx.x * kLz4Waves + wave; b < n;
+       b = Q ? lz4_claim(qctr, lane) : b + gridDim.x * kLz4Waves) {
     const Lz4Chunk C = chunks[b];
     const uint8_t* src = data + C.src;
     const uint32_t len = C.len;
@@ -545,7 +558,7 @@ Lz4Workspace lz4_workspace_layout(uint64_t data_bytes, uint32_t maps, uint32_t R
 hipError_t launch_lz4_compress(const uint8_t* d_data, const int64_t* d_index, uint32_t maps,
                                uint32_t R, uint32_t bs, uint8_t* d_out, int64_t* d_out_index,
                                uint8_t* d_out_index_be, uint64_t* d_out_bytes, uint8_t* d_ws,
-                               const Lz4Workspace& w, hipStream_t s) {
+                               const Lz4Workspace& w, bool queue, hipStream_t s) {
   const uint64_t runs = (uint64_t)maps * R;
   uint64_t* map_base = reinterpret_cast<uint64_t*>(d_ws + w.map_base_off);
   uint32_t* nb = reinterpret_cast<uint32_t*>(d_ws + w.nb_off);
@@ -570,8 +583,16 @@ hipError_t launch_lz4_compress(const uint8_t* d_data, const int64_t* d_index, ui
   const uint32_t cg = (uint32_t)std::min<uint64_t>((w.chunk_bound + 3) / 4, 8192);
   const uint32_t zg = (uint32_t)std::min<uint64_t>((w.chunk_bound + kLz4Waves - 1) / kLz4Waves,
                                                    256u * 16u);
-  hipLaunchKernelGGL(k_lz4_default, dim3(zg), dim3(kLz4Waves * kLWave), 0, s, d_data, chunks,
-                     nchunks, scratch);
+  uint32_t* qctr = nchunks + 1;  // the work queue's counter (nchunks_off holds 256 bytes)
+  if (queue) {
+    e = hipMemsetAsync(qctr, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_lz4_default<true>, dim3(zg), dim3(kLz4Waves * kLWave), 0, s, d_data,
+                       chunks, nchunks, scratch, qctr);
+  } else {
+    hipLaunchKernelGGL(k_lz4_default<false>, dim3(zg), dim3(kLz4Waves * kLWave), 0, s, d_data,
+                       chunks, nchunks, scratch, qctr);
+  }
   const uint32_t xg = (uint32_t)std::min<uint64_t>((w.chunk_bound + 63) / 64, 4096);
   hipLaunchKernelGGL(k_xxh32, dim3(xg), dim3(256), 0, s, d_data, chunks, nchunks);
   const uint32_t bg = (uint32_t)((w.chunk_bound + 255) / 256);

@@ -13,51 +13,20 @@
 //                1024-thread workgroup per CU, 1024-record chunks staged straight into a
 //                partition-sorted LDS image in destination-unit space, written out as aligned
 //                16-byte stores; the next chunk's loads fly during the write-out.
-// Older shapes (other record sizes, R beyond the LDS image) use the v1/v2/v3/v6 kernels below.
+// Other shapes: k_scatter7 (R <= 512) and k_scatter6 (R up to the LDS image) for 100-byte
+// records; k_hist3 / k_hist + k_scatter (v1) for any record size; 16-byte records with R > 1024
+// go to sux_small.hip.
 //
 // Stability: records are visited in input order (waves in order inside a chunk, chunks in order
 // inside a tile range, tile ranges ordered by the partition-major tile prefix); equal pids inside
 // 64 lanes are ranked by a ballot match.  So records keep input order inside a partition, as
 // Spark's writers do (P2).
-#include <hip/hip_runtime.h>
-
-#include <algorithm>
-#include <cstdlib>
-
-#include "sux_internal.h"
+#include "sux_part.h"
 
 namespace sux {
 
-typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
-
-constexpr int kWave = 64;
-
-// P1: partition functions — sux_p1.h
-#include "sux_p1.h"
-
-// ------------------------------------------------------------------------------------------
-// geometry helpers
-// ------------------------------------------------------------------------------------------
-struct TileRange {
-  uint32_t map, tile;
-  uint64_t begin, end;  // record indices within the group
-};
-
-__device__ __forceinline__ TileRange tile_range(const MapGroup& g, uint32_t gtile) {
-  TileRange tr;
-  tr.map = gtile / g.tiles_per_map;
-  tr.tile = gtile - tr.map * g.tiles_per_map;
-  uint64_t map_begin = (uint64_t)tr.map * g.records_per_map;
-  uint64_t map_end = map_begin + g.records_per_map;
-  if (map_end > g.num_records) map_end = g.num_records;
-  tr.begin = map_begin + (uint64_t)tr.tile * g.tile_recs;
-  tr.end = tr.begin + g.tile_recs;
-  if (tr.end > map_end) tr.end = map_end;
-  if (tr.begin > tr.end) tr.begin = tr.end;
-  return tr;
-}
-
-// xcd_map: sux_p1.h
+// geometry (TileRange, tile_range), scans (wave_incl_scan, block_excl_scan) and the P1
+// partition functions: sux_part.h / sux_p1.h
 
 // ------------------------------------------------------------------------------------------
 // K1: partition ids + per-tile histogram
@@ -89,14 +58,6 @@ __global__ __launch_bounds__(WPG * kWave) void k_hist(PartDev pd, MapGroup g, ui
 // ------------------------------------------------------------------------------------------
 // K2a: exclusive scan over tiles of each (map, partition) row; row totals
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    uint32_t t = __shfl_up(v, d, kWave);
-    if (lane >= d) v += t;
-  }
-  return v;
-}
 
 __global__ __launch_bounds__(256) void k_tile_scan(uint32_t* counts, uint64_t* totals,
                                                    uint32_t rows, uint32_t tiles) {
@@ -191,46 +152,7 @@ __global__ __launch_bounds__(256) void k_tile_scan_tm(uint32_t* counts, uint64_t
 // ------------------------------------------------------------------------------------------
 // K2b: per-group scans -> index tables and destination bases
 // ------------------------------------------------------------------------------------------
-constexpr int kScanThreads = 1024;
 
-// Block-wide exclusive scan of one u64 per thread; returns the exclusive prefix, *total = sum.
-__device__ uint64_t block_excl_scan(uint64_t v, uint64_t* sh, uint64_t* total) {
-  const int lane = threadIdx.x % kWave, wave = threadIdx.x / kWave;
-  constexpr int nw = kScanThreads / kWave;
-  uint64_t inc = v;
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    uint64_t t = __shfl_up(inc, d, kWave);
-    if (lane >= d) inc += t;
-  }
-  if (lane == kWave - 1) sh[wave] = inc;
-  __syncthreads();
-  if (wave == 0) {
-    uint64_t w = lane < nw ? sh[lane] : 0;
-    uint64_t wi = w;
-#pragma unroll
-    for (int d = 1; d < nw; d <<= 1) {
-      uint64_t t = __shfl_up(wi, d, kWave);
-      if (lane >= d) wi += t;
-    }
-    if (lane < nw) sh[kWave + lane] = wi - w;
-    if (lane == nw - 1) sh[2 * kWave] = wi;
-  }
-  __syncthreads();
-  uint64_t r = sh[kWave + wave] + inc - v;
-  *total = sh[2 * kWave];
-  __syncthreads();
-  return r;
-}
-
-__device__ __forceinline__ uint64_t bswap64(uint64_t v) {
-  return ((uint64_t)__builtin_bswap32((uint32_t)v) << 32) | __builtin_bswap32((uint32_t)(v >> 32));
-}
-
-__device__ __forceinline__ uint32_t owner_of(uint32_t p, int R, int G) {
-  // largest h with floor(h*R/G) <= p
-  return (uint32_t)((((uint64_t)p + 1) * G + R - 1) / R) - 1;
-}
 
 // K2b: one workgroup per map.  In-map exclusive scan of the partition totals -> the map's index
 // file (P3: native and big-endian), and
@@ -397,148 +319,6 @@ __global__ __launch_bounds__(WPG * kWave) void k_scatter(MapGroup g, int R, int 
       const uint32_t dst = r0 + (uint32_t)__popcll(peers & lt_mask);
       copy_record<S>(g.recs + i * rs, out + (uint64_t)dst * rs, rs);
     }
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// v2 kernels: a wave stages CH records of its tile in LDS with fully coalesced 16-byte loads
-// (1 KiB per wave instruction), works on them there, and (scatter) writes them out record-
-// coalesced: consecutive lanes store consecutive dwords, so a wave instruction covers ~2.5
-// whole records instead of touching 64 cache lines.
-// ------------------------------------------------------------------------------------------
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-template <uint32_t S, uint32_t CH>
-struct Stage {
-  static constexpr uint32_t kUnits = (CH * S + 12 + 15) / 16;  // 16-B units incl. a <=12 B head
-  static constexpr uint32_t kPer = (kUnits + kWave - 1) / kWave;
-  static constexpr uint32_t kBufBytes = kUnits * 16;
-};
-
-// Load the 16-byte units covering [a, a + len) into `dst` (a is 4-byte aligned); returns the
-// offset of `a` in dst.  Every unit holds a requested byte, so no load leaves the buffer's pages.
-template <uint32_t PER>
-__device__ __forceinline__ uint32_t stage_units(const uint8_t* a, uint32_t len, u32x4* dst,
-                                                int lane) {
-  const uintptr_t p = reinterpret_cast<uintptr_t>(a);
-  const uint32_t head = (uint32_t)(p & 15u);
-  const u32x4* src = reinterpret_cast<const u32x4*>(p - head);
-  const uint32_t units = (head + len + 15) >> 4;
-  u32x4 v[PER];
-#pragma unroll
-  for (uint32_t k = 0; k < PER; ++k) {
-    const uint32_t u = lane + k * kWave;
-    if (u < units) v[k] = src[u];
-  }
-#pragma unroll
-  for (uint32_t k = 0; k < PER; ++k) {
-    const uint32_t u = lane + k * kWave;
-    if (u < units) dst[u] = v[k];
-  }
-  return head;
-}
-
-template <uint32_t S, uint32_t CH>
-__host__ __device__ constexpr uint32_t hist2_wave_bytes(int R) {
-  return Stage<S, CH>::kBufBytes + (((uint32_t)R * 4 + 15) / 16) * 16;
-}
-template <uint32_t S, uint32_t CH>
-__host__ __device__ constexpr uint32_t scatter2_wave_bytes(int R) {
-  return Stage<S, CH>::kBufBytes + CH * 4 + (((uint32_t)R * 4 + 15) / 16) * 16;
-}
-
-template <uint32_t S, uint32_t CH>
-__global__ __launch_bounds__(256) void k_hist2(PartDev pd, MapGroup g, uint16_t* __restrict__ pids,
-                                               uint32_t* __restrict__ counts) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
-  using St = Stage<S, CH>;
-  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-  const int R = pd.R;
-  uint8_t* wb = lds8 + wave * hist2_wave_bytes<S, CH>(R);
-  u32x4* buf = reinterpret_cast<u32x4*>(wb);
-  uint32_t* hist = reinterpret_cast<uint32_t*>(wb + St::kBufBytes);
-  for (int p = lane; p < R; p += kWave) hist[p] = 0;
-  const uint32_t gtile = blockIdx.x * 4 + wave;
-  if (gtile >= g.num_maps * g.tiles_per_map) return;
-  const TileRange tr = tile_range(g, gtile);
-  for (uint64_t c0 = tr.begin; c0 < tr.end; c0 += CH) {
-    const uint32_t nrec = (uint32_t)min<uint64_t>(CH, tr.end - c0);
-    const uint32_t head = stage_units<St::kPer>(g.recs + c0 * S, nrec * S, buf, lane);
-    __builtin_amdgcn_wave_barrier();
-    const uint8_t* b = reinterpret_cast<const uint8_t*>(buf) + head;
-#pragma unroll
-    for (uint32_t j = 0; j < CH / kWave; ++j) {
-      const uint32_t r = j * kWave + lane;
-      if (r < nrec) {
-        const int p = get_partition(pd, b + r * S);
-        pids[c0 + r] = (uint16_t)p;
-        atomicAdd(&hist[p], 1u);
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  uint32_t* dst = counts + ((uint64_t)tr.map * R) * g.tiles_per_map + tr.tile;
-  for (int p = lane; p < R; p += kWave) dst[(uint64_t)p * g.tiles_per_map] = hist[p];
-}
-
-template <uint32_t S, uint32_t CH>
-__global__ __launch_bounds__(256) void k_scatter2(MapGroup g, int R, int pid_bits,
-                                                  const uint16_t* __restrict__ pids,
-                                                  const uint32_t* __restrict__ prefix,
-                                                  const uint64_t* __restrict__ base,
-                                                  uint8_t* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
-  using St = Stage<S, CH>;
-  constexpr uint32_t W = S / 4;  // dwords per record
-  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-  const uint32_t gtile = xcd_map(blockIdx.x, gridDim.x) * 4 + wave;
-  if (gtile >= g.num_maps * g.tiles_per_map) return;
-  const TileRange tr = tile_range(g, gtile);
-  if (tr.begin >= tr.end) return;
-  uint8_t* wb = lds8 + wave * scatter2_wave_bytes<S, CH>(R);
-  u32x4* buf = reinterpret_cast<u32x4*>(wb);
-  uint32_t* dest = reinterpret_cast<uint32_t*>(wb + St::kBufBytes);
-  uint32_t* run = dest + CH;
-  const uint64_t* bm = base + (uint64_t)tr.map * R;
-  const uint32_t* pm = prefix + (uint64_t)tr.map * R * g.tiles_per_map + tr.tile;
-  for (int p = lane; p < R; p += kWave)
-    run[p] = (uint32_t)(bm[p] + pm[(uint64_t)p * g.tiles_per_map]);
-  __builtin_amdgcn_wave_barrier();
-  const uint64_t lt_mask = (1ull << lane) - 1ull;
-  uint32_t* out32 = reinterpret_cast<uint32_t*>(out);
-  for (uint64_t c0 = tr.begin; c0 < tr.end; c0 += CH) {
-    const uint32_t nrec = (uint32_t)min<uint64_t>(CH, tr.end - c0);
-    const uint32_t head = stage_units<St::kPer>(g.recs + c0 * S, nrec * S, buf, lane);
-    // destinations, in input order (stable: lane order inside 64, chunk order across)
-#pragma unroll
-    for (uint32_t j = 0; j < CH / kWave; ++j) {
-      const uint32_t r = j * kWave + lane;
-      const bool valid = r < nrec;
-      const uint32_t pid = valid ? pids[c0 + r] : 0u;
-      uint64_t peers = __ballot(valid);
-      for (int bb = 0; bb < pid_bits; ++bb) {
-        const bool bit = (pid >> bb) & 1u;
-        const uint64_t m = __ballot(bit);
-        peers &= bit ? m : ~m;
-      }
-      uint32_t r0 = 0;
-      if (valid) r0 = run[pid];
-      __builtin_amdgcn_wave_barrier();
-      if (valid && (peers & lt_mask) == 0) run[pid] = r0 + (uint32_t)__popcll(peers);
-      if (valid) dest[r] = r0 + (uint32_t)__popcll(peers & lt_mask);
-      __builtin_amdgcn_wave_barrier();
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    // record-coalesced write-out: lane -> dword d of the chunk, in input order
-    const uint32_t* bw = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(buf) + head);
-    const uint32_t total = nrec * W;
-#pragma unroll 4
-    for (uint32_t d = lane; d < total; d += kWave) {
-      const uint32_t r = d / W, w = d - r * W;
-      out32[(uint64_t)dest[r] * W + w] = bw[d];
-    }
-    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -1763,1311 +1543,6 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
   }
 }
 
-// ------------------------------------------------------------------------------------------
-// Small records (S = 16, SURVEY.md config C5: 16-byte key/value rows, 10,000 partitions).
-// A record is one aligned 16-byte unit and R is far too large for per-wave counters, so:
-//   k_hist16   persistent workgroups of 1024 threads, one tile at a time; every lane loads whole
-//              records (coalesced 16-byte units, 8 in flight per lane), hashes the key from its
-//              registers and counts into ONE per-workgroup LDS histogram of R counters.
-//   k_scatter16 persistent 1024-thread workgroups, one tile range at a time with an LDS cursor
-//              per partition.  The tile is cut into 64-record groups dealt to the waves in order;
-//              a group ranks its equal pids with a ballot match, then, when the LDS turn counter
-//              reaches it, reads and advances the cursors of its pids and hands the turn on.  Only
-//              that short step is serialised; loads and the 16-byte stores are not.
-// ------------------------------------------------------------------------------------------
-template <int KW>
-__global__ __launch_bounds__(1024) void k_hist16(PartDev pd, MapGroup g, uint16_t* __restrict__ pids,
-                                                uint32_t* __restrict__ counts) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t hist[];  // [R]
-  const int R = pd.R;
-  const uint32_t ntiles = g.num_maps * g.tiles_per_map;
-  const u32x4* recs = reinterpret_cast<const u32x4*>(g.recs);
-  const int kw0 = pd.key_offset / 4;
-  for (int p = threadIdx.x; p < R; p += 1024) hist[p] = 0;
-  __syncthreads();
-  for (uint32_t gt = blockIdx.x; gt < ntiles; gt += gridDim.x) {
-    const TileRange tr = tile_range(g, gt);
-    for (uint64_t i0 = tr.begin; i0 < tr.end; i0 += 8 * 1024) {
-      u32x4 v[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint64_t i = i0 + k * 1024 + threadIdx.x;
-        v[k] = recs[i < tr.end ? i : tr.begin];
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint64_t i = i0 + k * 1024 + threadIdx.x;
-        if (i < tr.end) {
-          uint32_t w[KW];
-#pragma unroll
-          for (int q = 0; q < KW; ++q) {
-            const int d = kw0 + q;
-            w[q] = d == 0 ? v[k][0] : d == 1 ? v[k][1] : d == 2 ? v[k][2] : v[k][3];
-          }
-          const int p = partition_words<KW, false>(pd, w, pd.bounds, pd.lut);
-          atomicAdd(&hist[p], 1u);
-          pids[i] = (uint16_t)p;
-        }
-      }
-    }
-    __syncthreads();
-    // tile-major counts [map][tile][p]: one contiguous row per tile (a partition-major column
-    // would touch R lines at a 4*tiles stride for R 4-byte counters)
-    uint32_t* dst = counts + ((uint64_t)tr.map * g.tiles_per_map + tr.tile) * R;
-    for (int p = threadIdx.x; p < R; p += 1024) {
-      dst[p] = hist[p];
-      hist[p] = 0;
-    }
-    __syncthreads();
-  }
-}
-
-// Wait until the LDS turn counter reaches `want`.  Bounded: after 2^22 sleeps (far beyond any
-// legitimate wait) the wave sets the node's device error word (sux_node_check reports it) and
-// the workgroup's stop flag, and every wave of the workgroup leaves without touching the
-// cursors again; a wave that sees the stop flag while it waits leaves too.  Returns false then.
-__device__ __forceinline__ bool wait_turn(uint32_t* turn, uint32_t want, uint32_t* stop,
-                                          uint32_t* err) {
-  for (uint32_t spin = 0;; ++spin) {
-    if (__hip_atomic_load(turn, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == want) return true;
-    if (__hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
-    if (spin > (1u << 22)) {
-      if (__lane_id() == 0) {
-        if (err) atomicOr(err, kErrTurnTimeout);
-        __hip_atomic_store(stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
-template <uint32_t NW>
-__global__ __launch_bounds__(NW * 64) void k_scatter16(MapGroup g, int R, int pid_bits,
-                                                       const uint16_t* __restrict__ pids,
-                                                       const uint32_t* __restrict__ prefix,
-                                                       const uint64_t* __restrict__ base,
-                                                       uint8_t* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t cur[];  // [R] next output record of p
-  __shared__ uint32_t turn, stop;
-  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
-  const uint32_t ntiles = g.num_maps * g.tiles_per_map;
-  const u32x4* recs = reinterpret_cast<const u32x4*>(g.recs);
-  u32x4* out4 = reinterpret_cast<u32x4*>(out);
-  const uint64_t lt_mask = (1ull << lane) - 1ull;
-  if (tid == 0) stop = 0;
-  for (uint32_t gt = xcd_map(blockIdx.x, gridDim.x); gt < ntiles; gt += gridDim.x) {
-    const TileRange tr = tile_range(g, gt);
-    const uint64_t* bm = base + (uint64_t)tr.map * R;
-    const uint32_t* pm = prefix + ((uint64_t)tr.map * g.tiles_per_map + tr.tile) * R;  // tile-major
-    for (int p = tid; p < R; p += NW * kWave) cur[p] = (uint32_t)(bm[p] + pm[p]);
-    if (tid == 0) turn = 0;
-    __syncthreads();
-    const uint32_t ngroups = (uint32_t)((tr.end - tr.begin + kWave - 1) / kWave);
-    // group q = wave + k * NW; the loads of the next two groups of this wave are in flight
-    // during this group's turn (clamped, unconditional: the compiler's waits stay counted)
-    auto load = [&](uint32_t qq, uint32_t& pv, u32x4& rv) {
-      const uint64_t i = tr.begin + (uint64_t)qq * kWave + lane;
-      const uint64_t ii = i < tr.end ? i : tr.end - 1;
-      pv = pids[ii];
-      rv = recs[ii];
-    };
-    uint32_t q = wave;
-    uint32_t pid0, pid1;
-    u32x4 rec0, rec1;
-    load(q, pid0, rec0);
-    load(q + NW, pid1, rec1);
-    while (q < ngroups) {
-      const uint64_t i = tr.begin + (uint64_t)q * kWave + lane;
-      const bool valid = i < tr.end;
-      uint32_t pid2;
-      u32x4 rec2;
-      load(q + 2 * NW, pid2, rec2);
-      const uint32_t p = valid ? pid0 : 0u;
-      uint64_t peers = __ballot(valid);
-      for (int bb = 0; bb < pid_bits; ++bb) {
-        const bool bit = (p >> bb) & 1u;
-        const uint64_t m = __ballot(bit);
-        peers &= bit ? m : ~m;
-      }
-      // this group's turn: groups update the cursors in input order (stability)
-      if (!wait_turn(&turn, q, &stop, g.err)) break;
-      uint32_t r0 = 0;
-      if (valid) r0 = cur[p];
-      __builtin_amdgcn_wave_barrier();
-      if (valid && (peers & lt_mask) == 0) cur[p] = r0 + (uint32_t)__popcll(peers);
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (lane == 0) __hip_atomic_store(&turn, q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (valid) out4[(uint64_t)r0 + (uint32_t)__popcll(peers & lt_mask)] = rec0;
-      pid0 = pid1;
-      rec0 = rec1;
-      pid1 = pid2;
-      rec1 = rec2;
-      q += NW;
-    }
-    __syncthreads();
-    if (stop) return;  // a turn timed out: the error word is set, nothing more is written
-  }
-}
-
-// k_scatter16 with the turn handed on once per batch of GB consecutive 64-record groups instead of
-// once per group: a wave ranks GB groups, then in its turn walks their cursor updates back to
-// back (LDS ops of one wave stay in order), so the cross-wave hand-off (acquire spin, release
-// fence) is paid GB x less often.  Same output bytes as k_scatter16 (input order kept).
-template <uint32_t NW, int GB>
-__global__ __launch_bounds__(NW * 64) void k_scatter16b(MapGroup g, int R, int pid_bits,
-                                                        const uint16_t* __restrict__ pids,
-                                                        const uint32_t* __restrict__ prefix,
-                                                        const uint64_t* __restrict__ base,
-                                                        uint8_t* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t cur[];  // [R] next output record of p
-  __shared__ uint32_t turn, stop;
-  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
-  const uint32_t ntiles = g.num_maps * g.tiles_per_map;
-  const u32x4* recs = reinterpret_cast<const u32x4*>(g.recs);
-  u32x4* out4 = reinterpret_cast<u32x4*>(out);
-  const uint64_t lt_mask = (1ull << lane) - 1ull;
-  if (tid == 0) stop = 0;
-  for (uint32_t gt = xcd_map(blockIdx.x, gridDim.x); gt < ntiles; gt += gridDim.x) {
-    const TileRange tr = tile_range(g, gt);
-    const uint64_t* bm = base + (uint64_t)tr.map * R;
-    const uint32_t* pm = prefix + ((uint64_t)tr.map * g.tiles_per_map + tr.tile) * R;  // tile-major
-    for (int p = tid; p < R; p += NW * kWave) cur[p] = (uint32_t)(bm[p] + pm[p]);
-    if (tid == 0) turn = 0;
-    __syncthreads();
-    const uint32_t ngroups = (uint32_t)((tr.end - tr.begin + kWave - 1) / kWave);
-    const uint32_t nbatch = (ngroups + GB - 1) / GB;
-    uint32_t pa[GB], pb[GB];
-    u32x4 ra[GB], rb[GB];
-    auto load = [&](uint32_t bb, uint32_t (&pv)[GB], u32x4 (&rv)[GB]) {
-#pragma unroll
-      for (int k = 0; k < GB; ++k) {
-        const uint64_t i = tr.begin + ((uint64_t)bb * GB + k) * kWave + lane;
-        const uint64_t ii = i < tr.end ? i : tr.end - 1;  // clamped, unconditional
-        pv[k] = pids[ii];
-        rv[k] = recs[ii];
-      }
-    };
-    uint32_t b = wave;
-    load(b, pa, ra);
-    while (b < nbatch) {
-      load(b + NW, pb, rb);  // next batch in flight during this one's turn
-      uint64_t peers[GB];
-      uint32_t pp[GB];
-      bool valid[GB];
-#pragma unroll
-      for (int k = 0; k < GB; ++k) {
-        const uint64_t i = tr.begin + ((uint64_t)b * GB + k) * kWave + lane;
-        valid[k] = i < tr.end;
-        pp[k] = valid[k] ? pa[k] : 0u;
-        uint64_t pe = __ballot(valid[k]);
-        for (int bb = 0; bb < pid_bits; ++bb) {
-          const bool bit = (pp[k] >> bb) & 1u;
-          const uint64_t m = __ballot(bit);
-          pe &= bit ? m : ~m;
-        }
-        peers[k] = pe;
-      }
-      if (!wait_turn(&turn, b, &stop, g.err)) break;
-      uint32_t dst[GB];
-#pragma unroll
-      for (int k = 0; k < GB; ++k) {
-        uint32_t r0 = 0;
-        if (valid[k]) r0 = cur[pp[k]];
-        __builtin_amdgcn_wave_barrier();
-        if (valid[k] && (peers[k] & lt_mask) == 0) cur[pp[k]] = r0 + (uint32_t)__popcll(peers[k]);
-        __builtin_amdgcn_wave_barrier();
-        dst[k] = r0 + (uint32_t)__popcll(peers[k] & lt_mask);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (lane == 0) __hip_atomic_store(&turn, b + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#pragma unroll
-      for (int k = 0; k < GB; ++k)
-        if (valid[k]) out4[dst[k]] = ra[k];
-#pragma unroll
-      for (int k = 0; k < GB; ++k) {
-        pa[k] = pb[k];
-        ra[k] = rb[k];
-      }
-      b += NW;
-    }
-    __syncthreads();
-    if (stop) return;  // a turn timed out: the error word is set, nothing more is written
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// k_scatter16s: the small-record scatter without turns (R <= kS16sMaxR).  A persistent
-// 1024-thread workgroup walks tile ranges in 4096-record chunks; a chunk's stable rank of every
-// record among the chunk's records of its partition comes from sorting the chunk's
-// (pid, position) keys in LDS, not from waves taking turns on the cursors:
-//   1. LSD radix passes of 7 pid bits over the 4096 keys (two for R <= 16384): a wave owns 256
-//      consecutive positions and ranks them group by group with a ballot match against its own
-//      per-digit counters; one block scan over (digit, wave) gives every wave's digit offsets, so
-//      each pass is stable and needs no atomics;
-//   2. run starts of the sorted keys (rs[p] = first sorted position of p), then every record's
-//      destination cursor[p] + (sorted position - rs[p]); run ends advance the cursors;
-//   3. every thread stores the records it loaded, in input order (16-byte stores).
-// Three barriers per pass and three for the rest; the next chunk's pids and records are in
-// flight the whole time.  Same bytes as k_scatter16 / k_scatter16b.
-// ------------------------------------------------------------------------------------------
-constexpr uint32_t kS16sChunk = 4096;    // records per chunk: 4 per thread of 1024
-constexpr uint32_t kS16sIdxBits = 12;    // log2(kS16sChunk)
-constexpr uint32_t kS16sDigit = 7;       // pid bits per LDS radix pass
-constexpr int kS16sMaxR = 16384;         // two passes; cursors + run starts fit the LDS
-
-struct Sc16s {
-  static constexpr uint32_t NT = 1024, NW = 16, PT = kS16sChunk / NT, NB = 1u << kS16sDigit;
-  // cur[R] u32 | rs[R] u16 (padded) | keys[2][chunk] u32 | wc[2][NW][NB] u32 | wsum[NW] u32
-  static __host__ __device__ constexpr uint32_t lds_bytes(int R) {
-    return (uint32_t)R * 4 + ((uint32_t)R * 2 + 15) / 16 * 16 + 2 * kS16sChunk * 4 +
-           2 * NW * NB * 4 + NW * 4;
-  }
-};
-
-__global__ __launch_bounds__(1024) void k_scatter16s(MapGroup g, int R, int pid_bits,
-                                                     const uint16_t* __restrict__ pids,
-                                                     const uint32_t* __restrict__ prefix,
-                                                     const uint64_t* __restrict__ base,
-                                                     uint8_t* __restrict__ out) {
-  using K = Sc16s;
-  constexpr uint32_t NT = K::NT, NW = K::NW, PT = K::PT, NB = K::NB, CH = kS16sChunk;
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
-  uint32_t* cur = reinterpret_cast<uint32_t*>(lds8);
-  uint16_t* rs = reinterpret_cast<uint16_t*>(cur + R);
-  uint32_t* keys0 = reinterpret_cast<uint32_t*>(lds8 + (uint32_t)R * 4 + ((uint32_t)R * 2 + 15) / 16 * 16);
-  uint32_t* keys1 = keys0 + CH;
-  uint32_t* wc0 = keys1 + CH;  // [2][NW][NB]
-  uint32_t* wsum = wc0 + 2 * NW * NB;
-
-  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
-  const uint64_t lt_mask = (1ull << lane) - 1ull;
-  const uint32_t ntiles = g.num_maps * g.tiles_per_map;
-  const u32x4* recs = reinterpret_cast<const u32x4*>(g.recs);
-  u32x4* out4 = reinterpret_cast<u32x4*>(out);
-  const int passes = pid_bits <= (int)kS16sDigit ? 1 : 2;
-
-  for (uint32_t i = tid; i < 2 * NW * NB; i += NT) wc0[i] = 0;
-  for (uint32_t gt = xcd_map(blockIdx.x, gridDim.x); gt < ntiles; gt += gridDim.x) {
-    const TileRange tr = tile_range(g, gt);
-    const uint64_t* bm = base + (uint64_t)tr.map * R;
-    const uint32_t* pm = prefix + ((uint64_t)tr.map * g.tiles_per_map + tr.tile) * R;  // tile-major
-    for (int p = tid; p < R; p += NT) cur[p] = (uint32_t)(bm[p] + pm[p]);
-    const uint32_t nchunks = (uint32_t)((tr.end - tr.begin + CH - 1) / CH);
-    // element e = wave * 256 + j * 64 + lane: a wave's positions are contiguous and visited in
-    // order, which is what keeps every radix pass stable
-    uint32_t pv[PT];
-    u32x4 rv[PT];
-    auto load = [&](uint32_t c, uint32_t (&p)[PT], u32x4 (&r)[PT]) {
-      const uint64_t c0 = tr.begin + (uint64_t)(c < nchunks ? c : 0) * CH;
-#pragma unroll
-      for (uint32_t j = 0; j < PT; ++j) {
-        const uint64_t i = c0 + wave * (PT * kWave) + j * kWave + lane;
-        const uint64_t ii = i < tr.end ? i : tr.end - 1;  // clamped, unconditional
-        p[j] = pids[ii];
-        r[j] = recs[ii];
-      }
-    };
-    if (nchunks) load(0, pv, rv);
-    __syncthreads();  // cursors ready
-    for (uint32_t c = 0; c < nchunks; ++c) {
-      const uint32_t n = (uint32_t)min<uint64_t>(CH, tr.end - tr.begin - (uint64_t)c * CH);
-      uint32_t pn[PT];
-      u32x4 rn[PT];
-      load(c + 1, pn, rn);  // the next chunk flies during this one
-      // 1. LSD radix passes over (pid << 12 | position)
-      uint32_t* kin = keys0;
-      uint32_t* kout = keys1;
-      for (int d = 0; d < passes; ++d) {
-        uint32_t* wc = wc0 + (d & 1) * NW * NB;
-        const uint32_t sh = kS16sIdxBits + d * kS16sDigit;
-        uint32_t key[PT], dig[PT], rank[PT];
-#pragma unroll
-        for (uint32_t j = 0; j < PT; ++j) {
-          const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
-          const bool valid = e < n;
-          key[j] = d == 0 ? ((pv[j] << kS16sIdxBits) | e) : (valid ? kin[e] : 0u);
-          dig[j] = valid ? (key[j] >> sh) & (NB - 1) : 0u;
-          uint64_t peers = __ballot(valid);
-#pragma unroll
-          for (uint32_t bb = 0; bb < kS16sDigit; ++bb) {
-            const bool bit = (dig[j] >> bb) & 1u;
-            const uint64_t m = __ballot(bit);
-            peers &= bit ? m : ~m;
-          }
-          uint32_t* w = wc + wave * NB + dig[j];
-          uint32_t r0 = 0;
-          if (valid) r0 = *w;
-          __builtin_amdgcn_wave_barrier();
-          if (valid && (peers & lt_mask) == 0) *w = r0 + (uint32_t)__popcll(peers);
-          __builtin_amdgcn_wave_barrier();
-          rank[j] = valid ? r0 + (uint32_t)__popcll(peers & lt_mask) : ~0u;
-        }
-        __syncthreads();
-        // block exclusive scan of the counters in (digit, wave) order: thread t owns digit
-        // t / 8 and waves 2(t % 8), 2(t % 8) + 1
-        {
-          const uint32_t dg = tid / (NW / 2), w0 = 2 * (tid % (NW / 2));
-          const uint32_t a = wc[w0 * NB + dg], b = wc[(w0 + 1) * NB + dg];
-          const uint32_t incl = wave_incl_scan(a + b, lane);
-          if (lane == kWave - 1) wsum[wave] = incl;
-          __syncthreads();
-          uint32_t before = 0;
-#pragma unroll
-          for (uint32_t w = 0; w < NW; ++w) before += w < (uint32_t)wave ? wsum[w] : 0u;
-          const uint32_t ex = before + incl - (a + b);
-          wc[w0 * NB + dg] = ex;
-          wc[(w0 + 1) * NB + dg] = ex + a;
-        }
-        __syncthreads();
-#pragma unroll
-        for (uint32_t j = 0; j < PT; ++j)
-          if (rank[j] != ~0u) kout[wc[wave * NB + dig[j]] + rank[j]] = key[j];
-        __syncthreads();
-        // this counter set is next used at least one barrier later (next chunk or pass)
-        for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
-        uint32_t* t = kin;
-        kin = kout;
-        kout = t;
-      }
-      // 2. run starts, destinations (into the free key buffer, by position), cursor advances
-      uint32_t* dsta = kout;
-      uint32_t endp[PT], endv[PT];
-#pragma unroll
-      for (uint32_t k = 0; k < PT; ++k) {
-        const uint32_t s = tid + k * NT;
-        endp[k] = ~0u;
-        if (s < n) {
-          const uint32_t p = kin[s] >> kS16sIdxBits;
-          if (s == 0 || (kin[s - 1] >> kS16sIdxBits) != p) rs[p] = (uint16_t)s;
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (uint32_t k = 0; k < PT; ++k) {
-        const uint32_t s = tid + k * NT;
-        if (s < n) {
-          const uint32_t key = kin[s], p = key >> kS16sIdxBits;
-          const uint32_t dst = cur[p] + (s - rs[p]);
-          dsta[key & (CH - 1)] = dst;
-          if (s + 1 == n || (kin[s + 1] >> kS16sIdxBits) != p) {
-            endp[k] = p;
-            endv[k] = dst + 1;
-          }
-        }
-      }
-      __syncthreads();
-      // 3. stores in input order; the cursors move on (every read of them is behind the barrier)
-#pragma unroll
-      for (uint32_t k = 0; k < PT; ++k)
-        if (endp[k] != ~0u) cur[endp[k]] = endv[k];
-#pragma unroll
-      for (uint32_t j = 0; j < PT; ++j) {
-        const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
-        if (e < n) out4[dsta[e]] = rv[j];
-      }
-#pragma unroll
-      for (uint32_t j = 0; j < PT; ++j) {
-        pv[j] = pn[j];
-        rv[j] = rn[j];
-      }
-      __syncthreads();
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// Two-pass small-record scatter (16-byte records, R > 1024): C5 writes ~0.4 record per
-// partition per 4096-record chunk, so a one-pass scatter stores every record alone — a partial
-// 128-B line each (PMC: 32 B written per 16-B record) at a random address.  Instead:
-//   pass A (k_bucket16a) regroups every tile by bucket = pid >> 6 (<= 256 buckets) into the
-//          workspace's temp buffer, at the bucket's final position: bucket h of map m starts at
-//          base[m][64h], the tile's share after the earlier tiles' (the K2 tile prefix summed
-//          over the bucket's 64 partitions).  A chunk is stable-sorted by bucket in LDS and
-//          written in sorted order: runs of ~26 records per bucket instead of ~0.4;
-//   pass B (k_bucket16b) takes one (map, bucket) segment — its output range is the same
-//          range of the output, [base[m][64h], base[m][64h+64]) — recomputes each record's pid
-//          from its key, stable-sorts by the low 6 bits in LDS and writes the segment back in
-//          order: one contiguous, fully coalesced range per segment.
-// 16 + 2 + 16 (A) and 16 + 16 (B) bytes per record, every write a long run.  Stable: pass A
-// keeps input order inside a bucket, pass B inside a partition.
-// ------------------------------------------------------------------------------------------
-constexpr uint32_t kB16Lo = 6;         // partitions per bucket: 64
-constexpr uint32_t kB16PT = 4;         // records per thread per LDS chunk (chunk = 256 x waves)
-
-template <uint32_t NW>  // stage[chunk] u32x4 | wc[NW][256] u32 | cb[256] u32 | wsum[NW] | hs[chunk] u8
-struct B16a {
-  static constexpr uint32_t NB = 256, CH = NW * kWave * kB16PT;
-  static constexpr uint32_t lds_bytes() { return CH * 16 + NW * NB * 4 + NB * 4 + NW * 4 + CH; }
-};
-template <uint32_t NW>  // stage[chunk] u32x4 | wc[NW][64] u32 | cur[64] u32 | wsum[NW] | los[chunk] u8
-struct B16b {
-  static constexpr uint32_t NB = 1u << kB16Lo, CH = NW * kWave * kB16PT;
-  static constexpr uint32_t lds_bytes() { return CH * 16 + NW * NB * 4 + NB * 4 + NW * 4 + CH; }
-};
-
-// Stable in-wave rank of `dig` (DB bits) against the wave's running per-digit counters wcw[]:
-// lanes of the group in lane order after the wave's earlier groups.  ~0 for invalid lanes.
-template <uint32_t DB, typename CT = uint32_t>
-__device__ __forceinline__ uint32_t wave_rank(uint32_t dig, bool valid, CT* wcw, uint64_t lt_mask) {
-  uint64_t peers = __ballot(valid);
-#pragma unroll
-  for (uint32_t bb = 0; bb < DB; ++bb) {
-    const bool bit = (dig >> bb) & 1u;
-    const uint64_t m = __ballot(bit);
-    peers &= bit ? m : ~m;
-  }
-  uint32_t r0 = 0;
-  if (valid) r0 = wcw[dig];
-  __builtin_amdgcn_wave_barrier();
-  if (valid && (peers & lt_mask) == 0) wcw[dig] = (CT)(r0 + (uint32_t)__popcll(peers));
-  __builtin_amdgcn_wave_barrier();
-  return valid ? r0 + (uint32_t)__popcll(peers & lt_mask) : ~0u;
-}
-
-// Block exclusive scan of wc[NW][NB] in (digit, wave) order, in place (NW*64 threads, NB*NW
-// entries, E = NB/64 consecutive entries per thread).  Two barriers.
-template <uint32_t NB, uint32_t NW>
-__device__ __forceinline__ void scan_digit_wave(uint32_t* wc, uint32_t* wsum, int tid, int lane, int wave) {
-  constexpr uint32_t E = NB / kWave;
-  static_assert(E >= 1 && NW % E == 0, "entries per thread");
-  const uint32_t dg = (uint32_t)tid * E / NW, w0 = ((uint32_t)tid * E) % NW;
-  uint32_t v[E], sum = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < E; ++k) {
-    v[k] = wc[(w0 + k) * NB + dg];
-    sum += v[k];
-  }
-  const uint32_t incl = wave_incl_scan(sum, lane);
-  if (lane == kWave - 1) wsum[wave] = incl;
-  __syncthreads();
-  uint32_t run = incl - sum;
-#pragma unroll
-  for (uint32_t w = 0; w < NW; ++w) run += w < (uint32_t)wave ? wsum[w] : 0u;
-#pragma unroll
-  for (uint32_t k = 0; k < E; ++k) {
-    wc[(w0 + k) * NB + dg] = run;
-    run += v[k];
-  }
-  __syncthreads();
-}
-
-template <uint32_t NW>
-__global__ __launch_bounds__(NW * 64) void k_bucket16a(MapGroup g, int R,
-                                                    const uint16_t* __restrict__ pids,
-                                                    const uint32_t* __restrict__ prefix,
-                                                    const uint64_t* __restrict__ base,
-                                                    uint8_t* __restrict__ tmp) {
-  constexpr uint32_t NB = B16a<NW>::NB, CH = B16a<NW>::CH, PT = kB16PT, NT = NW * kWave;
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
-  u32x4* stage = reinterpret_cast<u32x4*>(lds8);
-  uint32_t* wc = reinterpret_cast<uint32_t*>(stage + CH);  // [NW][NB]
-  uint32_t* cb = wc + NW * NB;
-  uint32_t* wsum = cb + NB;
-  uint8_t* hs = reinterpret_cast<uint8_t*>(wsum + NW);
-  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
-  const uint64_t lt_mask = (1ull << lane) - 1ull;
-  const uint32_t ntiles = g.num_maps * g.tiles_per_map;
-  const uint32_t nbk = ((uint32_t)R + (1u << kB16Lo) - 1) >> kB16Lo;
-  const u32x4* recs = reinterpret_cast<const u32x4*>(g.recs);
-  u32x4* t4 = reinterpret_cast<u32x4*>(tmp);
-  for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
-  for (uint32_t gt = xcd_map(blockIdx.x, gridDim.x); gt < ntiles; gt += gridDim.x) {
-    const TileRange tr = tile_range(g, gt);
-    if (tid < (int)nbk) {  // bucket cursor: its base + the earlier tiles' records of its partitions
-      const uint32_t p0 = (uint32_t)tid << kB16Lo, p1 = min(p0 + (1u << kB16Lo), (uint32_t)R);
-      const uint32_t* pm = prefix + ((uint64_t)tr.map * g.tiles_per_map + tr.tile) * R;
-      uint32_t s = 0;
-      for (uint32_t p = p0; p < p1; ++p) s += pm[p];
-      cb[tid] = (uint32_t)base[(uint64_t)tr.map * R + p0] + s;
-    }
-    const uint32_t nchunks = (uint32_t)((tr.end - tr.begin + CH - 1) / CH);
-    uint32_t pv[PT];
-    u32x4 rv[PT];
-    auto load = [&](uint32_t c, uint32_t (&p)[PT], u32x4 (&r)[PT]) {
-      const uint64_t c0 = tr.begin + (uint64_t)(c < nchunks ? c : 0) * CH;
-#pragma unroll
-      for (uint32_t j = 0; j < PT; ++j) {
-        const uint64_t i = c0 + wave * (PT * kWave) + j * kWave + lane;
-        const uint64_t ii = i < tr.end ? i : tr.end - 1;
-        p[j] = pids[ii];
-        r[j] = recs[ii];
-      }
-    };
-    if (nchunks) load(0, pv, rv);
-    __syncthreads();
-    for (uint32_t c = 0; c < nchunks; ++c) {
-      const uint32_t n = (uint32_t)min<uint64_t>(CH, tr.end - tr.begin - (uint64_t)c * CH);
-      uint32_t pn[PT];
-      u32x4 rn[PT];
-      load(c + 1, pn, rn);
-      uint32_t h[PT], rank[PT];
-#pragma unroll
-      for (uint32_t j = 0; j < PT; ++j) {
-        const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
-        h[j] = (pv[j] >> kB16Lo) & (NB - 1);
-        rank[j] = wave_rank<8>(h[j], e < n, wc + wave * NB, lt_mask);
-      }
-      __syncthreads();
-      scan_digit_wave<NB, NW>(wc, wsum, tid, lane, wave);
-#pragma unroll
-      for (uint32_t j = 0; j < PT; ++j)
-        if (rank[j] != ~0u) {
-          const uint32_t pos = wc[wave * NB + h[j]] + rank[j];
-          stage[pos] = rv[j];
-          hs[pos] = (uint8_t)h[j];
-        }
-      __syncthreads();
-      // sorted order: consecutive positions of a bucket go to consecutive temp records
-#pragma unroll
-      for (uint32_t k = 0; k < PT; ++k) {
-        const uint32_t i = tid + k * NT;
-        if (i < n) {
-          const uint32_t b = hs[i];
-          const uint64_t dst = (uint64_t)cb[b] + (i - wc[b]);  // wc[0 * NB + b]: bucket start
-          if (dst < g.num_records) t4[dst] = stage[i];         // (a bad pid cannot fault)
-        }
-      }
-      uint32_t ncb = 0;
-      if (tid < (int)nbk) {
-        const uint32_t end = (uint32_t)tid + 1 < NB ? wc[tid + 1] : n;
-        ncb = cb[tid] + (end - wc[tid]);
-      }
-      __syncthreads();
-      if (tid < (int)nbk) cb[tid] = ncb;
-      for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
-#pragma unroll
-      for (uint32_t j = 0; j < PT; ++j) {
-        pv[j] = pn[j];
-        rv[j] = rn[j];
-      }
-      __syncthreads();
-    }
-  }
-}
-
-// Pass B walks a stream of (segment, chunk) pairs: the next chunk's records — across a segment
-// seam too, with the next segment's 64 cursors — are loaded while this chunk is sorted and
-// written, so no chunk waits for its loads.
-template <int KW, uint32_t NW>
-__global__ __launch_bounds__(NW * 64) void k_bucket16b(PartDev pd, MapGroup g,
-                                                    const uint64_t* __restrict__ base,
-                                                    const uint64_t* __restrict__ totals,
-                                                    const uint8_t* __restrict__ tmp,
-                                                    uint8_t* __restrict__ out) {
-  constexpr uint32_t NB = B16b<NW>::NB, CH = B16b<NW>::CH, PT = kB16PT, NT = NW * kWave;
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
-  u32x4* stage = reinterpret_cast<u32x4*>(lds8);
-  uint32_t* wc = reinterpret_cast<uint32_t*>(stage + CH);  // [NW][NB]
-  uint32_t* cur = wc + NW * NB;
-  uint32_t* wsum = cur + NB;
-  uint8_t* los = reinterpret_cast<uint8_t*>(wsum + NW);
-  const int R = pd.R;
-  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
-  const uint64_t lt_mask = (1ull << lane) - 1ull;
-  const uint32_t nbk = ((uint32_t)R + NB - 1) / NB;
-  const uint32_t nitems = g.num_maps * nbk, G = gridDim.x;
-  const int kw0 = pd.key_offset / 4;
-  const u32x4* t4 = reinterpret_cast<const u32x4*>(tmp);
-  u32x4* out4 = reinterpret_cast<u32x4*>(out);
-
-  struct Cur {
-    uint32_t it, p0;
-    uint64_t c0, b1;
-    bool valid, first;
-  };
-  auto seg = [&](uint32_t it) {  // first chunk of segment `it` (an empty segment: c0 == b1)
-    Cur k;
-    k.it = it;
-    k.valid = it < nitems;
-    k.first = true;
-    const uint32_t m = k.valid ? it / nbk : 0, hb = k.valid ? it - m * nbk : 0;
-    k.p0 = hb * NB;
-    const uint32_t p1 = min(k.p0 + NB, (uint32_t)R);
-    const uint64_t* bm = base + (uint64_t)m * R;
-    k.c0 = bm[k.p0];
-    k.b1 = bm[p1 - 1] + totals[(uint64_t)m * R + p1 - 1];
-    return k;
-  };
-  auto next = [&](const Cur& k) {
-    Cur nk = k;
-    nk.first = false;
-    nk.c0 = k.c0 + CH;
-    if (nk.c0 >= k.b1) nk = seg(k.it + G);
-    return nk;
-  };
-  // loads of chunk k (clamped, unconditional) and, at a segment's first chunk, its cursors
-  auto issue = [&](const Cur& k, u32x4 (&r)[PT], uint32_t& cv) {
-    const uint32_t n = k.valid && k.b1 > k.c0 ? (uint32_t)min<uint64_t>(CH, k.b1 - k.c0) : 1u;
-    const uint64_t c0 = k.valid && k.b1 > k.c0 ? k.c0 : 0;
-#pragma unroll
-    for (uint32_t j = 0; j < PT; ++j) {
-      const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
-      r[j] = t4[c0 + (e < n ? e : n - 1)];
-    }
-    if (k.valid && k.first && tid < (int)NB) {
-      const uint32_t m = k.it / nbk;
-      const uint32_t p = min(k.p0 + (uint32_t)tid, (uint32_t)R - 1);
-      cv = (uint32_t)base[(uint64_t)m * R + p];
-    }
-  };
-
-  for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
-  Cur k = seg(xcd_map(blockIdx.x, G));
-  u32x4 rv[PT];
-  uint32_t cv = 0;
-  issue(k, rv, cv);
-  while (k.valid) {
-    if (k.first && tid < (int)NB) cur[tid] = cv;  // nothing reads cur until the write phase
-    const Cur nk = next(k);
-    u32x4 rn[PT];
-    uint32_t cn = cv;
-    issue(nk, rn, cn);
-    const uint32_t n = k.b1 > k.c0 ? (uint32_t)min<uint64_t>(CH, k.b1 - k.c0) : 0u;
-    uint32_t lo[PT], rank[PT];
-#pragma unroll
-    for (uint32_t j = 0; j < PT; ++j) {
-      const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
-      uint32_t w[KW];
-#pragma unroll
-      for (int q = 0; q < KW; ++q) {
-        const int d = kw0 + q;
-        w[q] = d == 0 ? rv[j][0] : d == 1 ? rv[j][1] : d == 2 ? rv[j][2] : rv[j][3];
-      }
-      lo[j] = ((uint32_t)partition_words<KW, false>(pd, w, pd.bounds, pd.lut) - k.p0) & (NB - 1);
-      rank[j] = wave_rank<kB16Lo>(lo[j], e < n, wc + wave * NB, lt_mask);
-    }
-    __syncthreads();
-    scan_digit_wave<NB, NW>(wc, wsum, tid, lane, wave);
-#pragma unroll
-    for (uint32_t j = 0; j < PT; ++j)
-      if (rank[j] != ~0u) {
-        const uint32_t pos = wc[wave * NB + lo[j]] + rank[j];
-        stage[pos] = rv[j];
-        los[pos] = (uint8_t)lo[j];
-      }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t q = 0; q < PT; ++q) {
-      const uint32_t i = tid + q * NT;
-      if (i < n) {
-        const uint32_t l = los[i];
-        const uint64_t dst = (uint64_t)cur[l] + (i - wc[l]);
-        if (dst < g.num_records) out4[dst] = stage[i];  // (a bad pid cannot fault)
-      }
-    }
-    uint32_t ncur = 0;
-    if (tid < (int)NB) {
-      const uint32_t end = (uint32_t)tid + 1 < NB ? wc[tid + 1] : n;
-      ncur = cur[tid] + (end - wc[tid]);
-    }
-    __syncthreads();
-    if (tid < (int)NB) cur[tid] = ncur;
-    for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
-    __syncthreads();
-#pragma unroll
-    for (uint32_t j = 0; j < PT; ++j) rv[j] = rn[j];
-    cv = cn;
-    k = nk;
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// Two-level (MSD) small-record map side without K1 (16-byte records, 1024 < R <= 16384,
-// map-major layout; tuning small_kernel = 4).  Every pass streams whole lines:
-//   pass A (k_msd16a) reads each 4096-record chunk once, computes every record's pid from its
-//          key, stable-sorts the chunk by bucket = pid >> 5 in LDS and writes it back to the
-//          temp copy AT THE CHUNK'S OWN POSITION (a contiguous write), with the chunk's bucket
-//          starts (u16) in offs[map][chunk][bucket];
-//   K2     (k_msd16_scan) one workgroup per map: bucket totals over the map's chunks ->
-//          segment bases segbase[map][bucket] and the index table's last entry;
-//   pass B (k_msd16b) one (map, bucket) segment at a time: the segment's runs (one ~13-record
-//          run per chunk at R = 10 000) are gathered into LDS, stable-sorted by pid & 31,
-//          written as ONE contiguous output range, and the bucket's 32 index entries (native +
-//          big-endian) are written.  A segment larger than the LDS (skewed keys) is counted
-//          first and then placed piece by piece through per-partition cursors.
-// 16 + 16 (A) and 16 + 16 (B) bytes per record, no pid array, no R-wide histogram: the
-// sorted-chunk scatter (k_hist16 + k_scatter16s) moves 19 + 54 bytes per record, 32 of them as
-// lone 16-byte stores.  Both passes run two 512-thread workgroups per CU, whose load, rank and
-// store phases interleave.  Stable: pass A keeps input order inside a bucket (chunks in order,
-// ranks in order inside a chunk), pass B keeps segment order inside a partition.
-// ------------------------------------------------------------------------------------------
-// Diagnostic build only (tools/msd_stamps.hip defines SUX_MSD_STAMPS): per-phase s_memtime
-// cycles of k_msd16b, summed per workgroup into g_msd_stamps[block][phase].
-#ifdef SUX_MSD_STAMPS
-__device__ unsigned long long* g_msd_stamps;
-#define SUX_MSD_STAMP_INIT()                 \
-  unsigned long long st_acc[5] = {0, 0, 0, 0, 0}; \
-  unsigned long long st_t = __builtin_amdgcn_s_memtime()
-#define SUX_MSD_STAMP(k)                                   \
-  do {                                                     \
-    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-    st_acc[k] += t_ - st_t;                                \
-    st_t = t_;                                             \
-  } while (0)
-#define SUX_MSD_STAMP_END()                                              \
-  do {                                                                   \
-    if (threadIdx.x == 0 && g_msd_stamps)                                \
-      for (int k_ = 0; k_ < 5; ++k_) g_msd_stamps[blockIdx.x * 8 + k_] = st_acc[k_]; \
-  } while (0)
-#else
-#define SUX_MSD_STAMP_INIT() do {} while (0)
-#define SUX_MSD_STAMP(k) do {} while (0)
-#define SUX_MSD_STAMP_END() do {} while (0)
-#endif
-constexpr uint32_t kM16Chunk = 4096;      // pass A records per chunk (the run table's unit)
-constexpr uint32_t kM16Lo = 4;            // partitions per bucket: 16
-constexpr uint32_t kM16MaxChunks = 512;   // chunks per map pass B's run table holds (2 Mi records)
-
-// Block exclusive scan, in (digit, wave) order, of u16 per-wave digit counters wc[NW][NB]
-// (NW*64 threads; each thread owns E = NB/64 consecutive (digit, wave) entries).  Counts and
-// prefixes fit u16: a chunk holds kM16Chunk records.  Two barriers; wsum[NW] scratch.
-template <uint32_t NB, uint32_t NW>
-__device__ __forceinline__ void scan_digit_wave16(uint16_t* wc, uint32_t* wsum, int tid, int lane,
-                                                  int wave) {
-  constexpr uint32_t E = NB / kWave;
-  uint32_t sum = 0;  // the entries are read twice instead of held (registers are the limit)
-#pragma unroll
-  for (uint32_t k = 0; k < E; ++k) {
-    const uint32_t idx = (uint32_t)tid * E + k, d = idx / NW, w = idx % NW;
-    sum += wc[w * NB + d];
-  }
-  const uint32_t incl = wave_incl_scan(sum, lane);
-  if (lane == kWave - 1) wsum[wave] = incl;
-  __syncthreads();
-  uint32_t run = incl - sum;
-#pragma unroll
-  for (uint32_t w = 0; w < NW; ++w) run += w < (uint32_t)wave ? wsum[w] : 0u;
-#pragma unroll
-  for (uint32_t k = 0; k < E; ++k) {
-    const uint32_t idx = (uint32_t)tid * E + k, d = idx / NW, w = idx % NW;
-    const uint32_t v = wc[w * NB + d];
-    wc[w * NB + d] = (uint16_t)run;
-    run += v;
-  }
-  __syncthreads();
-}
-
-template <uint32_t NW, uint32_t DB>  // stage[CH] u32x4 (its first NW words double as wsum) | wc[NW][2^DB] u16
-struct M16a {
-  static constexpr uint32_t NB = 1u << DB, NT = NW * kWave, PT = kM16Chunk / NT;
-  static constexpr uint32_t lds_bytes() { return kM16Chunk * 16 + NW * NB * 2; }
-};
-template <uint32_t NW, uint32_t PT>  // stage[CAP] u32x4 | wc[NW][64] | cur[64] | wsum[NW] | los[CAP] u8 | rp[MAXCH+1] u32 | ro[MAXCH] u16
-struct M16b {
-  static constexpr uint32_t NB = 64, NT = NW * kWave, CAP = NT * PT;
-  static constexpr uint32_t lds_bytes() {
-    return CAP * 16 + NW * NB * 4 + NB * 4 + NW * 4 + CAP + (kM16MaxChunks + 1) * 4 +
-           kM16MaxChunks * 2;
-  }
-};
-
-// records of map m in the group, and of its chunk c
-__device__ __forceinline__ uint32_t m16_map_len(const MapGroup& g, uint32_t m) {
-  const uint64_t b = (uint64_t)m * g.records_per_map;
-  const uint64_t e = min(b + g.records_per_map, g.num_records);
-  return (uint32_t)(e > b ? e - b : 0);
-}
-__device__ __forceinline__ uint32_t m16_chunk_len(uint32_t map_len, uint32_t c) {
-  const uint32_t b = c * kM16Chunk;
-  return map_len > b ? min(kM16Chunk, map_len - b) : 0u;
-}
-
-template <int KW>
-__device__ __forceinline__ uint32_t m16_pid(const PartDev& pd, const u32x4& r, int kw0) {
-  uint32_t w[KW];
-#pragma unroll
-  for (int q = 0; q < KW; ++q) {
-    const int d = kw0 + q;
-    w[q] = d == 0 ? r[0] : d == 1 ? r[1] : d == 2 ? r[2] : r[3];
-  }
-  return (uint32_t)partition_words<KW, false>(pd, w, pd.bounds, pd.lut);
-}
-
-template <int KW, uint32_t NW, uint32_t DB>
-__global__ __launch_bounds__(NW * 64, 4) void k_msd16a(PartDev pd, MapGroup g, uint32_t cpm,
-                                                 uint32_t nbk, uint16_t* __restrict__ offs,
-                                                 uint16_t* __restrict__ pids_out,
-                                                 uint8_t* __restrict__ tmp) {
-  using K = M16a<NW, DB>;
-  constexpr uint32_t NB = K::NB, NT = K::NT, PT = K::PT, CH = kM16Chunk;
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
-  u32x4* stage = reinterpret_cast<u32x4*>(lds8);
-  uint16_t* wc = reinterpret_cast<uint16_t*>(stage + CH);  // [NW][NB]
-  uint32_t* wsum = reinterpret_cast<uint32_t*>(lds8);       // only inside the scan: stage is idle
-  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
-  const uint64_t lt_mask = (1ull << lane) - 1ull;
-  const int kw0 = pd.key_offset / 4;
-  const u32x4* recs = reinterpret_cast<const u32x4*>(g.recs);
-  u32x4* t4 = reinterpret_cast<u32x4*>(tmp);
-  // one contiguous, balanced range of (map, chunk) items per workgroup
-  const uint32_t items = g.num_maps * cpm, G = gridDim.x, b = xcd_map(blockIdx.x, G);
-  const uint32_t it0 = (uint32_t)((uint64_t)items * b / G), it1 = (uint32_t)((uint64_t)items * (b + 1) / G);
-  struct Item {
-    uint64_t c0;  // first record of the chunk (group index)
-    uint32_t n;   // its records (0 past the range)
-  };
-  auto item = [&](uint32_t it) {
-    const uint32_t m = it / cpm, c = it - m * cpm;
-    Item k;
-    k.c0 = (uint64_t)m * g.records_per_map + (uint64_t)c * CH;
-    k.n = it < it1 ? m16_chunk_len(m16_map_len(g, m), c) : 0u;
-    return k;
-  };
-  auto load = [&](const Item& k, u32x4 (&r)[PT]) {
-    if (k.n == 0) return;
-#pragma unroll
-    for (uint32_t j = 0; j < PT; ++j) {  // unconditional (clamped) loads: no per-load wait
-      const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
-      r[j] = recs[k.c0 + min(e, k.n - 1)];
-    }
-  };
-  for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
-  __syncthreads();
-  u32x4 rv[PT];
-  for (uint32_t it = it0; it < it1; ++it) {
-    const Item k = item(it);
-    load(k, rv);
-    uint32_t h[PT], rank[PT];
-#pragma unroll
-    for (uint32_t j = 0; j < PT; ++j) {
-      const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
-      const bool valid = e < k.n;
-      uint32_t p = 0;
-      if (valid) {
-        p = m16_pid<KW>(pd, rv[j], kw0);
-        if (pids_out) pids_out[k.c0 + e] = (uint16_t)p;
-      }
-      h[j] = (p >> kM16Lo) & (NB - 1);
-      rank[j] = wave_rank<DB, uint16_t>(h[j], valid, wc + wave * NB, lt_mask);
-    }
-    __syncthreads();
-    scan_digit_wave16<NB, NW>(wc, wsum, tid, lane, wave);
-#pragma unroll
-    for (uint32_t j = 0; j < PT; ++j)
-      if (rank[j] != ~0u) stage[wc[wave * NB + h[j]] + rank[j]] = rv[j];
-    __syncthreads();
-    // the chunk goes back to its own place, in bucket order: one contiguous write
-#pragma unroll
-    for (uint32_t q = 0; q < PT; ++q) {
-      const uint32_t i = tid + q * NT;
-      if (i < k.n) t4[k.c0 + i] = stage[i];
-    }
-    for (uint32_t hb = tid; hb < nbk; hb += NT)
-      offs[(uint64_t)it * nbk + hb] = (uint16_t)wc[hb];  // wc[0][hb]: bucket start in the chunk
-    __syncthreads();
-    for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
-    __syncthreads();
-  }
-}
-
-// K2 of the MSD path: one workgroup (kScanThreads) per map.  Bucket totals over the map's chunks
-// (one thread per bucket), exclusive scan over buckets ->
-// segbase[m][h] (record index in the group's output), the index table's last entry and, at
-// world 1, the peer byte count.
-__global__ __launch_bounds__(kScanThreads) void k_msd16_scan(MapGroup g, uint32_t cpm, uint32_t nbk,
-                                                             const uint16_t* __restrict__ offs,
-                                                             uint64_t* __restrict__ segbase,
-                                                             int64_t* __restrict__ index,
-                                                             uint8_t* __restrict__ index_be,
-                                                             uint64_t* __restrict__ peer_bytes,
-                                                             int R) {
-  constexpr uint32_t HG = 1024, NG = kScanThreads / HG;  // one thread per bucket (nbk <= 1024)
-  __shared__ uint64_t sh[2 * kWave + 1];
-  __shared__ uint32_t part[kScanThreads];
-  const uint32_t m = blockIdx.x, tid = threadIdx.x;
-  const uint32_t len = m16_map_len(g, m), nch = (len + kM16Chunk - 1) / kM16Chunk;
-  const uint32_t h = tid % HG, cg = tid / HG;
-  uint32_t t = 0;
-  if (h < nbk) {
-    const uint16_t* om = offs + (uint64_t)m * cpm * nbk;
-    for (uint32_t c = cg; c < nch; c += NG) {
-      const uint32_t o = om[(uint64_t)c * nbk + h];
-      const uint32_t e = h + 1 < nbk ? om[(uint64_t)c * nbk + h + 1] : m16_chunk_len(len, c);
-      t += e - o;
-    }
-  }
-  part[tid] = t;
-  __syncthreads();
-  uint64_t v = 0;
-  if (tid < HG)
-    for (uint32_t q = 0; q < NG; ++q) v += part[tid + q * HG];
-  uint64_t tot;
-  const uint64_t ex = block_excl_scan(tid < nbk ? v : 0, sh, &tot);
-  if (tid < nbk) segbase[(uint64_t)m * nbk + tid] = (uint64_t)m * g.records_per_map + ex;
-  if (tid == 0) {
-    const int64_t off = (int64_t)len * g.rec_size;
-    index[(uint64_t)m * (R + 1) + R] = off;
-    if (index_be) reinterpret_cast<uint64_t*>(index_be)[(uint64_t)m * (R + 1) + R] = bswap64((uint64_t)off);
-    if (m == 0 && peer_bytes) peer_bytes[0] = g.num_records * g.rec_size;
-  }
-}
-
-template <int KW, uint32_t NW, uint32_t PT>
-__global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, uint32_t cpm,
-                                                 uint32_t nbk, const uint16_t* __restrict__ offs,
-                                                 const uint64_t* __restrict__ segbase,
-                                                 const uint8_t* __restrict__ tmp,
-                                                 uint8_t* __restrict__ out,
-                                                 int64_t* __restrict__ index,
-                                                 uint8_t* __restrict__ index_be) {
-  using K = M16b<NW, PT>;
-  constexpr uint32_t NB = K::NB, NT = K::NT, CAP = K::CAP, MC = kM16MaxChunks, PB = 1u << kM16Lo;
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
-  u32x4* stage = reinterpret_cast<u32x4*>(lds8);
-  uint32_t* wc = reinterpret_cast<uint32_t*>(stage + CAP);  // [NW][NB]
-  uint32_t* cur = wc + NW * NB;
-  uint32_t* wsum = cur + NB;
-  uint8_t* los = reinterpret_cast<uint8_t*>(wsum + NW);
-  uint32_t* rp = reinterpret_cast<uint32_t*>(los + CAP);   // [MC + 1] run starts in the segment
-  uint16_t* ro = reinterpret_cast<uint16_t*>(rp + MC + 1);  // [MC] run starts in their chunk
-  const int R = pd.R;
-  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
-  const uint64_t lt_mask = (1ull << lane) - 1ull;
-  const int kw0 = pd.key_offset / 4;
-  const u32x4* t4 = reinterpret_cast<const u32x4*>(tmp);
-  u32x4* out4 = reinterpret_cast<u32x4*>(out);
-  uint64_t* ibe = reinterpret_cast<uint64_t*>(index_be);
-  const uint32_t items = g.num_maps * nbk, G = gridDim.x, b = xcd_map(blockIdx.x, G);
-  // segments dealt round robin (segment it to workgroup it % G, an XCD's workgroups taking
-  // consecutive segments): at any moment the grid works on ~G consecutive segments, i.e. on
-  // every bucket of a map or two, so the runs it gathers cover whole chunks of the temp copy
-  // (DRAM rows and L2 lines shared by neighbouring runs are read together), and the outputs it
-  // writes are adjacent.  (One contiguous range of segments per workgroup: 2.45 TB/s.)
-  const uint32_t it0 = b, it1 = items;
-
-  struct Seg {
-    uint32_t m, h, nch, T, len;
-    uint64_t mbase, out;  // first record of map m, first output record of the segment
-  };
-  // the global reads a segment's run table starts from (offs pair of chunk tid, segment base),
-  // issued one segment ahead so that build() does not wait for them
-  struct Pre {
-    uint32_t o, e;
-    uint64_t sb;
-  };
-  auto seg = [&](uint32_t it) {
-    Seg s;
-    s.m = it / nbk;
-    s.h = it - s.m * nbk;
-    s.len = m16_map_len(g, s.m);
-    s.nch = (s.len + kM16Chunk - 1) / kM16Chunk;
-    s.mbase = (uint64_t)s.m * g.records_per_map;
-    return s;
-  };
-  auto run_ends = [&](const Seg& s, uint32_t c, uint32_t& o, uint32_t& e) {
-    const uint16_t* oc = offs + ((uint64_t)s.m * cpm + c) * nbk;
-    o = oc[s.h];
-    e = s.h + 1 < nbk ? oc[s.h + 1] : m16_chunk_len(s.len, c);
-  };
-  auto prefetch = [&](uint32_t it) {
-    Pre p{0, 0, 0};
-    if (it < it1) {
-      const Seg s = seg(it);
-      if ((uint32_t)tid < s.nch) run_ends(s, tid, p.o, p.e);
-      p.sb = segbase[it];
-    }
-    return p;
-  };
-  // run table of segment `it` (run c = the bucket's records of chunk c; rp = exclusive prefix
-  // over chunks); all threads, barriers inside
-  auto build = [&](uint32_t it, const Pre& pre) {
-    Seg s = seg(it);
-    s.out = pre.sb;
-    uint32_t carry = 0;
-    // the last batch's thread 0 also writes rp[nch] = T, the search's sentinel (no extra batch
-    // when nch is a multiple of the workgroup: 2^20-record maps have exactly 256 chunks)
-    for (uint32_t c0 = 0; c0 < s.nch; c0 += NT) {
-      const uint32_t c = c0 + (uint32_t)tid;
-      uint32_t o = pre.o, e = pre.e;
-      if (c0 && c < s.nch) run_ends(s, c, o, e);
-      const uint32_t cnt = c < s.nch ? e - o : 0u;
-      const uint32_t incl = wave_incl_scan(cnt, lane);
-      if (lane == kWave - 1) wsum[wave] = incl;
-      __syncthreads();
-      uint32_t run = carry + incl - cnt, blk = 0;
-#pragma unroll
-      for (uint32_t w = 0; w < NW; ++w) {
-        run += w < (uint32_t)wave ? wsum[w] : 0u;
-        blk += wsum[w];
-      }
-      if (c < s.nch) {
-        ro[c] = (uint16_t)o;
-        rp[c] = run;
-      }
-      if (tid == 0 && c0 + NT >= s.nch) rp[s.nch] = carry + blk;
-      carry += blk;
-      __syncthreads();
-    }
-    s.T = carry;
-    return s;
-  };
-  // loads of segment elements [e0, min(T, e0 + CAP)) in wave-contiguous order
-  auto load = [&](const Seg& s, uint32_t e0, u32x4 (&r)[PT]) {
-    const uint32_t lim = min(s.T, e0 + CAP);
-    if (lim <= e0) return;
-    // element e's run = the largest c with rp[c] <= e: a branch-free search whose PT lookups
-    // interleave step by step (rp[nch] = T > e stops every search inside the segment).  Lanes
-    // past the piece re-read its last element: the loads are unconditional — a load under a
-    // branch made the compiler wait for every earlier load before the next one's address
-    // (s_waitcnt vmcnt(0) per element), serialising the gather.
-    uint32_t lo[PT], ev[PT];
-#pragma unroll
-    for (uint32_t j = 0; j < PT; ++j) {
-      lo[j] = 0;
-      ev[j] = min(e0 + wave * (PT * kWave) + j * kWave + lane, lim - 1);
-    }
-#pragma unroll
-    for (uint32_t step = MC / 2; step; step >>= 1) {
-      uint32_t v[PT];
-#pragma unroll
-      for (uint32_t j = 0; j < PT; ++j) v[j] = rp[min(lo[j] + step, s.nch)];
-#pragma unroll
-      for (uint32_t j = 0; j < PT; ++j) lo[j] = v[j] <= ev[j] ? min(lo[j] + step, s.nch) : lo[j];
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < PT; ++j) {
-#ifdef SUX_MSD_LINEAR  // diagnostic (tools/msd_stamps): contiguous in-map reads, wrong data
-      r[j] = t4[s.mbase + ((uint64_t)s.h * 3350 + ev[j]) % s.len];
-#else
-      r[j] = t4[s.mbase + (uint64_t)lo[j] * kM16Chunk + ro[lo[j]] + (ev[j] - rp[lo[j]])];
-#endif
-    }
-  };
-  auto digit = [&](const Seg& s, const u32x4& r) {
-    return (m16_pid<KW>(pd, r, kw0) - (s.h << kM16Lo)) & (NB - 1);
-  };
-  // stable rank by pid & 31 -> stage/los in sorted order; wc[0][l] = digit starts afterwards
-  auto rank_stage = [&](const Seg& s, uint32_t n, const u32x4 (&r)[PT]) {
-    uint32_t lo[PT], rk[PT];
-#pragma unroll
-    for (uint32_t j = 0; j < PT; ++j) {
-      const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
-      const bool valid = e < n;
-      lo[j] = valid ? digit(s, r[j]) : 0u;
-      rk[j] = wave_rank<kM16Lo>(lo[j], valid, wc + wave * NB, lt_mask);
-    }
-    __syncthreads();
-    scan_digit_wave<NB, NW>(wc, wsum, tid, lane, wave);
-#pragma unroll
-    for (uint32_t j = 0; j < PT; ++j)
-      if (rk[j] != ~0u) {
-        const uint32_t pos = wc[wave * NB + lo[j]] + rk[j];
-        stage[pos] = r[j];
-        los[pos] = (uint8_t)lo[j];
-      }
-  };
-  auto write_index = [&](const Seg& s, uint32_t start_l) {
-    const uint64_t seg_out = s.out;
-    const uint32_t p = (s.h << kM16Lo) + (uint32_t)tid;  // in-segment record offset of partition p
-    if (tid < (int)PB && p < (uint32_t)R) {
-      const int64_t off = (int64_t)((seg_out - s.mbase + start_l) * g.rec_size);
-      index[(uint64_t)s.m * (R + 1) + p] = off;
-      if (ibe) ibe[(uint64_t)s.m * (R + 1) + p] = bswap64((uint64_t)off);
-    }
-  };
-  // sorted stage -> output through the per-partition cursors; cursors advance; wc cleared
-  auto place = [&](const Seg& s, uint32_t n) {
-#pragma unroll
-    for (uint32_t q = 0; q < PT; ++q) {
-      const uint32_t i = tid + q * NT;
-      if (i < n) {
-        const uint32_t l = los[i];
-        out4[s.mbase + cur[l] + (i - wc[l])] = stage[i];
-      }
-    }
-    uint32_t ncur = 0;
-    if (tid < (int)NB) ncur = cur[tid] + ((uint32_t)tid + 1 < NB ? wc[tid + 1] : n) - wc[tid];
-    __syncthreads();
-    if (tid < (int)NB) cur[tid] = ncur;
-    for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
-    __syncthreads();
-  };
-
-  for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
-  __syncthreads();
-  if (it0 >= it1) return;
-  Seg s = build(it0, prefetch(it0));
-  u32x4 rv[PT];
-  SUX_MSD_STAMP_INIT();
-  for (uint32_t it = it0; it < it1; it += G) {
-    const uint32_t seg_rel = (uint32_t)(s.out - s.mbase);  // in-map record offset of the segment
-    const bool multi = s.T > CAP;
-    if (multi) {
-      // larger than the LDS (skewed keys): count the digits first, then place piece by piece
-      for (uint32_t e0 = 0; e0 < s.T; e0 += CAP) {
-        load(s, e0, rv);
-        const uint32_t n = min(CAP, s.T - e0);
-#pragma unroll
-        for (uint32_t j = 0; j < PT; ++j) {
-          const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
-          if (e < n) atomicAdd(&wc[wave * NB + digit(s, rv[j])], 1u);
-        }
-      }
-      __syncthreads();
-      scan_digit_wave<NB, NW>(wc, wsum, tid, lane, wave);
-      if (tid < (int)NB) cur[tid] = seg_rel + wc[tid];
-      write_index(s, tid < (int)NB ? wc[tid] : 0u);
-      __syncthreads();
-      for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
-      __syncthreads();
-    }
-    // one piece (the whole segment) unless multi; an empty segment still writes its index
-    for (uint32_t e0 = 0; e0 == 0 || e0 < s.T; e0 += CAP) {
-      load(s, e0, rv);
-      SUX_MSD_STAMP(0);
-      const uint32_t n = min(CAP, s.T - e0);
-      rank_stage(s, n, rv);
-      __syncthreads();
-      SUX_MSD_STAMP(1);
-      if (!multi) {
-        if (tid < (int)NB) cur[tid] = seg_rel + wc[tid];
-        write_index(s, tid < (int)NB ? wc[tid] : 0u);
-      }
-      __syncthreads();
-      SUX_MSD_STAMP(2);
-      place(s, n);
-      SUX_MSD_STAMP(3);
-    }
-    if (it + G < it1) s = build(it + G, prefetch(it + G));
-    SUX_MSD_STAMP(4);
-  }
-  SUX_MSD_STAMP_END();
-}
-
-// ------------------------------------------------------------------------------------------
-// Reduce-side sort, MSD finish (sux_sort_records / sux_sort_segments): one stable digit pass
-// over the top bits of the keys' varying range leaves R buckets of <= kSortLocalCap pairs
-// (checked on the host); k_sort_local then sorts every bucket inside LDS by a stable LSD radix
-// over the lower key digits that vary (8-bit digits: wave-ballot ranks + one block scan per
-// digit; the pairs live in registers, one LDS buffer takes each digit's permutation) and writes
-// it back.  Each pair crosses HBM twice
-// after the top pass instead of twice per digit.  Stable: the top pass keeps input order inside
-// a bucket and every LDS pass is stable.
-// ------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t pair_digit8(const u32x4& w, uint32_t sh) {
-  const uint64_t hi = ((uint64_t)__builtin_bswap32(w[0]) << 32) | __builtin_bswap32(w[1]);
-  const uint64_t lo = ((uint64_t)__builtin_bswap32(w[2]) << 32) | __builtin_bswap32(w[3]);
-  const uint64_t v = sh >= 64 ? (hi >> (sh - 64)) : ((lo >> sh) | (sh ? (hi << (64 - sh)) : 0));
-  return (uint32_t)v & 255u;
-}
-
-template <uint32_t NW, uint32_t CAP>  // buf[CAP] u32x4 | wc[NW][256] u32 | wsum[NW]
-struct SortLocal {
-  static constexpr uint32_t NT = NW * kWave, PT = CAP / NT, NB = 256;
-  static constexpr uint32_t lds_bytes() { return CAP * 16 + NW * NB * 4 + NW * 4; }
-};
-
-// <8 waves, 4096 pairs>: two workgroups per CU; <4 waves, 1024 pairs>: six per CU, for the
-// ~600-pair buckets of a 5 M-record reduce partition
-template <uint32_t NW, uint32_t CAP>
-__global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : CAP == 1024 ? 6 : 4) void k_sort_local(const u32x4* __restrict__ in,
-                                                        u32x4* __restrict__ out,
-                                                        const int64_t* __restrict__ index,
-                                                        uint32_t R, SortDigits dg) {
-  using K = SortLocal<NW, CAP>;
-  constexpr uint32_t NT = K::NT, PT = K::PT, NB = K::NB;
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
-  u32x4* buf = reinterpret_cast<u32x4*>(lds8);
-  uint32_t* wc = reinterpret_cast<uint32_t*>(buf + CAP);  // [NW][NB]
-  uint32_t* wsum = wc + NW * NB;
-  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
-  const uint64_t lt_mask = (1ull << lane) - 1ull;
-  for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
-  __syncthreads();
-  for (uint32_t b = xcd_map(blockIdx.x, gridDim.x); b < R; b += gridDim.x) {
-    const uint64_t s0 = (uint64_t)index[b] / 16, s1 = (uint64_t)index[b + 1] / 16;
-    const uint32_t n = (uint32_t)(s1 - s0);
-    if (n == 0 || n > CAP) continue;  // (the host never passes a bucket above CAP)
-    u32x4 v[PT];
-#pragma unroll
-    for (uint32_t j = 0; j < PT; ++j) {  // unconditional (clamped) loads: no per-load wait
-      const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
-      v[j] = in[s0 + min(e, n - 1)];
-    }
-#pragma unroll 1
-    for (int d = 0; d < (n > 1 ? dg.n : 0); ++d) {
-      const uint64_t w = d < 8 ? dg.lo : dg.hi;  // shifts packed 8 bits apiece
-      const uint32_t sh = (uint32_t)(w >> (8 * (d & 7))) & 255u;
-      uint32_t dig[PT], rank[PT];
-#pragma unroll
-      for (uint32_t j = 0; j < PT; ++j) {
-        const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
-        const bool valid = e < n;
-        dig[j] = valid ? pair_digit8(v[j], sh) : 0u;
-        rank[j] = wave_rank<8>(dig[j], valid, wc + wave * NB, lt_mask);
-      }
-      __syncthreads();
-      scan_digit_wave<NB, NW>(wc, wsum, tid, lane, wave);
-#pragma unroll
-      for (uint32_t j = 0; j < PT; ++j)
-        if (rank[j] != ~0u) buf[wc[wave * NB + dig[j]] + rank[j]] = v[j];
-      __syncthreads();
-      for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
-      // the next digit ranks the pairs in this digit's order: reload them, wave-contiguous
-#pragma unroll
-      for (uint32_t j = 0; j < PT; ++j) {
-        const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
-        if (e < n) v[j] = buf[e];
-      }
-      __syncthreads();  // every pair is back in registers before the next digit rewrites buf
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < PT; ++j) {
-      const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
-      if (e < n) out[s0 + e] = v[j];
-    }
-  }
-}
-
-// Largest bucket of an index table, in records of 16 bytes: one workgroup.
-__global__ __launch_bounds__(1024) void k_index_maxdiff(const int64_t* __restrict__ index,
-                                                        uint32_t R, uint64_t* __restrict__ out) {
-  __shared__ unsigned long long m;
-  if (threadIdx.x == 0) m = 0;
-  __syncthreads();
-  unsigned long long local = 0;
-  for (uint32_t p = threadIdx.x; p < R; p += 1024)
-    local = max(local, (unsigned long long)((index[p + 1] - index[p]) / 16));
-  atomicMax(&m, local);
-  __syncthreads();
-  if (threadIdx.x == 0) *out = m;
-}
-
-hipError_t launch_sort_local(const void* in_pairs, void* out_pairs, const int64_t* d_index,
-                             uint32_t R, const SortDigits& dg, uint64_t* d_maxbucket, bool max_only,
-                             hipStream_t s) {
-  if (max_only) {
-    hipLaunchKernelGGL(k_index_maxdiff, dim3(1), dim3(1024), 0, s, d_index, R, d_maxbucket);
-    return hipGetLastError();
-  }
-  const uint32_t ncu = (uint32_t)std::max(1, stream_cus(s));
-  // the smallest shape holding the largest bucket (d_maxbucket carries it, host-read, in
-  // SortDigits::pad)
-  if (dg.pad <= 1024) {
-    constexpr size_t lds = SortLocal<4, 1024>::lds_bytes();
-    hipLaunchKernelGGL((k_sort_local<4, 1024>), dim3(std::min<uint32_t>(R, 6 * ncu)), dim3(4 * kWave),
-                       lds, s, static_cast<const u32x4*>(in_pairs), static_cast<u32x4*>(out_pairs),
-                       d_index, R, dg);
-  } else if (dg.pad <= 2048) {
-    constexpr size_t lds = SortLocal<4, 2048>::lds_bytes();
-    static_assert(4 * lds <= 160 * 1024, "four workgroups per CU");
-    hipLaunchKernelGGL((k_sort_local<4, 2048>), dim3(std::min<uint32_t>(R, 4 * ncu)), dim3(4 * kWave),
-                       lds, s, static_cast<const u32x4*>(in_pairs), static_cast<u32x4*>(out_pairs),
-                       d_index, R, dg);
-  } else {
-    constexpr size_t lds = SortLocal<8, kSortLocalCap>::lds_bytes();
-    static_assert(2 * lds <= 160 * 1024, "two workgroups per CU");
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_local<8, kSortLocalCap>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((k_sort_local<8, kSortLocalCap>), dim3(std::min<uint32_t>(R, 2 * ncu)),
-                       dim3(8 * kWave), lds, s, static_cast<const u32x4*>(in_pairs),
-                       static_cast<u32x4*>(out_pairs), d_index, R, dg);
-  }
-  return hipGetLastError();
-}
-
 template <int KW, bool TAB>
 static void launch_hist3_kw(dim3 grid, size_t lds, hipStream_t s, const PartDev& pd,
                             const MapGroup& g, uint16_t* pids, uint32_t* counts) {
@@ -3095,11 +1570,8 @@ uint32_t choose_tile_recs(uint32_t R, uint32_t rec_size, uint64_t records_per_ma
   uint32_t t = 4096;
   while (t < 4u * R && t < (1u << 22)) t <<= 1;
   // small records, many partitions: the sorted-chunk scatter re-reads R cursors per tile
-  // (32 Ki records measured best at R = 10000, profiles/r02_small_b); the two-pass scatter's
-  // pass A walks whole tiles too (one tile per persistent workgroup at a time: a launch group
-  // needs >> 256 tiles)
+  // (32 Ki records measured best at R = 10000, profiles/r02_small_b)
   if (small_two_pass_shape(R, rec_size) && tn.small_kernel == 2) t = 32768;
-  if (small_two_pass_shape(R, rec_size) && tn.small_kernel == 3) t = 32768;
   // very long maps: longer tiles, so that a map has <= 2048 of them — k_tile_scan gives one wave
   // to each (map, partition) row of tile counts, and a 2^27-record map at 4096-record tiles has
   // 32768 per row (3.9 ms of scan per 13.4 GB launch group, profiles/r02_configs)
@@ -3139,7 +1611,7 @@ Workspace workspace_layout(uint32_t R, uint32_t rec_size, uint64_t records_per_m
   w.op_off = off;
   w.op_bytes = (rec_size == 100 && R <= 1024) ? onepass_sync_bytes(R) : 0;
   off += w.op_bytes;
-  w.tmp_off = off;  // the two-pass small-record scatter's bucketed copy of the records
+  w.tmp_off = off;  // the two-level small-record path's chunk-sorted copy of the records
   w.tmp_bytes = small_tmp ? align_up(num_records * rec_size, 256) : 0;
   off += w.tmp_bytes;
   w.total = off;
@@ -3147,12 +1619,6 @@ Workspace workspace_layout(uint32_t R, uint32_t rec_size, uint64_t records_per_m
 }
 
 static int waves_per_group(int R) { return (R * 4 * 4 <= 64 * 1024) ? 4 : 1; }
-
-// Dynamic LDS above 64 KiB must be opted into per kernel (gfx950 allows 160 KiB per workgroup).
-static void allow_lds(const void* fn, size_t lds) {
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-}
 
 template <int WPG>
 static hipError_t launch_scatter(uint32_t S, dim3 grid, size_t lds, hipStream_t s, const MapGroup& g,
@@ -3175,31 +1641,6 @@ static hipError_t launch_scatter(uint32_t S, dim3 grid, size_t lds, hipStream_t 
                          prefix, base, out);
   }
   return hipGetLastError();
-}
-
-// The MSD small-record path (k_msd16a / k_msd16_scan / k_msd16b) applies: tuning small_kernel 4,
-// 16-byte records with a fixed-width key in the first 16 bytes, 1024 < R <= 16384, 16-byte
-// aligned input and output, map-major layout, maps of <= kM16MaxChunks chunks, and a workspace
-// with the temp copy (its chunk-offset table lives in the counts region, the segment bases in
-// the totals region).
-static bool msd16_eligible(const PartDev& pd, const MapGroup& g, const LayoutDesc& lay,
-                           const uint8_t* d_out, const Workspace& ws, const Tuning& tn) {
-  if (tn.small_kernel != 4 || g.rec_size != 16 || lay.world != 1) return false;
-  if (pd.R <= 1024 || pd.R > 16384 || pd.kind == 4 || pd.key_offset % 4 != 0 ||
-      pd.key_offset + pd.key_len > 16)
-    return false;
-  if (((reinterpret_cast<uintptr_t>(g.recs) | reinterpret_cast<uintptr_t>(d_out)) & 15) != 0)
-    return false;
-  const uint64_t cpm = (g.records_per_map + kM16Chunk - 1) / kM16Chunk;
-  const uint64_t nbk = ((uint64_t)pd.R + (1u << kM16Lo) - 1) >> kM16Lo;
-  // by default only when a (map, bucket) segment holds >= 1024 records on average: a segment
-  // costs ~6 us of run table, search and barriers whatever its size, so short maps run the
-  // sorted-chunk scatter instead (64 Ki-record maps at R = 10 000: 105-record segments, 194 vs
-  // 507 GB/s; 2^20-record maps: 1677-record segments, 1027 vs 750 GB/s)
-  if (tn.small_auto && g.records_per_map < 1024 * nbk) return false;
-  return cpm >= 1 && cpm <= kM16MaxChunks && ws.tmp_bytes >= g.num_records * 16 &&
-         (uint64_t)g.num_maps * cpm * nbk * 2 <= ws.counts_bytes &&
-         (uint64_t)g.num_maps * nbk * 8 <= ws.totals_bytes;
 }
 
 hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g_in, const LayoutDesc& lay,
@@ -3232,71 +1673,9 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g_in, const
   uint16_t* pids = d_pids ? d_pids : reinterpret_cast<uint16_t*>(d_ws + ws.pids_off);
 
   // ---- small records, many partitions, map-major: the two-level path without K1 (k_msd16*)
-  if (msd16_eligible(pd, g, lay, d_out, ws, tn)) {
-    const uint32_t cpm = (uint32_t)((g.records_per_map + kM16Chunk - 1) / kM16Chunk);
-    const uint32_t nbk = ((uint32_t)R + (1u << kM16Lo) - 1) >> kM16Lo;
-    uint16_t* offs = reinterpret_cast<uint16_t*>(counts);  // [map][chunk][bucket]
-    uint64_t* segbase = totals;                              // [map][bucket]
-    uint8_t* tmp = d_ws + ws.tmp_off;
-    const int kw = (pd.key_len + 3) / 4;
-    // two 512-thread workgroups per CU in both passes: their load / rank / store phases
-    // interleave (one prefetching 1024-thread workgroup measured slower: 9.4 vs 8.4 ms of
-    // pass A per 17 GB step, and pass B spills; profiles/r02_sweeps/msd)
-    constexpr uint32_t NWA = 8, NWB = 4, PTB = 8;
-    timer_note(timer, kHist, "k_msd16a");
-    timer_begin(timer, kHist, s);
-    const uint32_t wpc = (uint32_t)tn.small_wgs_per_cu;
-    const dim3 ga(std::min<uint32_t>(g.num_maps * cpm, ncu * wpc));
-#define SUX_M16A(KW, DB)                                                                           \
-  do {                                                                                             \
-    constexpr size_t ldsa = M16a<NWA, DB>::lds_bytes();                                            \
-    allow_lds(reinterpret_cast<const void*>(&k_msd16a<KW, NWA, DB>), ldsa);                        \
-    hipLaunchKernelGGL((k_msd16a<KW, NWA, DB>), ga, dim3(NWA * kWave), ldsa, s, pd, g, cpm, nbk,   \
-                       offs, d_pids, tmp);                                                         \
-  } while (0)
-#define SUX_M16AK(DB)                   \
-  do {                                  \
-    if (kw <= 1) SUX_M16A(1, DB);       \
-    else if (kw == 2) SUX_M16A(2, DB);  \
-    else if (kw == 3) SUX_M16A(3, DB);  \
-    else SUX_M16A(4, DB);               \
-  } while (0)
-    if (nbk > 512) SUX_M16AK(10);
-    else if (nbk > 256) SUX_M16AK(9);
-    else SUX_M16AK(8);
-#undef SUX_M16AK
-#undef SUX_M16A
-    timer_end(timer, kHist, s);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    timer_note(timer, kScan, "k_msd16_scan");
-    timer_begin(timer, kScan, s);
-    hipLaunchKernelGGL(k_msd16_scan, dim3(g.num_maps), dim3(kScanThreads), 0, s, g, cpm, nbk, offs,
-                       segbase, d_index, d_index_be, d_peer_bytes, R);
-    timer_end(timer, kScan, s);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    timer_note(timer, kScatter, "k_msd16b");
-    timer_begin(timer, kScatter, s);
-    // pass B's 256-thread workgroups are half the size of pass A's: twice as many per CU
-    const dim3 gb(std::min<uint32_t>(g.num_maps * nbk, ncu * 2 * wpc));
-    constexpr size_t ldsb = M16b<NWB, PTB>::lds_bytes();
-    static_assert(4 * ldsb <= 160 * 1024, "pass B: four workgroups per CU");
-    static_assert(2 * M16a<NWA, 10>::lds_bytes() <= 160 * 1024, "pass A: two workgroups per CU");
-#define SUX_M16B(KW)                                                                               \
-  do {                                                                                             \
-    allow_lds(reinterpret_cast<const void*>(&k_msd16b<KW, NWB, PTB>), ldsb);                      \
-    hipLaunchKernelGGL((k_msd16b<KW, NWB, PTB>), gb, dim3(NWB * kWave), ldsb, s, pd, g, cpm, nbk,  \
-                       offs, segbase, tmp, d_out, d_index, d_index_be);                            \
-  } while (0)
-    if (kw <= 1) SUX_M16B(1);
-    else if (kw == 2) SUX_M16B(2);
-    else if (kw == 3) SUX_M16B(3);
-    else SUX_M16B(4);
-#undef SUX_M16B
-    timer_end(timer, kScatter, s);
-    return hipGetLastError();
-  }
+  if (msd16_eligible(pd, g, lay, d_out, ws, tn))
+    return launch_msd16(pd, g, d_out, d_index, d_index_be, d_pids, d_ws, ws, d_peer_bytes, tn,
+                        timer, s);
   int bits = 0;
   while ((1 << bits) < R) ++bits;
   const int wpg = waves_per_group(R);
@@ -3329,7 +1708,6 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g_in, const
                   Sc7<100, 1024, 16>::lds_bytes(R) <= 160 * 1024;
   // ---- K1: pids + tile histograms
   const int hv = tn.hist_kernel;
-  const bool shaped = (S == 100 || S == 16) && R <= 4096;  // v2 instantiations
   const bool words = pd.kind != 4 && pd.key_offset % 4 == 0 && pd.key_len <= 16;
   // small records with many partitions: k_hist16 + tile-major counts + k_scatter16, together
   const bool s16 = hv >= 4 && sv >= 7 && words && S == 16 && R > 1024 &&
@@ -3339,27 +1717,15 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g_in, const
   if (s16) hist = 16;
   else if (hv >= 4 && words && R <= 4096 && S == 100 && (pd.key_offset + pd.key_len) <= (int)S) hist = 4;
   else if (hv >= 3 && words && R <= 4096) hist = 3;
-  else if (hv >= 2 && shaped) hist = 2;
   // k_hist4 feeding k_scatter7/8: tile-major counts (one contiguous store per tile; k_hist4 with
   // strided counts wrote ~2 B per record in partial-line dword stores, profiles/pmc_r02.json)
   g.counts_tm = (hist == 4 && (v8 || v7) && tn.counts_tm) ? 1u : 0u;
   timer_note(timer, kHist, hist == 16 ? "k_hist16" : hist == 4 ? "k_hist4" : hist == 3 ? "k_hist3"
-                          : hist == 2 ? "k_hist2" : "k_hist");
+                                                                               : "k_hist");
   timer_begin(timer, kHist, s);
+  hipError_t e = hipSuccess;
   if (hist == 16) {
-    const size_t lds = (size_t)R * 4;
-    const int kw = (pd.key_len + 3) / 4;
-    const dim3 gridp(std::min<uint32_t>(total_tiles, ncu * std::max<uint32_t>(1, (160u * 1024) / (uint32_t)lds)));
-#define SUX_H16(KW)                                                                        \
-  do {                                                                                     \
-    allow_lds(reinterpret_cast<const void*>(&k_hist16<KW>), lds);                          \
-    hipLaunchKernelGGL((k_hist16<KW>), gridp, dim3(1024), lds, s, pd, g, pids, counts);     \
-  } while (0)
-    if (kw <= 1) SUX_H16(1);
-    else if (kw == 2) SUX_H16(2);
-    else if (kw == 3) SUX_H16(3);
-    else SUX_H16(4);
-#undef SUX_H16
+    e = launch_hist16(pd, g, pids, counts, s);
   } else if (hist == 4) {
     const int hch = tn.hist_stage;
     const bool tab = pd.kind == 1 && R > 1 &&
@@ -3410,14 +1776,6 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g_in, const
     else if (kw == 3) SUX_H3(3);
     else SUX_H3(4);
 #undef SUX_H3
-  } else if (hist == 2) {
-    const size_t lds = 4 * (size_t)(S == 100 ? hist2_wave_bytes<100, 128>(R) : hist2_wave_bytes<16, 512>(R));
-    allow_lds(reinterpret_cast<const void*>(&k_hist2<100, 128>), lds);
-    allow_lds(reinterpret_cast<const void*>(&k_hist2<16, 512>), lds);
-    if (S == 100)
-      hipLaunchKernelGGL((k_hist2<100, 128>), grid4, dim3(256), lds, s, pd, g, pids, counts);
-    else
-      hipLaunchKernelGGL((k_hist2<16, 512>), grid4, dim3(256), lds, s, pd, g, pids, counts);
   } else {
     allow_lds(reinterpret_cast<const void*>(&k_hist<1>), lds1);
     if (wpg == 4)
@@ -3426,7 +1784,7 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g_in, const
       hipLaunchKernelGGL((k_hist<1>), grid1, dim3(kWave), lds1, s, pd, g, pids, counts);
   }
   timer_end(timer, kHist, s);
-  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipGetLastError();
   if (e != hipSuccess) return e;
 
   // ---- K2: scans -> index tables + destination bases
@@ -3457,75 +1815,15 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g_in, const
   e = hipGetLastError();
   if (e != hipSuccess) return e;
 
-  // ---- K3: stable scatter.  S = 100 (TeraSort rows): v7 for R <= 512, v6 for the R whose
-  // LDS image still fits; any other shape: the v2 (R <= 4096, S in {16, 100}) or v1 kernels.
+  // ---- K3: stable scatter.  S = 100 (TeraSort rows): v8 for R <= 208, v7 for R <= 512, v6 for
+  // the R whose LDS image still fits; 16-byte rows with R > 1024: sux_small.hip; any other
+  // shape: the v1 kernel.
   // tuning (Tuning): s6_chunk caps the v6 chunk, tiles_per_item sets the v6/v7 work item,
   // scatter_chunk/scatter_depth pick the v7 shape (768-record chunks leave room for a K1
   // workgroup on the CU: the co-resident pipeline)
   timer_begin(timer, kScatter, s);
-  const bool two16 = s16 && small_two_pass_shape((uint32_t)R, S) && tn.small_kernel == 3 &&
-                     ws.tmp_bytes >= g.num_records * 16;
-  const bool sorted16 = s16 && R <= kS16sMaxR && tn.small_kernel != 1;
-  if (two16) {
-    timer_note(timer, kScatter, "k_bucket16a+k_bucket16b");
-    uint8_t* tmp = d_ws + ws.tmp_off;
-    const uint32_t items = g.num_maps * (((uint32_t)R + B16b<8>::NB - 1) / B16b<8>::NB);
-    const int kw = (pd.key_len + 3) / 4;
-    // wave count per workgroup: 8 = two 512-thread workgroups per CU (their phases interleave),
-    // 16 = one 1024-thread workgroup (tuning small_waves; default 8)
-    const bool w16 = tn.small_waves == 16;
-#define SUX_B16(NWV)                                                                             \
-  do {                                                                                           \
-    allow_lds(reinterpret_cast<const void*>(&k_bucket16a<NWV>), B16a<NWV>::lds_bytes());         \
-    hipLaunchKernelGGL((k_bucket16a<NWV>), dim3(std::min<uint32_t>(total_tiles, ncu * (16 / NWV))), \
-                       dim3(NWV * kWave), B16a<NWV>::lds_bytes(), s, g, R, pids, counts, base, tmp); \
-    const dim3 gridb(std::min<uint32_t>(items, ncu * (16 / NWV)));                              \
-    if (kw <= 1) SUX_B16B(1, NWV);                                                               \
-    else if (kw == 2) SUX_B16B(2, NWV);                                                          \
-    else if (kw == 3) SUX_B16B(3, NWV);                                                          \
-    else SUX_B16B(4, NWV);                                                                       \
-  } while (0)
-#define SUX_B16B(KW, NWV)                                                                        \
-  do {                                                                                           \
-    allow_lds(reinterpret_cast<const void*>(&k_bucket16b<KW, NWV>), B16b<NWV>::lds_bytes());     \
-    hipLaunchKernelGGL((k_bucket16b<KW, NWV>), gridb, dim3(NWV * kWave), B16b<NWV>::lds_bytes(), \
-                       s, pd, g, base, totals, tmp, d_out);                                      \
-  } while (0)
-    if (w16) SUX_B16(16);
-    else SUX_B16(8);
-#undef SUX_B16
-#undef SUX_B16B
-    e = hipGetLastError();
-  } else if (sorted16) {
-    timer_note(timer, kScatter, "k_scatter16s");
-    const size_t lds = Sc16s::lds_bytes(R);
-    allow_lds(reinterpret_cast<const void*>(&k_scatter16s), lds);
-    const dim3 grid(std::min<uint32_t>(total_tiles, ncu));  // one LDS-bound workgroup per CU
-    hipLaunchKernelGGL(k_scatter16s, grid, dim3(1024), lds, s, g, R, bits, pids, counts, base,
-                       d_out);
-    e = hipGetLastError();
-  } else if (s16) {
-    timer_note(timer, kScatter, "k_scatter16b");
-    const size_t lds = (size_t)R * 4;
-    const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(2, (160u * 1024) / (uint32_t)lds));
-    const dim3 grid(std::min<uint32_t>(total_tiles, ncu * per_cu));
-    const int gb = tn.small_groups;  // groups per turn (1 = k_scatter16)
-    if (gb == 2 || gb == 4) {
-      const void* kf = gb == 2 ? reinterpret_cast<const void*>(&k_scatter16b<16, 2>)
-                               : reinterpret_cast<const void*>(&k_scatter16b<16, 4>);
-      allow_lds(kf, lds);
-      if (gb == 2)
-        hipLaunchKernelGGL((k_scatter16b<16, 2>), grid, dim3(1024), lds, s, g, R, bits, pids,
-                           counts, base, d_out);
-      else
-        hipLaunchKernelGGL((k_scatter16b<16, 4>), grid, dim3(1024), lds, s, g, R, bits, pids,
-                           counts, base, d_out);
-    } else {
-      allow_lds(reinterpret_cast<const void*>(&k_scatter16<16>), lds);
-      hipLaunchKernelGGL((k_scatter16<16>), grid, dim3(1024), lds, s, g, R, bits, pids, counts,
-                         base, d_out);
-    }
-    e = hipGetLastError();
+  if (s16) {
+    e = launch_scatter16(g, R, bits, pids, counts, base, d_out, tn, timer, s);
   } else if (v8) {
     timer_note(timer, kScatter, "k_scatter8");
     // one contiguous, balanced tile range per workgroup (k_scatter8), one workgroup per CU
@@ -3601,19 +1899,6 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g_in, const
     else if (c6 == 384) SUX_S6L(384, 6);
     else SUX_S6L(256, 4);
 #undef SUX_S6L
-    e = hipGetLastError();
-  } else if (sv >= 2 && shaped) {
-    timer_note(timer, kScatter, "k_scatter2");
-    const size_t lds = 4 * (size_t)(S == 100 ? scatter2_wave_bytes<100, 128>(R)
-                                             : scatter2_wave_bytes<16, 512>(R));
-    allow_lds(reinterpret_cast<const void*>(&k_scatter2<100, 128>), lds);
-    allow_lds(reinterpret_cast<const void*>(&k_scatter2<16, 512>), lds);
-    if (S == 100)
-      hipLaunchKernelGGL((k_scatter2<100, 128>), grid4, dim3(256), lds, s, g, R, bits, pids,
-                         counts, base, d_out);
-    else
-      hipLaunchKernelGGL((k_scatter2<16, 512>), grid4, dim3(256), lds, s, g, R, bits, pids,
-                         counts, base, d_out);
     e = hipGetLastError();
   } else if (wpg == 4) {
     timer_note(timer, kScatter, "k_scatter");

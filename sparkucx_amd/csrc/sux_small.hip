@@ -1,0 +1,965 @@
+// sux_small.hip — the map side for small records (16-byte rows, R > 1024: SURVEY.md §8 C5).
+// Called from sux_partition.hip's launch_partition_group when the group's records are 16-byte
+// units with a word-aligned key of <= 16 bytes; the 100-byte TeraSort path lives there.  Output
+// contract identical to the large-record kernels: stable per-partition regroup (P2), index tables
+// native + big-endian (P3).
+#include "sux_part.h"
+
+namespace sux {
+
+// ------------------------------------------------------------------------------------------
+// Small records (S = 16, SURVEY.md config C5: 16-byte key/value rows, 10,000 partitions).
+// A record is one aligned 16-byte unit and R is far too large for per-wave counters, so:
+//   k_hist16    persistent workgroups of 1024 threads, one tile at a time; every lane loads whole
+//               records (coalesced 16-byte units, 8 in flight per lane), hashes the key from its
+//               registers and counts into ONE per-workgroup LDS histogram of R counters.
+//   k_scatter16b persistent 1024-thread workgroups, one tile range at a time with an LDS cursor
+//               per partition.  The tile is cut into 64-record groups dealt to the waves in
+//               order; a wave ranks GB groups' equal pids with ballot matches, then, when the LDS
+//               turn counter reaches it, reads and advances the cursors of its pids and hands the
+//               turn on.  Only that short step is serialised; loads and 16-byte stores are not.
+//   k_scatter16s the same without turns: chunks sorted by pid in LDS (below).
+//   k_msd16a/b  the two-level path without K1 (below; the default for long maps).
+// ------------------------------------------------------------------------------------------
+template <int KW>
+__global__ __launch_bounds__(1024) void k_hist16(PartDev pd, MapGroup g, uint16_t* __restrict__ pids,
+                                                uint32_t* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t hist[];  // [R]
+  const int R = pd.R;
+  const uint32_t ntiles = g.num_maps * g.tiles_per_map;
+  const u32x4* recs = reinterpret_cast<const u32x4*>(g.recs);
+  const int kw0 = pd.key_offset / 4;
+  for (int p = threadIdx.x; p < R; p += 1024) hist[p] = 0;
+  __syncthreads();
+  for (uint32_t gt = blockIdx.x; gt < ntiles; gt += gridDim.x) {
+    const TileRange tr = tile_range(g, gt);
+    for (uint64_t i0 = tr.begin; i0 < tr.end; i0 += 8 * 1024) {
+      u32x4 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint64_t i = i0 + k * 1024 + threadIdx.x;
+        v[k] = recs[i < tr.end ? i : tr.begin];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint64_t i = i0 + k * 1024 + threadIdx.x;
+        if (i < tr.end) {
+          uint32_t w[KW];
+#pragma unroll
+          for (int q = 0; q < KW; ++q) {
+            const int d = kw0 + q;
+            w[q] = d == 0 ? v[k][0] : d == 1 ? v[k][1] : d == 2 ? v[k][2] : v[k][3];
+          }
+          const int p = partition_words<KW, false>(pd, w, pd.bounds, pd.lut);
+          atomicAdd(&hist[p], 1u);
+          pids[i] = (uint16_t)p;
+        }
+      }
+    }
+    __syncthreads();
+    // tile-major counts [map][tile][p]: one contiguous row per tile (a partition-major column
+    // would touch R lines at a 4*tiles stride for R 4-byte counters)
+    uint32_t* dst = counts + ((uint64_t)tr.map * g.tiles_per_map + tr.tile) * R;
+    for (int p = threadIdx.x; p < R; p += 1024) {
+      dst[p] = hist[p];
+      hist[p] = 0;
+    }
+    __syncthreads();
+  }
+}
+
+// Wait until the LDS turn counter reaches `want`.  Bounded: after 2^22 sleeps (far beyond any
+// legitimate wait) the wave sets the node's device error word (sux_node_check reports it) and
+// the workgroup's stop flag, and every wave of the workgroup leaves without touching the
+// cursors again; a wave that sees the stop flag while it waits leaves too.  Returns false then.
+__device__ __forceinline__ bool wait_turn(uint32_t* turn, uint32_t want, uint32_t* stop,
+                                          uint32_t* err) {
+  for (uint32_t spin = 0;; ++spin) {
+    if (__hip_atomic_load(turn, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == want) return true;
+    if (__hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
+    if (spin > (1u << 22)) {
+      if (__lane_id() == 0) {
+        if (err) atomicOr(err, kErrTurnTimeout);
+        __hip_atomic_store(stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// The turn is handed on once per batch of GB consecutive 64-record groups: a wave ranks GB groups,
+// then in its turn walks their cursor updates back to back (LDS ops of one wave stay in order), so
+// the cross-wave hand-off (acquire spin, release fence) is paid GB x less often (GB = 1: once per
+// group, round 1's k_scatter16).  The next batch's loads fly during this batch's turn.
+template <uint32_t NW, int GB>
+__global__ __launch_bounds__(NW * 64) void k_scatter16b(MapGroup g, int R, int pid_bits,
+                                                        const uint16_t* __restrict__ pids,
+                                                        const uint32_t* __restrict__ prefix,
+                                                        const uint64_t* __restrict__ base,
+                                                        uint8_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t cur[];  // [R] next output record of p
+  __shared__ uint32_t turn, stop;
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const uint32_t ntiles = g.num_maps * g.tiles_per_map;
+  const u32x4* recs = reinterpret_cast<const u32x4*>(g.recs);
+  u32x4* out4 = reinterpret_cast<u32x4*>(out);
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  if (tid == 0) stop = 0;
+  for (uint32_t gt = xcd_map(blockIdx.x, gridDim.x); gt < ntiles; gt += gridDim.x) {
+    const TileRange tr = tile_range(g, gt);
+    const uint64_t* bm = base + (uint64_t)tr.map * R;
+    const uint32_t* pm = prefix + ((uint64_t)tr.map * g.tiles_per_map + tr.tile) * R;  // tile-major
+    for (int p = tid; p < R; p += NW * kWave) cur[p] = (uint32_t)(bm[p] + pm[p]);
+    if (tid == 0) turn = 0;
+    __syncthreads();
+    const uint32_t ngroups = (uint32_t)((tr.end - tr.begin + kWave - 1) / kWave);
+    const uint32_t nbatch = (ngroups + GB - 1) / GB;
+    uint32_t pa[GB], pb[GB];
+    u32x4 ra[GB], rb[GB];
+    auto load = [&](uint32_t bb, uint32_t (&pv)[GB], u32x4 (&rv)[GB]) {
+#pragma unroll
+      for (int k = 0; k < GB; ++k) {
+        const uint64_t i = tr.begin + ((uint64_t)bb * GB + k) * kWave + lane;
+        const uint64_t ii = i < tr.end ? i : tr.end - 1;  // clamped, unconditional
+        pv[k] = pids[ii];
+        rv[k] = recs[ii];
+      }
+    };
+    uint32_t b = wave;
+    load(b, pa, ra);
+    while (b < nbatch) {
+      load(b + NW, pb, rb);  // next batch in flight during this one's turn
+      uint64_t peers[GB];
+      uint32_t pp[GB];
+      bool valid[GB];
+#pragma unroll
+      for (int k = 0; k < GB; ++k) {
+        const uint64_t i = tr.begin + ((uint64_t)b * GB + k) * kWave + lane;
+        valid[k] = i < tr.end;
+        pp[k] = valid[k] ? pa[k] : 0u;
+        uint64_t pe = __ballot(valid[k]);
+        for (int bb = 0; bb < pid_bits; ++bb) {
+          const bool bit = (pp[k] >> bb) & 1u;
+          const uint64_t m = __ballot(bit);
+          pe &= bit ? m : ~m;
+        }
+        peers[k] = pe;
+      }
+      if (!wait_turn(&turn, b, &stop, g.err)) break;
+      uint32_t dst[GB];
+#pragma unroll
+      for (int k = 0; k < GB; ++k) {
+        uint32_t r0 = 0;
+        if (valid[k]) r0 = cur[pp[k]];
+        __builtin_amdgcn_wave_barrier();
+        if (valid[k] && (peers[k] & lt_mask) == 0) cur[pp[k]] = r0 + (uint32_t)__popcll(peers[k]);
+        __builtin_amdgcn_wave_barrier();
+        dst[k] = r0 + (uint32_t)__popcll(peers[k] & lt_mask);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&turn, b + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+      for (int k = 0; k < GB; ++k)
+        if (valid[k]) out4[dst[k]] = ra[k];
+#pragma unroll
+      for (int k = 0; k < GB; ++k) {
+        pa[k] = pb[k];
+        ra[k] = rb[k];
+      }
+      b += NW;
+    }
+    __syncthreads();
+    if (stop) return;  // a turn timed out: the error word is set, nothing more is written
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_scatter16s: the small-record scatter without turns (R <= kS16sMaxR).  A persistent
+// 1024-thread workgroup walks tile ranges in 4096-record chunks; a chunk's stable rank of every
+// record among the chunk's records of its partition comes from sorting the chunk's
+// (pid, position) keys in LDS, not from waves taking turns on the cursors:
+//   1. LSD radix passes of 7 pid bits over the 4096 keys (two for R <= 16384): a wave owns 256
+//      consecutive positions and ranks them group by group with a ballot match against its own
+//      per-digit counters; one block scan over (digit, wave) gives every wave's digit offsets, so
+//      each pass is stable and needs no atomics;
+//   2. run starts of the sorted keys (rs[p] = first sorted position of p), then every record's
+//      destination cursor[p] + (sorted position - rs[p]); run ends advance the cursors;
+//   3. every thread stores the records it loaded, in input order (16-byte stores).
+// Three barriers per pass and three for the rest; the next chunk's pids and records are in
+// flight the whole time.  Same bytes as k_scatter16 / k_scatter16b.
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t kS16sChunk = 4096;    // records per chunk: 4 per thread of 1024
+constexpr uint32_t kS16sIdxBits = 12;    // log2(kS16sChunk)
+constexpr uint32_t kS16sDigit = 7;       // pid bits per LDS radix pass
+constexpr int kS16sMaxR = 16384;         // two passes; cursors + run starts fit the LDS
+
+struct Sc16s {
+  static constexpr uint32_t NT = 1024, NW = 16, PT = kS16sChunk / NT, NB = 1u << kS16sDigit;
+  // cur[R] u32 | rs[R] u16 (padded) | keys[2][chunk] u32 | wc[2][NW][NB] u32 | wsum[NW] u32
+  static __host__ __device__ constexpr uint32_t lds_bytes(int R) {
+    return (uint32_t)R * 4 + ((uint32_t)R * 2 + 15) / 16 * 16 + 2 * kS16sChunk * 4 +
+           2 * NW * NB * 4 + NW * 4;
+  }
+};
+
+__global__ __launch_bounds__(1024) void k_scatter16s(MapGroup g, int R, int pid_bits,
+                                                     const uint16_t* __restrict__ pids,
+                                                     const uint32_t* __restrict__ prefix,
+                                                     const uint64_t* __restrict__ base,
+                                                     uint8_t* __restrict__ out) {
+  using K = Sc16s;
+  constexpr uint32_t NT = K::NT, NW = K::NW, PT = K::PT, NB = K::NB, CH = kS16sChunk;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  uint32_t* cur = reinterpret_cast<uint32_t*>(lds8);
+  uint16_t* rs = reinterpret_cast<uint16_t*>(cur + R);
+  uint32_t* keys0 = reinterpret_cast<uint32_t*>(lds8 + (uint32_t)R * 4 + ((uint32_t)R * 2 + 15) / 16 * 16);
+  uint32_t* keys1 = keys0 + CH;
+  uint32_t* wc0 = keys1 + CH;  // [2][NW][NB]
+  uint32_t* wsum = wc0 + 2 * NW * NB;
+
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  const uint32_t ntiles = g.num_maps * g.tiles_per_map;
+  const u32x4* recs = reinterpret_cast<const u32x4*>(g.recs);
+  u32x4* out4 = reinterpret_cast<u32x4*>(out);
+  const int passes = pid_bits <= (int)kS16sDigit ? 1 : 2;
+
+  for (uint32_t i = tid; i < 2 * NW * NB; i += NT) wc0[i] = 0;
+  for (uint32_t gt = xcd_map(blockIdx.x, gridDim.x); gt < ntiles; gt += gridDim.x) {
+    const TileRange tr = tile_range(g, gt);
+    const uint64_t* bm = base + (uint64_t)tr.map * R;
+    const uint32_t* pm = prefix + ((uint64_t)tr.map * g.tiles_per_map + tr.tile) * R;  // tile-major
+    for (int p = tid; p < R; p += NT) cur[p] = (uint32_t)(bm[p] + pm[p]);
+    const uint32_t nchunks = (uint32_t)((tr.end - tr.begin + CH - 1) / CH);
+    // element e = wave * 256 + j * 64 + lane: a wave's positions are contiguous and visited in
+    // order, which is what keeps every radix pass stable
+    uint32_t pv[PT];
+    u32x4 rv[PT];
+    auto load = [&](uint32_t c, uint32_t (&p)[PT], u32x4 (&r)[PT]) {
+      const uint64_t c0 = tr.begin + (uint64_t)(c < nchunks ? c : 0) * CH;
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) {
+        const uint64_t i = c0 + wave * (PT * kWave) + j * kWave + lane;
+        const uint64_t ii = i < tr.end ? i : tr.end - 1;  // clamped, unconditional
+        p[j] = pids[ii];
+        r[j] = recs[ii];
+      }
+    };
+    if (nchunks) load(0, pv, rv);
+    __syncthreads();  // cursors ready
+    for (uint32_t c = 0; c < nchunks; ++c) {
+      const uint32_t n = (uint32_t)min<uint64_t>(CH, tr.end - tr.begin - (uint64_t)c * CH);
+      uint32_t pn[PT];
+      u32x4 rn[PT];
+      load(c + 1, pn, rn);  // the next chunk flies during this one
+      // 1. LSD radix passes over (pid << 12 | position)
+      uint32_t* kin = keys0;
+      uint32_t* kout = keys1;
+      for (int d = 0; d < passes; ++d) {
+        uint32_t* wc = wc0 + (d & 1) * NW * NB;
+        const uint32_t sh = kS16sIdxBits + d * kS16sDigit;
+        uint32_t key[PT], dig[PT], rank[PT];
+#pragma unroll
+        for (uint32_t j = 0; j < PT; ++j) {
+          const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+          const bool valid = e < n;
+          key[j] = d == 0 ? ((pv[j] << kS16sIdxBits) | e) : (valid ? kin[e] : 0u);
+          dig[j] = valid ? (key[j] >> sh) & (NB - 1) : 0u;
+          uint64_t peers = __ballot(valid);
+#pragma unroll
+          for (uint32_t bb = 0; bb < kS16sDigit; ++bb) {
+            const bool bit = (dig[j] >> bb) & 1u;
+            const uint64_t m = __ballot(bit);
+            peers &= bit ? m : ~m;
+          }
+          uint32_t* w = wc + wave * NB + dig[j];
+          uint32_t r0 = 0;
+          if (valid) r0 = *w;
+          __builtin_amdgcn_wave_barrier();
+          if (valid && (peers & lt_mask) == 0) *w = r0 + (uint32_t)__popcll(peers);
+          __builtin_amdgcn_wave_barrier();
+          rank[j] = valid ? r0 + (uint32_t)__popcll(peers & lt_mask) : ~0u;
+        }
+        __syncthreads();
+        // block exclusive scan of the counters in (digit, wave) order: thread t owns digit
+        // t / 8 and waves 2(t % 8), 2(t % 8) + 1
+        {
+          const uint32_t dg = tid / (NW / 2), w0 = 2 * (tid % (NW / 2));
+          const uint32_t a = wc[w0 * NB + dg], b = wc[(w0 + 1) * NB + dg];
+          const uint32_t incl = wave_incl_scan(a + b, lane);
+          if (lane == kWave - 1) wsum[wave] = incl;
+          __syncthreads();
+          uint32_t before = 0;
+#pragma unroll
+          for (uint32_t w = 0; w < NW; ++w) before += w < (uint32_t)wave ? wsum[w] : 0u;
+          const uint32_t ex = before + incl - (a + b);
+          wc[w0 * NB + dg] = ex;
+          wc[(w0 + 1) * NB + dg] = ex + a;
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < PT; ++j)
+          if (rank[j] != ~0u) kout[wc[wave * NB + dig[j]] + rank[j]] = key[j];
+        __syncthreads();
+        // this counter set is next used at least one barrier later (next chunk or pass)
+        for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
+        uint32_t* t = kin;
+        kin = kout;
+        kout = t;
+      }
+      // 2. run starts, destinations (into the free key buffer, by position), cursor advances
+      uint32_t* dsta = kout;
+      uint32_t endp[PT], endv[PT];
+#pragma unroll
+      for (uint32_t k = 0; k < PT; ++k) {
+        const uint32_t s = tid + k * NT;
+        endp[k] = ~0u;
+        if (s < n) {
+          const uint32_t p = kin[s] >> kS16sIdxBits;
+          if (s == 0 || (kin[s - 1] >> kS16sIdxBits) != p) rs[p] = (uint16_t)s;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t k = 0; k < PT; ++k) {
+        const uint32_t s = tid + k * NT;
+        if (s < n) {
+          const uint32_t key = kin[s], p = key >> kS16sIdxBits;
+          const uint32_t dst = cur[p] + (s - rs[p]);
+          dsta[key & (CH - 1)] = dst;
+          if (s + 1 == n || (kin[s + 1] >> kS16sIdxBits) != p) {
+            endp[k] = p;
+            endv[k] = dst + 1;
+          }
+        }
+      }
+      __syncthreads();
+      // 3. stores in input order; the cursors move on (every read of them is behind the barrier)
+#pragma unroll
+      for (uint32_t k = 0; k < PT; ++k)
+        if (endp[k] != ~0u) cur[endp[k]] = endv[k];
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) {
+        const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+        if (e < n) out4[dsta[e]] = rv[j];
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) {
+        pv[j] = pn[j];
+        rv[j] = rn[j];
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Two-level (MSD) small-record map side without K1 (16-byte records, 1024 < R <= 16384,
+// map-major layout; tuning small_kernel = 4).  Every pass streams whole lines:
+//   pass A (k_msd16a) reads each 4096-record chunk once, computes every record's pid from its
+//          key, stable-sorts the chunk by bucket = pid >> 5 in LDS and writes it back to the
+//          temp copy AT THE CHUNK'S OWN POSITION (a contiguous write), with the chunk's bucket
+//          starts (u16) in offs[map][chunk][bucket];
+//   K2     (k_msd16_scan) one workgroup per map: bucket totals over the map's chunks ->
+//          segment bases segbase[map][bucket] and the index table's last entry;
+//   pass B (k_msd16b) one (map, bucket) segment at a time: the segment's runs (one ~13-record
+//          run per chunk at R = 10 000) are gathered into LDS, stable-sorted by pid & 31,
+//          written as ONE contiguous output range, and the bucket's 32 index entries (native +
+//          big-endian) are written.  A segment larger than the LDS (skewed keys) is counted
+//          first and then placed piece by piece through per-partition cursors.
+// 16 + 16 (A) and 16 + 16 (B) bytes per record, no pid array, no R-wide histogram: the
+// sorted-chunk scatter (k_hist16 + k_scatter16s) moves 19 + 54 bytes per record, 32 of them as
+// lone 16-byte stores.  Both passes run two 512-thread workgroups per CU, whose load, rank and
+// store phases interleave.  Stable: pass A keeps input order inside a bucket (chunks in order,
+// ranks in order inside a chunk), pass B keeps segment order inside a partition.
+// ------------------------------------------------------------------------------------------
+// Diagnostic build only (tools/msd_stamps.hip defines SUX_MSD_STAMPS): per-phase s_memtime
+// cycles of k_msd16b, summed per workgroup into g_msd_stamps[block][phase].
+#ifdef SUX_MSD_STAMPS
+__device__ unsigned long long* g_msd_stamps;
+#define SUX_MSD_STAMP_INIT()                 \
+  unsigned long long st_acc[5] = {0, 0, 0, 0, 0}; \
+  unsigned long long st_t = __builtin_amdgcn_s_memtime()
+#define SUX_MSD_STAMP(k)                                   \
+  do {                                                     \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    st_acc[k] += t_ - st_t;                                \
+    st_t = t_;                                             \
+  } while (0)
+#define SUX_MSD_STAMP_END()                                              \
+  do {                                                                   \
+    if (threadIdx.x == 0 && g_msd_stamps)                                \
+      for (int k_ = 0; k_ < 5; ++k_) g_msd_stamps[blockIdx.x * 8 + k_] = st_acc[k_]; \
+  } while (0)
+#else
+#define SUX_MSD_STAMP_INIT() do {} while (0)
+#define SUX_MSD_STAMP(k) do {} while (0)
+#define SUX_MSD_STAMP_END() do {} while (0)
+#endif
+constexpr uint32_t kM16Chunk = 4096;      // pass A records per chunk (the run table's unit)
+constexpr uint32_t kM16Lo = 4;            // partitions per bucket: 16
+constexpr uint32_t kM16MaxChunks = 512;   // chunks per map pass B's run table holds (2 Mi records)
+
+// Block exclusive scan, in (digit, wave) order, of u16 per-wave digit counters wc[NW][NB]
+// (NW*64 threads; each thread owns E = NB/64 consecutive (digit, wave) entries).  Counts and
+// prefixes fit u16: a chunk holds kM16Chunk records.  Two barriers; wsum[NW] scratch.
+template <uint32_t NB, uint32_t NW>
+__device__ __forceinline__ void scan_digit_wave16(uint16_t* wc, uint32_t* wsum, int tid, int lane,
+                                                  int wave) {
+  constexpr uint32_t E = NB / kWave;
+  uint32_t sum = 0;  // the entries are read twice instead of held (registers are the limit)
+#pragma unroll
+  for (uint32_t k = 0; k < E; ++k) {
+    const uint32_t idx = (uint32_t)tid * E + k, d = idx / NW, w = idx % NW;
+    sum += wc[w * NB + d];
+  }
+  const uint32_t incl = wave_incl_scan(sum, lane);
+  if (lane == kWave - 1) wsum[wave] = incl;
+  __syncthreads();
+  uint32_t run = incl - sum;
+#pragma unroll
+  for (uint32_t w = 0; w < NW; ++w) run += w < (uint32_t)wave ? wsum[w] : 0u;
+#pragma unroll
+  for (uint32_t k = 0; k < E; ++k) {
+    const uint32_t idx = (uint32_t)tid * E + k, d = idx / NW, w = idx % NW;
+    const uint32_t v = wc[w * NB + d];
+    wc[w * NB + d] = (uint16_t)run;
+    run += v;
+  }
+  __syncthreads();
+}
+
+template <uint32_t NW, uint32_t DB>  // stage[CH] u32x4 (its first NW words double as wsum) | wc[NW][2^DB] u16
+struct M16a {
+  static constexpr uint32_t NB = 1u << DB, NT = NW * kWave, PT = kM16Chunk / NT;
+  static constexpr uint32_t lds_bytes() { return kM16Chunk * 16 + NW * NB * 2; }
+};
+template <uint32_t NW, uint32_t PT>  // stage[CAP] u32x4 | wc[NW][64] | cur[64] | wsum[NW] | los[CAP] u8 | rp[MAXCH+1] u32 | ro[MAXCH] u16
+struct M16b {
+  static constexpr uint32_t NB = 64, NT = NW * kWave, CAP = NT * PT;
+  static constexpr uint32_t lds_bytes() {
+    return CAP * 16 + NW * NB * 4 + NB * 4 + NW * 4 + CAP + (kM16MaxChunks + 1) * 4 +
+           kM16MaxChunks * 2;
+  }
+};
+
+// records of map m in the group, and of its chunk c
+__device__ __forceinline__ uint32_t m16_map_len(const MapGroup& g, uint32_t m) {
+  const uint64_t b = (uint64_t)m * g.records_per_map;
+  const uint64_t e = min(b + g.records_per_map, g.num_records);
+  return (uint32_t)(e > b ? e - b : 0);
+}
+__device__ __forceinline__ uint32_t m16_chunk_len(uint32_t map_len, uint32_t c) {
+  const uint32_t b = c * kM16Chunk;
+  return map_len > b ? min(kM16Chunk, map_len - b) : 0u;
+}
+
+template <int KW>
+__device__ __forceinline__ uint32_t m16_pid(const PartDev& pd, const u32x4& r, int kw0) {
+  uint32_t w[KW];
+#pragma unroll
+  for (int q = 0; q < KW; ++q) {
+    const int d = kw0 + q;
+    w[q] = d == 0 ? r[0] : d == 1 ? r[1] : d == 2 ? r[2] : r[3];
+  }
+  return (uint32_t)partition_words<KW, false>(pd, w, pd.bounds, pd.lut);
+}
+
+template <int KW, uint32_t NW, uint32_t DB>
+__global__ __launch_bounds__(NW * 64, 4) void k_msd16a(PartDev pd, MapGroup g, uint32_t cpm,
+                                                 uint32_t nbk, uint16_t* __restrict__ offs,
+                                                 uint16_t* __restrict__ pids_out,
+                                                 uint8_t* __restrict__ tmp) {
+  using K = M16a<NW, DB>;
+  constexpr uint32_t NB = K::NB, NT = K::NT, PT = K::PT, CH = kM16Chunk;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  u32x4* stage = reinterpret_cast<u32x4*>(lds8);
+  uint16_t* wc = reinterpret_cast<uint16_t*>(stage + CH);  // [NW][NB]
+  uint32_t* wsum = reinterpret_cast<uint32_t*>(lds8);       // only inside the scan: stage is idle
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  const int kw0 = pd.key_offset / 4;
+  const u32x4* recs = reinterpret_cast<const u32x4*>(g.recs);
+  u32x4* t4 = reinterpret_cast<u32x4*>(tmp);
+  // one contiguous, balanced range of (map, chunk) items per workgroup
+  const uint32_t items = g.num_maps * cpm, G = gridDim.x, b = xcd_map(blockIdx.x, G);
+  const uint32_t it0 = (uint32_t)((uint64_t)items * b / G), it1 = (uint32_t)((uint64_t)items * (b + 1) / G);
+  struct Item {
+    uint64_t c0;  // first record of the chunk (group index)
+    uint32_t n;   // its records (0 past the range)
+  };
+  auto item = [&](uint32_t it) {
+    const uint32_t m = it / cpm, c = it - m * cpm;
+    Item k;
+    k.c0 = (uint64_t)m * g.records_per_map + (uint64_t)c * CH;
+    k.n = it < it1 ? m16_chunk_len(m16_map_len(g, m), c) : 0u;
+    return k;
+  };
+  auto load = [&](const Item& k, u32x4 (&r)[PT]) {
+    if (k.n == 0) return;
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j) {  // unconditional (clamped) loads: no per-load wait
+      const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+      r[j] = recs[k.c0 + min(e, k.n - 1)];
+    }
+  };
+  for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
+  __syncthreads();
+  u32x4 rv[PT];
+  for (uint32_t it = it0; it < it1; ++it) {
+    const Item k = item(it);
+    load(k, rv);
+    uint32_t h[PT], rank[PT];
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j) {
+      const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+      const bool valid = e < k.n;
+      uint32_t p = 0;
+      if (valid) {
+        p = m16_pid<KW>(pd, rv[j], kw0);
+        if (pids_out) pids_out[k.c0 + e] = (uint16_t)p;
+      }
+      h[j] = (p >> kM16Lo) & (NB - 1);
+      rank[j] = wave_rank<DB, uint16_t>(h[j], valid, wc + wave * NB, lt_mask);
+    }
+    __syncthreads();
+    scan_digit_wave16<NB, NW>(wc, wsum, tid, lane, wave);
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j)
+      if (rank[j] != ~0u) stage[wc[wave * NB + h[j]] + rank[j]] = rv[j];
+    __syncthreads();
+    // the chunk goes back to its own place, in bucket order: one contiguous write
+#pragma unroll
+    for (uint32_t q = 0; q < PT; ++q) {
+      const uint32_t i = tid + q * NT;
+      if (i < k.n) t4[k.c0 + i] = stage[i];
+    }
+    for (uint32_t hb = tid; hb < nbk; hb += NT)
+      offs[(uint64_t)it * nbk + hb] = (uint16_t)wc[hb];  // wc[0][hb]: bucket start in the chunk
+    __syncthreads();
+    for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
+    __syncthreads();
+  }
+}
+
+// K2 of the MSD path: one workgroup (kScanThreads) per map.  Bucket totals over the map's chunks
+// (one thread per bucket), exclusive scan over buckets ->
+// segbase[m][h] (record index in the group's output), the index table's last entry and, at
+// world 1, the peer byte count.
+__global__ __launch_bounds__(kScanThreads) void k_msd16_scan(MapGroup g, uint32_t cpm, uint32_t nbk,
+                                                             const uint16_t* __restrict__ offs,
+                                                             uint64_t* __restrict__ segbase,
+                                                             int64_t* __restrict__ index,
+                                                             uint8_t* __restrict__ index_be,
+                                                             uint64_t* __restrict__ peer_bytes,
+                                                             int R) {
+  constexpr uint32_t HG = 1024, NG = kScanThreads / HG;  // one thread per bucket (nbk <= 1024)
+  __shared__ uint64_t sh[2 * kWave + 1];
+  __shared__ uint32_t part[kScanThreads];
+  const uint32_t m = blockIdx.x, tid = threadIdx.x;
+  const uint32_t len = m16_map_len(g, m), nch = (len + kM16Chunk - 1) / kM16Chunk;
+  const uint32_t h = tid % HG, cg = tid / HG;
+  uint32_t t = 0;
+  if (h < nbk) {
+    const uint16_t* om = offs + (uint64_t)m * cpm * nbk;
+    for (uint32_t c = cg; c < nch; c += NG) {
+      const uint32_t o = om[(uint64_t)c * nbk + h];
+      const uint32_t e = h + 1 < nbk ? om[(uint64_t)c * nbk + h + 1] : m16_chunk_len(len, c);
+      t += e - o;
+    }
+  }
+  part[tid] = t;
+  __syncthreads();
+  uint64_t v = 0;
+  if (tid < HG)
+    for (uint32_t q = 0; q < NG; ++q) v += part[tid + q * HG];
+  uint64_t tot;
+  const uint64_t ex = block_excl_scan(tid < nbk ? v : 0, sh, &tot);
+  if (tid < nbk) segbase[(uint64_t)m * nbk + tid] = (uint64_t)m * g.records_per_map + ex;
+  if (tid == 0) {
+    const int64_t off = (int64_t)len * g.rec_size;
+    index[(uint64_t)m * (R + 1) + R] = off;
+    if (index_be) reinterpret_cast<uint64_t*>(index_be)[(uint64_t)m * (R + 1) + R] = bswap64((uint64_t)off);
+    if (m == 0 && peer_bytes) peer_bytes[0] = g.num_records * g.rec_size;
+  }
+}
+
+template <int KW, uint32_t NW, uint32_t PT>
+__global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, uint32_t cpm,
+                                                 uint32_t nbk, const uint16_t* __restrict__ offs,
+                                                 const uint64_t* __restrict__ segbase,
+                                                 const uint8_t* __restrict__ tmp,
+                                                 uint8_t* __restrict__ out,
+                                                 int64_t* __restrict__ index,
+                                                 uint8_t* __restrict__ index_be) {
+  using K = M16b<NW, PT>;
+  constexpr uint32_t NB = K::NB, NT = K::NT, CAP = K::CAP, MC = kM16MaxChunks, PB = 1u << kM16Lo;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  u32x4* stage = reinterpret_cast<u32x4*>(lds8);
+  uint32_t* wc = reinterpret_cast<uint32_t*>(stage + CAP);  // [NW][NB]
+  uint32_t* cur = wc + NW * NB;
+  uint32_t* wsum = cur + NB;
+  uint8_t* los = reinterpret_cast<uint8_t*>(wsum + NW);
+  uint32_t* rp = reinterpret_cast<uint32_t*>(los + CAP);   // [MC + 1] run starts in the segment
+  uint16_t* ro = reinterpret_cast<uint16_t*>(rp + MC + 1);  // [MC] run starts in their chunk
+  const int R = pd.R;
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  const int kw0 = pd.key_offset / 4;
+  const u32x4* t4 = reinterpret_cast<const u32x4*>(tmp);
+  u32x4* out4 = reinterpret_cast<u32x4*>(out);
+  uint64_t* ibe = reinterpret_cast<uint64_t*>(index_be);
+  const uint32_t items = g.num_maps * nbk, G = gridDim.x, b = xcd_map(blockIdx.x, G);
+  // segments dealt round robin (segment it to workgroup it % G, an XCD's workgroups taking
+  // consecutive segments): at any moment the grid works on ~G consecutive segments, i.e. on
+  // every bucket of a map or two, so the runs it gathers cover whole chunks of the temp copy
+  // (DRAM rows and L2 lines shared by neighbouring runs are read together), and the outputs it
+  // writes are adjacent.  (One contiguous range of segments per workgroup: 2.45 TB/s.)
+  const uint32_t it0 = b, it1 = items;
+
+  struct Seg {
+    uint32_t m, h, nch, T, len;
+    uint64_t mbase, out;  // first record of map m, first output record of the segment
+  };
+  // the global reads a segment's run table starts from (offs pair of chunk tid, segment base),
+  // issued one segment ahead so that build() does not wait for them
+  struct Pre {
+    uint32_t o, e;
+    uint64_t sb;
+  };
+  auto seg = [&](uint32_t it) {
+    Seg s;
+    s.m = it / nbk;
+    s.h = it - s.m * nbk;
+    s.len = m16_map_len(g, s.m);
+    s.nch = (s.len + kM16Chunk - 1) / kM16Chunk;
+    s.mbase = (uint64_t)s.m * g.records_per_map;
+    return s;
+  };
+  auto run_ends = [&](const Seg& s, uint32_t c, uint32_t& o, uint32_t& e) {
+    const uint16_t* oc = offs + ((uint64_t)s.m * cpm + c) * nbk;
+    o = oc[s.h];
+    e = s.h + 1 < nbk ? oc[s.h + 1] : m16_chunk_len(s.len, c);
+  };
+  auto prefetch = [&](uint32_t it) {
+    Pre p{0, 0, 0};
+    if (it < it1) {
+      const Seg s = seg(it);
+      if ((uint32_t)tid < s.nch) run_ends(s, tid, p.o, p.e);
+      p.sb = segbase[it];
+    }
+    return p;
+  };
+  // run table of segment `it` (run c = the bucket's records of chunk c; rp = exclusive prefix
+  // over chunks); all threads, barriers inside
+  auto build = [&](uint32_t it, const Pre& pre) {
+    Seg s = seg(it);
+    s.out = pre.sb;
+    uint32_t carry = 0;
+    // the last batch's thread 0 also writes rp[nch] = T, the search's sentinel (no extra batch
+    // when nch is a multiple of the workgroup: 2^20-record maps have exactly 256 chunks)
+    for (uint32_t c0 = 0; c0 < s.nch; c0 += NT) {
+      const uint32_t c = c0 + (uint32_t)tid;
+      uint32_t o = pre.o, e = pre.e;
+      if (c0 && c < s.nch) run_ends(s, c, o, e);
+      const uint32_t cnt = c < s.nch ? e - o : 0u;
+      const uint32_t incl = wave_incl_scan(cnt, lane);
+      if (lane == kWave - 1) wsum[wave] = incl;
+      __syncthreads();
+      uint32_t run = carry + incl - cnt, blk = 0;
+#pragma unroll
+      for (uint32_t w = 0; w < NW; ++w) {
+        run += w < (uint32_t)wave ? wsum[w] : 0u;
+        blk += wsum[w];
+      }
+      if (c < s.nch) {
+        ro[c] = (uint16_t)o;
+        rp[c] = run;
+      }
+      if (tid == 0 && c0 + NT >= s.nch) rp[s.nch] = carry + blk;
+      carry += blk;
+      __syncthreads();
+    }
+    s.T = carry;
+    return s;
+  };
+  // loads of segment elements [e0, min(T, e0 + CAP)) in wave-contiguous order
+  auto load = [&](const Seg& s, uint32_t e0, u32x4 (&r)[PT]) {
+    const uint32_t lim = min(s.T, e0 + CAP);
+    if (lim <= e0) return;
+    // element e's run = the largest c with rp[c] <= e: a branch-free search whose PT lookups
+    // interleave step by step (rp[nch] = T > e stops every search inside the segment).  Lanes
+    // past the piece re-read its last element: the loads are unconditional — a load under a
+    // branch made the compiler wait for every earlier load before the next one's address
+    // (s_waitcnt vmcnt(0) per element), serialising the gather.
+    uint32_t lo[PT], ev[PT];
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j) {
+      lo[j] = 0;
+      ev[j] = min(e0 + wave * (PT * kWave) + j * kWave + lane, lim - 1);
+    }
+#pragma unroll
+    for (uint32_t step = MC / 2; step; step >>= 1) {
+      uint32_t v[PT];
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) v[j] = rp[min(lo[j] + step, s.nch)];
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) lo[j] = v[j] <= ev[j] ? min(lo[j] + step, s.nch) : lo[j];
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j) {
+      r[j] = t4[s.mbase + (uint64_t)lo[j] * kM16Chunk + ro[lo[j]] + (ev[j] - rp[lo[j]])];
+    }
+  };
+  auto digit = [&](const Seg& s, const u32x4& r) {
+    return (m16_pid<KW>(pd, r, kw0) - (s.h << kM16Lo)) & (NB - 1);
+  };
+  // stable rank by pid & 31 -> stage/los in sorted order; wc[0][l] = digit starts afterwards
+  auto rank_stage = [&](const Seg& s, uint32_t n, const u32x4 (&r)[PT]) {
+    uint32_t lo[PT], rk[PT];
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j) {
+      const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+      const bool valid = e < n;
+      lo[j] = valid ? digit(s, r[j]) : 0u;
+      rk[j] = wave_rank<kM16Lo>(lo[j], valid, wc + wave * NB, lt_mask);
+    }
+    __syncthreads();
+    scan_digit_wave<NB, NW>(wc, wsum, tid, lane, wave);
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j)
+      if (rk[j] != ~0u) {
+        const uint32_t pos = wc[wave * NB + lo[j]] + rk[j];
+        stage[pos] = r[j];
+        los[pos] = (uint8_t)lo[j];
+      }
+  };
+  auto write_index = [&](const Seg& s, uint32_t start_l) {
+    const uint64_t seg_out = s.out;
+    const uint32_t p = (s.h << kM16Lo) + (uint32_t)tid;  // in-segment record offset of partition p
+    if (tid < (int)PB && p < (uint32_t)R) {
+      const int64_t off = (int64_t)((seg_out - s.mbase + start_l) * g.rec_size);
+      index[(uint64_t)s.m * (R + 1) + p] = off;
+      if (ibe) ibe[(uint64_t)s.m * (R + 1) + p] = bswap64((uint64_t)off);
+    }
+  };
+  // sorted stage -> output through the per-partition cursors; cursors advance; wc cleared
+  auto place = [&](const Seg& s, uint32_t n) {
+#pragma unroll
+    for (uint32_t q = 0; q < PT; ++q) {
+      const uint32_t i = tid + q * NT;
+      if (i < n) {
+        const uint32_t l = los[i];
+        out4[s.mbase + cur[l] + (i - wc[l])] = stage[i];
+      }
+    }
+    uint32_t ncur = 0;
+    if (tid < (int)NB) ncur = cur[tid] + ((uint32_t)tid + 1 < NB ? wc[tid + 1] : n) - wc[tid];
+    __syncthreads();
+    if (tid < (int)NB) cur[tid] = ncur;
+    for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
+    __syncthreads();
+  };
+
+  for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
+  __syncthreads();
+  if (it0 >= it1) return;
+  Seg s = build(it0, prefetch(it0));
+  u32x4 rv[PT];
+  SUX_MSD_STAMP_INIT();
+  for (uint32_t it = it0; it < it1; it += G) {
+    const uint32_t seg_rel = (uint32_t)(s.out - s.mbase);  // in-map record offset of the segment
+    const bool multi = s.T > CAP;
+    if (multi) {
+      // larger than the LDS (skewed keys): count the digits first, then place piece by piece
+      for (uint32_t e0 = 0; e0 < s.T; e0 += CAP) {
+        load(s, e0, rv);
+        const uint32_t n = min(CAP, s.T - e0);
+#pragma unroll
+        for (uint32_t j = 0; j < PT; ++j) {
+          const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+          if (e < n) atomicAdd(&wc[wave * NB + digit(s, rv[j])], 1u);
+        }
+      }
+      __syncthreads();
+      scan_digit_wave<NB, NW>(wc, wsum, tid, lane, wave);
+      if (tid < (int)NB) cur[tid] = seg_rel + wc[tid];
+      write_index(s, tid < (int)NB ? wc[tid] : 0u);
+      __syncthreads();
+      for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
+      __syncthreads();
+    }
+    // one piece (the whole segment) unless multi; an empty segment still writes its index
+    for (uint32_t e0 = 0; e0 == 0 || e0 < s.T; e0 += CAP) {
+      load(s, e0, rv);
+      SUX_MSD_STAMP(0);
+      const uint32_t n = min(CAP, s.T - e0);
+      rank_stage(s, n, rv);
+      __syncthreads();
+      SUX_MSD_STAMP(1);
+      if (!multi) {
+        if (tid < (int)NB) cur[tid] = seg_rel + wc[tid];
+        write_index(s, tid < (int)NB ? wc[tid] : 0u);
+      }
+      __syncthreads();
+      SUX_MSD_STAMP(2);
+      place(s, n);
+      SUX_MSD_STAMP(3);
+    }
+    if (it + G < it1) s = build(it + G, prefetch(it + G));
+    SUX_MSD_STAMP(4);
+  }
+  SUX_MSD_STAMP_END();
+}
+// ------------------------------------------------------------------------------------------
+// host launchers (called by launch_partition_group, sux_partition.hip)
+// ------------------------------------------------------------------------------------------
+// The MSD small-record path (k_msd16a / k_msd16_scan / k_msd16b) applies: tuning small_kernel 4,
+// 16-byte records with a fixed-width key in the first 16 bytes, 1024 < R <= 16384, 16-byte
+// aligned input and output, map-major layout, maps of <= kM16MaxChunks chunks, and a workspace
+// with the temp copy (its chunk-offset table lives in the counts region, the segment bases in
+// the totals region).
+bool msd16_eligible(const PartDev& pd, const MapGroup& g, const LayoutDesc& lay,
+                    const uint8_t* d_out, const Workspace& ws, const Tuning& tn) {
+  if (tn.small_kernel != 4 || g.rec_size != 16 || lay.world != 1) return false;
+  if (pd.R <= 1024 || pd.R > 16384 || pd.kind == 4 || pd.key_offset % 4 != 0 ||
+      pd.key_offset + pd.key_len > 16)
+    return false;
+  if (((reinterpret_cast<uintptr_t>(g.recs) | reinterpret_cast<uintptr_t>(d_out)) & 15) != 0)
+    return false;
+  const uint64_t cpm = (g.records_per_map + kM16Chunk - 1) / kM16Chunk;
+  const uint64_t nbk = ((uint64_t)pd.R + (1u << kM16Lo) - 1) >> kM16Lo;
+  // by default only when a (map, bucket) segment holds >= 1024 records on average: a segment
+  // costs ~6 us of run table, search and barriers whatever its size, so short maps run the
+  // sorted-chunk scatter instead (64 Ki-record maps at R = 10 000: 105-record segments, 194 vs
+  // 507 GB/s; 2^20-record maps: 1677-record segments, 1027 vs 750 GB/s)
+  if (tn.small_auto && g.records_per_map < 1024 * nbk) return false;
+  return cpm >= 1 && cpm <= kM16MaxChunks && ws.tmp_bytes >= g.num_records * 16 &&
+         (uint64_t)g.num_maps * cpm * nbk * 2 <= ws.counts_bytes &&
+         (uint64_t)g.num_maps * nbk * 8 <= ws.totals_bytes;
+}
+
+hipError_t launch_msd16(const PartDev& pd, const MapGroup& g, uint8_t* d_out, int64_t* d_index,
+                        uint8_t* d_index_be, uint16_t* d_pids, uint8_t* d_ws, const Workspace& ws,
+                        uint64_t* d_peer_bytes, const Tuning& tn, Timer* timer, hipStream_t s) {
+  const int R = pd.R;
+  const uint32_t ncu = (uint32_t)std::max(1, stream_cus(s));
+  const uint32_t cpm = (uint32_t)((g.records_per_map + kM16Chunk - 1) / kM16Chunk);
+  const uint32_t nbk = ((uint32_t)R + (1u << kM16Lo) - 1) >> kM16Lo;
+  uint16_t* offs = reinterpret_cast<uint16_t*>(d_ws + ws.counts_off);  // [map][chunk][bucket]
+  uint64_t* segbase = reinterpret_cast<uint64_t*>(d_ws + ws.totals_off);  // [map][bucket]
+  uint8_t* tmp = d_ws + ws.tmp_off;
+  const int kw = (pd.key_len + 3) / 4;
+  // two 512-thread workgroups per CU in both passes: their load / rank / store phases
+  // interleave (one prefetching 1024-thread workgroup measured slower: 9.4 vs 8.4 ms of
+  // pass A per 17 GB step, and pass B spills; profiles/r02_sweeps/msd)
+  constexpr uint32_t NWA = 8, NWB = 4, PTB = 8;
+  timer_note(timer, kHist, "k_msd16a");
+  timer_begin(timer, kHist, s);
+  const uint32_t wpc = (uint32_t)tn.small_wgs_per_cu;
+  const dim3 ga(std::min<uint32_t>(g.num_maps * cpm, ncu * wpc));
+#define SUX_M16A(KW, DB)                                                                           \
+  do {                                                                                             \
+    constexpr size_t ldsa = M16a<NWA, DB>::lds_bytes();                                            \
+    allow_lds(reinterpret_cast<const void*>(&k_msd16a<KW, NWA, DB>), ldsa);                        \
+    hipLaunchKernelGGL((k_msd16a<KW, NWA, DB>), ga, dim3(NWA * kWave), ldsa, s, pd, g, cpm, nbk,   \
+                       offs, d_pids, tmp);                                                         \
+  } while (0)
+#define SUX_M16AK(DB)                   \
+  do {                                  \
+    if (kw <= 1) SUX_M16A(1, DB);       \
+    else if (kw == 2) SUX_M16A(2, DB);  \
+    else if (kw == 3) SUX_M16A(3, DB);  \
+    else SUX_M16A(4, DB);               \
+  } while (0)
+  if (nbk > 512) SUX_M16AK(10);
+  else if (nbk > 256) SUX_M16AK(9);
+  else SUX_M16AK(8);
+#undef SUX_M16AK
+#undef SUX_M16A
+  timer_end(timer, kHist, s);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  timer_note(timer, kScan, "k_msd16_scan");
+  timer_begin(timer, kScan, s);
+  hipLaunchKernelGGL(k_msd16_scan, dim3(g.num_maps), dim3(kScanThreads), 0, s, g, cpm, nbk, offs,
+                     segbase, d_index, d_index_be, d_peer_bytes, R);
+  timer_end(timer, kScan, s);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  timer_note(timer, kScatter, "k_msd16b");
+  timer_begin(timer, kScatter, s);
+  // pass B's 256-thread workgroups are half the size of pass A's: twice as many per CU
+  const dim3 gb(std::min<uint32_t>(g.num_maps * nbk, ncu * 2 * wpc));
+  constexpr size_t ldsb = M16b<NWB, PTB>::lds_bytes();
+  static_assert(4 * ldsb <= 160 * 1024, "pass B: four workgroups per CU");
+  static_assert(2 * M16a<NWA, 10>::lds_bytes() <= 160 * 1024, "pass A: two workgroups per CU");
+#define SUX_M16B(KW)                                                                               \
+  do {                                                                                             \
+    allow_lds(reinterpret_cast<const void*>(&k_msd16b<KW, NWB, PTB>), ldsb);                      \
+    hipLaunchKernelGGL((k_msd16b<KW, NWB, PTB>), gb, dim3(NWB * kWave), ldsb, s, pd, g, cpm, nbk,  \
+                       offs, segbase, tmp, d_out, d_index, d_index_be);                            \
+  } while (0)
+  if (kw <= 1) SUX_M16B(1);
+  else if (kw == 2) SUX_M16B(2);
+  else if (kw == 3) SUX_M16B(3);
+  else SUX_M16B(4);
+#undef SUX_M16B
+  timer_end(timer, kScatter, s);
+  return hipGetLastError();
+}
+
+hipError_t launch_hist16(const PartDev& pd, const MapGroup& g, uint16_t* pids, uint32_t* counts,
+                         hipStream_t s) {
+  const uint32_t ncu = (uint32_t)std::max(1, stream_cus(s));
+  const size_t lds = (size_t)pd.R * 4;
+  const int kw = (pd.key_len + 3) / 4;
+  const dim3 gridp(std::min<uint32_t>(g.num_maps * g.tiles_per_map,
+                                      ncu * std::max<uint32_t>(1, (160u * 1024) / (uint32_t)lds)));
+#define SUX_H16(KW)                                                                        \
+  do {                                                                                     \
+    allow_lds(reinterpret_cast<const void*>(&k_hist16<KW>), lds);                          \
+    hipLaunchKernelGGL((k_hist16<KW>), gridp, dim3(1024), lds, s, pd, g, pids, counts);     \
+  } while (0)
+  if (kw <= 1) SUX_H16(1);
+  else if (kw == 2) SUX_H16(2);
+  else if (kw == 3) SUX_H16(3);
+  else SUX_H16(4);
+#undef SUX_H16
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter16(const MapGroup& g, int R, int pid_bits, const uint16_t* pids,
+                            const uint32_t* prefix, const uint64_t* base, uint8_t* d_out,
+                            const Tuning& tn, Timer* timer, hipStream_t s) {
+  const uint32_t ncu = (uint32_t)std::max(1, stream_cus(s));
+  const uint32_t total_tiles = g.num_maps * g.tiles_per_map;
+  if (R <= kS16sMaxR && tn.small_kernel != 1) {
+    timer_note(timer, kScatter, "k_scatter16s");
+    const size_t lds = Sc16s::lds_bytes(R);
+    allow_lds(reinterpret_cast<const void*>(&k_scatter16s), lds);
+    const dim3 grid(std::min<uint32_t>(total_tiles, ncu));  // one LDS-bound workgroup per CU
+    hipLaunchKernelGGL(k_scatter16s, grid, dim3(1024), lds, s, g, R, pid_bits, pids, prefix, base,
+                       d_out);
+    return hipGetLastError();
+  }
+  timer_note(timer, kScatter, "k_scatter16b");
+  const size_t lds = (size_t)R * 4;
+  const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(2, (160u * 1024) / (uint32_t)lds));
+  const dim3 grid(std::min<uint32_t>(total_tiles, ncu * per_cu));
+  const int gb = tn.small_groups;  // 64-record groups per turn
+#define SUX_S16B(GB)                                                                               \
+  do {                                                                                             \
+    allow_lds(reinterpret_cast<const void*>(&k_scatter16b<16, GB>), lds);                          \
+    hipLaunchKernelGGL((k_scatter16b<16, GB>), grid, dim3(1024), lds, s, g, R, pid_bits, pids,     \
+                       prefix, base, d_out);                                                       \
+  } while (0)
+  if (gb == 1) SUX_S16B(1);
+  else if (gb == 2) SUX_S16B(2);
+  else SUX_S16B(4);
+#undef SUX_S16B
+  return hipGetLastError();
+}
+
+}  // namespace sux

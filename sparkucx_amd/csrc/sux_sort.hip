@@ -14,13 +14,9 @@
 // Equal keys keep their input order (every pass is stable and the index is never a digit).
 // Segmented (sux_sort_segments): the record's segment id, big-endian, sits above the key bytes,
 // so one sort orders every segment (a reducer's partitions) in place.
-#include <hip/hip_runtime.h>
-
-#include "sux_internal.h"
+#include "sux_part.h"
 
 namespace sux {
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // Pair bytes: [0, kbytes) the order key (segment id big-endian, then the key big-endian, sign
 // flipped for signed kinds); then either the record index as u32 LE at [12, 16) (gather mode) or,
@@ -263,6 +259,138 @@ hipError_t launch_gather_records(const void* in, const void* pairs, uint64_t n, 
   hipLaunchKernelGGL(k_gather_records, dim3((uint32_t)blocks), dim3(256), 0, s,
                      static_cast<const uint32_t*>(in), static_cast<const u32x4*>(pairs), n, W,
                      magic, static_cast<uint32_t*>(out));
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// MSD finish (sux_sort_records / sux_sort_segments): one stable digit pass
+// over the top bits of the keys' varying range leaves R buckets of <= kSortLocalCap pairs
+// (checked on the host); k_sort_local then sorts every bucket inside LDS by a stable LSD radix
+// over the lower key digits that vary (8-bit digits: wave-ballot ranks + one block scan per
+// digit; the pairs live in registers, one LDS buffer takes each digit's permutation) and writes
+// it back.  Each pair crosses HBM twice
+// after the top pass instead of twice per digit.  Stable: the top pass keeps input order inside
+// a bucket and every LDS pass is stable.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t pair_digit8(const u32x4& w, uint32_t sh) {
+  const uint64_t hi = ((uint64_t)__builtin_bswap32(w[0]) << 32) | __builtin_bswap32(w[1]);
+  const uint64_t lo = ((uint64_t)__builtin_bswap32(w[2]) << 32) | __builtin_bswap32(w[3]);
+  const uint64_t v = sh >= 64 ? (hi >> (sh - 64)) : ((lo >> sh) | (sh ? (hi << (64 - sh)) : 0));
+  return (uint32_t)v & 255u;
+}
+
+template <uint32_t NW, uint32_t CAP>  // buf[CAP] u32x4 | wc[NW][256] u32 | wsum[NW]
+struct SortLocal {
+  static constexpr uint32_t NT = NW * kWave, PT = CAP / NT, NB = 256;
+  static constexpr uint32_t lds_bytes() { return CAP * 16 + NW * NB * 4 + NW * 4; }
+};
+
+// <8 waves, 4096 pairs>: two workgroups per CU; <4 waves, 1024 pairs>: six per CU, for the
+// ~600-pair buckets of a 5 M-record reduce partition
+template <uint32_t NW, uint32_t CAP>
+__global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : CAP == 1024 ? 6 : 4) void k_sort_local(const u32x4* __restrict__ in,
+                                                        u32x4* __restrict__ out,
+                                                        const int64_t* __restrict__ index,
+                                                        uint32_t R, SortDigits dg) {
+  using K = SortLocal<NW, CAP>;
+  constexpr uint32_t NT = K::NT, PT = K::PT, NB = K::NB;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  u32x4* buf = reinterpret_cast<u32x4*>(lds8);
+  uint32_t* wc = reinterpret_cast<uint32_t*>(buf + CAP);  // [NW][NB]
+  uint32_t* wsum = wc + NW * NB;
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
+  __syncthreads();
+  for (uint32_t b = xcd_map(blockIdx.x, gridDim.x); b < R; b += gridDim.x) {
+    const uint64_t s0 = (uint64_t)index[b] / 16, s1 = (uint64_t)index[b + 1] / 16;
+    const uint32_t n = (uint32_t)(s1 - s0);
+    if (n == 0 || n > CAP) continue;  // (the host never passes a bucket above CAP)
+    u32x4 v[PT];
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j) {  // unconditional (clamped) loads: no per-load wait
+      const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+      v[j] = in[s0 + min(e, n - 1)];
+    }
+#pragma unroll 1
+    for (int d = 0; d < (n > 1 ? dg.n : 0); ++d) {
+      const uint64_t w = d < 8 ? dg.lo : dg.hi;  // shifts packed 8 bits apiece
+      const uint32_t sh = (uint32_t)(w >> (8 * (d & 7))) & 255u;
+      uint32_t dig[PT], rank[PT];
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) {
+        const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+        const bool valid = e < n;
+        dig[j] = valid ? pair_digit8(v[j], sh) : 0u;
+        rank[j] = wave_rank<8>(dig[j], valid, wc + wave * NB, lt_mask);
+      }
+      __syncthreads();
+      scan_digit_wave<NB, NW>(wc, wsum, tid, lane, wave);
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j)
+        if (rank[j] != ~0u) buf[wc[wave * NB + dig[j]] + rank[j]] = v[j];
+      __syncthreads();
+      for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
+      // the next digit ranks the pairs in this digit's order: reload them, wave-contiguous
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) {
+        const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+        if (e < n) v[j] = buf[e];
+      }
+      __syncthreads();  // every pair is back in registers before the next digit rewrites buf
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j) {
+      const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+      if (e < n) out[s0 + e] = v[j];
+    }
+  }
+}
+
+// Largest bucket of an index table, in records of 16 bytes: one workgroup.
+__global__ __launch_bounds__(1024) void k_index_maxdiff(const int64_t* __restrict__ index,
+                                                        uint32_t R, uint64_t* __restrict__ out) {
+  __shared__ unsigned long long m;
+  if (threadIdx.x == 0) m = 0;
+  __syncthreads();
+  unsigned long long local = 0;
+  for (uint32_t p = threadIdx.x; p < R; p += 1024)
+    local = max(local, (unsigned long long)((index[p + 1] - index[p]) / 16));
+  atomicMax(&m, local);
+  __syncthreads();
+  if (threadIdx.x == 0) *out = m;
+}
+
+hipError_t launch_sort_local(const void* in_pairs, void* out_pairs, const int64_t* d_index,
+                             uint32_t R, const SortDigits& dg, uint64_t* d_maxbucket, bool max_only,
+                             hipStream_t s) {
+  if (max_only) {
+    hipLaunchKernelGGL(k_index_maxdiff, dim3(1), dim3(1024), 0, s, d_index, R, d_maxbucket);
+    return hipGetLastError();
+  }
+  const uint32_t ncu = (uint32_t)std::max(1, stream_cus(s));
+  // the smallest shape holding the largest bucket (d_maxbucket carries it, host-read, in
+  // SortDigits::pad)
+  if (dg.pad <= 1024) {
+    constexpr size_t lds = SortLocal<4, 1024>::lds_bytes();
+    hipLaunchKernelGGL((k_sort_local<4, 1024>), dim3(std::min<uint32_t>(R, 6 * ncu)), dim3(4 * kWave),
+                       lds, s, static_cast<const u32x4*>(in_pairs), static_cast<u32x4*>(out_pairs),
+                       d_index, R, dg);
+  } else if (dg.pad <= 2048) {
+    constexpr size_t lds = SortLocal<4, 2048>::lds_bytes();
+    static_assert(4 * lds <= 160 * 1024, "four workgroups per CU");
+    hipLaunchKernelGGL((k_sort_local<4, 2048>), dim3(std::min<uint32_t>(R, 4 * ncu)), dim3(4 * kWave),
+                       lds, s, static_cast<const u32x4*>(in_pairs), static_cast<u32x4*>(out_pairs),
+                       d_index, R, dg);
+  } else {
+    constexpr size_t lds = SortLocal<8, kSortLocalCap>::lds_bytes();
+    static_assert(2 * lds <= 160 * 1024, "two workgroups per CU");
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_local<8, kSortLocalCap>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((k_sort_local<8, kSortLocalCap>), dim3(std::min<uint32_t>(R, 2 * ncu)),
+                       dim3(8 * kWave), lds, s, static_cast<const u32x4*>(in_pairs),
+                       static_cast<u32x4*>(out_pairs), d_index, R, dg);
+  }
   return hipGetLastError();
 }
 

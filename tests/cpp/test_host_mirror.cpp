@@ -244,11 +244,11 @@ int main() {
   {
     UcxShuffleConf tc(std::map<std::string, std::string>{
         {"spark.shuffle.ucx.gpu.tuning.scatter_kernel", "7"},
-        {"spark.shuffle.ucx.gpu.tuning.small_kernel", "3"}});
+        {"spark.shuffle.ucx.gpu.tuning.small_kernel", "2"}});
     UcxNode node(tc, /*isDriver=*/false);
     sux_tuning t;
     EXPECT(sux_node_get_tuning(node.native(), &t) == SUX_OK && t.scatter_kernel == 7 &&
-               t.small_kernel == 3 && t.hist_kernel == 0,
+               t.small_kernel == 2 && t.hist_kernel == 0,
            "tuning keys reach the node");
     node.check();  // nothing ran: the device error word is clear
     bool threw = false;

@@ -57,6 +57,14 @@ def partitioned(recs, rs, R, rpm, kind="tera"):
     return data, index, index.size // (R + 1)
 
 
+@pytest.fixture(autouse=True, params=["grid", "queue"])
+def deal(request, tuned):
+    """Every test runs under both chunk deals of the compressor (tuning lz4_queue: 2 the fixed
+    grid-stride deal, 1 the device work queue); the bytes must not depend on the deal."""
+    tuned(lz4_queue=1 if request.param == "queue" else 2)
+    return request.param
+
+
 @pytest.mark.parametrize("bs", [1024, 32768, 65536])
 def test_terasort_map_outputs(gpu_node, bs):
     data, index, maps = partitioned(O.gen_terasort(31, 0, 40_000), 100, 200, 10_000)

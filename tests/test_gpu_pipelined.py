@@ -151,7 +151,6 @@ TUNINGS = [
     {"scatter_order": 2, "tile_records": 1024},
     {"scatter_kernel": 6},
     {"scatter_kernel": 6, "s6_chunk": 384},
-    {"scatter_kernel": 2, "hist_kernel": 2},
     {"scatter_kernel": 1, "hist_kernel": 1},
     {"hist_kernel": 3},
     {"tile_records": 1024},
@@ -174,12 +173,11 @@ def test_tuning_shapes_are_bit_exact(gpu_node, tuned, tn, R):
     gp.close()
 
 
-@pytest.mark.parametrize("kernel,groups", [(1, 1), (1, 2), (1, 4), (2, 0), (3, 0), (3, -1), (4, 0)])
+@pytest.mark.parametrize("kernel,groups", [(1, 1), (1, 2), (1, 4), (2, 0), (4, 0)])
 def test_small_record_kernels_bit_exact(gpu_node, tuned, kernel, groups):
     """Every small-record scatter: turn-taking k_scatter16b (1, 2, 4 groups per turn), the
-    turn-free sorted-chunk k_scatter16s, the two-pass bucketed k_bucket16a + k_bucket16b and
-    the two-level k_msd16a + k_msd16b (no K1)."""
-    tuned(small_kernel=kernel, small_groups=max(groups, 0), small_waves=16 if groups < 0 else 0)
+    turn-free sorted-chunk k_scatter16s and the two-level k_msd16a + k_msd16b (no K1)."""
+    tuned(small_kernel=kernel, small_groups=groups)
     recs = O.gen_small(36, 0, 200000)
     opart = O.Partitioner(O.MURMUR3_LONG, 3000, 0, 8, seed=42)
     gp = gpu_part(gpu_node, opart)
@@ -201,12 +199,11 @@ def test_small_record_kernels_bit_exact(gpu_node, tuned, kernel, groups):
     (2000, 300000, 300000, "one"),      # one bucket holds the whole map (many LDS chunks)
     (1100, 90000, 30000, "zipf"),       # a short last bucket (1100 = 17 x 64 + 12)
 ])
-@pytest.mark.parametrize("kernel", [2, 3, 316, 4])
+@pytest.mark.parametrize("kernel", [2, 4])
 def test_sorted_chunk_scatter_shapes(gpu_node, tuned, kernel, R, n, rpm, skew):
-    """kernel 316: the two-pass path with 16-wave workgroups; kernel 4: the two-level MSD path
-    (segments larger than its LDS piece in the 'one' and 'zipf' rows)"""
-    tuned(small_kernel=kernel // 100 if kernel > 100 else kernel,
-          small_waves=16 if kernel > 100 else 0)
+    """kernel 2: the sorted-chunk scatter; kernel 4: the two-level MSD path (segments larger
+    than its LDS piece in the 'one' and 'zipf' rows)"""
+    tuned(small_kernel=kernel)
     if skew == "zipf":
         recs = O.gen_zipf(39, 0, n, 1.1, 1 << 12)
         recs = recs.reshape(-1, 100)[:, :16].copy().ravel()
@@ -219,8 +216,7 @@ def test_sorted_chunk_scatter_shapes(gpu_node, tuned, kernel, R, n, rpm, skew):
     out, index, index_be = gpu_node.partition_maps(gp, torch.from_numpy(recs).cuda(), 16, rpm)
     torch.cuda.synchronize()
     expect(opart, recs, 16, rpm, out, index, index_be)
-    want = ("k_scatter16b" if R > 16384 else "k_scatter16s" if kernel == 2
-            else "k_msd16b" if kernel == 4 else "k_bucket16a+k_bucket16b")
+    want = "k_scatter16b" if R > 16384 else "k_scatter16s" if kernel == 2 else "k_msd16b"
     assert gpu_node.kernel_variant(2) == want
     gp.close()
     gpu_node.check()

@@ -1,5 +1,5 @@
 // msd_stamps.hip — per-phase cycle profile of the two-level small-record pass B (k_msd16b),
-// diagnostic build of sux_partition.hip.  Build (from the repo root):
+// diagnostic build of sux_small.hip.  Build (from the repo root):
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I sparkucx_amd/csrc \
 //         -o tools/msd_stamps tools/msd_stamps.hip
 // Runs pass A + scan + pass B over 200 maps x 2^20 16-byte random records (Spark SQL murmur3 of
@@ -8,21 +8,14 @@
 //   0 load issue (run search)  1 rank + scan + stage (waits for the loads)  2 cursors + index
 //   3 place (LDS -> HBM)       4 run table of the next segment
 #define SUX_MSD_STAMPS 1
-#include "../sparkucx_amd/csrc/sux_partition.hip"
+#include "../sparkucx_amd/csrc/sux_small.hip"
 
 #include <cstdio>
 #include <vector>
 
-// host symbols launch_partition_group refers to (never called by this tool)
+// host symbols sux_small.hip's launchers refer to (never called by this tool)
 namespace sux {
-uint64_t onepass_sync_bytes(uint32_t) { return 0; }
 int stream_cus(hipStream_t) { return 256; }
-bool onepass_eligible(const PartDev&, const MapGroup&, int, const void*, const uint64_t*,
-                      hipStream_t, uint32_t*, uint32_t*) { return false; }
-hipError_t launch_onepass(const PartDev&, const MapGroup&, uint8_t*, int64_t*, uint8_t*,
-                          uint16_t*, uint8_t*, uint32_t, uint32_t, hipStream_t) {
-  return hipErrorInvalidValue;
-}
 void timer_note(Timer*, int, const char*) {}
 void timer_begin(Timer*, int, hipStream_t) {}
 void timer_end(Timer*, int, hipStream_t) {}

@@ -26,6 +26,20 @@ hipError_t launch_onepass(const PartDev&, const MapGroup&, uint8_t*, int64_t*, u
                           uint16_t*, uint8_t*, uint32_t, uint32_t, hipStream_t) {
   return hipSuccess;
 }
+// the small-record path (sux_small.hip) is not built here
+bool msd16_eligible(const PartDev&, const MapGroup&, const LayoutDesc&, const uint8_t*,
+                    const Workspace&, const Tuning&) { return false; }
+hipError_t launch_msd16(const PartDev&, const MapGroup&, uint8_t*, int64_t*, uint8_t*, uint16_t*,
+                        uint8_t*, const Workspace&, uint64_t*, const Tuning&, Timer*, hipStream_t) {
+  return hipErrorInvalidValue;
+}
+hipError_t launch_hist16(const PartDev&, const MapGroup&, uint16_t*, uint32_t*, hipStream_t) {
+  return hipErrorInvalidValue;
+}
+hipError_t launch_scatter16(const MapGroup&, int, int, const uint16_t*, const uint32_t*,
+                            const uint64_t*, uint8_t*, const Tuning&, Timer*, hipStream_t) {
+  return hipErrorInvalidValue;
+}
 }  // namespace sux
 
 #define CK(x)                                                                    \
