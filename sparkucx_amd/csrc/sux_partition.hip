@@ -409,13 +409,17 @@ struct Hs4 {
   static constexpr uint32_t kUnits = (CH * S + 12 + 15) / 16;
   static constexpr uint32_t kPer = (kUnits + kWave - 1) / kWave;
   static constexpr uint32_t kStage = kPer * kWave * 16;  // bytes per wave
-  // stage[4] | bounds 2(R-1) u64 | lut | hist[4][R] u32
+  // stage[4] | bounds 2(R-1) u64 | lut | hist[4][R] u32 | pid line[4][CH] u16
   static __host__ __device__ constexpr uint32_t lds_bytes(int R, bool tab) {
-    return 4 * kStage + (tab ? (uint32_t)(R - 1) * 16 + (4u << kLutBits) : 0u) + 16u * R;
+    return 4 * kStage + (tab ? (uint32_t)(R - 1) * 16 + (4u << kLutBits) : 0u) + 16u * R + 8 * CH;
   }
 };
 
-template <uint32_t S, uint32_t CH, int KW, bool TAB, bool NTL>
+// PK: the pids of a full chunk leave as 16-byte stores of 8 pids (through a wave LDS line),
+// chosen by the host when every chunk a wave's steady-state loop handles starts 16-B aligned
+// (aligned pid array, maps and tiles multiples of 8 records).  Lane-wise 2-byte stores wrote
+// 4.1 B per record (PMC, profiles/pmc_r02.json), the packed ones the 2 B of the pids.
+template <uint32_t S, uint32_t CH, int KW, bool TAB, bool NTL, bool PK>
 __global__ __launch_bounds__(256) void k_hist4(PartDev pd, MapGroup g, uint16_t* __restrict__ pids,
                                                uint32_t* __restrict__ counts) {
   using H = Hs4<S, CH>;
@@ -427,6 +431,7 @@ __global__ __launch_bounds__(256) void k_hist4(PartDev pd, MapGroup g, uint16_t*
   uint64_t* sb = reinterpret_cast<uint64_t*>(lds8 + 4 * H::kStage);
   uint32_t* slut = reinterpret_cast<uint32_t*>(sb + nb);
   uint32_t* hist_all = slut + (TAB ? (1 << kLutBits) : 0);
+  uint16_t* pline_all = reinterpret_cast<uint16_t*>(hist_all + 4 * R);  // 16-B aligned
   if constexpr (TAB) {
     for (int i = threadIdx.x; i < nb; i += 256) sb[i] = pd.bounds[i];
     for (int i = threadIdx.x; i < (1 << kLutBits); i += 256) slut[i] = pd.lut[i];
@@ -438,6 +443,7 @@ __global__ __launch_bounds__(256) void k_hist4(PartDev pd, MapGroup g, uint16_t*
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   uint32_t* hist = hist_all + wave * R;
   u32x4* stage = stage_all + wave * (H::kStage / 16);
+  uint16_t* pline = pline_all + wave * CH;
   const uint32_t* st32 = reinterpret_cast<const uint32_t*>(stage);
   const uint32_t ntiles = g.num_maps * g.tiles_per_map;
   const uint32_t Q = (g.tile_recs + 3) / 4;  // records per wave per tile
@@ -458,8 +464,10 @@ __global__ __launch_bounds__(256) void k_hist4(PartDev pd, MapGroup g, uint16_t*
   };
   // chunk c0 (held in v) -> stage -> keys -> pids + histogram; if `next` v is refilled with
   // the chunk at c0 + 2CH.  Every lane stores a pid (lanes past the chunk's end repeat the last
-  // record's), so a step issues a fixed set of memory instructions.
-  auto step = [&](uint64_t c0, u32x4 (&v)[PER], bool next) {
+  // record's), so a step issues a fixed set of memory instructions.  pk (compile-time): the
+  // chunk is full and 16-B aligned, its pids leave packed.
+  auto step = [&](uint64_t c0, u32x4 (&v)[PER], bool next, auto pk) {
+    constexpr bool packed = decltype(pk)::value;
     const uint32_t n = (uint32_t)min<uint64_t>(CH, we - c0);
     const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(g.recs + c0 * S) & 15u);
 #pragma unroll
@@ -477,10 +485,21 @@ __global__ __launch_bounds__(256) void k_hist4(PartDev pd, MapGroup g, uint16_t*
       for (int q = 0; q < KW; ++q) w[q] = st32[o + q];
       const int p = partition_words<KW, TAB>(pd, w, bounds, lut);
       if (r < n) atomicAdd(&hist[p], 1u);
-      pids[c0 + rr] = (uint16_t)p;
+      if constexpr (packed) pline[r] = (uint16_t)p;
+      else pids[c0 + rr] = (uint16_t)p;
     }
     __builtin_amdgcn_wave_barrier();
+    if constexpr (packed) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      // every lane stores (lanes past CH / 8 repeat a lower lane's unit: same bytes, same
+      // address), so no branch makes the compiler's vmcnt for the prefetched chunk conservative
+      const uint32_t u = (uint32_t)lane % (CH / 8);
+      reinterpret_cast<u32x4*>(pids + c0)[u] = reinterpret_cast<const u32x4*>(pline)[u];
+      __builtin_amdgcn_wave_barrier();
+    }
   };
+  using Packed = std::integral_constant<bool, PK>;
+  using Lanes = std::integral_constant<bool, false>;
 
   // Persistent: the workgroup walks tiles gridDim.x apart (the table above is loaded once);
   // the 4 waves split a tile, so a tile takes a quarter of a wave's time and the launch's tail
@@ -497,20 +516,21 @@ __global__ __launch_bounds__(256) void k_hist4(PartDev pd, MapGroup g, uint16_t*
       issue(wb, va);
       issue(wb + CH, vb);
       uint32_t i = 0;
-      for (; i + 3 < nch; i += 2) {
-        step(wb + (uint64_t)i * CH, va, true);
-        step(wb + (uint64_t)(i + 1) * CH, vb, true);
+      for (; i + 3 < nch; i += 2) {  // full chunks
+        step(wb + (uint64_t)i * CH, va, true, Packed{});
+        step(wb + (uint64_t)(i + 1) * CH, vb, true, Packed{});
       }
-      // tail: 2 or 3 chunks left (the third is loaded into va by the first tail step)
-      step(wb + (uint64_t)i * CH, va, i + 2 < nch);
-      step(wb + (uint64_t)(i + 1) * CH, vb, false);
-      if (i + 2 < nch) step(wb + (uint64_t)(i + 2) * CH, va, false);
+      // tail: 2 or 3 chunks left (the third is loaded into va by the first tail step); the
+      // first is full
+      step(wb + (uint64_t)i * CH, va, i + 2 < nch, Packed{});
+      step(wb + (uint64_t)(i + 1) * CH, vb, false, Lanes{});
+      if (i + 2 < nch) step(wb + (uint64_t)(i + 2) * CH, va, false, Lanes{});
     } else if (nch > 0) {
       issue(wb, va);
       if (nch > 1) issue(wb + CH, vb);
-      step(wb, va, nch > 2);
-      if (nch > 1) step(wb + CH, vb, false);
-      if (nch > 2) step(wb + 2 * CH, va, false);
+      step(wb, va, nch > 2, Lanes{});
+      if (nch > 1) step(wb + CH, vb, false, Lanes{});
+      if (nch > 2) step(wb + 2 * CH, va, false, Lanes{});
     }
     // an empty tile (the tail of a short last map) still publishes its zero counts; tile-major
     // counts are one contiguous 4R-byte store per tile, partition-major ones R strided dwords
@@ -1731,7 +1751,15 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g_in, const
     const bool tab = pd.kind == 1 && R > 1 &&
                      Hs4<100, 128>::lds_bytes(R, true) <= 160 * 1024;
     const int kw = (pd.key_len + 3) / 4;
-    (void)tab;
+    // packed pid stores: every full chunk of a wave's loop starts 16-B aligned in the pid array
+    const bool pk = (reinterpret_cast<uintptr_t>(pids) & 15) == 0 && g.records_per_map % 8 == 0 &&
+                    g.tile_recs % 32 == 0;
+#define SUX_H4V(CHV, KW, TV, NV, PV)                                                               \
+  do {                                                                                             \
+    allow_lds(reinterpret_cast<const void*>(&k_hist4<100, CHV, KW, TV, NV, PV>), lds);             \
+    hipLaunchKernelGGL((k_hist4<100, CHV, KW, TV, NV, PV>), gridp, dim3(256), lds, s, pd, g, pids,  \
+                       counts);                                                                    \
+  } while (0)
 #define SUX_H4(CHV, KW)                                                                            \
   do {                                                                                             \
     const size_t lds = Hs4<100, CHV>::lds_bytes(R, tab);                                           \
@@ -1739,17 +1767,14 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g_in, const
     if (tn.hist_wgs_per_cu > 0) per_cu = std::min<uint32_t>(per_cu, (uint32_t)tn.hist_wgs_per_cu); \
     const dim3 gridp(std::min<uint32_t>(total_tiles, ncu * per_cu));                              \
     if (tab && tn.hist_nt) {                                                                       \
-      allow_lds(reinterpret_cast<const void*>(&k_hist4<100, CHV, KW, true, true>), lds);          \
-      hipLaunchKernelGGL((k_hist4<100, CHV, KW, true, true>), gridp, dim3(256), lds, s, pd, g,     \
-                         pids, counts);                                                            \
+      if (pk) SUX_H4V(CHV, KW, true, true, true);                                                  \
+      else SUX_H4V(CHV, KW, true, true, false);                                                    \
     } else if (tab) {                                                                              \
-      allow_lds(reinterpret_cast<const void*>(&k_hist4<100, CHV, KW, true, false>), lds);         \
-      hipLaunchKernelGGL((k_hist4<100, CHV, KW, true, false>), gridp, dim3(256), lds, s, pd, g,    \
-                         pids, counts);                                                            \
+      if (pk) SUX_H4V(CHV, KW, true, false, true);                                                 \
+      else SUX_H4V(CHV, KW, true, false, false);                                                   \
     } else {                                                                                       \
-      allow_lds(reinterpret_cast<const void*>(&k_hist4<100, CHV, KW, false, false>), lds);        \
-      hipLaunchKernelGGL((k_hist4<100, CHV, KW, false, false>), gridp, dim3(256), lds, s, pd, g,   \
-                         pids, counts);                                                            \
+      if (pk) SUX_H4V(CHV, KW, false, false, true);                                                \
+      else SUX_H4V(CHV, KW, false, false, false);                                                  \
     }                                                                                              \
   } while (0)
 #define SUX_H4K(CHV)                 \
@@ -1763,6 +1788,7 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g_in, const
     else SUX_H4K(64);
 #undef SUX_H4K
 #undef SUX_H4
+#undef SUX_H4V
   } else if (hist == 3) {
     const bool tab = pd.kind == 1 && R > 1 &&
                      (size_t)(R - 1) * 16 + (4u << kLutBits) + 2048 + 16u * R <= 64 * 1024;

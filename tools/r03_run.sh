@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 3 GPU session driver: numbered steps, each under its own time limit; stops at the first
 # step that crashed or timed out (rc >= 124), records every rc.  usage: tools/r03_run.sh TAG STEP...
-#   STEP = t:<pytest args>   (python -u -m pytest ... -x -v --timeout 300)
+#   STEP = t:<pytest args>   (python -u -m pytest ... -x -v --timeout 300; shell-quoted, eval'd)
 #        = b:<bench args>    (python bench.py ... > TAG/bench_N.json)
 #        = p:<rocprof args>  (rocprofv3 --kernel-trace --stats -d TAG/prof_N -o run -- python bench.py ...)
 #        = s:<shell>         (anything else, e.g. make)
@@ -15,7 +15,7 @@ for st in "$@"; do
   n=$((n+1))
   kind=${st%%:*}; arg=${st#*:}
   case $kind in
-    t) timeout -k 10 900 python -u -m pytest $arg -x -v --timeout 300 --timeout-method thread > $out/tests_$n.log 2>&1; rc=$?
+    t) eval "timeout -k 10 900 python -u -m pytest $arg -x -v --timeout 300 --timeout-method thread" > $out/tests_$n.log 2>&1; rc=$?
        tail -3 $out/tests_$n.log ;;
     b) timeout -k 10 600 python -u bench.py $arg > $out/bench_$n.json 2> $out/bench_$n.err; rc=$?
        cat $out/bench_$n.json | head -c 600; echo ;;
