@@ -3133,6 +3133,18 @@ bool span_varies(const uint32_t* span, int lo, int hi) {
   return false;
 }
 
+// The device plan's slot (SortPlanDev): past every digit width's layout, so no pass of any width
+// writes over it.
+uint64_t sort_plan_offset(uint64_t n, uint32_t record_size) {
+  uint64_t most = 0;
+  for (int d = kSortMinDigitBits; d <= kSortMaxDigitBits; ++d) {
+    SortPlan P;
+    sort_plan(n, record_size, P, d);
+    most = std::max(most, P.total);
+  }
+  return most;
+}
+
 int sort_key_bits(int32_t kind, int32_t key_len) {
   switch (kind) {
     case SUX_SORT_BYTES:
@@ -3153,13 +3165,7 @@ int sort_key_bits(int32_t kind, int32_t key_len) {
 int sux_sort_workspace_size(uint64_t n, uint32_t record_size, uint64_t* bytes) {
   return guard([&] {
     require(bytes, SUX_EINVAL, "NULL argument");
-    uint64_t most = 0;
-    for (int d = kSortMinDigitBits; d <= kSortMaxDigitBits; ++d) {
-      SortPlan P;
-      sort_plan(n, record_size, P, d);
-      most = std::max(most, P.total);
-    }
-    *bytes = most;
+    *bytes = sort_plan_offset(n, record_size) + sux::kSortPlanBytes;
   });
 }
 
@@ -3196,8 +3202,10 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
   sort_plan(n, record_size, P, digit);
   if (n == 0) return;
   require(d_in && d_out && d_ws, SUX_EINVAL, "NULL buffer");
-  require(ws_bytes >= P.total, SUX_EINVAL,
-          "sort workspace too small: need " + std::to_string(P.total) + " bytes");
+  const uint64_t plan_off = sort_plan_offset(n, record_size);
+  require(ws_bytes >= plan_off + sux::kSortPlanBytes, SUX_EINVAL,
+          "sort workspace too small: need sux_sort_workspace_size = " +
+              std::to_string(plan_off + sux::kSortPlanBytes) + " bytes");
   require(((uintptr_t)d_in & 3) == 0 && ((uintptr_t)d_out & 3) == 0 &&
               ((uintptr_t)d_ws & 255) == 0,
           SUX_EINVAL, "records (4 B) and workspace (256 B) must be aligned");
@@ -3205,35 +3213,11 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
   node->bind();
   hipStream_t s = node->stream(stream);
   uint8_t* ws = static_cast<uint8_t*>(d_ws);
-  uint8_t* pa = ws;
-  uint8_t* pb = ws + P.pairs_bytes;
+  uint8_t* const a = ws;                  // pair buffers (both plans lay them out alike)
+  uint8_t* const b = ws + P.pairs_bytes;
   int64_t* index = reinterpret_cast<int64_t*>(ws + P.index_off);
   // records of <= 16 bytes (with the segment id) travel inside the pairs: no gather at the end
   const bool inline_rec = node->tuning.sort_gather != 1 && record_size + (uint32_t)sbytes <= 16;
-  hip_check(sux::launch_sort_pairs(static_cast<const uint8_t*>(d_in), n, record_size, key_kind,
-                                   key_offset, key_len, d_seg, nseg, sbytes, pa, ws + P.span_off,
-                                   inline_rec, s),
-            "sort pairs");
-  // which digits vary: one 24-byte read-back (the only host wait in the sort).  A stream being
-  // captured into a HIP graph cannot be waited on: then every digit pass runs (the skipped
-  // passes are identity permutations, so the bytes are the same) and the call stays async.
-  const bool all_passes = node->tuning.sort_all_passes == 1;
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  hip_check(hipStreamIsCapturing(s, &cap), "hipStreamIsCapturing");
-  const bool run_all = all_passes || cap != hipStreamCaptureStatusNone;
-  uint32_t span[6] = {0, 0, 0, ~0u, ~0u, ~0u};  // AND = 0, OR = ~0: every bit varies
-  // the read-backs land in pinned staging (a true async copy, not a pageable bounce); only a call
-  // that reads back takes it: under graph capture a cold pool would hipHostMalloc mid-capture
-  std::unique_ptr<HostLease> hrb;
-  uint8_t* hrd = nullptr;
-  if (!run_all) {
-    hrb = std::make_unique<HostLease>(node->hpool, 64);
-    hrd = static_cast<uint8_t*>(hrb->b.first);
-    hip_check(hipMemcpyAsync(hrd, ws + P.span_off, sizeof span, hipMemcpyDeviceToHost, s),
-              "sort key span");
-    hip_check(hipStreamSynchronize(s), "sort key span");
-    std::memcpy(span, hrd, sizeof span);
-  }
   sux::PartDev pd{};
   pd.kind = sux::kPartRadix;
   pd.R = 1 << digit;
@@ -3241,68 +3225,94 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
   pd.key_len = 16;
   pd.ascending = 1;
   sux::LayoutDesc lay{1, 16};
-  // digit passes: the turn-taking small-record scatter for short sorts (few tiles: 5 M TeraSort
-  // records 1.53 vs 1.69 ms), the sorted-chunk one for long ones (32 Mi int64 rows 2.55 vs
-  // 2.67 ms; profiles/r02_v14/sort_ab.txt) unless the node's tuning names one
+  // the digit passes use the turn-free sorted-chunk small-record scatter: the turn-taking one can
+  // time out into the device error word, and the sort returns before its kernels run
   sux::Tuning sort_tn = resolve_tuning(node->tuning, false);
-  // the sort's digit passes use the turn-free sorted-chunk scatter: the turn-taking one (10 %
-  // faster on the LSD passes of a 5 M-record sort, profiles/r02_v14/sort_ab.txt) can time out
-  // into the device error word, and the sort returns before its kernels run — nothing would
-  // read it (the MSD finish takes common key sets off the LSD path anyway)
-  if (node->tuning.small_kernel == 0) sort_tn.small_kernel = 2;
-  // MSD finish: one stable digit pass over the top tb varying bits, then every bucket sorted in
-  // LDS by the lower varying digits (k_sort_local) — each pair crosses HBM twice after the top
-  // pass instead of twice per digit.  Needs the key span (not under graph capture) and buckets
-  // of <= kSortLocalCap pairs: the largest is read back (a second host wait); a skewed key set
-  // falls back to the LSD passes below, from the untouched pairs.
-  bool done = false;
-  int hb = -1;  // highest varying key bit
-  if (!run_all)
-    for (int b = 127; b >= 128 - bits && hb < 0; --b)
-      if (span_varies(span, b, b + 1)) hb = b;
-  if (!run_all && hb >= 0 && node->tuning.sort_msd != 2) {
-    // at most ~1536 pairs per bucket on average (fewer, fuller buckets: the per-bucket barriers
-    // of the LDS sort are paid fewer times), at most 2^14 buckets
-    int tb = kSortMinDigitBits;
-    while (tb < 14 && (n >> tb) > 1536) ++tb;
-    const int top_lo = std::max(hb + 1 - tb, 128 - bits);
+  if (node->tuning.small_kernel == 0 || node->tuning.small_kernel == 4) sort_tn.small_kernel = 2;
+  const bool all_passes = node->tuning.sort_all_passes == 1;
+
+  // ---- the default: MSD planned on the device, no host wait (graph-capturable).  One stable
+  // digit pass over the top tb varying key bits (k_sort_plan finds them in the key span), then
+  // every bucket sorted in LDS by the lower varying 8-bit digits (k_sort_local) — each pair
+  // crosses HBM twice after the top pass instead of twice per digit.  k_sort_bucket_max checks
+  // every bucket fits; a skewed key set instead runs the LSD passes below from the untouched
+  // pairs, which the plan otherwise retires (their kernels return at once: MapGroup::skip).
+  int tb = kSortMinDigitBits;  // ~<= 1536 pairs per bucket on average, at most 2^14 buckets
+  while (tb < 14 && (n >> tb) > 1536) ++tb;
+  if (node->tuning.sort_msd != 2 && !all_passes && (n >> tb) <= sux::kSortLocalCap / 2) {
     SortPlan P1;
     sort_plan(n, record_size, P1, tb);
-    if ((n >> tb) <= sux::kSortLocalCap / 2 && P1.total <= ws_bytes) {
-      int64_t* index1 = reinterpret_cast<int64_t*>(ws + P1.index_off);
-      sux::PartDev pd1 = pd;
-      pd1.R = 1 << tb;
-      pd1.seed = top_lo;
-      P1.g.recs = pa;
-      P1.g.err = node->d_err;
-      hip_check(sux::launch_partition_group(pd1, P1.g, lay, pb, index1, nullptr, nullptr,
-                                            ws + P1.part_off, P1.ws, nullptr, sort_tn,
-                                            &node->timer, s),
-                "sort top digit pass");
-      uint64_t* d_max = reinterpret_cast<uint64_t*>(ws + P1.span_off + 32);
-      sux::SortDigits dg{};
-      hip_check(sux::launch_sort_local(nullptr, nullptr, index1, (uint32_t)pd1.R, dg, d_max, true, s),
-                "sort bucket max");
-      uint64_t maxb = 0;
-      hip_check(hipMemcpyAsync(hrd + 32, d_max, 8, hipMemcpyDeviceToHost, s), "sort bucket max");
-      hip_check(hipStreamSynchronize(s), "sort bucket max");
-      std::memcpy(&maxb, hrd + 32, 8);
-      if (maxb <= sux::kSortLocalCap) {
-        dg.pad = (int32_t)maxb;
-        for (int sh = 128 - bits; sh < top_lo; sh += 8)
-          if (span_varies(span, sh, std::min(sh + 8, top_lo))) dg.push((uint32_t)sh);
-        if (dg.n) {
-          hip_check(sux::launch_sort_local(pb, pa, index1, (uint32_t)pd1.R, dg, nullptr, false, s),
-                    "sort buckets");
-        } else {
-          std::swap(pa, pb);  // the top digit held every varying bit
-        }
-        done = true;
-      }
+    sux::SortPlanDev* plan = reinterpret_cast<sux::SortPlanDev*>(ws + plan_off);
+    hip_check(sux::launch_sort_pairs(static_cast<const uint8_t*>(d_in), n, record_size, key_kind,
+                                     key_offset, key_len, d_seg, nseg, sbytes, a,
+                                     ws + P1.span_off, inline_rec, s),
+              "sort pairs");
+    hip_check(sux::launch_sort_plan(ws + P1.span_off, bits, tb, plan, s), "sort plan");
+    int64_t* index1 = reinterpret_cast<int64_t*>(ws + P1.index_off);
+    sux::PartDev pd1 = pd;
+    pd1.R = 1 << tb;
+    pd1.dseed = &plan->top_lo;
+    P1.g.recs = a;
+    P1.g.err = node->d_err;
+    hip_check(sux::launch_partition_group(pd1, P1.g, lay, b, index1, nullptr, nullptr,
+                                          ws + P1.part_off, P1.ws, nullptr, sort_tn, &node->timer,
+                                          s),
+              "sort top digit pass");
+    int npass = 0;
+    for (int sh = 128 - bits; sh < 128; sh += digit) ++npass;
+    hip_check(sux::launch_sort_bucket_max(index1, (uint32_t)pd1.R, npass & 1, plan, s),
+              "sort bucket max");
+    hip_check(sux::launch_sort_local_planned(b, a, index1, (uint32_t)pd1.R, plan, s),
+              "sort buckets");
+    uint8_t *x = a, *y = b;
+    for (int sh = 128 - bits; sh < 128; sh += digit) {  // the fallback (retired by the plan)
+      pd.seed = sh;
+      P.g.recs = x;
+      P.g.err = node->d_err;
+      P.g.skip = &plan->lsd_skip;
+      hip_check(sux::launch_partition_group(pd, P.g, lay, y, index, nullptr, nullptr,
+                                            ws + P.part_off, P.ws, nullptr, sort_tn, &node->timer,
+                                            s),
+                "sort fallback digit pass");
+      std::swap(x, y);
     }
+    if (inline_rec)
+      hip_check(sux::launch_unpair_records_sel(a, b, &plan->final_b, n, record_size, key_kind,
+                                               key_offset, key_len, sbytes, d_out, s),
+                "sort unpair");
+    else
+      hip_check(sux::launch_gather_records_sel(d_in, a, b, &plan->final_b, n, record_size, d_out,
+                                               s),
+                "sort gather");
+    return;
+  }
+
+  // ---- LSD digit passes (sort_msd = 2, sort_all_passes = 1, or more than 2^14 x 2048 pairs).
+  // Passes whose digit never varies are skipped — which needs the key span on the host (one
+  // 24-byte read-back); a stream being captured into a HIP graph cannot be waited on, so there
+  // every pass runs (a skipped pass is an identity permutation: the bytes are the same).
+  uint8_t* pa = a;
+  uint8_t* pb = b;
+  hip_check(sux::launch_sort_pairs(static_cast<const uint8_t*>(d_in), n, record_size, key_kind,
+                                   key_offset, key_len, d_seg, nseg, sbytes, pa, ws + P.span_off,
+                                   inline_rec, s),
+            "sort pairs");
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  hip_check(hipStreamIsCapturing(s, &cap), "hipStreamIsCapturing");
+  const bool run_all = all_passes || cap != hipStreamCaptureStatusNone;
+  uint32_t span[6] = {0, 0, 0, ~0u, ~0u, ~0u};  // AND = 0, OR = ~0: every bit varies
+  if (!run_all) {
+    // pinned staging (a true async copy, not a pageable bounce); taken only when reading back:
+    // under graph capture a cold pool would hipHostMalloc mid-capture
+    HostLease hrb(node->hpool, 64);
+    uint8_t* hrd = static_cast<uint8_t*>(hrb.b.first);
+    hip_check(hipMemcpyAsync(hrd, ws + P.span_off, sizeof span, hipMemcpyDeviceToHost, s),
+              "sort key span");
+    hip_check(hipStreamSynchronize(s), "sort key span");
+    std::memcpy(span, hrd, sizeof span);
   }
   // the key occupies bits [128 - bits, 128) of the big-endian pair; least significant digit first
-  for (int sh = 128 - bits; sh < 128 && !done; sh += digit) {
+  for (int sh = 128 - bits; sh < 128; sh += digit) {
     if (!run_all && !span_varies(span, sh, sh + digit)) continue;  // identity pass
     pd.seed = sh;
     P.g.recs = pa;

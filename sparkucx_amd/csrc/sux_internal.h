@@ -29,6 +29,9 @@ struct PartDev {
   const uint32_t* lut;
   int32_t lut_bits;
   int32_t pad;
+  // a sort pass's digit shift decided on the device (k_sort_plan): when set, K1 replaces `seed`
+  // with *dseed before computing any pid
+  const int32_t* dseed;
 };
 
 // Kernel tuning of one launch: the node's sux_tuning with every default filled in (sux_api.cpp,
@@ -74,9 +77,12 @@ struct MapGroup {
   // the scan), 1 tile-major [map][tile][p] (k_hist4 with k_scatter7/8: each tile's R counters
   // are one contiguous store instead of R scattered 4-byte writes)
   uint32_t counts_tm;
+  // a sort pass the device plan may retire: when *skip != 0, K1 and K3 return at once (the
+  // pass's data buffers are not touched)
+  const uint32_t* skip;
 };
 // Device error word bits (sux_node_check turns a set word into SUX_EHIP).
-constexpr uint32_t kErrTurnTimeout = 1u;  // k_scatter16/16b: a wave waited 2^22 sleeps for its turn
+constexpr uint32_t kErrTurnTimeout = 1u;  // k_scatter16b: a wave waited 2^22 sleeps for its turn
 
 // Per-launch geometry of a group of variable-length record maps (sux_varlen.hip): record i is
 // data[offs[i] - offs[0], offs[i+1] - offs[0]).
@@ -207,25 +213,52 @@ hipError_t launch_unpair_records(const void* pairs, uint64_t n, uint32_t rs, int
 // span_ws: 8 u32 (AND of key words 0..2, OR of key words 0..2) + kSortSpanBlocks x 8 u32 partials
 constexpr uint32_t kSortSpanBlocks = 2048;
 constexpr uint64_t kSortSpanBytes = 4ull * 8 * (kSortSpanBlocks + 1);
+hipError_t launch_gather_records_sel(const void* in, const void* pairs_a, const void* pairs_b,
+                                     const uint32_t* sel, uint64_t n, uint32_t rs, void* out,
+                                     hipStream_t s);
+hipError_t launch_unpair_records_sel(const void* pairs_a, const void* pairs_b, const uint32_t* sel,
+                                     uint64_t n, uint32_t rs, int kind, int key_offset,
+                                     int key_len, int sbytes, void* out, hipStream_t s);
 hipError_t launch_gather_records(const void* in, const void* pairs, uint64_t n, uint32_t rs,
                                  void* out, hipStream_t s);
 // MSD finish of the sort (sux_sort.hip): buckets of <= kSortLocalCap pairs sorted in LDS by
-// the listed 8-bit digits (shifts into the big-endian pair, least significant first); with
-// max_only, only the largest bucket (in pairs) is written to d_maxbucket.
+// the listed 8-bit digits (shifts into the big-endian pair, least significant first).
 constexpr uint32_t kSortLocalCap = 4096;
 struct SortDigits {
   uint64_t lo, hi;  // shift of digit d in byte d (lo: digits 0..7, hi: 8..15)
   int32_t n;
-  int32_t pad;  // the largest bucket, in pairs (picks the kernel shape)
-  void push(uint32_t sh) {
+  int32_t pad;
+  __host__ __device__ void push(uint32_t sh) {
     if (n < 8) lo |= (uint64_t)sh << (8 * n);
     else hi |= (uint64_t)sh << (8 * (n - 8));
     ++n;
   }
 };
-hipError_t launch_sort_local(const void* in_pairs, void* out_pairs, const int64_t* d_index,
-                             uint32_t R, const SortDigits& dg, uint64_t* d_maxbucket, bool max_only,
-                             hipStream_t s);
+// The device-planned sort (sux_sort_records with no host wait): k_sort_plan fills the first
+// fields from the key span, k_sort_bucket_max the rest after the top-digit pass; every later
+// kernel of the sort reads its decision from here.
+struct SortPlanDev {
+  int32_t top_lo;    // shift of the top digit (the tb highest varying key bits)
+  int32_t hb;        // highest varying key bit; -1: every key is equal (the sort is the identity)
+  uint32_t msd_ok;   // 1: every top-digit bucket fits the LDS sort, which finishes the sort
+  uint32_t lsd_skip; // 1: the LSD fallback passes are not needed (msd_ok, or hb < 0)
+  uint32_t final_b;  // 1: the sorted pairs end in buffer b, 0: in buffer a
+  uint32_t pad;
+  uint64_t maxb;     // the largest top-digit bucket, in pairs
+  SortDigits dg;     // the LDS sort's digits: 8-bit, below top_lo, only those that vary
+};
+constexpr uint64_t kSortPlanBytes = 256;
+static_assert(sizeof(SortPlanDev) <= kSortPlanBytes, "plan slot");
+hipError_t launch_sort_plan(const void* span, int bits, int tb, SortPlanDev* plan, hipStream_t s);
+// Largest bucket of the top-digit index -> plan (msd_ok, lsd_skip, final_b; lsd_odd: the
+// fallback runs an odd number of passes).
+hipError_t launch_sort_bucket_max(const int64_t* d_index, uint32_t R, bool lsd_odd,
+                                  SortPlanDev* plan, hipStream_t s);
+// The LDS sort of every top-digit bucket, driven by the plan (a no-op unless plan->msd_ok):
+// one launch per bucket-size class, so each bucket runs on the smallest shape that holds it.
+hipError_t launch_sort_local_planned(const void* in_pairs, void* out_pairs, const int64_t* d_index,
+                                     uint32_t R, const SortPlanDev* plan, hipStream_t s);
+
 
 // Generators (sux_gen.hip).
 hipError_t launch_generate(int kind, uint64_t seed, uint64_t first, uint64_t n,

@@ -34,6 +34,8 @@ namespace sux {
 template <int WPG>
 __global__ __launch_bounds__(WPG * kWave) void k_hist(PartDev pd, MapGroup g, uint16_t* pids,
                                                       uint32_t* counts) {
+  if (pass_skipped(g)) return;
+  resolve_seed(pd);
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const uint32_t gtile = blockIdx.x * WPG + wave;
@@ -60,7 +62,9 @@ __global__ __launch_bounds__(WPG * kWave) void k_hist(PartDev pd, MapGroup g, ui
 // ------------------------------------------------------------------------------------------
 
 __global__ __launch_bounds__(256) void k_tile_scan(uint32_t* counts, uint64_t* totals,
-                                                   uint32_t rows, uint32_t tiles) {
+                                                   uint32_t rows, uint32_t tiles,
+    const uint32_t* __restrict__ skip) {
+  if (skip && *skip) return;  // a retired sort pass (MapGroup::skip)
   const int lane = threadIdx.x % kWave;
   const uint32_t row = blockIdx.x * 4 + threadIdx.x / kWave;
   if (row >= rows) return;
@@ -88,7 +92,9 @@ __global__ __launch_bounds__(256) void k_tile_scan(uint32_t* counts, uint64_t* t
 // Few tiles per map (large R: 10,000 partitions x 16 tiles): one thread per row, so a row of
 // T <= 64 counters is not a whole (mostly idle) wave.
 __global__ __launch_bounds__(256) void k_tile_scan_rows(uint32_t* counts, uint64_t* totals,
-                                                        uint32_t rows, uint32_t tiles) {
+                                                        uint32_t rows, uint32_t tiles,
+    const uint32_t* __restrict__ skip) {
+  if (skip && *skip) return;  // a retired sort pass (MapGroup::skip)
   const uint32_t row = blockIdx.x * 256 + threadIdx.x;
   if (row >= rows) return;
   uint32_t* c = counts + (uint64_t)row * tiles;
@@ -117,7 +123,9 @@ __global__ __launch_bounds__(256) void k_tile_scan_rows(uint32_t* counts, uint64
 // the tile column (reads: 16 consecutive counters of one tile row per wave quarter), the 16
 // segment sums of a partition are scanned in LDS, and every thread rewrites its segment.
 __global__ __launch_bounds__(256) void k_tile_scan_tm(uint32_t* counts, uint64_t* totals,
-                                                      uint32_t maps, uint32_t R, uint32_t tiles) {
+                                                      uint32_t maps, uint32_t R, uint32_t tiles,
+    const uint32_t* __restrict__ skip) {
+  if (skip && *skip) return;  // a retired sort pass (MapGroup::skip)
   __shared__ uint32_t seg[16][17];
   const uint32_t pl = threadIdx.x % 16, sg = threadIdx.x / 16;
   const uint32_t pgroups = (R + 15) / 16;
@@ -170,7 +178,9 @@ __global__ __launch_bounds__(kScanThreads) void k_map_scan(const uint64_t* __res
                                                            int R, int G, uint32_t rec_size,
                                                            uint64_t records_per_map,
                                                            uint64_t num_records,
-                                                           const uint64_t* __restrict__ map_offs) {
+                                                           const uint64_t* __restrict__ map_offs,
+    const uint32_t* __restrict__ skip) {
+  if (skip && *skip) return;  // a retired sort pass (MapGroup::skip)
   __shared__ uint64_t sh[2 * kWave + 1];
   __shared__ unsigned long long hs[1024];
   const uint32_t m = blockIdx.x;
@@ -284,6 +294,7 @@ __global__ __launch_bounds__(WPG * kWave) void k_scatter(MapGroup g, int R, int 
                                                          const uint32_t* __restrict__ prefix,
                                                          const uint64_t* __restrict__ base,
                                                          uint8_t* __restrict__ out) {
+  if (pass_skipped(g)) return;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const uint32_t gtile = blockIdx.x * WPG + wave;
@@ -334,6 +345,8 @@ __global__ __launch_bounds__(WPG * kWave) void k_scatter(MapGroup g, int R, int 
 template <int KW, int RPL, bool TAB>
 __global__ __launch_bounds__(256) void k_hist3(PartDev pd, MapGroup g, uint16_t* __restrict__ pids,
                                                uint32_t* __restrict__ counts) {
+  if (pass_skipped(g)) return;
+  resolve_seed(pd);
   extern __shared__ __attribute__((aligned(16))) uint64_t ldsq[];
   const int R = pd.R;
   const int nb = TAB ? 2 * (R - 1) : 0;
@@ -422,6 +435,8 @@ struct Hs4 {
 template <uint32_t S, uint32_t CH, int KW, bool TAB, bool NTL, bool PK>
 __global__ __launch_bounds__(256) void k_hist4(PartDev pd, MapGroup g, uint16_t* __restrict__ pids,
                                                uint32_t* __restrict__ counts) {
+  if (pass_skipped(g)) return;
+  resolve_seed(pd);
   using H = Hs4<S, CH>;
   constexpr uint32_t PER = H::kPer;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
@@ -641,6 +656,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter6(MapGroup g, int R, int pid
                                                      const uint64_t* __restrict__ base,
                                                      uint8_t* __restrict__ out, uint32_t tpw,
                                                      uint32_t wg_per_map) {
+  if (pass_skipped(g)) return;
   using K = Sc6<S, C, NW>;
   constexpr uint32_t NT = K::NT, W = K::W, RPW = K::RPW, NG = K::NG, PER = K::kPer;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
@@ -867,6 +883,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter7(MapGroup g, int R, int pid
                                                      const uint64_t* __restrict__ base,
                                                      uint8_t* __restrict__ out, uint32_t tpw,
                                                      uint32_t wg_per_map) {
+  if (pass_skipped(g)) return;
   using K = Sc7<S, C, NW>;
   constexpr uint32_t NT = K::NT, W = K::W, RPW = K::RPW, NG = K::NG, PER = K::kPer;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
@@ -1224,6 +1241,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
                                                      const uint64_t* __restrict__ base,
                                                      uint8_t* __restrict__ out, uint32_t cyc,
                                                      uint32_t tw0, uint32_t tw1) {
+  if (pass_skipped(g)) return;
   using K = Sc8<S, C, NW>;
   constexpr uint32_t NT = K::NT, W = K::W, RPW = K::RPW, NG = K::NG, PER = K::kPer;
   constexpr uint32_t RM = 208;  // K's RMAX: the tables' compile-time stride
@@ -1729,8 +1747,8 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g_in, const
   // ---- K1: pids + tile histograms
   const int hv = tn.hist_kernel;
   const bool words = pd.kind != 4 && pd.key_offset % 4 == 0 && pd.key_len <= 16;
-  // small records with many partitions: k_hist16 + tile-major counts + k_scatter16, together
-  const bool s16 = hv >= 4 && sv >= 7 && words && S == 16 && R > 1024 &&
+  // 16-byte records, R >= 256: k_hist16 + tile-major counts + k_scatter16s / k_scatter16b (sux_small.hip)
+  const bool s16 = hv >= 4 && sv >= 7 && words && S == 16 && R >= 256 &&
                    (reinterpret_cast<uintptr_t>(g.recs) & 15) == 0 &&
                    (reinterpret_cast<uintptr_t>(d_out) & 15) == 0;
   int hist = 1;
@@ -1818,19 +1836,19 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g_in, const
   const uint32_t rows = g.num_maps * (uint32_t)R;
   if (s16 || g.counts_tm)
     hipLaunchKernelGGL(k_tile_scan_tm, dim3(g.num_maps * ((R + 15) / 16)), dim3(256), 0, s, counts,
-                       totals, g.num_maps, (uint32_t)R, g.tiles_per_map);
+                       totals, g.num_maps, (uint32_t)R, g.tiles_per_map, g.skip);
   else if (g.tiles_per_map <= 64)
     hipLaunchKernelGGL(k_tile_scan_rows, dim3((rows + 255) / 256), dim3(256), 0, s, counts, totals,
-                       rows, g.tiles_per_map);
+                       rows, g.tiles_per_map, g.skip);
   else
     hipLaunchKernelGGL(k_tile_scan, dim3((rows + 3) / 4), dim3(256), 0, s, counts, totals, rows,
-                       g.tiles_per_map);
+                       g.tiles_per_map, g.skip);
   const uint64_t L = (uint64_t)g.num_maps * R;
   uint64_t* pre = base + L;
   uint64_t* mh = base + 2 * L;
   hipLaunchKernelGGL(k_map_scan, dim3(g.num_maps), dim3(kScanThreads), 0, s, totals, base, pre, mh,
                      d_index, d_index_be, lay.world == 1 ? d_peer_bytes : nullptr, R, lay.world,
-                     g.rec_size, g.records_per_map, g.num_records, nullptr);
+                     g.rec_size, g.records_per_map, g.num_records, nullptr, g.skip);
   if (lay.world > 1) {
     hipLaunchKernelGGL(k_peer_off, dim3(1), dim3(kScanThreads), 0, s, mh, d_peer_bytes,
                        g.num_maps, lay.world, g.rec_size);
@@ -1952,7 +1970,7 @@ hipError_t launch_varlen_map_scan(const VarGroup& g, int R, const uint64_t* tota
   const uint64_t L = (uint64_t)g.num_maps * R;
   hipLaunchKernelGGL(k_map_scan, dim3(g.num_maps), dim3(kScanThreads), 0, s, totals, base,
                      base + L, base + 2 * L, d_index, d_index_be, nullptr, R, 1, 1u,
-                     g.records_per_map, g.num_records, g.offs);
+                     g.records_per_map, g.num_records, g.offs, nullptr);
   return hipGetLastError();
 }
 
@@ -1962,7 +1980,7 @@ hipError_t launch_rows_index(const uint64_t* sizes, uint32_t maps, uint32_t R, u
   const uint64_t L = (uint64_t)maps * R;
   hipLaunchKernelGGL(k_map_scan, dim3(maps), dim3(kScanThreads), 0, s, sizes, base, base + L,
                      base + 2 * L, d_index, d_index_be, nullptr, (int)R, 1, 1u, 0ull, 0ull,
-                     nullptr);
+                     nullptr, nullptr);
   return hipGetLastError();
 }
 

@@ -98,12 +98,16 @@ __device__ inline u128 inline_unpair(u128 pr, int kind, int off, int klen, int s
 }
 
 // Inline mode's final pass: sorted pair j -> output record j.  Streaming: 16 B read, rs B written.
+// sel (device-planned sort): *sel != 0 takes the pairs from pairs_b.
 __global__ __launch_bounds__(256) void k_unpair_records(const u32x4* __restrict__ pairs, uint64_t n,
                                                         uint32_t rs, int kind, int key_offset,
                                                         int key_len, int sbytes,
-                                                        uint32_t* __restrict__ out) {
+                                                        uint32_t* __restrict__ out,
+                                                        const u32x4* __restrict__ pairs_b,
+                                                        const uint32_t* __restrict__ sel) {
   const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (j >= n) return;
+  if (sel && *sel) pairs = pairs_b;
   const u32x4 p = pairs[j];
   const u128 pr = (u128)p[0] | ((u128)p[1] << 32) | ((u128)p[2] << 64) | ((u128)p[3] << 96);
   const u128 rec = inline_unpair(pr, kind, key_offset, key_len, sbytes, rs);
@@ -200,7 +204,10 @@ __global__ __launch_bounds__(256) void k_span_reduce(const uint32_t* __restrict_
 __global__ __launch_bounds__(256) void k_gather_records(const uint32_t* __restrict__ in,
                                                         const u32x4* __restrict__ pairs,
                                                         uint64_t n, uint32_t W, uint32_t magic,
-                                                        uint32_t* __restrict__ out) {
+                                                        uint32_t* __restrict__ out,
+                                                        const u32x4* __restrict__ pairs_b,
+                                                        const uint32_t* __restrict__ sel) {
+  if (sel && *sel) pairs = pairs_b;
   const uint64_t total = n * W;
   const uint32_t* idx = reinterpret_cast<const uint32_t*>(pairs) + 3;  // pairs[j][3]
   if (magic) {
@@ -238,17 +245,30 @@ hipError_t launch_sort_pairs(const uint8_t* in, uint64_t n, uint32_t rs, int kin
   return hipGetLastError();
 }
 
-hipError_t launch_unpair_records(const void* pairs, uint64_t n, uint32_t rs, int kind,
-                                 int key_offset, int key_len, int sbytes, void* out, hipStream_t s) {
+hipError_t launch_unpair_records_sel(const void* pairs_a, const void* pairs_b, const uint32_t* sel,
+                                     uint64_t n, uint32_t rs, int kind, int key_offset,
+                                     int key_len, int sbytes, void* out, hipStream_t s) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_unpair_records, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
-                     static_cast<const u32x4*>(pairs), n, rs, kind, key_offset, key_len, sbytes,
-                     static_cast<uint32_t*>(out));
+                     static_cast<const u32x4*>(pairs_a), n, rs, kind, key_offset, key_len, sbytes,
+                     static_cast<uint32_t*>(out), static_cast<const u32x4*>(pairs_b), sel);
   return hipGetLastError();
+}
+
+hipError_t launch_unpair_records(const void* pairs, uint64_t n, uint32_t rs, int kind,
+                                 int key_offset, int key_len, int sbytes, void* out, hipStream_t s) {
+  return launch_unpair_records_sel(pairs, nullptr, nullptr, n, rs, kind, key_offset, key_len,
+                                   sbytes, out, s);
 }
 
 hipError_t launch_gather_records(const void* in, const void* pairs, uint64_t n, uint32_t rs,
                                  void* out, hipStream_t s) {
+  return launch_gather_records_sel(in, pairs, nullptr, nullptr, n, rs, out, s);
+}
+
+hipError_t launch_gather_records_sel(const void* in, const void* pairs, const void* pairs_b,
+                                     const uint32_t* sel, uint64_t n, uint32_t rs, void* out,
+                                     hipStream_t s) {
   if (n == 0) return hipSuccess;
   const uint64_t total = n * (rs / 4);
   const uint64_t blocks = std::min<uint64_t>((total + 255) / 256, 256ull * 32);
@@ -258,14 +278,14 @@ hipError_t launch_gather_records(const void* in, const void* pairs, uint64_t n, 
                              ? (uint32_t)(((1ull << 32) + W - 1) / W) : 0u;
   hipLaunchKernelGGL(k_gather_records, dim3((uint32_t)blocks), dim3(256), 0, s,
                      static_cast<const uint32_t*>(in), static_cast<const u32x4*>(pairs), n, W,
-                     magic, static_cast<uint32_t*>(out));
+                     magic, static_cast<uint32_t*>(out), static_cast<const u32x4*>(pairs_b), sel);
   return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------
 // MSD finish (sux_sort_records / sux_sort_segments): one stable digit pass
 // over the top bits of the keys' varying range leaves R buckets of <= kSortLocalCap pairs
-// (checked on the host); k_sort_local then sorts every bucket inside LDS by a stable LSD radix
+// (checked on the device, k_sort_bucket_max); k_sort_local then sorts every bucket inside LDS by a stable LSD radix
 // over the lower key digits that vary (8-bit digits: wave-ballot ranks + one block scan per
 // digit; the pairs live in registers, one LDS buffer takes each digit's permutation) and writes
 // it back.  Each pair crosses HBM twice
@@ -286,12 +306,16 @@ struct SortLocal {
 };
 
 // <8 waves, 4096 pairs>: two workgroups per CU; <4 waves, 1024 pairs>: six per CU, for the
-// ~600-pair buckets of a 5 M-record reduce partition
+// ~600-pair buckets of a 5 M-record reduce partition.  A launch sorts the buckets of
+// lo_cap < n <= CAP (one launch per size class) when the plan says the MSD path finishes the sort.
 template <uint32_t NW, uint32_t CAP>
 __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : CAP == 1024 ? 6 : 4) void k_sort_local(const u32x4* __restrict__ in,
                                                         u32x4* __restrict__ out,
                                                         const int64_t* __restrict__ index,
-                                                        uint32_t R, SortDigits dg) {
+                                                        uint32_t R, uint32_t lo_cap,
+                                                        const SortPlanDev* __restrict__ plan) {
+  if (!plan->msd_ok || plan->dg.n == 0) return;  // the LSD fallback, or the top digit was all
+  const SortDigits dg = plan->dg;
   using K = SortLocal<NW, CAP>;
   constexpr uint32_t NT = K::NT, PT = K::PT, NB = K::NB;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
@@ -305,7 +329,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : CAP == 1024 ? 6 : 4) void k_
   for (uint32_t b = xcd_map(blockIdx.x, gridDim.x); b < R; b += gridDim.x) {
     const uint64_t s0 = (uint64_t)index[b] / 16, s1 = (uint64_t)index[b + 1] / 16;
     const uint32_t n = (uint32_t)(s1 - s0);
-    if (n == 0 || n > CAP) continue;  // (the host never passes a bucket above CAP)
+    if (n <= lo_cap || n > CAP) continue;  // another size class (n = 0: nothing to do)
     u32x4 v[PT];
 #pragma unroll
     for (uint32_t j = 0; j < PT; ++j) {  // unconditional (clamped) loads: no per-load wait
@@ -347,9 +371,39 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : CAP == 1024 ? 6 : 4) void k_
   }
 }
 
-// Largest bucket of an index table, in records of 16 bytes: one workgroup.
-__global__ __launch_bounds__(1024) void k_index_maxdiff(const int64_t* __restrict__ index,
-                                                        uint32_t R, uint64_t* __restrict__ out) {
+// True when bits [lo, hi) of the big-endian 128-bit pair differ between some records (span: the
+// AND of key words 0..2, then their OR) — sux_api.cpp's span_varies, on the device.
+__device__ bool span_varies_dev(const uint32_t* span, int lo, int hi) {
+  for (int b = max(lo, 32); b < min(hi, 128); ++b) {
+    const int byte = 15 - b / 8;
+    const uint32_t diff = span[byte / 4] ^ span[3 + byte / 4];
+    if ((diff >> (8 * (byte % 4) + b % 8)) & 1u) return true;
+  }
+  return false;
+}
+
+// The plan's first half from the key span: the highest varying key bit, the top digit (its tb
+// bits end there) and the LDS sort's 8-bit digits below it that vary.  One thread.
+__global__ void k_sort_plan(const uint32_t* __restrict__ span, int bits, int tb,
+                            SortPlanDev* __restrict__ plan) {
+  if (threadIdx.x != 0) return;
+  int hb = -1;
+  for (int b = 127; b >= 128 - bits && hb < 0; --b)
+    if (span_varies_dev(span, b, b + 1)) hb = b;
+  const int top_lo = hb >= 0 ? max(hb + 1 - tb, 128 - bits) : 128 - bits;
+  SortDigits dg{};
+  for (int sh = 128 - bits; sh < top_lo; sh += 8)
+    if (span_varies_dev(span, sh, min(sh + 8, top_lo))) dg.push((uint32_t)sh);
+  plan->top_lo = top_lo;
+  plan->hb = hb;
+  plan->dg = dg;
+}
+
+// The plan's second half: the largest bucket of the top-digit index decides between the LDS
+// finish and the LSD fallback, and where the sorted pairs end.  One workgroup.
+__global__ __launch_bounds__(1024) void k_sort_bucket_max(const int64_t* __restrict__ index,
+                                                          uint32_t R, uint32_t lsd_odd,
+                                                          SortPlanDev* __restrict__ plan) {
   __shared__ unsigned long long m;
   if (threadIdx.x == 0) m = 0;
   __syncthreads();
@@ -358,39 +412,50 @@ __global__ __launch_bounds__(1024) void k_index_maxdiff(const int64_t* __restric
     local = max(local, (unsigned long long)((index[p + 1] - index[p]) / 16));
   atomicMax(&m, local);
   __syncthreads();
-  if (threadIdx.x == 0) *out = m;
+  if (threadIdx.x == 0) {
+    const bool all_equal = plan->hb < 0;
+    const bool ok = !all_equal && m <= kSortLocalCap;
+    plan->maxb = m;
+    plan->msd_ok = ok ? 1u : 0u;
+    plan->lsd_skip = (ok || all_equal) ? 1u : 0u;
+    // a -> top pass -> b -> LDS sort -> a; no lower digit varies: the top pass's b; the LSD
+    // fallback: a after an even number of passes; every key equal: a (the input order)
+    plan->final_b = all_equal ? 0u : ok ? (plan->dg.n ? 0u : 1u) : lsd_odd;
+  }
 }
 
-hipError_t launch_sort_local(const void* in_pairs, void* out_pairs, const int64_t* d_index,
-                             uint32_t R, const SortDigits& dg, uint64_t* d_maxbucket, bool max_only,
-                             hipStream_t s) {
-  if (max_only) {
-    hipLaunchKernelGGL(k_index_maxdiff, dim3(1), dim3(1024), 0, s, d_index, R, d_maxbucket);
-    return hipGetLastError();
-  }
+hipError_t launch_sort_plan(const void* span, int bits, int tb, SortPlanDev* plan, hipStream_t s) {
+  hipLaunchKernelGGL(k_sort_plan, dim3(1), dim3(64), 0, s, static_cast<const uint32_t*>(span),
+                     bits, tb, plan);
+  return hipGetLastError();
+}
+
+hipError_t launch_sort_bucket_max(const int64_t* d_index, uint32_t R, bool lsd_odd,
+                                  SortPlanDev* plan, hipStream_t s) {
+  hipLaunchKernelGGL(k_sort_bucket_max, dim3(1), dim3(1024), 0, s, d_index, R,
+                     lsd_odd ? 1u : 0u, plan);
+  return hipGetLastError();
+}
+
+hipError_t launch_sort_local_planned(const void* in_pairs, void* out_pairs, const int64_t* d_index,
+                                     uint32_t R, const SortPlanDev* plan, hipStream_t s) {
   const uint32_t ncu = (uint32_t)std::max(1, stream_cus(s));
-  // the smallest shape holding the largest bucket (d_maxbucket carries it, host-read, in
-  // SortDigits::pad)
-  if (dg.pad <= 1024) {
-    constexpr size_t lds = SortLocal<4, 1024>::lds_bytes();
-    hipLaunchKernelGGL((k_sort_local<4, 1024>), dim3(std::min<uint32_t>(R, 6 * ncu)), dim3(4 * kWave),
-                       lds, s, static_cast<const u32x4*>(in_pairs), static_cast<u32x4*>(out_pairs),
-                       d_index, R, dg);
-  } else if (dg.pad <= 2048) {
-    constexpr size_t lds = SortLocal<4, 2048>::lds_bytes();
-    static_assert(4 * lds <= 160 * 1024, "four workgroups per CU");
-    hipLaunchKernelGGL((k_sort_local<4, 2048>), dim3(std::min<uint32_t>(R, 4 * ncu)), dim3(4 * kWave),
-                       lds, s, static_cast<const u32x4*>(in_pairs), static_cast<u32x4*>(out_pairs),
-                       d_index, R, dg);
-  } else {
-    constexpr size_t lds = SortLocal<8, kSortLocalCap>::lds_bytes();
-    static_assert(2 * lds <= 160 * 1024, "two workgroups per CU");
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_local<8, kSortLocalCap>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((k_sort_local<8, kSortLocalCap>), dim3(std::min<uint32_t>(R, 2 * ncu)),
-                       dim3(8 * kWave), lds, s, static_cast<const u32x4*>(in_pairs),
-                       static_cast<u32x4*>(out_pairs), d_index, R, dg);
-  }
+  const u32x4* in = static_cast<const u32x4*>(in_pairs);
+  u32x4* out = static_cast<u32x4*>(out_pairs);
+  // size classes (0, 1024], (1024, 2048], (2048, kSortLocalCap]: each bucket on the smallest
+  // shape that holds it (the classes a key set leaves empty cost one index sweep each)
+  constexpr size_t l1 = SortLocal<4, 1024>::lds_bytes();
+  hipLaunchKernelGGL((k_sort_local<4, 1024>), dim3(std::min<uint32_t>(R, 6 * ncu)), dim3(4 * kWave),
+                     l1, s, in, out, d_index, R, 0u, plan);
+  constexpr size_t l2 = SortLocal<4, 2048>::lds_bytes();
+  static_assert(4 * l2 <= 160 * 1024, "four workgroups per CU");
+  hipLaunchKernelGGL((k_sort_local<4, 2048>), dim3(std::min<uint32_t>(R, 4 * ncu)), dim3(4 * kWave),
+                     l2, s, in, out, d_index, R, 1024u, plan);
+  constexpr size_t l3 = SortLocal<8, kSortLocalCap>::lds_bytes();
+  static_assert(2 * l3 <= 160 * 1024, "two workgroups per CU");
+  allow_lds(reinterpret_cast<const void*>(&k_sort_local<8, kSortLocalCap>), l3);
+  hipLaunchKernelGGL((k_sort_local<8, kSortLocalCap>), dim3(std::min<uint32_t>(R, 2 * ncu)),
+                     dim3(8 * kWave), l3, s, in, out, d_index, R, 2048u, plan);
   return hipGetLastError();
 }
 
