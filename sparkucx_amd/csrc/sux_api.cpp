@@ -1655,12 +1655,16 @@ bool spill_some(sux_node* node, uint64_t need) {
 }
 
 // A pool buffer; on SUX_ENOMEM spill map outputs (if configured) and retry.
+// Idle cached allocations go back first (a fetch after the writes spilled everything they could
+// finds the pool full of the writers' freed workspaces and slabs, not of map outputs).
 PoolBuf pool_get_or_spill(sux_node* node, uint64_t bytes) {
   for (int attempt = 0;; ++attempt) {
     try {
       return node->pool->get(bytes);
     } catch (const SuxError& e) {
-      if (e.code != SUX_ENOMEM || attempt >= 64 || !spill_some(node, bytes)) throw;
+      if (e.code != SUX_ENOMEM || attempt >= 64) throw;
+      if (node->pool->trim() > 0) continue;
+      if (!spill_some(node, bytes)) throw;
     }
   }
 }
@@ -2110,7 +2114,7 @@ int sux_write_map_output_host(sux_node* node, int32_t shuffle_id, int32_t map_in
   PoolBuf stage;
   rc = guard([&] {
     node->bind();
-    stage = node->pool->get(n * (uint64_t)rs);
+    stage = pool_get_or_spill(node, n * (uint64_t)rs);
     hip_check(hipMemcpyAsync(stage.ptr, host_records, n * (uint64_t)rs, hipMemcpyHostToDevice,
                              node->stream(stream)),
               "H2D records");
@@ -2152,7 +2156,7 @@ int sux_commit_map_output(sux_node* node, int32_t shuffle_id, int32_t map_index,
     }
     std::shared_ptr<Slab> slab;
     try {
-      slab = std::make_shared<Slab>(node->pool.get(), node->pool->get(bytes));
+      slab = std::make_shared<Slab>(node->pool.get(), pool_get_or_spill(node, bytes));
       hip_check(hipMemcpyAsync(slab->buf.ptr, d_data, bytes, hipMemcpyDefault, s), "adopt data");
       hip_check(hipStreamSynchronize(s), "sync commit");
     } catch (...) {
@@ -2319,7 +2323,7 @@ void host_allgather(sux_node* node, uint64_t tag, const void* send, uint64_t byt
           "world_size > 1 needs an RCCL communicator (comm_id) or a bootstrap "
           "(sux_node_set_bootstrap)");
   const uint64_t pad = (bytes + 255) / 256 * 256;
-  PoolBuf tmp = node->pool->get(pad * (W + 1));
+  PoolBuf tmp = pool_get_or_spill(node, pad * (W + 1));
   try {
     hip_check(hipMemcpyAsync(tmp.ptr, send, bytes, hipMemcpyHostToDevice, s), "H2D all-gather");
     nccl_check(ncclAllGather(tmp.ptr, tmp.ptr + pad, pad, ncclUint8, node->comm, s),
@@ -2410,7 +2414,7 @@ void launch_copies(sux_node* node, const std::vector<sux::CopyDesc>& desc, PoolB
   require(chunks < (1ull << 31), SUX_ERANGE, "copy request too large");
   const uint64_t dbytes = desc.size() * sizeof(sux::CopyDesc), fbytes = first.size() * 4;
   const uint64_t dpad = ((dbytes + 255) / 256) * 256;
-  aux = node->pool->get(dpad + fbytes);
+  aux = pool_get_or_spill(node, dpad + fbytes);
   hostblk = node->hpool.get(dpad + fbytes);
   uint8_t* h = static_cast<uint8_t*>(hostblk.first);
   std::memcpy(h, desc.data(), dbytes);
@@ -2985,7 +2989,7 @@ int sux_fetch_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* blo
         if (!desc.empty()) {
           const uint64_t dbytes = desc.size() * sizeof(sux::CopyDesc), fbytes = first.size() * 4;
           const uint64_t dpad = ((dbytes + 255) / 256) * 256;
-          buf->aux = node->pool->get(dpad + fbytes);
+          buf->aux = pool_get_or_spill(node, dpad + fbytes);
           uint8_t* d_desc = buf->aux.ptr;
           uint8_t* d_first = buf->aux.ptr + dpad;
           // both tables through one pinned staging block: one true async upload instead of two

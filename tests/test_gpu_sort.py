@@ -243,24 +243,51 @@ def test_msd_finish_and_lsd_agree_with_oracle(gpu_node, tuned, msd, shape):
     gpu_node.check()
 
 
-def test_sort_records_captured_in_a_graph(gpu_node):
-    """sux_sort_records on a stream being captured into a HIP graph: no host wait, no host
-    allocation mid-capture (every digit pass runs); the replay equals the eager result."""
-    n, rs = 200_000, 100
-    recs = gpu_node.generate(N.GEN_TERASORT, 77, 0, n, rs)
-    want = gpu_node.sort_records(recs, rs, N.SORT_BYTES, 0, 10)
-    torch.cuda.synchronize()
-    out = torch.empty_like(want)
+@pytest.mark.parametrize("shape", ["terasort", "skewed_top", "equal", "top_only", "long_small"])
+def test_sort_records_captured_in_a_graph(gpu_node, shape):
+    """sux_sort_records on a stream being captured into a HIP graph: the plan is made on the
+    device (k_sort_plan / k_sort_bucket_max), so there is no host wait and no host allocation
+    mid-capture, and every branch runs inside the graph — the LDS finish ('terasort'), the LSD
+    fallback of a bucket above the LDS capacity ('skewed_top'), the identity of equal keys
+    ('equal'), a key whose varying bits all sit in the top digit ('top_only': the result stays in
+    the second pair buffer), int64 keys with constant top digits ('long_small').  Replays equal
+    the oracle."""
+    rng = np.random.default_rng(81)
+    rs, kind, off, klen = 100, N.SORT_BYTES, 0, 10
+    if shape == "terasort":
+        h = O.gen_terasort(77, 0, 200_000)
+    elif shape == "skewed_top":
+        h = O.gen_terasort(78, 0, 150_000).reshape(-1, 100)
+        h[:90_000, :4] = 5
+        h = h.ravel()
+    elif shape == "equal":
+        h = O.gen_terasort(79, 0, 50_000).reshape(-1, 100)
+        h[:, :10] = 7
+        h = h.ravel()
+    elif shape == "top_only":
+        h = O.gen_terasort(80, 0, 60_000).reshape(-1, 100)
+        h[:, :10] = 0
+        h[:, 3] = rng.integers(0, 256, h.shape[0], dtype=np.uint8)  # 8 varying bits: one digit
+        h = h.ravel()
+    else:
+        rows = np.zeros((300_000, 2), dtype=np.int64)
+        rows[:, 0] = rng.integers(0, 1 << 20, rows.shape[0])
+        rows[:, 1] = np.arange(rows.shape[0])
+        h, rs, kind, off, klen = rows.view(np.uint8).ravel(), 16, N.SORT_LONG, 0, 8
+    okind = {N.SORT_BYTES: O.SORT_BYTES, N.SORT_LONG: O.SORT_LONG}[kind]
+    want = O.sort_records(h, rs, okind, off, klen)
+    n = h.size // rs
+    recs = to_dev(h)
+    out = torch.empty_like(recs)
     ws = torch.empty(gpu_node.sort_workspace_size(n, rs), dtype=torch.uint8, device=recs.device)
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=s):
-        gpu_node.sort_records(recs, rs, N.SORT_BYTES, 0, 10, out=out, workspace=ws, stream=s)
-    out.zero_()
-    g.replay()
-    torch.cuda.synchronize()
-    assert torch.equal(out, want)
-    g.replay()  # a second replay of the same graph
-    torch.cuda.synchronize()
-    assert torch.equal(out, want)
+        gpu_node.sort_records(recs, rs, kind, off, klen, out=out, workspace=ws, stream=s)
+    for _ in range(2):  # two replays of the same graph
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert out.cpu().numpy().tobytes() == want.tobytes()
+    gpu_node.check()
