@@ -1627,6 +1627,10 @@ bool spill_some(sux_node* node, uint64_t need) {
     Staging st;
     for (auto& v : victims) {
       if (freed >= need) break;
+      // a slab some reader still holds (a fetch's copy, an exchange) would stay allocated:
+      // spilling its maps frees nothing now
+      const auto& s0 = v.second.front();
+      if ((size_t)s0.first->maps[s0.second].slab.use_count() > v.second.size()) continue;
       const uint64_t cap = v.first->buf.cap;
       for (auto& sm : v.second) {
         Shuffle& sh = *sm.first;
@@ -2939,31 +2943,40 @@ int sux_fetch_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* blo
     std::vector<std::string> files((size_t)n);  // copies: the slot may be spilled/freed later
     std::vector<std::shared_ptr<Event>> waits;
     uint64_t total = 0;
-    {
+    auto resolve_all = [&] {
       std::unique_lock<std::mutex> lk(node->mu);
       Shuffle& sh = node->shuffle(shuffle_id);
       drain(node, sh, lk);  // maps written without a wait are published first
       // phase 1 (UcxShuffleClient.submitFetchOffsets :50-92 / OnOffsetsFetchCallback :53-72):
       // sizes from the index tables of the directory
+      total = 0;
+      waits.clear();
       const Slab* last = nullptr;
       for (int i = 0; i < n; ++i) {
         loc[i] = resolve(node, sh, blocks[i]);
         sizes[i] = loc[i].size;
         total += (uint64_t)loc[i].size;
-        if (loc[i].file) files[i] = *loc[i].file;
+        files[i] = loc[i].file ? *loc[i].file : std::string();
         // blocks received by an exchange still in flight: the copy waits for it
         if (loc[i].rslab && loc[i].rslab != last && loc[i].rslab->ready) {
           waits.push_back(loc[i].rslab->ready);
           last = loc[i].rslab;
         }
       }
-    }
-    for (auto& w : waits) hip_check(hipStreamWaitEvent(s, w->e, 0), "wait for the exchange");
+    };
+    resolve_all();
     auto buf = std::make_unique<sux_buffer>();
     buf->node = node;
     buf->size = total;
     buf->refs = n > 0 ? n : 1;  // one reference per block slice (OnBlocksFetchCallback :35)
-    // OnOffsetsFetchCallback :75-76: one pooled buffer for the whole request
+    // OnOffsetsFetchCallback :75-76: one pooled buffer for the whole request.  Taken with the
+    // blocks' device buffers released: when the pool is full, the allocation spills map outputs
+    // (which then must be free to go), and the blocks are resolved again afterwards — a spilled
+    // map's blocks come from its file (same sizes, so the layout of the buffer holds)
+    loc.assign((size_t)n, BlockLoc{});
+    buf->buf = pool_get_or_spill(node, total ? total : 1);
+    resolve_all();
+    for (auto& w : waits) hip_check(hipStreamWaitEvent(s, w->e, 0), "wait for the exchange");
     buf->buf = pool_get_or_spill(node, total ? total : 1);
     try {
       if (total) {

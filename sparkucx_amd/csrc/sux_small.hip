@@ -402,8 +402,13 @@ __device__ unsigned long long* g_msd_stamps;
 #define SUX_MSD_STAMP_END() do {} while (0)
 #endif
 constexpr uint32_t kM16Chunk = 4096;      // pass A records per chunk (the run table's unit)
-constexpr uint32_t kM16Lo = 4;            // partitions per bucket: 16
+// Partitions per bucket, 2^LO: 16 (LO 4) for long maps; 256 (LO 8) for short maps, whose 16-
+// partition segments would be too short to pay a segment's fixed cost (64 Ki-record maps at
+// R = 10 000: 105 records at LO 4, 1677 at LO 8 — the 2^20-record maps' segment at LO 4).
+constexpr uint32_t kM16Lo = 4;
+constexpr uint32_t kM16LoShort = 8;
 constexpr uint32_t kM16MaxChunks = 512;   // chunks per map pass B's run table holds (2 Mi records)
+constexpr uint32_t kM16MaxChunksShort = 64;  // LO 8: maps of <= 256 Ki records
 
 // Block exclusive scan, in (digit, wave) order, of u16 per-wave digit counters wc[NW][NB]
 // (NW*64 threads; each thread owns E = NB/64 consecutive (digit, wave) entries).  Counts and
@@ -439,12 +444,12 @@ struct M16a {
   static constexpr uint32_t NB = 1u << DB, NT = NW * kWave, PT = kM16Chunk / NT;
   static constexpr uint32_t lds_bytes() { return kM16Chunk * 16 + NW * NB * 2; }
 };
-template <uint32_t NW, uint32_t PT>  // stage[CAP] u32x4 | wc[NW][64] | cur[64] | wsum[NW] | los[CAP] u8 | rp[MAXCH+1] u32 | ro[MAXCH] u16
+// stage[CAP] u32x4 | wc[NW][NB] | cur[NB] | wsum[NW] | los[CAP] u8 | rp[MC+1] u32 | ro[MC] u16
+template <uint32_t NW, uint32_t PT, uint32_t LO = kM16Lo, uint32_t MC = kM16MaxChunks>
 struct M16b {
-  static constexpr uint32_t NB = 64, NT = NW * kWave, CAP = NT * PT;
+  static constexpr uint32_t NB = (1u << LO) > 64 ? (1u << LO) : 64, NT = NW * kWave, CAP = NT * PT;
   static constexpr uint32_t lds_bytes() {
-    return CAP * 16 + NW * NB * 4 + NB * 4 + NW * 4 + CAP + (kM16MaxChunks + 1) * 4 +
-           kM16MaxChunks * 2;
+    return CAP * 16 + NW * NB * 4 + NB * 4 + NW * 4 + CAP + (MC + 1) * 4 + MC * 2;
   }
 };
 
@@ -470,7 +475,7 @@ __device__ __forceinline__ uint32_t m16_pid(const PartDev& pd, const u32x4& r, i
   return (uint32_t)partition_words<KW, false>(pd, w, pd.bounds, pd.lut);
 }
 
-template <int KW, uint32_t NW, uint32_t DB>
+template <int KW, uint32_t NW, uint32_t DB, uint32_t LO>
 __global__ __launch_bounds__(NW * 64, 4) void k_msd16a(PartDev pd, MapGroup g, uint32_t cpm,
                                                  uint32_t nbk, uint16_t* __restrict__ offs,
                                                  uint16_t* __restrict__ pids_out,
@@ -526,7 +531,7 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16a(PartDev pd, MapGroup g, u
         p = m16_pid<KW>(pd, rv[j], kw0);
         if (pids_out) pids_out[k.c0 + e] = (uint16_t)p;
       }
-      h[j] = (p >> kM16Lo) & (NB - 1);
+      h[j] = (p >> LO) & (NB - 1);
       rank[j] = wave_rank<DB, uint16_t>(h[j], valid, wc + wave * NB, lt_mask);
     }
     __syncthreads();
@@ -592,7 +597,7 @@ __global__ __launch_bounds__(kScanThreads) void k_msd16_scan(MapGroup g, uint32_
   }
 }
 
-template <int KW, uint32_t NW, uint32_t PT>
+template <int KW, uint32_t NW, uint32_t PT, uint32_t LO, uint32_t MCH>
 __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, uint32_t cpm,
                                                  uint32_t nbk, const uint16_t* __restrict__ offs,
                                                  const uint64_t* __restrict__ segbase,
@@ -602,8 +607,8 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
                                                  uint8_t* __restrict__ index_be) {
   if (pass_skipped(g)) return;
   resolve_seed(pd);
-  using K = M16b<NW, PT>;
-  constexpr uint32_t NB = K::NB, NT = K::NT, CAP = K::CAP, MC = kM16MaxChunks, PB = 1u << kM16Lo;
+  using K = M16b<NW, PT, LO, MCH>;
+  constexpr uint32_t NB = K::NB, NT = K::NT, CAP = K::CAP, MC = MCH, PB = 1u << LO;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
   u32x4* stage = reinterpret_cast<u32x4*>(lds8);
   uint32_t* wc = reinterpret_cast<uint32_t*>(stage + CAP);  // [NW][NB]
@@ -722,7 +727,7 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
     }
   };
   auto digit = [&](const Seg& s, const u32x4& r) {
-    return (m16_pid<KW>(pd, r, kw0) - (s.h << kM16Lo)) & (NB - 1);
+    return (m16_pid<KW>(pd, r, kw0) - (s.h << LO)) & (NB - 1);
   };
   // stable rank by pid & 31 -> stage/los in sorted order; wc[0][l] = digit starts afterwards
   auto rank_stage = [&](const Seg& s, uint32_t n, const u32x4 (&r)[PT]) {
@@ -732,7 +737,7 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
       const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
       const bool valid = e < n;
       lo[j] = valid ? digit(s, r[j]) : 0u;
-      rk[j] = wave_rank<kM16Lo>(lo[j], valid, wc + wave * NB, lt_mask);
+      rk[j] = wave_rank<LO>(lo[j], valid, wc + wave * NB, lt_mask);
     }
     __syncthreads();
     scan_digit_wave<NB, NW>(wc, wsum, tid, lane, wave);
@@ -746,7 +751,7 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
   };
   auto write_index = [&](const Seg& s, uint32_t start_l) {
     const uint64_t seg_out = s.out;
-    const uint32_t p = (s.h << kM16Lo) + (uint32_t)tid;  // in-segment record offset of partition p
+    const uint32_t p = (s.h << LO) + (uint32_t)tid;  // in-segment record offset of partition p
     if (tid < (int)PB && p < (uint32_t)R) {
       const int64_t off = (int64_t)((seg_out - s.mbase + start_l) * g.rec_size);
       index[(uint64_t)s.m * (R + 1) + p] = off;
@@ -826,27 +831,39 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
 // ------------------------------------------------------------------------------------------
 // The MSD small-record path (k_msd16a / k_msd16_scan / k_msd16b) applies: tuning small_kernel 4,
 // 16-byte records with a fixed-width key in the first 16 bytes, 1024 < R <= 16384, 16-byte
-// aligned input and output, map-major layout, maps of <= kM16MaxChunks chunks, and a workspace
-// with the temp copy (its chunk-offset table lives in the counts region, the segment bases in
-// the totals region).
-bool msd16_eligible(const PartDev& pd, const MapGroup& g, const LayoutDesc& lay,
-                    const uint8_t* d_out, const Workspace& ws, const Tuning& tn) {
-  if (tn.small_kernel != 4 || g.rec_size != 16 || lay.world != 1) return false;
+// aligned input and output, map-major layout, maps of <= MC chunks, and a workspace with the
+// temp copy (its chunk-offset table lives in the counts region, the segment bases in the totals
+// region).  Returns the bucket width LO it runs with (16 partitions per bucket; 256 for maps too
+// short for 16), 0 when it does not apply.
+static uint32_t msd16_lo(const PartDev& pd, const MapGroup& g, const LayoutDesc& lay,
+                         const uint8_t* d_out, const Workspace& ws, const Tuning& tn) {
+  if (tn.small_kernel != 4 || g.rec_size != 16 || lay.world != 1) return 0;
   if (pd.R <= 1024 || pd.R > 16384 || pd.kind == 4 || pd.key_offset % 4 != 0 ||
       pd.key_offset + pd.key_len > 16)
-    return false;
+    return 0;
   if (((reinterpret_cast<uintptr_t>(g.recs) | reinterpret_cast<uintptr_t>(d_out)) & 15) != 0)
-    return false;
+    return 0;
   const uint64_t cpm = (g.records_per_map + kM16Chunk - 1) / kM16Chunk;
-  const uint64_t nbk = ((uint64_t)pd.R + (1u << kM16Lo) - 1) >> kM16Lo;
-  // by default only when a (map, bucket) segment holds >= 1024 records on average: a segment
-  // costs ~6 us of run table, search and barriers whatever its size, so short maps run the
-  // sorted-chunk scatter instead (64 Ki-record maps at R = 10 000: 105-record segments, 194 vs
-  // 507 GB/s; 2^20-record maps: 1677-record segments, 1027 vs 750 GB/s)
-  if (tn.small_auto && g.records_per_map < 1024 * nbk) return false;
-  return cpm >= 1 && cpm <= kM16MaxChunks && ws.tmp_bytes >= g.num_records * 16 &&
-         (uint64_t)g.num_maps * cpm * nbk * 2 <= ws.counts_bytes &&
-         (uint64_t)g.num_maps * nbk * 8 <= ws.totals_bytes;
+  if (cpm < 1 || ws.tmp_bytes < g.num_records * 16) return 0;
+  for (const uint32_t lo : {kM16Lo, kM16LoShort}) {
+    const uint64_t nbk = ((uint64_t)pd.R + (1u << lo) - 1) >> lo;
+    if (cpm > (lo == kM16Lo ? kM16MaxChunks : kM16MaxChunksShort)) continue;
+    // by default only when a (map, bucket) segment holds >= 1024 records on average: a segment
+    // costs ~6 us of run table, search and barriers whatever its size (64 Ki-record maps at
+    // R = 10 000 and 16 partitions per bucket: 105-record segments, 194 GB/s vs 553 for the
+    // sorted-chunk scatter; 2^20-record maps: 1677-record segments, 1027 vs 750 GB/s) — short
+    // maps take 256-partition buckets, longer segments again
+    if (tn.small_auto && g.records_per_map < 1024 * nbk) continue;
+    if ((uint64_t)g.num_maps * cpm * nbk * 2 <= ws.counts_bytes &&
+        (uint64_t)g.num_maps * nbk * 8 <= ws.totals_bytes)
+      return lo;
+  }
+  return 0;
+}
+
+bool msd16_eligible(const PartDev& pd, const MapGroup& g, const LayoutDesc& lay,
+                    const uint8_t* d_out, const Workspace& ws, const Tuning& tn) {
+  return msd16_lo(pd, g, lay, d_out, ws, tn) != 0;
 }
 
 hipError_t launch_msd16(const PartDev& pd, const MapGroup& g, uint8_t* d_out, int64_t* d_index,
@@ -855,7 +872,10 @@ hipError_t launch_msd16(const PartDev& pd, const MapGroup& g, uint8_t* d_out, in
   const int R = pd.R;
   const uint32_t ncu = (uint32_t)std::max(1, stream_cus(s));
   const uint32_t cpm = (uint32_t)((g.records_per_map + kM16Chunk - 1) / kM16Chunk);
-  const uint32_t nbk = ((uint32_t)R + (1u << kM16Lo) - 1) >> kM16Lo;
+  const LayoutDesc lay1{1, 16};
+  const uint32_t LO = msd16_lo(pd, g, lay1, d_out, ws, tn);
+  if (LO == 0) return hipErrorInvalidValue;  // (the caller checked msd16_eligible)
+  const uint32_t nbk = ((uint32_t)R + (1u << LO) - 1) >> LO;
   uint16_t* offs = reinterpret_cast<uint16_t*>(d_ws + ws.counts_off);  // [map][chunk][bucket]
   uint64_t* segbase = reinterpret_cast<uint64_t*>(d_ws + ws.totals_off);  // [map][bucket]
   uint8_t* tmp = d_ws + ws.tmp_off;
@@ -868,23 +888,24 @@ hipError_t launch_msd16(const PartDev& pd, const MapGroup& g, uint8_t* d_out, in
   timer_begin(timer, kHist, s);
   const uint32_t wpc = (uint32_t)tn.small_wgs_per_cu;
   const dim3 ga(std::min<uint32_t>(g.num_maps * cpm, ncu * wpc));
-#define SUX_M16A(KW, DB)                                                                           \
+#define SUX_M16A(KW, DB, LOV)                                                                      \
   do {                                                                                             \
     constexpr size_t ldsa = M16a<NWA, DB>::lds_bytes();                                            \
-    allow_lds(reinterpret_cast<const void*>(&k_msd16a<KW, NWA, DB>), ldsa);                        \
-    hipLaunchKernelGGL((k_msd16a<KW, NWA, DB>), ga, dim3(NWA * kWave), ldsa, s, pd, g, cpm, nbk,   \
-                       offs, d_pids, tmp);                                                         \
+    allow_lds(reinterpret_cast<const void*>(&k_msd16a<KW, NWA, DB, LOV>), ldsa);                   \
+    hipLaunchKernelGGL((k_msd16a<KW, NWA, DB, LOV>), ga, dim3(NWA * kWave), ldsa, s, pd, g, cpm,   \
+                       nbk, offs, d_pids, tmp);                                                    \
   } while (0)
-#define SUX_M16AK(DB)                   \
-  do {                                  \
-    if (kw <= 1) SUX_M16A(1, DB);       \
-    else if (kw == 2) SUX_M16A(2, DB);  \
-    else if (kw == 3) SUX_M16A(3, DB);  \
-    else SUX_M16A(4, DB);               \
+#define SUX_M16AK(DB, LOV)                   \
+  do {                                       \
+    if (kw <= 1) SUX_M16A(1, DB, LOV);       \
+    else if (kw == 2) SUX_M16A(2, DB, LOV);  \
+    else if (kw == 3) SUX_M16A(3, DB, LOV);  \
+    else SUX_M16A(4, DB, LOV);               \
   } while (0)
-  if (nbk > 512) SUX_M16AK(10);
-  else if (nbk > 256) SUX_M16AK(9);
-  else SUX_M16AK(8);
+  if (LO == kM16LoShort) SUX_M16AK(6, kM16LoShort);  // R <= 16384: <= 64 buckets
+  else if (nbk > 512) SUX_M16AK(10, kM16Lo);
+  else if (nbk > 256) SUX_M16AK(9, kM16Lo);
+  else SUX_M16AK(8, kM16Lo);
 #undef SUX_M16AK
 #undef SUX_M16A
   timer_end(timer, kHist, s);
@@ -901,19 +922,28 @@ hipError_t launch_msd16(const PartDev& pd, const MapGroup& g, uint8_t* d_out, in
   timer_begin(timer, kScatter, s);
   // pass B's 256-thread workgroups are half the size of pass A's: twice as many per CU
   const dim3 gb(std::min<uint32_t>(g.num_maps * nbk, ncu * 2 * wpc));
-  constexpr size_t ldsb = M16b<NWB, PTB>::lds_bytes();
-  static_assert(4 * ldsb <= 160 * 1024, "pass B: four workgroups per CU");
+  using MB4 = M16b<NWB, PTB, kM16Lo, kM16MaxChunks>;
+  using MB8 = M16b<NWB, PTB, kM16LoShort, kM16MaxChunksShort>;
+  static_assert(4 * MB4::lds_bytes() <= 160 * 1024, "pass B: four workgroups per CU");
+  static_assert(4 * MB8::lds_bytes() <= 160 * 1024, "pass B (256-partition buckets): four per CU");
   static_assert(2 * M16a<NWA, 10>::lds_bytes() <= 160 * 1024, "pass A: two workgroups per CU");
-#define SUX_M16B(KW)                                                                               \
+#define SUX_M16B(KW, LOV, MCV)                                                                     \
   do {                                                                                             \
-    allow_lds(reinterpret_cast<const void*>(&k_msd16b<KW, NWB, PTB>), ldsb);                      \
-    hipLaunchKernelGGL((k_msd16b<KW, NWB, PTB>), gb, dim3(NWB * kWave), ldsb, s, pd, g, cpm, nbk,  \
-                       offs, segbase, tmp, d_out, d_index, d_index_be);                            \
+    constexpr size_t ldsb = M16b<NWB, PTB, LOV, MCV>::lds_bytes();                                 \
+    allow_lds(reinterpret_cast<const void*>(&k_msd16b<KW, NWB, PTB, LOV, MCV>), ldsb);            \
+    hipLaunchKernelGGL((k_msd16b<KW, NWB, PTB, LOV, MCV>), gb, dim3(NWB * kWave), ldsb, s, pd, g,  \
+                       cpm, nbk, offs, segbase, tmp, d_out, d_index, d_index_be);                  \
   } while (0)
-  if (kw <= 1) SUX_M16B(1);
-  else if (kw == 2) SUX_M16B(2);
-  else if (kw == 3) SUX_M16B(3);
-  else SUX_M16B(4);
+#define SUX_M16BK(LOV, MCV)                   \
+  do {                                        \
+    if (kw <= 1) SUX_M16B(1, LOV, MCV);       \
+    else if (kw == 2) SUX_M16B(2, LOV, MCV);  \
+    else if (kw == 3) SUX_M16B(3, LOV, MCV);  \
+    else SUX_M16B(4, LOV, MCV);               \
+  } while (0)
+  if (LO == kM16LoShort) SUX_M16BK(kM16LoShort, kM16MaxChunksShort);
+  else SUX_M16BK(kM16Lo, kM16MaxChunks);
+#undef SUX_M16BK
 #undef SUX_M16B
   timer_end(timer, kScatter, s);
   return hipGetLastError();

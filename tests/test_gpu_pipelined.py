@@ -341,11 +341,13 @@ def test_msd16_falls_back_for_the_exchange_layout(gpu_node, tuned):
     gp.close()
 
 
-@pytest.mark.parametrize("rpm,want", [(65536, "k_scatter16s"), (655360, "k_msd16b")])
+@pytest.mark.parametrize("rpm,want", [(16384, "k_scatter16s"), (65536, "k_msd16b"),
+                                      (100000, "k_msd16b"), (655360, "k_msd16b")])
 def test_default_small_kernel_picks_by_segment_length(gpu_node, rpm, want):
-    """Default tuning: the two-level path only when a (map, 16-partition bucket) segment holds
-    >= 1024 records on average (R = 10 000: maps of >= 640 000 records); shorter maps take the
-    sorted-chunk scatter.  Both bit-exact."""
+    """Default tuning: the two-level path only when a (map, bucket) segment holds >= 1024
+    records on average — 16-partition buckets for maps of >= 640 000 records at R = 10 000,
+    256-partition buckets for maps of >= 40 960 (64 Ki-record maps: 1677-record segments);
+    shorter maps take the sorted-chunk scatter.  All bit-exact."""
     n = 2 * rpm + 12345
     recs = O.gen_small(43, 0, n)
     opart = O.Partitioner(O.MURMUR3_LONG, 10000, 0, 8, seed=42)

@@ -77,8 +77,8 @@ int main(int argc, char** argv) {
   CK(hipMemset(st, 0, gb * 8 * 8));
   CK(hipMemcpyToSymbol(HIP_SYMBOL(g_msd_stamps), &st, sizeof st));
   constexpr size_t lda = M16a<8, 10>::lds_bytes(), ldb = M16b<4, 8>::lds_bytes();
-  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_msd16a<2, 8, 10>), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lda));
-  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_msd16b<2, 4, 8>), hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldb));
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_msd16a<2, 8, 10, kM16Lo>), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lda));
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_msd16b<2, 4, 8, kM16Lo, kM16MaxChunks>), hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldb));
   hipEvent_t e0, e1, e2, e3;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -86,11 +86,11 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e3));
   for (int rep = 0; rep < 2; ++rep) {
     CK(hipEventRecord(e0, 0));
-    hipLaunchKernelGGL((k_msd16a<2, 8, 10>), dim3(std::min<uint32_t>(maps * cpm, ncu * 2)), dim3(512), lda, 0, pd, g, cpm, nbk, offs, (uint16_t*)nullptr, tmp);
+    hipLaunchKernelGGL((k_msd16a<2, 8, 10, kM16Lo>), dim3(std::min<uint32_t>(maps * cpm, ncu * 2)), dim3(512), lda, 0, pd, g, cpm, nbk, offs, (uint16_t*)nullptr, tmp);
     CK(hipEventRecord(e1, 0));
     hipLaunchKernelGGL(k_msd16_scan, dim3(maps), dim3(kScanThreads), 0, 0, g, cpm, nbk, offs, segbase, idx, ibe, (uint64_t*)nullptr, (int)R);
     CK(hipEventRecord(e2, 0));
-    hipLaunchKernelGGL((k_msd16b<2, 4, 8>), dim3(gb), dim3(256), ldb, 0, pd, g, cpm, nbk, offs, segbase, tmp, out, idx, ibe);
+    hipLaunchKernelGGL((k_msd16b<2, 4, 8, kM16Lo, kM16MaxChunks>), dim3(gb), dim3(256), ldb, 0, pd, g, cpm, nbk, offs, segbase, tmp, out, idx, ibe);
     CK(hipEventRecord(e3, 0));
     CK(hipDeviceSynchronize());
   }
