@@ -341,6 +341,37 @@ def test_msd16_falls_back_for_the_exchange_layout(gpu_node, tuned):
     gp.close()
 
 
+@pytest.mark.parametrize("R,n,rpm,skew", [
+    (10000, 3 * 65536 + 777, 65536, None),   # C5's R, 64 Ki-record maps, a ragged last map
+    (10000, 2 * 65536, 65536, "one"),        # one segment far above the LDS piece
+    (16384, 2 * 65536, 65536, "zipf"),       # 64 buckets of 256 partitions, skewed
+    (1025, 3 * 8192, 8192, None),            # 5 buckets (the last of 1 partition), 2-chunk maps
+    (10000, 2 * 262144, 262144, None),       # 64 chunks per map: the short run table's limit
+])
+def test_msd16_short_maps_256_partition_buckets(gpu_node, R, n, rpm, skew):
+    """Default tuning, maps too short for 16-partition segments: the two-level path with
+    256-partition buckets (pass A digits pid >> 8, pass B sorts by pid & 255).  Bytes, both index
+    tables and the pids equal the oracle's."""
+    if skew == "zipf":
+        recs = O.gen_zipf(45, 0, n, 1.1, 1 << 12)
+        recs = recs.reshape(-1, 100)[:, :16].copy().ravel()
+    else:
+        recs = O.gen_small(44, 0, n)
+    if skew == "one":
+        recs.reshape(-1, 16)[: n // 2, :8] = 5
+    opart = O.Partitioner(O.MURMUR3_LONG, R, 0, 8, seed=42)
+    gp = gpu_part(gpu_node, opart)
+    pids = torch.empty(n, dtype=torch.int16, device="cuda")
+    out, index, index_be = gpu_node.partition_maps(gp, torch.from_numpy(recs).cuda(), 16, rpm,
+                                                   pids=pids)
+    torch.cuda.synchronize()
+    expect(opart, recs, 16, rpm, out, index, index_be)
+    assert (host(pids).view(np.uint16) == opart.ids(recs, 16)).all()
+    assert gpu_node.kernel_variant(2) == "k_msd16b"
+    gp.close()
+    gpu_node.check()
+
+
 @pytest.mark.parametrize("rpm,want", [(16384, "k_scatter16s"), (65536, "k_msd16b"),
                                       (100000, "k_msd16b"), (655360, "k_msd16b")])
 def test_default_small_kernel_picks_by_segment_length(gpu_node, rpm, want):
