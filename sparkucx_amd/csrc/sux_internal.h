@@ -243,7 +243,7 @@ struct SortPlanDev {
   uint32_t msd_ok;   // 1: every top-digit bucket fits the LDS sort, which finishes the sort
   uint32_t lsd_skip; // 1: the LSD fallback passes are not needed (msd_ok, or hb < 0)
   uint32_t final_b;  // 1: the sorted pairs end in buffer b, 0: in buffer a
-  uint32_t pad;
+  int32_t kbits;     // key bits (with the segment id): the top kbits of the big-endian pair
   uint64_t maxb;     // the largest top-digit bucket, in pairs
   SortDigits dg;     // the LDS sort's digits: 8-bit, below top_lo, only those that vary
 };

@@ -299,6 +299,20 @@ __device__ __forceinline__ uint32_t pair_digit8(const u32x4& w, uint32_t sh) {
   return (uint32_t)v & 255u;
 }
 
+// key(a) > key(b): the top kbits bits of the big-endian 128-bit pairs (the order key; in
+// inline mode the bits below are record payload, which must not order equal keys)
+__device__ __forceinline__ bool key_greater(const u32x4& a, const u32x4& b, int kbits) {
+  const uint64_t ah = ((uint64_t)__builtin_bswap32(a[0]) << 32) | __builtin_bswap32(a[1]);
+  const uint64_t bh = ((uint64_t)__builtin_bswap32(b[0]) << 32) | __builtin_bswap32(b[1]);
+  if (kbits <= 64) return (ah >> (64 - kbits)) > (bh >> (64 - kbits));
+  if (ah != bh) return ah > bh;
+  const uint64_t al = ((uint64_t)__builtin_bswap32(a[2]) << 32) | __builtin_bswap32(a[3]);
+  const uint64_t bl = ((uint64_t)__builtin_bswap32(b[2]) << 32) | __builtin_bswap32(b[3]);
+  return (al >> (128 - kbits)) > (bl >> (128 - kbits));
+}
+constexpr int kTopDigits = 2;          // LDS digit passes before the tie fix-up
+constexpr uint32_t kMaxTieRun = 16;    // longer tie runs: every digit pass instead
+
 template <uint32_t NW, uint32_t CAP>  // buf[CAP] u32x4 | wc[NW][256] u32 | wsum[NW]
 struct SortLocal {
   static constexpr uint32_t NT = NW * kWave, PT = CAP / NT, NB = 256;
@@ -316,6 +330,9 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : CAP == 1024 ? 6 : 4) void k_
                                                         const SortPlanDev* __restrict__ plan) {
   if (!plan->msd_ok || plan->dg.n == 0) return;  // the LSD fallback, or the top digit was all
   const SortDigits dg = plan->dg;
+  const int kbits = plan->kbits;
+  __shared__ uint32_t tie_redo;
+  if (threadIdx.x == 0) tie_redo = 0;
   using K = SortLocal<NW, CAP>;
   constexpr uint32_t NT = K::NT, PT = K::PT, NB = K::NB;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
@@ -336,8 +353,9 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : CAP == 1024 ? 6 : 4) void k_
       const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
       v[j] = in[s0 + min(e, n - 1)];
     }
-#pragma unroll 1
-    for (int d = 0; d < (n > 1 ? dg.n : 0); ++d) {
+    // one stable 8-bit digit pass in LDS (digit d of dg): ranks, block scan, permutation into
+    // buf, the pairs back into registers in the new order
+    auto digit_pass = [&](int d) {
       const uint64_t w = d < 8 ? dg.lo : dg.hi;  // shifts packed 8 bits apiece
       const uint32_t sh = (uint32_t)(w >> (8 * (d & 7))) & 255u;
       uint32_t dig[PT], rank[PT];
@@ -362,6 +380,54 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : CAP == 1024 ? 6 : 4) void k_
         if (e < n) v[j] = buf[e];
       }
       __syncthreads();  // every pair is back in registers before the next digit rewrites buf
+    };
+    // The top kTopDigits digits below the bucket's digit first (LSD among them): after them the
+    // pairs are in order but for runs whose top digits tie — with random keys a few runs of 2
+    // per bucket.  Each run is then finished in place by one thread (a stable insertion sort on
+    // the key bits); a run longer than kMaxTieRun (duplicate-heavy keys) sends the bucket through
+    // every digit pass instead, from this order (equal keys are still in input order, so the
+    // LSD result stays stable).  With random TeraSort keys: 2 LDS passes instead of 9.
+    const int nd = n > 1 ? dg.n : 0;
+    const int K = nd < kTopDigits ? nd : kTopDigits;
+    for (int d = nd - K; d < nd; ++d) digit_pass(d);
+    if (nd > K) {
+      const uint64_t wt = (nd - 1) < 8 ? dg.lo : dg.hi, wt2 = (nd - 2) < 8 ? dg.lo : dg.hi;
+      const uint32_t sh1 = (uint32_t)(wt >> (8 * ((nd - 1) & 7))) & 255u;
+      const uint32_t sh0 = (uint32_t)(wt2 >> (8 * ((nd - 2) & 7))) & 255u;
+      auto top = [&](const u32x4& x) { return (pair_digit8(x, sh1) << 8) | pair_digit8(x, sh0); };
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) {
+        const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+        if (e >= n) continue;
+        const uint32_t t = top(v[j]);
+        if ((e > 0 && top(buf[e - 1]) == t) || e + 1 >= n || top(buf[e + 1]) != t) continue;
+        uint32_t L = 2;  // a run of >= 2 starts at e
+        while (e + L < n && L <= kMaxTieRun && top(buf[e + L]) == t) ++L;
+        if (L > kMaxTieRun) {
+          atomicOr(&tie_redo, 1u);
+          continue;
+        }
+        for (uint32_t i = 1; i < L; ++i) {  // stable: only strictly greater keys move up
+          const u32x4 x = buf[e + i];
+          uint32_t k = i;
+          while (k > 0 && key_greater(buf[e + k - 1], x, kbits)) {
+            buf[e + k] = buf[e + k - 1];
+            --k;
+          }
+          buf[e + k] = x;
+        }
+      }
+      __syncthreads();
+      const bool redo = tie_redo != 0;
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) {
+        const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+        if (e < n) v[j] = buf[e];
+      }
+      __syncthreads();  // every thread read the flag and its pairs before anyone moves on
+      if (tid == 0) tie_redo = 0;  // (read again only after the next bucket's first barrier)
+      if (redo)
+        for (int d = 0; d < nd; ++d) digit_pass(d);
     }
 #pragma unroll
     for (uint32_t j = 0; j < PT; ++j) {
@@ -396,6 +462,7 @@ __global__ void k_sort_plan(const uint32_t* __restrict__ span, int bits, int tb,
     if (span_varies_dev(span, sh, min(sh + 8, top_lo))) dg.push((uint32_t)sh);
   plan->top_lo = top_lo;
   plan->hb = hb;
+  plan->kbits = bits;
   plan->dg = dg;
 }
 

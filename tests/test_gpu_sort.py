@@ -243,6 +243,32 @@ def test_msd_finish_and_lsd_agree_with_oracle(gpu_node, tuned, msd, shape):
     gpu_node.check()
 
 
+@pytest.mark.parametrize("shape", ["tie_runs", "long_tie_runs"])
+def test_lds_sort_tie_fixup_and_redo(gpu_node, shape):
+    """k_sort_local sorts a bucket by its two most significant varying digits, then finishes the
+    runs whose two digits tie with a stable insertion sort: 'tie_runs' leaves ~512 top-digit
+    combinations per 781-pair bucket (short runs, fixed in place); 'long_tie_runs' leaves 4
+    (runs of ~200 > 16: the bucket runs every digit pass instead).  Bytes vs the oracle."""
+    rng = np.random.default_rng(91)
+    n = 200_000
+    recs = O.gen_terasort(92, 0, n).reshape(-1, 100)
+    recs[:, :10] = 0
+    recs[:, 0] = rng.integers(0, 256, n, dtype=np.uint8)           # the bucket digit
+    if shape == "tie_runs":
+        recs[:, 1] = rng.integers(0, 256, n, dtype=np.uint8)
+        recs[:, 2] = rng.integers(0, 2, n, dtype=np.uint8)
+        recs[:, 4] = rng.integers(0, 256, n, dtype=np.uint8)
+    else:
+        recs[:, 1] = rng.integers(0, 2, n, dtype=np.uint8)
+        recs[:, 2] = rng.integers(0, 2, n, dtype=np.uint8)
+        recs[:, 4] = rng.integers(0, 256, n, dtype=np.uint8)
+        recs[:, 6] = rng.integers(0, 256, n, dtype=np.uint8)
+    recs = recs.ravel()
+    got = gpu_sort(gpu_node, recs, 100, N.SORT_BYTES, 0, 10)
+    assert got.tobytes() == O.sort_records(recs, 100, O.SORT_BYTES, 0, 10).tobytes()
+    gpu_node.check()
+
+
 @pytest.mark.parametrize("shape", ["terasort", "skewed_top", "equal", "top_only", "long_small"])
 def test_sort_records_captured_in_a_graph(gpu_node, shape):
     """sux_sort_records on a stream being captured into a HIP graph: the plan is made on the
