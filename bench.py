@@ -765,8 +765,15 @@ def main():
         # committed in place (sux_adopt_map_outputs: index tables read back on the stream,
         # published on completion) and sux_resolve_blocks returns each block's device address
         # and size (OnOffsetsFetchCallback.java:53-72's offsets -> sizes, zero-copy at N = 1)
-        all_blocks = np.stack([np.repeat(np.arange(maps), R), np.tile(np.arange(R), maps)],
-                              1).astype(np.int32)
+        # Reduce tasks: at most 200 (TeraSort's R = 200: one ShuffleBlockId per (map, task)); at
+        # larger R each task reads a contiguous range of partitions as one ShuffleBlockBatchId per
+        # map, as Spark's reducers do with batch fetch (UcxShuffleClient.java:67-73; C5's R = 10 000
+        # in 200 tasks of 50 partitions: per-partition resolves would be 10^7 host calls a step)
+        tasks = min(R, 200)
+        lo_t = (np.arange(tasks) * R) // tasks
+        hi_t = (np.arange(1, tasks + 1) * R) // tasks
+        all_blocks = np.stack([np.repeat(np.arange(maps), tasks), np.tile(lo_t, maps),
+                               np.tile(hi_t, maps)], 1).astype(np.int32)
         resolved = {"blocks": 0, "bytes": 0}
         sid_next = [5000]
 
@@ -1020,7 +1027,9 @@ def main():
                                   f" on {args.streams} streams" if not pipelined and args.streams > 1
                                   else "")
                                + (f", map side on {256 - reserve} CUs" if reserve > 0 else "")
-                               + (", zero-copy local block resolve" if not pipelined else
+                               + (", zero-copy local block resolve (one block per map and "
+                                  "reduce task, <= 200 tasks)" if not pipelined and args.resolve else
+                                  "" if not pipelined else
                                   ", partition-aligned ncclAllToAllv exchange"
                                   if args.transport == "rccl" else
                                   ", partition-aligned one-sided IPC pull exchange"),
@@ -1121,7 +1130,8 @@ def main():
         result["resolve"] = {"blocks_per_step": resolved["blocks"] // max(1, steps_run),
                              "bytes_per_step": resolved["bytes"] // max(1, steps_run),
                              "path": "sux_register_shuffle -> partition -> sux_adopt_map_outputs "
-                                     "-> sux_resolve_blocks(every (map, reduce) block) -> "
+                                     "-> sux_resolve_blocks(one block per (map, reduce task): "
+                                     "min(R, 200) tasks, ShuffleBlockBatchId ranges when R > 200) -> "
                                      "sux_unregister_shuffle, inside every timed step"}
         if resolved["bytes"] != n * rs * steps_run:
             raise RuntimeError("resolved blocks do not cover the input")

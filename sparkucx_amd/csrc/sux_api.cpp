@@ -2977,7 +2977,6 @@ int sux_fetch_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* blo
     buf->buf = pool_get_or_spill(node, total ? total : 1);
     resolve_all();
     for (auto& w : waits) hip_check(hipStreamWaitEvent(s, w->e, 0), "wait for the exchange");
-    buf->buf = pool_get_or_spill(node, total ? total : 1);
     try {
       if (total) {
         // phase 2 (:80-87): block i -> contiguous destination at a running offset; device blocks
