@@ -187,8 +187,8 @@ typedef struct sux_tuning {
                                tile-major (one contiguous store of a tile's R counters)        */
   int32_t scatter_counters; /* k_scatter8 per-wave rank counters in LDS: 1 partition-major
                                [R][waves] (round 2), 2 (0) wave-major [waves][R]               */
-  int32_t lz4_queue;        /* LZ4 compressor chunk deal: 1 a device work queue (one atomic per
-                               chunk), 2 (0) the fixed grid-stride deal                        */
+  int32_t lz4_queue;        /* LZ4 compressor chunk deal: 1 (0) a device work queue (one atomic
+                               per chunk), 2 the fixed grid-stride deal                        */
   int32_t reserved[5];
 } sux_tuning;
 int sux_node_set_tuning(sux_node* node, const sux_tuning* tuning);

@@ -60,7 +60,7 @@ struct Tuning {
   bool hist_nt = false;     // k_hist4: non-temporal (streaming) record loads
   bool counts_tm = true;    // k_hist4 + k_scatter7/8: tile-major counts (MapGroup::counts_tm)
   int scatter_counters = 2; // k_scatter8 per-wave counters: 1 partition-major, 2 wave-major
-  bool lz4_queue = false;   // k_lz4_default: chunks from a device work queue (else grid-stride)
+  bool lz4_queue = true;    // k_lz4_default: chunks from a device work queue (else grid-stride)
 };
 
 // Per-launch geometry of a group of consecutive map batches.
