@@ -3249,10 +3249,10 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
 
   // ---- the default: MSD planned on the device, no host wait (graph-capturable).  One stable
   // digit pass over the top tb varying key bits (k_sort_plan finds them in the key span), then
-  // every bucket sorted in LDS by the lower varying 8-bit digits (k_sort_local) — each pair
-  // crosses HBM twice after the top pass instead of twice per digit.  k_sort_bucket_max checks
-  // every bucket fits; a skewed key set instead runs the LSD passes below from the untouched
-  // pairs, which the plan otherwise retires (their kernels return at once: MapGroup::skip).
+  // every bucket sorted by the lower varying 8-bit digits — in LDS (k_sort_local, <= 4096 pairs)
+  // or, for a skewed key set's larger buckets, through global memory by one workgroup each
+  // (k_sort_bucket_global).  Each pair crosses HBM twice after the top pass instead of twice per
+  // digit, and nothing is decided on the host.
   int tb = kSortMinDigitBits;  // ~<= 1536 pairs per bucket on average, at most 2^14 buckets
   while (tb < 14 && (n >> tb) > 1536) ++tb;
   if (node->tuning.sort_msd != 2 && !all_passes && (n >> tb) <= sux::kSortLocalCap / 2) {
@@ -3274,24 +3274,10 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
                                           ws + P1.part_off, P1.ws, nullptr, sort_tn, &node->timer,
                                           s),
               "sort top digit pass");
-    int npass = 0;
-    for (int sh = 128 - bits; sh < 128; sh += digit) ++npass;
-    hip_check(sux::launch_sort_bucket_max(index1, (uint32_t)pd1.R, npass & 1, plan, s),
+    hip_check(sux::launch_sort_bucket_max(index1, (uint32_t)pd1.R, plan, s),
               "sort bucket max");
     hip_check(sux::launch_sort_local_planned(b, a, index1, (uint32_t)pd1.R, plan, s),
               "sort buckets");
-    uint8_t *x = a, *y = b;
-    for (int sh = 128 - bits; sh < 128; sh += digit) {  // the fallback (retired by the plan)
-      pd.seed = sh;
-      P.g.recs = x;
-      P.g.err = node->d_err;
-      P.g.skip = &plan->lsd_skip;
-      hip_check(sux::launch_partition_group(pd, P.g, lay, y, index, nullptr, nullptr,
-                                            ws + P.part_off, P.ws, nullptr, sort_tn, &node->timer,
-                                            s),
-                "sort fallback digit pass");
-      std::swap(x, y);
-    }
     if (inline_rec)
       hip_check(sux::launch_unpair_records_sel(a, b, &plan->final_b, n, record_size, key_kind,
                                                key_offset, key_len, sbytes, d_out, s),

@@ -77,9 +77,6 @@ struct MapGroup {
   // the scan), 1 tile-major [map][tile][p] (k_hist4 with k_scatter7/8: each tile's R counters
   // are one contiguous store instead of R scattered 4-byte writes)
   uint32_t counts_tm;
-  // a sort pass the device plan may retire: when *skip != 0, K1 and K3 return at once (the
-  // pass's data buffers are not touched)
-  const uint32_t* skip;
 };
 // Device error word bits (sux_node_check turns a set word into SUX_EHIP).
 constexpr uint32_t kErrTurnTimeout = 1u;  // k_scatter16b: a wave waited 2^22 sleeps for its turn
@@ -240,8 +237,8 @@ struct SortDigits {
 struct SortPlanDev {
   int32_t top_lo;    // shift of the top digit (the tb highest varying key bits)
   int32_t hb;        // highest varying key bit; -1: every key is equal (the sort is the identity)
-  uint32_t msd_ok;   // 1: every top-digit bucket fits the LDS sort, which finishes the sort
-  uint32_t lsd_skip; // 1: the LSD fallback passes are not needed (msd_ok, or hb < 0)
+  uint32_t msd_ok;   // 1: the bucket sorts finish the sort (0: every key is equal)
+  uint32_t pad;
   uint32_t final_b;  // 1: the sorted pairs end in buffer b, 0: in buffer a
   int32_t kbits;     // key bits (with the segment id): the top kbits of the big-endian pair
   uint64_t maxb;     // the largest top-digit bucket, in pairs
@@ -250,12 +247,12 @@ struct SortPlanDev {
 constexpr uint64_t kSortPlanBytes = 256;
 static_assert(sizeof(SortPlanDev) <= kSortPlanBytes, "plan slot");
 hipError_t launch_sort_plan(const void* span, int bits, int tb, SortPlanDev* plan, hipStream_t s);
-// Largest bucket of the top-digit index -> plan (msd_ok, lsd_skip, final_b; lsd_odd: the
-// fallback runs an odd number of passes).
-hipError_t launch_sort_bucket_max(const int64_t* d_index, uint32_t R, bool lsd_odd,
-                                  SortPlanDev* plan, hipStream_t s);
-// The LDS sort of every top-digit bucket, driven by the plan (a no-op unless plan->msd_ok):
-// one launch per bucket-size class, so each bucket runs on the smallest shape that holds it.
+// Largest bucket of the top-digit index -> plan (maxb, msd_ok, final_b).
+hipError_t launch_sort_bucket_max(const int64_t* d_index, uint32_t R, SortPlanDev* plan,
+                                  hipStream_t s);
+// The sort of every top-digit bucket, driven by the plan (a no-op unless plan->msd_ok): one LDS
+// launch per bucket-size class (each bucket on the smallest shape that holds it), then buckets
+// above kSortLocalCap through global memory.
 hipError_t launch_sort_local_planned(const void* in_pairs, void* out_pairs, const int64_t* d_index,
                                      uint32_t R, const SortPlanDev* plan, hipStream_t s);
 

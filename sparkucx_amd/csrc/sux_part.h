@@ -139,8 +139,6 @@ __device__ __forceinline__ void scan_digit_wave(uint32_t* wc, uint32_t* wsum, in
   __syncthreads();
 }
 
-// A sort's digit pass the device plan retired (MapGroup::skip): the whole grid returns at once.
-__device__ __forceinline__ bool pass_skipped(const MapGroup& g) { return g.skip && *g.skip; }
 // PartDev::dseed: the digit shift of a sort pass decided on the device (k_sort_plan).
 __device__ __forceinline__ void resolve_seed(PartDev& pd) {
   if (pd.dseed) pd.seed = *pd.dseed;

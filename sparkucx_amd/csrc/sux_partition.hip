@@ -34,7 +34,6 @@ namespace sux {
 template <int WPG>
 __global__ __launch_bounds__(WPG * kWave) void k_hist(PartDev pd, MapGroup g, uint16_t* pids,
                                                       uint32_t* counts) {
-  if (pass_skipped(g)) return;
   resolve_seed(pd);
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
@@ -62,9 +61,7 @@ __global__ __launch_bounds__(WPG * kWave) void k_hist(PartDev pd, MapGroup g, ui
 // ------------------------------------------------------------------------------------------
 
 __global__ __launch_bounds__(256) void k_tile_scan(uint32_t* counts, uint64_t* totals,
-                                                   uint32_t rows, uint32_t tiles,
-    const uint32_t* __restrict__ skip) {
-  if (skip && *skip) return;  // a retired sort pass (MapGroup::skip)
+                                                   uint32_t rows, uint32_t tiles) {
   const int lane = threadIdx.x % kWave;
   const uint32_t row = blockIdx.x * 4 + threadIdx.x / kWave;
   if (row >= rows) return;
@@ -92,9 +89,7 @@ __global__ __launch_bounds__(256) void k_tile_scan(uint32_t* counts, uint64_t* t
 // Few tiles per map (large R: 10,000 partitions x 16 tiles): one thread per row, so a row of
 // T <= 64 counters is not a whole (mostly idle) wave.
 __global__ __launch_bounds__(256) void k_tile_scan_rows(uint32_t* counts, uint64_t* totals,
-                                                        uint32_t rows, uint32_t tiles,
-    const uint32_t* __restrict__ skip) {
-  if (skip && *skip) return;  // a retired sort pass (MapGroup::skip)
+                                                        uint32_t rows, uint32_t tiles) {
   const uint32_t row = blockIdx.x * 256 + threadIdx.x;
   if (row >= rows) return;
   uint32_t* c = counts + (uint64_t)row * tiles;
@@ -123,9 +118,7 @@ __global__ __launch_bounds__(256) void k_tile_scan_rows(uint32_t* counts, uint64
 // the tile column (reads: 16 consecutive counters of one tile row per wave quarter), the 16
 // segment sums of a partition are scanned in LDS, and every thread rewrites its segment.
 __global__ __launch_bounds__(256) void k_tile_scan_tm(uint32_t* counts, uint64_t* totals,
-                                                      uint32_t maps, uint32_t R, uint32_t tiles,
-    const uint32_t* __restrict__ skip) {
-  if (skip && *skip) return;  // a retired sort pass (MapGroup::skip)
+                                                      uint32_t maps, uint32_t R, uint32_t tiles) {
   __shared__ uint32_t seg[16][17];
   const uint32_t pl = threadIdx.x % 16, sg = threadIdx.x / 16;
   const uint32_t pgroups = (R + 15) / 16;
@@ -178,9 +171,7 @@ __global__ __launch_bounds__(kScanThreads) void k_map_scan(const uint64_t* __res
                                                            int R, int G, uint32_t rec_size,
                                                            uint64_t records_per_map,
                                                            uint64_t num_records,
-                                                           const uint64_t* __restrict__ map_offs,
-    const uint32_t* __restrict__ skip) {
-  if (skip && *skip) return;  // a retired sort pass (MapGroup::skip)
+                                                           const uint64_t* __restrict__ map_offs) {
   __shared__ uint64_t sh[2 * kWave + 1];
   __shared__ unsigned long long hs[1024];
   const uint32_t m = blockIdx.x;
@@ -294,7 +285,6 @@ __global__ __launch_bounds__(WPG * kWave) void k_scatter(MapGroup g, int R, int 
                                                          const uint32_t* __restrict__ prefix,
                                                          const uint64_t* __restrict__ base,
                                                          uint8_t* __restrict__ out) {
-  if (pass_skipped(g)) return;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const uint32_t gtile = blockIdx.x * WPG + wave;
@@ -345,7 +335,6 @@ __global__ __launch_bounds__(WPG * kWave) void k_scatter(MapGroup g, int R, int 
 template <int KW, int RPL, bool TAB>
 __global__ __launch_bounds__(256) void k_hist3(PartDev pd, MapGroup g, uint16_t* __restrict__ pids,
                                                uint32_t* __restrict__ counts) {
-  if (pass_skipped(g)) return;
   resolve_seed(pd);
   extern __shared__ __attribute__((aligned(16))) uint64_t ldsq[];
   const int R = pd.R;
@@ -435,7 +424,6 @@ struct Hs4 {
 template <uint32_t S, uint32_t CH, int KW, bool TAB, bool NTL, bool PK>
 __global__ __launch_bounds__(256) void k_hist4(PartDev pd, MapGroup g, uint16_t* __restrict__ pids,
                                                uint32_t* __restrict__ counts) {
-  if (pass_skipped(g)) return;
   resolve_seed(pd);
   using H = Hs4<S, CH>;
   constexpr uint32_t PER = H::kPer;
@@ -656,7 +644,6 @@ __global__ __launch_bounds__(NW * 64) void k_scatter6(MapGroup g, int R, int pid
                                                      const uint64_t* __restrict__ base,
                                                      uint8_t* __restrict__ out, uint32_t tpw,
                                                      uint32_t wg_per_map) {
-  if (pass_skipped(g)) return;
   using K = Sc6<S, C, NW>;
   constexpr uint32_t NT = K::NT, W = K::W, RPW = K::RPW, NG = K::NG, PER = K::kPer;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
@@ -883,7 +870,6 @@ __global__ __launch_bounds__(NW * 64) void k_scatter7(MapGroup g, int R, int pid
                                                      const uint64_t* __restrict__ base,
                                                      uint8_t* __restrict__ out, uint32_t tpw,
                                                      uint32_t wg_per_map) {
-  if (pass_skipped(g)) return;
   using K = Sc7<S, C, NW>;
   constexpr uint32_t NT = K::NT, W = K::W, RPW = K::RPW, NG = K::NG, PER = K::kPer;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
@@ -1241,7 +1227,6 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
                                                      const uint64_t* __restrict__ base,
                                                      uint8_t* __restrict__ out, uint32_t cyc,
                                                      uint32_t tw0, uint32_t tw1) {
-  if (pass_skipped(g)) return;
   using K = Sc8<S, C, NW>;
   constexpr uint32_t NT = K::NT, W = K::W, RPW = K::RPW, NG = K::NG, PER = K::kPer;
   constexpr uint32_t RM = 208;  // K's RMAX: the tables' compile-time stride
@@ -1836,19 +1821,19 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g_in, const
   const uint32_t rows = g.num_maps * (uint32_t)R;
   if (s16 || g.counts_tm)
     hipLaunchKernelGGL(k_tile_scan_tm, dim3(g.num_maps * ((R + 15) / 16)), dim3(256), 0, s, counts,
-                       totals, g.num_maps, (uint32_t)R, g.tiles_per_map, g.skip);
+                       totals, g.num_maps, (uint32_t)R, g.tiles_per_map);
   else if (g.tiles_per_map <= 64)
     hipLaunchKernelGGL(k_tile_scan_rows, dim3((rows + 255) / 256), dim3(256), 0, s, counts, totals,
-                       rows, g.tiles_per_map, g.skip);
+                       rows, g.tiles_per_map);
   else
     hipLaunchKernelGGL(k_tile_scan, dim3((rows + 3) / 4), dim3(256), 0, s, counts, totals, rows,
-                       g.tiles_per_map, g.skip);
+                       g.tiles_per_map);
   const uint64_t L = (uint64_t)g.num_maps * R;
   uint64_t* pre = base + L;
   uint64_t* mh = base + 2 * L;
   hipLaunchKernelGGL(k_map_scan, dim3(g.num_maps), dim3(kScanThreads), 0, s, totals, base, pre, mh,
                      d_index, d_index_be, lay.world == 1 ? d_peer_bytes : nullptr, R, lay.world,
-                     g.rec_size, g.records_per_map, g.num_records, nullptr, g.skip);
+                     g.rec_size, g.records_per_map, g.num_records, nullptr);
   if (lay.world > 1) {
     hipLaunchKernelGGL(k_peer_off, dim3(1), dim3(kScanThreads), 0, s, mh, d_peer_bytes,
                        g.num_maps, lay.world, g.rec_size);
@@ -1970,7 +1955,7 @@ hipError_t launch_varlen_map_scan(const VarGroup& g, int R, const uint64_t* tota
   const uint64_t L = (uint64_t)g.num_maps * R;
   hipLaunchKernelGGL(k_map_scan, dim3(g.num_maps), dim3(kScanThreads), 0, s, totals, base,
                      base + L, base + 2 * L, d_index, d_index_be, nullptr, R, 1, 1u,
-                     g.records_per_map, g.num_records, g.offs, nullptr);
+                     g.records_per_map, g.num_records, g.offs);
   return hipGetLastError();
 }
 
@@ -1980,7 +1965,7 @@ hipError_t launch_rows_index(const uint64_t* sizes, uint32_t maps, uint32_t R, u
   const uint64_t L = (uint64_t)maps * R;
   hipLaunchKernelGGL(k_map_scan, dim3(maps), dim3(kScanThreads), 0, s, sizes, base, base + L,
                      base + 2 * L, d_index, d_index_be, nullptr, (int)R, 1, 1u, 0ull, 0ull,
-                     nullptr, nullptr);
+                     nullptr);
   return hipGetLastError();
 }
 

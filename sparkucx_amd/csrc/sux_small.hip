@@ -24,7 +24,6 @@ namespace sux {
 template <int KW>
 __global__ __launch_bounds__(1024) void k_hist16(PartDev pd, MapGroup g, uint16_t* __restrict__ pids,
                                                 uint32_t* __restrict__ counts) {
-  if (pass_skipped(g)) return;
   resolve_seed(pd);
   extern __shared__ __attribute__((aligned(16))) uint32_t hist[];  // [R]
   const int R = pd.R;
@@ -100,7 +99,6 @@ __global__ __launch_bounds__(NW * 64) void k_scatter16b(MapGroup g, int R, int p
                                                         const uint32_t* __restrict__ prefix,
                                                         const uint64_t* __restrict__ base,
                                                         uint8_t* __restrict__ out) {
-  if (pass_skipped(g)) return;
   extern __shared__ __attribute__((aligned(16))) uint32_t cur[];  // [R] next output record of p
   __shared__ uint32_t turn, stop;
   const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
@@ -211,7 +209,6 @@ __global__ __launch_bounds__(1024) void k_scatter16s(MapGroup g, int R, int pid_
                                                      const uint32_t* __restrict__ prefix,
                                                      const uint64_t* __restrict__ base,
                                                      uint8_t* __restrict__ out) {
-  if (pass_skipped(g)) return;
   using K = Sc16s;
   constexpr uint32_t NT = K::NT, NW = K::NW, PT = K::PT, NB = K::NB, CH = kS16sChunk;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
@@ -480,7 +477,6 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16a(PartDev pd, MapGroup g, u
                                                  uint32_t nbk, uint16_t* __restrict__ offs,
                                                  uint16_t* __restrict__ pids_out,
                                                  uint8_t* __restrict__ tmp) {
-  if (pass_skipped(g)) return;
   resolve_seed(pd);
   using K = M16a<NW, DB>;
   constexpr uint32_t NB = K::NB, NT = K::NT, PT = K::PT, CH = kM16Chunk;
@@ -565,7 +561,6 @@ __global__ __launch_bounds__(kScanThreads) void k_msd16_scan(MapGroup g, uint32_
                                                              uint8_t* __restrict__ index_be,
                                                              uint64_t* __restrict__ peer_bytes,
                                                              int R) {
-  if (pass_skipped(g)) return;
   constexpr uint32_t HG = 1024, NG = kScanThreads / HG;  // one thread per bucket (nbk <= 1024)
   __shared__ uint64_t sh[2 * kWave + 1];
   __shared__ uint32_t part[kScanThreads];
@@ -605,7 +600,6 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
                                                  uint8_t* __restrict__ out,
                                                  int64_t* __restrict__ index,
                                                  uint8_t* __restrict__ index_be) {
-  if (pass_skipped(g)) return;
   resolve_seed(pd);
   using K = M16b<NW, PT, LO, MCH>;
   constexpr uint32_t NB = K::NB, NT = K::NT, CAP = K::CAP, MC = MCH, PB = 1u << LO;

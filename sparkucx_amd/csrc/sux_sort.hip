@@ -437,6 +437,96 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : CAP == 1024 ? 6 : 4) void k_
   }
 }
 
+// Buckets above kSortLocalCap (skewed keys: heavy hitters, long duplicate runs): one
+// 1024-thread workgroup per bucket runs a stable LSD over the plan's digits through global
+// memory — per digit a count sweep and a ranked scatter sweep in 4096-element chunks (wave-ballot
+// ranks + one (digit, wave) scan per chunk, per-digit cursors carried across chunks), ping-ponging
+// between the bucket's range of the top pass's output (`in`) and of the final buffer (`out`), and
+// ends in `out` (one copy when the digit count is even).  Slow per bucket (one CU), but only a
+// skewed key set has such buckets, and it replaces round 2's fallback to the whole LSD sort.
+template <uint32_t NW>
+__global__ __launch_bounds__(NW * 64) void k_sort_bucket_global(u32x4* __restrict__ in,
+                                                                u32x4* __restrict__ out,
+                                                                const int64_t* __restrict__ index,
+                                                                uint32_t R,
+                                                                const SortPlanDev* __restrict__ plan) {
+  if (!plan->msd_ok || plan->dg.n == 0) return;
+  const SortDigits dg = plan->dg;
+  constexpr uint32_t NT = NW * kWave, NB = 256, PT = 4, CH = NT * PT;
+  __shared__ uint32_t wc[NW * NB];
+  __shared__ uint32_t wsum[NW];
+  __shared__ uint32_t cur[NB];
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
+  __syncthreads();
+  for (uint32_t b = blockIdx.x; b < R; b += gridDim.x) {
+    const uint64_t s0 = (uint64_t)index[b] / 16, s1 = (uint64_t)index[b + 1] / 16;
+    const uint32_t n = (uint32_t)(s1 - s0);
+    if (n <= kSortLocalCap) continue;  // k_sort_local's
+    u32x4* src = in + s0;
+    u32x4* dst = out + s0;
+    for (int d = 0; d < dg.n; ++d) {
+      const uint64_t w = d < 8 ? dg.lo : dg.hi;
+      const uint32_t sh = (uint32_t)(w >> (8 * (d & 7))) & 255u;
+      // count sweep -> exclusive digit starts in cur
+      if (tid < (int)NB) cur[tid] = 0;
+      __syncthreads();
+      for (uint32_t e = tid; e < n; e += NT) atomicAdd(&cur[pair_digit8(src[e], sh)], 1u);
+      __syncthreads();
+      uint32_t x = 0, incl = 0;
+      if (tid < (int)NB) {
+        x = cur[tid];
+        incl = wave_incl_scan(x, lane);
+        if (lane == kWave - 1) wsum[wave] = incl;
+      }
+      __syncthreads();
+      if (tid < (int)NB) {
+        uint32_t base = 0;
+        for (int q = 0; q < wave; ++q) base += wsum[q];
+        cur[tid] = base + incl - x;
+      }
+      __syncthreads();
+      // ranked scatter, chunk by chunk in element order (stable)
+      for (uint32_t c0 = 0; c0 < n; c0 += CH) {
+        u32x4 v[PT];
+        uint32_t dig[PT], rank[PT];
+#pragma unroll
+        for (uint32_t j = 0; j < PT; ++j) {
+          const uint32_t e = c0 + wave * (PT * kWave) + j * kWave + lane;
+          const bool valid = e < n;
+          v[j] = src[valid ? e : n - 1];
+          dig[j] = valid ? pair_digit8(v[j], sh) : 0u;
+          rank[j] = wave_rank<8>(dig[j], valid, wc + wave * NB, lt_mask);
+        }
+        __syncthreads();
+        scan_digit_wave<NB, NW>(wc, wsum, tid, lane, wave);
+#pragma unroll
+        for (uint32_t j = 0; j < PT; ++j)
+          if (rank[j] != ~0u) dst[cur[dig[j]] + wc[wave * NB + dig[j]] + rank[j]] = v[j];
+        __syncthreads();
+        // the chunk's digit counts advance the cursors: start of digit t+1 minus start of t
+        const uint32_t cn = min(CH, n - c0);
+        uint32_t adv = 0;
+        if (tid < (int)NB) adv = ((uint32_t)tid + 1 < NB ? wc[tid + 1] : cn) - wc[tid];
+        __syncthreads();
+        if (tid < (int)NB) cur[tid] += adv;
+        for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
+        __syncthreads();
+      }
+      u32x4* t = src;
+      src = dst;
+      dst = t;
+      __threadfence_block();
+      __syncthreads();
+    }
+    if (src != out + s0) {  // an even number of digits: the result sits in `in`
+      for (uint32_t e = tid; e < n; e += NT) out[s0 + e] = src[e];
+      __syncthreads();
+    }
+  }
+}
+
 // True when bits [lo, hi) of the big-endian 128-bit pair differ between some records (span: the
 // AND of key words 0..2, then their OR) — sux_api.cpp's span_varies, on the device.
 __device__ bool span_varies_dev(const uint32_t* span, int lo, int hi) {
@@ -466,10 +556,10 @@ __global__ void k_sort_plan(const uint32_t* __restrict__ span, int bits, int tb,
   plan->dg = dg;
 }
 
-// The plan's second half: the largest bucket of the top-digit index decides between the LDS
-// finish and the LSD fallback, and where the sorted pairs end.  One workgroup.
+// The plan's second half: the largest bucket of the top-digit index, and where the sorted pairs
+// end.  One workgroup.
 __global__ __launch_bounds__(1024) void k_sort_bucket_max(const int64_t* __restrict__ index,
-                                                          uint32_t R, uint32_t lsd_odd,
+                                                          uint32_t R,
                                                           SortPlanDev* __restrict__ plan) {
   __shared__ unsigned long long m;
   if (threadIdx.x == 0) m = 0;
@@ -481,13 +571,13 @@ __global__ __launch_bounds__(1024) void k_sort_bucket_max(const int64_t* __restr
   __syncthreads();
   if (threadIdx.x == 0) {
     const bool all_equal = plan->hb < 0;
-    const bool ok = !all_equal && m <= kSortLocalCap;
     plan->maxb = m;
-    plan->msd_ok = ok ? 1u : 0u;
-    plan->lsd_skip = (ok || all_equal) ? 1u : 0u;
-    // a -> top pass -> b -> LDS sort -> a; no lower digit varies: the top pass's b; the LSD
-    // fallback: a after an even number of passes; every key equal: a (the input order)
-    plan->final_b = all_equal ? 0u : ok ? (plan->dg.n ? 0u : 1u) : lsd_odd;
+    // buckets up to kSortLocalCap sort in LDS (k_sort_local), larger ones through global memory
+    // (k_sort_bucket_global): the MSD path always finishes once some key bit varies
+    plan->msd_ok = all_equal ? 0u : 1u;
+    // a -> top pass -> b -> bucket sorts -> a; no lower digit varies: the top pass's b; every
+    // key equal: a (the input order)
+    plan->final_b = all_equal ? 0u : (plan->dg.n ? 0u : 1u);
   }
 }
 
@@ -497,10 +587,9 @@ hipError_t launch_sort_plan(const void* span, int bits, int tb, SortPlanDev* pla
   return hipGetLastError();
 }
 
-hipError_t launch_sort_bucket_max(const int64_t* d_index, uint32_t R, bool lsd_odd,
-                                  SortPlanDev* plan, hipStream_t s) {
-  hipLaunchKernelGGL(k_sort_bucket_max, dim3(1), dim3(1024), 0, s, d_index, R,
-                     lsd_odd ? 1u : 0u, plan);
+hipError_t launch_sort_bucket_max(const int64_t* d_index, uint32_t R, SortPlanDev* plan,
+                                  hipStream_t s) {
+  hipLaunchKernelGGL(k_sort_bucket_max, dim3(1), dim3(1024), 0, s, d_index, R, plan);
   return hipGetLastError();
 }
 
@@ -523,6 +612,8 @@ hipError_t launch_sort_local_planned(const void* in_pairs, void* out_pairs, cons
   allow_lds(reinterpret_cast<const void*>(&k_sort_local<8, kSortLocalCap>), l3);
   hipLaunchKernelGGL((k_sort_local<8, kSortLocalCap>), dim3(std::min<uint32_t>(R, 2 * ncu)),
                      dim3(8 * kWave), l3, s, in, out, d_index, R, 2048u, plan);
+  hipLaunchKernelGGL((k_sort_bucket_global<16>), dim3(std::min<uint32_t>(R, ncu)), dim3(16 * kWave),
+                     0, s, const_cast<u32x4*>(in), out, d_index, R, plan);
   return hipGetLastError();
 }
 
