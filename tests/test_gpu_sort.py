@@ -221,18 +221,21 @@ def test_segmented_inline_small_records(gpu_node, nseg):
 
 
 @pytest.mark.parametrize("msd", [1, 2])
-@pytest.mark.parametrize("shape", ["terasort", "skewed_top", "long", "int_inline"])
+@pytest.mark.parametrize("shape", ["terasort", "skewed_top", "skewed_top9", "long", "int_inline"])
 def test_msd_finish_and_lsd_agree_with_oracle(gpu_node, tuned, msd, shape):
-    """sort_msd 1: one top-digit pass + every bucket sorted in LDS (k_sort_local); 2: LSD digit
-    passes only.  'skewed_top': 60 % of the keys share their top bytes, so a bucket passes the
-    LDS capacity and the MSD path must fall back to the LSD passes from the untouched pairs."""
+    """sort_msd 1: one top-digit pass + every bucket sorted by the lower digits (k_sort_local in
+    LDS; k_sort_bucket_global for a bucket above the LDS capacity); 2: LSD digit passes only.
+    'skewed_top' / 'skewed_top9': 60 % of the keys share their top bytes, so one bucket passes the
+    LDS capacity and is sorted through global memory (10- and 9-byte keys: both parities of its
+    digit count)."""
     tuned(sort_msd=msd)
     if shape == "terasort":
         recs, rs, kind, off, klen = O.gen_terasort(61, 0, 700_000), 100, N.SORT_BYTES, 0, 10
-    elif shape == "skewed_top":
+    elif shape in ("skewed_top", "skewed_top9"):
         recs = O.gen_terasort(62, 0, 300_000).reshape(-1, 100)
         recs[: 180_000, :4] = 9
-        recs, rs, kind, off, klen = recs.ravel(), 100, N.SORT_BYTES, 0, 10
+        klen = 10 if shape == "skewed_top" else 9
+        recs, rs, kind, off = recs.ravel(), 100, N.SORT_BYTES, 0
     elif shape == "long":
         recs, rs, kind, off, klen = O.gen_small(63, 0, 500_000), 16, N.SORT_LONG, 0, 8
     else:
