@@ -369,6 +369,9 @@ struct MapSlot {
   std::vector<uint64_t> seg;   // per peer: offset of the map's range for that peer in the slab
   uint64_t bytes = 0;
   std::vector<int64_t> index;  // R+1 cumulative offsets (the index file, native order)
+  // adopted map outputs (world 1): the caller's device index table; the host copy above is made
+  // on first use (host_index) — resolves read only the entries they need, on the device
+  const int64_t* d_index = nullptr;
   std::shared_ptr<Slab> rslab; // receive buffer holding this rank's owned range of the map
   uint64_t recv_off = 0;       // offset of that range in rslab
   // after an exchange, per rank h: where h serves its owned range of this map — an index into
@@ -379,6 +382,16 @@ struct MapSlot {
   uint8_t* data() const { return slab ? slab->buf.ptr + off : nullptr; }
   bool spilled() const { return !spill_data.empty(); }
 };
+
+// The map's index table on the host: an adopted map's is read back from the device on first use.
+const std::vector<int64_t>& host_index(MapSlot& sl, int R) {
+  if (sl.index.empty() && sl.d_index) {
+    sl.index.resize((size_t)R + 1);
+    hip_check(hipMemcpy(sl.index.data(), sl.d_index, 8 * ((size_t)R + 1), hipMemcpyDeviceToHost),
+              "index read-back");
+  }
+  return sl.index;
+}
 
 // One sux_write_map_outputs / sux_adopt_map_outputs call in flight: published by progress()
 // once `done` has fired.
@@ -392,6 +405,8 @@ struct WriteJob {
   std::shared_ptr<Slab> slab;
   PoolBuf ws;
   std::pair<void*, uint64_t> hidx{nullptr, 0};  // pinned copy of the batch's index tables
+  const int64_t* dindex = nullptr;  // adopted at world 1: the index tables stay on the device
+  uint32_t rs = 0;                  // (and the maps' sizes come from their record counts)
   std::shared_ptr<Event> done;
 };
 
@@ -556,6 +571,27 @@ uint32_t take_device_err(sux_node* node) {
 // data location (map-major offset, or per-peer segments of a peer-major slab) and the batch.
 void publish_job(sux_node* node, Shuffle& sh, WriteJob& j) {
   const int R = sh.R, W = j.world;
+  if (j.dindex) {  // adopted at world 1: no host copy of the index tables
+    for (uint32_t k = 0; k < j.maps; ++k) {
+      if (!j.claimed[k]) continue;
+      MapSlot& slot = sh.maps[j.first + k];
+      slot.pending = false;
+      slot.present = true;
+      slot.sent = false;
+      slot.owner = node->conf.rank;
+      slot.slab = j.slab;
+      slot.batch = j.batch;
+      slot.off = (uint64_t)k * j.rpm * (uint64_t)j.rs;
+      const uint64_t recs = std::min<uint64_t>(j.rpm, j.n - (uint64_t)k * j.rpm);
+      slot.bytes = recs * j.rs;
+      slot.index.clear();
+      slot.d_index = j.dindex + (uint64_t)k * (R + 1);
+      slot.rslab.reset();
+      slot.seg.assign(1, slot.off);  // world 1: the one peer's range starts at the data file
+      publish_slot(node, sh, j.first + (int32_t)k, (uint64_t)(uintptr_t)slot.d_index);
+    }
+    return;
+  }
   const int64_t* hx = static_cast<const int64_t*>(j.hidx.first);
   auto ix = [&](uint32_t k, int p) { return hx[(uint64_t)k * (R + 1) + p]; };
   // peer-major: sections [h] of the whole job (every map the kernels wrote, claimed or not)
@@ -580,6 +616,7 @@ void publish_job(sux_node* node, Shuffle& sh, WriteJob& j) {
       slot.off = (uint64_t)k * j.rpm * (uint64_t)sh.rec_size;
       slot.bytes = (uint64_t)ix(k, R);
       slot.index.assign(hx + (uint64_t)k * (R + 1), hx + (uint64_t)(k + 1) * (R + 1));
+      slot.d_index = nullptr;
       slot.rslab.reset();
       if (W > 1) {
         slot.seg = run;
@@ -1638,7 +1675,8 @@ bool spill_some(sux_node* node, uint64_t need) {
         const std::string base = node->spill_dir + "/shuffle_" + std::to_string(sh.id) + "_" +
                                  std::to_string(sm.second) + "_0";
         std::vector<int64_t> lengths((size_t)sh.R);
-        for (int p = 0; p < sh.R; ++p) lengths[p] = sl.index[p + 1] - sl.index[p];
+        const std::vector<int64_t>& ix = host_index(sl, sh.R);
+        for (int p = 0; p < sh.R; ++p) lengths[p] = ix[p + 1] - ix[p];
         write_map_file(sl.data(), sl.bytes, lengths.data(), sh.R, base + ".data", base + ".index",
                        s, st, nullptr);
         sl.spill_data = base + ".data";
@@ -2187,6 +2225,7 @@ int sux_commit_map_output(sux_node* node, int32_t shuffle_id, int32_t map_index,
     slot.off = 0;
     slot.bytes = bytes;
     slot.index = std::move(index);
+    slot.d_index = nullptr;
     slot.rslab.reset();
     const int NW = node->conf.world_size;
     slot.seg.resize((size_t)NW);
@@ -2206,7 +2245,7 @@ int sux_adopt_map_outputs(sux_node* node, int32_t shuffle_id, int32_t first,
     hipStream_t s = node->stream(stream);
     const uint64_t maps = (n + rpm - 1) / rpm;
     auto job = std::make_unique<WriteJob>();
-    int R = 0;
+    int R = 0, rs = 0;
     {
       std::unique_lock<std::mutex> lk(node->mu);
       Shuffle& sh = node->shuffle(shuffle_id);
@@ -2215,6 +2254,7 @@ int sux_adopt_map_outputs(sux_node* node, int32_t shuffle_id, int32_t first,
                   ") out of [0, " + std::to_string(sh.num_maps) + ")");
       progress(node, sh, lk, false);
       R = sh.R;
+      rs = sh.rec_size;
       job->claimed.assign((size_t)maps, 0);
       bool any = false;
       for (uint64_t k = 0; k < maps; ++k) {
@@ -2239,10 +2279,18 @@ int sux_adopt_map_outputs(sux_node* node, int32_t shuffle_id, int32_t first,
     borrowed.cap = 0;
     job->slab = std::make_shared<Slab>(nullptr, borrowed);  // not the node's: nothing to free
     try {
-      job->hidx = node->hpool.get(8 * maps * (uint64_t)(R + 1));
-      hip_check(hipMemcpyAsync(job->hidx.first, d_index, 8 * maps * (uint64_t)(R + 1),
-                               hipMemcpyDeviceToHost, s),
-                "D2H index");
+      if (node->conf.world_size == 1) {
+        // the index tables stay where the caller keeps them (like the data): no read-back of
+        // maps x (R + 1) entries — 82 MB a step at C5's R = 10 000 — blocks resolve from them on
+        // the device
+        job->dindex = d_index;
+        job->rs = (uint32_t)rs;
+      } else {
+        job->hidx = node->hpool.get(8 * maps * (uint64_t)(R + 1));
+        hip_check(hipMemcpyAsync(job->hidx.first, d_index, 8 * maps * (uint64_t)(R + 1),
+                                 hipMemcpyDeviceToHost, s),
+                  "D2H index");
+      }
       job->done = std::make_shared<Event>();
       hip_check(hipEventRecord(job->done->e, s), "hipEventRecord");
     } catch (...) {
@@ -2275,10 +2323,11 @@ int sux_map_output_index(sux_node* node, int32_t shuffle_id, int32_t map_index, 
     Shuffle& sh = node->shuffle(shuffle_id);
     require(map_index >= 0 && map_index < sh.num_maps, SUX_EINVAL, "map index out of range");
     progress(node, sh, lk, false);
-    const MapSlot& slot = sh.maps[map_index];
+    MapSlot& slot = sh.maps[map_index];
     require(slot.present, SUX_ENOENT, "map " + std::to_string(map_index) + " has no output");
     require(out_len >= 8 * (uint64_t)(sh.R + 1), SUX_EINVAL, "index buffer too small");
-    for (int r = 0; r <= sh.R; ++r) store_be64(out + 8 * (size_t)r, (uint64_t)slot.index[r]);
+    const std::vector<int64_t>& ix = host_index(slot, sh.R);
+    for (int r = 0; r <= sh.R; ++r) store_be64(out + 8 * (size_t)r, (uint64_t)ix[r]);
   });
 }
 
@@ -2593,13 +2642,13 @@ int sux_exchange_maps(sux_node* node, int32_t shuffle_id, int32_t first, int32_t
       tag = ((uint64_t)(uint32_t)shuffle_id << 32) | sh.gathers;
       sh.gathers += 3;
       for (int m = first; m < first + count; ++m) {
-        const MapSlot& sl = sh.maps[m];
+        MapSlot& sl = sh.maps[m];
         if (!sl.present || sl.owner != me || sl.sent || !sl.slab || sl.spilled()) continue;
         DirEntry d;
         d.map = m;
         d.owner = me;
         d.batch = sl.batch;
-        d.index = sl.index;
+        d.index = host_index(sl, sh.R);
         d.seg = sl.seg;
         mine.push_back(std::move(d));
         mine_slab.push_back(sl.slab);
@@ -2840,7 +2889,11 @@ struct BlockLoc {
 // Resolve one block; throws SUX_ENOENT for a block not readable here.  At world > 1 a rank
 // reads its owned partitions of every map (after the exchange) and any partitions of its own
 // maps (within one peer's range: an own peer-major slab holds each peer's share separately).
-BlockLoc resolve(sux_node* node, Shuffle& sh, const sux_block_id& b) {
+// ae: the block's two index entries when the caller already gathered them (adopted maps, whose
+// index tables stay on the device); hold = false: no reference on the buffer (a zero-copy
+// resolve that returns bare addresses).
+BlockLoc resolve(sux_node* node, Shuffle& sh, const sux_block_id& b, const int64_t* ae = nullptr,
+                 bool hold = true) {
   const int R = sh.R;
   auto name = [&] {
     return "shuffle_" + std::to_string(sh.id) + "_" + std::to_string(b.map_index) + "_" +
@@ -2851,18 +2904,19 @@ BlockLoc resolve(sux_node* node, Shuffle& sh, const sux_block_id& b) {
   if (!(b.map_index >= 0 && b.map_index < sh.num_maps && b.start_reduce >= 0 &&
         b.end_reduce > b.start_reduce && b.end_reduce <= R))
     raise(SUX_EINVAL, "malformed block " + name());
-  const MapSlot& sl = sh.maps[b.map_index];
+  MapSlot& sl = sh.maps[b.map_index];
   if (!sl.present) raise(SUX_ENOENT, "Unknown block " + name() + ": map output not committed");
   BlockLoc L;
-  const int64_t a = sl.index[b.start_reduce], e = sl.index[b.end_reduce];
+  const int64_t a = ae ? ae[0] : host_index(sl, R)[b.start_reduce];
+  const int64_t e = ae ? ae[1] : host_index(sl, R)[b.end_reduce];
   L.size = e - a;
   const int W = node->conf.world_size, me = node->conf.rank;
   const int lo = owner_lo(me, R, W), hi = owner_lo(me + 1, R, W);
   const bool owned = b.start_reduce >= lo && b.end_reduce <= hi;
   if (sl.rslab && owned) {  // received (or looped back) by an exchange
-    L.addr = (uint64_t)(uintptr_t)(sl.rslab->buf.ptr + sl.recv_off + (a - sl.index[lo]));
+    L.addr = (uint64_t)(uintptr_t)(sl.rslab->buf.ptr + sl.recv_off + (a - host_index(sl, R)[lo]));
     L.rslab = sl.rslab.get();
-    L.hold = sl.rslab;
+    if (hold) L.hold = sl.rslab;
     return L;
   }
   if (sl.owner == me) {
@@ -2871,7 +2925,7 @@ BlockLoc resolve(sux_node* node, Shuffle& sh, const sux_block_id& b) {
       L.file_off = (uint64_t)a;
       return L;
     }
-    L.hold = sl.slab;
+    if (hold) L.hold = sl.slab;
     if (W == 1 || sl.seg.empty()) {
       L.addr = (uint64_t)(uintptr_t)(sl.data() + a);
       return L;
@@ -2882,7 +2936,7 @@ BlockLoc resolve(sux_node* node, Shuffle& sh, const sux_block_id& b) {
     if (b.end_reduce > owner_lo(h + 1, R, W))
       raise(SUX_EINVAL, "block " + name() + " spans the partition ranges of two ranks; split it");
     L.addr = (uint64_t)(uintptr_t)(sl.slab->buf.ptr + sl.seg[h] +
-                                   (uint64_t)(a - sl.index[owner_lo(h, R, W)]));
+                                   (uint64_t)(a - host_index(sl, R)[owner_lo(h, R, W)]));
     return L;
   }
   if (sl.serve.empty())
@@ -2906,8 +2960,58 @@ BlockLoc resolve(sux_node* node, Shuffle& sh, const sux_block_id& b) {
   uint64_t doff;
   std::memcpy(&doff, desc.data() + 64, 8);
   L.addr = (uint64_t)(uintptr_t)(static_cast<uint8_t*>(base) + doff + sv.second +
-                                 (uint64_t)(a - sl.index[owner_lo(h, R, W)]));
+                                 (uint64_t)(a - host_index(sl, R)[owner_lo(h, R, W)]));
   return L;
+}
+
+// The (start, end) index entries of every block whose map keeps its index table on the device
+// (adopted outputs), gathered in one device pass: ae[2i], ae[2i+1]; has[i] = 1 for those blocks.
+// Called with the node lock held (no pool spill from here: the device buffer is a plain get).
+void gather_device_entries(sux_node* node, Shuffle& sh, const sux_block_id* blocks, int32_t n,
+                           std::vector<int64_t>& ae, std::vector<uint8_t>& has) {
+  has.assign((size_t)n, 0);
+  std::vector<const int64_t*> ptrs;
+  std::vector<int32_t> at;
+  for (int i = 0; i < n; ++i) {
+    const sux_block_id& b = blocks[i];
+    if (b.map_index < 0 || b.map_index >= sh.num_maps || b.start_reduce < 0 ||
+        b.end_reduce <= b.start_reduce || b.end_reduce > sh.R)
+      continue;  // resolve() reports it
+    const MapSlot& sl = sh.maps[b.map_index];
+    if (!sl.present || !sl.index.empty() || !sl.d_index) continue;
+    ptrs.push_back(sl.d_index + b.start_reduce);
+    ptrs.push_back(sl.d_index + b.end_reduce);
+    at.push_back(i);
+  }
+  if (at.empty()) return;
+  const uint64_t k = ptrs.size(), pbytes = 8 * k, pad = (pbytes + 255) / 256 * 256;
+  node->bind();
+  hipStream_t s = node->stream(nullptr);
+  PoolBuf dev = node->pool->get(pad + 8 * k);
+  HostLease hp(node->hpool, pad + 8 * k);
+  uint8_t* h = static_cast<uint8_t*>(hp.b.first);
+  try {
+    std::memcpy(h, ptrs.data(), pbytes);
+    hip_check(hipMemcpyAsync(dev.ptr, h, pbytes, hipMemcpyHostToDevice, s), "H2D entry pointers");
+    hip_check(sux::launch_gather_i64(reinterpret_cast<const int64_t* const*>(dev.ptr), (uint32_t)k,
+                                     reinterpret_cast<int64_t*>(dev.ptr + pad), s),
+              "gather index entries");
+    hip_check(hipMemcpyAsync(h + pad, dev.ptr + pad, 8 * k, hipMemcpyDeviceToHost, s),
+              "D2H index entries");
+    hip_check(hipStreamSynchronize(s), "sync index entries");
+  } catch (...) {
+    (void)hipStreamSynchronize(s);
+    node->pool->put(dev);
+    throw;
+  }
+  node->pool->put(dev);
+  ae.resize(2 * (size_t)n);
+  const int64_t* r = reinterpret_cast<const int64_t*>(h + pad);
+  for (size_t j = 0; j < at.size(); ++j) {
+    ae[2 * (size_t)at[j]] = r[2 * j];
+    ae[2 * (size_t)at[j] + 1] = r[2 * j + 1];
+    has[(size_t)at[j]] = 1;
+  }
 }
 }  // namespace
 
@@ -2921,8 +3025,11 @@ int sux_resolve_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* b
     std::unique_lock<std::mutex> lk(node->mu);
     Shuffle& sh = node->shuffle(shuffle_id);
     drain(node, sh, lk);
+    std::vector<int64_t> ae;
+    std::vector<uint8_t> has;
+    gather_device_entries(node, sh, blocks, n, ae, has);
     for (int i = 0; i < n; ++i) {
-      const BlockLoc L = resolve(node, sh, blocks[i]);
+      const BlockLoc L = resolve(node, sh, blocks[i], has[i] ? &ae[2 * (size_t)i] : nullptr, false);
       if (L.file)
         raise(SUX_ESTATE, "map " + std::to_string(blocks[i].map_index) +
                               " was spilled to " + *L.file + ": fetch its blocks");
@@ -2951,9 +3058,12 @@ int sux_fetch_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* blo
       // sizes from the index tables of the directory
       total = 0;
       waits.clear();
+      std::vector<int64_t> ae;
+      std::vector<uint8_t> has;
+      gather_device_entries(node, sh, blocks, n, ae, has);
       const Slab* last = nullptr;
       for (int i = 0; i < n; ++i) {
-        loc[i] = resolve(node, sh, blocks[i]);
+        loc[i] = resolve(node, sh, blocks[i], has[i] ? &ae[2 * (size_t)i] : nullptr);
         sizes[i] = loc[i].size;
         total += (uint64_t)loc[i].size;
         files[i] = loc[i].file ? *loc[i].file : std::string();

@@ -148,6 +148,21 @@ __global__ __launch_bounds__(256) void k_pull(int32_t W, int32_t me, const uint6
   for (uint64_t i = n4 * 4 + t0; i < size; i += step) dst[i] = src[i];
 }
 
+// out[i] = *ptrs[i]: the index entries a batch of block resolves needs from device-resident index
+// tables (adopted map outputs), 16 bytes per block each way instead of every table.
+__global__ __launch_bounds__(256) void k_gather_i64(const int64_t* const* __restrict__ ptrs,
+                                                    uint32_t n, int64_t* __restrict__ out) {
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) out[i] = *ptrs[i];
+}
+
+hipError_t launch_gather_i64(const int64_t* const* d_ptrs, uint32_t n, int64_t* d_out,
+                             hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint32_t g = (n + 255) / 256;
+  hipLaunchKernelGGL(k_gather_i64, dim3(g < 2048 ? g : 2048), dim3(256), 0, s, d_ptrs, n, d_out);
+  return hipGetLastError();
+}
+
 hipError_t launch_pull(int32_t W, int32_t me, const uint64_t* srcs, const int64_t* gi, int32_t M,
                        int32_t R, uint8_t* recv, uint64_t cap, uint64_t* recv_bytes,
                        hipStream_t s) {

@@ -194,6 +194,10 @@ struct CopyDesc {
 hipError_t launch_gather_copy(const CopyDesc* d_desc, uint32_t n, uint32_t chunks_total,
                               const uint32_t* d_chunk_first, Timer* timer, hipStream_t s);
 
+// out[i] = *ptrs[i] (device pointers to int64 index entries; sux_copy.hip).
+hipError_t launch_gather_i64(const int64_t* const* d_ptrs, uint32_t n, int64_t* d_out,
+                             hipStream_t s);
+
 // One-sided pull of a peer-major group from mapped peer buffers (sux_copy.hip).
 hipError_t launch_pull(int32_t W, int32_t me, const uint64_t* srcs, const int64_t* gi, int32_t M,
                        int32_t R, uint8_t* recv, uint64_t cap, uint64_t* recv_bytes,

@@ -264,10 +264,10 @@ def test_launch_group_over_8_gib_keeps_the_image_scatter(gpu_node, tuned, kernel
 @pytest.mark.parametrize("R,n,rpm,tile,tpi", [
     (200, 300000, 300000, 4096, 1),     # an item per tile: a seam every 4 chunks
     (200, 250001, 70001, 4096, 0),      # ragged maps: items end mid-line everywhere
-    (215, 200000, 100000, 4096, 3),     # largest R of k_scatter8 (LDS)
+    (208, 200000, 100000, 4096, 3),     # largest R of k_scatter8 (its LDS tables' RMAX)
     (7, 100000, 50000, 4096, 2),        # few partitions: long runs, many full lines per chunk
     (150, 90000, 90000, 1024, 1),       # short tiles: one chunk per item
-    (220, 60000, 60000, 4096, 0),       # above k_scatter8 LDS: k_scatter7
+    (209, 60000, 60000, 4096, 0),       # above k_scatter8's RMAX: k_scatter7
 ])
 def test_line_carry_scatter_shapes(gpu_node, tuned, R, n, rpm, tile, tpi):
     """k_scatter8 (whole-line writes, carried partial lines): item seams at every tile, runs
@@ -282,7 +282,7 @@ def test_line_carry_scatter_shapes(gpu_node, tuned, R, n, rpm, tile, tpi):
     out, index, index_be = gpu_node.partition_maps(gp, torch.from_numpy(recs).cuda(), 100, rpm)
     torch.cuda.synchronize()
     expect(opart, recs, 100, rpm, out, index, index_be)
-    assert gpu_node.kernel_variant(2) == ("k_scatter8" if R <= 215 else "k_scatter7")
+    assert gpu_node.kernel_variant(2) == ("k_scatter8" if R <= 208 else "k_scatter7")
     gp.close()
 
 
