@@ -135,6 +135,12 @@ def test_adopt_map_outputs_resolves_in_place(gpu_node):
         for i, (m, p) in enumerate(blocks):
             assert addrs[i] == base + m * rpm * 100 + ix[m, p]
             assert sizes[i] == ix[m, p + 1] - ix[m, p]
+        # ShuffleBlockBatchId ranges resolve from the device-resident index tables too
+        ranges = [(m, 3, 40) for m in range(M)] + [(M - 1, 0, R)]
+        addrs, sizes = gpu_node.resolve_blocks(11, ranges)
+        for i, (m, a, b) in enumerate(ranges):
+            assert addrs[i] == base + m * rpm * 100 + ix[m, a]
+            assert sizes[i] == ix[m, b] - ix[m, a]
         # first commit wins: adopting again changes nothing
         gpu_node.adopt_map_outputs(11, 0, out, rpm, n, index)
         want = O.write_maps(opart, O.gen_terasort(SEED, 0, n), 100, rpm)
