@@ -340,10 +340,14 @@ struct Event {  // one completion event, shared by a write job and a thread that
 struct Slab {
   DevicePool* pool = nullptr;
   PoolBuf buf;
+  PoolBuf aux;  // the device index tables of the slab's maps (world-1 writes), freed with it
   std::shared_ptr<Event> ready;
   Slab(DevicePool* p, PoolBuf b) : pool(p), buf(b) {}
   ~Slab() {
-    if (pool) pool->put(buf);
+    if (pool) {
+      pool->put(buf);
+      pool->put(aux);
+    }
   }
   Slab(const Slab&) = delete;
   Slab& operator=(const Slab&) = delete;
@@ -590,6 +594,8 @@ void publish_job(sux_node* node, Shuffle& sh, WriteJob& j) {
       slot.seg.assign(1, slot.off);  // world 1: the one peer's range starts at the data file
       publish_slot(node, sh, j.first + (int32_t)k, (uint64_t)(uintptr_t)slot.d_index);
     }
+    node->pool->put(j.ws);
+    j.ws = PoolBuf{};
     return;
   }
   const int64_t* hx = static_cast<const int64_t*>(j.hidx.first);
@@ -1681,6 +1687,7 @@ bool spill_some(sux_node* node, uint64_t need) {
                        s, st, nullptr);
         sl.spill_data = base + ".data";
         sl.spill_index = base + ".index";
+        sl.d_index = nullptr;  // (host_index above made the host copy)
         sl.slab.reset();
         node->spills++;
       }
@@ -2072,7 +2079,16 @@ int sux_write_map_outputs(sux_node* node, int32_t shuffle_id, int32_t first,
       job->slab = std::make_shared<Slab>(node->pool.get(), pool_get_or_spill(node, n * rs));
       job->ws = pool_get_or_spill(node, G.ws.total + 8 * maps * (uint64_t)(R + 1) + 256);
       int64_t* d_idx = reinterpret_cast<int64_t*>(job->ws.ptr + (G.ws.total + 255) / 256 * 256);
-      job->hidx = node->hpool.get(8 * maps * (uint64_t)(R + 1));
+      if (W == 1) {
+        // world 1: the index tables stay on the device with the slab (no maps x (R + 1) read-back
+        // per batch; resolves gather the entries they need, host_index the rest on demand)
+        job->slab->aux = pool_get_or_spill(node, 8 * maps * (uint64_t)(R + 1));
+        d_idx = reinterpret_cast<int64_t*>(job->slab->aux.ptr);
+        job->dindex = d_idx;
+        job->rs = (uint32_t)rs;
+      } else {
+        job->hidx = node->hpool.get(8 * maps * (uint64_t)(R + 1));
+      }
       {
         std::lock_guard<std::mutex> lk(node->mu);
         job->batch = node->shuffle(shuffle_id).next_batch++;
@@ -2084,9 +2100,10 @@ int sux_write_map_outputs(sux_node* node, int32_t shuffle_id, int32_t first,
       hip_check(hipStreamWaitEvent(ms, node->pipe_ev[0], 0), "fork");
       run_group(node, part, G, W, job->slab->buf.ptr, d_idx, nullptr, nullptr, nullptr,
                 job->ws.ptr, G.ws.total, ms, true);
-      hip_check(hipMemcpyAsync(job->hidx.first, d_idx, 8 * maps * (uint64_t)(R + 1),
-                               hipMemcpyDeviceToHost, ms),
-                "D2H index");
+      if (W != 1)
+        hip_check(hipMemcpyAsync(job->hidx.first, d_idx, 8 * maps * (uint64_t)(R + 1),
+                                 hipMemcpyDeviceToHost, ms),
+                  "D2H index");
       job->done = std::make_shared<Event>();
       hip_check(hipEventRecord(job->done->e, ms), "hipEventRecord");
       hip_check(hipStreamWaitEvent(s, job->done->e, 0), "join");
