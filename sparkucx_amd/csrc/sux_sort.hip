@@ -501,9 +501,12 @@ __global__ __launch_bounds__(NW * 64) void k_sort_bucket_global(u32x4* __restric
         }
         __syncthreads();
         scan_digit_wave<NB, NW>(wc, wsum, tid, lane, wave);
+        // wc[w][t] is the chunk-wide (digit, wave) prefix; wc[0][t] = where digit t starts in
+        // the chunk, so wc[w][t] - wc[0][t] is wave w's offset inside the chunk's digit-t run
 #pragma unroll
         for (uint32_t j = 0; j < PT; ++j)
-          if (rank[j] != ~0u) dst[cur[dig[j]] + wc[wave * NB + dig[j]] + rank[j]] = v[j];
+          if (rank[j] != ~0u)
+            dst[cur[dig[j]] + (wc[wave * NB + dig[j]] - wc[dig[j]]) + rank[j]] = v[j];
         __syncthreads();
         // the chunk's digit counts advance the cursors: start of digit t+1 minus start of t
         const uint32_t cn = min(CH, n - c0);

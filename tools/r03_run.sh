@@ -15,11 +15,11 @@ for st in "$@"; do
   n=$((n+1))
   kind=${st%%:*}; arg=${st#*:}
   case $kind in
-    t) eval "timeout -k 10 900 python -u -m pytest $arg -x -v --timeout 300 --timeout-method thread" > $out/tests_$n.log 2>&1; rc=$?
+    t) eval "timeout -k 10 900 python -u -m pytest $arg -x -v --timeout 150 --timeout-method thread" > $out/tests_$n.log 2>&1; rc=$?
        tail -3 $out/tests_$n.log ;;
     b) timeout -k 10 600 python -u bench.py $arg > $out/bench_$n.json 2> $out/bench_$n.err; rc=$?
        cat $out/bench_$n.json | head -c 600; echo ;;
-    p) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $out/prof_$n -o run -- python -u bench.py $arg > $out/prof_$n.json 2> $out/prof_$n.err; rc=$? ;;
+    p) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $out/prof_$n -o run --output-format csv -- python -u bench.py $arg > $out/prof_$n.json 2> $out/prof_$n.err; rc=$? ;;
     s) timeout -k 10 600 bash -c "$arg" > $out/step_$n.log 2>&1; rc=$? ;;
   esac
   echo "step $n ($kind) rc=$rc: $arg" | tee -a $out/steps.txt
