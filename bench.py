@@ -351,7 +351,7 @@ def maps_2e27_leg(node, part, data, out, n: int, rs: int, R: int, dev, steps: in
             "GB/s": round(n * rs / dt / 1e9, 1), "index_consistent": ok}
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r02.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r03.json")
 
 
 def plugin_leg(node, part, data, rs: int, R: int, rpm: int, gm: int, groups: int, dev,
@@ -367,7 +367,9 @@ def plugin_leg(node, part, data, rs: int, R: int, rpm: int, gm: int, groups: int
     n = maps * rpm
     stream = torch.cuda.current_stream(dev)
     # every (map, reduce partition) block, reducer by reducer
-    blocks = np.stack([np.tile(np.arange(maps), R), np.repeat(np.arange(R), maps)], 1).astype(np.int32)
+    # (sux_block_id rows (map, p, p + 1, 0), built once)
+    blocks = node._blocks(np.stack([np.tile(np.arange(maps), R), np.repeat(np.arange(R), maps)],
+                                   1).astype(np.int32))
 
     phase = {"register": 0.0, "write": 0.0, "wait": 0.0, "resolve": 0.0, "unregister": 0.0}
 
@@ -568,7 +570,7 @@ def self_check(node, part, data, out, index, n: int, rs: int, rpm: int, R: int,
 
 def load_traffic(workload: str, kernel: str) -> dict | None:
     """HBM bytes per record of `kernel` under `workload`, from the committed PMC summary
-    (profiles/pmc_r02.json, written by profiles/collect_pmc.py: one rocprofv3 pass per counter
+    (profiles/pmc_r03.json, written by profiles/collect_pmc.py: one rocprofv3 pass per counter
     group; 2 x FETCH_SIZE + WRITE_SIZE per the microarch guide).  The entry is keyed by workload
     and by the kernel the library reports it launched (sux_kernel_variant), so a line never
     borrows another kernel's counters; None when that pair was not profiled."""
@@ -578,7 +580,7 @@ def load_traffic(workload: str, kernel: str) -> dict | None:
         # a slot that runs several kernels ("k_bucket16a+k_bucket16b") sums their bytes
         per = sum(ks[k]["hbm_bytes_per_launch"] / ks[k]["records_per_launch"]
                   for k in kernel.split("+"))
-        return {"bytes_per_record": per, "source": f"profiles/pmc_r02.json:{workload}/{kernel}"}
+        return {"bytes_per_record": per, "source": f"profiles/pmc_r03.json:{workload}/{kernel}"}
     except (OSError, KeyError, ValueError, ZeroDivisionError):
         return None
 
@@ -772,8 +774,10 @@ def main():
         tasks = min(R, 200)
         lo_t = (np.arange(tasks) * R) // tasks
         hi_t = (np.arange(1, tasks + 1) * R) // tasks
-        all_blocks = np.stack([np.repeat(np.arange(maps), tasks), np.tile(lo_t, maps),
-                               np.tile(hi_t, maps)], 1).astype(np.int32)
+        # sux_block_id rows (map, start, end, 0), built once: a reducer keeps its block list
+        all_blocks = np.ascontiguousarray(np.stack(
+            [np.repeat(np.arange(maps), tasks), np.tile(lo_t, maps), np.tile(hi_t, maps),
+             np.zeros(maps * tasks, np.int64)], 1).astype(np.int32))
         resolved = {"blocks": 0, "bytes": 0}
         sid_next = [5000]
 

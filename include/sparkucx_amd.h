@@ -182,7 +182,7 @@ typedef struct sux_tuning {
   int32_t exchange_self;    /* 1: the exchange also moves this rank's own maps' owned ranges
                                through its transport into the receive buffer (loopback; at
                                world 1 it runs the whole RCCL / IPC path on one GPU); 0 or -1: no */
-  int32_t hist_nt;          /* k_hist4 record loads: 1 non-temporal (streaming), -1 or 0 plain   */
+  int32_t hist_nt;          /* k_hist4 record loads: 1 or 0 non-temporal (streaming), -1 plain  */
   int32_t counts_layout;    /* k_hist4 + k_scatter7/8 tile counts: 1 partition-major, 2 (0)
                                tile-major (one contiguous store of a tile's R counters)        */
   int32_t scatter_counters; /* k_scatter8 per-wave rank counters in LDS: 1 partition-major

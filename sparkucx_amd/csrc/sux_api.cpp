@@ -777,7 +777,7 @@ sux::Tuning resolve_tuning(const sux_tuning& t, bool pipelined) {
   r.small_auto = t.small_kernel == 0;
   r.scatter_order = t.scatter_order;
   if (t.small_wgs_per_cu) r.small_wgs_per_cu = t.small_wgs_per_cu;
-  r.hist_nt = t.hist_nt > 0;
+  r.hist_nt = t.hist_nt >= 0;  // 0: non-temporal (round 3 A/B: 1639 vs 1596 GB/s), -1: plain
   r.counts_tm = t.counts_layout != 1;
   if (t.scatter_counters) r.scatter_counters = t.scatter_counters;
   r.lz4_queue = t.lz4_queue != 2;  // the work queue: 46.6 -> 53.0 GB/s (profiles/r03)
@@ -2987,6 +2987,48 @@ BlockLoc resolve(sux_node* node, Shuffle& sh, const sux_block_id& b, const int64
 void gather_device_entries(sux_node* node, Shuffle& sh, const sux_block_id* blocks, int32_t n,
                            std::vector<int64_t>& ae, std::vector<uint8_t>& has) {
   has.assign((size_t)n, 0);
+  // A dense request (a whole stage's reducers: about as many entries per map as the map's table
+  // has) reads the referenced maps' whole tables back instead — fewer bytes than two pointers
+  // and two entries per block — in one copy per run of maps whose tables are adjacent in device
+  // memory (one adopt call's tables are), and keeps them as the maps' host copies, so later
+  // resolves of those maps are host arithmetic.
+  {
+    std::vector<uint8_t> seen((size_t)sh.num_maps, 0);
+    uint64_t entries = 0;
+    for (int i = 0; i < n; ++i) {
+      const sux_block_id& b = blocks[i];
+      if (b.map_index < 0 || b.map_index >= sh.num_maps) continue;
+      const MapSlot& sl = sh.maps[b.map_index];
+      if (!sl.present || !sl.index.empty() || !sl.d_index) continue;
+      seen[(size_t)b.map_index] = 1;
+      entries += 2;
+    }
+    if (!entries) return;
+    std::vector<int32_t> mm;  // the distinct maps, ascending
+    for (int32_t m = 0; m < sh.num_maps; ++m)
+      if (seen[(size_t)m]) mm.push_back(m);
+    const uint64_t row = (uint64_t)sh.R + 1;
+    if (entries >= mm.size() * row) {
+      node->bind();
+      hipStream_t s = node->stream(nullptr);
+      HostLease hp(node->hpool, 8 * row * mm.size());
+      int64_t* h = static_cast<int64_t*>(hp.b.first);
+      for (size_t j = 0; j < mm.size();) {  // one copy per run of adjacent tables
+        size_t k = j + 1;
+        while (k < mm.size() && mm[k] == mm[k - 1] + 1 &&
+               sh.maps[mm[k]].d_index == sh.maps[mm[k - 1]].d_index + row)
+          ++k;
+        hip_check(hipMemcpyAsync(h + j * row, sh.maps[mm[j]].d_index, 8 * row * (k - j),
+                                 hipMemcpyDeviceToHost, s),
+                  "index tables read-back");
+        j = k;
+      }
+      hip_check(hipStreamSynchronize(s), "index tables read-back");
+      for (size_t j = 0; j < mm.size(); ++j)
+        sh.maps[mm[j]].index.assign(h + j * row, h + (j + 1) * row);
+      return;  // every block's map has its host copy now
+    }
+  }
   std::vector<const int64_t*> ptrs;
   std::vector<int32_t> at;
   for (int i = 0; i < n; ++i) {
@@ -3045,7 +3087,35 @@ int sux_resolve_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* b
     std::vector<int64_t> ae;
     std::vector<uint8_t> has;
     gather_device_entries(node, sh, blocks, n, ae, has);
-    for (int i = 0; i < n; ++i) {
+    // the common case first — this rank's own committed, device-resident maps at world 1 (the
+    // zero-copy local read): address and size are two table reads; anything else (a block of
+    // another owner, a received range, a spilled map, a malformed id) takes resolve() below
+    const int R = sh.R;
+    int i0 = 0;
+    if (node->conf.world_size == 1) {
+      for (; i0 < n; ++i0) {
+        const sux_block_id& b = blocks[i0];
+        if (b.map_index < 0 || b.map_index >= sh.num_maps || b.start_reduce < 0 ||
+            b.end_reduce <= b.start_reduce || b.end_reduce > R)
+          break;
+        const MapSlot& sl = sh.maps[b.map_index];
+        if (!sl.present || sl.rslab || !sl.slab || sl.spilled() || sl.owner != node->conf.rank)
+          break;
+        int64_t a, e;
+        if (has[(size_t)i0]) {
+          a = ae[2 * (size_t)i0];
+          e = ae[2 * (size_t)i0 + 1];
+        } else if (!sl.index.empty()) {
+          a = sl.index[b.start_reduce];
+          e = sl.index[b.end_reduce];
+        } else {
+          break;
+        }
+        addrs[i0] = (uint64_t)(uintptr_t)(sl.data() + a);
+        sizes[i0] = e - a;
+      }
+    }
+    for (int i = i0; i < n; ++i) {
       const BlockLoc L = resolve(node, sh, blocks[i], has[i] ? &ae[2 * (size_t)i] : nullptr, false);
       if (L.file)
         raise(SUX_ESTATE, "map " + std::to_string(blocks[i].map_index) +

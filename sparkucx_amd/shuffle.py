@@ -442,43 +442,51 @@ class Node:
         return a.value, b.value
 
     @staticmethod
-    def _blocks(blocks):
-        """sux_block_id array from (map, start[, end]) tuples or an int (n, 2|3) numpy array."""
+    def _blocks(blocks) -> np.ndarray:
+        """sux_block_id rows (map, start, end, 0) as one C-contiguous int32 (n, 4) array, from
+        (map, start[, end]) tuples or an int (n, 2|3|4) numpy array.  An int32 (n, 4) array is
+        used as it is (no copy: a reducer that keeps its block list resolves without converting)."""
         if isinstance(blocks, np.ndarray):
+            if (blocks.dtype == np.int32 and blocks.ndim == 2 and blocks.shape[1] == 4
+                    and blocks.flags.c_contiguous and len(blocks)):
+                return blocks
             b = np.zeros((max(1, len(blocks)), 4), np.int32)
-            b[:len(blocks), :2] = blocks[:, :2]
-            b[:len(blocks), 2] = blocks[:, 2] if blocks.shape[1] > 2 else blocks[:, 1] + 1
-            return (N.BlockId * len(b)).from_buffer_copy(b.tobytes())
+            if len(blocks):
+                b[:len(blocks), :2] = blocks[:, :2]
+                b[:len(blocks), 2] = blocks[:, 2] if blocks.shape[1] > 2 else blocks[:, 1] + 1
+            return b
         if len(blocks) and len({len(b) for b in blocks}) == 1 and len(blocks[0]) in (2, 3):
-            try:  # uniform tuples: one numpy conversion instead of a ctypes object per block
+            try:  # uniform tuples: one numpy conversion
                 return Node._blocks(np.asarray(blocks, dtype=np.int64))
             except (TypeError, ValueError, OverflowError):
                 pass
-        arr = (N.BlockId * max(1, len(blocks)))()
-        for i, b in enumerate(blocks):
-            m, s = b[0], b[1]
-            e = b[2] if len(b) > 2 else s + 1
-            arr[i] = N.BlockId(m, s, e, 0)
-        return arr
+        b = np.zeros((max(1, len(blocks)), 4), np.int32)
+        for i, t in enumerate(blocks):
+            b[i, 0], b[i, 1] = t[0], t[1]
+            b[i, 2] = t[2] if len(t) > 2 else t[1] + 1
+        return b
 
     def fetch_blocks(self, shuffle_id: int, blocks, stream=None):
         """Returns (FetchedBuffer, sizes[list])."""
         arr = self._blocks(blocks)
-        sizes = (C.c_int64 * max(1, len(blocks)))()
+        k = len(blocks)
+        sizes = np.empty(max(1, k), np.int64)
         h = C.c_void_p()
-        N.check(self.lib.sux_fetch_blocks(self.h, shuffle_id, arr, len(blocks), sizes,
-                                          C.byref(h), _stream(stream)), "sux_fetch_blocks")
-        return FetchedBuffer(self, h, len(blocks)), list(sizes)[:len(blocks)]
+        N.check(self.lib.sux_fetch_blocks(self.h, shuffle_id, arr.ctypes.data, k,
+                                          sizes.ctypes.data, C.byref(h), _stream(stream)),
+                "sux_fetch_blocks")
+        return FetchedBuffer(self, h, k), sizes[:k].tolist()
 
     def resolve_blocks(self, shuffle_id: int, blocks):
+        """(device addresses uint64[n], sizes int64[n]) of the blocks (zero-copy)."""
         arr = self._blocks(blocks)
-        addrs = (C.c_uint64 * max(1, len(blocks)))()
-        sizes = (C.c_int64 * max(1, len(blocks)))()
-        N.check(self.lib.sux_resolve_blocks(self.h, shuffle_id, arr, len(blocks), addrs, sizes),
-                "sux_resolve_blocks")
         k = len(blocks)
-        return (np.frombuffer(addrs, np.uint64)[:k].copy(),
-                np.frombuffer(sizes, np.int64)[:k].copy())
+        addrs = np.empty(max(1, k), np.uint64)
+        sizes = np.empty(max(1, k), np.int64)
+        N.check(self.lib.sux_resolve_blocks(self.h, shuffle_id, arr.ctypes.data, k,
+                                            addrs.ctypes.data, sizes.ctypes.data),
+                "sux_resolve_blocks")
+        return addrs[:k], sizes[:k]
 
     # ---- measurement -------------------------------------------------------------------------
     def sort_records(self, records: torch.Tensor, record_size: int, key_kind: int,

@@ -166,7 +166,6 @@ def test_block_lists_convert_the_same_by_every_path(blocks):
 
     arr = Node._blocks(blocks)
     want = [(int(b[0]), int(b[1]), int(b[2]) if len(b) > 2 else int(b[1]) + 1, 0) for b in blocks]
-    got = [(a.map_index, a.start_reduce, a.end_reduce, a.reserved)
-           for a in arr][:len(want)] if want else []
+    got = [tuple(int(x) for x in row) for row in arr][:len(want)] if want else []
     assert got == want
     assert len(arr) == max(1, len(want))

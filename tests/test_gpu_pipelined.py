@@ -154,6 +154,9 @@ TUNINGS = [
     {"scatter_kernel": 1, "hist_kernel": 1},
     {"hist_kernel": 3},
     {"tile_records": 1024},
+    {"hist_nt": -1},                                     # plain K1 loads (non-temporal: default)
+    {"counts_layout": 1},                                # partition-major tile counts
+    {"scatter_counters": 1},                             # partition-major k_scatter8 counters
 ]
 
 
