@@ -1,0 +1,607 @@
+// jni_harness.cpp — drives the JNI binding (src/main/native/sux_jni.c, compiled unchanged against
+// the test double tests/jni/jni.h) through an in-process fake JVM, on one GPU, the way the JVM
+// plugin classes call it (SuxNative.java): node -> partitioner -> registerShuffle ->
+// writeMapOutputs (GpuShuffleWriter) -> waitMapOutputs -> mapOutputIndex (the index file) ->
+// fetchBlocks + bufferRead (UcxShuffleClient / DeviceManagedBuffer) -> sortRecords (the reader's
+// key sort) -> bootstrap all-gather through a Java callback (GpuNode's control plane) ->
+// exchange -> indexFileCommit -> unregister / destroy.  Every byte is compared with the CPU
+// oracle (oracle/oracle.c, test infrastructure); every failed call must surface as a pending
+// SuxException carrying the C-ABI status, as a JVM caller would see it.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstddef>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <numeric>
+#include <string>
+#include <unistd.h>
+#include <vector>
+
+#include "../../include/sparkucx_amd.h"
+#include "../../oracle/oracle.h"
+#include "jni.h"
+
+// ---- the fake JVM --------------------------------------------------------------------------
+struct _jobject {
+  enum Kind { kClass, kString, kBytes, kInts, kLongs, kDirect, kThrowable, kBootstrap } kind;
+  std::string name;             // class name / string value
+  std::vector<jbyte> b;         // byte[]
+  std::vector<jint> i;          // int[]
+  std::vector<jlong> l;         // long[]
+  void* addr = nullptr;         // direct ByteBuffer
+  jlong cap = 0;
+  jint code = 0;                // SuxException code
+  std::string msg;              // exception message
+  int boot_calls = 0;           // Bootstrap: allGather invocations
+  int boot_mode = 0;            // 0: world x bytes back (world 1: the input); 1: a short reply
+};
+struct _jmethodID {
+  std::string name, sig;
+};
+
+static std::vector<std::unique_ptr<_jobject>> heap;  // every object lives to the end
+static std::vector<std::unique_ptr<_jmethodID>> methods;
+static jobject pending = nullptr;  // the pending exception
+static JNIEnv g_env;
+static JavaVM g_vm;
+
+static jobject alloc(_jobject::Kind k) {
+  heap.emplace_back(new _jobject());
+  heap.back()->kind = k;
+  return heap.back().get();
+}
+
+extern "C" {
+static jclass FindClass(JNIEnv*, const char* name) {
+  jobject c = alloc(_jobject::kClass);
+  c->name = name;
+  return c;
+}
+static jint Throw(JNIEnv*, jthrowable t) {
+  pending = t;
+  return 0;
+}
+static jint ThrowNew(JNIEnv*, jclass c, const char* msg) {
+  jobject t = alloc(_jobject::kThrowable);
+  t->name = c ? c->name : "?";
+  t->msg = msg ? msg : "";
+  pending = t;
+  return 0;
+}
+static jboolean ExceptionCheck(JNIEnv*) { return pending ? JNI_TRUE : JNI_FALSE; }
+static void ExceptionClear(JNIEnv*) { pending = nullptr; }
+static jobject NewGlobalRef(JNIEnv*, jobject o) { return o; }
+static void DeleteGlobalRef(JNIEnv*, jobject) {}
+static jobject NewObject(JNIEnv*, jclass c, jmethodID m, ...) {
+  jobject t = alloc(_jobject::kThrowable);
+  t->name = c->name;
+  va_list ap;
+  va_start(ap, m);
+  if (m->sig == "(ILjava/lang/String;)V") {  // SuxException(int code, String message)
+    t->code = va_arg(ap, jint);
+    jstring s = va_arg(ap, jstring);
+    t->msg = s ? s->name : "";
+  }
+  va_end(ap);
+  return t;
+}
+static jclass GetObjectClass(JNIEnv*, jobject o) {
+  jobject c = alloc(_jobject::kClass);
+  c->name = o->kind == _jobject::kBootstrap ? "org/apache/spark/shuffle/ucx/gpu/Bootstrap" : "?";
+  return c;
+}
+static jmethodID GetMethodID(JNIEnv*, jclass, const char* name, const char* sig) {
+  methods.emplace_back(new _jmethodID{name, sig});
+  return methods.back().get();
+}
+static jobject CallObjectMethod(JNIEnv*, jobject o, jmethodID m, ...) {
+  va_list ap;
+  va_start(ap, m);
+  jobject r = nullptr;
+  if (o->kind == _jobject::kBootstrap && m->name == "allGather" && m->sig == "(J[B)[B") {
+    (void)va_arg(ap, jlong);  // tag
+    jbyteArray in = va_arg(ap, jbyteArray);
+    o->boot_calls++;
+    r = alloc(_jobject::kBytes);
+    r->b = in->b;  // world 1: every rank's contribution = this one
+    if (o->boot_mode == 1 && !r->b.empty()) r->b.pop_back();
+  }
+  va_end(ap);
+  return r;
+}
+static jstring NewStringUTF(JNIEnv*, const char* s) {
+  jobject o = alloc(_jobject::kString);
+  o->name = s;
+  return o;
+}
+static const char* GetStringUTFChars(JNIEnv*, jstring s, jboolean* c) {
+  if (c) *c = JNI_FALSE;
+  return s->name.c_str();
+}
+static void ReleaseStringUTFChars(JNIEnv*, jstring, const char*) {}
+static jsize GetArrayLength(JNIEnv*, jarray a) {
+  return a->kind == _jobject::kBytes ? (jsize)a->b.size()
+         : a->kind == _jobject::kInts ? (jsize)a->i.size()
+                                      : (jsize)a->l.size();
+}
+static jbyteArray NewByteArray(JNIEnv*, jsize n) {
+  jobject o = alloc(_jobject::kBytes);
+  o->b.assign((size_t)n, 0);
+  return o;
+}
+static jintArray NewIntArray(JNIEnv*, jsize n) {
+  jobject o = alloc(_jobject::kInts);
+  o->i.assign((size_t)n, 0);
+  return o;
+}
+static jlongArray NewLongArray(JNIEnv*, jsize n) {
+  jobject o = alloc(_jobject::kLongs);
+  o->l.assign((size_t)n, 0);
+  return o;
+}
+static jbyte* GetByteArrayElements(JNIEnv*, jbyteArray a, jboolean* c) {
+  if (c) *c = JNI_FALSE;
+  return a->b.data();
+}
+static jint* GetIntArrayElements(JNIEnv*, jintArray a, jboolean* c) {
+  if (c) *c = JNI_FALSE;
+  return a->i.data();
+}
+static jlong* GetLongArrayElements(JNIEnv*, jlongArray a, jboolean* c) {
+  if (c) *c = JNI_FALSE;
+  return a->l.data();
+}
+static void ReleaseByteArrayElements(JNIEnv*, jbyteArray, jbyte*, jint) {}
+static void ReleaseIntArrayElements(JNIEnv*, jintArray, jint*, jint) {}
+static void ReleaseLongArrayElements(JNIEnv*, jlongArray, jlong*, jint) {}
+static void GetByteArrayRegion(JNIEnv*, jbyteArray a, jsize s, jsize n, jbyte* buf) {
+  std::memcpy(buf, a->b.data() + s, (size_t)n);
+}
+static void GetIntArrayRegion(JNIEnv*, jintArray a, jsize s, jsize n, jint* buf) {
+  std::memcpy(buf, a->i.data() + s, 4 * (size_t)n);
+}
+static void SetByteArrayRegion(JNIEnv*, jbyteArray a, jsize s, jsize n, const jbyte* buf) {
+  std::memcpy(a->b.data() + s, buf, (size_t)n);
+}
+static void SetIntArrayRegion(JNIEnv*, jintArray a, jsize s, jsize n, const jint* buf) {
+  std::memcpy(a->i.data() + s, buf, 4 * (size_t)n);
+}
+static void SetLongArrayRegion(JNIEnv*, jlongArray a, jsize s, jsize n, const jlong* buf) {
+  std::memcpy(a->l.data() + s, buf, 8 * (size_t)n);
+}
+static jint GetJavaVM(JNIEnv*, JavaVM** vm) {
+  *vm = &g_vm;
+  return JNI_OK;
+}
+static void* GetDirectBufferAddress(JNIEnv*, jobject b) {
+  return b && b->kind == _jobject::kDirect ? b->addr : nullptr;
+}
+static jlong GetDirectBufferCapacity(JNIEnv*, jobject b) {
+  return b && b->kind == _jobject::kDirect ? b->cap : -1;
+}
+static jint AttachCurrentThread(JavaVM*, void** penv, void*) {
+  *penv = &g_env;
+  return JNI_OK;
+}
+static jint DetachCurrentThread(JavaVM*) { return JNI_OK; }
+static jint GetEnv(JavaVM*, void** penv, jint) {
+  *penv = &g_env;
+  return JNI_OK;
+}
+}  // extern "C"
+
+static const JNINativeInterface_ g_fns = {
+    FindClass, Throw, ThrowNew, ExceptionCheck, ExceptionClear, NewGlobalRef, DeleteGlobalRef,
+    NewObject, GetObjectClass, GetMethodID, CallObjectMethod, NewStringUTF, GetStringUTFChars,
+    ReleaseStringUTFChars, GetArrayLength, NewByteArray, NewIntArray, NewLongArray,
+    GetByteArrayElements, GetIntArrayElements, GetLongArrayElements, ReleaseByteArrayElements,
+    ReleaseIntArrayElements, ReleaseLongArrayElements, GetByteArrayRegion, GetIntArrayRegion,
+    SetByteArrayRegion, SetIntArrayRegion, SetLongArrayRegion, GetJavaVM, GetDirectBufferAddress,
+    GetDirectBufferCapacity};
+static const JNIInvokeInterface_ g_inv = {AttachCurrentThread, DetachCurrentThread, GetEnv};
+
+// ---- the binding's native methods (SuxNative.java) -----------------------------------------
+#define FN(name) Java_org_apache_spark_shuffle_ucx_gpu_SuxNative_##name
+extern "C" {
+jint FN(abiVersion)(JNIEnv*, jclass);
+jlong FN(nodeCreate)(JNIEnv*, jclass, jint, jint, jint, jbyteArray, jlong, jlong, jlong, jstring,
+                     jint, jboolean);
+void FN(nodeDestroy)(JNIEnv*, jclass, jlong);
+jlong FN(setBootstrap)(JNIEnv*, jclass, jlong, jobject, jint);
+void FN(releaseBootstrap)(JNIEnv*, jclass, jlong);
+jlongArray FN(poolStats)(JNIEnv*, jclass, jlong);
+jbyteArray FN(commUniqueId)(JNIEnv*, jclass);
+void FN(setSpillDir)(JNIEnv*, jclass, jlong, jstring);
+jlong FN(spills)(JNIEnv*, jclass, jlong);
+void FN(commitMapOutput)(JNIEnv*, jclass, jlong, jint, jint, jobject, jlong, jlongArray, jlong);
+void FN(exchangeMaps)(JNIEnv*, jclass, jlong, jint, jint, jint, jlong);
+void FN(exchangeWait)(JNIEnv*, jclass, jlong, jint);
+void FN(setTuning)(JNIEnv*, jclass, jlong, jintArray);
+jintArray FN(getTuning)(JNIEnv*, jclass, jlong);
+void FN(nodeCheck)(JNIEnv*, jclass, jlong);
+jlong FN(streamCreate)(JNIEnv*, jclass, jlong);
+void FN(streamDestroy)(JNIEnv*, jclass, jlong, jlong);
+jlong FN(partitionerCreate)(JNIEnv*, jclass, jlong, jint, jint, jint, jint, jint, jboolean,
+                            jbyteArray);
+void FN(partitionerDestroy)(JNIEnv*, jclass, jlong);
+jlong FN(registerShuffle)(JNIEnv*, jclass, jlong, jint, jint, jint, jint);
+void FN(unregisterShuffle)(JNIEnv*, jclass, jlong, jint);
+void FN(writeMapOutputHost)(JNIEnv*, jclass, jlong, jint, jint, jlong, jobject, jlong, jint, jlong);
+void FN(writeMapOutputs)(JNIEnv*, jclass, jlong, jint, jint, jlong, jlong, jlong, jlong, jlong);
+void FN(waitMapOutputs)(JNIEnv*, jclass, jlong, jint);
+jbyteArray FN(mapOutputIndex)(JNIEnv*, jclass, jlong, jint, jint, jint);
+void FN(exchange)(JNIEnv*, jclass, jlong, jint, jlong);
+jintArray FN(ownedPartitions)(JNIEnv*, jclass, jlong, jint, jint);
+jlong FN(fetchBlocks)(JNIEnv*, jclass, jlong, jint, jintArray, jlongArray, jlong);
+jlong FN(sortRecords)(JNIEnv*, jclass, jlong, jint, jlong, jlong, jint, jint, jint, jlong);
+jlong FN(bufferDevicePtr)(JNIEnv*, jclass, jlong);
+void FN(bufferRead)(JNIEnv*, jclass, jlong, jlong, jobject, jlong, jlong);
+void FN(bufferRetain)(JNIEnv*, jclass, jlong, jint);
+void FN(bufferRelease)(JNIEnv*, jclass, jlong);
+jboolean FN(indexFileCommit)(JNIEnv*, jclass, jstring, jstring, jstring, jlongArray, jlongArray);
+}
+
+static int failures = 0;
+#define EXPECT(cond, ...)                                               \
+  do {                                                                  \
+    if (!(cond)) {                                                      \
+      ++failures;                                                       \
+      fprintf(stderr, "FAIL %s:%d: %s  ", __FILE__, __LINE__, #cond);   \
+      fprintf(stderr, __VA_ARGS__);                                     \
+      fprintf(stderr, "\n");                                            \
+    }                                                                   \
+  } while (0)
+
+// a call that must not throw
+#define OK_CALL(expr)                                                                     \
+  do {                                                                                    \
+    expr;                                                                                 \
+    if (pending) {                                                                        \
+      fprintf(stderr, "FAIL %s:%d: %s threw %s: %s\n", __FILE__, __LINE__, #expr,         \
+              pending->name.c_str(), pending->msg.c_str());                               \
+      exit(1);                                                                            \
+    }                                                                                     \
+  } while (0)
+
+// a call that must leave a SuxException with `code` pending (then cleared)
+static void expect_sux(int code, const char* what, int line) {
+  if (!pending) {
+    ++failures;
+    fprintf(stderr, "FAIL line %d: %s did not throw\n", line, what);
+    return;
+  }
+  const bool ok = pending->name == "org/apache/spark/shuffle/ucx/gpu/SuxException" &&
+                  pending->code == code && !pending->msg.empty();
+  if (!ok) {
+    ++failures;
+    fprintf(stderr, "FAIL line %d: %s threw %s code %d (%s), want SuxException %d\n", line, what,
+            pending->name.c_str(), pending->code, pending->msg.c_str(), code);
+  }
+  pending = nullptr;
+}
+#define THROWS(code, expr) \
+  do {                     \
+    expr;                  \
+    expect_sux(code, #expr, __LINE__); \
+  } while (0)
+
+static jbyteArray bytes_of(const void* p, size_t n) {
+  jobject o = alloc(_jobject::kBytes);
+  o->b.assign((const jbyte*)p, (const jbyte*)p + n);
+  return o;
+}
+static jintArray ints_of(const std::vector<jint>& v) {
+  jobject o = alloc(_jobject::kInts);
+  o->i = v;
+  return o;
+}
+static jlongArray longs_of(const std::vector<jlong>& v) {
+  jobject o = alloc(_jobject::kLongs);
+  o->l = v;
+  return o;
+}
+static jobject direct_buffer(std::vector<uint8_t>& host) {
+  jobject o = alloc(_jobject::kDirect);
+  o->addr = host.data();
+  o->cap = (jlong)host.size();
+  return o;
+}
+
+int main() {
+  g_env = &g_fns;
+  g_vm = &g_inv;
+  JNIEnv* env = &g_env;
+  jclass cls = FindClass(env, "org/apache/spark/shuffle/ucx/gpu/SuxNative");
+
+  EXPECT(FN(abiVersion)(env, cls) == sux_abi_version(), "abiVersion");
+
+  // a bad RCCL id length is an IllegalArgument-like SuxException before anything is created
+  THROWS(SUX_EINVAL, FN(nodeCreate)(env, cls, 0, 0, 1, NewByteArray(env, 5), 1024, 4 << 20, 300,
+                                    nullptr, 0, JNI_FALSE));
+  jlong node = 0;
+  OK_CALL(node = FN(nodeCreate)(env, cls, 0, 0, 1, nullptr, 1024, 4 << 20, 300,
+                                NewStringUTF(env, "1m:4"), 0, JNI_FALSE));
+  EXPECT(node != 0, "nodeCreate");
+  jlongArray ps = nullptr;
+  OK_CALL(ps = FN(poolStats)(env, cls, node));
+  EXPECT(ps && ps->l.size() == 4 && ps->l[3] >= 1, "preAllocateBuffers 1m:4 -> %ld preallocs",
+         ps ? (long)ps->l[3] : -1L);
+
+  jbyteArray uid = nullptr;
+  OK_CALL(uid = FN(commUniqueId)(env, cls));
+  EXPECT(uid && uid->b.size() == 128, "RCCL unique id is 128 bytes");
+  char spill_tmpl[] = "/tmp/sux_jni_spill_XXXXXX";
+  const char* spill_dir = mkdtemp(spill_tmpl);
+  OK_CALL(FN(setSpillDir)(env, cls, node, NewStringUTF(env, spill_dir ? spill_dir : "/tmp")));
+  jlong nsp = -1;
+  OK_CALL(nsp = FN(spills)(env, cls, node));
+  EXPECT(nsp == 0, "no spills yet: %ld", (long)nsp);
+
+  // tuning table round trip (fields in the header's order); a bad value is rejected
+  {
+    jintArray t0 = nullptr;
+    OK_CALL(t0 = FN(getTuning)(env, cls, node));
+    std::vector<jint> f = t0->i;
+    const size_t k_tile = offsetof(sux_tuning, tile_records) / 4;
+    f[k_tile] = 2048;
+    OK_CALL(FN(setTuning)(env, cls, node, ints_of(f)));
+    jintArray t1 = nullptr;
+    OK_CALL(t1 = FN(getTuning)(env, cls, node));
+    EXPECT(t1->i[k_tile] == 2048, "tile_records round trip: %d", t1->i[k_tile]);
+    f[k_tile] = 3000;  // not a power of two
+    THROWS(SUX_EINVAL, FN(setTuning)(env, cls, node, ints_of(f)));
+    f[k_tile] = 0;
+    OK_CALL(FN(setTuning)(env, cls, node, ints_of(f)));
+  }
+
+  // the dependency's partitioner: TeraSort range bounds over 10-byte keys
+  const int R = 40, S = 100, M = 5, rpm = 4000;
+  const int n = M * rpm - 1234;  // a ragged last map
+  std::vector<uint8_t> bounds((R - 1) * 10);
+  o_range_bounds_uniform(R, 10, bounds.data());
+  o_part opart{SUX_PART_RANGE_BYTES, R, 0, 10, 42, 1, bounds.data()};
+  THROWS(SUX_EINVAL, FN(partitionerCreate)(env, cls, node, SUX_PART_RANGE_BYTES, R, 0, 13, 42,
+                                           JNI_TRUE, bytes_of(bounds.data(), bounds.size())));
+  jlong part = 0;
+  OK_CALL(part = FN(partitionerCreate)(env, cls, node, SUX_PART_RANGE_BYTES, R, 0, 10, 42,
+                                       JNI_TRUE, bytes_of(bounds.data(), bounds.size())));
+  jlong stream = 0;
+  OK_CALL(stream = FN(streamCreate)(env, cls, node));
+
+  // records resident on the device (GpuShuffleWriter's batch)
+  std::vector<uint8_t> recs((size_t)n * S);
+  o_gen_terasort(77, 0, (uint64_t)n, recs.data());
+  void* drec = nullptr;
+  if (hipMalloc(&drec, recs.size()) != hipSuccess ||
+      hipMemcpy(drec, recs.data(), recs.size(), hipMemcpyHostToDevice) != hipSuccess) {
+    fprintf(stderr, "hip setup failed\n");
+    return 2;
+  }
+
+  const int sid = 3;
+  jlong dir = 0;
+  OK_CALL(dir = FN(registerShuffle)(env, cls, node, sid, M, R, S));
+  EXPECT(dir == (jlong)M * 300, "directory bytes %ld", (long)dir);
+  THROWS(SUX_ESTATE, FN(registerShuffle)(env, cls, node, sid, M, R, S));  // registered twice
+  OK_CALL(FN(writeMapOutputs)(env, cls, node, sid, 0, part, (jlong)(intptr_t)drec, rpm, n, stream));
+  OK_CALL(FN(waitMapOutputs)(env, cls, node, sid));
+  OK_CALL(FN(nodeCheck)(env, cls, node));
+
+  // the oracle's map outputs
+  std::vector<std::vector<uint8_t>> wdata(M), wbe(M);
+  std::vector<std::vector<int64_t>> widx(M);
+  for (int m = 0; m < M; ++m) {
+    const int cnt = std::min(rpm, n - m * rpm);
+    wdata[m].resize((size_t)cnt * S);
+    widx[m].resize(R + 1);
+    wbe[m].resize(8 * (R + 1));
+    std::vector<int64_t> len(R);
+    o_write_map(&opart, recs.data() + (size_t)m * rpm * S, (uint64_t)cnt, S, wdata[m].data(),
+                len.data(), widx[m].data(), wbe[m].data());
+  }
+  // the index file bytes (IndexShuffleBlockResolver's big-endian longs)
+  for (int m = 0; m < M; ++m) {
+    jbyteArray ix = nullptr;
+    OK_CALL(ix = FN(mapOutputIndex)(env, cls, node, sid, m, R));
+    EXPECT(ix && ix->b.size() == wbe[m].size() &&
+               std::memcmp(ix->b.data(), wbe[m].data(), wbe[m].size()) == 0,
+           "index file of map %d", m);
+  }
+  THROWS(SUX_EINVAL, FN(mapOutputIndex)(env, cls, node, sid, M + 3, R));
+
+  // reducers: partition p of every map into one pooled buffer, read through a direct buffer
+  auto reduce_want = [&](int lo, int hi) {
+    std::vector<uint8_t> w;
+    for (int m = 0; m < M; ++m)
+      w.insert(w.end(), wdata[m].begin() + widx[m][lo], wdata[m].begin() + widx[m][hi]);
+    return w;
+  };
+  for (int p : {0, 7, R - 1}) {
+    std::vector<jint> tri;
+    for (int m = 0; m < M; ++m) tri.insert(tri.end(), {m, p, p + 1});
+    jlongArray sizes = NewLongArray(env, M);
+    jlong buf = 0;
+    OK_CALL(buf = FN(fetchBlocks)(env, cls, node, sid, ints_of(tri), sizes, stream));
+    const std::vector<uint8_t> want = reduce_want(p, p + 1);
+    jlong tot = 0;
+    for (int m = 0; m < M; ++m) {
+      EXPECT(sizes->l[m] == widx[m][p + 1] - widx[m][p], "size of block (%d, %d)", m, p);
+      tot += sizes->l[m];
+    }
+    EXPECT(tot == (jlong)want.size(), "fetched %ld bytes, want %zu", (long)tot, want.size());
+    std::vector<uint8_t> host(want.size() + 16, 0xEE);
+    if (!want.empty()) {
+      OK_CALL(FN(bufferRead)(env, cls, buf, 0, direct_buffer(host), (jlong)want.size(), stream));
+      EXPECT(std::memcmp(host.data(), want.data(), want.size()) == 0, "partition %d bytes", p);
+      // a heap buffer (not direct) or a short one is an IllegalArgumentException
+      std::vector<uint8_t> small(4);
+      FN(bufferRead)(env, cls, buf, 0, direct_buffer(small), (jlong)want.size(), stream);
+      EXPECT(pending && pending->name == "java/lang/IllegalArgumentException", "short buffer");
+      pending = nullptr;
+    }
+    // the reader's key sort on the GPU: stable by the 10-byte key
+    const jlong nrec = tot / S;
+    jlong sorted = 0;
+    OK_CALL(sorted = FN(sortRecords)(env, cls, node, SUX_SORT_BYTES, buf, nrec, S, 0, 10, stream));
+    std::vector<size_t> ord((size_t)nrec);
+    std::iota(ord.begin(), ord.end(), 0);
+    std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) {
+      return std::memcmp(&want[a * S], &want[b * S], 10) < 0;
+    });
+    std::vector<uint8_t> swant((size_t)tot);
+    for (size_t k = 0; k < ord.size(); ++k)
+      std::memcpy(&swant[k * S], &want[ord[k] * S], S);
+    std::vector<uint8_t> sh((size_t)tot + 1);
+    if (tot) OK_CALL(FN(bufferRead)(env, cls, sorted, 0, direct_buffer(sh), tot, stream));
+    EXPECT(std::memcmp(sh.data(), swant.data(), (size_t)tot) == 0, "sorted partition %d", p);
+    THROWS(SUX_EINVAL, FN(sortRecords)(env, cls, node, SUX_SORT_BYTES, buf, nrec + 1, S, 0, 10,
+                                       stream));
+    OK_CALL(FN(bufferRelease)(env, cls, sorted));
+    // one reference per block slice (OnBlocksFetchCallback): release them all
+    OK_CALL(FN(bufferRetain)(env, cls, buf, 1));
+    for (int m = 0; m < M + 1; ++m) OK_CALL(FN(bufferRelease)(env, cls, buf));
+  }
+  // a ShuffleBlockBatchId range and malformed / unknown requests
+  {
+    std::vector<jint> tri = {1, 3, 9, 4, 0, R};
+    jlongArray sizes = NewLongArray(env, 2);
+    jlong buf = 0;
+    OK_CALL(buf = FN(fetchBlocks)(env, cls, node, sid, ints_of(tri), sizes, stream));
+    EXPECT(sizes->l[0] == widx[1][9] - widx[1][3] && sizes->l[1] == widx[4][R], "batch sizes");
+    for (int k = 0; k < 2; ++k) OK_CALL(FN(bufferRelease)(env, cls, buf));
+    THROWS(SUX_EINVAL, FN(fetchBlocks)(env, cls, node, sid, ints_of({0, 1, 2, 3}),
+                                       NewLongArray(env, 2), stream));  // not triples
+    THROWS(SUX_ENOENT, FN(fetchBlocks)(env, cls, node, sid + 100, ints_of({0, 1, 2}),
+                                       NewLongArray(env, 1), stream));  // unknown shuffle
+  }
+  // the other writers: a host batch partitioned on the GPU (writeMapOutputHost) and a map output
+  // Spark's own writer produced (commitMapOutput = writeIndexFileAndCommit with its lengths)
+  {
+    const int sidh = 6;
+    OK_CALL(FN(registerShuffle)(env, cls, node, sidh, 2, R, S));
+    std::vector<uint8_t> h0(recs.begin(), recs.begin() + (size_t)rpm * S);
+    OK_CALL(FN(writeMapOutputHost)(env, cls, node, sidh, 0, part, direct_buffer(h0), rpm, S,
+                                   stream));
+    std::vector<uint8_t> d1 = wdata[1];
+    std::vector<jlong> len1(R);
+    for (int p = 0; p < R; ++p) len1[p] = widx[1][p + 1] - widx[1][p];
+    OK_CALL(FN(commitMapOutput)(env, cls, node, sidh, 1, direct_buffer(d1), (jlong)d1.size(),
+                                longs_of(len1), stream));
+    THROWS(SUX_EINVAL, FN(commitMapOutput)(env, cls, node, sidh, 2, direct_buffer(d1),
+                                           (jlong)d1.size(), longs_of(len1), stream));
+    OK_CALL(FN(waitMapOutputs)(env, cls, node, sidh));
+    jlongArray sizes = NewLongArray(env, 2);
+    jlong buf = 0;
+    OK_CALL(buf = FN(fetchBlocks)(env, cls, node, sidh, ints_of({0, 0, R, 1, 0, R}), sizes, stream));
+    jlong dp = 0;
+    OK_CALL(dp = FN(bufferDevicePtr)(env, cls, buf));
+    EXPECT(dp != 0, "bufferDevicePtr");
+    std::vector<uint8_t> want = wdata[0];
+    want.insert(want.end(), wdata[1].begin(), wdata[1].end());
+    std::vector<uint8_t> host(want.size());
+    OK_CALL(FN(bufferRead)(env, cls, buf, 0, direct_buffer(host), (jlong)want.size(), stream));
+    EXPECT(host == want, "host-written and committed map outputs");
+    for (int k = 0; k < 2; ++k) OK_CALL(FN(bufferRelease)(env, cls, buf));
+    OK_CALL(FN(unregisterShuffle)(env, cls, node, sidh));
+  }
+  jintArray own = nullptr;
+  OK_CALL(own = FN(ownedPartitions)(env, cls, node, sid, 0));
+  EXPECT(own && own->i[0] == 0 && own->i[1] == R, "world 1 owns [0, R)");
+
+  // GpuNode's control plane: the bootstrap all-gather calls back into a Java object.  With the
+  // exchange looping this rank's maps through the transport (tuning exchange_self = 1), the
+  // exchange of world 1 all-gathers the directory through it.
+  {
+    jobject boot = alloc(_jobject::kBootstrap);
+    jlong ctx = 0;
+    OK_CALL(ctx = FN(setBootstrap)(env, cls, node, boot, 1));
+    jintArray t0 = nullptr;
+    OK_CALL(t0 = FN(getTuning)(env, cls, node));
+    std::vector<jint> f = t0->i;
+    f[offsetof(sux_tuning, exchange_self) / 4] = 1;
+    OK_CALL(FN(setTuning)(env, cls, node, ints_of(f)));
+    const int sid2 = 4;
+    OK_CALL(FN(registerShuffle)(env, cls, node, sid2, M, R, S));
+    OK_CALL(FN(writeMapOutputs)(env, cls, node, sid2, 0, part, (jlong)(intptr_t)drec, rpm, n,
+                                stream));
+    // the reader's windows: two asynchronous exchanges, then their completion
+    OK_CALL(FN(exchangeMaps)(env, cls, node, sid2, 0, 2, stream));
+    OK_CALL(FN(exchangeMaps)(env, cls, node, sid2, 2, M - 2, stream));
+    OK_CALL(FN(exchangeWait)(env, cls, node, sid2));
+    EXPECT(boot->boot_calls > 0, "the exchange all-gathered through the Java bootstrap");
+    std::vector<jint> tri;
+    for (int m = 0; m < M; ++m) tri.insert(tri.end(), {m, 0, R});
+    jlongArray sizes = NewLongArray(env, M);
+    jlong buf = 0;
+    OK_CALL(buf = FN(fetchBlocks)(env, cls, node, sid2, ints_of(tri), sizes, stream));
+    const std::vector<uint8_t> want = reduce_want(0, R);
+    std::vector<uint8_t> host(want.size());
+    OK_CALL(FN(bufferRead)(env, cls, buf, 0, direct_buffer(host), (jlong)want.size(), stream));
+    EXPECT(host == want, "every block after the looped-back exchange");
+    for (int m = 0; m < M; ++m) OK_CALL(FN(bufferRelease)(env, cls, buf));
+    OK_CALL(FN(unregisterShuffle)(env, cls, node, sid2));
+    // a reply of the wrong size (a desynchronised round) fails the exchange, never overflows
+    boot->boot_mode = 1;
+    const int sid3 = 5;
+    OK_CALL(FN(registerShuffle)(env, cls, node, sid3, M, R, S));
+    OK_CALL(FN(writeMapOutputs)(env, cls, node, sid3, 0, part, (jlong)(intptr_t)drec, rpm, n,
+                                stream));
+    THROWS(SUX_ECOMM, FN(exchange)(env, cls, node, sid3, stream));
+    OK_CALL(FN(unregisterShuffle)(env, cls, node, sid3));
+    f[offsetof(sux_tuning, exchange_self) / 4] = 0;
+    OK_CALL(FN(setTuning)(env, cls, node, ints_of(f)));
+    // (the bootstrap context is released after the node, as GpuNode.close does)
+    OK_CALL(FN(unregisterShuffle)(env, cls, node, sid));
+    THROWS(SUX_ENOENT, FN(unregisterShuffle)(env, cls, node, sid));
+    OK_CALL(FN(partitionerDestroy)(env, cls, part));
+    OK_CALL(FN(streamDestroy)(env, cls, node, stream));
+    OK_CALL(FN(nodeDestroy)(env, cls, node));
+    FN(releaseBootstrap)(env, cls, ctx);
+  }
+
+  // Spark's index file commit (writeIndexFileAndCommit) on a temp directory
+  {
+    char tmpl[] = "/tmp/sux_jni_XXXXXX";
+    const char* d = mkdtemp(tmpl);
+    EXPECT(d != nullptr, "mkdtemp");
+    if (d) {
+      const std::string ip = std::string(d) + "/shuffle_0_0_0.index";
+      const std::string dp = std::string(d) + "/shuffle_0_0_0.data";
+      const std::string tp = dp + ".tmp";
+      std::vector<jlong> lens = {10, 0, 30};
+      FILE* f = fopen(tp.c_str(), "wb");
+      std::vector<uint8_t> body(40, 7);
+      fwrite(body.data(), 1, body.size(), f);
+      fclose(f);
+      jlongArray out = NewLongArray(env, 3);
+      jboolean reused = JNI_TRUE;
+      OK_CALL(reused = FN(indexFileCommit)(env, cls, NewStringUTF(env, ip.c_str()),
+                                           NewStringUTF(env, dp.c_str()),
+                                           NewStringUTF(env, tp.c_str()), longs_of(lens), out));
+      EXPECT(reused == JNI_FALSE && access(dp.c_str(), F_OK) == 0 && access(ip.c_str(), F_OK) == 0,
+             "first commit renames the temp data and writes the index");
+      std::vector<uint8_t> be(32), want(32);
+      int64_t idx[4];
+      std::vector<int64_t> l64(lens.begin(), lens.end());
+      o_index_from_lengths(l64.data(), 3, idx, want.data());
+      f = fopen(ip.c_str(), "rb");
+      const size_t got = f ? fread(be.data(), 1, be.size(), f) : 0;
+      if (f) fclose(f);
+      EXPECT(got == 32 && be == want, "index file bytes");
+      unlink(ip.c_str());
+      unlink(dp.c_str());
+      rmdir(d);
+    }
+  }
+
+  if (failures) {
+    fprintf(stderr, "%d failure(s)\n", failures);
+    return 1;
+  }
+  printf("jni harness ok: every native method of SuxNative driven through sux_jni.c\n");
+  return 0;
+}

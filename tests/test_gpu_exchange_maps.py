@@ -153,6 +153,45 @@ def test_adopt_map_outputs_resolves_in_place(gpu_node):
         gpu_node.unregister_shuffle(11)
 
 
+def test_adopt_resolve_sparse_dense_and_errors(gpu_node):
+    """Resolve paths of adopted (device-indexed) map outputs: a sparse request gathers just its
+    entries on the device; a dense one reads the maps' whole tables back once (then host
+    copies); mixed maps (some with host copies, some not) and a malformed block in the middle
+    (the whole call fails, nothing half-written is trusted)."""
+    R, rpm, n = 300, 20000, 7 * 20000 + 999
+    opart, part = _terasort(gpu_node, R)
+    recs = gpu_node.generate(N.GEN_TERASORT, SEED + 5, 0, n, 100)
+    out, index, _ = gpu_node.partition_maps(part, recs, 100, rpm)
+    M = -(-n // rpm)
+    ix = index.cpu().numpy().reshape(M, R + 1)
+    base = out.data_ptr()
+
+    def check(blocks):
+        addrs, sizes = gpu_node.resolve_blocks(21, blocks)
+        for i, b in enumerate(blocks):
+            m, a = int(b[0]), int(b[1])
+            e = int(b[2]) if len(b) > 2 else a + 1
+            assert addrs[i] == base + m * rpm * 100 + ix[m, a], (m, a, e)
+            assert sizes[i] == ix[m, e] - ix[m, a], (m, a, e)
+
+    gpu_node.register_shuffle(21, M, R, 100)
+    try:
+        gpu_node.adopt_map_outputs(21, 0, out, rpm, n, index)
+        check([(m, (37 * m) % R) for m in range(M)])          # sparse: device entry gather
+        with pytest.raises(N.SuxError) as e:                  # malformed block in the middle
+            gpu_node.resolve_blocks(21, [(0, 1), (2, R - 1, R + 1), (3, 4)])
+        assert e.value.code == N.SUX_EINVAL
+        check([(m, 0, R) for m in range(0, M, 2)])            # sparse ranges
+        dense = np.stack([np.repeat(np.arange(0, M, 2), R),   # dense over the even maps: their
+                          np.tile(np.arange(R), (M + 1) // 2)], 1)  # tables come back whole
+        check(dense)
+        mixed = [(m, p, min(R, p + 7)) for m in range(M) for p in (0, 150, 299)]
+        check(mixed)                                          # host copies + device entries
+        check(np.stack([np.repeat(np.arange(M), R), np.tile(np.arange(R), M)], 1))
+    finally:
+        gpu_node.unregister_shuffle(21)
+
+
 def test_spill_when_the_pool_is_full(tmp_path):
     """pool capped at 64 MiB, 12 map outputs of 8 MB: the writer spills committed outputs to
     Spark's files and every block still fetches byte-exact."""

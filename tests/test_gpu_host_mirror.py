@@ -29,3 +29,17 @@ def test_cpp_host_mirror():
     assert os.path.exists(BIN), "build it first: make -C tests/cpp"
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+JNI = os.path.join(ROOT, "tests", "jni", "jni_harness")
+
+
+def test_jni_binding_through_a_fake_jvm():
+    """src/main/native/sux_jni.c, compiled unchanged against the JNI test double (tests/jni/jni.h),
+    driven like SuxNative.java's callers: write -> index file -> fetch -> sort -> bootstrap
+    all-gather through a Java callback -> exchange -> file commit; bytes vs the oracle, every
+    failure a pending SuxException with the C-ABI status (tests/jni/jni_harness.cpp)."""
+    assert os.path.exists(JNI), "build it first: make -C tests/jni"
+    r = subprocess.run([JNI], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "jni harness ok" in r.stdout

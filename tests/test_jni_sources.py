@@ -85,3 +85,14 @@ def test_constants_match_header(java_name, define):
     h = re.search(rf"#define {define} (-?\d+)", _read(HEADER))
     j = re.search(rf"\b{java_name} = (-?\d+)", _read(JAVA))
     assert h and j and int(h.group(1)) == int(j.group(1)), (java_name, define)
+
+
+def test_jni_binding_compiles_warning_free():
+    """sux_jni.c compiles with -Wall -Wextra -Werror against the JNI test double (no JDK here):
+    every JNI call it makes names a JNI function with the specification's signature."""
+    import subprocess
+    src = os.path.join(ROOT, "src", "main", "native", "sux_jni.c")
+    r = subprocess.run(["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", "-fsyntax-only",
+                        "-I", os.path.join(ROOT, "tests", "jni"), src],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-3000:]
