@@ -17,9 +17,9 @@ def test_traffic_lookup_is_keyed_by_workload_and_kernel():
     assert bench.load_traffic("terasort", "k_no_such_kernel") is None
     assert bench.load_traffic("no_such_workload", "k_scatter8") is None
     # a slot running two kernels sums them
-    a = bench.load_traffic("small", "k_hist16")["bytes_per_record"]
-    b = bench.load_traffic("small", "k_scatter16s")["bytes_per_record"]
-    ab = bench.load_traffic("small", "k_hist16+k_scatter16s")["bytes_per_record"]
+    a = bench.load_traffic("small", "k_msd16a")["bytes_per_record"]
+    b = bench.load_traffic("small", "k_msd16b")["bytes_per_record"]
+    ab = bench.load_traffic("small", "k_msd16a+k_msd16b")["bytes_per_record"]
     assert ab == pytest.approx(a + b)
 
 
