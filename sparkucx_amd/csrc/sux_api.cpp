@@ -2984,51 +2984,51 @@ BlockLoc resolve(sux_node* node, Shuffle& sh, const sux_block_id& b, const int64
 // The (start, end) index entries of every block whose map keeps its index table on the device
 // (adopted outputs), gathered in one device pass: ae[2i], ae[2i+1]; has[i] = 1 for those blocks.
 // Called with the node lock held (no pool spill from here: the device buffer is a plain get).
+// A dense request (a whole stage's reducers: about as many entries per map as the map's table
+// has) reads the referenced maps' whole tables back — fewer bytes than two pointers and two
+// entries per block — in one copy per run of maps whose tables are adjacent in device memory (one
+// adopt call's tables are), and keeps them as the maps' host copies, so later resolves of those
+// maps are host arithmetic.  Returns true when every referenced map has its host copy afterwards.
+bool dense_index_readback(sux_node* node, Shuffle& sh, const sux_block_id* blocks, int32_t n) {
+  std::vector<uint8_t> seen((size_t)sh.num_maps, 0);
+  uint64_t entries = 0;
+  for (int i = 0; i < n; ++i) {
+    const sux_block_id& b = blocks[i];
+    if (b.map_index < 0 || b.map_index >= sh.num_maps) continue;
+    const MapSlot& sl = sh.maps[b.map_index];
+    if (!sl.present || !sl.index.empty() || !sl.d_index) continue;
+    seen[(size_t)b.map_index] = 1;
+    entries += 2;
+  }
+  if (!entries) return true;
+  std::vector<int32_t> mm;  // the distinct maps, ascending
+  for (int32_t m = 0; m < sh.num_maps; ++m)
+    if (seen[(size_t)m]) mm.push_back(m);
+  const uint64_t row = (uint64_t)sh.R + 1;
+  if (entries < mm.size() * row) return false;
+  node->bind();
+  hipStream_t s = node->stream(nullptr);
+  HostLease hp(node->hpool, 8 * row * mm.size());
+  int64_t* h = static_cast<int64_t*>(hp.b.first);
+  for (size_t j = 0; j < mm.size();) {  // one copy per run of adjacent tables
+    size_t k = j + 1;
+    while (k < mm.size() && mm[k] == mm[k - 1] + 1 &&
+           sh.maps[mm[k]].d_index == sh.maps[mm[k - 1]].d_index + row)
+      ++k;
+    hip_check(hipMemcpyAsync(h + j * row, sh.maps[mm[j]].d_index, 8 * row * (k - j),
+                             hipMemcpyDeviceToHost, s),
+              "index tables read-back");
+    j = k;
+  }
+  hip_check(hipStreamSynchronize(s), "index tables read-back");
+  for (size_t j = 0; j < mm.size(); ++j) sh.maps[mm[j]].index.assign(h + j * row, h + (j + 1) * row);
+  return true;
+}
+
 void gather_device_entries(sux_node* node, Shuffle& sh, const sux_block_id* blocks, int32_t n,
                            std::vector<int64_t>& ae, std::vector<uint8_t>& has) {
   has.assign((size_t)n, 0);
-  // A dense request (a whole stage's reducers: about as many entries per map as the map's table
-  // has) reads the referenced maps' whole tables back instead — fewer bytes than two pointers
-  // and two entries per block — in one copy per run of maps whose tables are adjacent in device
-  // memory (one adopt call's tables are), and keeps them as the maps' host copies, so later
-  // resolves of those maps are host arithmetic.
-  {
-    std::vector<uint8_t> seen((size_t)sh.num_maps, 0);
-    uint64_t entries = 0;
-    for (int i = 0; i < n; ++i) {
-      const sux_block_id& b = blocks[i];
-      if (b.map_index < 0 || b.map_index >= sh.num_maps) continue;
-      const MapSlot& sl = sh.maps[b.map_index];
-      if (!sl.present || !sl.index.empty() || !sl.d_index) continue;
-      seen[(size_t)b.map_index] = 1;
-      entries += 2;
-    }
-    if (!entries) return;
-    std::vector<int32_t> mm;  // the distinct maps, ascending
-    for (int32_t m = 0; m < sh.num_maps; ++m)
-      if (seen[(size_t)m]) mm.push_back(m);
-    const uint64_t row = (uint64_t)sh.R + 1;
-    if (entries >= mm.size() * row) {
-      node->bind();
-      hipStream_t s = node->stream(nullptr);
-      HostLease hp(node->hpool, 8 * row * mm.size());
-      int64_t* h = static_cast<int64_t*>(hp.b.first);
-      for (size_t j = 0; j < mm.size();) {  // one copy per run of adjacent tables
-        size_t k = j + 1;
-        while (k < mm.size() && mm[k] == mm[k - 1] + 1 &&
-               sh.maps[mm[k]].d_index == sh.maps[mm[k - 1]].d_index + row)
-          ++k;
-        hip_check(hipMemcpyAsync(h + j * row, sh.maps[mm[j]].d_index, 8 * row * (k - j),
-                                 hipMemcpyDeviceToHost, s),
-                  "index tables read-back");
-        j = k;
-      }
-      hip_check(hipStreamSynchronize(s), "index tables read-back");
-      for (size_t j = 0; j < mm.size(); ++j)
-        sh.maps[mm[j]].index.assign(h + j * row, h + (j + 1) * row);
-      return;  // every block's map has its host copy now
-    }
-  }
+  if (dense_index_readback(node, sh, blocks, n)) return;  // every block's map has its host copy
   std::vector<const int64_t*> ptrs;
   std::vector<int32_t> at;
   for (int i = 0; i < n; ++i) {
@@ -3084,13 +3084,65 @@ int sux_resolve_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* b
     std::unique_lock<std::mutex> lk(node->mu);
     Shuffle& sh = node->shuffle(shuffle_id);
     drain(node, sh, lk);
+    const int R = sh.R;
+    if (node->conf.world_size == 1 && n > 0 && !dense_index_readback(node, sh, blocks, n)) {
+      // a sparse request over maps whose index tables live on the device: the whole resolve
+      // runs there (block ids up, addresses and sizes down, no per-block host work); blocks the
+      // kernel cannot place (another owner's range, a received or spilled map, a malformed id)
+      // come back with size -1 and are resolved on the host below, which reports their errors
+      std::vector<sux::ResolveMap> tab((size_t)sh.num_maps, sux::ResolveMap{nullptr, 0});
+      for (int32_t m = 0; m < sh.num_maps; ++m) {
+        const MapSlot& sl = sh.maps[m];
+        if (sl.present && sl.d_index && sl.slab && !sl.rslab && !sl.spilled() &&
+            sl.owner == node->conf.rank)
+          tab[m] = sux::ResolveMap{sl.d_index, (uint64_t)(uintptr_t)sl.data()};
+      }
+      node->bind();
+      hipStream_t s = node->stream(nullptr);
+      auto up = [](uint64_t v) { return (v + 255) / 256 * 256; };
+      const uint64_t bb = up(16ull * n), tb = up(sizeof(sux::ResolveMap) * tab.size()),
+                     ab = up(8ull * n);
+      PoolBuf dev = node->pool->get(bb + tb + 2 * ab);
+      try {
+        hip_check(hipMemcpyAsync(dev.ptr, blocks, 16ull * n, hipMemcpyHostToDevice, s),
+                  "H2D block ids");
+        hip_check(hipMemcpyAsync(dev.ptr + bb, tab.data(), sizeof(sux::ResolveMap) * tab.size(),
+                                 hipMemcpyHostToDevice, s),
+                  "H2D map table");
+        hip_check(sux::launch_resolve_blocks(
+                      dev.ptr, (uint32_t)n, reinterpret_cast<const sux::ResolveMap*>(dev.ptr + bb),
+                      sh.num_maps, R, reinterpret_cast<uint64_t*>(dev.ptr + bb + tb),
+                      reinterpret_cast<int64_t*>(dev.ptr + bb + tb + ab), s),
+                  "resolve blocks");
+        hip_check(hipMemcpyAsync(addrs, dev.ptr + bb + tb, 8ull * n, hipMemcpyDeviceToHost, s),
+                  "D2H addresses");
+        hip_check(hipMemcpyAsync(sizes, dev.ptr + bb + tb + ab, 8ull * n, hipMemcpyDeviceToHost, s),
+                  "D2H sizes");
+        hip_check(hipStreamSynchronize(s), "resolve blocks");
+      } catch (...) {
+        (void)hipStreamSynchronize(s);
+        node->pool->put(dev);
+        throw;
+      }
+      node->pool->put(dev);
+      for (int i = 0; i < n; ++i) {
+        if (sizes[i] >= 0) continue;
+        const BlockLoc L = resolve(node, sh, blocks[i], nullptr, false);
+        if (L.file)
+          raise(SUX_ESTATE, "map " + std::to_string(blocks[i].map_index) +
+                                " was spilled to " + *L.file + ": fetch its blocks");
+        addrs[i] = L.addr;
+        sizes[i] = L.size;
+      }
+      return;
+    }
     std::vector<int64_t> ae;
     std::vector<uint8_t> has;
     gather_device_entries(node, sh, blocks, n, ae, has);
-    // the common case first — this rank's own committed, device-resident maps at world 1 (the
-    // zero-copy local read): address and size are two table reads; anything else (a block of
-    // another owner, a received range, a spilled map, a malformed id) takes resolve() below
-    const int R = sh.R;
+    // the common case first — this rank's own committed maps at world 1 with host copies of
+    // their index tables (the zero-copy local read): address and size are two table reads;
+    // anything else (a block of another owner, a received range, a spilled map, a malformed id)
+    // takes resolve() below
     int i0 = 0;
     if (node->conf.world_size == 1) {
       for (; i0 < n; ++i0) {

@@ -163,6 +163,43 @@ hipError_t launch_gather_i64(const int64_t* const* d_ptrs, uint32_t n, int64_t* 
   return hipGetLastError();
 }
 
+// Zero-copy resolve of world-1 local blocks on the device (sux_resolve_blocks): block i =
+// {map, start, end, 0} -> addrs[i] = data base of the map + index[start], sizes[i] = index[end] -
+// index[start], from the per-map table {index table, data base} (index = nullptr: the map is not
+// resolvable here).  A malformed id or such a map gets sizes[i] = -1 and is resolved again on the
+// host, which raises the reference's error for it.
+__global__ __launch_bounds__(256) void k_resolve_blocks(const int4* __restrict__ blocks, uint32_t n,
+                                                        const ResolveMap* __restrict__ maps,
+                                                        int32_t num_maps, int32_t R,
+                                                        uint64_t* __restrict__ addrs,
+                                                        int64_t* __restrict__ sizes) {
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int4 b = blocks[i];
+    uint64_t a = 0;
+    int64_t sz = -1;
+    if (b.x >= 0 && b.x < num_maps && b.y >= 0 && b.z > b.y && b.z <= R) {
+      const ResolveMap mp = maps[b.x];
+      if (mp.index) {
+        const int64_t lo = mp.index[b.y], hi = mp.index[b.z];
+        a = mp.base + (uint64_t)lo;
+        sz = hi - lo;
+      }
+    }
+    addrs[i] = a;
+    sizes[i] = sz;
+  }
+}
+
+hipError_t launch_resolve_blocks(const void* d_blocks, uint32_t n, const ResolveMap* d_maps,
+                                 int32_t num_maps, int32_t R, uint64_t* d_addrs, int64_t* d_sizes,
+                                 hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint32_t g = (n + 255) / 256;
+  hipLaunchKernelGGL(k_resolve_blocks, dim3(g < 4096 ? g : 4096), dim3(256), 0, s,
+                     static_cast<const int4*>(d_blocks), n, d_maps, num_maps, R, d_addrs, d_sizes);
+  return hipGetLastError();
+}
+
 hipError_t launch_pull(int32_t W, int32_t me, const uint64_t* srcs, const int64_t* gi, int32_t M,
                        int32_t R, uint8_t* recv, uint64_t cap, uint64_t* recv_bytes,
                        hipStream_t s) {

@@ -195,6 +195,15 @@ hipError_t launch_gather_copy(const CopyDesc* d_desc, uint32_t n, uint32_t chunk
                               const uint32_t* d_chunk_first, Timer* timer, hipStream_t s);
 
 // out[i] = *ptrs[i] (device pointers to int64 index entries; sux_copy.hip).
+// one map of a device resolve: its index table (nullptr: not resolvable on the device) and the
+// device address of its data file
+struct ResolveMap {
+  const int64_t* index;
+  uint64_t base;
+};
+hipError_t launch_resolve_blocks(const void* d_blocks, uint32_t n, const ResolveMap* d_maps,
+                                 int32_t num_maps, int32_t R, uint64_t* d_addrs, int64_t* d_sizes,
+                                 hipStream_t s);
 hipError_t launch_gather_i64(const int64_t* const* d_ptrs, uint32_t n, int64_t* d_out,
                              hipStream_t s);
 

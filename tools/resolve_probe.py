@@ -87,3 +87,4 @@ def main(maps=954, rpm=1024, R=200, rs=100):
 if __name__ == "__main__":
     main()
     main(maps=1024, rpm=1024, R=10000, rs=16)
+    main(maps=16384, rpm=64, R=10000, rs=16)
