@@ -443,26 +443,47 @@ def plugin_leg_multi(node, part, data, rs: int, R: int, rpm: int, gm: int, group
     ShuffleBlockBatchId per map) and checks them on the device: partition ids (k_pids) inside
     its range, non-decreasing per map, run lengths = the map's index file, and the word multiset
     of all ranks' fetched bytes = the inputs'."""
-    sid = 7000
     M = groups * world * gm
-    node.register_shuffle(sid, M, R, rs)
     stream = torch.cuda.current_stream(dev)
-    torch.cuda.synchronize(dev)
-    dist.barrier()
-    t0 = time.perf_counter()
-    for g in range(groups):
-        r0 = g * gm * rpm
-        node.write_map_outputs(sid, (g * world + rank) * gm, part, data[r0 * rs:(r0 + gm * rpm) * rs],
-                               rpm, gm * rpm, stream=stream)
-        if g:
-            node.exchange_maps(sid, (g - 1) * world * gm, world * gm, stream=xstream)
-    node.exchange_maps(sid, (groups - 1) * world * gm, world * gm, stream=xstream)
-    node.exchange_wait(sid)
-    torch.cuda.synchronize(dev)
-    dt = time.perf_counter() - t0
-    tt = torch.tensor([dt], dtype=torch.float64, device=ctl)
-    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    dt = float(tt.item())
+
+    def max_over_ranks(v):
+        tt = torch.tensor([v], dtype=torch.float64, device=ctl)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt.item())
+
+    def run(sid, overlap):
+        """(seconds to the exchange's completion, seconds to the last write's completion) of
+        one shuffle; overlap=False exchanges only after every write completed (the reference's
+        order: the reduce stage starts after the map stage)"""
+        node.register_shuffle(sid, M, R, rs)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for g in range(groups):
+            r0 = g * gm * rpm
+            node.write_map_outputs(sid, (g * world + rank) * gm, part,
+                                   data[r0 * rs:(r0 + gm * rpm) * rs], rpm, gm * rpm, stream=stream)
+            if overlap and g:
+                node.exchange_maps(sid, (g - 1) * world * gm, world * gm, stream=xstream)
+        tw = None
+        if not overlap:
+            node.wait_map_outputs(sid)
+            torch.cuda.synchronize(dev)
+            tw = time.perf_counter() - t0
+            for g in range(groups - 1):
+                node.exchange_maps(sid, g * world * gm, world * gm, stream=xstream)
+        node.exchange_maps(sid, (groups - 1) * world * gm, world * gm, stream=xstream)
+        node.exchange_wait(sid)
+        torch.cuda.synchronize(dev)
+        return time.perf_counter() - t0, tw
+
+    # an untimed first pass fills the device pool (the slabs' first allocations), then the
+    # timed shuffle; after its check, the map stage and the exchange once more, serially: how
+    # long each takes alone
+    run(7001, False)
+    node.unregister_shuffle(7001)
+    sid = 7000
+    dt = max_over_ranks(run(sid, True)[0])
     # ---- untimed device check of everything this rank now serves
     lo, hi = node.owned_partitions(sid)
     sums = torch.zeros(4, dtype=torch.int64, device=dev)
@@ -498,12 +519,15 @@ def plugin_leg_multi(node, part, data, rs: int, R: int, rpm: int, gm: int, group
                 ix = np.frombuffer(node.map_output_index(sid, m, R), dtype=">i8").astype(np.int64)
                 want.append((ix[lo + 1:hi + 1] - ix[lo:hi]) // rs)
             want = torch.from_numpy(np.concatenate(want)).to(dev)
-            ok = bool(((pid >= lo) & (pid < hi)).all()) and \
-                bool(((pid[1:] >= pid[:-1]) | (seg[1:] != seg[:-1])).all()) and \
-                torch.equal(runs, want)
-            if not ok:
+            inr = bool(((pid >= lo) & (pid < hi)).all())
+            rise = bool(((pid[1:] >= pid[:-1]) | (seg[1:] != seg[:-1])).all())
+            eq = torch.equal(runs, want)
+            if not (inr and rise and eq):
                 raise RuntimeError(f"plugin leg: rank {rank} maps {ms[0]}..{ms[-1]} fetched "
-                                   "blocks are not this rank's partitions as indexed")
+                                   "blocks are not this rank's partitions as indexed (in range "
+                                   f"{inr}, grouped {rise}, runs = index {eq}; pids "
+                                   f"{int(pid.min())}..{int(pid.max())} for [{lo}, {hi}); "
+                                   f"{size} B fetched)")
             sums[2:] += wsum(t)
     tot = sums.to(ctl)
     dist.all_reduce(tot)
@@ -511,9 +535,15 @@ def plugin_leg_multi(node, part, data, rs: int, R: int, rpm: int, gm: int, group
     if tot[0] != tot[2] or tot[1] != tot[3]:
         raise RuntimeError("plugin leg: fetched words differ from the inputs' over all ranks")
     node.unregister_shuffle(sid)
+    ts, tw = run(7002, False)
+    ts, tw = max_over_ranks(ts), max_over_ranks(tw)
+    node.unregister_shuffle(7002)
     n_all = world * groups * gm * rpm
+    tx = max(ts - tw, 1e-9)  # the exchange alone, after the map stage
     return {"maps": M, "records": n_all, "bytes": n_all * rs, "ms": round(dt * 1e3, 3),
             "GB/s": round(n_all * rs / dt / 1e9, 1), "fetched_bytes_rank": fetched,
+            "serial_ms": {"writes": round(tw * 1e3, 3), "then_exchange": round(tx * 1e3, 3)},
+            "exchange_hidden": round(min(1.0, max(0.0, (ts - dt) / tx)), 3),
             "self_check": "ok",
             "path": f"register -> write_map_outputs x{groups} per rank ({gm} maps each) with "
                     f"sux_exchange_maps of the previous window on a second stream -> "
@@ -1105,7 +1135,19 @@ def main():
             "remote_bytes_per_rank": remote // args.steps, "exchange_ms": round(xms, 2)}
     if pipelined and world > 1 and args.plugin_groups != 0:
         # the stateless pipeline's rings go back first: the plugin leg's slabs and receive
-        # buffers take their HBM
+        # buffers take their HBM.  Every rank first unmaps its peers' send buffers and all
+        # ranks agree on it before any buffer is freed: a freed allocation's address comes back
+        # for the next one, and an importer still holding the old mapping of that address would
+        # be handed the stale memory when it opens the new allocation's handle
+        if args.transport == "ipc":
+            torch.cuda.synchronize(dev)
+            for tab in srcs:
+                for g, ptr in enumerate(tab.tolist()):
+                    if g != rank:
+                        node.ipc_close(ptr)
+            srcs.clear()
+            torch.cuda.synchronize(dev)
+            dist.barrier()
         send.clear()
         recv.clear()
         ws.clear()

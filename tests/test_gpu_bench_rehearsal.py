@@ -42,6 +42,9 @@ def test_bench_two_ranks_one_gpu():
     # windowed sux_exchange_maps -> wait -> fetch) passed its own device check
     assert res["self_check"]["ok"] and res["self_check"]["groups"] == 6
     assert res["plugin"]["self_check"] == "ok" and res["plugin"]["maps"] == 5 * 2 * 2
+    # the same shuffle also ran map stage first, exchange after: both phases were timed
+    assert res["plugin"]["serial_ms"]["writes"] > 0 and res["plugin"]["serial_ms"]["then_exchange"] > 0
+    assert 0.0 <= res["plugin"]["exchange_hidden"] <= 1.0
 
 
 @pytest.mark.parametrize("workload", ["terasort", "zipf"])
@@ -56,3 +59,13 @@ def test_bench_eight_ranks_verified(workload):
     assert ex["remote_bytes_per_rank"] > 0
     assert res["self_check"]["ok"] and res["self_check"]["groups"] == 3
     assert res["plugin"]["self_check"] == "ok" and res["plugin"]["maps"] == 2 * 8 * 2
+
+
+def test_bench_eight_ranks_plugin_leg_after_the_pipeline():
+    """100 MB batches at W = 8: the plugin leg runs after the stateless pipeline freed its IPC-
+    shared send buffers, whose addresses come back for the plugin's slabs.  Each rank unmaps
+    its peers' buffers (and all agree) before any is freed; a stale mapping handed out for a
+    reused address used to feed the exchange the old bytes (its device check failed)."""
+    res = _run(8, "--records", "4194304", "--map-records", "524288", "--group-maps", "2",
+               "--plugin-groups", "4", "--steps", "1", "--warmup", "0", "--self-check", "0")
+    assert res["plugin"]["self_check"] == "ok" and res["plugin"]["maps"] == 4 * 8 * 2
