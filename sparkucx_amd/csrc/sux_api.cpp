@@ -450,7 +450,11 @@ struct sux_node {
   std::mutex mu;
   std::condition_variable cv;  // a write job was published (Shuffle::jobs/busy/submitting moved)
   std::map<int32_t, std::unique_ptr<Shuffle>> shuffles;
-  std::map<void*, void*> ipc_bases;  // opened peer pointer -> mapped allocation base
+  std::map<void*, std::pair<void*, std::string>> ipc_bases;  // sux_ipc_open: pointer -> (base, handle)
+  // every peer allocation this process has mapped (the exchange, the serve path, sux_ipc_open):
+  // mapped base -> (64-byte handle, references taken) — see ipc_open_fresh
+  std::mutex ipc_mu;
+  std::map<void*, std::pair<std::string, int>> ipc_maps;
   sux_allgather_fn boot = nullptr;   // host all-gather of the embedding runtime
   void* boot_ctx = nullptr;
   sux_tuning tuning{};               // all zero = measured defaults (resolve_tuning)
@@ -730,11 +734,51 @@ void drain(sux_node* node, Shuffle& sh, std::unique_lock<std::mutex>& lk) {
   }
 }
 
+// Map a peer allocation by its 64-byte IPC handle.  The HIP runtime keys the mappings it hands
+// out by the exporter's address: when a peer frees an allocation this process still maps and its
+// allocator gives the address to a new allocation, opening the NEW handle returns the old mapping
+// — the freed memory, not the new bytes (tests/test_gpu_ipc_reuse.py).  A returned base this
+// process already holds under another handle is that stale mapping: every reference to it is
+// dropped (its allocation is gone; whoever still held it held freed memory) and the handle is
+// opened again.
+void* ipc_open_fresh(sux_node* node, const uint8_t* handle) {
+  std::lock_guard<std::mutex> lk(node->ipc_mu);
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, 64);
+  const std::string key(reinterpret_cast<const char*>(handle), 64);
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    void* base = nullptr;
+    hip_check(hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    auto it = node->ipc_maps.find(base);
+    if (it == node->ipc_maps.end()) {
+      node->ipc_maps[base] = {key, 1};
+      return base;
+    }
+    if (it->second.first == key) {
+      it->second.second++;
+      return base;
+    }
+    (void)hipIpcCloseMemHandle(base);  // the reference just taken
+    for (int r = 0; r < it->second.second; ++r) (void)hipIpcCloseMemHandle(base);
+    node->ipc_maps.erase(it);
+  }
+  raise(SUX_EHIP, "hipIpcOpenMemHandle keeps returning the mapping of a freed allocation");
+  return nullptr;
+}
+
+// Drop one reference taken by ipc_open_fresh (none if the mapping was already dropped as stale).
+void ipc_close_ref(sux_node* node, void* base, const std::string& key) {
+  std::lock_guard<std::mutex> lk(node->ipc_mu);
+  auto it = node->ipc_maps.find(base);
+  if (it == node->ipc_maps.end() || it->second.first != key) return;
+  (void)hipIpcCloseMemHandle(base);
+  if (--it->second.second == 0) node->ipc_maps.erase(it);
+}
+
 // Everything a shuffle holds on the device: slabs and receive buffers (via the slots), IPC
 // mappings, spill files.
 void release_shuffle(sux_node* node, Shuffle& sh) {
-  (void)node;
-  for (auto& kv : sh.ipc_bases) (void)hipIpcCloseMemHandle(kv.second);
+  for (auto& kv : sh.ipc_bases) ipc_close_ref(node, kv.second, kv.first);
   sh.ipc_bases.clear();
   for (auto& m : sh.maps) {
     m.slab.reset();
@@ -781,6 +825,7 @@ sux::Tuning resolve_tuning(const sux_tuning& t, bool pipelined) {
   r.counts_tm = t.counts_layout != 1;
   if (t.scatter_counters) r.scatter_counters = t.scatter_counters;
   r.lz4_queue = t.lz4_queue != 2;  // the work queue: 46.6 -> 53.0 GB/s (profiles/r03)
+  r.scatter_nt = t.scatter_nt > 0 ? t.scatter_nt : 0;
   return r;
 }
 
@@ -1045,6 +1090,7 @@ int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
     require(in(t->counts_layout, {1, 2}), SUX_EINVAL, "counts_layout must be 1 or 2");
     require(in(t->scatter_counters, {1, 2}), SUX_EINVAL, "scatter_counters must be 1 or 2");
     require(in(t->lz4_queue, {1, 2}), SUX_EINVAL, "lz4_queue must be 1 or 2");
+    require(t->scatter_nt >= -1 && t->scatter_nt <= 3, SUX_EINVAL, "scatter_nt must be -1 .. 3");
     for (int32_t r : t->reserved) require(r == 0, SUX_EINVAL, "reserved tuning fields must be 0");
     require(node, SUX_EINVAL, "NULL node");
     std::lock_guard<std::mutex> lk(node->mu);
@@ -1099,7 +1145,8 @@ int sux_node_destroy(sux_node* node) {
     if (node->d_err) (void)hipFree(node->d_err);
     for (auto& kv : node->shuffles) release_shuffle(node, *kv.second);
     node->shuffles.clear();
-    for (auto& kv : node->ipc_bases) (void)hipIpcCloseMemHandle(kv.second);
+    for (auto& kv : node->ipc_bases) ipc_close_ref(node, kv.second.first, kv.second.second);
+    node->ipc_bases.clear();
     if (node->comm) (void)ncclCommDestroy(node->comm);
     (void)hipGetLastError();  // see nccl_check
     delete node;
@@ -1914,15 +1961,14 @@ int sux_ipc_open(sux_node* node, const uint8_t desc[SUX_IPC_DESC_BYTES], void** 
   return guard([&] {
     require(node && desc && d_ptr, SUX_EINVAL, "NULL argument");
     node->bind();
-    hipIpcMemHandle_t h;
     uint64_t off;
-    std::memcpy(&h, desc, 64);
     std::memcpy(&off, desc + 64, 8);
-    void* base = nullptr;
-    hip_check(hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    void* base = ipc_open_fresh(node, desc);
     *d_ptr = static_cast<uint8_t*>(base) + off;
     std::lock_guard<std::mutex> lk(node->mu);
-    node->ipc_bases[*d_ptr] = base;
+    auto& slot = node->ipc_bases[*d_ptr];
+    if (slot.first) ipc_close_ref(node, slot.first, slot.second);  // opened twice: one reference
+    slot = {base, std::string(reinterpret_cast<const char*>(desc), 64)};
   });
 }
 
@@ -1930,15 +1976,15 @@ int sux_ipc_close(sux_node* node, void* d_ptr) {
   return guard([&] {
     require(node && d_ptr, SUX_EINVAL, "NULL argument");
     node->bind();
-    void* base = nullptr;
+    std::pair<void*, std::string> m;
     {
       std::lock_guard<std::mutex> lk(node->mu);
       auto it = node->ipc_bases.find(d_ptr);
       require(it != node->ipc_bases.end(), SUX_ENOENT, "pointer was not opened by sux_ipc_open");
-      base = it->second;
+      m = it->second;
       node->ipc_bases.erase(it);
     }
-    hip_check(hipIpcCloseMemHandle(base), "hipIpcCloseMemHandle");
+    ipc_close_ref(node, m.first, m.second);
   });
 }
 
@@ -2754,12 +2800,12 @@ int sux_exchange_maps(sux_node* node, int32_t shuffle_id, int32_t first, int32_t
                 if (f != ib.end()) base = f->second;
               }
               if (!base) {
-                hipIpcMemHandle_t h;
-                std::memcpy(&h, all[pe].ipc, 64);
-                hip_check(hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess),
-                          "hipIpcOpenMemHandle");
+                base = ipc_open_fresh(node, all[pe].ipc);
                 std::lock_guard<std::mutex> lk(node->mu);
-                node->shuffle(shuffle_id).ipc_bases[key] = base;
+                void*& slot = node->shuffle(shuffle_id).ipc_bases[key];
+                if (slot) ipc_close_ref(node, base, key);  // another thread mapped it meanwhile
+                else slot = base;
+                base = slot;
               }
               uint64_t off;
               std::memcpy(&off, all[pe].ipc + 64, 8);
@@ -2968,11 +3014,13 @@ BlockLoc resolve(sux_node* node, Shuffle& sh, const sux_block_id& b, const int64
   if (sv.first < 0) raise(SUX_ENOENT, "block " + name() + " has no serving rank");
   const std::string& desc = sh.serve_desc[sv.first];
   const std::string key = desc.substr(0, 64);  // the allocation's handle (see the pull path)
-  void*& base = sh.ipc_bases[key];
-  if (!base) {
-    hipIpcMemHandle_t hd;
-    std::memcpy(&hd, desc.data(), 64);
-    hip_check(hipIpcOpenMemHandle(&base, hd, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+  void* base = nullptr;
+  auto f = sh.ipc_bases.find(key);
+  if (f != sh.ipc_bases.end()) {
+    base = f->second;
+  } else {
+    base = ipc_open_fresh(node, reinterpret_cast<const uint8_t*>(desc.data()));
+    sh.ipc_bases[key] = base;
   }
   uint64_t doff;
   std::memcpy(&doff, desc.data() + 64, 8);

@@ -25,7 +25,9 @@ def _run(world, *args, timeout=300):
            os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--rehearse-one-gpu", *args]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout,
                        env=dict(os.environ, OMP_NUM_THREADS="1"))
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    if r.returncode != 0:  # the ranks' own exceptions first (the launcher's summary is long)
+        errs = [l for l in r.stderr.splitlines() if "Error" in l and "amdgpu.ids" not in l]
+        raise AssertionError("\n".join(errs[:20]) + "\n" + r.stderr[-2000:])
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     return json.loads(lines[0])
