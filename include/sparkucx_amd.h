@@ -189,7 +189,11 @@ typedef struct sux_tuning {
                                [R][waves] (round 2), 2 (0) wave-major [waves][R]               */
   int32_t lz4_queue;        /* LZ4 compressor chunk deal: 1 (0) a device work queue (one atomic
                                per chunk), 2 the fixed grid-stride deal                        */
-  int32_t reserved[5];
+  int32_t scatter_nt;       /* k_scatter8 non-temporal accesses: 1 loads, 2 stores, 3 both,
+                               -1 or 0 none                                                    */
+  int32_t gather_kernel;    /* sort's record gather: 1 (0) 16-byte units, L lanes per record;
+                               2 one dword per lane                                            */
+  int32_t reserved[3];
 } sux_tuning;
 int sux_node_set_tuning(sux_node* node, const sux_tuning* tuning);
 /* Waits for the device, then reports (and clears) failures the kernels recorded in the node's

@@ -826,6 +826,7 @@ sux::Tuning resolve_tuning(const sux_tuning& t, bool pipelined) {
   if (t.scatter_counters) r.scatter_counters = t.scatter_counters;
   r.lz4_queue = t.lz4_queue != 2;  // the work queue: 46.6 -> 53.0 GB/s (profiles/r03)
   r.scatter_nt = t.scatter_nt > 0 ? t.scatter_nt : 0;
+  r.gather16 = t.gather_kernel != 2;
   return r;
 }
 
@@ -1091,6 +1092,7 @@ int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
     require(in(t->scatter_counters, {1, 2}), SUX_EINVAL, "scatter_counters must be 1 or 2");
     require(in(t->lz4_queue, {1, 2}), SUX_EINVAL, "lz4_queue must be 1 or 2");
     require(t->scatter_nt >= -1 && t->scatter_nt <= 3, SUX_EINVAL, "scatter_nt must be -1 .. 3");
+    require(in(t->gather_kernel, {1, 2}), SUX_EINVAL, "gather_kernel must be 1 or 2");
     for (int32_t r : t->reserved) require(r == 0, SUX_EINVAL, "reserved tuning fields must be 0");
     require(node, SUX_EINVAL, "NULL node");
     std::lock_guard<std::mutex> lk(node->mu);
@@ -3581,7 +3583,7 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
                 "sort unpair");
     else
       hip_check(sux::launch_gather_records_sel(d_in, a, b, &plan->final_b, n, record_size, d_out,
-                                               s),
+                                               s, resolve_tuning(node->tuning, false).gather16),
                 "sort gather");
     return;
   }

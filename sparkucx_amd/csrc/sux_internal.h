@@ -61,6 +61,8 @@ struct Tuning {
   bool counts_tm = true;    // k_hist4 + k_scatter7/8: tile-major counts (MapGroup::counts_tm)
   int scatter_counters = 2; // k_scatter8 per-wave counters: 1 partition-major, 2 wave-major
   bool lz4_queue = true;    // k_lz4_default: chunks from a device work queue (else grid-stride)
+  int scatter_nt = 0;       // k_scatter8 non-temporal record loads (bit 0) / line stores (bit 1)
+  bool gather16 = true;     // the sort's record gather in 16-byte units (else one dword per lane)
 };
 
 // Per-launch geometry of a group of consecutive map batches.
@@ -225,7 +227,7 @@ constexpr uint32_t kSortSpanBlocks = 2048;
 constexpr uint64_t kSortSpanBytes = 4ull * 8 * (kSortSpanBlocks + 1);
 hipError_t launch_gather_records_sel(const void* in, const void* pairs_a, const void* pairs_b,
                                      const uint32_t* sel, uint64_t n, uint32_t rs, void* out,
-                                     hipStream_t s);
+                                     hipStream_t s, bool gather16 = true);
 hipError_t launch_unpair_records_sel(const void* pairs_a, const void* pairs_b, const uint32_t* sel,
                                      uint64_t n, uint32_t rs, int kind, int key_offset,
                                      int key_len, int sbytes, void* out, hipStream_t s);

@@ -1220,7 +1220,7 @@ struct Sc8 {
   }
 };
 
-template <uint32_t S, uint32_t C, uint32_t NW, bool WM>
+template <uint32_t S, uint32_t C, uint32_t NW, bool WM, int NTMODE = 0>
 __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid_bits,
                                                      const uint16_t* __restrict__ pids,
                                                      const uint32_t* __restrict__ prefix,
@@ -1230,6 +1230,7 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
   using K = Sc8<S, C, NW>;
   constexpr uint32_t NT = K::NT, W = K::W, RPW = K::RPW, NG = K::NG, PER = K::kPer;
   constexpr uint32_t RM = 208;  // K's RMAX: the tables' compile-time stride
+  constexpr int NTM = NTMODE;   // non-temporal: bit 0 record loads, bit 1 line stores
   extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
   const uint32_t SP = K::space(R);
   u32x4* img = reinterpret_cast<u32x4*>(lds8 + K::kImg);
@@ -1362,7 +1363,10 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
     const u32x4* src = reinterpret_cast<const u32x4*>(a - head);
     const uint32_t units = (head + n * S + 15) >> 4;
 #pragma unroll
-    for (uint32_t k2 = 0; k2 < PER; ++k2) v[k2] = src[min(tid + k2 * NT, units - 1)];
+    for (uint32_t k2 = 0; k2 < PER; ++k2) {
+      const u32x4* a4 = &src[min(tid + k2 * NT, units - 1)];
+      v[k2] = (NTM & 1) ? __builtin_nontemporal_load(a4) : *a4;  // streamed once
+    }
   };
 
   if (owner) {
@@ -1511,7 +1515,10 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
       const u32x4 x = img[q];
       const uint32_t f = kq < 8 ? fhead[p] : 0u;
       if (f <= 4 * kq) {
-        out4[A] = x;
+        if (NTM & 2)
+          __builtin_nontemporal_store(x, &out4[A]);  // whole lines, never read back here
+        else
+          out4[A] = x;
       } else if (f < 4 * kq + 4) {
 #pragma unroll
         for (uint32_t cc = 0; cc < 4; ++cc)
@@ -1861,6 +1868,9 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g_in, const
     const bool wm = tn.scatter_counters != 1;
     allow_lds(reinterpret_cast<const void*>(&k_scatter8<100, 1024, 16, true>), lds8b);
     allow_lds(reinterpret_cast<const void*>(&k_scatter8<100, 1024, 16, false>), lds8b);
+    allow_lds(reinterpret_cast<const void*>(&k_scatter8<100, 1024, 16, true, 1>), lds8b);
+    allow_lds(reinterpret_cast<const void*>(&k_scatter8<100, 1024, 16, true, 2>), lds8b);
+    allow_lds(reinterpret_cast<const void*>(&k_scatter8<100, 1024, 16, true, 3>), lds8b);
     // tile order: contiguous ranges (default; scatter_order 1) or block-cyclic inside an XCD's
     // workgroups (2: 2^27-record maps 49.7 -> 50.3 ms, 2^20 42.9 -> 46.3, profiles/r02_m27_b)
     const uint32_t tiles_per_wg = (g.num_maps * g.tiles_per_map + grid.x - 1) / grid.x;
@@ -1877,9 +1887,19 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g_in, const
     for (uint32_t w = 0; w < nwin; ++w) {
       const uint32_t tw0 = (uint32_t)((uint64_t)T * w / nwin), tw1 = (uint32_t)((uint64_t)T * (w + 1) / nwin);
       const dim3 gw(std::min<uint32_t>(tw1 - tw0, ncu));
-      if (wm)
+      const uint32_t cy = cyc ? per_xcd : 0u;
+      if (wm && tn.scatter_nt == 1)
+        hipLaunchKernelGGL((k_scatter8<100, 1024, 16, true, 1>), gw, dim3(1024), lds8b, s, g, R,
+                           bits, pids, counts, base, d_out, cy, tw0, tw1);
+      else if (wm && tn.scatter_nt == 2)
+        hipLaunchKernelGGL((k_scatter8<100, 1024, 16, true, 2>), gw, dim3(1024), lds8b, s, g, R,
+                           bits, pids, counts, base, d_out, cy, tw0, tw1);
+      else if (wm && tn.scatter_nt == 3)
+        hipLaunchKernelGGL((k_scatter8<100, 1024, 16, true, 3>), gw, dim3(1024), lds8b, s, g, R,
+                           bits, pids, counts, base, d_out, cy, tw0, tw1);
+      else if (wm)
         hipLaunchKernelGGL((k_scatter8<100, 1024, 16, true>), gw, dim3(1024), lds8b, s, g, R, bits,
-                           pids, counts, base, d_out, cyc ? per_xcd : 0u, tw0, tw1);
+                           pids, counts, base, d_out, cy, tw0, tw1);
       else
         hipLaunchKernelGGL((k_scatter8<100, 1024, 16, false>), gw, dim3(1024), lds8b, s, g, R, bits,
                            pids, counts, base, d_out, cyc ? per_xcd : 0u, tw0, tw1);

@@ -229,6 +229,36 @@ __global__ __launch_bounds__(256) void k_gather_records(const uint32_t* __restri
   }
 }
 
+// Record gather with whole 16-byte units: L lanes per record (L = the power of two covering its
+// units, <= 64), 64 / L records per wave and step; lane l moves units l, l + L, ... of its record
+// (a record starts at a 4-byte phase: dword-aligned 16-byte accesses; the last unit's tail as
+// dwords).  One load instruction carries 64 x 16 B instead of k_gather_records' 64 x 4 B.
+__global__ __launch_bounds__(256) void k_gather_records16(const uint8_t* __restrict__ in,
+                                                          const u32x4* __restrict__ pairs,
+                                                          uint64_t n, uint32_t rs, uint32_t L,
+                                                          uint8_t* __restrict__ out,
+                                                          const u32x4* __restrict__ pairs_b,
+                                                          const uint32_t* __restrict__ sel) {
+  if (sel && *sel) pairs = pairs_b;
+  const uint32_t* idx = reinterpret_cast<const uint32_t*>(pairs) + 3;  // pairs[j][3]
+  const uint32_t lane = threadIdx.x % kWave, l = lane % L, per_wave = kWave / L;
+  const uint32_t full = rs / 16, tail = (rs % 16) / 4;  // whole units, dwords after them
+  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / kWave);
+  const uint64_t w0 = (uint64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+  for (uint64_t j = w0 * per_wave + lane / L; j < n; j += waves * per_wave) {
+    const uint32_t src = idx[4 * j];
+    const uint8_t* s = in + (uint64_t)src * rs;
+    uint8_t* d = out + j * rs;
+    for (uint32_t u = l; u < full; u += L)
+      *reinterpret_cast<u32x4a4*>(d + 16 * u) = *reinterpret_cast<const u32x4a4*>(s + 16 * u);
+    if (tail && l == full % L) {
+      const uint32_t* s4 = reinterpret_cast<const uint32_t*>(s + 16 * full);
+      uint32_t* d4 = reinterpret_cast<uint32_t*>(d + 16 * full);
+      for (uint32_t t = 0; t < tail; ++t) d4[t] = s4[t];
+    }
+  }
+}
+
 hipError_t launch_sort_pairs(const uint8_t* in, uint64_t n, uint32_t rs, int kind, int key_offset,
                              int key_len, const int64_t* seg, int nseg, int sbytes, void* pairs,
                              void* span_ws, bool inline_rec, hipStream_t s) {
@@ -263,13 +293,22 @@ hipError_t launch_unpair_records(const void* pairs, uint64_t n, uint32_t rs, int
 
 hipError_t launch_gather_records(const void* in, const void* pairs, uint64_t n, uint32_t rs,
                                  void* out, hipStream_t s) {
-  return launch_gather_records_sel(in, pairs, nullptr, nullptr, n, rs, out, s);
+  return launch_gather_records_sel(in, pairs, nullptr, nullptr, n, rs, out, s, true);
 }
 
 hipError_t launch_gather_records_sel(const void* in, const void* pairs, const void* pairs_b,
                                      const uint32_t* sel, uint64_t n, uint32_t rs, void* out,
-                                     hipStream_t s) {
+                                     hipStream_t s, bool gather16) {
   if (n == 0) return hipSuccess;
+  if (rs >= 16 && rs % 4 == 0 && gather16) {
+    uint32_t L = 1;
+    while (L < 64 && 16 * L < rs) L <<= 1;
+    const uint64_t blocks = std::min<uint64_t>((n * L + 255) / 256, 256ull * 16);
+    hipLaunchKernelGGL(k_gather_records16, dim3((uint32_t)blocks), dim3(256), 0, s,
+                       static_cast<const uint8_t*>(in), static_cast<const u32x4*>(pairs), n, rs, L,
+                       static_cast<uint8_t*>(out), static_cast<const u32x4*>(pairs_b), sel);
+    return hipGetLastError();
+  }
   const uint64_t total = n * (rs / 4);
   const uint64_t blocks = std::min<uint64_t>((total + 255) / 256, 256ull * 32);
   const uint32_t W = rs / 4;

@@ -320,3 +320,15 @@ def test_sort_records_captured_in_a_graph(gpu_node, shape):
         torch.cuda.synchronize()
         assert out.cpu().numpy().tobytes() == want.tobytes()
     gpu_node.check()
+
+
+@pytest.mark.parametrize("gk", [1, 2])
+@pytest.mark.parametrize("rs,n", [(100, 300_000), (20, 50_000), (36, 7777), (1028, 3000), (4096, 500)])
+def test_record_gather_kernels(gpu_node, tuned, gk, rs, n):
+    """Both record gathers (tuning gather_kernel: 1 = 16-byte units with L lanes per record,
+    2 = one dword per lane) over record sizes with 0..3 tail dwords and L from 2 to 64."""
+    tuned(gather_kernel=gk)
+    rng = np.random.default_rng(rs + n)
+    recs = rng.integers(0, 256, n * rs, dtype=np.uint8)
+    got = gpu_sort(gpu_node, recs, rs, N.SORT_BYTES, 0, 10)
+    assert got.tobytes() == O.sort_records(recs, rs, O.SORT_BYTES, 0, 10).tobytes()
