@@ -28,7 +28,14 @@ __device__ inline u32x4 make_pair(const uint8_t* __restrict__ in, uint64_t i, ui
                                   int nseg, int sbytes) {
   const uint8_t* r = in + i * rs + key_offset;
   uint8_t kb[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  if (kind == 1 && (key_offset & 3) == 0) {  // unsigned bytes, dword-aligned: dword loads
+  if (kind == 1 && (key_offset & 3) == 0 && key_offset + 16 <= (int)rs) {
+    // unsigned bytes, dword-aligned, 16 bytes inside the record: ONE 16-byte load per record
+    // (a wave instruction brings 64 keys; three dword loads made three passes over the same
+    // lines), streamed (the records are read again only by the final gather, long after)
+    const u32x4 w = __builtin_nontemporal_load(reinterpret_cast<const u32x4a4*>(r));
+#pragma unroll
+    for (int k = 0; k < 12; ++k) kb[k] = k < key_len ? (uint8_t)(w[k / 4] >> (8 * (k % 4))) : 0u;
+  } else if (kind == 1 && (key_offset & 3) == 0) {  // unsigned bytes, dword-aligned: dword loads
     // all three loads issued unconditionally (the key's last dword repeated when shorter), then
     // bytes picked with constant indices: a load per loop trip made every record wait for its
     // previous key dword
