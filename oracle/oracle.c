@@ -24,7 +24,10 @@
  *
  * Pinning.  The reference has no unit tests, fixtures or golden vectors and is
  * JVM-only (no JDK here), so it cannot be run.  The Murmur3 primitive is pinned by the known
- * answers of Spark's Murmur3_x86_32Suite (tests/test_oracle.py).  Everything else (partition
+ * answers of Spark's Murmur3_x86_32Suite (tests/test_oracle.py) and by an independent
+ * implementation, scikit-learn's MurmurHash3_x86_32 (tests/test_oracle_pins.py, which also checks
+ * the partitioners, the map write, the index bytes and the key sort against plain-Python/numpy
+ * restatements that share no code with this file).  Everything else (partition
  * grouping, index bytes, fetch packing) is a restatement of the cited code and is therefore
  * "parity unpinned" against the reference itself; tests/golden/ freezes the restatement's
  * outputs so that later rounds cannot drift.
