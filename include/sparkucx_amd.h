@@ -191,8 +191,10 @@ typedef struct sux_tuning {
                                per chunk), 2 the fixed grid-stride deal                        */
   int32_t scatter_nt;       /* k_scatter8 non-temporal accesses: 1 loads, 2 stores, 3 both,
                                -1 or 0 none                                                    */
-  int32_t gather_kernel;    /* sort's record gather: 1 (0) 16-byte units, L lanes per record;
-                               2 one dword per lane                                            */
+  int32_t gather_kernel;    /* sort's record gather: 3 (0) fused into the LDS bucket sort (each
+                               sorted bucket gathers its own records; records <= 1024 B), 1 its
+                               own launch in 16-byte units, L lanes per record, 2 its own
+                               launch, one dword per lane                                      */
   int32_t reserved[3];
 } sux_tuning;
 int sux_node_set_tuning(sux_node* node, const sux_tuning* tuning);

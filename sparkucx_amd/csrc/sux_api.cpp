@@ -826,7 +826,8 @@ sux::Tuning resolve_tuning(const sux_tuning& t, bool pipelined) {
   if (t.scatter_counters) r.scatter_counters = t.scatter_counters;
   r.lz4_queue = t.lz4_queue != 2;  // the work queue: 46.6 -> 53.0 GB/s (profiles/r03)
   r.scatter_nt = t.scatter_nt > 0 ? t.scatter_nt : 0;
-  r.gather16 = t.gather_kernel != 2;
+  r.gather_kernel = t.gather_kernel ? t.gather_kernel : 3;
+  r.gather16 = r.gather_kernel != 2;
   return r;
 }
 
@@ -1092,7 +1093,7 @@ int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
     require(in(t->scatter_counters, {1, 2}), SUX_EINVAL, "scatter_counters must be 1 or 2");
     require(in(t->lz4_queue, {1, 2}), SUX_EINVAL, "lz4_queue must be 1 or 2");
     require(t->scatter_nt >= -1 && t->scatter_nt <= 3, SUX_EINVAL, "scatter_nt must be -1 .. 3");
-    require(in(t->gather_kernel, {1, 2}), SUX_EINVAL, "gather_kernel must be 1 or 2");
+    require(in(t->gather_kernel, {1, 2, 3}), SUX_EINVAL, "gather_kernel must be 1, 2 or 3");
     for (int32_t r : t->reserved) require(r == 0, SUX_EINVAL, "reserved tuning fields must be 0");
     require(node, SUX_EINVAL, "NULL node");
     std::lock_guard<std::mutex> lk(node->mu);
@@ -3575,6 +3576,17 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
               "sort top digit pass");
     hip_check(sux::launch_sort_bucket_max(index1, (uint32_t)pd1.R, plan, s),
               "sort bucket max");
+    const sux::Tuning gt = resolve_tuning(node->tuning, false);
+    if (!inline_rec && gt.gather_kernel == 3 && sux::sort_gather_fusable(record_size)) {
+      // the fused sort: sorted buckets gather their records themselves, the rest after them
+      hip_check(sux::launch_sort_local_planned(b, a, index1, (uint32_t)pd1.R, plan, s, d_in,
+                                               d_out, record_size),
+                "sort buckets");
+      hip_check(sux::launch_gather_rest(d_in, a, b, index1, (uint32_t)pd1.R, n, plan, record_size,
+                                        d_out, s),
+                "sort gather rest");
+      return;
+    }
     hip_check(sux::launch_sort_local_planned(b, a, index1, (uint32_t)pd1.R, plan, s),
               "sort buckets");
     if (inline_rec)
@@ -3583,7 +3595,7 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
                 "sort unpair");
     else
       hip_check(sux::launch_gather_records_sel(d_in, a, b, &plan->final_b, n, record_size, d_out,
-                                               s, resolve_tuning(node->tuning, false).gather16),
+                                               s, gt.gather16),
                 "sort gather");
     return;
   }

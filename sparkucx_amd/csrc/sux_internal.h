@@ -62,7 +62,9 @@ struct Tuning {
   int scatter_counters = 2; // k_scatter8 per-wave counters: 1 partition-major, 2 wave-major
   bool lz4_queue = true;    // k_lz4_default: chunks from a device work queue (else grid-stride)
   int scatter_nt = 0;       // k_scatter8 non-temporal record loads (bit 0) / line stores (bit 1)
-  bool gather16 = true;     // the sort's record gather in 16-byte units (else one dword per lane)
+  int gather_kernel = 3;    // the sort's record gather: 1 its own launch in 16-byte units, 2 its
+                            // own launch, one dword per lane, 3 fused into the bucket sort
+  bool gather16 = true;     // (1 and 3) 16-byte units
 };
 
 // Per-launch geometry of a group of consecutive map batches.
@@ -268,8 +270,17 @@ hipError_t launch_sort_bucket_max(const int64_t* d_index, uint32_t R, SortPlanDe
 // The sort of every top-digit bucket, driven by the plan (a no-op unless plan->msd_ok): one LDS
 // launch per bucket-size class (each bucket on the smallest shape that holds it), then buckets
 // above kSortLocalCap through global memory.
+// recs_out != nullptr (the fused sort): the LDS launches gather their buckets' records from
+// recs_in straight into recs_out instead of writing sorted pairs; launch_gather_rest then gathers
+// every record they did not (needs sort_gather_fusable(rs)).
 hipError_t launch_sort_local_planned(const void* in_pairs, void* out_pairs, const int64_t* d_index,
-                                     uint32_t R, const SortPlanDev* plan, hipStream_t s);
+                                     uint32_t R, const SortPlanDev* plan, hipStream_t s,
+                                     const void* recs_in = nullptr, void* recs_out = nullptr,
+                                     uint32_t rs = 0);
+bool sort_gather_fusable(uint32_t rs);
+hipError_t launch_gather_rest(const void* recs_in, const void* pairs_a, const void* pairs_b,
+                              const int64_t* d_index, uint32_t R, uint64_t n,
+                              const SortPlanDev* plan, uint32_t rs, void* recs_out, hipStream_t s);
 
 
 // Generators (sux_gen.hip).

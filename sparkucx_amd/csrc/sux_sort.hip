@@ -359,6 +359,59 @@ __device__ __forceinline__ bool key_greater(const u32x4& a, const u32x4& b, int 
 constexpr int kTopDigits = 2;          // LDS digit passes before the tie fix-up
 constexpr uint32_t kMaxTieRun = 16;    // longer tie runs: every digit pass instead
 
+// Gather of records [0, n) of one bucket (fused sort): output record e = input record sidx[e].
+// L = 2^lsh lanes per record, each moving at most one 16-byte unit (lane l < rs / 16) or the
+// record's tail dwords (lane rs / 16) — so rs <= 1024 (L <= 64); NT / L records per step, U steps'
+// loads issued before their stores (clamped, unconditional: no per-load wait).  Records start at a
+// 4-byte phase (dword-aligned 16-byte accesses).
+template <uint32_t NT, uint32_t U>
+__device__ __forceinline__ void gather_run(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                           const uint32_t* sidx, uint32_t n, uint32_t rs,
+                                           uint32_t lsh, uint32_t tid) {
+  const uint32_t L = 1u << lsh, l = tid & (L - 1), G = NT >> lsh;
+  const uint32_t full = rs / 16, tail = (rs % 16) / 4;
+  const bool unit = l < full, tl = tail != 0 && l == full;
+  if (!unit && !tl) return;
+  for (uint32_t r0 = tid >> lsh; r0 < n; r0 += U * G) {
+    u32x4 v[U];
+#pragma unroll
+    for (uint32_t k = 0; k < U; ++k) {
+      const uint32_t e = min(r0 + k * G, n - 1);
+      const uint8_t* s = in + (uint64_t)sidx[e] * rs + 16 * l;
+      if (unit) {
+        v[k] = *reinterpret_cast<const u32x4a4*>(s);
+      } else {
+        const uint32_t* s4 = reinterpret_cast<const uint32_t*>(s);
+        v[k][0] = s4[0];
+        v[k][1] = tail > 1 ? s4[1] : 0u;
+        v[k][2] = tail > 2 ? s4[2] : 0u;
+      }
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < U; ++k) {
+      const uint32_t e = r0 + k * G;
+      if (e >= n) break;
+      uint8_t* d = out + (uint64_t)e * rs + 16 * l;
+      if (unit) {
+        *reinterpret_cast<u32x4a4*>(d) = v[k];
+      } else {
+        uint32_t* d4 = reinterpret_cast<uint32_t*>(d);
+        d4[0] = v[k][0];
+        if (tail > 1) d4[1] = v[k][1];
+        if (tail > 2) d4[2] = v[k][2];
+      }
+    }
+  }
+}
+
+// Where the fused sort gathers records (k_sort_local with GATHER): the input records, the output
+// records, the record size and log2 of the lanes per record.
+struct SortGather {
+  const uint8_t* in;
+  uint8_t* out;
+  uint32_t rs, lsh;
+};
+
 template <uint32_t NW, uint32_t CAP>  // buf[CAP] u32x4 | wc[NW][256] u32 | wsum[NW]
 struct SortLocal {
   static constexpr uint32_t NT = NW * kWave, PT = CAP / NT, NB = 256;
@@ -368,12 +421,18 @@ struct SortLocal {
 // <8 waves, 4096 pairs>: two workgroups per CU; <4 waves, 1024 pairs>: six per CU, for the
 // ~600-pair buckets of a 5 M-record reduce partition.  A launch sorts the buckets of
 // lo_cap < n <= CAP (one launch per size class) when the plan says the MSD path finishes the sort.
-template <uint32_t NW, uint32_t CAP>
+// GATHER (the fused sort, tuning gather_kernel 3): a sorted bucket is not written back as pairs —
+// its record indices go to LDS and the workgroup gathers the bucket's records straight into the
+// output (gather_run).  The random record reads of one workgroup then overlap the LDS digit
+// passes of the others on the CU, and the pairs' last write + read (2 x 16 B per record) and the
+// separate gather launch are gone.
+template <uint32_t NW, uint32_t CAP, bool GATHER = false>
 __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : CAP == 1024 ? 6 : 4) void k_sort_local(const u32x4* __restrict__ in,
                                                         u32x4* __restrict__ out,
                                                         const int64_t* __restrict__ index,
                                                         uint32_t R, uint32_t lo_cap,
-                                                        const SortPlanDev* __restrict__ plan) {
+                                                        const SortPlanDev* __restrict__ plan,
+                                                        SortGather gth) {
   if (!plan->msd_ok || plan->dg.n == 0) return;  // the LSD fallback, or the top digit was all
   const SortDigits dg = plan->dg;
   const int kbits = plan->kbits;
@@ -475,11 +534,68 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : CAP == 1024 ? 6 : 4) void k_
       if (redo)
         for (int d = 0; d < nd; ++d) digit_pass(d);
     }
+    if constexpr (GATHER) {
+      // every thread passed a barrier after its last read of buf (each digit pass and the tie
+      // fix-up end in one), so buf's first CAP dwords can take the record indices; the next
+      // bucket writes buf only after a barrier, so the gather's reads of them are safe too
+      uint32_t* sidx = reinterpret_cast<uint32_t*>(buf);
 #pragma unroll
-    for (uint32_t j = 0; j < PT; ++j) {
-      const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
-      if (e < n) out[s0 + e] = v[j];
+      for (uint32_t j = 0; j < PT; ++j) {
+        const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+        if (e < n) sidx[e] = v[j][3];
+      }
+      __syncthreads();
+      gather_run<NT, 8>(gth.in, gth.out + s0 * gth.rs, sidx, n, gth.rs, gth.lsh, (uint32_t)tid);
+    } else {
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) {
+        const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+        if (e < n) out[s0 + e] = v[j];
+      }
     }
+  }
+}
+
+// The fused sort's other records: a workgroup per 4096-record chunk of the output gathers the
+// parts of the buckets overlapping it that k_sort_local<GATHER> did not — every bucket when the
+// plan finished without it (no lower digit varies: the top pass's order; every key equal: the
+// input order), else the buckets above kSortLocalCap (sorted as pairs by k_sort_bucket_global).
+// Chunks of done buckets cost a binary search over the bucket index and nothing else.
+constexpr uint32_t kGatherRestChunk = 4096;
+__global__ __launch_bounds__(256) void k_gather_rest(const u32x4* __restrict__ pairs_a,
+                                                     const u32x4* __restrict__ pairs_b,
+                                                     const int64_t* __restrict__ index, uint32_t R,
+                                                     uint64_t n, const SortPlanDev* __restrict__ plan,
+                                                     SortGather gth) {
+  __shared__ uint32_t sidx[kGatherRestChunk];
+  __shared__ uint32_t b_first;
+  const bool all = !plan->msd_ok || plan->dg.n == 0;
+  const u32x4* pairs = plan->final_b ? pairs_b : pairs_a;
+  const uint32_t tid = threadIdx.x;
+  for (uint64_t c0 = (uint64_t)blockIdx.x * kGatherRestChunk; c0 < n;
+       c0 += (uint64_t)gridDim.x * kGatherRestChunk) {
+    const uint64_t c1 = min<uint64_t>(c0 + kGatherRestChunk, n);
+    if (tid == 0) {  // the last bucket starting at or before c0
+      uint32_t lo = 0, hi = R;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((uint64_t)index[mid] / 16 <= c0) lo = mid; else hi = mid;
+      }
+      b_first = lo;
+    }
+    __syncthreads();
+    for (uint32_t b = b_first; b < R; ++b) {
+      const uint64_t s0 = (uint64_t)index[b] / 16, s1 = (uint64_t)index[b + 1] / 16;
+      if (s0 >= c1) break;
+      const uint64_t r0 = max(s0, c0), r1 = min(s1, c1);
+      if (r0 >= r1 || (!all && s1 - s0 <= kSortLocalCap)) continue;
+      const uint32_t m = (uint32_t)(r1 - r0);
+      for (uint32_t e = tid; e < m; e += 256) sidx[e] = pairs[r0 + e][3];
+      __syncthreads();
+      gather_run<256, 4>(gth.in, gth.out + r0 * gth.rs, sidx, m, gth.rs, gth.lsh, tid);
+      __syncthreads();
+    }
+    __syncthreads();  // b_first is rewritten for the next chunk
   }
 }
 
@@ -502,6 +618,7 @@ __global__ __launch_bounds__(NW * 64) void k_sort_bucket_global(u32x4* __restric
   __shared__ uint32_t wc[NW * NB];
   __shared__ uint32_t wsum[NW];
   __shared__ uint32_t cur[NB];
+  __shared__ uint32_t span[6];
   const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
   const uint64_t lt_mask = (1ull << lane) - 1ull;
   for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
@@ -512,17 +629,50 @@ __global__ __launch_bounds__(NW * 64) void k_sort_bucket_global(u32x4* __restric
     if (n <= kSortLocalCap) continue;  // k_sort_local's
     u32x4* src = in + s0;
     u32x4* dst = out + s0;
+    // the bucket's own key span (AND / OR of the key words): a digit constant inside the bucket
+    // is an identity pass and is skipped — a heavy hitter's bucket of equal keys skips them all
+    // (500 000 equal TeraSort keys: 10.3 ms of count + scatter sweeps by one workgroup)
+    if (tid < 3) {
+      span[tid] = ~0u;
+      span[3 + tid] = 0u;
+    }
+    __syncthreads();
+    {
+      uint32_t a0 = ~0u, a1 = ~0u, a2 = ~0u, o0 = 0u, o1 = 0u, o2 = 0u;
+      for (uint32_t e = tid; e < n; e += NT) {
+        const u32x4 x = src[e];
+        a0 &= x[0], a1 &= x[1], a2 &= x[2], o0 |= x[0], o1 |= x[1], o2 |= x[2];
+      }
+      atomicAnd(&span[0], a0), atomicAnd(&span[1], a1), atomicAnd(&span[2], a2);
+      atomicOr(&span[3], o0), atomicOr(&span[4], o1), atomicOr(&span[5], o2);
+    }
+    __syncthreads();
+    const u32x4 span_and{span[0], span[1], span[2], 0u}, span_or{span[3], span[4], span[5], 0u};
+    __syncthreads();  // read by every thread before the next bucket resets it
     for (int d = 0; d < dg.n; ++d) {
       const uint64_t w = d < 8 ? dg.lo : dg.hi;
       const uint32_t sh = (uint32_t)(w >> (8 * (d & 7))) & 255u;
-      // count sweep -> exclusive digit starts in cur
-      if (tid < (int)NB) cur[tid] = 0;
-      __syncthreads();
-      for (uint32_t e = tid; e < n; e += NT) atomicAdd(&cur[pair_digit8(src[e], sh)], 1u);
+      if (pair_digit8(span_and, sh) == pair_digit8(span_or, sh)) continue;  // uniform
+      // count sweep -> exclusive digit starts in cur.  Per-wave counters through the ballot
+      // match (wave_rank): a wave's equal digits cost one LDS update — one LDS atomic per pair
+      // serialised a heavy hitter's equal keys on a single counter
+      for (uint32_t c0 = 0; c0 < n; c0 += CH) {
+#pragma unroll
+        for (uint32_t j = 0; j < PT; ++j) {
+          const uint32_t e = c0 + wave * (PT * kWave) + j * kWave + lane;
+          const bool valid = e < n;
+          const u32x4 p = src[valid ? e : n - 1];
+          (void)wave_rank<8>(valid ? pair_digit8(p, sh) : 0u, valid, wc + wave * NB, lt_mask);
+        }
+      }
       __syncthreads();
       uint32_t x = 0, incl = 0;
       if (tid < (int)NB) {
-        x = cur[tid];
+#pragma unroll
+        for (uint32_t q = 0; q < NW; ++q) {
+          x += wc[q * NB + tid];
+          wc[q * NB + tid] = 0;  // zero again for the scatter sweep's ranks
+        }
         incl = wave_incl_scan(x, lane);
         if (lane == kWave - 1) wsum[wave] = incl;
       }
@@ -642,27 +792,55 @@ hipError_t launch_sort_bucket_max(const int64_t* d_index, uint32_t R, SortPlanDe
   return hipGetLastError();
 }
 
-hipError_t launch_sort_local_planned(const void* in_pairs, void* out_pairs, const int64_t* d_index,
-                                     uint32_t R, const SortPlanDev* plan, hipStream_t s) {
-  const uint32_t ncu = (uint32_t)std::max(1, stream_cus(s));
-  const u32x4* in = static_cast<const u32x4*>(in_pairs);
-  u32x4* out = static_cast<u32x4*>(out_pairs);
+template <bool GATHER>
+static void launch_sort_local_classes(const u32x4* in, u32x4* out, const int64_t* d_index,
+                                      uint32_t R, const SortPlanDev* plan, const SortGather& gth,
+                                      uint32_t ncu, hipStream_t s) {
   // size classes (0, 1024], (1024, 2048], (2048, kSortLocalCap]: each bucket on the smallest
   // shape that holds it (the classes a key set leaves empty cost one index sweep each)
   constexpr size_t l1 = SortLocal<4, 1024>::lds_bytes();
-  hipLaunchKernelGGL((k_sort_local<4, 1024>), dim3(std::min<uint32_t>(R, 6 * ncu)), dim3(4 * kWave),
-                     l1, s, in, out, d_index, R, 0u, plan);
+  hipLaunchKernelGGL((k_sort_local<4, 1024, GATHER>), dim3(std::min<uint32_t>(R, 6 * ncu)),
+                     dim3(4 * kWave), l1, s, in, out, d_index, R, 0u, plan, gth);
   constexpr size_t l2 = SortLocal<4, 2048>::lds_bytes();
   static_assert(4 * l2 <= 160 * 1024, "four workgroups per CU");
-  hipLaunchKernelGGL((k_sort_local<4, 2048>), dim3(std::min<uint32_t>(R, 4 * ncu)), dim3(4 * kWave),
-                     l2, s, in, out, d_index, R, 1024u, plan);
+  hipLaunchKernelGGL((k_sort_local<4, 2048, GATHER>), dim3(std::min<uint32_t>(R, 4 * ncu)),
+                     dim3(4 * kWave), l2, s, in, out, d_index, R, 1024u, plan, gth);
   constexpr size_t l3 = SortLocal<8, kSortLocalCap>::lds_bytes();
   static_assert(2 * l3 <= 160 * 1024, "two workgroups per CU");
-  allow_lds(reinterpret_cast<const void*>(&k_sort_local<8, kSortLocalCap>), l3);
-  hipLaunchKernelGGL((k_sort_local<8, kSortLocalCap>), dim3(std::min<uint32_t>(R, 2 * ncu)),
-                     dim3(8 * kWave), l3, s, in, out, d_index, R, 2048u, plan);
+  allow_lds(reinterpret_cast<const void*>(&k_sort_local<8, kSortLocalCap, GATHER>), l3);
+  hipLaunchKernelGGL((k_sort_local<8, kSortLocalCap, GATHER>), dim3(std::min<uint32_t>(R, 2 * ncu)),
+                     dim3(8 * kWave), l3, s, in, out, d_index, R, 2048u, plan, gth);
+}
+
+hipError_t launch_sort_local_planned(const void* in_pairs, void* out_pairs, const int64_t* d_index,
+                                     uint32_t R, const SortPlanDev* plan, hipStream_t s,
+                                     const void* recs_in, void* recs_out, uint32_t rs) {
+  const uint32_t ncu = (uint32_t)std::max(1, stream_cus(s));
+  const u32x4* in = static_cast<const u32x4*>(in_pairs);
+  u32x4* out = static_cast<u32x4*>(out_pairs);
+  SortGather gth{static_cast<const uint8_t*>(recs_in), static_cast<uint8_t*>(recs_out), rs, 0};
+  while (gth.lsh < 6 && (16u << gth.lsh) < rs) ++gth.lsh;
+  if (recs_out)
+    launch_sort_local_classes<true>(in, out, d_index, R, plan, gth, ncu, s);
+  else
+    launch_sort_local_classes<false>(in, out, d_index, R, plan, gth, ncu, s);
   hipLaunchKernelGGL((k_sort_bucket_global<16>), dim3(std::min<uint32_t>(R, ncu)), dim3(16 * kWave),
                      0, s, const_cast<u32x4*>(in), out, d_index, R, plan);
+  return hipGetLastError();
+}
+
+bool sort_gather_fusable(uint32_t rs) { return rs >= 16 && rs % 4 == 0 && rs <= 1024; }
+
+hipError_t launch_gather_rest(const void* recs_in, const void* pairs_a, const void* pairs_b,
+                              const int64_t* d_index, uint32_t R, uint64_t n,
+                              const SortPlanDev* plan, uint32_t rs, void* recs_out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  SortGather gth{static_cast<const uint8_t*>(recs_in), static_cast<uint8_t*>(recs_out), rs, 0};
+  while (gth.lsh < 6 && (16u << gth.lsh) < rs) ++gth.lsh;
+  const uint64_t chunks = (n + kGatherRestChunk - 1) / kGatherRestChunk;
+  hipLaunchKernelGGL(k_gather_rest, dim3((uint32_t)std::min<uint64_t>(chunks, 8192)), dim3(256), 0,
+                     s, static_cast<const u32x4*>(pairs_a), static_cast<const u32x4*>(pairs_b),
+                     d_index, R, n, plan, gth);
   return hipGetLastError();
 }
 

@@ -221,15 +221,29 @@ def test_segmented_inline_small_records(gpu_node, nseg):
 
 
 @pytest.mark.parametrize("msd", [1, 2])
-@pytest.mark.parametrize("shape", ["terasort", "skewed_top", "skewed_top9", "long", "int_inline"])
+@pytest.mark.parametrize("shape", ["terasort", "skewed_top", "skewed_top9", "long", "int_inline",
+                                   "distinct50", "distinct50_k9", "skewed_const_mid"])
 def test_msd_finish_and_lsd_agree_with_oracle(gpu_node, tuned, msd, shape):
     """sort_msd 1: one top-digit pass + every bucket sorted by the lower digits (k_sort_local in
     LDS; k_sort_bucket_global for a bucket above the LDS capacity); 2: LSD digit passes only.
     'skewed_top' / 'skewed_top9': 60 % of the keys share their top bytes, so one bucket passes the
     LDS capacity and is sorted through global memory (10- and 9-byte keys: both parities of its
-    digit count)."""
+    digit count).  'distinct50*': 50 distinct keys, so every non-empty bucket holds ~6 000 equal
+    keys and k_sort_bucket_global skips every digit (its per-bucket key span); 'skewed_const_mid':
+    the big bucket's middle key bytes are constant, so it skips some digits and runs others."""
     tuned(sort_msd=msd)
-    if shape == "terasort":
+    if shape in ("distinct50", "distinct50_k9"):
+        recs = O.gen_terasort(65, 0, 300_000).reshape(-1, 100)
+        pick = np.random.default_rng(65).integers(0, 50, recs.shape[0])
+        recs[:, :10] = recs[:50, :10][pick]
+        klen = 10 if shape == "distinct50" else 9
+        recs, rs, kind, off = recs.ravel(), 100, N.SORT_BYTES, 0
+    elif shape == "skewed_const_mid":
+        recs = O.gen_terasort(66, 0, 300_000).reshape(-1, 100)
+        recs[: 180_000, :4] = 9
+        recs[: 180_000, 4:7] = 77
+        recs, rs, kind, off, klen = recs.ravel(), 100, N.SORT_BYTES, 0, 10
+    elif shape == "terasort":
         recs, rs, kind, off, klen = O.gen_terasort(61, 0, 700_000), 100, N.SORT_BYTES, 0, 10
     elif shape in ("skewed_top", "skewed_top9"):
         recs = O.gen_terasort(62, 0, 300_000).reshape(-1, 100)
@@ -322,11 +336,13 @@ def test_sort_records_captured_in_a_graph(gpu_node, shape):
     gpu_node.check()
 
 
-@pytest.mark.parametrize("gk", [1, 2])
-@pytest.mark.parametrize("rs,n", [(100, 300_000), (20, 50_000), (36, 7777), (1028, 3000), (4096, 500)])
+@pytest.mark.parametrize("gk", [1, 2, 3])
+@pytest.mark.parametrize("rs,n", [(100, 300_000), (20, 50_000), (36, 7777), (44, 123_457), (1024, 3000),
+                                  (1028, 3000), (4096, 500)])
 def test_record_gather_kernels(gpu_node, tuned, gk, rs, n):
-    """Both record gathers (tuning gather_kernel: 1 = 16-byte units with L lanes per record,
-    2 = one dword per lane) over record sizes with 0..3 tail dwords and L from 2 to 64."""
+    """Every record gather (tuning gather_kernel: 1 = its own launch in 16-byte units with L lanes
+    per record, 2 = one dword per lane, 3 = fused into the LDS bucket sort, records <= 1024 B)
+    over record sizes with 0..3 tail dwords and L from 2 to 64."""
     tuned(gather_kernel=gk)
     rng = np.random.default_rng(rs + n)
     recs = rng.integers(0, 256, n * rs, dtype=np.uint8)
