@@ -3554,8 +3554,14 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
   // (k_sort_bucket_global).  Each pair crosses HBM twice after the top pass instead of twice per
   // digit, and nothing is decided on the host.
   int tb = kSortMinDigitBits;  // ~<= 1536 pairs per bucket on average, at most 2^14 buckets
-  while (tb < 14 && (n >> tb) > 1536) ++tb;
-  if (node->tuning.sort_msd != 2 && !all_passes && (n >> tb) <= sux::kSortLocalCap / 2) {
+#ifndef SUX_SORT_BUCKET_TARGET
+#define SUX_SORT_BUCKET_TARGET 1536
+#endif
+#ifndef SUX_SORT_BUCKET_MSD_MAX
+#define SUX_SORT_BUCKET_MSD_MAX (sux::kSortLocalCap / 2)
+#endif
+  while (tb < 14 && (n >> tb) > SUX_SORT_BUCKET_TARGET) ++tb;
+  if (node->tuning.sort_msd != 2 && !all_passes && (n >> tb) <= SUX_SORT_BUCKET_MSD_MAX) {
     SortPlan P1;
     sort_plan(n, record_size, P1, tb);
     sux::SortPlanDev* plan = reinterpret_cast<sux::SortPlanDev*>(ws + plan_off);
@@ -3574,8 +3580,6 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
                                           ws + P1.part_off, P1.ws, nullptr, sort_tn, &node->timer,
                                           s),
               "sort top digit pass");
-    hip_check(sux::launch_sort_bucket_max(index1, (uint32_t)pd1.R, plan, s),
-              "sort bucket max");
     const sux::Tuning gt = resolve_tuning(node->tuning, false);
     if (!inline_rec && gt.gather_kernel == 3 && sux::sort_gather_fusable(record_size)) {
       // the fused sort: sorted buckets gather their records themselves, the rest after them

@@ -249,7 +249,7 @@ struct SortDigits {
   }
 };
 // The device-planned sort (sux_sort_records with no host wait): k_sort_plan fills the first
-// fields from the key span, k_sort_bucket_max the rest after the top-digit pass; every later
+// fields from the key span (k_sort_plan, before the top-digit pass); every later
 // kernel of the sort reads its decision from here.
 struct SortPlanDev {
   int32_t top_lo;    // shift of the top digit (the tb highest varying key bits)
@@ -258,15 +258,12 @@ struct SortPlanDev {
   uint32_t pad;
   uint32_t final_b;  // 1: the sorted pairs end in buffer b, 0: in buffer a
   int32_t kbits;     // key bits (with the segment id): the top kbits of the big-endian pair
-  uint64_t maxb;     // the largest top-digit bucket, in pairs
+  uint64_t maxb;     // unused (round 3: k_sort_plan decides msd_ok / final_b, no bucket sweep)
   SortDigits dg;     // the LDS sort's digits: 8-bit, below top_lo, only those that vary
 };
 constexpr uint64_t kSortPlanBytes = 256;
 static_assert(sizeof(SortPlanDev) <= kSortPlanBytes, "plan slot");
 hipError_t launch_sort_plan(const void* span, int bits, int tb, SortPlanDev* plan, hipStream_t s);
-// Largest bucket of the top-digit index -> plan (maxb, msd_ok, final_b).
-hipError_t launch_sort_bucket_max(const int64_t* d_index, uint32_t R, SortPlanDev* plan,
-                                  hipStream_t s);
 // The sort of every top-digit bucket, driven by the plan (a no-op unless plan->msd_ok): one LDS
 // launch per bucket-size class (each bucket on the smallest shape that holds it), then buckets
 // above kSortLocalCap through global memory.

@@ -331,7 +331,7 @@ hipError_t launch_gather_records_sel(const void* in, const void* pairs, const vo
 // ------------------------------------------------------------------------------------------
 // MSD finish (sux_sort_records / sux_sort_segments): one stable digit pass
 // over the top bits of the keys' varying range leaves R buckets of <= kSortLocalCap pairs
-// (checked on the device, k_sort_bucket_max); k_sort_local then sorts every bucket inside LDS by a stable LSD radix
+// (k_sort_local; larger ones k_sort_bucket_global); k_sort_local then sorts every bucket inside LDS by a stable LSD radix
 // over the lower key digits that vary (8-bit digits: wave-ballot ranks + one block scan per
 // digit; the pairs live in registers, one LDS buffer takes each digit's permutation) and writes
 // it back.  Each pair crosses HBM twice
@@ -364,6 +364,12 @@ constexpr uint32_t kMaxTieRun = 16;    // longer tie runs: every digit pass inst
 // record's tail dwords (lane rs / 16) — so rs <= 1024 (L <= 64); NT / L records per step, U steps'
 // loads issued before their stores (clamped, unconditional: no per-load wait).  Records start at a
 // 4-byte phase (dword-aligned 16-byte accesses).
+#ifndef SUX_SORT_GATHER_U
+#define SUX_SORT_GATHER_U 8  // records per lane group in flight in the fused sort's gather
+#endif
+#ifndef SUX_SORT_GATHER_NT
+#define SUX_SORT_GATHER_NT 0
+#endif
 template <uint32_t NT, uint32_t U>
 __device__ __forceinline__ void gather_run(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                            const uint32_t* sidx, uint32_t n, uint32_t rs,
@@ -379,7 +385,11 @@ __device__ __forceinline__ void gather_run(const uint8_t* __restrict__ in, uint8
       const uint32_t e = min(r0 + k * G, n - 1);
       const uint8_t* s = in + (uint64_t)sidx[e] * rs + 16 * l;
       if (unit) {
+#if SUX_SORT_GATHER_NT
+        v[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4a4*>(s));
+#else
         v[k] = *reinterpret_cast<const u32x4a4*>(s);
+#endif
       } else {
         const uint32_t* s4 = reinterpret_cast<const uint32_t*>(s);
         v[k][0] = s4[0];
@@ -545,7 +555,8 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : CAP == 1024 ? 6 : 4) void k_
         if (e < n) sidx[e] = v[j][3];
       }
       __syncthreads();
-      gather_run<NT, 8>(gth.in, gth.out + s0 * gth.rs, sidx, n, gth.rs, gth.lsh, (uint32_t)tid);
+      gather_run<NT, SUX_SORT_GATHER_U>(gth.in, gth.out + s0 * gth.rs, sidx, n, gth.rs, gth.lsh,
+                                        (uint32_t)tid);
     } else {
 #pragma unroll
       for (uint32_t j = 0; j < PT; ++j) {
@@ -753,42 +764,18 @@ __global__ void k_sort_plan(const uint32_t* __restrict__ span, int bits, int tb,
   plan->hb = hb;
   plan->kbits = bits;
   plan->dg = dg;
-}
-
-// The plan's second half: the largest bucket of the top-digit index, and where the sorted pairs
-// end.  One workgroup.
-__global__ __launch_bounds__(1024) void k_sort_bucket_max(const int64_t* __restrict__ index,
-                                                          uint32_t R,
-                                                          SortPlanDev* __restrict__ plan) {
-  __shared__ unsigned long long m;
-  if (threadIdx.x == 0) m = 0;
-  __syncthreads();
-  unsigned long long local = 0;
-  for (uint32_t p = threadIdx.x; p < R; p += 1024)
-    local = max(local, (unsigned long long)((index[p + 1] - index[p]) / 16));
-  atomicMax(&m, local);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const bool all_equal = plan->hb < 0;
-    plan->maxb = m;
-    // buckets up to kSortLocalCap sort in LDS (k_sort_local), larger ones through global memory
-    // (k_sort_bucket_global): the MSD path always finishes once some key bit varies
-    plan->msd_ok = all_equal ? 0u : 1u;
-    // a -> top pass -> b -> bucket sorts -> a; no lower digit varies: the top pass's b; every
-    // key equal: a (the input order)
-    plan->final_b = all_equal ? 0u : (plan->dg.n ? 0u : 1u);
-  }
+  // buckets up to kSortLocalCap sort in LDS (k_sort_local), larger ones through global memory
+  // (k_sort_bucket_global): the MSD path always finishes once some key bit varies.  The pairs
+  // go a -> top pass -> b -> bucket sorts -> a; with no lower digit varying they end in the top
+  // pass's b; with every key equal, in a (the input order)
+  plan->msd_ok = hb >= 0 ? 1u : 0u;
+  plan->final_b = hb < 0 ? 0u : (dg.n ? 0u : 1u);
+  plan->maxb = 0;
 }
 
 hipError_t launch_sort_plan(const void* span, int bits, int tb, SortPlanDev* plan, hipStream_t s) {
   hipLaunchKernelGGL(k_sort_plan, dim3(1), dim3(64), 0, s, static_cast<const uint32_t*>(span),
                      bits, tb, plan);
-  return hipGetLastError();
-}
-
-hipError_t launch_sort_bucket_max(const int64_t* d_index, uint32_t R, SortPlanDev* plan,
-                                  hipStream_t s) {
-  hipLaunchKernelGGL(k_sort_bucket_max, dim3(1), dim3(1024), 0, s, d_index, R, plan);
   return hipGetLastError();
 }
 

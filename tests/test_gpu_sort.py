@@ -289,7 +289,7 @@ def test_lds_sort_tie_fixup_and_redo(gpu_node, shape):
 @pytest.mark.parametrize("shape", ["terasort", "skewed_top", "equal", "top_only", "long_small"])
 def test_sort_records_captured_in_a_graph(gpu_node, shape):
     """sux_sort_records on a stream being captured into a HIP graph: the plan is made on the
-    device (k_sort_plan / k_sort_bucket_max), so there is no host wait and no host allocation
+    device (k_sort_plan), so there is no host wait and no host allocation
     mid-capture, and every branch runs inside the graph — the LDS finish ('terasort'), the LSD
     fallback of a bucket above the LDS capacity ('skewed_top'), the identity of equal keys
     ('equal'), a key whose varying bits all sit in the top digit ('top_only': the result stays in
