@@ -23,6 +23,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -748,7 +749,17 @@ void* ipc_open_fresh(sux_node* node, const uint8_t* handle) {
   const std::string key(reinterpret_cast<const char*>(handle), 64);
   for (int attempt = 0; attempt < 2; ++attempt) {
     void* base = nullptr;
-    hip_check(hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    // One W = 8 one-GPU rehearsal (8 processes importing each other's buffers at once) saw a
+    // single hipErrorInvalidDevicePointer from an open of a live, just-exported allocation that
+    // the same run opens fine otherwise (profiles/r03_v6/ipc_open_flake.txt): retried a few
+    // times, a few ms apart, before it is an error
+    hipError_t e = hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess);
+    for (int retry = 0; e == hipErrorInvalidDevicePointer && retry < 4; ++retry) {
+      (void)hipGetLastError();
+      std::this_thread::sleep_for(std::chrono::milliseconds(2 << retry));
+      e = hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess);
+    }
+    hip_check(e, "hipIpcOpenMemHandle");
     auto it = node->ipc_maps.find(base);
     if (it == node->ipc_maps.end()) {
       node->ipc_maps[base] = {key, 1};
