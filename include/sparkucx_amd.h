@@ -195,7 +195,11 @@ typedef struct sux_tuning {
                                sorted bucket gathers its own records; records <= 1024 B), 1 its
                                own launch in 16-byte units, L lanes per record, 2 its own
                                launch, one dword per lane                                      */
-  int32_t reserved[3];
+  int32_t split_cus;        /* sux_partition_maps_pipelined: 32..224 (multiple of 32) K1 of
+                               group g runs on that many CUs beside group g-1's K2 + K3 on the
+                               others (K1 holds its rate on few CUs, K3 scales with them);
+                               -1 or 0 every group's K1 -> K2 -> K3 on one of two streams    */
+  int32_t reserved[2];
 } sux_tuning;
 int sux_node_set_tuning(sux_node* node, const sux_tuning* tuning);
 /* Waits for the device, then reports (and clears) failures the kernels recorded in the node's

@@ -475,6 +475,14 @@ struct sux_node {
     for (hipEvent_t& e : pipe_ev)
       if (!e) hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "map event");
   }
+  // split mode of sux_partition_maps_pipelined: [0] K1 on `cus` CUs, [1] K2 + K3 on the rest;
+  // split_ev [0, 1] K1 done per workspace slot, [2, 3] K3 done per slot.  pipe_mu held.
+  hipStream_t pipe_split[2] = {nullptr, nullptr};
+  int pipe_split_cus = 0;
+  hipEvent_t split_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  void make_split(int cus);
+  int cus = 0;  // the device's CU count (device_cus)
+  int device_cus();
 
   void bind() { hip_check(hipSetDevice(conf.device), "hipSetDevice"); }
 
@@ -837,6 +845,7 @@ sux::Tuning resolve_tuning(const sux_tuning& t, bool pipelined) {
   if (t.scatter_counters) r.scatter_counters = t.scatter_counters;
   r.lz4_queue = t.lz4_queue != 2;  // the work queue: 46.6 -> 53.0 GB/s (profiles/r03)
   r.scatter_nt = t.scatter_nt > 0 ? t.scatter_nt : 0;
+  r.split_cus = t.split_cus > 0 ? t.split_cus : 0;
   r.gather_kernel = t.gather_kernel ? t.gather_kernel : 3;
   r.gather16 = r.gather_kernel != 2;
   return r;
@@ -869,7 +878,7 @@ Group make_group(const sux_partitioner* part, const void* recs, uint32_t rs, uin
 void run_group(sux_node* node, const sux_partitioner* part, const Group& G, int32_t world,
                void* d_out, int64_t* d_index, uint8_t* d_index_be, uint16_t* d_pids,
                uint64_t* d_peer_bytes, void* d_ws, uint64_t ws_bytes, hipStream_t s,
-               bool pipelined = false) {
+               bool pipelined = false, hipStream_t s_k1 = nullptr, hipEvent_t k1_done = nullptr) {
   require(d_ws || G.ws.total == 0, SUX_EINVAL, "workspace is NULL");
   require(ws_bytes >= G.ws.total, SUX_EINVAL,
           "workspace too small: need " + std::to_string(G.ws.total) + " bytes");
@@ -882,7 +891,7 @@ void run_group(sux_node* node, const sux_partitioner* part, const Group& G, int3
   hip_check(sux::launch_partition_group(part->pd, G.g, lay, static_cast<uint8_t*>(d_out), d_index,
                                         d_index_be, d_pids, static_cast<uint8_t*>(d_ws), G.ws,
                                         d_peer_bytes, resolve_tuning(node->tuning, pipelined),
-                                        &node->timer, s),
+                                        &node->timer, s, s_k1, k1_done),
             "partition launch");
 }
 }  // namespace
@@ -1105,6 +1114,8 @@ int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
     require(in(t->lz4_queue, {1, 2}), SUX_EINVAL, "lz4_queue must be 1 or 2");
     require(t->scatter_nt >= -1 && t->scatter_nt <= 3, SUX_EINVAL, "scatter_nt must be -1 .. 3");
     require(in(t->gather_kernel, {1, 2, 3}), SUX_EINVAL, "gather_kernel must be 1, 2 or 3");
+    require(t->split_cus == -1 || (t->split_cus >= 0 && t->split_cus <= 224 && t->split_cus % 32 == 0),
+            SUX_EINVAL, "split_cus must be -1, 0 or a multiple of 32 up to 224");
     for (int32_t r : t->reserved) require(r == 0, SUX_EINVAL, "reserved tuning fields must be 0");
     require(node, SUX_EINVAL, "NULL node");
     std::lock_guard<std::mutex> lk(node->mu);
@@ -1155,6 +1166,10 @@ int sux_node_destroy(sux_node* node) {
       node->pool->put(node->pipe_ws[i]);
     }
     for (hipEvent_t e : node->pipe_ev)
+      if (e) (void)hipEventDestroy(e);
+    for (hipStream_t p : node->pipe_split)
+      if (p) (void)hipStreamDestroy(p);
+    for (hipEvent_t e : node->split_ev)
       if (e) (void)hipEventDestroy(e);
     if (node->d_err) (void)hipFree(node->d_err);
     for (auto& kv : node->shuffles) release_shuffle(node, *kv.second);
@@ -1316,10 +1331,37 @@ int sux_partition_maps_pipelined(sux_node* node, const sux_partitioner* part,
       }
     }
     hipStream_t s = node->stream(stream);
-    hip_check(hipEventRecord(node->pipe_ev[0], s), "fork");
-    for (hipStream_t p : node->pipe) hip_check(hipStreamWaitEvent(p, node->pipe_ev[0], 0), "fork");
     const uint8_t* recs = static_cast<const uint8_t*>(d_records);
     uint8_t* out = static_cast<uint8_t*>(d_out);
+    const int split = resolve_tuning(node->tuning, true).split_cus;
+    if (split > 0 && sux::stream_cus(s) == node->device_cus()) {
+      // split mode: K1 of group g on `split` CUs (pipe_split[0]) beside K2 + K3 of group g - 1
+      // on the other CUs (pipe_split[1]) — K1 streams at nearly its full rate on a quarter of
+      // the CUs while K3, which scales with its CUs, keeps the rest (tools/cu_split_probe.py).
+      // A group's workspace slot is reused by group g + 2: its K1 waits for K3 of group g.
+      node->make_split(split);
+      hipStream_t h = node->pipe_split[0], k = node->pipe_split[1];
+      hip_check(hipEventRecord(node->pipe_ev[0], s), "fork");
+      hip_check(hipStreamWaitEvent(h, node->pipe_ev[0], 0), "fork");
+      hip_check(hipStreamWaitEvent(k, node->pipe_ev[0], 0), "fork");
+      for (uint64_t r0 = 0, g = 0; r0 < n; r0 += group_records, ++g) {
+        const uint64_t r1 = std::min(n, r0 + group_records), m0 = r0 / rpm;
+        const Group G = make_group(part, recs + r0 * rs, rs, rpm, r1 - r0);
+        if (g >= 2) hip_check(hipStreamWaitEvent(h, node->split_ev[2 + g % 2], 0), "slot free");
+        run_group(node, part, G, 1, out + r0 * rs, d_index + m0 * (R + 1),
+                  d_index_be ? d_index_be + m0 * (R + 1) * 8 : nullptr, nullptr, nullptr,
+                  node->pipe_ws[g % 2].ptr, node->pipe_ws[g % 2].cap, k, true, h,
+                  node->split_ev[g % 2]);
+        hip_check(hipEventRecord(node->split_ev[2 + g % 2], k), "slot done");
+      }
+      hip_check(hipEventRecord(node->pipe_ev[1], k), "join");
+      hip_check(hipStreamWaitEvent(s, node->pipe_ev[1], 0), "join");
+      hip_check(hipEventRecord(node->pipe_ev[2], h), "join");
+      hip_check(hipStreamWaitEvent(s, node->pipe_ev[2], 0), "join");
+      return;
+    }
+    hip_check(hipEventRecord(node->pipe_ev[0], s), "fork");
+    for (hipStream_t p : node->pipe) hip_check(hipStreamWaitEvent(p, node->pipe_ev[0], 0), "fork");
     for (uint64_t r0 = 0, g = 0; r0 < n; r0 += group_records, ++g) {
       const uint64_t r1 = std::min(n, r0 + group_records), m0 = r0 / rpm;
       const Group G = make_group(part, recs + r0 * rs, rs, rpm, r1 - r0);
@@ -3689,34 +3731,63 @@ int sux_sort_segments(sux_node* node, int32_t key_kind, const void* d_in, uint64
 // take the reserved CUs round-robin over all 32 (XCD, SE) pairs: keep C a multiple of 32.
 static uint32_t reserved_cu(uint32_t k) { return k; }
 
+// A stream on num_cus CUs picked round robin over the (XCD, SE) pairs, or on the other CUs.
+static hipStream_t create_cu_stream(sux_node* node, int32_t num_cus, int32_t complement) {
+  const uint32_t P = (uint32_t)node->device_cus();
+  require(num_cus >= 0 && (uint32_t)num_cus <= P, SUX_EINVAL,
+          "num_cus must be in [0, " + std::to_string(P) + "]");
+  hipStream_t st = nullptr;
+  if (num_cus == 0 || (uint32_t)num_cus == P) {
+    // nothing to partition: an ordinary stream (all CUs, or all CUs for the complement of 0)
+    require(!(num_cus == (int32_t)P && complement), SUX_EINVAL, "empty CU set");
+    require(!(num_cus == 0 && !complement), SUX_EINVAL, "empty CU set");
+    hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+  } else {
+    std::vector<uint32_t> mask((P + 31) / 32, 0u);
+    std::vector<uint8_t> pick(P, 0);
+    for (uint32_t k = 0; k < (uint32_t)num_cus; ++k) {
+      uint32_t i = reserved_cu(k);
+      pick[i] = 1;
+    }
+    for (uint32_t i = 0; i < P; ++i)
+      if (pick[i] != (complement ? 1 : 0)) mask[i / 32] |= 1u << (i % 32);
+    hip_check(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()),
+              "hipExtStreamCreateWithCUMask");
+  }
+  return st;
+}
+
+int sux_node::device_cus() {
+  if (!cus) {
+    hipDeviceProp_t prop;
+    hip_check(hipGetDeviceProperties(&prop, conf.device), "hipGetDeviceProperties");
+    cus = prop.multiProcessorCount;
+  }
+  return cus;
+}
+
+void sux_node::make_split(int n) {  // pipe_mu held
+  if (pipe_split_cus != n) {
+    for (hipStream_t& p : pipe_split) {
+      if (p) {
+        hip_check(hipStreamSynchronize(p), "split stream drain");
+        (void)hipStreamDestroy(p);
+        p = nullptr;
+      }
+    }
+    pipe_split[0] = create_cu_stream(this, n, 0);
+    pipe_split[1] = create_cu_stream(this, n, 1);
+    pipe_split_cus = n;
+  }
+  for (hipEvent_t& e : split_ev)
+    if (!e) hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "split event");
+}
+
 int sux_stream_create(sux_node* node, int32_t num_cus, int32_t complement, void** out) {
   return guard([&] {
     require(node && out, SUX_EINVAL, "NULL argument");
     node->bind();
-    hipDeviceProp_t prop;
-    hip_check(hipGetDeviceProperties(&prop, node->conf.device), "hipGetDeviceProperties");
-    const uint32_t P = (uint32_t)prop.multiProcessorCount;
-    require(num_cus >= 0 && (uint32_t)num_cus <= P, SUX_EINVAL,
-            "num_cus must be in [0, " + std::to_string(P) + "]");
-    hipStream_t st = nullptr;
-    if (num_cus == 0 || (uint32_t)num_cus == P) {
-      // nothing to partition: an ordinary stream (all CUs, or all CUs for the complement of 0)
-      require(!(num_cus == (int32_t)P && complement), SUX_EINVAL, "empty CU set");
-      require(!(num_cus == 0 && !complement), SUX_EINVAL, "empty CU set");
-      hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
-    } else {
-      std::vector<uint32_t> mask((P + 31) / 32, 0u);
-      std::vector<uint8_t> pick(P, 0);
-      for (uint32_t k = 0; k < (uint32_t)num_cus; ++k) {
-        uint32_t i = reserved_cu(k);
-        pick[i] = 1;
-      }
-      for (uint32_t i = 0; i < P; ++i)
-        if (pick[i] != (complement ? 1 : 0)) mask[i / 32] |= 1u << (i % 32);
-      hip_check(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()),
-                "hipExtStreamCreateWithCUMask");
-    }
-    *out = st;
+    *out = create_cu_stream(node, num_cus, complement);
   });
 }
 

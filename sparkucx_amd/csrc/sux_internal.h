@@ -65,6 +65,8 @@ struct Tuning {
   int gather_kernel = 3;    // the sort's record gather: 1 its own launch in 16-byte units, 2 its
                             // own launch, one dword per lane, 3 fused into the bucket sort
   bool gather16 = true;     // (1 and 3) 16-byte units
+  int split_cus = 0;        // sux_partition_maps_pipelined: K1 on this many CUs beside the
+                            // previous group's K3 on the others (0: one stream per group)
 };
 
 // Per-launch geometry of a group of consecutive map batches.
@@ -155,7 +157,8 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g, const La
                                   uint8_t* d_out, int64_t* d_index, uint8_t* d_index_be,
                                   uint16_t* d_pids, uint8_t* d_ws, const Workspace& ws,
                                   uint64_t* d_peer_bytes, const Tuning& tn, Timer* timer,
-                                  hipStream_t s);
+                                  hipStream_t s, hipStream_t s_k1 = nullptr,
+                                  hipEvent_t k1_done = nullptr);
 hipError_t launch_varlen_group(const PartDev& pd, const VarGroup& g, uint8_t* d_out,
                                int64_t* d_index, uint8_t* d_index_be, const uint16_t* d_pids_in,
                                uint16_t* d_pids, uint8_t* d_ws, const VarWorkspace& ws,

@@ -1677,7 +1677,7 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g_in, const
                                   uint8_t* d_out, int64_t* d_index, uint8_t* d_index_be,
                                   uint16_t* d_pids, uint8_t* d_ws, const Workspace& ws,
                                   uint64_t* d_peer_bytes, const Tuning& tn, Timer* timer,
-                                  hipStream_t s) {
+                                  hipStream_t s, hipStream_t s_k1, hipEvent_t k1_done) {
   MapGroup g = g_in;  // counts_tm is decided below, with the K1 / K3 pair
   g.counts_tm = 0;
   const int R = pd.R;
@@ -1686,6 +1686,8 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g_in, const
   // with static work items, workgroups beyond the resident ones would start only after a
   // resident one finished ALL its items
   const uint32_t ncu = (uint32_t)std::max(1, stream_cus(s));
+  const hipStream_t s_main = s;
+  const uint32_t ncu_main = ncu;
   // one pass (sux_onepass.hip) whenever a map batch fits on chip: every record read once
   uint32_t op_grid = 0, op_cs = 0;
   if (tn.onepass && ws.op_bytes && onepass_eligible(pd, g, lay.world, d_out, d_peer_bytes, s, &op_grid, &op_cs)) {
@@ -1752,8 +1754,13 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g_in, const
   g.counts_tm = (hist == 4 && (v8 || v7) && tn.counts_tm) ? 1u : 0u;
   timer_note(timer, kHist, hist == 16 ? "k_hist16" : hist == 4 ? "k_hist4" : hist == 3 ? "k_hist3"
                                                                                : "k_hist");
-  timer_begin(timer, kHist, s);
   hipError_t e = hipSuccess;
+  {
+  // K1 on its own stream when given one (sux_partition_maps_pipelined's split mode: K1 of group
+  // g on a few CUs beside group g - 1's K3 on the others); K2 and K3 wait for it on s
+  hipStream_t s = s_k1 ? s_k1 : s_main;
+  const uint32_t ncu = s_k1 ? (uint32_t)std::max(1, stream_cus(s_k1)) : ncu_main;
+  timer_begin(timer, kHist, s);
   if (hist == 16) {
     e = launch_hist16(pd, g, pids, counts, s);
   } else if (hist == 4) {
@@ -1820,8 +1827,14 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g_in, const
       hipLaunchKernelGGL((k_hist<1>), grid1, dim3(kWave), lds1, s, pd, g, pids, counts);
   }
   timer_end(timer, kHist, s);
+  }
   if (e == hipSuccess) e = hipGetLastError();
   if (e != hipSuccess) return e;
+  if (s_k1) {
+    e = hipEventRecord(k1_done, s_k1);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s_main, k1_done, 0);
+    if (e != hipSuccess) return e;
+  }
 
   // ---- K2: scans -> index tables + destination bases
   timer_begin(timer, kScan, s);

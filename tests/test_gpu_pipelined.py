@@ -66,6 +66,30 @@ def test_pipelined_coresident_shapes(gpu_node, tuned, co):
     gp.close()
 
 
+@pytest.mark.parametrize("split", [32, 64, 96, 224])
+@pytest.mark.parametrize("R,n,rpm,gmaps", [
+    (200, 7 * 20000 + 1234, 20000, 2),     # 4 groups: both workspace slots reused
+    (200, 9 * 8192, 8192, 1),              # 9 one-map groups
+    (64, 50000, 50000, 3),                 # one group
+    (1000, 5 * 12000 + 17, 12000, 2),
+])
+def test_pipelined_split_mode_matches_oracle(gpu_node, tuned, split, R, n, rpm, gmaps):
+    """split_cus: K1 of group g on `split` CUs beside K2 + K3 of group g - 1 on the others
+    (workspace slots reused by group g + 2 behind an event); twice in a row on one node, the
+    second call reusing the split streams.  Bytes and both index forms vs the oracle."""
+    tuned(split_cus=split)
+    recs = O.gen_terasort(33 + split, 0, n)
+    opart = O.terasort_partitioner(R)
+    gp = gpu_part(gpu_node, opart)
+    d = torch.from_numpy(recs).cuda()
+    for _ in range(2):
+        out, index, index_be = gpu_node.partition_maps_pipelined(gp, d, 100, rpm,
+                                                                 group_records=gmaps * rpm)
+        torch.cuda.synchronize()
+        expect(opart, recs, 100, rpm, out, index, index_be)
+    gp.close()
+
+
 @pytest.mark.parametrize("kind,key_len,off", [(O.MURMUR3_LONG, 8, 0), (O.HASH_INT, 4, 4),
                                               (O.MURMUR3_BYTES, 12, 8)])
 def test_pipelined_hash_kinds_and_skew(gpu_node, kind, key_len, off):
