@@ -8,7 +8,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.environ.get("SUX_PKG_ROOT") or os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from sparkucx_amd import native as N  # noqa: E402
 from sparkucx_amd.shuffle import Node  # noqa: E402
 
@@ -46,6 +46,13 @@ def main():
     tk = node.generate(N.GEN_TERASORT, 27, 0, n, 100).view(n, 100).clone()
     tk[:, 1:10] = 0  # keys vary in their first byte only: the top pass finishes the sort
     cases["top_digit_only_5M"] = (tk.view(-1), n, 100, N.SORT_BYTES, 0, 10)
+    ns = 32 << 20  # the bench's reduce_sort_long: int64 keys in [0, 2^31) + int64 values
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    rows = torch.empty((ns, 2), dtype=torch.int64, device="cuda")
+    rows[:, 0] = torch.randint(0, 1 << 31, (ns,), generator=g, device="cuda")
+    rows[:, 1] = torch.arange(ns, device="cuda")
+    cases["long_2e31_32M"] = (rows.view(torch.uint8).view(-1), ns, 16, N.SORT_LONG, 0, 8)
     res = {}
     only = os.environ.get("CASES")
     for name, (recs, nn, rs, kind, off, klen) in cases.items():
