@@ -2,15 +2,21 @@
 // records by key, the step Spark's reader runs after the fetch when the dependency has a key
 // ordering (ExternalSorter, compat/spark_3_0/UcxShuffleReader.scala:138-154; TeraSort's reducer).
 //
-// LSD radix sort over 16-byte (key, index) pairs, then one gather of the whole records:
-//   k_sort_pairs    record i -> pair {key as big-endian bytes [0, 12), i as u32 LE at [12, 16)};
-//                   signed keys get their sign bit flipped so unsigned order = signed order;
-//                   also the AND / OR of all key words (k_span_reduce), so that digit passes
-//                   whose bits never vary are skipped
-//   digit passes    stable partitions of the pairs by a 12-bit digit of the big-endian 128-bit
-//                   pair value (least significant key digit first) — the map-side kernels with
-//                   the internal radix partitioner (kind 7, R = 4096: k_hist16 + k_scatter16)
-//   k_gather_records out record j = in record pairs[j].index (coalesced dword writes)
+// Default path (planned on the device, no host wait, graph-capturable):
+//   k_sort_pairs    record i -> 16-byte pair {order key big-endian in [0, 12), i as u32 LE at
+//                   [12, 16)} (or, for records of <= 16 bytes with the segment id, the record
+//                   itself re-laid so its key leads: inline mode); signed keys get their sign bit
+//                   flipped so unsigned order = signed order; per-block AND / OR of the key words
+//   k_span_reduce + k_sort_plan   the key span -> the top digit (the tb highest varying bits)
+//                   and the 8-bit LDS digits below it that vary (SortPlanDev)
+//   top pass        one stable partition of the pairs by the top digit (the map-side small-record
+//                   kernels with the internal radix partitioner, digit shift read on the device)
+//   k_sort_local    every bucket of <= 4096 pairs sorted inside LDS by the lower digits; in
+//                   gather mode it then gathers the bucket's records straight into the output
+//                   (k_sort_bucket_global sorts larger buckets through global memory,
+//                   k_gather_rest gathers them); inline mode ends in k_unpair_records
+// LSD path (sort_msd = 2, sort_all_passes, or more pairs than 2^14 LDS buckets hold): 12-bit
+// digit passes with the constant ones skipped after a host read of the span, then the gather.
 // Equal keys keep their input order (every pass is stable and the index is never a digit).
 // Segmented (sux_sort_segments): the record's segment id, big-endian, sits above the key bytes,
 // so one sort orders every segment (a reducer's partitions) in place.
