@@ -618,7 +618,8 @@ __global__ __launch_bounds__(256) void k_gather_rest(const u32x4* __restrict__ p
 
 // Buckets above kSortLocalCap (skewed keys: heavy hitters, long duplicate runs): one
 // 1024-thread workgroup per bucket runs a stable LSD over the plan's digits through global
-// memory — per digit a count sweep and a ranked scatter sweep in 4096-element chunks (wave-ballot
+// memory — one counting sweep for every digit, then per varying digit a ranked scatter sweep in
+// 4096-element chunks (wave-ballot
 // ranks + one (digit, wave) scan per chunk, per-digit cursors carried across chunks), ping-ponging
 // between the bucket's range of the top pass's output (`in`) and of the final buffer (`out`), and
 // ends in `out` (one copy when the digit count is even).  Slow per bucket (one CU), but only a
@@ -635,7 +636,8 @@ __global__ __launch_bounds__(NW * 64) void k_sort_bucket_global(u32x4* __restric
   __shared__ uint32_t wc[NW * NB];
   __shared__ uint32_t wsum[NW];
   __shared__ uint32_t cur[NB];
-  __shared__ uint32_t span[6];
+  __shared__ uint32_t hist[16 * NB];  // [digit][value] counts of the bucket (SortDigits: <= 16)
+  __shared__ uint32_t one_bin;
   const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
   const uint64_t lt_mask = (1ull << lane) - 1ull;
   for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
@@ -646,54 +648,56 @@ __global__ __launch_bounds__(NW * 64) void k_sort_bucket_global(u32x4* __restric
     if (n <= kSortLocalCap) continue;  // k_sort_local's
     u32x4* src = in + s0;
     u32x4* dst = out + s0;
-    // the bucket's own key span (AND / OR of the key words): a digit constant inside the bucket
-    // is an identity pass and is skipped — a heavy hitter's bucket of equal keys skips them all
-    // (500 000 equal TeraSort keys: 10.3 ms of count + scatter sweeps by one workgroup)
-    if (tid < 3) {
-      span[tid] = ~0u;
-      span[3 + tid] = 0u;
-    }
+    // ONE counting sweep for every digit (the per-digit count sweeps read the bucket once more
+    // per digit): each wave's equal digits are matched by ballots and added by their first lane
+    // (one LDS atomic per distinct digit value per wave, so a heavy hitter's equal keys do not
+    // serialise on one counter).  A digit whose histogram is one bin is constant inside the
+    // bucket — an identity pass, skipped (a bucket of equal keys skips them all).
+    for (uint32_t i = tid; i < 16 * NB; i += NT) hist[i] = 0;
     __syncthreads();
-    {
-      uint32_t a0 = ~0u, a1 = ~0u, a2 = ~0u, o0 = 0u, o1 = 0u, o2 = 0u;
-      for (uint32_t e = tid; e < n; e += NT) {
-        const u32x4 x = src[e];
-        a0 &= x[0], a1 &= x[1], a2 &= x[2], o0 |= x[0], o1 |= x[1], o2 |= x[2];
+    for (uint32_t c0 = 0; c0 < n; c0 += CH) {
+      u32x4 v[PT];
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) {
+        const uint32_t e = c0 + wave * (PT * kWave) + j * kWave + lane;
+        v[j] = src[e < n ? e : n - 1];
       }
-      atomicAnd(&span[0], a0), atomicAnd(&span[1], a1), atomicAnd(&span[2], a2);
-      atomicOr(&span[3], o0), atomicOr(&span[4], o1), atomicOr(&span[5], o2);
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) {
+        const uint32_t e = c0 + wave * (PT * kWave) + j * kWave + lane;
+        const bool valid = e < n;
+        for (int d = 0; d < dg.n; ++d) {
+          const uint64_t w = d < 8 ? dg.lo : dg.hi;
+          const uint32_t dig = pair_digit8(v[j], (uint32_t)(w >> (8 * (d & 7))) & 255u);
+          uint64_t peers = __ballot(valid);
+#pragma unroll
+          for (uint32_t bb = 0; bb < 8; ++bb) {
+            const bool bit = (dig >> bb) & 1u;
+            const uint64_t m = __ballot(bit);
+            peers &= bit ? m : ~m;
+          }
+          if (valid && (peers & lt_mask) == 0) atomicAdd(&hist[d * NB + dig], (uint32_t)__popcll(peers));
+        }
+      }
     }
     __syncthreads();
-    const u32x4 span_and{span[0], span[1], span[2], 0u}, span_or{span[3], span[4], span[5], 0u};
-    __syncthreads();  // read by every thread before the next bucket resets it
     for (int d = 0; d < dg.n; ++d) {
       const uint64_t w = d < 8 ? dg.lo : dg.hi;
       const uint32_t sh = (uint32_t)(w >> (8 * (d & 7))) & 255u;
-      if (pair_digit8(span_and, sh) == pair_digit8(span_or, sh)) continue;  // uniform
-      // count sweep -> exclusive digit starts in cur.  Per-wave counters through the ballot
-      // match (wave_rank): a wave's equal digits cost one LDS update — one LDS atomic per pair
-      // serialised a heavy hitter's equal keys on a single counter
-      for (uint32_t c0 = 0; c0 < n; c0 += CH) {
-#pragma unroll
-        for (uint32_t j = 0; j < PT; ++j) {
-          const uint32_t e = c0 + wave * (PT * kWave) + j * kWave + lane;
-          const bool valid = e < n;
-          const u32x4 p = src[valid ? e : n - 1];
-          (void)wave_rank<8>(valid ? pair_digit8(p, sh) : 0u, valid, wc + wave * NB, lt_mask);
-        }
-      }
+      // exclusive digit starts in cur; one bin holding every pair: the digit is constant
+      if (tid == 0) one_bin = 0;
       __syncthreads();
       uint32_t x = 0, incl = 0;
       if (tid < (int)NB) {
-#pragma unroll
-        for (uint32_t q = 0; q < NW; ++q) {
-          x += wc[q * NB + tid];
-          wc[q * NB + tid] = 0;  // zero again for the scatter sweep's ranks
-        }
+        x = hist[d * NB + tid];
+        if (x == n) one_bin = 1;
         incl = wave_incl_scan(x, lane);
         if (lane == kWave - 1) wsum[wave] = incl;
       }
       __syncthreads();
+      const bool constant = one_bin != 0;
+      __syncthreads();  // every thread has read one_bin before the next digit resets it
+      if (constant) continue;
       if (tid < (int)NB) {
         uint32_t base = 0;
         for (int q = 0; q < wave; ++q) base += wsum[q];
