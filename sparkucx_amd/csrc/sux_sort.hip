@@ -704,15 +704,28 @@ __global__ __launch_bounds__(NW * 64) void k_sort_bucket_global(u32x4* __restric
         cur[tid] = base + incl - x;
       }
       __syncthreads();
-      // ranked scatter, chunk by chunk in element order (stable)
+      // ranked scatter, chunk by chunk in element order (stable).  The next chunk's pairs are
+      // loaded while this one is ranked and scattered (src and dst are different buffers inside
+      // a digit pass): one workgroup's sweep otherwise waited a full memory round trip per chunk
+      u32x4 vn[PT];
+      auto load_chunk = [&](uint32_t c0, u32x4 (&x)[PT]) {
+#pragma unroll
+        for (uint32_t j = 0; j < PT; ++j) {
+          const uint32_t e = c0 + wave * (PT * kWave) + j * kWave + lane;
+          x[j] = src[e < n ? e : n - 1];
+        }
+      };
+      load_chunk(0, vn);
       for (uint32_t c0 = 0; c0 < n; c0 += CH) {
         u32x4 v[PT];
         uint32_t dig[PT], rank[PT];
 #pragma unroll
+        for (uint32_t j = 0; j < PT; ++j) v[j] = vn[j];
+        if (c0 + CH < n) load_chunk(c0 + CH, vn);  // uniform
+#pragma unroll
         for (uint32_t j = 0; j < PT; ++j) {
           const uint32_t e = c0 + wave * (PT * kWave) + j * kWave + lane;
           const bool valid = e < n;
-          v[j] = src[valid ? e : n - 1];
           dig[j] = valid ? pair_digit8(v[j], sh) : 0u;
           rank[j] = wave_rank<8>(dig[j], valid, wc + wave * NB, lt_mask);
         }
