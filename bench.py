@@ -615,6 +615,48 @@ def load_traffic(workload: str, kernel: str) -> dict | None:
         return None
 
 
+def launched_rank() -> bool:
+    """True when a launcher (torch.distributed.run / torchrun / the driver) started this process
+    as one rank of a job: it exports WORLD_SIZE and RANK."""
+    return "WORLD_SIZE" in os.environ and "RANK" in os.environ
+
+
+def launch_ranks(args) -> int:
+    """`python bench.py --gpus N` (N > 1) with no launcher: start the N ranks as CHILD processes
+    (python -m torch.distributed.run, one rank per GPU, rendezvous on 127.0.0.1), relay rank 0's
+    JSON line, and return the children's exit status.  Runs before this process touches the GPU
+    (no HIP call has been made: torch's CUDA state is initialised lazily, the library is loaded
+    but not called), and it never replaces itself (no exec): the parent only waits and relays."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__), *sys.argv[1:]]
+    log(f"bench: --gpus {args.gpus} without a launcher: starting {args.gpus} ranks: "
+        + " ".join(cmd))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    # the ranks' stderr is inherited (progress stays visible); their stdout carries rank 0's line
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, env=env)
+    lines = [l for l in p.stdout.decode(errors="replace").splitlines() if l.startswith("{")]
+    if p.returncode != 0:
+        log(f"bench: the {args.gpus} ranks exited with status {p.returncode}")
+        return p.returncode
+    if len(lines) != 1:
+        log(f"bench: expected one JSON line from rank 0, got {len(lines)}")
+        return 1
+    res = json.loads(lines[0])
+    if res.get("n_gpus") != args.gpus:
+        log(f"bench: rank 0 reported n_gpus={res.get('n_gpus')} for --gpus {args.gpus}")
+        return 1
+    res["launch"] = f"bench.py started {args.gpus} ranks (torch.distributed.run, child processes)"
+    sys.stdout.write(json.dumps(res) + "\n")
+    sys.stdout.flush()
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -685,6 +727,11 @@ def main():
                     help="test mode (N>1): check every received block of every group against "
                          "the CPU oracle; timing is then not a benchmark")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and not launched_rank():
+        # no launcher: this process becomes the parent of the N ranks (before any GPU call)
+        sys.exit(launch_ranks(args))
     # stdout carries exactly one JSON line: RCCL and the HIP runtime print banners from C code,
     # so file descriptor 1 goes to stderr for the whole run and the result is written to a
     # duplicate of the original stdout
@@ -696,7 +743,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+        # a line whose n_gpus differs from --gpus would misreport the scaling curve
+        raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} "
+                         "ranks; pass --gpus equal to --nproc-per-node")
     rehearse = args.rehearse_one_gpu and world > 1
     if rehearse:
         args.transport, local = "ipc", 0
@@ -1210,11 +1259,19 @@ def main():
         vr = args.varlen_rows if args.varlen_rows > 0 else 32 << 20
         result["varlen"] = varlen_leg(node, vr, min(vr, 1 << 20), 200, dev,
                                       compress=args.compress_maps != 0)
-    if rank == 0 and not pipelined and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
+        # the reference CPU shuffle beside every line, N > 1 included (north_star: "at 1, 2, 4
+        # and 8 GPUs beside the reference CPU shuffle"): the same bounded sample on rank 0's host
+        # cores.  Rank 0's shard starts at global record 0, so its first records ARE the
+        # sample, and the GPU parity check partitions them on this rank's device.
         cpu_n = min(args.cpu_records, n)
         args.cpu_records = cpu_n
         result["cpu_baseline"] = cpu_baseline(
             args, seed, node, part, data if args.workload == "terasort" and R == 200 else None)
+        if world > 1 and result["cpu_baseline"]:
+            result["cpu_baseline"]["beside"] = f"N={world}: rank 0 only, after the timed steps"
+    if world > 1:
+        dist.barrier()  # the other ranks wait for rank 0's baseline before tearing down
     if rank == 0:
         os.write(result_fd, (json.dumps(result) + "\n").encode())
     node.close()

@@ -2,6 +2,10 @@
 sizing, and the untimed self-check every bench line carries (it must pass on a correct map-side
 output and reject a corrupted one).  The self-check runs here on CPU tensors, with the CPU oracle
 standing in for the device's k_pids kernel (test infrastructure only)."""
+import os
+import subprocess
+import sys
+
 import numpy as np
 import pytest
 import torch
@@ -84,3 +88,30 @@ def test_self_check_rejects_a_wrong_index_table():
     def shift(out, index, rs, rpm):
         index[3] += rs
     _expect_reject(shift)
+
+
+def _bench_cmd(*args):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    return [sys.executable, os.path.join(root, "bench.py"), *args]
+
+
+def test_bench_refuses_a_world_size_other_than_gpus():
+    """A rank whose launcher started a different number of ranks than --gpus stops before it
+    touches a GPU: its line would misreport n_gpus."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run(_bench_cmd("--gpus", "2"), capture_output=True, text=True, env=env,
+                       timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_bench_without_a_launcher_starts_its_ranks():
+    """--gpus 2 and no WORLD_SIZE: bench.py becomes the parent of two ranks (torch.distributed.run
+    child processes).  Without a GPU the ranks fail; the parent reports their status and prints
+    no result line."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run(_bench_cmd("--gpus", "2", "--records", "1000"), capture_output=True,
+                       text=True, env=env, timeout=300)
+    assert "starting 2 ranks" in r.stderr and "torch.distributed.run" in r.stderr
+    assert r.returncode != 0 and "ranks exited with status" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]

@@ -71,3 +71,27 @@ def test_bench_eight_ranks_plugin_leg_after_the_pipeline():
     res = _run(8, "--records", "4194304", "--map-records", "524288", "--group-maps", "2",
                "--plugin-groups", "4", "--steps", "1", "--warmup", "0", "--self-check", "0")
     assert res["plugin"]["self_check"] == "ok" and res["plugin"]["maps"] == 4 * 8 * 2
+
+
+def test_bench_starts_its_own_ranks():
+    """`python bench.py --gpus 2` with no launcher: bench.py starts its two ranks itself (child
+    processes of torch.distributed.run), relays rank 0's line, and that line carries the N > 1
+    self-check, the exchange roofline and the CPU baseline beside it."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rehearse-one-gpu",
+           "--records", "3000000", "--map-records", "262144", "--group-maps", "2", "--steps", "1",
+           "--warmup", "0", "--plugin-groups", "0", "--cpu-records", "1000000", "--cpu-reps", "1"]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300,
+                       env=dict(env, OMP_NUM_THREADS="1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "starting 2 ranks" in r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["value"] > 0
+    assert res["self_check"]["ok"]
+    assert res["roofline_exchange"]["remote_bytes_per_rank"] > 0
+    cb = res["cpu_baseline"]
+    assert cb and cb["value"] > 0 and cb["cores"] >= 1
+    assert cb["parity"]["index_tables_equal"] and cb["parity"]["fetch_checksum_equal"]
