@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define SUX_ABI_VERSION 4
+#define SUX_ABI_VERSION 5
 
 /* ---- status codes ---------------------------------------------------------------------- */
 #define SUX_OK 0
@@ -125,13 +125,36 @@ typedef int (*sux_allgather_fn)(void* ctx, uint64_t tag, const void* send, uint6
                                 void* recv);
 int sux_node_set_bootstrap(sux_node* node, sux_allgather_fn fn, void* ctx);
 
+/* ---- executor group membership (driver side) --------------------------------------------- *
+ * The reference's executors introduce themselves to the driver with their BlockManagerId
+ * (UcxNode.startExecutor, UcxNode.java:111-145) and the driver fans every address out to every
+ * peer (RpcConnectionCallback.java:47-89).  The executors of a GPU group all start from the SAME
+ * SparkConf, so nothing in it can tell an executor its rank: the driver keeps one sux_group per
+ * application and answers each executor's hello with its rank, in order of first arrival, keyed
+ * by executor id (a repeated hello — a lost reply, a retried RPC — gets the same answer), and its
+ * local index = how many executors of the same host joined before it: the GPU an executor takes
+ * when Spark assigned it none.  Host-only (no HIP call, usable on a driver without a GPU) and
+ * thread-safe.  An executor that joins a complete group is SUX_ERANGE (the group is formed once:
+ * an RCCL communicator cannot take a replacement rank). */
+typedef struct sux_group sux_group;
+int sux_group_create(int32_t world_size, sux_group** out);
+int sux_group_destroy(sux_group* group);
+int sux_group_join(sux_group* group, const char* executor_id, const char* host, int32_t* rank,
+                   int32_t* local_index);
+/* Executors joined so far. */
+int sux_group_size(sux_group* group, int32_t* joined);
+
 /* HBM-capacity fallback (the reference serves every block from Spark's disk files,
  * CommonUcxShuffleBlockResolver.scala:45-58; here map outputs live in HBM): when the device pool
- * cannot hold a new map output, the node writes committed map outputs of its shuffles (world 1,
- * or maps whose ranges were already exchanged) to Spark's data + index files under `dir`
- * (spark.local.dir), frees their device memory and retries.  Spilled blocks are served by
- * sux_fetch_blocks from the files; sux_resolve_blocks reports them as not device-resident.
- * NULL or "" disables spilling (allocation failures then return SUX_ENOMEM). */
+ * cannot hold a new map output, the node writes committed map outputs of its shuffles to
+ * Spark's data + index files under `dir` (spark.local.dir), frees their device memory and
+ * retries.  Spilling runs at world size 1 only (a node of a larger group never spills: its peers
+ * may read its slabs).  A shuffle any of whose blocks sux_resolve_blocks returned is never
+ * spilled before sux_unregister_shuffle (its addresses are read without a reference).  Spilled
+ * blocks are served by sux_fetch_blocks from the files; sux_resolve_blocks reports them as not
+ * device-resident.  `dir` should be private to this executor and application (two nodes spilling
+ * into one directory would overwrite each other's files) and must exist.  NULL or ""
+ * disables spilling (allocation failures then return SUX_ENOMEM). */
 int sux_node_set_spill_dir(sux_node* node, const char* dir);
 /* Map outputs spilled so far by this node. */
 int sux_node_spills(sux_node* node, uint64_t* spilled_maps);
@@ -418,9 +441,10 @@ int sux_commit_map_output(sux_node* node, int32_t shuffle_id, int32_t map_index,
 /* writeIndexFileAndCommit for map outputs a stateless call (sux_partition_maps*) already wrote
  * into the caller's device memory: maps first_map_index .. of records_per_map records each, map m
  * at d_out + m*records_per_map*record_size (the shuffle's record size), native index tables in
- * d_index (num_maps*(R+1) int64, device).  Nothing is copied: the node keeps the pointers (the
- * caller keeps the memory alive and unchanged until sux_unregister_shuffle) and reads the index
- * tables back asynchronously on `stream`; the maps are published like sux_write_map_outputs
+ * d_index (num_maps*(R+1) int64, device).  Nothing is copied: the node keeps BOTH pointers —
+ * d_out and d_index must stay allocated and unchanged until sux_unregister_shuffle (at world 1
+ * the index tables are read from d_index when blocks are resolved; at world > 1 they are also
+ * read back on `stream` for the directory).  The maps are published like sux_write_map_outputs
  * (first commit wins).  The Spark analog is a writer whose output Spark did not copy. */
 int sux_adopt_map_outputs(sux_node* node, int32_t shuffle_id, int32_t first_map_index,
                           const void* d_out, uint64_t records_per_map, uint64_t num_records,
@@ -494,7 +518,9 @@ typedef struct sux_block_id {
  * with SUX_ENOENT and names it in sux_last_error(). */
 int sux_fetch_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* blocks, int32_t n,
                      int64_t* sizes, sux_buffer** out, void* stream);
-/* Zero-copy resolve: device address and size of each block (no copy; local blocks only). */
+/* Zero-copy resolve: device address and size of each block (no copy; local blocks only).  No
+ * reference is taken: the addresses stay valid until sux_unregister_shuffle of this shuffle —
+ * from this call on, the node never spills the shuffle's map outputs (sux_node_set_spill_dir). */
 int sux_resolve_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* blocks, int32_t n,
                        uint64_t* dev_addrs, int64_t* sizes);
 int sux_buffer_info(sux_buffer* buf, void** dev_ptr, uint64_t* size, uint64_t* capacity);

@@ -423,6 +423,10 @@ struct Shuffle {
   int busy = 0;        // jobs taken out of `jobs` by a thread that is waiting on them
   int submitting = 0;  // writes that claimed slots and have not queued their job yet
   bool exchanging = false;
+  // sux_resolve_blocks handed out raw device addresses of this shuffle's map outputs: callers
+  // read them without holding a reference, so its slabs are never spilled (spill_some) until
+  // the shuffle is unregistered
+  bool zero_copy = false;
   int32_t next_batch = 0;
   // exchanges enqueued and not yet waited for (sux_exchange_wait): their completion events and,
   // with the IPC transport, whether the closing all-gather (every peer finished its pulls) is due
@@ -456,6 +460,19 @@ struct sux_node {
   // mapped base -> (64-byte handle, references taken) — see ipc_open_fresh
   std::mutex ipc_mu;
   std::map<void*, std::pair<std::string, int>> ipc_maps;
+  // allocations this process exported (export_ipc): base -> (the allocation's buffer id, size,
+  // handle).  ONE handle per live allocation: the runtime may hand out a new handle per
+  // hipIpcGetMemHandle call (hsa_amd_ipc_memory_create: "repeated calls for the same allocation
+  // may ... return unique handles"), and an importer that opens two handles of one allocation
+  // gets one mapping under two keys — which ipc_open_fresh must be able to read as "the exporter
+  // freed the old allocation" (the IPC open failure of round 3)
+  struct IpcExport {
+    unsigned long long id;
+    size_t size;
+    uint8_t handle[64];
+  };
+  std::mutex export_mu;
+  std::map<void*, IpcExport> ipc_exports;
   sux_allgather_fn boot = nullptr;   // host all-gather of the embedding runtime
   void* boot_ctx = nullptr;
   sux_tuning tuning{};               // all zero = measured defaults (resolve_tuning)
@@ -743,6 +760,10 @@ void drain(sux_node* node, Shuffle& sh, std::unique_lock<std::mutex>& lk) {
   }
 }
 
+}  // namespace
+void export_ipc(sux_node* node, const void* p, uint8_t out[SUX_IPC_DESC_BYTES]);
+namespace {
+
 // Map a peer allocation by its 64-byte IPC handle.  The HIP runtime keys the mappings it hands
 // out by the exporter's address: when a peer frees an allocation this process still maps and its
 // allocator gives the address to a new allocation, opening the NEW handle returns the old mapping
@@ -757,17 +778,8 @@ void* ipc_open_fresh(sux_node* node, const uint8_t* handle) {
   const std::string key(reinterpret_cast<const char*>(handle), 64);
   for (int attempt = 0; attempt < 2; ++attempt) {
     void* base = nullptr;
-    // One W = 8 one-GPU rehearsal (8 processes importing each other's buffers at once) saw a
-    // single hipErrorInvalidDevicePointer from an open of a live, just-exported allocation that
-    // the same run opens fine otherwise (profiles/r03_v6/ipc_open_flake.txt): retried a few
-    // times, a few ms apart, before it is an error
-    hipError_t e = hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess);
-    for (int retry = 0; e == hipErrorInvalidDevicePointer && retry < 4; ++retry) {
-      (void)hipGetLastError();
-      std::this_thread::sleep_for(std::chrono::milliseconds(2 << retry));
-      e = hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess);
-    }
-    hip_check(e, "hipIpcOpenMemHandle");
+    hip_check(hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess),
+              "hipIpcOpenMemHandle");
     auto it = node->ipc_maps.find(base);
     if (it == node->ipc_maps.end()) {
       node->ipc_maps[base] = {key, 1};
@@ -1030,6 +1042,79 @@ int sux_node_set_bootstrap(sux_node* node, sux_allgather_fn fn, void* ctx) {
     std::lock_guard<std::mutex> lk(node->mu);
     node->boot = fn;
     node->boot_ctx = ctx;
+  });
+}
+
+// ---- executor group membership (driver side; host-only: no HIP call, so a driver without a
+// GPU, or a parent process that forks its executors, never initialises the runtime) ----------
+}  // extern "C"
+struct sux_group {
+  int32_t world = 0;
+  std::mutex mu;
+  std::map<std::string, std::pair<int32_t, int32_t>> members;  // executor id -> (rank, local)
+  std::map<std::string, int32_t> per_host;                     // host -> executors joined
+};
+
+namespace {
+template <class F>
+int host_guard(F&& f) {
+  try {
+    f();
+    return SUX_OK;
+  } catch (const SuxError& e) {
+    g_err = e.msg;
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    g_err = "host allocation failed";
+    return SUX_ENOMEM;
+  } catch (...) {
+    g_err = "unknown error";
+    return SUX_EINVAL;
+  }
+}
+}  // namespace
+
+extern "C" {
+int sux_group_create(int32_t world_size, sux_group** out) {
+  return host_guard([&] {
+    require(out, SUX_EINVAL, "NULL argument");
+    require(world_size >= 1, SUX_EINVAL, "world size must be >= 1");
+    auto g = std::make_unique<sux_group>();
+    g->world = world_size;
+    *out = g.release();
+  });
+}
+
+int sux_group_destroy(sux_group* group) {
+  return host_guard([&] { delete group; });
+}
+
+int sux_group_join(sux_group* group, const char* executor_id, const char* host, int32_t* rank,
+                   int32_t* local_index) {
+  return host_guard([&] {
+    require(group && executor_id && host && rank && local_index, SUX_EINVAL, "NULL argument");
+    const std::string id(executor_id);
+    require(!id.empty(), SUX_EINVAL, "empty executor id");
+    std::lock_guard<std::mutex> lk(group->mu);
+    auto it = group->members.find(id);
+    if (it == group->members.end()) {
+      require((int32_t)group->members.size() < group->world, SUX_ERANGE,
+              "executor " + id + " joins a GPU group of " + std::to_string(group->world) +
+                  " that is already complete");
+      const int32_t r = (int32_t)group->members.size();
+      const int32_t l = group->per_host[host]++;
+      it = group->members.emplace(id, std::make_pair(r, l)).first;
+    }
+    *rank = it->second.first;
+    *local_index = it->second.second;
+  });
+}
+
+int sux_group_size(sux_group* group, int32_t* joined) {
+  return host_guard([&] {
+    require(group && joined, SUX_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(group->mu);
+    *joined = (int32_t)group->members.size();
   });
 }
 
@@ -1751,6 +1836,7 @@ bool spill_some(sux_node* node, uint64_t need) {
   std::map<Slab*, size_t> at;
   for (auto& kv : node->shuffles) {
     Shuffle& sh = *kv.second;
+    if (sh.zero_copy) continue;  // resolved addresses may still be read
     for (int32_t m = 0; m < sh.num_maps; ++m) {
       MapSlot& sl = sh.maps[m];
       if (!(sl.present && !sl.spilled() && sl.slab && sl.slab->pool && sl.owner == node->conf.rank))
@@ -1999,17 +2085,8 @@ int sux_ipc_export(sux_node* node, const void* d_ptr, uint8_t out[SUX_IPC_DESC_B
   return guard([&] {
     require(node && d_ptr && out, SUX_EINVAL, "NULL argument");
     node->bind();
-    // the handle names the whole allocation (allocators sub-allocate): ship the offset too
-    hipDeviceptr_t base = nullptr;
-    size_t size = 0;
-    hip_check(hipMemGetAddressRange(&base, &size, const_cast<void*>(d_ptr)),
-              "hipMemGetAddressRange");
-    hipIpcMemHandle_t h;
-    static_assert(sizeof(h) == 64, "hipIpcMemHandle_t is 64 bytes");
-    hip_check(hipIpcGetMemHandle(&h, base), "hipIpcGetMemHandle");
-    const uint64_t off = (uint64_t)((const uint8_t*)d_ptr - (const uint8_t*)base);
-    std::memcpy(out, &h, 64);
-    std::memcpy(out + 64, &off, 8);
+    static_assert(sizeof(hipIpcMemHandle_t) == 64, "hipIpcMemHandle_t is 64 bytes");
+    export_ipc(node, d_ptr, out);
   });
 }
 
@@ -2559,16 +2636,34 @@ std::vector<DirEntry> gather_directory(sux_node* node, uint64_t tag, int R,
   return all;
 }
 
-void export_ipc(const void* p, uint8_t out[SUX_IPC_DESC_BYTES]) {
+}  // namespace
+
+// The 72-byte descriptor of device pointer p: the 64-byte IPC handle of the allocation holding
+// it (allocators sub-allocate: the handle names the whole allocation) + p's offset in it.  An
+// allocation is exported once while it lives: later calls return the cached handle, recognised
+// by the allocation's base, size and buffer id (HIP_POINTER_ATTRIBUTE_BUFFER_ID: unique per
+// allocation, so a new allocation at a freed one's address is exported afresh).
+void export_ipc(sux_node* node, const void* p, uint8_t out[SUX_IPC_DESC_BYTES]) {
   hipDeviceptr_t base = nullptr;
   size_t size = 0;
   hip_check(hipMemGetAddressRange(&base, &size, const_cast<void*>(p)), "hipMemGetAddressRange");
-  hipIpcMemHandle_t h;
-  hip_check(hipIpcGetMemHandle(&h, base), "hipIpcGetMemHandle");
+  unsigned long long id = 0;
+  hip_check(hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, base),
+            "hipPointerGetAttribute(BUFFER_ID)");
   const uint64_t off = (uint64_t)(static_cast<const uint8_t*>(p) - static_cast<const uint8_t*>(base));
-  std::memcpy(out, &h, 64);
+  std::lock_guard<std::mutex> lk(node->export_mu);
+  auto it = node->ipc_exports.find(base);
+  if (it == node->ipc_exports.end() || it->second.id != id || it->second.size != size) {
+    hipIpcMemHandle_t h;
+    hip_check(hipIpcGetMemHandle(&h, base), "hipIpcGetMemHandle");
+    sux_node::IpcExport e{id, size, {}};
+    std::memcpy(e.handle, &h, 64);
+    it = node->ipc_exports.insert_or_assign(base, e).first;
+  }
+  std::memcpy(out, it->second.handle, 64);
   std::memcpy(out + 64, &off, 8);
 }
+namespace {
 
 // Copy descriptors -> one gather-copy launch (64 KiB chunks, block i to its own destination).
 // `aux` (device tables) and `hostblk` (their pinned staging) stay with the caller until the
@@ -2777,7 +2872,7 @@ int sux_exchange_maps(sux_node* node, int32_t shuffle_id, int32_t first, int32_t
     const bool ipc = node->comm == nullptr;
     // every batch slab is exported (the IPC transport pulls from it; with either transport any
     // rank may later read a block its owner serves from it)
-    for (size_t k = 0; k < mine.size(); ++k) export_ipc(mine_slab[k]->buf.ptr, mine[k].ipc);
+    for (size_t k = 0; k < mine.size(); ++k) export_ipc(node, mine_slab[k]->buf.ptr, mine[k].ipc);
     // 1. directory of the window (replaces the driver table + the phase-1 offset GETs)
     std::vector<DirEntry> all = gather_directory(node, tag, R, mine, s);
     const int n = (int)all.size();
@@ -2886,7 +2981,7 @@ int sux_exchange_maps(sux_node* node, int32_t shuffle_id, int32_t first, int32_t
     std::vector<uint8_t> rdesc((size_t)W * SUX_IPC_DESC_BYTES, 0);
     {
       std::vector<uint8_t> mine_desc(SUX_IPC_DESC_BYTES, 0);
-      if (recv->buf.ptr) export_ipc(recv->buf.ptr, mine_desc.data());
+      if (recv->buf.ptr) export_ipc(node, recv->buf.ptr, mine_desc.data());
       host_allgather(node, tag + 2, mine_desc.data(), SUX_IPC_DESC_BYTES, rdesc.data(), s);
     }
     std::vector<std::vector<uint64_t>> peer_off((size_t)W);
@@ -3189,6 +3284,10 @@ int sux_resolve_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* b
     Shuffle& sh = node->shuffle(shuffle_id);
     drain(node, sh, lk);
     const int R = sh.R;
+    // the addresses returned below are read with no reference held: pin the shuffle's slabs
+    // against spilling until it is unregistered (set before anything is returned, under mu,
+    // which spill_some takes too)
+    if (n > 0) sh.zero_copy = true;
     if (node->conf.world_size == 1 && n > 0 && !dense_index_readback(node, sh, blocks, n)) {
       // a sparse request over maps whose index tables live on the device: the whole resolve
       // runs there (block ids up, addresses and sizes down, no per-block host work); blocks the

@@ -82,6 +82,11 @@ _SIGS = {
     "sux_conf_init": (None, [C.POINTER(Conf)]),
     "sux_conf_set_prealloc": (C.c_int, [C.POINTER(Conf), C.c_char_p]),
     "sux_node_set_bootstrap": (C.c_int, [P, ALLGATHER_FN, P]),
+    "sux_group_create": (C.c_int, [C.c_int32, C.POINTER(P)]),
+    "sux_group_destroy": (C.c_int, [P]),
+    "sux_group_join": (C.c_int, [P, C.c_char_p, C.c_char_p, C.POINTER(C.c_int32),
+                                 C.POINTER(C.c_int32)]),
+    "sux_group_size": (C.c_int, [P, C.POINTER(C.c_int32)]),
     "sux_node_set_tuning": (C.c_int, [P, C.POINTER(Tuning)]),
     "sux_node_get_tuning": (C.c_int, [P, C.POINTER(Tuning)]),
     "sux_node_check": (C.c_int, [P]),

@@ -20,7 +20,7 @@ public final class SuxNative {
     }
   }
 
-  public static final int ABI_VERSION = 4;
+  public static final int ABI_VERSION = 5;
 
   // status codes (SUX_*)
   public static final int OK = 0, EINVAL = -1, ENOMEM = -2, EHIP = -3, ECOMM = -4, ENOENT = -5,
@@ -41,6 +41,13 @@ public final class SuxNative {
   /** Returns a context to pass to releaseBootstrap once the node is destroyed.  Every reply of
    * the bootstrap must be exactly worldSize * the contribution's bytes. */
   public static native long setBootstrap(long node, Bootstrap bootstrap, int worldSize);
+  // ---- executor group membership (driver) ----
+  /** One per application on the driver: ranks of a GPU group's executors (sux_group). */
+  public static native long groupCreate(int worldSize);
+  public static native void groupDestroy(long group);
+  /** {rank, localIndex}: rank by first arrival, keyed by executor id; localIndex = executors of
+   * the same host that joined earlier.  SuxException(ERANGE) once the group is complete. */
+  public static native int[] groupJoin(long group, String executorId, String host);
   /** HBM-capacity fallback: committed map outputs spill to Spark's files under dir. */
   public static native void setSpillDir(long node, String dir);
   public static native long spills(long node);
@@ -77,6 +84,10 @@ public final class SuxNative {
   public static native void writeMapOutputHost(long node, int shuffleId, int mapIndex, long part,
                                                ByteBuffer records, long numRecords, int recordSize,
                                                long stream);
+  /** Records at a raw host address (a staging area of any size, no 2 GiB ByteBuffer limit). */
+  public static native void writeMapOutputHostAddr(long node, int shuffleId, int mapIndex,
+                                                   long part, long hostAddr, long numRecords,
+                                                   long stream);
   public static native void writeMapOutputs(long node, int shuffleId, int firstMapIndex, long part,
                                             long deviceRecords, long recordsPerMap,
                                             long numRecords, long stream);
@@ -84,6 +95,13 @@ public final class SuxNative {
   public static native void commitMapOutput(long node, int shuffleId, int mapIndex,
                                             ByteBuffer data, long dataBytes, long[] lengths,
                                             long stream);
+  /** A committed data file of any size by address (mmapped past FileChannel.map's 2 GiB). */
+  public static native void commitMapOutputAddr(long node, int shuffleId, int mapIndex,
+                                                long dataAddr, long dataBytes, long[] lengths,
+                                                long stream);
+  /** Spark's committed data file by path, mapped natively (any size) and adopted. */
+  public static native void commitMapOutputFile(long node, int shuffleId, int mapIndex,
+                                                String dataPath, long[] lengths, long stream);
   public static native byte[] mapOutputIndex(long node, int shuffleId, int mapIndex,
                                              int numPartitions);
 

@@ -16,11 +16,16 @@
  *
  * Build (needs a JDK, absent from this image): src/main/native/Makefile.
  */
+#define _POSIX_C_SOURCE 200809L /* O_CLOEXEC, mmap */
+#include <fcntl.h>
 #include <jni.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include "../../../include/sparkucx_amd.h"
 
@@ -198,6 +203,39 @@ JNIEXPORT void JNICALL FN(releaseBootstrap)(JNIEnv* env, jclass cls, jlong ctx) 
   free(b);
 }
 
+/* ---- executor group membership, on the driver (GpuControlEndpoint's Hello) ----------------- */
+JNIEXPORT jlong JNICALL FN(groupCreate)(JNIEnv* env, jclass cls, jint worldSize) {
+  (void)cls;
+  sux_group* g = NULL;
+  if (failed(env, sux_group_create(worldSize, &g), "groupCreate")) return 0;
+  return (jlong)(intptr_t)g;
+}
+
+JNIEXPORT void JNICALL FN(groupDestroy)(JNIEnv* env, jclass cls, jlong group) {
+  (void)cls;
+  failed(env, sux_group_destroy((sux_group*)(intptr_t)group), "groupDestroy");
+}
+
+/* {rank, localIndex} of an executor (a repeated hello of the same id gets the same pair). */
+JNIEXPORT jintArray JNICALL FN(groupJoin)(JNIEnv* env, jclass cls, jlong group,
+                                          jstring executorId, jstring host) {
+  (void)cls;
+  if (!executorId || !host) {
+    throw_sux(env, SUX_EINVAL, "groupJoin: executor id and host are required");
+    return NULL;
+  }
+  const char* id = (*env)->GetStringUTFChars(env, executorId, NULL);
+  const char* h = (*env)->GetStringUTFChars(env, host, NULL);
+  int32_t v[2] = {-1, -1};
+  int rc = sux_group_join((sux_group*)(intptr_t)group, id, h, &v[0], &v[1]);
+  (*env)->ReleaseStringUTFChars(env, host, h);
+  (*env)->ReleaseStringUTFChars(env, executorId, id);
+  if (failed(env, rc, "groupJoin")) return NULL;
+  jintArray out = (*env)->NewIntArray(env, 2);
+  if (out) (*env)->SetIntArrayRegion(env, out, 0, 2, (const jint*)v);
+  return out;
+}
+
 /* HBM-capacity fallback: spill committed map outputs to Spark's files under spark.local.dir. */
 JNIEXPORT void JNICALL FN(setSpillDir)(JNIEnv* env, jclass cls, jlong node, jstring dir) {
   (void)cls;
@@ -326,6 +364,23 @@ JNIEXPORT void JNICALL FN(writeMapOutputHost)(JNIEnv* env, jclass cls, jlong nod
          "ShuffleWriter.write");
 }
 
+/* The same from a raw host address (records of any size: a staging area the writer grew past
+ * the 2 GiB a ByteBuffer can hold, Platform.allocateMemory / UnsafeUtils.mmap addresses). */
+JNIEXPORT void JNICALL FN(writeMapOutputHostAddr)(JNIEnv* env, jclass cls, jlong node,
+                                                  jint shuffleId, jint mapIndex, jlong part,
+                                                  jlong hostAddr, jlong numRecords,
+                                                  jlong stream) {
+  (void)cls;
+  if (numRecords < 0 || (numRecords > 0 && hostAddr == 0)) {
+    throw_sux(env, SUX_EINVAL, "writeMapOutputHostAddr: bad address or record count");
+    return;
+  }
+  failed(env, sux_write_map_output_host(NODE(node), shuffleId, mapIndex, PART(part),
+                                        (const void*)(intptr_t)hostAddr, (uint64_t)numRecords,
+                                        STREAM(stream)),
+         "ShuffleWriter.write");
+}
+
 JNIEXPORT void JNICALL FN(writeMapOutputs)(JNIEnv* env, jclass cls, jlong node, jint shuffleId,
                                            jint firstMapIndex, jlong part, jlong deviceRecords,
                                            jlong recordsPerMap, jlong numRecords, jlong stream) {
@@ -352,6 +407,64 @@ JNIEXPORT void JNICALL FN(commitMapOutput)(JNIEnv* env, jclass cls, jlong node, 
                                  (const int64_t*)len, STREAM(stream));
   (*env)->ReleaseLongArrayElements(env, lengths, len, JNI_ABORT);
   failed(env, rc, "writeIndexFileAndCommit");
+}
+
+/* writeIndexFileAndCommit of a data file of any size, by address: Spark's committed file
+ * mapped past FileChannel.map's 2 GiB limit (the reference's UnsafeUtils.mmap,
+ * UnsafeUtils.java:48-57, used at CommonUcxShuffleBlockResolver.scala:45-52). */
+JNIEXPORT void JNICALL FN(commitMapOutputAddr)(JNIEnv* env, jclass cls, jlong node,
+                                               jint shuffleId, jint mapIndex, jlong dataAddr,
+                                               jlong dataBytes, jlongArray lengths, jlong stream) {
+  (void)cls;
+  if (dataBytes < 0 || (dataBytes > 0 && dataAddr == 0) || !lengths) {
+    throw_sux(env, SUX_EINVAL, "commitMapOutputAddr: bad address, size or lengths");
+    return;
+  }
+  jlong* len = (*env)->GetLongArrayElements(env, lengths, NULL);
+  int rc = sux_commit_map_output(NODE(node), shuffleId, mapIndex, (const void*)(intptr_t)dataAddr,
+                                 (uint64_t)dataBytes, (const int64_t*)len, STREAM(stream));
+  (*env)->ReleaseLongArrayElements(env, lengths, len, JNI_ABORT);
+  failed(env, rc, "writeIndexFileAndCommit");
+}
+
+/* writeIndexFileAndCommit of Spark's committed data file by path: mapped here (any size — the
+ * reference maps files past 2 GiB through FileChannelImpl.map0, UnsafeUtils.java:48-57), adopted
+ * into the node's HBM (sux_commit_map_output copies it before returning) and unmapped. */
+JNIEXPORT void JNICALL FN(commitMapOutputFile)(JNIEnv* env, jclass cls, jlong node,
+                                               jint shuffleId, jint mapIndex, jstring dataPath,
+                                               jlongArray lengths, jlong stream) {
+  (void)cls;
+  if (!dataPath || !lengths) {
+    throw_sux(env, SUX_EINVAL, "commitMapOutputFile: path and lengths are required");
+    return;
+  }
+  const char* path = (*env)->GetStringUTFChars(env, dataPath, NULL);
+  char what[512];
+  snprintf(what, sizeof what, "writeIndexFileAndCommit(%s)", path);
+  const int fd = open(path, O_RDONLY | O_CLOEXEC);
+  (*env)->ReleaseStringUTFChars(env, dataPath, path);
+  struct stat st;
+  if (fd < 0 || fstat(fd, &st) != 0) {
+    if (fd >= 0) close(fd);
+    throw_sux(env, SUX_EIO, what);
+    return;
+  }
+  void* p = NULL;
+  if (st.st_size > 0) {
+    p = mmap(NULL, (size_t)st.st_size, PROT_READ, MAP_SHARED, fd, 0);
+    if (p == MAP_FAILED) {
+      close(fd);
+      throw_sux(env, SUX_EIO, what);
+      return;
+    }
+  }
+  jlong* len = (*env)->GetLongArrayElements(env, lengths, NULL);
+  int rc = sux_commit_map_output(NODE(node), shuffleId, mapIndex, p, (uint64_t)st.st_size,
+                                 (const int64_t*)len, STREAM(stream));
+  (*env)->ReleaseLongArrayElements(env, lengths, len, JNI_ABORT);
+  if (p) munmap(p, (size_t)st.st_size);
+  close(fd);
+  failed(env, rc, what);
 }
 
 JNIEXPORT jbyteArray JNICALL FN(mapOutputIndex)(JNIEnv* env, jclass cls, jlong node,

@@ -10,8 +10,7 @@
  */
 package org.apache.spark.shuffle.compat.spark_3_0
 
-import java.io.{File, RandomAccessFile}
-import java.nio.channels.FileChannel
+import java.io.File
 
 import org.apache.spark.{SparkConf, TaskContext}
 import org.apache.spark.shuffle.IndexShuffleBlockResolver
@@ -25,25 +24,19 @@ class UcxShuffleBlockResolver(conf: SparkConf) extends IndexShuffleBlockResolver
     super.writeIndexFileAndCommit(shuffleId, mapId, lengths, dataTmp)
     val slot = TaskContext.getPartitionId()
     val file = getDataFile(shuffleId, mapId)
-    val raf = new RandomAccessFile(file, "r")
-    try {
-      val len = raf.length()
-      if (len == 0) return
-      // the first commit of the map wins (another attempt's file has the same lengths)
-      val committed = {
-        val idx = new Array[Long](lengths.length)
-        val index = getIndexFile(shuffleId, mapId)
-        SuxNative.indexFileCommit(index.getPath, file.getPath, null, lengths, idx)
-        idx
-      }
-      // FileChannel.map stops at 2 GiB; a larger output is committed in the reference through its
-      // own mmap (UnsafeUtils.mmap, UnsafeUtils.java:48-57) — here Spark's map tasks stay below
-      val map = raf.getChannel.map(FileChannel.MapMode.READ_ONLY, 0, len)
-      val node = GpuNode.get
-      SuxNative.commitMapOutput(node.handle, shuffleId, slot, map, len, committed,
-        node.threadStream())
-    } finally {
-      raf.close()
+    if (file.length() == 0) return
+    // the first commit of the map wins (another attempt's file has the same lengths)
+    val committed = {
+      val idx = new Array[Long](lengths.length)
+      val index = getIndexFile(shuffleId, mapId)
+      SuxNative.indexFileCommit(index.getPath, file.getPath, null, lengths, idx)
+      idx
     }
+    // the file is mapped natively, whatever its size: FileChannel.map stops at 2 GiB, which is
+    // why the reference maps through FileChannelImpl.map0 (UnsafeUtils.mmap, UnsafeUtils.java:
+    // 48-57, used at CommonUcxShuffleBlockResolver.scala:45-58)
+    val node = GpuNode.get
+    SuxNative.commitMapOutputFile(node.handle, shuffleId, slot, file.getPath, committed,
+      node.threadStream())
   }
 }

@@ -83,7 +83,8 @@ class UcxShuffleManager(val conf: SparkConf, isDriver: Boolean) extends SortShuf
         Some(s.asInstanceOf[FixedWidthRowSerializer[K, V]].rows)
       case _ => None
     }
-    val gpu = rows.flatMap(r => GpuPartitioning.of(dep.partitioner, r.keyLen).map(r -> _))
+    val gpu = rows.flatMap(r =>
+      GpuPartitioning.of(dep.partitioner, r.keyLen, dep.keyClassName).map(r -> _))
     gpu match {
       case Some((r, p)) =>
         val part = partitioners.computeIfAbsent(h.shuffleId, _ =>

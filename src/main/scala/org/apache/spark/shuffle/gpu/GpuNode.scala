@@ -3,12 +3,20 @@
  * reference calls UcxNode (UcxNode.java:60-96), started lazily and closed at stop().
  *
  *  - configuration: the reference's spark.shuffle.ucx.* keys (UcxShuffleConf.scala:17-90) plus
- *    spark.shuffle.ucx.gpu.* (device, rank and size of the node's exchange group, pool cap,
- *    spill directory, exchange window);
+ *    spark.shuffle.ucx.gpu.* (size of the node's exchange group, transport, pool cap, exchange
+ *    window).  Every executor of a group reads the SAME conf: its rank comes from the driver
+ *    (Hello -> Welcome, in order of first arrival, keyed by executor id: sux_group), the way the
+ *    reference's executors introduce themselves with their BlockManagerId and the driver fans
+ *    them out (UcxNode.java:111-145, RpcConnectionCallback.java:47-89); its GPU is the task's
+ *    Spark-assigned "gpu" resource (spark.executor.resource.gpu.*), else its local index on the
+ *    host (executors of one host take devices 0, 1, ... in join order);
  *  - one HIP stream per task thread, the analog of getThreadLocalWorker (:147-176);
  *  - the exchange group's control plane over Spark RPC through the driver (GpuControlEndpoint):
  *    a host all-gather matched by tag, which replaces the UCX tag messages of the reference's
- *    bootstrap, and the driver -> executor messages of GpuExchangeCoordinator;
+ *    bootstrap, and the driver -> executor messages of GpuExchangeCoordinator.  With
+ *    spark.shuffle.ucx.gpu.transport = rccl (default) rank 0's RCCL unique id travels through
+ *    that all-gather and the node builds an RCCL communicator (ncclAllToAllv over xGMI); with
+ *    ipc the exchange pulls blocks over HIP IPC (several executors on one GPU);
  *  - the exchange: a collective over the group, so it is not run by whichever reduce task comes
  *    first (an executor without reduce tasks would never join it) but by every executor when the
  *    driver's coordinator says so — window by window as map tasks finish, the last when the map
@@ -22,22 +30,47 @@ import scala.collection.mutable
 import scala.concurrent.{Await, Promise}
 import scala.concurrent.duration.Duration
 
-import org.apache.spark.{SparkConf, SparkContext, SparkEnv, Success => TaskSuccess}
+import org.apache.spark.{SparkConf, SparkContext, SparkEnv, TaskContext, Success => TaskSuccess}
 import org.apache.spark.internal.Logging
 import org.apache.spark.network.util.JavaUtils
 import org.apache.spark.rpc.{RpcCallContext, RpcEndpointRef, RpcEnv, ThreadSafeRpcEndpoint}
 import org.apache.spark.scheduler.{SparkListener, SparkListenerStageCompleted,
   SparkListenerStageSubmitted, SparkListenerTaskEnd}
 import org.apache.spark.shuffle.ucx.gpu.{Bootstrap, SuxNative}
-import org.apache.spark.util.RpcUtils
+import org.apache.spark.util.{RpcUtils, Utils}
 
 class GpuNode private (conf: SparkConf, isDriver: Boolean) extends Logging {
   private def ucx(k: String) = "spark.shuffle.ucx." + k
   private def bytes(k: String, dflt: String): Long = JavaUtils.byteStringAsBytes(conf.get(k, dflt))
 
-  val device: Int = conf.getInt(ucx("gpu.device"), 0)
-  val rank: Int = conf.getInt(ucx("gpu.rank"), 0)
   val worldSize: Int = conf.getInt(ucx("gpu.worldSize"), 1)
+  private val transport: String = conf.get(ucx("gpu.transport"), "rccl")
+  require(transport == "rccl" || transport == "ipc",
+    s"spark.shuffle.ucx.gpu.transport must be rccl or ipc, not $transport")
+  private val member = worldSize > 1 && !isDriver
+
+  // executors of a group register with the driver's control endpoint (which also relays the
+  // coordinator's messages to them) and learn their rank from its reply
+  private val (rank0, localIndex) =
+    if (member) {
+      val env = SparkEnv.get
+      val me = env.rpcEnv.setupEndpoint(GpuControlEndpoint.EXECUTOR + env.executorId,
+        new GpuExecutorEndpoint(env.rpcEnv, this))
+      val w = RpcUtils.makeDriverRef(GpuControlEndpoint.NAME, conf, env.rpcEnv)
+        .askSync[GpuControlEndpoint.Welcome](
+          GpuControlEndpoint.Hello(env.executorId, Utils.localHostName(), worldSize, me))
+      (w.rank, w.localIndex)
+    } else (0, 0)
+  val rank: Int = rank0
+
+  // the task's "gpu" resource (Spark 3.0 resource scheduling; the node starts inside the first
+  // task that needs it), else the local index on the host; spark.shuffle.ucx.gpu.device pins it
+  // (one executor per host)
+  val device: Int =
+    if (conf.contains(ucx("gpu.device"))) conf.getInt(ucx("gpu.device"), 0)
+    else Option(TaskContext.get()).flatMap(_.resources().get("gpu"))
+      .flatMap(_.addresses.headOption).map(_.toInt).getOrElse(localIndex)
+
   // UcxShuffleConf.scala:32-40: the directory slot is 2 * rkeySize
   val metadataBlockSize: Long = 2 * bytes(ucx("rkeySize"), "150")
   // :74-81: a bare number is MiB
@@ -46,24 +79,39 @@ class GpuNode private (conf: SparkConf, isDriver: Boolean) extends Logging {
     if (v.nonEmpty && v.last.isDigit) v.toLong << 20 else JavaUtils.byteStringAsBytes(v)
   }
 
-  private val handle0: Long = SuxNative.nodeCreate(device, rank, worldSize, null,
+  private val boot: Bootstrap = if (member) new RpcBootstrap(conf, rank, worldSize) else null
+
+  // rccl: rank 0 creates the communicator's unique id (its process hosts RCCL's bootstrap
+  // root) and every rank takes it from the first slot of one all-gather
+  private val commId: Array[Byte] =
+    if (member && transport == "rccl") {
+      val mine = if (rank == 0) SuxNative.commUniqueId() else new Array[Byte](128)
+      java.util.Arrays.copyOfRange(boot.allGather(GpuNode.COMM_ID_TAG, mine), 0, 128)
+    } else null
+
+  private val handle0: Long = SuxNative.nodeCreate(device, rank, worldSize, commId,
     bytes(ucx("memory.minBufferSize"), "1024"), minAllocationSize, metadataBlockSize,
     conf.get(ucx("memory.preAllocateBuffers"), ""), conf.getInt(ucx("gpu.poolLimitMiB"), 0),
     isDriver)
 
   private val bootCtx: Long =
-    if (worldSize > 1 && !isDriver) {
-      SuxNative.setBootstrap(handle0, new RpcBootstrap(conf, rank, worldSize), worldSize)
-    } else 0L
+    if (member) SuxNative.setBootstrap(handle0, boot, worldSize) else 0L
 
-  // HBM-capacity fallback: committed map outputs spill to Spark's files under the first local
-  // directory (the reference serves every block from such files)
-  if (!isDriver) {
-    val dirs = conf.get("spark.local.dir", System.getProperty("java.io.tmpdir")).split(",")
-    val d = new java.io.File(dirs.head.trim, s"sparkucx-gpu-$rank")
-    d.mkdirs()
-    SuxNative.setSpillDir(handle0, d.getAbsolutePath)
-  }
+  // HBM-capacity fallback: committed map outputs spill to Spark's files.  The directory is
+  // private to this executor and application (a uniquely named subdirectory of the block
+  // manager's first local dir, blockmgr-<uuid> under spark.local.dir), so executors and
+  // applications sharing a host never overwrite or unlink each other's files; it is deleted
+  // when the node stops.  (A node of a larger group never spills: its peers read its slabs.)
+  private val spillDir: java.io.File =
+    if (!isDriver) {
+      val root = Option(SparkEnv.get).flatMap(e => Option(e.blockManager))
+        .map(_.diskBlockManager.localDirs.head)
+        .getOrElse(new java.io.File(System.getProperty("java.io.tmpdir")))
+      val id = Option(SparkEnv.get).map(_.executorId).getOrElse("executor")
+      val d = Utils.createDirectory(root.getAbsolutePath, s"sparkucx-gpu-${conf.getAppId}-$id")
+      SuxNative.setSpillDir(handle0, d.getAbsolutePath)
+      d
+    } else null
 
   // spark.shuffle.ucx.gpu.tuning.<field> = <int>: the node's kernel tuning table (sux_tuning);
   // unset fields keep the measured defaults
@@ -145,15 +193,6 @@ class GpuNode private (conf: SparkConf, isDriver: Boolean) extends Logging {
   def awaitExchange(shuffleId: Int): Unit =
     if (worldSize > 1) Await.result(promiseOf(shuffleId).future, exchangeTimeout)
 
-  // executors of a group register with the driver's control endpoint, which relays the
-  // coordinator's messages to them
-  if (worldSize > 1 && !isDriver) {
-    val env = SparkEnv.get.rpcEnv
-    val me = env.setupEndpoint(GpuControlEndpoint.EXECUTOR + rank, new GpuExecutorEndpoint(env, this))
-    RpcUtils.makeDriverRef(GpuControlEndpoint.NAME, conf, env)
-      .askSync[Boolean](GpuControlEndpoint.Hello(rank, worldSize, me))
-  }
-
   def close(): Unit = synchronized {
     exchangeThread.shutdown()
     exchangeThread.awaitTermination(10, TimeUnit.SECONDS)
@@ -161,11 +200,15 @@ class GpuNode private (conf: SparkConf, isDriver: Boolean) extends Logging {
     streams.clear()
     SuxNative.nodeDestroy(handle0)
     if (bootCtx != 0L) SuxNative.releaseBootstrap(bootCtx)
+    if (spillDir != null) Utils.deleteRecursively(spillDir)
   }
 }
 
 object GpuNode {
   @volatile private var instance: GpuNode = _
+  /** The bootstrap all-gather of rank 0's RCCL unique id: outside every shuffle's tags
+   * ((shuffle id << 32) | count, shuffle ids >= 0). */
+  val COMM_ID_TAG: Long = 0xFFFFFFFF00000000L
 
   /** CommonUcxShuffleManager.startUcxNodeIfMissing (:67-71): lazy and synchronized. */
   def startIfMissing(conf: SparkConf, isDriver: Boolean): GpuNode = synchronized {
@@ -207,7 +250,9 @@ private[gpu] object GpuControlEndpoint {
   val NAME = "SparkUcxGpuControl"
   val EXECUTOR = "SparkUcxGpuExecutor-"
   case class Contribute(tag: Long, rank: Int, world: Int, bytes: Array[Byte])
-  case class Hello(rank: Int, world: Int, ref: RpcEndpointRef)
+  /** An executor joins the group: every executor sends the same conf's world size. */
+  case class Hello(executorId: String, host: String, world: Int, ref: RpcEndpointRef)
+  case class Welcome(rank: Int, localIndex: Int, world: Int)
   /** Map tasks [first, first + count) of a shuffle (numMaps / numPartitions / recordSize: what an
    * executor that ran none of its tasks needs to register it before the collective). */
   case class ExchangeWindow(shuffleId: Int, numMaps: Int, numPartitions: Int, recordSize: Int,
@@ -228,16 +273,27 @@ private class GpuControlEndpoint(override val rpcEnv: RpcEnv, world: Int)
   import GpuControlEndpoint._
   private val pending = mutable.Map[Long, Array[(Array[Byte], RpcCallContext)]]()
   private val executors = new Array[RpcEndpointRef](world)
+  // ranks by first arrival, keyed by executor id (sux_group: a repeated hello gets its rank back)
+  private val group: Long = SuxNative.groupCreate(world)
+
+  override def onStop(): Unit = SuxNative.groupDestroy(group)
 
   override def receive: PartialFunction[Any, Unit] = {
     case m @ (_: ExchangeWindow | _: ExchangeDone) => executors.filter(_ != null).foreach(_.send(m))
   }
 
   override def receiveAndReply(context: RpcCallContext): PartialFunction[Any, Unit] = {
-    case Hello(rank, w, ref) =>
-      require(w == world && rank >= 0 && rank < world, s"executor rank $rank of $w, driver expects $world")
-      executors(rank) = ref
-      context.reply(true)
+    case Hello(executorId, host, w, ref) =>
+      if (w != world) {
+        context.sendFailure(new IllegalStateException(
+          s"executor $executorId expects a GPU group of $w, the driver's is $world"))
+      } else {
+        try {
+          val Array(rank, local) = SuxNative.groupJoin(group, executorId, host)
+          executors(rank) = ref
+          context.reply(Welcome(rank, local, world))
+        } catch { case e: Exception => context.sendFailure(e) }
+      }
     case Contribute(tag, rank, w, bytes) =>
       require(w == world, s"bootstrap: executor reports world $w, driver expects $world")
       val slots = pending.getOrElseUpdate(tag, new Array(world))
@@ -320,13 +376,17 @@ object GpuExchangeCoordinator extends Logging {
     override def onStageSubmitted(e: SparkListenerStageSubmitted): Unit =
       e.stageInfo.shuffleDepId.foreach(id => stageShuffle.put(e.stageInfo.stageId, id))
 
-    override def onTaskEnd(e: SparkListenerTaskEnd): Unit = if (e.reason == TaskSuccess) {
-      Option(stageShuffle.get(e.stageId)).flatMap(id => Option(watched.get(id)).map(id -> _))
-        .foreach { case (id, w) =>
-          w.synchronized { w.done += e.taskInfo.index }  // ShuffleMapTask index = map index
-          advance(id, w, stageDone = false)
-        }
-    }
+    // taskInfo.index is the task's index in its TaskSet, which equals the map (partition) index
+    // only in a stage's first attempt: a resubmitted attempt holds just the missing partitions.
+    // Later attempts therefore mark nothing; their maps are exchanged at the stage's end.
+    override def onTaskEnd(e: SparkListenerTaskEnd): Unit =
+      if (e.reason == TaskSuccess && e.stageAttemptId == 0) {
+        Option(stageShuffle.get(e.stageId)).flatMap(id => Option(watched.get(id)).map(id -> _))
+          .foreach { case (id, w) =>
+            w.synchronized { w.done += e.taskInfo.index }
+            advance(id, w, stageDone = false)
+          }
+      }
 
     override def onStageCompleted(e: SparkListenerStageCompleted): Unit =
       if (e.stageInfo.failureReason.isEmpty) {

@@ -27,12 +27,19 @@ case class GpuPartitioning(kind: Int, numPartitions: Int, keyOffset: Int, keyLen
                            ascending: Boolean, rangeBounds: Array[Byte])
 
 object GpuPartitioning {
-  /** None when the partitioner has no bit-exact restatement on the GPU. */
-  def of(p: Partitioner, keyLen: Int): Option[GpuPartitioning] = p match {
-    case h: HashPartitioner if keyLen == 8 =>
+  private val longKeys = Set("long", "java.lang.Long", "scala.Long")
+  private val intKeys = Set("int", "java.lang.Integer", "scala.Int")
+
+  /** None when the partitioner has no bit-exact restatement on the GPU.  keyClassName is the
+   * dependency's key class (ShuffleDependency.keyClassName): a HashPartitioner takes the GPU
+   * path only for Long / Int keys, whose hashCode the kernels restate (Long.hashCode,
+   * Integer.hashCode) — an 8-byte key of another type hashes differently in Spark. */
+  def of(p: Partitioner, keyLen: Int, keyClassName: String): Option[GpuPartitioning] = p match {
+    case h: HashPartitioner if keyLen == 8 && longKeys(keyClassName) =>
       Some(GpuPartitioning(SuxNative.PART_HASH_LONG, h.numPartitions, 0, 8, true, null))
-    case h: HashPartitioner if keyLen == 4 =>
+    case h: HashPartitioner if keyLen == 4 && intKeys(keyClassName) =>
       Some(GpuPartitioning(SuxNative.PART_HASH_INT, h.numPartitions, 0, 4, true, null))
+    case _: HashPartitioner => None
     case r: RangePartitioner[_, _] if keyLen > 0 && keyLen <= 16 =>
       // the bounds RangePartitioner sampled (private; reached by reflection, as the reference
       // reaches Spark internals it needs) must be byte arrays of keyLen bytes
@@ -200,37 +207,56 @@ class GpuShuffleWriter[K, V](
   private var lengths: Array[Long] = _
 
   override def write(records: Iterator[Product2[K, V]]): Unit = {
+    import org.apache.spark.unsafe.Platform
     val rs = rows.recordSize
-    var buf = ByteBuffer.allocateDirect(rs * 65536).order(ByteOrder.LITTLE_ENDIAN)
+    // rows are serialized into a small direct chunk and appended to native staging memory that
+    // grows in long arithmetic (a ByteBuffer stops at 2 GiB; a map task's output need not)
+    val chunk = ByteBuffer.allocateDirect(rs * 4096).order(ByteOrder.LITTLE_ENDIAN)
+    val chunkAddr = chunk.asInstanceOf[sun.nio.ch.DirectBuffer].address()
+    var cap = rs.toLong * 65536
+    var base = Platform.allocateMemory(cap)
+    var used = 0L
+    def flushChunk(): Unit = {
+      val len = chunk.position().toLong
+      if (used + len > cap) {
+        var bigger = cap * 2
+        while (used + len > bigger) bigger *= 2
+        base = Platform.reallocateMemory(base, cap, bigger)
+        cap = bigger
+      }
+      Platform.copyMemory(null, chunkAddr, null, base + used, len)
+      used += len
+      chunk.clear()
+    }
     var n = 0L
     val t0 = System.nanoTime()
-    records.foreach { kv =>
-      if (buf.remaining() < rs) {  // grow the staging buffer (map tasks are bounded by Spark)
-        val bigger = ByteBuffer.allocateDirect(buf.capacity() * 2).order(ByteOrder.LITTLE_ENDIAN)
-        buf.flip()
-        bigger.put(buf)
-        buf = bigger
+    try {
+      records.foreach { kv =>
+        if (chunk.remaining() < rs) flushChunk()
+        val before = chunk.position()
+        rows.write(kv._1, kv._2, chunk)
+        require(chunk.position() - before == rs, s"row is not $rs bytes")
+        n += 1
       }
-      val before = buf.position()
-      rows.write(kv._1, kv._2, buf)
-      require(buf.position() - before == rs, s"row is not $rs bytes")
-      n += 1
-    }
-    // slot = TaskContext.getPartitionId (compat/spark_3_0/UcxShuffleBlockResolver.scala:38)
-    val slot = TaskContext.getPartitionId()
-    if (n > 0) {
-      SuxNative.writeMapOutputHost(node.handle, shuffleId, slot, partitioner, buf, n, rs,
-        node.threadStream())
-    }
-    lengths = new Array[Long](numPartitions)
-    if (n > 0) {
-      val idx = ByteBuffer.wrap(SuxNative.mapOutputIndex(node.handle, shuffleId, slot, numPartitions))
-      var prev = idx.getLong(0)  // big-endian, Spark's index file bytes
-      for (p <- 0 until numPartitions) {
-        val next = idx.getLong(8 * (p + 1))
-        lengths(p) = next - prev
-        prev = next
+      flushChunk()
+      // slot = TaskContext.getPartitionId (compat/spark_3_0/UcxShuffleBlockResolver.scala:38)
+      val slot = TaskContext.getPartitionId()
+      if (n > 0) {
+        SuxNative.writeMapOutputHostAddr(node.handle, shuffleId, slot, partitioner, base, n,
+          node.threadStream())
       }
+      lengths = new Array[Long](numPartitions)
+      if (n > 0) {
+        val idx = ByteBuffer.wrap(SuxNative.mapOutputIndex(node.handle, shuffleId, slot, numPartitions))
+        var prev = idx.getLong(0)  // big-endian, Spark's index file bytes
+        for (p <- 0 until numPartitions) {
+          val next = idx.getLong(8 * (p + 1))
+          lengths(p) = next - prev
+          prev = next
+        }
+      }
+    } finally {
+      Platform.freeMemory(base)  // the write copied the rows to HBM before returning
     }
     metrics.incRecordsWritten(n)
     metrics.incBytesWritten(n * rs)

@@ -8,6 +8,10 @@
 // oracle (oracle/oracle.c, test infrastructure); every failed call must surface as a pending
 // SuxException carrying the C-ABI status, as a JVM caller would see it.
 #include <hip/hip_runtime_api.h>
+#include <poll.h>
+#include <pthread.h>
+#include <sys/mman.h>
+#include <sys/wait.h>
 
 #include <algorithm>
 #include <cstdarg>
@@ -25,6 +29,17 @@
 #include "../../oracle/oracle.h"
 #include "jni.h"
 
+// ---- the executors' group all-gather (GpuControlEndpoint.Contribute through the driver): with
+// forked executor processes, one shared-memory slot per rank and a process-shared barrier
+constexpr int kGroupWorld = 8;
+constexpr size_t kSlotBytes = 4u << 20;
+struct GroupShm {
+  pthread_barrier_t bar;
+  uint64_t sizes[kGroupWorld];
+  uint8_t data[kGroupWorld][kSlotBytes];
+};
+static GroupShm* g_shm = nullptr;
+
 // ---- the fake JVM --------------------------------------------------------------------------
 struct _jobject {
   enum Kind { kClass, kString, kBytes, kInts, kLongs, kDirect, kThrowable, kBootstrap } kind;
@@ -37,7 +52,8 @@ struct _jobject {
   jint code = 0;                // SuxException code
   std::string msg;              // exception message
   int boot_calls = 0;           // Bootstrap: allGather invocations
-  int boot_mode = 0;            // 0: world x bytes back (world 1: the input); 1: a short reply
+  int boot_mode = 0;            // 0: world x bytes back (world 1: the input); 1: a short reply;
+                                // 2: the forked group's shared-memory all-gather (rank in `code`)
 };
 struct _jmethodID {
   std::string name, sig;
@@ -107,7 +123,20 @@ static jobject CallObjectMethod(JNIEnv*, jobject o, jmethodID m, ...) {
     jbyteArray in = va_arg(ap, jbyteArray);
     o->boot_calls++;
     r = alloc(_jobject::kBytes);
-    r->b = in->b;  // world 1: every rank's contribution = this one
+    if (o->boot_mode == 2) {
+      const size_t n = in->b.size();
+      if (n <= kSlotBytes) std::memcpy(g_shm->data[o->code], in->b.data(), n);
+      g_shm->sizes[o->code] = n;
+      pthread_barrier_wait(&g_shm->bar);
+      bool same = n <= kSlotBytes;
+      for (int k = 0; k < kGroupWorld; ++k) same = same && g_shm->sizes[k] == n;
+      if (same)
+        for (int k = 0; k < kGroupWorld; ++k)
+          r->b.insert(r->b.end(), g_shm->data[k], g_shm->data[k] + n);
+      pthread_barrier_wait(&g_shm->bar);  // every rank read its copy before the next round
+    } else {
+      r->b = in->b;  // world 1: every rank's contribution = this one
+    }
     if (o->boot_mode == 1 && !r->b.empty()) r->b.pop_back();
   }
   va_end(ap);
@@ -232,6 +261,12 @@ jlong FN(registerShuffle)(JNIEnv*, jclass, jlong, jint, jint, jint, jint);
 void FN(unregisterShuffle)(JNIEnv*, jclass, jlong, jint);
 void FN(writeMapOutputHost)(JNIEnv*, jclass, jlong, jint, jint, jlong, jobject, jlong, jint, jlong);
 void FN(writeMapOutputs)(JNIEnv*, jclass, jlong, jint, jint, jlong, jlong, jlong, jlong, jlong);
+void FN(writeMapOutputHostAddr)(JNIEnv*, jclass, jlong, jint, jint, jlong, jlong, jlong, jlong);
+void FN(commitMapOutputAddr)(JNIEnv*, jclass, jlong, jint, jint, jlong, jlong, jlongArray, jlong);
+void FN(commitMapOutputFile)(JNIEnv*, jclass, jlong, jint, jint, jstring, jlongArray, jlong);
+jlong FN(groupCreate)(JNIEnv*, jclass, jint);
+void FN(groupDestroy)(JNIEnv*, jclass, jlong);
+jintArray FN(groupJoin)(JNIEnv*, jclass, jlong, jstring, jstring);
 void FN(waitMapOutputs)(JNIEnv*, jclass, jlong, jint);
 jbyteArray FN(mapOutputIndex)(JNIEnv*, jclass, jlong, jint, jint, jint);
 void FN(exchange)(JNIEnv*, jclass, jlong, jint, jlong);
@@ -311,9 +346,14 @@ static jobject direct_buffer(std::vector<uint8_t>& host) {
   return o;
 }
 
-int main() {
+static int group_main();
+static int large_main();
+
+int main(int argc, char** argv) {
   g_env = &g_fns;
   g_vm = &g_inv;
+  if (argc > 1 && std::string(argv[1]) == "group8") return group_main();
+  if (argc > 1 && std::string(argv[1]) == "large") return large_main();
   JNIEnv* env = &g_env;
   jclass cls = FindClass(env, "org/apache/spark/shuffle/ucx/gpu/SuxNative");
 
@@ -603,5 +643,264 @@ int main() {
     return 1;
   }
   printf("jni harness ok: every native method of SuxNative driven through sux_jni.c\n");
+  return 0;
+}
+
+// ---- group8: eight executors with IDENTICAL confs form a group through the driver ---------------
+// The parent plays the driver (GpuControlEndpoint: Hello -> groupJoin -> Welcome; it makes no HIP
+// call, so its forked children start the runtime fresh); eight forked children play executors
+// that all read the same conf (world 8, no rank, no device): each learns its rank and local index
+// from the driver, creates its node on device local % count, writes its two map tasks, runs the
+// exchange (IPC pulls — the eight share one GPU — with the all-gathers through a Bootstrap object
+// whose allGather is the shared-memory round above) and fetches the partitions it owns from every
+// map, compared with the CPU oracle.
+struct Hello {
+  int32_t child;
+  char id[60];
+};
+struct Welcome {
+  int32_t rank, local;
+};
+
+static int executor_main(int child, int req_fd, int rep_fd) {
+  JNIEnv* env = &g_env;
+  jclass cls = FindClass(env, "org/apache/spark/shuffle/ucx/gpu/SuxNative");
+  // the shared conf: world 8, every other key the same for every executor
+  const int W = kGroupWorld, R = 40, S = 100, rpm = 5000, maps_per = 2, M = W * maps_per;
+  Hello h{child, {}};
+  snprintf(h.id, sizeof h.id, "executor-%d", (int)getpid());
+  if (write(req_fd, &h, sizeof h) != (ssize_t)sizeof h) return 10;
+  Welcome w{};
+  if (read(rep_fd, &w, sizeof w) != (ssize_t)sizeof w || w.rank < 0) return 11;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return 12;
+  const int device = w.local % ndev;
+  jlong node = 0;
+  OK_CALL(node = FN(nodeCreate)(env, cls, device, w.rank, W, nullptr, 1024, 4 << 20, 300, nullptr,
+                                0, JNI_FALSE));
+  jobject boot = alloc(_jobject::kBootstrap);
+  boot->boot_mode = 2;
+  boot->code = w.rank;
+  jlong ctx = 0;
+  OK_CALL(ctx = FN(setBootstrap)(env, cls, node, boot, W));
+  std::vector<uint8_t> bounds((R - 1) * 10);
+  o_range_bounds_uniform(R, 10, bounds.data());
+  o_part opart{SUX_PART_RANGE_BYTES, R, 0, 10, 42, 1, bounds.data()};
+  jlong part = 0, stream = 0;
+  OK_CALL(part = FN(partitionerCreate)(env, cls, node, SUX_PART_RANGE_BYTES, R, 0, 10, 42, JNI_TRUE,
+                                       bytes_of(bounds.data(), bounds.size())));
+  OK_CALL(stream = FN(streamCreate)(env, cls, node));
+  const int sid = 9;
+  OK_CALL(FN(registerShuffle)(env, cls, node, sid, M, R, S));
+  // this executor's map tasks: maps [rank * maps_per, +maps_per), records at their global offset
+  std::vector<uint8_t> mine((size_t)maps_per * rpm * S);
+  o_gen_terasort(31, (uint64_t)w.rank * maps_per * rpm, (uint64_t)maps_per * rpm, mine.data());
+  void* drec = nullptr;
+  if (hipMalloc(&drec, mine.size()) != hipSuccess ||
+      hipMemcpy(drec, mine.data(), mine.size(), hipMemcpyHostToDevice) != hipSuccess)
+    return 13;
+  OK_CALL(FN(writeMapOutputs)(env, cls, node, sid, w.rank * maps_per, part, (jlong)(intptr_t)drec,
+                              rpm, (jlong)maps_per * rpm, stream));
+  OK_CALL(FN(waitMapOutputs)(env, cls, node, sid));
+  OK_CALL(FN(exchange)(env, cls, node, sid, stream));
+  jintArray own = nullptr;
+  OK_CALL(own = FN(ownedPartitions)(env, cls, node, sid, w.rank));
+  const int lo = own->i[0], hi = own->i[1];
+  EXPECT(lo == (w.rank * R) / W && hi == ((w.rank + 1) * R) / W, "rank %d owns [%d, %d)", w.rank,
+         lo, hi);
+  // every map's owned range (ShuffleBlockBatchId per map), vs the oracle
+  std::vector<jint> tri;
+  for (int m = 0; m < M; ++m) tri.insert(tri.end(), {m, lo, hi});
+  jlongArray sizes = NewLongArray(env, M);
+  jlong buf = 0;
+  OK_CALL(buf = FN(fetchBlocks)(env, cls, node, sid, ints_of(tri), sizes, stream));
+  std::vector<uint8_t> want;
+  std::vector<uint8_t> recs((size_t)rpm * S), data((size_t)rpm * S), be(8 * (R + 1));
+  std::vector<int64_t> len(R), idx(R + 1);
+  for (int m = 0; m < M; ++m) {
+    o_gen_terasort(31, (uint64_t)m * rpm, rpm, recs.data());
+    o_write_map(&opart, recs.data(), rpm, S, data.data(), len.data(), idx.data(), be.data());
+    EXPECT(sizes->l[m] == idx[hi] - idx[lo], "rank %d map %d size", w.rank, m);
+    want.insert(want.end(), data.begin() + idx[lo], data.begin() + idx[hi]);
+  }
+  std::vector<uint8_t> got(want.size() + 1);
+  if (!want.empty()) OK_CALL(FN(bufferRead)(env, cls, buf, 0, direct_buffer(got), (jlong)want.size(),
+                                            stream));
+  EXPECT(std::memcmp(got.data(), want.data(), want.size()) == 0,
+         "rank %d: owned partitions [%d, %d) of all %d maps", w.rank, lo, hi, M);
+  for (int m = 0; m < M; ++m) OK_CALL(FN(bufferRelease)(env, cls, buf));
+  OK_CALL(FN(exchangeWait)(env, cls, node, sid));
+  OK_CALL(FN(unregisterShuffle)(env, cls, node, sid));
+  OK_CALL(FN(partitionerDestroy)(env, cls, part));
+  OK_CALL(FN(streamDestroy)(env, cls, node, stream));
+  OK_CALL(FN(nodeDestroy)(env, cls, node));
+  FN(releaseBootstrap)(env, cls, ctx);
+  (void)hipFree(drec);
+  if (failures) return 1;
+  printf("executor rank %d (local %d, device %d): %zu owned bytes of %d maps ok\n", w.rank, w.local,
+         device, want.size(), M);
+  return 0;
+}
+
+static int group_main() {
+  JNIEnv* env = &g_env;
+  jclass cls = FindClass(env, "org/apache/spark/shuffle/ucx/gpu/SuxNative");
+  g_shm = static_cast<GroupShm*>(mmap(nullptr, sizeof(GroupShm), PROT_READ | PROT_WRITE,
+                                      MAP_SHARED | MAP_ANONYMOUS, -1, 0));
+  if (g_shm == MAP_FAILED) return 2;
+  pthread_barrierattr_t ba;
+  pthread_barrierattr_init(&ba);
+  pthread_barrierattr_setpshared(&ba, PTHREAD_PROCESS_SHARED);
+  pthread_barrier_init(&g_shm->bar, &ba, kGroupWorld);
+  int req[2];
+  if (pipe(req) != 0) return 2;
+  int rep[kGroupWorld][2];
+  std::vector<pid_t> pids;
+  for (int c = 0; c < kGroupWorld; ++c) {
+    if (pipe(rep[c]) != 0) return 2;
+    const pid_t pid = fork();
+    if (pid == 0) {
+      close(req[0]);
+      fflush(stdout);
+      _exit(executor_main(c, req[1], rep[c][0]));
+    }
+    pids.push_back(pid);
+  }
+  close(req[1]);
+  // the driver: hellos in arrival order -> ranks (no HIP call in this process)
+  jlong group = 0;
+  OK_CALL(group = FN(groupCreate)(env, cls, kGroupWorld));
+  std::vector<int> rank_of(kGroupWorld, -1);
+  for (int k = 0; k < kGroupWorld; ++k) {
+    Hello h{};
+    pollfd pf{req[0], POLLIN, 0};
+    if (poll(&pf, 1, 120000) != 1 || read(req[0], &h, sizeof h) != (ssize_t)sizeof h) {
+      fprintf(stderr, "FAIL: hello %d never came\n", k);
+      ++failures;
+      break;
+    }
+    jintArray r = nullptr;
+    OK_CALL(r = FN(groupJoin)(env, cls, group, NewStringUTF(env, h.id), NewStringUTF(env, "host0")));
+    rank_of[h.child] = r->i[0];
+    EXPECT(r->i[0] == k && r->i[1] == k, "hello %d got rank %d local %d", k, r->i[0], r->i[1]);
+    // a repeated hello (a retried RPC) gets the same rank back
+    jintArray again = nullptr;
+    OK_CALL(again = FN(groupJoin)(env, cls, group, NewStringUTF(env, h.id), NewStringUTF(env, "host0")));
+    EXPECT(again->i[0] == r->i[0], "repeated hello");
+    Welcome w{r->i[0], r->i[1]};
+    if (write(rep[h.child][1], &w, sizeof w) != (ssize_t)sizeof w) ++failures;
+  }
+  THROWS(SUX_ERANGE, FN(groupJoin)(env, cls, group, NewStringUTF(env, "executor-late"),
+                                   NewStringUTF(env, "host0")));
+  int bad = 0;
+  for (int c = 0; c < kGroupWorld; ++c) {
+    int st = 0;
+    waitpid(pids[c], &st, 0);
+    if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) {
+      fprintf(stderr, "FAIL: executor %d (rank %d) exited with %d\n", c, rank_of[c],
+              WIFEXITED(st) ? WEXITSTATUS(st) : -WTERMSIG(st));
+      ++bad;
+    }
+  }
+  OK_CALL(FN(groupDestroy)(env, cls, group));
+  std::vector<int> sorted = rank_of;
+  std::sort(sorted.begin(), sorted.end());
+  for (int k = 0; k < kGroupWorld; ++k) EXPECT(sorted[k] == k, "ranks are 0..7");
+  if (failures || bad) {
+    fprintf(stderr, "%d failure(s), %d executor(s) failed\n", failures, bad);
+    return 1;
+  }
+  printf("jni group ok: 8 executors with identical confs formed a group and exchanged\n");
+  return 0;
+}
+
+// ---- large: map outputs past 2 GiB through the address-based writers --------------------------
+// GpuShuffleWriter stages rows in native memory grown in long arithmetic and passes its address
+// (writeMapOutputHostAddr); the resolver commits Spark's data file by path, mapped natively
+// (commitMapOutputFile) or by address (commitMapOutputAddr).  A ByteBuffer-based path stops at
+// 2 GiB (FileChannel.map, int capacities); these maps are 3.3 GB.
+static int large_main() {
+  JNIEnv* env = &g_env;
+  jclass cls = FindClass(env, "org/apache/spark/shuffle/ucx/gpu/SuxNative");
+  const int R = 64, S = 100;
+  const uint64_t n = 33000000;  // 3.3 GB of records
+  const uint64_t nb = n * S;
+  jlong node = 0, part = 0, stream = 0;
+  OK_CALL(node = FN(nodeCreate)(env, cls, 0, 0, 1, nullptr, 1024, 4 << 20, 300, nullptr, 0,
+                                JNI_FALSE));
+  std::vector<uint8_t> bounds((R - 1) * 10);
+  o_range_bounds_uniform(R, 10, bounds.data());
+  o_part opart{SUX_PART_RANGE_BYTES, R, 0, 10, 42, 1, bounds.data()};
+  OK_CALL(part = FN(partitionerCreate)(env, cls, node, SUX_PART_RANGE_BYTES, R, 0, 10, 42, JNI_TRUE,
+                                       bytes_of(bounds.data(), bounds.size())));
+  OK_CALL(stream = FN(streamCreate)(env, cls, node));
+  std::vector<uint8_t> recs(nb), data(nb), be(8 * (R + 1));
+  std::vector<int64_t> len(R), idx(R + 1);
+  o_gen_terasort(41, 0, n, recs.data());
+  o_write_map(&opart, recs.data(), n, S, data.data(), len.data(), idx.data(), be.data());
+  const int sid = 11;
+  OK_CALL(FN(registerShuffle)(env, cls, node, sid, 3, R, S));
+  // map 0: the writer's rows by address; map 1: Spark's data file by address
+  OK_CALL(FN(writeMapOutputHostAddr)(env, cls, node, sid, 0, part, (jlong)(intptr_t)recs.data(),
+                                     (jlong)n, stream));
+  OK_CALL(FN(commitMapOutputAddr)(env, cls, node, sid, 1, (jlong)(intptr_t)data.data(), (jlong)nb,
+                                  longs_of(std::vector<jlong>(len.begin(), len.end())), stream));
+  THROWS(SUX_EINVAL, FN(commitMapOutputAddr)(env, cls, node, sid, 2, (jlong)(intptr_t)data.data(),
+                                             (jlong)nb - 1,
+                                             longs_of(std::vector<jlong>(len.begin(), len.end())),
+                                             stream));  // lengths do not sum to the size
+  // map 2: a small committed file by path (mapped natively)
+  {
+    char tmpl[] = "/tmp/sux_jni_large_XXXXXX";
+    const char* d = mkdtemp(tmpl);
+    EXPECT(d != nullptr, "mkdtemp");
+    const std::string path = std::string(d ? d : "/tmp") + "/shuffle_11_2_0.data";
+    const uint64_t small = idx[8];  // partitions 0..7 of the big map's output
+    FILE* f = fopen(path.c_str(), "wb");
+    fwrite(data.data(), 1, small, f);
+    fclose(f);
+    std::vector<jlong> l2(R, 0);
+    for (int p = 0; p < 8; ++p) l2[p] = len[p];
+    OK_CALL(FN(commitMapOutputFile)(env, cls, node, sid, 2, NewStringUTF(env, path.c_str()),
+                                    longs_of(l2), stream));
+    unlink(path.c_str());
+    if (d) rmdir(d);
+    jlongArray sz = NewLongArray(env, 1);
+    jlong buf = 0;
+    OK_CALL(buf = FN(fetchBlocks)(env, cls, node, sid, ints_of({2, 0, R}), sz, stream));
+    std::vector<uint8_t> host(small + 1);
+    OK_CALL(FN(bufferRead)(env, cls, buf, 0, direct_buffer(host), (jlong)small, stream));
+    EXPECT(sz->l[0] == (jlong)small && std::memcmp(host.data(), data.data(), small) == 0,
+           "file-committed map");
+    OK_CALL(FN(bufferRelease)(env, cls, buf));
+  }
+  OK_CALL(FN(waitMapOutputs)(env, cls, node, sid));
+  jbyteArray ix = nullptr;
+  OK_CALL(ix = FN(mapOutputIndex)(env, cls, node, sid, 0, R));
+  EXPECT(std::memcmp(ix->b.data(), be.data(), be.size()) == 0, "index file of the 3.3 GB map");
+  // partitions at the start, middle and end (offsets past 2^31 and 2^32) of both maps, and a
+  // batch range
+  for (int m = 0; m < 2; ++m)
+    for (auto [a, b] : std::vector<std::pair<int, int>>{{0, 1}, {R / 2, R / 2 + 1}, {R - 1, R},
+                                                         {20, 44}}) {
+      jlongArray sz = NewLongArray(env, 1);
+      jlong buf = 0;
+      OK_CALL(buf = FN(fetchBlocks)(env, cls, node, sid, ints_of({m, a, b}), sz, stream));
+      const uint64_t want = (uint64_t)(idx[b] - idx[a]);
+      std::vector<uint8_t> host(want + 1);
+      OK_CALL(FN(bufferRead)(env, cls, buf, 0, direct_buffer(host), (jlong)want, stream));
+      EXPECT(sz->l[0] == (jlong)want && std::memcmp(host.data(), data.data() + idx[a], want) == 0,
+             "map %d partitions [%d, %d) at offset %lld", m, a, b, (long long)idx[a]);
+      OK_CALL(FN(bufferRelease)(env, cls, buf));
+    }
+  OK_CALL(FN(unregisterShuffle)(env, cls, node, sid));
+  OK_CALL(FN(partitionerDestroy)(env, cls, part));
+  OK_CALL(FN(streamDestroy)(env, cls, node, stream));
+  OK_CALL(FN(nodeDestroy)(env, cls, node));
+  if (failures) {
+    fprintf(stderr, "%d failure(s)\n", failures);
+    return 1;
+  }
+  printf("jni large ok: 3.3 GB map outputs written and committed by address, fetched bit-exact\n");
   return 0;
 }

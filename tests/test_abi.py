@@ -18,7 +18,7 @@ def test_library_loads_and_exports_every_header_symbol():
     missing = [s for s in declared if not hasattr(lib, s)]
     assert not missing, missing
     assert set(declared) == set(N._SIGS), set(declared) ^ set(N._SIGS)
-    assert lib.sux_abi_version() == 4
+    assert lib.sux_abi_version() == 5
     assert C.sizeof(N.Conf) == 432  # sux_conf of ABI v2 (prealloc pairs appended)
     assert C.sizeof(N.Tuning) == 128  # sux_tuning of ABI v4: 27 knobs + 5 reserved
 
@@ -169,3 +169,34 @@ def test_block_lists_convert_the_same_by_every_path(blocks):
     got = [tuple(int(x) for x in row) for row in arr][:len(want)] if want else []
     assert got == want
     assert len(arr) == max(1, len(want))
+
+
+def test_group_ranks_executors_by_first_arrival():
+    """sux_group (the driver's Hello handling, GpuNode.scala): eight executors with identical
+    confs get ranks 0..7 in arrival order, a repeated hello its own rank back, local indices per
+    host, and a ninth executor SUX_ERANGE.  Host-only: no HIP call."""
+    lib = N.load()
+    g = C.c_void_p()
+    assert lib.sux_group_create(8, C.byref(g)) == 0
+    try:
+        order = [5, 2, 7, 0, 3, 1, 6, 4]
+        got = {}
+        for k, e in enumerate(order):
+            r, l = C.c_int32(), C.c_int32()
+            host = b"hostA" if e % 2 == 0 else b"hostB"
+            assert lib.sux_group_join(g, f"exec-{e}".encode(), host, C.byref(r), C.byref(l)) == 0
+            got[e] = (r.value, l.value)
+            assert r.value == k
+        assert sorted(v[0] for v in got.values()) == list(range(8))
+        for host_parity in (0, 1):
+            locals_ = [got[e][1] for e in order if e % 2 == host_parity]
+            assert locals_ == [0, 1, 2, 3]
+        r, l = C.c_int32(), C.c_int32()
+        assert lib.sux_group_join(g, b"exec-7", b"hostB", C.byref(r), C.byref(l)) == 0
+        assert (r.value, l.value) == got[7]
+        assert lib.sux_group_join(g, b"exec-8", b"hostA", C.byref(r), C.byref(l)) == N.SUX_ERANGE
+        assert lib.sux_group_join(g, b"", b"hostA", C.byref(r), C.byref(l)) == N.SUX_EINVAL
+        n = C.c_int32()
+        assert lib.sux_group_size(g, C.byref(n)) == 0 and n.value == 8
+    finally:
+        assert lib.sux_group_destroy(g) == 0

@@ -234,3 +234,43 @@ def test_pool_limit_without_spill_dir_fails_cleanly():
         node.unregister_shuffle(13)
     finally:
         node.close()
+
+
+def test_resolved_shuffle_is_never_spilled(tmp_path):
+    """sux_resolve_blocks hands out raw device addresses with no reference held: a
+    later write that needs memory must not spill and free the resolved shuffle's slabs.  Resolve
+    shuffle 14's blocks, fill the capped pool with shuffle 15's maps (which spill among
+    themselves), then read the resolved ranges: still the oracle's bytes."""
+    node = Node(device=0, pool_limit_mib=64)
+    try:
+        node.set_spill_dir(str(tmp_path))
+        R, rpm = 40, 80000
+        opart, part = _terasort(node, R)
+        node.register_shuffle(14, 2, R, 100)
+        recs = node.generate(N.GEN_TERASORT, SEED, 0, 2 * rpm, 100)
+        node.write_map_output(14, 0, part, recs[:rpm * 100], rpm)
+        node.write_map_output(14, 1, part, recs[rpm * 100:], rpm)
+        blocks = [(m, p) for m in range(2) for p in (0, 9, R - 1)]
+        addrs, sizes = node.resolve_blocks(14, blocks)
+        node.register_shuffle(15, 10, R, 100)
+        for m in range(10):
+            r = node.generate(N.GEN_TERASORT, SEED + 1, m * rpm, rpm, 100)
+            node.write_map_output(15, m, part, r, rpm)
+        assert node.spills() > 0  # shuffle 15 spilled its own maps
+        assert not any(p.name.startswith("shuffle_14_") for p in tmp_path.iterdir())
+        torch.cuda.synchronize()
+        host = recs.cpu().numpy()
+        for m in range(2):
+            want, _, ix, _ = O.write_map(opart, host[m * rpm * 100:(m + 1) * rpm * 100], 100)
+            for k, (mm, p) in enumerate(blocks):
+                if mm != m:
+                    continue
+                assert int(sizes[k]) == ix[p + 1] - ix[p]
+                got = np.empty(int(sizes[k]), np.uint8)
+                if got.size:
+                    N.hip_memcpy(got.ctypes.data, int(addrs[k]), got.size, N.HIP_D2H)
+                assert got.tobytes() == bytes(want[ix[p]:ix[p + 1]]), (m, p)
+        node.unregister_shuffle(15)
+        node.unregister_shuffle(14)
+    finally:
+        node.close()

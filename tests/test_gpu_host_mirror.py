@@ -43,3 +43,25 @@ def test_jni_binding_through_a_fake_jvm():
     r = subprocess.run([JNI], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "jni harness ok" in r.stdout
+
+
+def test_jni_eight_identical_executors_form_a_group():
+    """eight executors that read the SAME conf (no rank, no device key) learn
+    their ranks from the driver's groupJoin (Hello -> Welcome, sux_group), build their nodes over
+    the JNI binding, exchange (IPC pulls: the eight share one GPU) and each fetches the partitions
+    it owns from all 16 maps, bit-exact vs the oracle (tests/jni/jni_harness.cpp group8)."""
+    assert os.path.exists(JNI), "build it first: make -C tests/jni"
+    r = subprocess.run([JNI, "group8"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "jni group ok" in r.stdout
+    assert r.stdout.count("owned bytes of 16 maps ok") == 8
+
+
+def test_jni_map_outputs_past_2_gib():
+    """a 3.3 GB map written from a raw host address (the writer's native staging)
+    and a 3.3 GB data file committed by address, plus a file committed by path (mapped natively),
+    fetched bit-exact at offsets past 2^31 and 2^32 (tests/jni/jni_harness.cpp large)."""
+    assert os.path.exists(JNI), "build it first: make -C tests/jni"
+    r = subprocess.run([JNI, "large"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "jni large ok" in r.stdout

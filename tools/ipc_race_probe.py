@@ -82,8 +82,35 @@ def torch_layout():
               f"size {size.value >> 20} MB offset {t.data_ptr() - base.value}")
 
 
+def buffer_ids():
+    """HIP_POINTER_ATTRIBUTE_BUFFER_ID of allocations, and of a new one at a freed address."""
+    hip = _hip()
+    hip.hipPointerGetAttribute.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+    attr = 7  # HIP_POINTER_ATTRIBUTE_BUFFER_ID (driver_types.h: CONTEXT = 1, ... BUFFER_ID = 7)
+
+    def bid(p):
+        v = C.c_ulonglong(0)
+        rc = hip.hipPointerGetAttribute(C.byref(v), attr, p)
+        return rc, v.value
+
+    a, b = C.c_void_p(), C.c_void_p()
+    hip.hipMalloc(C.byref(a), 20 * MB)
+    hip.hipMalloc(C.byref(b), 20 * MB)
+    print("buffer id a", hex(a.value), bid(a), "b", hex(b.value), bid(b))
+    print("buffer id a+4MB (inside a)", bid(C.c_void_p(a.value + 4 * MB)))
+    old = a.value
+    hip.hipFree(a)
+    c = C.c_void_p()
+    hip.hipMalloc(C.byref(c), 20 * MB)
+    print("after free: new allocation at", hex(c.value), "same address:", c.value == old,
+          "buffer id", bid(c))
+
+
 def main():
     ctx = mp.get_context("spawn")
+    p = ctx.Process(target=buffer_ids)
+    p.start()
+    p.join()
     p = ctx.Process(target=torch_layout)
     p.start()
     p.join()

@@ -1,7 +1,12 @@
 #!/bin/bash
-# round 4, first GPU call: the IPC double-export probe, then bench.py's self-launched ranks
+# round 4, first GPU call: the IPC double-export probe, bench.py's self-launched ranks, the JVM
+# group formation / large maps through the JNI harness, resolve-vs-spill
 set -o pipefail
 mkdir -p gpurun_out/r04_a
 timeout -k 10 120 python -u tools/ipc_race_probe.py > gpurun_out/r04_a/ipc_race_probe.txt 2>&1 &&
-timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
-  tests/test_gpu_bench_rehearsal.py -k "own_ranks or two_ranks" > gpurun_out/r04_a/rehearsal.txt 2>&1
+timeout -k 10 500 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+  tests/test_gpu_host_mirror.py tests/test_gpu_exchange_maps.py \
+  > gpurun_out/r04_a/jni_and_maps.txt 2>&1 &&
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+  tests/test_gpu_bench_rehearsal.py tests/test_gpu_ipc_reuse.py tests/test_gpu_shuffle_exchange.py \
+  > gpurun_out/r04_a/rehearsal.txt 2>&1
