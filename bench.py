@@ -431,6 +431,68 @@ def plugin_leg(node, part, data, rs: int, R: int, rpm: int, gm: int, groups: int
             "pool": st}
 
 
+def plugin_host_leg(node, part, data, rs: int, R: int, rpm: int, maps: int, dev,
+                    threads: int = 8, reps: int = 2) -> dict:
+    """The drop-in path from the JVM writer's real entry: Spark's map tasks
+    serialize rows into HOST memory and GpuShuffleWriter hands them over by address
+    (SuxNative.writeMapOutputHostAddr -> sux_write_map_output_host: H2D staging, partition,
+    publish, one call per map task), `threads` task threads at once, each on its own stream
+    (the executor's cores; getThreadLocalWorker), then every block resolved.  The rows sit in
+    pinned memory (a writer's staging area), so the bound is the host->device copy over PCIe:
+    `h2d_GB/s` is a plain pinned copy of the same bytes on one stream, measured beside it."""
+    import threading
+    n = maps * rpm
+    host = torch.empty(n * rs, dtype=torch.uint8, pin_memory=True)
+    host.copy_(data[:n * rs])  # the rows the tasks serialized (untimed)
+    stage = torch.empty(n * rs, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    stage.copy_(host, non_blocking=True)
+    torch.cuda.synchronize(dev)
+    h2d = n * rs / (time.perf_counter() - t0) / 1e9
+    del stage
+    streams = [torch.cuda.Stream(dev) for _ in range(threads)]
+    blocks = node._blocks(np.stack([np.tile(np.arange(maps), R), np.repeat(np.arange(R), maps)],
+                                   1).astype(np.int32))
+
+    def one(sid):
+        node.register_shuffle(sid, maps, R, rs)
+        errs = []
+
+        def task(k):
+            try:
+                for m in range(k, maps, threads):
+                    node.write_map_output_host(sid, m, part, host[m * rpm * rs:(m + 1) * rpm * rs],
+                                               rpm, stream=streams[k])
+            except Exception as e:  # pragma: no cover
+                errs.append(e)
+        ts = [threading.Thread(target=task, args=(k,)) for k in range(threads)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        if errs:
+            raise errs[0]
+        _, sizes = node.resolve_blocks(sid, blocks)
+        assert int(sizes.sum()) == n * rs
+        node.unregister_shuffle(sid)
+
+    one(3000)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(reps):
+        one(3001 + k)
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / reps
+    gbs = n * rs / dt / 1e9
+    return {"maps": maps, "records": n, "bytes": n * rs, "threads": threads,
+            "ms": round(dt * 1e3, 3), "GB/s": round(gbs, 1), "h2d_GB/s": round(h2d, 1),
+            "of_pcie_bound": round(gbs / h2d, 3),
+            "path": f"register -> {threads} task threads x sux_write_map_output_host (pinned host "
+                    f"rows, one map task per call) -> resolve {len(blocks)} blocks -> unregister",
+            "bound": "PCIe host->device copy (h2d_GB/s: pinned copy of the same bytes, one stream)"}
+
+
 def plugin_leg_multi(node, part, data, rs: int, R: int, rpm: int, gm: int, groups: int,
                      world: int, rank: int, dev, ctl, xstream) -> dict:
     """The drop-in path at N > 1, as Spark drives it, through the C-ABI:
@@ -709,6 +771,10 @@ def main():
     ap.add_argument("--plugin-groups", type=int, default=-1,
                     help="N=1: also time the plugin path (register -> write -> resolve -> "
                          "unregister) over this many launch groups of map tasks (-1: 16; 0: skip)")
+    ap.add_argument("--plugin-host-maps", type=int, default=-1,
+                    help="N=1: also time the plugin path from pinned host rows through "
+                         "sux_write_map_output_host (the JVM writer's entry) over this many map "
+                         "tasks (-1: 64; 0: skip)")
     ap.add_argument("--resolve", type=int, default=1,
                     help="N=1: the timed step also commits the map outputs in place and resolves "
                          "every (map, reduce partition) block through sux_resolve_blocks (C2's "
@@ -906,6 +972,24 @@ def main():
                 srcs.append(torch.tensor([sb.data_ptr() if g == rank else node.ipc_open(hs[g])
                                           for g in range(world)], dtype=torch.int64, device=dev))
 
+        # rccl: the index all-gather of group k is POSTED on its own stream right after group k's
+        # partition is enqueued, and the all-to-all of group k - 1 is ISSUED on `comm` after that
+        # (sux_exchange_group_post / _issue): the host's wait for the gathered counts happens one
+        # group late, so `comm` is fed before its previous all-to-all drains and never waits on
+        # the host; the all-gather and the all-to-all use two communicators
+        gstream = torch.cuda.Stream(dev)
+        tickets = {}
+
+        def post(j):
+            s = j % NB
+            r0 = j * group_recs
+            r1 = min(n, r0 + group_recs)
+            m0 = j * gm
+            mg = -(-(r1 - r0) // rpm)
+            gstream.wait_event(part_done[s])
+            tickets[j] = node.exchange_group_post(index[m0 * (R + 1):(m0 + mg) * (R + 1)], mg, R,
+                                                  gidx[j, :world * mg * (R + 1)], stream=gstream)
+
         def exchange(j):
             s = j % NB
             r0 = j * group_recs
@@ -931,7 +1015,7 @@ def main():
                     node.pull_group(world, rank, srcs[s], gi, mg, R, recv[j % 2],
                                     rbytes[j:j + 1], stream=comm)
             else:
-                rb = node.exchange_group(send[s], ix, mg, R, gi, recv[j % 2], stream=comm)
+                rb = node.exchange_group_issue(tickets.pop(j), send[s], recv[j % 2], stream=comm)
                 rbytes[j] = int(rb.sum())
                 send_free[s].record(comm)
             e1.record(comm)
@@ -1036,10 +1120,13 @@ def main():
                                                index=index[m0 * (R + 1):(m0 + mg) * (R + 1)],
                                                peer_bytes=peer[s], workspace=ws[s], stream=comp)
                 part_done[s].record(comp)
+                if args.transport == "rccl":
+                    post(k)
                 if k >= 1:
                     exchange(k - 1)
             exchange(groups - 1)
             comp.wait_stream(comm)
+            comp.wait_stream(gstream)
 
     def barrier():
         torch.cuda.synchronize(dev)
@@ -1255,6 +1342,9 @@ def main():
         pg = min(groups, args.plugin_groups if args.plugin_groups > 0 else 16)
         if pg and n >= pg * group_recs:
             result["plugin"] = plugin_leg(node, part, data, rs, R, rpm, gm, pg, dev)
+        if args.plugin_host_maps != 0:
+            hm = min(maps, args.plugin_host_maps if args.plugin_host_maps > 0 else 64)
+            result["plugin_host"] = plugin_host_leg(node, part, data, rs, R, rpm, hm, dev)
     if not pipelined and args.varlen_rows != 0:
         vr = args.varlen_rows if args.varlen_rows > 0 else 32 << 20
         result["varlen"] = varlen_leg(node, vr, min(vr, 1 << 20), 200, dev,

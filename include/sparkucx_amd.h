@@ -299,6 +299,24 @@ int64_t sux_plan_block_offset(int32_t world, int32_t rank, int32_t num_maps,
 int sux_exchange_group(sux_node* node, const void* d_send, const int64_t* d_index,
                        int32_t num_maps, int32_t num_partitions, int64_t* d_gathered_index,
                        void* d_recv, uint64_t recv_capacity, uint64_t* recv_bytes, void* stream);
+/* sux_exchange_group in two halves, so that the stream carrying the all-to-alls never waits on
+ * the host between an all-gather and the all-to-all it plans.  _post enqueues
+ * the all-gather of this launch group's index tables into d_gathered and their asynchronous
+ * read-back into pinned staging on `stream` and returns a ticket; _issue (any thread) waits on
+ * the host for that read-back, plans the counts (sux_plan_group) and enqueues the
+ * partition-aligned ncclAllToAllv on ITS stream, over a second communicator split from the
+ * node's (made by the first _post of every rank, a collective).  The bench posts group k right
+ * after enqueueing its partition and then issues group k - 1: the all-gather of k overlaps the
+ * all-to-all of k - 1 and the all-to-all stream is fed before its previous transfer drains.
+ * _issue consumes the ticket (also on failure).  Every rank posts and issues the same groups in
+ * the same order. */
+typedef struct sux_xticket sux_xticket;
+int sux_exchange_group_post(sux_node* node, const int64_t* d_index, int32_t num_maps,
+                            int32_t num_partitions, int64_t* d_gathered, void* stream,
+                            sux_xticket** out);
+int sux_exchange_group_issue(sux_node* node, sux_xticket* ticket, const void* d_send,
+                             void* d_recv, uint64_t recv_capacity, uint64_t* recv_bytes,
+                             void* stream);
 
 /* ---- one-sided exchange over HIP IPC (xGMI peer access) ----------------------------------- *
  * The GET model of UcxShuffleClient (UcxShuffleClient.java:50-127, OnOffsetsFetchCallback.java

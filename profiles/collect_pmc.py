@@ -47,7 +47,8 @@ WORKLOAD_ARGS = {  # one PMC run: 8 launch groups of 32 maps x 2^20 records per 
 }
 COMMON = ["--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--varlen-rows", "0",
           "--compress-maps", "0", "--file-maps", "0", "--reduce-sort-records", "0",
-          "--plugin-groups", "0", "--self-check", "0", "--maps-2e27", "0", "--resolve", "0"]
+          "--plugin-groups", "0", "--self-check", "0", "--maps-2e27", "0", "--resolve", "0",
+          "--plugin-host-maps", "0"]
 
 
 def short(name: str) -> str | None:

@@ -449,6 +449,10 @@ struct sux_node {
   sux_conf conf{};
   bool is_driver = false;
   ncclComm_t comm = nullptr;
+  // the all-to-alls' own communicator (ncclCommSplit of `comm`, made on first use by
+  // sux_exchange_group_post): the index all-gather of launch group k and the all-to-all of group
+  // k - 1 then run on two streams at once without sharing one communicator's ordering
+  ncclComm_t comm_x = nullptr;
   std::unique_ptr<DevicePool> pool;
   HostPool hpool;
   sux::Timer timer;
@@ -1261,6 +1265,7 @@ int sux_node_destroy(sux_node* node) {
     node->shuffles.clear();
     for (auto& kv : node->ipc_bases) ipc_close_ref(node, kv.second.first, kv.second.second);
     node->ipc_bases.clear();
+    if (node->comm_x) (void)ncclCommDestroy(node->comm_x);
     if (node->comm) (void)ncclCommDestroy(node->comm);
     (void)hipGetLastError();  // see nccl_check
     delete node;
@@ -2076,6 +2081,82 @@ int sux_exchange_group(sux_node* node, const void* d_send, const int64_t* d_inde
     }
     nccl_check(ncclAllToAllv(d_send, a.data(), b.data(), d_recv, c.data(), d.data(), ncclUint8,
                              node->comm, s),
+               "ncclAllToAllv");
+  });
+}
+
+// ---- the same exchange in two halves (no host wait in front of an all-to-all) -------------------
+}  // extern "C"
+struct sux_xticket {
+  int32_t M = 0, R = 0;
+  int64_t* d_gathered = nullptr;
+  std::unique_ptr<HostLease> host;  // the gathered index tables, read back asynchronously
+  Event done;                       // after the read-back
+};
+extern "C" {
+
+int sux_exchange_group_post(sux_node* node, const int64_t* d_index, int32_t M, int32_t R,
+                            int64_t* d_gathered, void* stream, sux_xticket** out) {
+  return guard([&] {
+    require(node && d_index && d_gathered && out, SUX_EINVAL, "NULL argument");
+    const int W = node->conf.world_size;
+    require(R >= W && M >= 1, SUX_EINVAL, "need R >= world and >= 1 map");
+    node->bind();
+    hipStream_t s = node->stream(stream);
+    if (node->comm && !node->comm_x)  // collective: every rank's first post makes it
+      nccl_check(ncclCommSplit(node->comm, 0, node->conf.rank, &node->comm_x, nullptr),
+                 "ncclCommSplit");
+    const size_t per_rank = (size_t)M * (R + 1);
+    auto t = std::make_unique<sux_xticket>();
+    t->M = M;
+    t->R = R;
+    t->d_gathered = d_gathered;
+    t->host = std::make_unique<HostLease>(node->hpool, per_rank * W * 8);
+    if (!node->comm)
+      hip_check(hipMemcpyAsync(d_gathered, d_index, per_rank * 8, hipMemcpyDeviceToDevice, s),
+                "copy index");
+    else
+      nccl_check(ncclAllGather(d_index, d_gathered, per_rank, ncclInt64, node->comm, s),
+                 "ncclAllGather(index)");
+    hip_check(hipMemcpyAsync(t->host->b.first, d_gathered, per_rank * W * 8,
+                             hipMemcpyDeviceToHost, s),
+              "D2H gathered index");
+    hip_check(hipEventRecord(t->done.e, s), "hipEventRecord(gathered index)");
+    *out = t.release();
+  });
+}
+
+int sux_exchange_group_issue(sux_node* node, sux_xticket* ticket, const void* d_send,
+                             void* d_recv, uint64_t recv_capacity, uint64_t* recv_bytes,
+                             void* stream) {
+  std::unique_ptr<sux_xticket> t(ticket);  // consumed, whatever happens
+  return guard([&] {
+    require(node && t, SUX_EINVAL, "NULL argument");
+    const int W = node->conf.world_size, rank = node->conf.rank;
+    node->bind();
+    hipStream_t s = node->stream(stream);
+    // the host waits here for the read-back posted a launch group earlier (long done when the
+    // caller issues group k - 1 after posting group k); `stream` itself never waits on the host
+    hip_check(hipEventSynchronize(t->done.e), "sync gathered index");
+    std::vector<uint64_t> sc(W), sd(W), rc(W), rd(W);
+    int rc_plan = sux_plan_group(W, rank, t->M, t->R, static_cast<const int64_t*>(t->host->b.first),
+                                 sc.data(), sd.data(), rc.data(), rd.data());
+    require(rc_plan == SUX_OK, rc_plan, g_err);
+    const uint64_t total = rd[W - 1] + rc[W - 1];
+    require(total <= recv_capacity, SUX_ERANGE,
+            "receive buffer too small: need " + std::to_string(total) + " bytes");
+    if (recv_bytes)
+      for (int g = 0; g < W; ++g) recv_bytes[g] = rc[g];
+    if (!node->comm) {
+      if (total)
+        hip_check(hipMemcpyAsync(d_recv, d_send, total, hipMemcpyDeviceToDevice, s), "self copy");
+      return;
+    }
+    require(d_send && d_recv, SUX_EINVAL, "send/recv buffer is NULL");
+    std::vector<size_t> a(sc.begin(), sc.end()), b(sd.begin(), sd.end()), c(rc.begin(), rc.end()),
+        d(rd.begin(), rd.end());
+    nccl_check(ncclAllToAllv(d_send, a.data(), b.data(), d_recv, c.data(), d.data(), ncclUint8,
+                             node->comm_x ? node->comm_x : node->comm, s),
                "ncclAllToAllv");
   });
 }

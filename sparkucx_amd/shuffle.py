@@ -342,6 +342,25 @@ class Node:
                                             _stream(stream)), "sux_exchange_group")
         return np.frombuffer(rb, dtype=np.uint64).copy()
 
+    def exchange_group_post(self, index: torch.Tensor, num_maps: int, R: int,
+                            gathered: torch.Tensor, stream=None):
+        """First half of exchange_group: the all-gather of the index tables + their async
+        read-back; returns the ticket exchange_group_issue consumes."""
+        t = C.c_void_p()
+        N.check(self.lib.sux_exchange_group_post(self.h, _ptr(index), num_maps, R, _ptr(gathered),
+                                                 _stream(stream), C.byref(t)),
+                "sux_exchange_group_post")
+        return t
+
+    def exchange_group_issue(self, ticket, send: torch.Tensor, recv: torch.Tensor,
+                             stream=None) -> np.ndarray:
+        """Second half: plan from the read-back (host wait) and enqueue the all-to-all."""
+        rb = (C.c_uint64 * self.world_size)()
+        N.check(self.lib.sux_exchange_group_issue(self.h, ticket, _ptr(send), _ptr(recv),
+                                                  recv.numel(), rb, _stream(stream)),
+                "sux_exchange_group_issue")
+        return np.frombuffer(rb, dtype=np.uint64).copy()
+
     # ---- one-sided exchange over HIP IPC ----------------------------------------------------
     def ipc_handle(self, t: torch.Tensor) -> bytes:
         """72-byte descriptor: IPC handle of t's allocation + t's offset in it."""
@@ -381,6 +400,16 @@ class Node:
         N.check(self.lib.sux_write_map_output(self.h, shuffle_id, map_index, part.h,
                                               _ptr(records), num_records, _stream(stream)),
                 "sux_write_map_output")
+
+    def write_map_output_host(self, shuffle_id: int, map_index: int, part: Partitioner,
+                              host_records: torch.Tensor, num_records: int, stream=None):
+        """The JVM writer's entry (GpuShuffleWriter -> SuxNative.writeMapOutputHostAddr): rows in
+        host memory (pinned or pageable) staged to HBM, partitioned and published; waits."""
+        assert host_records.device.type == "cpu", "host rows"
+        N.check(self.lib.sux_write_map_output_host(self.h, shuffle_id, map_index, part.h,
+                                                   _ptr(host_records), num_records,
+                                                   _stream(stream)),
+                "sux_write_map_output_host")
 
     def write_map_outputs(self, shuffle_id: int, first_map: int, part: Partitioner,
                           records: torch.Tensor, records_per_map: int, num_records: int,

@@ -95,3 +95,18 @@ def test_bench_starts_its_own_ranks():
     cb = res["cpu_baseline"]
     assert cb and cb["value"] > 0 and cb["cores"] >= 1
     assert cb["parity"]["index_tables_equal"] and cb["parity"]["fetch_checksum_equal"]
+
+
+def test_bench_rccl_at_one_posts_and_issues():
+    """The N > 1 RCCL pipeline on a one-rank communicator (every byte to self): the index
+    all-gather of group k posted on its own stream, the all-to-all of group k - 1 issued after it
+    over the split communicator (sux_exchange_group_post / _issue), every group self-checked."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--rccl-at-one", "--records", "3000000",
+           "--map-records", "262144", "--group-maps", "2", "--steps", "2", "--warmup", "1",
+           "--no-cpu-baseline"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert res["n_gpus"] == 1 and res["self_check"]["ok"] and res["self_check"]["groups"] == 6
+    assert res["roofline_exchange"]["exchange_ms"] > 0
