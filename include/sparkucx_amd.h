@@ -222,7 +222,11 @@ typedef struct sux_tuning {
                                group g runs on that many CUs beside group g-1's K2 + K3 on the
                                others (K1 holds its rate on few CUs, K3 scales with them);
                                -1 or 0 every group's K1 -> K2 -> K3 on one of two streams    */
-  int32_t reserved[2];
+  int32_t msd_direct;       /* two-level small-record passes (small_kernel 4): bit 0 pass A, bit 1
+                               pass B store each record from its registers straight to its
+                               sorted place instead of through the LDS stage (the L2 merges a
+                               chunk's / segment's lines); -1 or 0 both staged                  */
+  int32_t reserved[1];
 } sux_tuning;
 int sux_node_set_tuning(sux_node* node, const sux_tuning* tuning);
 /* Waits for the device, then reports (and clears) failures the kernels recorded in the node's

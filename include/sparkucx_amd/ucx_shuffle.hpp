@@ -133,7 +133,8 @@ class UcxShuffleConf {
         "varlen_kernel", "varlen_tile", "sort_max_digit_bits", "sort_gather", "sort_all_passes",
         "hist_wgs_per_cu", "small_kernel", "small_waves", "scatter_order",
         "small_wgs_per_cu", "sort_msd", "exchange_self", "hist_nt", "counts_layout",
-        "scatter_counters", "lz4_queue", "scatter_nt", "gather_kernel"};
+        "scatter_counters", "lz4_queue", "scatter_nt", "gather_kernel", "split_cus",
+        "msd_direct"};
     sux_tuning t;
     std::memset(&t, 0, sizeof t);
     int32_t* f = reinterpret_cast<int32_t*>(&t);

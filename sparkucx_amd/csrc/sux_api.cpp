@@ -863,6 +863,7 @@ sux::Tuning resolve_tuning(const sux_tuning& t, bool pipelined) {
   r.scatter_nt = t.scatter_nt > 0 ? t.scatter_nt : 0;
   r.split_cus = t.split_cus > 0 ? t.split_cus : 0;
   r.gather_kernel = t.gather_kernel ? t.gather_kernel : 3;
+  r.msd_direct = t.msd_direct > 0 ? t.msd_direct : 0;
   r.gather16 = r.gather_kernel != 2;
   return r;
 }
@@ -1205,6 +1206,7 @@ int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
     require(in(t->gather_kernel, {1, 2, 3}), SUX_EINVAL, "gather_kernel must be 1, 2 or 3");
     require(t->split_cus == -1 || (t->split_cus >= 0 && t->split_cus <= 224 && t->split_cus % 32 == 0),
             SUX_EINVAL, "split_cus must be -1, 0 or a multiple of 32 up to 224");
+    require(t->msd_direct >= -1 && t->msd_direct <= 3, SUX_EINVAL, "msd_direct must be -1 .. 3");
     for (int32_t r : t->reserved) require(r == 0, SUX_EINVAL, "reserved tuning fields must be 0");
     require(node, SUX_EINVAL, "NULL node");
     std::lock_guard<std::mutex> lk(node->mu);

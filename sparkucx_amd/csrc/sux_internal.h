@@ -67,6 +67,8 @@ struct Tuning {
   bool gather16 = true;     // (1 and 3) 16-byte units
   int split_cus = 0;        // sux_partition_maps_pipelined: K1 on this many CUs beside the
                             // previous group's K3 on the others (0: one stream per group)
+  int msd_direct = 0;       // k_msd16a (bit 0) / k_msd16b (bit 1): records stored from registers
+                            // to their sorted place, no LDS stage
 };
 
 // Per-launch geometry of a group of consecutive map batches.

@@ -472,7 +472,7 @@ __device__ __forceinline__ uint32_t m16_pid(const PartDev& pd, const u32x4& r, i
   return (uint32_t)partition_words<KW, false>(pd, w, pd.bounds, pd.lut);
 }
 
-template <int KW, uint32_t NW, uint32_t DB, uint32_t LO>
+template <int KW, uint32_t NW, uint32_t DB, uint32_t LO, bool DIRECT = false>
 __global__ __launch_bounds__(NW * 64, 4) void k_msd16a(PartDev pd, MapGroup g, uint32_t cpm,
                                                  uint32_t nbk, uint16_t* __restrict__ offs,
                                                  uint16_t* __restrict__ pids_out,
@@ -532,15 +532,23 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16a(PartDev pd, MapGroup g, u
     }
     __syncthreads();
     scan_digit_wave16<NB, NW>(wc, wsum, tid, lane, wave);
+    if constexpr (DIRECT) {
+      // each record straight from its registers to its bucket-sorted place in the chunk's own
+      // 64 KB window (the window is written whole, so its lines merge in the L2)
 #pragma unroll
-    for (uint32_t j = 0; j < PT; ++j)
-      if (rank[j] != ~0u) stage[wc[wave * NB + h[j]] + rank[j]] = rv[j];
-    __syncthreads();
-    // the chunk goes back to its own place, in bucket order: one contiguous write
+      for (uint32_t j = 0; j < PT; ++j)
+        if (rank[j] != ~0u) t4[k.c0 + wc[wave * NB + h[j]] + rank[j]] = rv[j];
+    } else {
 #pragma unroll
-    for (uint32_t q = 0; q < PT; ++q) {
-      const uint32_t i = tid + q * NT;
-      if (i < k.n) t4[k.c0 + i] = stage[i];
+      for (uint32_t j = 0; j < PT; ++j)
+        if (rank[j] != ~0u) stage[wc[wave * NB + h[j]] + rank[j]] = rv[j];
+      __syncthreads();
+      // the chunk goes back to its own place, in bucket order: one contiguous write
+#pragma unroll
+      for (uint32_t q = 0; q < PT; ++q) {
+        const uint32_t i = tid + q * NT;
+        if (i < k.n) t4[k.c0 + i] = stage[i];
+      }
     }
     for (uint32_t hb = tid; hb < nbk; hb += NT)
       offs[(uint64_t)it * nbk + hb] = (uint16_t)wc[hb];  // wc[0][hb]: bucket start in the chunk
@@ -592,7 +600,7 @@ __global__ __launch_bounds__(kScanThreads) void k_msd16_scan(MapGroup g, uint32_
   }
 }
 
-template <int KW, uint32_t NW, uint32_t PT, uint32_t LO, uint32_t MCH>
+template <int KW, uint32_t NW, uint32_t PT, uint32_t LO, uint32_t MCH, bool DIRECT = false>
 __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, uint32_t cpm,
                                                  uint32_t nbk, const uint16_t* __restrict__ offs,
                                                  const uint64_t* __restrict__ segbase,
@@ -723,7 +731,9 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
   auto digit = [&](const Seg& s, const u32x4& r) {
     return (m16_pid<KW>(pd, r, kw0) - (s.h << LO)) & (NB - 1);
   };
-  // stable rank by pid & 31 -> stage/los in sorted order; wc[0][l] = digit starts afterwards
+  // stable rank by pid & 31 -> stage/los in sorted order; wc[0][l] = digit starts afterwards.
+  // DIRECT: the sorted positions stay in registers (pos[j], ~0u for none) for place_direct
+  uint32_t dl[PT], dp[PT];
   auto rank_stage = [&](const Seg& s, uint32_t n, const u32x4 (&r)[PT]) {
     uint32_t lo[PT], rk[PT];
 #pragma unroll
@@ -739,8 +749,15 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
     for (uint32_t j = 0; j < PT; ++j)
       if (rk[j] != ~0u) {
         const uint32_t pos = wc[wave * NB + lo[j]] + rk[j];
-        stage[pos] = r[j];
-        los[pos] = (uint8_t)lo[j];
+        if constexpr (DIRECT) {
+          dl[j] = lo[j];
+          dp[j] = pos;
+        } else {
+          stage[pos] = r[j];
+          los[pos] = (uint8_t)lo[j];
+        }
+      } else if constexpr (DIRECT) {
+        dp[j] = ~0u;
       }
   };
   auto write_index = [&](const Seg& s, uint32_t start_l) {
@@ -752,14 +769,21 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
       if (ibe) ibe[(uint64_t)s.m * (R + 1) + p] = bswap64((uint64_t)off);
     }
   };
-  // sorted stage -> output through the per-partition cursors; cursors advance; wc cleared
-  auto place = [&](const Seg& s, uint32_t n) {
+  // sorted stage -> output through the per-partition cursors; cursors advance; wc cleared.
+  // DIRECT: every record from its registers to cur[l] + its rank among the piece's digit l
+  auto place = [&](const Seg& s, uint32_t n, const u32x4 (&r)[PT]) {
+    if constexpr (DIRECT) {
 #pragma unroll
-    for (uint32_t q = 0; q < PT; ++q) {
-      const uint32_t i = tid + q * NT;
-      if (i < n) {
-        const uint32_t l = los[i];
-        out4[s.mbase + cur[l] + (i - wc[l])] = stage[i];
+      for (uint32_t j = 0; j < PT; ++j)
+        if (dp[j] != ~0u) out4[s.mbase + cur[dl[j]] + (dp[j] - wc[dl[j]])] = r[j];
+    } else {
+#pragma unroll
+      for (uint32_t q = 0; q < PT; ++q) {
+        const uint32_t i = tid + q * NT;
+        if (i < n) {
+          const uint32_t l = los[i];
+          out4[s.mbase + cur[l] + (i - wc[l])] = stage[i];
+        }
       }
     }
     uint32_t ncur = 0;
@@ -812,7 +836,7 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
       }
       __syncthreads();
       SUX_MSD_STAMP(2);
-      place(s, n);
+      place(s, n, rv);
       SUX_MSD_STAMP(3);
     }
     if (it + G < it1) s = build(it + G, prefetch(it + G));
@@ -882,12 +906,17 @@ hipError_t launch_msd16(const PartDev& pd, const MapGroup& g, uint8_t* d_out, in
   timer_begin(timer, kHist, s);
   const uint32_t wpc = (uint32_t)tn.small_wgs_per_cu;
   const dim3 ga(std::min<uint32_t>(g.num_maps * cpm, ncu * wpc));
-#define SUX_M16A(KW, DB, LOV)                                                                      \
+#define SUX_M16A_D(KW, DB, LOV, D)                                                                 \
   do {                                                                                             \
     constexpr size_t ldsa = M16a<NWA, DB>::lds_bytes();                                            \
-    allow_lds(reinterpret_cast<const void*>(&k_msd16a<KW, NWA, DB, LOV>), ldsa);                   \
-    hipLaunchKernelGGL((k_msd16a<KW, NWA, DB, LOV>), ga, dim3(NWA * kWave), ldsa, s, pd, g, cpm,   \
-                       nbk, offs, d_pids, tmp);                                                    \
+    allow_lds(reinterpret_cast<const void*>(&k_msd16a<KW, NWA, DB, LOV, D>), ldsa);                \
+    hipLaunchKernelGGL((k_msd16a<KW, NWA, DB, LOV, D>), ga, dim3(NWA * kWave), ldsa, s, pd, g,     \
+                       cpm, nbk, offs, d_pids, tmp);                                               \
+  } while (0)
+#define SUX_M16A(KW, DB, LOV)                                 \
+  do {                                                        \
+    if (tn.msd_direct & 1) SUX_M16A_D(KW, DB, LOV, true);     \
+    else SUX_M16A_D(KW, DB, LOV, false);                      \
   } while (0)
 #define SUX_M16AK(DB, LOV)                   \
   do {                                       \
@@ -902,6 +931,7 @@ hipError_t launch_msd16(const PartDev& pd, const MapGroup& g, uint8_t* d_out, in
   else SUX_M16AK(8, kM16Lo);
 #undef SUX_M16AK
 #undef SUX_M16A
+#undef SUX_M16A_D
   timer_end(timer, kHist, s);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -921,12 +951,17 @@ hipError_t launch_msd16(const PartDev& pd, const MapGroup& g, uint8_t* d_out, in
   static_assert(4 * MB4::lds_bytes() <= 160 * 1024, "pass B: four workgroups per CU");
   static_assert(4 * MB8::lds_bytes() <= 160 * 1024, "pass B (256-partition buckets): four per CU");
   static_assert(2 * M16a<NWA, 10>::lds_bytes() <= 160 * 1024, "pass A: two workgroups per CU");
-#define SUX_M16B(KW, LOV, MCV)                                                                     \
+#define SUX_M16B_D(KW, LOV, MCV, D)                                                                \
   do {                                                                                             \
     constexpr size_t ldsb = M16b<NWB, PTB, LOV, MCV>::lds_bytes();                                 \
-    allow_lds(reinterpret_cast<const void*>(&k_msd16b<KW, NWB, PTB, LOV, MCV>), ldsb);            \
-    hipLaunchKernelGGL((k_msd16b<KW, NWB, PTB, LOV, MCV>), gb, dim3(NWB * kWave), ldsb, s, pd, g,  \
-                       cpm, nbk, offs, segbase, tmp, d_out, d_index, d_index_be);                  \
+    allow_lds(reinterpret_cast<const void*>(&k_msd16b<KW, NWB, PTB, LOV, MCV, D>), ldsb);         \
+    hipLaunchKernelGGL((k_msd16b<KW, NWB, PTB, LOV, MCV, D>), gb, dim3(NWB * kWave), ldsb, s, pd, \
+                       g, cpm, nbk, offs, segbase, tmp, d_out, d_index, d_index_be);               \
+  } while (0)
+#define SUX_M16B(KW, LOV, MCV)                               \
+  do {                                                       \
+    if (tn.msd_direct & 2) SUX_M16B_D(KW, LOV, MCV, true);   \
+    else SUX_M16B_D(KW, LOV, MCV, false);                    \
   } while (0)
 #define SUX_M16BK(LOV, MCV)                   \
   do {                                        \
@@ -939,6 +974,7 @@ hipError_t launch_msd16(const PartDev& pd, const MapGroup& g, uint8_t* d_out, in
   else SUX_M16BK(kM16Lo, kM16MaxChunks);
 #undef SUX_M16BK
 #undef SUX_M16B
+#undef SUX_M16B_D
   timer_end(timer, kScatter, s);
   return hipGetLastError();
 }

@@ -44,11 +44,12 @@ TUNING_FIELDS = ("hist_kernel", "scatter_kernel", "coresident", "scatter_chunk",
                  "onepass", "varlen_kernel", "varlen_tile", "sort_max_digit_bits", "sort_gather",
                  "sort_all_passes", "hist_wgs_per_cu", "small_kernel", "small_waves", "scatter_order",
                  "small_wgs_per_cu", "sort_msd", "exchange_self", "hist_nt", "counts_layout",
-                 "scatter_counters", "lz4_queue", "scatter_nt", "gather_kernel", "split_cus")
+                 "scatter_counters", "lz4_queue", "scatter_nt", "gather_kernel", "split_cus",
+                 "msd_direct")
 
 
 class Tuning(C.Structure):
-    _fields_ = [(f, C.c_int32) for f in TUNING_FIELDS] + [("reserved", C.c_int32 * 2)]
+    _fields_ = [(f, C.c_int32) for f in TUNING_FIELDS] + [("reserved", C.c_int32 * 1)]
 
 
 # int (*sux_allgather_fn)(void* ctx, uint64_t tag, const void* send, uint64_t bytes, void* recv)

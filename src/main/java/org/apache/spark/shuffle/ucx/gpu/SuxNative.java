@@ -64,7 +64,7 @@ public final class SuxNative {
       "varlen_kernel", "varlen_tile", "sort_max_digit_bits", "sort_gather", "sort_all_passes",
       "hist_wgs_per_cu", "small_kernel", "small_waves", "scatter_order",
       "small_wgs_per_cu", "sort_msd", "exchange_self", "hist_nt", "counts_layout",
-      "scatter_counters", "lz4_queue", "scatter_nt", "gather_kernel", "split_cus"};
+      "scatter_counters", "lz4_queue", "scatter_nt", "gather_kernel", "split_cus", "msd_direct"};
   public static native long streamCreate(long node);
   public static native void streamDestroy(long node, long stream);
 

@@ -263,7 +263,7 @@ JNIEXPORT jlongArray JNICALL FN(poolStats)(JNIEnv* env, jclass cls, jlong node) 
 
 /* ---- kernel tuning table (sux_tuning) and the device error word ------------------------------
  * fields[] in the header's field order (hist_kernel .. split_cus); 0 keeps the default. */
-#define SUX_TUNING_FIELDS ((int)(sizeof(sux_tuning) / sizeof(int32_t)) - 2)
+#define SUX_TUNING_FIELDS ((int)(sizeof(sux_tuning) / sizeof(int32_t)) - 1)
 JNIEXPORT void JNICALL FN(setTuning)(JNIEnv* env, jclass cls, jlong node, jintArray fields) {
   (void)cls;
   sux_tuning t;

@@ -62,21 +62,25 @@ __device__ __forceinline__ uint32_t hash_pid(uint64_t g) {
 // stored write-through (sc1) and every storing wave drained its stores (vmcnt(0)) before the
 // workgroup barrier; one lane adds (agent scope) and polls with sc1 loads; the payload is read
 // with sc1 loads after the closing workgroup barrier.  Bounded: err set, wait abandoned after ~1 s.
-__device__ void grid_sync(unsigned* ctr, unsigned target, unsigned* err) {
+__device__ bool grid_sync(unsigned* ctr, unsigned target, unsigned* err) {
+  __shared__ unsigned failed;
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   if (threadIdx.x == 0) {
+    failed = 0;
     __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(2);
       if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {
         __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        failed = 1;
         break;
       }
     }
   }
   __syncthreads();
+  return failed == 0;  // a timed-out barrier ends the workgroup (every one leaves in ~1 s)
 }
 
 template <int MODE>
@@ -113,7 +117,7 @@ __global__ __launch_bounds__(NT, 1) void k_onemap(const u32x4* __restrict__ in,
       for (uint32_t p = tid; p < R; p += NT)
         __hip_atomic_store(&counts[(uint64_t)w * R + p], cnt[p], __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-      grid_sync(&sync[2 * m], G, err);
+      if (!grid_sync(&sync[2 * m], G, err)) return;
       // column scan: CU p < R owns partition p
       if (w < R) {
         uint32_t acc = 0;
@@ -146,7 +150,7 @@ __global__ __launch_bounds__(NT, 1) void k_onemap(const u32x4* __restrict__ in,
           __hip_atomic_store(&pre[(uint64_t)G * (R + 1) + w], acc, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
       }
-      grid_sync(&sync[2 * m + 1], G, err);
+      if (!grid_sync(&sync[2 * m + 1], G, err)) return;
       for (uint32_t p = tid; p < R; p += NT) {
         off[p] = __hip_atomic_load(&pre[(uint64_t)w * (R + 1) + p], __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
