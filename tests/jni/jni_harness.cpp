@@ -762,7 +762,10 @@ static int group_main() {
     if (pid == 0) {
       close(req[0]);
       fflush(stdout);
-      _exit(executor_main(c, req[1], rep[c][0]));
+      const int rc = executor_main(c, req[1], rep[c][0]);
+      fflush(stdout);  // _exit does not flush stdio
+      fflush(stderr);
+      _exit(rc);
     }
     pids.push_back(pid);
   }

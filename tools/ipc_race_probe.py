@@ -21,6 +21,10 @@ import time
 MB = 1 << 20
 
 
+class IpcHandle(C.Structure):  # hipIpcMemHandle_t, passed BY VALUE to hipIpcOpenMemHandle
+    _fields_ = [("reserved", C.c_char * 64)]
+
+
 def _hip():
     h = C.CDLL("libamdhip64.so")
     h.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
@@ -28,7 +32,7 @@ def _hip():
     h.hipMemset.argtypes = [C.c_void_p, C.c_int, C.c_size_t]
     h.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
     h.hipIpcGetMemHandle.argtypes = [C.c_void_p, C.c_void_p]
-    h.hipIpcOpenMemHandle.argtypes = [C.POINTER(C.c_void_p), C.c_char * 64, C.c_uint]
+    h.hipIpcOpenMemHandle.argtypes = [C.POINTER(C.c_void_p), IpcHandle, C.c_uint]
     h.hipIpcCloseMemHandle.argtypes = [C.c_void_p]
     h.hipSetDevice(0)
     return h
@@ -65,7 +69,9 @@ def exporter(conn, n_exports):
 
 def open_h(hip, h):
     base = C.c_void_p()
-    rc = hip.hipIpcOpenMemHandle(C.byref(base), (C.c_char * 64).from_buffer_copy(h), 1)
+    hh = IpcHandle()
+    C.memmove(C.addressof(hh), h, 64)
+    rc = hip.hipIpcOpenMemHandle(C.byref(base), hh, 1)
     return rc, base.value
 
 
