@@ -51,11 +51,15 @@ def worker(rank, W, rounds, handles, bar, q):
     bar.wait()
     stats = {"burst": [0, 0, {}], "staggered": [0, 0, {}]}  # opens, failures, codes
 
+    slowest = [0.0]
+
     def one(g):
         hh = IpcHandle()
         C.memmove(C.addressof(hh), handles[g], 64)
         base = C.c_void_p()
+        t0 = time.perf_counter()
         rc = hip.hipIpcOpenMemHandle(C.byref(base), hh, 1)
+        slowest[0] = max(slowest[0], time.perf_counter() - t0)
         if rc != 0:
             hip.hipGetLastError()
             return rc, None
@@ -65,9 +69,12 @@ def worker(rank, W, rounds, handles, bar, q):
         hip.hipIpcCloseMemHandle(base)
         return (0 if ok else -1000), base
 
+    print(f"rank {rank} exported, {time.strftime('%X')}", flush=True)
     for mode in ("burst", "staggered"):
         st = stats[mode]
-        for _ in range(rounds):
+        for rd in range(rounds):
+            print(f"rank {rank} {mode} round {rd}: {st[1]} failed of {st[0]}, slowest open "
+                  f"{1e3 * slowest[0]:.1f} ms", flush=True)
             bar.wait()
             if mode == "burst":
                 for g in range(W):
