@@ -3367,10 +3367,9 @@ int sux_resolve_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* b
     Shuffle& sh = node->shuffle(shuffle_id);
     drain(node, sh, lk);
     const int R = sh.R;
-    // the addresses returned below are read with no reference held: pin the shuffle's slabs
-    // against spilling until it is unregistered (set before anything is returned, under mu,
-    // which spill_some takes too)
-    if (n > 0) sh.zero_copy = true;
+    // the addresses returned are read with no reference held: a successful resolve pins the
+    // shuffle's slabs against spilling until it is unregistered (set under mu, which spill_some
+    // takes too, before the call returns; a failed resolve returns no address and pins nothing)
     if (node->conf.world_size == 1 && n > 0 && !dense_index_readback(node, sh, blocks, n)) {
       // a sparse request over maps whose index tables live on the device: the whole resolve
       // runs there (block ids up, addresses and sizes down, no per-block host work); blocks the
@@ -3420,6 +3419,7 @@ int sux_resolve_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* b
         addrs[i] = L.addr;
         sizes[i] = L.size;
       }
+      sh.zero_copy = true;
       return;
     }
     std::vector<int64_t> ae;
@@ -3461,6 +3461,7 @@ int sux_resolve_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* b
       addrs[i] = L.addr;
       sizes[i] = L.size;
     }
+    if (n > 0) sh.zero_copy = true;
   });
 }
 

@@ -6,13 +6,11 @@ that re-exporting one allocation returns the SAME 64 handle bytes (so the librar
 handles of one allocation), that HIP_POINTER_ATTRIBUTE_BUFFER_ID is unique per allocation, and
 that torch's caching allocator carves the rehearsal's three 4 MB send buffers out of ONE 20 MB
 allocation.  This probe asks whether the failure is a runtime limit on CONCURRENT imports:
-W processes each export one allocation (memset to its rank), all-gather the handles, then
-  - mode "burst": every process opens all W - 1 peers' handles at the same moment (a barrier
-    before), reads one byte of each, closes them — the rehearsal's pattern;
-  - mode "staggered": step k, process r opens only peer (r + k) % W, so every exporter serves
-    exactly one importer at a time;
-repeated for `rounds` rounds; every failed open is counted with its error code.
-usage: python tools/ipc_stress_probe.py [W=8] [rounds=30]
+W processes each export one allocation (memset to its rank), all-gather the handles, then open
+each other's handles in five patterns (below), all opens of a pattern at the same moment; each
+opened mapping is read (one byte) and closed; every failed open is counted with its error code
+and the slowest open is timed.
+usage: python tools/ipc_stress_probe.py [W=8] [rounds=1]
 """
 import ctypes as C
 import multiprocessing as mp
@@ -49,8 +47,6 @@ def worker(rank, W, rounds, handles, bar, q):
     assert hip.hipIpcGetMemHandle(C.byref(h), p) == 0
     handles[rank] = bytes(h.reserved)
     bar.wait()
-    stats = {"burst": [0, 0, {}], "staggered": [0, 0, {}]}  # opens, failures, codes
-
     slowest = [0.0]
 
     def one(g):
@@ -70,36 +66,41 @@ def worker(rank, W, rounds, handles, bar, q):
         return (0 if ok else -1000), base
 
     print(f"rank {rank} exported, {time.strftime('%X')}", flush=True)
-    for mode in ("burst", "staggered"):
+    # who opens whom, all at the same moment (a barrier before each pattern):
+    #   fanin  - every other rank opens rank 0's handle; rank 0 opens nothing
+    #   mutual - ranks 0 and 1 open each other's handle; the rest open nothing
+    #   chain  - rank r opens r + 1 (the last opens nothing): no cycle
+    #   ring   - rank r opens (r + 1) % W: one cycle through every rank
+    # (every rank opening every peer at once — the rehearsal's pattern — failed every open after
+    # ~10.5 s in this probe's first version: profiles/r04/ipc_stress_burst.txt)
+    plans = {
+        "fanin": [0] if rank else [],
+        "mutual": [1 - rank] if rank < 2 else [],
+        "chain": [rank + 1] if rank + 1 < W else [],
+        "ring": [(rank + 1) % W],
+    }
+    stats = {m: [0, 0, {}, 0.0] for m in plans}
+    for mode, targets in plans.items():
         st = stats[mode]
         for rd in range(rounds):
-            print(f"rank {rank} {mode} round {rd}: {st[1]} failed of {st[0]}, slowest open "
-                  f"{1e3 * slowest[0]:.1f} ms", flush=True)
             bar.wait()
-            if mode == "burst":
-                for g in range(W):
-                    if g == rank:
-                        continue
-                    rc, _ = one(g)
-                    st[0] += 1
-                    if rc:
-                        st[1] += 1
-                        st[2][rc] = st[2].get(rc, 0) + 1
-            else:
-                for k in range(1, W):
-                    bar.wait()
-                    rc, _ = one((rank + k) % W)
-                    st[0] += 1
-                    if rc:
-                        st[1] += 1
-                        st[2][rc] = st[2].get(rc, 0) + 1
+            slowest[0] = 0.0
+            for g in targets:
+                rc, _ = one(g)
+                st[0] += 1
+                if rc:
+                    st[1] += 1
+                    st[2][rc] = st[2].get(rc, 0) + 1
+            st[3] = max(st[3], slowest[0])
+        print(f"rank {rank} {mode}: {st[1]} of {st[0]} opens failed {st[2]}, slowest "
+              f"{1e3 * st[3]:.1f} ms", flush=True)
     bar.wait()
     q.put((rank, stats))
 
 
 def main():
     W = int(sys.argv[1]) if len(sys.argv) > 1 else 8
-    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 1
     ctx = mp.get_context("spawn")
     mgr = ctx.Manager()
     handles = mgr.list([b""] * W)
@@ -112,20 +113,19 @@ def main():
     res = [q.get(timeout=300) for _ in ps]
     for p in ps:
         p.join()
-    tot = {"burst": [0, 0, {}], "staggered": [0, 0, {}]}
     for rank, st in sorted(res):
-        for m in tot:
-            tot[m][0] += st[m][0]
-            tot[m][1] += st[m][1]
-            for c, n in st[m][2].items():
-                tot[m][2][c] = tot[m][2].get(c, 0) + n
-        print(f"rank {rank}: burst {st['burst'][1]}/{st['burst'][0]} failed {st['burst'][2]}, "
-              f"staggered {st['staggered'][1]}/{st['staggered'][0]} failed {st['staggered'][2]}")
-    print(f"W={W} rounds={rounds} ({time.time() - t0:.1f} s): burst {tot['burst'][1]} of "
-          f"{tot['burst'][0]} opens failed {tot['burst'][2]}; staggered {tot['staggered'][1]} of "
-          f"{tot['staggered'][0]} failed {tot['staggered'][2]} (1 = invalid value, "
-          f"17 = invalid device pointer, -1000 = wrong bytes)")
-
+        pass
+    for mode in ("fanin", "mutual", "chain", "ring"):
+        opens = sum(st[mode][0] for _, st in res)
+        fails = sum(st[mode][1] for _, st in res)
+        codes = {}
+        for _, st in res:
+            for c, n in st[mode][2].items():
+                codes[c] = codes.get(c, 0) + n
+        slow = max(st[mode][3] for _, st in res)
+        print(f"W={W} {mode}: {fails} of {opens} opens failed {codes}, slowest {1e3 * slow:.1f} ms "
+              f"(17 = hipErrorInvalidDevicePointer, -1000 = wrong bytes)", flush=True)
+    print(f"total {time.time() - t0:.1f} s")
 
 if __name__ == "__main__":
     main()
