@@ -37,7 +37,12 @@ def _hip():
     return h
 
 
-def worker(rank, W, rounds, handles, bar, q):
+def worker(rank, W, rounds, handles, bar, q, ptracer_any=False, plans_only=None):
+    if ptracer_any:  # let any process of this user read this one's fds (Yama ptrace_scope 1)
+        libc = C.CDLL(None)
+        libc.prctl.argtypes = [C.c_int, C.c_ulong, C.c_ulong, C.c_ulong, C.c_ulong]
+        print(f"rank {rank} prctl(PR_SET_PTRACER, ANY) = {libc.prctl(0x59616d61, C.c_ulong(-1).value, 0, 0, 0)}",
+              flush=True)
     hip = _hip()
     p = C.c_void_p()
     assert hip.hipMalloc(C.byref(p), 20 * MB) == 0
@@ -79,6 +84,8 @@ def worker(rank, W, rounds, handles, bar, q):
         "chain": [rank + 1] if rank + 1 < W else [],
         "ring": [(rank + 1) % W],
     }
+    if plans_only:
+        plans = {m: t for m, t in plans.items() if m in plans_only}
     stats = {m: [0, 0, {}, 0.0] for m in plans}
     for mode, targets in plans.items():
         st = stats[mode]
@@ -98,24 +105,21 @@ def worker(rank, W, rounds, handles, bar, q):
     q.put((rank, stats))
 
 
-def main():
-    W = int(sys.argv[1]) if len(sys.argv) > 1 else 8
-    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 1
-    ctx = mp.get_context("spawn")
+def run(W, rounds, method, ptracer_any, modes):
+    ctx = mp.get_context(method)
     mgr = ctx.Manager()
     handles = mgr.list([b""] * W)
     bar = ctx.Barrier(W)
     q = ctx.Queue()
-    ps = [ctx.Process(target=worker, args=(r, W, rounds, handles, bar, q)) for r in range(W)]
+    ps = [ctx.Process(target=worker, args=(r, W, rounds, handles, bar, q, ptracer_any, modes))
+          for r in range(W)]
     t0 = time.time()
     for p in ps:
         p.start()
     res = [q.get(timeout=300) for _ in ps]
     for p in ps:
         p.join()
-    for rank, st in sorted(res):
-        pass
-    for mode in ("fanin", "mutual", "chain", "ring"):
+    for mode in modes:
         opens = sum(st[mode][0] for _, st in res)
         fails = sum(st[mode][1] for _, st in res)
         codes = {}
@@ -123,9 +127,24 @@ def main():
             for c, n in st[mode][2].items():
                 codes[c] = codes.get(c, 0) + n
         slow = max(st[mode][3] for _, st in res)
-        print(f"W={W} {mode}: {fails} of {opens} opens failed {codes}, slowest {1e3 * slow:.1f} ms "
-              f"(17 = hipErrorInvalidDevicePointer, -1000 = wrong bytes)", flush=True)
-    print(f"total {time.time() - t0:.1f} s")
+        print(f"== start={method} ptracer_any={ptracer_any} W={W} {mode}: {fails} of {opens} opens "
+              f"failed {codes}, slowest {1e3 * slow:.1f} ms  (17 = hipErrorInvalidDevicePointer)",
+              flush=True)
+    print(f"   ({time.time() - t0:.1f} s)", flush=True)
+
+
+def main():
+    W = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    try:
+        with open("/proc/sys/kernel/yama/ptrace_scope") as f:
+            print("kernel.yama.ptrace_scope =", f.read().strip(), flush=True)
+    except OSError as e:
+        print("no yama:", e, flush=True)
+    # siblings started by spawn, with and without PR_SET_PTRACER_ANY, then by fork
+    run(W, rounds, "spawn", True, ["fanin", "mutual", "ring"])
+    run(W, rounds, "fork", False, ["fanin"])
+    run(W, rounds, "spawn", False, ["fanin"])
 
 if __name__ == "__main__":
     main()
