@@ -558,10 +558,12 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16a(PartDev pd, MapGroup g, u
   }
 }
 
-// K2 of the MSD path: one workgroup (kScanThreads) per map.  Bucket totals over the map's chunks
-// (one thread per bucket), exclusive scan over buckets ->
-// segbase[m][h] (record index in the group's output), the index table's last entry and, at
-// world 1, the peer byte count.
+// K2 of the MSD path: one workgroup (kScanThreads) per map.  Bucket totals over the map's chunks,
+// exclusive scan over buckets -> segbase[m][h] (record index in the group's output), the index
+// table's last entry and, at world 1, the peer byte count.  A bucket's total is S[h+1] - S[h]
+// with S[h] = the sum over chunks of the bucket's start in the chunk (offs) and S[nbk] = the map's
+// records: one u16 read per (chunk, bucket), a thread per bucket with 16 reads in flight (round
+// 3's two dependent reads per chunk kept each launch ~0.76 ms: 256 chunks of latency in a row).
 __global__ __launch_bounds__(kScanThreads) void k_msd16_scan(MapGroup g, uint32_t cpm, uint32_t nbk,
                                                              const uint16_t* __restrict__ offs,
                                                              uint64_t* __restrict__ segbase,
@@ -569,28 +571,32 @@ __global__ __launch_bounds__(kScanThreads) void k_msd16_scan(MapGroup g, uint32_
                                                              uint8_t* __restrict__ index_be,
                                                              uint64_t* __restrict__ peer_bytes,
                                                              int R) {
-  constexpr uint32_t HG = 1024, NG = kScanThreads / HG;  // one thread per bucket (nbk <= 1024)
+  constexpr uint32_t HG = kScanThreads;  // one thread per bucket (nbk <= 1024)
+  constexpr uint32_t U = 16;             // chunk reads in flight per thread
   __shared__ uint64_t sh[2 * kWave + 1];
-  __shared__ uint32_t part[kScanThreads];
+  __shared__ uint32_t colsum[HG + 1];
   const uint32_t m = blockIdx.x, tid = threadIdx.x;
   const uint32_t len = m16_map_len(g, m), nch = (len + kM16Chunk - 1) / kM16Chunk;
-  const uint32_t h = tid % HG, cg = tid / HG;
-  uint32_t t = 0;
-  if (h < nbk) {
-    const uint16_t* om = offs + (uint64_t)m * cpm * nbk;
-    for (uint32_t c = cg; c < nch; c += NG) {
-      const uint32_t o = om[(uint64_t)c * nbk + h];
-      const uint32_t e = h + 1 < nbk ? om[(uint64_t)c * nbk + h + 1] : m16_chunk_len(len, c);
-      t += e - o;
+  uint32_t S = 0;
+  if (tid < nbk) {
+    const uint16_t* om = offs + (uint64_t)m * cpm * nbk + tid;
+    uint32_t c = 0;
+    for (; c + U <= nch; c += U) {
+      uint32_t v[U];
+#pragma unroll
+      for (uint32_t k = 0; k < U; ++k) v[k] = om[(uint64_t)(c + k) * nbk];
+#pragma unroll
+      for (uint32_t k = 0; k < U; ++k) S += v[k];
     }
+    for (; c < nch; ++c) S += om[(uint64_t)c * nbk];
   }
-  part[tid] = t;
+  // S[nbk] = every chunk's records: written by thread nbk (or thread 0 when nbk == HG)
+  colsum[tid] = tid == nbk ? len : S;
+  if (tid == 0 && nbk == HG) colsum[HG] = len;
   __syncthreads();
-  uint64_t v = 0;
-  if (tid < HG)
-    for (uint32_t q = 0; q < NG; ++q) v += part[tid + q * HG];
+  const uint64_t v = tid < nbk ? (uint64_t)(colsum[tid + 1] - colsum[tid]) : 0u;
   uint64_t tot;
-  const uint64_t ex = block_excl_scan(tid < nbk ? v : 0, sh, &tot);
+  const uint64_t ex = block_excl_scan(v, sh, &tot);
   if (tid < nbk) segbase[(uint64_t)m * nbk + tid] = (uint64_t)m * g.records_per_map + ex;
   if (tid == 0) {
     const int64_t off = (int64_t)len * g.rec_size;
