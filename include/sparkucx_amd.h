@@ -224,8 +224,9 @@ typedef struct sux_tuning {
                                -1 or 0 every group's K1 -> K2 -> K3 on one of two streams    */
   int32_t msd_direct;       /* two-level small-record passes (small_kernel 4): bit 0 pass A, bit 1
                                pass B store each record from its registers straight to its
-                               sorted place instead of through the LDS stage (the L2 merges a
-                               chunk's / segment's lines); -1 or 0 both staged                  */
+                               sorted place instead of through the LDS stage (measured slower);
+                               bit 2: pass A prefetches its next chunk into LDS by DMA
+                               (global_load_lds), one workgroup per CU; -1 or 0 none            */
   int32_t reserved[1];
 } sux_tuning;
 int sux_node_set_tuning(sux_node* node, const sux_tuning* tuning);

@@ -407,10 +407,19 @@ constexpr uint32_t kM16LoShort = 8;
 constexpr uint32_t kM16MaxChunks = 512;   // chunks per map pass B's run table holds (2 Mi records)
 constexpr uint32_t kM16MaxChunksShort = 64;  // LO 8: maps of <= 256 Ki records
 
+// A workgroup barrier that leaves LDS-DMA prefetches in flight: this wave's LDS accesses are
+// complete (lgkmcnt(0)) and every wave arrived — no vmcnt wait, which __syncthreads' fence would
+// emit while a global_load_lds is outstanding (cdna_hip_programming.md, "Pipelining across
+// barriers").  The "memory" clobber keeps the compiler from moving memory accesses across it.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // Block exclusive scan, in (digit, wave) order, of u16 per-wave digit counters wc[NW][NB]
 // (NW*64 threads; each thread owns E = NB/64 consecutive (digit, wave) entries).  Counts and
-// prefixes fit u16: a chunk holds kM16Chunk records.  Two barriers; wsum[NW] scratch.
-template <uint32_t NB, uint32_t NW>
+// prefixes fit u16: a chunk holds kM16Chunk records.  Two barriers (RAW: lds_barrier); wsum[NW]
+// scratch.
+template <uint32_t NB, uint32_t NW, bool RAW = false>
 __device__ __forceinline__ void scan_digit_wave16(uint16_t* wc, uint32_t* wsum, int tid, int lane,
                                                   int wave) {
   constexpr uint32_t E = NB / kWave;
@@ -422,7 +431,7 @@ __device__ __forceinline__ void scan_digit_wave16(uint16_t* wc, uint32_t* wsum, 
   }
   const uint32_t incl = wave_incl_scan(sum, lane);
   if (lane == kWave - 1) wsum[wave] = incl;
-  __syncthreads();
+  if constexpr (RAW) lds_barrier(); else __syncthreads();
   uint32_t run = incl - sum;
 #pragma unroll
   for (uint32_t w = 0; w < NW; ++w) run += w < (uint32_t)wave ? wsum[w] : 0u;
@@ -433,7 +442,7 @@ __device__ __forceinline__ void scan_digit_wave16(uint16_t* wc, uint32_t* wsum, 
     wc[w * NB + d] = (uint16_t)run;
     run += v;
   }
-  __syncthreads();
+  if constexpr (RAW) lds_barrier(); else __syncthreads();
 }
 
 template <uint32_t NW, uint32_t DB>  // stage[CH] u32x4 (its first NW words double as wsum) | wc[NW][2^DB] u16
@@ -555,6 +564,99 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16a(PartDev pd, MapGroup g, u
     __syncthreads();
     for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
     __syncthreads();
+  }
+}
+
+// Pass A with its next chunk prefetched by LDS-DMA (msd_direct bit 2, round 4): one 512-thread
+// workgroup per CU and two 64 KB chunk buffers in LDS.  While chunk k is ranked, bucket-sorted
+// in place in its buffer and written back, chunk k + 1 streams into the other buffer through
+// global_load_lds_dwordx4 (no VGPRs: the two-workgroup k_msd16a has no registers for a second
+// chunk and no prefetch at all).  Barriers inside the loop are raw (lds_barrier), so the
+// prefetch stays in flight across them; the only vmcnt(0) is at the top of an iteration, where
+// the chunk about to be read must have landed.  Same bytes as k_msd16a.
+template <int KW, uint32_t DB, uint32_t LO>
+__global__ __launch_bounds__(512, 1) void k_msd16a_dma(PartDev pd, MapGroup g, uint32_t cpm,
+                                                      uint32_t nbk, uint16_t* __restrict__ offs,
+                                                      uint16_t* __restrict__ pids_out,
+                                                      uint8_t* __restrict__ tmp) {
+  resolve_seed(pd);
+  constexpr uint32_t NW = 8, NB = 1u << DB, NT = NW * kWave, CH = kM16Chunk, PT = CH / NT;
+  __shared__ __attribute__((aligned(16))) u32x4 buf0[CH];
+  __shared__ __attribute__((aligned(16))) u32x4 buf1[CH];
+  __shared__ uint16_t wc[NW * NB];
+  __shared__ uint32_t wsum[NW];
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  const int kw0 = pd.key_offset / 4;
+  const u32x4* recs = reinterpret_cast<const u32x4*>(g.recs);
+  u32x4* t4 = reinterpret_cast<u32x4*>(tmp);
+  const uint32_t items = g.num_maps * cpm, G = gridDim.x, b = xcd_map(blockIdx.x, G);
+  const uint32_t it0 = (uint32_t)((uint64_t)items * b / G), it1 = (uint32_t)((uint64_t)items * (b + 1) / G);
+  struct Item {
+    uint64_t c0;
+    uint32_t n;
+  };
+  auto item = [&](uint32_t it) {
+    const uint32_t m = it / cpm, c = it - m * cpm;
+    Item k;
+    k.c0 = (uint64_t)m * g.records_per_map + (uint64_t)c * CH;
+    k.n = it < it1 ? m16_chunk_len(m16_map_len(g, m), c) : 0u;
+    return k;
+  };
+  // the chunk's records, in order, land linearly in `dst` (a wave-instruction writes 1 KB: the
+  // LDS address is wave-uniform + 16 x lane); records past a short chunk re-read its last one
+  auto prefetch = [&](const Item& k, u32x4* dst) {
+    if (k.n == 0) return;
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j) {
+      const uint32_t e0 = wave * (PT * kWave) + j * kWave;
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(recs + k.c0 + min(e0 + (uint32_t)lane, k.n - 1)),
+          (__attribute__((address_space(3))) void*)(dst + e0), 16, 0, 0);
+    }
+  };
+  for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
+  if (it0 < it1) prefetch(item(it0), buf0);
+  for (uint32_t it = it0; it < it1; ++it) {
+    u32x4* cur = ((it - it0) & 1) ? buf1 : buf0;
+    u32x4* nxt = ((it - it0) & 1) ? buf0 : buf1;
+    const Item k = item(it);
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA of chunk `it` (and earlier stores) done
+    lds_barrier();                  // ... and every other wave's; nxt was last read before here
+    if (it + 1 < it1) prefetch(item(it + 1), nxt);
+    u32x4 rv[PT];
+    uint32_t h[PT], rank[PT];
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j) rv[j] = cur[wave * (PT * kWave) + j * kWave + lane];
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j) {
+      const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+      const bool valid = e < k.n;
+      uint32_t p = 0;
+      if (valid) {
+        p = m16_pid<KW>(pd, rv[j], kw0);
+        if (pids_out) pids_out[k.c0 + e] = (uint16_t)p;
+      }
+      h[j] = (p >> LO) & (NB - 1);
+      rank[j] = wave_rank<DB, uint16_t>(h[j], valid, wc + wave * NB, lt_mask);
+    }
+    lds_barrier();
+    scan_digit_wave16<NB, NW, true>(wc, wsum, tid, lane, wave);
+    // every wave read its records of `cur` before the first barrier above: sort them into it
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j)
+      if (rank[j] != ~0u) cur[wc[wave * NB + h[j]] + rank[j]] = rv[j];
+    lds_barrier();
+    // the chunk goes back to its own place, in bucket order: one contiguous write
+#pragma unroll
+    for (uint32_t q = 0; q < PT; ++q) {
+      const uint32_t i = tid + q * NT;
+      if (i < k.n) t4[k.c0 + i] = cur[i];
+    }
+    for (uint32_t hb = tid; hb < nbk; hb += NT)
+      offs[(uint64_t)it * nbk + hb] = (uint16_t)wc[hb];  // wc[0][hb]: bucket start in the chunk
+    lds_barrier();
+    for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
   }
 }
 
@@ -919,10 +1021,17 @@ hipError_t launch_msd16(const PartDev& pd, const MapGroup& g, uint8_t* d_out, in
     hipLaunchKernelGGL((k_msd16a<KW, NWA, DB, LOV, D>), ga, dim3(NWA * kWave), ldsa, s, pd, g,     \
                        cpm, nbk, offs, d_pids, tmp);                                               \
   } while (0)
-#define SUX_M16A(KW, DB, LOV)                                 \
-  do {                                                        \
-    if (tn.msd_direct & 1) SUX_M16A_D(KW, DB, LOV, true);     \
-    else SUX_M16A_D(KW, DB, LOV, false);                      \
+#define SUX_M16A(KW, DB, LOV)                                                              \
+  do {                                                                                     \
+    if (tn.msd_direct & 4) {                                                               \
+      const dim3 gd(std::min<uint32_t>(g.num_maps * cpm, ncu));                            \
+      hipLaunchKernelGGL((k_msd16a_dma<KW, DB, LOV>), gd, dim3(512), 0, s, pd, g, cpm, nbk, \
+                         offs, d_pids, tmp);                                               \
+    } else if (tn.msd_direct & 1) {                                                        \
+      SUX_M16A_D(KW, DB, LOV, true);                                                       \
+    } else {                                                                               \
+      SUX_M16A_D(KW, DB, LOV, false);                                                      \
+    }                                                                                      \
   } while (0)
 #define SUX_M16AK(DB, LOV)                   \
   do {                                       \
