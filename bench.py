@@ -351,7 +351,8 @@ def maps_2e27_leg(node, part, data, out, n: int, rs: int, R: int, dev, steps: in
             "GB/s": round(n * rs / dt / 1e9, 1), "index_consistent": ok}
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r03.json")
+# newest first: a (workload, kernel) pair not profiled in round 4 falls back to round 3's counters
+PMC_FILES = [os.path.join(ROOT, "profiles", f) for f in ("pmc_r04.json", "pmc_r03.json")]
 
 
 def plugin_leg(node, part, data, rs: int, R: int, rpm: int, gm: int, groups: int, dev,
@@ -662,19 +663,22 @@ def self_check(node, part, data, out, index, n: int, rs: int, rpm: int, R: int,
 
 def load_traffic(workload: str, kernel: str) -> dict | None:
     """HBM bytes per record of `kernel` under `workload`, from the committed PMC summary
-    (profiles/pmc_r03.json, written by profiles/collect_pmc.py: one rocprofv3 pass per counter
+    (profiles/pmc_r04.json, else pmc_r03.json; written by profiles/collect_pmc.py: one rocprofv3 pass per counter
     group; 2 x FETCH_SIZE + WRITE_SIZE per the microarch guide).  The entry is keyed by workload
     and by the kernel the library reports it launched (sux_kernel_variant), so a line never
     borrows another kernel's counters; None when that pair was not profiled."""
-    try:
-        with open(PMC_FILE) as f:
-            ks = json.load(f)["workloads"][workload]["kernels"]
-        # a slot that runs several kernels ("k_bucket16a+k_bucket16b") sums their bytes
-        per = sum(ks[k]["hbm_bytes_per_launch"] / ks[k]["records_per_launch"]
-                  for k in kernel.split("+"))
-        return {"bytes_per_record": per, "source": f"profiles/pmc_r03.json:{workload}/{kernel}"}
-    except (OSError, KeyError, ValueError, ZeroDivisionError):
-        return None
+    for path in PMC_FILES:
+        try:
+            with open(path) as f:
+                ks = json.load(f)["workloads"][workload]["kernels"]
+            # a slot that runs several kernels ("k_bucket16a+k_bucket16b") sums their bytes
+            per = sum(ks[k]["hbm_bytes_per_launch"] / ks[k]["records_per_launch"]
+                      for k in kernel.split("+"))
+            return {"bytes_per_record": per,
+                    "source": f"profiles/{os.path.basename(path)}:{workload}/{kernel}"}
+        except (OSError, KeyError, ValueError, ZeroDivisionError):
+            continue
+    return None
 
 
 def launched_rank() -> bool:

@@ -8,6 +8,8 @@
 #include <rccl/rccl.h>
 
 #include <fcntl.h>
+#include <dirent.h>
+#include <sys/resource.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -782,8 +784,30 @@ void* ipc_open_fresh(sux_node* node, const uint8_t* handle) {
   const std::string key(reinterpret_cast<const char*>(handle), 64);
   for (int attempt = 0; attempt < 2; ++attempt) {
     void* base = nullptr;
-    hip_check(hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess),
-              "hipIpcOpenMemHandle");
+    const hipError_t e = hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) {
+      // reported at once, with what a diagnosis needs (the round-3 failure): the
+      // exporter's address and pid as ROCm 7.2 lays them in the handle, and this process's open
+      // descriptors against its limit (an import opens one)
+      uint64_t va = 0;
+      uint32_t pid = 0;
+      std::memcpy(&va, handle, 8);
+      std::memcpy(&pid, handle + 8, 4);
+      struct rlimit rl {};
+      (void)getrlimit(RLIMIT_NOFILE, &rl);
+      long fds = 0;
+      if (DIR* d = opendir("/proc/self/fd")) {
+        while (readdir(d)) ++fds;
+        closedir(d);
+      }
+      char msg[256];
+      std::snprintf(msg, sizeof msg,
+                    "hipIpcOpenMemHandle: %s (handle of exporter pid %u, address 0x%llx; "
+                    "%ld open descriptors, limit %llu)",
+                    hipGetErrorString(e), pid, (unsigned long long)va, fds - 2,
+                    (unsigned long long)rl.rlim_cur);
+      raise(SUX_EHIP, msg);
+    }
     auto it = node->ipc_maps.find(base);
     if (it == node->ipc_maps.end()) {
       node->ipc_maps[base] = {key, 1};

@@ -89,3 +89,24 @@ def test_reopened_address_maps_the_new_allocation():
     finally:
         proc.join(60)
         assert proc.exitcode == 0
+
+
+def test_unresolvable_handle_fails_once_with_a_diagnosis():
+    """A handle the runtime cannot resolve (here: a live handle with its exporter pid field
+    pointing at a process that exported nothing) fails at once — no retry loop (round 3 had
+    one) — with the exporter pid / address and this process's descriptor count in the message
+    (DESIGN.md §5).  The runtime itself spends ~10 s on it before it gives up."""
+    sys.path.insert(0, ROOT)
+    from sparkucx_amd import native as N
+    from sparkucx_amd.shuffle import Node
+    node = Node(device=0)
+    try:
+        desc = bytearray(72)
+        desc[0:8] = (0x7f0000000000).to_bytes(8, "little")
+        desc[8:12] = (1).to_bytes(4, "little")  # pid 1 exported nothing
+        with pytest.raises(N.SuxError) as e:
+            node.ipc_open(bytes(desc))
+        assert e.value.code == N.SUX_EHIP
+        assert "exporter pid 1" in str(e.value) and "open descriptors" in str(e.value)
+    finally:
+        node.close()
