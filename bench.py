@@ -746,6 +746,9 @@ def main():
                     help="test mode at N=1: run the N>1 pipeline (peer-major partition, "
                          "overlapped ncclAllGather + ncclAllToAllv) on a one-rank RCCL "
                          "communicator, so the RCCL calls run on a 1-GPU box")
+    ap.add_argument("--exchange-one-call", action="store_true",
+                    help="rccl: each group's all-gather + plan + all-to-all in one "
+                         "sux_exchange_group call on the comm stream (A/B against post/issue)")
     ap.add_argument("--map-pipeline", type=int, default=1,
                     help="N=1: 1 = one sux_partition_maps_pipelined call per step (launch "
                          "groups on the node's two map streams, co-resident K1/K3 shapes); "
@@ -1018,6 +1021,10 @@ def main():
                     send_free[(j - 1) % NB].record(comm)
                     node.pull_group(world, rank, srcs[s], gi, mg, R, recv[j % 2],
                                     rbytes[j:j + 1], stream=comm)
+            elif args.exchange_one_call:
+                rb = node.exchange_group(send[s], ix, mg, R, gi, recv[j % 2], stream=comm)
+                rbytes[j] = int(rb.sum())
+                send_free[s].record(comm)
             else:
                 rb = node.exchange_group_issue(tickets.pop(j), send[s], recv[j % 2], stream=comm)
                 rbytes[j] = int(rb.sum())
@@ -1100,8 +1107,36 @@ def main():
                 runs = torch.bincount(seg * (hi - lo) + (pid - lo), minlength=world * mg * (hi - lo))
                 want = ((t[:, :, lo + 1:hi + 1] - t[:, :, lo:hi]) // rs).reshape(-1)
                 if not (bool(rise.all()) and torch.equal(runs, want)):
-                    raise RuntimeError(f"self-check: rank {rank} group {j}: received blocks are "
-                                       "not grouped by partition as the index says")
+                    bad = (~rise).nonzero().flatten()
+                    sb = send[j % NB]
+                    same = world == 1 and torch.equal(rbuf[:exp], sb[:exp])
+                    spid = node.partition_ids(part, sb[:exp], rs).to(torch.int64) if world == 1 else None
+                    sdesc = "" if spid is None else (
+                        f"; send slab falls {int((spid[1:] < spid[:-1]).sum())} times, "
+                        f"first at {(spid[1:] < spid[:-1]).nonzero().flatten()[:4].tolist()}")
+                    if world == 1:
+                        diff = (rbuf[:exp] != sb[:exp]).nonzero().flatten()
+                        d0 = int(diff[0]) if diff.numel() else -1
+                        sdesc += (f"; {diff.numel()} bytes differ, first at {d0}, last at "
+                                  f"{int(diff[-1]) if diff.numel() else -1}; received bytes there "
+                                  f"{rbuf[d0:d0 + 8].tolist()} send {sb[d0:d0 + 8].tolist()}; "
+                                  f"zero bytes in the received tail: "
+                                  f"{int((rbuf[d0:exp] == 0).sum())} of {exp - d0}")
+                        del diff
+                        if args.transport == "rccl":  # again, synchronously, on one stream
+                            torch.cuda.synchronize(dev)
+                            node.exchange_group(sb, index[j * gm * (R + 1):(j * gm + mg) * (R + 1)],
+                                                mg, R, gi, rbuf)
+                            torch.cuda.synchronize(dev)
+                            sdesc += f"; equal after a synchronous re-exchange: {torch.equal(rbuf[:exp], sb[:exp])}"
+                    raise RuntimeError(
+                        f"self-check: rank {rank} group {j}: received blocks are not grouped by "
+                        f"partition as the index says ({bad.numel()} falls, first at records "
+                        f"{bad[:4].tolist()}, pids there {pid[bad[:4]].tolist()} -> "
+                        f"{pid[bad[:4] + 1].tolist()}; runs differ at "
+                        f"{(runs != want).nonzero().flatten()[:4].tolist()} of {runs.numel()}, "
+                        f"{cnt.tolist()[:4]} records in the first blocks; received == send slab: "
+                        f"{same}{sdesc})")
                 msums[2:] += word_sums(rbuf[:exp])
             msums[:2] += word_sums(data[r0 * rs:r1 * rs])
             check_stats["groups"] += 1
@@ -1124,7 +1159,7 @@ def main():
                                                index=index[m0 * (R + 1):(m0 + mg) * (R + 1)],
                                                peer_bytes=peer[s], workspace=ws[s], stream=comp)
                 part_done[s].record(comp)
-                if args.transport == "rccl":
+                if args.transport == "rccl" and not args.exchange_one_call:
                     post(k)
                 if k >= 1:
                     exchange(k - 1)

@@ -286,7 +286,7 @@ int sux_partition_maps_peer_major(sux_node* node, const sux_partitioner* part,
 
 /* Exchange plan of one peer-major group (host arithmetic, no device access; usable on CPU):
  * from the all-gathered index tables gathered[g][m][0..R] (world*num_maps*(R+1) int64) compute,
- * for `rank`, the byte counts/displacements of ncclAllToAllv.  Received layout on rank h:
+ * for `rank`, the per-peer byte counts/displacements of the all-to-all.  Received layout on rank h:
  * [source g][map m of g][partitions owned by h]. */
 int sux_plan_group(int32_t world, int32_t rank, int32_t num_maps, int32_t num_partitions,
                    const int64_t* gathered_index, uint64_t* sendcounts, uint64_t* sdispls,
@@ -299,7 +299,9 @@ int64_t sux_plan_block_offset(int32_t world, int32_t rank, int32_t num_maps,
 
 /* One pipelined exchange step over the node's RCCL communicator: all-gather this rank's
  * num_maps index tables into d_gathered_index (device, world*num_maps*(R+1) int64), bring them
- * to the host (the only host sync), plan (sux_plan_group) and ncclAllToAllv d_send -> d_recv.
+ * to the host (the only host sync), plan (sux_plan_group) and all-to-all d_send -> d_recv.
+ * Every all-to-all of the library is grouped ncclSend/ncclRecv pieces of <= 256 MiB per peer:
+ * the RCCL that torch ships (2.26.6) drops the second half of an ncclAllToAllv count past 1 GiB.
  * recv_bytes (host, world u64, nullable) receives the per-source byte counts. */
 int sux_exchange_group(sux_node* node, const void* d_send, const int64_t* d_index,
                        int32_t num_maps, int32_t num_partitions, int64_t* d_gathered_index,
@@ -309,7 +311,7 @@ int sux_exchange_group(sux_node* node, const void* d_send, const int64_t* d_inde
  * the all-gather of this launch group's index tables into d_gathered and their asynchronous
  * read-back into pinned staging on `stream` and returns a ticket; _issue (any thread) waits on
  * the host for that read-back, plans the counts (sux_plan_group) and enqueues the
- * partition-aligned ncclAllToAllv on ITS stream, over a second communicator split from the
+ * partition-aligned all-to-all on ITS stream, over a second communicator split from the
  * node's (made by the first _post of every rank, a collective).  The bench posts group k right
  * after enqueueing its partition and then issues group k - 1: the all-gather of k overlaps the
  * all-to-all of k - 1 and the all-to-all stream is fed before its previous transfer drains.
@@ -482,7 +484,7 @@ int sux_map_output_index(sux_node* node, int32_t shuffle_id, int32_t map_index,
  * Replaces the driver-table GET (UcxWorkerWrapper.fetchDriverMetadataBuffer :176-196) by an
  * all-gather of the committed maps' directory entries, and the phase-1/phase-2 GETs
  * (UcxShuffleClient.java:50-127, OnOffsetsFetchCallback.java:44-92) by one partition-aligned
- * ncclAllToAllv per round of map batches over xGMI (RCCL communicator) or, with a bootstrap and
+ * all-to-all per round of map batches over xGMI (RCCL communicator) or, with a bootstrap and
  * no communicator, by the same plan as one-sided pulls from the owners' IPC-mapped batch slabs.
  * The receive buffer is sized exactly from the gathered index tables.  sux_exchange is
  * sux_exchange_maps over every map + sux_exchange_wait: it returns when this rank's blocks are
@@ -491,7 +493,7 @@ int sux_exchange(sux_node* node, int32_t shuffle_id, void* stream);
 /* The exchange of one window of map tasks, asynchronous: every rank calls it with the same
  * [first_map_index, first_map_index + num_maps) once the maps it writes there are enqueued.  It
  * waits only for this rank's writes of that window (later batches keep running), all-gathers
- * their directory entries, and enqueues on `stream` one partition-aligned ncclAllToAllv per round
+ * their directory entries, and enqueues on `stream` one partition-aligned all-to-all per round
  * of batches (round k = every rank's k-th batch of the window; counts/displacements straight from
  * the index tables; a batch's peer-major slab is the send buffer as it stands), or the same plan
  * as one-sided IPC pulls.  Maps already exchanged are skipped.  Returns without a host wait on

@@ -55,6 +55,30 @@ void nccl_check(ncclResult_t r, const char* what) {
   // hipGetLastError(), so it must not survive a successful RCCL call
   (void)hipGetLastError();
 }
+// The all-to-all of every exchange: per peer, the byte range [sd[h], sd[h] + sc[h]) of `send` goes
+// to peer h and [rd[h], rd[h] + rc[h]) of `recv` arrives from it, as grouped ncclSend/ncclRecv
+// pieces of at most kA2aPiece bytes.  ncclAllToAllv itself is not used: the RCCL that torch
+// ships (2.26.6) delivers only the first half of a 1.68 GB per-peer count (torch's own
+// all_to_all_single shows it too; 0.84 GB arrives whole — tools/a2a_probe.py,
+// profiles/r04_f/a2a_probe.txt).  Both sides of a pair cut the same count the same way, so the
+// pieces pair up in order without any agreement between ranks.
+constexpr size_t kA2aPiece = size_t(256) << 20;
+void all_to_all_pieces(const uint8_t* send, const uint64_t* sc, const uint64_t* sd, uint8_t* recv,
+                       const uint64_t* rc, const uint64_t* rd, int W, ncclComm_t comm,
+                       hipStream_t s) {
+  nccl_check(ncclGroupStart(), "ncclGroupStart");
+  ncclResult_t r = ncclSuccess;
+  for (int h = 0; h < W && r == ncclSuccess; ++h) {
+    for (uint64_t o = 0; o < sc[h] && r == ncclSuccess; o += kA2aPiece)
+      r = ncclSend(send + sd[h] + o, std::min<uint64_t>(kA2aPiece, sc[h] - o), ncclUint8, h, comm, s);
+    for (uint64_t o = 0; o < rc[h] && r == ncclSuccess; o += kA2aPiece)
+      r = ncclRecv(recv + rd[h] + o, std::min<uint64_t>(kA2aPiece, rc[h] - o), ncclUint8, h, comm, s);
+  }
+  const ncclResult_t e = ncclGroupEnd();
+  nccl_check(r, "ncclSend/ncclRecv");
+  nccl_check(e, "ncclGroupEnd(all-to-all)");
+}
+
 // A failed check throws SuxError; the message expression is evaluated only then (some checks run
 // once per block of a fetch).
 #define require(ok, code, ...)                    \
@@ -2098,16 +2122,8 @@ int sux_exchange_group(sux_node* node, const void* d_send, const int64_t* d_inde
       return;
     }
     require(d_send && d_recv, SUX_EINVAL, "send/recv buffer is NULL");
-    std::vector<size_t> a(W), b(W), c(W), d(W);
-    for (int h = 0; h < W; ++h) {
-      a[h] = sc[h];
-      b[h] = sd[h];
-      c[h] = rc[h];
-      d[h] = rd[h];
-    }
-    nccl_check(ncclAllToAllv(d_send, a.data(), b.data(), d_recv, c.data(), d.data(), ncclUint8,
-                             node->comm, s),
-               "ncclAllToAllv");
+    all_to_all_pieces(static_cast<const uint8_t*>(d_send), sc.data(), sd.data(),
+                      static_cast<uint8_t*>(d_recv), rc.data(), rd.data(), W, node->comm, s);
   });
 }
 
@@ -2179,11 +2195,9 @@ int sux_exchange_group_issue(sux_node* node, sux_xticket* ticket, const void* d_
       return;
     }
     require(d_send && d_recv, SUX_EINVAL, "send/recv buffer is NULL");
-    std::vector<size_t> a(sc.begin(), sc.end()), b(sd.begin(), sd.end()), c(rc.begin(), rc.end()),
-        d(rd.begin(), rd.end());
-    nccl_check(ncclAllToAllv(d_send, a.data(), b.data(), d_recv, c.data(), d.data(), ncclUint8,
-                             node->comm_x ? node->comm_x : node->comm, s),
-               "ncclAllToAllv");
+    all_to_all_pieces(static_cast<const uint8_t*>(d_send), sc.data(), sd.data(),
+                      static_cast<uint8_t*>(d_recv), rc.data(), rd.data(), W,
+                      node->comm_x ? node->comm_x : node->comm, s);
   });
 }
 
@@ -3015,25 +3029,14 @@ int sux_exchange_maps(sux_node* node, int32_t shuffle_id, int32_t first, int32_t
     std::pair<void*, uint64_t> hostblk{nullptr, 0};
     try {
       if (!ipc) {
-        // 3a. RCCL: one ncclAllToAllv per round (grouped send/recv over xGMI inside RCCL)
-        std::vector<size_t> a((size_t)W), b((size_t)W), c((size_t)W), d((size_t)W);
+        // 3a. RCCL: one all-to-all per round (grouped send/recv pieces over xGMI)
         for (int k = 0; k < P.rounds; ++k) {
           const int32_t pe = P.piece[(size_t)k * W + me];
           uint8_t* sendbuf = pe >= 0 ? my_slab.at(all[pe].batch) : nullptr;
           uint8_t* recvbuf = recv->buf.ptr ? recv->buf.ptr + P.base[k] : nullptr;
-          // RCCL rejects NULL buffers even for zero counts: any device word will do
-          uint8_t* dummy = reinterpret_cast<uint8_t*>(node->d_err);
-          for (int h = 0; h < W; ++h) {
-            const size_t kh = (size_t)k * W + h;
-            a[h] = P.sc[kh];
-            b[h] = P.sd[kh];
-            c[h] = P.rc[kh];
-            d[h] = P.rd[kh];
-          }
-          nccl_check(ncclAllToAllv(sendbuf ? sendbuf : dummy, a.data(), b.data(),
-                                   recvbuf ? recvbuf : dummy, c.data(), d.data(), ncclUint8,
-                                   node->comm, s),
-                     "ncclAllToAllv");
+          const size_t kw = (size_t)k * W;
+          all_to_all_pieces(sendbuf, &P.sc[kw], &P.sd[kw], recvbuf, &P.rc[kw], &P.rd[kw], W,
+                            node->comm, s);
         }
       } else {
         // 3b. bootstrap: the same plan as one-sided pulls (OnOffsetsFetchCallback.java:80-87's

@@ -238,6 +238,32 @@ def test_exchange_group_rccl_one_rank():
         gp.close()
 
 
+def test_exchange_past_1_gib_per_peer_arrives_whole():
+    """A per-peer count past 1 GiB (1.68 GB: a 32-map TeraSort group at two ranks) arrives whole
+    through the one-rank communicator, by sux_exchange_group and by post/issue.  torch's RCCL
+    2.26.6 ncclAllToAllv delivers only the first half of such a count (round 4,
+    tools/a2a_probe.py); the library sends it as 256 MiB send/recv pieces."""
+    from sparkucx_amd.shuffle import Node
+    MAP, R, maps = 104857600, 200, 16
+    nbytes = MAP * maps
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    send = torch.randint(1, 256, (nbytes,), dtype=torch.uint8, device="cuda", generator=g)
+    row = torch.div(torch.arange(R + 1, dtype=torch.int64) * MAP, R, rounding_mode="floor")
+    index = row.repeat(maps).to("cuda")
+    gathered = torch.empty_like(index)
+    recv = torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
+    with Node(device=0, rank=0, world_size=1, comm_id=N.unique_id()) as node:
+        rb = node.exchange_group(send, index, maps, R, gathered, recv)
+        torch.cuda.synchronize()
+        assert rb.tolist() == [nbytes] and torch.equal(recv, send)
+        recv.zero_()
+        t = node.exchange_group_post(index, maps, R, gathered)
+        rb = node.exchange_group_issue(t, send, recv)
+        torch.cuda.synchronize()
+        assert rb.tolist() == [nbytes] and torch.equal(recv, send)
+
+
 # ---- full-size properties (BASELINE-scale batches, size-independent checks) ----------------------
 def test_large_batch_properties(gpu_node):
     """10^8 TeraSort records (10 GB, config-2 batch scale): multiset preserved, stable, sorted by
