@@ -200,8 +200,10 @@ typedef struct sux_tuning {
   int32_t small_wgs_per_cu; /* two-level small-record kernels (small_kernel 4): workgroups per CU
                                of each pass, 1 or 2 (0: 2); 1 lets two launch groups' passes
                                share every CU                                                  */
-  int32_t sort_msd;         /* reduce-side sort: 1 (0) one top-digit pass + per-bucket LDS sort
-                               when the buckets fit, 2 LSD digit passes only                   */
+  int32_t sort_msd;         /* reduce-side sort: 1 (0) top digit + per-bucket LDS sort, the top
+                               digit chunked (chunks sorted in place, buckets read as runs) when
+                               it has <= 12 bits and n <= 2048 x 4096; 3 the same with the one-
+                               pass top-digit partition; 2 LSD digit passes only               */
   int32_t exchange_self;    /* 1: the exchange also moves this rank's own maps' owned ranges
                                through its transport into the receive buffer (loopback; at
                                world 1 it runs the whole RCCL / IPC path on one GPU); 0 or -1: no */

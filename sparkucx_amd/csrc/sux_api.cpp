@@ -1225,7 +1225,7 @@ int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
     require(in(t->small_waves, {8, 16}), SUX_EINVAL, "small_waves must be 8 or 16");
     require(in(t->scatter_order, {1, 2}), SUX_EINVAL, "scatter_order must be 1 or 2");
     require(in(t->small_wgs_per_cu, {1, 2}), SUX_EINVAL, "small_wgs_per_cu must be 1 or 2");
-    require(in(t->sort_msd, {1, 2}), SUX_EINVAL, "sort_msd must be 1 or 2");
+    require(in(t->sort_msd, {1, 2, 3}), SUX_EINVAL, "sort_msd must be 1, 2 or 3");
     require(in(t->s6_chunk, {256, 384, 512, 1024}), SUX_EINVAL, "s6_chunk must be 256..1024");
     require(t->tiles_per_item >= 0 && t->tiles_per_item <= 4096, SUX_EINVAL,
             "tiles_per_item must be 0..4096");
@@ -3724,6 +3724,17 @@ uint64_t sort_plan_offset(uint64_t n, uint32_t record_size) {
   return most;
 }
 
+// The chunked top pass's workspace, after the plan slot: the chunked pairs, the chunks' bucket
+// starts (sized for 2^kTopMaxBits buckets), the bucket totals.  0: n takes the one-pass top pass
+// (more than kTopMaxChunks chunks).
+uint64_t top_chunked_bytes(uint64_t n) {
+  const uint64_t nch = (n + sux::kTopChunk - 1) / sux::kTopChunk;
+  if (n == 0 || nch > sux::kTopMaxChunks) return 0;
+  auto up = [](uint64_t v) { return (v + 255) / 256 * 256; };
+  const uint64_t R = 1ull << sux::kTopMaxBits;
+  return up(16 * n) + up(nch * (R + 1) * 2) + up(R * 4);
+}
+
 int sort_key_bits(int32_t kind, int32_t key_len) {
   switch (kind) {
     case SUX_SORT_BYTES:
@@ -3744,7 +3755,7 @@ int sort_key_bits(int32_t kind, int32_t key_len) {
 int sux_sort_workspace_size(uint64_t n, uint32_t record_size, uint64_t* bytes) {
   return guard([&] {
     require(bytes, SUX_EINVAL, "NULL argument");
-    *bytes = sort_plan_offset(n, record_size) + sux::kSortPlanBytes;
+    *bytes = sort_plan_offset(n, record_size) + sux::kSortPlanBytes + top_chunked_bytes(n);
   });
 }
 
@@ -3811,7 +3822,7 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
   const bool all_passes = node->tuning.sort_all_passes == 1;
 
   // ---- the default: MSD planned on the device, no host wait (graph-capturable).  One stable
-  // digit pass over the top tb varying key bits (k_sort_plan finds them in the key span), then
+  // digit pass over the top tb varying key bits (the span reduction finds them in the key span), then
   // every bucket sorted by the lower varying 8-bit digits — in LDS (k_sort_local, <= 4096 pairs)
   // or, for a skewed key set's larger buckets, through global memory by one workgroup each
   // (k_sort_bucket_global).  Each pair crosses HBM twice after the top pass instead of twice per
@@ -3830,31 +3841,52 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
     sux::SortPlanDev* plan = reinterpret_cast<sux::SortPlanDev*>(ws + plan_off);
     hip_check(sux::launch_sort_pairs(static_cast<const uint8_t*>(d_in), n, record_size, key_kind,
                                      key_offset, key_len, d_seg, nseg, sbytes, a,
-                                     ws + P1.span_off, inline_rec, s),
-              "sort pairs");
-    hip_check(sux::launch_sort_plan(ws + P1.span_off, bits, tb, plan, s), "sort plan");
+                                     ws + P1.span_off, inline_rec, s, bits, tb, plan),
+              "sort pairs + plan");
     int64_t* index1 = reinterpret_cast<int64_t*>(ws + P1.index_off);
     sux::PartDev pd1 = pd;
     pd1.R = 1 << tb;
     pd1.dseed = &plan->top_lo;
-    P1.g.recs = a;
-    P1.g.err = node->d_err;
-    hip_check(sux::launch_partition_group(pd1, P1.g, lay, b, index1, nullptr, nullptr,
-                                          ws + P1.part_off, P1.ws, nullptr, sort_tn, &node->timer,
-                                          s),
-              "sort top digit pass");
+    // the top digit: chunked (each chunk sorted in place, buckets read as runs; sort_msd 0 / 1)
+    // or one stable partition pass (sort_msd 3, more pairs than kTopMaxChunks chunks, or a top
+    // digit of more than 12 bits)
+    const uint64_t top_bytes = top_chunked_bytes(n);
+    const bool chunked = node->tuning.sort_msd != 3 && tb <= sux::kTopMaxBits && top_bytes &&
+                         ws_bytes >= plan_off + sux::kSortPlanBytes + top_bytes;
+    sux::SortRuns runs;
+    if (chunked) {
+      auto up = [](uint64_t v) { return (v + 255) / 256 * 256; };
+      const uint64_t nch = (n + sux::kTopChunk - 1) / sux::kTopChunk;
+      uint8_t* top = ws + plan_off + sux::kSortPlanBytes;
+      uint16_t* offs = reinterpret_cast<uint16_t*>(top + up(16 * n));
+      uint32_t* tot = reinterpret_cast<uint32_t*>(
+          top + up(16 * n) + up(nch * ((1ull << sux::kTopMaxBits) + 1) * 2));
+      hip_check(sux::launch_top_chunks(a, n, tb, plan, top, offs, tot, index1, s),
+                "sort top digit (chunked)");
+      runs.pairs = top;
+      runs.offs = offs;
+      runs.nch = (uint32_t)nch;
+    } else {
+      P1.g.recs = a;
+      P1.g.err = node->d_err;
+      hip_check(sux::launch_partition_group(pd1, P1.g, lay, b, index1, nullptr, nullptr,
+                                            ws + P1.part_off, P1.ws, nullptr, sort_tn,
+                                            &node->timer, s),
+                "sort top digit pass");
+    }
     const sux::Tuning gt = resolve_tuning(node->tuning, false);
     if (!inline_rec && gt.gather_kernel == 3 && sux::sort_gather_fusable(record_size)) {
       // the fused sort: sorted buckets gather their records themselves, the rest after them
       hip_check(sux::launch_sort_local_planned(b, a, index1, (uint32_t)pd1.R, plan, s, d_in,
-                                               d_out, record_size),
+                                               d_out, record_size, runs),
                 "sort buckets");
       hip_check(sux::launch_gather_rest(d_in, a, b, index1, (uint32_t)pd1.R, n, plan, record_size,
                                         d_out, s),
                 "sort gather rest");
       return;
     }
-    hip_check(sux::launch_sort_local_planned(b, a, index1, (uint32_t)pd1.R, plan, s),
+    hip_check(sux::launch_sort_local_planned(b, a, index1, (uint32_t)pd1.R, plan, s, nullptr,
+                                             nullptr, 0, runs),
               "sort buckets");
     if (inline_rec)
       hip_check(sux::launch_unpair_records_sel(a, b, &plan->final_b, n, record_size, key_kind,

@@ -29,7 +29,7 @@ struct PartDev {
   const uint32_t* lut;
   int32_t lut_bits;
   int32_t pad;
-  // a sort pass's digit shift decided on the device (k_sort_plan): when set, K1 replaces `seed`
+  // a sort pass's digit shift decided on the device (make_sort_plan): when set, K1 replaces `seed`
   // with *dseed before computing any pid
   const int32_t* dseed;
 };
@@ -224,9 +224,13 @@ hipError_t launch_pull(int32_t W, int32_t me, const uint64_t* srcs, const int64_
 // Reduce-side sort (sux_sort.hip): (key, index) pairs, and the final gather of whole records.
 constexpr int kPartRadix = 7;  // internal partitioner: 12-bit digit (shift in PartDev::seed)
 constexpr int kRadixBits = 12;
+struct SortPlanDev;
+// k_sort_pairs + the key span; with `plan`, the span's reduction also plans the MSD sort (bits:
+// key bits with the segment id, tb: top-digit bits).
 hipError_t launch_sort_pairs(const uint8_t* in, uint64_t n, uint32_t rs, int kind, int key_offset,
                              int key_len, const int64_t* seg, int nseg, int sbytes, void* pairs,
-                             void* span_ws, bool inline_rec, hipStream_t s);
+                             void* span_ws, bool inline_rec, hipStream_t s, int bits = 0,
+                             int tb = 0, SortPlanDev* plan = nullptr);
 hipError_t launch_unpair_records(const void* pairs, uint64_t n, uint32_t rs, int kind,
                                  int key_offset, int key_len, int sbytes, void* out, hipStream_t s);
 // span_ws: 8 u32 (AND of key words 0..2, OR of key words 0..2) + kSortSpanBlocks x 8 u32 partials
@@ -253,8 +257,8 @@ struct SortDigits {
     ++n;
   }
 };
-// The device-planned sort (sux_sort_records with no host wait): k_sort_plan fills the first
-// fields from the key span (k_sort_plan, before the top-digit pass); every later
+// The device-planned sort (sux_sort_records with no host wait): make_sort_plan (in k_span_reduce) fills the first
+// fields from the key span (before the top-digit pass); every later
 // kernel of the sort reads its decision from here.
 struct SortPlanDev {
   int32_t top_lo;    // shift of the top digit (the tb highest varying key bits)
@@ -263,22 +267,38 @@ struct SortPlanDev {
   uint32_t pad;
   uint32_t final_b;  // 1: the sorted pairs end in buffer b, 0: in buffer a
   int32_t kbits;     // key bits (with the segment id): the top kbits of the big-endian pair
-  uint64_t maxb;     // unused (round 3: k_sort_plan decides msd_ok / final_b, no bucket sweep)
+  uint64_t maxb;     // unused (round 3: the plan decides msd_ok / final_b, no bucket sweep)
   SortDigits dg;     // the LDS sort's digits: 8-bit, below top_lo, only those that vary
 };
 constexpr uint64_t kSortPlanBytes = 256;
 static_assert(sizeof(SortPlanDev) <= kSortPlanBytes, "plan slot");
-hipError_t launch_sort_plan(const void* span, int bits, int tb, SortPlanDev* plan, hipStream_t s);
 // The sort of every top-digit bucket, driven by the plan (a no-op unless plan->msd_ok): one LDS
 // launch per bucket-size class (each bucket on the smallest shape that holds it), then buckets
 // above kSortLocalCap through global memory.
 // recs_out != nullptr (the fused sort): the LDS launches gather their buckets' records from
 // recs_in straight into recs_out instead of writing sorted pairs; launch_gather_rest then gathers
 // every record they did not (needs sort_gather_fusable(rs)).
+// Chunked top pass (round 4): each 4096-pair chunk of the pairs sorted by the top digit in place
+// into `chunked`, offs[chunk][0..R] its bucket starts (u16), then the bucket index (bytes).  A
+// sort with R = 2^tb <= 4096 buckets and at most kTopMaxChunks chunks takes it.
+constexpr uint32_t kTopChunk = 4096;
+constexpr uint32_t kTopSegs = 32;        // chunk segments of the bucket-size column sums
+constexpr uint32_t kTopMaxChunks = 2048; // run table of the 1024-pair LDS shape (2 u32 per chunk)
+constexpr int kTopMaxBits = 12;
+hipError_t launch_top_chunks(const void* pairs, uint64_t n, int tb, const SortPlanDev* plan,
+                             void* chunked, uint16_t* offs, uint32_t* tot, int64_t* index,
+                             hipStream_t s);
+// Where k_sort_local finds its buckets after the chunked top pass (pairs == nullptr: contiguous
+// at their index range of in_pairs, the one-pass top pass's output).
+struct SortRuns {
+  const void* pairs = nullptr;
+  const uint16_t* offs = nullptr;
+  uint32_t nch = 0;
+};
 hipError_t launch_sort_local_planned(const void* in_pairs, void* out_pairs, const int64_t* d_index,
                                      uint32_t R, const SortPlanDev* plan, hipStream_t s,
                                      const void* recs_in = nullptr, void* recs_out = nullptr,
-                                     uint32_t rs = 0);
+                                     uint32_t rs = 0, const SortRuns& runs = SortRuns{});
 bool sort_gather_fusable(uint32_t rs);
 hipError_t launch_gather_rest(const void* recs_in, const void* pairs_a, const void* pairs_b,
                               const int64_t* d_index, uint32_t R, uint64_t n,

@@ -139,7 +139,7 @@ __device__ __forceinline__ void scan_digit_wave(uint32_t* wc, uint32_t* wsum, in
   __syncthreads();
 }
 
-// PartDev::dseed: the digit shift of a sort pass decided on the device (k_sort_plan).
+// PartDev::dseed: the digit shift of a sort pass decided on the device (make_sort_plan).
 __device__ __forceinline__ void resolve_seed(PartDev& pd) {
   if (pd.dseed) pd.seed = *pd.dseed;
 }

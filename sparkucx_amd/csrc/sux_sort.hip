@@ -7,7 +7,7 @@
 //                   [12, 16)} (or, for records of <= 16 bytes with the segment id, the record
 //                   itself re-laid so its key leads: inline mode); signed keys get their sign bit
 //                   flipped so unsigned order = signed order; per-block AND / OR of the key words
-//   k_span_reduce + k_sort_plan   the key span -> the top digit (the tb highest varying bits)
+//   k_span_reduce (+ make_sort_plan) the key span -> the top digit (the tb highest varying bits)
 //                   and the 8-bit LDS digits below it that vary (SortPlanDev)
 //   top pass        one stable partition of the pairs by the top digit (the map-side small-record
 //                   kernels with the internal radix partitioner, digit shift read on the device)
@@ -192,8 +192,13 @@ __global__ __launch_bounds__(256) void k_sort_pairs(const uint8_t* __restrict__ 
   }
 }
 
+__device__ void make_sort_plan(const uint32_t* span, int bits, int tb, SortPlanDev* plan);
+
+// The key span; with `plan`, thread 0 then plans the sort from it (the device-planned MSD path:
+// one launch fewer than a separate planning kernel).
 __global__ __launch_bounds__(256) void k_span_reduce(const uint32_t* __restrict__ part,
-                                                     uint32_t blocks, uint32_t* __restrict__ span) {
+                                                     uint32_t blocks, uint32_t* __restrict__ span,
+                                                     int bits, int tb, SortPlanDev* __restrict__ plan) {
   __shared__ uint32_t red[256][6];
   uint32_t v[6] = {~0u, ~0u, ~0u, 0, 0, 0};
   for (uint32_t b = threadIdx.x; b < blocks; b += 256)
@@ -208,6 +213,7 @@ __global__ __launch_bounds__(256) void k_span_reduce(const uint32_t* __restrict_
     __syncthreads();
   }
   if (threadIdx.x < 6) span[threadIdx.x] = red[0][threadIdx.x];
+  if (plan && threadIdx.x == 0) make_sort_plan(&red[0][0], bits, tb, plan);
 }
 
 // One output dword per thread and step: record j = d / W, dword w of it, read from the record
@@ -274,7 +280,8 @@ __global__ __launch_bounds__(256) void k_gather_records16(const uint8_t* __restr
 
 hipError_t launch_sort_pairs(const uint8_t* in, uint64_t n, uint32_t rs, int kind, int key_offset,
                              int key_len, const int64_t* seg, int nseg, int sbytes, void* pairs,
-                             void* span_ws, bool inline_rec, hipStream_t s) {
+                             void* span_ws, bool inline_rec, hipStream_t s, int bits, int tb,
+                             SortPlanDev* plan) {
   if (n == 0) return hipSuccess;
   const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, kSortSpanBlocks);
   uint32_t* part = static_cast<uint32_t*>(span_ws) + 8;
@@ -284,7 +291,7 @@ hipError_t launch_sort_pairs(const uint8_t* in, uint64_t n, uint32_t rs, int kin
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_span_reduce, dim3(1), dim3(256), 0, s, part, blocks,
-                     static_cast<uint32_t*>(span_ws));
+                     static_cast<uint32_t*>(span_ws), bits, tb, plan);
   return hipGetLastError();
 }
 
@@ -364,6 +371,244 @@ __device__ __forceinline__ bool key_greater(const u32x4& a, const u32x4& b, int 
 }
 constexpr int kTopDigits = 2;          // LDS digit passes before the tie fix-up
 constexpr uint32_t kMaxTieRun = 16;    // longer tie runs: every digit pass instead
+
+// Bits [sh, sh + nb) of the big-endian 128-bit pair (nb <= 32).
+__device__ __forceinline__ uint32_t pair_bits(const u32x4& w, uint32_t sh, uint32_t nb) {
+  const uint64_t hi = ((uint64_t)__builtin_bswap32(w[0]) << 32) | __builtin_bswap32(w[1]);
+  const uint64_t lo = ((uint64_t)__builtin_bswap32(w[2]) << 32) | __builtin_bswap32(w[3]);
+  const uint64_t v = sh >= 64 ? (hi >> (sh - 64)) : ((lo >> sh) | (sh ? (hi << (64 - sh)) : 0));
+  return (uint32_t)v & (uint32_t)((1ull << nb) - 1);
+}
+
+// ------------------------------------------------------------------------------------------
+// Chunked top pass (round 4; the default when the top digit has <= 12 bits and the pairs fit
+// kTopMaxChunks chunks).  The one-pass top-digit partition (k_hist16 + scans + k_scatter16s)
+// puts ~1 pair per bucket per 4096-pair chunk: every pair leaves as a lone 16-byte store (2x
+// write amplification, 131 us of the 0.64 ms sort).  Here every pass streams whole lines:
+//   k_top_chunks   each 4096-pair chunk stable-sorted by the top digit in LDS and written back to
+//                  ITS OWN place in the chunked copy, with the chunk's bucket starts (u16,
+//                  offs[chunk][0..R], the last = the chunk's pairs);
+//   k_top_colsum + k_top_scan   bucket sizes summed over the chunks -> the bucket index (bytes);
+//   k_sort_local   gathers its bucket's run from every chunk (run table in LDS: the adjacent
+//                  buckets a CU's neighbours sort read the same lines, so they come from L2);
+//   k_top_materialize   only the buckets the LDS shapes do not take (above kSortLocalCap), or
+//                  every bucket when no lower digit varies, are copied contiguously into b.
+// Stable: chunks keep input order between them and the LDS passes keep it inside a chunk.
+// ------------------------------------------------------------------------------------------
+template <uint32_t NT>
+__global__ __launch_bounds__(NT, 2 * NT / 256) void k_top_chunks(const u32x4* __restrict__ pairs,
+                                                                uint64_t n, int tb,
+                                                                const SortPlanDev* __restrict__ plan,
+                                                                u32x4* __restrict__ outp,
+                                                                uint16_t* __restrict__ offs,
+                                                                uint32_t* __restrict__ tot) {
+  if (!plan->msd_ok) return;  // every key equal: nothing reads the chunked copy
+  if (blockIdx.x == 0)         // k_top_colsum's bucket totals (atomic adds), after this launch
+    for (uint32_t b = threadIdx.x; b < (1u << tb); b += NT) tot[b] = 0;
+  constexpr uint32_t NW = NT / kWave, PT = kTopChunk / NT, CH = kTopChunk, IDX = 12, ND = 64;
+  static_assert(CH == 1u << IDX && ND * NW == NT, "chunk index bits, one scan entry per thread");
+  __shared__ uint32_t keys0[CH], keys1[CH];
+  __shared__ uint32_t wc0[2 * NW * ND];  // [pass parity][wave][digit]
+  __shared__ uint32_t wsum[NW];
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  const uint32_t R = 1u << tb, top_lo = (uint32_t)plan->top_lo;
+  const int passes = tb <= 6 ? 1 : 2;
+  const uint32_t D = passes == 1 ? (uint32_t)tb : (uint32_t)(tb + 1) / 2;  // <= 6 bits a pass
+  const uint32_t nch = (uint32_t)((n + CH - 1) / CH);
+  for (uint32_t i = tid; i < 2 * NW * ND; i += NT) wc0[i] = 0;
+  // Two workgroups per CU within 64 VGPRs: the pairs are not held across the ranking — only
+  // their keys (LDS); the sorted write reads each pair again, from the chunk just read (L2 /
+  // Infinity Cache), in sorted order, and stores it coalesced
+  for (uint32_t c = xcd_map(blockIdx.x, gridDim.x); c < nch; c += gridDim.x) {
+    const uint64_t c0 = (uint64_t)c * CH;
+    const uint32_t nc = (uint32_t)min<uint64_t>(CH, n - c0);
+    uint32_t* kin = keys0;
+    uint32_t* kout = keys1;
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j) {  // clamped, unconditional loads
+      const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+      const u32x4 p = pairs[c0 + min(e, nc - 1)];
+      if (e < nc) kin[e] = (pair_bits(p, top_lo, (uint32_t)tb) << IDX) | e;
+    }
+    __syncthreads();
+    // 1. LSD passes over (bucket << 12 | position), D bits each: wave-ballot ranks against the
+    //    wave's own digit counters, one block scan over (digit, wave)
+    for (int d = 0; d < passes; ++d) {
+      uint32_t* wc = wc0 + (d & 1) * NW * ND;
+      const uint32_t sh = IDX + d * D;
+      uint32_t key[PT], dig[PT], rank[PT];
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) {
+        const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+        const bool valid = e < nc;
+        key[j] = valid ? kin[e] : 0u;
+        dig[j] = valid ? (key[j] >> sh) & ((1u << D) - 1) : 0u;
+        rank[j] = wave_rank<6>(dig[j], valid, wc + wave * ND, lt_mask);
+      }
+      __syncthreads();
+      {  // exclusive scan in (digit, wave) order: thread t owns (digit t / NW, wave t % NW)
+        const uint32_t dg = (uint32_t)tid / NW, w = (uint32_t)tid % NW;
+        const uint32_t a = wc[w * ND + dg];
+        const uint32_t incl = wave_incl_scan(a, lane);
+        if (lane == kWave - 1) wsum[wave] = incl;
+        __syncthreads();
+        uint32_t before = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < NW; ++q) before += q < (uint32_t)wave ? wsum[q] : 0u;
+        wc[w * ND + dg] = before + incl - a;
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j)
+        if (rank[j] != ~0u) kout[wc[wave * ND + dig[j]] + rank[j]] = key[j];
+      __syncthreads();
+      for (uint32_t i = tid; i < NW * ND; i += NT) wc[i] = 0;  // next used a barrier later
+      uint32_t* t = kin;
+      kin = kout;
+      kout = t;
+    }
+    // 2. the chunk's bucket starts (a run start fills the starts of the empty buckets before
+    //    it) and the chunk back to its own place in bucket order: sorted position s takes pair
+    //    kin[s] & 4095, coalesced 16-byte stores
+    uint16_t* row = offs + (uint64_t)c * (R + 1);
+#pragma unroll
+    for (uint32_t k = 0; k < PT; ++k) {
+      const uint32_t s = tid + k * NT;
+      if (s >= nc) continue;
+      const uint32_t key = kin[s], p = key >> IDX;
+      outp[c0 + s] = pairs[c0 + (key & (CH - 1))];
+      const uint32_t q0 = s == 0 ? 0u : (kin[s - 1] >> IDX) + 1;
+      for (uint32_t q = q0; q <= p; ++q) row[q] = (uint16_t)s;
+      if (s + 1 == nc)
+        for (uint32_t q = p + 1; q <= R; ++q) row[q] = (uint16_t)nc;
+    }
+    __syncthreads();  // kin / kout are rewritten by the next chunk
+  }
+}
+
+// Bucket sizes: each workgroup sums one of kTopSegs chunk segments for 256 buckets and adds it
+// to the bucket's total (32 atomic adds per bucket; tot zeroed by k_top_chunks).
+__global__ __launch_bounds__(256) void k_top_colsum(const uint16_t* __restrict__ offs, uint32_t nch,
+                                                    uint32_t R, const SortPlanDev* __restrict__ plan,
+                                                    uint32_t* __restrict__ tot) {
+  if (!plan->msd_ok) return;
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x, sg = blockIdx.y;
+  if (b >= R) return;
+  const uint32_t c0 = (uint32_t)((uint64_t)nch * sg / kTopSegs);
+  const uint32_t c1 = (uint32_t)((uint64_t)nch * (sg + 1) / kTopSegs);
+  uint32_t sum = 0, c = c0;
+  for (; c + 8 <= c1; c += 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+      const uint16_t* row = offs + (uint64_t)(c + k) * (R + 1) + b;
+      v[k] = (uint32_t)row[1] - row[0];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) sum += v[k];
+  }
+  for (; c < c1; ++c) {
+    const uint16_t* row = offs + (uint64_t)c * (R + 1) + b;
+    sum += (uint32_t)row[1] - row[0];
+  }
+  if (sum) atomicAdd(&tot[b], sum);
+}
+
+// The bucket index (bytes, R + 1 entries) from the bucket totals; every key equal: one bucket.
+__global__ __launch_bounds__(1024) void k_top_scan(const uint32_t* __restrict__ tot, uint32_t R,
+                                                   uint64_t n, const SortPlanDev* __restrict__ plan,
+                                                   int64_t* __restrict__ index) {
+  __shared__ uint64_t sh[2 * kWave + 1];
+  const uint32_t tid = threadIdx.x;
+  if (!plan->msd_ok) {
+    for (uint32_t b = tid; b <= R; b += 1024) index[b] = b == 0 ? 0 : (int64_t)(16 * n);
+    return;
+  }
+  const uint32_t E = (R + 1023) / 1024;  // <= 4 (R <= 4096)
+  uint32_t t[4] = {0, 0, 0, 0};
+  uint64_t v = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    const uint32_t b = tid * E + k;
+    t[k] = k < E && b < R ? tot[b] : 0u;
+    v += t[k];
+  }
+  uint64_t all;
+  uint64_t ex = block_excl_scan(v, sh, &all);
+  for (uint32_t k = 0; k < E; ++k) {
+    const uint32_t b = tid * E + k;
+    if (b >= R) break;
+    index[b] = (int64_t)(16 * ex);
+    ex += t[k];
+  }
+  if (tid == 0) index[R] = (int64_t)(16 * n);
+}
+
+// The buckets k_sort_local leaves (above kSortLocalCap; every bucket when no lower digit varies,
+// whose final order is then this one) copied from their runs into b at their index range.
+__global__ __launch_bounds__(256) void k_top_materialize(const u32x4* __restrict__ runs,
+                                                         const uint16_t* __restrict__ offs,
+                                                         uint32_t nch, uint32_t R,
+                                                         const int64_t* __restrict__ index,
+                                                         const SortPlanDev* __restrict__ plan,
+                                                         u32x4* __restrict__ outb) {
+  if (!plan->msd_ok) return;
+  const bool all = plan->dg.n == 0;
+  __shared__ uint32_t st[256], pre[256], wsum[4];
+  const uint32_t tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
+  for (uint32_t b = blockIdx.x; b < R; b += gridDim.x) {
+    const uint64_t s0 = (uint64_t)index[b] / 16, s1 = (uint64_t)index[b + 1] / 16;
+    if (s1 == s0 || (!all && s1 - s0 <= kSortLocalCap)) continue;
+    uint64_t done = 0;
+    for (uint32_t t0 = 0; t0 < nch; t0 += 256) {
+      const uint32_t c = t0 + tid;
+      uint32_t len = 0, start = 0;
+      if (c < nch) {
+        const uint16_t* row = offs + (uint64_t)c * (R + 1);
+        len = (uint32_t)row[b + 1] - row[b];
+        start = c * kTopChunk + row[b];
+      }
+      const uint32_t incl = wave_incl_scan(len, (int)lane);
+      if (lane == kWave - 1) wsum[wave] = incl;
+      __syncthreads();
+      uint32_t before = 0, total = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < 4; ++q) {
+        before += q < wave ? wsum[q] : 0u;
+        total += wsum[q];
+      }
+      pre[tid] = before + incl - len;
+      st[tid] = start;
+      __syncthreads();
+      const uint32_t m = min(256u, nch - t0);
+      for (uint32_t e = tid; e < total; e += 256) {
+        uint32_t lo = 0, hi = m;  // the last run starting at or before e
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (pre[mid] <= e) lo = mid; else hi = mid;
+        }
+        outb[s0 + done + e] = runs[st[lo] + (e - pre[lo])];
+      }
+      done += total;
+      __syncthreads();
+    }
+  }
+}
+
+hipError_t launch_top_chunks(const void* pairs, uint64_t n, int tb, const SortPlanDev* plan,
+                             void* chunked, uint16_t* offs, uint32_t* tot, int64_t* index,
+                             hipStream_t s) {
+  const uint32_t ncu = (uint32_t)std::max(1, stream_cus(s));
+  const uint32_t nch = (uint32_t)((n + kTopChunk - 1) / kTopChunk), R = 1u << tb;
+  hipLaunchKernelGGL(k_top_chunks<512>, dim3(std::min(nch, 2 * ncu)), dim3(512), 0, s,
+                     static_cast<const u32x4*>(pairs), n, tb, plan, static_cast<u32x4*>(chunked),
+                     offs, tot);
+  hipLaunchKernelGGL(k_top_colsum, dim3((R + 255) / 256, kTopSegs), dim3(256), 0, s, offs, nch, R,
+                     plan, tot);
+  hipLaunchKernelGGL(k_top_scan, dim3(1), dim3(1024), 0, s, tot, R, n, plan, index);
+  return hipGetLastError();
+}
 
 // Gather of records [0, n) of one bucket (fused sort): output record e = input record sidx[e].
 // L = 2^lsh lanes per record, each moving at most one 16-byte unit (lane l < rs / 16) or the
@@ -448,7 +693,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : CAP == 1024 ? 6 : 4) void k_
                                                         const int64_t* __restrict__ index,
                                                         uint32_t R, uint32_t lo_cap,
                                                         const SortPlanDev* __restrict__ plan,
-                                                        SortGather gth) {
+                                                        SortGather gth, SortRuns runs) {
   if (!plan->msd_ok || plan->dg.n == 0) return;  // the LSD fallback, or the top digit was all
   const SortDigits dg = plan->dg;
   const int kbits = plan->kbits;
@@ -469,10 +714,63 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : CAP == 1024 ? 6 : 4) void k_
     const uint32_t n = (uint32_t)(s1 - s0);
     if (n <= lo_cap || n > CAP) continue;  // another size class (n = 0: nothing to do)
     u32x4 v[PT];
+    if (runs.pairs) {
+      __syncthreads();  // the previous bucket's gather has read its record indices out of buf
+      // chunked top pass: the bucket is one run per chunk.  Its run table goes to buf (free until
+      // the first digit pass): the run's first pair and its offset in the bucket, per chunk;
+      // thread t owns chunks [t K, (t + 1) K)
+      uint32_t* rstart = reinterpret_cast<uint32_t*>(buf);
+      uint32_t* rpre = rstart + runs.nch;
+      const uint32_t K = (runs.nch + NT - 1) / NT;
+      uint32_t sum = 0;
+      for (uint32_t k = 0; k < K; ++k) {
+        const uint32_t c = tid * K + k;
+        if (c >= runs.nch) break;
+        const uint16_t* row = runs.offs + (uint64_t)c * (R + 1) + b;
+        const uint32_t o = row[0];
+        rstart[c] = c * kTopChunk + o;
+        rpre[c] = sum;
+        sum += (uint32_t)row[1] - o;
+      }
+      const uint32_t incl = wave_incl_scan(sum, lane);
+      if (lane == kWave - 1) wsum[wave] = incl;
+      __syncthreads();
+      uint32_t ex = incl - sum;
 #pragma unroll
-    for (uint32_t j = 0; j < PT; ++j) {  // unconditional (clamped) loads: no per-load wait
-      const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
-      v[j] = in[s0 + min(e, n - 1)];
+      for (uint32_t q = 0; q < NW; ++q) ex += q < (uint32_t)wave ? wsum[q] : 0u;
+      for (uint32_t k = 0; k < K; ++k) {
+        const uint32_t c = tid * K + k;
+        if (c >= runs.nch) break;
+        rpre[c] += ex;
+      }
+      __syncthreads();
+      // the last run starting at or before e: a branch-free search of fixed depth (kTopMaxChunks
+      // = 2^11 runs), so the PT searches interleave
+      static_assert(kTopMaxChunks == 2048, "search depth");
+      uint32_t e[PT], lo[PT];
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) {
+        e[j] = min(wave * (PT * kWave) + j * kWave + lane, n - 1);
+        lo[j] = 0;
+      }
+#pragma unroll
+      for (uint32_t step = kTopMaxChunks / 2; step > 0; step >>= 1) {
+#pragma unroll
+        for (uint32_t j = 0; j < PT; ++j) {
+          const uint32_t t = lo[j] + step;
+          if (t < runs.nch && rpre[t] <= e[j]) lo[j] = t;
+        }
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j)  // unconditional (clamped) loads
+        v[j] = static_cast<const u32x4*>(runs.pairs)[rstart[lo[j]] + (e[j] - rpre[lo[j]])];
+      __syncthreads();  // every run-table read is done before a digit pass rewrites buf
+    } else {
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) {  // unconditional (clamped) loads: no per-load wait
+        const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+        v[j] = in[s0 + min(e, n - 1)];
+      }
     }
     // one stable 8-bit digit pass in LDS (digit d of dg): ranks, block scan, permutation into
     // buf, the pairs back into registers in the new order
@@ -771,11 +1069,10 @@ __device__ bool span_varies_dev(const uint32_t* span, int lo, int hi) {
   return false;
 }
 
-// The plan's first half from the key span: the highest varying key bit, the top digit (its tb
-// bits end there) and the LDS sort's 8-bit digits below it that vary.  One thread.
-__global__ void k_sort_plan(const uint32_t* __restrict__ span, int bits, int tb,
-                            SortPlanDev* __restrict__ plan) {
-  if (threadIdx.x != 0) return;
+// The plan from the key span (AND of key words 0..2, then their OR): the highest varying key
+// bit, the top digit (its tb bits end there) and the LDS sort's 8-bit digits below it that vary.
+// One thread (k_span_reduce's thread 0).
+__device__ void make_sort_plan(const uint32_t* span, int bits, int tb, SortPlanDev* plan) {
   int hb = -1;
   for (int b = 127; b >= 128 - bits && hb < 0; --b)
     if (span_varies_dev(span, b, b + 1)) hb = b;
@@ -809,44 +1106,43 @@ __global__ void k_sort_plan(const uint32_t* __restrict__ span, int bits, int tb,
   plan->maxb = 0;
 }
 
-hipError_t launch_sort_plan(const void* span, int bits, int tb, SortPlanDev* plan, hipStream_t s) {
-  hipLaunchKernelGGL(k_sort_plan, dim3(1), dim3(64), 0, s, static_cast<const uint32_t*>(span),
-                     bits, tb, plan);
-  return hipGetLastError();
-}
-
 template <bool GATHER>
 static void launch_sort_local_classes(const u32x4* in, u32x4* out, const int64_t* d_index,
                                       uint32_t R, const SortPlanDev* plan, const SortGather& gth,
-                                      uint32_t ncu, hipStream_t s) {
+                                      const SortRuns& runs, uint32_t ncu, hipStream_t s) {
   // size classes (0, 1024], (1024, 2048], (2048, kSortLocalCap]: each bucket on the smallest
   // shape that holds it (the classes a key set leaves empty cost one index sweep each)
   constexpr size_t l1 = SortLocal<4, 1024>::lds_bytes();
   hipLaunchKernelGGL((k_sort_local<4, 1024, GATHER>), dim3(std::min<uint32_t>(R, 6 * ncu)),
-                     dim3(4 * kWave), l1, s, in, out, d_index, R, 0u, plan, gth);
+                     dim3(4 * kWave), l1, s, in, out, d_index, R, 0u, plan, gth, runs);
   constexpr size_t l2 = SortLocal<4, 2048>::lds_bytes();
   static_assert(4 * l2 <= 160 * 1024, "four workgroups per CU");
   hipLaunchKernelGGL((k_sort_local<4, 2048, GATHER>), dim3(std::min<uint32_t>(R, 4 * ncu)),
-                     dim3(4 * kWave), l2, s, in, out, d_index, R, 1024u, plan, gth);
+                     dim3(4 * kWave), l2, s, in, out, d_index, R, 1024u, plan, gth, runs);
   constexpr size_t l3 = SortLocal<8, kSortLocalCap>::lds_bytes();
   static_assert(2 * l3 <= 160 * 1024, "two workgroups per CU");
   allow_lds(reinterpret_cast<const void*>(&k_sort_local<8, kSortLocalCap, GATHER>), l3);
   hipLaunchKernelGGL((k_sort_local<8, kSortLocalCap, GATHER>), dim3(std::min<uint32_t>(R, 2 * ncu)),
-                     dim3(8 * kWave), l3, s, in, out, d_index, R, 2048u, plan, gth);
+                     dim3(8 * kWave), l3, s, in, out, d_index, R, 2048u, plan, gth, runs);
 }
 
 hipError_t launch_sort_local_planned(const void* in_pairs, void* out_pairs, const int64_t* d_index,
                                      uint32_t R, const SortPlanDev* plan, hipStream_t s,
-                                     const void* recs_in, void* recs_out, uint32_t rs) {
+                                     const void* recs_in, void* recs_out, uint32_t rs,
+                                     const SortRuns& runs) {
   const uint32_t ncu = (uint32_t)std::max(1, stream_cus(s));
   const u32x4* in = static_cast<const u32x4*>(in_pairs);
   u32x4* out = static_cast<u32x4*>(out_pairs);
   SortGather gth{static_cast<const uint8_t*>(recs_in), static_cast<uint8_t*>(recs_out), rs, 0};
   while (gth.lsh < 6 && (16u << gth.lsh) < rs) ++gth.lsh;
   if (recs_out)
-    launch_sort_local_classes<true>(in, out, d_index, R, plan, gth, ncu, s);
+    launch_sort_local_classes<true>(in, out, d_index, R, plan, gth, runs, ncu, s);
   else
-    launch_sort_local_classes<false>(in, out, d_index, R, plan, gth, ncu, s);
+    launch_sort_local_classes<false>(in, out, d_index, R, plan, gth, runs, ncu, s);
+  if (runs.pairs)  // the buckets left to the global sort (or the whole order) into `in` = b
+    hipLaunchKernelGGL(k_top_materialize, dim3(std::min<uint32_t>(R, 4 * ncu)), dim3(256), 0, s,
+                       static_cast<const u32x4*>(runs.pairs), runs.offs, runs.nch, R, d_index, plan,
+                       const_cast<u32x4*>(in));
   hipLaunchKernelGGL((k_sort_bucket_global<16>), dim3(std::min<uint32_t>(R, ncu)), dim3(16 * kWave),
                      0, s, const_cast<u32x4*>(in), out, d_index, R, plan);
   return hipGetLastError();

@@ -60,7 +60,7 @@ def test_bootstrap_and_pool_entry_points_validate_arguments():
 
 @pytest.mark.parametrize("field,value", [
     ("hist_kernel", 5), ("scatter_kernel", 3), ("coresident", 2), ("scatter_chunk", 256),
-    ("scatter_depth", 3), ("hist_stage", 32), ("hist_wgs_per_cu", 9), ("small_kernel", 5), ("small_waves", 12), ("scatter_order", 3), ("small_wgs_per_cu", 3), ("sort_msd", 3), ("s6_chunk", 100), ("tiles_per_item", -1),
+    ("scatter_depth", 3), ("hist_stage", 32), ("hist_wgs_per_cu", 9), ("small_kernel", 5), ("small_waves", 12), ("scatter_order", 3), ("small_wgs_per_cu", 3), ("sort_msd", 4), ("s6_chunk", 100), ("tiles_per_item", -1),
     ("small_groups", 3), ("tile_records", 96), ("tile_records", 32), ("onepass", 2),
     ("varlen_kernel", 4), ("varlen_tile", 100), ("sort_max_digit_bits", 17), ("sort_gather", 2),
     ("sort_all_passes", -1), ("hist_kernel", 2), ("scatter_kernel", 2), ("small_kernel", 3),

@@ -220,12 +220,14 @@ def test_segmented_inline_small_records(gpu_node, nseg):
     assert out.cpu().numpy()[: n * rs].tobytes() == exp.tobytes()
 
 
-@pytest.mark.parametrize("msd", [1, 2])
+@pytest.mark.parametrize("msd", [1, 2, 3])
 @pytest.mark.parametrize("shape", ["terasort", "skewed_top", "skewed_top9", "long", "int_inline",
                                    "distinct50", "distinct50_k9", "skewed_const_mid"])
 def test_msd_finish_and_lsd_agree_with_oracle(gpu_node, tuned, msd, shape):
-    """sort_msd 1: one top-digit pass + every bucket sorted by the lower digits (k_sort_local in
-    LDS; k_sort_bucket_global for a bucket above the LDS capacity); 2: LSD digit passes only.
+    """sort_msd 1: the top digit (chunked: each 4096-pair chunk sorted in place, buckets read as
+    runs) + every bucket sorted by the lower digits (k_sort_local in LDS; k_sort_bucket_global for
+    a bucket above the LDS capacity, copied out of its runs first); 3: the same after a one-pass
+    top-digit partition; 2: LSD digit passes only.
     'skewed_top' / 'skewed_top9': 60 % of the keys share their top bytes, so one bucket passes the
     LDS capacity and is sorted through global memory (10- and 9-byte keys: both parities of its
     digit count).  'distinct50*': 50 distinct keys, so every non-empty bucket holds ~6 000 equal
@@ -260,6 +262,27 @@ def test_msd_finish_and_lsd_agree_with_oracle(gpu_node, tuned, msd, shape):
     gpu_node.check()
 
 
+@pytest.mark.parametrize("msd", [1, 3])
+@pytest.mark.parametrize("n", [1, 4095, 4096, 4097, 70_001, 1_000_000])
+@pytest.mark.parametrize("kind", ["terasort", "top_only", "equal"])
+def test_chunked_top_digit(gpu_node, tuned, msd, n, kind):
+    """The chunked top pass (sort_msd 1) against the one-pass partition (3) and the oracle: chunk
+    counts around the 4096-pair chunk (a partial last chunk, one exact chunk), top digits of 8..10
+    bits; 'top_only': keys that vary only inside the top digit (no lower digit: every bucket is
+    copied out of its runs in order); 'equal': one key (the plan's identity)."""
+    tuned(sort_msd=msd)
+    recs = O.gen_terasort(70, 0, n).reshape(-1, 100)
+    if kind == "top_only":
+        recs[:, 1:10] = 0
+        recs[:, 0] = np.random.default_rng(70).integers(0, 256, n)
+    elif kind == "equal":
+        recs[:, :10] = recs[0, :10]
+    recs = recs.ravel()
+    got = gpu_sort(gpu_node, recs, 100, N.SORT_BYTES, 0, 10)
+    assert got.tobytes() == O.sort_records(recs, 100, O.SORT_BYTES, 0, 10).tobytes()
+    gpu_node.check()
+
+
 @pytest.mark.parametrize("shape", ["tie_runs", "long_tie_runs"])
 def test_lds_sort_tie_fixup_and_redo(gpu_node, shape):
     """k_sort_local sorts a bucket by its two most significant varying digits, then finishes the
@@ -289,7 +312,7 @@ def test_lds_sort_tie_fixup_and_redo(gpu_node, shape):
 @pytest.mark.parametrize("shape", ["terasort", "skewed_top", "equal", "top_only", "long_small"])
 def test_sort_records_captured_in_a_graph(gpu_node, shape):
     """sux_sort_records on a stream being captured into a HIP graph: the plan is made on the
-    device (k_sort_plan), so there is no host wait and no host allocation
+    device (make_sort_plan, in the span reduction), so there is no host wait and no host allocation
     mid-capture, and every branch runs inside the graph — the LDS finish ('terasort'), the LSD
     fallback of a bucket above the LDS capacity ('skewed_top'), the identity of equal keys
     ('equal'), a key whose varying bits all sit in the top digit ('top_only': the result stays in

@@ -1,0 +1,39 @@
+"""The reduce-side sort alone, for a kernel-trace profile: 5 M TeraSort records (one reduce
+partition of the bench), `reps` timed calls after two warm-ups; prints the HIP-event mean.
+usage: python tools/sort_prof.py [reps=20] [tuning field=value,...] [library path (A/B builds)]"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from sparkucx_amd import native as N  # noqa: E402
+from sparkucx_amd.shuffle import Node  # noqa: E402
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    if len(sys.argv) > 3:
+        N.LIB_PATH = os.path.abspath(sys.argv[3])
+    node = Node(device=0)
+    if len(sys.argv) > 2 and sys.argv[2]:
+        node.set_tuning(**{k: int(v) for k, v in (kv.split("=") for kv in sys.argv[2].split(","))})
+    n, rs = 5_000_000, 100
+    d = node.generate(N.GEN_TERASORT, 25, 0, n, rs)
+    out = torch.empty(n * rs, dtype=torch.uint8, device="cuda")
+    ws = torch.empty(node.sort_workspace_size(n, rs), dtype=torch.uint8, device="cuda")
+    for _ in range(2):
+        node.sort_records(d, rs, N.SORT_BYTES, 0, 10, num_records=n, out=out, workspace=ws)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        node.sort_records(d, rs, N.SORT_BYTES, 0, 10, num_records=n, out=out, workspace=ws)
+    e1.record()
+    torch.cuda.synchronize()
+    node.check()
+    print(f"sort 5M TeraSort: {e0.elapsed_time(e1) / reps:.4f} ms per call ({N.LIB_PATH})", flush=True)
+
+
+if __name__ == "__main__":
+    main()
