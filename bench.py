@@ -764,7 +764,8 @@ def main():
                          "else 0)")
     ap.add_argument("--reduce-sort-records", type=int, default=-1,
                     help="N=1: also time the reduce-side sort (sux_sort_records) of one reduce "
-                         "partition's worth of records (-1: records/R; 0: skip)")
+                         "partition (-1: partition R/2's blocks of every map; > 0: that many "
+                         "records from the start of the map outputs; 0: skip)")
     ap.add_argument("--varlen-rows", type=int, default=-1,
                     help="N=1: also time the map side over variable-length UnsafeRow-framed rows "
                          "(sux_partition_varlen; -1: 32 Mi rows in 1 Mi-row maps; 0: skip)")
@@ -1356,11 +1357,23 @@ def main():
                                      "sux_unregister_shuffle, inside every timed step"}
         if resolved["bytes"] != n * rs * steps_run:
             raise RuntimeError("resolved blocks do not cover the input")
-    if not pipelined:
-        ns = args.reduce_sort_records if args.reduce_sort_records >= 0 else n // R
-        ns = min(ns, n)
-        if ns > 0 and args.workload == "terasort":
-            result["reduce_sort"] = reduce_sort(node, out[:ns * rs], ns, rs, dev)
+    if not pipelined and args.workload == "terasort" and args.reduce_sort_records != 0:
+        if args.reduce_sort_records > 0:  # the first records of the map outputs
+            ns = min(args.reduce_sort_records, n)
+            recs, what = out[:ns * rs], f"the first {ns} records of the map outputs"
+        else:
+            # one real reduce partition: partition R/2's block of every map, in map order (what
+            # a reducer fetches: random order inside one 1/R slice of the key range)
+            p = R // 2
+            idx = index.view(maps, R + 1)[:, p:p + 2].cpu().tolist()
+            recs = torch.cat([out[m * rpm * rs + a:m * rpm * rs + b]
+                              for m, (a, b) in enumerate(idx) if b > a])
+            ns = recs.numel() // rs
+            what = f"reduce partition {p}: its block of each of the {maps} map outputs"
+        if ns > 0:
+            result["reduce_sort"] = reduce_sort(node, recs, ns, rs, dev)
+            result["reduce_sort"]["input"] = what
+            del recs
             result["reduce_sort_long"] = reduce_sort_long(node, 32 << 20, dev)
     if not pipelined and args.maps_2e27 and args.workload == "terasort" and n >= (1 << 27) \
             and rpm != (1 << 27):

@@ -468,20 +468,24 @@ __global__ __launch_bounds__(NT, 2 * NT / 256) void k_top_chunks(const u32x4* __
       kin = kout;
       kout = t;
     }
-    // 2. the chunk's bucket starts (a run start fills the starts of the empty buckets before
-    //    it) and the chunk back to its own place in bucket order: sorted position s takes pair
+    // 2. the chunk back to its own place in bucket order: sorted position s takes pair
     //    kin[s] & 4095, coalesced 16-byte stores
-    uint16_t* row = offs + (uint64_t)c * (R + 1);
 #pragma unroll
     for (uint32_t k = 0; k < PT; ++k) {
       const uint32_t s = tid + k * NT;
-      if (s >= nc) continue;
-      const uint32_t key = kin[s], p = key >> IDX;
-      outp[c0 + s] = pairs[c0 + (key & (CH - 1))];
-      const uint32_t q0 = s == 0 ? 0u : (kin[s - 1] >> IDX) + 1;
-      for (uint32_t q = q0; q <= p; ++q) row[q] = (uint16_t)s;
-      if (s + 1 == nc)
-        for (uint32_t q = p + 1; q <= R; ++q) row[q] = (uint16_t)nc;
+      if (s < nc) outp[c0 + s] = pairs[c0 + (kin[s] & (CH - 1))];
+    }
+    // 3. the chunk's bucket starts, row[q] = the pairs of buckets below q: a branch-free lower
+    //    bound per bucket (adjacent threads, adjacent u16 stores; the same work whatever the
+    //    chunk's key order — a run-start thread filling the gap before it was serial when a chunk
+    //    held few buckets)
+    uint16_t* row = offs + (uint64_t)c * (R + 1);
+    for (uint32_t q = tid; q <= R; q += NT) {
+      uint32_t pos = 0;
+#pragma unroll
+      for (uint32_t step = CH; step > 0; step >>= 1)
+        if (pos + step <= nc && (kin[pos + step - 1] >> IDX) < q) pos += step;
+      row[q] = (uint16_t)pos;
     }
     __syncthreads();  // kin / kout are rewritten by the next chunk
   }
