@@ -570,11 +570,14 @@ int sux_buffer_release(sux_buffer* buf);
  * (sux_fetch_blocks) gives one deterministic answer where Spark's depends on fetch order (Q4).
  * Keys: SUX_SORT_BYTES = key_len (1..12) bytes compared unsigned lexicographically (TeraSort's
  * 10-byte keys); SUX_SORT_LONG / SUX_SORT_INT = signed little-endian int64 / int32 (Spark's
- * LongType / IntegerType orderings).  Workspace: sux_sort_workspace_size (about 32 B/record).
- * The call waits on `stream` once, after the key pass, to read back which key bits vary (24
- * bytes): digit passes over bits that never vary are skipped.  While `stream` is being captured
- * into a HIP graph the call does not wait and runs every digit pass (same bytes), so it can be
- * captured.  The output is complete when the stream's later work runs. */
+ * LongType / IntegerType orderings).  Workspace: sux_sort_workspace_size (about 32 B/record;
+ * about 50 B/record up to 2048 x 4096 records, where the top digit is chunked).
+ * The default path (tuning sort_msd 0 / 1 / 3) is planned on the device from the key span and
+ * never waits on the host, so it can be captured into a HIP graph.  The LSD path (sort_msd 2,
+ * sort_all_passes, or more than about 2^14 x 2048 records) waits on `stream` once, after the key pass,
+ * to read back which key bits vary (24 bytes) and skips the digit passes over bits that never
+ * vary; under graph capture it does not wait and runs every pass (same bytes).  The output is
+ * complete when the stream's later work runs. */
 #define SUX_SORT_BYTES 1
 #define SUX_SORT_LONG 2
 #define SUX_SORT_INT 3

@@ -1486,6 +1486,8 @@ __global__ __launch_bounds__(NW * 64) void k_scatter8(MapGroup g, int R, int pid
       const int32_t b0 = (int32_t)(16 * u) - (int32_t)head;
       const uint32_t r0 = b0 >= 0 ? (uint32_t)b0 / S : 0u, off0 = (uint32_t)b0 - r0 * S;
       if (u < units && b0 >= 0 && (uint32_t)b0 + 16 <= n * S && off0 + 16 <= S) {
+        // two ds_write2_b32 (4-byte-aligned units); four lane-rotated ds_write_b32 that cover
+        // all 64 banks measured slower (round 4)
         *reinterpret_cast<u32x4a4*>(img32 + ((recoff[r0] + off0) >> 2)) = v[k2];
       } else if (u < units) {
 #pragma unroll
