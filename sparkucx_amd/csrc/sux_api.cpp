@@ -528,6 +528,11 @@ struct sux_node {
   int pipe_split_cus = 0;
   hipEvent_t split_ev[4] = {nullptr, nullptr, nullptr, nullptr};
   void make_split(int cus);
+  // sux_sort_records: the side stream of the large-bucket launches and its fork / join events;
+  // sort_mu held while a sort enqueues on them
+  hipStream_t sort_side = nullptr;
+  hipEvent_t sort_ev[2] = {nullptr, nullptr};
+  std::mutex sort_mu;
   int cus = 0;  // the device's CU count (device_cus)
   int device_cus();
 
@@ -1309,6 +1314,9 @@ int sux_node_destroy(sux_node* node) {
     for (hipStream_t p : node->pipe_split)
       if (p) (void)hipStreamDestroy(p);
     for (hipEvent_t e : node->split_ev)
+      if (e) (void)hipEventDestroy(e);
+    if (node->sort_side) (void)hipStreamDestroy(node->sort_side);
+    for (hipEvent_t e : node->sort_ev)
       if (e) (void)hipEventDestroy(e);
     if (node->d_err) (void)hipFree(node->d_err);
     for (auto& kv : node->shuffles) release_shuffle(node, *kv.second);
@@ -3875,10 +3883,26 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
                 "sort top digit pass");
     }
     const sux::Tuning gt = resolve_tuning(node->tuning, false);
+    // the large-bucket launches on the node's side stream, unless `s` is being captured into a
+    // graph (the side stream is shared by the node's sorts)
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    hip_check(hipStreamIsCapturing(s, &cap), "hipStreamIsCapturing");
+    std::unique_lock<std::mutex> side_lk(node->sort_mu, std::defer_lock);
+    sux::SortSide side;
+    if (cap == hipStreamCaptureStatusNone) {
+      side_lk.lock();
+      if (!node->sort_side)
+        hip_check(hipStreamCreateWithFlags(&node->sort_side, hipStreamNonBlocking), "sort stream");
+      for (hipEvent_t& e : node->sort_ev)
+        if (!e) hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "sort event");
+      side.s = node->sort_side;
+      side.fork = node->sort_ev[0];
+      side.join = node->sort_ev[1];
+    }
     if (!inline_rec && gt.gather_kernel == 3 && sux::sort_gather_fusable(record_size)) {
       // the fused sort: sorted buckets gather their records themselves, the rest after them
       hip_check(sux::launch_sort_local_planned(b, a, index1, (uint32_t)pd1.R, plan, s, d_in,
-                                               d_out, record_size, runs),
+                                               d_out, record_size, runs, side),
                 "sort buckets");
       hip_check(sux::launch_gather_rest(d_in, a, b, index1, (uint32_t)pd1.R, n, plan, record_size,
                                         d_out, s),
@@ -3886,7 +3910,7 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
       return;
     }
     hip_check(sux::launch_sort_local_planned(b, a, index1, (uint32_t)pd1.R, plan, s, nullptr,
-                                             nullptr, 0, runs),
+                                             nullptr, 0, runs, side),
               "sort buckets");
     if (inline_rec)
       hip_check(sux::launch_unpair_records_sel(a, b, &plan->final_b, n, record_size, key_kind,

@@ -295,10 +295,17 @@ struct SortRuns {
   const uint16_t* offs = nullptr;
   uint32_t nch = 0;
 };
+// A side stream (with its fork / join events) for the large-bucket launches; s == nullptr: all on
+// the caller's stream (under graph capture).
+struct SortSide {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
 hipError_t launch_sort_local_planned(const void* in_pairs, void* out_pairs, const int64_t* d_index,
                                      uint32_t R, const SortPlanDev* plan, hipStream_t s,
                                      const void* recs_in = nullptr, void* recs_out = nullptr,
-                                     uint32_t rs = 0, const SortRuns& runs = SortRuns{});
+                                     uint32_t rs = 0, const SortRuns& runs = SortRuns{},
+                                     const SortSide& side = SortSide{});
 bool sort_gather_fusable(uint32_t rs);
 hipError_t launch_gather_rest(const void* recs_in, const void* pairs_a, const void* pairs_b,
                               const int64_t* d_index, uint32_t R, uint64_t n,

@@ -1114,8 +1114,9 @@ template <bool GATHER>
 static void launch_sort_local_classes(const u32x4* in, u32x4* out, const int64_t* d_index,
                                       uint32_t R, const SortPlanDev* plan, const SortGather& gth,
                                       const SortRuns& runs, uint32_t ncu, hipStream_t s) {
-  // size classes (0, 1024], (1024, 2048], (2048, kSortLocalCap]: each bucket on the smallest
-  // shape that holds it (the classes a key set leaves empty cost one index sweep each)
+  // size classes (0, 1024], (1024, 2048] (the third, (2048, kSortLocalCap], is launched by the
+  // caller on the side stream): each bucket on the smallest shape that holds it (the classes a
+  // key set leaves empty cost one index sweep each)
   constexpr size_t l1 = SortLocal<4, 1024>::lds_bytes();
   hipLaunchKernelGGL((k_sort_local<4, 1024, GATHER>), dim3(std::min<uint32_t>(R, 6 * ncu)),
                      dim3(4 * kWave), l1, s, in, out, d_index, R, 0u, plan, gth, runs);
@@ -1123,32 +1124,54 @@ static void launch_sort_local_classes(const u32x4* in, u32x4* out, const int64_t
   static_assert(4 * l2 <= 160 * 1024, "four workgroups per CU");
   hipLaunchKernelGGL((k_sort_local<4, 2048, GATHER>), dim3(std::min<uint32_t>(R, 4 * ncu)),
                      dim3(4 * kWave), l2, s, in, out, d_index, R, 1024u, plan, gth, runs);
-  constexpr size_t l3 = SortLocal<8, kSortLocalCap>::lds_bytes();
-  static_assert(2 * l3 <= 160 * 1024, "two workgroups per CU");
-  allow_lds(reinterpret_cast<const void*>(&k_sort_local<8, kSortLocalCap, GATHER>), l3);
-  hipLaunchKernelGGL((k_sort_local<8, kSortLocalCap, GATHER>), dim3(std::min<uint32_t>(R, 2 * ncu)),
-                     dim3(8 * kWave), l3, s, in, out, d_index, R, 2048u, plan, gth, runs);
 }
 
 hipError_t launch_sort_local_planned(const void* in_pairs, void* out_pairs, const int64_t* d_index,
                                      uint32_t R, const SortPlanDev* plan, hipStream_t s,
                                      const void* recs_in, void* recs_out, uint32_t rs,
-                                     const SortRuns& runs) {
+                                     const SortRuns& runs, const SortSide& side) {
   const uint32_t ncu = (uint32_t)std::max(1, stream_cus(s));
   const u32x4* in = static_cast<const u32x4*>(in_pairs);
   u32x4* out = static_cast<u32x4*>(out_pairs);
   SortGather gth{static_cast<const uint8_t*>(recs_in), static_cast<uint8_t*>(recs_out), rs, 0};
   while (gth.lsh < 6 && (16u << gth.lsh) < rs) ++gth.lsh;
+  // The buckets above the common 2048-pair shape (a few of them when the buckets average close
+  // to 2048 pairs: a range partition's keys fill only part of the top digit) and those for the
+  // global sort go on a side stream, launched first, so they overlap the main LDS launch instead
+  // of trailing it one bucket per workgroup.  Every launch writes only its own buckets' ranges.
+  hipStream_t sb = s;
+  if (side.s) {
+    hipError_t e = hipEventRecord(side.fork, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(side.s, side.fork, 0);
+    if (e != hipSuccess) return e;
+    sb = side.s;
+  }
+  constexpr size_t l3 = SortLocal<8, kSortLocalCap>::lds_bytes();
+  static_assert(2 * l3 <= 160 * 1024, "two workgroups per CU");
+  if (recs_out) {
+    allow_lds(reinterpret_cast<const void*>(&k_sort_local<8, kSortLocalCap, true>), l3);
+    hipLaunchKernelGGL((k_sort_local<8, kSortLocalCap, true>), dim3(std::min<uint32_t>(R, 2 * ncu)),
+                       dim3(8 * kWave), l3, sb, in, out, d_index, R, 2048u, plan, gth, runs);
+  } else {
+    allow_lds(reinterpret_cast<const void*>(&k_sort_local<8, kSortLocalCap, false>), l3);
+    hipLaunchKernelGGL((k_sort_local<8, kSortLocalCap, false>), dim3(std::min<uint32_t>(R, 2 * ncu)),
+                       dim3(8 * kWave), l3, sb, in, out, d_index, R, 2048u, plan, gth, runs);
+  }
+  if (runs.pairs)  // the buckets left to the global sort (or the whole order) into `in` = b
+    hipLaunchKernelGGL(k_top_materialize, dim3(std::min<uint32_t>(R, 4 * ncu)), dim3(256), 0, sb,
+                       static_cast<const u32x4*>(runs.pairs), runs.offs, runs.nch, R, d_index, plan,
+                       const_cast<u32x4*>(in));
+  hipLaunchKernelGGL((k_sort_bucket_global<16>), dim3(std::min<uint32_t>(R, ncu)), dim3(16 * kWave),
+                     0, sb, const_cast<u32x4*>(in), out, d_index, R, plan);
   if (recs_out)
     launch_sort_local_classes<true>(in, out, d_index, R, plan, gth, runs, ncu, s);
   else
     launch_sort_local_classes<false>(in, out, d_index, R, plan, gth, runs, ncu, s);
-  if (runs.pairs)  // the buckets left to the global sort (or the whole order) into `in` = b
-    hipLaunchKernelGGL(k_top_materialize, dim3(std::min<uint32_t>(R, 4 * ncu)), dim3(256), 0, s,
-                       static_cast<const u32x4*>(runs.pairs), runs.offs, runs.nch, R, d_index, plan,
-                       const_cast<u32x4*>(in));
-  hipLaunchKernelGGL((k_sort_bucket_global<16>), dim3(std::min<uint32_t>(R, ncu)), dim3(16 * kWave),
-                     0, s, const_cast<u32x4*>(in), out, d_index, R, plan);
+  if (side.s) {
+    hipError_t e = hipEventRecord(side.join, side.s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, side.join, 0);
+    if (e != hipSuccess) return e;
+  }
   return hipGetLastError();
 }
 

@@ -1,5 +1,8 @@
 """The reduce-side sort alone, for a kernel-trace profile: 5 M TeraSort records (one reduce
 partition of the bench), `reps` timed calls after two warm-ups; prints the HIP-event mean.
+With SORT_PROF_INPUT=partition the keys are those of one range partition of 200 (TeraSort's
+uniform bounds, partition 100: the first key byte 0x80 or, for 22 % of the keys, 0x81 with the
+second byte below 0x47), the shape of the bench's reduce_sort leg.
 usage: python tools/sort_prof.py [reps=20] [tuning field=value,...] [library path (A/B builds)]"""
 import os
 import sys
@@ -20,6 +23,14 @@ def main():
         node.set_tuning(**{k: int(v) for k, v in (kv.split("=") for kv in sys.argv[2].split(","))})
     n, rs = 5_000_000, 100
     d = node.generate(N.GEN_TERASORT, 25, 0, n, rs)
+    if os.environ.get("SORT_PROF_INPUT") == "partition":
+        v = d.view(n, rs)
+        g = torch.Generator(device="cuda")
+        g.manual_seed(5)
+        hi = torch.rand(n, device="cuda", generator=g) < 0.22
+        v[:, 0] = torch.where(hi, 0x81, 0x80).to(torch.uint8)
+        b1 = torch.randint(0, 0x47, (n,), device="cuda", generator=g, dtype=torch.int32)
+        v[:, 1] = torch.where(hi, b1.to(torch.uint8), v[:, 1])  # uniform, no modulo bias
     out = torch.empty(n * rs, dtype=torch.uint8, device="cuda")
     ws = torch.empty(node.sort_workspace_size(n, rs), dtype=torch.uint8, device="cuda")
     for _ in range(2):
@@ -32,7 +43,8 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     node.check()
-    print(f"sort 5M TeraSort: {e0.elapsed_time(e1) / reps:.4f} ms per call ({N.LIB_PATH})", flush=True)
+    print(f"sort 5M TeraSort ({os.environ.get('SORT_PROF_INPUT', 'random')} keys): "
+          f"{e0.elapsed_time(e1) / reps:.4f} ms per call ({N.LIB_PATH})", flush=True)
 
 
 if __name__ == "__main__":
