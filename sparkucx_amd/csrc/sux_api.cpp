@@ -3843,6 +3843,16 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
 #define SUX_SORT_BUCKET_MSD_MAX (sux::kSortLocalCap / 2)
 #endif
   while (tb < 14 && (n >> tb) > SUX_SORT_BUCKET_TARGET) ++tb;
+  // the chunked top digit (sort_msd 0 / 1; up to kTopMaxChunks chunks) aims at ~768-pair buckets
+  // (<= 13 bits): most buckets then take the six-per-CU 1024-pair LDS shape, and a range
+  // partition's keys, which fill only part of the top digit, still stay below 2048
+  const uint64_t top_bytes = top_chunked_bytes(n);
+  const bool chunked = node->tuning.sort_msd != 3 && node->tuning.sort_msd != 2 && !all_passes &&
+                       top_bytes && ws_bytes >= plan_off + sux::kSortPlanBytes + top_bytes;
+  if (chunked) {
+    tb = kSortMinDigitBits;
+    while (tb < sux::kTopMaxBits && (n >> tb) > sux::kTopBucketTarget) ++tb;
+  }
   if (node->tuning.sort_msd != 2 && !all_passes && (n >> tb) <= SUX_SORT_BUCKET_MSD_MAX) {
     SortPlan P1;
     sort_plan(n, record_size, P1, tb);
@@ -3856,11 +3866,7 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
     pd1.R = 1 << tb;
     pd1.dseed = &plan->top_lo;
     // the top digit: chunked (each chunk sorted in place, buckets read as runs; sort_msd 0 / 1)
-    // or one stable partition pass (sort_msd 3, more pairs than kTopMaxChunks chunks, or a top
-    // digit of more than 12 bits)
-    const uint64_t top_bytes = top_chunked_bytes(n);
-    const bool chunked = node->tuning.sort_msd != 3 && tb <= sux::kTopMaxBits && top_bytes &&
-                         ws_bytes >= plan_off + sux::kSortPlanBytes + top_bytes;
+    // or one stable partition pass (sort_msd 3, or more pairs than kTopMaxChunks chunks)
     sux::SortRuns runs;
     if (chunked) {
       auto up = [](uint64_t v) { return (v + 255) / 256 * 256; };

@@ -395,7 +395,7 @@ __device__ __forceinline__ uint32_t pair_bits(const u32x4& w, uint32_t sh, uint3
 //                  every bucket when no lower digit varies, are copied contiguously into b.
 // Stable: chunks keep input order between them and the LDS passes keep it inside a chunk.
 // ------------------------------------------------------------------------------------------
-template <uint32_t NT>
+template <uint32_t NT, uint32_t DB>  // DB: bits per LSD pass (6: top digits of <= 12 bits, 7: 13)
 __global__ __launch_bounds__(NT, 2 * NT / 256) void k_top_chunks(const u32x4* __restrict__ pairs,
                                                                 uint64_t n, int tb,
                                                                 const SortPlanDev* __restrict__ plan,
@@ -405,16 +405,17 @@ __global__ __launch_bounds__(NT, 2 * NT / 256) void k_top_chunks(const u32x4* __
   if (!plan->msd_ok) return;  // every key equal: nothing reads the chunked copy
   if (blockIdx.x == 0)         // k_top_colsum's bucket totals (atomic adds), after this launch
     for (uint32_t b = threadIdx.x; b < (1u << tb); b += NT) tot[b] = 0;
-  constexpr uint32_t NW = NT / kWave, PT = kTopChunk / NT, CH = kTopChunk, IDX = 12, ND = 64;
-  static_assert(CH == 1u << IDX && ND * NW == NT, "chunk index bits, one scan entry per thread");
+  constexpr uint32_t NW = NT / kWave, PT = kTopChunk / NT, CH = kTopChunk, IDX = 12, ND = 1u << DB;
+  constexpr uint32_t SE = ND * NW / NT;  // scan entries per thread
+  static_assert(CH == 1u << IDX && SE >= 1 && ND * NW == SE * NT, "chunk index bits, scan shape");
   __shared__ uint32_t keys0[CH], keys1[CH];
   __shared__ uint32_t wc0[2 * NW * ND];  // [pass parity][wave][digit]
   __shared__ uint32_t wsum[NW];
   const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
   const uint64_t lt_mask = (1ull << lane) - 1ull;
   const uint32_t R = 1u << tb, top_lo = (uint32_t)plan->top_lo;
-  const int passes = tb <= 6 ? 1 : 2;
-  const uint32_t D = passes == 1 ? (uint32_t)tb : (uint32_t)(tb + 1) / 2;  // <= 6 bits a pass
+  const int passes = tb <= (int)DB ? 1 : 2;
+  const uint32_t D = passes == 1 ? (uint32_t)tb : (uint32_t)(tb + 1) / 2;  // <= DB bits a pass
   const uint32_t nch = (uint32_t)((n + CH - 1) / CH);
   for (uint32_t i = tid; i < 2 * NW * ND; i += NT) wc0[i] = 0;
   // Two workgroups per CU within 64 VGPRs: the pairs are not held across the ranking — only
@@ -444,19 +445,29 @@ __global__ __launch_bounds__(NT, 2 * NT / 256) void k_top_chunks(const u32x4* __
         const bool valid = e < nc;
         key[j] = valid ? kin[e] : 0u;
         dig[j] = valid ? (key[j] >> sh) & ((1u << D) - 1) : 0u;
-        rank[j] = wave_rank<6>(dig[j], valid, wc + wave * ND, lt_mask);
+        rank[j] = wave_rank<DB>(dig[j], valid, wc + wave * ND, lt_mask);
       }
       __syncthreads();
-      {  // exclusive scan in (digit, wave) order: thread t owns (digit t / NW, wave t % NW)
-        const uint32_t dg = (uint32_t)tid / NW, w = (uint32_t)tid % NW;
-        const uint32_t a = wc[w * ND + dg];
-        const uint32_t incl = wave_incl_scan(a, lane);
+      {  // exclusive scan in (digit, wave) order: thread t owns entries [t SE, (t + 1) SE)
+        uint32_t a[SE], sum = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < SE; ++k) {
+          const uint32_t idx = (uint32_t)tid * SE + k;
+          a[k] = wc[(idx % NW) * ND + idx / NW];
+          sum += a[k];
+        }
+        const uint32_t incl = wave_incl_scan(sum, lane);
         if (lane == kWave - 1) wsum[wave] = incl;
         __syncthreads();
-        uint32_t before = 0;
+        uint32_t run = incl - sum;
 #pragma unroll
-        for (uint32_t q = 0; q < NW; ++q) before += q < (uint32_t)wave ? wsum[q] : 0u;
-        wc[w * ND + dg] = before + incl - a;
+        for (uint32_t q = 0; q < NW; ++q) run += q < (uint32_t)wave ? wsum[q] : 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < SE; ++k) {
+          const uint32_t idx = (uint32_t)tid * SE + k;
+          wc[(idx % NW) * ND + idx / NW] = run;
+          run += a[k];
+        }
       }
       __syncthreads();
 #pragma unroll
@@ -529,11 +540,11 @@ __global__ __launch_bounds__(1024) void k_top_scan(const uint32_t* __restrict__ 
     for (uint32_t b = tid; b <= R; b += 1024) index[b] = b == 0 ? 0 : (int64_t)(16 * n);
     return;
   }
-  const uint32_t E = (R + 1023) / 1024;  // <= 4 (R <= 4096)
-  uint32_t t[4] = {0, 0, 0, 0};
+  const uint32_t E = (R + 1023) / 1024;  // <= 8 (R <= 8192)
+  uint32_t t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t v = 0;
 #pragma unroll
-  for (uint32_t k = 0; k < 4; ++k) {
+  for (uint32_t k = 0; k < 8; ++k) {
     const uint32_t b = tid * E + k;
     t[k] = k < E && b < R ? tot[b] : 0u;
     v += t[k];
@@ -605,9 +616,14 @@ hipError_t launch_top_chunks(const void* pairs, uint64_t n, int tb, const SortPl
                              hipStream_t s) {
   const uint32_t ncu = (uint32_t)std::max(1, stream_cus(s));
   const uint32_t nch = (uint32_t)((n + kTopChunk - 1) / kTopChunk), R = 1u << tb;
-  hipLaunchKernelGGL(k_top_chunks<512>, dim3(std::min(nch, 2 * ncu)), dim3(512), 0, s,
-                     static_cast<const u32x4*>(pairs), n, tb, plan, static_cast<u32x4*>(chunked),
-                     offs, tot);
+  if (tb <= 12)
+    hipLaunchKernelGGL((k_top_chunks<512, 6>), dim3(std::min(nch, 2 * ncu)), dim3(512), 0, s,
+                       static_cast<const u32x4*>(pairs), n, tb, plan, static_cast<u32x4*>(chunked),
+                       offs, tot);
+  else
+    hipLaunchKernelGGL((k_top_chunks<512, 7>), dim3(std::min(nch, 2 * ncu)), dim3(512), 0, s,
+                       static_cast<const u32x4*>(pairs), n, tb, plan, static_cast<u32x4*>(chunked),
+                       offs, tot);
   hipLaunchKernelGGL(k_top_colsum, dim3((R + 255) / 256, kTopSegs), dim3(256), 0, s, offs, nch, R,
                      plan, tot);
   hipLaunchKernelGGL(k_top_scan, dim3(1), dim3(1024), 0, s, tot, R, n, plan, index);

@@ -283,6 +283,24 @@ def test_chunked_top_digit(gpu_node, tuned, msd, n, kind):
     gpu_node.check()
 
 
+@pytest.mark.parametrize("kind", ["random", "range_partition"])
+def test_chunked_top_digit_13_bits(gpu_node, kind):
+    """4 M records: the chunked top digit's 13-bit shape (two 7-bit LDS passes per chunk, 8192
+    buckets); 'range_partition': the keys of one of 200 TeraSort range partitions (first byte 0x80,
+    or 0x81 with the second below 0x47), whose buckets fill only part of the top digit."""
+    n = 4_000_000
+    recs = O.gen_terasort(71, 0, n).reshape(-1, 100)
+    if kind == "range_partition":
+        rng = np.random.default_rng(71)
+        hi = rng.random(n) < 0.22
+        recs[:, 0] = np.where(hi, 0x81, 0x80)
+        recs[:, 1] = np.where(hi, rng.integers(0, 0x47, n), recs[:, 1])
+    recs = recs.ravel()
+    got = gpu_sort(gpu_node, recs, 100, N.SORT_BYTES, 0, 10)
+    assert got.tobytes() == O.sort_records(recs, 100, O.SORT_BYTES, 0, 10).tobytes()
+    gpu_node.check()
+
+
 @pytest.mark.parametrize("shape", ["tie_runs", "long_tie_runs"])
 def test_lds_sort_tie_fixup_and_redo(gpu_node, shape):
     """k_sort_local sorts a bucket by its two most significant varying digits, then finishes the
