@@ -284,8 +284,7 @@ static_assert(sizeof(SortPlanDev) <= kSortPlanBytes, "plan slot");
 constexpr uint32_t kTopChunk = 4096;
 constexpr uint32_t kTopSegs = 32;        // chunk segments of the bucket-size column sums
 constexpr uint32_t kTopMaxChunks = 2048; // run table of the 1024-pair LDS shape (2 u32 per chunk)
-constexpr int kTopMaxBits = 13;
-constexpr uint32_t kTopBucketTarget = 768;  // pairs per top-digit bucket on average (<= 13 bits)
+constexpr int kTopMaxBits = 12;
 hipError_t launch_top_chunks(const void* pairs, uint64_t n, int tb, const SortPlanDev* plan,
                              void* chunked, uint16_t* offs, uint32_t* tot, int64_t* index,
                              hipStream_t s);

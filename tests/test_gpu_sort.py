@@ -284,10 +284,11 @@ def test_chunked_top_digit(gpu_node, tuned, msd, n, kind):
 
 
 @pytest.mark.parametrize("kind", ["random", "range_partition"])
-def test_chunked_top_digit_13_bits(gpu_node, kind):
-    """4 M records: the chunked top digit's 13-bit shape (two 7-bit LDS passes per chunk, 8192
-    buckets); 'range_partition': the keys of one of 200 TeraSort range partitions (first byte 0x80,
-    or 0x81 with the second below 0x47), whose buckets fill only part of the top digit."""
+def test_chunked_top_digit_4m(gpu_node, kind):
+    """4 M records: the chunked top digit at 12 bits (4096 buckets of ~1 000 pairs);
+    'range_partition': the keys of one of 200 TeraSort range partitions (first byte 0x80, or 0x81
+    with the second below 0x47), whose buckets fill only part of the top digit, so some pass 2048
+    pairs and take the side stream's 4096-pair shape."""
     n = 4_000_000
     recs = O.gen_terasort(71, 0, n).reshape(-1, 100)
     if kind == "range_partition":
