@@ -5,8 +5,9 @@
 
 A step = one full shuffle of the rank's resident input: every map batch is partitioned by the
 gfx950 kernels (P1-P3) and, for N > 1, its partition-aligned share is exchanged with every other
-GPU (ncclAllToAllv, overlapped with the next launch group on a second stream).  At N = 1 the
-reduce side resolves its blocks zero-copy from the index tables (no bytes move).
+GPU (RCCL grouped send/recv, overlapped with the next launch group on a second stream).  At N = 1
+the reduce side resolves its blocks zero-copy from the index tables (no bytes move), and the line
+also carries BASELINE configs C4 (Zipf keys) and C5 (16-byte records, R = 10 000) as `c4` / `c5`.
 Inputs are generated on the device before timing (counter-based) and stay in HBM.
 
 value = input bytes of all ranks / max-over-ranks wall time of K steps, in GB/s (1e9 B/s).
@@ -661,6 +662,300 @@ def self_check(node, part, data, out, index, n: int, rs: int, rpm: int, R: int,
                       "non-decreasing per map with counts = index runs"}
 
 
+def make_n1_step(node, part, data, out, index, index_be, n: int, rs: int, R: int, rpm: int,
+                 gm: int, comp, resolve: int, map_pipeline: int, nstreams: int, ws_bytes: int,
+                 dev):
+    """The N = 1 step: every map batch of `data` partitioned (P1-P3) into `out` / `index`,
+    either as one sux_partition_maps_pipelined call (two launch groups in flight) or one
+    sux_partition_maps call per launch group dealt over `nstreams` streams; with `resolve`, the
+    reduce side's local block resolve of config C2 inside the step.  Returns (step, resolved
+    counters)."""
+    maps = -(-n // rpm)
+    group_recs = gm * rpm
+    groups = -(-maps // gm)
+    ns = max(1, nstreams)
+    streams = [comp] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
+    wss = [torch.empty(ws_bytes, dtype=torch.uint8, device=dev) for _ in range(ns)] \
+        if not map_pipeline else []
+
+    def step_groups():
+        for s in streams[1:]:
+            s.wait_stream(comp)
+        for g in range(groups):
+            r0 = g * group_recs
+            r1 = min(n, r0 + group_recs)
+            m0 = g * gm
+            mg = -(-(r1 - r0) // rpm)
+            node.partition_maps(part, data[r0 * rs:r1 * rs], rs, rpm, num_records=r1 - r0,
+                                out=out[r0 * rs:r1 * rs],
+                                index=index[m0 * (R + 1):(m0 + mg) * (R + 1)],
+                                index_be=index_be[m0 * (R + 1) * 8:(m0 + mg) * (R + 1) * 8],
+                                workspace=wss[g % ns], stream=streams[g % ns])
+        for s in streams[1:]:
+            comp.wait_stream(s)
+
+    def step_pipelined():
+        node.partition_maps_pipelined(part, data, rs, rpm, num_records=n,
+                                      group_records=group_recs, out=out, index=index,
+                                      index_be=index_be, stream=comp)
+
+    # the reduce side's local block resolve (config C2): every (map, reduce partition) block
+    # of the step's shuffle is resolved through the plugin's C-ABI — the map outputs are
+    # committed in place (sux_adopt_map_outputs: index tables read back on the stream,
+    # published on completion) and sux_resolve_blocks returns each block's device address
+    # and size (OnOffsetsFetchCallback.java:53-72's offsets -> sizes, zero-copy at N = 1)
+    # Reduce tasks: at most 200 (TeraSort's R = 200: one ShuffleBlockId per (map, task)); at
+    # larger R each task reads a contiguous range of partitions as one ShuffleBlockBatchId per
+    # map, as Spark's reducers do with batch fetch (UcxShuffleClient.java:67-73; C5's R = 10 000
+    # in 200 tasks of 50 partitions: per-partition resolves would be 10^7 host calls a step)
+    tasks = min(R, 200)
+    lo_t = (np.arange(tasks) * R) // tasks
+    hi_t = (np.arange(1, tasks + 1) * R) // tasks
+    # sux_block_id rows (map, start, end, 0), built once: a reducer keeps its block list
+    all_blocks = np.ascontiguousarray(np.stack(
+        [np.repeat(np.arange(maps), tasks), np.tile(lo_t, maps), np.tile(hi_t, maps),
+         np.zeros(maps * tasks, np.int64)], 1).astype(np.int32))
+    resolved = {"blocks": 0, "bytes": 0}
+    sid_next = [5000]
+
+    def step_resolved(inner):
+        def run():
+            sid = sid_next[0]
+            sid_next[0] += 1
+            node.register_shuffle(sid, maps, R, rs)
+            inner()
+            node.adopt_map_outputs(sid, 0, out, rpm, n, index, stream=comp)
+            _, sizes = node.resolve_blocks(sid, all_blocks)
+            node.unregister_shuffle(sid)
+            resolved["blocks"] += len(sizes)
+            resolved["bytes"] += int(sizes.sum())
+        return run
+
+    step = step_pipelined if map_pipeline else step_groups
+    if resolve:
+        step = step_resolved(step)
+    return step, resolved
+
+
+# Measured ceilings on the box (tools/copy_probe.hip sweep, profiles/r02_sweeps/copy_probe.txt:
+# streaming read 6.1-6.4 TB/s, copy 5.65-5.76 TB/s of read + write bytes; they move +-5 % from
+# box to box).  They set the floor of a two-pass map side (DESIGN.md §4): a design cannot run
+# faster than reading every record once at the read ceiling and then moving it at the copy one.
+READ_CEIL_GBS = 6300.0
+COPY_CEIL_GBS = 5760.0
+
+
+def map_side_floor(kernels: dict, rs: int) -> dict:
+    """The map side's design floor (VERDICT r04 #7): the fastest the launched kernel set can run
+    at the measured read and copy ceilings, as GB/s of algorithmic bytes (2 x S per record) and
+    as a fraction of the 8 TB/s spec.  Three designs:
+    - K1 histogram + K3 scatter (k_hist*, k_scatter*): S read, then 2 S copied per record;
+    - two-level MSD (k_msd16a + k_msd16b): two passes that each copy 2 S per record;
+    - one pass (no K1): 2 S copied per record."""
+    h = kernels.get("hist") or ""
+    if h.startswith("k_msd16"):
+        t, design = 2 * (2 * rs) / COPY_CEIL_GBS, "two copy passes (MSD pass A + pass B)"
+    elif not h:
+        t, design = 2 * rs / COPY_CEIL_GBS, "one copy pass"
+    else:
+        t, design = rs / READ_CEIL_GBS + 2 * rs / COPY_CEIL_GBS, "K1 read + K3 copy"
+    ach = 2 * rs / t
+    return {"floor_achieved": round(ach, 1), "floor_frac": round(ach / HBM_PEAK_GBS, 4),
+            "floor_design": design,
+            "ceilings": {"read": READ_CEIL_GBS, "copy": COPY_CEIL_GBS,
+                         "source": "tools/copy_probe.hip, profiles/r02_sweeps/copy_probe.txt"}}
+
+
+def rooflines(node, kt, elapsed: float, steps: int, n: int, rs: int, R: int, maps: int,
+              workload: str, pipelined: bool, overlapped: bool):
+    """(roofline of the dominant kernel K3, roofline of the whole map side) for one timed run.
+    K3: algorithmic bytes (2 x S per record) per launch / its mean launch duration (HIP events on
+    the launch stream, node.kernel_times); traffic = PMC bytes per record of the kernel the library
+    reports it launched (profiles/pmc_r0x.json).  Map side: (2 N S + 8 (R + 1) per map) per step /
+    the wall clock of the timed steps when launch groups overlap (N = 1), else / the sum of the map
+    kernels' durations (N > 1: one map stream); floor_frac = the design's two-pass floor."""
+    launches, sc_ms = kt["scatter"]
+    recs_per_launch = n * steps / max(1, launches)
+    alg = 2 * recs_per_launch * rs                       # read + write every record once
+    sc_avg = sc_ms / max(1, launches) / 1e3
+    achieved = alg / sc_avg / 1e9 if sc_avg else None
+    map_ms = kt["hist"][1] + kt["scan"][1] + kt["scatter"][1]
+    map_alg = (2 * n * rs + 8 * (R + 1) * maps) * steps
+    map_time_ms = elapsed * 1e3 if not pipelined else map_ms
+    map_side = map_alg / (map_time_ms / 1e3) / 1e9 if map_time_ms else None
+    names = {k: node.kernel_variant(i) for i, k in enumerate(N.KERNELS)}
+    tr = {k: load_traffic(workload, names[k]) for k in ("hist", "scatter") if names[k]}
+    sc_tr = tr.get("scatter")
+    traffic = round(sc_tr["bytes_per_record"] * recs_per_launch) if sc_tr else None
+    map_traffic = None
+    if sc_tr and (tr.get("hist") or names["hist"] == ""):  # one-pass kernels have no K1
+        per_rec = sc_tr["bytes_per_record"] + (tr["hist"]["bytes_per_record"] if tr.get("hist") else 0)
+        map_traffic = round(per_rec * n)  # per step; the scans' few KB per map are left out
+    roof = {"bound": "hbm", "achieved": None if achieved is None else round(achieved, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": None if achieved is None else round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic, "kernel": names["scatter"],
+            "traffic_source": sc_tr["source"] if sc_tr else None,
+            "alg_bytes_per_launch": int(alg),
+            "avg_launch_ms": round(sc_avg * 1e3, 4)}
+    floor = map_side_floor(names, rs)
+    roof_map = {"bound": "hbm",
+                "achieved": None if map_side is None else round(map_side, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": None if map_side is None else round(map_side / HBM_PEAK_GBS, 4),
+                "floor_frac": floor["floor_frac"],
+                "of_floor": None if map_side is None else round(map_side / floor["floor_achieved"], 4),
+                "floor": floor,
+                "traffic_per_step": map_traffic,
+                "alg_bytes_per_step": int(map_alg / steps),
+                "time": ("wall clock of the timed steps (launch groups overlap)"
+                         if overlapped else "wall clock of the timed steps"
+                         if not pipelined else "sum of the map kernels' durations"),
+                "kernels": names,
+                "kernels_ms": {k: round(v[1], 3) for k, v in kt.items()},
+                "launches": {k: v[0] for k, v in kt.items()}}
+    return roof, roof_map
+
+
+def xgmi_probe(node, world: int, rank: int, dev, nbytes: int = 256 << 20, reps: int = 5) -> dict:
+    """Measured peer-read peak (VERDICT r04 #5; SURVEY §5 calls 153 GB/s per xGMI link "an
+    assumption to re-measure on the box"): every rank exports one nbytes-per-peer buffer over HIP
+    IPC, maps every peer's, and then all ranks at once pull their share from every source with the
+    library's own one-sided pull kernel (sux_pull_group over a one-map, R = world group: rank h
+    owns partition h, nbytes from each source) — the whole node's xGMI fabric loaded the way the
+    exchange loads it.  Returns the remote bytes per rank per second (the off-GPU share: the own
+    source is a local copy and is left out of the bytes, as in roofline_exchange)."""
+    R = world
+    send = torch.empty(world * nbytes, dtype=torch.uint8, device=dev)
+    send.fill_(rank & 255)
+    recv = torch.empty(world * nbytes, dtype=torch.uint8, device=dev)
+    rb = torch.zeros(1, dtype=torch.int64, device=dev)
+    one = torch.arange(R + 1, dtype=torch.int64, device=dev) * nbytes
+    gathered = one.repeat(world)
+    hs = [None] * world
+    dist.all_gather_object(hs, node.ipc_handle(send))
+    ptrs = [send.data_ptr() if g == rank else node.ipc_open(hs[g]) for g in range(world)]
+    srcs = torch.tensor(ptrs, dtype=torch.int64, device=dev)
+    st = torch.cuda.Stream(dev)
+    try:
+        for _ in range(2):
+            node.pull_group(world, rank, srcs, gathered, 1, R, recv, rb, stream=st)
+        st.synchronize()
+        dist.barrier()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            node.pull_group(world, rank, srcs, gathered, 1, R, recv, rb, stream=st)
+        e1.record(st)
+        st.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        ok = int(rb.item()) == world * nbytes and all(
+            int(recv[g * nbytes]) == (g & 255) and int(recv[(g + 1) * nbytes - 1]) == (g & 255)
+            for g in range(world))
+        dist.barrier()  # every rank is done reading before any mapping goes away
+    finally:
+        for g, p in enumerate(ptrs):
+            if g != rank:
+                node.ipc_close(p)
+    remote = (world - 1) * nbytes
+    return {"GB/s": round(remote / (ms / 1e3) / 1e9, 1), "bytes_per_source": nbytes,
+            "ms": round(ms, 3), "reps": reps, "ok": ok,
+            "what": "every rank pulls nbytes from every peer's IPC-mapped buffer at once "
+                    "(sux_pull_group); GB/s = remote bytes per rank / time"}
+
+
+def first_mismatch(a: torch.Tensor, b: torch.Tensor, chunk: int = 1 << 28) -> tuple[int, int]:
+    """(index of the first differing byte, differing bytes counted up to and including the chunk
+    that holds it) of two equal-length byte tensors, in bounded chunks: a whole-buffer
+    `(a != b).nonzero()` over a >= 2^31-byte group asks torch for an index tensor of the whole
+    buffer's size (VERDICT r04 #8), so it would report a bogus OOM instead of the mismatch."""
+    n = min(a.numel(), b.numel())
+    seen = 0
+    for c0 in range(0, n, chunk):
+        d = (a[c0:c0 + chunk] != b[c0:c0 + chunk])
+        k = int(d.sum())
+        if k:
+            return c0 + int(d.nonzero()[0, 0]), seen + k
+    return -1, 0
+
+
+SEEDS = {"terasort": 0x5EED0002, "zipf": 0x5EED0004, "small": 0x5EED0005}
+
+
+def make_partitioner(node, kind: int, R: int, key_len: int):
+    if kind == N.PART_RANGE_BYTES:
+        return node.partitioner(kind, R, key_offset=0, key_len=key_len, bounds=uniform_bounds(R))
+    return node.partitioner(kind, R, key_offset=0, key_len=key_len, seed=42)
+
+
+def generate_input(node, gen: int, seed: int, first: int, n: int, rs: int, out) -> None:
+    """Counter-based records [first, first + n) of the workload, written on the device."""
+    chunk = 1 << 27
+    for c0 in range(0, n, chunk):
+        c1 = min(n, c0 + chunk)
+        node.generate(gen, seed, first + c0, c1 - c0, rs, zipf_s=1.1, zipf_n=1 << 24,
+                      out=out[c0 * rs:c1 * rs])
+
+
+def config_leg(wl: str, data_buf, dev, steps: int, warmup: int = 1) -> dict:
+    """BASELINE configs C4 (Zipf-skewed keys) and C5 (small records) on the driver-timed line
+    (VERDICT r04 #2): the same N = 1 step as `value` — every map batch partitioned with two launch
+    groups in flight, then the local block resolve — on the workload's own full-size input
+    (regenerated into the headline's input buffer), on a fresh node; `warmup` untimed steps, then
+    `steps` timed ones (wall clock, synchronised), its own roofline / roofline_map_side (PMC
+    traffic keyed by workload and kernel), and one more step into zeroed outputs self-checked."""
+    rs, R, gen, kind, key_len, n, _ = WORKLOADS[wl]
+    rpm = 1 << 20
+    gm = max(1, round(GROUP_BYTES / (rpm * rs)))
+    maps = -(-n // rpm)
+    node = Node(device=dev.index)
+    part = None
+    try:
+        part = make_partitioner(node, kind, R, key_len)
+        data = data_buf[:n * rs] if data_buf.numel() >= n * rs else \
+            torch.empty(n * rs, dtype=torch.uint8, device=dev)
+        generate_input(node, gen, SEEDS[wl], 0, n, rs, data)
+        out = torch.empty(n * rs, dtype=torch.uint8, device=dev)
+        index = torch.empty(maps * (R + 1), dtype=torch.int64, device=dev)
+        index_be = torch.empty(maps * (R + 1) * 8, dtype=torch.uint8, device=dev)
+        comp = torch.cuda.current_stream(dev)
+        step, resolved = make_n1_step(node, part, data, out, index, index_be, n, rs, R, rpm, gm,
+                                      comp, 1, 1, 1, 0, dev)
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        node.kernel_times()
+        node.set_kernel_timing(True)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        node.set_kernel_timing(False)
+        kt = node.kernel_times()
+        node.check()
+        roof, roof_map = rooflines(node, kt, el, steps, n, rs, R, maps, wl, False, True)
+        out.zero_()
+        index.zero_()
+        step()
+        torch.cuda.synchronize(dev)
+        sc = self_check(node, part, data, out, index, n, rs, rpm, R, gm * rpm, dev)
+        node.check()
+        if resolved["bytes"] != n * rs * (warmup + steps + 1):
+            raise RuntimeError(f"{wl}: resolved blocks do not cover the input")
+        return {"workload": f"{wl}: {n} x {rs}-byte records ({n * rs / 1e9:.0f} GB), R={R}, map "
+                            f"batches of {rpm} records, {gm} maps per launch group, two launch "
+                            "groups in flight, zero-copy local block resolve",
+                "value": round(n * rs * steps / el / 1e9, 2), "unit": "GB/s", "steps": steps,
+                "warmup": warmup, "ms_per_step": round(el / steps * 1e3, 3),
+                "roofline": roof, "roofline_map_side": roof_map, "self_check": sc,
+                "resolve_blocks_per_step": resolved["blocks"] // (warmup + steps + 1)}
+    finally:
+        if part is not None:
+            part.close()
+        node.close()
+
+
 def load_traffic(workload: str, kernel: str) -> dict | None:
     """HBM bytes per record of `kernel` under `workload`, from the committed PMC summary
     (profiles/pmc_r04.json, else pmc_r03.json; written by profiles/collect_pmc.py: one rocprofv3 pass per counter
@@ -746,9 +1041,25 @@ def main():
                     help="test mode at N=1: run the N>1 pipeline (peer-major partition, "
                          "overlapped ncclAllGather + ncclAllToAllv) on a one-rank RCCL "
                          "communicator, so the RCCL calls run on a 1-GPU box")
-    ap.add_argument("--exchange-one-call", action="store_true",
-                    help="rccl: each group's all-gather + plan + all-to-all in one "
-                         "sux_exchange_group call on the comm stream (A/B against post/issue)")
+    ap.add_argument("--exchange", default="one-call", choices=["one-call", "post-issue"],
+                    help="rccl: 'one-call' = each group's all-gather + plan + all-to-all in one "
+                         "sux_exchange_group call on one communicator (the default until a "
+                         "multi-rank run has verified the other); 'post-issue' = the all-gather "
+                         "of group k (sux_exchange_group_post) beside the all-to-all of k - 1 "
+                         "(sux_exchange_group_issue) on a split communicator")
+    ap.add_argument("--xgmi-probe-mib", type=int, default=256,
+                    help="N>1: before the run, time every rank pulling this many MiB from every "
+                         "peer at once over IPC (the measured exchange peak; 0: skip)")
+    ap.add_argument("--c4-steps", type=int, default=3,
+                    help="N=1: after the headline, also time BASELINE config C4 (Zipf-skewed "
+                         "keys, 100 GB, R=200) for this many steps, self-checked (0: skip)")
+    ap.add_argument("--c5-steps", type=int, default=3,
+                    help="N=1: after the headline, also time BASELINE config C5 (2^30 16-byte "
+                         "records, R=10000) for this many steps, self-checked (0: skip)")
+    ap.add_argument("--force-mismatch", action="store_true",
+                    help="test mode (pipelined self-check): flip a key byte in the middle of the "
+                         "first checked group's received bytes, so the check must fail and "
+                         "report the first differing byte")
     ap.add_argument("--map-pipeline", type=int, default=1,
                     help="N=1: 1 = one sux_partition_maps_pipelined call per step (launch "
                          "groups on the node's two map streams, co-resident K1/K3 shapes); "
@@ -863,19 +1174,12 @@ def main():
     if args.tuning:
         node.set_tuning(**{k.strip(): int(v) for k, v in
                            (kv.split("=") for kv in args.tuning.split(",") if kv.strip())})
-    if kind == N.PART_RANGE_BYTES:
-        part = node.partitioner(kind, R, key_offset=0, key_len=key_len, bounds=uniform_bounds(R))
-    else:
-        part = node.partitioner(kind, R, key_offset=0, key_len=key_len, seed=42)
+    part = make_partitioner(node, kind, R, key_len)
 
     # ---- resident input (generated on device, untimed) ---------------------------------------
-    seed = {"terasort": 0x5EED0002, "zipf": 0x5EED0004, "small": 0x5EED0005}[args.workload]
+    seed = SEEDS[args.workload]
     data = torch.empty(n * rs, dtype=torch.uint8, device=dev)
-    chunk = 1 << 27
-    for c0 in range(0, n, chunk):
-        c1 = min(n, c0 + chunk)
-        node.generate(gen, seed, rank * n + c0, c1 - c0, rs, zipf_s=1.1, zipf_n=1 << 24,
-                      out=data[c0 * rs:c1 * rs])
+    generate_input(node, gen, seed, rank * n, n, rs, data)
     index = torch.empty(maps * (R + 1), dtype=torch.int64, device=dev)
     ws_bytes = node.workspace_size(part, rs, rpm, min(n, group_recs))
     comp = torch.cuda.current_stream(dev)
@@ -890,66 +1194,9 @@ def main():
     if not pipelined:
         out = torch.empty(n * rs, dtype=torch.uint8, device=dev)
         index_be = torch.empty(maps * (R + 1) * 8, dtype=torch.uint8, device=dev)
-        ns = max(1, args.streams)
-        streams = [comp] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
-        wss = [torch.empty(ws_bytes, dtype=torch.uint8, device=dev) for _ in range(ns)]
-
-        def step_groups():
-            for s in streams[1:]:
-                s.wait_stream(comp)
-            for g in range(groups):
-                r0 = g * group_recs
-                r1 = min(n, r0 + group_recs)
-                m0 = g * gm
-                mg = -(-(r1 - r0) // rpm)
-                node.partition_maps(part, data[r0 * rs:r1 * rs], rs, rpm, num_records=r1 - r0,
-                                    out=out[r0 * rs:r1 * rs],
-                                    index=index[m0 * (R + 1):(m0 + mg) * (R + 1)],
-                                    index_be=index_be[m0 * (R + 1) * 8:(m0 + mg) * (R + 1) * 8],
-                                    workspace=wss[g % ns], stream=streams[g % ns])
-            for s in streams[1:]:
-                comp.wait_stream(s)
-
-        def step_pipelined():
-            node.partition_maps_pipelined(part, data, rs, rpm, num_records=n,
-                                          group_records=group_recs, out=out, index=index,
-                                          index_be=index_be, stream=comp)
-
-        # the reduce side's local block resolve (config C2): every (map, reduce partition) block
-        # of the step's shuffle is resolved through the plugin's C-ABI — the map outputs are
-        # committed in place (sux_adopt_map_outputs: index tables read back on the stream,
-        # published on completion) and sux_resolve_blocks returns each block's device address
-        # and size (OnOffsetsFetchCallback.java:53-72's offsets -> sizes, zero-copy at N = 1)
-        # Reduce tasks: at most 200 (TeraSort's R = 200: one ShuffleBlockId per (map, task)); at
-        # larger R each task reads a contiguous range of partitions as one ShuffleBlockBatchId per
-        # map, as Spark's reducers do with batch fetch (UcxShuffleClient.java:67-73; C5's R = 10 000
-        # in 200 tasks of 50 partitions: per-partition resolves would be 10^7 host calls a step)
-        tasks = min(R, 200)
-        lo_t = (np.arange(tasks) * R) // tasks
-        hi_t = (np.arange(1, tasks + 1) * R) // tasks
-        # sux_block_id rows (map, start, end, 0), built once: a reducer keeps its block list
-        all_blocks = np.ascontiguousarray(np.stack(
-            [np.repeat(np.arange(maps), tasks), np.tile(lo_t, maps), np.tile(hi_t, maps),
-             np.zeros(maps * tasks, np.int64)], 1).astype(np.int32))
-        resolved = {"blocks": 0, "bytes": 0}
-        sid_next = [5000]
-
-        def step_resolved(inner):
-            def run():
-                sid = sid_next[0]
-                sid_next[0] += 1
-                node.register_shuffle(sid, maps, R, rs)
-                inner()
-                node.adopt_map_outputs(sid, 0, out, rpm, n, index, stream=comp)
-                _, sizes = node.resolve_blocks(sid, all_blocks)
-                node.unregister_shuffle(sid)
-                resolved["blocks"] += len(sizes)
-                resolved["bytes"] += int(sizes.sum())
-            return run
-
-        step = step_pipelined if args.map_pipeline else step_groups
-        if args.resolve:
-            step = step_resolved(step)
+        step, resolved = make_n1_step(node, part, data, out, index, index_be, n, rs, R, rpm, gm,
+                                      comp, args.resolve, args.map_pipeline, args.streams,
+                                      ws_bytes, dev)
     else:
         comm = torch.cuda.Stream(dev)
         # send-buffer ring: rccl frees slot s when ITS all-to-all is done (2 slots); ipc frees
@@ -1022,7 +1269,7 @@ def main():
                     send_free[(j - 1) % NB].record(comm)
                     node.pull_group(world, rank, srcs[s], gi, mg, R, recv[j % 2],
                                     rbytes[j:j + 1], stream=comm)
-            elif args.exchange_one_call:
+            elif args.exchange == "one-call":
                 rb = node.exchange_group(send[s], ix, mg, R, gi, recv[j % 2], stream=comm)
                 rbytes[j] = int(rb.sum())
                 send_free[s].record(comm)
@@ -1097,6 +1344,10 @@ def main():
             if got != exp:
                 raise RuntimeError(f"self-check: rank {rank} group {j} received {got} bytes, "
                                    f"the gathered index says {exp}")
+            if exp and args.force_mismatch and check_stats["groups"] == 0:
+                # test mode: corrupt the first key byte of the middle received record
+                k = (exp // rs // 2) * rs
+                rbuf[k:k + 1].bitwise_xor_(0x80)
             if exp:
                 pid = node.partition_ids(part, rbuf[:exp], rs).to(torch.int64)
                 if not bool(((pid >= lo) & (pid < hi)).all()):
@@ -1116,14 +1367,11 @@ def main():
                         f"; send slab falls {int((spid[1:] < spid[:-1]).sum())} times, "
                         f"first at {(spid[1:] < spid[:-1]).nonzero().flatten()[:4].tolist()}")
                     if world == 1:
-                        diff = (rbuf[:exp] != sb[:exp]).nonzero().flatten()
-                        d0 = int(diff[0]) if diff.numel() else -1
-                        sdesc += (f"; {diff.numel()} bytes differ, first at {d0}, last at "
-                                  f"{int(diff[-1]) if diff.numel() else -1}; received bytes there "
-                                  f"{rbuf[d0:d0 + 8].tolist()} send {sb[d0:d0 + 8].tolist()}; "
-                                  f"zero bytes in the received tail: "
-                                  f"{int((rbuf[d0:exp] == 0).sum())} of {exp - d0}")
-                        del diff
+                        d0, nd = first_mismatch(rbuf[:exp], sb[:exp])
+                        sdesc += (f"; first differing byte at {d0} ({nd} differ up to the end of "
+                                  f"its 256 MiB chunk); received bytes there "
+                                  f"{rbuf[max(d0, 0):max(d0, 0) + 8].tolist()} send "
+                                  f"{sb[max(d0, 0):max(d0, 0) + 8].tolist()}")
                         if args.transport == "rccl":  # again, synchronously, on one stream
                             torch.cuda.synchronize(dev)
                             node.exchange_group(sb, index[j * gm * (R + 1):(j * gm + mg) * (R + 1)],
@@ -1160,7 +1408,7 @@ def main():
                                                index=index[m0 * (R + 1):(m0 + mg) * (R + 1)],
                                                peer_bytes=peer[s], workspace=ws[s], stream=comp)
                 part_done[s].record(comp)
-                if args.transport == "rccl" and not args.exchange_one_call:
+                if args.transport == "rccl" and args.exchange == "post-issue":
                     post(k)
                 if k >= 1:
                     exchange(k - 1)
@@ -1174,6 +1422,12 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
+    xprobe = None
+    if pipelined and world > 1 and args.xgmi_probe_mib > 0:
+        xprobe = xgmi_probe(node, world, rank, dev, args.xgmi_probe_mib << 20)
+        if rehearse:
+            xprobe["one_gpu"] = "every rank on cuda:0: an on-chip copy, not xGMI"
+        log(f"[rank {rank}] xgmi probe: {xprobe}")
     log(f"[rank {rank}] {args.workload}: {n} records x {rs} B = {n * rs / 1e9:.1f} GB/GPU, "
         f"R={R}, {maps} maps of {rpm}, {groups} launch groups of {gm} maps, world={world}")
     for _ in range(args.warmup):
@@ -1203,27 +1457,9 @@ def main():
     value = total_bytes / elapsed / 1e9
 
     # ---- roofline of the dominant kernel (scatter) + the whole map-side pass --------------
-    launches, sc_ms = kt["scatter"]
-    recs_per_launch = n * args.steps / max(1, launches)
-    alg = 2 * recs_per_launch * rs                       # read + write every record once
-    sc_avg = sc_ms / max(1, launches) / 1e3
-    achieved = alg / sc_avg / 1e9 if sc_avg else None
-    map_ms = kt["hist"][1] + kt["scan"][1] + kt["scatter"][1]
-    map_alg = (2 * n * rs + 8 * (R + 1) * maps) * args.steps
-    # N=1: the step IS the map side, and with two launch groups in flight the kernels overlap,
-    # so the map side's time is the wall clock of the timed steps (the kernel sum would count
-    # the overlapped K1 twice); N>1: the map kernels run one after another on one stream
     overlapped = not pipelined and (args.map_pipeline or args.streams > 1)
-    map_time_ms = elapsed * 1e3 if not pipelined else map_ms
-    map_side = map_alg / (map_time_ms / 1e3) / 1e9 if map_time_ms else None
-    names = {k: node.kernel_variant(i) for i, k in enumerate(N.KERNELS)}
-    tr = {k: load_traffic(args.workload, names[k]) for k in ("hist", "scatter") if names[k]}
-    sc_tr = tr.get("scatter")
-    traffic = round(sc_tr["bytes_per_record"] * recs_per_launch) if sc_tr else None
-    map_traffic = None
-    if sc_tr and (tr.get("hist") or names["hist"] == ""):  # one-pass kernels have no K1
-        per_rec = sc_tr["bytes_per_record"] + (tr["hist"]["bytes_per_record"] if tr.get("hist") else 0)
-        map_traffic = round(per_rec * n)  # per step; the scans' few KB per map are left out
+    roof, roof_map = rooflines(node, kt, elapsed, args.steps, n, rs, R, maps, args.workload,
+                               pipelined, overlapped)
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
@@ -1240,29 +1476,12 @@ def main():
                                + (", zero-copy local block resolve (one block per map and "
                                   "reduce task, <= 200 tasks)" if not pipelined and args.resolve else
                                   "" if not pipelined else
-                                  ", partition-aligned ncclAllToAllv exchange"
-                                  if args.transport == "rccl" else
+                                  ", partition-aligned all-to-all exchange (RCCL grouped "
+                                  "send/recv)" if args.transport == "rccl" else
                                   ", partition-aligned one-sided IPC pull exchange"),
                    "global_batch": n * world, "seq_len": rs, "parallelism": f"shuffle{world}"},
-        "roofline": {"bound": "hbm", "achieved": None if achieved is None else round(achieved, 1),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": None if achieved is None else round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "kernel": names["scatter"],
-                     "traffic_source": sc_tr["source"] if sc_tr else None,
-                     "alg_bytes_per_launch": int(alg),
-                     "avg_launch_ms": round(sc_avg * 1e3, 4)},
-        "roofline_map_side": {"bound": "hbm",
-                              "achieved": None if map_side is None else round(map_side, 1),
-                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                              "frac": None if map_side is None else round(map_side / HBM_PEAK_GBS, 4),
-                              "traffic_per_step": map_traffic,
-                              "alg_bytes_per_step": int(map_alg / args.steps),
-                              "time": ("wall clock of the timed steps (launch groups overlap)"
-                                       if overlapped else "wall clock of the timed steps"
-                                       if not pipelined else "sum of the map kernels' durations"),
-                              "kernels": names,
-                              "kernels_ms": {k: round(v[1], 3) for k, v in kt.items()},
-                              "launches": {k: v[0] for k, v in kt.items()}},
+        "roofline": roof,
+        "roofline_map_side": roof_map,
         "cpu_baseline": None,
     }
     if pipelined:
@@ -1307,8 +1526,20 @@ def main():
                                               "ranks = the inputs'"}
         result["roofline_exchange"] = {
             "bound": "xgmi", "achieved": None if ach is None else round(ach, 1), "peak": peak,
+            "peak_source": f"(world - 1) x {XGMI_LINK_GBS} GB/s per xGMI link (spec assumption)",
             "unit": "GB/s", "frac": None if ach is None else round(ach / peak, 4),
-            "remote_bytes_per_rank": remote // args.steps, "exchange_ms": round(xms, 2)}
+            "remote_bytes_per_rank": remote // args.steps, "exchange_ms": round(xms, 2),
+            "exchange": args.exchange if args.transport == "rccl" else "ipc pull"}
+        if xprobe is not None:
+            mp = xprobe["GB/s"]
+            if world > 1:  # the slowest rank's peer-read rate bounds the node
+                tt = torch.tensor([mp], dtype=torch.float64, device=ctl)
+                dist.all_reduce(tt, op=dist.ReduceOp.MIN)
+                mp = float(tt.item())
+            result["roofline_exchange"]["measured_peak"] = round(mp, 1)
+            result["roofline_exchange"]["frac_of_measured"] = (
+                None if ach is None or not mp else round(ach / mp, 4))
+            result["roofline_exchange"]["probe"] = xprobe
     if pipelined and world > 1 and args.plugin_groups != 0:
         # the stateless pipeline's rings go back first: the plugin leg's slabs and receive
         # buffers take their HBM.  Every rank first unmaps its peers' send buffers and all
@@ -1332,9 +1563,7 @@ def main():
             node = Node(device=local, rank=rank, world_size=world)
             node.set_bootstrap(lambda b: (lambda out: (dist.all_gather_object(out, b), out)[1])(
                 [None] * world))
-            part = (node.partitioner(kind, R, key_offset=0, key_len=key_len,
-                                     bounds=uniform_bounds(R)) if kind == N.PART_RANGE_BYTES
-                    else node.partitioner(kind, R, key_offset=0, key_len=key_len, seed=42))
+            part = make_partitioner(node, kind, R, key_len)
         pg = min(n // group_recs, args.plugin_groups if args.plugin_groups > 0 else 8)
         if pg:
             xs = torch.cuda.Stream(dev)
@@ -1412,10 +1641,26 @@ def main():
             args, seed, node, part, data if args.workload == "terasort" and R == 200 else None)
         if world > 1 and result["cpu_baseline"]:
             result["cpu_baseline"]["beside"] = f"N={world}: rank 0 only, after the timed steps"
+    if not pipelined and args.workload == "terasort" and (args.c4_steps > 0 or args.c5_steps > 0):
+        # the other BASELINE configs on the same driver-timed line: the headline's node and
+        # output go first (the config legs take a fresh node and the input buffer)
+        part.close()
+        node.close()
+        out = None
+        torch.cuda.empty_cache()
+        cfg = {}
+        if args.c4_steps > 0:
+            cfg["c4"] = config_leg("zipf", data, dev, args.c4_steps)
+            log(f"c4: {cfg['c4']['value']} GB/s")
+        if args.c5_steps > 0:
+            cfg["c5"] = config_leg("small", data, dev, args.c5_steps)
+            log(f"c5: {cfg['c5']['value']} GB/s")
+        result.update(cfg)
     if world > 1:
         dist.barrier()  # the other ranks wait for rank 0's baseline before tearing down
     if rank == 0:
         os.write(result_fd, (json.dumps(result) + "\n").encode())
+    part.close()
     node.close()
     if world > 1:
         dist.destroy_process_group()

@@ -47,6 +47,10 @@ def test_bench_two_ranks_one_gpu():
     # the same shuffle also ran map stage first, exchange after: both phases were timed
     assert res["plugin"]["serial_ms"]["writes"] > 0 and res["plugin"]["serial_ms"]["then_exchange"] > 0
     assert 0.0 <= res["plugin"]["exchange_hidden"] <= 1.0
+    # the peer-read probe ran before the pipeline (flagged: both ranks share one GPU)
+    probe = ex["probe"]
+    assert probe["ok"] and probe["GB/s"] > 0 and "one_gpu" in probe
+    assert ex["measured_peak"] > 0 and ex["frac_of_measured"] is not None
 
 
 @pytest.mark.parametrize("workload", ["terasort", "zipf"])
@@ -97,16 +101,37 @@ def test_bench_starts_its_own_ranks():
     assert cb["parity"]["index_tables_equal"] and cb["parity"]["fetch_checksum_equal"]
 
 
-def test_bench_rccl_at_one_posts_and_issues():
-    """The N > 1 RCCL pipeline on a one-rank communicator (every byte to self): the index
-    all-gather of group k posted on its own stream, the all-to-all of group k - 1 issued after it
-    over the split communicator (sux_exchange_group_post / _issue), every group self-checked."""
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--rccl-at-one", "--records", "3000000",
-           "--map-records", "262144", "--group-maps", "2", "--steps", "2", "--warmup", "1",
-           "--no-cpu-baseline"]
+def _rccl_at_one(*args, timeout=300):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--rccl-at-one", "--no-cpu-baseline",
+           *args]
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
+
+
+@pytest.mark.parametrize("mode", ["one-call", "post-issue"])
+def test_bench_rccl_at_one(mode):
+    """The N > 1 RCCL pipeline on a one-rank communicator (every byte to self), every group
+    self-checked: 'one-call' (the default: all-gather + plan + all-to-all in one
+    sux_exchange_group call) and 'post-issue' (the index all-gather of group k posted on its own
+    stream, the all-to-all of group k - 1 issued after it over the split communicator)."""
+    r = _rccl_at_one("--exchange", mode, "--records", "3000000", "--map-records", "262144",
+                     "--group-maps", "2", "--steps", "2", "--warmup", "1")
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
     assert res["n_gpus"] == 1 and res["self_check"]["ok"] and res["self_check"]["groups"] == 6
     assert res["roofline_exchange"]["exchange_ms"] > 0
+    assert res["roofline_exchange"]["exchange"] == mode
+
+
+def test_forced_mismatch_on_a_3_gb_group_reports_its_first_byte():
+    """the self-check's diagnostic on a 3.36 GB group (32 maps of 2^20 TeraSort
+    records) finds the first differing byte in bounded chunks instead of a whole-buffer
+    nonzero() that asked torch for tens of exabytes."""
+    r = _rccl_at_one("--records", str(32 << 20), "--map-records", str(1 << 20), "--group-maps",
+                     "32", "--steps", "1", "--warmup", "0", "--force-mismatch", timeout=400)
+    assert r.returncode != 0
+    assert "first differing byte at" in r.stderr, r.stderr[-3000:]
+    assert "Tried to allocate" not in r.stderr
+    # the corrupted byte: the first key byte of the group's middle record
+    want = (32 << 20) // 2 * 100
+    assert f"first differing byte at {want} " in r.stderr, r.stderr[-3000:]
