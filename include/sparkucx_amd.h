@@ -125,6 +125,19 @@ typedef int (*sux_allgather_fn)(void* ctx, uint64_t tag, const void* send, uint6
                                 void* recv);
 int sux_node_set_bootstrap(sux_node* node, sux_allgather_fn fn, void* ctx);
 
+/* Join the group's RCCL communicator now, after the node exists: rank 0 makes the unique id,
+ * the node's bootstrap all-gathers it (tag SUX_TAG_COMM_ID), and every rank calls
+ * ncclCommInitRank — a collective over the whole group, so a runtime calls it where every rank
+ * gets to it without depending on its tasks: the JVM's exchange thread, before the first
+ * exchange window the driver relays to every executor.  A node then starts without blocking on
+ * its peers (hello -> rank -> node), the way the reference's executors connect to a peer only
+ * when they first fetch from it (UcxWorkerWrapper.getConnection, UcxWorkerWrapper.scala:129-152).
+ * Idempotent (a node that has a communicator returns SUX_OK); needs the bootstrap
+ * (SUX_ESTATE without one); at world size 1 it makes a one-rank communicator.  Not concurrent
+ * with the node's own exchange calls. */
+#define SUX_TAG_COMM_ID 0xFFFFFFFF00000000ull
+int sux_node_connect(sux_node* node);
+
 /* ---- executor group membership (driver side) --------------------------------------------- *
  * The reference's executors introduce themselves to the driver with their BlockManagerId
  * (UcxNode.startExecutor, UcxNode.java:111-145) and the driver fans every address out to every

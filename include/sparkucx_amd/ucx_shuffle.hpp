@@ -32,6 +32,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -110,6 +111,9 @@ class UcxShuffleConf {
   uint32_t poolLimitMiB() const { return (uint32_t)std::stoul(get(ucx("gpu.poolLimitMiB"), "0")); }
   // spill directory (spark.local.dir): "" = no spill
   std::string spillDir() const { return get(ucx("gpu.spillDir"), ""); }
+  // the group's exchange transport: "rccl" (a communicator joined on the exchange thread) or
+  // "ipc" (one-sided pulls; several executors on one GPU)
+  std::string transport() const { return get(ucx("gpu.transport"), "rccl"); }
 
   sux_conf toNative() const {
     sux_conf c;
@@ -170,6 +174,12 @@ class UcxNode {
   }
   // device-side failures recorded by the kernels (sux_node_check)
   void check() const { sparkucx::check(sux_node_check(node_), "device error word"); }
+  // the group's control plane (GpuNode's RpcBootstrap) and its RCCL communicator, joined
+  // through it after the node exists (sux_node_connect: a collective over the group)
+  void setBootstrap(sux_allgather_fn fn, void* ctx) {
+    sparkucx::check(sux_node_set_bootstrap(node_, fn, ctx), "setBootstrap");
+  }
+  void connect() { sparkucx::check(sux_node_connect(node_), "nodeConnect"); }
   ~UcxNode() { close(); }
   UcxNode(const UcxNode&) = delete;
   UcxNode& operator=(const UcxNode&) = delete;
@@ -323,6 +333,10 @@ struct UcxShuffleHandle {
   int numPartitions = 0;
   int recordSize = 0;
   sux_handle_desc desc{};
+  // the dependency's partitioner as it travels to the executors (each builds its own on its
+  // node: the JVM's GpuPartitioning); `partitioner` is the registering manager's instance
+  sux_partitioner_desc partitionerDesc{};
+  std::shared_ptr<const std::vector<uint8_t>> rangeBounds;
   std::shared_ptr<sux_partitioner> partitioner;
   bool hasLayout = false;
   GpuRowLayout layout{};
@@ -502,8 +516,40 @@ class UcxShuffleReader {
   std::map<int64_t, int> mapIds_;
 };
 
+class UcxShuffleManager;
+
+// ---------------------------------------------------------------------------------------------
+// compat/spark_3_0/UcxLocalDiskShuffleExecutorComponents.scala: the executor's ShuffleDataIO
+// components.  initializeExecutor starts the node; a map-output writer asked for before it
+// throws IllegalStateException (:31-33, :41-44).
+// ---------------------------------------------------------------------------------------------
+class UcxLocalDiskShuffleExecutorComponents {
+ public:
+  explicit UcxLocalDiskShuffleExecutorComponents(UcxShuffleManager& manager) : manager_(manager) {}
+  inline void initializeExecutor(const std::string& appId, const std::string& execId);
+  // createMapOutputWriter / createSingleFileMapOutputWriter: the resolver Spark's writers commit to
+  UcxShuffleBlockResolver& createMapOutputWriter(int /*shuffleId*/, int64_t /*mapTaskId*/,
+                                                 int /*numPartitions*/) {
+    if (!resolver_)
+      throw UcxException(SUX_ESTATE, "Executor components must be initialized before getting writers.");
+    return *resolver_;
+  }
+  bool initialized() const { return resolver_ != nullptr; }
+
+ private:
+  UcxShuffleManager& manager_;
+  UcxShuffleBlockResolver* resolver_ = nullptr;
+};
+
 // ---------------------------------------------------------------------------------------------
 // compat/spark_3_0/UcxShuffleManager.scala + CommonUcxShuffleManager.scala
+//
+// Lifecycle, as the reference's (compat/spark_3_0/UcxShuffleManager.scala:21,46,49,63-72): a node
+// starts lazily — on the driver at construction (CommonUcxShuffleManager.scala:35-37), on an
+// executor the first time a writer is asked for (the lazy executor components) or a reader.  A
+// node never waits for its peers at start: it joins the group's communicator on the exchange
+// thread, before its first exchange window (UcxWorkerWrapper.getConnection's lazy connect,
+// UcxWorkerWrapper.scala:129-152).
 // ---------------------------------------------------------------------------------------------
 class UcxShuffleManager {
  public:
@@ -518,7 +564,26 @@ class UcxShuffleManager {
     if (!node_) {
       node_ = std::make_unique<UcxNode>(conf_, isDriver_, commId);
       resolver_ = std::make_unique<UcxShuffleBlockResolver>(*node_);
+      if (boot_) node_->setBootstrap(boot_, bootCtx_);
     }
+  }
+
+  // the group's control plane for this executor's node (GpuNode's RpcBootstrap); kept for a node
+  // that starts later
+  void setBootstrap(sux_allgather_fn fn, void* ctx) {
+    std::lock_guard<std::mutex> lk(mu_);
+    boot_ = fn;
+    bootCtx_ = ctx;
+    if (node_) node_->setBootstrap(fn, ctx);
+  }
+
+  // the reference's `private lazy val shuffleExecutorComponents` (:21, :63-72), forced by getWriter
+  UcxLocalDiskShuffleExecutorComponents& shuffleExecutorComponents() {
+    std::call_once(componentsOnce_, [&] {
+      components_ = std::make_unique<UcxLocalDiskShuffleExecutorComponents>(*this);
+      components_->initializeExecutor("app", isDriver_ ? "driver" : "executor");
+    });
+    return *components_;
   }
 
   // registerShuffle (:25-30) -> registerShuffleCommon (:39-56).  The directory is sized by the
@@ -548,18 +613,32 @@ class UcxShuffleManager {
     check(sux_register_shuffle(node_->native(), shuffleId, numMaps, partitioner.num_partitions,
                                recordSize, &h.desc),
           "registerShuffle");
+    h.partitionerDesc = partitioner;
+    if (partitioner.kind == SUX_PART_RANGE_BYTES && partitioner.range_bounds) {
+      const uint8_t* b = static_cast<const uint8_t*>(partitioner.range_bounds);
+      h.rangeBounds = std::make_shared<const std::vector<uint8_t>>(
+          b, b + (size_t)(partitioner.num_partitions - 1) * partitioner.key_len);
+      h.partitionerDesc.range_bounds = h.rangeBounds->data();
+    }
     sux_partitioner* p = nullptr;
-    check(sux_partitioner_create(node_->native(), &partitioner, &p), "partitioner");
+    check(sux_partitioner_create(node_->native(), &h.partitionerDesc, &p), "partitioner");
     h.partitioner = std::shared_ptr<sux_partitioner>(p, [](sux_partitioner* x) { sux_partitioner_destroy(x); });
     std::lock_guard<std::mutex> lk(mu_);
     handles_[shuffleId] = h;
+    registered_.insert(shuffleId);
+    partitioners_[shuffleId] = h.partitioner;
     return h;
   }
 
-  // getWriter(handle, mapId, context, metrics) (:32-51)
+  // getWriter(handle, mapId, context, metrics) (:32-51): on an executor that has done nothing
+  // else, forcing the executor components starts the node (:21, :46, :49, :63-72); the shuffle
+  // is registered on this node and its partitioner built here from the handle's description
   UcxShuffleWriter getWriter(const UcxShuffleHandle& h, int64_t mapId, int partitionId) {
-    requireNode();
-    return UcxShuffleWriter(*node_, h, mapId, partitionId);
+    shuffleExecutorComponents();
+    startUcxNodeIfMissing();
+    UcxShuffleHandle mine = h;
+    mine.partitioner = ensureRegistered(h);
+    return UcxShuffleWriter(*node_, mine, mapId, partitionId);
   }
 
   // getReader(handle, startPartition, endPartition, context, metrics) (:53-60)
@@ -579,6 +658,10 @@ class UcxShuffleManager {
   // `stream`), then the completion every reduce task waits for.
   void exchangeWindow(int shuffleId, int firstMap, int numMaps, void* stream = nullptr) {
     requireNode();
+    if (!connected_ && conf_.worldSize() > 1 && conf_.transport() == "rccl") {
+      node_->connect();  // the group's communicator, once, on the exchange thread
+      connected_ = true;
+    }
     check(sux_exchange_maps(node_->native(), shuffleId, firstMap, numMaps, stream), "exchangeMaps");
   }
   void exchangeDone(int shuffleId) {
@@ -589,7 +672,9 @@ class UcxShuffleManager {
   // unregisterShuffle (:73-77)
   bool unregisterShuffle(int shuffleId) {
     std::lock_guard<std::mutex> lk(mu_);
-    if (!node_ || !handles_.erase(shuffleId)) return false;
+    partitioners_.erase(shuffleId);
+    const bool known = handles_.erase(shuffleId) + registered_.erase(shuffleId) > 0;
+    if (!node_ || !known) return false;
     return sux_unregister_shuffle(node_->native(), shuffleId) == SUX_OK;
   }
 
@@ -602,6 +687,8 @@ class UcxShuffleManager {
     }
     for (int id : ids) unregisterShuffle(id);
     std::lock_guard<std::mutex> lk(mu_);
+    partitioners_.clear();
+    registered_.clear();
     resolver_.reset();
     node_.reset();
   }
@@ -620,12 +707,48 @@ class UcxShuffleManager {
     // UcxLocalDiskShuffleExecutorComponents.scala:31-33
     if (!node_) throw UcxException(SUX_ESTATE, "Executor components must be initialized before getting writers.");
   }
+  // the executor learns a shuffle from its first task (GpuNode.ensureRegistered): registered on
+  // this node once, its partitioner built on this node from the handle's description
+  std::shared_ptr<sux_partitioner> ensureRegistered(const UcxShuffleHandle& h) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!registered_.count(h.shuffleId)) {
+      sux_handle_desc d{};
+      check(sux_register_shuffle(node_->native(), h.shuffleId, h.numMaps, h.numPartitions,
+                                 h.recordSize, &d),
+            "registerShuffle");
+      registered_.insert(h.shuffleId);
+    }
+    auto it = partitioners_.find(h.shuffleId);
+    if (it != partitioners_.end()) return it->second;
+    sux_partitioner_desc pd = h.partitionerDesc;
+    if (h.rangeBounds) pd.range_bounds = h.rangeBounds->data();
+    sux_partitioner* p = nullptr;
+    check(sux_partitioner_create(node_->native(), &pd, &p), "partitioner");
+    auto sp = std::shared_ptr<sux_partitioner>(p, [](sux_partitioner* x) { sux_partitioner_destroy(x); });
+    partitioners_[h.shuffleId] = sp;
+    return sp;
+  }
   UcxShuffleConf conf_;
   bool isDriver_;
   std::mutex mu_;
   std::unique_ptr<UcxNode> node_;
   std::unique_ptr<UcxShuffleBlockResolver> resolver_;
   std::map<int, UcxShuffleHandle> handles_;
+  std::set<int> registered_;
+  std::map<int, std::shared_ptr<sux_partitioner>> partitioners_;
+  std::once_flag componentsOnce_;
+  std::unique_ptr<UcxLocalDiskShuffleExecutorComponents> components_;
+  sux_allgather_fn boot_ = nullptr;
+  void* bootCtx_ = nullptr;
+  bool connected_ = false;  // exchange thread only
 };
+
+// UcxLocalDiskShuffleExecutorComponents.initializeExecutor (:26-30): start the node, keep its
+// resolver for Spark's writers
+inline void UcxLocalDiskShuffleExecutorComponents::initializeExecutor(const std::string&,
+                                                                      const std::string&) {
+  manager_.startUcxNodeIfMissing();
+  resolver_ = &manager_.shuffleBlockResolver();
+}
 
 }  // namespace sparkucx

@@ -1103,6 +1103,33 @@ int sux_node_set_bootstrap(sux_node* node, sux_allgather_fn fn, void* ctx) {
   });
 }
 
+int sux_node_connect(sux_node* node) {
+  return guard([&] {
+    require(node, SUX_EINVAL, "NULL node");
+    {
+      std::lock_guard<std::mutex> lk(node->mu);
+      if (node->comm) return;
+      require(node->boot != nullptr, SUX_ESTATE,
+              "sux_node_connect needs the group's bootstrap (sux_node_set_bootstrap)");
+    }
+    node->bind();
+    const int W = node->conf.world_size, r = node->conf.rank;
+    ncclUniqueId mine;
+    std::memset(&mine, 0, sizeof mine);
+    if (r == 0) nccl_check(ncclGetUniqueId(&mine), "ncclGetUniqueId");
+    std::vector<uint8_t> all((size_t)W * sizeof mine);
+    const int rc = node->boot(node->boot_ctx, SUX_TAG_COMM_ID, &mine, sizeof mine, all.data());
+    require(rc == 0, SUX_ECOMM, "bootstrap all-gather of the RCCL unique id failed (" +
+                                    std::to_string(rc) + ")");
+    ncclUniqueId id;
+    std::memcpy(&id, all.data(), sizeof id);  // rank 0's
+    ncclComm_t comm = nullptr;
+    nccl_check(ncclCommInitRank(&comm, W, id, r), "ncclCommInitRank");
+    std::lock_guard<std::mutex> lk(node->mu);
+    node->comm = comm;
+  });
+}
+
 // ---- executor group membership (driver side; host-only: no HIP call, so a driver without a
 // GPU, or a parent process that forks its executors, never initialises the runtime) ----------
 }  // extern "C"

@@ -83,6 +83,7 @@ _SIGS = {
     "sux_conf_init": (None, [C.POINTER(Conf)]),
     "sux_conf_set_prealloc": (C.c_int, [C.POINTER(Conf), C.c_char_p]),
     "sux_node_set_bootstrap": (C.c_int, [P, ALLGATHER_FN, P]),
+    "sux_node_connect": (C.c_int, [P]),
     "sux_exchange_group_post": (C.c_int, [P, P, I32, I32, P, P, C.POINTER(P)]),
     "sux_exchange_group_issue": (C.c_int, [P, P, P, P, U64, P, P]),
     "sux_group_create": (C.c_int, [C.c_int32, C.POINTER(P)]),

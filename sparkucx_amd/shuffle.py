@@ -91,6 +91,11 @@ class Node:
         self._boot = N.ALLGATHER_FN(fn)  # kept alive as long as the node
         N.check(self.lib.sux_node_set_bootstrap(self.h, self._boot, None), "sux_node_set_bootstrap")
 
+    def connect(self):
+        """sux_node_connect: join the group's RCCL communicator through the bootstrap (rank 0's
+        unique id all-gathered, then ncclCommInitRank) — a collective over the group."""
+        N.check(self.lib.sux_node_connect(self.h), "sux_node_connect")
+
     def tuning(self) -> dict:
         t = N.Tuning()
         N.check(self.lib.sux_node_get_tuning(self.h, C.byref(t)), "sux_node_get_tuning")

@@ -51,6 +51,11 @@ public final class SuxNative {
   /** HBM-capacity fallback: committed map outputs spill to Spark's files under dir. */
   public static native void setSpillDir(long node, String dir);
   public static native long spills(long node);
+  /** Join the group's RCCL communicator (a collective over the group: rank 0's unique id
+   * through the node's bootstrap, then ncclCommInitRank); called on the exchange thread before
+   * the first exchange window, so starting a node never waits for the other executors. */
+  public static native void nodeConnect(long node);
+
   public static native void releaseBootstrap(long ctx);
   public static native long[] poolStats(long node);
   /** sux_tuning fields in header order (TUNING_FIELDS); 0 = the measured default. */

@@ -195,6 +195,13 @@ JNIEXPORT jlong JNICALL FN(setBootstrap)(JNIEnv* env, jclass cls, jlong node, jo
   return (jlong)(intptr_t)b; /* freed by releaseBootstrap after nodeDestroy */
 }
 
+/* The group's RCCL communicator, joined on the exchange thread (sux_node_connect: rank 0's
+ * unique id through the bootstrap above, then ncclCommInitRank) */
+JNIEXPORT void JNICALL FN(nodeConnect)(JNIEnv* env, jclass cls, jlong node) {
+  (void)cls;
+  failed(env, sux_node_connect(NODE(node)), "nodeConnect");
+}
+
 JNIEXPORT void JNICALL FN(releaseBootstrap)(JNIEnv* env, jclass cls, jlong ctx) {
   (void)cls;
   boot_ctx* b = (boot_ctx*)(intptr_t)ctx;

@@ -17,8 +17,11 @@ package org.apache.spark.shuffle
 
 import java.util.concurrent.ConcurrentHashMap
 
+import scala.collection.JavaConverters._
+
 import org.apache.spark.{ShuffleDependency, SparkConf, SparkEnv, TaskContext}
 import org.apache.spark.internal.Logging
+import org.apache.spark.shuffle.api.ShuffleExecutorComponents
 import org.apache.spark.shuffle.compat.spark_3_0.{UcxShuffleBlockResolver, UcxShuffleReader}
 import org.apache.spark.shuffle.gpu.{FixedWidthRowSerializer, GpuExchangeCoordinator, GpuNode,
   GpuPartitioning, GpuRowLayout, GpuShuffleWriter}
@@ -41,7 +44,25 @@ class UcxShuffleManager(val conf: SparkConf, isDriver: Boolean) extends SortShuf
   with Logging {
 
   ShutdownHookManager.addShutdownHook(Int.MaxValue - 1)(() => stop())
-  if (isDriver) GpuNode.startIfMissing(conf, isDriver = true)
+  // Spark builds this manager inside SparkEnv.create, before SparkEnv.set: nothing here may need
+  // SparkEnv.  The driver sets up the group's control endpoint from the plugin's driver
+  // components or its first registerShuffle; an executor of a group joins in the background once
+  // its SparkEnv exists (so it is in every exchange even without tasks); a lone GPU starts its
+  // node with the first task, through the executor components, as the reference does.
+  if (!isDriver && conf.getInt("spark.shuffle.ucx.gpu.worldSize", 1) > 1) {
+    GpuNode.joinInBackground(conf, isDriver)
+  }
+
+  // compat/spark_3_0/UcxShuffleManager.scala:21,46,49,63-72 of the reference: the executor's
+  // ShuffleDataIO components, initialised the first time a writer is asked for — initializeExecutor
+  // starts the node (UcxLocalDiskShuffleExecutorComponents), so getWriter works on an executor
+  // that has done nothing else.  Spark 3.0 initialises them nowhere else on an executor.
+  private lazy val shuffleExecutorComponents: ShuffleExecutorComponents = {
+    val components = ShuffleDataIOUtils.loadShuffleDataIO(conf).executor()
+    val extraConfigs = conf.getAllWithPrefix(ShuffleDataIOUtils.SHUFFLE_SPARK_CONF_PREFIX).toMap
+    components.initializeExecutor(conf.getAppId, SparkEnv.get.executorId, extraConfigs.asJava)
+    components
+  }
 
   override val shuffleBlockResolver = new UcxShuffleBlockResolver(conf)
 
@@ -61,6 +82,7 @@ class UcxShuffleManager(val conf: SparkConf, isDriver: Boolean) extends SortShuf
     }
     val handle = new UcxGpuShuffleHandle(shuffleId, numMaps, layout, base)
     if (isDriver) {
+      GpuNode.setupDriver(conf)  // SparkEnv is set by now (a no-op for a lone GPU)
       GpuExchangeCoordinator.watch(conf, shuffleId, numMaps, dependency.partitioner.numPartitions,
         handle.recordSize)
     }
@@ -75,7 +97,8 @@ class UcxShuffleManager(val conf: SparkConf, isDriver: Boolean) extends SortShuf
   override def getWriter[K, V](handle: ShuffleHandle, mapId: Long, context: TaskContext,
                                metrics: ShuffleWriteMetricsReporter): ShuffleWriter[K, V] = {
     val h = handle.asInstanceOf[UcxGpuShuffleHandle[K, V, _]]
-    val node = GpuNode.get  // IllegalStateException before the executor components start
+    shuffleExecutorComponents  // Spark's SPI init; ours starts the node (initializeExecutor)
+    val node = startUcxNodeIfMissing()  // and whatever plugin class is configured, so does this
     ensureRegistered(h, node)
     val dep = h.baseHandle.dependency
     val rows = dep.serializer match {

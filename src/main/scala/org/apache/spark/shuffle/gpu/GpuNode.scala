@@ -14,9 +14,18 @@
  *  - the exchange group's control plane over Spark RPC through the driver (GpuControlEndpoint):
  *    a host all-gather matched by tag, which replaces the UCX tag messages of the reference's
  *    bootstrap, and the driver -> executor messages of GpuExchangeCoordinator.  With
- *    spark.shuffle.ucx.gpu.transport = rccl (default) rank 0's RCCL unique id travels through
- *    that all-gather and the node builds an RCCL communicator (ncclAllToAllv over xGMI); with
- *    ipc the exchange pulls blocks over HIP IPC (several executors on one GPU);
+ *    spark.shuffle.ucx.gpu.transport = rccl (default) the node joins the group's RCCL
+ *    communicator on its exchange thread, before its first exchange window (sux_node_connect:
+ *    rank 0's unique id through that all-gather, then ncclCommInitRank); with ipc the exchange
+ *    pulls blocks over HIP IPC (several executors on one GPU);
+ *  - lifecycle (the reference's: UcxShuffleManager.scala:21,46,49,63-72 and
+ *    UcxWorkerWrapper.getConnection, UcxWorkerWrapper.scala:129-152): starting a node never waits
+ *    for the other executors — Hello -> rank (the driver answers at once), node, bootstrap, then
+ *    Ready; the driver relays exchange messages to an executor only after its Ready, replaying
+ *    the ones it missed; the one group-wide wait (the communicator) runs on the exchange thread.
+ *    An executor of a group starts its node in the background as soon as its SparkEnv exists
+ *    (UcxShuffleManager), so it joins every exchange even if it never runs a task; any map task
+ *    starts it too, through the executor components (getWriter), as in the reference;
  *  - the exchange: a collective over the group, so it is not run by whichever reduce task comes
  *    first (an executor without reduce tasks would never join it) but by every executor when the
  *    driver's coordinator says so — window by window as map tasks finish, the last when the map
@@ -50,17 +59,19 @@ class GpuNode private (conf: SparkConf, isDriver: Boolean) extends Logging {
   private val member = worldSize > 1 && !isDriver
 
   // executors of a group register with the driver's control endpoint (which also relays the
-  // coordinator's messages to them) and learn their rank from its reply
-  private val (rank0, localIndex) =
+  // coordinator's messages to them) and learn their rank from its reply.  The executor endpoint
+  // holds every message it gets until the node is built (ready(), the constructor's last step);
+  // the driver relays nothing to this executor before its Ready anyway (ADVICE r04).
+  private val (rank0, localIndex, myEndpoint) =
     if (member) {
       val env = SparkEnv.get
-      val me = env.rpcEnv.setupEndpoint(GpuControlEndpoint.EXECUTOR + env.executorId,
-        new GpuExecutorEndpoint(env.rpcEnv, this))
-      val w = RpcUtils.makeDriverRef(GpuControlEndpoint.NAME, conf, env.rpcEnv)
+      val ep = new GpuExecutorEndpoint(env.rpcEnv)
+      val me = env.rpcEnv.setupEndpoint(GpuControlEndpoint.EXECUTOR + env.executorId, ep)
+      val w = GpuControlEndpoint.driverRef(conf, env.rpcEnv)
         .askSync[GpuControlEndpoint.Welcome](
           GpuControlEndpoint.Hello(env.executorId, Utils.localHostName(), worldSize, me))
-      (w.rank, w.localIndex)
-    } else (0, 0)
+      (w.rank, w.localIndex, Some((ep, me)))
+    } else (0, 0, None)
   val rank: Int = rank0
 
   // the task's "gpu" resource (Spark 3.0 resource scheduling; the node starts inside the first
@@ -81,15 +92,9 @@ class GpuNode private (conf: SparkConf, isDriver: Boolean) extends Logging {
 
   private val boot: Bootstrap = if (member) new RpcBootstrap(conf, rank, worldSize) else null
 
-  // rccl: rank 0 creates the communicator's unique id (its process hosts RCCL's bootstrap
-  // root) and every rank takes it from the first slot of one all-gather
-  private val commId: Array[Byte] =
-    if (member && transport == "rccl") {
-      val mine = if (rank == 0) SuxNative.commUniqueId() else new Array[Byte](128)
-      java.util.Arrays.copyOfRange(boot.allGather(GpuNode.COMM_ID_TAG, mine), 0, 128)
-    } else null
-
-  private val handle0: Long = SuxNative.nodeCreate(device, rank, worldSize, commId,
+  // no communicator yet: the node is built without waiting for any other executor; rccl joins
+  // the group's communicator on the exchange thread (connectOnce)
+  private val handle0: Long = SuxNative.nodeCreate(device, rank, worldSize, null,
     bytes(ucx("memory.minBufferSize"), "1024"), minAllocationSize, metadataBlockSize,
     conf.get(ucx("memory.preAllocateBuffers"), ""), conf.getInt(ucx("gpu.poolLimitMiB"), 0),
     isDriver)
@@ -163,6 +168,13 @@ class GpuNode private (conf: SparkConf, isDriver: Boolean) extends Logging {
     }
   })
   private lazy val exchangeStream: Long = SuxNative.streamCreate(handle0)
+  // exchange thread only: the group's RCCL communicator, joined before the first exchange
+  // (every executor of the group gets the same first window, so every rank reaches it)
+  private var connected = !(member && transport == "rccl")
+  private def connectOnce(): Unit = if (!connected) {
+    SuxNative.nodeConnect(handle0)
+    connected = true
+  }
   private val exchanges = new ConcurrentHashMap[Int, Promise[Unit]]()
   private def promiseOf(id: Int): Promise[Unit] = exchanges.computeIfAbsent(id, _ => Promise[Unit]())
   private val exchangeTimeout: Duration =
@@ -176,6 +188,7 @@ class GpuNode private (conf: SparkConf, isDriver: Boolean) extends Logging {
     exchangeThread.execute(() => {
       try {
         ensureRegistered(w.shuffleId, w.numMaps, w.numPartitions, w.recordSize)
+        connectOnce()
         SuxNative.exchangeMaps(handle0, w.shuffleId, w.first, w.count, exchangeStream)
       } catch { case e: Throwable => promiseOf(w.shuffleId).tryFailure(e) }
     })
@@ -193,6 +206,13 @@ class GpuNode private (conf: SparkConf, isDriver: Boolean) extends Logging {
   def awaitExchange(shuffleId: Int): Unit =
     if (worldSize > 1) Await.result(promiseOf(shuffleId).future, exchangeTimeout)
 
+  // the node is built: deliver what the endpoint held, then tell the driver it may relay
+  myEndpoint.foreach { case (ep, me) =>
+    ep.ready(this)
+    GpuControlEndpoint.driverRef(conf, SparkEnv.get.rpcEnv)
+      .askSync[Boolean](GpuControlEndpoint.Ready(rank, me))
+  }
+
   def close(): Unit = synchronized {
     exchangeThread.shutdown()
     exchangeThread.awaitTermination(10, TimeUnit.SECONDS)
@@ -204,21 +224,39 @@ class GpuNode private (conf: SparkConf, isDriver: Boolean) extends Logging {
   }
 }
 
-object GpuNode {
+object GpuNode extends Logging {
   @volatile private var instance: GpuNode = _
-  /** The bootstrap all-gather of rank 0's RCCL unique id: outside every shuffle's tags
-   * ((shuffle id << 32) | count, shuffle ids >= 0). */
+  /** The bootstrap all-gather of rank 0's RCCL unique id (SUX_TAG_COMM_ID, made by
+   * sux_node_connect): outside every shuffle's tags ((shuffle id << 32) | count, ids >= 0). */
   val COMM_ID_TAG: Long = 0xFFFFFFFF00000000L
 
-  /** CommonUcxShuffleManager.startUcxNodeIfMissing (:67-71): lazy and synchronized. */
+  /** CommonUcxShuffleManager.startUcxNodeIfMissing (:67-71): lazy and synchronized.  Needs
+   * SparkEnv (an executor's endpoint, the block manager's dirs), so it is never called from a
+   * ShuffleManager constructor: Spark builds the manager inside SparkEnv.create. */
   def startIfMissing(conf: SparkConf, isDriver: Boolean): GpuNode = synchronized {
-    if (instance == null) {
-      if (isDriver && conf.getInt("spark.shuffle.ucx.gpu.worldSize", 1) > 1) {
-        GpuControlEndpoint.setup(SparkEnv.get.rpcEnv, conf.getInt("spark.shuffle.ucx.gpu.worldSize", 1))
-      }
-      instance = new GpuNode(conf, isDriver)
-    }
+    if (instance == null) instance = new GpuNode(conf, isDriver)
     instance
+  }
+
+  /** Driver: the group's control endpoint (idempotent; needs SparkEnv, see ensureSetup). */
+  def setupDriver(conf: SparkConf): Unit = GpuControlEndpoint.ensureSetup(conf)
+
+  /** An executor of a group joins it as soon as its SparkEnv exists, on a daemon thread, so that
+   * it takes part in every exchange even if the scheduler never gives it a task (the exchange is
+   * a collective over the group).  A failed join is logged; the first task retries it. */
+  def joinInBackground(conf: SparkConf, isDriver: Boolean): Unit = {
+    val t = new Thread(() => {
+      try {
+        val deadline = System.currentTimeMillis() +
+          conf.getTimeAsMs("spark.network.timeout", "120s")
+        while (SparkEnv.get == null && System.currentTimeMillis() < deadline) Thread.sleep(20)
+        if (SparkEnv.get != null) startIfMissing(conf, isDriver)
+      } catch {
+        case e: Throwable => logWarning("GPU group join failed; the first task retries it", e)
+      }
+    }, "sparkucx-gpu-join")
+    t.setDaemon(true)
+    t.start()
   }
 
   def get: GpuNode = {
@@ -253,6 +291,11 @@ private[gpu] object GpuControlEndpoint {
   /** An executor joins the group: every executor sends the same conf's world size. */
   case class Hello(executorId: String, host: String, world: Int, ref: RpcEndpointRef)
   case class Welcome(rank: Int, localIndex: Int, world: Int)
+  /** The executor's node is built: from now on the driver relays exchange messages to it,
+   * starting with every relayed message it missed. */
+  case class Ready(rank: Int, ref: RpcEndpointRef)
+  /** Driver-internal: a shuffle's relayed messages leave the backlog. */
+  case class Forget(shuffleId: Int)
   /** Map tasks [first, first + count) of a shuffle (numMaps / numPartitions / recordSize: what an
    * executor that ran none of its tasks needs to register it before the collective). */
   case class ExchangeWindow(shuffleId: Int, numMaps: Int, numPartitions: Int, recordSize: Int,
@@ -261,8 +304,34 @@ private[gpu] object GpuControlEndpoint {
 
   @volatile private var endpoint: RpcEndpointRef = _
 
-  def setup(rpcEnv: RpcEnv, world: Int): Unit =
-    endpoint = rpcEnv.setupEndpoint(NAME, new GpuControlEndpoint(rpcEnv, world))
+  /** Driver: the control endpoint, set up once SparkEnv exists — from the plugin's driver
+   * components (ShuffleDriverComponents.initializeApplication, which SparkContext calls after
+   * SparkEnv.set) or from the first registerShuffle, whichever comes first.  Never from the
+   * ShuffleManager's constructor: SparkEnv.get is still null there. */
+  def ensureSetup(conf: SparkConf): Unit = synchronized {
+    val world = conf.getInt("spark.shuffle.ucx.gpu.worldSize", 1)
+    if (endpoint == null && world > 1) {
+      val env = SparkEnv.get
+      require(env != null, "the GPU control endpoint needs the driver's SparkEnv")
+      endpoint = env.rpcEnv.setupEndpoint(NAME, new GpuControlEndpoint(env.rpcEnv, world))
+    }
+  }
+
+  /** Executor: the driver's endpoint, waiting for it to exist (an executor's background join
+   * can start before the driver set it up), bounded by spark.network.timeout. */
+  def driverRef(conf: SparkConf, rpcEnv: RpcEnv): RpcEndpointRef = {
+    val deadline = System.currentTimeMillis() + conf.getTimeAsMs("spark.network.timeout", "120s")
+    var ref: RpcEndpointRef = null
+    while (ref == null) {
+      try ref = RpcUtils.makeDriverRef(NAME, conf, rpcEnv)
+      catch {
+        case e: Exception =>
+          if (System.currentTimeMillis() > deadline) throw e
+          Thread.sleep(200)
+      }
+    }
+    ref
+  }
 
   /** Driver: relay a coordinator message to every executor of the group, in order. */
   def broadcast(msg: Any): Unit = Option(endpoint).foreach(_.send(msg))
@@ -272,14 +341,25 @@ private class GpuControlEndpoint(override val rpcEnv: RpcEnv, world: Int)
   extends ThreadSafeRpcEndpoint {
   import GpuControlEndpoint._
   private val pending = mutable.Map[Long, Array[(Array[Byte], RpcCallContext)]]()
+  // executors that are Ready (null until then) and every relayed message of the live shuffles,
+  // in order: a late executor gets the ones it missed before any new one
   private val executors = new Array[RpcEndpointRef](world)
+  private val backlog = mutable.ArrayBuffer[Any]()
   // ranks by first arrival, keyed by executor id (sux_group: a repeated hello gets its rank back)
   private val group: Long = SuxNative.groupCreate(world)
 
   override def onStop(): Unit = SuxNative.groupDestroy(group)
 
   override def receive: PartialFunction[Any, Unit] = {
-    case m @ (_: ExchangeWindow | _: ExchangeDone) => executors.filter(_ != null).foreach(_.send(m))
+    case m @ (_: ExchangeWindow | _: ExchangeDone) =>
+      backlog += m
+      executors.filter(_ != null).foreach(_.send(m))
+    case Forget(id) =>
+      backlog --= backlog.filter {
+        case w: ExchangeWindow => w.shuffleId == id
+        case d: ExchangeDone => d.shuffleId == id
+        case _ => false
+      }
   }
 
   override def receiveAndReply(context: RpcCallContext): PartialFunction[Any, Unit] = {
@@ -290,9 +370,16 @@ private class GpuControlEndpoint(override val rpcEnv: RpcEnv, world: Int)
       } else {
         try {
           val Array(rank, local) = SuxNative.groupJoin(group, executorId, host)
-          executors(rank) = ref
           context.reply(Welcome(rank, local, world))
         } catch { case e: Exception => context.sendFailure(e) }
+      }
+    case Ready(rank, ref) =>
+      if (rank < 0 || rank >= world) {
+        context.sendFailure(new IllegalStateException(s"Ready from rank $rank of $world"))
+      } else {
+        backlog.foreach(ref.send)
+        executors(rank) = ref
+        context.reply(true)
       }
     case Contribute(tag, rank, w, bytes) =>
       require(w == world, s"bootstrap: executor reports world $w, driver expects $world")
@@ -312,12 +399,27 @@ private class GpuControlEndpoint(override val rpcEnv: RpcEnv, world: Int)
   }
 }
 
-private class GpuExecutorEndpoint(override val rpcEnv: RpcEnv, node: GpuNode)
-  extends ThreadSafeRpcEndpoint {
+private class GpuExecutorEndpoint(override val rpcEnv: RpcEnv) extends ThreadSafeRpcEndpoint {
   import GpuControlEndpoint._
-  override def receive: PartialFunction[Any, Unit] = {
+  // messages that arrive before the node is built wait here, in order (ThreadSafeRpcEndpoint:
+  // receive and ready() never run at once, both synchronized on this endpoint)
+  private var node: GpuNode = _
+  private val held = mutable.ArrayBuffer[Any]()
+
+  def ready(n: GpuNode): Unit = synchronized {
+    node = n
+    held.foreach(deliver)
+    held.clear()
+  }
+
+  private def deliver(m: Any): Unit = m match {
     case w: ExchangeWindow => node.exchangeWindow(w)
     case ExchangeDone(id) => node.exchangeDone(id)
+  }
+
+  override def receive: PartialFunction[Any, Unit] = {
+    case m @ (_: ExchangeWindow | _: ExchangeDone) =>
+      synchronized { if (node == null) held += m else deliver(m) }
   }
 }
 
@@ -352,7 +454,10 @@ object GpuExchangeCoordinator extends Logging {
     }
   }
 
-  def forget(shuffleId: Int): Unit = watched.remove(shuffleId)
+  def forget(shuffleId: Int): Unit = {
+    watched.remove(shuffleId)
+    GpuControlEndpoint.broadcast(GpuControlEndpoint.Forget(shuffleId))
+  }
 
   private def advance(id: Int, w: Watch, stageDone: Boolean): Unit = w.synchronized {
     if (w.window > 0) {

@@ -52,17 +52,22 @@ int main() {
   sux_partitioner_desc pdesc{SUX_PART_RANGE_BYTES, R, 0, 10, 42, 1, bounds.data()};
   o_part opart{1, R, 0, 10, 42, 1, bounds.data()};
 
-  // executor components must be initialised before writers (IllegalStateException analog)
+  // the executor components refuse a map-output writer before initializeExecutor
+  // (UcxLocalDiskShuffleExecutorComponents.scala:31-33, IllegalStateException analog)
   {
     UcxShuffleManager m(UcxShuffleConf(std::map<std::string, std::string>{{"spark.shuffle.ucx.gpu.device", "0"}}), false);
+    UcxLocalDiskShuffleExecutorComponents c(m);
     bool threw = false;
     try {
-      UcxShuffleHandle h;
-      m.getWriter(h, 1, 0);
+      c.createMapOutputWriter(1, 1, R);
     } catch (const UcxException& e) {
-      threw = e.code() == SUX_ESTATE;
+      threw = e.code() == SUX_ESTATE &&
+              std::string(e.what()).find("must be initialized before getting writers") != std::string::npos;
     }
-    EXPECT(threw, "getWriter before the node starts must throw IllegalStateException-like");
+    EXPECT(threw, "a writer before initializeExecutor must throw IllegalStateException-like");
+    c.initializeExecutor("app-1", "1");
+    EXPECT(c.initialized(), "initializeExecutor starts the node");
+    c.createMapOutputWriter(1, 1, R);  // now fine
   }
 
   UcxShuffleConf conf(std::map<std::string, std::string>{{"spark.shuffle.ucx.memory.minBufferSize", "1k"},
@@ -98,6 +103,33 @@ int main() {
     EXPECT(manager.shuffleBlockResolver().getIndexFile(7, i, R) == want_be[i], "map %d index", i);
     mapIdToBlockIndex[100 + i] = i;
     first += counts[i];
+  }
+
+  // getWriter on a FRESH executor-side manager, with no manual start: the
+  // reference's getWriter forces its lazy executor components, whose initializeExecutor starts
+  // the node (compat/spark_3_0/UcxShuffleManager.scala:21,46,49,63-72).  The handle comes from
+  // the driver; the executor registers the shuffle and builds the partitioner on its own node.
+  {
+    UcxShuffleManager exec(UcxShuffleConf(std::map<std::string, std::string>{
+                               {"spark.shuffle.ucx.gpu.device", "0"}}),
+                           /*isDriver=*/false);
+    void* dev = nullptr;
+    HIP_OK(hipMalloc(&dev, in[2].size()));
+    HIP_OK(hipMemcpy(dev, in[2].data(), in[2].size(), hipMemcpyHostToDevice));
+    UcxShuffleWriter w = exec.getWriter(h, 102, 2);  // the executor's first call of any kind
+    w.write(dev, counts[2]);
+    HIP_OK(hipFree(dev));
+    EXPECT(w.getPartitionLengths() == want_len[2], "fresh executor: map lengths");
+    EXPECT(exec.shuffleBlockResolver().getIndexFile(7, 2, R) == want_be[2], "fresh executor: index");
+    auto got = exec.getReader(h, 0, R, {{102, 2}}).read();
+    EXPECT(got.failures.empty() && got.blocks.size() == 1, "fresh executor: read back");
+    if (!got.blocks.empty()) {
+      EXPECT(d2h(got.blocks[0].second.devicePtr(), got.blocks[0].second.size()) == want_data[2],
+             "fresh executor: map output bytes");
+      got.blocks[0].second.release();
+    }
+    EXPECT(exec.shuffleExecutorComponents().initialized(), "components initialised by getWriter");
+    EXPECT(exec.unregisterShuffle(7), "the executor unregisters its copy");
   }
 
   // reduce side: batch fetch of [10, 23) from every map, through the reader

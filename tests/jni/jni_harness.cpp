@@ -35,6 +35,7 @@ constexpr int kGroupWorld = 8;
 constexpr size_t kSlotBytes = 4u << 20;
 struct GroupShm {
   pthread_barrier_t bar;
+  volatile int relayed;  // lifecycle: the driver relayed the exchange before the late Ready
   uint64_t sizes[kGroupWorld];
   uint8_t data[kGroupWorld][kSlotBytes];
 };
@@ -242,6 +243,7 @@ jlong FN(nodeCreate)(JNIEnv*, jclass, jint, jint, jint, jbyteArray, jlong, jlong
 void FN(nodeDestroy)(JNIEnv*, jclass, jlong);
 jlong FN(setBootstrap)(JNIEnv*, jclass, jlong, jobject, jint);
 void FN(releaseBootstrap)(JNIEnv*, jclass, jlong);
+void FN(nodeConnect)(JNIEnv*, jclass, jlong);
 jlongArray FN(poolStats)(JNIEnv*, jclass, jlong);
 jbyteArray FN(commUniqueId)(JNIEnv*, jclass);
 void FN(setSpillDir)(JNIEnv*, jclass, jlong, jstring);
@@ -348,12 +350,14 @@ static jobject direct_buffer(std::vector<uint8_t>& host) {
 
 static int group_main();
 static int large_main();
+static int lifecycle_main();
 
 int main(int argc, char** argv) {
   g_env = &g_fns;
   g_vm = &g_inv;
   if (argc > 1 && std::string(argv[1]) == "group8") return group_main();
   if (argc > 1 && std::string(argv[1]) == "large") return large_main();
+  if (argc > 1 && std::string(argv[1]) == "lifecycle") return lifecycle_main();
   JNIEnv* env = &g_env;
   jclass cls = FindClass(env, "org/apache/spark/shuffle/ucx/gpu/SuxNative");
 
@@ -558,7 +562,14 @@ int main(int argc, char** argv) {
   {
     jobject boot = alloc(_jobject::kBootstrap);
     jlong ctx = 0;
+    // the communicator is joined after the node exists, through the bootstrap (GpuNode's
+    // exchange thread): without one it is a state error
+    THROWS(SUX_ESTATE, FN(nodeConnect)(env, cls, node));
     OK_CALL(ctx = FN(setBootstrap)(env, cls, node, boot, 1));
+    OK_CALL(FN(nodeConnect)(env, cls, node));
+    EXPECT(boot->boot_calls == 1, "nodeConnect all-gathers the unique id once (%d)", boot->boot_calls);
+    OK_CALL(FN(nodeConnect)(env, cls, node));  // idempotent
+    EXPECT(boot->boot_calls == 1, "a connected node does not gather again");
     jintArray t0 = nullptr;
     OK_CALL(t0 = FN(getTuning)(env, cls, node));
     std::vector<jint> f = t0->i;
@@ -581,7 +592,7 @@ int main(int argc, char** argv) {
     const std::vector<uint8_t> want = reduce_want(0, R);
     std::vector<uint8_t> host(want.size());
     OK_CALL(FN(bufferRead)(env, cls, buf, 0, direct_buffer(host), (jlong)want.size(), stream));
-    EXPECT(host == want, "every block after the looped-back exchange");
+    EXPECT(host == want, "every block after the looped-back exchange (one-rank RCCL)");
     for (int m = 0; m < M; ++m) OK_CALL(FN(bufferRelease)(env, cls, buf));
     OK_CALL(FN(unregisterShuffle)(env, cls, node, sid2));
     // a reply of the wrong size (a desynchronised round) fails the exchange, never overflows
@@ -905,5 +916,216 @@ static int large_main() {
     return 1;
   }
   printf("jni large ok: 3.3 GB map outputs written and committed by address, fetched bit-exact\n");
+  return 0;
+}
+
+// ---- lifecycle: the JVM sequence of VERDICT r04 #1, eight executors, three of them writers ----
+// The parent plays the driver's GpuControlEndpoint, the children the executors' GpuNode:
+//   executor: Hello -> Welcome(rank) -> node WITHOUT a communicator (no wait on any peer: the
+//             background join of an executor that may never run a task) -> bootstrap -> Ready;
+//             ranks 0..2 then run map tasks (register the shuffle, write 5 maps each) and report
+//             them; every executor's "exchange thread" takes the driver's relayed messages:
+//             ExchangeWindow -> ensureRegistered + (connect once: rccl only) + exchangeMaps,
+//             ExchangeDone -> exchangeWait; then reduce tasks fetch the owned partitions of
+//             all 15 maps, bit-exact vs the oracle.
+//   driver:   Hello -> groupJoin -> Welcome; relays only to Ready executors and replays the
+//             relayed messages an executor missed when its Ready comes late — the last rank
+//             sends Ready only after the driver relayed the exchange to the others.
+struct LcMsg {
+  int32_t child, kind;  // kind 0 Hello, 1 Ready, 2 MapsDone
+  char id[56];
+};
+struct LcCmd {
+  int32_t kind, a, b;  // kind 0 Welcome(rank, local), 1 Window(first, count), 2 Done
+};
+constexpr int kLcWriters = 3, kLcMapsPer = 5, kLcMaps = kLcWriters * kLcMapsPer;
+
+static int lifecycle_executor(int child, int req_fd, int rep_fd) {
+  JNIEnv* env = &g_env;
+  jclass cls = FindClass(env, "org/apache/spark/shuffle/ucx/gpu/SuxNative");
+  const int W = kGroupWorld, R = 40, S = 100, rpm = 4000, M = kLcMaps, sid = 21;
+  LcMsg hello{child, 0, {}};
+  snprintf(hello.id, sizeof hello.id, "executor-%d", (int)getpid());
+  if (write(req_fd, &hello, sizeof hello) != (ssize_t)sizeof hello) return 10;
+  LcCmd w{};
+  if (read(rep_fd, &w, sizeof w) != (ssize_t)sizeof w || w.kind != 0 || w.a < 0) return 11;
+  const int rank = w.a;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return 12;
+  jlong node = 0;
+  OK_CALL(node = FN(nodeCreate)(env, cls, w.b % ndev, rank, W, nullptr, 1024, 4 << 20, 300, nullptr,
+                                0, JNI_FALSE));
+  jobject boot = alloc(_jobject::kBootstrap);
+  boot->boot_mode = 2;
+  boot->code = rank;
+  jlong ctx = 0, stream = 0, xstream = 0;
+  OK_CALL(ctx = FN(setBootstrap)(env, cls, node, boot, W));
+  OK_CALL(stream = FN(streamCreate)(env, cls, node));
+  OK_CALL(xstream = FN(streamCreate)(env, cls, node));
+  // Ready: the last rank only after the driver relayed the exchange (it gets the backlog)
+  if (rank == W - 1)
+    while (!g_shm->relayed) usleep(1000);
+  LcMsg ready{child, 1, {}};
+  if (write(req_fd, &ready, sizeof ready) != (ssize_t)sizeof ready) return 13;
+  std::vector<uint8_t> bounds((R - 1) * 10);
+  o_range_bounds_uniform(R, 10, bounds.data());
+  o_part opart{SUX_PART_RANGE_BYTES, R, 0, 10, 42, 1, bounds.data()};
+  bool registered = false;
+  void* drec = nullptr;
+  jlong part = 0;
+  if (rank < kLcWriters) {  // a map task: getWriter -> write (the executor components started)
+    OK_CALL(FN(registerShuffle)(env, cls, node, sid, M, R, S));
+    registered = true;
+    OK_CALL(part = FN(partitionerCreate)(env, cls, node, SUX_PART_RANGE_BYTES, R, 0, 10, 42,
+                                         JNI_TRUE, bytes_of(bounds.data(), bounds.size())));
+    std::vector<uint8_t> mine((size_t)kLcMapsPer * rpm * S);
+    o_gen_terasort(47, (uint64_t)rank * kLcMapsPer * rpm, (uint64_t)kLcMapsPer * rpm, mine.data());
+    if (hipMalloc(&drec, mine.size()) != hipSuccess ||
+        hipMemcpy(drec, mine.data(), mine.size(), hipMemcpyHostToDevice) != hipSuccess)
+      return 14;
+    OK_CALL(FN(writeMapOutputs)(env, cls, node, sid, rank * kLcMapsPer, part,
+                                (jlong)(intptr_t)drec, rpm, (jlong)kLcMapsPer * rpm, stream));
+    OK_CALL(FN(waitMapOutputs)(env, cls, node, sid));
+    LcMsg done{child, 2, {}};
+    if (write(req_fd, &done, sizeof done) != (ssize_t)sizeof done) return 15;
+  }
+  // the exchange thread: the driver's relayed messages, in order
+  int windows = 0;
+  for (;;) {
+    LcCmd c{};
+    if (read(rep_fd, &c, sizeof c) != (ssize_t)sizeof c) return 16;
+    if (c.kind == 1) {
+      if (!registered) {  // an executor that ran no task learns the shuffle from the window
+        OK_CALL(FN(registerShuffle)(env, cls, node, sid, M, R, S));
+        registered = true;
+      }
+      OK_CALL(FN(exchangeMaps)(env, cls, node, sid, c.a, c.b, xstream));
+      ++windows;
+    } else if (c.kind == 2) {
+      OK_CALL(FN(exchangeWait)(env, cls, node, sid));
+      break;
+    }
+  }
+  jintArray own = nullptr;
+  OK_CALL(own = FN(ownedPartitions)(env, cls, node, sid, rank));
+  const int lo = own->i[0], hi = own->i[1];
+  std::vector<jint> tri;
+  for (int m = 0; m < M; ++m) tri.insert(tri.end(), {m, lo, hi});
+  jlongArray sizes = NewLongArray(env, M);
+  jlong buf = 0;
+  OK_CALL(buf = FN(fetchBlocks)(env, cls, node, sid, ints_of(tri), sizes, stream));
+  std::vector<uint8_t> want, recs((size_t)rpm * S), data((size_t)rpm * S), be(8 * (R + 1));
+  std::vector<int64_t> len(R), idx(R + 1);
+  for (int m = 0; m < M; ++m) {
+    o_gen_terasort(47, (uint64_t)m * rpm, rpm, recs.data());
+    o_write_map(&opart, recs.data(), rpm, S, data.data(), len.data(), idx.data(), be.data());
+    EXPECT(sizes->l[m] == idx[hi] - idx[lo], "rank %d map %d size", rank, m);
+    want.insert(want.end(), data.begin() + idx[lo], data.begin() + idx[hi]);
+  }
+  std::vector<uint8_t> got(want.size() + 1);
+  if (!want.empty())
+    OK_CALL(FN(bufferRead)(env, cls, buf, 0, direct_buffer(got), (jlong)want.size(), stream));
+  EXPECT(std::memcmp(got.data(), want.data(), want.size()) == 0,
+         "rank %d: owned partitions [%d, %d) of all %d maps", rank, lo, hi, M);
+  for (int m = 0; m < M; ++m) OK_CALL(FN(bufferRelease)(env, cls, buf));
+  OK_CALL(FN(unregisterShuffle)(env, cls, node, sid));
+  if (part) OK_CALL(FN(partitionerDestroy)(env, cls, part));
+  OK_CALL(FN(streamDestroy)(env, cls, node, stream));
+  OK_CALL(FN(streamDestroy)(env, cls, node, xstream));
+  OK_CALL(FN(nodeDestroy)(env, cls, node));
+  FN(releaseBootstrap)(env, cls, ctx);
+  if (drec) (void)hipFree(drec);
+  if (failures) return 1;
+  printf("lifecycle rank %d (%s, %d window): %zu owned bytes of %d maps ok\n", rank,
+         rank < kLcWriters ? "writer" : "no task", windows, want.size(), M);
+  return 0;
+}
+
+static int lifecycle_main() {
+  JNIEnv* env = &g_env;
+  jclass cls = FindClass(env, "org/apache/spark/shuffle/ucx/gpu/SuxNative");
+  g_shm = static_cast<GroupShm*>(mmap(nullptr, sizeof(GroupShm), PROT_READ | PROT_WRITE,
+                                      MAP_SHARED | MAP_ANONYMOUS, -1, 0));
+  if (g_shm == MAP_FAILED) return 2;
+  g_shm->relayed = 0;
+  pthread_barrierattr_t ba;
+  pthread_barrierattr_init(&ba);
+  pthread_barrierattr_setpshared(&ba, PTHREAD_PROCESS_SHARED);
+  pthread_barrier_init(&g_shm->bar, &ba, kGroupWorld);
+  int req[2];
+  if (pipe(req) != 0) return 2;
+  int rep[kGroupWorld][2];
+  std::vector<pid_t> pids;
+  for (int c = 0; c < kGroupWorld; ++c) {
+    if (pipe(rep[c]) != 0) return 2;
+    const pid_t pid = fork();
+    if (pid == 0) {
+      close(req[0]);
+      fflush(stdout);
+      const int rc = lifecycle_executor(c, req[1], rep[c][0]);
+      fflush(stdout);
+      fflush(stderr);
+      _exit(rc);
+    }
+    pids.push_back(pid);
+  }
+  close(req[1]);
+  // the driver's endpoint (no HIP call in this process)
+  jlong group = 0;
+  OK_CALL(group = FN(groupCreate)(env, cls, kGroupWorld));
+  std::vector<bool> ready(kGroupWorld, false);
+  std::vector<int> rank_of(kGroupWorld, -1);
+  std::vector<LcCmd> backlog;
+  int readies = 0, writers_done = 0, late_replays = 0;
+  auto relay = [&](const LcCmd& c) {
+    backlog.push_back(c);
+    for (int k = 0; k < kGroupWorld; ++k)
+      if (ready[k] && write(rep[k][1], &c, sizeof c) != (ssize_t)sizeof c) ++failures;
+  };
+  while (readies < kGroupWorld) {
+    LcMsg m{};
+    pollfd pf{req[0], POLLIN, 0};
+    if (poll(&pf, 1, 120000) != 1 || read(req[0], &m, sizeof m) != (ssize_t)sizeof m) {
+      fprintf(stderr, "FAIL: the driver heard nothing for 120 s (%d ready)\n", readies);
+      ++failures;
+      break;
+    }
+    if (m.kind == 0) {  // Hello -> Welcome at once: no executor waits for another to start
+      jintArray r = nullptr;
+      OK_CALL(r = FN(groupJoin)(env, cls, group, NewStringUTF(env, m.id), NewStringUTF(env, "host0")));
+      rank_of[m.child] = r->i[0];
+      LcCmd wel{0, r->i[0], r->i[1]};
+      if (write(rep[m.child][1], &wel, sizeof wel) != (ssize_t)sizeof wel) ++failures;
+    } else if (m.kind == 1) {  // Ready: replay what it missed, then it gets every new message
+      for (const LcCmd& c : backlog)
+        if (write(rep[m.child][1], &c, sizeof c) != (ssize_t)sizeof c) ++failures;
+      late_replays += !backlog.empty();
+      ready[m.child] = true;
+      ++readies;
+    } else if (m.kind == 2 && ++writers_done == kLcWriters) {
+      // the map stage completed (GpuExchangeCoordinator): one window of every map + completion
+      relay(LcCmd{1, 0, kLcMaps});
+      relay(LcCmd{2, 0, 0});
+      g_shm->relayed = 1;
+    }
+  }
+  int bad = 0;
+  for (int c = 0; c < kGroupWorld; ++c) {
+    int st = 0;
+    waitpid(pids[c], &st, 0);
+    if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) {
+      fprintf(stderr, "FAIL: executor %d (rank %d) exited with %d\n", c, rank_of[c],
+              WIFEXITED(st) ? WEXITSTATUS(st) : -WTERMSIG(st));
+      ++bad;
+    }
+  }
+  OK_CALL(FN(groupDestroy)(env, cls, group));
+  EXPECT(late_replays >= 1, "the last executor got the relayed exchange as a replay (%d)",
+         late_replays);
+  if (failures || bad) {
+    fprintf(stderr, "%d failure(s), %d executor(s) failed\n", failures, bad);
+    return 1;
+  }
+  printf("jni lifecycle ok: 8 executors joined without tasks, 3 wrote maps, all exchanged\n");
   return 0;
 }

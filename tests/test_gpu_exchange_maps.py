@@ -65,6 +65,42 @@ def _check_all_blocks(node, sid, opart, M, rpm, R, parts=None):
     assert pos == got.size
 
 
+def test_node_connect_joins_rccl_through_the_bootstrap():
+    """a node starts without a communicator (no group-wide wait at start) and
+    joins RCCL later with sux_node_connect — rank 0's unique id through the node's bootstrap, then
+    ncclCommInitRank — as the JVM's exchange thread does before the first exchange window.  The
+    exchange then runs through RCCL (loopback): every block arrives byte-exact."""
+    node = Node(device=0, rank=0, world_size=1)
+    try:
+        tags = []
+        node.set_bootstrap(lambda b: (tags.append(len(b)), [b])[1])
+        node.connect()
+        node.connect()  # idempotent: the second call finds the communicator
+        assert tags == [128], tags  # one all-gather of the 128-byte unique id
+        node.set_tuning(exchange_self=1)
+        R, M, rpm = 40, 5, 20000
+        opart, part = _terasort(node, R)
+        node.register_shuffle(3, M, R, 100)
+        _write_windows(node, 3, part, M, rpm, 2, 2)
+        addrs, _ = node.resolve_blocks(3, [(m, p) for m in range(M) for p in (0, R - 1)])
+        assert len(set(addrs.tolist())) > 1  # served from the receive buffers
+        _check_all_blocks(node, 3, opart, M, rpm, R)
+        node.unregister_shuffle(3)
+        part.close()
+    finally:
+        node.close()
+
+
+def test_node_connect_without_a_bootstrap_is_a_state_error():
+    node = Node(device=0, rank=0, world_size=1)
+    try:
+        with pytest.raises(N.SuxError) as e:
+            node.connect()
+        assert e.value.code == N.SUX_ESTATE
+    finally:
+        node.close()
+
+
 @pytest.mark.parametrize("windows,batch", [(1, 4), (3, 2), (2, 1)])
 def test_rccl_loopback_exchange_maps(windows, batch):
     """One-rank RCCL communicator + loopback: ncclAllToAllv rounds carry every block."""

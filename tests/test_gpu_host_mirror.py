@@ -57,6 +57,20 @@ def test_jni_eight_identical_executors_form_a_group():
     assert r.stdout.count("owned bytes of 16 maps ok") == 8
 
 
+def test_jni_group_lifecycle_three_writers_of_eight():
+    """the JVM's start-up sequence through the binding — every executor joins
+    without a task (Hello -> rank -> node without a communicator -> Ready; no executor waits for
+    another to start), only 3 of the 8 run map tasks, the driver relays the exchange to the Ready
+    executors and replays it to the one whose Ready comes late, and all 8 exchange and fetch
+    their owned partitions of the 15 maps bit-exact (tests/jni/jni_harness.cpp lifecycle)."""
+    assert os.path.exists(JNI), "build it first: make -C tests/jni"
+    r = subprocess.run([JNI, "lifecycle"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "jni lifecycle ok" in r.stdout
+    assert r.stdout.count("owned bytes of 15 maps ok") == 8
+    assert r.stdout.count("(writer, 1 window)") == 3 and r.stdout.count("(no task, 1 window)") == 5
+
+
 def test_jni_map_outputs_past_2_gib():
     """a 3.3 GB map written from a raw host address (the writer's native staging)
     and a 3.3 GB data file committed by address, plus a file committed by path (mapped natively),
