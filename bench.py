@@ -817,51 +817,70 @@ def rooflines(node, kt, elapsed: float, steps: int, n: int, rs: int, R: int, map
     return roof, roof_map
 
 
-def xgmi_probe(node, world: int, rank: int, dev, nbytes: int = 256 << 20, reps: int = 5) -> dict:
-    """Measured peer-read peak (SURVEY §5 calls 153 GB/s per xGMI link "an
-    assumption to re-measure on the box"): every rank exports one nbytes-per-peer buffer over HIP
-    IPC, maps every peer's, and then all ranks at once pull their share from every source with the
-    library's own one-sided pull kernel (sux_pull_group over a one-map, R = world group: rank h
-    owns partition h, nbytes from each source) — the whole node's xGMI fabric loaded the way the
-    exchange loads it.  Returns the remote bytes per rank per second (the off-GPU share: the own
-    source is a local copy and is left out of the bytes, as in roofline_exchange)."""
+def xgmi_probe(node, world: int, rank: int, dev, nbytes: int, transport: str,
+               reps: int = 5) -> dict:
+    """Measured exchange peak (SURVEY §5 calls 153 GB/s per xGMI link "an
+    assumption to re-measure on the box"): every rank sends nbytes to every peer at once, through
+    the transport the run's exchange uses, with no map side beside it —
+    - rccl: the library's own all-to-all (sux_exchange_group over a one-map, R = world group:
+      rank h owns partition h, nbytes from each source; grouped ncclSend/ncclRecv pieces);
+    - ipc: every rank pulls its share from every peer's IPC-mapped buffer (sux_pull_group).
+    Returns the remote bytes per rank per second (the own share is a local copy and is left out
+    of the bytes, as in roofline_exchange)."""
     R = world
+
+    def sync_ranks():
+        if dist.is_initialized():
+            dist.barrier()
     send = torch.empty(world * nbytes, dtype=torch.uint8, device=dev)
     send.fill_(rank & 255)
     recv = torch.empty(world * nbytes, dtype=torch.uint8, device=dev)
     rb = torch.zeros(1, dtype=torch.int64, device=dev)
-    one = torch.arange(R + 1, dtype=torch.int64, device=dev) * nbytes
-    gathered = one.repeat(world)
-    hs = [None] * world
-    dist.all_gather_object(hs, node.ipc_handle(send))
-    ptrs = [send.data_ptr() if g == rank else node.ipc_open(hs[g]) for g in range(world)]
-    srcs = torch.tensor(ptrs, dtype=torch.int64, device=dev)
+    index = torch.arange(R + 1, dtype=torch.int64, device=dev) * nbytes
+    gathered = index.repeat(world)
     st = torch.cuda.Stream(dev)
+    st.wait_stream(torch.cuda.current_stream(dev))
+    torch.cuda.synchronize(dev)
+    ptrs = []
+    if transport == "rccl":
+        def once():
+            node.exchange_group(send, index, 1, R, gathered, recv, stream=st)
+    else:
+        hs = [None] * world
+        dist.all_gather_object(hs, node.ipc_handle(send))
+        ptrs = [send.data_ptr() if g == rank else node.ipc_open(hs[g]) for g in range(world)]
+        srcs = torch.tensor(ptrs, dtype=torch.int64, device=dev)
+
+        def once():
+            node.pull_group(world, rank, srcs, gathered, 1, R, recv, rb, stream=st)
+    sync_ranks()  # every rank's buffer is filled (and mapped) before anyone reads it
     try:
         for _ in range(2):
-            node.pull_group(world, rank, srcs, gathered, 1, R, recv, rb, stream=st)
+            once()
         st.synchronize()
-        dist.barrier()
+        sync_ranks()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
         for _ in range(reps):
-            node.pull_group(world, rank, srcs, gathered, 1, R, recv, rb, stream=st)
+            once()
         e1.record(st)
         st.synchronize()
         ms = e0.elapsed_time(e1) / reps
-        ok = int(rb.item()) == world * nbytes and all(
-            int(recv[g * nbytes]) == (g & 255) and int(recv[(g + 1) * nbytes - 1]) == (g & 255)
-            for g in range(world))
-        dist.barrier()  # every rank is done reading before any mapping goes away
+        ok = all(int(recv[g * nbytes]) == (g & 255) and int(recv[(g + 1) * nbytes - 1]) == (g & 255)
+                 for g in range(world))
+        sync_ranks()  # every rank is done reading before any mapping goes away
     finally:
         for g, p in enumerate(ptrs):
             if g != rank:
                 node.ipc_close(p)
-    remote = (world - 1) * nbytes
-    return {"GB/s": round(remote / (ms / 1e3) / 1e9, 1), "bytes_per_source": nbytes,
-            "ms": round(ms, 3), "reps": reps, "ok": ok,
-            "what": "every rank pulls nbytes from every peer's IPC-mapped buffer at once "
-                    "(sux_pull_group); GB/s = remote bytes per rank / time"}
+    remote = max(world - 1, 1) * nbytes  # world 1 (--rccl-at-one): the self copy, flagged
+    return {"GB/s": round(remote / (ms / 1e3) / 1e9, 1), "bytes_per_peer": nbytes,
+            "ms": round(ms, 3), "reps": reps, "ok": ok, "transport": transport,
+            "what": ("every rank sends bytes_per_peer to every peer at once, nothing else "
+                     "running: " + ("sux_exchange_group (RCCL grouped send/recv)"
+                                    if transport == "rccl" else
+                                    "sux_pull_group from IPC-mapped peer buffers")
+                     + "; GB/s = remote bytes per rank / time")}
 
 
 def first_mismatch(a: torch.Tensor, b: torch.Tensor, chunk: int = 1 << 28) -> tuple[int, int]:
@@ -1048,8 +1067,9 @@ def main():
                          "of group k (sux_exchange_group_post) beside the all-to-all of k - 1 "
                          "(sux_exchange_group_issue) on a split communicator")
     ap.add_argument("--xgmi-probe-mib", type=int, default=256,
-                    help="N>1: before the run, time every rank pulling this many MiB from every "
-                         "peer at once over IPC (the measured exchange peak; 0: skip)")
+                    help="N>1: before the run, time every rank sending this many MiB to every "
+                         "peer at once through the run's transport (the measured exchange peak; "
+                         "0: skip)")
     ap.add_argument("--c4-steps", type=int, default=3,
                     help="N=1: after the headline, also time BASELINE config C4 (Zipf-skewed "
                          "keys, 100 GB, R=200) for this many steps, self-checked (0: skip)")
@@ -1423,10 +1443,16 @@ def main():
         torch.cuda.synchronize(dev)
 
     xprobe = None
-    if pipelined and world > 1 and args.xgmi_probe_mib > 0:
-        xprobe = xgmi_probe(node, world, rank, dev, args.xgmi_probe_mib << 20)
+    if pipelined and (world > 1 or args.rccl_at_one) and args.xgmi_probe_mib > 0:
+        # IPC imports of large allocations by many processes of one GPU were measured to stall
+        # for minutes (a 2 GB buffer per rank at W = 8, round 5): the one-GPU rehearsal probes
+        # with 16 MiB per peer
+        mib = min(args.xgmi_probe_mib, 16) if rehearse else args.xgmi_probe_mib
+        xprobe = xgmi_probe(node, world, rank, dev, mib << 20, args.transport)
         if rehearse:
             xprobe["one_gpu"] = "every rank on cuda:0: an on-chip copy, not xGMI"
+        elif world == 1:
+            xprobe["one_gpu"] = "--rccl-at-one: the self copy through a one-rank communicator"
         log(f"[rank {rank}] xgmi probe: {xprobe}")
     log(f"[rank {rank}] {args.workload}: {n} records x {rs} B = {n * rs / 1e9:.1f} GB/GPU, "
         f"R={R}, {maps} maps of {rpm}, {groups} launch groups of {gm} maps, world={world}")

@@ -241,7 +241,8 @@ typedef struct sux_tuning {
                                pass B store each record from its registers straight to its
                                sorted place instead of through the LDS stage (measured slower);
                                bit 2: pass A prefetches its next chunk into LDS by DMA
-                               (global_load_lds), one workgroup per CU; -1 or 0 none            */
+                               (global_load_lds), one workgroup per CU; bit 3: 32-partition
+                               buckets, 512-thread pass-B workgroups; -1 or 0 none              */
   int32_t reserved[1];
 } sux_tuning;
 int sux_node_set_tuning(sux_node* node, const sux_tuning* tuning);
@@ -339,6 +340,9 @@ int sux_exchange_group_post(sux_node* node, const int64_t* d_index, int32_t num_
 int sux_exchange_group_issue(sux_node* node, sux_xticket* ticket, const void* d_send,
                              void* d_recv, uint64_t recv_capacity, uint64_t* recv_bytes,
                              void* stream);
+/* A posted ticket that will not be issued (another rank failed, teardown): waits for its
+ * read-back and frees it.  Tickets never outlive their node: sux_node_destroy frees any left. */
+int sux_exchange_group_discard(sux_node* node, sux_xticket* ticket);
 
 /* ---- one-sided exchange over HIP IPC (xGMI peer access) ----------------------------------- *
  * The GET model of UcxShuffleClient (UcxShuffleClient.java:50-127, OnOffsetsFetchCallback.java

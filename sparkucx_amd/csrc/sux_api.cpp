@@ -22,6 +22,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <map>
+#include <set>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -503,6 +504,8 @@ struct sux_node {
   };
   std::mutex export_mu;
   std::map<void*, IpcExport> ipc_exports;
+  // sux_exchange_group_post tickets not yet issued or discarded (freed by sux_node_destroy)
+  std::set<sux_xticket*> tickets;
   sux_allgather_fn boot = nullptr;   // host all-gather of the embedding runtime
   void* boot_ctx = nullptr;
   sux_tuning tuning{};               // all zero = measured defaults (resolve_tuning)
@@ -797,6 +800,7 @@ void drain(sux_node* node, Shuffle& sh, std::unique_lock<std::mutex>& lk) {
 
 }  // namespace
 void export_ipc(sux_node* node, const void* p, uint8_t out[SUX_IPC_DESC_BYTES]);
+void free_ticket(sux_xticket* t);
 namespace {
 
 // Map a peer allocation by its 64-byte IPC handle.  The HIP runtime keys the mappings it hands
@@ -1286,7 +1290,7 @@ int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
     require(in(t->gather_kernel, {1, 2, 3}), SUX_EINVAL, "gather_kernel must be 1, 2 or 3");
     require(t->split_cus == -1 || (t->split_cus >= 0 && t->split_cus <= 224 && t->split_cus % 32 == 0),
             SUX_EINVAL, "split_cus must be -1, 0 or a multiple of 32 up to 224");
-    require(t->msd_direct >= -1 && t->msd_direct <= 7, SUX_EINVAL, "msd_direct must be -1 .. 7");
+    require(t->msd_direct >= -1 && t->msd_direct <= 15, SUX_EINVAL, "msd_direct must be -1 .. 15");
     for (int32_t r : t->reserved) require(r == 0, SUX_EINVAL, "reserved tuning fields must be 0");
     require(node, SUX_EINVAL, "NULL node");
     std::lock_guard<std::mutex> lk(node->mu);
@@ -1332,6 +1336,8 @@ int sux_node_destroy(sux_node* node) {
       for (auto& kv : node->shuffles) drain(node, *kv.second, lk);
     }
     (void)hipDeviceSynchronize();
+    for (sux_xticket* t : node->tickets) free_ticket(t);  // posted, never issued: leases return
+    node->tickets.clear();
     for (int i = 0; i < 2; ++i) {
       if (node->pipe[i]) (void)hipStreamDestroy(node->pipe[i]);
       node->pool->put(node->pipe_ws[i]);
@@ -2170,6 +2176,10 @@ struct sux_xticket {
   std::unique_ptr<HostLease> host;  // the gathered index tables, read back asynchronously
   Event done;                       // after the read-back
 };
+void free_ticket(sux_xticket* t) {
+  (void)hipEventSynchronize(t->done.e);
+  delete t;
+}
 extern "C" {
 
 int sux_exchange_group_post(sux_node* node, const int64_t* d_index, int32_t M, int32_t R,
@@ -2199,7 +2209,24 @@ int sux_exchange_group_post(sux_node* node, const int64_t* d_index, int32_t M, i
                              hipMemcpyDeviceToHost, s),
               "D2H gathered index");
     hip_check(hipEventRecord(t->done.e, s), "hipEventRecord(gathered index)");
+    std::lock_guard<std::mutex> lk(node->mu);
+    node->tickets.insert(t.get());
     *out = t.release();
+  });
+}
+
+int sux_exchange_group_discard(sux_node* node, sux_xticket* ticket) {
+  std::unique_ptr<sux_xticket> t(ticket);
+  return guard([&] {
+    require(node, SUX_EINVAL, "NULL node");
+    if (!t) return;
+    {
+      std::lock_guard<std::mutex> lk(node->mu);
+      node->tickets.erase(t.get());
+    }
+    node->bind();
+    // the read-back into the pinned lease must land before the lease goes back to the pool
+    (void)hipEventSynchronize(t->done.e);
   });
 }
 
@@ -2207,6 +2234,10 @@ int sux_exchange_group_issue(sux_node* node, sux_xticket* ticket, const void* d_
                              void* d_recv, uint64_t recv_capacity, uint64_t* recv_bytes,
                              void* stream) {
   std::unique_ptr<sux_xticket> t(ticket);  // consumed, whatever happens
+  if (node && ticket) {
+    std::lock_guard<std::mutex> lk(node->mu);
+    node->tickets.erase(ticket);
+  }
   return guard([&] {
     require(node && t, SUX_EINVAL, "NULL argument");
     const int W = node->conf.world_size, rank = node->conf.rank;
@@ -2810,6 +2841,18 @@ void export_ipc(sux_node* node, const void* p, uint8_t out[SUX_IPC_DESC_BYTES]) 
   std::lock_guard<std::mutex> lk(node->export_mu);
   auto it = node->ipc_exports.find(base);
   if (it == node->ipc_exports.end() || it->second.id != id || it->second.size != size) {
+    // a new export: first drop the entries of allocations that were freed since (their base no
+    // longer resolves to the same buffer id), so the cache holds live allocations only (ADVICE
+    // r04: it used to keep one entry per base for the node's whole life)
+    for (auto e = node->ipc_exports.begin(); e != node->ipc_exports.end();) {
+      unsigned long long eid = 0;
+      const bool live = e->first != base &&
+                        hipPointerGetAttribute(&eid, HIP_POINTER_ATTRIBUTE_BUFFER_ID,
+                                               e->first) == hipSuccess &&
+                        eid == e->second.id;
+      e = live ? std::next(e) : node->ipc_exports.erase(e);
+    }
+    (void)hipGetLastError();  // a freed base's failed query must not linger as the last error
     hipIpcMemHandle_t h;
     hip_check(hipIpcGetMemHandle(&h, base), "hipIpcGetMemHandle");
     sux_node::IpcExport e{id, size, {}};
@@ -3882,7 +3925,7 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
     sux::SortPlanDev* plan = reinterpret_cast<sux::SortPlanDev*>(ws + plan_off);
     hip_check(sux::launch_sort_pairs(static_cast<const uint8_t*>(d_in), n, record_size, key_kind,
                                      key_offset, key_len, d_seg, nseg, sbytes, a,
-                                     ws + P1.span_off, inline_rec, s, bits, tb, plan),
+                                     ws + P1.span_off, inline_rec, s, bits, tb, plan, chunked),
               "sort pairs + plan");
     int64_t* index1 = reinterpret_cast<int64_t*>(ws + P1.index_off);
     sux::PartDev pd1 = pd;

@@ -230,12 +230,14 @@ struct SortPlanDev;
 hipError_t launch_sort_pairs(const uint8_t* in, uint64_t n, uint32_t rs, int kind, int key_offset,
                              int key_len, const int64_t* seg, int nseg, int sbytes, void* pairs,
                              void* span_ws, bool inline_rec, hipStream_t s, int bits = 0,
-                             int tb = 0, SortPlanDev* plan = nullptr);
+                             int tb = 0, SortPlanDev* plan = nullptr, bool ranged = false);
 hipError_t launch_unpair_records(const void* pairs, uint64_t n, uint32_t rs, int kind,
                                  int key_offset, int key_len, int sbytes, void* out, hipStream_t s);
 // span_ws: 8 u32 (AND of key words 0..2, OR of key words 0..2) + kSortSpanBlocks x 8 u32 partials
 constexpr uint32_t kSortSpanBlocks = 2048;
-constexpr uint64_t kSortSpanBytes = 4ull * 8 * (kSortSpanBlocks + 1);
+// header (8 u32) + per block 16 u32: AND of key words 0..2, OR of them, 2 spare, then the
+// smallest and the largest pair as big-endian 128-bit values (4 u32 each)
+constexpr uint64_t kSortSpanBytes = 4ull * (8 + 16ull * kSortSpanBlocks);
 hipError_t launch_gather_records_sel(const void* in, const void* pairs_a, const void* pairs_b,
                                      const uint32_t* sel, uint64_t n, uint32_t rs, void* out,
                                      hipStream_t s, bool gather16 = true);
@@ -267,7 +269,10 @@ struct SortPlanDev {
   uint32_t pad;
   uint32_t final_b;  // 1: the sorted pairs end in buffer b, 0: in buffer a
   int32_t kbits;     // key bits (with the segment id): the top kbits of the big-endian pair
-  uint64_t maxb;     // unused (round 3: the plan decides msd_ok / final_b, no bucket sweep)
+  uint64_t top_base; // the top digit is ((key >> top_lo) - top_base) & (2^tb - 1): with the key
+                     // range (min, max) of a ranged plan, top_lo is the lowest shift whose
+                     // aligned blocks [min, max] spans fit 2^tb buckets and top_base = min >>
+                     // top_lo, so every bucket is used; 0 = the bits [top_lo, top_lo + tb)
   SortDigits dg;     // the LDS sort's digits: 8-bit, below top_lo, only those that vary
 };
 constexpr uint64_t kSortPlanBytes = 256;

@@ -404,6 +404,9 @@ constexpr uint32_t kM16Chunk = 4096;      // pass A records per chunk (the run t
 // R = 10 000: 105 records at LO 4, 1677 at LO 8 — the 2^20-record maps' segment at LO 4).
 constexpr uint32_t kM16Lo = 4;
 constexpr uint32_t kM16LoShort = 8;
+// msd_direct bit 3: 32-partition buckets (runs of ~13 records = ~210 B per (chunk, bucket) at
+// R = 10 000 instead of ~6.5 = ~105 B) with 512-thread, 4096-record pass-B workgroups
+constexpr uint32_t kM16LoWide = 5;
 constexpr uint32_t kM16MaxChunks = 512;   // chunks per map pass B's run table holds (2 Mi records)
 constexpr uint32_t kM16MaxChunksShort = 64;  // LO 8: maps of <= 256 Ki records
 
@@ -971,9 +974,9 @@ static uint32_t msd16_lo(const PartDev& pd, const MapGroup& g, const LayoutDesc&
     return 0;
   const uint64_t cpm = (g.records_per_map + kM16Chunk - 1) / kM16Chunk;
   if (cpm < 1 || ws.tmp_bytes < g.num_records * 16) return 0;
-  for (const uint32_t lo : {kM16Lo, kM16LoShort}) {
+  for (const uint32_t lo : {(tn.msd_direct & 8) ? kM16LoWide : kM16Lo, kM16LoShort}) {
     const uint64_t nbk = ((uint64_t)pd.R + (1u << lo) - 1) >> lo;
-    if (cpm > (lo == kM16Lo ? kM16MaxChunks : kM16MaxChunksShort)) continue;
+    if (cpm > (lo == kM16LoShort ? kM16MaxChunksShort : kM16MaxChunks)) continue;
     // by default only when a (map, bucket) segment holds >= 1024 records on average: a segment
     // costs ~6 us of run table, search and barriers whatever its size (64 Ki-record maps at
     // R = 10 000 and 16 partitions per bucket: 105-record segments, 194 GB/s vs 553 for the
@@ -1060,17 +1063,20 @@ hipError_t launch_msd16(const PartDev& pd, const MapGroup& g, uint8_t* d_out, in
   timer_note(timer, kScatter, "k_msd16b");
   timer_begin(timer, kScatter, s);
   // pass B's 256-thread workgroups are half the size of pass A's: twice as many per CU
-  const dim3 gb(std::min<uint32_t>(g.num_maps * nbk, ncu * 2 * wpc));
+  const dim3 gb(std::min<uint32_t>(g.num_maps * nbk, ncu * (LO == kM16LoWide ? 1 : 2) * wpc));
   using MB4 = M16b<NWB, PTB, kM16Lo, kM16MaxChunks>;
+  using MB5 = M16b<8, PTB, kM16LoWide, kM16MaxChunks>;
+  static_assert(2 * MB5::lds_bytes() <= 160 * 1024, "pass B (32-partition buckets): two per CU");
   using MB8 = M16b<NWB, PTB, kM16LoShort, kM16MaxChunksShort>;
   static_assert(4 * MB4::lds_bytes() <= 160 * 1024, "pass B: four workgroups per CU");
   static_assert(4 * MB8::lds_bytes() <= 160 * 1024, "pass B (256-partition buckets): four per CU");
   static_assert(2 * M16a<NWA, 10>::lds_bytes() <= 160 * 1024, "pass A: two workgroups per CU");
 #define SUX_M16B_D(KW, LOV, MCV, D)                                                                \
   do {                                                                                             \
-    constexpr size_t ldsb = M16b<NWB, PTB, LOV, MCV>::lds_bytes();                                 \
-    allow_lds(reinterpret_cast<const void*>(&k_msd16b<KW, NWB, PTB, LOV, MCV, D>), ldsb);         \
-    hipLaunchKernelGGL((k_msd16b<KW, NWB, PTB, LOV, MCV, D>), gb, dim3(NWB * kWave), ldsb, s, pd, \
+    constexpr uint32_t nwb = LOV == kM16LoWide ? 8 : NWB;                                          \
+    constexpr size_t ldsb = M16b<nwb, PTB, LOV, MCV>::lds_bytes();                                 \
+    allow_lds(reinterpret_cast<const void*>(&k_msd16b<KW, nwb, PTB, LOV, MCV, D>), ldsb);         \
+    hipLaunchKernelGGL((k_msd16b<KW, nwb, PTB, LOV, MCV, D>), gb, dim3(nwb * kWave), ldsb, s, pd, \
                        g, cpm, nbk, offs, segbase, tmp, d_out, d_index, d_index_be);               \
   } while (0)
 #define SUX_M16B(KW, LOV, MCV)                               \
@@ -1086,6 +1092,7 @@ hipError_t launch_msd16(const PartDev& pd, const MapGroup& g, uint8_t* d_out, in
     else SUX_M16B(4, LOV, MCV);               \
   } while (0)
   if (LO == kM16LoShort) SUX_M16BK(kM16LoShort, kM16MaxChunksShort);
+  else if (LO == kM16LoWide) SUX_M16BK(kM16LoWide, kM16MaxChunks);
   else SUX_M16BK(kM16Lo, kM16MaxChunks);
 #undef SUX_M16BK
 #undef SUX_M16B

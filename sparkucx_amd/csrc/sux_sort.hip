@@ -138,10 +138,30 @@ __global__ __launch_bounds__(256) void k_unpair_records(const u32x4* __restrict_
   if (rs > 12) dst[3] = (uint32_t)(rec >> 96);
 }
 
+// The pair as one big-endian 128-bit value (the order key in its top bits).
+__device__ __forceinline__ u128 pair_be128(const u32x4& w) {
+  return ((u128)__builtin_bswap32(w[0]) << 96) | ((u128)__builtin_bswap32(w[1]) << 64) |
+         ((u128)__builtin_bswap32(w[2]) << 32) | (u128)__builtin_bswap32(w[3]);
+}
+__device__ __forceinline__ u128 shfl_xor128(u128 v, int m) {
+  const unsigned long long lo = __shfl_xor((unsigned long long)(uint64_t)v, m);
+  const unsigned long long hi = __shfl_xor((unsigned long long)(uint64_t)(v >> 64), m);
+  return ((u128)hi << 64) | (u128)lo;
+}
+__device__ __forceinline__ void put128(uint32_t* d, u128 v) {
+  for (int k = 0; k < 4; ++k) d[k] = (uint32_t)(v >> (96 - 32 * k));
+}
+__device__ __forceinline__ u128 get128(const uint32_t* d) {
+  return ((u128)d[0] << 96) | ((u128)d[1] << 64) | ((u128)d[2] << 32) | (u128)d[3];
+}
+
 // Grid-stride pair build that also records which key bits vary: each workgroup writes the AND and
-// the OR of its pairs' key words to part[block][0..5]; k_span_reduce folds them.  A digit whose
-// bits are equal in AND and OR is the same for every record, so its pass is the identity and the
-// host skips it (Spark long / int keys of small magnitude leave the top digits constant).
+// the OR of its pairs' key words to part[block][0..5] and its smallest and largest pair to
+// part[block][8..15]; k_span_reduce folds them.  A digit whose bits are equal in AND and OR is the
+// same for every record, so its pass is the identity and the host skips it (Spark long / int keys
+// of small magnitude leave the top digits constant); the key range places the top digit's
+// buckets over [min, max] only (a reducer's keys are one range partition's: round 4's bit span
+// left a third of the 4096 buckets of such a partition empty and the rest ~1.5x fuller).
 __global__ __launch_bounds__(256) void k_sort_pairs(const uint8_t* __restrict__ in, uint64_t n,
                                                     uint32_t rs, int kind, int key_offset,
                                                     int key_len, const int64_t* __restrict__ seg,
@@ -149,6 +169,7 @@ __global__ __launch_bounds__(256) void k_sort_pairs(const uint8_t* __restrict__ 
                                                     u32x4* __restrict__ pairs,
                                                     uint32_t* __restrict__ part, int inline_rec) {
   uint32_t a0 = ~0u, a1 = ~0u, a2 = ~0u, o0 = 0, o1 = 0, o2 = 0;
+  u128 mn = ~(u128)0, mx = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * 256) {
     u32x4 p;
@@ -172,48 +193,81 @@ __global__ __launch_bounds__(256) void k_sort_pairs(const uint8_t* __restrict__ 
     pairs[i] = p;
     a0 &= p[0]; a1 &= p[1]; a2 &= p[2];
     o0 |= p[0]; o1 |= p[1]; o2 |= p[2];
+    const u128 v = pair_be128(p);
+    mn = v < mn ? v : mn;
+    mx = v > mx ? v : mx;
   }
   for (int m = 32; m >= 1; m >>= 1) {
     a0 &= __shfl_xor(a0, m); a1 &= __shfl_xor(a1, m); a2 &= __shfl_xor(a2, m);
     o0 |= __shfl_xor(o0, m); o1 |= __shfl_xor(o1, m); o2 |= __shfl_xor(o2, m);
+    const u128 vn = shfl_xor128(mn, m), vx = shfl_xor128(mx, m);
+    mn = vn < mn ? vn : mn;
+    mx = vx > mx ? vx : mx;
   }
   __shared__ uint32_t red[4][6];
+  __shared__ u128 rmm[4][2];
   const int wv = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
     red[wv][0] = a0; red[wv][1] = a1; red[wv][2] = a2;
     red[wv][3] = o0; red[wv][4] = o1; red[wv][5] = o2;
+    rmm[wv][0] = mn;
+    rmm[wv][1] = mx;
   }
   __syncthreads();
   if (threadIdx.x < 6) {
     uint32_t v = red[0][threadIdx.x];
     for (int w = 1; w < 4; ++w)
       v = threadIdx.x < 3 ? (v & red[w][threadIdx.x]) : (v | red[w][threadIdx.x]);
-    part[blockIdx.x * 8 + threadIdx.x] = v;
+    part[blockIdx.x * 16 + threadIdx.x] = v;
+  } else if (threadIdx.x == 8) {
+    u128 a = rmm[0][0], b = rmm[0][1];
+    for (int w = 1; w < 4; ++w) {
+      a = rmm[w][0] < a ? rmm[w][0] : a;
+      b = rmm[w][1] > b ? rmm[w][1] : b;
+    }
+    put128(part + blockIdx.x * 16 + 8, a);
+    put128(part + blockIdx.x * 16 + 12, b);
   }
 }
 
-__device__ void make_sort_plan(const uint32_t* span, int bits, int tb, SortPlanDev* plan);
+__device__ void make_sort_plan(const uint32_t* span, int bits, int tb, SortPlanDev* plan,
+                               const u128* range);
 
 // The key span; with `plan`, thread 0 then plans the sort from it (the device-planned MSD path:
-// one launch fewer than a separate planning kernel).
+// one launch fewer than a separate planning kernel); `ranged` plans the top digit over the key
+// range [min, max] instead of the varying bits.
 __global__ __launch_bounds__(256) void k_span_reduce(const uint32_t* __restrict__ part,
                                                      uint32_t blocks, uint32_t* __restrict__ span,
-                                                     int bits, int tb, SortPlanDev* __restrict__ plan) {
+                                                     int bits, int tb, SortPlanDev* __restrict__ plan,
+                                                     int ranged) {
   __shared__ uint32_t red[256][6];
+  __shared__ u128 rmm[256][2];
   uint32_t v[6] = {~0u, ~0u, ~0u, 0, 0, 0};
-  for (uint32_t b = threadIdx.x; b < blocks; b += 256)
-    for (int k = 0; k < 6; ++k) v[k] = k < 3 ? (v[k] & part[b * 8 + k]) : (v[k] | part[b * 8 + k]);
+  u128 mn = ~(u128)0, mx = 0;
+  for (uint32_t b = threadIdx.x; b < blocks; b += 256) {
+    for (int k = 0; k < 6; ++k)
+      v[k] = k < 3 ? (v[k] & part[b * 16 + k]) : (v[k] | part[b * 16 + k]);
+    const u128 a = get128(part + b * 16 + 8), c = get128(part + b * 16 + 12);
+    mn = a < mn ? a : mn;
+    mx = c > mx ? c : mx;
+  }
   for (int k = 0; k < 6; ++k) red[threadIdx.x][k] = v[k];
+  rmm[threadIdx.x][0] = mn;
+  rmm[threadIdx.x][1] = mx;
   __syncthreads();
   for (uint32_t h = 128; h >= 1; h >>= 1) {
-    if (threadIdx.x < h)
+    if (threadIdx.x < h) {
       for (int k = 0; k < 6; ++k)
         red[threadIdx.x][k] = k < 3 ? (red[threadIdx.x][k] & red[threadIdx.x + h][k])
                                     : (red[threadIdx.x][k] | red[threadIdx.x + h][k]);
+      const u128 a = rmm[threadIdx.x + h][0], c = rmm[threadIdx.x + h][1];
+      if (a < rmm[threadIdx.x][0]) rmm[threadIdx.x][0] = a;
+      if (c > rmm[threadIdx.x][1]) rmm[threadIdx.x][1] = c;
+    }
     __syncthreads();
   }
   if (threadIdx.x < 6) span[threadIdx.x] = red[0][threadIdx.x];
-  if (plan && threadIdx.x == 0) make_sort_plan(&red[0][0], bits, tb, plan);
+  if (plan && threadIdx.x == 0) make_sort_plan(&red[0][0], bits, tb, plan, ranged ? rmm[0] : nullptr);
 }
 
 // One output dword per thread and step: record j = d / W, dword w of it, read from the record
@@ -281,7 +335,7 @@ __global__ __launch_bounds__(256) void k_gather_records16(const uint8_t* __restr
 hipError_t launch_sort_pairs(const uint8_t* in, uint64_t n, uint32_t rs, int kind, int key_offset,
                              int key_len, const int64_t* seg, int nseg, int sbytes, void* pairs,
                              void* span_ws, bool inline_rec, hipStream_t s, int bits, int tb,
-                             SortPlanDev* plan) {
+                             SortPlanDev* plan, bool ranged) {
   if (n == 0) return hipSuccess;
   const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, kSortSpanBlocks);
   uint32_t* part = static_cast<uint32_t*>(span_ws) + 8;
@@ -291,7 +345,7 @@ hipError_t launch_sort_pairs(const uint8_t* in, uint64_t n, uint32_t rs, int kin
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_span_reduce, dim3(1), dim3(256), 0, s, part, blocks,
-                     static_cast<uint32_t*>(span_ws), bits, tb, plan);
+                     static_cast<uint32_t*>(span_ws), bits, tb, plan, ranged ? 1 : 0);
   return hipGetLastError();
 }
 
@@ -380,6 +434,17 @@ __device__ __forceinline__ uint32_t pair_bits(const u32x4& w, uint32_t sh, uint3
   return (uint32_t)v & (uint32_t)((1ull << nb) - 1);
 }
 
+// The top digit of a pair: ((key >> sh) - base) & (2^nb - 1) — bits [sh, sh + nb) when base is
+// 0; with a ranged plan (base = min >> sh) the bucket of the key's aligned 2^sh block counted from
+// the smallest key's (the difference is exact in 64 bits: it is < 2^nb).
+__device__ __forceinline__ uint32_t top_digit(const u32x4& w, uint32_t sh, uint64_t base,
+                                              uint32_t nb) {
+  const uint64_t hi = ((uint64_t)__builtin_bswap32(w[0]) << 32) | __builtin_bswap32(w[1]);
+  const uint64_t lo = ((uint64_t)__builtin_bswap32(w[2]) << 32) | __builtin_bswap32(w[3]);
+  const uint64_t v = sh >= 64 ? (hi >> (sh - 64)) : ((lo >> sh) | (sh ? (hi << (64 - sh)) : 0));
+  return (uint32_t)(v - base) & (uint32_t)((1ull << nb) - 1);
+}
+
 // ------------------------------------------------------------------------------------------
 // Chunked top pass (round 4; the default when the top digit has <= 12 bits and the pairs fit
 // kTopMaxChunks chunks).  The one-pass top-digit partition (k_hist16 + scans + k_scatter16s)
@@ -414,6 +479,7 @@ __global__ __launch_bounds__(NT, 2 * NT / 256) void k_top_chunks(const u32x4* __
   const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
   const uint64_t lt_mask = (1ull << lane) - 1ull;
   const uint32_t R = 1u << tb, top_lo = (uint32_t)plan->top_lo;
+  const uint64_t top_base = plan->top_base;
   const int passes = tb <= (int)DB ? 1 : 2;
   const uint32_t D = passes == 1 ? (uint32_t)tb : (uint32_t)(tb + 1) / 2;  // <= DB bits a pass
   const uint32_t nch = (uint32_t)((n + CH - 1) / CH);
@@ -430,7 +496,7 @@ __global__ __launch_bounds__(NT, 2 * NT / 256) void k_top_chunks(const u32x4* __
     for (uint32_t j = 0; j < PT; ++j) {  // clamped, unconditional loads
       const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
       const u32x4 p = pairs[c0 + min(e, nc - 1)];
-      if (e < nc) kin[e] = (pair_bits(p, top_lo, (uint32_t)tb) << IDX) | e;
+      if (e < nc) kin[e] = (top_digit(p, top_lo, top_base, (uint32_t)tb) << IDX) | e;
     }
     __syncthreads();
     // 1. LSD passes over (bucket << 12 | position), D bits each: wave-ballot ranks against the
@@ -1088,11 +1154,26 @@ __device__ bool span_varies_dev(const uint32_t* span, int lo, int hi) {
 // The plan from the key span (AND of key words 0..2, then their OR): the highest varying key
 // bit, the top digit (its tb bits end there) and the LDS sort's 8-bit digits below it that vary.
 // One thread (k_span_reduce's thread 0).
-__device__ void make_sort_plan(const uint32_t* span, int bits, int tb, SortPlanDev* plan) {
+__device__ void make_sort_plan(const uint32_t* span, int bits, int tb, SortPlanDev* plan,
+                               const u128* range) {
   int hb = -1;
   for (int b = 127; b >= 128 - bits && hb < 0; --b)
     if (span_varies_dev(span, b, b + 1)) hb = b;
-  const int top_lo = hb >= 0 ? max(hb + 1 - tb, 128 - bits) : 128 - bits;
+  int top_lo = hb >= 0 ? max(hb + 1 - tb, 128 - bits) : 128 - bits;
+  uint64_t top_base = 0;
+  if (range && hb >= 0) {
+    // the lowest shift at which the aligned blocks the keys [min, max] touch number <= 2^tb (the
+    // bit-span shift above always qualifies: every key shares the bits above hb)
+    const u128 mn = range[0], mx = range[1];
+    int sh = 128 - bits;
+    const u128 d = mx - mn;
+    const int dl = 128 - (int)(d >> 64 ? __builtin_clzll((uint64_t)(d >> 64))
+                                       : 64 + ((uint64_t)d ? __builtin_clzll((uint64_t)d) : 64));
+    sh = max(sh, dl - tb);  // below it the span alone needs more than 2^tb blocks
+    while (sh < top_lo && ((mx >> sh) - (mn >> sh)) >= ((u128)1 << tb)) ++sh;
+    top_lo = min(sh, top_lo);
+    top_base = (uint64_t)(mn >> top_lo);
+  }
   // The LDS digits hang down from the top digit — [top_lo - 8, top_lo), [top_lo - 16, top_lo -
   // 8), ... — so the two the bucket sort runs first (and whose ties its insertion sort finishes)
   // hold 16 bits that vary inside a bucket.  Counted up from the key's lowest bit instead, the
@@ -1110,6 +1191,7 @@ __device__ void make_sort_plan(const uint32_t* span, int bits, int tb, SortPlanD
   }
   for (int i = m - 1; i >= 0; --i) dg.push(shs[i]);  // least significant first
   plan->top_lo = top_lo;
+  plan->top_base = top_base;
   plan->hb = hb;
   plan->kbits = bits;
   plan->dg = dg;
@@ -1119,7 +1201,6 @@ __device__ void make_sort_plan(const uint32_t* span, int bits, int tb, SortPlanD
   // pass's b; with every key equal, in a (the input order)
   plan->msd_ok = hb >= 0 ? 1u : 0u;
   plan->final_b = hb < 0 ? 0u : (dg.n ? 0u : 1u);
-  plan->maxb = 0;
 }
 
 template <bool GATHER>

@@ -86,6 +86,7 @@ _SIGS = {
     "sux_node_connect": (C.c_int, [P]),
     "sux_exchange_group_post": (C.c_int, [P, P, I32, I32, P, P, C.POINTER(P)]),
     "sux_exchange_group_issue": (C.c_int, [P, P, P, P, U64, P, P]),
+    "sux_exchange_group_discard": (C.c_int, [P, P]),
     "sux_group_create": (C.c_int, [C.c_int32, C.POINTER(P)]),
     "sux_group_destroy": (C.c_int, [P]),
     "sux_group_join": (C.c_int, [P, C.c_char_p, C.c_char_p, C.POINTER(C.c_int32),

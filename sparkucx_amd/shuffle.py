@@ -366,6 +366,10 @@ class Node:
                 "sux_exchange_group_issue")
         return np.frombuffer(rb, dtype=np.uint64).copy()
 
+    def exchange_group_discard(self, ticket):
+        """A posted ticket that will not be issued: wait for its read-back and free it."""
+        N.check(self.lib.sux_exchange_group_discard(self.h, ticket), "sux_exchange_group_discard")
+
     # ---- one-sided exchange over HIP IPC ----------------------------------------------------
     def ipc_handle(self, t: torch.Tensor) -> bytes:
         """72-byte descriptor: IPC handle of t's allocation + t's offset in it."""

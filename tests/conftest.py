@@ -36,3 +36,22 @@ def tuned(gpu_node):
     yield set_
     gpu_node.set_tuning(**saved)
     gpu_node.check()  # no kernel recorded a failure under the test's tuning
+
+
+@pytest.fixture(autouse=True)
+def no_stale_hip_error(request):
+    """After every GPU test: no HIP error may be left in this thread's last-error slot.  torch
+    checks hipGetLastError() after its own kernel launches, so a stale error left by a library
+    call (RCCL leaves "invalid device ordinal" behind some of its calls) would fail whatever
+    torch launch comes next, in another test; this names the test that left it."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import ctypes
+    try:
+        hip = ctypes.CDLL("libamdhip64.so.7")
+    except OSError:
+        return
+    hip.hipGetLastError.restype = ctypes.c_int
+    err = hip.hipGetLastError()  # reads and clears
+    assert err == 0, f"the test left HIP error {err} in the last-error slot"

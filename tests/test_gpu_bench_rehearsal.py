@@ -121,6 +121,8 @@ def test_bench_rccl_at_one(mode):
     assert res["n_gpus"] == 1 and res["self_check"]["ok"] and res["self_check"]["groups"] == 6
     assert res["roofline_exchange"]["exchange_ms"] > 0
     assert res["roofline_exchange"]["exchange"] == mode
+    probe = res["roofline_exchange"]["probe"]  # the RCCL probe ran through the library
+    assert probe["ok"] and probe["transport"] == "rccl" and probe["GB/s"] > 0
 
 
 def test_forced_mismatch_on_a_3_gb_group_reports_its_first_byte():

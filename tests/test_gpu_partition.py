@@ -264,6 +264,41 @@ def test_exchange_past_1_gib_per_peer_arrives_whole():
         assert rb.tolist() == [nbytes] and torch.equal(recv, send)
 
 
+def test_exchange_tickets_discarded_or_left_to_the_node():
+    """a posted ticket that is never issued is freed by sux_exchange_group_discard
+    (after its read-back) or, when the caller walks away, by sux_node_destroy; a later post and
+    issue on the same node still works."""
+    from sparkucx_amd.shuffle import Node
+    R, maps, MAP = 8, 2, 4096
+    row = torch.div(torch.arange(R + 1, dtype=torch.int64) * MAP, R, rounding_mode="floor")
+    index = row.repeat(maps).to("cuda")
+    gathered = torch.empty_like(index)
+    send = torch.randint(0, 256, (MAP * maps,), dtype=torch.uint8, device="cuda")
+    recv = torch.zeros_like(send)
+    with Node(device=0, rank=0, world_size=1, comm_id=N.unique_id()) as node:
+        node.exchange_group_discard(node.exchange_group_post(index, maps, R, gathered))
+        node.exchange_group_post(index, maps, R, gathered)  # left behind: the node frees it
+        t = node.exchange_group_post(index, maps, R, gathered)
+        rb = node.exchange_group_issue(t, send, recv)
+        torch.cuda.synchronize()
+        assert rb.tolist() == [MAP * maps] and torch.equal(recv, send)
+
+
+def test_ipc_export_cache_keeps_live_allocations_only():
+    """exporting a new allocation drops the cache entries of freed ones, and a
+    re-export of a live allocation returns the same descriptor."""
+    from sparkucx_amd.shuffle import Node
+    with Node(device=0) as node:
+        keep = torch.empty(1 << 22, dtype=torch.uint8, device="cuda")
+        d0 = node.ipc_handle(keep)
+        for _ in range(4):  # allocations freed right after their export (caching allocator off)
+            x = torch.empty(1 << 26, dtype=torch.uint8, device="cuda")
+            node.ipc_handle(x)
+            del x
+            torch.cuda.empty_cache()
+        assert node.ipc_handle(keep) == d0
+
+
 # ---- full-size properties (BASELINE-scale batches, size-independent checks) ----------------------
 def test_large_batch_properties(gpu_node):
     """10^8 TeraSort records (10 GB, config-2 batch scale): multiset preserved, stable, sorted by

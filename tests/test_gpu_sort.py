@@ -302,6 +302,27 @@ def test_chunked_top_digit_4m(gpu_node, kind):
     gpu_node.check()
 
 
+@pytest.mark.parametrize("base,width", [(0x7FFF_FFFF_FFF0_1234, 1 << 40),   # crosses 2^63
+                                        (0x0123_4567_89AB_CDEF, 1 << 20),   # few blocks
+                                        (0x8000_0000_0000_0000, 0x0147_AE14_7AE1_47AE),
+                                        (0xFFFF_FFFF_0000_0007, (1 << 32) - 8)])  # ends at 2^64 - 1
+def test_ranged_top_digit(gpu_node, base, width):
+    """The chunked top digit over the key RANGE (round 5): the bucket of a key is its aligned
+    block counted from the smallest key's, so keys that fill only part of the varying bits — a
+    range partition's, or ones straddling a power of two, where the bit span put everything in
+    two buckets — spread over every bucket.  Keys: 8-byte big-endian prefixes uniform in
+    [base, base + width) (with their other two key bytes random), vs the oracle."""
+    n = 600_000
+    rng = np.random.default_rng(width & 0xFFFF)
+    recs = O.gen_terasort(73, 0, n).reshape(-1, 100)
+    k = (np.uint64(base) + (rng.random(n) * width).astype(np.uint64)).astype(">u8")
+    recs[:, :8] = k.view(np.uint8).reshape(n, 8)
+    recs = recs.ravel()
+    got = gpu_sort(gpu_node, recs, 100, N.SORT_BYTES, 0, 10)
+    assert got.tobytes() == O.sort_records(recs, 100, O.SORT_BYTES, 0, 10).tobytes()
+    gpu_node.check()
+
+
 @pytest.mark.parametrize("shape", ["tie_runs", "long_tie_runs"])
 def test_lds_sort_tie_fixup_and_redo(gpu_node, shape):
     """k_sort_local sorts a bucket by its two most significant varying digits, then finishes the
