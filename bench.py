@@ -1066,6 +1066,11 @@ def main():
                          "multi-rank run has verified the other); 'post-issue' = the all-gather "
                          "of group k (sux_exchange_group_post) beside the all-to-all of k - 1 "
                          "(sux_exchange_group_issue) on a split communicator")
+    ap.add_argument("--ownership", default="auto", choices=["auto", "balanced", "equal"],
+                    help="N>1: reduce-partition ownership — contiguous ranges balanced by the "
+                         "sampled partition bytes (sux_plan_ownership), the equal split, or "
+                         "'auto' (balanced when the equal split's busiest owner is > 5 %% over "
+                         "the mean)")
     ap.add_argument("--xgmi-probe-mib", type=int, default=256,
                     help="N>1: before the run, time every rank sending this many MiB to every "
                          "peer at once through the run's transport (the measured exchange peak; "
@@ -1316,15 +1321,16 @@ def main():
             torch.cuda.synchronize(dev)
             got = rbuf.cpu().numpy()
             gnp = np.ascontiguousarray(gi.cpu().numpy())
-            lo, hi = (rank * R) // world, ((rank + 1) * R) // world
+            lo, hi = int(owner[rank]), int(owner[rank + 1])
             for g in range(world):
                 grecs = ogen(seed, g * n + r0, r1 - r0)
                 for m in range(mg):
                     a, b = m * rpm, min(r1 - r0, (m + 1) * rpm)
                     d, _, ix, _ = O.write_map(opart, grecs[a * rs:b * rs], rs)
                     for p in range(lo, hi):
-                        off = lib.sux_plan_block_offset(world, rank, mg, R, gnp.ctypes.data,
-                                                        g, m, p)
+                        off = lib.sux_plan_block_offset_owned(world, rank, mg, R,
+                                                              gnp.ctypes.data,
+                                                              owner.ctypes.data, g, m, p)
                         want = d[ix[p]:ix[p + 1]]
                         if off < 0 or got[off:off + len(want)].tobytes() != want.tobytes():
                             raise RuntimeError(f"verify: rank {rank} group {j} source {g} "
@@ -1356,7 +1362,7 @@ def main():
             range, is non-decreasing within each (source, map) block run and counts exactly the
             index runs; the word multiset is checked across ranks at the end of the step."""
             torch.cuda.synchronize(dev)
-            lo, hi = (rank * R) // world, ((rank + 1) * R) // world
+            lo, hi = int(owner[rank]), int(owner[rank + 1])
             t = gi.view(world, mg, R + 1)
             own = t[:, :, hi] - t[:, :, lo]
             exp = int(own.sum())
@@ -1442,6 +1448,36 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
+    # ---- reduce-partition ownership (N > 1): contiguous ranges, balanced by bytes ----------
+    # Planned once, before the shuffle, from a sample: the partition sizes of every rank's first
+    # launch group, summed over ranks (as Spark's RangePartitioner samples keys in a job of its
+    # own before a sort's shuffle).  'auto' takes the balanced split when the equal one leaves
+    # its busiest owner > 5 % above the mean (Zipf keys, C4), else keeps the equal split.
+    owner = np.array([(h * R) // world for h in range(world + 1)], np.int32)
+    own_info = None
+    if pipelined and world > 1 and args.ownership != "equal":
+        torch.cuda.synchronize(dev)
+        t_own = time.perf_counter()
+        sn = min(n, group_recs)
+        pid = node.partition_ids(part, data[:sn * rs], rs).to(torch.int64)
+        cnt = (torch.bincount(pid, minlength=R) * rs).to(ctl)
+        del pid
+        dist.all_reduce(cnt)
+        cnt = cnt.cpu().numpy()
+        bal = N.plan_ownership(world, cnt)
+        mean = cnt.sum() / world
+        r_eq = max(int(cnt[owner[h]:owner[h + 1]].sum()) for h in range(world)) / mean
+        r_bal = max(int(cnt[bal[h]:bal[h + 1]].sum()) for h in range(world)) / mean
+        use = args.ownership == "balanced" or r_eq > 1.05
+        if use:
+            owner = bal
+            node.set_ownership(world, R, owner)
+        own_info = {"plan": "balanced" if use else "equal", "sample_records_per_rank": sn,
+                    "sampled_max_over_mean": {"equal": round(r_eq, 4), "balanced": round(r_bal, 4)},
+                    "plan_ms": round((time.perf_counter() - t_own) * 1e3, 3),
+                    "bounds": owner.tolist() if world <= 16 else None}
+        log(f"[rank {rank}] ownership: {own_info}")
+
     xprobe = None
     if pipelined and (world > 1 or args.rccl_at_one) and args.xgmi_probe_mib > 0:
         # IPC imports of large allocations by many processes of one GPU were measured to stall
@@ -1516,13 +1552,21 @@ def main():
         xfer_n = len(xfer_ev)
         # exact off-GPU bytes per step from the all-gathered index tables
         gh = gidx.cpu().numpy()
-        lo, hi = (rank * R) // world, ((rank + 1) * R) // world
-        remote = 0
+        lo, hi = int(owner[rank]), int(owner[rank + 1])
+        remote = ingress = 0
         for j in range(groups):
             mg = -(-(min(n, (j + 1) * group_recs) - j * group_recs) // rpm)
             t = gh[j, :world * mg * (R + 1)].reshape(world, mg, R + 1)
             own = t[:, :, hi] - t[:, :, lo]
             remote += int(own.sum() - own[rank].sum())
+            ingress += int(own.sum())
+        # the exchange runs at its busiest owner's ingress: max / mean of the ranks' received bytes
+        ing = torch.tensor([ingress, ingress], dtype=torch.float64, device=ctl)
+        if world > 1:
+            dist.all_reduce(ing[0:1], op=dist.ReduceOp.MAX)
+            dist.all_reduce(ing[1:2])
+        ing = ing.cpu().tolist()
+        ingress_ratio = ing[0] / (ing[1] / world) if ing[1] else None
         if int(rbytes.min().item()) < 0:
             raise RuntimeError("exchange overflowed a receive buffer")
         remote *= args.steps
@@ -1555,7 +1599,9 @@ def main():
             "peak_source": f"(world - 1) x {XGMI_LINK_GBS} GB/s per xGMI link (spec assumption)",
             "unit": "GB/s", "frac": None if ach is None else round(ach / peak, 4),
             "remote_bytes_per_rank": remote // args.steps, "exchange_ms": round(xms, 2),
-            "exchange": args.exchange if args.transport == "rccl" else "ipc pull"}
+            "exchange": args.exchange if args.transport == "rccl" else "ipc pull",
+            "ingress_max_over_mean": None if ingress_ratio is None else round(ingress_ratio, 4),
+            "ownership": own_info}
         if xprobe is not None:
             mp = xprobe["GB/s"]
             if world > 1:  # the slowest rank's peer-read rate bounds the node

@@ -313,6 +313,33 @@ int64_t sux_plan_block_offset(int32_t world, int32_t rank, int32_t num_maps,
                               int32_t num_partitions, const int64_t* gathered_index, int32_t g,
                               int32_t m, int32_t p);
 
+/* Partition ownership (round 5).  Reduce partitions are owned in contiguous ranges: peer h owns
+ * [owner_bounds[h], owner_bounds[h + 1]) (world + 1 rising int32 from 0 to R).  The default is
+ * the equal split [h R / world, (h + 1) R / world); with skewed keys (Zipf: one partition can
+ * hold ~12 % of a shuffle) an equal count of partitions per owner leaves one owner with far more
+ * bytes than the others, and the exchange runs at that owner's ingress.  The reference fetches
+ * per block (OnOffsetsFetchCallback.java:53-87), so any partition-aligned ownership is legal.
+ * sux_plan_ownership: the contiguous split of R partitions of `partition_bytes` into `world`
+ * non-empty ranges whose largest range holds the fewest bytes (exact: binary search on that
+ * bound with a greedy fill).  Host arithmetic; usable on CPU. */
+int sux_plan_ownership(int32_t world, int32_t num_partitions, const int64_t* partition_bytes,
+                       int32_t* owner_bounds);
+/* The node's ownership for the stateless group calls with `world` peers and R partitions —
+ * sux_partition_maps_peer_major (the send layout), sux_exchange_group / _post / _issue (the
+ * plan) and sux_pull_group — until set again; NULL owner_bounds restores the equal split.
+ * Every rank must set the same table before its next group call (the plugin path's
+ * sux_exchange_maps keeps the equal split). */
+int sux_node_set_ownership(sux_node* node, int32_t world, int32_t num_partitions,
+                           const int32_t* owner_bounds);
+/* sux_plan_group / sux_plan_block_offset under an ownership table (NULL = the equal split). */
+int sux_plan_group_owned(int32_t world, int32_t rank, int32_t num_maps, int32_t num_partitions,
+                         const int64_t* gathered_index, const int32_t* owner_bounds,
+                         uint64_t* sendcounts, uint64_t* sdispls, uint64_t* recvcounts,
+                         uint64_t* rdispls);
+int64_t sux_plan_block_offset_owned(int32_t world, int32_t rank, int32_t num_maps,
+                                    int32_t num_partitions, const int64_t* gathered_index,
+                                    const int32_t* owner_bounds, int32_t g, int32_t m, int32_t p);
+
 /* One pipelined exchange step over the node's RCCL communicator: all-gather this rank's
  * num_maps index tables into d_gathered_index (device, world*num_maps*(R+1) int64), bring them
  * to the host (the only host sync), plan (sux_plan_group) and all-to-all d_send -> d_recv.

@@ -188,8 +188,45 @@ def owner_start(h: int, R: int, G: int) -> int:
     return (h * R) // G
 
 
-def peer_major(part: Partitioner, recs: np.ndarray, rec_size: int, rpm: int, world: int):
-    """Oracle of sux_partition_maps_peer_major: [peer h][map m][partitions owned by h]."""
+def plan_ownership(world: int, partition_bytes) -> list[int]:
+    """Oracle of sux_plan_ownership, by dynamic programming (not the library's binary search):
+    the contiguous split of R partitions into `world` non-empty ranges minimising the largest
+    range's bytes; of the optimal splits, the one whose owners end as early as possible (the
+    library's greedy fill).  Returns world + 1 bounds.  O(world R^2): test sizes only."""
+    b = [int(x) for x in partition_bytes]
+    R = len(b)
+    pre = [0]
+    for x in b:
+        pre.append(pre[-1] + x)
+    INF = float("inf")
+    # best[h][p]: smallest possible largest range when owners h.. cover partitions p..R-1
+    best = [[INF] * (R + 1) for _ in range(world + 1)]
+    best[world][R] = 0
+    for h in range(world - 1, -1, -1):
+        for p in range(R - (world - h) + 1):
+            for q in range(p + 1, R - (world - h - 1) + 1):
+                v = max(pre[q] - pre[p], best[h + 1][q])
+                if v < best[h][p]:
+                    best[h][p] = v
+    cap = best[0][0]
+    # the greedy fill at the optimal cap: each owner as long as the cap allows, leaving one
+    # partition per later owner
+    bounds, p = [0], 0
+    for h in range(world - 1):
+        s = b[p]
+        p += 1
+        while p < R - (world - 1 - h) and s + b[p] <= cap:
+            s += b[p]
+            p += 1
+        bounds.append(p)
+    bounds.append(R)
+    return bounds
+
+
+def peer_major(part: Partitioner, recs: np.ndarray, rec_size: int, rpm: int, world: int,
+               own=None):
+    """Oracle of sux_partition_maps_peer_major: [peer h][map m][partitions owned by h]; `own`:
+    the ownership bounds (world + 1; None = the equal split)."""
     n = recs.size // rec_size
     maps = []
     for m0 in range(0, n, rpm):
@@ -197,7 +234,8 @@ def peer_major(part: Partitioner, recs: np.ndarray, rec_size: int, rpm: int, wor
         maps.append((d, ix))
     chunks, peer_bytes = [], []
     for h in range(world):
-        lo, hi = owner_start(h, part.R, world), owner_start(h + 1, part.R, world)
+        lo, hi = ((owner_start(h, part.R, world), owner_start(h + 1, part.R, world))
+                  if own is None else (int(own[h]), int(own[h + 1])))
         b = 0
         for d, ix in maps:
             chunks.append(d[ix[lo]:ix[hi]])

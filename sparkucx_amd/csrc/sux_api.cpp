@@ -470,6 +470,16 @@ struct Shuffle {
 };
 
 int32_t owner_lo(int32_t h, int32_t R, int32_t G) { return (int32_t)(((int64_t)h * R) / G); }
+// First partition of peer h under an ownership table (nullptr = the equal split).
+int32_t own_lo(const int32_t* own, int32_t h, int32_t R, int32_t G) {
+  return own ? own[h] : owner_lo(h, R, G);
+}
+// An ownership table is W + 1 rising bounds from 0 to R.
+void check_ownership(int32_t W, int32_t R, const int32_t* own) {
+  require(own[0] == 0 && own[W] == R, SUX_EINVAL, "ownership must run from 0 to R");
+  for (int h = 0; h < W; ++h)
+    require(own[h] <= own[h + 1], SUX_EINVAL, "ownership bounds must not fall");
+}
 }  // namespace
 
 struct sux_node {
@@ -506,6 +516,18 @@ struct sux_node {
   std::map<void*, IpcExport> ipc_exports;
   // sux_exchange_group_post tickets not yet issued or discarded (freed by sux_node_destroy)
   std::set<sux_xticket*> tickets;
+  // sux_node_set_ownership: which contiguous partition range each peer owns in the stateless
+  // group calls (peer-major partition, exchange_group / post / issue, pull) for groups of
+  // own_R partitions among own_W peers; empty = the equal split
+  int32_t own_W = 0, own_R = 0;
+  std::vector<int32_t> own;
+  int32_t* d_own = nullptr;  // device copy (own_W + 1 int32)
+  const int32_t* own_host(int W, int R) const {
+    return (!own.empty() && own_W == W && own_R == R) ? own.data() : nullptr;
+  }
+  const int32_t* own_dev(int W, int R) const {
+    return (!own.empty() && own_W == W && own_R == R) ? d_own : nullptr;
+  }
   sux_allgather_fn boot = nullptr;   // host all-gather of the embedding runtime
   void* boot_ctx = nullptr;
   sux_tuning tuning{};               // all zero = measured defaults (resolve_tuning)
@@ -952,7 +974,8 @@ Group make_group(const sux_partitioner* part, const void* recs, uint32_t rs, uin
 void run_group(sux_node* node, const sux_partitioner* part, const Group& G, int32_t world,
                void* d_out, int64_t* d_index, uint8_t* d_index_be, uint16_t* d_pids,
                uint64_t* d_peer_bytes, void* d_ws, uint64_t ws_bytes, hipStream_t s,
-               bool pipelined = false, hipStream_t s_k1 = nullptr, hipEvent_t k1_done = nullptr) {
+               bool pipelined = false, hipStream_t s_k1 = nullptr, hipEvent_t k1_done = nullptr,
+               const int32_t* d_own = nullptr) {
   require(d_ws || G.ws.total == 0, SUX_EINVAL, "workspace is NULL");
   require(ws_bytes >= G.ws.total, SUX_EINVAL,
           "workspace too small: need " + std::to_string(G.ws.total) + " bytes");
@@ -961,7 +984,7 @@ void run_group(sux_node* node, const sux_partitioner* part, const Group& G, int3
               ((uintptr_t)d_index_be & 7) == 0 && ((uintptr_t)d_ws & 255) == 0,
           SUX_EINVAL, "output (4 B), index (8 B) and workspace (256 B) must be aligned");
   if (G.g.num_records == 0) return;
-  sux::LayoutDesc lay{world, G.g.rec_size};
+  sux::LayoutDesc lay{world, G.g.rec_size, d_own};
   hip_check(sux::launch_partition_group(part->pd, G.g, lay, static_cast<uint8_t*>(d_out), d_index,
                                         d_index_be, d_pids, static_cast<uint8_t*>(d_ws), G.ws,
                                         d_peer_bytes, resolve_tuning(node->tuning, pipelined),
@@ -1352,6 +1375,7 @@ int sux_node_destroy(sux_node* node) {
     for (hipEvent_t e : node->sort_ev)
       if (e) (void)hipEventDestroy(e);
     if (node->d_err) (void)hipFree(node->d_err);
+    if (node->d_own) (void)hipFree(node->d_own);
     for (auto& kv : node->shuffles) release_shuffle(node, *kv.second);
     node->shuffles.clear();
     for (auto& kv : node->ipc_bases) ipc_close_ref(node, kv.second.first, kv.second.second);
@@ -1570,7 +1594,8 @@ int sux_partition_maps_peer_major(sux_node* node, const sux_partitioner* part,
     node->bind();
     Group G = make_group(part, d_records, rs, rpm, n);
     run_group(node, part, G, world, d_send, d_index, d_index_be, nullptr, d_peer_bytes, d_ws,
-              ws_bytes, node->stream(stream));
+              ws_bytes, node->stream(stream), false, nullptr, nullptr,
+              node->own_dev(world, part->desc.num_partitions));
   });
 }
 
@@ -2082,24 +2107,96 @@ int sux_read_file_blocks(sux_node* node, const char* data_path, const char* inde
 }
 
 // ---- exchange plan (host arithmetic) -----------------------------------------------------------
+int sux_plan_ownership(int32_t W, int32_t R, const int64_t* bytes, int32_t* own) {
+  return host_guard([&] {
+    require(W >= 1 && R >= W && bytes && own, SUX_EINVAL, "bad ownership shape");
+    // min over contiguous splits into W non-empty ranges of the largest range's bytes: binary
+    // search on that cap; a cap is feasible when greedy ranges — each as long as the cap allows,
+    // leaving one partition for every owner after it — cover all R partitions
+    int64_t total = 0, most = 0;
+    for (int p = 0; p < R; ++p) {
+      require(bytes[p] >= 0, SUX_EINVAL, "negative partition size");
+      total += bytes[p];
+      most = std::max(most, bytes[p]);
+    }
+    auto fill = [&](int64_t cap, int32_t* out) {
+      int p = 0;
+      for (int h = 0; h < W; ++h) {
+        if (out) out[h] = p;
+        if (h == W - 1) {
+          int64_t rest = 0;
+          for (int q = p; q < R; ++q) rest += bytes[q];
+          p = R;
+          if (rest > cap) return false;
+          break;
+        }
+        int64_t sum = bytes[p++];  // every owner takes at least one partition
+        if (sum > cap) return false;
+        while (p < R - (W - 1 - h) && sum + bytes[p] <= cap) sum += bytes[p++];
+      }
+      if (out) out[W] = R;
+      return p == R;
+    };
+    int64_t lo = most, hi = total;  // fill(hi) always succeeds
+    while (lo < hi) {
+      const int64_t mid = lo + (hi - lo) / 2;
+      if (fill(mid, nullptr)) hi = mid; else lo = mid + 1;
+    }
+    const bool ok = fill(lo, own);
+    require(ok, SUX_EINVAL, "ownership plan failed");
+  });
+}
+
+int sux_node_set_ownership(sux_node* node, int32_t W, int32_t R, const int32_t* own) {
+  return guard([&] {
+    require(node && W >= 1 && R >= W, SUX_EINVAL, "bad ownership shape");
+    if (own) check_ownership(W, R, own);
+    node->bind();
+    std::lock_guard<std::mutex> lk(node->mu);
+    if (!own) {
+      node->own.clear();
+      return;
+    }
+    if (!node->d_own || node->own_W < W) {
+      if (node->d_own) (void)hipFree(node->d_own);
+      node->d_own = nullptr;
+      hip_check(hipMalloc(&node->d_own, sizeof(int32_t) * (W + 1)), "hipMalloc(ownership)");
+    }
+    // ordered on the null stream: the next group call on any stream sees the new table
+    hip_check(hipMemcpy(node->d_own, own, sizeof(int32_t) * (W + 1), hipMemcpyHostToDevice),
+              "ownership upload");
+    node->own.assign(own, own + W + 1);
+    node->own_W = W;
+    node->own_R = R;
+  });
+}
+
 int sux_plan_group(int32_t W, int32_t rank, int32_t M, int32_t R, const int64_t* gi,
                    uint64_t* sendcounts, uint64_t* sdispls, uint64_t* recvcounts,
                    uint64_t* rdispls) {
+  return sux_plan_group_owned(W, rank, M, R, gi, nullptr, sendcounts, sdispls, recvcounts,
+                              rdispls);
+}
+
+int sux_plan_group_owned(int32_t W, int32_t rank, int32_t M, int32_t R, const int64_t* gi,
+                         const int32_t* own, uint64_t* sendcounts, uint64_t* sdispls,
+                         uint64_t* recvcounts, uint64_t* rdispls) {
   return guard([&] {
     require(W >= 1 && rank >= 0 && rank < W && M >= 0 && R >= W, SUX_EINVAL, "bad plan shape");
     require(gi || M == 0, SUX_EINVAL, "gathered index is NULL");
+    if (own) check_ownership(W, R, own);
     const int64_t stride = (int64_t)R + 1;
     auto idx = [&](int g, int m, int p) { return gi[((int64_t)g * M + m) * stride + p]; };
     uint64_t sacc = 0, racc = 0;
     for (int h = 0; h < W; ++h) {
-      int lo = owner_lo(h, R, W), hi = owner_lo(h + 1, R, W);
+      int lo = own_lo(own, h, R, W), hi = own_lo(own, h + 1, R, W);
       uint64_t s = 0;
       for (int m = 0; m < M; ++m) s += (uint64_t)(idx(rank, m, hi) - idx(rank, m, lo));
       if (sendcounts) sendcounts[h] = s;
       if (sdispls) sdispls[h] = sacc;
       sacc += s;
     }
-    int lo = owner_lo(rank, R, W), hi = owner_lo(rank + 1, R, W);
+    int lo = own_lo(own, rank, R, W), hi = own_lo(own, rank + 1, R, W);
     for (int g = 0; g < W; ++g) {
       uint64_t r = 0;
       for (int m = 0; m < M; ++m) r += (uint64_t)(idx(g, m, hi) - idx(g, m, lo));
@@ -2112,9 +2209,15 @@ int sux_plan_group(int32_t W, int32_t rank, int32_t M, int32_t R, const int64_t*
 
 int64_t sux_plan_block_offset(int32_t W, int32_t rank, int32_t M, int32_t R, const int64_t* gi,
                               int32_t g, int32_t m, int32_t p) {
+  return sux_plan_block_offset_owned(W, rank, M, R, gi, nullptr, g, m, p);
+}
+
+int64_t sux_plan_block_offset_owned(int32_t W, int32_t rank, int32_t M, int32_t R,
+                                    const int64_t* gi, const int32_t* own, int32_t g, int32_t m,
+                                    int32_t p) {
   if (!gi || W < 1 || rank < 0 || rank >= W || g < 0 || g >= W || m < 0 || m >= M || R < W)
     return -1;
-  int lo = owner_lo(rank, R, W), hi = owner_lo(rank + 1, R, W);
+  int lo = own_lo(own, rank, R, W), hi = own_lo(own, rank + 1, R, W);
   if (p < lo || p >= hi) return -1;
   const int64_t stride = (int64_t)R + 1;
   auto idx = [&](int gg, int mm, int pp) { return gi[((int64_t)gg * M + mm) * stride + pp]; };
@@ -2149,8 +2252,8 @@ int sux_exchange_group(sux_node* node, const void* d_send, const int64_t* d_inde
               "D2H gathered index");
     hip_check(hipStreamSynchronize(s), "sync gathered index");
     std::vector<uint64_t> sc(W), sd(W), rc(W), rd(W);
-    int rc_plan = sux_plan_group(W, rank, M, R, host, sc.data(), sd.data(), rc.data(),
-                                 rd.data());
+    int rc_plan = sux_plan_group_owned(W, rank, M, R, host, node->own_host(W, R), sc.data(),
+                                       sd.data(), rc.data(), rd.data());
     require(rc_plan == SUX_OK, rc_plan, g_err);
     uint64_t total = rd[W - 1] + rc[W - 1];
     require(total <= recv_capacity, SUX_ERANGE,
@@ -2247,8 +2350,10 @@ int sux_exchange_group_issue(sux_node* node, sux_xticket* ticket, const void* d_
     // caller issues group k - 1 after posting group k); `stream` itself never waits on the host
     hip_check(hipEventSynchronize(t->done.e), "sync gathered index");
     std::vector<uint64_t> sc(W), sd(W), rc(W), rd(W);
-    int rc_plan = sux_plan_group(W, rank, t->M, t->R, static_cast<const int64_t*>(t->host->b.first),
-                                 sc.data(), sd.data(), rc.data(), rd.data());
+    int rc_plan = sux_plan_group_owned(W, rank, t->M, t->R,
+                                       static_cast<const int64_t*>(t->host->b.first),
+                                       node->own_host(W, t->R), sc.data(), sd.data(), rc.data(),
+                                       rd.data());
     require(rc_plan == SUX_OK, rc_plan, g_err);
     const uint64_t total = rd[W - 1] + rc[W - 1];
     require(total <= recv_capacity, SUX_ERANGE,
@@ -2317,7 +2422,7 @@ int sux_pull_group(sux_node* node, int32_t W, int32_t rank, const uint64_t* d_sr
     node->bind();
     hip_check(sux::launch_pull(W, rank, d_src_ptrs, d_gathered, M, R,
                                static_cast<uint8_t*>(d_recv), cap, d_recv_bytes,
-                               node->stream(stream)),
+                               node->stream(stream), node->own_dev(W, R)),
               "pull launch");
   });
 }

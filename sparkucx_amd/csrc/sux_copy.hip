@@ -76,19 +76,21 @@ namespace sux {
 // ---------------------------------------------------------------------------------------------
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 
-__device__ __forceinline__ int32_t owner_lo_d(int32_t h, int32_t R, int32_t W) {
-  return (int32_t)(((int64_t)h * R) / W);
+__device__ __forceinline__ int32_t owner_lo_d(int32_t h, int32_t R, int32_t W,
+                                              const int32_t* own) {
+  return own ? own[h] : (int32_t)(((int64_t)h * R) / W);
 }
 
 __global__ __launch_bounds__(256) void k_pull(int32_t W, int32_t me, const uint64_t* __restrict__ srcs,
                                               const int64_t* __restrict__ gi, int32_t M, int32_t R,
                                               uint8_t* __restrict__ recv, uint64_t cap,
-                                              uint64_t* recv_bytes, uint32_t per_src) {
+                                              uint64_t* recv_bytes, uint32_t per_src,
+                                              const int32_t* __restrict__ own) {
   __shared__ uint64_t red[3][256];
   const int32_t g = blockIdx.x / per_src;
   const uint32_t slot = blockIdx.x - g * per_src;
   const int64_t stride = (int64_t)R + 1;
-  const int32_t lo = owner_lo_d(me, R, W), hi = owner_lo_d(me + 1, R, W);
+  const int32_t lo = owner_lo_d(me, R, W, own), hi = owner_lo_d(me + 1, R, W, own);
   // per thread partial sums: [0] offset of my share in g's buffer, [1] its size,
   // [2] bytes from sources before g (my receive offset), [3] everything (total received)
   uint64_t a = 0, b = 0, c = 0, tot = 0;
@@ -202,10 +204,10 @@ hipError_t launch_resolve_blocks(const void* d_blocks, uint32_t n, const Resolve
 
 hipError_t launch_pull(int32_t W, int32_t me, const uint64_t* srcs, const int64_t* gi, int32_t M,
                        int32_t R, uint8_t* recv, uint64_t cap, uint64_t* recv_bytes,
-                       hipStream_t s) {
+                       hipStream_t s, const int32_t* own) {
   const uint32_t per_src = 1024 / (uint32_t)(W > 0 ? W : 1) + 1;
   hipLaunchKernelGGL(k_pull, dim3(per_src * W), dim3(256), 0, s, W, me, srcs, gi, M, R, recv, cap,
-                     recv_bytes, per_src);
+                     recv_bytes, per_src, own);
   return hipGetLastError();
 }
 

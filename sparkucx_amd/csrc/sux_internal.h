@@ -132,6 +132,9 @@ uint32_t choose_tile_recs(uint32_t R, uint32_t rec_size, uint64_t records_per_ma
 struct LayoutDesc {
   int32_t world;  // 1 = map-major
   uint32_t rec_size;
+  // peer h owns partitions [own[h], own[h + 1]) (device, world + 1 int32; sux_node_set_ownership);
+  // nullptr = the equal split [h R / world, (h + 1) R / world)
+  const int32_t* own = nullptr;
 };
 
 // CUs a stream may use: its CU mask's population, or every CU of the device (sux_onepass.hip).
@@ -219,7 +222,7 @@ hipError_t launch_gather_i64(const int64_t* const* d_ptrs, uint32_t n, int64_t* 
 // One-sided pull of a peer-major group from mapped peer buffers (sux_copy.hip).
 hipError_t launch_pull(int32_t W, int32_t me, const uint64_t* srcs, const int64_t* gi, int32_t M,
                        int32_t R, uint8_t* recv, uint64_t cap, uint64_t* recv_bytes,
-                       hipStream_t s);
+                       hipStream_t s, const int32_t* own = nullptr);
 
 // Reduce-side sort (sux_sort.hip): (key, index) pairs, and the final gather of whole records.
 constexpr int kPartRadix = 7;  // internal partitioner: 12-bit digit (shift in PartDev::seed)

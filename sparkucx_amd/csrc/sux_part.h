@@ -88,9 +88,22 @@ __device__ __forceinline__ uint64_t bswap64(uint64_t v) {
   return ((uint64_t)__builtin_bswap32((uint32_t)v) << 32) | __builtin_bswap32((uint32_t)(v >> 32));
 }
 
-__device__ __forceinline__ uint32_t owner_of(uint32_t p, int R, int G) {
+__device__ __forceinline__ uint32_t owner_of(uint32_t p, int R, int G,
+                                             const int32_t* own = nullptr) {
+  if (own) {  // largest h with own[h] <= p (an empty range's owner is never the answer)
+    uint32_t lo = 0, hi = (uint32_t)G;  // own[lo] <= p < own[hi]
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if ((uint32_t)own[mid] <= p) lo = mid; else hi = mid;
+    }
+    return lo;
+  }
   // largest h with floor(h*R/G) <= p
   return (uint32_t)((((uint64_t)p + 1) * G + R - 1) / R) - 1;
+}
+// First partition peer h owns (h = G: R).
+__device__ __forceinline__ uint32_t owner_lo_of(uint32_t h, int R, int G, const int32_t* own) {
+  return own ? (uint32_t)own[h] : (uint32_t)(((int64_t)h * R) / G);
 }
 
 // Stable in-wave rank of `dig` (DB bits) against the wave's running per-digit counters wcw[]:

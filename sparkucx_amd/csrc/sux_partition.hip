@@ -171,7 +171,8 @@ __global__ __launch_bounds__(kScanThreads) void k_map_scan(const uint64_t* __res
                                                            int R, int G, uint32_t rec_size,
                                                            uint64_t records_per_map,
                                                            uint64_t num_records,
-                                                           const uint64_t* __restrict__ map_offs) {
+                                                           const uint64_t* __restrict__ map_offs,
+                                                           const int32_t* __restrict__ own) {
   __shared__ uint64_t sh[2 * kWave + 1];
   __shared__ unsigned long long hs[1024];
   const uint32_t m = blockIdx.x;
@@ -196,7 +197,7 @@ __global__ __launch_bounds__(kScanThreads) void k_map_scan(const uint64_t* __res
         base[(uint64_t)m * R + p] = (uint64_t)m * records_per_map + ex;
       } else {
         pre[(uint64_t)m * R + p] = ex;
-        atomicAdd(&hs[owner_of((uint32_t)p, R, G)], (unsigned long long)v);
+        atomicAdd(&hs[owner_of((uint32_t)p, R, G, own)], (unsigned long long)v);
       }
     }
     carry += tot;
@@ -247,13 +248,13 @@ __global__ __launch_bounds__(kScanThreads) void k_peer_off(uint64_t* __restrict_
 __global__ __launch_bounds__(256) void k_peer_base(const uint64_t* __restrict__ pre,
                                                    const uint64_t* __restrict__ mh,
                                                    uint64_t* __restrict__ base, uint32_t M, int R,
-                                                   int G) {
+                                                   int G, const int32_t* __restrict__ own) {
   const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (j >= (uint64_t)M * R) return;
   const uint64_t m = j / R;
   const uint32_t p = (uint32_t)(j - m * R);
-  const uint32_t h = owner_of(p, R, G);
-  const uint32_t lo = (uint32_t)(((int64_t)h * R) / G);
+  const uint32_t h = owner_of(p, R, G, own);
+  const uint32_t lo = owner_lo_of(h, R, G, own);
   base[j] = mh[m * G + h] + pre[j] - pre[m * R + lo];
 }
 
@@ -1855,12 +1856,12 @@ hipError_t launch_partition_group(const PartDev& pd, const MapGroup& g_in, const
   uint64_t* mh = base + 2 * L;
   hipLaunchKernelGGL(k_map_scan, dim3(g.num_maps), dim3(kScanThreads), 0, s, totals, base, pre, mh,
                      d_index, d_index_be, lay.world == 1 ? d_peer_bytes : nullptr, R, lay.world,
-                     g.rec_size, g.records_per_map, g.num_records, nullptr);
+                     g.rec_size, g.records_per_map, g.num_records, nullptr, lay.own);
   if (lay.world > 1) {
     hipLaunchKernelGGL(k_peer_off, dim3(1), dim3(kScanThreads), 0, s, mh, d_peer_bytes,
                        g.num_maps, lay.world, g.rec_size);
     hipLaunchKernelGGL(k_peer_base, dim3((uint32_t)((L + 255) / 256)), dim3(256), 0, s, pre, mh,
-                       base, g.num_maps, R, lay.world);
+                       base, g.num_maps, R, lay.world, lay.own);
   }
   timer_end(timer, kScan, s);
   e = hipGetLastError();
@@ -1990,7 +1991,7 @@ hipError_t launch_varlen_map_scan(const VarGroup& g, int R, const uint64_t* tota
   const uint64_t L = (uint64_t)g.num_maps * R;
   hipLaunchKernelGGL(k_map_scan, dim3(g.num_maps), dim3(kScanThreads), 0, s, totals, base,
                      base + L, base + 2 * L, d_index, d_index_be, nullptr, R, 1, 1u,
-                     g.records_per_map, g.num_records, g.offs);
+                     g.records_per_map, g.num_records, g.offs, nullptr);
   return hipGetLastError();
 }
 
@@ -2000,7 +2001,7 @@ hipError_t launch_rows_index(const uint64_t* sizes, uint32_t maps, uint32_t R, u
   const uint64_t L = (uint64_t)maps * R;
   hipLaunchKernelGGL(k_map_scan, dim3(maps), dim3(kScanThreads), 0, s, sizes, base, base + L,
                      base + 2 * L, d_index, d_index_be, nullptr, (int)R, 1, 1u, 0ull, 0ull,
-                     nullptr);
+                     nullptr, nullptr);
   return hipGetLastError();
 }
 

@@ -113,6 +113,10 @@ _SIGS = {
                                                 P]),
     "sux_plan_group": (C.c_int, [I32, I32, I32, I32, P, P, P, P, P]),
     "sux_plan_block_offset": (I64, [I32, I32, I32, I32, P, I32, I32, I32]),
+    "sux_plan_group_owned": (C.c_int, [I32, I32, I32, I32, P, P, P, P, P, P]),
+    "sux_plan_block_offset_owned": (I64, [I32, I32, I32, I32, P, P, I32, I32, I32]),
+    "sux_plan_ownership": (C.c_int, [I32, I32, P, P]),
+    "sux_node_set_ownership": (C.c_int, [P, I32, I32, P]),
     "sux_exchange_group": (C.c_int, [P, P, P, I32, I32, P, P, U64, P, P]),
     "sux_partition_ids": (C.c_int, [P, P, P, U32, U64, P, P]),
     "sux_partition_varlen_workspace_size": (C.c_int, [P, U64, U64, C.POINTER(U64)]),
@@ -242,6 +246,17 @@ def hip_memcpy(dst: int, src: int, nbytes: int, kind: int) -> None:
     rc = _hip.hipMemcpy(dst, src, nbytes, kind)
     if rc != 0:
         raise SuxError(SUX_EHIP, f"hipMemcpy failed ({rc})")
+
+
+def plan_ownership(world: int, partition_bytes) -> "np.ndarray":
+    """sux_plan_ownership: the contiguous split of R partitions into `world` non-empty owner
+    ranges whose largest holds the fewest bytes; returns the world + 1 int32 bounds."""
+    import numpy as np
+    b = np.ascontiguousarray(np.asarray(partition_bytes, dtype=np.int64))
+    own = np.zeros(world + 1, dtype=np.int32)
+    check(load().sux_plan_ownership(world, b.size, b.ctypes.data, own.ctypes.data),
+          "sux_plan_ownership")
+    return own
 
 
 def unique_id() -> bytes:

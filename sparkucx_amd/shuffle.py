@@ -366,6 +366,17 @@ class Node:
                 "sux_exchange_group_issue")
         return np.frombuffer(rb, dtype=np.uint64).copy()
 
+    def set_ownership(self, world: int, R: int, bounds=None):
+        """sux_node_set_ownership: peer h owns partitions [bounds[h], bounds[h + 1]) in the
+        stateless group calls; None restores the equal split."""
+        if bounds is None:
+            N.check(self.lib.sux_node_set_ownership(self.h, world, R, None),
+                    "sux_node_set_ownership")
+            return
+        b = np.ascontiguousarray(np.asarray(bounds, dtype=np.int32))
+        N.check(self.lib.sux_node_set_ownership(self.h, world, R, b.ctypes.data),
+                "sux_node_set_ownership")
+
     def exchange_group_discard(self, ticket):
         """A posted ticket that will not be issued: wait for its read-back and free it."""
         N.check(self.lib.sux_exchange_group_discard(self.h, ticket), "sux_exchange_group_discard")

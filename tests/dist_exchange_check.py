@@ -33,14 +33,33 @@ def main():
     ap.add_argument("--rpm", type=int, default=500)
     ap.add_argument("--R", type=int, default=8)
     ap.add_argument("--golden", default="")
+    ap.add_argument("--zipf", action="store_true",
+                    help="Zipf(1.1) int64 keys, Spark SQL murmur3 partitioner (C4's shape)")
+    ap.add_argument("--balanced", action="store_true",
+                    help="ownership balanced by the all-reduced partition bytes "
+                         "(sux_plan_ownership) instead of the equal split")
     a = ap.parse_args()
     dist.init_process_group("gloo")
     rank, W = dist.get_rank(), dist.get_world_size()
     R, M, rpm = a.R, a.maps, a.rpm
-    part = O.terasort_partitioner(R)
-    seed = 11 + rank
-    recs = O.gen_terasort(seed, 0, M * rpm)
-    send, index, peer_bytes = O.peer_major(part, recs, 100, rpm, W)
+    if a.zipf:
+        part = O.Partitioner(O.MURMUR3_LONG, R, 0, 8, 42)
+        gen = lambda g: O.gen_zipf(11, g * M * rpm, M * rpm)  # noqa: E731
+    else:
+        part = O.terasort_partitioner(R)
+        gen = lambda g: O.gen_terasort(11 + g, 0, M * rpm)  # noqa: E731
+    recs = gen(rank)
+    own = np.array([(h * R) // W for h in range(W + 1)], np.int32)
+    if a.balanced:
+        # partition bytes of every rank's maps, summed over ranks -> the balanced ownership
+        lens = np.zeros(R, np.int64)
+        for m0 in range(0, M * rpm, rpm):
+            lens += np.asarray(O.write_map(part, recs[m0 * 100:(m0 + rpm) * 100], 100)[1])
+        t = torch.from_numpy(lens * 100)
+        dist.all_reduce(t)
+        own = N.plan_ownership(W, t.numpy())
+        assert own.tolist() == O.plan_ownership(W, t.numpy())
+    send, index, peer_bytes = O.peer_major(part, recs, 100, rpm, W, own=own)
 
     # 1. all-gather the index tables (replaces the driver metadata table + phase-1 GETs)
     idx = torch.from_numpy(index.astype(np.int64))
@@ -51,7 +70,8 @@ def main():
     # 2. plan with the library's host planner
     lib = N.load()
     sc, sd, rc, rd = [(C.c_uint64 * W)() for _ in range(4)]
-    assert lib.sux_plan_group(W, rank, M, R, gi.ctypes.data, sc, sd, rc, rd) == 0, N.last_error()
+    assert lib.sux_plan_group_owned(W, rank, M, R, gi.ctypes.data, own.ctypes.data,
+                                    sc, sd, rc, rd) == 0, N.last_error()
     assert list(sc) == peer_bytes.tolist(), (list(sc), peer_bytes.tolist())
     assert list(sd) == np.concatenate([[0], np.cumsum(peer_bytes)[:-1]]).tolist()
 
@@ -61,14 +81,15 @@ def main():
     rbuf = recv.numpy()
 
     # 4. every block this rank owns, from every source map, bit-exact
-    lo, hi = (rank * R) // W, ((rank + 1) * R) // W
+    lo, hi = int(own[rank]), int(own[rank + 1])
     blocks = {}
     for g in range(W):
-        grecs = O.gen_terasort(11 + g, 0, M * rpm)
+        grecs = gen(g)
         for m in range(M):
             d, _, ix, _ = O.write_map(part, grecs[m * rpm * 100:(m + 1) * rpm * 100], 100)
             for p in range(lo, hi):
-                off = lib.sux_plan_block_offset(W, rank, M, R, gi.ctypes.data, g, m, p)
+                off = lib.sux_plan_block_offset_owned(W, rank, M, R, gi.ctypes.data,
+                                                      own.ctypes.data, g, m, p)
                 assert off >= 0
                 want = d[ix[p]:ix[p + 1]]
                 got = rbuf[off:off + len(want)]
@@ -83,8 +104,14 @@ def main():
                 for p in range(lo, hi):
                     assert blocks[f"{m}_{p}"][g] == gold["ranks"][g]["blocks"][f"{m}_{p}"]
     dist.barrier()
+    # received bytes per rank: max over mean (what the exchange's busiest owner carries)
+    ing = torch.tensor([float(sum(rc))])
+    mx, tot = ing.clone(), ing.clone()
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    dist.all_reduce(tot)
     if rank == 0:
-        print(f"exchange ok: world={W} maps={M} R={R}", flush=True)
+        print(f"exchange ok: world={W} maps={M} R={R} ownership={own.tolist()} "
+              f"ingress max/mean={float(mx) / (float(tot) / W):.3f}", flush=True)
     dist.destroy_process_group()
 
 

@@ -23,6 +23,7 @@ def _run(world, *args):
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "exchange ok" in r.stdout
+    return r.stdout
 
 
 def test_exchange_world2_matches_golden():
@@ -32,3 +33,14 @@ def test_exchange_world2_matches_golden():
 @pytest.mark.parametrize("world,R,maps", [(2, 200, 2), (3, 10, 4)])
 def test_exchange_world_sizes(world, R, maps):
     _run(world, "--R", str(R), "--maps", str(maps), "--rpm", "700")
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_exchange_zipf_balanced_ownership(world):
+    """Zipf keys (C4), ownership balanced from the all-reduced partition bytes;
+    every block bit-exact through the owned plan, and the busiest owner's ingress closer to the
+    mean than under the equal split."""
+    bal = _run(world, "--zipf", "--balanced", "--R", "200", "--maps", "2", "--rpm", "5000")
+    eq = _run(world, "--zipf", "--R", "200", "--maps", "2", "--rpm", "5000")
+    ratio = lambda out: float(out.split("ingress max/mean=")[1].split()[0])  # noqa: E731
+    assert ratio(bal) <= ratio(eq) + 1e-9

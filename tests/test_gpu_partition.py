@@ -196,6 +196,38 @@ def test_peer_major_layout(gpu_node, world):
     assert host(peer).tolist() == want_peer.tolist()
 
 
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("kind", ["zipf", "terasort"])
+def test_peer_major_layout_owned(gpu_node, world, kind):
+    """sux_node_set_ownership: the peer-major send layout follows a balanced ownership table
+    (Zipf keys: sux_plan_ownership of the maps' partition bytes), bit-exact vs the oracle; the
+    equal split comes back with None."""
+    R, rpm, n = 200, 7000, 30000
+    if kind == "zipf":
+        opart = O.Partitioner(O.MURMUR3_LONG, R, 0, 8, 42)
+        recs = O.gen_zipf(0x5EED0004, 0, n)
+    else:
+        opart = O.terasort_partitioner(R)
+        recs = O.gen_terasort(8, 0, n)
+    gp = gpu_part(gpu_node, opart)
+    lens = O.write_map(opart, recs, 100)[1]
+    own = N.plan_ownership(world, np.asarray(lens, np.int64) * 100)
+    gpu_node.set_ownership(world, R, own)
+    try:
+        out, index, peer = gpu_node.partition_maps_peer_major(gp, to_dev(recs), 100, rpm, world)
+        torch.cuda.synchronize()
+        want, want_index, want_peer = O.peer_major(opart, recs, 100, rpm, world, own=own)
+        assert host(out).tobytes() == bytes(want)
+        assert host(index).tolist() == want_index.tolist()
+        assert host(peer).tolist() == want_peer.tolist()
+    finally:
+        gpu_node.set_ownership(world, R, None)
+    out, _, peer = gpu_node.partition_maps_peer_major(gp, to_dev(recs), 100, rpm, world)
+    torch.cuda.synchronize()
+    want, _, want_peer = O.peer_major(opart, recs, 100, rpm, world)
+    assert host(out).tobytes() == bytes(want) and host(peer).tolist() == want_peer.tolist()
+
+
 def test_exchange_group_single_rank(gpu_node):
     R, rpm = 64, 5000
     recs = O.gen_terasort(10, 0, 12000)
