@@ -12,3 +12,4 @@ timeout -k 10 200 python3 bench.py $L > $O/c5_lo4_$i.json 2> $O/c5_lo4_$i.err ||
 timeout -k 10 200 python3 bench.py $L --tuning msd_direct=8 > $O/c5_lo5_$i.json 2> $O/c5_lo5_$i.err || exit 1
 echo "round $i done"
 done
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_partition.py -k "owned or peer_major or tickets or export_cache or single_rank" tests/test_gpu_bench_rehearsal.py > $O/own_tests.txt 2>&1; echo "own tests rc=$?"; tail -3 $O/own_tests.txt
