@@ -711,7 +711,8 @@ __global__ __launch_bounds__(kScanThreads) void k_msd16_scan(MapGroup g, uint32_
   }
 }
 
-template <int KW, uint32_t NW, uint32_t PT, uint32_t LO, uint32_t MCH, bool DIRECT = false>
+template <int KW, uint32_t NW, uint32_t PT, uint32_t LO, uint32_t MCH, bool DIRECT = false,
+          bool ERUN = false>
 __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, uint32_t cpm,
                                                  uint32_t nbk, const uint16_t* __restrict__ offs,
                                                  const uint64_t* __restrict__ segbase,
@@ -730,6 +731,10 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
   uint8_t* los = reinterpret_cast<uint8_t*>(wsum + NW);
   uint32_t* rp = reinterpret_cast<uint32_t*>(los + CAP);   // [MC + 1] run starts in the segment
   uint16_t* ro = reinterpret_cast<uint16_t*>(rp + MC + 1);  // [MC] run starts in their chunk
+  // ERUN (msd_direct bit 4): element -> run map of a segment that fits the stage, over the
+  // stage's first 2 CAP bytes (idle between place() and the next rank_stage): one LDS read per
+  // element instead of the run table's log2(MC)-step search
+  uint16_t* erun = reinterpret_cast<uint16_t*>(lds8);
   const int R = pd.R;
   const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
   const uint64_t lt_mask = (1ull << lane) - 1ull;
@@ -809,6 +814,13 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
       __syncthreads();
     }
     s.T = carry;
+    if constexpr (ERUN) {
+      if (s.T <= CAP) {
+        for (uint32_t c = tid; c < s.nch; c += NT)
+          for (uint32_t k = rp[c], e = rp[c + 1]; k < e; ++k) erun[k] = (uint16_t)c;
+        __syncthreads();
+      }
+    }
     return s;
   };
   // loads of segment elements [e0, min(T, e0 + CAP)) in wave-contiguous order
@@ -825,6 +837,16 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
     for (uint32_t j = 0; j < PT; ++j) {
       lo[j] = 0;
       ev[j] = min(e0 + wave * (PT * kWave) + j * kWave + lane, lim - 1);
+    }
+    if constexpr (ERUN) {
+      if (s.T <= CAP) {
+#pragma unroll
+        for (uint32_t j = 0; j < PT; ++j) lo[j] = erun[ev[j]];
+#pragma unroll
+        for (uint32_t j = 0; j < PT; ++j)
+          r[j] = t4[s.mbase + (uint64_t)lo[j] * kM16Chunk + ro[lo[j]] + (ev[j] - rp[lo[j]])];
+        return;
+      }
     }
 #pragma unroll
     for (uint32_t step = MC / 2; step; step >>= 1) {
@@ -1071,18 +1093,19 @@ hipError_t launch_msd16(const PartDev& pd, const MapGroup& g, uint8_t* d_out, in
   static_assert(4 * MB4::lds_bytes() <= 160 * 1024, "pass B: four workgroups per CU");
   static_assert(4 * MB8::lds_bytes() <= 160 * 1024, "pass B (256-partition buckets): four per CU");
   static_assert(2 * M16a<NWA, 10>::lds_bytes() <= 160 * 1024, "pass A: two workgroups per CU");
-#define SUX_M16B_D(KW, LOV, MCV, D)                                                                \
+#define SUX_M16B_D(KW, LOV, MCV, D, ER)                                                            \
   do {                                                                                             \
     constexpr uint32_t nwb = LOV == kM16LoWide ? 8 : NWB;                                          \
     constexpr size_t ldsb = M16b<nwb, PTB, LOV, MCV>::lds_bytes();                                 \
-    allow_lds(reinterpret_cast<const void*>(&k_msd16b<KW, nwb, PTB, LOV, MCV, D>), ldsb);         \
-    hipLaunchKernelGGL((k_msd16b<KW, nwb, PTB, LOV, MCV, D>), gb, dim3(nwb * kWave), ldsb, s, pd, \
-                       g, cpm, nbk, offs, segbase, tmp, d_out, d_index, d_index_be);               \
+    allow_lds(reinterpret_cast<const void*>(&k_msd16b<KW, nwb, PTB, LOV, MCV, D, ER>), ldsb);     \
+    hipLaunchKernelGGL((k_msd16b<KW, nwb, PTB, LOV, MCV, D, ER>), gb, dim3(nwb * kWave), ldsb, s, \
+                       pd, g, cpm, nbk, offs, segbase, tmp, d_out, d_index, d_index_be);           \
   } while (0)
-#define SUX_M16B(KW, LOV, MCV)                               \
-  do {                                                       \
-    if (tn.msd_direct & 2) SUX_M16B_D(KW, LOV, MCV, true);   \
-    else SUX_M16B_D(KW, LOV, MCV, false);                    \
+#define SUX_M16B(KW, LOV, MCV)                                      \
+  do {                                                              \
+    if (tn.msd_direct & 2) SUX_M16B_D(KW, LOV, MCV, true, false);   \
+    else if (tn.msd_direct & 16) SUX_M16B_D(KW, LOV, MCV, false, true); \
+    else SUX_M16B_D(KW, LOV, MCV, false, false);                    \
   } while (0)
 #define SUX_M16BK(LOV, MCV)                   \
   do {                                        \
