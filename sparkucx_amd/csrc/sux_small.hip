@@ -1065,7 +1065,10 @@ hipError_t launch_msd16(const PartDev& pd, const MapGroup& g, uint8_t* d_out, in
     else if (kw == 3) SUX_M16A(3, DB, LOV);  \
     else SUX_M16A(4, DB, LOV);               \
   } while (0)
+  // pass A's digit is the bucket pid >> LO: the template's LO must be the LO chosen above
   if (LO == kM16LoShort) SUX_M16AK(6, kM16LoShort);  // R <= 16384: <= 64 buckets
+  else if (LO == kM16LoWide && nbk > 256) SUX_M16AK(9, kM16LoWide);  // R <= 16384: <= 512
+  else if (LO == kM16LoWide) SUX_M16AK(8, kM16LoWide);
   else if (nbk > 512) SUX_M16AK(10, kM16Lo);
   else if (nbk > 256) SUX_M16AK(9, kM16Lo);
   else SUX_M16AK(8, kM16Lo);
