@@ -516,6 +516,13 @@ struct sux_node {
   std::map<void*, IpcExport> ipc_exports;
   // sux_exchange_group_post tickets not yet issued or discarded (freed by sux_node_destroy)
   std::set<sux_xticket*> tickets;
+  // live partitioners and pooled buffers of this node: sux_node_destroy orphans them (their
+  // node pointer cleared), so a handle released after its node — a garbage-collected wrapper,
+  // a JVM finalizer — never dereferences the freed node (a partitioner destroyed late used to
+  // bind the freed node's device: hipSetDevice(garbage) left "invalid device ordinal" behind)
+  std::mutex live_mu;
+  std::set<sux_partitioner*> live_parts;
+  std::set<sux_buffer*> live_bufs;
   // sux_node_set_ownership: which contiguous partition range each peer owns in the stateless
   // group calls (peer-major partition, exchange_group / post / issue, pull) for groups of
   // own_R partitions among own_W peers; empty = the equal split
@@ -576,7 +583,8 @@ struct sux_node {
 };
 
 struct sux_partitioner {
-  sux_node* node = nullptr;
+  sux_node* node = nullptr;  // nullptr once the node is destroyed (sux_node_destroy orphans it)
+  int device = 0;            // the node's device: a partitioner destroyed after its node frees here
   sux_partitioner_desc desc{};
   sux::PartDev pd{};
   void* d_bounds = nullptr;
@@ -584,7 +592,7 @@ struct sux_partitioner {
 };
 
 struct sux_buffer {
-  sux_node* node = nullptr;
+  sux_node* node = nullptr;  // nullptr once the node is destroyed (its pool freed the memory)
   PoolBuf buf;
   PoolBuf aux;  // copy descriptors
   uint64_t size = 0;
@@ -942,7 +950,9 @@ sux::Tuning resolve_tuning(const sux_tuning& t, bool pipelined) {
   r.scatter_nt = t.scatter_nt > 0 ? t.scatter_nt : 0;
   r.split_cus = t.split_cus > 0 ? t.split_cus : 0;
   r.gather_kernel = t.gather_kernel ? t.gather_kernel : 3;
-  r.msd_direct = t.msd_direct > 0 ? t.msd_direct : 0;
+  // 0: 32-partition buckets + pass B's element -> run map (bits 3 + 4; round 5, C5 965 -> 993
+  // GB/s, profiles/r05_h); -1: round 4's shape (16-partition buckets, run-table search)
+  r.msd_direct = t.msd_direct > 0 ? t.msd_direct : t.msd_direct == 0 ? 24 : 0;
   r.gather16 = r.gather_kernel != 2;
   return r;
 }
@@ -958,6 +968,7 @@ Group make_group(const sux_partitioner* part, const void* recs, uint32_t rs, uin
   require(((uintptr_t)recs & 3) == 0, SUX_EINVAL, "records must be 4-byte aligned");
   Group G;
   uint32_t R = (uint32_t)part->desc.num_partitions;
+  require(part->node != nullptr, SUX_ESTATE, "the partitioner's node was destroyed");
   uint32_t tile = sux::choose_tile_recs(R, rs, rpm, resolve_tuning(part->node->tuning, false));
   G.g.recs = static_cast<const uint8_t*>(recs);
   G.g.records_per_map = rpm;
@@ -1361,6 +1372,13 @@ int sux_node_destroy(sux_node* node) {
     (void)hipDeviceSynchronize();
     for (sux_xticket* t : node->tickets) free_ticket(t);  // posted, never issued: leases return
     node->tickets.clear();
+    {
+      std::lock_guard<std::mutex> lk(node->live_mu);
+      for (sux_partitioner* p : node->live_parts) p->node = nullptr;
+      for (sux_buffer* b : node->live_bufs) b->node = nullptr;
+      node->live_parts.clear();
+      node->live_bufs.clear();
+    }
     for (int i = 0; i < 2; ++i) {
       if (node->pipe[i]) (void)hipStreamDestroy(node->pipe[i]);
       node->pool->put(node->pipe_ws[i]);
@@ -1417,6 +1435,7 @@ int sux_partitioner_create(sux_node* node, const sux_partitioner_desc* d, sux_pa
     node->bind();
     auto p = std::make_unique<sux_partitioner>();
     p->node = node;
+    p->device = node->conf.device;
     p->desc = *d;
     p->desc.range_bounds = nullptr;
     p->pd.kind = d->kind;
@@ -1471,6 +1490,10 @@ int sux_partitioner_create(sux_node* node, const sux_partitioner_desc* d, sux_pa
       p->pd.lut = static_cast<const uint32_t*>(p->d_lut);
       p->pd.lut_bits = bits;
     }
+    {
+      std::lock_guard<std::mutex> lk(node->live_mu);
+      node->live_parts.insert(p.get());
+    }
     *out = p.release();
   });
 }
@@ -1478,7 +1501,11 @@ int sux_partitioner_create(sux_node* node, const sux_partitioner_desc* d, sux_pa
 int sux_partitioner_destroy(sux_partitioner* p) {
   return guard([&] {
     if (!p) return;
-    p->node->bind();
+    if (p->node) {
+      std::lock_guard<std::mutex> lk(p->node->live_mu);
+      p->node->live_parts.erase(p);
+    }
+    hip_check(hipSetDevice(p->device), "hipSetDevice");
     if (p->d_bounds) (void)hipFree(p->d_bounds);
     if (p->d_lut) (void)hipFree(p->d_lut);
     delete p;
@@ -1634,6 +1661,7 @@ VGroup make_vgroup(const sux_partitioner* part, const void* data, const uint64_t
   require(((uintptr_t)data & 3) == 0 && ((uintptr_t)offs & 7) == 0, SUX_EINVAL,
           "data must be 4-byte and offsets 8-byte aligned");
   VGroup G;
+  require(part->node != nullptr, SUX_ESTATE, "the partitioner's node was destroyed");
   const uint32_t tile =
       sux::choose_varlen_tile((uint32_t)R, n, resolve_tuning(part->node->tuning, false));
   G.g.data = static_cast<const uint8_t*>(data);
@@ -3779,6 +3807,10 @@ int sux_fetch_blocks(sux_node* node, int32_t shuffle_id, const sux_block_id* blo
       node->pool->put(buf->aux);
       throw;
     }
+    {
+      std::lock_guard<std::mutex> lk(node->live_mu);
+      node->live_bufs.insert(buf.get());
+    }
     *out = buf.release();
   });
 }
@@ -3792,6 +3824,10 @@ int sux_buffer_alloc(sux_node* node, uint64_t bytes, sux_buffer** out) {
     buf->size = bytes;
     buf->refs = 1;
     buf->buf = pool_get_or_spill(node, bytes ? bytes : 1);
+    {
+      std::lock_guard<std::mutex> lk(node->live_mu);
+      node->live_bufs.insert(buf.get());
+    }
     *out = buf.release();
   });
 }
@@ -3808,6 +3844,7 @@ int sux_buffer_info(sux_buffer* b, void** ptr, uint64_t* size, uint64_t* cap) {
 int sux_buffer_read(sux_buffer* b, uint64_t offset, void* dst, uint64_t len, void* stream) {
   return guard([&] {
     require(b && (dst || len == 0), SUX_EINVAL, "NULL argument");
+    require(b->node, SUX_ESTATE, "the buffer's node was destroyed");
     require(offset <= b->size && len <= b->size - offset, SUX_ERANGE,
             "read of [" + std::to_string(offset) + ", +" + std::to_string(len) +
                 ") past a buffer of " + std::to_string(b->size) + " bytes");
@@ -3834,8 +3871,14 @@ int sux_buffer_release(sux_buffer* b) {
     int32_t left = --b->refs;
     require(left >= 0, SUX_ESTATE, "buffer released more often than referenced");
     if (left == 0) {
-      b->node->pool->put(b->buf);
-      b->node->pool->put(b->aux);
+      if (b->node) {  // else the node is gone and its pool freed the memory
+        {
+          std::lock_guard<std::mutex> lk(b->node->live_mu);
+          b->node->live_bufs.erase(b);
+        }
+        b->node->pool->put(b->buf);
+        b->node->pool->put(b->aux);
+      }
       delete b;
     }
   });

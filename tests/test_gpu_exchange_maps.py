@@ -310,3 +310,30 @@ def test_resolved_shuffle_is_never_spilled(tmp_path):
         node.unregister_shuffle(14)
     finally:
         node.close()
+
+
+def test_handles_released_after_their_node():
+    """A partitioner destroyed, or a fetched buffer released, after its node is destroyed (a
+    garbage-collected wrapper, a JVM finalizer) touches nothing of the freed node: round 5 found a
+    late partitioner destroy binding the freed node's device (hipSetDevice of garbage left
+    "invalid device ordinal" for the next torch launch).  Using such a partitioner is a state
+    error; the conftest fixture checks that no HIP error is left behind."""
+    node = Node(device=0)
+    opart, part = _terasort(node, 16)
+    recs = node.generate(N.GEN_TERASORT, SEED, 0, 4000, 100)
+    node.register_shuffle(31, 1, 16, 100)
+    node.write_map_outputs(31, 0, part, recs, 4000, 4000)
+    node.wait_map_outputs(31)
+    buf, _ = node.fetch_blocks(31, [(0, 0, 16)])
+    node.close()
+    with pytest.raises(N.SuxError) as e:
+        node2 = Node(device=0)
+        try:
+            node2.partition_maps(part, recs, 100, 4000)
+        finally:
+            node2.close()
+    assert e.value.code == N.SUX_ESTATE
+    part.close()
+    buf.release(1)
+    torch.randint(0, 256, (16,), dtype=torch.uint8, device="cuda")  # torch's launch check
+    torch.cuda.synchronize()

@@ -323,8 +323,8 @@ def test_line_carry_scatter_shapes(gpu_node, tuned, R, n, rpm, tile, tpi):
     (1025, 4096 * 3, 4096, "one"),              # whole chunks of one partition
     (3000, 1, 1, None),                         # a single record
 ])
-@pytest.mark.parametrize("wpc,direct", [(2, 0), (1, 0), (2, 3), (1, 3), (2, 1), (2, 2), (2, 4),
-                                        (2, 6), (2, 8), (2, 16), (2, 24), (1, 24)])
+@pytest.mark.parametrize("wpc,direct", [(2, 0), (1, 0), (2, -1), (1, -1), (2, 3), (1, 3), (2, 1),
+                                        (2, 2), (2, 4), (2, 6), (2, 8), (2, 16), (1, 16)])
 def test_msd16_pids_and_shapes(gpu_node, tuned, R, n, rpm, skew, wpc, direct):
     """The two-level small-record path (small_kernel 4, 2 or 1 workgroups per CU; msd_direct:
     each pass stores records from registers instead of through its LDS stage (bits 0, 1), pass A
@@ -378,7 +378,7 @@ def test_msd16_falls_back_for_the_exchange_layout(gpu_node, tuned):
     (1025, 3 * 8192, 8192, None),            # 5 buckets (the last of 1 partition), 2-chunk maps
     (10000, 2 * 262144, 262144, None),       # 64 chunks per map: the short run table's limit
 ])
-@pytest.mark.parametrize("direct", [0, 3, 4, 16, 24])
+@pytest.mark.parametrize("direct", [0, -1, 3, 4, 16])
 def test_msd16_short_maps_256_partition_buckets(gpu_node, tuned, R, n, rpm, skew, direct):
     """Default tuning, maps too short for 16-partition segments: the two-level path with
     256-partition buckets (pass A digits pid >> 8, pass B sorts by pid & 255).  Bytes, both index
