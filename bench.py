@@ -973,6 +973,10 @@ def config_leg(wl: str, data_buf, dev, steps: int, warmup: int = 1) -> dict:
         if part is not None:
             part.close()
         node.close()
+        # the leg's 100 GB output goes back to the device, not to torch's cache: the next leg's
+        # node allocates its workspaces with hipMalloc
+        out = index = index_be = step = None
+        torch.cuda.empty_cache()
 
 
 def load_traffic(workload: str, kernel: str) -> dict | None:
