@@ -4071,9 +4071,14 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
     SortPlan P1;
     sort_plan(n, record_size, P1, tb);
     sux::SortPlanDev* plan = reinterpret_cast<sux::SortPlanDev*>(ws + plan_off);
+    // the fused sort (sorted buckets gather their own records by index) may rebase its buckets'
+    // keys: the pairs' key bits are not read after the LDS sort
+    const bool fused = !inline_rec && resolve_tuning(node->tuning, false).gather_kernel == 3 &&
+                       sux::sort_gather_fusable(record_size);
     hip_check(sux::launch_sort_pairs(static_cast<const uint8_t*>(d_in), n, record_size, key_kind,
                                      key_offset, key_len, d_seg, nseg, sbytes, a,
-                                     ws + P1.span_off, inline_rec, s, bits, tb, plan, chunked),
+                                     ws + P1.span_off, inline_rec, s, bits, tb, plan,
+                                     chunked ? (fused ? 2 : 1) : 0),
               "sort pairs + plan");
     int64_t* index1 = reinterpret_cast<int64_t*>(ws + P1.index_off);
     sux::PartDev pd1 = pd;

@@ -233,7 +233,7 @@ struct SortPlanDev;
 hipError_t launch_sort_pairs(const uint8_t* in, uint64_t n, uint32_t rs, int kind, int key_offset,
                              int key_len, const int64_t* seg, int nseg, int sbytes, void* pairs,
                              void* span_ws, bool inline_rec, hipStream_t s, int bits = 0,
-                             int tb = 0, SortPlanDev* plan = nullptr, bool ranged = false);
+                             int tb = 0, SortPlanDev* plan = nullptr, int ranged = 0);
 hipError_t launch_unpair_records(const void* pairs, uint64_t n, uint32_t rs, int kind,
                                  int key_offset, int key_len, int sbytes, void* out, hipStream_t s);
 // span_ws: 8 u32 (AND of key words 0..2, OR of key words 0..2) + kSortSpanBlocks x 8 u32 partials
@@ -277,6 +277,19 @@ struct SortPlanDev {
                      // aligned blocks [min, max] spans fit 2^tb buckets and top_base = min >>
                      // top_lo, so every bucket is used; 0 = the bits [top_lo, top_lo + tb)
   SortDigits dg;     // the LDS sort's digits: 8-bit, below top_lo, only those that vary
+  // Rebased plan (fused-gather sorts whose key range fills too few aligned buckets, e.g. one
+  // range partition's keys): the top digit is ((K - kmin) >> rq) * rm >> 32 over the key K (the
+  // pair's top kbits), every bucket an equal slice of [kmin, kmax]; k_sort_local then sorts a
+  // bucket by u = K - (the bucket's smallest K) < 2^rbits, placed in the pair's top rbits (the
+  // record index stays), with `dg` hanging down from bit 128; dg_raw = the whole key's digits,
+  // for the global-memory sort of oversized buckets (their pairs are not rebased).
+  int32_t rebase;
+  int32_t rbits;
+  uint32_t rq;
+  uint32_t pad2;
+  uint64_t rm;
+  uint64_t kmin_hi, kmin_lo;  // kmin (the key, right-aligned) as a 128-bit value
+  SortDigits dg_raw;
 };
 constexpr uint64_t kSortPlanBytes = 256;
 static_assert(sizeof(SortPlanDev) <= kSortPlanBytes, "plan slot");

@@ -231,7 +231,7 @@ __global__ __launch_bounds__(256) void k_sort_pairs(const uint8_t* __restrict__ 
 }
 
 __device__ void make_sort_plan(const uint32_t* span, int bits, int tb, SortPlanDev* plan,
-                               const u128* range);
+                               const u128* range, bool rebase_ok);
 
 // The key span; with `plan`, thread 0 then plans the sort from it (the device-planned MSD path:
 // one launch fewer than a separate planning kernel); `ranged` plans the top digit over the key
@@ -267,7 +267,8 @@ __global__ __launch_bounds__(256) void k_span_reduce(const uint32_t* __restrict_
     __syncthreads();
   }
   if (threadIdx.x < 6) span[threadIdx.x] = red[0][threadIdx.x];
-  if (plan && threadIdx.x == 0) make_sort_plan(&red[0][0], bits, tb, plan, ranged ? rmm[0] : nullptr);
+  if (plan && threadIdx.x == 0)
+    make_sort_plan(&red[0][0], bits, tb, plan, ranged ? rmm[0] : nullptr, ranged == 2);
 }
 
 // One output dword per thread and step: record j = d / W, dword w of it, read from the record
@@ -335,7 +336,7 @@ __global__ __launch_bounds__(256) void k_gather_records16(const uint8_t* __restr
 hipError_t launch_sort_pairs(const uint8_t* in, uint64_t n, uint32_t rs, int kind, int key_offset,
                              int key_len, const int64_t* seg, int nseg, int sbytes, void* pairs,
                              void* span_ws, bool inline_rec, hipStream_t s, int bits, int tb,
-                             SortPlanDev* plan, bool ranged) {
+                             SortPlanDev* plan, int ranged) {
   if (n == 0) return hipSuccess;
   const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, kSortSpanBlocks);
   uint32_t* part = static_cast<uint32_t*>(span_ws) + 8;
@@ -345,7 +346,7 @@ hipError_t launch_sort_pairs(const uint8_t* in, uint64_t n, uint32_t rs, int kin
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_span_reduce, dim3(1), dim3(256), 0, s, part, blocks,
-                     static_cast<uint32_t*>(span_ws), bits, tb, plan, ranged ? 1 : 0);
+                     static_cast<uint32_t*>(span_ws), bits, tb, plan, ranged);
   return hipGetLastError();
 }
 
@@ -445,6 +446,17 @@ __device__ __forceinline__ uint32_t top_digit(const u32x4& w, uint32_t sh, uint6
   return (uint32_t)(v - base) & (uint32_t)((1ull << nb) - 1);
 }
 
+// The key of a pair (its top kbits bits) as a right-aligned 128-bit value.
+__device__ __forceinline__ u128 pair_key(const u32x4& w, int kbits) {
+  return pair_be128(w) >> (128 - kbits);
+}
+// Rebased plan's top digit: the key's slice of [kmin, kmax] (monotone in the key, < 2^tb).
+__device__ __forceinline__ uint32_t rebased_digit(const u32x4& w, const SortPlanDev* plan) {
+  const u128 kmin = ((u128)plan->kmin_hi << 64) | plan->kmin_lo;
+  const uint64_t v = (uint64_t)((pair_key(w, plan->kbits) - kmin) >> plan->rq);  // < 2^32
+  return (uint32_t)((v * plan->rm) >> 32);
+}
+
 // ------------------------------------------------------------------------------------------
 // Chunked top pass (round 4; the default when the top digit has <= 12 bits and the pairs fit
 // kTopMaxChunks chunks).  The one-pass top-digit partition (k_hist16 + scans + k_scatter16s)
@@ -480,6 +492,7 @@ __global__ __launch_bounds__(NT, 2 * NT / 256) void k_top_chunks(const u32x4* __
   const uint64_t lt_mask = (1ull << lane) - 1ull;
   const uint32_t R = 1u << tb, top_lo = (uint32_t)plan->top_lo;
   const uint64_t top_base = plan->top_base;
+  const bool rebase = plan->rebase != 0;
   const int passes = tb <= (int)DB ? 1 : 2;
   const uint32_t D = passes == 1 ? (uint32_t)tb : (uint32_t)(tb + 1) / 2;  // <= DB bits a pass
   const uint32_t nch = (uint32_t)((n + CH - 1) / CH);
@@ -496,7 +509,9 @@ __global__ __launch_bounds__(NT, 2 * NT / 256) void k_top_chunks(const u32x4* __
     for (uint32_t j = 0; j < PT; ++j) {  // clamped, unconditional loads
       const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
       const u32x4 p = pairs[c0 + min(e, nc - 1)];
-      if (e < nc) kin[e] = (top_digit(p, top_lo, top_base, (uint32_t)tb) << IDX) | e;
+      if (e < nc)
+        kin[e] = ((rebase ? rebased_digit(p, plan) : top_digit(p, top_lo, top_base, (uint32_t)tb))
+                  << IDX) | e;
     }
     __syncthreads();
     // 1. LSD passes over (bucket << 12 | position), D bits each: wave-ballot ranks against the
@@ -779,7 +794,10 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : CAP == 1024 ? 6 : 4) void k_
   if (!plan->msd_ok || plan->dg.n == 0) return;  // the LSD fallback, or the top digit was all
   const SortDigits dg = plan->dg;
   const int kbits = plan->kbits;
+  // the tie fix-up compares keys: a rebased bucket's keys are u, in the pair's top rbits bits
+  const int tkbits = GATHER && plan->rebase ? plan->rbits : kbits;
   __shared__ uint32_t tie_redo;
+  __shared__ u128 rmin[NW];
   if (threadIdx.x == 0) tie_redo = 0;
   using K = SortLocal<NW, CAP>;
   constexpr uint32_t NT = K::NT, PT = K::PT, NB = K::NB;
@@ -854,6 +872,38 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : CAP == 1024 ? 6 : 4) void k_
         v[j] = in[s0 + min(e, n - 1)];
       }
     }
+    if constexpr (GATHER) {
+      if (plan->rebase) {
+        // u = K - (the bucket's smallest key), in the pair's top rbits bits; the record index
+        // (word 3) stays.  u < 2^rbits: the plan bounds every bucket's key width
+        u128 m = ~(u128)0;
+#pragma unroll
+        for (uint32_t j = 0; j < PT; ++j) {
+          const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+          const u128 k = pair_key(v[j], kbits);
+          if (e < n && k < m) m = k;
+        }
+        for (int sft = 32; sft >= 1; sft >>= 1) {
+          const u128 o = shfl_xor128(m, sft);
+          m = o < m ? o : m;
+        }
+        if (lane == 0) rmin[wave] = m;
+        __syncthreads();
+        m = rmin[0];
+#pragma unroll
+        for (uint32_t q = 1; q < NW; ++q) m = rmin[q] < m ? rmin[q] : m;
+        const int rb = plan->rbits;
+#pragma unroll
+        for (uint32_t j = 0; j < PT; ++j) {
+          const u128 u = pair_key(v[j], kbits) - m;
+          const u128 nv = (u << (128 - rb)) | (u128)__builtin_bswap32(v[j][3]);
+          v[j][0] = __builtin_bswap32((uint32_t)(nv >> 96));
+          v[j][1] = __builtin_bswap32((uint32_t)(nv >> 64));
+          v[j][2] = __builtin_bswap32((uint32_t)(nv >> 32));
+        }
+        __syncthreads();  // rmin is rewritten by the next bucket only after this
+      }
+    }
     // one stable 8-bit digit pass in LDS (digit d of dg): ranks, block scan, permutation into
     // buf, the pairs back into registers in the new order
     auto digit_pass = [&](int d) {
@@ -911,7 +961,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : CAP == 1024 ? 6 : 4) void k_
         for (uint32_t i = 1; i < L; ++i) {  // stable: only strictly greater keys move up
           const u32x4 x = buf[e + i];
           uint32_t k = i;
-          while (k > 0 && key_greater(buf[e + k - 1], x, kbits)) {
+          while (k > 0 && key_greater(buf[e + k - 1], x, tkbits)) {
             buf[e + k] = buf[e + k - 1];
             --k;
           }
@@ -1011,7 +1061,7 @@ __global__ __launch_bounds__(NW * 64) void k_sort_bucket_global(u32x4* __restric
                                                                 uint32_t R,
                                                                 const SortPlanDev* __restrict__ plan) {
   if (!plan->msd_ok || plan->dg.n == 0) return;
-  const SortDigits dg = plan->dg;
+  const SortDigits dg = plan->rebase ? plan->dg_raw : plan->dg;  // its pairs are not rebased
   constexpr uint32_t NT = NW * kWave, NB = 256, PT = 4, CH = NT * PT;
   __shared__ uint32_t wc[NW * NB];
   __shared__ uint32_t wsum[NW];
@@ -1155,12 +1205,13 @@ __device__ bool span_varies_dev(const uint32_t* span, int lo, int hi) {
 // bit, the top digit (its tb bits end there) and the LDS sort's 8-bit digits below it that vary.
 // One thread (k_span_reduce's thread 0).
 __device__ void make_sort_plan(const uint32_t* span, int bits, int tb, SortPlanDev* plan,
-                               const u128* range) {
+                               const u128* range, bool rebase_ok) {
   int hb = -1;
   for (int b = 127; b >= 128 - bits && hb < 0; --b)
     if (span_varies_dev(span, b, b + 1)) hb = b;
   int top_lo = hb >= 0 ? max(hb + 1 - tb, 128 - bits) : 128 - bits;
   uint64_t top_base = 0;
+  plan->rebase = 0;
   if (range && hb >= 0) {
     // the lowest shift at which the aligned blocks the keys [min, max] touch number <= 2^tb (the
     // bit-span shift above always qualifies: every key shares the bits above hb)
@@ -1173,6 +1224,30 @@ __device__ void make_sort_plan(const uint32_t* span, int bits, int tb, SortPlanD
     while (sh < top_lo && ((mx >> sh) - (mn >> sh)) >= ((u128)1 << tb)) ++sh;
     top_lo = min(sh, top_lo);
     top_base = (uint64_t)(mn >> top_lo);
+    // Rebase (fused-gather sorts only) when the aligned blocks leave more than a third of the
+    // 2^tb buckets empty — a range partition's keys, whose width is no power of two: equal
+    // slices of [kmin, kmax] instead, each bucket sorted by its keys' offset from its smallest
+    const u128 blocks = (mx >> top_lo) - (mn >> top_lo) + 1;
+    if (rebase_ok && blocks * 3 < ((u128)2 << tb)) {
+      const u128 kmin = mn >> (128 - bits), kd = (mx >> (128 - bits)) - kmin;
+      const int kl = kd >> 64 ? 128 - __builtin_clzll((uint64_t)(kd >> 64))
+                              : ((uint64_t)kd ? 64 - __builtin_clzll((uint64_t)kd) : 0);
+      const uint32_t q = kl > 32 ? (uint32_t)(kl - 32) : 0u;
+      const uint64_t dd = (uint64_t)(kd >> q) + 1;  // <= 2^32
+      const uint64_t rm = (((uint64_t)1 << tb) << 32) / dd;
+      // a bucket's key width: < (ceil(2^32 / rm) + 1) << q
+      const u128 w = ((u128)(((uint64_t)1 << 32) / rm + 2)) << q;
+      const int rb = w >> 64 ? 128 - __builtin_clzll((uint64_t)(w >> 64))
+                             : 64 - __builtin_clzll((uint64_t)w);
+      if (rb <= 96 && rm > 0) {
+        plan->rebase = 1;
+        plan->rbits = rb;
+        plan->rq = q;
+        plan->rm = rm;
+        plan->kmin_hi = (uint64_t)(kmin >> 64);
+        plan->kmin_lo = (uint64_t)kmin;
+      }
+    }
   }
   // The LDS digits hang down from the top digit — [top_lo - 8, top_lo), [top_lo - 16, top_lo -
   // 8), ... — so the two the bucket sort runs first (and whose ties its insertion sort finishes)
@@ -1190,6 +1265,22 @@ __device__ void make_sort_plan(const uint32_t* span, int bits, int tb, SortPlanD
     if (span_varies_dev(span, sh, hi)) shs[m++] = (uint32_t)sh;
   }
   for (int i = m - 1; i >= 0; --i) dg.push(shs[i]);  // least significant first
+  if (plan->rebase) {
+    // the global sort of oversized buckets orders raw pairs by every key digit; the LDS sort
+    // orders rebased pairs by u's digits, hanging down from bit 128 to 128 - rbits
+    SortDigits raw{};
+    uint32_t rsh[16];
+    int rn = 0;
+    for (int hi = 128; hi > 128 - bits && rn < 16; hi -= 8) rsh[rn++] = (uint32_t)max(hi - 8, 128 - bits);
+    for (int i = rn - 1; i >= 0; --i) raw.push(rsh[i]);
+    plan->dg_raw = raw;
+    SortDigits ud{};
+    rn = 0;
+    for (int hi = 128; hi > 128 - plan->rbits && rn < 16; hi -= 8)
+      rsh[rn++] = (uint32_t)max(hi - 8, 128 - plan->rbits);
+    for (int i = rn - 1; i >= 0; --i) ud.push(rsh[i]);
+    dg = ud;
+  }
   plan->top_lo = top_lo;
   plan->top_base = top_base;
   plan->hb = hb;
