@@ -488,6 +488,7 @@ __global__ __launch_bounds__(NT, 2 * NT / 256) void k_top_chunks(const u32x4* __
   __shared__ uint32_t keys0[CH], keys1[CH];
   __shared__ uint32_t wc0[2 * NW * ND];  // [pass parity][wave][digit]
   __shared__ uint32_t wsum[NW];
+  __shared__ uint16_t rs[1u << kTopMaxBits];  // bucket -> its first sorted position (~0: empty)
   const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
   const uint64_t lt_mask = (1ull << lane) - 1ull;
   const uint32_t R = 1u << tb, top_lo = (uint32_t)plan->top_lo;
@@ -497,6 +498,7 @@ __global__ __launch_bounds__(NT, 2 * NT / 256) void k_top_chunks(const u32x4* __
   const uint32_t D = passes == 1 ? (uint32_t)tb : (uint32_t)(tb + 1) / 2;  // <= DB bits a pass
   const uint32_t nch = (uint32_t)((n + CH - 1) / CH);
   for (uint32_t i = tid; i < 2 * NW * ND; i += NT) wc0[i] = 0;
+  for (uint32_t i = tid; i < (1u << kTopMaxBits); i += NT) rs[i] = 0xFFFFu;
   // Two workgroups per CU within 64 VGPRs: the pairs are not held across the ranking — only
   // their keys (LDS); the sorted write reads each pair again, from the chunk just read (L2 /
   // Infinity Cache), in sorted order, and stores it coalesced
@@ -561,25 +563,57 @@ __global__ __launch_bounds__(NT, 2 * NT / 256) void k_top_chunks(const u32x4* __
       kout = t;
     }
     // 2. the chunk back to its own place in bucket order: sorted position s takes pair
-    //    kin[s] & 4095, coalesced 16-byte stores
+    //    kin[s] & 4095, coalesced 16-byte stores; a bucket's first position (its bucket differs
+    //    from the previous position's) is noted in rs
 #pragma unroll
     for (uint32_t k = 0; k < PT; ++k) {
       const uint32_t s = tid + k * NT;
-      if (s < nc) outp[c0 + s] = pairs[c0 + (kin[s] & (CH - 1))];
+      if (s < nc) {
+        const uint32_t ks = kin[s];
+        outp[c0 + s] = pairs[c0 + (ks & (CH - 1))];
+        if (s == 0 || (kin[s - 1] >> IDX) != (ks >> IDX)) rs[ks >> IDX] = (uint16_t)s;
+      }
     }
-    // 3. the chunk's bucket starts, row[q] = the pairs of buckets below q: a branch-free lower
-    //    bound per bucket (adjacent threads, adjacent u16 stores; the same work whatever the
-    //    chunk's key order — a run-start thread filling the gap before it was serial when a chunk
-    //    held few buckets)
-    uint16_t* row = offs + (uint64_t)c * (R + 1);
-    for (uint32_t q = tid; q <= R; q += NT) {
-      uint32_t pos = 0;
+    __syncthreads();
+    // 3. the chunk's bucket starts, row[q] = the pairs of buckets below q = the first position of
+    //    the first non-empty bucket >= q (nc past the last): a suffix minimum over rs.  Thread t
+    //    owns buckets [t E, (t + 1) E); rs is reset behind the reads for the next chunk.  (Round 4
+    //    ran a 13-step lower-bound search per bucket here: 117 dependent LDS reads per thread.)
+    {
+      constexpr uint32_t EQ = (1u << kTopMaxBits) / NT;
+      const uint32_t E = (R + NT - 1) / NT;
+      uint32_t m = 0xFFFFu;
 #pragma unroll
-      for (uint32_t step = CH; step > 0; step >>= 1)
-        if (pos + step <= nc && (kin[pos + step - 1] >> IDX) < q) pos += step;
-      row[q] = (uint16_t)pos;
+      for (uint32_t k = 0; k < EQ; ++k) {
+        const uint32_t q = (uint32_t)tid * E + k;
+        if (k < E && q < R) m = min(m, (uint32_t)rs[q]);
+      }
+      uint32_t suf = m;  // min over this lane and the lanes above it
+#pragma unroll
+      for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t t = __shfl_down(suf, d, kWave);
+        if (lane + d < kWave) suf = min(suf, t);
+      }
+      if (lane == 0) wsum[wave] = suf;
+      __syncthreads();
+      uint32_t run = nc;
+#pragma unroll
+      for (uint32_t q = 0; q < NW; ++q) run = q > (uint32_t)wave ? min(run, wsum[q]) : run;
+      const uint32_t above = __shfl_down(suf, 1, kWave);
+      if (lane + 1 < kWave) run = min(run, above);
+      uint16_t* row = offs + (uint64_t)c * (R + 1);
+#pragma unroll
+      for (int k = (int)EQ - 1; k >= 0; --k) {
+        const uint32_t q = (uint32_t)tid * E + (uint32_t)k;
+        if ((uint32_t)k < E && q < R) {
+          run = min(run, (uint32_t)rs[q]);
+          row[q] = (uint16_t)run;
+          rs[q] = 0xFFFFu;
+        }
+      }
+      if (tid == 0) row[R] = (uint16_t)nc;
     }
-    __syncthreads();  // kin / kout are rewritten by the next chunk
+    __syncthreads();  // kin / kout / wsum are rewritten by the next chunk
   }
 }
 

@@ -13,6 +13,7 @@
 #   pmc WORKLOAD...         profiles/collect_pmc.py passes (one counter group per rocprofv3 run)
 #   sortpmc                 PMC passes of tools/sort_prof.py (5 M TeraSort records)
 #   sorttrace [N]           rocprofv3 kernel trace of tools/sort_prof.py on range-partition keys
+#   sortprof                the sort tests, then tools/sort_prof.py on random and range-partition keys, 2 x
 #   ab LIB_B [bench args]   bench.py alternating with a copy of the tree linking LIB_B, 2 x each
 #   cmd SECONDS CMD...      any other command under a time limit
 set -o pipefail
@@ -64,6 +65,14 @@ case $job in
   sorttrace)
     SORT_PROF_INPUT=partition timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv \
       -d $O/prof_sort -o run -- python3 tools/sort_prof.py ${1:-20} > $O/prof_sort.txt 2>&1 ;;
+  sortprof)
+    run_tests tests/test_gpu_sort.py || exit 1
+    for i in 1 2; do
+      timeout -k 10 120 python3 tools/sort_prof.py 20 > $O/sort_random_$i.txt 2>&1 || exit 1
+      SORT_PROF_INPUT=partition timeout -k 10 120 python3 tools/sort_prof.py 20 \
+        > $O/sort_partition_$i.txt 2>&1 || exit 1
+    done
+    tail -qn 1 $O/sort_random_*.txt $O/sort_partition_*.txt ;;
   ab)
     lib=${1:?LIB_B}; shift
     B=/tmp/ab_b; rm -rf $B; mkdir -p $B && cp -r bench.py sparkucx_amd profiles oracle $B/ \
