@@ -473,7 +473,7 @@ __device__ __forceinline__ uint32_t rebased_digit(const u32x4& w, const SortPlan
 // Stable: chunks keep input order between them and the LDS passes keep it inside a chunk.
 // ------------------------------------------------------------------------------------------
 template <uint32_t NT, uint32_t DB>  // DB: bits per LSD pass (6: top digits of <= 12 bits)
-__global__ __launch_bounds__(NT, 2 * NT / 256) void k_top_chunks(const u32x4* __restrict__ pairs,
+__global__ __launch_bounds__(NT, 3 * NT / 256) void k_top_chunks(const u32x4* __restrict__ pairs,
                                                                 uint64_t n, int tb,
                                                                 const SortPlanDev* __restrict__ plan,
                                                                 u32x4* __restrict__ outp,
@@ -732,7 +732,7 @@ hipError_t launch_top_chunks(const void* pairs, uint64_t n, int tb, const SortPl
   const uint32_t ncu = (uint32_t)std::max(1, stream_cus(s));
   const uint32_t nch = (uint32_t)((n + kTopChunk - 1) / kTopChunk), R = 1u << tb;
   static_assert(kTopMaxBits <= 12, "two 6-bit LDS passes");
-  hipLaunchKernelGGL((k_top_chunks<512, 6>), dim3(std::min(nch, 2 * ncu)), dim3(512), 0, s,
+  hipLaunchKernelGGL((k_top_chunks<512, 6>), dim3(std::min(nch, 3 * ncu)), dim3(512), 0, s,
                      static_cast<const u32x4*>(pairs), n, tb, plan, static_cast<u32x4*>(chunked),
                      offs, tot);
   hipLaunchKernelGGL(k_top_colsum, dim3((R + 255) / 256, kTopSegs), dim3(256), 0, s, offs, nch, R,

@@ -14,6 +14,7 @@
 #   sortpmc                 PMC passes of tools/sort_prof.py (5 M TeraSort records)
 #   sorttrace [N]           rocprofv3 kernel trace of tools/sort_prof.py on range-partition keys
 #   sortprof                the sort tests, then tools/sort_prof.py on random and range-partition keys, 2 x
+#   sortab LIB_A LIB_B      tools/sort_prof.py on both inputs, A and B alternating, 2 x each
 #   ab LIB_B [bench args]   bench.py alternating with a copy of the tree linking LIB_B, 2 x each
 #   cmd SECONDS CMD...      any other command under a time limit
 set -o pipefail
@@ -73,6 +74,16 @@ case $job in
         > $O/sort_partition_$i.txt 2>&1 || exit 1
     done
     tail -qn 1 $O/sort_random_*.txt $O/sort_partition_*.txt ;;
+  sortab)
+    for i in 1 2; do
+      for lib in "$1" "$2"; do
+        for inp in random partition; do
+          SORT_PROF_INPUT=$inp timeout -k 10 120 python3 tools/sort_prof.py 20 "" $lib \
+            >> $O/sortab.txt 2>&1 || exit 1
+        done
+      done
+    done
+    grep "per call" $O/sortab.txt ;;
   ab)
     lib=${1:?LIB_B}; shift
     B=/tmp/ab_b; rm -rf $B; mkdir -p $B && cp -r bench.py sparkucx_amd profiles oracle $B/ \
