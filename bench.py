@@ -1062,6 +1062,12 @@ def main():
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="test mode: every rank on cuda:0, gloo process group, ipc transport "
                          "(exercises the N>1 pipeline on a 1-GPU box; not a benchmark)")
+    ap.add_argument("--loopback-rccl", action="store_true",
+                    help="test mode: like --rehearse-one-gpu (every rank on cuda:0, gloo process "
+                         "group) but the exchange keeps the rccl transport, through the library "
+                         "build whose RCCL calls go to tests/loopback_rccl (files under /dev/shm): "
+                         "the RCCL code path's pairing and bytes at W > 1 on a 1-GPU box, where "
+                         "RCCL itself refuses two ranks on one GPU; not a benchmark")
     ap.add_argument("--rccl-at-one", action="store_true",
                     help="test mode at N=1: run the N>1 pipeline (peer-major partition, "
                          "overlapped ncclAllGather + ncclAllToAllv) on a one-rank RCCL "
@@ -1162,9 +1168,13 @@ def main():
         # a line whose n_gpus differs from --gpus would misreport the scaling curve
         raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} "
                          "ranks; pass --gpus equal to --nproc-per-node")
-    rehearse = args.rehearse_one_gpu and world > 1
+    if args.loopback_rccl:  # before the library is first loaded (Node below)
+        N.LIB_PATH = os.path.join(os.path.dirname(N.LIB_PATH), "libsparkucx_amd_loop.so")
+    rehearse = (args.rehearse_one_gpu or args.loopback_rccl) and world > 1
     if rehearse:
-        args.transport, local = "ipc", 0
+        local = 0
+        if not args.loopback_rccl:
+            args.transport = "ipc"
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -1194,7 +1204,7 @@ def main():
     if world == 1 and args.rccl_at_one:
         comm_id = N.unique_id()
     elif world > 1 and args.transport == "rccl":
-        t = torch.zeros(128, dtype=torch.uint8, device=dev)
+        t = torch.zeros(128, dtype=torch.uint8, device=ctl)
         if rank == 0:
             t.copy_(torch.frombuffer(bytearray(N.unique_id()), dtype=torch.uint8))
         dist.broadcast(t, 0)

@@ -991,6 +991,7 @@ static int lifecycle_executor(int child, int req_fd, int rep_fd) {
   }
   // the exchange thread: the driver's relayed messages, in order
   int windows = 0;
+  const bool connect = getenv("SUX_LC_CONNECT") != nullptr;
   for (;;) {
     LcCmd c{};
     if (read(rep_fd, &c, sizeof c) != (ssize_t)sizeof c) return 16;
@@ -999,6 +1000,10 @@ static int lifecycle_executor(int child, int req_fd, int rep_fd) {
         OK_CALL(FN(registerShuffle)(env, cls, node, sid, M, R, S));
         registered = true;
       }
+      // rccl transport (SUX_LC_CONNECT, the loopback build on one GPU): GpuNode's exchange
+      // thread joins the communicator before its first window — the unique id all-gathered
+      // through the Java bootstrap by all 8, the late-Ready one from its replayed window
+      if (connect && windows == 0) OK_CALL(FN(nodeConnect)(env, cls, node));
       OK_CALL(FN(exchangeMaps)(env, cls, node, sid, c.a, c.b, xstream));
       ++windows;
     } else if (c.kind == 2) {
@@ -1036,8 +1041,9 @@ static int lifecycle_executor(int child, int req_fd, int rep_fd) {
   FN(releaseBootstrap)(env, cls, ctx);
   if (drec) (void)hipFree(drec);
   if (failures) return 1;
-  printf("lifecycle rank %d (%s, %d window): %zu owned bytes of %d maps ok\n", rank,
-         rank < kLcWriters ? "writer" : "no task", windows, want.size(), M);
+  printf("lifecycle rank %d (%s, %d window): %zu owned bytes of %d maps ok (%s)\n", rank,
+         rank < kLcWriters ? "writer" : "no task", windows, want.size(), M,
+         connect ? "rccl" : "ipc");
   return 0;
 }
 

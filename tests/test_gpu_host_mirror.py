@@ -71,6 +71,24 @@ def test_jni_group_lifecycle_three_writers_of_eight():
     assert r.stdout.count("(writer, 1 window)") == 3 and r.stdout.count("(no task, 1 window)") == 5
 
 
+def test_jni_group_lifecycle_joins_the_rccl_communicator(tmp_path):
+    """The same lifecycle with the rccl transport, through the loopback build (RCCL refuses eight
+    ranks on one GPU; tests/loopback_rccl): each executor's exchange thread joins the
+    communicator before its first window (nodeConnect: rank 0's unique id all-gathered through
+    the Java bootstrap — the late-Ready executor from its replayed window), the windows exchange
+    over grouped send/recv and the directory over the all-gather, and all 8 fetch their owned
+    partitions bit-exact."""
+    loop = JNI + "_loop"
+    assert os.path.exists(loop), "build it first: make -C tests/jni"
+    env = dict(os.environ, SUX_LC_CONNECT="1", SUX_LOOPBACK_DIR=str(tmp_path),
+               SUX_LOOPBACK_TIMEOUT="100")
+    r = subprocess.run([loop, "lifecycle"], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "jni lifecycle ok" in r.stdout
+    assert r.stdout.count("owned bytes of 15 maps ok (rccl)") == 8
+    assert not [f for _, _, fs in os.walk(tmp_path) for f in fs]  # every message received
+
+
 def test_jni_map_outputs_past_2_gib():
     """a 3.3 GB map written from a raw host address (the writer's native staging)
     and a 3.3 GB data file committed by address, plus a file committed by path (mapped natively),
