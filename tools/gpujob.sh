@@ -12,7 +12,8 @@
 #   trace [bench args]      rocprofv3 --kernel-trace --stats of a headline-only bench run
 #   pmc WORKLOAD...         profiles/collect_pmc.py passes (one counter group per rocprofv3 run)
 #   sortpmc                 PMC passes of tools/sort_prof.py (5 M TeraSort records)
-#   sorttrace [N]           rocprofv3 kernel trace of tools/sort_prof.py on range-partition keys
+#   sorttrace [N] [INPUT]   rocprofv3 kernel trace of tools/sort_prof.py (INPUT: partition (default),
+#                           random, long)
 #   sortprof                the sort tests, then tools/sort_prof.py on random and range-partition keys, 2 x
 #   sortab LIB_A LIB_B      tools/sort_prof.py on both inputs, A and B alternating, 2 x each
 #   ab LIB_B [bench args]   bench.py alternating with a copy of the tree linking LIB_B, 2 x each
@@ -64,7 +65,7 @@ case $job in
       i=$((i+1))
     done ;;
   sorttrace)
-    SORT_PROF_INPUT=partition timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv \
+    SORT_PROF_INPUT=${2:-partition} timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv \
       -d $O/prof_sort -o run -- python3 tools/sort_prof.py ${1:-20} > $O/prof_sort.txt 2>&1 ;;
   sortprof)
     run_tests tests/test_gpu_sort.py || exit 1

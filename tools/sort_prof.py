@@ -22,7 +22,17 @@ def main():
     if len(sys.argv) > 2 and sys.argv[2]:
         node.set_tuning(**{k: int(v) for k, v in (kv.split("=") for kv in sys.argv[2].split(","))})
     n, rs = 5_000_000, 100
-    d = node.generate(N.GEN_TERASORT, 25, 0, n, rs)
+    kind, klen = N.SORT_BYTES, 10
+    if os.environ.get("SORT_PROF_INPUT") == "long":  # bench.py reduce_sort_long's 32 Mi rows
+        n, rs, kind, klen = 32 << 20, 16, N.SORT_LONG, 8
+        g = torch.Generator(device="cuda")
+        g.manual_seed(5)
+        rows = torch.empty((n, 2), dtype=torch.int64, device="cuda")
+        rows[:, 0] = torch.randint(0, 1 << 31, (n,), generator=g, device="cuda")
+        rows[:, 1] = torch.arange(n, device="cuda")
+        d = rows.view(torch.uint8).view(-1)
+    else:
+        d = node.generate(N.GEN_TERASORT, 25, 0, n, rs)
     if os.environ.get("SORT_PROF_INPUT") == "partition":
         v = d.view(n, rs)
         g = torch.Generator(device="cuda")
@@ -34,16 +44,16 @@ def main():
     out = torch.empty(n * rs, dtype=torch.uint8, device="cuda")
     ws = torch.empty(node.sort_workspace_size(n, rs), dtype=torch.uint8, device="cuda")
     for _ in range(2):
-        node.sort_records(d, rs, N.SORT_BYTES, 0, 10, num_records=n, out=out, workspace=ws)
+        node.sort_records(d, rs, kind, 0, klen, num_records=n, out=out, workspace=ws)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
-        node.sort_records(d, rs, N.SORT_BYTES, 0, 10, num_records=n, out=out, workspace=ws)
+        node.sort_records(d, rs, kind, 0, klen, num_records=n, out=out, workspace=ws)
     e1.record()
     torch.cuda.synchronize()
     node.check()
-    print(f"sort 5M TeraSort ({os.environ.get('SORT_PROF_INPUT', 'random')} keys): "
+    print(f"sort {n} x {rs} B ({os.environ.get('SORT_PROF_INPUT', 'random')} keys): "
           f"{e0.elapsed_time(e1) / reps:.4f} ms per call ({N.LIB_PATH})", flush=True)
 
 
