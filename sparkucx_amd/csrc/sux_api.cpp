@@ -4127,7 +4127,7 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
     if (!inline_rec && gt.gather_kernel == 3 && sux::sort_gather_fusable(record_size)) {
       // the fused sort: sorted buckets gather their records themselves, the rest after them
       hip_check(sux::launch_sort_local_planned(b, a, index1, (uint32_t)pd1.R, plan, s, d_in,
-                                               d_out, record_size, runs, side),
+                                               d_out, record_size, runs, side, n >> tb),
                 "sort buckets");
       hip_check(sux::launch_gather_rest(d_in, a, b, index1, (uint32_t)pd1.R, n, plan, record_size,
                                         d_out, s),
@@ -4135,7 +4135,7 @@ void sort_impl(sux_node* node, int32_t key_kind, const void* d_in, uint64_t n,
       return;
     }
     hip_check(sux::launch_sort_local_planned(b, a, index1, (uint32_t)pd1.R, plan, s, nullptr,
-                                             nullptr, 0, runs, side),
+                                             nullptr, 0, runs, side, n >> tb),
               "sort buckets");
     if (inline_rec)
       hip_check(sux::launch_unpair_records_sel(a, b, &plan->final_b, n, record_size, key_kind,

@@ -269,7 +269,8 @@ struct SortPlanDev {
   int32_t top_lo;    // shift of the top digit (the tb highest varying key bits)
   int32_t hb;        // highest varying key bit; -1: every key is equal (the sort is the identity)
   uint32_t msd_ok;   // 1: the bucket sorts finish the sort (0: every key is equal)
-  uint32_t pad;
+  uint32_t big;      // 1: some bucket may exceed kSortLocalCap (k_gather_rest has work); set by
+                     // make_sort_plan, cleared by k_top_scan when every bucket fits
   uint32_t final_b;  // 1: the sorted pairs end in buffer b, 0: in buffer a
   int32_t kbits;     // key bits (with the segment id): the top kbits of the big-endian pair
   uint64_t top_base; // the top digit is ((key >> top_lo) - top_base) & (2^tb - 1): with the key
@@ -298,7 +299,8 @@ static_assert(sizeof(SortPlanDev) <= kSortPlanBytes, "plan slot");
 // above kSortLocalCap through global memory.
 // recs_out != nullptr (the fused sort): the LDS launches gather their buckets' records from
 // recs_in straight into recs_out instead of writing sorted pairs; launch_gather_rest then gathers
-// every record they did not (needs sort_gather_fusable(rs)).
+// every record they did not (needs sort_gather_fusable(rs)).  avg: the pairs per bucket on
+// average (n >> tb): above 1024 the (0, 1024] class is left to the 2048-pair shape.
 // Chunked top pass (round 4): each 4096-pair chunk of the pairs sorted by the top digit in place
 // into `chunked`, offs[chunk][0..R] its bucket starts (u16), then the bucket index (bytes).  A
 // sort with R = 2^tb <= 4096 buckets and at most kTopMaxChunks chunks takes it.
@@ -306,7 +308,7 @@ constexpr uint32_t kTopChunk = 4096;
 constexpr uint32_t kTopSegs = 32;        // chunk segments of the bucket-size column sums
 constexpr uint32_t kTopMaxChunks = 2048; // run table of the 1024-pair LDS shape (2 u32 per chunk)
 constexpr int kTopMaxBits = 12;
-hipError_t launch_top_chunks(const void* pairs, uint64_t n, int tb, const SortPlanDev* plan,
+hipError_t launch_top_chunks(const void* pairs, uint64_t n, int tb, SortPlanDev* plan,
                              void* chunked, uint16_t* offs, uint32_t* tot, int64_t* index,
                              hipStream_t s);
 // Where k_sort_local finds its buckets after the chunked top pass (pairs == nullptr: contiguous
@@ -326,7 +328,7 @@ hipError_t launch_sort_local_planned(const void* in_pairs, void* out_pairs, cons
                                      uint32_t R, const SortPlanDev* plan, hipStream_t s,
                                      const void* recs_in = nullptr, void* recs_out = nullptr,
                                      uint32_t rs = 0, const SortRuns& runs = SortRuns{},
-                                     const SortSide& side = SortSide{});
+                                     const SortSide& side = SortSide{}, uint64_t avg = 0);
 bool sort_gather_fusable(uint32_t rs);
 hipError_t launch_gather_rest(const void* recs_in, const void* pairs_a, const void* pairs_b,
                               const int64_t* d_index, uint32_t R, uint64_t n,

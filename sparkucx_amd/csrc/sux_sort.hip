@@ -236,39 +236,50 @@ __device__ void make_sort_plan(const uint32_t* span, int bits, int tb, SortPlanD
 // The key span; with `plan`, thread 0 then plans the sort from it (the device-planned MSD path:
 // one launch fewer than a separate planning kernel); `ranged` plans the top digit over the key
 // range [min, max] instead of the varying bits.
-__global__ __launch_bounds__(256) void k_span_reduce(const uint32_t* __restrict__ part,
-                                                     uint32_t blocks, uint32_t* __restrict__ span,
-                                                     int bits, int tb, SortPlanDev* __restrict__ plan,
-                                                     int ranged) {
-  __shared__ uint32_t red[256][6];
-  __shared__ u128 rmm[256][2];
+__global__ __launch_bounds__(1024) void k_span_reduce(const uint32_t* __restrict__ part,
+                                                      uint32_t blocks, uint32_t* __restrict__ span,
+                                                      int bits, int tb, SortPlanDev* __restrict__ plan,
+                                                      int ranged) {
+  // wave folds by shuffles, one barrier, then thread 0 folds the 16 waves' results and plans
+  // (round 4's 256-thread LDS tree took 8 barriers: 14 us of the 0.6 ms sort)
+  constexpr int NW = 1024 / kWave;
+  __shared__ uint32_t red[NW][6];
+  __shared__ u128 rmm[NW][2];
+  const int tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
   uint32_t v[6] = {~0u, ~0u, ~0u, 0, 0, 0};
   u128 mn = ~(u128)0, mx = 0;
-  for (uint32_t b = threadIdx.x; b < blocks; b += 256) {
+  for (uint32_t b = tid; b < blocks; b += 1024) {
     for (int k = 0; k < 6; ++k)
       v[k] = k < 3 ? (v[k] & part[b * 16 + k]) : (v[k] | part[b * 16 + k]);
     const u128 a = get128(part + b * 16 + 8), c = get128(part + b * 16 + 12);
     mn = a < mn ? a : mn;
     mx = c > mx ? c : mx;
   }
-  for (int k = 0; k < 6; ++k) red[threadIdx.x][k] = v[k];
-  rmm[threadIdx.x][0] = mn;
-  rmm[threadIdx.x][1] = mx;
-  __syncthreads();
-  for (uint32_t h = 128; h >= 1; h >>= 1) {
-    if (threadIdx.x < h) {
-      for (int k = 0; k < 6; ++k)
-        red[threadIdx.x][k] = k < 3 ? (red[threadIdx.x][k] & red[threadIdx.x + h][k])
-                                    : (red[threadIdx.x][k] | red[threadIdx.x + h][k]);
-      const u128 a = rmm[threadIdx.x + h][0], c = rmm[threadIdx.x + h][1];
-      if (a < rmm[threadIdx.x][0]) rmm[threadIdx.x][0] = a;
-      if (c > rmm[threadIdx.x][1]) rmm[threadIdx.x][1] = c;
+  for (int m = kWave / 2; m >= 1; m >>= 1) {
+    for (int k = 0; k < 6; ++k) {
+      const uint32_t o = __shfl_xor(v[k], m, kWave);
+      v[k] = k < 3 ? (v[k] & o) : (v[k] | o);
     }
-    __syncthreads();
+    const u128 vn = shfl_xor128(mn, m), vx = shfl_xor128(mx, m);
+    mn = vn < mn ? vn : mn;
+    mx = vx > mx ? vx : mx;
   }
-  if (threadIdx.x < 6) span[threadIdx.x] = red[0][threadIdx.x];
-  if (plan && threadIdx.x == 0)
-    make_sort_plan(&red[0][0], bits, tb, plan, ranged ? rmm[0] : nullptr, ranged == 2);
+  if (lane == 0) {
+    for (int k = 0; k < 6; ++k) red[wave][k] = v[k];
+    rmm[wave][0] = mn;
+    rmm[wave][1] = mx;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < NW; ++w) {
+      for (int k = 0; k < 6; ++k)
+        red[0][k] = k < 3 ? (red[0][k] & red[w][k]) : (red[0][k] | red[w][k]);
+      if (rmm[w][0] < rmm[0][0]) rmm[0][0] = rmm[w][0];
+      if (rmm[w][1] > rmm[0][1]) rmm[0][1] = rmm[w][1];
+    }
+    for (int k = 0; k < 6; ++k) span[k] = red[0][k];
+    if (plan) make_sort_plan(&red[0][0], bits, tb, plan, ranged ? rmm[0] : nullptr, ranged == 2);
+  }
 }
 
 // One output dword per thread and step: record j = d / W, dword w of it, read from the record
@@ -345,7 +356,7 @@ hipError_t launch_sort_pairs(const uint8_t* in, uint64_t n, uint32_t rs, int kin
                      inline_rec ? 1 : 0);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_span_reduce, dim3(1), dim3(256), 0, s, part, blocks,
+  hipLaunchKernelGGL(k_span_reduce, dim3(1), dim3(1024), 0, s, part, blocks,
                      static_cast<uint32_t*>(span_ws), bits, tb, plan, ranged);
   return hipGetLastError();
 }
@@ -647,7 +658,7 @@ __global__ __launch_bounds__(256) void k_top_colsum(const uint16_t* __restrict__
 
 // The bucket index (bytes, R + 1 entries) from the bucket totals; every key equal: one bucket.
 __global__ __launch_bounds__(1024) void k_top_scan(const uint32_t* __restrict__ tot, uint32_t R,
-                                                   uint64_t n, const SortPlanDev* __restrict__ plan,
+                                                   uint64_t n, SortPlanDev* __restrict__ plan,
                                                    int64_t* __restrict__ index) {
   __shared__ uint64_t sh[2 * kWave + 1];
   const uint32_t tid = threadIdx.x;
@@ -666,6 +677,11 @@ __global__ __launch_bounds__(1024) void k_top_scan(const uint32_t* __restrict__ 
   }
   uint64_t all;
   uint64_t ex = block_excl_scan(v, sh, &all);
+  bool big = false;
+#pragma unroll
+  for (uint32_t k = 0; k < 8; ++k) big = big || t[k] > kSortLocalCap;
+  // k_gather_rest has work only for a bucket above the LDS shapes
+  if (!__syncthreads_or(big) && tid == 0) plan->big = 0u;
   for (uint32_t k = 0; k < E; ++k) {
     const uint32_t b = tid * E + k;
     if (b >= R) break;
@@ -726,7 +742,7 @@ __global__ __launch_bounds__(256) void k_top_materialize(const u32x4* __restrict
   }
 }
 
-hipError_t launch_top_chunks(const void* pairs, uint64_t n, int tb, const SortPlanDev* plan,
+hipError_t launch_top_chunks(const void* pairs, uint64_t n, int tb, SortPlanDev* plan,
                              void* chunked, uint16_t* offs, uint32_t* tot, int64_t* index,
                              hipStream_t s) {
   const uint32_t ncu = (uint32_t)std::max(1, stream_cus(s));
@@ -1051,6 +1067,7 @@ __global__ __launch_bounds__(256) void k_gather_rest(const u32x4* __restrict__ p
   __shared__ uint32_t sidx[kGatherRestChunk];
   __shared__ uint32_t b_first;
   const bool all = !plan->msd_ok || plan->dg.n == 0;
+  if (!all && !plan->big) return;  // every bucket fit the LDS shapes, which gathered it
   const u32x4* pairs = plan->final_b ? pairs_b : pairs_a;
   const uint32_t tid = threadIdx.x;
   for (uint64_t c0 = (uint64_t)blockIdx.x * kGatherRestChunk; c0 < n;
@@ -1226,13 +1243,21 @@ __global__ __launch_bounds__(NW * 64) void k_sort_bucket_global(u32x4* __restric
 
 // True when bits [lo, hi) of the big-endian 128-bit pair differ between some records (span: the
 // AND of key words 0..2, then their OR) — sux_api.cpp's span_varies, on the device.
-__device__ bool span_varies_dev(const uint32_t* span, int lo, int hi) {
-  for (int b = max(lo, 32); b < min(hi, 128); ++b) {
-    const int byte = 15 - b / 8;
-    const uint32_t diff = span[byte / 4] ^ span[3 + byte / 4];
-    if ((diff >> (8 * (byte % 4) + b % 8)) & 1u) return true;
-  }
-  return false;
+// The key bits that vary, as the big-endian 128-bit pair value (bit b = pair bit b; the index word's
+// bits, below 32, are 0): AND ^ OR of the key words, byte-swapped like pair_be128.  Held in
+// registers: testing the span bit by bit from LDS cost ~10 us of single-thread latency per sort.
+__device__ __forceinline__ u128 span_vary_mask(const uint32_t* span) {
+  u32x4 d;
+  d[0] = span[0] ^ span[3];
+  d[1] = span[1] ^ span[4];
+  d[2] = span[2] ^ span[5];
+  d[3] = 0u;
+  return pair_be128(d);
+}
+// some bit in [lo, hi) varies (lo < hi <= 128)
+__device__ __forceinline__ bool vary_in(u128 v, int lo, int hi) {
+  const u128 m = (hi - lo >= 128) ? ~(u128)0 : ((((u128)1) << (hi - lo)) - 1);
+  return ((v >> lo) & m) != 0;
 }
 
 // The plan from the key span (AND of key words 0..2, then their OR): the highest varying key
@@ -1240,9 +1265,9 @@ __device__ bool span_varies_dev(const uint32_t* span, int lo, int hi) {
 // One thread (k_span_reduce's thread 0).
 __device__ void make_sort_plan(const uint32_t* span, int bits, int tb, SortPlanDev* plan,
                                const u128* range, bool rebase_ok) {
-  int hb = -1;
-  for (int b = 127; b >= 128 - bits && hb < 0; --b)
-    if (span_varies_dev(span, b, b + 1)) hb = b;
+  const u128 vary = span_vary_mask(span) & (~(u128)0 << (128 - bits));
+  const uint64_t vh = (uint64_t)(vary >> 64), vl = (uint64_t)vary;
+  const int hb = vh ? 127 - __builtin_clzll(vh) : vl ? 63 - __builtin_clzll(vl) : -1;
   int top_lo = hb >= 0 ? max(hb + 1 - tb, 128 - bits) : 128 - bits;
   uint64_t top_base = 0;
   plan->rebase = 0;
@@ -1296,7 +1321,7 @@ __device__ void make_sort_plan(const uint32_t* span, int bits, int tb, SortPlanD
   int m = 0;
   for (int hi = top_lo; hi > 128 - bits && m < 16; hi -= 8) {
     const int sh = max(hi - 8, 128 - bits);
-    if (span_varies_dev(span, sh, hi)) shs[m++] = (uint32_t)sh;
+    if (vary_in(vary, sh, hi)) shs[m++] = (uint32_t)sh;
   }
   for (int i = m - 1; i >= 0; --i) dg.push(shs[i]);  // least significant first
   if (plan->rebase) {
@@ -1325,29 +1350,37 @@ __device__ void make_sort_plan(const uint32_t* span, int bits, int tb, SortPlanD
   // go a -> top pass -> b -> bucket sorts -> a; with no lower digit varying they end in the top
   // pass's b; with every key equal, in a (the input order)
   plan->msd_ok = hb >= 0 ? 1u : 0u;
+  plan->big = 1u;  // until k_top_scan has seen every bucket fit
   plan->final_b = hb < 0 ? 0u : (dg.n ? 0u : 1u);
 }
 
 template <bool GATHER>
 static void launch_sort_local_classes(const u32x4* in, u32x4* out, const int64_t* d_index,
                                       uint32_t R, const SortPlanDev* plan, const SortGather& gth,
-                                      const SortRuns& runs, uint32_t ncu, hipStream_t s) {
+                                      const SortRuns& runs, uint32_t ncu, uint64_t avg,
+                                      hipStream_t s) {
   // size classes (0, 1024], (1024, 2048] (the third, (2048, kSortLocalCap], is launched by the
-  // caller on the side stream): each bucket on the smallest shape that holds it (the classes a
-  // key set leaves empty cost one index sweep each)
-  constexpr size_t l1 = SortLocal<4, 1024>::lds_bytes();
-  hipLaunchKernelGGL((k_sort_local<4, 1024, GATHER>), dim3(std::min<uint32_t>(R, 6 * ncu)),
-                     dim3(4 * kWave), l1, s, in, out, d_index, R, 0u, plan, gth, runs);
+  // caller on the side stream): each bucket on the smallest shape that holds it — unless the
+  // buckets average above 1024 pairs: then the few small ones (the key range's edge buckets) go to
+  // the 2048-pair launch too, instead of a launch of their own whose one or two buckets cost a
+  // bucket's whole latency chain (~30 us: run table, digit passes, gather) ahead of it
+  const bool small_class = avg <= 1024;
+  if (small_class) {
+    constexpr size_t l1 = SortLocal<4, 1024>::lds_bytes();
+    hipLaunchKernelGGL((k_sort_local<4, 1024, GATHER>), dim3(std::min<uint32_t>(R, 6 * ncu)),
+                       dim3(4 * kWave), l1, s, in, out, d_index, R, 0u, plan, gth, runs);
+  }
   constexpr size_t l2 = SortLocal<4, 2048>::lds_bytes();
   static_assert(4 * l2 <= 160 * 1024, "four workgroups per CU");
   hipLaunchKernelGGL((k_sort_local<4, 2048, GATHER>), dim3(std::min<uint32_t>(R, 4 * ncu)),
-                     dim3(4 * kWave), l2, s, in, out, d_index, R, 1024u, plan, gth, runs);
+                     dim3(4 * kWave), l2, s, in, out, d_index, R, small_class ? 1024u : 0u, plan,
+                     gth, runs);
 }
 
 hipError_t launch_sort_local_planned(const void* in_pairs, void* out_pairs, const int64_t* d_index,
                                      uint32_t R, const SortPlanDev* plan, hipStream_t s,
                                      const void* recs_in, void* recs_out, uint32_t rs,
-                                     const SortRuns& runs, const SortSide& side) {
+                                     const SortRuns& runs, const SortSide& side, uint64_t avg) {
   const uint32_t ncu = (uint32_t)std::max(1, stream_cus(s));
   const u32x4* in = static_cast<const u32x4*>(in_pairs);
   u32x4* out = static_cast<u32x4*>(out_pairs);
@@ -1382,9 +1415,9 @@ hipError_t launch_sort_local_planned(const void* in_pairs, void* out_pairs, cons
   hipLaunchKernelGGL((k_sort_bucket_global<16>), dim3(std::min<uint32_t>(R, ncu)), dim3(16 * kWave),
                      0, sb, const_cast<u32x4*>(in), out, d_index, R, plan);
   if (recs_out)
-    launch_sort_local_classes<true>(in, out, d_index, R, plan, gth, runs, ncu, s);
+    launch_sort_local_classes<true>(in, out, d_index, R, plan, gth, runs, ncu, avg, s);
   else
-    launch_sort_local_classes<false>(in, out, d_index, R, plan, gth, runs, ncu, s);
+    launch_sort_local_classes<false>(in, out, d_index, R, plan, gth, runs, ncu, avg, s);
   if (side.s) {
     hipError_t e = hipEventRecord(side.join, side.s);
     if (e == hipSuccess) e = hipStreamWaitEvent(s, side.join, 0);
