@@ -295,9 +295,36 @@ def compress_leg(node, data, index, maps: int, R: int, dev, bs: int = 32768) -> 
     e1.record()
     torch.cuda.synchronize(dev)
     ms = e0.elapsed_time(e1) / reps
-    return {"input_bytes": nb, "maps": maps, "R": R, "block_size": bs, "ms": round(ms, 3),
-            "GB/s": round(nb / (ms / 1e3) / 1e9, 1),
-            "ratio": round(int(ob.item()) / nb, 4)}
+    res = {"input_bytes": nb, "maps": maps, "R": R, "block_size": bs, "ms": round(ms, 3),
+           "GB/s": round(nb / (ms / 1e3) / 1e9, 1), "ratio": round(int(ob.item()) / nb, 4)}
+    # the reader's side: every (map, partition) stream decoded back (sux_decompress_blocks, lz4-
+    # java's LZ4BlockInputStream checks included); GB/s of decoded bytes; checked = the input
+    ox = oix.view(maps, R + 1)
+    base = torch.cumsum(ox[:, R], 0) - ox[:, R]
+    boffs = torch.cat([(base[:, None] + ox[:, :R]).reshape(-1), (base[-1] + ox[-1, R]).view(1)])
+    cb = int(ob.item())
+    dec = torch.empty(nb + 16, dtype=torch.uint8, device=dev)
+    doff = torch.empty(maps * R + 1, dtype=torch.int64, device=dev)
+    dws = torch.empty(node.decompress_workspace_size(cb, maps * R, bs), dtype=torch.uint8,
+                      device=dev)
+    drun = lambda: node.decompress_blocks(out, boffs, bs, out=dec, out_offsets=doff,  # noqa: E731
+                                          workspace=dws, in_bytes=cb)
+    drun()
+    torch.cuda.synchronize(dev)
+    node.check()
+    tot = int(index.view(maps, R + 1)[:, R].sum().item())  # the runs' bytes (maps consecutive)
+    ok = int(doff[-1].item()) == tot and torch.equal(dec[:tot], data[:tot])
+    if not ok:
+        raise RuntimeError("compress leg: the decoded streams differ from the map outputs")
+    e0.record()
+    for _ in range(reps):
+        drun()
+    e1.record()
+    torch.cuda.synchronize(dev)
+    dms = e0.elapsed_time(e1) / reps
+    res["decompress"] = {"ms": round(dms, 3), "GB/s": round(tot / (dms / 1e3) / 1e9, 1),
+                         "blocks": maps * R, "checked": "decoded bytes = the map outputs"}
+    return res
 
 
 def files_leg(node, out, index, maps: int, R: int, dev) -> dict:

@@ -442,6 +442,30 @@ int sux_compress_map_outputs(sux_node* node, const void* d_data, uint64_t data_b
                              uint64_t* d_out_bytes, void* d_workspace, uint64_t workspace_bytes,
                              void* stream);
 
+/* ---- reading compressed blocks: the reducer's side of spark.shuffle.compress=true ----------
+ * Replaces the decompression stream Spark's reader wraps around every fetched block ([ext]
+ * BlockStoreShuffleReader -> SerializerManager.wrapStream -> LZ4CompressionCodec.
+ * compressedInputStream = lz4-java LZ4BlockInputStream, stream concatenation on), for the blocks
+ * one fetch delivered (compat/spark_3_0/UcxShuffleReader.scala:58-96, sux_fetch_blocks): num_blocks
+ * byte ranges of d_in (in_bytes in all), block k = [d_in_offsets[k], d_in_offsets[k + 1])
+ * (num_blocks + 1 int64 on the device; an empty range is an empty block).  Each range is a
+ * sequence of LZ4Block chunks and end marks checked as LZ4BlockInputStream checks them (magic,
+ * method raw / LZ4, lengths against the block size the token declares and max_block_size, the
+ * LZ4 block decoding to exactly its original length, the XXH32 & 0x0FFFFFFF checksum of the
+ * decoded bytes) and decoded into d_out, blocks consecutive; d_out_offsets (num_blocks + 1 int64,
+ * device) receives each block's decoded start and the total.  d_out == NULL: only d_out_offsets
+ * (the decoded sizes; read the total, then call again with an output that holds it).  A malformed
+ * block, or decoded bytes past out_capacity, sets the node's device error word (sux_node_check
+ * reports it) and nothing is written outside d_out.  max_block_size: the largest chunk the blocks
+ * may carry (spark.io.compression.lz4.blockSize, 64..65536); workspace: 256-byte aligned,
+ * sux_decompress_workspace_size bytes.  Asynchronous on `stream`, no host wait. */
+int sux_decompress_workspace_size(uint64_t in_bytes, int32_t num_blocks, int32_t max_block_size,
+                                  uint64_t* bytes);
+int sux_decompress_blocks(sux_node* node, const void* d_in, uint64_t in_bytes,
+                          const int64_t* d_in_offsets, int32_t num_blocks, int32_t max_block_size,
+                          void* d_out, uint64_t out_capacity, int64_t* d_out_offsets,
+                          void* d_workspace, uint64_t workspace_bytes, void* stream);
+
 /* ---- Spark's on-disk shuffle files (local-disk fallback / external shuffle service) ---------
  * sux_index_file_commit: IndexShuffleBlockResolver.writeIndexFileAndCommit [ext] (the super call
  * at compat/spark_3_0/UcxShuffleBlockResolver.scala:35), host-only: if index_path + data_path

@@ -1345,6 +1345,10 @@ int sux_node_check(sux_node* node) {
     if (w & sux::kErrTurnTimeout)
       what += "a small-record scatter wave timed out waiting for its turn (the launch stopped "
               "without writing its remaining records); ";
+    if (w & sux::kErrLz4Stream) what += "a compressed block is corrupted (sux_decompress_blocks: header, lengths "
+                        "or LZ4 sequence); ";
+    if (w & sux::kErrLz4Capacity) what += "decompressed bytes exceed the output capacity (nothing decoded); ";
+    if (w & sux::kErrLz4Checksum) what += "a decompressed chunk's XXH32 differs from its header (stream corrupted); ";
     raise(SUX_EHIP, "device error word 0x" + [&] {
       char b[16];
       std::snprintf(b, sizeof b, "%x", w);
@@ -1778,6 +1782,51 @@ int sux_compress_map_outputs(sux_node* node, const void* d_data, uint64_t data_b
                                        resolve_tuning(node->tuning, false).lz4_queue,
                                        node->stream(stream)),
               "compress launch");
+  });
+}
+
+}  // extern "C"
+namespace {
+void check_lz4d_args(uint64_t in_bytes, int32_t nb, int32_t max_bs) {
+  require(nb >= 0 && nb < (1 << 30), SUX_EINVAL, "num_blocks must be in [0, 2^30)");
+  require(max_bs >= 64 && max_bs <= 65536, SUX_EINVAL,
+          "max_block_size must be in [64, 65536], got " + std::to_string(max_bs));
+  require(sux::lz4d_chunk_bound(in_bytes) < (1ull << 32), SUX_ERANGE,
+          "too many compressed chunks in one call");
+}
+}  // namespace
+extern "C" {
+
+int sux_decompress_workspace_size(uint64_t in_bytes, int32_t num_blocks, int32_t max_block_size,
+                                  uint64_t* bytes) {
+  return guard([&] {
+    require(bytes, SUX_EINVAL, "NULL argument");
+    check_lz4d_args(in_bytes, num_blocks, max_block_size);
+    *bytes = sux::lz4d_workspace_layout(in_bytes, (uint32_t)num_blocks).total;
+  });
+}
+
+int sux_decompress_blocks(sux_node* node, const void* d_in, uint64_t in_bytes,
+                          const int64_t* d_in_offsets, int32_t num_blocks, int32_t max_block_size,
+                          void* d_out, uint64_t out_capacity, int64_t* d_out_offsets, void* d_ws,
+                          uint64_t ws_bytes, void* stream) {
+  return guard([&] {
+    require(node && d_in_offsets && d_out_offsets, SUX_EINVAL, "NULL argument");
+    require(d_in || in_bytes == 0, SUX_EINVAL, "input pointer is NULL");
+    check_lz4d_args(in_bytes, num_blocks, max_block_size);
+    const sux::Lz4DWorkspace w = sux::lz4d_workspace_layout(in_bytes, (uint32_t)num_blocks);
+    require(d_ws && ws_bytes >= w.total, SUX_EINVAL,
+            "workspace too small: need " + std::to_string(w.total) + " bytes");
+    require(((uintptr_t)d_ws & 255) == 0 && ((uintptr_t)d_in_offsets & 7) == 0 &&
+                ((uintptr_t)d_out_offsets & 7) == 0,
+            SUX_EINVAL, "offsets (8 B) and workspace (256 B) must be aligned");
+    node->bind();
+    hip_check(sux::launch_lz4_decompress(static_cast<const uint8_t*>(d_in), in_bytes, d_in_offsets,
+                                         (uint32_t)num_blocks, (uint32_t)max_block_size,
+                                         static_cast<uint8_t*>(d_out), out_capacity,
+                                         d_out_offsets, static_cast<uint8_t*>(d_ws), w,
+                                         node->d_err, node->stream(stream)),
+              "decompress launch");
   });
 }
 

@@ -88,6 +88,9 @@ struct MapGroup {
 };
 // Device error word bits (sux_node_check turns a set word into SUX_EHIP).
 constexpr uint32_t kErrTurnTimeout = 1u;  // k_scatter16b: a wave waited 2^22 sleeps for its turn
+constexpr uint32_t kErrLz4Stream = 2u;    // sux_decompress_blocks: a corrupted block
+constexpr uint32_t kErrLz4Capacity = 4u;  // sux_decompress_blocks: output past the capacity
+constexpr uint32_t kErrLz4Checksum = 8u;  // sux_decompress_blocks: a chunk's XXH32 differs
 
 // Per-launch geometry of a group of variable-length record maps (sux_varlen.hip): record i is
 // data[offs[i] - offs[0], offs[i+1] - offs[0]).
@@ -192,6 +195,21 @@ hipError_t launch_lz4_compress(const uint8_t* d_data, const int64_t* d_index, ui
                                uint32_t R, uint32_t bs, uint8_t* d_out, int64_t* d_out_index,
                                uint8_t* d_out_index_be, uint64_t* d_out_bytes, uint8_t* d_ws,
                                const Lz4Workspace& w, bool queue, hipStream_t s);
+// The reader's side (sux_decompress_blocks): one LZ4Block chunk of a fetched block.
+struct Lz4DChunk {
+  uint64_t src, dst;                  // payload offset in the input, decoded offset in the output
+  uint32_t clen, olen, method, csum;  // header fields (method 0x10 raw / 0x20 LZ4)
+};
+struct Lz4DWorkspace {
+  uint64_t counts_off, cbase_off, obytes_off, misc_off, chunks_off, xc_off, temp_off, temp_bytes,
+      chunk_bound, total;
+};
+uint64_t lz4d_chunk_bound(uint64_t in_bytes);
+Lz4DWorkspace lz4d_workspace_layout(uint64_t in_bytes, uint32_t num_blocks);
+hipError_t launch_lz4_decompress(const uint8_t* d_in, uint64_t in_bytes, const int64_t* d_in_off,
+                                 uint32_t nb, uint32_t max_bs, uint8_t* d_out, uint64_t cap,
+                                 int64_t* d_out_off, uint8_t* d_ws, const Lz4DWorkspace& w,
+                                 uint32_t* d_err, hipStream_t s);
 hipError_t launch_rows_index(const uint64_t* sizes, uint32_t maps, uint32_t R, uint64_t* base,
                              int64_t* d_index, uint8_t* d_index_be, hipStream_t s);
 hipError_t launch_partition_ids(const PartDev& pd, const uint8_t* recs, uint32_t rec_size,

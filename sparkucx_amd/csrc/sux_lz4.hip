@@ -610,4 +610,343 @@ hipError_t launch_lz4_compress(const uint8_t* d_data, const int64_t* d_index, ui
   return hipGetLastError();
 }
 
+
+// ---- the reader's side: LZ4BlockInputStream over fetched blocks (sux_decompress_blocks) ----------
+// lz4-java 1.7.1 [ext] LZ4BlockInputStream.refill, as Spark's LZ4CompressionCodec opens it (stream
+// concatenation on: after an end mark the next stream's header may follow, and the input may end
+// at any header boundary): per chunk a 21-byte header — magic, token (method | level), compressed
+// and original LE32 lengths, XXH32 & 0x0FFFFFFF — then the payload; a chunk is corrupted when the
+// original length exceeds 1 << (10 + level) (or our max_block_size), a length is negative, exactly
+// one of them is 0, a raw chunk's lengths differ, the LZ4 block does not decode to exactly the
+// original length from exactly the compressed bytes, or the checksum differs.  An end mark
+// (original length 0) must carry compressed length 0 and checksum 0.
+//   k_lz4d_walk<false>  one thread per block: validate every header, count chunks + decoded bytes
+//   (rocPRIM scans)     -> chunk bases, decoded block offsets (the caller's d_out_offsets)
+//   k_lz4d_total        the totals; output past the capacity: error, nothing decoded
+//   k_lz4d_walk<true>   the chunk table (payload offset, output offset, lengths, method, checksum)
+//   k_lz4d_decode       one wave per chunk: raw -> copy; LZ4 -> payload staged in LDS, decoded
+//                       in LDS, written out as one contiguous range
+//   k_xxh32 + k_lz4d_verify   the checksum of every decoded chunk
+__device__ __forceinline__ uint32_t rd_le32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+__host__ __device__ __forceinline__ uint32_t lz4d_in_cap(uint32_t max_bs) {
+  return max_bs + max_bs / 255u + 16u;  // LZ4_compressBound: the largest block for max_bs bytes
+}
+// the decoder's payload buffer: the payload at its dword phase + the parse window's overhang
+__host__ __device__ __forceinline__ uint32_t lz4d_ib_bytes(uint32_t in_cap) {
+  return (in_cap + 4u + 4u * 64u + 15u) & ~15u;
+}
+
+template <bool FILL>
+__global__ __launch_bounds__(256) void k_lz4d_walk(const uint8_t* __restrict__ in,
+                                                   const int64_t* __restrict__ in_off, uint32_t nb,
+                                                   uint64_t in_bytes, uint32_t max_bs, uint32_t* __restrict__ counts,
+                                                   uint64_t* __restrict__ obytes,
+                                                   const uint32_t* __restrict__ cbase,
+                                                   const int64_t* __restrict__ out_off,
+                                                   const uint32_t* __restrict__ ok,
+                                                   Lz4DChunk* __restrict__ chunks,
+                                                   Lz4Chunk* __restrict__ xc,
+                                                   uint32_t* __restrict__ err) {
+  const uint32_t k = blockIdx.x * 256u + threadIdx.x;
+  if (k >= nb) return;
+  if (FILL && (!*ok || counts[k] == 0)) return;  // capacity error, or an empty / corrupted block
+  const uint64_t b = (uint64_t)in_off[k], e = (uint64_t)in_off[k + 1];
+  uint64_t p = b, o = FILL ? (uint64_t)out_off[k] : 0ull;
+  uint32_t c = 0;
+  bool bad = in_off[k] < 0 || e < b || e > in_bytes;  // a range outside the input
+  while (!bad && p < e) {
+    if (e - p < (uint64_t)kLz4Hdr) { bad = true; break; }  // "Stream ended prematurely"
+    const uint8_t* h = in + p;
+    const char* magic = "LZ4Block";
+    for (int i = 0; i < 8; ++i) bad = bad || h[i] != (uint8_t)magic[i];
+    const uint32_t method = h[8] & 0xF0u, level = h[8] & 0x0Fu;
+    const uint32_t clen = rd_le32(h + 9), olen = rd_le32(h + 13), chk = rd_le32(h + 17);
+    p += kLz4Hdr;
+    if (bad) break;
+    if (olen == 0) {  // an end mark; concatenated streams may follow
+      bad = clen != 0 || chk != 0 || (method != 0x10u && method != 0x20u);
+      continue;
+    }
+    const uint64_t blk = 1ull << (10u + level);
+    bad = (method != 0x10u && method != 0x20u) || (int32_t)clen <= 0 || (int32_t)olen < 0 ||
+          olen > blk || olen > max_bs || (method == 0x10u && clen != olen) ||
+          (method == 0x20u && clen > lz4d_in_cap(max_bs)) || e - p < clen;
+    if (bad) break;
+    if (FILL) {
+      const uint32_t i = cbase[k] + c;
+      chunks[i] = Lz4DChunk{p, o, clen, olen, method, chk};
+      Lz4Chunk x;
+      x.src = o;
+      x.len = olen;
+      x.run = k;
+      x.last = 0;
+      x.clen = 0;
+      x.csum = 0;
+      x.pad = 0;
+      xc[i] = x;
+    }
+    ++c;
+    o += olen;
+    p += clen;
+  }
+  if (FILL) return;
+  if (bad) {
+    atomicOr(err, kErrLz4Stream);
+    c = 0;
+    o = 0;
+  }
+  counts[k] = c;
+  obytes[k] = o;
+}
+
+// The totals after the scans: chunk count (0 when the decoded bytes exceed the capacity, which
+// sets the error word instead), and the decoded total at out_off[nb].
+__global__ void k_lz4d_total(const uint32_t* __restrict__ counts, const uint32_t* __restrict__ cbase,
+                             const uint64_t* __restrict__ obytes, int64_t* __restrict__ out_off,
+                             uint32_t nb, uint64_t cap, uint64_t chunk_bound,
+                             uint32_t* __restrict__ nchunks, uint32_t* __restrict__ ok,
+                             uint32_t* __restrict__ err) {
+  if (threadIdx.x != 0) return;
+  const uint64_t total = nb ? (uint64_t)out_off[nb - 1] + obytes[nb - 1] : 0ull;
+  const uint64_t chunks = nb ? (uint64_t)cbase[nb - 1] + counts[nb - 1] : 0ull;
+  out_off[nb] = (int64_t)total;
+  const bool fits = total <= cap;
+  // the ranges overlap (more headers than the input holds): a caller error, nothing decoded
+  const bool table = chunks <= chunk_bound;
+  if (!fits) atomicOr(err, kErrLz4Capacity);
+  if (!table) atomicOr(err, kErrLz4Stream);
+  *ok = fits && table ? 1u : 0u;
+  *nchunks = fits && table ? (uint32_t)chunks : 0u;
+}
+
+// One wave per chunk (one wave per workgroup, its LDS = the payload + the decoded chunk).  The
+// parse is LZ4's, sequence by sequence, on every lane at once (uniform control flow, the values
+// made scalar with readfirstlane): a 64-byte window at the token serves the token, its length
+// bytes and the offset in one LDS round trip (bytes past the window: one uniform read each); the
+// literal and match copies are wave-wide, one byte per lane and step.  A match byte j is
+// out[op - off + j % off] — inside what was decoded before this match even when the match
+// overlaps itself — so a step's 64 bytes never depend on each other.  The decoded chunk sits in
+// LDS at the output's dword phase, so it leaves as aligned dword stores (bytes at the ends).
+__device__ __forceinline__ uint32_t sgpr(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+__global__ __launch_bounds__(kLWave) void k_lz4d_decode(const uint8_t* __restrict__ in,
+                                                        const Lz4DChunk* __restrict__ chunks,
+                                                        const uint32_t* __restrict__ nchunks,
+                                                        uint32_t in_cap, uint32_t max_bs,
+                                                        uint8_t* __restrict__ out,
+                                                        uint32_t* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int lane = threadIdx.x;
+  const uint32_t n = *nchunks;
+  uint8_t* ib = lds;                           // payload, at its source's dword phase
+  uint8_t* ob = lds + lz4d_ib_bytes(in_cap);  // decoded chunk, at its output's phase
+  uint8_t* sink = lds + lz4d_ib_bytes(in_cap) + ((max_bs + 4u + 15u) & ~15u) + 4u * lane;
+  for (uint32_t c = blockIdx.x; c < n; c += gridDim.x) {
+    const Lz4DChunk C = chunks[c];
+    uint8_t* dst = out + C.dst;
+    if (C.method == 0x10u) {  // stored raw
+      wave_copy(dst, in + C.src, C.olen, lane);
+      continue;
+    }
+    // stage the payload: every aligned dword holding a payload byte (such a dword lies in
+    // mapped memory), so the copy is aligned both sides
+    const uint8_t* src = in + C.src;
+    const uint32_t ia = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 3u);
+    const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src - ia);
+    const uint32_t nd = (ia + C.clen + 3u) / 4u;
+    uint32_t* i4 = reinterpret_cast<uint32_t*>(ib);
+    // 32 loads in flight per lane: a 32 KiB payload in 4 memory round trips (4 at a time took
+    // 32 — the staging, not the parse, bounded the decoder)
+    constexpr uint32_t SU = 32;
+    for (uint32_t t = lane; t < nd; t += SU * kLWave) {
+      uint32_t v[SU];
+#pragma unroll
+      for (uint32_t u = 0; u < SU; ++u) v[u] = s4[min(t + u * kLWave, nd - 1u)];
+#pragma unroll
+      for (uint32_t u = 0; u < SU; ++u)
+        if (t + u * kLWave < nd) i4[t + u * kLWave] = v[u];
+    }
+    wave_lds_sync();
+    const uint8_t* ip8 = ib + ia;
+    const uint32_t oa = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 3u);
+    uint8_t* op8 = ob + oa;
+    const uint32_t iend = C.clen, oend = C.olen;
+    uint32_t ip = 0, op = 0;
+    bool bad = false;
+    const uint32_t* ib32 = reinterpret_cast<const uint32_t*>(ib);
+    while (true) {
+      // a block ends with a literal-only sequence (the LZ4 format; liblz4's safe decoder rejects
+      // a block ending in a match)
+      if (ip >= iend) { bad = true; break; }
+      // a 256-byte window at the token: lane l holds the dword at payload position wp + 4 l
+      // (wp = the token's dword boundary; up to 3 bytes before the token, the LDS padding after
+      // the payload keeps the read in bounds); the token, the length bytes, the offset and the
+      // literals inside it need no LDS read of their own
+      const uint32_t wq = (ia + ip) & ~3u;  // LDS offset of the window in ib
+      const int wp = (int)wq - (int)ia;       // payload position of the window's first byte
+      const uint32_t wv = ib32[(wq >> 2) + (uint32_t)lane];
+      auto byte_at = [&](uint32_t x) -> uint32_t {  // payload byte x (< iend: checked)
+        const uint32_t q = (uint32_t)((int)x - wp);
+        return q < 4u * kLWave
+                   ? ((uint32_t)__builtin_amdgcn_readlane((int)wv, (int)(q >> 2)) >> (8u * (q & 3u))) &
+                         255u
+                   : sgpr(ip8[x]);
+      };
+      const uint32_t tok = byte_at(ip);
+      uint32_t x = ip + 1u, lit = tok >> 4;
+      if (lit == 15u) {
+        uint32_t b;
+        do {
+          if (x >= iend) { bad = true; break; }
+          b = byte_at(x++);
+          lit += b;
+        } while (b == 255u);
+        if (bad) break;
+      }
+      if (iend - x < lit || oend - op < lit) { bad = true; break; }
+      // literals [x, x + lit) -> out[op, ...): the window's bytes by byte stores from this lane's
+      // dword, the rest (a literal run past the window) LDS to LDS
+      const int wend = wp + 4 * kLWave;
+      {
+        // unconditional byte stores (a byte outside the literal goes to this lane's slot past the
+        // buffers): no branch per byte, so no wait between them
+        const int p0 = wp + 4 * lane;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int pj = p0 + j;
+          const bool in = pj >= (int)x && pj < (int)(x + lit);
+          uint8_t* d = in ? op8 + op + (uint32_t)(pj - (int)x) : sink + j;
+          *d = (uint8_t)(wv >> (8 * j));
+        }
+        const uint32_t from = (int)(x + lit) > wend ? (uint32_t)max(wend, (int)x) : x + lit;
+        for (uint32_t k = from + lane; k < x + lit; k += kLWave) op8[op + (k - x)] = ip8[k];
+      }
+      op += lit;
+      x += lit;
+      if (x == iend) break;  // the last sequence: literals only
+      if (iend - x < 2u) { bad = true; break; }
+      const uint32_t off = byte_at(x) | (byte_at(x + 1u) << 8);
+      x += 2u;
+      uint32_t ml = (tok & 15u) + 4u;
+      if ((tok & 15u) == 15u) {
+        uint32_t b;
+        do {
+          if (x >= iend) { bad = true; break; }
+          b = byte_at(x++);
+          ml += b;
+        } while (b == 255u);
+        if (bad) break;
+      }
+      if (off == 0u || off > op || oend - op < ml) { bad = true; break; }
+      // The literals just written may be the match's source: a wave's LDS operations execute
+      // in issue order, so only the compiler must keep them in order (no wait for the writes)
+      asm volatile("" ::: "memory");
+      const uint32_t from = op - off;
+      if (off >= ml) {
+        for (uint32_t k = lane; k < ml; k += kLWave) op8[op + k] = op8[from + k];
+      } else {
+        for (uint32_t k = lane; k < ml; k += kLWave) op8[op + k] = op8[from + k % off];
+      }
+      asm volatile("" ::: "memory");
+      op += ml;
+      ip = x;
+    }
+    if (bad || op != oend) {
+      if (lane == 0) atomicOr(err, kErrLz4Stream);
+      continue;
+    }
+    wave_lds_sync();
+    // out: head bytes up to dst's dword boundary, aligned dwords, tail bytes
+    const uint32_t head = min(oend, (4u - oa) & 3u);
+    if ((uint32_t)lane < head) dst[lane] = op8[lane];
+    const uint32_t body = (oend - head) / 4u;
+    const uint32_t* o4 = reinterpret_cast<const uint32_t*>(op8 + head);  // = ob + 4 (or ob)
+    uint32_t* d4 = reinterpret_cast<uint32_t*>(dst + head);
+    for (uint32_t t = lane; t < body; t += kLWave) d4[t] = o4[t];
+    const uint32_t done = head + 4u * body;
+    if ((uint32_t)lane < oend - done) dst[done + lane] = op8[done + lane];
+    wave_lds_sync();  // the next chunk overwrites the buffers only after every lane read them
+  }
+}
+
+__global__ __launch_bounds__(256) void k_lz4d_verify(const Lz4DChunk* __restrict__ chunks,
+                                                     const Lz4Chunk* __restrict__ xc,
+                                                     const uint32_t* __restrict__ nchunks,
+                                                     uint32_t* __restrict__ err) {
+  const uint32_t n = *nchunks;
+  for (uint32_t c = blockIdx.x * 256u + threadIdx.x; c < n; c += gridDim.x * 256u)
+    if (xc[c].csum != chunks[c].csum) atomicOr(err, kErrLz4Checksum);
+}
+
+uint64_t lz4d_chunk_bound(uint64_t in_bytes) { return in_bytes / kLz4Hdr + 1; }
+
+Lz4DWorkspace lz4d_workspace_layout(uint64_t in_bytes, uint32_t nb) {
+  Lz4DWorkspace w{};
+  const uint64_t cb = lz4d_chunk_bound(in_bytes);
+  uint64_t o = 0;
+  w.counts_off = o;  o += up256((nb + 1) * 4ull);
+  w.cbase_off = o;   o += up256((nb + 1) * 4ull);
+  w.obytes_off = o;  o += up256((nb + 1) * 8ull);
+  w.misc_off = o;    o += 256;  // nchunks, ok
+  w.chunks_off = o;  o += up256(cb * sizeof(Lz4DChunk));
+  w.xc_off = o;      o += up256(cb * sizeof(Lz4Chunk));
+  w.temp_off = o;
+  w.temp_bytes = up256(scan_temp_bytes(nb, nb));
+  o += w.temp_bytes;
+  w.chunk_bound = cb;
+  w.total = o;
+  return w;
+}
+
+hipError_t launch_lz4_decompress(const uint8_t* d_in, uint64_t in_bytes, const int64_t* d_in_off,
+                                 uint32_t nb, uint32_t max_bs, uint8_t* d_out, uint64_t cap,
+                                 int64_t* d_out_off, uint8_t* d_ws, const Lz4DWorkspace& w,
+                                 uint32_t* d_err, hipStream_t s) {
+  uint32_t* counts = reinterpret_cast<uint32_t*>(d_ws + w.counts_off);
+  uint32_t* cbase = reinterpret_cast<uint32_t*>(d_ws + w.cbase_off);
+  uint64_t* obytes = reinterpret_cast<uint64_t*>(d_ws + w.obytes_off);
+  uint32_t* nchunks = reinterpret_cast<uint32_t*>(d_ws + w.misc_off);
+  uint32_t* ok = nchunks + 1;
+  Lz4DChunk* chunks = reinterpret_cast<Lz4DChunk*>(d_ws + w.chunks_off);
+  Lz4Chunk* xc = reinterpret_cast<Lz4Chunk*>(d_ws + w.xc_off);
+  void* temp = d_ws + w.temp_off;
+  const uint32_t g = (nb + 255) / 256;
+  if (nb) {
+    hipLaunchKernelGGL(k_lz4d_walk<false>, dim3(g), dim3(256), 0, s, d_in, d_in_off, nb, in_bytes,
+                       max_bs, counts, obytes, nullptr, nullptr, nullptr, nullptr, nullptr, d_err);
+    size_t tb = w.temp_bytes;
+    hipError_t e = rocprim::exclusive_scan(temp, tb, counts, cbase, 0u, (size_t)nb,
+                                           rocprim::plus<uint32_t>(), s);
+    if (e != hipSuccess) return e;
+    tb = w.temp_bytes;
+    e = rocprim::exclusive_scan(temp, tb, obytes, reinterpret_cast<uint64_t*>(d_out_off), 0ull,
+                                (size_t)nb, rocprim::plus<uint64_t>(), s);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_lz4d_total, dim3(1), dim3(64), 0, s, counts, cbase, obytes, d_out_off, nb,
+                     d_out ? cap : ~0ull, w.chunk_bound, nchunks, ok, d_err);
+  if (nb == 0 || !d_out) return hipGetLastError();  // no output: the decoded sizes only
+  hipLaunchKernelGGL(k_lz4d_walk<true>, dim3(g), dim3(256), 0, s, d_in, d_in_off, nb, in_bytes,
+                     max_bs, counts, obytes, cbase, d_out_off, ok, chunks, xc, d_err);
+  const uint32_t in_cap = lz4d_in_cap(max_bs);
+  const size_t lds = lz4d_ib_bytes(in_cap) + ((max_bs + 4u + 15u) & ~15u) + 4u * kLWave;
+  const uint32_t ncu = (uint32_t)std::max(1, stream_cus(s));
+  const uint32_t per_cu = std::max<uint32_t>(1u, (uint32_t)((160u * 1024u) / lds));
+  const uint32_t dg = (uint32_t)std::min<uint64_t>(w.chunk_bound, (uint64_t)ncu * per_cu);
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lz4d_decode),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(k_lz4d_decode, dim3(dg), dim3(kLWave), lds, s, d_in, chunks, nchunks, in_cap,
+                     max_bs, d_out, d_err);
+  const uint32_t xg = (uint32_t)std::min<uint64_t>((w.chunk_bound + 63) / 64, 4096);
+  hipLaunchKernelGGL(k_xxh32, dim3(xg), dim3(256), 0, s, d_out, xc, nchunks);
+  const uint32_t vg = (uint32_t)std::min<uint64_t>((w.chunk_bound + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_lz4d_verify, dim3(vg), dim3(256), 0, s, chunks, xc, nchunks, d_err);
+  return hipGetLastError();
+}
+
 }  // namespace sux

@@ -129,6 +129,8 @@ _SIGS = {
     "sux_compress_workspace_size": (C.c_int, [U64, I32, I32, I32, C.POINTER(U64)]),
     "sux_compress_map_outputs": (C.c_int, [P, P, U64, P, I32, I32, I32, P, U64, P, P, P, P, U64,
                                            P]),
+    "sux_decompress_workspace_size": (C.c_int, [U64, I32, I32, C.POINTER(U64)]),
+    "sux_decompress_blocks": (C.c_int, [P, P, U64, P, I32, I32, P, U64, P, P, U64, P]),
     "sux_register_shuffle": (C.c_int, [P, I32, I32, I32, I32, C.POINTER(HandleDesc)]),
     "sux_unregister_shuffle": (C.c_int, [P, I32]),
     "sux_write_map_output": (C.c_int, [P, I32, I32, P, P, U64, P]),

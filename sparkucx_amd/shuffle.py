@@ -339,6 +339,47 @@ class Node:
                 "sux_compress_map_outputs")
         return out, out_index, out_index_be, out_bytes
 
+    def decompress_workspace_size(self, in_bytes: int, num_blocks: int,
+                                  max_block_size: int = 32768) -> int:
+        b = C.c_uint64()
+        N.check(self.lib.sux_decompress_workspace_size(in_bytes, num_blocks, max_block_size,
+                                                       C.byref(b)),
+                "sux_decompress_workspace_size")
+        return b.value
+
+    def decompress_blocks(self, data: torch.Tensor, offsets: torch.Tensor,
+                          max_block_size: int = 32768, out: torch.Tensor | None = None,
+                          out_offsets: torch.Tensor | None = None,
+                          workspace: torch.Tensor | None = None, in_bytes: int | None = None,
+                          stream=None):
+        """The reader's side of spark.shuffle.compress=true: the LZ4Block streams of the fetched
+        blocks [offsets[k], offsets[k + 1]) of `data` (device int64 offsets) decoded, blocks
+        consecutive.  Returns (out, out_offsets).  With out=None the decoded size is read first
+        (one host wait: sux_decompress_blocks without an output, then with one).  Corruption or a
+        too-small `out` sets the node's error word: call check()."""
+        nb = offsets.numel() - 1
+        ib = data.numel() if in_bytes is None else in_bytes
+        if out_offsets is None:
+            out_offsets = torch.empty(nb + 1, dtype=torch.int64, device=self.dev)
+        if workspace is None:
+            workspace = torch.empty(self.decompress_workspace_size(ib, nb, max_block_size),
+                                    dtype=torch.uint8, device=self.dev)
+        if out is None:
+            N.check(self.lib.sux_decompress_blocks(self.h, _ptr(data), ib, _ptr(offsets), nb,
+                                                   max_block_size, None, 0, _ptr(out_offsets),
+                                                   _ptr(workspace), workspace.numel(),
+                                                   _stream(stream)),
+                    "sux_decompress_blocks (sizes)")
+            torch.cuda.synchronize(self.dev)
+            total = int(out_offsets[nb].item())
+            out = torch.empty(max(16, total), dtype=torch.uint8, device=self.dev)
+        N.check(self.lib.sux_decompress_blocks(self.h, _ptr(data), ib, _ptr(offsets), nb,
+                                               max_block_size, _ptr(out), out.numel(),
+                                               _ptr(out_offsets), _ptr(workspace),
+                                               workspace.numel(), _stream(stream)),
+                "sux_decompress_blocks")
+        return out, out_offsets
+
     def exchange_group(self, send: torch.Tensor, index: torch.Tensor, num_maps: int, R: int,
                        gathered: torch.Tensor, recv: torch.Tensor, stream=None) -> np.ndarray:
         rb = (C.c_uint64 * self.world_size)()
