@@ -446,7 +446,7 @@ int sux_compress_map_outputs(sux_node* node, const void* d_data, uint64_t data_b
  * Replaces the decompression stream Spark's reader wraps around every fetched block ([ext]
  * BlockStoreShuffleReader -> SerializerManager.wrapStream -> LZ4CompressionCodec.
  * compressedInputStream = lz4-java LZ4BlockInputStream, stream concatenation on), for the blocks
- * one fetch delivered (compat/spark_3_0/UcxShuffleReader.scala:58-96, sux_fetch_blocks): num_blocks
+ * one fetch delivered (compat/spark_3_0/UcxShuffleReader.scala:39-61 wraps them, sux_fetch_blocks): num_blocks
  * byte ranges of d_in (in_bytes in all), block k = [d_in_offsets[k], d_in_offsets[k + 1])
  * (num_blocks + 1 int64 on the device; an empty range is an empty block).  Each range is a
  * sequence of LZ4Block chunks and end marks checked as LZ4BlockInputStream checks them (magic,
