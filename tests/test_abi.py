@@ -200,3 +200,20 @@ def test_group_ranks_executors_by_first_arrival():
         assert lib.sux_group_size(g, C.byref(n)) == 0 and n.value == 8
     finally:
         assert lib.sux_group_destroy(g) == 0
+
+
+def test_decompress_entry_points_validate_arguments():
+    """sux_decompress_blocks / _workspace_size (the reader's side of spark.shuffle.compress):
+    block-size range, block count, NULL arguments — all checked before any HIP call."""
+    lib = N.load()
+    b = C.c_uint64()
+    assert lib.sux_decompress_workspace_size(1 << 20, 10, 32768, C.byref(b)) == 0 and b.value > 0
+    small = b.value
+    assert lib.sux_decompress_workspace_size(1 << 30, 10, 32768, C.byref(b)) == 0 and b.value > small
+    for bs in (0, 63, 65537):
+        assert lib.sux_decompress_workspace_size(1 << 20, 10, bs, C.byref(b)) == N.SUX_EINVAL
+        assert "max_block_size" in N.last_error()
+    assert lib.sux_decompress_workspace_size(1 << 20, -1, 32768, C.byref(b)) == N.SUX_EINVAL
+    assert lib.sux_decompress_workspace_size(1 << 20, 10, 32768, None) == N.SUX_EINVAL
+    assert lib.sux_decompress_blocks(None, None, 0, None, 0, 32768, None, 0, None, None, 0,
+                                     None) == N.SUX_EINVAL
