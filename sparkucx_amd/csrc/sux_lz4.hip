@@ -633,9 +633,16 @@ __device__ __forceinline__ uint32_t rd_le32(const uint8_t* p) {
 __host__ __device__ __forceinline__ uint32_t lz4d_in_cap(uint32_t max_bs) {
   return max_bs + max_bs / 255u + 16u;  // LZ4_compressBound: the largest block for max_bs bytes
 }
-// the decoder's payload buffer: the payload at its dword phase + the parse window's overhang
-__host__ __device__ __forceinline__ uint32_t lz4d_ib_bytes(uint32_t in_cap) {
-  return (in_cap + 4u + 4u * 64u + 15u) & ~15u;
+// The decoder's one buffer per wave: LZ4 in-place decompression (lz4.h, LZ4_DECOMPRESS_INPLACE_
+// MARGIN): the payload staged at the END of a buffer of the decoded size + (clen >> 8) + 32, the
+// output written from its start — the output never overtakes the unread input — then the parse
+// window's 256-byte overhang; the byte-store sink after it.
+__host__ __device__ __forceinline__ uint32_t lz4d_buf_bytes(uint32_t max_bs, uint32_t in_cap) {
+  const uint32_t a = max_bs + (in_cap >> 8) + 32u + 16u, b = in_cap + 16u;
+  return ((a > b ? a : b) + 15u) & ~15u;
+}
+__host__ __device__ __forceinline__ uint32_t lz4d_lds_bytes(uint32_t max_bs, uint32_t in_cap) {
+  return lz4d_buf_bytes(max_bs, in_cap) + 4u * 64u + 4u * 64u;
 }
 
 template <bool FILL>
@@ -721,7 +728,8 @@ __global__ void k_lz4d_total(const uint32_t* __restrict__ counts, const uint32_t
   *nchunks = fits && table ? (uint32_t)chunks : 0u;
 }
 
-// One wave per chunk (one wave per workgroup, its LDS = the payload + the decoded chunk).  The
+// One wave per chunk (one wave per workgroup, its LDS = one in-place buffer: four per CU at
+// 32 KiB blocks, where separate payload and output buffers allowed two).  The
 // parse is LZ4's, sequence by sequence, on every lane at once (uniform control flow, the values
 // made scalar with readfirstlane): a 64-byte window at the token serves the token, its length
 // bytes and the offset in one LDS round trip (bytes past the window: one uniform read each); the
@@ -742,9 +750,8 @@ __global__ __launch_bounds__(kLWave) void k_lz4d_decode(const uint8_t* __restric
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x;
   const uint32_t n = *nchunks;
-  uint8_t* ib = lds;                           // payload, at its source's dword phase
-  uint8_t* ob = lds + lz4d_ib_bytes(in_cap);  // decoded chunk, at its output's phase
-  uint8_t* sink = lds + lz4d_ib_bytes(in_cap) + ((max_bs + 4u + 15u) & ~15u) + 4u * lane;
+  uint8_t* ob = lds;  // decoded chunk, at its output's dword phase
+  uint8_t* sink = lds + lz4d_buf_bytes(max_bs, in_cap) + 4u * kLWave + 4u * lane;
   for (uint32_t c = blockIdx.x; c < n; c += gridDim.x) {
     const Lz4DChunk C = chunks[c];
     uint8_t* dst = out + C.dst;
@@ -756,6 +763,11 @@ __global__ __launch_bounds__(kLWave) void k_lz4d_decode(const uint8_t* __restric
     // mapped memory), so the copy is aligned both sides
     const uint8_t* src = in + C.src;
     const uint32_t ia = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 3u);
+    const uint32_t oa = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 3u);
+    // in place: the payload ends >= the in-place margin past the decoded bytes (a payload longer
+    // than that — no LZ4 encoder makes one — starts at 0 and decodes to a checksum error at worst)
+    const uint32_t pend = oa + C.olen + (C.clen >> 8) + 32u;
+    uint8_t* ib = lds + (pend > C.clen ? ((pend - C.clen + 3u) & ~3u) : 0u);
     const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src - ia);
     const uint32_t nd = (ia + C.clen + 3u) / 4u;
     uint32_t* i4 = reinterpret_cast<uint32_t*>(ib);
@@ -772,7 +784,6 @@ __global__ __launch_bounds__(kLWave) void k_lz4d_decode(const uint8_t* __restric
     }
     wave_lds_sync();
     const uint8_t* ip8 = ib + ia;
-    const uint32_t oa = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 3u);
     uint8_t* op8 = ob + oa;
     const uint32_t iend = C.clen, oend = C.olen;
     uint32_t ip = 0, op = 0;
@@ -933,7 +944,7 @@ hipError_t launch_lz4_decompress(const uint8_t* d_in, uint64_t in_bytes, const i
   hipLaunchKernelGGL(k_lz4d_walk<true>, dim3(g), dim3(256), 0, s, d_in, d_in_off, nb, in_bytes,
                      max_bs, counts, obytes, cbase, d_out_off, ok, chunks, xc, d_err);
   const uint32_t in_cap = lz4d_in_cap(max_bs);
-  const size_t lds = lz4d_ib_bytes(in_cap) + ((max_bs + 4u + 15u) & ~15u) + 4u * kLWave;
+  const size_t lds = lz4d_lds_bytes(max_bs, in_cap);
   const uint32_t ncu = (uint32_t)std::max(1, stream_cus(s));
   const uint32_t per_cu = std::max<uint32_t>(1u, (uint32_t)((160u * 1024u) / lds));
   const uint32_t dg = (uint32_t)std::min<uint64_t>(w.chunk_bound, (uint64_t)ncu * per_cu);
