@@ -1280,7 +1280,16 @@ __device__ void make_sort_plan(const uint32_t* span, int bits, int tb, SortPlanD
     const int dl = 128 - (int)(d >> 64 ? __builtin_clzll((uint64_t)(d >> 64))
                                        : 64 + ((uint64_t)d ? __builtin_clzll((uint64_t)d) : 64));
     sh = max(sh, dl - tb);  // below it the span alone needs more than 2^tb blocks
-    while (sh < top_lo && ((mx >> sh) - (mn >> sh)) >= ((u128)1 << tb)) ++sh;
+    // the lowest sh in [sh, top_lo] with (mx >> sh) - (mn >> sh) < 2^tb (non-increasing in sh,
+    // and true at top_lo): a binary search, not a step per bit (one thread plans the sort)
+    if (sh < top_lo && ((mx >> sh) - (mn >> sh)) >= ((u128)1 << tb)) {
+      int lo = sh, hi = top_lo;  // f(lo) fails, f(hi) holds
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (((mx >> mid) - (mn >> mid)) >= ((u128)1 << tb)) lo = mid; else hi = mid;
+      }
+      sh = hi;
+    }
     top_lo = min(sh, top_lo);
     top_base = (uint64_t)(mn >> top_lo);
     // Rebase (fused-gather sorts only) when the aligned blocks leave more than a third of the
