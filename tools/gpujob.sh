@@ -78,7 +78,7 @@ case $job in
   sortab)
     for i in 1 2; do
       for lib in "$1" "$2"; do
-        for inp in random partition; do
+        for inp in random partition ${SORTAB_EXTRA:-}; do
           SORT_PROF_INPUT=$inp timeout -k 10 120 python3 tools/sort_prof.py 20 "" $lib \
             >> $O/sortab.txt 2>&1 || exit 1
         done
