@@ -252,3 +252,40 @@ def test_sizes_only_call(gpu_node):
     torch.cuda.synchronize()
     gpu_node.check()
     assert oo.cpu().tolist() == [0, len(raw)]
+
+
+def test_fuzzed_blocks_never_write_outside_the_output(gpu_node):
+    """300 corrupted variants of a multi-chunk stream (a flipped byte anywhere — header, lengths,
+    tokens, offsets, literals — or a cut at any length) decoded as 300 blocks of one call: the
+    call completes, nothing past the output capacity changes, and the decoder decodes a good
+    stream afterwards.  (Which variants are rejected is the error word's business; a variant that
+    still parses decodes to bytes of its own.)"""
+    rng = np.random.default_rng(11)
+    raw = np.concatenate([O.gen_terasort(70, 0, 600).ravel(),
+                          np.tile(np.arange(9, dtype=np.uint8), 4000)]).tobytes()
+    good = bytes(_one_stream(raw, 4096))
+    variants = []
+    for k in range(300):
+        v = bytearray(good)
+        if k % 5 == 4:
+            v = v[:int(rng.integers(0, len(v)))]
+        else:
+            pos = int(rng.integers(0, len(v)))
+            v[pos] ^= int(rng.integers(1, 256))
+        variants.append(bytes(v))
+    blob = b"".join(variants)
+    offs = np.concatenate([[0], np.cumsum([len(v) for v in variants])]).astype(np.int64)
+    cap = 300 * len(raw) + 4096
+    out = torch.zeros(cap + 4096, dtype=torch.uint8, device="cuda")
+    guard = out[cap:].clone()
+    gpu_node.decompress_blocks(to_dev(blob), to_dev(offs), 4096, out=out[:cap],
+                               in_bytes=len(blob))
+    torch.cuda.synchronize()
+    try:
+        gpu_node.check()
+    except N.SuxError as e:
+        assert e.code == N.SUX_EHIP
+    assert torch.equal(out[cap:], guard)
+    got, oo = decode(gpu_node, good, np.array([0, len(good)], np.int64), 4096)
+    gpu_node.check()
+    assert got[:len(raw)].cpu().numpy().tobytes() == raw
