@@ -149,3 +149,14 @@ def test_eight_ranks_verified_with_the_plugin_leg(tmp_path):
     assert res["self_check"]["ok"] and res["self_check"]["groups"] == 3
     assert res["plugin"]["self_check"] == "ok" and res["plugin"]["maps"] == 2 * 8 * 2
     assert len({(r, p) for _, r, p, _ in msgs}) == 64  # every ordered pair, self included
+
+
+def test_three_ranks_uneven_partitions_verified(tmp_path):
+    """W = 3 over R = 10 (owners of 3, 3 and 4 partitions), post-issue, every block checked
+    against the CPU oracle: an odd world and an uneven split through the RCCL path."""
+    res, msgs = _run(3, tmp_path, "--exchange", "post-issue", "--partitions", "10", "--records",
+                     "120000", "--map-records", "20000", "--group-maps", "2", "--steps", "1",
+                     "--warmup", "0", "--verify", "--plugin-groups", "0")
+    assert res["n_gpus"] == 3 and res["verified_groups"] == 3
+    assert res["self_check"]["ok"]
+    assert {(r, p) for _, r, p, _ in msgs} >= {(r, p) for r in range(3) for p in range(3) if r != p}
