@@ -726,6 +726,7 @@ __global__ void k_lz4d_total(const uint32_t* __restrict__ counts, const uint32_t
   if (!table) atomicOr(err, kErrLz4Stream);
   *ok = fits && table ? 1u : 0u;
   *nchunks = fits && table ? (uint32_t)chunks : 0u;
+  nchunks[2] = 0u;  // k_lz4d_decode's work-queue counter
 }
 
 // One wave per chunk (one wave per workgroup, its LDS = one in-place buffer: four per CU at
@@ -746,13 +747,17 @@ __global__ __launch_bounds__(kLWave) void k_lz4d_decode(const uint8_t* __restric
                                                         const uint32_t* __restrict__ nchunks,
                                                         uint32_t in_cap, uint32_t max_bs,
                                                         uint8_t* __restrict__ out,
+                                                        uint32_t* __restrict__ qctr,
                                                         uint32_t* __restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x;
   const uint32_t n = *nchunks;
   uint8_t* ob = lds;  // decoded chunk, at its output's dword phase
   uint8_t* sink = lds + lz4d_buf_bytes(max_bs, in_cap) + 4u * kLWave + 4u * lane;
-  for (uint32_t c = blockIdx.x; c < n; c += gridDim.x) {
+  // chunks from a work queue (k_lz4d_total zeroed its counter on this stream): a chunk's cost
+  // varies with its sequences, so a fixed deal left the launch's tail to the unlucky waves; the
+  // counter only grows, the index reaches the wave through readfirstlane (a wave-uniform exit)
+  for (uint32_t c = lz4_claim(qctr, lane); c < n; c = lz4_claim(qctr, lane)) {
     const Lz4DChunk C = chunks[c];
     uint8_t* dst = out + C.dst;
     if (C.method == 0x10u) {  // stored raw
@@ -902,7 +907,7 @@ Lz4DWorkspace lz4d_workspace_layout(uint64_t in_bytes, uint32_t nb) {
   w.counts_off = o;  o += up256((nb + 1) * 4ull);
   w.cbase_off = o;   o += up256((nb + 1) * 4ull);
   w.obytes_off = o;  o += up256((nb + 1) * 8ull);
-  w.misc_off = o;    o += 256;  // nchunks, ok
+  w.misc_off = o;    o += 256;  // nchunks, ok, the decode queue counter
   w.chunks_off = o;  o += up256(cb * sizeof(Lz4DChunk));
   w.xc_off = o;      o += up256(cb * sizeof(Lz4Chunk));
   w.temp_off = o;
@@ -952,7 +957,7 @@ hipError_t launch_lz4_decompress(const uint8_t* d_in, uint64_t in_bytes, const i
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lz4d_decode),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(k_lz4d_decode, dim3(dg), dim3(kLWave), lds, s, d_in, chunks, nchunks, in_cap,
-                     max_bs, d_out, d_err);
+                     max_bs, d_out, nchunks + 2, d_err);
   const uint32_t xg = (uint32_t)std::min<uint64_t>((w.chunk_bound + 63) / 64, 4096);
   hipLaunchKernelGGL(k_xxh32, dim3(xg), dim3(256), 0, s, d_out, xc, nchunks);
   const uint32_t vg = (uint32_t)std::min<uint64_t>((w.chunk_bound + 255) / 256, 1024);
