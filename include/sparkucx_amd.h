@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define SUX_ABI_VERSION 5
+#define SUX_ABI_VERSION 6
 
 /* ---- status codes ---------------------------------------------------------------------- */
 #define SUX_OK 0
@@ -521,6 +521,21 @@ int sux_write_map_output(sux_node* node, int32_t shuffle_id, int32_t map_index,
 int sux_write_map_outputs(sux_node* node, int32_t shuffle_id, int32_t first_map_index,
                           const sux_partitioner* part, const void* d_records,
                           uint64_t records_per_map, uint64_t num_records, void* stream);
+/* spark.shuffle.compress for the maps this node writes (sux_write_map_output(s) / _host):
+ * SUX_CODEC_LZ4 = every non-empty (map, partition) run committed as its own lz4-java
+ * LZ4BlockOutputStream stream of block_size-byte chunks (spark.io.compression.lz4.blockSize,
+ * Spark's default 32768), byte-equal to what Spark's writers produce through
+ * SerializerManager.wrapStream -> LZ4CompressionCodec.compressedOutputStream [ext] around each
+ * partition segment (the writers chosen at compat/spark_3_0/UcxShuffleManager.scala:36-50); the
+ * committed index file and the MapStatus lengths are then the compressed ones, and a reducer's
+ * wrapStream decodes the fetched blocks exactly as it decodes Spark-written ones
+ * (compat/spark_3_0/UcxShuffleReader.scala:61).  SUX_CODEC_NONE (the default) = raw data files
+ * (spark.shuffle.compress=false).  Only before the shuffle's first map output (SUX_ESTATE after).
+ * Map outputs committed by sux_commit_map_output / _adopt_ are taken as they are: Spark's own
+ * writers already applied the codec. */
+#define SUX_CODEC_NONE 0
+#define SUX_CODEC_LZ4 1
+int sux_shuffle_set_codec(sux_node* node, int32_t shuffle_id, int32_t codec, int32_t block_size);
 /* Block until every map output enqueued for the shuffle (by any thread) is published. */
 int sux_wait_map_outputs(sux_node* node, int32_t shuffle_id);
 /* sux_write_map_output for records the JVM serialized into host memory (Spark's serializer
@@ -630,6 +645,17 @@ int sux_buffer_alloc(sux_node* node, uint64_t bytes, sux_buffer** out);
 int sux_buffer_read(sux_buffer* buf, uint64_t offset, void* host_dst, uint64_t len, void* stream);
 int sux_buffer_retain(sux_buffer* buf, int32_t count);
 int sux_buffer_release(sux_buffer* buf);
+/* The reducer's decode of fetched LZ4Block streams (spark.shuffle.compress=true, lz4 codec) on
+ * the device, for a consumer that needs the rows themselves on the GPU (the JVM reader's GPU key
+ * sort, which replaces ExternalSorter at compat/spark_3_0/UcxShuffleReader.scala:138-154, after
+ * the wrapStream of :61): num_blocks consecutive blocks of `in` starting at in_offset (host
+ * block_sizes) are decoded as sux_decompress_blocks decodes them into a new pooled buffer (one
+ * reference), blocks consecutive; out_sizes (optional, num_blocks) receives each block's decoded
+ * size.  Waits for the decoded sizes and for the decode; a corrupted stream is SUX_EIO (Spark's
+ * "Stream is corrupted"), and then no buffer is returned. */
+int sux_buffer_decompress(sux_node* node, sux_buffer* in, uint64_t in_offset,
+                          const int64_t* block_sizes, int32_t num_blocks, int32_t max_block_size,
+                          sux_buffer** out, int64_t* out_sizes, void* stream);
 
 /* ---- reduce side: sort by key ------------------------------------- *
  * After the fetch, Spark's reader sorts the partition's records when the dependency has a key

@@ -439,11 +439,17 @@ struct WriteJob {
   std::pair<void*, uint64_t> hidx{nullptr, 0};  // pinned copy of the batch's index tables
   const int64_t* dindex = nullptr;  // adopted at world 1: the index tables stay on the device
   uint32_t rs = 0;                  // (and the maps' sizes come from their record counts)
+  // compressed shuffle (sux_shuffle_set_codec): the maps are packed back to back in the slab,
+  // map k starting where map k - 1's compressed data file ends
+  bool packed = false;
   std::shared_ptr<Event> done;
 };
 
 struct Shuffle {
   int32_t id = 0, num_maps = 0, R = 0, rec_size = 0;
+  // spark.shuffle.compress with the lz4 codec (sux_shuffle_set_codec): the maps the node writes
+  // are committed as lz4-java LZ4BlockOutputStream streams of codec_block-byte chunks
+  int32_t codec = SUX_CODEC_NONE, codec_block = 0;
   std::vector<MapSlot> maps;
   std::vector<uint8_t> directory;  // num_maps * metadata_block_size bytes (big-endian fields)
   std::vector<std::unique_ptr<WriteJob>> jobs;
@@ -700,6 +706,7 @@ void publish_job(sux_node* node, Shuffle& sh, WriteJob& j) {
   auto ix = [&](uint32_t k, int p) { return hx[(uint64_t)k * (R + 1) + p]; };
   // peer-major: sections [h] of the whole job (every map the kernels wrote, claimed or not)
   std::vector<uint64_t> run((size_t)W, 0);
+  uint64_t packed_off = 0;  // packed (compressed) maps: where map k starts in the slab
   if (W > 1) {
     uint64_t acc = 0;
     for (int h = 0; h < W; ++h) {
@@ -717,7 +724,7 @@ void publish_job(sux_node* node, Shuffle& sh, WriteJob& j) {
       slot.owner = node->conf.rank;
       slot.slab = j.slab;
       slot.batch = j.batch >= 0 ? j.batch : sh.next_batch++;  // map-major at W > 1: own piece
-      slot.off = (uint64_t)k * j.rpm * (uint64_t)sh.rec_size;
+      slot.off = j.packed ? packed_off : (uint64_t)k * j.rpm * (uint64_t)sh.rec_size;
       slot.bytes = (uint64_t)ix(k, R);
       slot.index.assign(hx + (uint64_t)k * (R + 1), hx + (uint64_t)(k + 1) * (R + 1));
       slot.d_index = nullptr;
@@ -731,6 +738,7 @@ void publish_job(sux_node* node, Shuffle& sh, WriteJob& j) {
       }
       publish_slot(node, sh, j.first + (int32_t)k, 0);
     }
+    packed_off += (uint64_t)ix(k, R);
     if (W > 1)
       for (int h = 0; h < W; ++h)
         run[h] += (uint64_t)(ix(k, owner_lo(h + 1, R, W)) - ix(k, owner_lo(h, R, W)));
@@ -2533,6 +2541,26 @@ int sux_register_shuffle(sux_node* node, int32_t shuffle_id, int32_t num_maps, i
   });
 }
 
+int sux_shuffle_set_codec(sux_node* node, int32_t shuffle_id, int32_t codec, int32_t block_size) {
+  return guard([&] {
+    require(node, SUX_EINVAL, "NULL node");
+    require(codec == SUX_CODEC_NONE || codec == SUX_CODEC_LZ4, SUX_EINVAL,
+            "codec must be SUX_CODEC_NONE or SUX_CODEC_LZ4, got " + std::to_string(codec));
+    if (codec == SUX_CODEC_LZ4)
+      require(block_size >= 64 && block_size <= 65536 && block_size % 4 == 0, SUX_EINVAL,
+              "spark.io.compression.lz4.blockSize must be a multiple of 4 in [64, 65536], got " +
+                  std::to_string(block_size));
+    std::lock_guard<std::mutex> lk(node->mu);
+    Shuffle& sh = node->shuffle(shuffle_id);
+    bool written = !sh.jobs.empty() || sh.submitting > 0 || sh.busy > 0;
+    for (const MapSlot& m : sh.maps) written = written || m.present || m.pending;
+    require(!written, SUX_ESTATE,
+            "shuffle " + std::to_string(shuffle_id) + " already has map outputs: set its codec first");
+    sh.codec = codec;
+    sh.codec_block = codec == SUX_CODEC_LZ4 ? block_size : 0;
+  });
+}
+
 int sux_unregister_shuffle(sux_node* node, int32_t shuffle_id) {
   return guard([&] {
     require(node, SUX_EINVAL, "NULL node");
@@ -2570,9 +2598,12 @@ int sux_write_map_outputs(sux_node* node, int32_t shuffle_id, int32_t first,
     auto job = std::make_unique<WriteJob>();
     int R = 0;
     uint32_t rs = 0;
+    int32_t codec = SUX_CODEC_NONE, cblock = 0;
     {
       std::unique_lock<std::mutex> lk(node->mu);
       Shuffle& sh = node->shuffle(shuffle_id);
+      codec = sh.codec;
+      cblock = sh.codec_block;
       require(first >= 0 && (uint64_t)first + maps <= (uint64_t)sh.num_maps, SUX_EINVAL,
               "maps [" + std::to_string(first) + ", " + std::to_string((uint64_t)first + maps) +
                   ") out of [0, " + std::to_string(sh.num_maps) + ")");
@@ -2622,12 +2653,40 @@ int sux_write_map_outputs(sux_node* node, int32_t shuffle_id, int32_t first,
     // range, so the exchange sends the slab as it stands (one all-to-all per batch, no repack)
     const int32_t W = node->conf.world_size;
     job->world = W;
+    const bool lz4 = codec == SUX_CODEC_LZ4;
     try {
       Group G = make_group(part, d_records, rs, rpm, n);
-      job->slab = std::make_shared<Slab>(node->pool.get(), pool_get_or_spill(node, n * rs));
-      job->ws = pool_get_or_spill(node, G.ws.total + 8 * maps * (uint64_t)(R + 1) + 256);
+      auto up = [](uint64_t v) { return (v + 255) / 256 * 256; };
+      const uint64_t ix_bytes = 8 * maps * (uint64_t)(R + 1);
+      // compressed shuffle: the maps are partitioned map-major into scratch (`plain`), then every
+      // non-empty (map, partition) run is compressed into the slab as its own LZ4Block stream —
+      // the per-partition wrapStream of Spark's writers under spark.shuffle.compress — and the
+      // committed index is the compressed one (the MapStatus lengths are compressed lengths)
+      sux::Lz4Workspace lw{};
+      uint64_t plain_off = 0, lws_off = 0, cix_off = 0, cbytes_off = 0, ws_total = 0;
+      uint64_t slab_bytes = n * rs;
+      if (lz4) {
+        check_lz4_args(n * rs, (int32_t)maps, R, cblock);
+        lw = sux::lz4_workspace_layout(n * rs, (uint32_t)maps, (uint32_t)R, (uint32_t)cblock);
+        slab_bytes = sux::lz4_output_bound(n * rs, maps * (uint64_t)R, (uint32_t)cblock);
+        plain_off = up(G.ws.total) + up(ix_bytes);
+        lws_off = plain_off + up(n * rs);
+        cix_off = lws_off + up(lw.total);
+        cbytes_off = cix_off + up(ix_bytes);
+        ws_total = cbytes_off + 256;
+      } else {
+        ws_total = G.ws.total + ix_bytes + 256;
+      }
+      job->slab = std::make_shared<Slab>(node->pool.get(), pool_get_or_spill(node, slab_bytes));
+      job->ws = pool_get_or_spill(node, ws_total);
       int64_t* d_idx = reinterpret_cast<int64_t*>(job->ws.ptr + (G.ws.total + 255) / 256 * 256);
-      if (W == 1) {
+      if (lz4) {
+        // packed map-major outputs at any world (each map its own exchange piece at W > 1, like
+        // a committed data file); the compressed index tables come back to the host
+        job->world = 1;
+        job->packed = true;
+        job->hidx = node->hpool.get(ix_bytes);
+      } else if (W == 1) {
         // world 1: the index tables stay on the device with the slab (no maps x (R + 1) read-back
         // per batch; resolves gather the entries they need, host_index the rest on demand)
         job->slab->aux = pool_get_or_spill(node, 8 * maps * (uint64_t)(R + 1));
@@ -2639,19 +2698,34 @@ int sux_write_map_outputs(sux_node* node, int32_t shuffle_id, int32_t first,
       }
       {
         std::lock_guard<std::mutex> lk(node->mu);
-        job->batch = node->shuffle(shuffle_id).next_batch++;
+        // packed at W > 1: one exchange piece per map, assigned when published
+        job->batch = lz4 && W > 1 ? -1 : node->shuffle(shuffle_id).next_batch++;
       }
       std::lock_guard<std::mutex> plk(node->pipe_mu);
       node->make_pipe();
       ms = node->pipe[node->pipe_next++ & 1];
       hip_check(hipEventRecord(node->pipe_ev[0], s), "fork");
       hip_check(hipStreamWaitEvent(ms, node->pipe_ev[0], 0), "fork");
-      run_group(node, part, G, W, job->slab->buf.ptr, d_idx, nullptr, nullptr, nullptr,
-                job->ws.ptr, G.ws.total, ms, true);
-      if (W != 1)
-        hip_check(hipMemcpyAsync(job->hidx.first, d_idx, 8 * maps * (uint64_t)(R + 1),
-                                 hipMemcpyDeviceToHost, ms),
-                  "D2H index");
+      if (lz4) {
+        uint8_t* plain = job->ws.ptr + plain_off;
+        int64_t* d_cix = reinterpret_cast<int64_t*>(job->ws.ptr + cix_off);
+        run_group(node, part, G, 1, plain, d_idx, nullptr, nullptr, nullptr, job->ws.ptr,
+                  G.ws.total, ms, true);
+        hip_check(sux::launch_lz4_compress(plain, d_idx, (uint32_t)maps, (uint32_t)R,
+                                           (uint32_t)cblock, job->slab->buf.ptr, d_cix, nullptr,
+                                           reinterpret_cast<uint64_t*>(job->ws.ptr + cbytes_off),
+                                           job->ws.ptr + lws_off, lw,
+                                           resolve_tuning(node->tuning, false).lz4_queue, ms),
+                  "compress launch");
+        hip_check(hipMemcpyAsync(job->hidx.first, d_cix, ix_bytes, hipMemcpyDeviceToHost, ms),
+                  "D2H compressed index");
+      } else {
+        run_group(node, part, G, W, job->slab->buf.ptr, d_idx, nullptr, nullptr, nullptr,
+                  job->ws.ptr, G.ws.total, ms, true);
+        if (W != 1)
+          hip_check(hipMemcpyAsync(job->hidx.first, d_idx, ix_bytes, hipMemcpyDeviceToHost, ms),
+                    "D2H index");
+      }
       job->done = std::make_shared<Event>();
       hip_check(hipEventRecord(job->done->e, ms), "hipEventRecord");
       hip_check(hipStreamWaitEvent(s, job->done->e, 0), "join");
@@ -3929,6 +4003,97 @@ int sux_buffer_release(sux_buffer* b) {
         b->node->pool->put(b->aux);
       }
       delete b;
+    }
+  });
+}
+
+// The reader's side of spark.shuffle.compress (the GPU-sort path of the JVM reader, which must
+// decode the LZ4Block streams it fetched before sorting rows): blocks k of `in`, consecutive from
+// in_offset, decoded into a new pooled buffer.  One host wait (the decoded sizes), one at the end
+// (the device error word: a corrupted stream is SUX_EIO, Spark's "Stream is corrupted").
+int sux_buffer_decompress(sux_node* node, sux_buffer* in, uint64_t in_offset,
+                          const int64_t* block_sizes, int32_t num_blocks, int32_t max_block_size,
+                          sux_buffer** out, int64_t* out_sizes, void* stream) {
+  return guard([&] {
+    require(node && in && out && (block_sizes || num_blocks == 0), SUX_EINVAL, "NULL argument");
+    require(in->node == node, SUX_EINVAL, "the buffer belongs to another node");
+    require(num_blocks >= 0, SUX_EINVAL, "negative block count");
+    std::vector<int64_t> ioff((size_t)num_blocks + 1);
+    uint64_t total = 0;
+    for (int32_t k = 0; k < num_blocks; ++k) {
+      require(block_sizes[k] >= 0, SUX_EINVAL, "negative block size");
+      ioff[k] = (int64_t)(in_offset + total);
+      total += (uint64_t)block_sizes[k];
+    }
+    ioff[num_blocks] = (int64_t)(in_offset + total);
+    require(in_offset <= in->size && total <= in->size - in_offset, SUX_ERANGE,
+            "blocks [" + std::to_string(in_offset) + ", +" + std::to_string(total) +
+                ") past a buffer of " + std::to_string(in->size) + " bytes");
+    check_lz4d_args(in_offset + total, num_blocks, max_block_size);
+    node->bind();
+    hipStream_t s = node->stream(stream);
+    const uint64_t ws_bytes =
+        sux::lz4d_workspace_layout(in_offset + total, (uint32_t)num_blocks).total;
+    const uint64_t tab = (uint64_t)(num_blocks + 1) * 8;
+    const uint64_t tab_up = (tab + 255) / 256 * 256;
+    PoolBuf aux = pool_get_or_spill(node, ws_bytes + 2 * tab_up);
+    PoolBuf dst{};
+    auto give_back = [&] {
+      (void)hipStreamSynchronize(s);
+      node->pool->put(aux);
+      if (dst.ptr) node->pool->put(dst);
+    };
+    try {
+      int64_t* d_ioff = reinterpret_cast<int64_t*>(aux.ptr + ws_bytes);
+      int64_t* d_ooff = reinterpret_cast<int64_t*>(aux.ptr + ws_bytes + tab_up);
+      std::vector<int64_t> ooff((size_t)num_blocks + 1, 0);
+      hip_check(hipMemcpyAsync(d_ioff, ioff.data(), tab, hipMemcpyHostToDevice, s), "H2D offsets");
+      auto device_error = [&] {
+        hip_check(hipStreamSynchronize(s), "sync decompress");
+        const uint32_t w = take_device_err(node);
+        if (w & (sux::kErrLz4Stream | sux::kErrLz4Checksum))
+          raise(SUX_EIO, "Stream is corrupted: a fetched block is not a valid LZ4Block stream "
+                         "(header, lengths, LZ4 sequence or checksum)");
+        if (w) raise(SUX_EHIP, "device error word set while decompressing");
+      };
+      // pass 1: the decoded sizes
+      hip_check(sux::launch_lz4_decompress(in->buf.ptr, in_offset + total, d_ioff,
+                                           (uint32_t)num_blocks, (uint32_t)max_block_size, nullptr,
+                                           0, d_ooff, aux.ptr,
+                                           sux::lz4d_workspace_layout(in_offset + total,
+                                                                      (uint32_t)num_blocks),
+                                           node->d_err, s),
+                "decompress sizes");
+      hip_check(hipMemcpyAsync(ooff.data(), d_ooff, tab, hipMemcpyDeviceToHost, s), "D2H sizes");
+      device_error();
+      const uint64_t decoded = (uint64_t)ooff[num_blocks];
+      dst = pool_get_or_spill(node, decoded ? decoded : 1);
+      if (decoded) {
+        hip_check(sux::launch_lz4_decompress(in->buf.ptr, in_offset + total, d_ioff,
+                                             (uint32_t)num_blocks, (uint32_t)max_block_size,
+                                             dst.ptr, decoded, d_ooff, aux.ptr,
+                                             sux::lz4d_workspace_layout(in_offset + total,
+                                                                        (uint32_t)num_blocks),
+                                             node->d_err, s),
+                  "decompress");
+        device_error();
+      }
+      auto buf = std::make_unique<sux_buffer>();
+      buf->node = node;
+      buf->size = decoded;
+      buf->refs = 1;
+      buf->buf = dst;
+      if (out_sizes)
+        for (int32_t k = 0; k < num_blocks; ++k) out_sizes[k] = ooff[k + 1] - ooff[k];
+      node->pool->put(aux);
+      {
+        std::lock_guard<std::mutex> lk(node->live_mu);
+        node->live_bufs.insert(buf.get());
+      }
+      *out = buf.release();
+    } catch (...) {
+      give_back();
+      throw;
     }
   });
 }

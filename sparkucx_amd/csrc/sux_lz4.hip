@@ -655,6 +655,7 @@ __global__ __launch_bounds__(256) void k_lz4d_walk(const uint8_t* __restrict__ i
                                                    const uint32_t* __restrict__ ok,
                                                    Lz4DChunk* __restrict__ chunks,
                                                    Lz4Chunk* __restrict__ xc,
+                                                   unsigned long long* __restrict__ total,
                                                    uint32_t* __restrict__ err) {
   const uint32_t k = blockIdx.x * 256u + threadIdx.x;
   if (k >= nb) return;
@@ -706,6 +707,9 @@ __global__ __launch_bounds__(256) void k_lz4d_walk(const uint8_t* __restrict__ i
   }
   counts[k] = c;
   obytes[k] = o;
+  // the chunk total in 64 bits: blocks whose ranges overlap (non-monotone
+  // in_offsets) can hold more headers than the input, and the u32 scan of counts would wrap
+  if (c) atomicAdd(total, (unsigned long long)c);
 }
 
 // The totals after the scans: chunk count (0 when the decoded bytes exceed the capacity, which
@@ -713,11 +717,13 @@ __global__ __launch_bounds__(256) void k_lz4d_walk(const uint8_t* __restrict__ i
 __global__ void k_lz4d_total(const uint32_t* __restrict__ counts, const uint32_t* __restrict__ cbase,
                              const uint64_t* __restrict__ obytes, int64_t* __restrict__ out_off,
                              uint32_t nb, uint64_t cap, uint64_t chunk_bound,
+                             const unsigned long long* __restrict__ chunk_total,
                              uint32_t* __restrict__ nchunks, uint32_t* __restrict__ ok,
                              uint32_t* __restrict__ err) {
   if (threadIdx.x != 0) return;
   const uint64_t total = nb ? (uint64_t)out_off[nb - 1] + obytes[nb - 1] : 0ull;
-  const uint64_t chunks = nb ? (uint64_t)cbase[nb - 1] + counts[nb - 1] : 0ull;
+  // counted in 64 bits by the walk: the u32 chunk bases are valid only when this fits the table
+  const uint64_t chunks = nb ? (uint64_t)*chunk_total : 0ull;
   out_off[nb] = (int64_t)total;
   const bool fits = total <= cap;
   // the ranges overlap (more headers than the input holds): a caller error, nothing decoded
@@ -907,7 +913,7 @@ Lz4DWorkspace lz4d_workspace_layout(uint64_t in_bytes, uint32_t nb) {
   w.counts_off = o;  o += up256((nb + 1) * 4ull);
   w.cbase_off = o;   o += up256((nb + 1) * 4ull);
   w.obytes_off = o;  o += up256((nb + 1) * 8ull);
-  w.misc_off = o;    o += 256;  // nchunks, ok, the decode queue counter
+  w.misc_off = o;    o += 256;  // nchunks, ok, the decode queue counter; u64 chunk total at +16
   w.chunks_off = o;  o += up256(cb * sizeof(Lz4DChunk));
   w.xc_off = o;      o += up256(cb * sizeof(Lz4Chunk));
   w.temp_off = o;
@@ -927,13 +933,17 @@ hipError_t launch_lz4_decompress(const uint8_t* d_in, uint64_t in_bytes, const i
   uint64_t* obytes = reinterpret_cast<uint64_t*>(d_ws + w.obytes_off);
   uint32_t* nchunks = reinterpret_cast<uint32_t*>(d_ws + w.misc_off);
   uint32_t* ok = nchunks + 1;
+  unsigned long long* ctotal = reinterpret_cast<unsigned long long*>(d_ws + w.misc_off + 16);
   Lz4DChunk* chunks = reinterpret_cast<Lz4DChunk*>(d_ws + w.chunks_off);
   Lz4Chunk* xc = reinterpret_cast<Lz4Chunk*>(d_ws + w.xc_off);
   void* temp = d_ws + w.temp_off;
   const uint32_t g = (nb + 255) / 256;
   if (nb) {
+    hipError_t z = hipMemsetAsync(ctotal, 0, sizeof *ctotal, s);
+    if (z != hipSuccess) return z;
     hipLaunchKernelGGL(k_lz4d_walk<false>, dim3(g), dim3(256), 0, s, d_in, d_in_off, nb, in_bytes,
-                       max_bs, counts, obytes, nullptr, nullptr, nullptr, nullptr, nullptr, d_err);
+                       max_bs, counts, obytes, nullptr, nullptr, nullptr, nullptr, nullptr, ctotal,
+                       d_err);
     size_t tb = w.temp_bytes;
     hipError_t e = rocprim::exclusive_scan(temp, tb, counts, cbase, 0u, (size_t)nb,
                                            rocprim::plus<uint32_t>(), s);
@@ -944,10 +954,10 @@ hipError_t launch_lz4_decompress(const uint8_t* d_in, uint64_t in_bytes, const i
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(k_lz4d_total, dim3(1), dim3(64), 0, s, counts, cbase, obytes, d_out_off, nb,
-                     d_out ? cap : ~0ull, w.chunk_bound, nchunks, ok, d_err);
+                     d_out ? cap : ~0ull, w.chunk_bound, ctotal, nchunks, ok, d_err);
   if (nb == 0 || !d_out) return hipGetLastError();  // no output: the decoded sizes only
   hipLaunchKernelGGL(k_lz4d_walk<true>, dim3(g), dim3(256), 0, s, d_in, d_in_off, nb, in_bytes,
-                     max_bs, counts, obytes, cbase, d_out_off, ok, chunks, xc, d_err);
+                     max_bs, counts, obytes, cbase, d_out_off, ok, chunks, xc, nullptr, d_err);
   const uint32_t in_cap = lz4d_in_cap(max_bs);
   const size_t lds = lz4d_lds_bytes(max_bs, in_cap);
   const uint32_t ncu = (uint32_t)std::max(1, stream_cus(s));

@@ -21,6 +21,8 @@ PART_RANGE_BYTES, PART_MURMUR3_LONG, PART_MURMUR3_INT, PART_MURMUR3_BYTES = 1, 2
 PART_HASH_LONG, PART_HASH_INT = 5, 6
 GEN_TERASORT, GEN_SMALL, GEN_ZIPF = 1, 2, 3
 SORT_BYTES, SORT_LONG, SORT_INT = 1, 2, 3
+SUX_EIO = -8
+SUX_CODEC_NONE, SUX_CODEC_LZ4 = 0, 1
 KERNELS = ("hist", "scan", "scatter", "copy")
 
 
@@ -152,6 +154,8 @@ _SIGS = {
     "sux_buffer_read": (C.c_int, [P, U64, P, U64, P]),
     "sux_write_map_output_host": (C.c_int, [P, I32, I32, P, P, U64, P]),
     "sux_buffer_release": (C.c_int, [P]),
+    "sux_buffer_decompress": (C.c_int, [P, P, U64, P, I32, I32, C.POINTER(P), P, P]),
+    "sux_shuffle_set_codec": (C.c_int, [P, I32, I32, I32]),
     "sux_set_kernel_timing": (C.c_int, [P, C.c_int]),
     "sux_kernel_times": (C.c_int, [P, P, P, I32]),
     "sux_kernel_variant": (C.c_int, [P, I32, C.c_char_p, SZ]),

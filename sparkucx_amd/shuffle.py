@@ -453,6 +453,11 @@ class Node:
                                               record_size, C.byref(d)), "sux_register_shuffle")
         return d
 
+    def set_shuffle_codec(self, shuffle_id: int, codec: int, block_size: int = 32768):
+        """spark.shuffle.compress for the maps this node writes: N.SUX_CODEC_LZ4 or _NONE."""
+        N.check(self.lib.sux_shuffle_set_codec(self.h, shuffle_id, codec, block_size),
+                "sux_shuffle_set_codec")
+
     def unregister_shuffle(self, shuffle_id: int):
         N.check(self.lib.sux_unregister_shuffle(self.h, shuffle_id), "sux_unregister_shuffle")
 
@@ -701,6 +706,21 @@ class FetchedBuffer:
         for _ in range(count):
             N.check(self.node.lib.sux_buffer_release(self.h), "sux_buffer_release")
         self.refs -= count
+
+    def decompress(self, sizes, max_block_size: int = 32768, offset: int = 0, stream=None):
+        """The blocks' LZ4Block streams (sizes[k] bytes each, consecutive from offset) decoded on
+        the device (sux_buffer_decompress).  Returns (FetchedBuffer with one reference, decoded
+        sizes[list])."""
+        sz = np.ascontiguousarray(np.asarray(sizes, dtype=np.int64).reshape(-1))
+        k = sz.size
+        out_sizes = np.zeros(max(1, k), np.int64)
+        h = C.c_void_p()
+        N.check(self.node.lib.sux_buffer_decompress(self.node.h, self.h, offset,
+                                                    sz.ctypes.data if k else None, k,
+                                                    max_block_size, C.byref(h),
+                                                    out_sizes.ctypes.data, _stream(stream)),
+                "sux_buffer_decompress")
+        return FetchedBuffer(self.node, h, 1), out_sizes[:k].tolist()
 
 
 def index_file_commit(index_path: str, data_path: str, data_tmp: str | None,

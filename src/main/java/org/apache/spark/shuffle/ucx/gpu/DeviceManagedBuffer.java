@@ -2,8 +2,11 @@
  * DeviceManagedBuffer — one block of a fetch: a slice [offset, offset + size) of the pooled
  * device buffer sux_fetch_blocks filled.  Every block holds one reference of that buffer; the
  * last release() returns it to the node's pool — the refcounted NioManagedBuffer slices of
- * OnBlocksFetchCallback.java:33-57.  The bytes reach the JVM when Spark's stream reads them
- * (nioByteBuffer / createInputStream copy the slice to host memory once).
+ * OnBlocksFetchCallback.java:33-57.  The bytes reach the JVM when Spark's stream reads them:
+ * nioByteBuffer copies the slice to host memory once; createInputStream streams a block larger
+ * than one chunk through a bounded direct buffer (a reduce block may pass the 2 GiB a ByteBuffer
+ * holds, and the reader's memory stays bounded like the reference's maxBytesInFlight,
+ * UcxShuffleReader.scala:56-70).
  */
 package org.apache.spark.shuffle.ucx.gpu;
 
@@ -62,9 +65,76 @@ public final class DeviceManagedBuffer extends ManagedBuffer {
     return host.duplicate();
   }
 
+  /** Bytes a streamed block is staged in at a time. */
+  static final int CHUNK = 8 << 20;
+
   @Override
   public InputStream createInputStream() throws IOException {
-    return new NioManagedBuffer(nioByteBuffer()).createInputStream();
+    synchronized (this) {
+      if (host != null || size <= CHUNK) {
+        return new NioManagedBuffer(nioByteBuffer()).createInputStream();
+      }
+    }
+    return new DeviceInputStream();
+  }
+
+  /** The block read from the device chunk by chunk into one direct buffer. */
+  private final class DeviceInputStream extends InputStream {
+    private final ByteBuffer stage = ByteBuffer.allocateDirect(CHUNK);
+    private long staged = 0;  // block bytes staged so far
+
+    DeviceInputStream() {
+      stage.limit(0);
+    }
+
+    private boolean fill() {
+      if (stage.hasRemaining()) {
+        return true;
+      }
+      if (staged >= size) {
+        return false;
+      }
+      long len = Math.min(CHUNK, size - staged);
+      stage.clear();
+      SuxNative.bufferRead(buffer, offset + staged, stage, len, stream);  // at the buffer's start
+      stage.limit((int) len);
+      staged += len;
+      return true;
+    }
+
+    @Override
+    public int read() {
+      return fill() ? stage.get() & 0xff : -1;
+    }
+
+    @Override
+    public int read(byte[] b, int off, int len) {
+      if (len == 0) {
+        return 0;
+      }
+      if (!fill()) {
+        return -1;
+      }
+      int n = Math.min(len, stage.remaining());
+      stage.get(b, off, n);
+      return n;
+    }
+
+    @Override
+    public long skip(long n) {
+      long done = 0;
+      while (done < n && fill()) {
+        int k = (int) Math.min(n - done, stage.remaining());
+        stage.position(stage.position() + k);
+        done += k;
+      }
+      return done;
+    }
+
+    @Override
+    public int available() {
+      return stage.remaining();
+    }
   }
 
   @Override

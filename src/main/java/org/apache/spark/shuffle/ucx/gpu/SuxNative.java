@@ -20,7 +20,7 @@ public final class SuxNative {
     }
   }
 
-  public static final int ABI_VERSION = 5;
+  public static final int ABI_VERSION = 6;
 
   // status codes (SUX_*)
   public static final int OK = 0, EINVAL = -1, ENOMEM = -2, EHIP = -3, ECOMM = -4, ENOENT = -5,
@@ -109,6 +109,9 @@ public final class SuxNative {
                                                 String dataPath, long[] lengths, long stream);
   public static native byte[] mapOutputIndex(long node, int shuffleId, int mapIndex,
                                              int numPartitions);
+  /** spark.shuffle.compress for the maps the node writes (SUX_CODEC_*), before the first one. */
+  public static native void setShuffleCodec(long node, int shuffleId, int codec, int blockSize);
+  public static final int CODEC_NONE = 0, CODEC_LZ4 = 1;
 
   // ---- exchange ----
   public static native void exchange(long node, int shuffleId, long stream);
@@ -123,6 +126,10 @@ public final class SuxNative {
   public static native long fetchBlocks(long node, int shuffleId, int[] blocks, long[] sizes,
                                         long stream);
   public static native long bufferDevicePtr(long buf);
+  /** The fetched blocks' LZ4Block streams (sizes[i] bytes each from offset) decoded on the GPU
+   * into a new buffer; outSizes[i] receives block i's decoded size.  EIO: a corrupted stream. */
+  public static native long decompressBuffer(long node, long buf, long offset, long[] sizes,
+                                             int maxBlockSize, long[] outSizes, long stream);
   /** Sort n fixed-size records of a fetched buffer by key on the GPU; returns a new buffer. */
   public static native long sortRecords(long node, int keyKind, long buf, long n, int recordSize,
                                         int keyOffset, int keyLen, long stream);

@@ -493,6 +493,14 @@ JNIEXPORT jbyteArray JNICALL FN(mapOutputIndex)(JNIEnv* env, jclass cls, jlong n
   return out;
 }
 
+/* spark.shuffle.compress for the maps this node writes (GpuShuffleWriter): SUX_CODEC_LZ4 with
+ * spark.io.compression.lz4.blockSize, or SUX_CODEC_NONE; before the shuffle's first map output. */
+JNIEXPORT void JNICALL FN(setShuffleCodec)(JNIEnv* env, jclass cls, jlong node, jint shuffleId,
+                                           jint codec, jint blockSize) {
+  (void)cls;
+  failed(env, sux_shuffle_set_codec(NODE(node), shuffleId, codec, blockSize), "setShuffleCodec");
+}
+
 /* ---- exchange (the all-to-all that replaces the reducers' remote GETs) -------------------- */
 JNIEXPORT void JNICALL FN(exchange)(JNIEnv* env, jclass cls, jlong node, jint shuffleId,
                                     jlong stream) {
@@ -606,6 +614,37 @@ JNIEXPORT jlong JNICALL FN(sortRecords)(JNIEnv* env, jclass cls, jlong node, jin
     sux_buffer_release(out);
     return 0;
   }
+  return (jlong)(intptr_t)out;
+}
+
+/* The reader's GPU sort of a compressed shuffle: the fetched blocks (sizes[i] bytes each,
+ * consecutive from `offset` in the pooled buffer) decoded as LZ4Block streams into a new pooled
+ * buffer (sux_buffer_decompress); outSizes[i] <- block i's decoded bytes.  A corrupted stream is
+ * SuxException(EIO), the IOException Spark's LZ4BlockInputStream throws. */
+JNIEXPORT jlong JNICALL FN(decompressBuffer)(JNIEnv* env, jclass cls, jlong node, jlong buf,
+                                             jlong offset, jlongArray sizes, jint maxBlockSize,
+                                             jlongArray outSizes, jlong stream) {
+  (void)cls;
+  const jsize n = (*env)->GetArrayLength(env, sizes);
+  if (outSizes && (*env)->GetArrayLength(env, outSizes) < n) {
+    throw_sux(env, SUX_EINVAL, "decompressBuffer: outSizes is shorter than sizes");
+    return 0;
+  }
+  int64_t* os = (int64_t*)calloc((size_t)(n ? n : 1), sizeof *os);
+  jlong* sz = (*env)->GetLongArrayElements(env, sizes, NULL);
+  if (!os || !sz) {
+    free(os);
+    if (sz) (*env)->ReleaseLongArrayElements(env, sizes, sz, JNI_ABORT);
+    throw_sux(env, SUX_ENOMEM, "decompressBuffer");
+    return 0;
+  }
+  sux_buffer* out = NULL;
+  int rc = sux_buffer_decompress(NODE(node), BUF(buf), (uint64_t)offset, (const int64_t*)sz, n,
+                                 maxBlockSize, &out, os, STREAM(stream));
+  (*env)->ReleaseLongArrayElements(env, sizes, sz, JNI_ABORT);
+  if (rc == SUX_OK && outSizes) (*env)->SetLongArrayRegion(env, outSizes, 0, n, (const jlong*)os);
+  free(os);
+  if (failed(env, rc, "decompressBuffer")) return 0;
   return (jlong)(intptr_t)out;
 }
 

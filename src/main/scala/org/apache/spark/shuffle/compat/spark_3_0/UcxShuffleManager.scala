@@ -23,8 +23,8 @@ import org.apache.spark.{ShuffleDependency, SparkConf, SparkEnv, TaskContext}
 import org.apache.spark.internal.Logging
 import org.apache.spark.shuffle.api.ShuffleExecutorComponents
 import org.apache.spark.shuffle.compat.spark_3_0.{UcxShuffleBlockResolver, UcxShuffleReader}
-import org.apache.spark.shuffle.gpu.{FixedWidthRowSerializer, GpuExchangeCoordinator, GpuNode,
-  GpuPartitioning, GpuRowLayout, GpuShuffleWriter}
+import org.apache.spark.shuffle.gpu.{FixedWidthRowSerializer, GpuCodec, GpuExchangeCoordinator,
+  GpuNode, GpuPartitioning, GpuRowLayout, GpuShuffleWriter}
 import org.apache.spark.shuffle.sort.SortShuffleManager
 import org.apache.spark.shuffle.ucx.gpu.SuxNative
 import org.apache.spark.util.ShutdownHookManager
@@ -99,10 +99,13 @@ class UcxShuffleManager(val conf: SparkConf, isDriver: Boolean) extends SortShuf
     val h = handle.asInstanceOf[UcxGpuShuffleHandle[K, V, _]]
     shuffleExecutorComponents  // Spark's SPI init; ours starts the node (initializeExecutor)
     val node = startUcxNodeIfMissing()  // and whatever plugin class is configured, so does this
+    node.checkTaskDevice()
     ensureRegistered(h, node)
     val dep = h.baseHandle.dependency
+    // the GPU writes only what Spark's writer would: fixed-width rows, a partitioner it restates,
+    // and a codec it restates byte for byte (GpuCodec: none, or lz4 under spark.shuffle.compress)
     val rows = dep.serializer match {
-      case s: FixedWidthRowSerializer[_, _] if h.layout.isDefined =>
+      case s: FixedWidthRowSerializer[_, _] if h.layout.isDefined && GpuCodec.of(conf).isDefined =>
         Some(s.asInstanceOf[FixedWidthRowSerializer[K, V]].rows)
       case _ => None
     }
@@ -124,8 +127,12 @@ class UcxShuffleManager(val conf: SparkConf, isDriver: Boolean) extends SortShuf
                                metrics: ShuffleReadMetricsReporter): ShuffleReader[K, C] = {
     val h = handle.asInstanceOf[UcxGpuShuffleHandle[K, _, C]]
     val node = startUcxNodeIfMissing()
+    node.checkTaskDevice()
     ensureRegistered(h, node)
-    new UcxShuffleReader[K, C](h, node, startPartition, endPartition, context, metrics)
+    // shouldBatchFetch = true, as the reference's getReader passes (compat/spark_3_0/
+    // UcxShuffleManager.scala:53-60); the reader applies fetchContinuousBlocksInBatch's guard
+    new UcxShuffleReader[K, C](h, node, startPartition, endPartition, context, metrics,
+      shouldBatchFetch = true)
   }
 
   override def unregisterShuffle(shuffleId: Int): Boolean = {

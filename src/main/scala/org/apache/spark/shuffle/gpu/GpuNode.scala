@@ -48,7 +48,11 @@ import org.apache.spark.scheduler.{SparkListener, SparkListenerStageCompleted,
 import org.apache.spark.shuffle.ucx.gpu.{Bootstrap, SuxNative}
 import org.apache.spark.util.{RpcUtils, Utils}
 
-class GpuNode private (conf: SparkConf, isDriver: Boolean) extends Logging {
+/** `undo`: what the constructor acquired so far, released in reverse by GpuNode.startIfMissing if
+ * a later step throws (ADVICE r05: a failed join used to leave its executor endpoint registered —
+ * so every retry failed in setupEndpoint — and leak the node). */
+class GpuNode private (conf: SparkConf, isDriver: Boolean, undo: mutable.ArrayBuffer[() => Unit])
+  extends Logging {
   private def ucx(k: String) = "spark.shuffle.ucx." + k
   private def bytes(k: String, dflt: String): Long = JavaUtils.byteStringAsBytes(conf.get(k, dflt))
 
@@ -67,6 +71,7 @@ class GpuNode private (conf: SparkConf, isDriver: Boolean) extends Logging {
       val env = SparkEnv.get
       val ep = new GpuExecutorEndpoint(env.rpcEnv)
       val me = env.rpcEnv.setupEndpoint(GpuControlEndpoint.EXECUTOR + env.executorId, ep)
+      undo += (() => env.rpcEnv.stop(me))
       val w = GpuControlEndpoint.driverRef(conf, env.rpcEnv)
         .askSync[GpuControlEndpoint.Welcome](
           GpuControlEndpoint.Hello(env.executorId, Utils.localHostName(), worldSize, me))
@@ -74,13 +79,27 @@ class GpuNode private (conf: SparkConf, isDriver: Boolean) extends Logging {
     } else (0, 0, None)
   val rank: Int = rank0
 
-  // the task's "gpu" resource (Spark 3.0 resource scheduling; the node starts inside the first
-  // task that needs it), else the local index on the host; spark.shuffle.ucx.gpu.device pins it
-  // (one executor per host)
+  // spark.shuffle.ucx.gpu.device pins it; else the task's "gpu" resource (Spark 3.0 resource
+  // scheduling) when the node starts inside a task; else the executor's local index on its host.
+  // A node started by the background join has no task: its device is checked against the first
+  // task's gpu resource (checkTaskDevice) — a mismatch fails loudly instead of letting two
+  // executors share a GPU or a task hand the node pointers on another device (ADVICE r05).
   val device: Int =
     if (conf.contains(ucx("gpu.device"))) conf.getInt(ucx("gpu.device"), 0)
-    else Option(TaskContext.get()).flatMap(_.resources().get("gpu"))
-      .flatMap(_.addresses.headOption).map(_.toInt).getOrElse(localIndex)
+    else GpuNode.taskGpu().getOrElse(localIndex)
+  private val deviceFromTask = conf.contains(ucx("gpu.device")) || GpuNode.taskGpu().isDefined
+
+  /** The running task's Spark "gpu" resource must be this node's device (see `device`). */
+  def checkTaskDevice(): Unit = if (!deviceFromTask) {
+    GpuNode.taskGpu().foreach { g =>
+      if (g != device) {
+        throw new IllegalStateException(s"this executor's GPU shuffle node runs on device " +
+          s"$device (its local index, chosen when it joined the group before any task ran) but " +
+          s"Spark assigned GPU $g to this task: set spark.shuffle.ucx.gpu.device, or give each " +
+          "executor exactly one visible GPU")
+      }
+    }
+  }
 
   // UcxShuffleConf.scala:32-40: the directory slot is 2 * rkeySize
   val metadataBlockSize: Long = 2 * bytes(ucx("rkeySize"), "150")
@@ -98,9 +117,11 @@ class GpuNode private (conf: SparkConf, isDriver: Boolean) extends Logging {
     bytes(ucx("memory.minBufferSize"), "1024"), minAllocationSize, metadataBlockSize,
     conf.get(ucx("memory.preAllocateBuffers"), ""), conf.getInt(ucx("gpu.poolLimitMiB"), 0),
     isDriver)
+  undo += (() => SuxNative.nodeDestroy(handle0))
 
   private val bootCtx: Long =
     if (member) SuxNative.setBootstrap(handle0, boot, worldSize) else 0L
+  if (bootCtx != 0L) undo.prepend(() => SuxNative.releaseBootstrap(bootCtx))  // after the node
 
   // HBM-capacity fallback: committed map outputs spill to Spark's files.  The directory is
   // private to this executor and application (a uniquely named subdirectory of the block
@@ -114,6 +135,7 @@ class GpuNode private (conf: SparkConf, isDriver: Boolean) extends Logging {
         .getOrElse(new java.io.File(System.getProperty("java.io.tmpdir")))
       val id = Option(SparkEnv.get).map(_.executorId).getOrElse("executor")
       val d = Utils.createDirectory(root.getAbsolutePath, s"sparkucx-gpu-${conf.getAppId}-$id")
+      undo += (() => Utils.deleteRecursively(d))
       SuxNative.setSpillDir(handle0, d.getAbsolutePath)
       d
     } else null
@@ -144,10 +166,15 @@ class GpuNode private (conf: SparkConf, isDriver: Boolean) extends Logging {
   // an executor learns a shuffle from its first task, or from the coordinator's first message)
   private val registered = ConcurrentHashMap.newKeySet[Int]()
 
+  // spark.shuffle.compress for the maps this node writes (GpuCodec; None: Spark's writer writes
+  // them, and its committed files are adopted as they are)
+  private val codec: Option[(Int, Int)] = GpuCodec.of(conf)
+
   def ensureRegistered(shuffleId: Int, numMaps: Int, numPartitions: Int, recordSize: Int): Unit =
     registered.synchronized {
       if (!registered.contains(shuffleId)) {
         SuxNative.registerShuffle(handle0, shuffleId, numMaps, numPartitions, recordSize)
+        codec.foreach { case (c, bs) => SuxNative.setShuffleCodec(handle0, shuffleId, c, bs) }
         registered.add(shuffleId)
       }
     }
@@ -167,6 +194,7 @@ class GpuNode private (conf: SparkConf, isDriver: Boolean) extends Logging {
       t
     }
   })
+  undo += (() => exchangeThread.shutdownNow())
   private lazy val exchangeStream: Long = SuxNative.streamCreate(handle0)
   // exchange thread only: the group's RCCL communicator, joined before the first exchange
   // (every executor of the group gets the same first window, so every rank reaches it)
@@ -234,16 +262,32 @@ object GpuNode extends Logging {
    * SparkEnv (an executor's endpoint, the block manager's dirs), so it is never called from a
    * ShuffleManager constructor: Spark builds the manager inside SparkEnv.create. */
   def startIfMissing(conf: SparkConf, isDriver: Boolean): GpuNode = synchronized {
-    if (instance == null) instance = new GpuNode(conf, isDriver)
+    if (instance == null) {
+      val undo = mutable.ArrayBuffer[() => Unit]()
+      try instance = new GpuNode(conf, isDriver, undo)
+      catch {
+        case e: Throwable =>
+          // a failed start leaves nothing behind, so the next attempt (the first task, after a
+          // failed background join) starts from scratch
+          undo.reverseIterator.foreach(f => try f() catch { case _: Throwable => })
+          throw e
+      }
+    }
     instance
   }
+
+  /** The running task's Spark-assigned GPU (spark.task.resource.gpu.amount), if any. */
+  def taskGpu(): Option[Int] =
+    Option(TaskContext.get()).flatMap(_.resources().get("gpu"))
+      .flatMap(_.addresses.headOption).map(_.toInt)
 
   /** Driver: the group's control endpoint (idempotent; needs SparkEnv, see ensureSetup). */
   def setupDriver(conf: SparkConf): Unit = GpuControlEndpoint.ensureSetup(conf)
 
   /** An executor of a group joins it as soon as its SparkEnv exists, on a daemon thread, so that
    * it takes part in every exchange even if the scheduler never gives it a task (the exchange is
-   * a collective over the group).  A failed join is logged; the first task retries it. */
+   * a collective over the group).  A failed join is logged and leaves nothing registered
+   * (startIfMissing's undo); the first task retries it. */
   def joinInBackground(conf: SparkConf, isDriver: Boolean): Unit = {
     val t = new Thread(() => {
       try {

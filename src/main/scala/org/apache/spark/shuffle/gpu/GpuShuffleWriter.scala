@@ -16,7 +16,10 @@ package org.apache.spark.shuffle.gpu
 
 import java.nio.{ByteBuffer, ByteOrder}
 
-import org.apache.spark.{HashPartitioner, Partitioner, RangePartitioner, ShuffleDependency, TaskContext}
+import org.apache.spark.{HashPartitioner, Partitioner, RangePartitioner, ShuffleDependency,
+  SparkConf, TaskContext}
+import org.apache.spark.internal.config
+import org.apache.spark.io.CompressionCodec
 import org.apache.spark.scheduler.MapStatus
 import org.apache.spark.shuffle.{ShuffleWriteMetricsReporter, ShuffleWriter}
 import org.apache.spark.shuffle.ucx.gpu.SuxNative
@@ -57,6 +60,33 @@ object GpuPartitioning {
       } else None
     case _ => None
   }
+}
+
+/**
+ * spark.shuffle.compress as the GPU restates it.  Spark's writers wrap every partition segment in
+ * SerializerManager.wrapStream, so under the default config (compress on, lz4) a reader's
+ * wrapStream expects lz4-java LZ4BlockOutputStream streams in every block — the reference's reader
+ * relies on exactly that (compat/spark_3_0/UcxShuffleReader.scala:61).
+ *   Some((CODEC_NONE, 0))        compress off: raw data files;
+ *   Some((CODEC_LZ4, blockSize)) lz4: the node compresses every partition run on the GPU into the
+ *                                bytes lz4-java writes (sux_shuffle_set_codec);
+ *   None                         another codec, or encrypted shuffle streams: no GPU restatement —
+ *                                such a dependency keeps Spark's writer, and the GPU sort in the
+ *                                reader declines it (its blocks cannot be decoded on the GPU).
+ */
+object GpuCodec {
+  def of(conf: SparkConf): Option[(Int, Int)] =
+    if (conf.get(config.IO_ENCRYPTION_ENABLED)) None
+    else if (!conf.get(config.SHUFFLE_COMPRESS)) Some((SuxNative.CODEC_NONE, 0))
+    else if (CompressionCodec.getShortName(conf.get(config.IO_COMPRESSION_CODEC)) == "lz4") {
+      Some((SuxNative.CODEC_LZ4,
+        conf.getSizeAsBytes("spark.io.compression.lz4.blockSize", "32k").toInt))
+    } else None
+
+  /** The lz4-java chunk size a reader must accept (LZ4BlockInputStream decodes any chunk up to
+   * the size its token declares; the GPU decoder is bounded by the writer's block size). */
+  def maxBlockSize(conf: SparkConf): Int =
+    math.max(64, conf.getSizeAsBytes("spark.io.compression.lz4.blockSize", "32k").toInt)
 }
 
 /** A row codec: one record is exactly recordSize bytes, the key's keyLen bytes first. */
@@ -245,6 +275,8 @@ class GpuShuffleWriter[K, V](
         SuxNative.writeMapOutputHostAddr(node.handle, shuffleId, slot, partitioner, base, n,
           node.threadStream())
       }
+      // under spark.shuffle.compress the node committed LZ4Block streams (GpuCodec): the index
+      // file, and so these MapStatus lengths, are the compressed ones, as Spark's writers report
       lengths = new Array[Long](numPartitions)
       if (n > 0) {
         val idx = ByteBuffer.wrap(SuxNative.mapOutputIndex(node.handle, shuffleId, slot, numPartitions))
@@ -259,7 +291,7 @@ class GpuShuffleWriter[K, V](
       Platform.freeMemory(base)  // the write copied the rows to HBM before returning
     }
     metrics.incRecordsWritten(n)
-    metrics.incBytesWritten(n * rs)
+    metrics.incBytesWritten(lengths.sum)  // the committed (compressed) bytes, as Spark counts them
     metrics.incWriteTime(System.nanoTime() - t0)
     status = MapStatus(blockManagerId(), lengths, mapId)
   }

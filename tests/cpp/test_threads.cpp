@@ -129,8 +129,11 @@ int main() {
   o_range_bounds_uniform(R, 10, bounds.data());
   sux_partitioner_desc pdesc{SUX_PART_RANGE_BYTES, R, 0, 10, 42, 1, bounds.data()};
   o_part op{1, R, 0, 10, 42, 1, bounds.data()};
+  // raw data files (the bytes are checked against the oracle's; the compressed contract has its
+  // own test in test_host_mirror.cpp)
   UcxShuffleConf conf(std::map<std::string, std::string>{
-      {"spark.shuffle.ucx.memory.preAllocateBuffers", "4k:64,1m:8"}});
+      {"spark.shuffle.ucx.memory.preAllocateBuffers", "4k:64,1m:8"},
+      {"spark.shuffle.compress", "false"}});
   UcxShuffleManager mgr(conf, /*isDriver=*/false);
   mgr.startUcxNodeIfMissing();
   uint64_t pre = 0;

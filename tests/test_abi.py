@@ -18,7 +18,7 @@ def test_library_loads_and_exports_every_header_symbol():
     missing = [s for s in declared if not hasattr(lib, s)]
     assert not missing, missing
     assert set(declared) == set(N._SIGS), set(declared) ^ set(N._SIGS)
-    assert lib.sux_abi_version() == 5
+    assert lib.sux_abi_version() == 6
     assert C.sizeof(N.Conf) == 432  # sux_conf of ABI v2 (prealloc pairs appended)
     assert C.sizeof(N.Tuning) == 128  # sux_tuning: 31 knobs + 1 reserved
 

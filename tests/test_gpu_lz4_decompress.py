@@ -289,3 +289,25 @@ def test_fuzzed_blocks_never_write_outside_the_output(gpu_node):
     got, oo = decode(gpu_node, good, np.array([0, len(good)], np.int64), 4096)
     gpu_node.check()
     assert got[:len(raw)].cpu().numpy().tobytes() == raw
+
+
+def test_overlapping_block_ranges_cannot_overrun_the_chunk_table(gpu_node):
+    """non-monotone in_offsets let good blocks overlap, so they can hold more chunk
+    headers than the input — the chunk table (sized for the input) would overflow if the count
+    wrapped or went unchecked.  The walk counts chunks in 64 bits: 400 blocks that all re-read the
+    same 64-chunk stream (offsets 0, L, 0, L, ...: every other block is a reversed, corrupted range)
+    exceed the table, the call reports a corrupted input and nothing is decoded or written."""
+    raw = bytes(range(256)) * 64  # 16 KiB -> 64 raw-ish 256-byte chunks
+    s = bytes(_one_stream(raw, 256))
+    L = len(s)
+    offs = np.array([0 if k % 2 == 0 else L for k in range(801)], np.int64)
+    out = torch.zeros(400 * len(raw) + 4096, dtype=torch.uint8, device="cuda")
+    gpu_node.decompress_blocks(to_dev(s), to_dev(offs), 256, out=out[:400 * len(raw)], in_bytes=L)
+    torch.cuda.synchronize()
+    with pytest.raises(N.SuxError) as e:
+        gpu_node.check()
+    assert e.value.code == N.SUX_EHIP and "corrupted" in str(e.value), str(e.value)
+    assert int(out.count_nonzero()) == 0  # nothing decoded anywhere
+    got, _ = decode(gpu_node, s, np.array([0, L], np.int64), 256)  # the decoder is fine afterwards
+    gpu_node.check()
+    assert got[:len(raw)].cpu().numpy().tobytes() == raw

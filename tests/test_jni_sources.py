@@ -151,3 +151,58 @@ def test_shuffle_manager_lifecycle_follows_the_reference():
     assert "case Ready(rank, ref)" in ep and "backlog.foreach(ref.send)" in ep
     hello = ep[ep.index("case Hello("):ep.index("case Ready(")]
     assert "executors(rank) = ref" not in hello
+
+
+def test_reader_restates_the_batch_guard_and_the_compressed_contract():
+    """VERDICT r05 #1, statically: the reader batches only under the reference's
+    fetchContinuousBlocksInBatch (compat/spark_3_0/UcxShuffleReader.scala:165-187: relocatable
+    serializer, concatenable codec, old fetch protocol off), wraps every block in wrapStream
+    (:61), and its GPU sort decodes LZ4Block streams before sorting, declines codecs it cannot
+    decode, and hands rows over in bounded chunks (no whole-partition ByteBuffer)."""
+    text = _read(os.path.join(SCALA, "compat", "spark_3_0", "UcxShuffleReader.scala"))
+    guard = text[text.index("private def fetchContinuousBlocksInBatch"):text.index("private def gpuSorted")]
+    for cond in ("supportsRelocationOfSerializedObjects", "config.SHUFFLE_COMPRESS",
+                 "supportsConcatenationOfSerializedStreams", "config.SHUFFLE_USE_OLD_FETCH_PROTOCOL",
+                 "shouldBatchFetch && serializerRelocatable"):
+        assert cond in guard, cond
+    read = text[text.index("override def read()"):text.index("private def fetchContinuousBlocksInBatch")]
+    assert "val batch = fetchContinuousBlocksInBatch && endPartition - startPartition > 1" in read
+    assert "if (!batch) wanted += id.name" in read  # Spark's own per-partition block ids
+    assert "serializerManager.wrapStream(BlockId(id)" in read
+    sort = text[text.index("private def gpuSorted"):]
+    assert "GpuCodec.of(conf)" in sort and "case None => return None" in sort
+    assert sort.index("SuxNative.decompressBuffer") < sort.index("SuxNative.sortRecords")
+    assert "nioByteBuffer" not in sort and "SuxNative.bufferRead(sorted, read, stage, len" in sort
+    mgr = _read(os.path.join(SCALA, "compat", "spark_3_0", "UcxShuffleManager.scala"))
+    assert "GpuCodec.of(conf).isDefined" in mgr[mgr.index("override def getWriter"):]
+    assert "shouldBatchFetch = true" in mgr
+    node = _read(os.path.join(SCALA, "gpu", "GpuNode.scala"))
+    reg = node[node.index("def ensureRegistered"):node.index("def unregister")]
+    assert reg.index("registerShuffle") < reg.index("setShuffleCodec")
+    writer = _read(os.path.join(SCALA, "gpu", "GpuShuffleWriter.scala"))
+    codec = writer[writer.index("object GpuCodec"):]
+    for k in ("IO_ENCRYPTION_ENABLED", "SHUFFLE_COMPRESS", "IO_COMPRESSION_CODEC",
+              "spark.io.compression.lz4.blockSize"):
+        assert k in codec, k
+
+
+def test_failed_node_start_leaves_nothing_registered():
+    """every resource the GpuNode constructor acquires (executor endpoint, node,
+    bootstrap context, spill directory, exchange thread) registers its release in `undo`, and
+    startIfMissing runs them in reverse when a later step throws — so the first task can retry a
+    failed background join (no "There is already an RpcEndpoint"), and nothing leaks.  A node
+    started before any task checks the first task's Spark GPU against its device."""
+    node = _read(os.path.join(SCALA, "gpu", "GpuNode.scala"))
+    ctor = node[node.index("class GpuNode private"):node.index("object GpuNode")]
+    acquired = ["env.rpcEnv.setupEndpoint", "SuxNative.nodeCreate", "SuxNative.setBootstrap",
+                "Utils.createDirectory", "Executors.newSingleThreadExecutor"]
+    released = ["env.rpcEnv.stop(me)", "SuxNative.nodeDestroy(handle0)",
+                "SuxNative.releaseBootstrap(bootCtx)", "Utils.deleteRecursively(d)",
+                "exchangeThread.shutdownNow()"]
+    for a, r in zip(acquired, released):
+        assert a in ctor and "undo" in ctor[ctor.index(a):ctor.index(r) + len(r)], (a, r)
+    start = node[node.index("def startIfMissing"):node.index("def taskGpu")]
+    assert "undo.reverseIterator.foreach" in start and "throw e" in start
+    assert "def checkTaskDevice()" in ctor
+    mgr = _read(os.path.join(SCALA, "compat", "spark_3_0", "UcxShuffleManager.scala"))
+    assert mgr.count("node.checkTaskDevice()") == 2
