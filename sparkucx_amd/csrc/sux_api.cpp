@@ -20,6 +20,7 @@
 #include <climits>
 #include <initializer_list>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <set>
@@ -848,6 +849,49 @@ namespace {
 // process already holds under another handle is that stale mapping: every reference to it is
 // dropped (its allocation is gone; whoever still held it held freed memory) and the handle is
 // opened again.
+//
+// The open itself is bounded: it runs on a helper thread and a caller that waits
+// longer than SUX_IPC_OPEN_TIMEOUT_S seconds (default 120) gets SUX_ECOMM naming the exporter
+// instead of a hang.  Measured on the box (profiles/r06_ipc/): hipIpcOpenMemHandle of a peer's
+// torch-allocated 2048 or 3072 MiB buffer never returns when the importing process holds a torch
+// buffer of its own of that size (1024, 1536 and 4096 MiB open in < 1 ms; raw hipMalloc buffers
+// of every size from 256 MiB to 8 GiB open in < 1 ms) — it reproduces with no call of this
+// library in either process, so it is the runtime's; a stuck helper thread is abandoned.
+hipError_t ipc_open_bounded(sux_node* node, void** base, const hipIpcMemHandle_t& h,
+                            double* waited_s) {
+  static const double limit_s = [] {
+    const char* v = std::getenv("SUX_IPC_OPEN_TIMEOUT_S");
+    const double t = v ? std::atof(v) : 120.0;
+    return t > 0 ? t : 120.0;
+  }();
+  struct Call {
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false;
+    hipError_t e = hipErrorUnknown;
+    void* base = nullptr;
+  };
+  auto c = std::make_shared<Call>();
+  const int device = node->conf.device;
+  std::thread([c, h, device] {
+    void* b = nullptr;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipIpcOpenMemHandle(&b, h, hipIpcMemLazyEnablePeerAccess);
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->e = e;
+    c->base = b;
+    c->done = true;
+    c->cv.notify_all();
+  }).detach();
+  const auto t0 = std::chrono::steady_clock::now();
+  std::unique_lock<std::mutex> lk(c->mu);
+  const bool done = c->cv.wait_for(lk, std::chrono::duration<double>(limit_s), [&] { return c->done; });
+  *waited_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  if (!done) return hipErrorNotReady;  // the helper keeps running; its mapping, if any, leaks
+  *base = c->base;
+  return c->e;
+}
+
 void* ipc_open_fresh(sux_node* node, const uint8_t* handle) {
   std::lock_guard<std::mutex> lk(node->ipc_mu);
   hipIpcMemHandle_t h;
@@ -855,7 +899,21 @@ void* ipc_open_fresh(sux_node* node, const uint8_t* handle) {
   const std::string key(reinterpret_cast<const char*>(handle), 64);
   for (int attempt = 0; attempt < 2; ++attempt) {
     void* base = nullptr;
-    const hipError_t e = hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess);
+    double waited = 0;
+    const hipError_t e = ipc_open_bounded(node, &base, h, &waited);
+    if (e == hipErrorNotReady) {
+      uint64_t va = 0;
+      uint32_t pid = 0;
+      std::memcpy(&va, handle, 8);
+      std::memcpy(&pid, handle + 8, 4);
+      char msg[320];
+      std::snprintf(msg, sizeof msg,
+                    "hipIpcOpenMemHandle of the allocation at 0x%llx exported by pid %u did not "
+                    "return in %.0f s (the import is abandoned; SUX_IPC_OPEN_TIMEOUT_S sets the "
+                    "bound)",
+                    (unsigned long long)va, pid, waited);
+      raise(SUX_ECOMM, msg);
+    }
     if (e != hipSuccess) {
       // reported at once, with what a diagnosis needs (the round-3 failure): the
       // exporter's address and pid as ROCm 7.2 lays them in the handle, and this process's open
@@ -2238,16 +2296,23 @@ int sux_node_set_ownership(sux_node* node, int32_t W, int32_t R, const int32_t* 
     if (own) check_ownership(W, R, own);
     node->bind();
     std::lock_guard<std::mutex> lk(node->mu);
+    // a posted exchange keeps the table it was posted with (its ticket's snapshot), but a table
+    // changed between post and issue would no longer match the send buffer's layout: refuse it
+    // 
+    require(node->tickets.empty(), SUX_ESTATE,
+            "exchange groups are posted and not yet issued: set the ownership between shuffles");
     if (!own) {
       node->own.clear();
       return;
     }
+    // the node's streams are non-blocking (a null-stream copy does not order against them): every
+    // partition or pull launch still reading the old table completes first
+    hip_check(hipDeviceSynchronize(), "sync before the ownership update");
     if (!node->d_own || node->own_W < W) {
       if (node->d_own) (void)hipFree(node->d_own);
       node->d_own = nullptr;
       hip_check(hipMalloc(&node->d_own, sizeof(int32_t) * (W + 1)), "hipMalloc(ownership)");
     }
-    // ordered on the null stream: the next group call on any stream sees the new table
     hip_check(hipMemcpy(node->d_own, own, sizeof(int32_t) * (W + 1), hipMemcpyHostToDevice),
               "ownership upload");
     node->own.assign(own, own + W + 1);
@@ -2360,6 +2425,7 @@ int sux_exchange_group(sux_node* node, const void* d_send, const int64_t* d_inde
 }  // extern "C"
 struct sux_xticket {
   int32_t M = 0, R = 0;
+  std::vector<int32_t> own;  // the ownership table at post time (empty: the equal split)
   int64_t* d_gathered = nullptr;
   std::unique_ptr<HostLease> host;  // the gathered index tables, read back asynchronously
   Event done;                       // after the read-back
@@ -2386,6 +2452,10 @@ int sux_exchange_group_post(sux_node* node, const int64_t* d_index, int32_t M, i
     t->M = M;
     t->R = R;
     t->d_gathered = d_gathered;
+    {
+      std::lock_guard<std::mutex> lk(node->mu);
+      if (const int32_t* o = node->own_host(W, R)) t->own.assign(o, o + W + 1);
+    }
     t->host = std::make_unique<HostLease>(node->hpool, per_rank * W * 8);
     if (!node->comm)
       hip_check(hipMemcpyAsync(d_gathered, d_index, per_rank * 8, hipMemcpyDeviceToDevice, s),
@@ -2437,8 +2507,8 @@ int sux_exchange_group_issue(sux_node* node, sux_xticket* ticket, const void* d_
     std::vector<uint64_t> sc(W), sd(W), rc(W), rd(W);
     int rc_plan = sux_plan_group_owned(W, rank, t->M, t->R,
                                        static_cast<const int64_t*>(t->host->b.first),
-                                       node->own_host(W, t->R), sc.data(), sd.data(), rc.data(),
-                                       rd.data());
+                                       t->own.empty() ? nullptr : t->own.data(), sc.data(),
+                                       sd.data(), rc.data(), rd.data());
     require(rc_plan == SUX_OK, rc_plan, g_err);
     const uint64_t total = rd[W - 1] + rc[W - 1];
     require(total <= recv_capacity, SUX_ERANGE,

@@ -67,13 +67,15 @@ def _read_byte(hip, ptr):
 def test_reopened_address_maps_the_new_allocation():
     sys.path.insert(0, ROOT)
     from sparkucx_amd.shuffle import Node
+    # this process's runtime first (torch, then the library), then the exporter child: a parent
+    # whose first HIP initialisation raced its freshly spawned child's once found no GPU
+    hip = _hip()
+    node = Node(device=0)
     ctx = mp.get_context("spawn")
     a, b = ctx.Pipe()
     proc = ctx.Process(target=_exporter, args=(b,))
     proc.start()
     try:
-        hip = _hip()
-        node = Node(device=0)
         va1, h1 = a.recv()
         p1 = node.ipc_open(h1)
         assert _read_byte(hip, p1) == 0x11
@@ -88,6 +90,9 @@ def test_reopened_address_maps_the_new_allocation():
         node.close()
     finally:
         proc.join(60)
+        if proc.is_alive():  # never leave the exporter waiting on the pipe
+            proc.kill()
+            proc.join()
         assert proc.exitcode == 0
 
 

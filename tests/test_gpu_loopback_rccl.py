@@ -160,3 +160,31 @@ def test_three_ranks_uneven_partitions_verified(tmp_path):
     assert res["n_gpus"] == 3 and res["verified_groups"] == 3
     assert res["self_check"]["ok"]
     assert {(r, p) for _, r, p, _ in msgs} >= {(r, p) for r in range(3) for p in range(3) if r != p}
+
+
+def test_eight_ranks_default_line_explains_itself(tmp_path):
+    """the N = 8 line (bench.py's defaults; sizes cut to fit one GPU, the RCCL
+    calls through the loopback stand-in) carries everything the first 8-GPU driver run needs to
+    explain itself: the measured peer peak and frac against it and against 7 x 153 GB/s, the
+    busiest owner's ingress over the mean, exchange_hidden, and the device self-check — and every
+    probe phase's duration."""
+    res, _ = _run(8, tmp_path, "--records", "200000", "--map-records", "20000", "--group-maps",
+                  "2", "--steps", "2", "--warmup", "1", "--plugin-groups", "0")
+    ex = res["roofline_exchange"]
+    for k in ("measured_peak", "frac", "frac_of_measured", "ingress_max_over_mean",
+              "exchange_hidden", "device_self_check", "peak", "achieved"):
+        assert ex.get(k) is not None, (k, ex)
+    assert ex["peak"] == 7 * 153.0 and 0.0 <= ex["exchange_hidden"] <= 1.0
+    assert ex["device_self_check"] == "ok" and res["self_check"]["ok"]
+    assert {"buffers", "barrier", "first_exchange"} <= set(ex["probe"]["phases_ms"])
+
+
+def test_eight_ranks_forced_mismatch_names_source_map_partition(tmp_path):
+    """A received record corrupted on every rank: the device self-check fails the run (non-zero
+    exit) and names the first mismatching (source, map, partition)."""
+    with pytest.raises(AssertionError) as e:
+        _run(8, tmp_path, "--records", "100000", "--map-records", "20000", "--group-maps", "2",
+             "--steps", "1", "--warmup", "0", "--plugin-groups", "0", "--xgmi-probe-mib", "0",
+             "--force-mismatch")
+    msg = str(e.value)
+    assert "first mismatch at source" in msg and "partition" in msg, msg[-3000:]

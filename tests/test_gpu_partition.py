@@ -247,6 +247,32 @@ def test_exchange_group_single_rank(gpu_node):
     assert e.value.code == N.SUX_ERANGE
 
 
+def test_ownership_is_fixed_while_an_exchange_is_posted(gpu_node):
+    """a posted exchange plans with the ownership table it was posted with (the
+    ticket's snapshot), and the table cannot change between post and issue — the send buffer was
+    laid out for it.  set_ownership refuses while a ticket is outstanding; after the issue (or a
+    discard) it works again."""
+    R, rpm, n = 64, 5000, 12000
+    recs = O.gen_terasort(12, 0, n)
+    opart = O.terasort_partitioner(R)
+    gp = gpu_part(gpu_node, opart)
+    send, index, _ = gpu_node.partition_maps_peer_major(gp, to_dev(recs), 100, rpm, 1)
+    maps = -(-n // rpm)
+    gathered = torch.empty(maps * (R + 1), dtype=torch.int64, device="cuda")
+    recv = torch.empty(recs.size, dtype=torch.uint8, device="cuda")
+    t = gpu_node.exchange_group_post(index, maps, R, gathered)
+    with pytest.raises(N.SuxError) as e:
+        gpu_node.set_ownership(1, R, [0, R])
+    assert e.value.code == N.SUX_ESTATE
+    rb = gpu_node.exchange_group_issue(t, send, recv)
+    torch.cuda.synchronize()
+    assert rb.tolist() == [recs.size] and host(recv).tobytes() == host(send).tobytes()
+    t = gpu_node.exchange_group_post(index, maps, R, gathered)
+    gpu_node.exchange_group_discard(t)
+    gpu_node.set_ownership(1, R, [0, R])
+    gpu_node.set_ownership(1, R, None)
+
+
 def test_exchange_group_rccl_one_rank():
     """The RCCL calls of sux_exchange_group (ncclAllGather of the index tables, ncclAllToAllv of
     the peer-major ranges) on a one-rank communicator: the argument plumbing the 8-GPU run uses."""
