@@ -243,7 +243,9 @@ typedef struct sux_tuning {
                                bit 2: pass A prefetches its next chunk into LDS by DMA
                                (global_load_lds), one workgroup per CU; bit 3: 32-partition
                                buckets, 512-thread pass-B workgroups; bit 4: pass B finds each
-                               element's run in an LDS map instead of a binary search; 0: bits
+                               element's run in an LDS map instead of a binary search; bit 5
+                               (with 3 + 4): pass B gathers the next segment while the current
+                               one is written out (maps of <= 256 chunks); 0: bits
                                3 + 4 (the measured default), -1: none (round 4's shape)       */
   int32_t reserved[1];
 } sux_tuning;

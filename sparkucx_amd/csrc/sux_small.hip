@@ -712,7 +712,7 @@ __global__ __launch_bounds__(kScanThreads) void k_msd16_scan(MapGroup g, uint32_
 }
 
 template <int KW, uint32_t NW, uint32_t PT, uint32_t LO, uint32_t MCH, bool DIRECT = false,
-          bool ERUN = false>
+          bool ERUN = false, bool PIPE = false>
 __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, uint32_t cpm,
                                                  uint32_t nbk, const uint16_t* __restrict__ offs,
                                                  const uint64_t* __restrict__ segbase,
@@ -735,6 +735,11 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
   // stage's first 2 CAP bytes (idle between place() and the next rank_stage): one LDS read per
   // element instead of the run table's log2(MC)-step search
   uint16_t* erun = reinterpret_cast<uint16_t*>(lds8);
+  // PIPE (msd_direct bit 5, round 6): the next segment's records are gathered into registers
+  // while this one's sorted stage is written out, so the element map cannot share the stage: it
+  // gets its own u8 region after the kernel's LDS (maps of <= 256 chunks)
+  uint8_t* erun8 = lds8 + K::lds_bytes();
+  static_assert(!PIPE || (ERUN && !DIRECT), "PIPE runs on the element map, stage path");
   const int R = pd.R;
   const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
   const uint64_t lt_mask = (1ull << lane) - 1ull;
@@ -817,7 +822,10 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
     if constexpr (ERUN) {
       if (s.T <= CAP) {
         for (uint32_t c = tid; c < s.nch; c += NT)
-          for (uint32_t k = rp[c], e = rp[c + 1]; k < e; ++k) erun[k] = (uint16_t)c;
+          for (uint32_t k = rp[c], e = rp[c + 1]; k < e; ++k) {
+            if constexpr (PIPE) erun8[k] = (uint8_t)c;
+            else erun[k] = (uint16_t)c;
+          }
         __syncthreads();
       }
     }
@@ -841,7 +849,7 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
     if constexpr (ERUN) {
       if (s.T <= CAP) {
 #pragma unroll
-        for (uint32_t j = 0; j < PT; ++j) lo[j] = erun[ev[j]];
+        for (uint32_t j = 0; j < PT; ++j) lo[j] = PIPE ? (uint32_t)erun8[ev[j]] : (uint32_t)erun[ev[j]];
 #pragma unroll
         for (uint32_t j = 0; j < PT; ++j)
           r[j] = t4[s.mbase + (uint64_t)lo[j] * kM16Chunk + ro[lo[j]] + (ev[j] - rp[lo[j]])];
@@ -921,10 +929,12 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
     }
     uint32_t ncur = 0;
     if (tid < (int)NB) ncur = cur[tid] + ((uint32_t)tid + 1 < NB ? wc[tid + 1] : n) - wc[tid];
-    __syncthreads();
+    // PIPE: the next segment's gather is in flight here — a __syncthreads() fence would wait for
+    // it (vmcnt(0)); these barriers only order LDS accesses, so a raw one keeps it flying
+    if constexpr (PIPE) lds_barrier(); else __syncthreads();
     if (tid < (int)NB) cur[tid] = ncur;
     for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
-    __syncthreads();
+    if constexpr (PIPE) lds_barrier(); else __syncthreads();
   };
 
   for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
@@ -932,6 +942,68 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16b(PartDev pd, MapGroup g, u
   if (it0 >= it1) return;
   Seg s = build(it0, prefetch(it0));
   u32x4 rv[PT];
+  // a segment larger than the stage (skewed keys): count the digits, then place piece by piece
+  auto multi_segment = [&](const Seg& s) {
+    const uint32_t seg_rel = (uint32_t)(s.out - s.mbase);
+    for (uint32_t e0 = 0; e0 < s.T; e0 += CAP) {
+      load(s, e0, rv);
+      const uint32_t n = min(CAP, s.T - e0);
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) {
+        const uint32_t e = wave * (PT * kWave) + j * kWave + lane;
+        if (e < n) atomicAdd(&wc[wave * NB + digit(s, rv[j])], 1u);
+      }
+    }
+    __syncthreads();
+    scan_digit_wave<NB, NW>(wc, wsum, tid, lane, wave);
+    if (tid < (int)NB) cur[tid] = seg_rel + wc[tid];
+    write_index(s, tid < (int)NB ? wc[tid] : 0u);
+    __syncthreads();
+    for (uint32_t i = tid; i < NW * NB; i += NT) wc[i] = 0;
+    __syncthreads();
+    for (uint32_t e0 = 0; e0 < s.T; e0 += CAP) {
+      load(s, e0, rv);
+      const uint32_t n = min(CAP, s.T - e0);
+      rank_stage(s, n, rv);
+      __syncthreads();
+      __syncthreads();
+      place(s, n, rv);
+    }
+  };
+  if constexpr (PIPE) {
+    // segment s's records are in rv when its iteration starts; after s is ranked into the
+    // stage, the next segment's run table is built and its records are gathered into rv while
+    // s's stage goes out (place) — the gather's latency hides behind the stores instead of
+    // stalling every segment (round 2 stamps: ~half a segment waited on its loads)
+    if (s.T <= CAP) load(s, 0, rv);
+    for (uint32_t it = it0; it < it1; it += G) {
+      const bool have = it + G < it1;
+      const Pre pre = prefetch(it + G);  // the next run table's reads fly during this segment
+      if (s.T > CAP) {
+        multi_segment(s);
+        if (have) {
+          s = build(it + G, pre);
+          if (s.T <= CAP) load(s, 0, rv);
+        }
+        continue;
+      }
+      const uint32_t seg_rel = (uint32_t)(s.out - s.mbase);
+      const uint32_t n = s.T;
+      rank_stage(s, n, rv);
+      __syncthreads();
+      if (tid < (int)NB) cur[tid] = seg_rel + wc[tid];
+      write_index(s, tid < (int)NB ? wc[tid] : 0u);
+      __syncthreads();
+      Seg nx = s;
+      if (have) {
+        nx = build(it + G, pre);  // rp / ro / erun8: place() reads none of them
+        if (nx.T <= CAP) load(nx, 0, rv);
+      }
+      place(s, n, rv);  // the stage path: reads stage / los / cur / wc, not rv
+      s = nx;
+    }
+    return;
+  }
   SUX_MSD_STAMP_INIT();
   for (uint32_t it = it0; it < it1; it += G) {
     const uint32_t seg_rel = (uint32_t)(s.out - s.mbase);  // in-map record offset of the segment
@@ -1096,17 +1168,25 @@ hipError_t launch_msd16(const PartDev& pd, const MapGroup& g, uint8_t* d_out, in
   static_assert(4 * MB4::lds_bytes() <= 160 * 1024, "pass B: four workgroups per CU");
   static_assert(4 * MB8::lds_bytes() <= 160 * 1024, "pass B (256-partition buckets): four per CU");
   static_assert(2 * M16a<NWA, 10>::lds_bytes() <= 160 * 1024, "pass A: two workgroups per CU");
-#define SUX_M16B_D(KW, LOV, MCV, D, ER)                                                            \
+#define SUX_M16B_P(KW, LOV, MCV, D, ER, P)                                                         \
   do {                                                                                             \
     constexpr uint32_t nwb = LOV == kM16LoWide ? 8 : NWB;                                          \
-    constexpr size_t ldsb = M16b<nwb, PTB, LOV, MCV>::lds_bytes();                                 \
-    allow_lds(reinterpret_cast<const void*>(&k_msd16b<KW, nwb, PTB, LOV, MCV, D, ER>), ldsb);     \
-    hipLaunchKernelGGL((k_msd16b<KW, nwb, PTB, LOV, MCV, D, ER>), gb, dim3(nwb * kWave), ldsb, s, \
-                       pd, g, cpm, nbk, offs, segbase, tmp, d_out, d_index, d_index_be);           \
+    using MBK = M16b<nwb, PTB, LOV, MCV>;                                                          \
+    constexpr size_t ldsb = MBK::lds_bytes() + (P ? MBK::CAP : 0);                                 \
+    static_assert(!P || 2 * ldsb <= 160 * 1024, "pipelined pass B: two workgroups per CU");      \
+    allow_lds(reinterpret_cast<const void*>(&k_msd16b<KW, nwb, PTB, LOV, MCV, D, ER, P>), ldsb);  \
+    hipLaunchKernelGGL((k_msd16b<KW, nwb, PTB, LOV, MCV, D, ER, P>), gb, dim3(nwb * kWave), ldsb, \
+                       s, pd, g, cpm, nbk, offs, segbase, tmp, d_out, d_index, d_index_be);        \
   } while (0)
+#define SUX_M16B_D(KW, LOV, MCV, D, ER) SUX_M16B_P(KW, LOV, MCV, D, ER, false)
+  // msd_direct bit 5: pass B gathers the next segment while the current one is written out
+  // (32-partition buckets, element map, maps of <= 256 chunks)
+  const bool pipe_b = (tn.msd_direct & 32) && (tn.msd_direct & 16) && !(tn.msd_direct & 2) &&
+                      LO == kM16LoWide && cpm <= 256;
 #define SUX_M16B(KW, LOV, MCV)                                      \
   do {                                                              \
     if (tn.msd_direct & 2) SUX_M16B_D(KW, LOV, MCV, true, false);   \
+    else if (pipe_b && LOV == kM16LoWide) SUX_M16B_P(KW, kM16LoWide, kM16MaxChunks, false, true, true); \
     else if (tn.msd_direct & 16) SUX_M16B_D(KW, LOV, MCV, false, true); \
     else SUX_M16B_D(KW, LOV, MCV, false, false);                    \
   } while (0)
@@ -1123,6 +1203,7 @@ hipError_t launch_msd16(const PartDev& pd, const MapGroup& g, uint8_t* d_out, in
 #undef SUX_M16BK
 #undef SUX_M16B
 #undef SUX_M16B_D
+#undef SUX_M16B_P
   timer_end(timer, kScatter, s);
   return hipGetLastError();
 }
