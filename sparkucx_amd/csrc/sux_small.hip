@@ -540,6 +540,11 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16a(PartDev pd, MapGroup g, u
         if (pids_out) pids_out[k.c0 + e] = (uint16_t)p;
       }
       h[j] = (p >> LO) & (NB - 1);
+#if defined(SUX_MSD_WHATIF) && SUX_MSD_WHATIF >= 2
+      // diagnostic (level 2): the ranking's counter read / update at a conflict-free digit (the
+      // lane's own), the pid kept alive through the digit's top bit
+      h[j] = ((uint32_t)lane | (p >> 31)) & (NB - 1);
+#endif
       rank[j] = wave_rank<DB, uint16_t>(h[j], valid, wc + wave * NB, lt_mask);
     }
     __syncthreads();
@@ -551,9 +556,18 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16a(PartDev pd, MapGroup g, u
       for (uint32_t j = 0; j < PT; ++j)
         if (rank[j] != ~0u) t4[k.c0 + wc[wave * NB + h[j]] + rank[j]] = rv[j];
     } else {
+#ifdef SUX_MSD_WHATIF
+      // diagnostic build only (tools/msd_whatif.sh; the output is NOT bucket-sorted): the stage
+      // store at the record's own, conflict-free slot, without the bucket-start read — what pass A
+      // would cost if its two random LDS accesses per record had no bank conflicts
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j)
+        if (rank[j] != ~0u) stage[wave * (PT * kWave) + j * kWave + lane] = rv[j];
+#else
 #pragma unroll
       for (uint32_t j = 0; j < PT; ++j)
         if (rank[j] != ~0u) stage[wc[wave * NB + h[j]] + rank[j]] = rv[j];
+#endif
       __syncthreads();
       // the chunk goes back to its own place, in bucket order: one contiguous write
 #pragma unroll

@@ -14,6 +14,7 @@
 #   sortpmc                 PMC passes of tools/sort_prof.py (5 M TeraSort records)
 #   sorttrace [N] [INPUT]   rocprofv3 kernel trace of tools/sort_prof.py (INPUT: partition (default),
 #                           random, long)
+#   msdprobe                kernel trace + FETCH/WRITE_SIZE passes of tools/sort_msd_probe.py
 #   sortprof                the sort tests, then tools/sort_prof.py on random and range-partition keys, 2 x
 #   sortab LIB_A LIB_B      tools/sort_prof.py on both inputs, A and B alternating, 2 x each
 #   ab LIB_B [bench args]   bench.py alternating with a copy of the tree linking LIB_B, 2 x each
@@ -67,6 +68,19 @@ case $job in
   sorttrace)
     SORT_PROF_INPUT=${2:-partition} timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv \
       -d $O/prof_sort -o run -- python3 tools/sort_prof.py ${1:-20} > $O/prof_sort.txt 2>&1 ;;
+  msdprobe)
+    # tools/sort_msd_probe.py (record-moving MSD first pass vs today's sort): kernel trace, then
+    # one PMC pass each for FETCH_SIZE and WRITE_SIZE
+    cd /tmp || exit 1
+    R=$GRAFT_REPO_ROOT; [ -n "$R" ] || R=/root/repo
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/trace -o run -- \
+      python3 $R/tools/sort_msd_probe.py > $R/$O/probe_trace.jsonl 2> $R/$O/probe_trace.err || exit 1
+    i=0
+    for cs in "FETCH_SIZE" "WRITE_SIZE"; do
+      timeout -s KILL 240 rocprofv3 --pmc $cs --output-format csv -d $R/$O/pass$i -o run -- \
+        python3 $R/tools/sort_msd_probe.py > $R/$O/pass$i.log 2>&1 || exit 1
+      i=$((i+1))
+    done; echo msdprobe done ;;
   sortprof)
     run_tests tests/test_gpu_sort.py || exit 1
     for i in 1 2; do
