@@ -245,8 +245,10 @@ typedef struct sux_tuning {
                                buckets, 512-thread pass-B workgroups; bit 4: pass B finds each
                                element's run in an LDS map instead of a binary search; bit 5
                                (with 3 + 4): pass B gathers the next segment while the current
-                               one is written out (maps of <= 256 chunks); 0: bits
-                               3 + 4 (the measured default), -1: none (round 4's shape)       */
+                               one is written out (maps of <= 256 chunks); bit 6 (with 3):
+                               pass A ranks with one returning LDS atomic per digit group on
+                               u32 counters; 0: bits 3 + 4 (the measured default), -1: none
+                               (round 4's shape)                                              */
   int32_t reserved[1];
 } sux_tuning;
 int sux_node_set_tuning(sux_node* node, const sux_tuning* tuning);

@@ -1390,7 +1390,7 @@ int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
     require(in(t->gather_kernel, {1, 2, 3}), SUX_EINVAL, "gather_kernel must be 1, 2 or 3");
     require(t->split_cus == -1 || (t->split_cus >= 0 && t->split_cus <= 224 && t->split_cus % 32 == 0),
             SUX_EINVAL, "split_cus must be -1, 0 or a multiple of 32 up to 224");
-    require(t->msd_direct >= -1 && t->msd_direct <= 63, SUX_EINVAL, "msd_direct must be -1 .. 63");
+    require(t->msd_direct >= -1 && t->msd_direct <= 127, SUX_EINVAL, "msd_direct must be -1 .. 127");
     for (int32_t r : t->reserved) require(r == 0, SUX_EINVAL, "reserved tuning fields must be 0");
     require(node, SUX_EINVAL, "NULL node");
     std::lock_guard<std::mutex> lk(node->mu);

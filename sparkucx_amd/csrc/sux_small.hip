@@ -3,6 +3,8 @@
 // units with a word-aligned key of <= 16 bytes; the 100-byte TeraSort path lives there.  Output
 // contract identical to the large-record kernels: stable per-partition regroup (P2), index tables
 // native + big-endian (P3).
+#include <type_traits>
+
 #include "sux_part.h"
 
 namespace sux {
@@ -422,8 +424,8 @@ __device__ __forceinline__ void lds_barrier() {
 // (NW*64 threads; each thread owns E = NB/64 consecutive (digit, wave) entries).  Counts and
 // prefixes fit u16: a chunk holds kM16Chunk records.  Two barriers (RAW: lds_barrier); wsum[NW]
 // scratch.
-template <uint32_t NB, uint32_t NW, bool RAW = false>
-__device__ __forceinline__ void scan_digit_wave16(uint16_t* wc, uint32_t* wsum, int tid, int lane,
+template <uint32_t NB, uint32_t NW, bool RAW = false, typename CT = uint16_t>
+__device__ __forceinline__ void scan_digit_wave16(CT* wc, uint32_t* wsum, int tid, int lane,
                                                   int wave) {
   constexpr uint32_t E = NB / kWave;
   uint32_t sum = 0;  // the entries are read twice instead of held (registers are the limit)
@@ -442,16 +444,17 @@ __device__ __forceinline__ void scan_digit_wave16(uint16_t* wc, uint32_t* wsum, 
   for (uint32_t k = 0; k < E; ++k) {
     const uint32_t idx = (uint32_t)tid * E + k, d = idx / NW, w = idx % NW;
     const uint32_t v = wc[w * NB + d];
-    wc[w * NB + d] = (uint16_t)run;
+    wc[w * NB + d] = (CT)run;
     run += v;
   }
   if constexpr (RAW) lds_barrier(); else __syncthreads();
 }
 
-template <uint32_t NW, uint32_t DB>  // stage[CH] u32x4 (its first NW words double as wsum) | wc[NW][2^DB] u16
+// stage[CH] u32x4 (its first NW words double as wsum) | wc[NW][2^DB] u16 (u32: atomic ranking)
+template <uint32_t NW, uint32_t DB, uint32_t CB = 2>
 struct M16a {
   static constexpr uint32_t NB = 1u << DB, NT = NW * kWave, PT = kM16Chunk / NT;
-  static constexpr uint32_t lds_bytes() { return kM16Chunk * 16 + NW * NB * 2; }
+  static constexpr uint32_t lds_bytes() { return kM16Chunk * 16 + NW * NB * CB; }
 };
 // stage[CAP] u32x4 | wc[NW][NB] | cur[NB] | wsum[NW] | los[CAP] u8 | rp[MC+1] u32 | ro[MC] u16
 template <uint32_t NW, uint32_t PT, uint32_t LO = kM16Lo, uint32_t MC = kM16MaxChunks>
@@ -484,17 +487,23 @@ __device__ __forceinline__ uint32_t m16_pid(const PartDev& pd, const u32x4& r, i
   return (uint32_t)partition_words<KW, false>(pd, w, pd.bounds, pd.lut);
 }
 
-template <int KW, uint32_t NW, uint32_t DB, uint32_t LO, bool DIRECT = false>
+// ATOM (msd_direct bit 6): the ranking's counters are u32 and each digit group's leader updates
+// its counter with one returning atomic, all PT rounds issued before any result is used — the
+// u16 read-by-every-lane + leader-write round trip of wave_rank, once per round, is pass A's
+// costliest bank-conflicted LDS traffic (tools/msd_whatif.hip: with conflict-free counters pass A
+// would be 14 % faster).
+template <int KW, uint32_t NW, uint32_t DB, uint32_t LO, bool DIRECT = false, bool ATOM = false>
 __global__ __launch_bounds__(NW * 64, 4) void k_msd16a(PartDev pd, MapGroup g, uint32_t cpm,
                                                  uint32_t nbk, uint16_t* __restrict__ offs,
                                                  uint16_t* __restrict__ pids_out,
                                                  uint8_t* __restrict__ tmp) {
   resolve_seed(pd);
-  using K = M16a<NW, DB>;
+  using CT = typename std::conditional<ATOM, uint32_t, uint16_t>::type;
+  using K = M16a<NW, DB, sizeof(CT)>;
   constexpr uint32_t NB = K::NB, NT = K::NT, PT = K::PT, CH = kM16Chunk;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
   u32x4* stage = reinterpret_cast<u32x4*>(lds8);
-  uint16_t* wc = reinterpret_cast<uint16_t*>(stage + CH);  // [NW][NB]
+  CT* wc = reinterpret_cast<CT*>(stage + CH);  // [NW][NB]
   uint32_t* wsum = reinterpret_cast<uint32_t*>(lds8);       // only inside the scan: stage is idle
   const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
   const uint64_t lt_mask = (1ull << lane) - 1ull;
@@ -540,15 +549,55 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16a(PartDev pd, MapGroup g, u
         if (pids_out) pids_out[k.c0 + e] = (uint16_t)p;
       }
       h[j] = (p >> LO) & (NB - 1);
-#if defined(SUX_MSD_WHATIF) && SUX_MSD_WHATIF >= 2
+#if defined(SUX_MSD_WHATIF) && SUX_MSD_WHATIF == 2
       // diagnostic (level 2): the ranking's counter read / update at a conflict-free digit (the
-      // lane's own), the pid kept alive through the digit's top bit
+      // lane's own), the pid kept alive through the digit's top bit (the compiler proves that
+      // bit and bits 6..8 of the digit zero, so three of the nine match ballots fold away too)
       h[j] = ((uint32_t)lane | (p >> 31)) & (NB - 1);
+#elif defined(SUX_MSD_WHATIF) && SUX_MSD_WHATIF == 3
+      // diagnostic (level 3): the digit's low 6 bits replaced by the lane — no two lanes of a
+      // wave share a digit and the counter accesses are at most 2-way conflicted — with every
+      // bit still data-dependent, so all nine match ballots stay
+      // (the lane XORed with a run-time zero the compiler cannot see through)
+      h[j] = (((uint32_t)lane ^ (uint32_t)(g.num_records >> 56)) & 63u) | (h[j] & ~63u);
 #endif
-      rank[j] = wave_rank<DB, uint16_t>(h[j], valid, wc + wave * NB, lt_mask);
+      if constexpr (ATOM) {
+        // the group's leader (its lowest lane) adds the group's size with a returning atomic;
+        // nothing waits for it here: the PT atomics of a wave queue back to back (one wave's LDS
+        // operations complete in order, so each returns the count before its own round) and
+        // the lanes fetch their leader's old count after the loop.  Meanwhile the record's
+        // digit, rank inside its group and leader lane are packed into h[j].
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (uint32_t bb = 0; bb < DB; ++bb) {
+          const bool bit = (h[j] >> bb) & 1u;
+          const uint64_t m = __ballot(bit);
+          peers &= bit ? m : ~m;
+        }
+        uint32_t o = 0;
+        if (valid && (peers & lt_mask) == 0)
+          o = atomicAdd(wc + wave * NB + h[j], (uint32_t)__popcll(peers));
+        rank[j] = o;
+        h[j] = valid ? h[j] | ((uint32_t)__popcll(peers & lt_mask) << 9) |
+                           ((uint32_t)__builtin_ctzll(peers) << 16)
+                     : ~0u;
+      } else {
+        rank[j] = wave_rank<DB, uint16_t>(h[j], valid, wc + wave * NB, lt_mask);
+      }
+    }
+    if constexpr (ATOM) {
+      static_assert(DB <= 9, "digit, group rank and leader packed into 9 + 7 + 6 bits");
+#pragma unroll
+      for (uint32_t j = 0; j < PT; ++j) {
+        const uint32_t pk = h[j];
+        const int ldr = pk == ~0u ? 0 : (int)((pk >> 16) & 63u);
+        const uint32_t o = (uint32_t)__builtin_amdgcn_ds_bpermute(ldr << 2, (int)rank[j]);
+        rank[j] = pk == ~0u ? ~0u : o + ((pk >> 9) & 127u);
+        h[j] = pk & (NB - 1);
+      }
     }
     __syncthreads();
-    scan_digit_wave16<NB, NW>(wc, wsum, tid, lane, wave);
+    scan_digit_wave16<NB, NW, false, CT>(wc, wsum, tid, lane, wave);
     if constexpr (DIRECT) {
       // each record straight from its registers to its bucket-sorted place in the chunk's own
       // 64 KB window (the window is written whole, so its lines merge in the L2)
@@ -1125,25 +1174,31 @@ hipError_t launch_msd16(const PartDev& pd, const MapGroup& g, uint8_t* d_out, in
   timer_begin(timer, kHist, s);
   const uint32_t wpc = (uint32_t)tn.small_wgs_per_cu;
   const dim3 ga(std::min<uint32_t>(g.num_maps * cpm, ncu * wpc));
-#define SUX_M16A_D(KW, DB, LOV, D)                                                                 \
+#define SUX_M16A_D(KW, DB, LOV, D, A)                                                              \
   do {                                                                                             \
-    constexpr size_t ldsa = M16a<NWA, DB>::lds_bytes();                                            \
-    allow_lds(reinterpret_cast<const void*>(&k_msd16a<KW, NWA, DB, LOV, D>), ldsa);                \
-    hipLaunchKernelGGL((k_msd16a<KW, NWA, DB, LOV, D>), ga, dim3(NWA * kWave), ldsa, s, pd, g,     \
+    constexpr size_t ldsa = M16a<NWA, DB, A ? 4 : 2>::lds_bytes();                                 \
+    static_assert(2 * ldsa <= 160 * 1024, "pass A: two workgroups per CU");                       \
+    allow_lds(reinterpret_cast<const void*>(&k_msd16a<KW, NWA, DB, LOV, D, A>), ldsa);             \
+    hipLaunchKernelGGL((k_msd16a<KW, NWA, DB, LOV, D, A>), ga, dim3(NWA * kWave), ldsa, s, pd, g,  \
                        cpm, nbk, offs, d_pids, tmp);                                               \
   } while (0)
-#define SUX_M16A(KW, DB, LOV)                                                              \
+  // msd_direct bit 6: the atomic ranking (u32 counters: 32-partition buckets, digits <= 9 bits)
+  const bool atom_a = (tn.msd_direct & 64) && !(tn.msd_direct & 5) && LO == kM16LoWide;
+#define SUX_M16A_X(KW, DB, LOV, ATOM_OK)                                                   \
   do {                                                                                     \
     if (tn.msd_direct & 4) {                                                               \
       const dim3 gd(std::min<uint32_t>(g.num_maps * cpm, ncu));                            \
       hipLaunchKernelGGL((k_msd16a_dma<KW, DB, LOV>), gd, dim3(512), 0, s, pd, g, cpm, nbk, \
                          offs, d_pids, tmp);                                               \
     } else if (tn.msd_direct & 1) {                                                        \
-      SUX_M16A_D(KW, DB, LOV, true);                                                       \
+      SUX_M16A_D(KW, DB, LOV, true, false);                                                \
+    } else if (ATOM_OK && atom_a) {                                                        \
+      SUX_M16A_D(KW, DB, LOV, false, ATOM_OK);                                             \
     } else {                                                                               \
-      SUX_M16A_D(KW, DB, LOV, false);                                                      \
+      SUX_M16A_D(KW, DB, LOV, false, false);                                               \
     }                                                                                      \
   } while (0)
+#define SUX_M16A(KW, DB, LOV) SUX_M16A_X(KW, DB, LOV, (LOV == kM16LoWide && DB <= 9))
 #define SUX_M16AK(DB, LOV)                   \
   do {                                       \
     if (kw <= 1) SUX_M16A(1, DB, LOV);       \
@@ -1160,6 +1215,7 @@ hipError_t launch_msd16(const PartDev& pd, const MapGroup& g, uint8_t* d_out, in
   else SUX_M16AK(8, kM16Lo);
 #undef SUX_M16AK
 #undef SUX_M16A
+#undef SUX_M16A_X
 #undef SUX_M16A_D
   timer_end(timer, kHist, s);
   hipError_t e = hipGetLastError();
