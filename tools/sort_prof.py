@@ -3,6 +3,7 @@ partition of the bench), `reps` timed calls after two warm-ups; prints the HIP-e
 With SORT_PROF_INPUT=partition the keys are those of one range partition of 200 (TeraSort's
 uniform bounds, partition 100: the first key byte 0x80 or, for 22 % of the keys, 0x81 with the
 second byte below 0x47), the shape of the bench's reduce_sort leg.
+SORT_PROF_N=<records> changes the record count (TeraSort inputs).
 usage: python tools/sort_prof.py [reps=20] [tuning field=value,...] [library path (A/B builds)]"""
 import os
 import sys
@@ -21,7 +22,7 @@ def main():
     node = Node(device=0)
     if len(sys.argv) > 2 and sys.argv[2]:
         node.set_tuning(**{k: int(v) for k, v in (kv.split("=") for kv in sys.argv[2].split(","))})
-    n, rs = 5_000_000, 100
+    n, rs = int(os.environ.get("SORT_PROF_N", 5_000_000)), 100
     kind, klen = N.SORT_BYTES, 10
     if os.environ.get("SORT_PROF_INPUT") == "long":  # bench.py reduce_sort_long's 32 Mi rows
         n, rs, kind, klen = 32 << 20, 16, N.SORT_LONG, 8
