@@ -1514,6 +1514,7 @@ int sux_partitioner_create(sux_node* node, const sux_partitioner_desc* d, sux_pa
     p->pd.key_len = d->key_len;
     p->pd.seed = d->seed;
     p->pd.ascending = d->ascending;
+    p->pd.rmagic = sux::part_magic(R);
     if (d->kind == SUX_PART_RANGE_BYTES && R > 1) {
       const int L = d->key_len;
       // strictly rising bounds (RangePartitioner.determineBounds guarantees it)

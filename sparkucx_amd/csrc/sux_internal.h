@@ -32,7 +32,12 @@ struct PartDev {
   // a sort pass's digit shift decided on the device (make_sort_plan): when set, K1 replaces `seed`
   // with *dseed before computing any pid
   const int32_t* dseed;
+  // floor((2^64 - 1) / R) + 1 (part_magic): the hash partitioners' modulo by R as two multiplies
+  // (Lemire's fastmod) instead of a 32-bit division sequence per record
+  uint64_t rmagic;
 };
+// PartDev::rmagic for R >= 1 (R = 1 wraps to 0, which the fastmod maps to remainder 0).
+inline uint64_t part_magic(int32_t R) { return ~0ull / (uint64_t)R + 1ull; }
 
 // Kernel tuning of one launch: the node's sux_tuning with every default filled in (sux_api.cpp,
 // resolve_tuning).  Replaces round 1's process-wide environment overrides.

@@ -22,9 +22,16 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h1, uint32_t len) {
   h1 *= 0xc2b2ae35u;
   return h1 ^ (h1 >> 16);
 }
-__device__ __forceinline__ int32_t pmod(int32_t a, int32_t n) {
-  int32_t r = a % n;
-  return r < 0 ? (r + n) % n : r;
+// a mod n in [0, n) for n >= 1 — Spark's pmod (Pmod of HashPartitioning) and nonNegativeMod
+// (HashPartitioner) agree with it for a positive modulus.  The remainder of |a| comes from
+// Lemire's fastmod with M = part_magic(n): ((M * u mod 2^64) * n) >> 64, exact for every 32-bit u
+// and n; a negative a with a non-zero remainder m maps to n - m.  (Checked against the C `%`
+// definition on 4.7e8 cases, every R the tests use among them; the GPU tests check it against
+// oracle.c.)
+__device__ __forceinline__ int32_t mod_pos(int32_t a, int32_t n, uint64_t M) {
+  const uint32_t u = a < 0 ? 0u - (uint32_t)a : (uint32_t)a;
+  const uint32_t m = (uint32_t)__umul64hi(M * (uint64_t)u, (uint64_t)(uint32_t)n);
+  return (a < 0 && m) ? n - (int32_t)m : (int32_t)m;
 }
 
 __device__ __forceinline__ uint32_t ld_u32(const uint8_t* p, int off) {
@@ -78,11 +85,11 @@ __device__ __forceinline__ int get_partition(const PartDev& pd, const uint8_t* r
       uint32_t lo32 = ld_u32(rec, pd.key_offset), hi32 = ld_u32(rec, pd.key_offset + 4);
       uint32_t h1 = mix_h1((uint32_t)pd.seed, mix_k1(lo32));
       h1 = mix_h1(h1, mix_k1(hi32));
-      return pmod((int32_t)fmix32(h1, 8), pd.R);
+      return mod_pos((int32_t)fmix32(h1, 8), pd.R, pd.rmagic);
     }
     case 3: {  // SUX_PART_MURMUR3_INT
       uint32_t v = ld_u32(rec, pd.key_offset);
-      return pmod((int32_t)fmix32(mix_h1((uint32_t)pd.seed, mix_k1(v)), 4), pd.R);
+      return mod_pos((int32_t)fmix32(mix_h1((uint32_t)pd.seed, mix_k1(v)), 4), pd.R, pd.rmagic);
     }
     case 4: {  // SUX_PART_MURMUR3_BYTES (legacy hashUnsafeBytes)
       const int off = pd.key_offset, len = pd.key_len, aligned = len - len % 4;
@@ -90,16 +97,14 @@ __device__ __forceinline__ int get_partition(const PartDev& pd, const uint8_t* r
       for (int i = 0; i < aligned; i += 4) h1 = mix_h1(h1, mix_k1(ld_u32(rec, off + i)));
       for (int i = aligned; i < len; ++i)
         h1 = mix_h1(h1, mix_k1((uint32_t)(int32_t)(int8_t)rec[off + i]));
-      return pmod((int32_t)fmix32(h1, (uint32_t)len), pd.R);
+      return mod_pos((int32_t)fmix32(h1, (uint32_t)len), pd.R, pd.rmagic);
     }
     case 5: {  // SUX_PART_HASH_LONG: nonNegativeMod(Long.hashCode)
       uint32_t h = ld_u32(rec, pd.key_offset) ^ ld_u32(rec, pd.key_offset + 4);
-      int32_t r = (int32_t)h % pd.R;
-      return r + (r < 0 ? pd.R : 0);
+      return mod_pos((int32_t)h, pd.R, pd.rmagic);
     }
     case 6: {  // SUX_PART_HASH_INT
-      int32_t r = (int32_t)ld_u32(rec, pd.key_offset) % pd.R;
-      return r + (r < 0 ? pd.R : 0);
+      return mod_pos((int32_t)ld_u32(rec, pd.key_offset), pd.R, pd.rmagic);
     }
     case kPartRadix: {  // internal: digit of the big-endian 128-bit (key, index) pair
       const uint64_t hi = ((uint64_t)__builtin_bswap32(ld_u32(rec, 0)) << 32) |
@@ -153,19 +158,17 @@ __device__ __forceinline__ int partition_words(const PartDev& pd, const uint32_t
     case 2: {
       uint32_t h1 = mix_h1((uint32_t)pd.seed, mix_k1(w[0]));
       if constexpr (KW > 1) h1 = mix_h1(h1, mix_k1(w[1]));
-      return pmod((int32_t)fmix32(h1, 8), R);
+      return mod_pos((int32_t)fmix32(h1, 8), R, pd.rmagic);
     }
     case 3:
-      return pmod((int32_t)fmix32(mix_h1((uint32_t)pd.seed, mix_k1(w[0])), 4), R);
+      return mod_pos((int32_t)fmix32(mix_h1((uint32_t)pd.seed, mix_k1(w[0])), 4), R, pd.rmagic);
     case 5: {
       uint32_t h = w[0];
       if constexpr (KW > 1) h ^= w[1];
-      const int32_t r = (int32_t)h % R;
-      return r + (r < 0 ? R : 0);
+      return mod_pos((int32_t)h, R, pd.rmagic);
     }
     case 6: {
-      const int32_t r = (int32_t)w[0] % R;
-      return r + (r < 0 ? R : 0);
+      return mod_pos((int32_t)w[0], R, pd.rmagic);
     }
     case kPartRadix:  // internal (sux_sort_records): digit of the big-endian 128-bit pair
       if constexpr (KW == 4) {

@@ -89,6 +89,7 @@ int main() {
   pd.key_len = 8;
   pd.seed = 42;
   pd.ascending = 1;
+  pd.rmagic = part_magic(pd.R);
   MapGroup g{};
   g.recs = recs;
   g.records_per_map = rpm;

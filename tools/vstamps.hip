@@ -90,6 +90,7 @@ int main(int argc, char** argv) {
   pd.key_len = 8;
   pd.seed = 42;
   pd.ascending = 1;
+  pd.rmagic = part_magic(pd.R);
   Tuning tn{};
   tn.varlen_kernel = ver;
   VarGroup g{};
