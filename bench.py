@@ -393,8 +393,8 @@ def maps_2e27_leg(node, part, data, out, n: int, rs: int, R: int, dev, steps: in
 
 # newest first: a (workload, kernel) pair not profiled in a later round falls back to an earlier
 # round's counters (round 5 re-profiled C5's small-record kernels, whose shape changed)
-PMC_FILES = [os.path.join(ROOT, "profiles", f) for f in ("pmc_r05.json", "pmc_r04.json",
-                                                          "pmc_r03.json")]
+PMC_FILES = [os.path.join(ROOT, "profiles", f) for f in ("pmc_r06.json", "pmc_r05.json",
+                                                          "pmc_r04.json", "pmc_r03.json")]
 
 
 def plugin_leg(node, part, data, rs: int, R: int, rpm: int, gm: int, groups: int, dev,
