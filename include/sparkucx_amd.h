@@ -247,8 +247,9 @@ typedef struct sux_tuning {
                                (with 3 + 4): pass B gathers the next segment while the current
                                one is written out (maps of <= 256 chunks); bit 6 (with 3):
                                pass A ranks with one returning LDS atomic per digit group on
-                               u32 counters; 0: bits 3 + 4 (the measured default), -1: none
-                               (round 4's shape)                                              */
+                               u32 counters; bit 7 (with 3): pass A matches digits on a 6-bit
+                               lane tag instead of the digit bits; 0: bits 3 + 4 + 7 (the
+                               measured default), -1: none (round 4's shape)                  */
   int32_t reserved[1];
 } sux_tuning;
 int sux_node_set_tuning(sux_node* node, const sux_tuning* tuning);

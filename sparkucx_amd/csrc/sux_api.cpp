@@ -1017,8 +1017,10 @@ sux::Tuning resolve_tuning(const sux_tuning& t, bool pipelined) {
   r.split_cus = t.split_cus > 0 ? t.split_cus : 0;
   r.gather_kernel = t.gather_kernel ? t.gather_kernel : 3;
   // 0: 32-partition buckets + pass B's element -> run map (bits 3 + 4; round 5, C5 965 -> 993
-  // GB/s, profiles/r05_h); -1: round 4's shape (16-partition buckets, run-table search)
-  r.msd_direct = t.msd_direct > 0 ? t.msd_direct : t.msd_direct == 0 ? 24 : 0;
+  // GB/s, profiles/r05_h) + pass A's tag match (bit 7; round 6: pass A alone 1.57-1.59 ->
+  // 1.49-1.52 ms, the C5 leg +0.4 %, profiles/r06_msd16a/tag_*); -1: round 4's shape
+  // (16-partition buckets, run-table search)
+  r.msd_direct = t.msd_direct > 0 ? t.msd_direct : t.msd_direct == 0 ? 152 : 0;
   r.gather16 = r.gather_kernel != 2;
   return r;
 }
@@ -1390,7 +1392,7 @@ int sux_node_set_tuning(sux_node* node, const sux_tuning* t) {
     require(in(t->gather_kernel, {1, 2, 3}), SUX_EINVAL, "gather_kernel must be 1, 2 or 3");
     require(t->split_cus == -1 || (t->split_cus >= 0 && t->split_cus <= 224 && t->split_cus % 32 == 0),
             SUX_EINVAL, "split_cus must be -1, 0 or a multiple of 32 up to 224");
-    require(t->msd_direct >= -1 && t->msd_direct <= 127, SUX_EINVAL, "msd_direct must be -1 .. 127");
+    require(t->msd_direct >= -1 && t->msd_direct <= 255, SUX_EINVAL, "msd_direct must be -1 .. 255");
     for (int32_t r : t->reserved) require(r == 0, SUX_EINVAL, "reserved tuning fields must be 0");
     require(node, SUX_EINVAL, "NULL node");
     std::lock_guard<std::mutex> lk(node->mu);

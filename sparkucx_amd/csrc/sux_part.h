@@ -125,6 +125,33 @@ __device__ __forceinline__ uint32_t wave_rank(uint32_t dig, bool valid, CT* wcw,
   return valid ? r0 + (uint32_t)__popcll(peers & lt_mask) : ~0u;
 }
 
+// wave_rank with the digit match on a 6-bit group tag instead of the DB digit bits: every valid
+// lane stores its lane index at tag[dig] (one byte per digit, the wave's own array) and reads it
+// back.  Whichever lane's store landed, all lanes of one digit read the same lane index and
+// lanes of different digits read different ones (a digit's slot only ever holds a lane of that
+// digit this round), so matching the 6 tag bits finds exactly the lanes of the same digit.
+// Same ranks as wave_rank; 6 ballots instead of DB.
+template <uint32_t DB, typename CT = uint32_t>
+__device__ __forceinline__ uint32_t wave_rank_tag(uint32_t dig, bool valid, CT* wcw, uint8_t* tag,
+                                                  int lane, uint64_t lt_mask) {
+  if (valid) tag[dig] = (uint8_t)lane;
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t t = valid ? (uint32_t)tag[dig] : 0u;
+  uint64_t peers = __ballot(valid);
+#pragma unroll
+  for (uint32_t bb = 0; bb < 6; ++bb) {
+    const bool bit = (t >> bb) & 1u;
+    const uint64_t m = __ballot(bit);
+    peers &= bit ? m : ~m;
+  }
+  uint32_t r0 = 0;
+  if (valid) r0 = wcw[dig];
+  __builtin_amdgcn_wave_barrier();
+  if (valid && (peers & lt_mask) == 0) wcw[dig] = (CT)(r0 + (uint32_t)__popcll(peers));
+  __builtin_amdgcn_wave_barrier();
+  return valid ? r0 + (uint32_t)__popcll(peers & lt_mask) : ~0u;
+}
+
 // Block exclusive scan of wc[NW][NB] in (digit, wave) order, in place (NW*64 threads, NB*NW
 // entries, E = NB/64 consecutive entries per thread).  Two barriers.
 template <uint32_t NB, uint32_t NW>

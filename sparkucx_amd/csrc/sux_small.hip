@@ -451,10 +451,11 @@ __device__ __forceinline__ void scan_digit_wave16(CT* wc, uint32_t* wsum, int ti
 }
 
 // stage[CH] u32x4 (its first NW words double as wsum) | wc[NW][2^DB] u16 (u32: atomic ranking)
-template <uint32_t NW, uint32_t DB, uint32_t CB = 2>
+// (| tag[NW][2^DB] u8 with the tag match, TAG)
+template <uint32_t NW, uint32_t DB, uint32_t CB = 2, bool TAG = false>
 struct M16a {
   static constexpr uint32_t NB = 1u << DB, NT = NW * kWave, PT = kM16Chunk / NT;
-  static constexpr uint32_t lds_bytes() { return kM16Chunk * 16 + NW * NB * CB; }
+  static constexpr uint32_t lds_bytes() { return kM16Chunk * 16 + NW * NB * CB + (TAG ? NW * NB : 0u); }
 };
 // stage[CAP] u32x4 | wc[NW][NB] | cur[NB] | wsum[NW] | los[CAP] u8 | rp[MC+1] u32 | ro[MC] u16
 template <uint32_t NW, uint32_t PT, uint32_t LO = kM16Lo, uint32_t MC = kM16MaxChunks>
@@ -492,18 +493,22 @@ __device__ __forceinline__ uint32_t m16_pid(const PartDev& pd, const u32x4& r, i
 // u16 read-by-every-lane + leader-write round trip of wave_rank, once per round, is pass A's
 // costliest bank-conflicted LDS traffic (tools/msd_whatif.hip: with conflict-free counters pass A
 // would be 14 % faster).
-template <int KW, uint32_t NW, uint32_t DB, uint32_t LO, bool DIRECT = false, bool ATOM = false>
+// TAG (msd_direct bit 7): the ranking matches digits on a 6-bit lane tag (wave_rank_tag).
+template <int KW, uint32_t NW, uint32_t DB, uint32_t LO, bool DIRECT = false, bool ATOM = false,
+          bool TAG = false>
 __global__ __launch_bounds__(NW * 64, 4) void k_msd16a(PartDev pd, MapGroup g, uint32_t cpm,
                                                  uint32_t nbk, uint16_t* __restrict__ offs,
                                                  uint16_t* __restrict__ pids_out,
                                                  uint8_t* __restrict__ tmp) {
+  static_assert(!(TAG && ATOM), "one ranking");
   resolve_seed(pd);
   using CT = typename std::conditional<ATOM, uint32_t, uint16_t>::type;
-  using K = M16a<NW, DB, sizeof(CT)>;
+  using K = M16a<NW, DB, sizeof(CT), TAG>;
   constexpr uint32_t NB = K::NB, NT = K::NT, PT = K::PT, CH = kM16Chunk;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
   u32x4* stage = reinterpret_cast<u32x4*>(lds8);
   CT* wc = reinterpret_cast<CT*>(stage + CH);  // [NW][NB]
+  uint8_t* tag8 = reinterpret_cast<uint8_t*>(wc + NW * NB);  // TAG: [NW][NB]
   uint32_t* wsum = reinterpret_cast<uint32_t*>(lds8);       // only inside the scan: stage is idle
   const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
   const uint64_t lt_mask = (1ull << lane) - 1ull;
@@ -581,6 +586,9 @@ __global__ __launch_bounds__(NW * 64, 4) void k_msd16a(PartDev pd, MapGroup g, u
         h[j] = valid ? h[j] | ((uint32_t)__popcll(peers & lt_mask) << 9) |
                            ((uint32_t)__builtin_ctzll(peers) << 16)
                      : ~0u;
+      } else if constexpr (TAG) {
+        rank[j] = wave_rank_tag<DB, uint16_t>(h[j], valid, wc + wave * NB, tag8 + wave * NB, lane,
+                                              lt_mask);
       } else {
         rank[j] = wave_rank<DB, uint16_t>(h[j], valid, wc + wave * NB, lt_mask);
       }
@@ -1174,16 +1182,18 @@ hipError_t launch_msd16(const PartDev& pd, const MapGroup& g, uint8_t* d_out, in
   timer_begin(timer, kHist, s);
   const uint32_t wpc = (uint32_t)tn.small_wgs_per_cu;
   const dim3 ga(std::min<uint32_t>(g.num_maps * cpm, ncu * wpc));
-#define SUX_M16A_D(KW, DB, LOV, D, A)                                                              \
+#define SUX_M16A_D(KW, DB, LOV, D, A, T)                                                           \
   do {                                                                                             \
-    constexpr size_t ldsa = M16a<NWA, DB, A ? 4 : 2>::lds_bytes();                                 \
+    constexpr size_t ldsa = M16a<NWA, DB, A ? 4 : 2, T>::lds_bytes();                              \
     static_assert(2 * ldsa <= 160 * 1024, "pass A: two workgroups per CU");                       \
-    allow_lds(reinterpret_cast<const void*>(&k_msd16a<KW, NWA, DB, LOV, D, A>), ldsa);             \
-    hipLaunchKernelGGL((k_msd16a<KW, NWA, DB, LOV, D, A>), ga, dim3(NWA * kWave), ldsa, s, pd, g,  \
-                       cpm, nbk, offs, d_pids, tmp);                                               \
+    allow_lds(reinterpret_cast<const void*>(&k_msd16a<KW, NWA, DB, LOV, D, A, T>), ldsa);          \
+    hipLaunchKernelGGL((k_msd16a<KW, NWA, DB, LOV, D, A, T>), ga, dim3(NWA * kWave), ldsa, s, pd,  \
+                       g, cpm, nbk, offs, d_pids, tmp);                                            \
   } while (0)
-  // msd_direct bit 6: the atomic ranking (u32 counters: 32-partition buckets, digits <= 9 bits)
+  // msd_direct bit 6: the atomic ranking (u32 counters: 32-partition buckets, digits <= 9 bits);
+  // bit 7: the tag match (same shapes)
   const bool atom_a = (tn.msd_direct & 64) && !(tn.msd_direct & 5) && LO == kM16LoWide;
+  const bool tag_a = (tn.msd_direct & 128) && !(tn.msd_direct & 69) && LO == kM16LoWide;
 #define SUX_M16A_X(KW, DB, LOV, ATOM_OK)                                                   \
   do {                                                                                     \
     if (tn.msd_direct & 4) {                                                               \
@@ -1191,11 +1201,13 @@ hipError_t launch_msd16(const PartDev& pd, const MapGroup& g, uint8_t* d_out, in
       hipLaunchKernelGGL((k_msd16a_dma<KW, DB, LOV>), gd, dim3(512), 0, s, pd, g, cpm, nbk, \
                          offs, d_pids, tmp);                                               \
     } else if (tn.msd_direct & 1) {                                                        \
-      SUX_M16A_D(KW, DB, LOV, true, false);                                                \
+      SUX_M16A_D(KW, DB, LOV, true, false, false);                                         \
     } else if (ATOM_OK && atom_a) {                                                        \
-      SUX_M16A_D(KW, DB, LOV, false, ATOM_OK);                                             \
+      SUX_M16A_D(KW, DB, LOV, false, ATOM_OK, false);                                      \
+    } else if (ATOM_OK && tag_a) {                                                         \
+      SUX_M16A_D(KW, DB, LOV, false, false, ATOM_OK);                                      \
     } else {                                                                               \
-      SUX_M16A_D(KW, DB, LOV, false, false);                                               \
+      SUX_M16A_D(KW, DB, LOV, false, false, false);                                        \
     }                                                                                      \
   } while (0)
 #define SUX_M16A(KW, DB, LOV) SUX_M16A_X(KW, DB, LOV, (LOV == kM16LoWide && DB <= 9))

@@ -64,7 +64,7 @@ def test_bootstrap_and_pool_entry_points_validate_arguments():
     ("small_groups", 3), ("tile_records", 96), ("tile_records", 32), ("onepass", 2),
     ("varlen_kernel", 4), ("varlen_tile", 100), ("sort_max_digit_bits", 17), ("sort_gather", 2),
     ("sort_all_passes", -1), ("hist_kernel", 2), ("scatter_kernel", 2), ("small_kernel", 3),
-    ("hist_nt", 2), ("counts_layout", 3), ("scatter_counters", 3), ("lz4_queue", 3), ("scatter_nt", 4), ("gather_kernel", 4), ("split_cus", 48), ("split_cus", 256), ("msd_direct", 128), ("msd_direct", -2),
+    ("hist_nt", 2), ("counts_layout", 3), ("scatter_counters", 3), ("lz4_queue", 3), ("scatter_nt", 4), ("gather_kernel", 4), ("split_cus", 48), ("split_cus", 256), ("msd_direct", 256), ("msd_direct", -2),
     ("exchange_self", 2), ("reserved", 1)])
 def test_tuning_table_rejects_values_outside_each_fields_set(field, value):
     """sux_node_set_tuning validates the whole table before it looks at the node, so every

@@ -325,13 +325,15 @@ def test_line_carry_scatter_shapes(gpu_node, tuned, R, n, rpm, tile, tpi):
 ])
 @pytest.mark.parametrize("wpc,direct", [(2, 0), (1, 0), (2, -1), (1, -1), (2, 3), (1, 3), (2, 1),
                                         (2, 2), (2, 4), (2, 6), (2, 8), (2, 16), (1, 16),
-                                        (2, 56), (1, 56), (2, 88), (1, 88), (2, 72)])
+                                        (2, 56), (1, 56), (2, 88), (1, 88), (2, 72),
+                                        (2, 152), (1, 152), (2, 136)])
 def test_msd16_pids_and_shapes(gpu_node, tuned, R, n, rpm, skew, wpc, direct):
     """The two-level small-record path (small_kernel 4, 2 or 1 workgroups per CU; msd_direct:
     each pass stores records from registers instead of through its LDS stage (bits 0, 1), pass A
     by LDS-DMA (bit 2), 32-partition buckets (bit 3), pass B's element -> run map (bit 4), pass B
     gathering the next segment while it writes the current one (bit 5), pass A ranking with
-    one LDS atomic per digit group (bit 6)): bytes, both
+    one LDS atomic per digit group (bit 6), pass A matching digits on a 6-bit lane tag (bit 7)):
+    bytes, both
     index tables and the caller-requested pid array (written by pass A in input order) equal
     the oracle's."""
     tuned(small_kernel=4, small_wgs_per_cu=wpc, msd_direct=direct)

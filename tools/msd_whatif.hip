@@ -79,6 +79,10 @@ int main() {
   constexpr size_t lda = M16a<NWA, DB, 4>::lds_bytes();
   auto* kern = &k_msd16a<2, NWA, DB, kM16LoWide, false, true>;
   const int level = 64;
+#elif defined(MSD_TOOL_TAG)  // msd_direct bit 7 (the 6-bit tag match)
+  constexpr size_t lda = M16a<NWA, DB, 2, true>::lds_bytes();
+  auto* kern = &k_msd16a<2, NWA, DB, kM16LoWide, false, false, true>;
+  const int level = 128;
 #else
   constexpr size_t lda = M16a<NWA, DB>::lds_bytes();
   auto* kern = &k_msd16a<2, NWA, DB, kM16LoWide, false>;
