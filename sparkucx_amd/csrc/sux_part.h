@@ -135,7 +135,10 @@ template <uint32_t DB, typename CT = uint32_t>
 __device__ __forceinline__ uint32_t wave_rank_tag(uint32_t dig, bool valid, CT* wcw, uint8_t* tag,
                                                   int lane, uint64_t lt_mask) {
   if (valid) tag[dig] = (uint8_t)lane;
+  // the read below must reload the byte (other lanes' stores), never forward this lane's own
+  // store: a compiler memory barrier; the wave's LDS operations complete in order
   __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
   const uint32_t t = valid ? (uint32_t)tag[dig] : 0u;
   uint64_t peers = __ballot(valid);
 #pragma unroll
