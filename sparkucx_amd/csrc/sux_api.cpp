@@ -868,6 +868,7 @@ hipError_t ipc_open_bounded(sux_node* node, void** base, const hipIpcMemHandle_t
     std::mutex mu;
     std::condition_variable cv;
     bool done = false;
+    bool abandoned = false;  // the caller stopped waiting: a late mapping is closed, not leaked
     hipError_t e = hipErrorUnknown;
     void* base = nullptr;
   };
@@ -877,17 +878,25 @@ hipError_t ipc_open_bounded(sux_node* node, void** base, const hipIpcMemHandle_t
     void* b = nullptr;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipIpcOpenMemHandle(&b, h, hipIpcMemLazyEnablePeerAccess);
-    std::lock_guard<std::mutex> lk(c->mu);
-    c->e = e;
-    c->base = b;
-    c->done = true;
-    c->cv.notify_all();
+    bool late = false;
+    {
+      std::lock_guard<std::mutex> lk(c->mu);
+      c->e = e;
+      c->base = b;
+      c->done = true;
+      late = c->abandoned;
+      c->cv.notify_all();
+    }
+    if (late && e == hipSuccess) (void)hipIpcCloseMemHandle(b);
   }).detach();
   const auto t0 = std::chrono::steady_clock::now();
   std::unique_lock<std::mutex> lk(c->mu);
   const bool done = c->cv.wait_for(lk, std::chrono::duration<double>(limit_s), [&] { return c->done; });
   *waited_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  if (!done) return hipErrorNotReady;  // the helper keeps running; its mapping, if any, leaks
+  if (!done) {  // the helper keeps running; a mapping it still gets is closed by the helper
+    c->abandoned = true;
+    return hipErrorNotReady;
+  }
   *base = c->base;
   return c->e;
 }
